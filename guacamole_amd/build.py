@@ -1,0 +1,41 @@
+"""Build helpers: compile the HIP library in-tree for gfx950 (hipcc) and the
+test oracle (g++).  Used by __graft_entry__.build()."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "guacamole_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIB_DIR, "libgqpileup.so")
+SOURCES = [os.path.join(CSRC, "gq_pileup.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
+    os.path.join(ROOT, "include", "gqpileup.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("GQ_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _stale(LIB, DEPS):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I" + os.path.join(ROOT, "include"), "-o", LIB] + SOURCES
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+    return LIB
+
+
+def build_oracle() -> str:
+    d = os.path.join(ROOT, "oracle")
+    subprocess.check_call(["make", "-s", "-C", d])
+    return os.path.join(d, "_build", "liboracle.so")

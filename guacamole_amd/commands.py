@@ -1,0 +1,127 @@
+"""Caller commands over the GPU engine — the host mirror of the reference's plugin surface.
+
+Reference surface (paths relative to /root/reference/src/main/scala/org/hammerlab/guacamole/):
+  * command registry + args       Guacamole.scala:37-77, Command.scala:33-62, Common.scala:48-136
+  * germline-threshold            commands/GermlineThresholdCaller.scala:40-88
+        --threshold (8), --emit-ref, --emit-no-call, + --reads/--loci/--out/--parallelism/...
+  * somatic-standard              commands/SomaticStandardCaller.scala:228-160
+        --tumor-reads, --normal-reads, --odds (20), --min-mapq (1), --filter-multi-allelic, ...
+  * loci partitioning             DistributedUtil.scala:55-69 (--parallelism, --partition-accuracy)
+
+The per-locus work (pileupFlatMap + callVariantsAtLocus / findPotentialVariantAtLocus)
+runs in libgqpileup on the GPU; this module only loads reads, builds LociSets and
+partitions, and formats output.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import native, soa
+from .loci import (LociSet, LociSetBuilder, flatten_partitions, partition_loci_by_approximate_depth,
+                   partition_loci_uniformly)
+from .reads import InputFilters, ReadSet, load_reads
+
+_UPLOADED: Dict[int, tuple] = {}
+
+
+def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
+    """Upload a ReadSet once per context and keep it resident."""
+    key = (id(ctx), id(rs))
+    hit = _UPLOADED.get(key)
+    if hit is not None and hit[0] is rs:
+        return hit[1]
+    d = ctx.upload(soa.pack(rs))
+    _UPLOADED[key] = (rs, d)
+    return d
+
+
+def partition(loci: LociSet, parallelism: int, accuracy: int, *read_sets: ReadSet):
+    """DistributedUtil.partitionLociAccordingToArgs (DistributedUtil.scala:55-69)."""
+    tasks = parallelism if parallelism > 0 else 1
+    if accuracy == 0:
+        return partition_loci_uniformly(tasks, loci)
+    return partition_loci_by_approximate_depth(tasks, loci, accuracy, *[r.regions() for r in read_sets])
+
+
+def germline_threshold_reads(ctx: native.Context, rs: ReadSet, loci, threshold: int = 8, emit_ref: bool = False,
+                             emit_no_call: bool = False) -> List[tuple]:
+    """pileupFlatMap(reads, partitions, skipEmpty=true, callVariantsAtLocus) on the GPU.
+    `loci` = flatten_partitions(...) arrays.  Rows: (contig, locus, sample, (gt0, gt1), ref, alt, flags)."""
+    calls = ctx.germline_threshold(device_reads(ctx, rs), loci, threshold, emit_ref, emit_no_call)
+    return calls.tuples(rs.contig_names)
+
+
+# ---------------------------------------------------------------------------------------------
+# CLI
+def _common_args(p: argparse.ArgumentParser) -> None:
+    p.add_argument("--loci", default="", help="Loci at which to call variants (e.g. 'all', 'chr1:0-1000,chr2')")
+    p.add_argument("--loci-from-file", default="", help="Path to file giving loci")
+    p.add_argument("--out", default="", help="Output path (.vcf or .json; empty = JSON to stdout)")
+    p.add_argument("--parallelism", type=int, default=0, help="Num variant calling tasks (loci partitions)")
+    p.add_argument("--partition-accuracy", type=int, default=250,
+                   help="Num micro partitions per task in loci partitioning; 0 = uniform")
+    p.add_argument("--device", type=int, default=0, help="GPU index")
+
+
+def _loci_builder(args) -> LociSetBuilder:
+    """Common.loci (Common.scala:223-239)."""
+    if args.loci and args.loci_from_file:
+        raise ValueError("Specify at most one of the 'loci' and 'loci-from-file' arguments")
+    if args.loci:
+        return LociSet.parse(args.loci)
+    if args.loci_from_file:
+        with open(args.loci_from_file) as fh:
+            return LociSet.parse(fh.read())
+    return LociSet.parse("all")
+
+
+def _write_genotypes(path: str, rows: List[dict]) -> None:
+    if path.lower().endswith(".vcf"):
+        from .output import write_vcf
+        write_vcf(path, rows)
+    else:
+        out = open(path, "w") if path else sys.stdout
+        for r in rows:
+            out.write(json.dumps(r) + "\n")
+        if path:
+            out.close()
+
+
+def germline_threshold_main(argv: Sequence[str]) -> int:
+    p = argparse.ArgumentParser(prog="germline-threshold",
+                                description="call variants by thresholding read counts (toy example)")
+    p.add_argument("--reads", required=True)
+    p.add_argument("--threshold", type=int, default=8, help="Make a call if at least X%% of reads support it")
+    p.add_argument("--emit-ref", action="store_true", help="Output homozygous reference calls.")
+    p.add_argument("--emit-no-call", action="store_true", help="Output no call calls.")
+    _common_args(p)
+    args = p.parse_args(argv)
+    builder = _loci_builder(args)
+    rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True))
+    loci = builder.result(rs.contig_lengths_map)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, rs)
+    ctx = native.Context(args.device)
+    rows = germline_threshold_reads(ctx, rs, flatten_partitions(parts, rs.contig_index()), args.threshold,
+                                    args.emit_ref, args.emit_no_call)
+    out = [dict(contig=c, start=l, sampleId=rs.sample_names[s] if s < len(rs.sample_names) else "default",
+                alleles=list(gt), referenceAllele=ref, alternateAllele=alt) for c, l, s, gt, ref, alt, fl in rows]
+    _write_genotypes(args.out, out)
+    print("Called %d genotypes." % len(out), file=sys.stderr)
+    return 0
+
+
+COMMANDS = {"germline-threshold": germline_threshold_main}
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in COMMANDS:
+        print("usage: python -m guacamole_amd <command> [args]\ncommands: " + ", ".join(sorted(COMMANDS)),
+              file=sys.stderr)
+        return 1
+    return COMMANDS[argv[0]](argv[1:])

@@ -1,0 +1,1410 @@
+// gq_pileup.hip — MI355X (gfx950) pileup + per-locus germline-threshold engine.
+//
+// Kernels (see DESIGN.md for the roofline of each):
+//   plan_tiles          one thread per locus tile: range lookup + binary search of the
+//                       tile's read window [rb, re) (prefix-max end / start).
+//   germline_tile<T>    one workgroup per tile of T loci: waves walk overlapping reads
+//                       (lanes = 64 consecutive loci of a CIGAR op) and histogram
+//                       elements into LDS with ds_add; then one thread per locus
+//                       makes the GermlineThreshold decision on-device for "simple"
+//                       loci (only Match/Mismatch elements with A/C/G/T/N bases and
+//                       an unambiguous MD-derived reference base) and queues the
+//                       rest for germline_complex.
+//   germline_complex    one wave per queued locus: exact PileupElement semantics,
+//                       variable-length alleles grouped by a 128-bit allele key in
+//                       registers, GermlineThreshold case split.
+//   counts_tile<T>      raw per-locus histogram (gq_pileup_counts).
+//   + hipcub radix sort of the call records by output ordinal.
+//
+// Semantics restated from /root/reference/src/main/scala/org/hammerlab/guacamole/:
+//   commands/GermlineThresholdCaller.scala:90-179, pileup/PileupElement.scala:68-248,
+//   pileup/Pileup.scala:49-186, DistributedUtil.scala:260-306, windowing/SlidingWindow.scala.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gqpileup.h"
+#include "gq_kernels.h"
+
+using namespace gq;
+
+namespace {
+thread_local std::string g_err;
+
+gq_status set_err(gq_status s, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return set_err(GQ_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+  } while (0)
+
+constexpr int kBlock = 256;
+constexpr int kGermT = 1024;  // loci per germline tile
+constexpr int kCountT = 512;  // loci per counts tile
+
+// ------------------------------------------------------------------------------------------
+// Tile planning
+// ------------------------------------------------------------------------------------------
+__global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *__restrict__ r_start,
+                           const int64_t *__restrict__ r_end, const int64_t *__restrict__ r_ord,
+                           const int64_t *__restrict__ r_tile0, int64_t n_ranges, int64_t n_tiles, int T,
+                           DevReads R, Tile *__restrict__ tiles) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  int64_t lo = 0, hi = n_ranges - 1;  // largest r with r_tile0[r] <= t
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (r_tile0[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t r = lo;
+  const int64_t L0 = r_start[r] + (t - r_tile0[r]) * (int64_t)T;
+  const int64_t L1 = min(L0 + (int64_t)T, r_end[r]);
+  const int32_t c = r_contig[r];
+  int64_t b = R.contig_read_begin[c], e = R.contig_read_begin[c + 1];
+  // rb: first read with pmax_end > L0 (pmax_end non-decreasing within the contig)
+  int64_t a0 = b, a1 = e;
+  while (a0 < a1) {
+    int64_t m = (a0 + a1) >> 1;
+    if ((int64_t)R.pmax_end[m] > L0) a1 = m;
+    else a0 = m + 1;
+  }
+  const int64_t rb = a0;
+  a0 = rb;
+  a1 = e;  // re: first read with start >= L1
+  while (a0 < a1) {
+    int64_t m = (a0 + a1) >> 1;
+    if ((int64_t)R.start[m] >= L1) a1 = m;
+    else a0 = m + 1;
+  }
+  Tile tl;
+  tl.ordinal0 = r_ord[r] + (L0 - r_start[r]);
+  tl.rb = rb;
+  tl.re = a0;
+  tl.contig = c;
+  tl.L0 = (int32_t)L0;
+  tl.L1 = (int32_t)L1;
+  tl.range = (int32_t)r;
+  tiles[t] = tl;
+}
+
+struct Counters {  // device-side run counters (one allocation, zeroed per call)
+  unsigned long long n_rec;
+  unsigned long long n_complex;
+  unsigned long long visited;
+  unsigned long long ambiguous;
+  unsigned long long ties;
+  unsigned long long pool_used;
+  int err;
+  int pad;
+  long long err_pos;
+};
+
+// Wave-aggregated reservation of `n` slots on a global counter.
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *ctr, unsigned n) {
+  const int lane = threadIdx.x & 63;
+  // inclusive scan of n across the wave
+  unsigned x = n;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    unsigned y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  const unsigned total = __shfl(x, 63, 64);
+  unsigned long long base = 0;
+  if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
+  base = __shfl(base, 63, 64);
+  return base + (x - n);
+}
+
+__device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, int alt_len) {
+  uint64_t v = r0;
+  for (int i = 0; i < alt_len; ++i) v |= (uint64_t)alt[i] << (8 * (1 + i));
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// germline_tile: LDS histogram + on-device decision for simple loci
+// ------------------------------------------------------------------------------------------
+// LDS categories (u32 per locus, SoA: cat * T + i => consecutive loci on consecutive banks)
+enum : int { C_A = 0, C_C, C_G, C_T, C_N, C_CPLX, C_MASK, C_EVA, C_EVC, C_EVG, C_EVT, C_NCAT };
+
+template <int T>
+struct GermSink {
+  uint32_t *cnt;
+  int32_t L0;
+  int *err;
+  long long *err_pos;
+  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t) {
+    const int i = l - L0;
+    if (kind == K_SNV) {
+      const int c = base_cat(base);  // 5 (= C_CPLX) for a non-ACGTN sequenced base
+      atomicAdd(&cnt[c * T + i], 1u);
+      if (ev) {  // MD mismatch at this position: MD-derived ref differs from the read base
+        if (c < 4) atomicAdd(&cnt[(C_EVA + c) * T + i], 1u);
+        const uint32_t b = std_bit(mdb);
+        if (b) atomicOr(&cnt[C_MASK * T + i], b);
+      }
+    } else {
+      atomicAdd(&cnt[C_CPLX * T + i], 1u);
+      const uint32_t b = std_bit(mdb);
+      if (b) atomicOr(&cnt[C_MASK * T + i], b);
+    }
+  }
+  __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
+};
+
+template <int T>
+__global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
+                                                        int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
+                                                        unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
+                                                        unsigned long long cplx_cap, Counters *ctr) {
+  __shared__ uint32_t cnt[C_NCAT * T];
+  const Tile tl = tiles[blockIdx.x];
+  const int32_t L0 = tl.L0, L1 = tl.L1;
+  for (int i = threadIdx.x; i < C_NCAT * T; i += blockDim.x) cnt[i] = 0u;
+  __syncthreads();
+
+  GermSink<T> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = blockDim.x >> 6;
+  for (int64_t r = tl.rb + wave; r < tl.re; r += nwaves) walk_read(R, r, L0, L1, sink);
+  __syncthreads();
+
+  const bool multi_sample = R.n_samples > 1;
+  unsigned visited = 0, amb = 0, ties = 0;
+  const int nloci = L1 - L0;
+  // uniform trip count so every wave reaches the wave-level reservations together
+  for (int i0 = 0; i0 < nloci; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    CallRec out[2];
+    unsigned nout = 0;
+    bool to_complex = false;
+    if (i < nloci) {
+      uint32_t c[5];
+      uint32_t depth = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        c[k] = cnt[k * T + i];
+        depth += c[k];
+      }
+      const uint32_t cx = cnt[C_CPLX * T + i];
+      depth += cx;
+      if (depth > 0) {
+        ++visited;
+        uint32_t mask = cnt[C_MASK * T + i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c[k] > cnt[(C_EVA + k) * T + i]) mask |= 1u << k;
+        const bool ambiguous = __popc(mask) > 1;
+        if (ambiguous) ++amb;
+        if (ambiguous || cx > 0 || multi_sample) {
+          to_complex = true;
+        } else {
+          // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles
+          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+          const uint8_t bases[5] = {'A', 'C', 'G', 'T', 'N'};
+          // canonical order for ties: Allele(ref, alt) compares alt bytes => A < C < G < N < T
+          const int order[5] = {0, 1, 2, 4, 3};
+          int top[3] = {-1, -1, -1};
+          int npass = 0;
+          for (int oi = 0; oi < 5; ++oi) {
+            const int k = order[oi];
+            if (c[k] == 0) continue;
+            if ((long long)c[k] * 100 / (long long)depth <= threshold) continue;
+            ++npass;
+            // insert into top-3 by count desc (stable w.r.t. canonical order)
+            int p = (npass - 1 < 3) ? npass - 1 : 3;
+            while (p > 0 && c[top[p - 1]] < c[k]) {
+              if (p < 3) top[p] = top[p - 1];
+              --p;
+            }
+            if (p < 3) top[p] = k;
+          }
+          const bool tie = npass >= 2 && (c[top[0]] == c[top[1]] || (npass >= 3 && c[top[1]] == c[top[2]]));
+          if (tie) ++ties;
+          const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
+          const int32_t pos = L0 + i;
+          const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
+          auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
+            CallRec rr;
+            rr.key = (ord << 12) | ((uint64_t)0 << 4) | (uint64_t)sub;
+            rr.contig = tl.contig;
+            rr.pos = pos;
+            rr.sample = 0;
+            rr.gt0 = g0;
+            rr.gt1 = g1;
+            rr.flags = fl;
+            rr.ref_len = 1;
+            if (alt_sym) {
+              const uint8_t sym[5] = {'<', 'A', 'L', 'T', '>'};
+              rr.alt_len = 5;
+              rr.allele = pack_inline(ref, sym, 5);
+            } else {
+              rr.alt_len = 1;
+              rr.allele = pack_inline(ref, &alt1, 1);
+            }
+            return rr;
+          };
+          if (npass == 0) {
+            if (emit_no_call) out[nout++] = mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0);
+          } else if (npass == 1 && bases[top[0]] == ref) {
+            if (emit_ref) out[nout++] = mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0);
+          } else if (npass == 1) {
+            out[nout++] = mk(GQ_GT_ALT, GQ_GT_ALT, bases[top[0]], false, 0);
+          } else {
+            const bool v1 = bases[top[0]] != ref, v2 = bases[top[1]] != ref;
+            if (v1 != v2) {
+              out[nout++] = mk(GQ_GT_REF, GQ_GT_ALT, v1 ? bases[top[0]] : bases[top[1]], false, 0);
+            } else if (v1 && v2) {
+              out[nout++] = mk(GQ_GT_ALT, GQ_GT_OTHERALT, bases[top[0]], false, 0);
+              out[nout++] = mk(GQ_GT_ALT, GQ_GT_OTHERALT, bases[top[1]], false, 1);
+            }
+            // two non-variant single-base alleles cannot occur (all Match alleles share ref)
+          }
+        }
+      }
+    }
+    // reserve + write records (wave-aggregated)
+    const unsigned long long base = wave_reserve(&ctr->n_rec, nout);
+    for (unsigned k = 0; k < nout; ++k)
+      if (base + k < rec_cap) recs[base + k] = out[k];
+    const unsigned long long cb = wave_reserve(&ctr->n_complex, to_complex ? 1u : 0u);
+    if (to_complex && cb < cplx_cap) cplx[cb] = ComplexItem{(int32_t)blockIdx.x, L0 + i};
+  }
+  // block-level reduction of run counters
+  __shared__ unsigned red[3];
+  if (threadIdx.x < 3) red[threadIdx.x] = 0;
+  __syncthreads();
+  if (visited) atomicAdd(&red[0], visited);
+  if (amb) atomicAdd(&red[1], amb);
+  if (ties) atomicAdd(&red[2], ties);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (red[0]) atomicAdd(&ctr->visited, (unsigned long long)red[0]);
+    if (red[1]) atomicAdd(&ctr->ambiguous, (unsigned long long)red[1]);
+    if (red[2]) atomicAdd(&ctr->ties, (unsigned long long)red[2]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// germline_complex: exact per-element classification for queued loci (one wave per locus)
+// ------------------------------------------------------------------------------------------
+struct AlleleDesc {  // enough to regenerate an allele's bytes
+  int64_t read;      // read index (for INS / DEL / MID byte access)
+  int32_t aux;       // INS: number of alt bytes; DEL: deleted length
+  int32_t rp;        // INS: first alt byte position in the read
+  uint8_t kind;
+  uint8_t rb;        // pileup ref base (SNV / DEL)
+  uint8_t base;      // SNV sequenced base / MID deleted base
+  uint8_t pad;
+};
+
+__device__ __forceinline__ int allele_ref_len(const AlleleDesc &d) {
+  switch (d.kind) {
+    case K_SNV: return 1;
+    case K_INS: return d.aux > 0 ? 1 : 0;
+    case K_DEL: return 1 + d.aux;
+    case K_MID: return 1;
+    default: return 0;
+  }
+}
+__device__ __forceinline__ int allele_alt_len(const AlleleDesc &d) {
+  switch (d.kind) {
+    case K_SNV: return 1;
+    case K_INS: return d.aux;
+    case K_DEL: return 1;
+    default: return 0;
+  }
+}
+// Byte i of the ref (which=0) / alt (which=1) allele.  DEL bytes 1.. come from the
+// read's MD deletion events at pos+1.. (PileupElement.scala:108-114).
+__device__ uint8_t allele_byte(const DevReads &R, const AlleleDesc &d, int32_t pos, int which, int i) {
+  switch (d.kind) {
+    case K_SNV: return which == 0 ? d.rb : d.base;
+    case K_INS: {
+      const uint8_t *s = R.seq + R.seq_off[d.read];
+      return which == 0 ? s[d.rp] : s[d.rp + i];
+    }
+    case K_DEL: {
+      if (which == 1 || i == 0) return d.rb;
+      const int32_t s = R.start[d.read];
+      const int v = md_find(R.md_ev + R.md_off[d.read], R.n_md[d.read], pos + i - s);
+      return v < 0 ? (uint8_t)'?' : (uint8_t)v;
+    }
+    case K_MID: return d.base;
+    default: return 0;
+  }
+}
+
+struct Key128 {
+  uint64_t lo, hi;
+};
+__device__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
+  const int rl = allele_ref_len(d), al = allele_alt_len(d);
+  Key128 k;
+  if (rl + al <= 13) {  // exact packing: lengths + bytes
+    uint8_t b[16] = {0};
+    b[0] = (uint8_t)rl;
+    b[1] = (uint8_t)al;
+    b[2] = (uint8_t)sample;
+    int j = 3;
+    for (int i = 0; i < rl; ++i) b[j++] = allele_byte(R, d, pos, 0, i);
+    for (int i = 0; i < al; ++i) b[j++] = allele_byte(R, d, pos, 1, i);
+    k.lo = k.hi = 0;
+    for (int i = 0; i < 8; ++i) k.lo |= (uint64_t)b[i] << (8 * i);
+    for (int i = 0; i < 8; ++i) k.hi |= (uint64_t)b[8 + i] << (8 * i);
+  } else {  // two independent 64-bit hashes; marker 0xFF in the length bytes
+    uint64_t h1 = 0xcbf29ce484222325ull ^ (uint64_t)rl, h2 = 0x9e3779b97f4a7c15ull ^ ((uint64_t)al << 32);
+    auto mix = [&](uint8_t x) {
+      h1 = (h1 ^ x) * 0x100000001b3ull;
+      h2 = (h2 + x + 0x632be59bd9b4e019ull) * 0xff51afd7ed558ccdull;
+      h2 ^= h2 >> 29;
+    };
+    for (int i = 0; i < rl; ++i) mix(allele_byte(R, d, pos, 0, i));
+    mix(0xFE);
+    for (int i = 0; i < al; ++i) mix(allele_byte(R, d, pos, 1, i));
+    k.lo = (h1 & ~0xFFFFFFull) | 0xFFFFull | ((uint64_t)sample << 16);
+    k.hi = h2;
+  }
+  return k;
+}
+
+// Allele ordering (variants/Allele.scala:31-36): ref string, then alt string.
+__device__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDesc &b, int32_t pos) {
+  for (int which = 0; which < 2; ++which) {
+    const int la = which ? allele_alt_len(a) : allele_ref_len(a);
+    const int lb = which ? allele_alt_len(b) : allele_ref_len(b);
+    const int n = la < lb ? la : lb;
+    for (int i = 0; i < n; ++i) {
+      const int x = allele_byte(R, a, pos, which, i), y = allele_byte(R, b, pos, which, i);
+      if (x != y) return x < y ? -1 : 1;
+    }
+    if (la != lb) return la < lb ? -1 : 1;
+  }
+  return 0;
+}
+
+// Locate the PileupElement of read r at `pos` (PileupElement.apply + advanceToLocus) and
+// classify it (PileupElement.alignment).  Returns false and sets *errc on a reference error.
+__device__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
+  const int32_t s = R.start[r];
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  int ci = 0;
+  int32_t ci_locus = s, within = 0, rp = 0;
+  for (;;) {
+    if (ci >= ncig) {
+      *errc = 1;
+      return false;
+    }
+    const uint32_t c = R.cigar[cig_off + ci];
+    const int op = (int)(c & 15u);
+    const int32_t len = (int32_t)(c >> 4);
+    const int32_t rlen = consumes_ref(op) ? len : 0;
+    if (ci_locus <= pos && pos < ci_locus + rlen) {
+      if (consumes_read(op)) rp += pos - ci_locus - within;
+      within = pos - ci_locus;
+      break;
+    } else if (pos == 0 && op == OP_I) {
+      break;
+    } else {
+      if (consumes_read(op)) rp += len - within;
+      ci_locus += rlen;
+      ++ci;
+      within = 0;
+    }
+  }
+  const uint32_t c = R.cigar[cig_off + ci];
+  const int op = (int)(c & 15u);
+  const int32_t len = (int32_t)(c >> 4);
+  const bool fin = within == len - 1;
+  const bool has_next = ci + 1 < ncig;
+  const uint32_t cn = has_next ? R.cigar[cig_off + ci + 1] : 0u;
+  const int nextop = fin ? (has_next ? (int)(cn & 15u) : -1) : op;
+  const int32_t slen = R.seq_len[r];
+  d.read = r;
+  d.rb = refbase;
+  d.pad = 0;
+  if ((op == OP_M || op == OP_EQ) && nextop == OP_I) {
+    const int32_t ilen = (int32_t)(cn >> 4);  // I consumes read bases
+    int32_t from = rp, until = rp + ilen + 1;
+    from = from < 0 ? 0 : (from > slen ? slen : from);
+    until = until > slen ? slen : until;
+    if (until < from) until = from;
+    d.kind = K_INS;
+    d.rp = from;
+    d.aux = until - from;
+    d.base = 0;
+    if (d.aux == 0) {
+      *errc = 1;
+      return false;
+    }
+  } else if (op == OP_I && nextop != -1 && ci_locus == 0) {
+    int32_t from = rp, until = rp + len + 1;
+    from = from < 0 ? 0 : (from > slen ? slen : from);
+    until = until > slen ? slen : until;
+    if (until < from) until = from;
+    d.kind = K_INS;
+    d.rp = from;
+    d.aux = until - from;
+    d.base = 0;
+    if (d.aux == 0) {
+      *errc = 1;
+      return false;
+    }
+  } else if (op == OP_I) {
+    *errc = 2;  // InvalidCigarElementException
+    return false;
+  } else if ((op == OP_M || op == OP_EQ || op == OP_X) && nextop == OP_D) {
+    d.kind = K_DEL;
+    d.aux = (int32_t)(cn >> 4);
+    d.rp = rp;
+    d.base = 0;
+    const uint32_t *ev = R.md_ev + R.md_off[r];
+    const int nmd = R.n_md[r];
+    for (int i = 1; i <= d.aux; ++i)
+      if (md_find(ev, nmd, pos + i - s) < 0) {
+        *errc = 3;
+        return false;
+      }
+  } else if (op == OP_D) {
+    const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
+    if (v < 0) {
+      *errc = 3;
+      return false;
+    }
+    d.kind = K_MID;
+    d.base = (uint8_t)v;
+    d.aux = 0;
+    d.rp = 0;
+  } else if (nextop == OP_D) {
+    *errc = 1;
+    return false;
+  } else if (op == OP_M || op == OP_EQ || op == OP_X) {
+    if (rp >= slen) {
+      *errc = 1;
+      return false;
+    }
+    d.kind = K_SNV;
+    d.base = R.seq[R.seq_off[r] + rp];
+    d.aux = 0;
+    d.rp = rp;
+  } else if (op == OP_S || op == OP_N || op == OP_H) {
+    d.kind = K_CLIP;
+    d.base = 0;
+    d.aux = 0;
+    d.rp = 0;
+  } else {
+    *errc = 1;
+    return false;
+  }
+  return true;
+}
+
+// MD-derived reference base of read r at pos (MappedRead.getReferenceBaseAtLocus) or -1 on error.
+__device__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
+  const int32_t s = R.start[r];
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  int32_t ref = s, rp = 0;
+  for (int k = 0; k < ncig; ++k) {
+    const uint32_t c = R.cigar[cig_off + k];
+    const int op = (int)(c & 15u);
+    const int32_t len = (int32_t)(c >> 4);
+    if (consumes_ref(op)) {
+      if (pos < ref + len) {
+        if (R.n_md[r] < 0) return -4;
+        const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
+        if (op == OP_D) return v < 0 ? -3 : v;
+        if (op == OP_N) return 'N';
+        if (v >= 0) return v;
+        const int32_t q = rp + (pos - ref);
+        if (q >= R.seq_len[r]) return -1;
+        return R.seq[R.seq_off[r] + q];
+      }
+      ref += len;
+    }
+    if (consumes_read(op)) rp += len;
+  }
+  return -1;
+}
+
+constexpr int kSlots = 2;  // table capacity = 64 * kSlots distinct (sample, allele) keys per locus
+
+__global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restrict__ tiles,
+                                                           const ComplexItem *__restrict__ items, DevReads R,
+                                                           int threshold, int emit_ref, int emit_no_call,
+                                                           CallRec *__restrict__ recs, unsigned long long rec_cap,
+                                                           uint8_t *__restrict__ pool, unsigned long long pool_cap,
+                                                           Counters *ctr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const unsigned long long n_items = ctr->n_complex;
+  for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
+    const ComplexItem item = items[it];
+    const Tile tl = tiles[item.tile];
+    const int32_t pos = item.pos;
+    // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
+    uint32_t mask = 0;
+    uint64_t best = ~0ull;  // (end, read) of the heap-root proxy among standard-base reads
+    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
+      const int64_t r = r0 + lane;
+      if (r < tl.re && R.start[r] <= pos && pos < R.end[r]) {
+        const int v = md_ref_at(R, r, pos);
+        if (v < 0) {
+          raise_error(&ctr->err, (int64_t *)&ctr->err_pos, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT,
+                      pos);
+        } else if (std_bit((uint8_t)v)) {
+          mask |= std_bit((uint8_t)v);
+          const uint64_t key = ((uint64_t)(uint32_t)R.end[r] << 32) | (uint64_t)(r - tl.rb);
+          best = key < best ? key : best;
+        }
+      }
+    }
+    for (int d = 1; d < 64; d <<= 1) {
+      mask |= __shfl_xor(mask, d, 64);
+      const uint64_t o = __shfl_xor(best, d, 64);
+      best = o < best ? o : best;
+    }
+    const bool ambiguous = __popc(mask) > 1;
+    uint8_t refbase = 'N';
+    if (ambiguous) {
+      const int64_t rr = tl.rb + (int64_t)(best & 0xFFFFFFFFull);
+      const int v = md_ref_at(R, rr, pos);
+      refbase = (uint8_t)v;
+    } else if (mask) {
+      refbase = bit_base(mask);
+    }
+    // ---- pass 2: classify elements, group alleles per (sample, allele) in registers
+    uint64_t tlo[kSlots], thi[kSlots];
+    uint32_t tcnt[kSlots];
+    AlleleDesc tdesc[kSlots];
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      tlo[s] = thi[s] = 0;
+      tcnt[s] = 0;
+    }
+    int nt = 0;  // used slots (uniform)
+    bool overflow = false;
+    uint32_t sample_total[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
+      const int64_t r = r0 + lane;
+      bool act = r < tl.re && R.start[r] <= pos && pos < R.end[r];
+      AlleleDesc d;
+      Key128 key{0, 0};
+      int smp = 0;
+      if (act) {
+        int errc = 0;
+        if (!classify(R, r, pos, refbase, d, &errc)) {
+          raise_error(&ctr->err, (int64_t *)&ctr->err_pos, errc, pos);
+          act = false;
+        } else {
+          smp = R.sample[r] & 7;
+          key = allele_key(R, d, pos, smp);
+        }
+      }
+      // per-sample totals
+      for (int sm = 0; sm < 8; ++sm) {
+        const unsigned long long b = __ballot(act && smp == sm);
+        sample_total[sm] += (uint32_t)__popcll(b);
+      }
+      unsigned long long pending = __ballot(act);
+      while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint64_t klo = __shfl(key.lo, leader, 64), khi = __shfl(key.hi, leader, 64);
+        const bool match = act && key.lo == klo && key.hi == khi;
+        const unsigned long long mb = __ballot(match);
+        const uint32_t n = (uint32_t)__popcll(mb);
+        // find the key in the table
+        int found = -1;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+          const bool hit = (s * 64 + lane) < nt && tlo[s] == klo && thi[s] == khi;
+          const unsigned long long hb = __ballot(hit);
+          if (found < 0 && hb) found = s * 64 + (__ffsll((long long)hb) - 1);
+        }
+        if (found < 0) {
+          if (nt >= 64 * kSlots) {
+            overflow = true;
+          } else {
+            found = nt++;
+            // leader's descriptor -> owning lane of the slot
+            const int owner = found & 63, sl = found >> 6;
+            AlleleDesc ld;
+            ld.read = __shfl(d.read, leader, 64);
+            ld.aux = __shfl(d.aux, leader, 64);
+            ld.rp = __shfl(d.rp, leader, 64);
+            ld.kind = (uint8_t)__shfl((int)d.kind, leader, 64);
+            ld.rb = (uint8_t)__shfl((int)d.rb, leader, 64);
+            ld.base = (uint8_t)__shfl((int)d.base, leader, 64);
+            ld.pad = (uint8_t)smp;  // sample in pad
+            ld.pad = (uint8_t)__shfl((int)smp, leader, 64);
+#pragma unroll
+            for (int s = 0; s < kSlots; ++s)
+              if (s == sl && lane == owner) {
+                tlo[s] = klo;
+                thi[s] = khi;
+                tcnt[s] = 0;
+                tdesc[s] = ld;
+              }
+          }
+        }
+        if (found >= 0) {
+          const int owner = found & 63, sl = found >> 6;
+#pragma unroll
+          for (int s = 0; s < kSlots; ++s)
+            if (s == sl && lane == owner) tcnt[s] += n;
+        }
+        pending &= ~mb;
+      }
+    }
+    if (overflow) {
+      raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_CAPACITY, pos);
+      continue;
+    }
+    // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
+    const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
+    for (int sm = 0; sm < 8; ++sm) {
+      const uint32_t total = sample_total[sm];
+      if (total == 0) continue;
+      // select top-3 passing entries by (count desc, allele asc)
+      int top[3] = {-1, -1, -1};
+      uint32_t topc[3] = {0, 0, 0};
+      AlleleDesc topd[3];
+      int npass = 0;
+      for (int j = 0; j < nt; ++j) {
+        const int owner = j & 63, sl = j >> 6;
+        uint32_t cj = 0;
+        AlleleDesc dj;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+          if (s == sl) {
+            cj = (uint32_t)__shfl((int)tcnt[s], owner, 64);
+            dj.read = __shfl(tdesc[s].read, owner, 64);
+            dj.aux = __shfl(tdesc[s].aux, owner, 64);
+            dj.rp = __shfl(tdesc[s].rp, owner, 64);
+            dj.kind = (uint8_t)__shfl((int)tdesc[s].kind, owner, 64);
+            dj.rb = (uint8_t)__shfl((int)tdesc[s].rb, owner, 64);
+            dj.base = (uint8_t)__shfl((int)tdesc[s].base, owner, 64);
+            dj.pad = (uint8_t)__shfl((int)tdesc[s].pad, owner, 64);
+          }
+        if (dj.pad != sm) continue;
+        if ((long long)cj * 100 / (long long)total <= threshold) continue;
+        ++npass;
+        int p = npass - 1 < 3 ? npass - 1 : 3;
+        while (p > 0 && (topc[p - 1] < cj || (topc[p - 1] == cj && allele_cmp(R, dj, topd[p - 1], pos) < 0))) {
+          if (p < 3) {
+            top[p] = top[p - 1];
+            topc[p] = topc[p - 1];
+            topd[p] = topd[p - 1];
+          }
+          --p;
+        }
+        if (p < 3) {
+          top[p] = j;
+          topc[p] = cj;
+          topd[p] = dj;
+        }
+      }
+      const bool tie = npass >= 2 && (topc[0] == topc[1] || (npass >= 3 && topc[1] == topc[2]));
+      const uint8_t fl = (tie ? GQ_FLAG_TIE : 0) | (ambiguous ? GQ_FLAG_AMBIGUOUS_REF : 0);
+      if (lane == 0 && tie) atomicAdd(&ctr->ties, 1ull);
+      // emit helper: alleles from descriptors, or symbolic "<ALT>" with an explicit ref
+      auto emit = [&](const AlleleDesc *a, uint8_t sym_ref_kind, const AlleleDesc *ref_src, uint8_t g0, uint8_t g1,
+                      int sub) {
+        // sym_ref_kind: 0 => allele `a`; 1 => (refbase, <ALT>); 2 => (ref of ref_src, <ALT>)
+        int rl, al;
+        if (sym_ref_kind == 0) {
+          rl = allele_ref_len(*a);
+          al = allele_alt_len(*a);
+        } else if (sym_ref_kind == 1) {
+          rl = 1;
+          al = 5;
+        } else {
+          rl = allele_ref_len(*ref_src);
+          al = 5;
+        }
+        auto byte_at = [&](int which, int i) -> uint8_t {
+          if (sym_ref_kind == 0) return allele_byte(R, *a, pos, which, i);
+          if (which == 1) return (uint8_t)"<ALT>"[i];
+          if (sym_ref_kind == 1) return refbase;
+          return allele_byte(R, *ref_src, pos, 0, i);
+        };
+        CallRec rr;
+        rr.key = (ord << 12) | ((uint64_t)sm << 4) | (uint64_t)sub;
+        rr.contig = tl.contig;
+        rr.pos = pos;
+        rr.sample = (uint8_t)sm;
+        rr.gt0 = g0;
+        rr.gt1 = g1;
+        rr.flags = fl;
+        rr.ref_len = (uint16_t)rl;
+        rr.alt_len = (uint16_t)al;
+        if (rl + al <= 8) {
+          uint64_t v = 0;
+          int j = 0;
+          for (int i = 0; i < rl; ++i) v |= (uint64_t)byte_at(0, i) << (8 * j++);
+          for (int i = 0; i < al; ++i) v |= (uint64_t)byte_at(1, i) << (8 * j++);
+          rr.allele = v;
+        } else {
+          unsigned long long off = 0;
+          if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + al));
+          off = __shfl(off, 0, 64);
+          if (off + rl + al <= pool_cap) {
+            for (int i = lane; i < rl + al; i += 64)
+              pool[off + i] = i < rl ? byte_at(0, i) : byte_at(1, i - rl);
+          }
+          rr.allele = off;
+        }
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
+          if (k < rec_cap) recs[k] = rr;
+        }
+      };
+      if (npass == 0) {
+        if (emit_no_call) emit(nullptr, 1, nullptr, GQ_GT_NOCALL, GQ_GT_NOCALL, 0);
+      } else {
+        auto isvar = [&](const AlleleDesc &a) {  // Allele.isVariant: refBases != altBases
+          const int rl = allele_ref_len(a), al = allele_alt_len(a);
+          if (rl != al) return true;
+          for (int i = 0; i < rl; ++i)
+            if (allele_byte(R, a, pos, 0, i) != allele_byte(R, a, pos, 1, i)) return true;
+          return false;
+        };
+        const bool v1 = isvar(topd[0]);
+        if (npass == 1 && !v1) {
+          if (emit_ref) emit(nullptr, 1, nullptr, GQ_GT_REF, GQ_GT_REF, 0);
+        } else if (npass == 1) {
+          emit(&topd[0], 0, nullptr, GQ_GT_ALT, GQ_GT_ALT, 0);
+        } else {
+          const bool v2 = isvar(topd[1]);
+          const bool e1 = allele_alt_len(topd[0]) == 0, e2 = allele_alt_len(topd[1]) == 0;
+          if ((!v1 || !v2) && (e1 != e2)) {
+            // heterozygous deletion: no call (GermlineThresholdCaller.scala:146-149)
+          } else if (v1 != v2) {
+            emit(v1 ? &topd[0] : &topd[1], 0, nullptr, GQ_GT_REF, GQ_GT_ALT, 0);
+          } else if (v1 && v2) {
+            emit(&topd[0], 0, nullptr, GQ_GT_ALT, GQ_GT_OTHERALT, 0);
+            emit(&topd[1], 0, nullptr, GQ_GT_ALT, GQ_GT_OTHERALT, 1);
+          } else {
+            const bool n1 = allele_ref_len(topd[0]) == 1 && allele_byte(R, topd[0], pos, 0, 0) == 'N';
+            const bool n2 = allele_ref_len(topd[1]) == 1 && allele_byte(R, topd[1], pos, 0, 0) == 'N';
+            if (n1 || n2) emit(nullptr, 2, n1 ? &topd[1] : &topd[0], GQ_GT_REF, GQ_GT_REF, 0);
+            else raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_MULTI_REF, pos);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// counts_tile: dense raw histogram (gq_pileup_counts)
+// ------------------------------------------------------------------------------------------
+enum : int { K2_A = 0, K2_C, K2_G, K2_T, K2_N, K2_O, K2_INS, K2_DEL, K2_MID, K2_CLIP, K2_POS, K2_MASK, K2_EVA, K2_EVC,
+             K2_EVG, K2_EVT, K2_NCAT };
+
+template <int T>
+struct CountSink {
+  uint32_t *cnt;
+  int32_t L0;
+  int *err;
+  long long *err_pos;
+  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
+    const int i = l - L0;
+    int c;
+    switch (kind) {
+      case K_SNV: c = base_cat(base); break;
+      case K_INS: c = K2_INS; break;
+      case K_DEL: c = K2_DEL; break;
+      case K_MID: c = K2_MID; break;
+      default: c = K2_CLIP; break;
+    }
+    atomicAdd(&cnt[c * T + i], 1u);
+    if (!(fl & 1)) atomicAdd(&cnt[K2_POS * T + i], 1u);
+    const uint32_t b = std_bit(mdb);
+    if (kind == K_SNV && !ev) return;  // mask derived from base counts below
+    if (kind == K_SNV && ev) {
+      const int bc = base_cat(base);
+      if (bc < 4) atomicAdd(&cnt[(K2_EVA + bc) * T + i], 1u);
+    }
+    if (b) atomicOr(&cnt[K2_MASK * T + i], b);
+  }
+  __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
+};
+
+template <int T>
+__global__ __launch_bounds__(kBlock) void counts_tile(const Tile *__restrict__ tiles, DevReads R,
+                                                      int32_t *__restrict__ depth, int32_t *__restrict__ pos_depth,
+                                                      int32_t *__restrict__ base_counts,
+                                                      int32_t *__restrict__ indel_counts,
+                                                      int32_t *__restrict__ ref_depth, uint8_t *__restrict__ ref_base,
+                                                      uint8_t *__restrict__ ambiguous, Counters *ctr) {
+  __shared__ uint32_t cnt[K2_NCAT * T];
+  const Tile tl = tiles[blockIdx.x];
+  const int32_t L0 = tl.L0, L1 = tl.L1;
+  for (int i = threadIdx.x; i < K2_NCAT * T; i += blockDim.x) cnt[i] = 0u;
+  __syncthreads();
+  CountSink<T> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int64_t r = tl.rb + wave; r < tl.re; r += (blockDim.x >> 6)) walk_read(R, r, L0, L1, sink);
+  __syncthreads();
+  for (int i = threadIdx.x; i < L1 - L0; i += blockDim.x) {
+    const int64_t o = tl.ordinal0 + i;
+    uint32_t dsum = 0;
+    for (int k = 0; k <= K2_CLIP; ++k) dsum += cnt[k * T + i];
+    uint32_t mask = cnt[K2_MASK * T + i];
+    for (int k = 0; k < 4; ++k)
+      if (cnt[k * T + i] > cnt[(K2_EVA + k) * T + i]) mask |= 1u << k;
+    const uint8_t rb = mask ? bit_base(mask) : (uint8_t)'N';
+    depth[o] = (int32_t)dsum;
+    pos_depth[o] = (int32_t)cnt[K2_POS * T + i];
+    for (int k = 0; k < 6; ++k) base_counts[o * 6 + k] = (int32_t)cnt[k * T + i];
+    for (int k = 0; k < 4; ++k) indel_counts[o * 4 + k] = (int32_t)cnt[(K2_INS + k) * T + i];
+    ref_depth[o] = (int32_t)cnt[base_cat(rb) * T + i];
+    ref_base[o] = rb;
+    ambiguous[o] = __popc(mask) > 1 ? 1 : 0;
+  }
+}
+
+}  // namespace
+
+// ==========================================================================================
+// Host side: context, resident read sets, entry points
+// ==========================================================================================
+struct DevBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t want = std::max(bytes, (size_t)256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct gq_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  gq_timings timings{};
+  int germ_tile = kGermT;
+  DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp;
+  DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb;
+};
+
+struct gq_dev_reads {
+  gq_ctx *ctx = nullptr;
+  DevReads d{};
+  std::vector<int64_t> contig_read_begin;  // host copy
+  std::vector<void *> owned;               // device allocations owned by this handle
+  int64_t seq_bytes = 0;
+};
+
+extern "C" {
+
+const char *gq_version(void) { return "guacamole-amd gqpileup 0.1 (gfx950)"; }
+const char *gq_last_error(void) { return g_err.c_str(); }
+
+gq_status gq_open(int device, gq_ctx **out) {
+  if (!out) return set_err(GQ_E_ARG, "gq_open: null out");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return set_err(GQ_E_ARG, "gq_open: device %d out of range (%d devices)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  gq_ctx *c = new gq_ctx();
+  c->device = device;
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  *out = c;
+  return GQ_OK;
+}
+
+void gq_close(gq_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
+                    &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->c_depth, &c->c_pos,
+                    &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb})
+    b->release();
+  for (auto &e : c->ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+gq_status gq_get_timings(const gq_ctx *c, gq_timings *out) {
+  if (!c || !out) return set_err(GQ_E_ARG, "gq_get_timings: null argument");
+  *out = c->timings;
+  return GQ_OK;
+}
+
+gq_status gq_set_tile(gq_ctx *c, int32_t t) {
+  if (!c) return set_err(GQ_E_ARG, "null ctx");
+  if (t == 0) t = kGermT;
+  if (t != 512 && t != 1024 && t != 2048) return set_err(GQ_E_ARG, "tile must be 512, 1024 or 2048");
+  c->germ_tile = t;
+  return GQ_OK;
+}
+
+static gq_status validate_reads(const gq_reads *h) {
+  if (!h) return set_err(GQ_E_ARG, "null read set");
+  if (h->n_reads < 0 || h->n_contigs <= 0) return set_err(GQ_E_ARG, "bad read-set sizes");
+  if (h->n_samples < 1 || h->n_samples > 8) return set_err(GQ_E_ARG, "n_samples must be in [1, 8]");
+  return GQ_OK;
+}
+
+gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
+  if (!c || !out) return set_err(GQ_E_ARG, "gq_reads_upload: null argument");
+  gq_status st = validate_reads(h);
+  if (st) return st;
+  HIP_TRY(hipSetDevice(c->device));
+  gq_dev_reads *d = new gq_dev_reads();
+  d->ctx = c;
+  const int64_t n = h->n_reads;
+  auto up = [&](const void *src, size_t bytes, void **dst) -> hipError_t {
+    *dst = nullptr;
+    hipError_t e = hipMalloc(dst, std::max(bytes, (size_t)16));
+    if (e != hipSuccess) return e;
+    d->owned.push_back(*dst);
+    if (bytes) e = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    return e;
+  };
+  void *p;
+#define UP(field, count, T)                                                     \
+  do {                                                                          \
+    hipError_t _e = up(h->field, (size_t)(count) * sizeof(T), &p);              \
+    if (_e != hipSuccess) {                                                     \
+      gq_reads_free(d);                                                         \
+      return set_err(GQ_E_HIP, "upload %s: %s", #field, hipGetErrorString(_e)); \
+    }                                                                           \
+    d->d.field = (const T *)p;                                                  \
+  } while (0)
+  UP(contig_read_begin, h->n_contigs + 1, int64_t);
+  UP(start, n, int32_t);
+  UP(end, n, int32_t);
+  UP(pmax_end, n, int32_t);
+  UP(mapq, n, uint8_t);
+  UP(flags, n, uint8_t);
+  UP(sample, n, uint8_t);
+  UP(seq_off, n, int64_t);
+  UP(seq_len, n, int32_t);
+  UP(cigar_off, n, int64_t);
+  UP(n_cigar, n, int32_t);
+  UP(md_off, n, int64_t);
+  UP(n_md, n, int32_t);
+  UP(n_mismatch, n, uint16_t);
+  UP(seq, h->seq_bytes, uint8_t);
+  UP(qual, h->seq_bytes, uint8_t);
+  UP(cigar, h->cigar_len, uint32_t);
+  UP(md_ev, h->md_len, uint32_t);
+#undef UP
+  d->d.n_reads = n;
+  d->d.n_contigs = h->n_contigs;
+  d->d.n_samples = h->n_samples;
+  d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
+  d->seq_bytes = h->seq_bytes;
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    gq_reads_free(d);
+    return set_err(GQ_E_HIP, "upload sync: %s", hipGetErrorString(e));
+  }
+  *out = d;
+  return GQ_OK;
+}
+
+gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
+  if (!c || !out) return set_err(GQ_E_ARG, "gq_reads_wrap_device: null argument");
+  gq_status st = validate_reads(h);
+  if (st) return st;
+  gq_dev_reads *d = new gq_dev_reads();
+  d->ctx = c;
+  d->d.n_reads = h->n_reads;
+  d->d.n_contigs = h->n_contigs;
+  d->d.n_samples = h->n_samples;
+  d->d.contig_read_begin = h->contig_read_begin;
+  d->d.start = h->start;
+  d->d.end = h->end;
+  d->d.pmax_end = h->pmax_end;
+  d->d.mapq = h->mapq;
+  d->d.flags = h->flags;
+  d->d.sample = h->sample;
+  d->d.seq_off = h->seq_off;
+  d->d.seq_len = h->seq_len;
+  d->d.cigar_off = h->cigar_off;
+  d->d.n_cigar = h->n_cigar;
+  d->d.md_off = h->md_off;
+  d->d.n_md = h->n_md;
+  d->d.n_mismatch = h->n_mismatch;
+  d->d.seq = h->seq;
+  d->d.qual = h->qual;
+  d->d.cigar = h->cigar;
+  d->d.md_ev = h->md_ev;
+  d->contig_read_begin.resize((size_t)h->n_contigs + 1);
+  hipError_t e = hipMemcpy(d->contig_read_begin.data(), h->contig_read_begin,
+                           sizeof(int64_t) * ((size_t)h->n_contigs + 1), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    delete d;
+    return set_err(GQ_E_HIP, "wrap: contig_read_begin D2H: %s", hipGetErrorString(e));
+  }
+  d->seq_bytes = h->seq_bytes;
+  *out = d;
+  return GQ_OK;
+}
+
+void gq_reads_free(gq_dev_reads *d) {
+  if (!d) return;
+  for (void *p : d->owned) (void)hipFree(p);
+  delete d;
+}
+
+// ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
+struct Plan {
+  int64_t n_tiles = 0;
+  int64_t n_loci = 0;
+};
+
+static gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl) {
+  if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
+  const int64_t R = loci->n_ranges;
+  std::vector<int32_t> rc;
+  std::vector<int64_t> rs, re, ro, rt;
+  int64_t ord = 0, tiles = 0;
+  for (int64_t i = 0; i < R; ++i) {
+    const int32_t cc = loci->contig[i];
+    const int64_t s = loci->start[i], e = loci->end[i];
+    if (cc < 0 || cc >= rd->d.n_contigs) return set_err(GQ_E_ARG, "loci range %lld: contig %d out of range", (long long)i, cc);
+    if (s < 0 || e < s || e > INT32_MAX) return set_err(GQ_E_ARG, "loci range %lld: bad interval", (long long)i);
+    if (e == s) continue;
+    rc.push_back(cc);
+    rs.push_back(s);
+    re.push_back(e);
+    ro.push_back(ord);
+    rt.push_back(tiles);
+    ord += e - s;
+    tiles += (e - s + T - 1) / T;
+  }
+  pl.n_tiles = tiles;
+  pl.n_loci = ord;
+  if (tiles == 0) return GQ_OK;
+  const size_t nr = rc.size();
+  HIP_TRY(c->ranges.ensure(nr * (4 + 8 * 4) + 64));
+  char *base = (char *)c->ranges.p;
+  int32_t *d_rc = (int32_t *)base;
+  int64_t *d_rs = (int64_t *)(base + ((nr * 4 + 15) & ~(size_t)15));
+  int64_t *d_re = d_rs + nr, *d_ro = d_re + nr, *d_rt = d_ro + nr;
+  HIP_TRY(c->ranges.ensure((size_t)((char *)(d_rt + nr) - base)));
+  HIP_TRY(hipMemcpyAsync(d_rc, rc.data(), nr * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_rs, rs.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_re, re.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_ro, ro.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_rt, rt.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c->tiles.ensure((size_t)tiles * sizeof(Tile)));
+  const int nb = (int)((tiles + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
+                     tiles, T, rd->d, (Tile *)c->tiles.p);
+  HIP_TRY(hipGetLastError());
+  return GQ_OK;
+}
+
+static gq_status check_device_error(gq_ctx *c, const Counters &h) {
+  if (h.err) {
+    static const char *names[] = {"ok", "assertion", "invalid cigar element", "CIGAR / MD tag mismatch",
+                                  "read without MD tag", "multiple reference bases", "unsorted", "argument", "hip",
+                                  "nomem", "allele table capacity"};
+    const char *nm = (h.err >= 0 && h.err <= 10) ? names[h.err] : "?";
+    return set_err((gq_status)h.err, "device error: %s near position %lld", nm, (long long)h.err_pos);
+  }
+  return GQ_OK;
+}
+
+extern "C++" template <int T>
+static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p, CallRec *recs,
+                            unsigned long long rec_cap, ComplexItem *cplx, unsigned long long cplx_cap,
+                            Counters *ctr) {
+  hipLaunchKernelGGL((germline_tile<T>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                     R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, cplx_cap, ctr);
+}
+
+gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,
+                                const gq_germline_params *p, gq_calls **out) {
+  if (!c || !rd || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_germline_threshold: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const int T = c->germ_tile;
+  c->timings = gq_timings{};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  Plan pl;
+  gq_status st = plan(c, rd, loci, T, pl);
+  if (st) return st;
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
+  if (!res) return set_err(GQ_E_NOMEM, "calloc");
+  if (pl.n_tiles == 0) {
+    *out = res;
+    return GQ_OK;
+  }
+  const int ns = rd->d.n_samples;
+  unsigned long long rec_cap = (p->emit_ref || p->emit_no_call) ? (unsigned long long)(2 * ns) * pl.n_loci + 1024
+                                                                 : std::max<unsigned long long>(1 << 16, pl.n_loci / 8);
+  unsigned long long cplx_cap = std::max<unsigned long long>(1 << 16, pl.n_loci / 8);
+  unsigned long long pool_cap = 1 << 22;
+  Counters hc{};
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c->recs.ensure(rec_cap * sizeof(CallRec)));
+    HIP_TRY(c->cplx.ensure(cplx_cap * sizeof(ComplexItem)));
+    HIP_TRY(c->pool.ensure(pool_cap));
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    Counters *ctr = (Counters *)c->counters.p;
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+    if (attempt == 0) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    switch (T) {
+      case 512: launch_germline<512>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
+      case 2048: launch_germline<2048>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
+      default: launch_germline<1024>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), 4096);
+    hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                       (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
+                       (CallRec *)c->recs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, ctr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bool retry = false;
+    if (hc.n_complex > cplx_cap) {
+      cplx_cap = hc.n_complex + 1024;
+      retry = true;
+    }
+    if (hc.n_rec > rec_cap) {
+      rec_cap = hc.n_rec + 1024;
+      retry = true;
+    }
+    if (hc.pool_used > pool_cap) {
+      pool_cap = hc.pool_used + 4096;
+      retry = true;
+    }
+    if (!retry) break;
+    if (attempt == 2) {
+      free(res);
+      return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
+    }
+  }
+  st = check_device_error(c, hc);
+  if (st) {
+    free(res);
+    return st;
+  }
+  // ---- sort records by key (output order) on device
+  const int64_t n = (int64_t)hc.n_rec;
+  HIP_TRY(c->keys.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  HIP_TRY(c->keys_sorted.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+  HIP_TRY(c->idx.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+  HIP_TRY(c->idx_sorted.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+  std::vector<CallRec> hrec((size_t)n);
+  std::vector<int32_t> order((size_t)n);
+  if (n > 0) {
+    // keys are the first 8 bytes of each record: strided copy into a dense key array
+    HIP_TRY(hipMemcpy2DAsync(c->keys.p, 8, c->recs.p, sizeof(CallRec), 8, (size_t)n, hipMemcpyDeviceToDevice,
+                             c->stream));
+    {
+      std::vector<int32_t> iota((size_t)n);
+      for (int64_t i = 0; i < n; ++i) iota[(size_t)i] = (int32_t)i;
+      HIP_TRY(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    int end_bit = 12;
+    while (end_bit < 64 && ((uint64_t)pl.n_loci >> (end_bit - 12)) != 0) ++end_bit;
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t *)c->keys.p, (uint64_t *)c->keys_sorted.p,
+                                               (const int32_t *)c->idx.p, (int32_t *)c->idx_sorted.p, (int)n, 0,
+                                               end_bit, c->stream));
+    HIP_TRY(c->sort_tmp.ensure(tmp));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (const uint64_t *)c->keys.p,
+                                               (uint64_t *)c->keys_sorted.p, (const int32_t *)c->idx.p,
+                                               (int32_t *)c->idx_sorted.p, (int)n, 0, end_bit, c->stream));
+    HIP_TRY(hipMemcpyAsync(hrec.data(), c->recs.p, (size_t)n * sizeof(CallRec), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(order.data(), c->idx_sorted.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  if (!hpool.empty())
+    HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  // ---- marshal into the result struct (output order)
+  res->n = n;
+  res->contig = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
+  res->pos = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
+  res->sample = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
+  res->gt0 = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
+  res->gt1 = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
+  res->flags = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
+  res->ref_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
+  res->alt_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
+  res->ref_len = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
+  res->alt_len = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
+  std::vector<uint8_t> apool;
+  apool.reserve((size_t)n * 3 + 16);
+  for (int64_t k = 0; k < n; ++k) {
+    const CallRec &r = hrec[(size_t)order[(size_t)k]];
+    res->contig[k] = r.contig;
+    res->pos[k] = r.pos;
+    res->sample[k] = r.sample;
+    res->gt0[k] = r.gt0;
+    res->gt1[k] = r.gt1;
+    res->flags[k] = r.flags;
+    res->ref_len[k] = r.ref_len;
+    res->alt_len[k] = r.alt_len;
+    res->ref_off[k] = (int64_t)apool.size();
+    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
+    if (r.ref_len + r.alt_len <= 8) {
+      for (int i = 0; i < r.ref_len + r.alt_len; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
+    } else {
+      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele,
+                   hpool.begin() + (ptrdiff_t)(r.allele + r.ref_len + r.alt_len));
+    }
+  }
+  res->pool_len = (int64_t)apool.size();
+  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
+  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  res->visited_loci = (int64_t)hc.visited;
+  res->complex_loci = (int64_t)hc.n_complex;
+  res->ambiguous_loci = (int64_t)hc.ambiguous;
+  res->tie_loci = (int64_t)hc.ties;
+  // timings
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+  c->timings.plan_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timings.pileup_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+  c->timings.complex_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[3], c->ev[4]);
+  c->timings.finalize_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[4]);
+  c->timings.total_ms = ms;
+  c->timings.pileup_launches = 1;
+  c->timings.tiles = pl.n_tiles;
+  *out = res;
+  return GQ_OK;
+}
+
+void gq_free_calls(gq_calls *r) {
+  if (!r) return;
+  free(r->contig);
+  free(r->pos);
+  free(r->sample);
+  free(r->gt0);
+  free(r->gt1);
+  free(r->flags);
+  free(r->ref_off);
+  free(r->alt_off);
+  free(r->ref_len);
+  free(r->alt_len);
+  free(r->allele_pool);
+  free(r);
+}
+
+gq_status gq_pileup_counts(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, gq_counts **out) {
+  if (!c || !rd || !loci || !out) return set_err(GQ_E_ARG, "gq_pileup_counts: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  Plan pl;
+  gq_status st = plan(c, rd, loci, kCountT, pl);
+  if (st) return st;
+  gq_counts *res = (gq_counts *)calloc(1, sizeof(gq_counts));
+  const int64_t n = pl.n_loci;
+  res->n_loci = n;
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  res->depth = (int32_t *)malloc(nn * 4);
+  res->pos_depth = (int32_t *)malloc(nn * 4);
+  res->base_counts = (int32_t *)malloc(nn * 24);
+  res->indel_counts = (int32_t *)malloc(nn * 16);
+  res->ref_depth = (int32_t *)malloc(nn * 4);
+  res->ref_base = (uint8_t *)malloc(nn);
+  res->ambiguous = (uint8_t *)malloc(nn);
+  if (n == 0) {
+    *out = res;
+    return GQ_OK;
+  }
+  HIP_TRY(c->c_depth.ensure(nn * 4));
+  HIP_TRY(c->c_pos.ensure(nn * 4));
+  HIP_TRY(c->c_base.ensure(nn * 24));
+  HIP_TRY(c->c_indel.ensure(nn * 16));
+  HIP_TRY(c->c_ref.ensure(nn * 4));
+  HIP_TRY(c->c_rb.ensure(nn));
+  HIP_TRY(c->c_amb.ensure(nn));
+  HIP_TRY(c->counters.ensure(sizeof(Counters)));
+  Counters *ctr = (Counters *)c->counters.p;
+  HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+  hipLaunchKernelGGL((counts_tile<kCountT>), dim3((unsigned)pl.n_tiles), dim3(kBlock), 0, c->stream,
+                     (const Tile *)c->tiles.p, rd->d, (int32_t *)c->c_depth.p, (int32_t *)c->c_pos.p,
+                     (int32_t *)c->c_base.p, (int32_t *)c->c_indel.p, (int32_t *)c->c_ref.p, (uint8_t *)c->c_rb.p,
+                     (uint8_t *)c->c_amb.p, ctr);
+  HIP_TRY(hipGetLastError());
+  Counters hc{};
+  HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->depth, c->c_depth.p, nn * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->pos_depth, c->c_pos.p, nn * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->base_counts, c->c_base.p, nn * 24, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->indel_counts, c->c_indel.p, nn * 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->ref_depth, c->c_ref.p, nn * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->ref_base, c->c_rb.p, nn, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(res->ambiguous, c->c_amb.p, nn, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  st = check_device_error(c, hc);
+  if (st) {
+    gq_free_counts(res);
+    return st;
+  }
+  *out = res;
+  return GQ_OK;
+}
+
+void gq_free_counts(gq_counts *r) {
+  if (!r) return;
+  free(r->depth);
+  free(r->pos_depth);
+  free(r->base_counts);
+  free(r->indel_counts);
+  free(r->ref_depth);
+  free(r->ref_base);
+  free(r->ambiguous);
+  free(r);
+}
+
+gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_reads *n, const gq_loci *loci,
+                              const gq_somatic_params *p, gq_somatic_calls **out) {
+  (void)c; (void)t; (void)n; (void)loci; (void)p; (void)out;
+  return set_err(GQ_E_ARG, "gq_somatic_standard: not built in this revision");
+}
+
+void gq_free_somatic(gq_somatic_calls *r) { free(r); }
+
+}  // extern "C"

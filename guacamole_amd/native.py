@@ -1,0 +1,267 @@
+"""ctypes binding of libgqpileup.so (include/gqpileup.h).
+
+The HIP library is the only compute path: if it is missing or the GPU cannot be
+opened, every entry point raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libgqpileup.so")
+_lib = None
+
+GT_NAMES = {0: "Ref", 1: "Alt", 2: "OtherAlt", 3: "NoCall"}
+FLAG_AMBIGUOUS_REF = 1
+FLAG_TIE = 2
+
+
+class GQError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("gqpileup error %d: %s" % (code, msg))
+        self.code = code
+
+
+class gq_reads(C.Structure):
+    _fields_ = [("n_reads", C.c_int64), ("n_contigs", C.c_int32), ("n_samples", C.c_int32)] + [
+        (n, C.c_void_p) for n in ("contig_read_begin", "start", "end", "pmax_end", "mapq", "flags", "sample",
+                                  "seq_off", "seq_len", "cigar_off", "n_cigar", "md_off", "n_md", "n_mismatch")] + [
+        ("seq_bytes", C.c_int64), ("cigar_len", C.c_int64), ("md_len", C.c_int64)] + [
+        (n, C.c_void_p) for n in ("seq", "qual", "cigar", "md_ev")]
+
+
+class gq_loci(C.Structure):
+    _fields_ = [("n_ranges", C.c_int64), ("contig", C.c_void_p), ("start", C.c_void_p), ("end", C.c_void_p),
+                ("task", C.c_void_p)]
+
+
+class gq_germline_params(C.Structure):
+    _fields_ = [("threshold", C.c_int32), ("emit_ref", C.c_int32), ("emit_no_call", C.c_int32)]
+
+
+class gq_calls(C.Structure):
+    _fields_ = [("n", C.c_int64), ("contig", C.POINTER(C.c_int32)), ("pos", C.POINTER(C.c_int64)),
+                ("sample", C.POINTER(C.c_uint8)), ("gt0", C.POINTER(C.c_uint8)), ("gt1", C.POINTER(C.c_uint8)),
+                ("flags", C.POINTER(C.c_uint8)), ("ref_off", C.POINTER(C.c_int64)), ("ref_len", C.POINTER(C.c_int32)),
+                ("alt_off", C.POINTER(C.c_int64)), ("alt_len", C.POINTER(C.c_int32)),
+                ("allele_pool", C.POINTER(C.c_uint8)), ("pool_len", C.c_int64), ("visited_loci", C.c_int64),
+                ("complex_loci", C.c_int64), ("ambiguous_loci", C.c_int64), ("tie_loci", C.c_int64)]
+
+
+class gq_counts(C.Structure):
+    _fields_ = [("n_loci", C.c_int64), ("depth", C.POINTER(C.c_int32)), ("pos_depth", C.POINTER(C.c_int32)),
+                ("base_counts", C.POINTER(C.c_int32)), ("indel_counts", C.POINTER(C.c_int32)),
+                ("ref_depth", C.POINTER(C.c_int32)), ("ref_base", C.POINTER(C.c_uint8)),
+                ("ambiguous", C.POINTER(C.c_uint8))]
+
+
+class gq_timings(C.Structure):
+    _fields_ = [("plan_ms", C.c_float), ("pileup_ms", C.c_float), ("complex_ms", C.c_float),
+                ("finalize_ms", C.c_float), ("total_ms", C.c_float), ("pileup_launches", C.c_int64),
+                ("tiles", C.c_int64)]
+
+
+class gq_somatic_params(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "odds", "min_mapq", "filter_multi_allelic", "max_read_depth", "min_tumor_read_depth",
+        "max_tumor_read_depth", "min_normal_read_depth", "min_tumor_alternate_read_depth", "min_lod",
+        "min_likelihood", "min_vaf", "min_average_mapping_quality", "min_average_base_quality",
+        "max_median_mismatches", "apply_filters")]
+
+
+class gq_evidence(C.Structure):
+    _fields_ = [("likelihood", C.c_double), ("read_depth", C.c_int32), ("allele_read_depth", C.c_int32),
+                ("forward_depth", C.c_int32), ("allele_forward_depth", C.c_int32), ("mean_mq", C.c_double),
+                ("median_mq", C.c_double), ("mean_bq", C.c_double), ("median_bq", C.c_double),
+                ("median_mismatches", C.c_double)]
+
+
+class gq_somatic_calls(C.Structure):
+    _fields_ = [("n", C.c_int64), ("contig", C.POINTER(C.c_int32)), ("pos", C.POINTER(C.c_int64)),
+                ("sample", C.POINTER(C.c_uint8)), ("ref_off", C.POINTER(C.c_int64)), ("ref_len", C.POINTER(C.c_int32)),
+                ("alt_off", C.POINTER(C.c_int64)), ("alt_len", C.POINTER(C.c_int32)),
+                ("allele_pool", C.POINTER(C.c_uint8)), ("pool_len", C.c_int64), ("log_odds", C.POINTER(C.c_double)),
+                ("gq", C.POINTER(C.c_int32)), ("tumor", C.POINTER(gq_evidence)), ("normal", C.POINTER(gq_evidence)),
+                ("flags", C.POINTER(C.c_uint8)), ("visited_loci", C.c_int64), ("candidate_loci", C.c_int64)]
+
+
+EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
+            "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_free_calls", "gq_pileup_counts",
+            "gq_free_counts", "gq_somatic_standard", "gq_free_somatic")
+
+
+def lib():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libgqpileup.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        L.gq_version.restype = C.c_char_p
+        L.gq_last_error.restype = C.c_char_p
+        for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device",
+                  "gq_germline_threshold", "gq_pileup_counts", "gq_somatic_standard"):
+            getattr(L, f).restype = C.c_int
+        L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
+                                            C.POINTER(C.POINTER(gq_calls))]
+        L.gq_pileup_counts.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(C.POINTER(gq_counts))]
+        L.gq_somatic_standard.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
+                                          C.POINTER(gq_somatic_params), C.POINTER(C.POINTER(gq_somatic_calls))]
+        L.gq_free_calls.argtypes = [C.POINTER(gq_calls)]
+        L.gq_free_counts.argtypes = [C.POINTER(gq_counts)]
+        L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
+        L.gq_reads_free.argtypes = [C.c_void_p]
+        L.gq_close.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise GQError(rc, lib().gq_last_error().decode())
+
+
+def _ptr(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data if a.size else 0
+    return int(a.data_ptr())  # torch tensor already in device memory
+
+
+def make_gq_reads(arrs: Dict[str, object]) -> Tuple[gq_reads, list]:
+    """gq_reads over numpy (host) or torch (device) arrays from soa.pack/assemble."""
+    keep = [arrs[k] for k in arrs]
+    n = int(arrs["start"].shape[0])
+    s = gq_reads(n, int(arrs["n_contigs"]), int(arrs["n_samples"]),
+                 *[_ptr(arrs[k]) for k in ("contig_read_begin", "start", "end", "pmax_end", "mapq", "flags",
+                                           "sample", "seq_off", "seq_len", "cigar_off", "n_cigar", "md_off", "n_md",
+                                           "n_mismatch")],
+                 int(arrs["seq"].shape[0]), int(arrs["cigar"].shape[0]), int(arrs["md_ev"].shape[0]),
+                 *[_ptr(arrs[k]) for k in ("seq", "qual", "cigar", "md_ev")])
+    return s, keep
+
+
+def make_gq_loci(contig, start, end, task) -> Tuple[gq_loci, list]:
+    keep = [np.ascontiguousarray(contig, np.int32), np.ascontiguousarray(start, np.int64),
+            np.ascontiguousarray(end, np.int64), np.ascontiguousarray(task, np.int64)]
+    return gq_loci(len(keep[0]), *[_ptr(a) for a in keep]), keep
+
+
+class Context:
+    """One gq_ctx per GPU (gq_open / gq_close)."""
+
+    def __init__(self, device: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().gq_open(int(device), C.byref(self.h)))
+        self.device = device
+
+    def close(self) -> None:
+        if self.h:
+            lib().gq_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_tile(self, t: int) -> None:
+        _check(lib().gq_set_tile(self.h, int(t)))
+
+    def timings(self) -> Dict[str, float]:
+        t = gq_timings()
+        _check(lib().gq_get_timings(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in gq_timings._fields_}
+
+    def upload(self, arrs: Dict[str, object]) -> "DeviceReads":
+        s, keep = make_gq_reads(arrs)
+        h = C.c_void_p()
+        _check(lib().gq_reads_upload(self.h, C.byref(s), C.byref(h)))
+        return DeviceReads(self, h, None)
+
+    def wrap_device(self, arrs: Dict[str, object]) -> "DeviceReads":
+        s, keep = make_gq_reads(arrs)
+        h = C.c_void_p()
+        _check(lib().gq_reads_wrap_device(self.h, C.byref(s), C.byref(h)))
+        return DeviceReads(self, h, keep)
+
+    def germline_threshold(self, reads: "DeviceReads", loci, threshold: int = 8, emit_ref: bool = False,
+                           emit_no_call: bool = False) -> "GermlineCalls":
+        L, keep = make_gq_loci(*loci)
+        p = gq_germline_params(int(threshold), int(bool(emit_ref)), int(bool(emit_no_call)))
+        out = C.POINTER(gq_calls)()
+        _check(lib().gq_germline_threshold(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
+        try:
+            return GermlineCalls.from_struct(out.contents)
+        finally:
+            lib().gq_free_calls(out)
+
+    def pileup_counts(self, reads: "DeviceReads", loci) -> Dict[str, np.ndarray]:
+        L, keep = make_gq_loci(*loci)
+        out = C.POINTER(gq_counts)()
+        _check(lib().gq_pileup_counts(self.h, reads.h, C.byref(L), C.byref(out)))
+        try:
+            c = out.contents
+            n = c.n_loci
+
+            def arr(p, k=1):
+                return np.ctypeslib.as_array(p, shape=(n * k,)).copy() if n else np.zeros(0)
+
+            return dict(depth=arr(c.depth), pos_depth=arr(c.pos_depth), base_counts=arr(c.base_counts, 6).reshape(-1, 6),
+                        indel_counts=arr(c.indel_counts, 4).reshape(-1, 4), ref_depth=arr(c.ref_depth),
+                        ref_base=arr(c.ref_base), ambiguous=arr(c.ambiguous))
+        finally:
+            lib().gq_free_counts(out)
+
+
+class DeviceReads:
+    def __init__(self, ctx: Context, h, keep):
+        self.ctx, self.h, self.keep = ctx, h, keep
+
+    def free(self) -> None:
+        if self.h:
+            lib().gq_reads_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class GermlineCalls:
+    """Germline genotype records in output order."""
+
+    def __init__(self, contig, pos, sample, gt0, gt1, flags, ref, alt, visited, complex_loci, ambiguous, ties):
+        self.contig, self.pos, self.sample = contig, pos, sample
+        self.gt0, self.gt1, self.flags = gt0, gt1, flags
+        self.ref, self.alt = ref, alt
+        self.visited_loci, self.complex_loci, self.ambiguous_loci, self.tie_loci = visited, complex_loci, ambiguous, ties
+
+    @staticmethod
+    def from_struct(c: gq_calls) -> "GermlineCalls":
+        n = c.n
+
+        def arr(p):
+            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+
+        pool = bytes(np.ctypeslib.as_array(c.allele_pool, shape=(c.pool_len,))) if c.pool_len else b""
+        ro, rl, ao, al = arr(c.ref_off), arr(c.ref_len), arr(c.alt_off), arr(c.alt_len)
+        ref = [pool[ro[i]:ro[i] + rl[i]].decode("latin-1") for i in range(n)]
+        alt = [pool[ao[i]:ao[i] + al[i]].decode("latin-1") for i in range(n)]
+        return GermlineCalls(arr(c.contig), arr(c.pos), arr(c.sample), arr(c.gt0), arr(c.gt1), arr(c.flags), ref, alt,
+                             c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
+
+    def __len__(self) -> int:
+        return len(self.ref)
+
+    def tuples(self, contig_names: Sequence[str]) -> List[tuple]:
+        """(contig, locus, sample, (gt0, gt1), ref, alt, flags) — same shape as the oracle's rows."""
+        return [(contig_names[self.contig[i]], int(self.pos[i]), int(self.sample[i]),
+                 (GT_NAMES[int(self.gt0[i])], GT_NAMES[int(self.gt1[i])]), self.ref[i], self.alt[i],
+                 int(self.flags[i])) for i in range(len(self))]

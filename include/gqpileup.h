@@ -1,0 +1,231 @@
+/*
+ * gqpileup.h — C-ABI drop-in boundary of the MI355X pileup engine.
+ *
+ * Replaces, for the two callers named by BASELINE.json's north_star, the Spark
+ * operator + per-locus callback pair of the reference (paths relative to
+ * /root/reference/src/main/scala/org/hammerlab/guacamole/):
+ *
+ *   DistributedUtil.pileupFlatMap[T](reads, lociPartitions, skipEmpty, function, reference)
+ *       DistributedUtil.scala:288-306
+ *   DistributedUtil.pileupFlatMapTwoRDDs[T](reads1, reads2, lociPartitions, skipEmpty, function, ref)
+ *       DistributedUtil.scala:316-335
+ *   GermlineThreshold.Caller.callVariantsAtLocus(pileup, thresholdPercent, emitRef, emitNoCall)
+ *       commands/GermlineThresholdCaller.scala:90-179
+ *   SomaticStandard.Caller.findPotentialVariantAtLocus(tumor, normal, odds, minMapq, multiAllelic, maxDepth)
+ *       commands/SomaticStandardCaller.scala:162-245  (+ driver filters :124-151)
+ *
+ * A JVM closure cannot cross a C ABI, so operator + callback are fused into
+ * fixed-function entry points (gq_germline_threshold, gq_somatic_standard) and
+ * a raw per-locus histogram (gq_pileup_counts).  skipEmpty = true is the only
+ * mode (both callers pass true: GermlineThresholdCaller.scala:76,
+ * SomaticStandardCaller.scala:289).
+ *
+ * Conventions: plain pointers + sizes, no exceptions across the ABI.  Every
+ * function returns a gq_status; gq_last_error() gives the thread-local message.
+ * Read sets are uploaded once to HBM (gq_reads_upload) and stay resident; the
+ * caller owns host buffers, the library owns device memory and result buffers
+ * (released with gq_free_calls / gq_free_somatic / gq_free_counts).
+ * One gq_ctx per device; calls on a context are serialized (not re-entrant);
+ * contexts on different devices may run concurrently from different threads.
+ */
+#ifndef GQPILEUP_H
+#define GQPILEUP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes mirror the reference's exception classes. */
+typedef enum {
+  GQ_OK = 0,
+  GQ_E_ASSERT = 1,          /* assume/assert failures (AssertionError)                    */
+  GQ_E_INVALID_CIGAR = 2,   /* InvalidCigarElementException  PileupElement.scala:277-285   */
+  GQ_E_MD = 3,              /* CigarMDTagMismatchException   MappedRead.scala:138-139     */
+  GQ_E_NO_MD = 4,           /* ReferenceWithoutMDTagException MappedRead.scala:141        */
+  GQ_E_MULTI_REF = 5,       /* "Multiple reference bases found" GermlineThresholdCaller:171 */
+  GQ_E_UNSORTED = 6,        /* "Regions must be sorted"       SlidingWindow.scala:55-56   */
+  GQ_E_ARG = 7,             /* IllegalArgumentException (bad arguments / loci)             */
+  GQ_E_HIP = 8,             /* device runtime error                                       */
+  GQ_E_NOMEM = 9,
+  GQ_E_CAPACITY = 10        /* a per-locus table overflowed (distinct alleles > capacity)  */
+} gq_status;
+
+/* CIGAR ops use BAM packing: len << 4 | op, op in M I D N S H P = X -> 0..8. */
+
+/* Read set, structure-of-arrays.  Reads are sorted by (contig, start), ties in
+ * input (file) order; contig c owns reads [contig_read_begin[c], contig_read_begin[c+1]).
+ * Coordinates are 0-based, contig-relative.  MD tags are pre-parsed into events:
+ * md_ev[i] = (offset from read start) << 8 | base, sorted by offset, covering both
+ * mismatches (on M/=/X positions) and deleted bases (on D positions).         */
+typedef struct {
+  int64_t n_reads;
+  int32_t n_contigs;
+  int32_t n_samples;
+  const int64_t *contig_read_begin; /* [n_contigs + 1]                                */
+  const int32_t *start;             /* [n_reads] alignment start                       */
+  const int32_t *end;               /* [n_reads] start + padded reference length       */
+  const int32_t *pmax_end;          /* [n_reads] prefix max of end within the contig   */
+  const uint8_t *mapq;              /* [n_reads]                                       */
+  const uint8_t *flags;             /* [n_reads] bit0 = reverse strand                 */
+  const uint8_t *sample;            /* [n_reads] sample slot                           */
+  const int64_t *seq_off;           /* [n_reads] offset into seq / qual pools          */
+  const int32_t *seq_len;           /* [n_reads]                                       */
+  const int64_t *cigar_off;         /* [n_reads]                                       */
+  const int32_t *n_cigar;           /* [n_reads]                                       */
+  const int64_t *md_off;            /* [n_reads]                                       */
+  const int32_t *n_md;              /* [n_reads] MD events; -1 => read has no MD tag   */
+  const uint16_t *n_mismatch;       /* [n_reads] MdTag.countOfMismatches               */
+  int64_t seq_bytes;                /* pool sizes                                      */
+  int64_t cigar_len;
+  int64_t md_len;
+  const uint8_t *seq;               /* ASCII bases                                     */
+  const uint8_t *qual;              /* phred, same offsets as seq                      */
+  const uint32_t *cigar;
+  const uint32_t *md_ev;
+} gq_reads;
+
+/* LociMap[Long] as flat ranges in partition order (task ascending, contigs
+ * lexicographic, start ascending); half-open [start, end).                    */
+typedef struct {
+  int64_t n_ranges;
+  const int32_t *contig;
+  const int64_t *start;
+  const int64_t *end;
+  const int64_t *task;
+} gq_loci;
+
+typedef struct {
+  int32_t threshold;    /* --threshold (default 8)   */
+  int32_t emit_ref;     /* --emit-ref                */
+  int32_t emit_no_call; /* --emit-no-call            */
+} gq_germline_params;
+
+/* GenotypeAllele codes (bdg-formats): */
+enum { GQ_GT_REF = 0, GQ_GT_ALT = 1, GQ_GT_OTHERALT = 2, GQ_GT_NOCALL = 3 };
+/* per-call flags */
+enum {
+  GQ_FLAG_AMBIGUOUS_REF = 1, /* pileup ref base decided by JVM heap order (MD tags disagree) */
+  GQ_FLAG_TIE = 2            /* count tie among passing alleles (JVM hash order unpinned)   */
+};
+
+/* Germline genotype records (Genotype.newBuilder, GermlineThresholdCaller.scala:106-117),
+ * in output order (partition order, then sample, then allele rank).          */
+typedef struct {
+  int64_t n;
+  int32_t *contig;
+  int64_t *pos;
+  uint8_t *sample;
+  uint8_t *gt0, *gt1;
+  uint8_t *flags;
+  int64_t *ref_off;  int32_t *ref_len;   /* into allele_pool */
+  int64_t *alt_off;  int32_t *alt_len;
+  uint8_t *allele_pool;
+  int64_t pool_len;
+  /* run counters */
+  int64_t visited_loci;   /* loci with depth > 0 (skipEmpty semantics)         */
+  int64_t complex_loci;   /* loci routed through the general-allele kernel     */
+  int64_t ambiguous_loci; /* loci whose ref base depends on heap order         */
+  int64_t tie_loci;
+} gq_calls;
+
+typedef struct gq_ctx gq_ctx;
+typedef struct gq_dev_reads gq_dev_reads;
+
+/* Per-kernel device times of the last call on this context (HIP events on the
+ * context's stream), in milliseconds. */
+typedef struct {
+  float plan_ms;
+  float pileup_ms;   /* dominant kernel: per-tile LDS histogram + on-device decision */
+  float complex_ms;
+  float finalize_ms; /* sort / compaction of the call records                        */
+  float total_ms;    /* first event to last event                                    */
+  int64_t pileup_launches;
+  int64_t tiles;
+} gq_timings;
+
+const char *gq_version(void);
+const char *gq_last_error(void);
+
+gq_status gq_open(int device, gq_ctx **out);
+void gq_close(gq_ctx *ctx);
+gq_status gq_get_timings(const gq_ctx *ctx, gq_timings *out);
+/* Tile size (loci per workgroup) used by the pileup kernel; 0 => default. */
+gq_status gq_set_tile(gq_ctx *ctx, int32_t loci_per_tile);
+
+/* Copy a host read set into HBM (SoA kept resident until gq_reads_free).     */
+gq_status gq_reads_upload(gq_ctx *ctx, const gq_reads *host, gq_dev_reads **out);
+/* Wrap read arrays that are ALREADY in device memory (e.g. torch tensors);  */
+/* the caller keeps them alive.                                              */
+gq_status gq_reads_wrap_device(gq_ctx *ctx, const gq_reads *device_ptrs, gq_dev_reads **out);
+void gq_reads_free(gq_dev_reads *r);
+
+/* germline-threshold over the given loci partitions.                         */
+gq_status gq_germline_threshold(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
+                                const gq_germline_params *params, gq_calls **out);
+void gq_free_calls(gq_calls *c);
+
+/* Raw per-locus pileup histogram for every locus of `loci` (dense, in range
+ * order).  Categories: Match/Mismatch by sequenced base A,C,G,T,N,other; then
+ * insertion, deletion, mid-deletion, clipped; positive-strand depth; the
+ * MD-derived reference base (or 'N'); ambiguous-ref flag.                     */
+typedef struct {
+  int64_t n_loci;
+  int32_t *depth;
+  int32_t *pos_depth;
+  int32_t *base_counts;   /* [n_loci * 6]  A C G T N other              */
+  int32_t *indel_counts;  /* [n_loci * 4]  ins del middel clipped       */
+  int32_t *ref_depth;     /* Match elements                             */
+  uint8_t *ref_base;
+  uint8_t *ambiguous;
+} gq_counts;
+gq_status gq_pileup_counts(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci, gq_counts **out);
+void gq_free_counts(gq_counts *c);
+
+/* somatic-standard.                                                          */
+typedef struct {
+  int32_t odds;                 /* --odds (20)                          */
+  int32_t min_mapq;             /* --min-mapq (1)                       */
+  int32_t filter_multi_allelic; /* --filter-multi-allelic               */
+  int32_t max_read_depth;       /* caller's maxReadDepth (= --max-tumor-read-depth) */
+  int32_t min_tumor_read_depth, max_tumor_read_depth, min_normal_read_depth;
+  int32_t min_tumor_alternate_read_depth;
+  int32_t min_lod, min_likelihood, min_vaf;
+  int32_t min_average_mapping_quality, min_average_base_quality;
+  int32_t max_median_mismatches;
+  int32_t apply_filters;        /* 0 => raw findPotentialVariantAtLocus output */
+} gq_somatic_params;
+
+typedef struct {
+  double likelihood;
+  int32_t read_depth, allele_read_depth, forward_depth, allele_forward_depth;
+  double mean_mq, median_mq, mean_bq, median_bq, median_mismatches;
+} gq_evidence;
+
+/* CalledSomaticAllele (variants/CalledSomaticAllele.scala:37-51)            */
+typedef struct {
+  int64_t n;
+  int32_t *contig;
+  int64_t *pos;
+  uint8_t *sample;
+  int64_t *ref_off;  int32_t *ref_len;
+  int64_t *alt_off;  int32_t *alt_len;
+  uint8_t *allele_pool;
+  int64_t pool_len;
+  double *log_odds;
+  int32_t *gq;               /* phredScaledSomaticLikelihood                 */
+  gq_evidence *tumor;        /* tumorVariantEvidence                         */
+  gq_evidence *normal;       /* normalReferenceEvidence                      */
+  uint8_t *flags;
+  int64_t visited_loci;
+  int64_t candidate_loci;    /* loci that reached the likelihood kernel      */
+} gq_somatic_calls;
+
+gq_status gq_somatic_standard(gq_ctx *ctx, const gq_dev_reads *tumor, const gq_dev_reads *normal,
+                              const gq_loci *loci, const gq_somatic_params *params, gq_somatic_calls **out);
+void gq_free_somatic(gq_somatic_calls *c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,221 @@
+"""ctypes wrapper around oracle/_build/liboracle.so.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker.  The product package
+(guacamole_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import List, Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("oracle error %d: %s" % (code, msg))
+        self.code = code
+
+
+class or_reads(C.Structure):
+    _fields_ = [("n_reads", C.c_int64), ("contig", C.c_void_p), ("start", C.c_void_p), ("mapq", C.c_void_p),
+                ("flags", C.c_void_p), ("sample", C.c_void_p), ("seq_off", C.c_void_p), ("seq_len", C.c_void_p),
+                ("seq", C.c_void_p), ("qual", C.c_void_p), ("cigar_off", C.c_void_p), ("n_cigar", C.c_void_p),
+                ("cigar", C.c_void_p), ("md_off", C.c_void_p), ("md_len", C.c_void_p), ("md", C.c_void_p)]
+
+
+class or_loci(C.Structure):
+    _fields_ = [("n_contigs", C.c_int32), ("contig_names", C.POINTER(C.c_char_p)), ("n_ranges", C.c_int64),
+                ("range_contig", C.c_void_p), ("range_start", C.c_void_p), ("range_end", C.c_void_p),
+                ("range_task", C.c_void_p)]
+
+
+class or_somatic_params(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "odds", "min_mapq", "filter_multi_allelic", "max_read_depth", "min_tumor_read_depth",
+        "max_tumor_read_depth", "min_normal_read_depth", "min_tumor_alternate_read_depth", "min_lod",
+        "min_likelihood", "min_vaf", "min_average_mapping_quality", "min_average_base_quality",
+        "max_median_mismatches", "apply_filters")]
+
+
+def build() -> str:
+    src = os.path.join(_HERE, "oracle.cpp")
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        _lib.or_last_error.restype = C.c_char_p
+        for fn in ("or_pileup_stats", "or_germline_threshold", "or_somatic_standard"):
+            getattr(_lib, fn).restype = C.c_int
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+class _Marshalled:
+    def __init__(self, rs):
+        self.keep = [np.ascontiguousarray(rs.contig, np.int32), np.ascontiguousarray(rs.start, np.int64),
+                     np.ascontiguousarray(rs.mapq, np.uint8), np.ascontiguousarray(rs.flags, np.uint8),
+                     np.ascontiguousarray(rs.sample, np.int32), np.ascontiguousarray(rs.seq_off, np.int64),
+                     np.ascontiguousarray(rs.seq_len, np.int32), np.ascontiguousarray(rs.seq, np.uint8),
+                     np.ascontiguousarray(rs.qual, np.uint8), np.ascontiguousarray(rs.cigar_off, np.int64),
+                     np.ascontiguousarray(rs.n_cigar, np.int32), np.ascontiguousarray(rs.cigar, np.uint32),
+                     np.ascontiguousarray(rs.md_off, np.int64), np.ascontiguousarray(rs.md_len, np.int32),
+                     np.ascontiguousarray(rs.md, np.uint8)]
+        k = self.keep
+        self.s = or_reads(rs.n, *[_ptr(a) for a in k])
+
+
+class _Loci:
+    def __init__(self, contig_names: List[str], contig, start, end, task):
+        self.names = (C.c_char_p * len(contig_names))(*[c.encode() for c in contig_names])
+        self.keep = [np.ascontiguousarray(contig, np.int32), np.ascontiguousarray(start, np.int64),
+                     np.ascontiguousarray(end, np.int64), np.ascontiguousarray(task, np.int64)]
+        self.s = or_loci(len(contig_names), C.cast(self.names, C.POINTER(C.c_char_p)), len(self.keep[0]),
+                         *[_ptr(a) for a in self.keep])
+
+
+def _call(fn, *args) -> str:
+    out = C.c_char_p()
+    n = C.c_int64()
+    rc = fn(*args, C.byref(out), C.byref(n))
+    if rc != 0:
+        raise OracleError(rc, lib().or_last_error().decode())
+    try:
+        return C.string_at(out, n.value).decode("latin-1")
+    finally:
+        lib().or_free(out)
+
+
+def pileup_stats(rs, loci) -> List[tuple]:
+    """Per visited locus raw histogram (see oracle.h)."""
+    m = _Marshalled(rs)
+    L = _Loci(rs.contig_names, *loci)
+    text = _call(lib().or_pileup_stats, C.byref(m.s), C.byref(L.s))
+    rows = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        rows.append((f[0], int(f[1]), f[2], int(f[3]), int(f[4]), tuple(int(x) for x in f[5].split()),
+                     tuple(int(x) for x in f[6].split()), int(f[7]), int(f[8])))
+    return rows
+
+
+def germline_threshold(rs, loci, threshold: int = 8, emit_ref: bool = False, emit_no_call: bool = False):
+    """Lines -> tuples (contig, locus, sample, (gt0, gt1), ref, alt, flags)."""
+    m = _Marshalled(rs)
+    L = _Loci(rs.contig_names, *loci)
+    text = _call(lib().or_germline_threshold, C.byref(m.s), C.byref(L.s), C.c_int32(threshold),
+                 C.c_int32(int(emit_ref)), C.c_int32(int(emit_no_call)))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        out.append((f[0], int(f[1]), int(f[2]), tuple(f[3].split(",")), f[4], f[5], int(f[6])))
+    return out
+
+
+SOMATIC_DEFAULTS = dict(odds=20, min_mapq=1, filter_multi_allelic=0, max_read_depth=2 ** 31 - 1,
+                        min_tumor_read_depth=0, max_tumor_read_depth=2 ** 31 - 1, min_normal_read_depth=0,
+                        min_tumor_alternate_read_depth=0, min_lod=0, min_likelihood=0, min_vaf=0,
+                        min_average_mapping_quality=0, min_average_base_quality=0,
+                        max_median_mismatches=2 ** 31 - 1, apply_filters=1)
+
+
+def somatic_standard(tumor, normal, loci, **params):
+    p = dict(SOMATIC_DEFAULTS)
+    p.update(params)
+    ps = or_somatic_params(**{k: int(v) for k, v in p.items()})
+    mt, mn = _Marshalled(tumor), _Marshalled(normal)
+    L = _Loci(tumor.contig_names, *loci)
+    text = _call(lib().or_somatic_standard, C.byref(mt.s), C.byref(mn.s), C.byref(L.s), C.byref(ps))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        ev = lambda a: (float(a[0]), int(a[1]), int(a[2]), int(a[3]), int(a[4])) + tuple(float(x) for x in a[5:10])
+        out.append(dict(contig=f[0], locus=int(f[1]), sample=int(f[2]), ref=f[3], alt=f[4], log_odds=float(f[5]),
+                        gq=int(f[6]), tumor=ev(f[7:17]), normal=ev(f[17:27]), flags=int(f[27])))
+    return out
+
+
+# ---- single-locus entry points (Pileup.apply semantics), used by the KAT tests
+def _contig_id(rs, contig: str) -> int:
+    return rs.contig_names.index(contig)
+
+
+def elements_at(rs, contig: str, locus: int, own_ref: bool = False):
+    """-> (pileup ref base, [dict(read, kind, ref, alt, quality, readPosition, cigarElementIndex, indexWithin)])."""
+    m = _Marshalled(rs)
+    lines = _call(lib().or_elements_at, C.byref(m.s), C.c_int32(_contig_id(rs, contig)), C.c_int64(locus),
+                  C.c_int32(int(own_ref))).splitlines()
+    ref = lines[0].split("\t")[1]
+    els = []
+    for line in lines[1:]:
+        f = line.split("\t")
+        els.append(dict(read=int(f[0]), kind=f[1], ref=f[2], alt=f[3], quality=int(f[4]), readPosition=int(f[5]),
+                        cigarElementIndex=int(f[6]), indexWithin=int(f[7])))
+    return ref, els
+
+
+def likelihoods_at(rs, contig: str, locus: int, genotypes=None, include_alignment=False, log_space=False,
+                   normalize=False):
+    """genotypes: list of ((ref, alt), (ref, alt)) or None for all possible genotypes."""
+    spec = "" if genotypes is None else "|".join("%s,%s;%s,%s" % (a[0], a[1], b[0], b[1]) for a, b in genotypes)
+    m = _Marshalled(rs)
+    text = _call(lib().or_likelihoods_at, C.byref(m.s), C.c_int32(_contig_id(rs, contig)), C.c_int64(locus),
+                 spec.encode(), C.c_int32(int(include_alignment)), C.c_int32(int(log_space)),
+                 C.c_int32(int(normalize)))
+    out = []
+    for line in text.splitlines():
+        g, v = line.split("\t")
+        a, b = g.split(";")
+        out.append(((tuple(a.split(",")), tuple(b.split(","))), float(v)))
+    return out
+
+
+def allele_evidence_at(rs, contig: str, locus: int, likelihood: float, ref: str, alt: str):
+    m = _Marshalled(rs)
+    f = _call(lib().or_allele_evidence_at, C.byref(m.s), C.c_int32(_contig_id(rs, contig)), C.c_int64(locus),
+              C.c_double(likelihood), ref.encode(), alt.encode()).strip("\n").split("\t")[1:]
+    keys = ("likelihood", "readDepth", "alleleReadDepth", "forwardDepth", "alleleForwardDepth", "meanMappingQuality",
+            "medianMappingQuality", "meanBaseQuality", "medianBaseQuality", "medianMismatchesPerRead")
+    return {k: (int(v) if k.endswith("Depth") else float(v)) for k, v in zip(keys, f)}
+
+
+def germline_at(rs, contig: str, locus: int, threshold: int, emit_ref: bool = True, emit_no_call: bool = True):
+    m = _Marshalled(rs)
+    text = _call(lib().or_germline_at, C.byref(m.s), C.c_int32(_contig_id(rs, contig)), C.c_int64(locus),
+                 C.c_int32(threshold), C.c_int32(int(emit_ref)), C.c_int32(int(emit_no_call)))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        out.append(dict(locus=int(f[1]), gt=tuple(f[3].split(",")), ref=f[4], alt=f[5]))
+    return out
+
+
+def somatic_at(tumor, normal, contig: str, locus: int, **params):
+    p = dict(SOMATIC_DEFAULTS)
+    p.update(params)
+    ps = or_somatic_params(**{k: int(v) for k, v in p.items()})
+    mt, mn = _Marshalled(tumor), _Marshalled(normal)
+    text = _call(lib().or_somatic_at, C.byref(mt.s), C.byref(mn.s), C.c_int32(_contig_id(tumor, contig)),
+                 C.c_int64(locus), C.byref(ps))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        out.append(dict(locus=int(f[1]), ref=f[3], alt=f[4], log_odds=float(f[5]), gq=int(f[6])))
+    return out

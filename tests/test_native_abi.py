@@ -1,0 +1,16 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol gqpileup.h declares."""
+import os
+import re
+
+from conftest import ROOT
+from guacamole_amd import native
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "gqpileup.h")).read()
+    declared = set(re.findall(r"\b(gq_[a-z_]+)\s*\(", hdr))
+    L = native.lib()
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(native.EXPORTED) == declared
+    assert b"gfx950" in L.gq_version()
