@@ -553,11 +553,12 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
                                                            int threshold, int emit_ref, int emit_no_call,
                                                            CallRec *__restrict__ recs, unsigned long long rec_cap,
                                                            uint8_t *__restrict__ pool, unsigned long long pool_cap,
-                                                           Counters *ctr) {
+                                                           unsigned long long cplx_cap, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const unsigned long long n_items = ctr->n_complex;
+  // items beyond the queue's capacity were never written (the host retries with a larger queue)
+  const unsigned long long n_items = ctr->n_complex < cplx_cap ? ctr->n_complex : cplx_cap;
   for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
     const ComplexItem item = items[it];
     const Tile tl = tiles[item.tile];
@@ -1194,7 +1195,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), 4096);
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                       (CallRec *)c->recs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, ctr);
+                       (CallRec *)c->recs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cplx_cap, ctr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
