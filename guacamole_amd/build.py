@@ -35,6 +35,18 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+SYNTH_SRC = os.path.join(CSRC, "gq_synth.cpp")
+SYNTH_LIB = os.path.join(LIB_DIR, "libgqsynth.so")
+
+
+def build_synth(force: bool = False) -> str:
+    """Host-side synthetic read generator (bench / test data), g++ -O3 -pthread."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _stale(SYNTH_LIB, [SYNTH_SRC]):
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", SYNTH_LIB, SYNTH_SRC])
+    return SYNTH_LIB
+
+
 def build_oracle() -> str:
     d = os.path.join(ROOT, "oracle")
     subprocess.check_call(["make", "-s", "-C", d])

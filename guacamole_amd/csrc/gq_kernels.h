@@ -38,6 +38,10 @@ struct DevReads {
   const uint16_t *n_mismatch;
   const uint8_t *seq, *qual;
   const uint32_t *cigar, *md_ev;
+  int64_t seq_bytes;
+  // derived at upload (read_shape):
+  const int16_t *lead;   // leading soft clip of a [S|H]*(M|=|X)[S|H]* CIGAR, -1 otherwise
+  const uint8_t *ev_rb;  // per MD event: the read's sequenced base at that position (0 for deletions)
 };
 
 // One locus tile: contiguous loci [L0, L1) of one contig, plus the index range
@@ -62,6 +66,7 @@ static_assert(sizeof(CallRec) == 32, "CallRec layout");
 struct ComplexItem {
   int32_t tile;
   int32_t pos;
+  int32_t flags;  // bit0: queued unconditionally (wide tile): the complex kernel counts the visit
 };
 
 enum : int { ERR_NONE = 0 };
@@ -70,27 +75,22 @@ __device__ __forceinline__ void raise_error(int *err, int64_t *err_pos, int code
   if (atomicCAS(err, 0, code) == 0) *err_pos = where;
 }
 
+// Base categories: A=0, C=1, T=2, G=3, N=4, other=5.  For A/C/T/G the index is
+// (b >> 1) & 3 of the ASCII byte, checked against the packed table 'A','C','T','G'.
 __device__ __forceinline__ int base_cat(uint8_t b) {
-  switch (b) {
-    case 'A': return 0;
-    case 'C': return 1;
-    case 'G': return 2;
-    case 'T': return 3;
-    case 'N': return 4;
-    default: return 5;
-  }
+  const uint32_t idx = ((uint32_t)b >> 1) & 3u;
+  const uint32_t expect = (0x47544341u >> (8u * idx)) & 0xFFu;
+  return ((uint32_t)b == expect) ? (int)idx : (b == 'N' ? 4 : 5);
 }
-__device__ __forceinline__ uint32_t std_bit(uint8_t b) {
-  switch (b) {
-    case 'A': return 1u;
-    case 'C': return 2u;
-    case 'G': return 4u;
-    case 'T': return 8u;
-    default: return 0u;
-  }
+__device__ __forceinline__ uint8_t cat_base(int c) {  // inverse of base_cat for 0..4
+  return (uint8_t)((0x4E47544341ull >> (8 * c)) & 0xFFu);
+}
+__device__ __forceinline__ uint32_t std_bit(uint8_t b) {  // one bit per standard base (bit = category)
+  const int c = base_cat(b);
+  return c < 4 ? (1u << c) : 0u;
 }
 __device__ __forceinline__ uint8_t bit_base(uint32_t m) {  // lowest set bit of a std mask -> base
-  return (m & 1u) ? 'A' : (m & 2u) ? 'C' : (m & 4u) ? 'G' : 'T';
+  return cat_base(__ffs((int)m) - 1);
 }
 
 // MD event lookup for reference offset `off` (events sorted by offset).
@@ -106,37 +106,110 @@ __device__ __forceinline__ int md_find(const uint32_t *ev, int32_t n, int32_t of
   return -1;
 }
 
-// Wave-cooperative walk of one read's CIGAR over the loci [L0, L1): lanes take 64
-// consecutive loci of each reference-consuming op.  `sink.elem(l, kind, base, mdb, ev)`
-// receives every pileup element (l, kind), the sequenced base for SNV/anchor
-// elements, the read's MD-derived reference base at l (MDTagUtils.getReference),
-// and whether an MD event (mismatch / deleted base) sits at l.
+// Fast path of walk_read_lane for CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming
+// op: every element is a Match/Mismatch).  Two passes:
+//   1. bases: the read's bytes over [max(s,L0), min(e,L1)) stream in as 16-byte aligned
+//      chunks through a 4-deep rotating register prefetch; each dword goes to
+//      sink.bases4(i, word, valid4) with no branch (bytes outside the read carry
+//      valid = 0 and add nothing; i may fall in the sink's guard band);
+//   2. MD events inside the window: sink.event_i(i, read base, MD reference base), with
+//      the first four events and their read bases prefetched alongside the chunks.
 template <class Sink>
-__device__ __forceinline__ void walk_read(const DevReads &R, int64_t r, int32_t L0, int32_t L1, Sink &sink) {
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_t e, int32_t lead, int64_t seq_off,
+                                            int32_t nmd, int64_t md_off, int32_t L0, int32_t L1, uint8_t fl,
+                                            Sink &sink) {
+  const int32_t a = s > L0 ? s : L0;
+  const int32_t b = e < L1 ? e : L1;
+  const int64_t p0 = seq_off + lead + (a - s);
+  const int64_t p1 = seq_off + lead + (b - s);
+  const int64_t cb0 = p0 & ~(int64_t)15;
+  const int nchunks = (int)((p1 - cb0 + 15) >> 4);
+  const int32_t ioff = (a - L0) - (int32_t)(p0 - cb0);  // tile index of byte cb0
+  const uint32_t *ev = R.md_ev + md_off;
+  const uint8_t *evb = R.ev_rb + md_off;
+  uint32_t e4[4], b4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    e4[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
+    b4[k] = k < nmd ? evb[k] : 0u;
+  }
+  if (cb0 + 16 * (int64_t)nchunks > R.seq_bytes) {  // last read of the pool: byte loads
+    for (int64_t p = p0; p < p1; ++p) {
+      const int32_t i = ioff + (int32_t)(p - cb0);
+      const int32_t sh = (int32_t)((p - cb0) & 3) * 8;
+      sink.bases4(i - (sh >> 3), (uint32_t)R.seq[p] << sh, 1u << (sh >> 3), fl);
+    }
+  } else {
+    auto ld = [&](int q) -> uint4 {  // clamped to the read's last chunk: every load in bounds
+      const int qc = q < nchunks ? q : nchunks - 1;
+      return *reinterpret_cast<const uint4 *>(R.seq + cb0 + 16 * (int64_t)qc);
+    };
+    const int32_t lo0 = (int32_t)(p0 - cb0);  // first valid byte of chunk 0
+    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
+    for (int q = 0; q < nchunks; ++q) {
+      const int32_t lo = q == 0 ? lo0 : 0;
+      const int64_t rem = p1 - (cb0 + 16 * (int64_t)q);
+      const int32_t hi = rem < 16 ? (int32_t)rem : 16;
+      const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);  // valid bytes [lo, hi)
+      const int32_t ib = ioff + 16 * q;
+      sink.bases4(ib, c0.x, vm & 15u, fl);
+      sink.bases4(ib + 4, c0.y, (vm >> 4) & 15u, fl);
+      sink.bases4(ib + 8, c0.z, (vm >> 8) & 15u, fl);
+      sink.bases4(ib + 12, c0.w, (vm >> 12) & 15u, fl);
+      c0 = c1;
+      c1 = c2;
+      c2 = c3;
+      c3 = ld(q + 4);
+    }
+  }
+  // MD events inside [a - s, b - s): mismatching reference bases on this read
+  for (int k = 0; k < nmd; ++k) {
+    const uint32_t v = k < 4 ? (k == 0 ? e4[0] : k == 1 ? e4[1] : k == 2 ? e4[2] : e4[3]) : ev[k];
+    const int32_t off = (int32_t)(v >> 8);
+    if (off < a - s) continue;
+    if (off >= b - s) break;
+    const uint32_t rb = k < 4 ? (k == 0 ? b4[0] : k == 1 ? b4[1] : k == 2 ? b4[2] : b4[3]) : evb[k];
+    sink.event_i(off + s - L0, (uint8_t)rb, (uint8_t)(v & 0xFFu), fl);
+  }
+}
+
+// Per-lane walk of one read's CIGAR over the loci [L0, L1): every lane owns one
+// read (64 reads in flight per wave).  `sink.elem(l, kind, base, mdb, ev, flags)`
+// receives each pileup element: locus, kind, the sequenced base for SNV / anchor
+// elements, the read's MD-derived reference base at l (MDTagUtils.getReference),
+// and whether an MD event (mismatch or deleted base) sits at l.
+//
+// Fast path: CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming op), bases
+// read as 16-byte aligned chunks.  General path: any CIGAR, byte loads.
+template <class Sink>
+__device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1, Sink &sink) {
   const int32_t s = R.start[r];
   const int32_t e = R.end[r];
   if (e <= L0 || s >= L1) return;
-  const int64_t seq_off = R.seq_off[r];
-  const int32_t slen = R.seq_len[r];
-  const int64_t cig_off = R.cigar_off[r];
-  const int32_t ncig = R.n_cigar[r];
-  const int64_t md_off = R.md_off[r];
   const int32_t nmd = R.n_md[r];
-  const uint8_t fl = R.flags[r];
   if (nmd < 0) {  // MappedRead.mdTagReferenceBases on a read without MD (MappedRead.scala:57-60)
-    sink.error(4 /*GQ_E_NO_MD*/, ((int64_t)s));
+    sink.error(4 /*GQ_E_NO_MD*/, (int64_t)s);
     return;
   }
-  const uint32_t *ev = R.md_ev + md_off;
-  // events preloaded into lanes (first 64); longer lists fall back to a binary search
-  const uint32_t ev_lane = lane < nmd ? ev[lane] : 0xFFFFFFFFu;
-  const int nev_reg = nmd < 64 ? nmd : 64;
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  const int64_t seq_off = R.seq_off[r];
+  const int32_t slen = R.seq_len[r];
+  const uint8_t fl = R.flags[r];
 
+  const int32_t lead = R.lead[r];
+  if (lead >= 0) {
+    walk_simple(R, s, e, lead, seq_off, nmd, R.md_off[r], L0, L1, fl, sink);
+    return;
+  }
+
+  // general CIGAR
   int32_t ref = s;
   int32_t rpos = 0;
   bool lead_ins = false;  // I before any reference-consuming op on a read at locus 0 (PileupElement.scala:102-103, 240-245)
   bool seen_ref = false;
+  int kev = 0;
   for (int k = 0; k < ncig; ++k) {
     const uint32_t c = R.cigar[cig_off + k];
     const int op = (int)(c & 15u);
@@ -148,35 +221,30 @@ __device__ __forceinline__ void walk_read(const DevReads &R, int64_t r, int32_t 
       seen_ref = true;
       const int32_t a = ref > L0 ? ref : L0;
       const int32_t b = (ref + len) < L1 ? (ref + len) : L1;
-      for (int32_t l0 = a; l0 < b; l0 += 64) {
-        const int32_t l = l0 + lane;
+      while (kev < nmd && (int32_t)(ev[kev] >> 8) < a - s) ++kev;
+      for (int32_t l = a; l < b; ++l) {
         const int32_t off = l - s;
-        // MD event at this reference offset (all lanes participate: readlane is uniform)
         int mdv = -1;
-        for (int j = 0; j < nev_reg; ++j) {
-          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)ev_lane, j);
-          if ((int32_t)(v >> 8) == off) mdv = (int)(v & 0xFFu);
+        if (kev < nmd && (int32_t)(ev[kev] >> 8) == off) {
+          mdv = (int)(ev[kev] & 0xFFu);
+          ++kev;
         }
-        if (nmd > 64 && mdv < 0 && l < b) mdv = md_find(ev, nmd, off);
-        if (l < b) {
-          if (op == OP_M || op == OP_EQ || op == OP_X) {
-            const int32_t rp = rpos + (l - ref);
-            uint8_t base = 0;
-            if (rp < slen) base = R.seq[seq_off + rp];
-            else sink.error(1, (int64_t)l);
-            const bool fin = (l == ref + len - 1);
-            int kind = K_SNV;
-            if (lead_ins && l == 0) kind = K_INS;
-            else if (fin && (op == OP_M || op == OP_EQ) && nextop == OP_I) kind = K_INS;
-            else if (fin && nextop == OP_D) kind = K_DEL;
-            const uint8_t mdb = mdv >= 0 ? (uint8_t)mdv : base;
-            sink.elem(l, kind, base, mdb, mdv >= 0, fl);
-          } else if (op == OP_D) {
-            if (mdv < 0) sink.error(3 /*GQ_E_MD*/, (int64_t)l);
-            sink.elem(l, K_MID, (uint8_t)0, mdv >= 0 ? (uint8_t)mdv : (uint8_t)'N', true, fl);
-          } else {  // N: Clipped, MD-derived reference 'N'
-            sink.elem(l, K_CLIP, (uint8_t)0, (uint8_t)'N', false, fl);
-          }
+        if (op == OP_M || op == OP_EQ || op == OP_X) {
+          const int32_t rp = rpos + (l - ref);
+          uint8_t base = 0;
+          if (rp < slen) base = R.seq[seq_off + rp];
+          else sink.error(1, (int64_t)l);
+          const bool fin = (l == ref + len - 1);
+          int kind = K_SNV;
+          if (lead_ins && l == 0) kind = K_INS;
+          else if (fin && (op == OP_M || op == OP_EQ) && nextop == OP_I) kind = K_INS;
+          else if (fin && nextop == OP_D) kind = K_DEL;
+          sink.elem(l, kind, base, mdv >= 0 ? (uint8_t)mdv : base, mdv >= 0, fl);
+        } else if (op == OP_D) {
+          if (mdv < 0) sink.error(3 /*GQ_E_MD*/, (int64_t)l);
+          sink.elem(l, K_MID, (uint8_t)0, mdv >= 0 ? (uint8_t)mdv : (uint8_t)'N', true, fl);
+        } else {  // N: Clipped, MD-derived reference 'N'
+          sink.elem(l, K_CLIP, (uint8_t)0, (uint8_t)'N', false, fl);
         }
       }
       ref += len;

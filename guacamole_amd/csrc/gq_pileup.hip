@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -104,6 +105,59 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   tiles[t] = tl;
 }
 
+// CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
+// [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
+__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const int64_t off = R.cigar_off[r];
+  const int32_t n = R.n_cigar[r];
+  int32_t ld = 0, mlen = 0;
+  int mi = -1;
+  bool simple = n > 0;
+  for (int k = 0; k < n && simple; ++k) {
+    const uint32_t c = R.cigar[off + k];
+    const int op = (int)(c & 15u);
+    if (op == OP_M || op == OP_EQ || op == OP_X) {
+      if (mi >= 0) simple = false;
+      mi = k;
+      mlen = (int32_t)(c >> 4);
+    } else if (op == OP_S) {
+      if (mi < 0) ld += (int32_t)(c >> 4);
+    } else if (op != OP_H) {
+      simple = false;
+    }
+  }
+  if (mi < 0 || ld > 32767 || ld + mlen > R.seq_len[r]) simple = false;
+  lead[r] = simple ? (int16_t)ld : (int16_t)-1;
+  // sequenced base under each MD event (0 where the event sits on a deletion / outside M)
+  const int32_t nmd = R.n_md[r];
+  if (nmd <= 0) return;
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  uint8_t *rb = ev_rb + R.md_off[r];
+  int32_t ref = 0, rp = 0;
+  int k = 0;
+  for (int c = 0; c < n && k < nmd; ++c) {
+    const uint32_t cc = R.cigar[off + c];
+    const int op = (int)(cc & 15u);
+    const int32_t len = (int32_t)(cc >> 4);
+    if (consumes_ref(op)) {
+      while (k < nmd && (int32_t)(ev[k] >> 8) < ref + len) {
+        const int32_t o = (int32_t)(ev[k] >> 8);
+        uint8_t v = 0;
+        if ((op == OP_M || op == OP_EQ || op == OP_X) && o >= ref) {
+          const int32_t q = rp + (o - ref);
+          if (q < R.seq_len[r]) v = R.seq[R.seq_off[r] + q];
+        }
+        rb[k++] = v;
+      }
+      ref += len;
+    }
+    if (consumes_read(op)) rp += len;
+  }
+  for (; k < nmd; ++k) rb[k] = 0;
+}
+
 struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_rec;
   unsigned long long n_complex;
@@ -142,50 +196,108 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ------------------------------------------------------------------------------------------
 // germline_tile: LDS histogram + on-device decision for simple loci
 // ------------------------------------------------------------------------------------------
-// LDS categories (u32 per locus, SoA: cat * T + i => consecutive loci on consecutive banks)
-enum : int { C_A = 0, C_C, C_G, C_T, C_N, C_CPLX, C_MASK, C_EVA, C_EVC, C_EVG, C_EVT, C_NCAT };
+// LDS histogram: seven u32 words per locus (SoA: word * S + guard + i, so consecutive loci
+// sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has
+// code (b >> 1) & 7, distinct for A 0, C 1, T 2, G 3, N 7; a base whose code does not
+// map back to it is "other" (slot 4).  slot = word * 2 + half:
+//   W_AC = A | C << 16, W_TG = T | G << 16, W_OX = other | complex << 16, W_NN = N << 16,
+//   W_EAC / W_ETG = A C / T G counts of Match/Mismatch elements carrying an MD mismatch
+//   event, W_MASK = OR of MD-derived standard reference bases of event / complex elements.
+// Tiles whose read window could exceed 65535 reads never use this path (wide tiles).
+enum : int { W_AC = 0, W_TG, W_OX, W_NN, W_EAC, W_ETG, W_MASK, W_N };
+// LDS arrays carry a 16-entry guard band on each side (stride T + 32, index 16 + i), so
+// the branch-free base pass may address i in [-16, T + 16) with a zero increment.
+constexpr int kGuard = 16;
 
-template <int T>
+template <int T, int ABL = 0>
 struct GermSink {
-  uint32_t *cnt;
+  uint32_t *cnt;  // W_N arrays of T + 2 * kGuard words
   int32_t L0;
   int *err;
   long long *err_pos;
-  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t) {
-    const int i = l - L0;
-    if (kind == K_SNV) {
-      const int c = base_cat(base);  // 5 (= C_CPLX) for a non-ACGTN sequenced base
-      atomicAdd(&cnt[c * T + i], 1u);
-      if (ev) {  // MD mismatch at this position: MD-derived ref differs from the read base
-        if (c < 4) atomicAdd(&cnt[(C_EVA + c) * T + i], 1u);
-        const uint32_t b = std_bit(mdb);
-        if (b) atomicOr(&cnt[C_MASK * T + i], b);
+  static constexpr int S = T + 2 * kGuard;
+  uint32_t acc = 0;  // ABL & 4 only
+  __device__ __forceinline__ ~GermSink() {
+    if ((ABL & 4) && acc == 0x12345u) atomicAdd(cnt, 1u);
+  }
+  __device__ __forceinline__ uint32_t *at(int w, int i) const { return cnt + w * S + kGuard + i; }
+  // four Match/Mismatch elements: the bytes of `w` at tile indices i..i+3 (valid4: bit per byte)
+  __device__ __forceinline__ void bases4(int i, uint32_t w, uint32_t valid4, uint8_t) {
+    const uint32_t code4 = (w >> 1) & 0x07070707u;
+    const uint32_t exp4 = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, code4);  // 'A','C','T','G',0,0,0,'N'
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t bj = (w >> (8 * j)) & 0xFFu, ej = (exp4 >> (8 * j)) & 0xFFu, cj = (code4 >> (8 * j)) & 7u;
+      const uint32_t slot = bj == ej ? cj : 4u;
+      if (ABL & 4) {
+        acc += ((valid4 >> j) & 1u) << ((slot & 1u) << 4);
+        acc ^= slot;
+      } else {
+        atomicAdd(at((int)(slot >> 1), i + j), ((valid4 >> j) & 1u) << ((slot & 1u) << 4));
       }
-    } else {
-      atomicAdd(&cnt[C_CPLX * T + i], 1u);
-      const uint32_t b = std_bit(mdb);
-      if (b) atomicOr(&cnt[C_MASK * T + i], b);
     }
+  }
+  // an MD mismatch event on a Match/Mismatch element: read base b, MD reference base m
+  __device__ __forceinline__ void event_i(int i, uint8_t b, uint8_t m, uint8_t) {
+    if (ABL & 8) return;
+    const int c = base_cat(b);
+    if (c < 4) atomicAdd(at(W_EAC + (c >> 1), i), 1u << ((c & 1) << 4));
+    const uint32_t bit = std_bit(m);
+    if (bit) atomicOr(at(W_MASK, i), bit);
+  }
+  // general walker elements
+  __device__ __forceinline__ void elem_i(int i, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
+    if (kind == K_SNV) {
+      const int sh = (i & 3) * 8;
+      bases4(i - (i & 3), (uint32_t)base << sh, 1u << (i & 3), fl);
+      if (ev) event_i(i, base, mdb, fl);
+    } else {
+      atomicAdd(at(W_OX, i), 1u << 16);
+      const uint32_t bit = std_bit(mdb);
+      if (bit) atomicOr(at(W_MASK, i), bit);
+    }
+  }
+  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
+    elem_i(l - L0, kind, base, mdb, ev, fl);
   }
   __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
 };
 
-template <int T>
+#define PUSH_OUT(rec)             \
+  do {                            \
+    if (nout == 0) out0 = (rec);  \
+    else out1 = (rec);            \
+    ++nout;                       \
+  } while (0)
+
+// ABL (diagnostic builds only, selected by env GQ_ABLATE; results are wrong when != 0):
+//   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
+//   8 = skip the MD-event pass.
+template <int T, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
                                                         int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
                                                         unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
                                                         unsigned long long cplx_cap, Counters *ctr) {
-  __shared__ uint32_t cnt[C_NCAT * T];
+  constexpr int S = T + 2 * kGuard;
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   const Tile tl = tiles[blockIdx.x];
   const int32_t L0 = tl.L0, L1 = tl.L1;
-  for (int i = threadIdx.x; i < C_NCAT * T; i += blockDim.x) cnt[i] = 0u;
+  // a window of >= 65535 reads could overflow the 16-bit counters: queue every locus of
+  // the tile for the exact (32-bit) kernel instead
+  const bool wide = (tl.re - tl.rb) >= 65535;
+  if (!wide) {
+    uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+    for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    GermSink<T, ABL> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+    if (!(ABL & 1))
+      for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, L0, L1, sink);
+  }
   __syncthreads();
-
-  GermSink<T> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwaves = blockDim.x >> 6;
-  for (int64_t r = tl.rb + wave; r < tl.re; r += nwaves) walk_read(R, r, L0, L1, sink);
-  __syncthreads();
+  if (ABL & 2) {
+    if (threadIdx.x == 0) atomicAdd(&ctr->visited, (unsigned long long)cnt[kGuard + (blockIdx.x & 63)]);
+    return;
+  }
 
   const bool multi_sample = R.n_samples > 1;
   unsigned visited = 0, amb = 0, ties = 0;
@@ -193,58 +305,61 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
   // uniform trip count so every wave reaches the wave-level reservations together
   for (int i0 = 0; i0 < nloci; i0 += blockDim.x) {
     const int i = i0 + threadIdx.x;
-    CallRec out[2];
+    CallRec out0, out1;  // named (not an array): no scratch
     unsigned nout = 0;
     bool to_complex = false;
-    if (i < nloci) {
-      uint32_t c[5];
-      uint32_t depth = 0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        c[k] = cnt[k * T + i];
-        depth += c[k];
-      }
-      const uint32_t cx = cnt[C_CPLX * T + i];
-      depth += cx;
+    if (wide && i < nloci) {
+      to_complex = true;
+    } else if (i < nloci) {
+      const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
+                     wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
+      const uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
+      const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
+      const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
       if (depth > 0) {
         ++visited;
-        uint32_t mask = cnt[C_MASK * T + i];
+        uint32_t mask = cnt[W_MASK * S + kGuard + i];
+        const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
+        const uint32_t ev[4] = {eac & 0xFFFFu, eac >> 16, etg & 0xFFFFu, etg >> 16};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (c[k] > cnt[(C_EVA + k) * T + i]) mask |= 1u << k;
+          if (c[k] > ev[k]) mask |= 1u << k;
         const bool ambiguous = __popc(mask) > 1;
         if (ambiguous) ++amb;
         if (ambiguous || cx > 0 || multi_sample) {
           to_complex = true;
         } else {
-          // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles
+          // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles.
+          // Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of
+          // Allele(ref, alt) for one ref is the alt byte order A < C < G < N < T, i.e. the
+          // categories 0, 1, 3, 4, 2.  Sorting keys descending = sortBy(-count), ties canonical.
           const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-          const uint8_t bases[5] = {'A', 'C', 'G', 'T', 'N'};
-          // canonical order for ties: Allele(ref, alt) compares alt bytes => A < C < G < N < T
-          const int order[5] = {0, 1, 2, 4, 3};
-          int top[3] = {-1, -1, -1};
+          uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
           int npass = 0;
-          for (int oi = 0; oi < 5; ++oi) {
-            const int k = order[oi];
-            if (c[k] == 0) continue;
-            if ((long long)c[k] * 100 / (long long)depth <= threshold) continue;
+#pragma unroll
+          for (int rank = 0; rank < 5; ++rank) {
+            const int cat = (0x24310 >> (4 * rank)) & 0xF;
+            const uint32_t cc = c[cat];
+            if (cc == 0 || (long long)cc * 100 / (long long)depth <= threshold) continue;
             ++npass;
-            // insert into top-3 by count desc (stable w.r.t. canonical order)
-            int p = (npass - 1 < 3) ? npass - 1 : 3;
-            while (p > 0 && c[top[p - 1]] < c[k]) {
-              if (p < 3) top[p] = top[p - 1];
-              --p;
-            }
-            if (p < 3) top[p] = k;
+            uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
+            // insert into (k0 >= k1 >= k2)
+            if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
+            if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
+            if (key > k2) { k2 = key; }
           }
-          const bool tie = npass >= 2 && (c[top[0]] == c[top[1]] || (npass >= 3 && c[top[1]] == c[top[2]]));
+          auto key_base = [](uint32_t key) -> uint8_t {
+            const int rank = 255 - (int)(key & 0xFFu);
+            return cat_base((0x24310 >> (4 * rank)) & 0xF);
+          };
+          const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
           if (tie) ++ties;
           const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
           const int32_t pos = L0 + i;
           const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
           auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
             CallRec rr;
-            rr.key = (ord << 12) | ((uint64_t)0 << 4) | (uint64_t)sub;
+            rr.key = (ord << 12) | (uint64_t)sub;
             rr.contig = tl.contig;
             rr.pos = pos;
             rr.sample = 0;
@@ -252,29 +367,30 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
             rr.gt1 = g1;
             rr.flags = fl;
             rr.ref_len = 1;
-            if (alt_sym) {
-              const uint8_t sym[5] = {'<', 'A', 'L', 'T', '>'};
+            if (alt_sym) {  // (ref, "<ALT>")
               rr.alt_len = 5;
-              rr.allele = pack_inline(ref, sym, 5);
+              rr.allele = (uint64_t)ref | ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                          ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
             } else {
               rr.alt_len = 1;
-              rr.allele = pack_inline(ref, &alt1, 1);
+              rr.allele = (uint64_t)ref | ((uint64_t)alt1 << 8);
             }
             return rr;
           };
+          const uint8_t b0 = key_base(k0), b1 = key_base(k1);
           if (npass == 0) {
-            if (emit_no_call) out[nout++] = mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0);
-          } else if (npass == 1 && bases[top[0]] == ref) {
-            if (emit_ref) out[nout++] = mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0);
+            if (emit_no_call) PUSH_OUT(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
+          } else if (npass == 1 && b0 == ref) {
+            if (emit_ref) PUSH_OUT(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
           } else if (npass == 1) {
-            out[nout++] = mk(GQ_GT_ALT, GQ_GT_ALT, bases[top[0]], false, 0);
+            PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
           } else {
-            const bool v1 = bases[top[0]] != ref, v2 = bases[top[1]] != ref;
+            const bool v1 = b0 != ref, v2 = b1 != ref;
             if (v1 != v2) {
-              out[nout++] = mk(GQ_GT_REF, GQ_GT_ALT, v1 ? bases[top[0]] : bases[top[1]], false, 0);
+              PUSH_OUT(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
             } else if (v1 && v2) {
-              out[nout++] = mk(GQ_GT_ALT, GQ_GT_OTHERALT, bases[top[0]], false, 0);
-              out[nout++] = mk(GQ_GT_ALT, GQ_GT_OTHERALT, bases[top[1]], false, 1);
+              PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
+              PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
             }
             // two non-variant single-base alleles cannot occur (all Match alleles share ref)
           }
@@ -283,10 +399,10 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
     }
     // reserve + write records (wave-aggregated)
     const unsigned long long base = wave_reserve(&ctr->n_rec, nout);
-    for (unsigned k = 0; k < nout; ++k)
-      if (base + k < rec_cap) recs[base + k] = out[k];
+    if (nout > 0 && base < rec_cap) recs[base] = out0;
+    if (nout > 1 && base + 1 < rec_cap) recs[base + 1] = out1;
     const unsigned long long cb = wave_reserve(&ctr->n_complex, to_complex ? 1u : 0u);
-    if (to_complex && cb < cplx_cap) cplx[cb] = ComplexItem{(int32_t)blockIdx.x, L0 + i};
+    if (to_complex && cb < cplx_cap) cplx[cb] = ComplexItem{(int32_t)blockIdx.x, L0 + i, wide ? 1 : 0};
   }
   // block-level reduction of run counters
   __shared__ unsigned red[3];
@@ -681,6 +797,15 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
       raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_CAPACITY, pos);
       continue;
     }
+    if (item.flags & 1) {  // queued from a wide tile: count the visit here
+      uint32_t tot = 0;
+      for (int sm = 0; sm < 8; ++sm) tot += sample_total[sm];
+      if (tot == 0) continue;
+      if (lane == 0) {
+        atomicAdd(&ctr->visited, 1ull);
+        if (ambiguous) atomicAdd(&ctr->ambiguous, 1ull);
+      }
+    }
     // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
     const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
     for (int sm = 0; sm < 8; ++sm) {
@@ -820,8 +945,8 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
 // ------------------------------------------------------------------------------------------
 // counts_tile: dense raw histogram (gq_pileup_counts)
 // ------------------------------------------------------------------------------------------
-enum : int { K2_A = 0, K2_C, K2_G, K2_T, K2_N, K2_O, K2_INS, K2_DEL, K2_MID, K2_CLIP, K2_POS, K2_MASK, K2_EVA, K2_EVC,
-             K2_EVG, K2_EVT, K2_NCAT };
+enum : int { K2_A = 0, K2_C, K2_T, K2_G, K2_N, K2_O, K2_INS, K2_DEL, K2_MID, K2_CLIP, K2_POS, K2_MASK, K2_EVA, K2_EVC,
+             K2_EVT, K2_EVG, K2_NCAT };  // base_cat order
 
 template <int T>
 struct CountSink {
@@ -830,7 +955,19 @@ struct CountSink {
   int *err;
   long long *err_pos;
   __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
-    const int i = l - L0;
+    elem_i(l - L0, kind, base, mdb, ev, fl);
+  }
+  __device__ __forceinline__ void bases4(int i, uint32_t w, uint32_t valid4, uint8_t fl) {
+    for (int j = 0; j < 4; ++j)
+      if (((valid4 >> j) & 1u) && i + j >= 0 && i + j < T) elem_i(i + j, K_SNV, (uint8_t)(w >> (8 * j)), 0, false, fl);
+  }
+  __device__ __forceinline__ void event_i(int i, uint8_t b, uint8_t m, uint8_t) {
+    const int bc = base_cat(b);
+    if (bc < 4) atomicAdd(&cnt[(K2_EVA + bc) * T + i], 1u);
+    const uint32_t bit = std_bit(m);
+    if (bit) atomicOr(&cnt[K2_MASK * T + i], bit);
+  }
+  __device__ __forceinline__ void elem_i(int i, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
     int c;
     switch (kind) {
       case K_SNV: c = base_cat(base); break;
@@ -865,8 +1002,7 @@ __global__ __launch_bounds__(kBlock) void counts_tile(const Tile *__restrict__ t
   for (int i = threadIdx.x; i < K2_NCAT * T; i += blockDim.x) cnt[i] = 0u;
   __syncthreads();
   CountSink<T> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int64_t r = tl.rb + wave; r < tl.re; r += (blockDim.x >> 6)) walk_read(R, r, L0, L1, sink);
+  for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, L0, L1, sink);
   __syncthreads();
   for (int i = threadIdx.x; i < L1 - L0; i += blockDim.x) {
     const int64_t o = tl.ordinal0 + i;
@@ -878,7 +1014,8 @@ __global__ __launch_bounds__(kBlock) void counts_tile(const Tile *__restrict__ t
     const uint8_t rb = mask ? bit_base(mask) : (uint8_t)'N';
     depth[o] = (int32_t)dsum;
     pos_depth[o] = (int32_t)cnt[K2_POS * T + i];
-    for (int k = 0; k < 6; ++k) base_counts[o * 6 + k] = (int32_t)cnt[k * T + i];
+    const int out_order[6] = {K2_A, K2_C, K2_G, K2_T, K2_N, K2_O};  // output: A C G T N other
+    for (int k = 0; k < 6; ++k) base_counts[o * 6 + k] = (int32_t)cnt[out_order[k] * T + i];
     for (int k = 0; k < 4; ++k) indel_counts[o * 4 + k] = (int32_t)cnt[(K2_INS + k) * T + i];
     ref_depth[o] = (int32_t)cnt[base_cat(rb) * T + i];
     ref_base[o] = rb;
@@ -982,6 +1119,23 @@ static gq_status validate_reads(const gq_reads *h) {
   return GQ_OK;
 }
 
+static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
+  void *p = nullptr, *q = nullptr;
+  HIP_TRY(hipMalloc(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
+  d->owned.push_back(p);
+  HIP_TRY(hipMalloc(&q, (size_t)std::max<int64_t>(md_len, 16)));
+  d->owned.push_back(q);
+  d->d.lead = (const int16_t *)p;
+  d->d.ev_rb = (const uint8_t *)q;
+  if (d->d.n_reads > 0) {
+    const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GQ_OK;
+}
+
 gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   if (!c || !out) return set_err(GQ_E_ARG, "gq_reads_upload: null argument");
   gq_status st = validate_reads(h);
@@ -1028,14 +1182,15 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   UP(md_ev, h->md_len, uint32_t);
 #undef UP
   d->d.n_reads = n;
+  d->d.seq_bytes = h->seq_bytes;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
   d->seq_bytes = h->seq_bytes;
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e != hipSuccess) {
+  gq_status st2 = derive_shape(c, d, h->md_len);
+  if (st2) {
     gq_reads_free(d);
-    return set_err(GQ_E_HIP, "upload sync: %s", hipGetErrorString(e));
+    return st2;
   }
   *out = d;
   return GQ_OK;
@@ -1048,6 +1203,7 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   gq_dev_reads *d = new gq_dev_reads();
   d->ctx = c;
   d->d.n_reads = h->n_reads;
+  d->d.seq_bytes = h->seq_bytes;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->d.contig_read_begin = h->contig_read_begin;
@@ -1076,6 +1232,11 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
     return set_err(GQ_E_HIP, "wrap: contig_read_begin D2H: %s", hipGetErrorString(e));
   }
   d->seq_bytes = h->seq_bytes;
+  gq_status st2 = derive_shape(c, d, h->md_len);
+  if (st2) {
+    gq_reads_free(d);
+    return st2;
+  }
   *out = d;
   return GQ_OK;
 }
@@ -1150,8 +1311,21 @@ extern "C++" template <int T>
 static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p, CallRec *recs,
                             unsigned long long rec_cap, ComplexItem *cplx, unsigned long long cplx_cap,
                             Counters *ctr) {
-  hipLaunchKernelGGL((germline_tile<T>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                     R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, cplx_cap, ctr);
+  static const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
+#define GQ_LAUNCH(A)                                                                                             \
+  hipLaunchKernelGGL((germline_tile<T, A>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,                   \
+                     (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, \
+                     cplx_cap, ctr)
+  switch (abl) {
+    case 1: GQ_LAUNCH(1); break;
+    case 2: GQ_LAUNCH(2); break;
+    case 4: GQ_LAUNCH(4); break;
+    case 8: GQ_LAUNCH(8); break;
+    case 12: GQ_LAUNCH(12); break;
+    case 14: GQ_LAUNCH(14); break;
+    default: GQ_LAUNCH(0); break;
+  }
+#undef GQ_LAUNCH
 }
 
 gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,

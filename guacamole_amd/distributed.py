@@ -1,0 +1,71 @@
+"""Multi-GPU driver pieces: static LociSet split across ranks + one terminal gather.
+
+Loci ranges shard embarrassingly (each locus depends only on reads overlapping it,
+DistributedUtil.scala:585-597 with halfWindowSize = 0), so every rank runs the
+pileup engine on its own contiguous loci range with no data-path collective.
+The single exchange is the end-of-job gather of the per-rank genotype buffers to
+rank 0: sizes are all-gathered, then each rank's packed
+buffer goes to rank 0 over RCCL (backend "nccl" on ROCm) — or gloo on CPU tests.
+Rank 0 concatenates in rank order = partition order.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .loci import LociMapBuilder, LociSet, partition_loci_uniformly
+
+
+def rank_info() -> Tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def split_loci(loci: LociSet, world: int) -> List[LociSet]:
+    """Static contiguous split of a LociSet into `world` parts in partition order
+    (partitionLociUniformly with tasks = world, DistributedUtil.scala:83-108)."""
+    inv = partition_loci_uniformly(world, loci).as_inverse_map()
+    return [inv.get(r, LociSet()) for r in range(world)]
+
+
+def pack_rows(rows: Sequence[tuple]) -> np.ndarray:
+    """Genotype rows -> one uint8 buffer (tab-separated lines)."""
+    text = "".join("%s\t%d\t%d\t%s,%s\t%s\t%s\t%d\n" % (c, l, s, g[0], g[1], r, a, f) for c, l, s, g, r, a, f in rows)
+    return np.frombuffer(text.encode("latin-1"), dtype=np.uint8).copy()
+
+
+def unpack_rows(buf: np.ndarray) -> List[tuple]:
+    out = []
+    for line in bytes(buf).decode("latin-1").splitlines():
+        c, l, s, g, r, a, f = line.split("\t")
+        out.append((c, int(l), int(s), tuple(g.split(",")), r, a, int(f)))
+    return out
+
+
+def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[List[np.ndarray]]:
+    """Variable-size gather of one uint8 buffer per rank to rank 0.
+
+    device: torch device for the collective ("cuda:k" => RCCL over xGMI; None => CPU/gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [buf]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = torch.device(device) if device else torch.device("cpu")
+    n = torch.tensor([int(buf.size)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(1, max(sizes))
+    mine = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    if buf.size:
+        mine[:buf.size] = torch.from_numpy(buf).to(dev)
+    if rank == 0:
+        parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
+        dist.gather(mine, gather_list=parts, dst=0)
+        return [parts[r][:sizes[r]].cpu().numpy() for r in range(world)]
+    dist.gather(mine, dst=0)
+    return None

@@ -235,12 +235,11 @@ class DeviceReads:
 
 
 class GermlineCalls:
-    """Germline genotype records in output order."""
+    """Germline genotype records in output order (numpy arrays; allele strings on demand)."""
 
-    def __init__(self, contig, pos, sample, gt0, gt1, flags, ref, alt, visited, complex_loci, ambiguous, ties):
-        self.contig, self.pos, self.sample = contig, pos, sample
-        self.gt0, self.gt1, self.flags = gt0, gt1, flags
-        self.ref, self.alt = ref, alt
+    def __init__(self, arrays: Dict[str, np.ndarray], pool: bytes, visited, complex_loci, ambiguous, ties):
+        self.a = arrays
+        self.pool = pool
         self.visited_loci, self.complex_loci, self.ambiguous_loci, self.tie_loci = visited, complex_loci, ambiguous, ties
 
     @staticmethod
@@ -250,18 +249,44 @@ class GermlineCalls:
         def arr(p):
             return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.int64)
 
-        pool = bytes(np.ctypeslib.as_array(c.allele_pool, shape=(c.pool_len,))) if c.pool_len else b""
-        ro, rl, ao, al = arr(c.ref_off), arr(c.ref_len), arr(c.alt_off), arr(c.alt_len)
-        ref = [pool[ro[i]:ro[i] + rl[i]].decode("latin-1") for i in range(n)]
-        alt = [pool[ao[i]:ao[i] + al[i]].decode("latin-1") for i in range(n)]
-        return GermlineCalls(arr(c.contig), arr(c.pos), arr(c.sample), arr(c.gt0), arr(c.gt1), arr(c.flags), ref, alt,
-                             c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
+        pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
+        a = {k: arr(getattr(c, k)) for k in ("contig", "pos", "sample", "gt0", "gt1", "flags", "ref_off", "ref_len",
+                                            "alt_off", "alt_len")}
+        return GermlineCalls(a, pool, c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
 
     def __len__(self) -> int:
-        return len(self.ref)
+        return int(self.a["pos"].shape[0])
+
+    def ref(self, i: int) -> str:
+        o = int(self.a["ref_off"][i])
+        return self.pool[o:o + int(self.a["ref_len"][i])].decode("latin-1")
+
+    def alt(self, i: int) -> str:
+        o = int(self.a["alt_off"][i])
+        return self.pool[o:o + int(self.a["alt_len"][i])].decode("latin-1")
+
+    def pack(self) -> np.ndarray:
+        """Flat uint8 buffer (fixed-width fields + allele pool) for the multi-GPU gather."""
+        parts = [np.array([len(self), len(self.pool)], np.int64).view(np.uint8)]
+        parts += [np.ascontiguousarray(self.a[k]).view(np.uint8) for k in sorted(self.a)]
+        parts.append(np.frombuffer(self.pool, dtype=np.uint8))
+        return np.concatenate(parts)
+
+    @staticmethod
+    def unpack(buf: np.ndarray) -> "GermlineCalls":
+        n, pl = (int(x) for x in buf[:16].view(np.int64))
+        dt = {"contig": np.int32, "pos": np.int64, "sample": np.uint8, "gt0": np.uint8, "gt1": np.uint8,
+              "flags": np.uint8, "ref_off": np.int64, "ref_len": np.int32, "alt_off": np.int64, "alt_len": np.int32}
+        off, a = 16, {}
+        for k in sorted(dt):
+            nb = n * np.dtype(dt[k]).itemsize
+            a[k] = buf[off:off + nb].copy().view(dt[k])
+            off += nb
+        return GermlineCalls(a, bytes(buf[off:off + pl]), 0, 0, 0, 0)
 
     def tuples(self, contig_names: Sequence[str]) -> List[tuple]:
         """(contig, locus, sample, (gt0, gt1), ref, alt, flags) — same shape as the oracle's rows."""
-        return [(contig_names[self.contig[i]], int(self.pos[i]), int(self.sample[i]),
-                 (GT_NAMES[int(self.gt0[i])], GT_NAMES[int(self.gt1[i])]), self.ref[i], self.alt[i],
-                 int(self.flags[i])) for i in range(len(self))]
+        a = self.a
+        return [(contig_names[a["contig"][i]], int(a["pos"][i]), int(a["sample"][i]),
+                 (GT_NAMES[int(a["gt0"][i])], GT_NAMES[int(a["gt1"][i])]), self.ref(i), self.alt(i),
+                 int(a["flags"][i])) for i in range(len(self))]
