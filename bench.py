@@ -84,13 +84,15 @@ def main() -> int:
     for _ in range(args.warmup):
         step()
     barrier()
-    pileup_ms, total_ms = [], []
+    pileup_ms, total_ms, host_ms, marshal_ms = [], [], [], []
     t = time.perf_counter()
     for _ in range(args.steps):
         calls = step()
         tm = ctx.timings()
         pileup_ms.append(tm["pileup_ms"])
         total_ms.append(tm["total_ms"])
+        host_ms.append(tm["host_ms"])
+        marshal_ms.append(tm["marshal_ms"])
     barrier()
     elapsed = time.perf_counter() - t
     if dist is not None:
@@ -143,6 +145,8 @@ def main() -> int:
                      "kernel": "germline_tile", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg},
         "kernel_only_loci_per_s": visited / (k_ms * 1e-3),
         "device_total_ms": float(np.mean(total_ms)),
+        "host_call_ms": float(np.mean(host_ms)),
+        "host_marshal_ms": float(np.mean(marshal_ms)),
         "calls": len(calls),
         "complex_loci": int(calls.complex_loci),
         "ambiguous_loci": int(calls.ambiguous_loci),

@@ -39,6 +39,7 @@ struct DevReads {
   const uint8_t *seq, *qual;
   const uint32_t *cigar, *md_ev;
   int64_t seq_bytes;
+  int64_t seq_cap;  // readable bytes of the device seq allocation (>= seq_bytes; padded on upload)
   // derived at upload (read_shape):
   const int16_t *lead;   // leading soft clip of a [S|H]*(M|=|X)[S|H]* CIGAR, -1 otherwise
   const uint8_t *ev_rb;  // per MD event: the read's sequenced base at that position (0 for deletions)
@@ -106,6 +107,13 @@ __device__ __forceinline__ int md_find(const uint32_t *ev, int32_t n, int32_t of
   return -1;
 }
 
+// Bytes [b0, b1) of the sequence pool staged in LDS at `lds` (b0 16-aligned); empty when
+// b1 <= b0.  A read whose chunk range lies inside is read from LDS, others from HBM.
+struct StageView {
+  const uint4 *lds;
+  int64_t b0, b1;
+};
+
 // Fast path of walk_read_lane for CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming
 // op: every element is a Match/Mismatch).  Two passes:
 //   1. bases: the read's bytes over [max(s,L0), min(e,L1)) stream in as 16-byte aligned
@@ -117,7 +125,7 @@ __device__ __forceinline__ int md_find(const uint32_t *ev, int32_t n, int32_t of
 template <class Sink>
 __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_t e, int32_t lead, int64_t seq_off,
                                             int32_t nmd, int64_t md_off, int32_t L0, int32_t L1, uint8_t fl,
-                                            Sink &sink) {
+                                            Sink &sink, const StageView &sv) {
   const int32_t a = s > L0 ? s : L0;
   const int32_t b = e < L1 ? e : L1;
   const int64_t p0 = seq_off + lead + (a - s);
@@ -133,17 +141,8 @@ __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_
     e4[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
     b4[k] = k < nmd ? evb[k] : 0u;
   }
-  if (cb0 + 16 * (int64_t)nchunks > R.seq_bytes) {  // last read of the pool: byte loads
-    for (int64_t p = p0; p < p1; ++p) {
-      const int32_t i = ioff + (int32_t)(p - cb0);
-      const int32_t sh = (int32_t)((p - cb0) & 3) * 8;
-      sink.bases4(i - (sh >> 3), (uint32_t)R.seq[p] << sh, 1u << (sh >> 3), fl);
-    }
-  } else {
-    auto ld = [&](int q) -> uint4 {  // clamped to the read's last chunk: every load in bounds
-      const int qc = q < nchunks ? q : nchunks - 1;
-      return *reinterpret_cast<const uint4 *>(R.seq + cb0 + 16 * (int64_t)qc);
-    };
+  const int64_t cend = cb0 + 16 * (int64_t)nchunks;
+  auto run = [&](auto ld) {  // ld(q): chunk q, clamped to the read's last chunk (every load in bounds)
     const int32_t lo0 = (int32_t)(p0 - cb0);  // first valid byte of chunk 0
     uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
     for (int q = 0; q < nchunks; ++q) {
@@ -161,6 +160,19 @@ __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_
       c2 = c3;
       c3 = ld(q + 4);
     }
+  };
+  if (cb0 >= sv.b0 && cend <= sv.b1) {  // staged in LDS
+    const uint4 *base = sv.lds + ((cb0 - sv.b0) >> 4);
+    run([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
+  } else if (cend > R.seq_cap) {  // last read of an unpadded pool: byte loads
+    for (int64_t p = p0; p < p1; ++p) {
+      const int32_t i = ioff + (int32_t)(p - cb0);
+      const int32_t sh = (int32_t)((p - cb0) & 3) * 8;
+      sink.bases4(i - (sh >> 3), (uint32_t)R.seq[p] << sh, 1u << (sh >> 3), fl);
+    }
+  } else {
+    const uint4 *base = reinterpret_cast<const uint4 *>(R.seq + cb0);
+    run([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
   }
   // MD events inside [a - s, b - s): mismatching reference bases on this read
   for (int k = 0; k < nmd; ++k) {
@@ -182,7 +194,8 @@ __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_
 // Fast path: CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming op), bases
 // read as 16-byte aligned chunks.  General path: any CIGAR, byte loads.
 template <class Sink>
-__device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1, Sink &sink) {
+__device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1, Sink &sink,
+                                               const StageView &sv = StageView{nullptr, 0, 0}) {
   const int32_t s = R.start[r];
   const int32_t e = R.end[r];
   if (e <= L0 || s >= L1) return;
@@ -200,7 +213,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
 
   const int32_t lead = R.lead[r];
   if (lead >= 0) {
-    walk_simple(R, s, e, lead, seq_off, nmd, R.md_off[r], L0, L1, fl, sink);
+    walk_simple(R, s, e, lead, seq_off, nmd, R.md_off[r], L0, L1, fl, sink, sv);
     return;
   }
 

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -58,6 +59,8 @@ gq_status set_err(gq_status s, const char *fmt, ...) {
 constexpr int kBlock = 256;
 constexpr int kGermT = 1024;  // loci per germline tile
 constexpr int kCountT = 512;  // loci per counts tile
+constexpr int kStageBytes = 40 * 1024;
+constexpr size_t kSeqPad = 2048;  // zeroed tail of the uploaded sequence pool  // LDS staging of a read batch's sequence bytes
 
 // ------------------------------------------------------------------------------------------
 // Tile planning
@@ -168,10 +171,14 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   int err;
   int pad;
   long long err_pos;
+  // per-tile run counters of germline_tile, spread over kSpread addresses (summed on the host)
+  unsigned long long spread[3][64];
 };
+constexpr int kSpread = 64;
 
 // Wave-aggregated reservation of `n` slots on a global counter.
 __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *ctr, unsigned n) {
+  if (__ballot(n != 0) == 0) return 0;  // nothing to reserve in this wave (the common case)
   const int lane = threadIdx.x & 63;
   // inclusive scan of n across the wave
   unsigned x = n;
@@ -273,25 +280,51 @@ struct GermSink {
 // ABL (diagnostic builds only, selected by env GQ_ABLATE; results are wrong when != 0):
 //   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
 //   8 = skip the MD-event pass.
-template <int T, int ABL = 0>
+template <int T, int ABL = 0, int STAGE = 0>
 __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
                                                         int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
                                                         unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
                                                         unsigned long long cplx_cap, Counters *ctr) {
   constexpr int S = T + 2 * kGuard;
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
+  __shared__ __attribute__((aligned(16))) uint4 stage[STAGE ? STAGE / 16 : 1];
   const Tile tl = tiles[blockIdx.x];
   const int32_t L0 = tl.L0, L1 = tl.L1;
   // a window of >= 65535 reads could overflow the 16-bit counters: queue every locus of
   // the tile for the exact (32-bit) kernel instead
   const bool wide = (tl.re - tl.rb) >= 65535;
   if (!wide) {
-    uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
-    for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
     GermSink<T, ABL> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-    if (!(ABL & 1))
-      for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, L0, L1, sink);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    // Reads are walked in batches of up to blockDim.x (one per lane).  A batch's reads
+    // sit in one contiguous byte range of the sequence pool (reads are stored in
+    // alignment order), which is copied into LDS by LDS-DMA (global_load_lds_dwordx4,
+    // 1 KiB per wave-instruction, fully coalesced) while the counters are zeroed; the
+    // lanes then read their bases from LDS instead of issuing scattered 16-byte loads.
+    for (int64_t r0 = tl.rb; r0 < tl.re || r0 == tl.rb; r0 += blockDim.x) {
+      const int64_t nb = min((int64_t)blockDim.x, tl.re - r0);
+      int64_t B0 = 0, n1k = 0;
+      if (STAGE && nb > 0) {
+        B0 = R.seq_off[r0] & ~(int64_t)15;
+        const int64_t B1 = R.seq_off[r0 + nb - 1] + R.seq_len[r0 + nb - 1];
+        n1k = B1 > B0 ? (B1 - B0 + 1023) >> 10 : 0;
+        if (n1k * 1024 > STAGE || B0 + n1k * 1024 > R.seq_cap) n1k = 0;  // not staged: HBM loads
+      }
+      if (!(ABL & 1))
+        for (int64_t q = wave; q < n1k; q += nwaves)
+          __builtin_amdgcn_global_load_lds((const void *)(R.seq + B0 + q * 1024 + lane * 16),
+                                           (__attribute__((address_space(3))) void *)(stage + q * 64), 16, 0, 0);
+      if (r0 == tl.rb) {
+        uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+        for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      if (STAGE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const StageView sv{stage, B0, B0 + n1k * 1024};
+      if (!(ABL & 1) && (int64_t)threadIdx.x < nb) walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink, sv);
+      __syncthreads();  // counters complete / stage free for the next batch
+      if (nb <= 0) break;
+    }
   }
   __syncthreads();
   if (ABL & 2) {
@@ -330,10 +363,33 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
           to_complex = true;
         } else {
           // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles.
+          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+          const int rc = mask ? (__ffs((int)mask) - 1) : 4;  // select chain: no dynamic register indexing
+          const uint32_t c_ref = rc == 0 ? c[0] : rc == 1 ? c[1] : rc == 2 ? c[2] : rc == 3 ? c[3] : c[4];
+          if ((long long)(depth - c_ref) * 100 / (long long)depth <= threshold) {
+            // fast path: every non-reference allele has count <= depth - c_ref, so none
+            // passes the threshold; the call is HomRef if the reference allele passes,
+            // else NoCall (same outcome as the general case split below)
+            const int32_t pos = L0 + i;
+            const bool ref_pass = c_ref > 0 && (long long)c_ref * 100 / (long long)depth > threshold;
+            if (ref_pass ? emit_ref : emit_no_call) {
+              CallRec rr;
+              rr.key = (uint64_t)(tl.ordinal0 + i) << 12;
+              rr.contig = tl.contig;
+              rr.pos = pos;
+              rr.sample = 0;
+              rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
+              rr.flags = 0;
+              rr.ref_len = 1;
+              rr.alt_len = 5;
+              rr.allele = (uint64_t)ref | ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                          ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+              PUSH_OUT(rr);
+            }
+          } else {
           // Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of
           // Allele(ref, alt) for one ref is the alt byte order A < C < G < N < T, i.e. the
           // categories 0, 1, 3, 4, 2.  Sorting keys descending = sortBy(-count), ties canonical.
-          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
           uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
           int npass = 0;
 #pragma unroll
@@ -394,6 +450,7 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
             }
             // two non-variant single-base alleles cannot occur (all Match alleles share ref)
           }
+          }
         }
       }
     }
@@ -413,9 +470,10 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
   if (ties) atomicAdd(&red[2], ties);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (red[0]) atomicAdd(&ctr->visited, (unsigned long long)red[0]);
-    if (red[1]) atomicAdd(&ctr->ambiguous, (unsigned long long)red[1]);
-    if (red[2]) atomicAdd(&ctr->ties, (unsigned long long)red[2]);
+    const int sl = blockIdx.x & (kSpread - 1);
+    if (red[0]) atomicAdd(&ctr->spread[0][sl], (unsigned long long)red[0]);
+    if (red[1]) atomicAdd(&ctr->spread[1][sl], (unsigned long long)red[1]);
+    if (red[2]) atomicAdd(&ctr->spread[2][sl], (unsigned long long)red[2]);
   }
 }
 
@@ -1023,6 +1081,72 @@ __global__ __launch_bounds__(kBlock) void counts_tile(const Tile *__restrict__ t
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Result image: the gq_calls arrays built on device in output order (one D2H copy)
+// ------------------------------------------------------------------------------------------
+struct CallsLayout {  // byte offsets inside the image; header = int64 pool_len
+  size_t contig, pos, ref_off, alt_off, ref_len, alt_len, sample, gt0, gt1, flags, pool, bytes;
+};
+static CallsLayout calls_layout(int64_t n, int64_t dev_pool_used) {
+  auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+  const size_t N = (size_t)n;
+  CallsLayout L;
+  L.contig = 64;
+  L.pos = al(L.contig + 4 * N);
+  L.ref_off = al(L.pos + 8 * N);
+  L.alt_off = al(L.ref_off + 8 * N);
+  L.ref_len = al(L.alt_off + 8 * N);
+  L.alt_len = al(L.ref_len + 4 * N);
+  L.sample = al(L.alt_len + 4 * N);
+  L.gt0 = al(L.sample + N);
+  L.gt1 = al(L.gt0 + N);
+  L.flags = al(L.gt1 + N);
+  L.pool = al(L.flags + N);
+  // inline alleles hold <= 8 bytes; longer ones live in the device pool (each used once)
+  L.bytes = al(L.pool + 8 * N + (size_t)dev_pool_used + 1);
+  return L;
+}
+
+__global__ void iota_i32(int32_t *__restrict__ v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (int32_t)i;
+}
+
+__global__ void calls_lengths(const CallRec *__restrict__ recs, const int32_t *__restrict__ order, int64_t n,
+                              int64_t *__restrict__ len) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const CallRec r = recs[order[k]];
+  len[k] = (int64_t)r.ref_len + (int64_t)r.alt_len;
+}
+
+__global__ void calls_image(const CallRec *__restrict__ recs, const int32_t *__restrict__ order,
+                            const int64_t *__restrict__ off, const uint8_t *__restrict__ dpool, int64_t n,
+                            CallsLayout L, uint8_t *__restrict__ img) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const CallRec r = recs[order[k]];
+  const int64_t o = off[k];
+  const int tot = (int)r.ref_len + (int)r.alt_len;
+  reinterpret_cast<int32_t *>(img + L.contig)[k] = r.contig;
+  reinterpret_cast<int64_t *>(img + L.pos)[k] = r.pos;
+  reinterpret_cast<int64_t *>(img + L.ref_off)[k] = o;
+  reinterpret_cast<int64_t *>(img + L.alt_off)[k] = o + r.ref_len;
+  reinterpret_cast<int32_t *>(img + L.ref_len)[k] = r.ref_len;
+  reinterpret_cast<int32_t *>(img + L.alt_len)[k] = r.alt_len;
+  img[L.sample + k] = r.sample;
+  img[L.gt0 + k] = r.gt0;
+  img[L.gt1 + k] = r.gt1;
+  img[L.flags + k] = r.flags;
+  uint8_t *dst = img + L.pool + o;
+  if (tot <= 8) {
+    for (int i = 0; i < tot; ++i) dst[i] = (uint8_t)(r.allele >> (8 * i));
+  } else {
+    for (int i = 0; i < tot; ++i) dst[i] = dpool[r.allele + i];
+  }
+  if (k == n - 1) *reinterpret_cast<int64_t *>(img) = o + tot;  // pool_len
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -1054,7 +1178,7 @@ struct gq_ctx {
   hipEvent_t ev[6] = {};
   gq_timings timings{};
   int germ_tile = kGermT;
-  DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp;
+  DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image;
   DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb;
 };
 
@@ -1090,7 +1214,7 @@ void gq_close(gq_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
-                    &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->c_depth, &c->c_pos,
+                    &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->c_depth, &c->c_pos,
                     &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
@@ -1144,24 +1268,30 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   gq_dev_reads *d = new gq_dev_reads();
   d->ctx = c;
   const int64_t n = h->n_reads;
-  auto up = [&](const void *src, size_t bytes, void **dst) -> hipError_t {
+  auto up = [&](const void *src, size_t bytes, void **dst, size_t pad) -> hipError_t {
     *dst = nullptr;
-    hipError_t e = hipMalloc(dst, std::max(bytes, (size_t)16));
+    hipError_t e = hipMalloc(dst, std::max(bytes + pad, (size_t)16));
     if (e != hipSuccess) return e;
     d->owned.push_back(*dst);
     if (bytes) e = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess && pad) e = hipMemsetAsync((char *)*dst + bytes, 0, pad, c->stream);
     return e;
   };
   void *p;
 #define UP(field, count, T)                                                     \
   do {                                                                          \
-    hipError_t _e = up(h->field, (size_t)(count) * sizeof(T), &p);              \
+    hipError_t _e = up(h->field, (size_t)(count) * sizeof(T), &p, pad_##field); \
     if (_e != hipSuccess) {                                                     \
       gq_reads_free(d);                                                         \
       return set_err(GQ_E_HIP, "upload %s: %s", #field, hipGetErrorString(_e)); \
     }                                                                           \
     d->d.field = (const T *)p;                                                  \
   } while (0)
+  // the sequence pool gets a zeroed tail so 1 KiB LDS-DMA pieces and 16-byte chunk loads
+  // past the last read stay inside the allocation (DevReads::seq_cap)
+  enum : size_t { pad_contig_read_begin = 0, pad_start = 0, pad_end = 0, pad_pmax_end = 0, pad_mapq = 0, pad_flags = 0,
+                  pad_sample = 0, pad_seq_off = 0, pad_seq_len = 0, pad_cigar_off = 0, pad_n_cigar = 0, pad_md_off = 0,
+                  pad_n_md = 0, pad_n_mismatch = 0, pad_seq = kSeqPad, pad_qual = 0, pad_cigar = 0, pad_md_ev = 0 };
   UP(contig_read_begin, h->n_contigs + 1, int64_t);
   UP(start, n, int32_t);
   UP(end, n, int32_t);
@@ -1183,6 +1313,7 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
 #undef UP
   d->d.n_reads = n;
   d->d.seq_bytes = h->seq_bytes;
+  d->d.seq_cap = h->seq_bytes + kSeqPad;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
@@ -1204,6 +1335,7 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   d->ctx = c;
   d->d.n_reads = h->n_reads;
   d->d.seq_bytes = h->seq_bytes;
+  d->d.seq_cap = h->seq_bytes;  // caller-owned buffer: no readable tail assumed
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->d.contig_read_begin = h->contig_read_begin;
@@ -1312,6 +1444,13 @@ static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const g
                             unsigned long long rec_cap, ComplexItem *cplx, unsigned long long cplx_cap,
                             Counters *ctr) {
   static const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
+  static const int stg = getenv("GQ_STAGE") ? atoi(getenv("GQ_STAGE")) : 0;
+  if (stg) {
+    hipLaunchKernelGGL((germline_tile<T, 0, kStageBytes>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
+                       cplx_cap, ctr);
+    return;
+  }
 #define GQ_LAUNCH(A)                                                                                             \
   hipLaunchKernelGGL((germline_tile<T, A>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,                   \
                      (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, \
@@ -1334,6 +1473,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   HIP_TRY(hipSetDevice(c->device));
   const int T = c->germ_tile;
   c->timings = gq_timings{};
+  const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
   gq_status st = plan(c, rd, loci, T, pl);
@@ -1393,82 +1533,82 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
       return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
     }
   }
+  for (int k = 0; k < kSpread; ++k) {
+    hc.visited += hc.spread[0][k];
+    hc.ambiguous += hc.spread[1][k];
+    hc.ties += hc.spread[2][k];
+  }
   st = check_device_error(c, hc);
   if (st) {
     free(res);
     return st;
   }
-  // ---- sort records by key (output order) on device
+  // ---- sort records by key (output order), then build the host result image on device:
+  //      one D2H copy of [header | SoA arrays | allele pool] instead of per-record marshalling
   const int64_t n = (int64_t)hc.n_rec;
-  HIP_TRY(c->keys.ensure((size_t)std::max<int64_t>(n, 1) * 8));
-  HIP_TRY(c->keys_sorted.ensure((size_t)std::max<int64_t>(n, 1) * 8));
-  HIP_TRY(c->idx.ensure((size_t)std::max<int64_t>(n, 1) * 4));
-  HIP_TRY(c->idx_sorted.ensure((size_t)std::max<int64_t>(n, 1) * 4));
-  std::vector<CallRec> hrec((size_t)n);
-  std::vector<int32_t> order((size_t)n);
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  HIP_TRY(c->keys.ensure(nn * 8));
+  HIP_TRY(c->keys_sorted.ensure(nn * 8));
+  HIP_TRY(c->idx.ensure(nn * 8));
+  HIP_TRY(c->idx_sorted.ensure(nn * 4));
+  const CallsLayout lay = calls_layout(n, (int64_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  HIP_TRY(c->image.ensure(lay.bytes));
   if (n > 0) {
+    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
     // keys are the first 8 bytes of each record: strided copy into a dense key array
     HIP_TRY(hipMemcpy2DAsync(c->keys.p, 8, c->recs.p, sizeof(CallRec), 8, (size_t)n, hipMemcpyDeviceToDevice,
                              c->stream));
-    {
-      std::vector<int32_t> iota((size_t)n);
-      for (int64_t i = 0; i < n; ++i) iota[(size_t)i] = (int32_t)i;
-      HIP_TRY(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-    }
+    hipLaunchKernelGGL(iota_i32, dim3(nb), dim3(kBlock), 0, c->stream, (int32_t *)c->idx.p, n);
+    HIP_TRY(hipGetLastError());
     int end_bit = 12;
     while (end_bit < 64 && ((uint64_t)pl.n_loci >> (end_bit - 12)) != 0) ++end_bit;
-    size_t tmp = 0;
+    size_t tmp = 0, tmp2 = 0;
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t *)c->keys.p, (uint64_t *)c->keys_sorted.p,
                                                (const int32_t *)c->idx.p, (int32_t *)c->idx_sorted.p, (int)n, 0,
                                                end_bit, c->stream));
-    HIP_TRY(c->sort_tmp.ensure(tmp));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p, (int)n,
+                                             c->stream));
+    HIP_TRY(c->sort_tmp.ensure(std::max(tmp, tmp2)));
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (const uint64_t *)c->keys.p,
                                                (uint64_t *)c->keys_sorted.p, (const int32_t *)c->idx.p,
                                                (int32_t *)c->idx_sorted.p, (int)n, 0, end_bit, c->stream));
-    HIP_TRY(hipMemcpyAsync(hrec.data(), c->recs.p, (size_t)n * sizeof(CallRec), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(order.data(), c->idx_sorted.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    // allele byte lengths in output order -> exclusive offsets into the pool
+    hipLaunchKernelGGL(calls_lengths, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const int32_t *)c->idx_sorted.p, n, (int64_t *)c->idx.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p,
+                                             (int)n, c->stream));
+    hipLaunchKernelGGL(calls_image, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const int32_t *)c->idx_sorted.p, (const int64_t *)c->keys.p, (const uint8_t *)c->pool.p, n,
+                       lay, (uint8_t *)c->image.p);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemsetAsync(c->image.p, 0, 64, c->stream));
   }
-  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
-  if (!hpool.empty())
-    HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  uint8_t *blk = (uint8_t *)malloc(lay.bytes);
+  if (!blk) {
+    free(res);
+    return set_err(GQ_E_NOMEM, "result block of %zu bytes", lay.bytes);
+  }
+  HIP_TRY(hipMemcpyAsync(blk, c->image.p, lay.bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipEventRecord(c->ev[4], c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  // ---- marshal into the result struct (output order)
+  // ---- point the result struct into the block (output order)
+  const auto h1 = std::chrono::steady_clock::now();
   res->n = n;
-  res->contig = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
-  res->pos = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
-  res->sample = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
-  res->gt0 = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
-  res->gt1 = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
-  res->flags = (uint8_t *)malloc((size_t)std::max<int64_t>(n, 1));
-  res->ref_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
-  res->alt_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
-  res->ref_len = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
-  res->alt_len = (int32_t *)malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
-  std::vector<uint8_t> apool;
-  apool.reserve((size_t)n * 3 + 16);
-  for (int64_t k = 0; k < n; ++k) {
-    const CallRec &r = hrec[(size_t)order[(size_t)k]];
-    res->contig[k] = r.contig;
-    res->pos[k] = r.pos;
-    res->sample[k] = r.sample;
-    res->gt0[k] = r.gt0;
-    res->gt1[k] = r.gt1;
-    res->flags[k] = r.flags;
-    res->ref_len[k] = r.ref_len;
-    res->alt_len[k] = r.alt_len;
-    res->ref_off[k] = (int64_t)apool.size();
-    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
-    if (r.ref_len + r.alt_len <= 8) {
-      for (int i = 0; i < r.ref_len + r.alt_len; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
-    } else {
-      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele,
-                   hpool.begin() + (ptrdiff_t)(r.allele + r.ref_len + r.alt_len));
-    }
-  }
-  res->pool_len = (int64_t)apool.size();
-  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
-  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  res->block_ = blk;
+  res->contig = (int32_t *)(blk + lay.contig);
+  res->pos = (int64_t *)(blk + lay.pos);
+  res->ref_off = (int64_t *)(blk + lay.ref_off);
+  res->alt_off = (int64_t *)(blk + lay.alt_off);
+  res->ref_len = (int32_t *)(blk + lay.ref_len);
+  res->alt_len = (int32_t *)(blk + lay.alt_len);
+  res->sample = blk + lay.sample;
+  res->gt0 = blk + lay.gt0;
+  res->gt1 = blk + lay.gt1;
+  res->flags = blk + lay.flags;
+  res->allele_pool = blk + lay.pool;
+  res->pool_len = *(const int64_t *)blk;
   res->visited_loci = (int64_t)hc.visited;
   res->complex_loci = (int64_t)hc.n_complex;
   res->ambiguous_loci = (int64_t)hc.ambiguous;
@@ -1487,23 +1627,16 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   c->timings.total_ms = ms;
   c->timings.pileup_launches = 1;
   c->timings.tiles = pl.n_tiles;
+  const auto h2 = std::chrono::steady_clock::now();
+  c->timings.host_ms = std::chrono::duration<float, std::milli>(h2 - h0).count();
+  c->timings.marshal_ms = std::chrono::duration<float, std::milli>(h2 - h1).count();
   *out = res;
   return GQ_OK;
 }
 
 void gq_free_calls(gq_calls *r) {
   if (!r) return;
-  free(r->contig);
-  free(r->pos);
-  free(r->sample);
-  free(r->gt0);
-  free(r->gt1);
-  free(r->flags);
-  free(r->ref_off);
-  free(r->alt_off);
-  free(r->ref_len);
-  free(r->alt_len);
-  free(r->allele_pool);
+  free(r->block_);
   free(r);
 }
 

@@ -49,7 +49,8 @@ class gq_calls(C.Structure):
                 ("flags", C.POINTER(C.c_uint8)), ("ref_off", C.POINTER(C.c_int64)), ("ref_len", C.POINTER(C.c_int32)),
                 ("alt_off", C.POINTER(C.c_int64)), ("alt_len", C.POINTER(C.c_int32)),
                 ("allele_pool", C.POINTER(C.c_uint8)), ("pool_len", C.c_int64), ("visited_loci", C.c_int64),
-                ("complex_loci", C.c_int64), ("ambiguous_loci", C.c_int64), ("tie_loci", C.c_int64)]
+                ("complex_loci", C.c_int64), ("ambiguous_loci", C.c_int64), ("tie_loci", C.c_int64),
+                ("block_", C.c_void_p)]
 
 
 class gq_counts(C.Structure):
@@ -62,7 +63,7 @@ class gq_counts(C.Structure):
 class gq_timings(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("pileup_ms", C.c_float), ("complex_ms", C.c_float),
                 ("finalize_ms", C.c_float), ("total_ms", C.c_float), ("pileup_launches", C.c_int64),
-                ("tiles", C.c_int64)]
+                ("tiles", C.c_int64), ("host_ms", C.c_float), ("marshal_ms", C.c_float)]
 
 
 class gq_somatic_params(C.Structure):
@@ -195,10 +196,7 @@ class Context:
         p = gq_germline_params(int(threshold), int(bool(emit_ref)), int(bool(emit_no_call)))
         out = C.POINTER(gq_calls)()
         _check(lib().gq_germline_threshold(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
-        try:
-            return GermlineCalls.from_struct(out.contents)
-        finally:
-            lib().gq_free_calls(out)
+        return GermlineCalls.from_result(out)
 
     def pileup_counts(self, reads: "DeviceReads", loci) -> Dict[str, np.ndarray]:
         L, keep = make_gq_loci(*loci)
@@ -243,15 +241,28 @@ class GermlineCalls:
         self.visited_loci, self.complex_loci, self.ambiguous_loci, self.tie_loci = visited, complex_loci, ambiguous, ties
 
     @staticmethod
-    def from_struct(c: gq_calls) -> "GermlineCalls":
+    def from_result(ptr) -> "GermlineCalls":
+        """Zero-copy numpy views over the result block (gq_calls.block_).  The views keep
+        a ctypes buffer object alive whose finalizer calls gq_free_calls."""
+        import weakref
+
+        c = ptr.contents
         n = c.n
-
-        def arr(p):
-            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.int64)
-
         pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
-        a = {k: arr(getattr(c, k)) for k in ("contig", "pos", "sample", "gt0", "gt1", "flags", "ref_off", "ref_len",
-                                            "alt_off", "alt_len")}
+        names = ("contig", "pos", "sample", "gt0", "gt1", "flags", "ref_off", "ref_len", "alt_off", "alt_len")
+        if n == 0 or not c.block_:
+            a = {k: np.zeros(0, np.dtype(getattr(c, k)._type_)) for k in names}
+            out = GermlineCalls(a, pool, c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
+            lib().gq_free_calls(ptr)
+            return out
+        ends = [C.cast(getattr(c, k), C.c_void_p).value + n * C.sizeof(getattr(c, k)._type_) for k in names]
+        size = max(ends) - c.block_
+        buf = (C.c_uint8 * size).from_address(c.block_)
+        weakref.finalize(buf, lib().gq_free_calls, ptr)
+        a = {}
+        for k in names:
+            t = getattr(c, k)._type_
+            a[k] = np.frombuffer(buf, dtype=np.dtype(t), count=n, offset=C.cast(getattr(c, k), C.c_void_p).value - c.block_)
         return GermlineCalls(a, pool, c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
 
     def __len__(self) -> int:

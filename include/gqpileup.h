@@ -127,6 +127,7 @@ typedef struct {
   int64_t complex_loci;   /* loci routed through the general-allele kernel     */
   int64_t ambiguous_loci; /* loci whose ref base depends on heap order         */
   int64_t tie_loci;
+  void *block_;           /* owner of the arrays above (freed by gq_free_calls) */
 } gq_calls;
 
 typedef struct gq_ctx gq_ctx;
@@ -142,6 +143,8 @@ typedef struct {
   float total_ms;    /* first event to last event                                    */
   int64_t pileup_launches;
   int64_t tiles;
+  float host_ms;     /* host wall time of the whole call (enqueue + waits + marshalling) */
+  float marshal_ms;  /* host time spent building the output arrays                      */
 } gq_timings;
 
 const char *gq_version(void);
