@@ -56,6 +56,20 @@ def germline_threshold_reads(ctx: native.Context, rs: ReadSet, loci, threshold: 
     return calls.tuples(rs.contig_names)
 
 
+def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet, loci, **params) -> List[dict]:
+    """pileupFlatMapTwoRDDs(tumor, normal, partitions, skipEmpty=true, findPotentialVariantAtLocus)
+    + the driver's filters on the GPU.  Rows as the oracle's somatic_standard (contig by name)."""
+    if tumor.contig_names != normal.contig_names:
+        raise ValueError("tumor and normal reads must share the contig list")
+    calls = ctx.somatic_standard(device_reads(ctx, tumor), device_reads(ctx, normal), loci, **params)
+    rows = []
+    for r in calls.rows:
+        r = dict(r)
+        r["contig"] = tumor.contig_names[r["contig"]]
+        rows.append(r)
+    return rows
+
+
 # ---------------------------------------------------------------------------------------------
 # CLI
 def _common_args(p: argparse.ArgumentParser) -> None:

@@ -1,0 +1,260 @@
+// gq_alleles.h — exact per-element classification and allele identity on device
+// (PileupElement.alignment, PileupElement.scala:68-135; Allele, variants/Allele.scala:26-43;
+// MappedRead.getReferenceBaseAtLocus, reads/MappedRead.scala:57-76).  Used by the
+// general-allele germline kernel and the somatic candidate kernel.
+#pragma once
+#include "gq_kernels.h"
+
+namespace gq {
+namespace {
+
+struct AlleleDesc {  // enough to regenerate an allele's bytes
+  int64_t read;      // read index (for INS / DEL / MID byte access)
+  int32_t aux;       // INS: number of alt bytes; DEL: deleted length
+  int32_t rp;        // INS: first alt byte position in the read
+  uint8_t kind;
+  uint8_t rb;        // pileup ref base (SNV / DEL)
+  uint8_t base;      // SNV sequenced base / MID deleted base
+  uint8_t pad;
+};
+
+__device__ __forceinline__ int allele_ref_len(const AlleleDesc &d) {
+  switch (d.kind) {
+    case K_SNV: return 1;
+    case K_INS: return d.aux > 0 ? 1 : 0;
+    case K_DEL: return 1 + d.aux;
+    case K_MID: return 1;
+    default: return 0;
+  }
+}
+__device__ __forceinline__ int allele_alt_len(const AlleleDesc &d) {
+  switch (d.kind) {
+    case K_SNV: return 1;
+    case K_INS: return d.aux;
+    case K_DEL: return 1;
+    default: return 0;
+  }
+}
+// Byte i of the ref (which=0) / alt (which=1) allele.  DEL bytes 1.. come from the
+// read's MD deletion events at pos+1.. (PileupElement.scala:108-114).
+__device__ uint8_t allele_byte(const DevReads &R, const AlleleDesc &d, int32_t pos, int which, int i) {
+  switch (d.kind) {
+    case K_SNV: return which == 0 ? d.rb : d.base;
+    case K_INS: {
+      const uint8_t *s = R.seq + R.seq_off[d.read];
+      return which == 0 ? s[d.rp] : s[d.rp + i];
+    }
+    case K_DEL: {
+      if (which == 1 || i == 0) return d.rb;
+      const int32_t s = R.start[d.read];
+      const int v = md_find(R.md_ev + R.md_off[d.read], R.n_md[d.read], pos + i - s);
+      return v < 0 ? (uint8_t)'?' : (uint8_t)v;
+    }
+    case K_MID: return d.base;
+    default: return 0;
+  }
+}
+
+struct Key128 {
+  uint64_t lo, hi;
+};
+// 128-bit allele identity: exact packing (lengths, sample, bytes) when ref + alt <= 13
+// bytes, else two independent 64-bit hashes with marker 0xFFFF in the length bytes.
+// byte(which, i) returns byte i of the ref (which = 0) or alt (which = 1) allele.
+template <class F>
+__device__ __forceinline__ Key128 key_from(int rl, int al, int sample, F byte) {
+  Key128 k{0, 0};
+  if (rl + al <= 13) {
+    k.lo = (uint64_t)(uint8_t)rl | ((uint64_t)(uint8_t)al << 8) | ((uint64_t)(uint8_t)sample << 16);
+    int j = 3;
+    auto put = [&](uint8_t x) {
+      if (j < 8) k.lo |= (uint64_t)x << (8 * j);
+      else k.hi |= (uint64_t)x << (8 * (j - 8));
+      ++j;
+    };
+    for (int i = 0; i < rl; ++i) put(byte(0, i));
+    for (int i = 0; i < al; ++i) put(byte(1, i));
+  } else {
+    uint64_t h1 = 0xcbf29ce484222325ull ^ (uint64_t)rl, h2 = 0x9e3779b97f4a7c15ull ^ ((uint64_t)al << 32);
+    auto mix = [&](uint8_t x) {
+      h1 = (h1 ^ x) * 0x100000001b3ull;
+      h2 = (h2 + x + 0x632be59bd9b4e019ull) * 0xff51afd7ed558ccdull;
+      h2 ^= h2 >> 29;
+    };
+    for (int i = 0; i < rl; ++i) mix(byte(0, i));
+    mix(0xFE);
+    for (int i = 0; i < al; ++i) mix(byte(1, i));
+    k.lo = (h1 & ~0xFFFFFFull) | 0xFFFFull | ((uint64_t)sample << 16);
+    k.hi = h2;
+  }
+  return k;
+}
+__device__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
+  return key_from(allele_ref_len(d), allele_alt_len(d), sample,
+                  [&](int which, int i) { return allele_byte(R, d, pos, which, i); });
+}
+
+// Allele ordering (variants/Allele.scala:31-36): ref string, then alt string.
+__device__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDesc &b, int32_t pos) {
+  for (int which = 0; which < 2; ++which) {
+    const int la = which ? allele_alt_len(a) : allele_ref_len(a);
+    const int lb = which ? allele_alt_len(b) : allele_ref_len(b);
+    const int n = la < lb ? la : lb;
+    for (int i = 0; i < n; ++i) {
+      const int x = allele_byte(R, a, pos, which, i), y = allele_byte(R, b, pos, which, i);
+      if (x != y) return x < y ? -1 : 1;
+    }
+    if (la != lb) return la < lb ? -1 : 1;
+  }
+  return 0;
+}
+
+// Locate the PileupElement of read r at `pos` (PileupElement.apply + advanceToLocus) and
+// classify it (PileupElement.alignment).  Returns false and sets *errc on a reference error.
+__device__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
+  const int32_t s = R.start[r];
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  int ci = 0;
+  int32_t ci_locus = s, within = 0, rp = 0;
+  for (;;) {
+    if (ci >= ncig) {
+      *errc = 1;
+      return false;
+    }
+    const uint32_t c = R.cigar[cig_off + ci];
+    const int op = (int)(c & 15u);
+    const int32_t len = (int32_t)(c >> 4);
+    const int32_t rlen = consumes_ref(op) ? len : 0;
+    if (ci_locus <= pos && pos < ci_locus + rlen) {
+      if (consumes_read(op)) rp += pos - ci_locus - within;
+      within = pos - ci_locus;
+      break;
+    } else if (pos == 0 && op == OP_I) {
+      break;
+    } else {
+      if (consumes_read(op)) rp += len - within;
+      ci_locus += rlen;
+      ++ci;
+      within = 0;
+    }
+  }
+  const uint32_t c = R.cigar[cig_off + ci];
+  const int op = (int)(c & 15u);
+  const int32_t len = (int32_t)(c >> 4);
+  const bool fin = within == len - 1;
+  const bool has_next = ci + 1 < ncig;
+  const uint32_t cn = has_next ? R.cigar[cig_off + ci + 1] : 0u;
+  const int nextop = fin ? (has_next ? (int)(cn & 15u) : -1) : op;
+  const int32_t slen = R.seq_len[r];
+  d.read = r;
+  d.rb = refbase;
+  d.pad = 0;
+  if ((op == OP_M || op == OP_EQ) && nextop == OP_I) {
+    const int32_t ilen = (int32_t)(cn >> 4);  // I consumes read bases
+    int32_t from = rp, until = rp + ilen + 1;
+    from = from < 0 ? 0 : (from > slen ? slen : from);
+    until = until > slen ? slen : until;
+    if (until < from) until = from;
+    d.kind = K_INS;
+    d.rp = from;
+    d.aux = until - from;
+    d.base = 0;
+    if (d.aux == 0) {
+      *errc = 1;
+      return false;
+    }
+  } else if (op == OP_I && nextop != -1 && ci_locus == 0) {
+    int32_t from = rp, until = rp + len + 1;
+    from = from < 0 ? 0 : (from > slen ? slen : from);
+    until = until > slen ? slen : until;
+    if (until < from) until = from;
+    d.kind = K_INS;
+    d.rp = from;
+    d.aux = until - from;
+    d.base = 0;
+    if (d.aux == 0) {
+      *errc = 1;
+      return false;
+    }
+  } else if (op == OP_I) {
+    *errc = 2;  // InvalidCigarElementException
+    return false;
+  } else if ((op == OP_M || op == OP_EQ || op == OP_X) && nextop == OP_D) {
+    d.kind = K_DEL;
+    d.aux = (int32_t)(cn >> 4);
+    d.rp = rp;
+    d.base = 0;
+    const uint32_t *ev = R.md_ev + R.md_off[r];
+    const int nmd = R.n_md[r];
+    for (int i = 1; i <= d.aux; ++i)
+      if (md_find(ev, nmd, pos + i - s) < 0) {
+        *errc = 3;
+        return false;
+      }
+  } else if (op == OP_D) {
+    const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
+    if (v < 0) {
+      *errc = 3;
+      return false;
+    }
+    d.kind = K_MID;
+    d.base = (uint8_t)v;
+    d.aux = 0;
+    d.rp = 0;
+  } else if (nextop == OP_D) {
+    *errc = 1;
+    return false;
+  } else if (op == OP_M || op == OP_EQ || op == OP_X) {
+    if (rp >= slen) {
+      *errc = 1;
+      return false;
+    }
+    d.kind = K_SNV;
+    d.base = R.seq[R.seq_off[r] + rp];
+    d.aux = 0;
+    d.rp = rp;
+  } else if (op == OP_S || op == OP_N || op == OP_H) {
+    d.kind = K_CLIP;
+    d.base = 0;
+    d.aux = 0;
+    d.rp = 0;
+  } else {
+    *errc = 1;
+    return false;
+  }
+  return true;
+}
+
+// MD-derived reference base of read r at pos (MappedRead.getReferenceBaseAtLocus) or -1 on error.
+__device__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
+  const int32_t s = R.start[r];
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  int32_t ref = s, rp = 0;
+  for (int k = 0; k < ncig; ++k) {
+    const uint32_t c = R.cigar[cig_off + k];
+    const int op = (int)(c & 15u);
+    const int32_t len = (int32_t)(c >> 4);
+    if (consumes_ref(op)) {
+      if (pos < ref + len) {
+        if (R.n_md[r] < 0) return -4;
+        const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
+        if (op == OP_D) return v < 0 ? -3 : v;
+        if (op == OP_N) return 'N';
+        if (v >= 0) return v;
+        const int32_t q = rp + (pos - ref);
+        if (q >= R.seq_len[r]) return -1;
+        return R.seq[R.seq_off[r] + q];
+      }
+      ref += len;
+    }
+    if (consumes_read(op)) rp += len;
+  }
+  return -1;
+}
+
+constexpr int kSlots = 2;  // table capacity = 64 * kSlots distinct (sample, allele) keys per locus
+
+}  // namespace
+}  // namespace gq

@@ -267,4 +267,71 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   }
 }
 
+// LDS histogram: seven u32 words per locus (SoA: word * S + guard + i, so consecutive loci
+// sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has
+// code (b >> 1) & 7, distinct for A 0, C 1, T 2, G 3, N 7; a base whose code does not
+// map back to it is "other" (slot 4).  slot = word * 2 + half:
+//   W_AC = A | C << 16, W_TG = T | G << 16, W_OX = other | complex << 16, W_NN = N << 16,
+//   W_EAC / W_ETG = A C / T G counts of Match/Mismatch elements carrying an MD mismatch
+//   event, W_MASK = OR of MD-derived standard reference bases of event / complex elements.
+// Tiles whose read window could exceed 65535 reads never use this path (wide tiles).
+enum : int { W_AC = 0, W_TG, W_OX, W_NN, W_EAC, W_ETG, W_MASK, W_N };
+// LDS arrays carry a 16-entry guard band on each side (stride T + 32, index 16 + i), so
+// the branch-free base pass may address i in [-16, T + 16) with a zero increment.
+constexpr int kGuard = 16;
+
+template <int T, int ABL = 0>
+struct GermSink {
+  uint32_t *cnt;  // W_N arrays of T + 2 * kGuard words
+  int32_t L0;
+  int *err;
+  long long *err_pos;
+  static constexpr int S = T + 2 * kGuard;
+  uint32_t acc = 0;  // ABL & 4 only
+  __device__ __forceinline__ ~GermSink() {
+    if ((ABL & 4) && acc == 0x12345u) atomicAdd(cnt, 1u);
+  }
+  __device__ __forceinline__ uint32_t *at(int w, int i) const { return cnt + w * S + kGuard + i; }
+  // four Match/Mismatch elements: the bytes of `w` at tile indices i..i+3 (valid4: bit per byte)
+  __device__ __forceinline__ void bases4(int i, uint32_t w, uint32_t valid4, uint8_t) {
+    const uint32_t code4 = (w >> 1) & 0x07070707u;
+    const uint32_t exp4 = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, code4);  // 'A','C','T','G',0,0,0,'N'
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t bj = (w >> (8 * j)) & 0xFFu, ej = (exp4 >> (8 * j)) & 0xFFu, cj = (code4 >> (8 * j)) & 7u;
+      const uint32_t slot = bj == ej ? cj : 4u;
+      if (ABL & 4) {
+        acc += ((valid4 >> j) & 1u) << ((slot & 1u) << 4);
+        acc ^= slot;
+      } else {
+        atomicAdd(at((int)(slot >> 1), i + j), ((valid4 >> j) & 1u) << ((slot & 1u) << 4));
+      }
+    }
+  }
+  // an MD mismatch event on a Match/Mismatch element: read base b, MD reference base m
+  __device__ __forceinline__ void event_i(int i, uint8_t b, uint8_t m, uint8_t) {
+    if (ABL & 8) return;
+    const int c = base_cat(b);
+    if (c < 4) atomicAdd(at(W_EAC + (c >> 1), i), 1u << ((c & 1) << 4));
+    const uint32_t bit = std_bit(m);
+    if (bit) atomicOr(at(W_MASK, i), bit);
+  }
+  // general walker elements
+  __device__ __forceinline__ void elem_i(int i, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
+    if (kind == K_SNV) {
+      const int sh = (i & 3) * 8;
+      bases4(i - (i & 3), (uint32_t)base << sh, 1u << (i & 3), fl);
+      if (ev) event_i(i, base, mdb, fl);
+    } else {
+      atomicAdd(at(W_OX, i), 1u << 16);
+      const uint32_t bit = std_bit(mdb);
+      if (bit) atomicOr(at(W_MASK, i), bit);
+    }
+  }
+  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
+    elem_i(l - L0, kind, base, mdb, ev, fl);
+  }
+  __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
+};
+
 }  // namespace gq

@@ -32,11 +32,12 @@
 #include <vector>
 
 #include "../../include/gqpileup.h"
-#include "gq_kernels.h"
+#include "gq_host.h"
+#include "gq_alleles.h"
 
 using namespace gq;
 
-namespace {
+namespace gq {
 thread_local std::string g_err;
 
 gq_status set_err(gq_status s, const char *fmt, ...) {
@@ -49,19 +50,9 @@ gq_status set_err(gq_status s, const char *fmt, ...) {
   return s;
 }
 
-#define HIP_TRY(expr)                                                                         \
-  do {                                                                                        \
-    hipError_t _e = (expr);                                                                   \
-    if (_e != hipSuccess)                                                                     \
-      return set_err(GQ_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
-  } while (0)
+}  // namespace gq
 
-constexpr int kBlock = 256;
-constexpr int kGermT = 1024;  // loci per germline tile
-constexpr int kCountT = 512;  // loci per counts tile
-constexpr int kStageBytes = 40 * 1024;
-constexpr size_t kSeqPad = 2048;  // zeroed tail of the uploaded sequence pool  // LDS staging of a read batch's sequence bytes
-
+namespace {
 // ------------------------------------------------------------------------------------------
 // Tile planning
 // ------------------------------------------------------------------------------------------
@@ -161,39 +152,6 @@ __global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__re
   for (; k < nmd; ++k) rb[k] = 0;
 }
 
-struct Counters {  // device-side run counters (one allocation, zeroed per call)
-  unsigned long long n_rec;
-  unsigned long long n_complex;
-  unsigned long long visited;
-  unsigned long long ambiguous;
-  unsigned long long ties;
-  unsigned long long pool_used;
-  int err;
-  int pad;
-  long long err_pos;
-  // per-tile run counters of germline_tile, spread over kSpread addresses (summed on the host)
-  unsigned long long spread[3][64];
-};
-constexpr int kSpread = 64;
-
-// Wave-aggregated reservation of `n` slots on a global counter.
-__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *ctr, unsigned n) {
-  if (__ballot(n != 0) == 0) return 0;  // nothing to reserve in this wave (the common case)
-  const int lane = threadIdx.x & 63;
-  // inclusive scan of n across the wave
-  unsigned x = n;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    unsigned y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  const unsigned total = __shfl(x, 63, 64);
-  unsigned long long base = 0;
-  if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
-  base = __shfl(base, 63, 64);
-  return base + (x - n);
-}
-
 __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, int alt_len) {
   uint64_t v = r0;
   for (int i = 0; i < alt_len; ++i) v |= (uint64_t)alt[i] << (8 * (1 + i));
@@ -203,73 +161,6 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ------------------------------------------------------------------------------------------
 // germline_tile: LDS histogram + on-device decision for simple loci
 // ------------------------------------------------------------------------------------------
-// LDS histogram: seven u32 words per locus (SoA: word * S + guard + i, so consecutive loci
-// sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has
-// code (b >> 1) & 7, distinct for A 0, C 1, T 2, G 3, N 7; a base whose code does not
-// map back to it is "other" (slot 4).  slot = word * 2 + half:
-//   W_AC = A | C << 16, W_TG = T | G << 16, W_OX = other | complex << 16, W_NN = N << 16,
-//   W_EAC / W_ETG = A C / T G counts of Match/Mismatch elements carrying an MD mismatch
-//   event, W_MASK = OR of MD-derived standard reference bases of event / complex elements.
-// Tiles whose read window could exceed 65535 reads never use this path (wide tiles).
-enum : int { W_AC = 0, W_TG, W_OX, W_NN, W_EAC, W_ETG, W_MASK, W_N };
-// LDS arrays carry a 16-entry guard band on each side (stride T + 32, index 16 + i), so
-// the branch-free base pass may address i in [-16, T + 16) with a zero increment.
-constexpr int kGuard = 16;
-
-template <int T, int ABL = 0>
-struct GermSink {
-  uint32_t *cnt;  // W_N arrays of T + 2 * kGuard words
-  int32_t L0;
-  int *err;
-  long long *err_pos;
-  static constexpr int S = T + 2 * kGuard;
-  uint32_t acc = 0;  // ABL & 4 only
-  __device__ __forceinline__ ~GermSink() {
-    if ((ABL & 4) && acc == 0x12345u) atomicAdd(cnt, 1u);
-  }
-  __device__ __forceinline__ uint32_t *at(int w, int i) const { return cnt + w * S + kGuard + i; }
-  // four Match/Mismatch elements: the bytes of `w` at tile indices i..i+3 (valid4: bit per byte)
-  __device__ __forceinline__ void bases4(int i, uint32_t w, uint32_t valid4, uint8_t) {
-    const uint32_t code4 = (w >> 1) & 0x07070707u;
-    const uint32_t exp4 = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, code4);  // 'A','C','T','G',0,0,0,'N'
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t bj = (w >> (8 * j)) & 0xFFu, ej = (exp4 >> (8 * j)) & 0xFFu, cj = (code4 >> (8 * j)) & 7u;
-      const uint32_t slot = bj == ej ? cj : 4u;
-      if (ABL & 4) {
-        acc += ((valid4 >> j) & 1u) << ((slot & 1u) << 4);
-        acc ^= slot;
-      } else {
-        atomicAdd(at((int)(slot >> 1), i + j), ((valid4 >> j) & 1u) << ((slot & 1u) << 4));
-      }
-    }
-  }
-  // an MD mismatch event on a Match/Mismatch element: read base b, MD reference base m
-  __device__ __forceinline__ void event_i(int i, uint8_t b, uint8_t m, uint8_t) {
-    if (ABL & 8) return;
-    const int c = base_cat(b);
-    if (c < 4) atomicAdd(at(W_EAC + (c >> 1), i), 1u << ((c & 1) << 4));
-    const uint32_t bit = std_bit(m);
-    if (bit) atomicOr(at(W_MASK, i), bit);
-  }
-  // general walker elements
-  __device__ __forceinline__ void elem_i(int i, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
-    if (kind == K_SNV) {
-      const int sh = (i & 3) * 8;
-      bases4(i - (i & 3), (uint32_t)base << sh, 1u << (i & 3), fl);
-      if (ev) event_i(i, base, mdb, fl);
-    } else {
-      atomicAdd(at(W_OX, i), 1u << 16);
-      const uint32_t bit = std_bit(mdb);
-      if (bit) atomicOr(at(W_MASK, i), bit);
-    }
-  }
-  __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
-    elem_i(l - L0, kind, base, mdb, ev, fl);
-  }
-  __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
-};
-
 #define PUSH_OUT(rec)             \
   do {                            \
     if (nout == 0) out0 = (rec);  \
@@ -480,247 +371,6 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
 // ------------------------------------------------------------------------------------------
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
 // ------------------------------------------------------------------------------------------
-struct AlleleDesc {  // enough to regenerate an allele's bytes
-  int64_t read;      // read index (for INS / DEL / MID byte access)
-  int32_t aux;       // INS: number of alt bytes; DEL: deleted length
-  int32_t rp;        // INS: first alt byte position in the read
-  uint8_t kind;
-  uint8_t rb;        // pileup ref base (SNV / DEL)
-  uint8_t base;      // SNV sequenced base / MID deleted base
-  uint8_t pad;
-};
-
-__device__ __forceinline__ int allele_ref_len(const AlleleDesc &d) {
-  switch (d.kind) {
-    case K_SNV: return 1;
-    case K_INS: return d.aux > 0 ? 1 : 0;
-    case K_DEL: return 1 + d.aux;
-    case K_MID: return 1;
-    default: return 0;
-  }
-}
-__device__ __forceinline__ int allele_alt_len(const AlleleDesc &d) {
-  switch (d.kind) {
-    case K_SNV: return 1;
-    case K_INS: return d.aux;
-    case K_DEL: return 1;
-    default: return 0;
-  }
-}
-// Byte i of the ref (which=0) / alt (which=1) allele.  DEL bytes 1.. come from the
-// read's MD deletion events at pos+1.. (PileupElement.scala:108-114).
-__device__ uint8_t allele_byte(const DevReads &R, const AlleleDesc &d, int32_t pos, int which, int i) {
-  switch (d.kind) {
-    case K_SNV: return which == 0 ? d.rb : d.base;
-    case K_INS: {
-      const uint8_t *s = R.seq + R.seq_off[d.read];
-      return which == 0 ? s[d.rp] : s[d.rp + i];
-    }
-    case K_DEL: {
-      if (which == 1 || i == 0) return d.rb;
-      const int32_t s = R.start[d.read];
-      const int v = md_find(R.md_ev + R.md_off[d.read], R.n_md[d.read], pos + i - s);
-      return v < 0 ? (uint8_t)'?' : (uint8_t)v;
-    }
-    case K_MID: return d.base;
-    default: return 0;
-  }
-}
-
-struct Key128 {
-  uint64_t lo, hi;
-};
-__device__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
-  const int rl = allele_ref_len(d), al = allele_alt_len(d);
-  Key128 k;
-  if (rl + al <= 13) {  // exact packing: lengths + bytes
-    uint8_t b[16] = {0};
-    b[0] = (uint8_t)rl;
-    b[1] = (uint8_t)al;
-    b[2] = (uint8_t)sample;
-    int j = 3;
-    for (int i = 0; i < rl; ++i) b[j++] = allele_byte(R, d, pos, 0, i);
-    for (int i = 0; i < al; ++i) b[j++] = allele_byte(R, d, pos, 1, i);
-    k.lo = k.hi = 0;
-    for (int i = 0; i < 8; ++i) k.lo |= (uint64_t)b[i] << (8 * i);
-    for (int i = 0; i < 8; ++i) k.hi |= (uint64_t)b[8 + i] << (8 * i);
-  } else {  // two independent 64-bit hashes; marker 0xFF in the length bytes
-    uint64_t h1 = 0xcbf29ce484222325ull ^ (uint64_t)rl, h2 = 0x9e3779b97f4a7c15ull ^ ((uint64_t)al << 32);
-    auto mix = [&](uint8_t x) {
-      h1 = (h1 ^ x) * 0x100000001b3ull;
-      h2 = (h2 + x + 0x632be59bd9b4e019ull) * 0xff51afd7ed558ccdull;
-      h2 ^= h2 >> 29;
-    };
-    for (int i = 0; i < rl; ++i) mix(allele_byte(R, d, pos, 0, i));
-    mix(0xFE);
-    for (int i = 0; i < al; ++i) mix(allele_byte(R, d, pos, 1, i));
-    k.lo = (h1 & ~0xFFFFFFull) | 0xFFFFull | ((uint64_t)sample << 16);
-    k.hi = h2;
-  }
-  return k;
-}
-
-// Allele ordering (variants/Allele.scala:31-36): ref string, then alt string.
-__device__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDesc &b, int32_t pos) {
-  for (int which = 0; which < 2; ++which) {
-    const int la = which ? allele_alt_len(a) : allele_ref_len(a);
-    const int lb = which ? allele_alt_len(b) : allele_ref_len(b);
-    const int n = la < lb ? la : lb;
-    for (int i = 0; i < n; ++i) {
-      const int x = allele_byte(R, a, pos, which, i), y = allele_byte(R, b, pos, which, i);
-      if (x != y) return x < y ? -1 : 1;
-    }
-    if (la != lb) return la < lb ? -1 : 1;
-  }
-  return 0;
-}
-
-// Locate the PileupElement of read r at `pos` (PileupElement.apply + advanceToLocus) and
-// classify it (PileupElement.alignment).  Returns false and sets *errc on a reference error.
-__device__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
-  const int32_t s = R.start[r];
-  const int64_t cig_off = R.cigar_off[r];
-  const int32_t ncig = R.n_cigar[r];
-  int ci = 0;
-  int32_t ci_locus = s, within = 0, rp = 0;
-  for (;;) {
-    if (ci >= ncig) {
-      *errc = 1;
-      return false;
-    }
-    const uint32_t c = R.cigar[cig_off + ci];
-    const int op = (int)(c & 15u);
-    const int32_t len = (int32_t)(c >> 4);
-    const int32_t rlen = consumes_ref(op) ? len : 0;
-    if (ci_locus <= pos && pos < ci_locus + rlen) {
-      if (consumes_read(op)) rp += pos - ci_locus - within;
-      within = pos - ci_locus;
-      break;
-    } else if (pos == 0 && op == OP_I) {
-      break;
-    } else {
-      if (consumes_read(op)) rp += len - within;
-      ci_locus += rlen;
-      ++ci;
-      within = 0;
-    }
-  }
-  const uint32_t c = R.cigar[cig_off + ci];
-  const int op = (int)(c & 15u);
-  const int32_t len = (int32_t)(c >> 4);
-  const bool fin = within == len - 1;
-  const bool has_next = ci + 1 < ncig;
-  const uint32_t cn = has_next ? R.cigar[cig_off + ci + 1] : 0u;
-  const int nextop = fin ? (has_next ? (int)(cn & 15u) : -1) : op;
-  const int32_t slen = R.seq_len[r];
-  d.read = r;
-  d.rb = refbase;
-  d.pad = 0;
-  if ((op == OP_M || op == OP_EQ) && nextop == OP_I) {
-    const int32_t ilen = (int32_t)(cn >> 4);  // I consumes read bases
-    int32_t from = rp, until = rp + ilen + 1;
-    from = from < 0 ? 0 : (from > slen ? slen : from);
-    until = until > slen ? slen : until;
-    if (until < from) until = from;
-    d.kind = K_INS;
-    d.rp = from;
-    d.aux = until - from;
-    d.base = 0;
-    if (d.aux == 0) {
-      *errc = 1;
-      return false;
-    }
-  } else if (op == OP_I && nextop != -1 && ci_locus == 0) {
-    int32_t from = rp, until = rp + len + 1;
-    from = from < 0 ? 0 : (from > slen ? slen : from);
-    until = until > slen ? slen : until;
-    if (until < from) until = from;
-    d.kind = K_INS;
-    d.rp = from;
-    d.aux = until - from;
-    d.base = 0;
-    if (d.aux == 0) {
-      *errc = 1;
-      return false;
-    }
-  } else if (op == OP_I) {
-    *errc = 2;  // InvalidCigarElementException
-    return false;
-  } else if ((op == OP_M || op == OP_EQ || op == OP_X) && nextop == OP_D) {
-    d.kind = K_DEL;
-    d.aux = (int32_t)(cn >> 4);
-    d.rp = rp;
-    d.base = 0;
-    const uint32_t *ev = R.md_ev + R.md_off[r];
-    const int nmd = R.n_md[r];
-    for (int i = 1; i <= d.aux; ++i)
-      if (md_find(ev, nmd, pos + i - s) < 0) {
-        *errc = 3;
-        return false;
-      }
-  } else if (op == OP_D) {
-    const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
-    if (v < 0) {
-      *errc = 3;
-      return false;
-    }
-    d.kind = K_MID;
-    d.base = (uint8_t)v;
-    d.aux = 0;
-    d.rp = 0;
-  } else if (nextop == OP_D) {
-    *errc = 1;
-    return false;
-  } else if (op == OP_M || op == OP_EQ || op == OP_X) {
-    if (rp >= slen) {
-      *errc = 1;
-      return false;
-    }
-    d.kind = K_SNV;
-    d.base = R.seq[R.seq_off[r] + rp];
-    d.aux = 0;
-    d.rp = rp;
-  } else if (op == OP_S || op == OP_N || op == OP_H) {
-    d.kind = K_CLIP;
-    d.base = 0;
-    d.aux = 0;
-    d.rp = 0;
-  } else {
-    *errc = 1;
-    return false;
-  }
-  return true;
-}
-
-// MD-derived reference base of read r at pos (MappedRead.getReferenceBaseAtLocus) or -1 on error.
-__device__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
-  const int32_t s = R.start[r];
-  const int64_t cig_off = R.cigar_off[r];
-  const int32_t ncig = R.n_cigar[r];
-  int32_t ref = s, rp = 0;
-  for (int k = 0; k < ncig; ++k) {
-    const uint32_t c = R.cigar[cig_off + k];
-    const int op = (int)(c & 15u);
-    const int32_t len = (int32_t)(c >> 4);
-    if (consumes_ref(op)) {
-      if (pos < ref + len) {
-        if (R.n_md[r] < 0) return -4;
-        const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
-        if (op == OP_D) return v < 0 ? -3 : v;
-        if (op == OP_N) return 'N';
-        if (v >= 0) return v;
-        const int32_t q = rp + (pos - ref);
-        if (q >= R.seq_len[r]) return -1;
-        return R.seq[R.seq_off[r] + q];
-      }
-      ref += len;
-    }
-    if (consumes_read(op)) rp += len;
-  }
-  return -1;
-}
-
-constexpr int kSlots = 2;  // table capacity = 64 * kSlots distinct (sample, allele) keys per locus
 
 __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
@@ -1152,44 +802,6 @@ __global__ void calls_image(const CallRec *__restrict__ recs, const int32_t *__r
 // ==========================================================================================
 // Host side: context, resident read sets, entry points
 // ==========================================================================================
-struct DevBuf {
-  void *p = nullptr;
-  size_t n = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= n) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    size_t want = std::max(bytes, (size_t)256);
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) n = want;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-};
-
-struct gq_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};
-  gq_timings timings{};
-  int germ_tile = kGermT;
-  DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image;
-  DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb;
-};
-
-struct gq_dev_reads {
-  gq_ctx *ctx = nullptr;
-  DevReads d{};
-  std::vector<int64_t> contig_read_begin;  // host copy
-  std::vector<void *> owned;               // device allocations owned by this handle
-  int64_t seq_bytes = 0;
-};
-
 extern "C" {
 
 const char *gq_version(void) { return "guacamole-amd gqpileup 0.1 (gfx950)"; }
@@ -1214,7 +826,7 @@ void gq_close(gq_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
-                    &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->c_depth, &c->c_pos,
+                    &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
                     &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
@@ -1379,13 +991,10 @@ void gq_reads_free(gq_dev_reads *d) {
   delete d;
 }
 
-// ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
-struct Plan {
-  int64_t n_tiles = 0;
-  int64_t n_loci = 0;
-};
+}  // extern "C"
 
-static gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl) {
+// ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
+gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles_buf) {
   if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
   const int64_t R = loci->n_ranges;
   std::vector<int32_t> rc;
@@ -1420,15 +1029,15 @@ static gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, in
   HIP_TRY(hipMemcpyAsync(d_re, re.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(d_ro, ro.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(d_rt, rt.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c->tiles.ensure((size_t)tiles * sizeof(Tile)));
+  HIP_TRY(tiles_buf.ensure((size_t)tiles * sizeof(Tile)));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
-                     tiles, T, rd->d, (Tile *)c->tiles.p);
+                     tiles, T, rd->d, (Tile *)tiles_buf.p);
   HIP_TRY(hipGetLastError());
   return GQ_OK;
 }
 
-static gq_status check_device_error(gq_ctx *c, const Counters &h) {
+gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
   if (h.err) {
     static const char *names[] = {"ok", "assertion", "invalid cigar element", "CIGAR / MD tag mismatch",
                                   "read without MD tag", "multiple reference bases", "unsorted", "argument", "hip",
@@ -1438,6 +1047,8 @@ static gq_status check_device_error(gq_ctx *c, const Counters &h) {
   }
   return GQ_OK;
 }
+
+extern "C" {
 
 extern "C++" template <int T>
 static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p, CallRec *recs,
@@ -1476,7 +1087,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = plan(c, rd, loci, T, pl);
+  gq_status st = plan(c, rd, loci, T, pl, c->tiles);
   if (st) return st;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
@@ -1644,7 +1255,7 @@ gq_status gq_pileup_counts(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loc
   if (!c || !rd || !loci || !out) return set_err(GQ_E_ARG, "gq_pileup_counts: null argument");
   HIP_TRY(hipSetDevice(c->device));
   Plan pl;
-  gq_status st = plan(c, rd, loci, kCountT, pl);
+  gq_status st = plan(c, rd, loci, kCountT, pl, c->tiles);
   if (st) return st;
   gq_counts *res = (gq_counts *)calloc(1, sizeof(gq_counts));
   const int64_t n = pl.n_loci;
@@ -1707,12 +1318,6 @@ void gq_free_counts(gq_counts *r) {
   free(r);
 }
 
-gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_reads *n, const gq_loci *loci,
-                              const gq_somatic_params *p, gq_somatic_calls **out) {
-  (void)c; (void)t; (void)n; (void)loci; (void)p; (void)out;
-  return set_err(GQ_E_ARG, "gq_somatic_standard: not built in this revision");
-}
 
-void gq_free_somatic(gq_somatic_calls *r) { free(r); }
 
 }  // extern "C"

@@ -1,0 +1,884 @@
+// gq_somatic.hip — somatic-standard on MI355X (gfx950).
+//
+// Restates, per locus, SomaticStandard.Caller.findPotentialVariantAtLocus and the driver's
+// filter chain (paths relative to /root/reference/src/main/scala/org/hammerlab/guacamole/):
+//   commands/SomaticStandardCaller.scala:162-245 (caller), :124-151 (driver filters)
+//   filters/PileupFilter.scala:29-89, filters/PileupElementsFilter.scala:25-36
+//   likelihood/Likelihood.scala:48-201, variants/AlleleEvidence.scala:41-102
+//   filters/SomaticGenotypeFilter.scala:58-307, variants/CalledSomaticAllele.scala:37-51
+//   DistributedUtil.pileupFlatMapTwoRDDs (DistributedUtil.scala:316-335, skipEmpty = true)
+//
+// Two kernels:
+//   somatic_tile<T>   one workgroup per tile of T loci: LDS histogram of the tumor reads
+//                     (the germline sink) -> per-locus "tumor has a non-Match element / the
+//                     MD reference is ambiguous" bit kept in registers; LDS re-zeroed, the
+//                     normal reads histogrammed -> normal depth.  Loci visited by either
+//                     sample are counted; loci with a tumor non-Match and normal depth > 0
+//                     are queued (a superset of the loci the caller can emit at: filters
+//                     only remove elements).
+//   somatic_call      one wave per queued locus: exact elements of both pileups
+//                     (classify), per-sample distinct-allele table in registers with the
+//                     FP64 per-allele sums of log(2pc), log(pc + (1 - pc)), log(2(1 - pc)),
+//                     genotype likelihoods for every (a_i, a_j), normalisation, the odds
+//                     test, allele evidence (mean / median via LDS), filters, record.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "gq_alleles.h"
+#include "gq_host.h"
+
+using namespace gq;
+
+namespace {
+
+constexpr int kSomT = 1024;
+constexpr int kEvCap = 1024;  // allele-supporting elements per sample held in LDS for medians
+
+struct SomRec {  // one emitted CalledSomaticAllele
+  uint64_t key;  // output ordinal << 12
+  int32_t contig, pos;
+  uint16_t ref_len, alt_len;
+  uint8_t flags, pad[3];
+  uint64_t allele;  // inline bytes (ref then alt) if ref_len + alt_len <= 8, else pool offset
+  double log_odds;
+  int32_t gq, pad2;
+  gq_evidence tumor, normal;
+};
+
+// ------------------------------------------------------------------------------------------
+// somatic_tile: candidate loci
+// ------------------------------------------------------------------------------------------
+template <int T>
+__global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ tiles_t,
+                                                       const Tile *__restrict__ tiles_n, DevReads RT, DevReads RN,
+                                                       ComplexItem *__restrict__ cand, unsigned long long cand_cap,
+                                                       Counters *ctr) {
+  constexpr int S = T + 2 * kGuard;
+  constexpr int KPT = T / kBlock;  // loci per thread
+  static_assert(KPT <= 8, "per-thread flag bits");
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
+  const Tile tt = tiles_t[blockIdx.x], tn = tiles_n[blockIdx.x];
+  const int32_t L0 = tt.L0, L1 = tt.L1;
+  const int nloci = L1 - L0;
+  const bool wide = (tt.re - tt.rb) >= 65535 || (tn.re - tn.rb) >= 65535;
+  unsigned visited = 0;
+  if (wide) {  // 16-bit counters could overflow: every locus goes to the exact kernel
+    for (int k = 0; k < KPT; ++k) {
+      const int i = threadIdx.x + k * kBlock;
+      const unsigned long long b = wave_reserve(&ctr->n_complex, i < nloci ? 1u : 0u);
+      if (i < nloci && b < cand_cap) cand[b] = ComplexItem{(int32_t)blockIdx.x, L0 + i, 1};
+    }
+    return;
+  }
+  uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+  for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  {
+    GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+    for (int64_t r = tt.rb + threadIdx.x; r < tt.re; r += blockDim.x) walk_read_lane(RT, r, L0, L1, sink);
+  }
+  __syncthreads();
+  uint32_t tflag = 0;  // bit k: tumor depth > 0 at locus tid + k * kBlock; bit 8 + k: tumor candidate
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    if (i >= nloci) continue;
+    const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
+                   wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
+    const uint32_t cA = wac & 0xFFFFu, cC = wac >> 16, cT = wtg & 0xFFFFu, cG = wtg >> 16, cN = wnn >> 16;
+    const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);
+    const uint32_t depth = cA + cC + cT + cG + cN + cx;
+    if (depth == 0) continue;
+    tflag |= 1u << k;
+    uint32_t mask = cnt[W_MASK * S + kGuard + i];
+    const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
+    if (cA > (eac & 0xFFFFu)) mask |= 1u;
+    if (cC > (eac >> 16)) mask |= 2u;
+    if (cT > (etg & 0xFFFFu)) mask |= 4u;
+    if (cG > (etg >> 16)) mask |= 8u;
+    const int rc = mask ? (__ffs((int)mask) - 1) : 4;
+    const uint32_t c_ref = rc == 0 ? cA : rc == 1 ? cC : rc == 2 ? cT : rc == 3 ? cG : cN;
+    if (__popc(mask) > 1 || cx > 0 || depth > c_ref) tflag |= 1u << (8 + k);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  {
+    GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+    for (int64_t r = tn.rb + threadIdx.x; r < tn.re; r += blockDim.x) walk_read_lane(RN, r, L0, L1, sink);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    bool q = false;
+    if (i < nloci) {
+      uint32_t dn = 0;
+#pragma unroll
+      for (int w = W_AC; w <= W_NN; ++w) {
+        const uint32_t v = cnt[w * S + kGuard + i];
+        dn += (v & 0xFFFFu) + (v >> 16);
+      }
+      if (((tflag >> k) & 1u) || dn > 0) ++visited;
+      q = ((tflag >> (8 + k)) & 1u) && dn > 0;
+    }
+    const unsigned long long b = wave_reserve(&ctr->n_complex, q ? 1u : 0u);
+    if (q && b < cand_cap) cand[b] = ComplexItem{(int32_t)blockIdx.x, L0 + i, 0};
+  }
+  __shared__ unsigned red;
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  if (visited) atomicAdd(&red, visited);
+  __syncthreads();
+  if (threadIdx.x == 0 && red) atomicAdd(&ctr->spread[0][blockIdx.x & (kSpread - 1)], (unsigned long long)red);
+}
+
+// ------------------------------------------------------------------------------------------
+// somatic_call: exact caller per queued locus (one wave per locus)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// ADAM PhredUtils (restated in oracle/oracle.cpp:201-219)
+__device__ __forceinline__ double phred_success(int q) {
+  if (q > 255) q = 255;
+  return 1.0 - pow(10.0, -(double)q / 10.0);
+}
+__device__ int success_to_phred(double p) {  // successProbabilityToPhred: round(-10 log10(1 - p)) (Math.round)
+  const double x = -10.0 * log10(1.0 - p);
+  if (isnan(x)) return 0;
+  const double r = floor(x + 0.5);
+  long long l;
+  if (r >= 9.2233720368547758e18) l = 0x7FFFFFFFFFFFFFFFll;
+  else if (r <= -9.2233720368547758e18) l = (long long)0x8000000000000000ull;
+  else l = (long long)r;
+  return (int)(int32_t)(uint32_t)(uint64_t)l;
+}
+
+// |a - b| within FP rounding noise of the reference's own (order-dependent) arithmetic
+__device__ __forceinline__ bool near_edge(double a, double b) { return fabs(a - b) <= 1e-9 * fmax(1.0, fabs(b)); }
+// successProbabilityToPhred(p) rounds -10 log10(1 - p); flag values within 1e-6 of a .5 step
+__device__ __forceinline__ bool phred_rounding_edge(double p) {
+  const double x = -10.0 * log10(1.0 - p);
+  if (!isfinite(x)) return false;
+  return fabs((x - floor(x)) - 0.5) <= 1e-6;
+}
+
+// Element quality (PileupElement.qualityScore, PileupElement.scala:166-171; quality bytes are
+// signed JVM bytes): SNV / Deletion = the base quality at the element's read position,
+// Insertion = min over its bases, MidDeletion / Clipped = the read's mapping quality.
+__device__ int elem_quality(const DevReads &R, const AlleleDesc &d) {
+  const int64_t r = d.read;
+  const uint8_t *q = R.qual + R.seq_off[r];
+  switch (d.kind) {
+    case K_SNV:
+    case K_DEL: return (int)(int8_t)q[d.rp];
+    case K_INS: {
+      int m = 1 << 30;
+      for (int i = 0; i < d.aux; ++i) m = min(m, (int)(int8_t)q[d.rp + i]);
+      return m;
+    }
+    default: return (int)R.mapq[r];
+  }
+}
+
+__device__ bool allele_is_variant(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Allele.isVariant
+  const int rl = allele_ref_len(a), al = allele_alt_len(a);
+  if (rl != al) return true;
+  for (int i = 0; i < rl; ++i)
+    if (allele_byte(R, a, pos, 0, i) != allele_byte(R, a, pos, 1, i)) return true;
+  return false;
+}
+__device__ bool allele_std_alt(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Likelihood.scala:106
+  const int al = allele_alt_len(a);
+  for (int i = 0; i < al; ++i)
+    if (!std_bit(allele_byte(R, a, pos, 1, i))) return false;
+  return true;
+}
+
+// Per-sample pileup summary held by one wave: a distinct-allele table (slot s * 64 + lane
+// lives in lane `lane`, register slot s) with per-allele counts and FP64 log sums.
+struct SamplePile {
+  uint64_t klo[kSlots], khi[kSlots];
+  AlleleDesc desc[kSlots];
+  uint32_t n_all[kSlots], n_f[kSlots];
+  double s1[kSlots], s0[kSlots], sh[kSlots];
+  int nt;             // used table entries (wave-uniform)
+  uint32_t depth_all; // elements
+  uint32_t depth_f;   // elements passing the mapping-quality filter
+  uint32_t fwd_f;     // ... on the positive strand
+  uint8_t refbase;
+  bool ambiguous, overflow;
+};
+
+__device__ void raise_at(Counters *ctr, int code, int64_t where) {
+  raise_error(&ctr->err, (int64_t *)&ctr->err_pos, code, where);
+}
+
+// Pileup.referenceBaseAtLocus over the reads of window [rb, re) covering pos (as in
+// germline_complex: first standard MD-derived base; heap order approximated by the minimum
+// (end, index) read when the bases disagree, flagged ambiguous).
+__device__ void pileup_ref(const DevReads &R, int64_t rb, int64_t re, int32_t pos, Counters *ctr, uint8_t &refbase,
+                           bool &ambiguous) {
+  const int lane = threadIdx.x & 63;
+  uint32_t mask = 0;
+  uint64_t best = ~0ull;
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    const int64_t r = r0 + lane;
+    if (r < re && R.start[r] <= pos && pos < R.end[r]) {
+      const int v = md_ref_at(R, r, pos);
+      if (v < 0) {
+        raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
+      } else if (std_bit((uint8_t)v)) {
+        mask |= std_bit((uint8_t)v);
+        const uint64_t key = ((uint64_t)(uint32_t)R.end[r] << 32) | (uint64_t)(r - rb);
+        best = key < best ? key : best;
+      }
+    }
+  }
+  for (int d = 1; d < 64; d <<= 1) {
+    mask |= __shfl_xor(mask, d, 64);
+    const uint64_t o = __shfl_xor(best, d, 64);
+    best = o < best ? o : best;
+  }
+  ambiguous = __popc(mask) > 1;
+  refbase = 'N';
+  if (ambiguous) refbase = (uint8_t)md_ref_at(R, rb + (int64_t)(best & 0xFFFFFFFFull), pos);
+  else if (mask) refbase = bit_base(mask);
+}
+
+// Build the allele table of one sample's pileup at pos.
+__device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
+                              bool include_alignment, Counters *ctr, SamplePile &P) {
+  const int lane = threadIdx.x & 63;
+  pileup_ref(R, rb, re, pos, ctr, P.refbase, P.ambiguous);
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    P.klo[s] = P.khi[s] = 0;
+    P.n_all[s] = P.n_f[s] = 0;
+    P.s1[s] = P.s0[s] = P.sh[s] = 0.0;
+  }
+  P.nt = 0;
+  P.depth_all = P.depth_f = P.fwd_f = 0;
+  P.overflow = false;
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    const int64_t r = r0 + lane;
+    bool act = r < re && R.start[r] <= pos && pos < R.end[r];
+    AlleleDesc d;
+    Key128 key{0, 0};
+    bool pass = false;
+    double l1 = 0.0, l0 = 0.0, lh = 0.0;
+    if (act) {
+      int errc = 0;
+      if (!classify(R, r, pos, P.refbase, d, &errc)) {
+        raise_at(ctr, errc, pos);
+        act = false;
+      } else {
+        key = allele_key(R, d, pos, 0);
+        const int mq = (int)R.mapq[r];
+        pass = min_mapq <= 0 || mq >= min_mapq;  // QualityAlignedReadsFilter (PileupElementsFilter.scala:25-36)
+        if (pass) {
+          const int q = elem_quality(R, d);
+          if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
+          double pc = phred_success(q < 0 ? 0 : q);
+          if (include_alignment) pc = pc * phred_success(mq);  // probabilityCorrectIncludingAlignment
+          // Likelihood.scala:166-188: log(P(e, a1) + P(e, a2)) with P = pc if e's allele is a, else 1 - pc
+          l1 = log(pc + pc);
+          lh = log(pc + (1.0 - pc));
+          l0 = log((1.0 - pc) + (1.0 - pc));
+        }
+      }
+    }
+    const unsigned long long actb = __ballot(act), passb = __ballot(act && pass);
+    P.depth_all += (uint32_t)__popcll(actb);
+    P.depth_f += (uint32_t)__popcll(passb);
+    P.fwd_f += (uint32_t)__popcll(__ballot(act && pass && !(R.flags[r < re ? r : rb] & 1)));
+    unsigned long long pending = actb;
+    while (pending) {
+      const int leader = __ffsll((long long)pending) - 1;
+      const uint64_t klo = __shfl(key.lo, leader, 64), khi = __shfl(key.hi, leader, 64);
+      const bool match = act && key.lo == klo && key.hi == khi;
+      const unsigned long long mb = __ballot(match);
+      const uint32_t na = (uint32_t)__popcll(mb), nf = (uint32_t)__popcll(mb & passb);
+      const bool mf = match && pass;
+      const double a1 = wave_sum(mf ? l1 : 0.0), a0 = wave_sum(mf ? l0 : 0.0), ah = wave_sum(mf ? lh : 0.0);
+      int found = -1;
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        const bool hit = (s * 64 + lane) < P.nt && P.klo[s] == klo && P.khi[s] == khi;
+        const unsigned long long hb = __ballot(hit);
+        if (found < 0 && hb) found = s * 64 + (__ffsll((long long)hb) - 1);
+      }
+      if (found < 0) {
+        if (P.nt >= 64 * kSlots) {
+          P.overflow = true;
+        } else {
+          found = P.nt++;
+          const int owner = found & 63, sl = found >> 6;
+          AlleleDesc ld;
+          ld.read = __shfl(d.read, leader, 64);
+          ld.aux = __shfl(d.aux, leader, 64);
+          ld.rp = __shfl(d.rp, leader, 64);
+          ld.kind = (uint8_t)__shfl((int)d.kind, leader, 64);
+          ld.rb = (uint8_t)__shfl((int)d.rb, leader, 64);
+          ld.base = (uint8_t)__shfl((int)d.base, leader, 64);
+          ld.pad = 0;
+#pragma unroll
+          for (int s = 0; s < kSlots; ++s)
+            if (s == sl && lane == owner) {
+              P.klo[s] = klo;
+              P.khi[s] = khi;
+              P.desc[s] = ld;
+            }
+        }
+      }
+      if (found >= 0) {
+        const int owner = found & 63, sl = found >> 6;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+          if (s == sl && lane == owner) {
+            P.n_all[s] += na;
+            P.n_f[s] += nf;
+            P.s1[s] += a1;
+            P.s0[s] += a0;
+            P.sh[s] += ah;
+          }
+      }
+      pending &= ~mb;
+    }
+  }
+}
+
+// Broadcast table entry j (owner lane j & 63, register slot j >> 6) of a SamplePile field.
+#define PILE_GET(P, field, j, out)                                  \
+  do {                                                              \
+    _Pragma("unroll") for (int _s = 0; _s < kSlots; ++_s) if (_s == ((j) >> 6)) \
+      out = __shfl(P.field[_s], (j) & 63, 64);                      \
+  } while (0)
+
+__device__ AlleleDesc pile_desc(const SamplePile &P, int j) {
+  AlleleDesc d{};
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s)
+    if (s == (j >> 6)) {
+      const int o = j & 63;
+      d.read = __shfl(P.desc[s].read, o, 64);
+      d.aux = __shfl(P.desc[s].aux, o, 64);
+      d.rp = __shfl(P.desc[s].rp, o, 64);
+      d.kind = (uint8_t)__shfl((int)P.desc[s].kind, o, 64);
+      d.rb = (uint8_t)__shfl((int)P.desc[s].rb, o, 64);
+      d.base = (uint8_t)__shfl((int)P.desc[s].base, o, 64);
+    }
+  return d;
+}
+
+// Genotype likelihoods of one sample (Likelihood.likelihoodsOfAllPossibleGenotypesFromPileup,
+// normalised, not log space).  Eligible alleles (filtered count > 0, standard alt bases) are
+// ranked by Allele order into `order[0..n)` (LDS, per wave); genotype g <-> (i <= j) in the
+// reference's enumeration order.  Returns n; per lane: likelihoods of genotypes lane, lane+64..
+// are reduced by the caller through the two callbacks.
+struct GenoResult {
+  int n;          // eligible alleles
+  int G;          // genotypes
+  int best_g;     // maxBy (first maximum)
+  double best_l;  // its normalised likelihood
+  double var_sum; // sum of normalised likelihoods of genotypes with a variant allele
+  int bi, bj;     // table entries of the best genotype's alleles
+};
+
+__device__ void genotype_index(int g, int n, int &i, int &j) {  // g -> (i, j), i <= j, row-major
+  int row = 0, rem = g;
+  while (rem >= n - row) {
+    rem -= n - row;
+    ++row;
+  }
+  i = row;
+  j = row + rem;
+}
+
+__device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, int32_t pos, int16_t *order,
+                                uint8_t *is_var) {
+  const int lane = threadIdx.x & 63;
+  GenoResult res{};
+  // eligibility + variant flag per entry (entry j on lane j & 63, slot j >> 6)
+  bool elig[kSlots], var[kSlots];
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    const int j = s * 64 + lane;
+    elig[s] = j < P.nt && P.n_f[s] > 0 && allele_std_alt(R, P.desc[s], pos);
+    var[s] = j < P.nt && allele_is_variant(R, P.desc[s], pos);
+  }
+  // rank of each eligible entry among eligible entries by Allele order
+  int n = 0;
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) n += __popcll(__ballot(elig[s]));
+  res.n = n;
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    int rank = 0;
+    for (int k = 0; k < P.nt; ++k) {
+      const AlleleDesc dk = pile_desc(P, k);
+      bool ek = false;
+      _Pragma("unroll") for (int t = 0; t < kSlots; ++t) if (t == (k >> 6)) ek = __shfl((int)elig[t], k & 63, 64);
+      if (elig[s] && ek && k != s * 64 + lane && allele_cmp(R, dk, P.desc[s], pos) < 0) ++rank;
+    }
+    if (elig[s]) order[rank] = (int16_t)(s * 64 + lane);
+    if (s * 64 + lane < 64 * kSlots) is_var[s * 64 + lane] = var[s] ? 1 : 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const int G = n * (n + 1) / 2;
+  res.G = G;
+  if (G == 0) return res;
+  const double ln2d = log(2.0) * (double)P.depth_f;
+  // log-likelihood of this lane's genotype in chunk g0 (wave-uniform call: the table
+  // broadcasts below need every lane)
+  auto ll_chunk = [&](int g0) -> double {
+    const int g = g0 + lane;
+    int ei = -1, ej = -1;
+    if (g < G) {
+      int i, j;
+      genotype_index(g, n, i, j);
+      ei = order[i];
+      ej = order[j];
+    }
+    double agg = 0.0;
+    for (int x = 0; x < P.nt; ++x) {
+      uint32_t nf = 0;
+      PILE_GET(P, n_f, x, nf);
+      if (nf == 0) continue;  // uniform
+      double a1 = 0, a0 = 0, ah = 0;
+      PILE_GET(P, s1, x, a1);
+      PILE_GET(P, s0, x, a0);
+      PILE_GET(P, sh, x, ah);
+      agg += (x == ei && x == ej) ? a1 : (x == ei || x == ej) ? ah : a0;
+    }
+    return agg + log(1.0) - ln2d;
+  };
+  double tot = 0.0;
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const double ll = ll_chunk(g0);
+    if (g0 + lane < G) tot += exp(ll);
+  }
+  const double lt = log(wave_sum(tot));
+  double best = -1.0, vsum = 0.0;
+  int bestg = 0x7FFFFFFF;
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const double ll = ll_chunk(g0);
+    const int g = g0 + lane;
+    if (g >= G) continue;
+    const double L = exp(ll - lt);
+    int i, j;
+    genotype_index(g, n, i, j);
+    if (is_var[order[i]] || is_var[order[j]]) vsum += L;
+    if (L > best) {
+      best = L;
+      bestg = g;
+    }
+  }
+  // wave argmax with first-maximum tie break (maxBy)
+  for (int d = 1; d < 64; d <<= 1) {
+    const double ob = __shfl_xor(best, d, 64);
+    const int og = __shfl_xor(bestg, d, 64);
+    if (ob > best || (ob == best && og < bestg)) {
+      best = ob;
+      bestg = og;
+    }
+  }
+  res.best_g = bestg;
+  res.best_l = best;
+  res.var_sum = wave_sum(vsum);
+  int i, j;
+  genotype_index(bestg, n, i, j);
+  res.bi = order[i];
+  res.bj = order[j];
+  return res;
+}
+
+// AlleleEvidence.apply (AlleleEvidence.scala:58-101) for the elements of one sample whose
+// allele key is `target`.  Supporting elements' (mapq, quality, mismatches) go to `ev_lds`
+// in element order for the running mean and the medians.
+__device__ void allele_evidence(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
+                                const SamplePile &P, Key128 target, double likelihood, uint32_t *ev_lds,
+                                Counters *ctr, gq_evidence &ev) {
+  const int lane = threadIdx.x & 63;
+  uint32_t n = 0, fwd = 0;
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    const int64_t r = r0 + lane;
+    bool hit = false;
+    uint32_t packed = 0;
+    if (r < re && R.start[r] <= pos && pos < R.end[r]) {
+      const int mq = (int)R.mapq[r];
+      if (min_mapq <= 0 || mq >= min_mapq) {
+        AlleleDesc d;
+        int errc = 0;
+        if (classify(R, r, pos, P.refbase, d, &errc)) {
+          const Key128 k = allele_key(R, d, pos, 0);
+          if (k.lo == target.lo && k.hi == target.hi) {
+            hit = true;
+            if (R.n_md[r] < 0) raise_at(ctr, GQ_E_NO_MD, pos);
+            packed = (uint32_t)mq | ((uint32_t)(uint8_t)(int8_t)elem_quality(R, d) << 8) |
+                     ((uint32_t)R.n_mismatch[r] << 16);
+          }
+        }
+      }
+    }
+    const unsigned long long hb = __ballot(hit);
+    const uint32_t before = (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
+    if (hit && n + before < (uint32_t)kEvCap) ev_lds[n + before] = packed;
+    fwd += (uint32_t)__popcll(__ballot(hit && !(R.flags[r < re ? r : rb] & 1)));
+    n += (uint32_t)__popcll(hb);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  ev.likelihood = likelihood;
+  ev.read_depth = (int32_t)P.depth_f;
+  ev.forward_depth = (int32_t)P.fwd_f;
+  ev.allele_read_depth = (int32_t)n;
+  ev.allele_forward_depth = (int32_t)fwd;
+  if (n == 0) {
+    ev.mean_mq = ev.median_mq = ev.mean_bq = ev.median_bq = ev.median_mismatches = __builtin_nan("");
+    return;
+  }
+  if (n > (uint32_t)kEvCap) {
+    raise_at(ctr, GQ_E_CAPACITY, pos);
+    ev.mean_mq = ev.median_mq = ev.mean_bq = ev.median_bq = ev.median_mismatches = __builtin_nan("");
+    return;
+  }
+  // breeze.stats.mean: running mean in element order
+  double mq = 0.0, bq = 0.0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t v = ev_lds[k];
+    mq += ((double)(v & 0xFFu) - mq) / (double)(k + 1);
+    bq += ((double)(int8_t)((v >> 8) & 0xFFu) - bq) / (double)(k + 1);
+  }
+  ev.mean_mq = mq;
+  ev.mean_bq = bq;
+  // k-th smallest by rank counting (lane-parallel over the elements)
+  auto kth = [&](int field, uint32_t k) -> int {
+    auto val = [&](uint32_t v) -> int {
+      return field == 0 ? (int)(v & 0xFFu) : field == 1 ? (int)(int8_t)((v >> 8) & 0xFFu) : (int)(v >> 16);
+    };
+    int found = 0x7FFFFFFF;
+    for (uint32_t e = lane; e < n; e += 64) {
+      const int x = val(ev_lds[e]);
+      uint32_t lt = 0, le = 0;
+      for (uint32_t f = 0; f < n; ++f) {
+        const int y = val(ev_lds[f]);
+        lt += y < x;
+        le += y <= x;
+      }
+      if (lt <= k && k < le) found = x;
+    }
+    for (int d = 1; d < 64; d <<= 1) found = min(found, __shfl_xor(found, d, 64));
+    return found;
+  };
+  if (n & 1) {
+    ev.median_mq = (double)kth(0, (n - 1) / 2);
+    ev.median_bq = (double)kth(1, (n - 1) / 2);
+    ev.median_mismatches = (double)kth(2, (n - 1) / 2);
+  } else {
+    ev.median_mq = ((double)kth(0, n / 2 - 1) + (double)kth(0, n / 2)) / 2.0;
+    ev.median_bq = ((double)kth(1, n / 2 - 1) + (double)kth(1, n / 2)) / 2.0;
+    ev.median_mismatches = (double)((kth(2, n / 2 - 1) + kth(2, n / 2)) / 2);  // Int median (parity unpinned)
+  }
+}
+
+constexpr int kSomWaves = kBlock / 64;
+
+__global__ __launch_bounds__(kBlock) void somatic_call(const Tile *__restrict__ tiles_t,
+                                                       const Tile *__restrict__ tiles_n,
+                                                       const ComplexItem *__restrict__ items, DevReads RT,
+                                                       DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
+                                                       unsigned long long rec_cap, uint8_t *__restrict__ pool,
+                                                       unsigned long long pool_cap, unsigned long long cand_cap,
+                                                       Counters *ctr) {
+  __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
+  __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
+  __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const unsigned long long n_items = ctr->n_complex < cand_cap ? ctr->n_complex : cand_cap;
+  for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
+    const ComplexItem item = items[it];
+    const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
+    const int32_t pos = item.pos;
+    SamplePile PT, PN;
+    gather_sample(RT, tt.rb, tt.re, pos, prm.min_mapq, true, ctr, PT);
+    gather_sample(RN, tn.rb, tn.re, pos, prm.min_mapq, false, ctr, PN);
+    if (PT.overflow || PN.overflow) {
+      raise_at(ctr, GQ_E_CAPACITY, pos);
+      continue;
+    }
+    if ((item.flags & 1) && (PT.depth_all + PN.depth_all) > 0 && lane == 0)
+      atomicAdd(&ctr->spread[0][it & (kSpread - 1)], 1ull);
+    // MultiAllelicPileupFilter (PileupFilter.scala:29-44): > 2 distinct alleles => no elements
+    if (prm.filter_multi_allelic) {
+      if (PT.nt > 2) PT.depth_f = 0;
+      if (PN.nt > 2) PN.depth_f = 0;
+    }
+    // SomaticStandardCaller.scala:184-190
+    if (PT.depth_f == 0 || PN.depth_f == 0 || (int64_t)PT.depth_f > (int64_t)prm.max_read_depth ||
+        (int64_t)PN.depth_f > (int64_t)prm.max_read_depth)
+      continue;
+    {  // tumor pileup must hold a non-Match element: Match = allele (ref, ref) of one byte
+      uint32_t ref_match = 0;
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        const bool m = (s * 64 + lane) < PT.nt && PT.desc[s].kind == K_SNV && PT.desc[s].base == PT.refbase;
+        ref_match += (uint32_t)wave_sum(m ? (double)PT.n_f[s] : 0.0);
+      }
+      if (ref_match == PT.depth_f) continue;
+    }
+    const GenoResult tg = genotypes(RT, PT, pos, order_lds[wv], var_lds[wv]);
+    if (tg.G == 0) continue;
+    const bool t_var = var_lds[wv][tg.bi] || var_lds[wv][tg.bj];
+    if (!t_var) continue;
+    const GenoResult ng = genotypes(RN, PN, pos, order_lds[wv], var_lds[wv]);
+    const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
+    const double odds = tg.best_l / nvs;
+    if (!(odds * 100.0 >= (double)prm.odds)) continue;
+    // decisions taken within FP rounding of a threshold are flagged (GQ_FLAG_KNIFE_EDGE):
+    // their outcome depends on summation order in the reference too
+    uint8_t knife = near_edge(odds * 100.0, (double)prm.odds) ? GQ_FLAG_KNIFE_EDGE : 0;
+    // first variant allele of the ML genotype with a non-empty alt (SomaticStandardCaller.scala:227)
+    const AlleleDesc a1 = pile_desc(PT, tg.bi), a2 = pile_desc(PT, tg.bj);
+    const bool v1 = allele_is_variant(RT, a1, pos) && allele_alt_len(a1) > 0;
+    const bool v2 = allele_is_variant(RT, a2, pos) && allele_alt_len(a2) > 0;
+    if (!v1 && !v2) continue;
+    const AlleleDesc al = v1 ? a1 : a2;
+    const int rl = allele_ref_len(al), alt_l = allele_alt_len(al);
+    const Key128 tkey = allele_key(RT, al, pos, 0);
+    const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
+    gq_evidence tev, nev;
+    allele_evidence(RT, tt.rb, tt.re, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev);
+    allele_evidence(RN, tn.rb, tn.re, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev);
+    const double log_odds = log(odds);
+    const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
+    if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
+    const float vaf = (float)tev.allele_read_depth / (float)tev.read_depth;
+    if (prm.apply_filters == 1) {  // SomaticStandardCaller.scala:124-137 then SomaticGenotypeFilter.apply (:285-307)
+      const bool depth_ok = tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
+                            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF;
+      if (!depth_ok) continue;
+      if (!(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth)) continue;
+      if (!(log_odds > (double)prm.min_lod)) continue;
+      if (near_edge(log_odds, (double)prm.min_lod)) knife |= GQ_FLAG_KNIFE_EDGE;
+      if (!(gqv >= prm.min_likelihood)) continue;
+      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
+      if (!(tev.mean_mq >= prm.min_average_mapping_quality && nev.mean_mq >= prm.min_average_mapping_quality)) continue;
+      if (near_edge(tev.mean_mq, prm.min_average_mapping_quality) || near_edge(nev.mean_mq, prm.min_average_mapping_quality) ||
+          near_edge(tev.mean_mq, prm.min_average_base_quality) || near_edge(nev.mean_mq, prm.min_average_base_quality))
+        knife |= GQ_FLAG_KNIFE_EDGE;
+      // the "average base quality" filter tests mean mapping quality (SomaticGenotypeFilter.scala:194-195)
+      if (!(tev.mean_mq >= prm.min_average_base_quality && nev.mean_mq >= prm.min_average_base_quality)) continue;
+      if (!(tev.median_mismatches <= (double)prm.max_median_mismatches)) continue;
+    } else if (prm.apply_filters == 2) {  // SomaticGenotypeFilter(Seq, ...) as the caller suite uses it
+      if (!(tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
+            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF))
+        continue;
+      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
+      if (!(gqv >= prm.min_likelihood)) continue;
+      if (prm.min_tumor_alternate_read_depth > 0 && !(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth))
+        continue;
+    }
+    SomRec rr;
+    rr.key = (uint64_t)(tt.ordinal0 + (pos - tt.L0)) << 12;
+    rr.contig = tt.contig;
+    rr.pos = pos;
+    rr.ref_len = (uint16_t)rl;
+    rr.alt_len = (uint16_t)alt_l;
+    rr.flags = (PT.ambiguous ? 1 : 0) | (PN.ambiguous ? 2 : 0) | knife;
+    rr.pad[0] = rr.pad[1] = rr.pad[2] = 0;
+    rr.log_odds = log_odds;
+    rr.gq = gqv;
+    rr.pad2 = 0;
+    rr.tumor = tev;
+    rr.normal = nev;
+    if (rl + alt_l <= 8) {
+      uint64_t v = 0;
+      int j = 0;
+      for (int i = 0; i < rl; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 0, i) << (8 * j++);
+      for (int i = 0; i < alt_l; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 1, i) << (8 * j++);
+      rr.allele = v;
+    } else {
+      unsigned long long off = 0;
+      if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + alt_l));
+      off = __shfl(off, 0, 64);
+      if (off + rl + alt_l <= pool_cap)
+        for (int i = lane; i < rl + alt_l; i += 64)
+          pool[off + i] = i < rl ? allele_byte(RT, al, pos, 0, i) : allele_byte(RT, al, pos, 1, i - rl);
+      rr.allele = off;
+    }
+    if (lane == 0) {
+      const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
+      if (k < rec_cap) recs[k] = rr;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_reads *n, const gq_loci *loci,
+                              const gq_somatic_params *p, gq_somatic_calls **out) {
+  if (!c || !t || !n || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_somatic_standard: null argument");
+  if (t->d.n_contigs != n->d.n_contigs)
+    return set_err(GQ_E_ARG, "tumor and normal read sets must share the contig list (%d vs %d contigs)",
+                   t->d.n_contigs, n->d.n_contigs);
+  HIP_TRY(hipSetDevice(c->device));
+  const auto h0 = std::chrono::steady_clock::now();
+  c->timings = gq_timings{};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  Plan pt, pn;
+  gq_status st = plan(c, t, loci, kSomT, pt, c->tiles);
+  if (st) return st;
+  st = plan(c, n, loci, kSomT, pn, c->tiles2);
+  if (st) return st;
+  gq_somatic_calls *res = (gq_somatic_calls *)calloc(1, sizeof(gq_somatic_calls));
+  if (!res) return set_err(GQ_E_NOMEM, "calloc");
+  if (pt.n_tiles == 0) {
+    *out = res;
+    return GQ_OK;
+  }
+  unsigned long long cand_cap = std::max<unsigned long long>(1 << 16, pt.n_loci / 4);
+  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20;
+  Counters hc{};
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c->cplx.ensure(cand_cap * sizeof(ComplexItem)));
+    HIP_TRY(c->srecs.ensure(rec_cap * sizeof(SomRec)));
+    HIP_TRY(c->pool.ensure(pool_cap));
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    Counters *ctr = (Counters *)c->counters.p;
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL((somatic_tile<kSomT>), dim3((unsigned)pt.n_tiles), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, t->d, n->d, (ComplexItem *)c->cplx.p,
+                       cand_cap, ctr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
+    hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                       (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bool retry = false;
+    if (hc.n_complex > cand_cap) {
+      cand_cap = hc.n_complex + 1024;
+      retry = true;
+    }
+    if (hc.n_rec > rec_cap) {
+      rec_cap = hc.n_rec + 1024;
+      retry = true;
+    }
+    if (hc.pool_used > pool_cap) {
+      pool_cap = hc.pool_used + 4096;
+      retry = true;
+    }
+    if (!retry) break;
+    if (attempt == 2) {
+      free(res);
+      return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
+    }
+  }
+  for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
+  st = check_device_error(c, hc);
+  if (st) {
+    free(res);
+    return st;
+  }
+  const int64_t nr = (int64_t)hc.n_rec;
+  std::vector<SomRec> recs((size_t)nr);
+  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
+  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::sort(recs.begin(), recs.end(), [](const SomRec &a, const SomRec &b) { return a.key < b.key; });
+  const size_t N = (size_t)std::max<int64_t>(nr, 1);
+  res->n = nr;
+  res->contig = (int32_t *)malloc(N * 4);
+  res->pos = (int64_t *)malloc(N * 8);
+  res->sample = (uint8_t *)calloc(N, 1);
+  res->ref_off = (int64_t *)malloc(N * 8);
+  res->alt_off = (int64_t *)malloc(N * 8);
+  res->ref_len = (int32_t *)malloc(N * 4);
+  res->alt_len = (int32_t *)malloc(N * 4);
+  res->log_odds = (double *)malloc(N * 8);
+  res->gq = (int32_t *)malloc(N * 4);
+  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->flags = (uint8_t *)malloc(N);
+  std::vector<uint8_t> apool;
+  for (int64_t k = 0; k < nr; ++k) {
+    const SomRec &r = recs[(size_t)k];
+    res->contig[k] = r.contig;
+    res->pos[k] = r.pos;
+    res->ref_len[k] = r.ref_len;
+    res->alt_len[k] = r.alt_len;
+    res->ref_off[k] = (int64_t)apool.size();
+    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
+    const int tot = r.ref_len + r.alt_len;
+    if (tot <= 8)
+      for (int i = 0; i < tot; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
+    else
+      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele, hpool.begin() + (ptrdiff_t)(r.allele + tot));
+    res->log_odds[k] = r.log_odds;
+    res->gq[k] = r.gq;
+    res->tumor[k] = r.tumor;
+    res->normal[k] = r.normal;
+    res->flags[k] = r.flags;
+  }
+  res->pool_len = (int64_t)apool.size();
+  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
+  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  res->visited_loci = (int64_t)hc.visited;
+  res->candidate_loci = (int64_t)hc.n_complex;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timings.pileup_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+  c->timings.complex_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[3], c->ev[4]);
+  c->timings.finalize_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[4]);
+  c->timings.total_ms = ms;
+  c->timings.pileup_launches = 1;
+  c->timings.tiles = pt.n_tiles;
+  c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
+  *out = res;
+  return GQ_OK;
+}
+
+void gq_free_somatic(gq_somatic_calls *r) {
+  if (!r) return;
+  free(r->contig);
+  free(r->pos);
+  free(r->sample);
+  free(r->ref_off);
+  free(r->alt_off);
+  free(r->ref_len);
+  free(r->alt_len);
+  free(r->allele_pool);
+  free(r->log_odds);
+  free(r->gq);
+  free(r->tumor);
+  free(r->normal);
+  free(r->flags);
+  free(r);
+}
+
+}  // extern "C"

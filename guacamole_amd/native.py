@@ -18,6 +18,7 @@ _lib = None
 GT_NAMES = {0: "Ref", 1: "Alt", 2: "OtherAlt", 3: "NoCall"}
 FLAG_AMBIGUOUS_REF = 1
 FLAG_TIE = 2
+FLAG_KNIFE_EDGE = 4
 
 
 class GQError(RuntimeError):
@@ -79,6 +80,18 @@ class gq_evidence(C.Structure):
                 ("forward_depth", C.c_int32), ("allele_forward_depth", C.c_int32), ("mean_mq", C.c_double),
                 ("median_mq", C.c_double), ("mean_bq", C.c_double), ("median_bq", C.c_double),
                 ("median_mismatches", C.c_double)]
+
+
+# SomaticStandard.Arguments defaults (commands/SomaticStandardCaller.scala:40-64 and
+# filters/SomaticGenotypeFilter.scala:31-56); apply_filters 1 = the driver's filter chain.
+SOMATIC_DEFAULTS = dict(odds=20, min_mapq=1, filter_multi_allelic=0, max_read_depth=2 ** 31 - 1,
+                        min_tumor_read_depth=0, max_tumor_read_depth=2 ** 31 - 1, min_normal_read_depth=0,
+                        min_tumor_alternate_read_depth=0, min_lod=0, min_likelihood=0, min_vaf=0,
+                        min_average_mapping_quality=0, min_average_base_quality=0,
+                        max_median_mismatches=2 ** 31 - 1, apply_filters=1)
+
+EVIDENCE_FIELDS = ("likelihood", "read_depth", "allele_read_depth", "forward_depth", "allele_forward_depth",
+                   "mean_mq", "median_mq", "mean_bq", "median_bq", "median_mismatches")
 
 
 class gq_somatic_calls(C.Structure):
@@ -198,6 +211,20 @@ class Context:
         _check(lib().gq_germline_threshold(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
         return GermlineCalls.from_result(out)
 
+    def somatic_standard(self, tumor: "DeviceReads", normal: "DeviceReads", loci, **params) -> "SomaticCalls":
+        """somatic-standard over the loci ranges (gq_somatic_standard).  params: the
+        gq_somatic_params fields; defaults SOMATIC_DEFAULTS (the CLI defaults)."""
+        L, keep = make_gq_loci(*loci)
+        p = dict(SOMATIC_DEFAULTS)
+        p.update(params)
+        ps = gq_somatic_params(**{k: int(v) for k, v in p.items()})
+        out = C.POINTER(gq_somatic_calls)()
+        _check(lib().gq_somatic_standard(self.h, tumor.h, normal.h, C.byref(L), C.byref(ps), C.byref(out)))
+        try:
+            return SomaticCalls.from_struct(out.contents)
+        finally:
+            lib().gq_free_somatic(out)
+
     def pileup_counts(self, reads: "DeviceReads", loci) -> Dict[str, np.ndarray]:
         L, keep = make_gq_loci(*loci)
         out = C.POINTER(gq_counts)()
@@ -301,3 +328,26 @@ class GermlineCalls:
         return [(contig_names[a["contig"][i]], int(a["pos"][i]), int(a["sample"][i]),
                  (GT_NAMES[int(a["gt0"][i])], GT_NAMES[int(a["gt1"][i])]), self.ref(i), self.alt(i),
                  int(a["flags"][i])) for i in range(len(self))]
+
+
+class SomaticCalls:
+    """CalledSomaticAllele records in output order."""
+
+    def __init__(self, rows: List[dict], visited: int, candidates: int):
+        self.rows, self.visited_loci, self.candidate_loci = rows, visited, candidates
+
+    @staticmethod
+    def from_struct(c: gq_somatic_calls) -> "SomaticCalls":
+        pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
+        rows = []
+        for i in range(c.n):
+            ro, rl, ao, al = c.ref_off[i], c.ref_len[i], c.alt_off[i], c.alt_len[i]
+            ev = lambda e: tuple(getattr(e, k) for k in EVIDENCE_FIELDS)
+            rows.append(dict(contig=int(c.contig[i]), locus=int(c.pos[i]), sample=int(c.sample[i]),
+                             ref=pool[ro:ro + rl].decode("latin-1"), alt=pool[ao:ao + al].decode("latin-1"),
+                             log_odds=float(c.log_odds[i]), gq=int(c.gq[i]), tumor=ev(c.tumor[i]),
+                             normal=ev(c.normal[i]), flags=int(c.flags[i])))
+        return SomaticCalls(rows, int(c.visited_loci), int(c.candidate_loci))
+
+    def __len__(self) -> int:
+        return len(self.rows)

@@ -106,6 +106,28 @@ class ReadSet:
                 out.append((name, self.start[m], self.end[m]))
         return out
 
+    def subset(self, idx) -> "ReadSet":
+        """ReadSet of the reads `idx` (kept in the given order; pools re-packed)."""
+        idx = np.asarray(idx, dtype=np.int64)
+
+        def pool(off, ln, data):
+            lens = np.maximum(ln[idx], 0).astype(np.int64)
+            new_off = np.zeros(len(idx), np.int64)
+            if len(idx):
+                new_off[1:] = np.cumsum(lens)[:-1]
+            parts = [data[off[i]:off[i] + max(int(ln[i]), 0)] for i in idx]
+            return new_off, (np.concatenate(parts) if parts else data[:0].copy())
+
+        seq_off, seq = pool(self.seq_off, self.seq_len, self.seq)
+        _, qual = pool(self.seq_off, self.seq_len, self.qual)
+        cigar_off, cigar = pool(self.cigar_off, self.n_cigar, self.cigar)
+        md_off, md = pool(self.md_off, self.md_len, self.md)
+        return ReadSet(self.contig_names, self.contig_lengths, self.sample_names, self.contig[idx].copy(),
+                       self.start[idx].copy(), self.end[idx].copy(), self.mapq[idx].copy(), self.flags[idx].copy(),
+                       self.sample[idx].copy(), seq_off, self.seq_len[idx].copy(), seq, qual, cigar_off,
+                       self.n_cigar[idx].copy(), cigar, md_off, self.md_len[idx].copy(), md,
+                       None if self.names is None else [self.names[i] for i in idx])
+
     def cigar_string(self, i: int) -> str:
         ops = self.cigar[self.cigar_off[i]:self.cigar_off[i] + self.n_cigar[i]]
         return "".join("%d%s" % (int(c) >> 4, CIGAR_OPS[int(c) & 15]) for c in ops)
@@ -228,8 +250,10 @@ def load_reads(path: str, filters: InputFilters = InputFilters()) -> ReadSet:
     samtools path, then ReadSet.mappedReads)."""
     with open(path, "rb") as fh:
         head = fh.read(2)
-    if head == b"\x1f\x8b":
-        return _load_bam(path, filters)
+    if head == b"\x1f\x8b":  # BGZF (BAM) or a gzip-compressed SAM
+        with gzip.open(path, "rb") as fh:
+            if fh.read(4) == b"BAM\x01":
+                return _load_bam(path, filters)
     return _load_sam(path, filters)
 
 

@@ -103,10 +103,13 @@ typedef struct {
 
 /* GenotypeAllele codes (bdg-formats): */
 enum { GQ_GT_REF = 0, GQ_GT_ALT = 1, GQ_GT_OTHERALT = 2, GQ_GT_NOCALL = 3 };
-/* per-call flags */
+/* per-call flags (somatic calls: bit0 / bit1 = tumor / normal reference base
+ * ambiguous, plus GQ_FLAG_KNIFE_EDGE) */
 enum {
   GQ_FLAG_AMBIGUOUS_REF = 1, /* pileup ref base decided by JVM heap order (MD tags disagree) */
-  GQ_FLAG_TIE = 2            /* count tie among passing alleles (JVM hash order unpinned)   */
+  GQ_FLAG_TIE = 2,           /* count tie among passing alleles (JVM hash order unpinned)   */
+  GQ_FLAG_KNIFE_EDGE = 4     /* somatic: a test or filter decided within FP rounding of its
+                                threshold (outcome depends on summation order)              */
 };
 
 /* Germline genotype records (Genotype.newBuilder, GermlineThresholdCaller.scala:106-117),

@@ -1013,6 +1013,10 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
         if (g.first.hasVariantAllele()) nvs += g.second;
       double odds = mll / nvs;
       if (!(odds * 100 >= prm->odds)) return;
+      // test-infrastructure flag (same rule as the device, GQ_FLAG_KNIFE_EDGE = 4): a decision
+      // within FP rounding of its threshold depends on summation order in the reference itself
+      auto nearEdge = [](double a, double b) { return std::fabs(a - b) <= 1e-9 * std::max(1.0, std::fabs(b)); };
+      if (nearEdge(odds * 100, prm->odds)) flags |= 4;
       const Allele *allele = nullptr;
       for (const Allele *a : {&mlg.a1, &mlg.a2})
         if (a->isVariant() && !a->alt.empty()) {
@@ -1024,6 +1028,10 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
       Evidence nev = alleleEvidence(1 - nvs, Allele{allele->ref, allele->ref}, fn);
       double logOdds = std::log(odds);
       int gq = successProbabilityToPhred(tev.likelihood * nev.likelihood - 1e-10);
+      {
+        double x = -10.0 * std::log10(1.0 - (tev.likelihood * nev.likelihood - 1e-10));
+        if (std::isfinite(x) && std::fabs((x - std::floor(x)) - 0.5) <= 1e-6) flags |= 4;
+      }
       if (filterMode == 1) {
         // SomaticStandardCaller.scala:124-137 then SomaticGenotypeFilter.apply (:285-307)
         auto depthOk = [&]() {
@@ -1036,10 +1044,14 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
         if (prm->min_tumor_alternate_read_depth > 0 && !(tev.alleleReadDepth >= prm->min_tumor_alternate_read_depth))
           return;
         if (!(logOdds > prm->min_lod)) return;
+        if (nearEdge(logOdds, prm->min_lod)) flags |= 4;
         if (!(gq >= prm->min_likelihood)) return;
         if (!((double)tev.vaf() * 100.0 > prm->min_vaf)) return;
         if (!(tev.meanMQ >= prm->min_average_mapping_quality && nev.meanMQ >= prm->min_average_mapping_quality))
           return;
+        if (nearEdge(tev.meanMQ, prm->min_average_mapping_quality) || nearEdge(nev.meanMQ, prm->min_average_mapping_quality) ||
+            nearEdge(tev.meanMQ, prm->min_average_base_quality) || nearEdge(nev.meanMQ, prm->min_average_base_quality))
+          flags |= 4;
         if (!(tev.meanMQ >= prm->min_average_base_quality && nev.meanMQ >= prm->min_average_base_quality)) return;
         if (!(tev.medianMismatches <= prm->max_median_mismatches)) return;
       }

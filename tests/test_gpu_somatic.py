@@ -1,0 +1,124 @@
+"""GPU parity: somatic-standard (HIP, gfx950) vs the CPU oracle.
+
+Tolerances (BASELINE.json north_star): loci, alleles, depths and flags bit-exact; somatic
+log-odds and likelihoods within 1e-6 (the GPU sums per-allele log terms in a different
+order than Colt's aggregate); mean / median evidence exact up to 1e-9 (NaN == NaN)."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import fixture
+from guacamole_amd import native
+from guacamole_amd.commands import somatic_standard_reads
+from guacamole_amd.loci import LociSet, flatten_partitions, partition_loci_uniformly
+from guacamole_amd.reads import InputFilters, load_reads, make_read as mr, make_read_set
+from guacamole_amd.synthetic import generate
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# SomaticStandard.Caller.run input filters (SomaticStandardCaller.scala:69-73)
+TN_FILTERS = InputFilters.make(mapped=True, non_duplicate=True, passed_vendor_quality_checks=True, has_md_tag=True)
+PAIRS = [("tumor.chr20.tough.sam", "normal.chr20.tough.sam"),
+         ("tumor.chr20.simplefp.sam", "normal.chr20.simplefp.sam"),
+         ("synthetic.challenge.set1.tumor.v2.withMDTags.chr2.syn1fp.sam",
+          "synthetic.challenge.set1.normal.v2.withMDTags.chr2.syn1fp.sam"),
+         ("synthetic.challenge.set1.tumor.v2.withMDTags.chr2.complexvar.sam",
+          "synthetic.challenge.set1.normal.v2.withMDTags.chr2.complexvar.sam")]
+SUITE = dict(odds=120, min_mapq=1, min_tumor_read_depth=8, max_tumor_read_depth=200, min_normal_read_depth=4,
+             min_tumor_alternate_read_depth=3, min_likelihood=70, min_vaf=5)
+
+
+def _loci(rs, expr="all"):
+    ls = LociSet.parse(expr).result(rs.contig_lengths_map)
+    return flatten_partitions(partition_loci_uniformly(1, ls), rs.contig_index())
+
+
+def _close(a, b, tol):
+    if a == b:
+        return True
+    if isinstance(a, float) and math.isnan(a):
+        return isinstance(b, float) and math.isnan(b)
+    if isinstance(a, float) or isinstance(b, float):
+        return abs(a - b) <= tol * max(1.0, abs(b))
+    return a == b
+
+
+KNIFE = native.FLAG_KNIFE_EDGE
+
+
+def assert_rows_match(got, want):
+    """Strict comparison, except rows that either side flags GQ_FLAG_KNIFE_EDGE (a decision
+    within FP rounding of its threshold): those may be present on one side only."""
+    key = lambda r: (r["contig"], r["locus"], r["ref"], r["alt"])
+    knife = {key(r) for r in got + want if r["flags"] & KNIFE}
+    got = [r for r in got if key(r) not in knife]
+    want = [r for r in want if key(r) not in knife]
+    assert [key(r) for r in got] == [key(r) for r in want]
+    for g, w in zip(got, want):
+        assert _close(g["log_odds"], w["log_odds"], 1e-6), (key(g), g["log_odds"], w["log_odds"])
+        assert abs(g["gq"] - w["gq"]) <= (0 if abs(w["gq"]) < 1e6 else 1), (key(g), g["gq"], w["gq"])
+        for side in ("tumor", "normal"):
+            gv, wv = g[side], w[side]
+            assert _close(gv[0], wv[0], 1e-6), (key(g), side, gv, wv)
+            assert tuple(gv[1:5]) == tuple(wv[1:5]), (key(g), side, gv, wv)
+            for x, y in zip(gv[5:], wv[5:]):
+                assert _close(x, y, 1e-9), (key(g), side, gv, wv)
+        assert g["flags"] == w["flags"]
+
+
+@pytest.mark.parametrize("tumor,normal", PAIRS, ids=["tough", "simplefp", "syn1fp", "complexvar"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fixture_pairs_match_oracle(gpu_ctx, tumor, normal, mode):
+    t = load_reads(fixture(tumor), TN_FILTERS)
+    n = load_reads(fixture(normal), TN_FILTERS)
+    loci = _loci(t)
+    params = dict(SUITE, apply_filters=mode) if mode else dict(apply_filters=0)
+    got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+    want = O.somatic_standard(t, n, loci, **params)
+    assert len(want) > 0 or mode == 2
+    assert_rows_match(got, want)
+
+
+def test_suite_positive_loci_are_called(gpu_ctx):
+    """SomaticStandardCallerSuite.scala:82-89 positives, through the GPU path."""
+    t = load_reads(fixture("tumor.chr20.tough.sam"), TN_FILTERS)
+    n = load_reads(fixture("normal.chr20.tough.sam"), TN_FILTERS)
+    got = somatic_standard_reads(gpu_ctx, t, n, _loci(t), **dict(SUITE, apply_filters=2))
+    called = {r["locus"] for r in got}
+    for locus in (42999694, 25031215, 44061033, 45175149, 755754, 1843813, 3555766, 3868620, 9896926, 14017900):
+        assert locus in called
+
+
+NORMAL8 = [mr("TCGATCGA", "8M", "8", 0)] * 3
+
+
+@pytest.mark.parametrize("tumor,normal,locus,expect", [
+    ([mr("TCGGTCGA", "8M", "3G4", 0)] * 3, NORMAL8, 2, None),
+    ([mr("TCGTCGA", "3M1D4M", "3^A4", 0)] * 3, NORMAL8, 2, ("GA", "G")),
+    ([mr("TCGAAAAGCT", "5M6D5M", "5^GCTTCG5", 0)] * 3, [mr("TCGAAGCTTCGAAGCT", "16M", "16", 0)] * 3, 4,
+     ("AGCTTCG", "A")),
+    ([mr("TCGAGTCGA", "4M1I4M", "8", 0)] * 3, NORMAL8, 3, ("A", "AG")),
+    ([mr("TCGAGGTCTCGA", "4M4I4M", "8", 0)] * 3, NORMAL8, 3, ("A", "AGGTC")),
+])
+def test_synthetic_indels(gpu_ctx, tumor, normal, locus, expect):  # SomaticStandardCallerSuite.scala:117-218
+    t, n = make_read_set(tumor), make_read_set(normal)
+    loci = (np.array([0], np.int32), np.array([locus], np.int64), np.array([locus + 1], np.int64),
+            np.array([0], np.int64))
+    got = somatic_standard_reads(gpu_ctx, t, n, loci, odds=2, apply_filters=0)
+    assert [(r["ref"], r["alt"]) for r in got] == ([] if expect is None else [expect])
+    assert_rows_match(got, O.somatic_standard(t, n, loci, odds=2, apply_filters=0))
+
+
+def test_synthetic_tumor_normal_window(gpu_ctx):
+    """Generator tumor (60x, somatic SNVs) / normal (30x) over a 300 kb contig: every locus."""
+    L = 300_000
+    tg = generate(L, 60.0, seed=20261015 + 3, somatic_rate=2e-4, tumor=True, read_seed=11)
+    ng = generate(L, 30.0, seed=20261015 + 3, somatic_rate=2e-4, tumor=False, read_seed=12)
+    t, n = tg.to_read_set(), ng.to_read_set()
+    loci = _loci(t)
+    for params in (dict(apply_filters=0), dict(apply_filters=1), dict(SUITE, apply_filters=1)):
+        got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+        want = O.somatic_standard(t, n, loci, **params)
+        assert_rows_match(got, want)
