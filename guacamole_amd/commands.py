@@ -94,16 +94,13 @@ def _loci_builder(args) -> LociSetBuilder:
     return LociSet.parse("all")
 
 
-def _write_genotypes(path: str, rows: List[dict]) -> None:
+def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None) -> None:
+    """Common.writeVariantsFromArguments (Common.scala:246-304): JSON for "" / .json, else VCF."""
+    from .output import write_json, write_vcf
     if path.lower().endswith(".vcf"):
-        from .output import write_vcf
-        write_vcf(path, rows)
+        write_vcf(path, genotypes, contig_lengths)
     else:
-        out = open(path, "w") if path else sys.stdout
-        for r in rows:
-            out.write(json.dumps(r) + "\n")
-        if path:
-            out.close()
+        write_json(path, genotypes)
 
 
 def germline_threshold_main(argv: Sequence[str]) -> int:
@@ -122,14 +119,64 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     ctx = native.Context(args.device)
     rows = germline_threshold_reads(ctx, rs, flatten_partitions(parts, rs.contig_index()), args.threshold,
                                     args.emit_ref, args.emit_no_call)
-    out = [dict(contig=c, start=l, sampleId=rs.sample_names[s] if s < len(rs.sample_names) else "default",
-                alleles=list(gt), referenceAllele=ref, alternateAllele=alt) for c, l, s, gt, ref, alt, fl in rows]
-    _write_genotypes(args.out, out)
+    from .output import germline_genotype
+    out = [germline_genotype(c, l, rs.sample_names[s] if s < len(rs.sample_names) else "default", gt, ref, alt)
+           for c, l, s, gt, ref, alt, fl in rows]
+    _write_genotypes(args.out, out, rs.contig_lengths_map)
     print("Called %d genotypes." % len(out), file=sys.stderr)
     return 0
 
 
-COMMANDS = {"germline-threshold": germline_threshold_main}
+def somatic_standard_main(argv: Sequence[str]) -> int:
+    """SomaticStandard.Caller.run (commands/SomaticStandardCaller.scala:66-160)."""
+    p = argparse.ArgumentParser(prog="somatic-standard",
+                                description="call somatic variants using independent callers on tumor and normal")
+    p.add_argument("--tumor-reads", required=True, help="Aligned reads: tumor")
+    p.add_argument("--normal-reads", required=True, help="Aligned reads: normal")
+    p.add_argument("--odds", type=int, default=20, help="Minimum log odds threshold for possible variant candidates")
+    p.add_argument("--min-mapq", type=int, default=1, help="Minimum read mapping quality for a read (Phred-scaled)")
+    p.add_argument("--filter-multi-allelic", action="store_true", help="Filter any pileups > 2 bases considered")
+    p.add_argument("--min-edge-distance", type=int, default=0, help="(accepted and ignored, as in the reference)")
+    p.add_argument("--min-likelihood", type=int, default=0)
+    p.add_argument("--min-vaf", type=int, default=0)
+    p.add_argument("--min-lod", type=int, default=0)
+    p.add_argument("--min-average-mapping-quality", type=int, default=0)
+    p.add_argument("--min-average-base-quality", type=int, default=0)
+    p.add_argument("--min-tumor-read-depth", type=int, default=0)
+    p.add_argument("--min-normal-read-depth", type=int, default=0)
+    p.add_argument("--max-tumor-read-depth", type=int, default=2 ** 31 - 1)
+    p.add_argument("--min-tumor-alternate-read-depth", type=int, default=0)
+    p.add_argument("--max-median-mismatches", type=int, default=2 ** 31 - 1)
+    _common_args(p)
+    args = p.parse_args(argv)
+    builder = _loci_builder(args)
+    f = InputFilters.make(overlaps_loci=builder, non_duplicate=True, passed_vendor_quality_checks=True,
+                          has_md_tag=True)
+    tumor, normal = load_reads(args.tumor_reads, f), load_reads(args.normal_reads, f)
+    if tumor.contig_lengths_map != normal.contig_lengths_map:
+        raise ValueError("Tumor and normal samples have different sequence dictionaries.")
+    loci = builder.result(normal.contig_lengths_map)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal)
+    ctx = native.Context(args.device)
+    rows = somatic_standard_reads(
+        ctx, tumor, normal, flatten_partitions(parts, tumor.contig_index()), odds=args.odds, min_mapq=args.min_mapq,
+        filter_multi_allelic=int(args.filter_multi_allelic), max_read_depth=args.max_tumor_read_depth,
+        min_tumor_read_depth=args.min_tumor_read_depth, max_tumor_read_depth=args.max_tumor_read_depth,
+        min_normal_read_depth=args.min_normal_read_depth,
+        min_tumor_alternate_read_depth=args.min_tumor_alternate_read_depth, min_lod=args.min_lod,
+        min_likelihood=args.min_likelihood, min_vaf=args.min_vaf,
+        min_average_mapping_quality=args.min_average_mapping_quality,
+        min_average_base_quality=args.min_average_base_quality, max_median_mismatches=args.max_median_mismatches,
+        apply_filters=1)
+    from .output import somatic_genotype
+    sample = tumor.sample_names[0] if tumor.sample_names else "default"
+    out = [somatic_genotype(r["contig"], r, sample) for r in rows]
+    _write_genotypes(args.out, out, tumor.contig_lengths_map)
+    print("Called %d somatic genotypes." % len(out), file=sys.stderr)
+    return 0
+
+
+COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main}
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

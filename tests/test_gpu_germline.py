@@ -100,3 +100,19 @@ def test_kat_pileups(gpu_ctx):
                 got = germline_threshold_reads(gpu_ctx, rs, loci, t, True, True)
                 want = O.germline_threshold(rs, loci, t, True, True)
                 assert got == want, (reads, expr, t)
+
+
+def test_cli_germline_vcf_and_somatic_json(tmp_path):
+    """End-to-end CLI (python -m guacamole_amd ...) writes the callers' outputs."""
+    import json
+    from guacamole_amd.commands import main
+    vcf = str(tmp_path / "g.vcf")
+    assert main(["germline-threshold", "--reads", fixture("chrM.sorted.bam"), "--loci", "chrM:0-16570",
+                 "--out", vcf]) == 0
+    lines = [l for l in open(vcf) if not l.startswith("#")]
+    assert len(lines) > 100 and all(l.split("\t")[0] == "chrM" for l in lines)
+    js = str(tmp_path / "s.json")
+    assert main(["somatic-standard", "--tumor-reads", fixture("tumor.chr20.tough.sam"), "--normal-reads",
+                 fixture("normal.chr20.tough.sam"), "--out", js, "--min-tumor-read-depth", "8"]) == 0
+    rows = [json.loads(l) for l in open(js)]
+    assert rows and all(r["alleles"] == ["Ref", "Alt"] and r["readDepth"] >= 8 for r in rows)
