@@ -142,23 +142,31 @@ __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_
     b4[k] = k < nmd ? evb[k] : 0u;
   }
   const int64_t cend = cb0 + 16 * (int64_t)nchunks;
-  auto run = [&](auto ld) {  // ld(q): chunk q, clamped to the read's last chunk (every load in bounds)
+  // ld(q): chunk q, clamped to the read's last chunk (every load in bounds).  Chunks are
+  // loaded kChunkGroup at a time, all issued before the first is used: one memory latency
+  // per group instead of one per few chunks.
+  constexpr int kChunkGroup = 8;
+  auto run = [&](auto ld) {
     const int32_t lo0 = (int32_t)(p0 - cb0);  // first valid byte of chunk 0
-    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
-    for (int q = 0; q < nchunks; ++q) {
-      const int32_t lo = q == 0 ? lo0 : 0;
-      const int64_t rem = p1 - (cb0 + 16 * (int64_t)q);
-      const int32_t hi = rem < 16 ? (int32_t)rem : 16;
-      const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);  // valid bytes [lo, hi)
-      const int32_t ib = ioff + 16 * q;
-      sink.bases4(ib, c0.x, vm & 15u, fl);
-      sink.bases4(ib + 4, c0.y, (vm >> 4) & 15u, fl);
-      sink.bases4(ib + 8, c0.z, (vm >> 8) & 15u, fl);
-      sink.bases4(ib + 12, c0.w, (vm >> 12) & 15u, fl);
-      c0 = c1;
-      c1 = c2;
-      c2 = c3;
-      c3 = ld(q + 4);
+    for (int g = 0; g < nchunks; g += kChunkGroup) {
+      uint4 c[kChunkGroup];
+#pragma unroll
+      for (int u = 0; u < kChunkGroup; ++u) c[u] = ld(g + u);
+#pragma unroll
+      for (int u = 0; u < kChunkGroup; ++u) {
+        const int q = g + u;
+        if (q < nchunks) {
+          const int32_t lo = q == 0 ? lo0 : 0;
+          const int64_t rem = p1 - (cb0 + 16 * (int64_t)q);
+          const int32_t hi = rem < 16 ? (int32_t)rem : 16;
+          const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);  // valid bytes [lo, hi)
+          const int32_t ib = ioff + 16 * q;
+          sink.bases4(ib, c[u].x, vm & 15u, fl);
+          sink.bases4(ib + 4, c[u].y, (vm >> 4) & 15u, fl);
+          sink.bases4(ib + 8, c[u].z, (vm >> 8) & 15u, fl);
+          sink.bases4(ib + 12, c[u].w, (vm >> 12) & 15u, fl);
+        }
+      }
     }
   };
   if (cb0 >= sv.b0 && cend <= sv.b1) {  // staged in LDS

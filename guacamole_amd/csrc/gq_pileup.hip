@@ -168,6 +168,8 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
     ++nout;                       \
   } while (0)
 
+#include "gq_germline_v2.h"
+
 // ABL (diagnostic builds only, selected by env GQ_ABLATE; results are wrong when != 0):
 //   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
 //   8 = skip the MD-event pass.
@@ -1056,6 +1058,29 @@ static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const g
                             Counters *ctr) {
   static const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
   static const int stg = getenv("GQ_STAGE") ? atoi(getenv("GQ_STAGE")) : 0;
+  static const int v2 = getenv("GQ_V2") ? atoi(getenv("GQ_V2")) : 0;
+  static const int abl2 = getenv("GQ_V2ABL") ? atoi(getenv("GQ_V2ABL")) : 0;
+  if (abl2) {  // diagnostic ablations of the locus-major kernel (results are wrong)
+#define GQ_V2A(A)                                                                                                  \
+  hipLaunchKernelGGL((germline_tile_v2<T / 256, A>), dim3((unsigned)tiles), dim3(T / 4), 0, c->stream,              \
+                     (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, \
+                     cplx_cap, ctr)
+    switch (abl2) {
+      case 1: GQ_V2A(1); break;
+      case 2: GQ_V2A(2); break;
+      case 4: GQ_V2A(4); break;
+      case 7: GQ_V2A(7); break;
+      default: GQ_V2A(0); break;
+    }
+#undef GQ_V2A
+    return;
+  }
+  if (v2 && !abl && !stg) {  // locus-major kernel (experimental: more VALU per element than v1)
+    hipLaunchKernelGGL((germline_tile_v2<T / 256>), dim3((unsigned)tiles), dim3(T / 4), 0, c->stream,
+                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
+                       cplx_cap, ctr);
+    return;
+  }
   if (stg) {
     hipLaunchKernelGGL((germline_tile<T, 0, kStageBytes>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
                        (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
