@@ -42,6 +42,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   long long err_pos;
   // per-tile run counters of germline_tile, spread over kSpread addresses (summed on the host)
   unsigned long long spread[3][64];
+  unsigned long long prof[8];  // diagnostic phase clocks (GQ_ABLATE=32 builds only)
 };
 constexpr int kSpread = 64;
 

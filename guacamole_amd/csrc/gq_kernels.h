@@ -114,39 +114,22 @@ struct StageView {
   int64_t b0, b1;
 };
 
-// Fast path of walk_read_lane for CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming
-// op: every element is a Match/Mismatch).  Two passes:
-//   1. bases: the read's bytes over [max(s,L0), min(e,L1)) stream in as 16-byte aligned
-//      chunks through a 4-deep rotating register prefetch; each dword goes to
-//      sink.bases4(i, word, valid4) with no branch (bytes outside the read carry
-//      valid = 0 and add nothing; i may fall in the sink's guard band);
-//   2. MD events inside the window: sink.event_i(i, read base, MD reference base), with
-//      the first four events and their read bases prefetched alongside the chunks.
+// Match/Mismatch elements of one read over the loci [a, b) whose sequenced bytes start at
+// global byte p0 (locus a): 16-byte aligned chunks, kChunkGroup loads issued before the
+// first is used (one memory latency per group); each dword goes to
+// sink.bases4(i, word, valid4) with no branch (bytes outside the run carry valid = 0 and
+// add nothing; i may fall in the sink's guard band).
 template <class Sink>
-__device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_t e, int32_t lead, int64_t seq_off,
-                                            int32_t nmd, int64_t md_off, int32_t L0, int32_t L1, uint8_t fl,
-                                            Sink &sink, const StageView &sv) {
-  const int32_t a = s > L0 ? s : L0;
-  const int32_t b = e < L1 ? e : L1;
-  const int64_t p0 = seq_off + lead + (a - s);
-  const int64_t p1 = seq_off + lead + (b - s);
+__device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t b, int64_t p0, int32_t L0, uint8_t fl,
+                                          Sink &sink, const StageView &sv) {
+  if (b <= a) return;
+  const int64_t p1 = p0 + (b - a);
   const int64_t cb0 = p0 & ~(int64_t)15;
   const int nchunks = (int)((p1 - cb0 + 15) >> 4);
   const int32_t ioff = (a - L0) - (int32_t)(p0 - cb0);  // tile index of byte cb0
-  const uint32_t *ev = R.md_ev + md_off;
-  const uint8_t *evb = R.ev_rb + md_off;
-  uint32_t e4[4], b4[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    e4[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
-    b4[k] = k < nmd ? evb[k] : 0u;
-  }
   const int64_t cend = cb0 + 16 * (int64_t)nchunks;
-  // ld(q): chunk q, clamped to the read's last chunk (every load in bounds).  Chunks are
-  // loaded kChunkGroup at a time, all issued before the first is used: one memory latency
-  // per group instead of one per few chunks.
-  constexpr int kChunkGroup = 8;
-  auto run = [&](auto ld) {
+  constexpr int kChunkGroup = 6;
+  auto run = [&](auto ld) {  // ld(q): chunk q, clamped to the last chunk (every load in bounds)
     const int32_t lo0 = (int32_t)(p0 - cb0);  // first valid byte of chunk 0
     for (int g = 0; g < nchunks; g += kChunkGroup) {
       uint4 c[kChunkGroup];
@@ -182,25 +165,43 @@ __device__ __forceinline__ void walk_simple(const DevReads &R, int32_t s, int32_
     const uint4 *base = reinterpret_cast<const uint4 *>(R.seq + cb0);
     run([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
   }
-  // MD events inside [a - s, b - s): mismatching reference bases on this read
-  for (int k = 0; k < nmd; ++k) {
-    const uint32_t v = k < 4 ? (k == 0 ? e4[0] : k == 1 ? e4[1] : k == 2 ? e4[2] : e4[3]) : ev[k];
-    const int32_t off = (int32_t)(v >> 8);
-    if (off < a - s) continue;
-    if (off >= b - s) break;
-    const uint32_t rb = k < 4 ? (k == 0 ? b4[0] : k == 1 ? b4[1] : k == 2 ? b4[2] : b4[3]) : evb[k];
-    sink.event_i(off + s - L0, (uint8_t)rb, (uint8_t)(v & 0xFFu), fl);
+}
+
+// MD events of a read (reference offsets relative to its start s) at loci [lo, hi):
+// sink.event_i(i, read base, MD reference base).  Events past the first four are loaded
+// four at a time (all issued before use).
+template <class Sink>
+__device__ __forceinline__ void events_run(const uint32_t *ev, const uint8_t *evb, uint4 e4, uint4 b4, int32_t nmd,
+                                           int32_t s, int32_t lo, int32_t hi, int32_t L0, uint8_t fl, Sink &sink) {
+  bool done = false;
+  for (int k0 = 0; k0 < nmd && !done; k0 += 4) {
+    uint32_t v4[4], r4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u;
+      const uint32_t ef = u == 0 ? e4.x : u == 1 ? e4.y : u == 2 ? e4.z : e4.w;
+      const uint32_t bf = u == 0 ? b4.x : u == 1 ? b4.y : u == 2 ? b4.z : b4.w;
+      v4[u] = k0 == 0 ? ef : (k < nmd ? ev[k] : 0xFFFFFFFFu);
+      r4[u] = k0 == 0 ? bf : (k < nmd ? evb[k] : 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (done || k0 + u >= nmd) continue;
+      const int32_t l = s + (int32_t)(v4[u] >> 8);
+      if (l < lo) continue;
+      if (l >= hi) {
+        done = true;
+        continue;
+      }
+      sink.event_i(l - L0, (uint8_t)r4[u], (uint8_t)(v4[u] & 0xFFu), fl);
+    }
   }
 }
 
-// Per-lane walk of one read's CIGAR over the loci [L0, L1): every lane owns one
-// read (64 reads in flight per wave).  `sink.elem(l, kind, base, mdb, ev, flags)`
-// receives each pileup element: locus, kind, the sequenced base for SNV / anchor
-// elements, the read's MD-derived reference base at l (MDTagUtils.getReference),
-// and whether an MD event (mismatch or deleted base) sits at l.
-//
-// Fast path: CIGAR = [S|H]* (M|=|X) [S|H]* (one reference-consuming op), bases
-// read as 16-byte aligned chunks.  General path: any CIGAR, byte loads.
+// Per-lane walk of one read over the loci [L0, L1): every lane owns one read (64 reads in
+// flight per wave).  Match/Mismatch runs go through bases_run + events_run; the other
+// elements (PileupElement.scala:68-135) go to sink.elem(l, kind, base, mdb, ev, flags)
+// with the read's MD-derived reference base mdb at l (MDTagUtils.getReference).
 template <class Sink>
 __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1, Sink &sink,
                                                const StageView &sv = StageView{nullptr, 0, 0}) {
@@ -212,78 +213,108 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
     sink.error(4 /*GQ_E_NO_MD*/, (int64_t)s);
     return;
   }
-  const int64_t cig_off = R.cigar_off[r];
-  const int32_t ncig = R.n_cigar[r];
-  const uint32_t *ev = R.md_ev + R.md_off[r];
+  const int64_t md_off = R.md_off[r];
   const int64_t seq_off = R.seq_off[r];
-  const int32_t slen = R.seq_len[r];
   const uint8_t fl = R.flags[r];
-
   const int32_t lead = R.lead[r];
-  if (lead >= 0) {
-    walk_simple(R, s, e, lead, seq_off, nmd, R.md_off[r], L0, L1, fl, sink, sv);
+  const uint32_t *ev = R.md_ev + md_off;
+  const uint8_t *evb = R.ev_rb + md_off;
+  uint4 e4, b4;  // first four MD events and the read bases under them, loaded with the metadata
+  e4.x = 0 < nmd ? ev[0] : 0xFFFFFFFFu;
+  e4.y = 1 < nmd ? ev[1] : 0xFFFFFFFFu;
+  e4.z = 2 < nmd ? ev[2] : 0xFFFFFFFFu;
+  e4.w = 3 < nmd ? ev[3] : 0xFFFFFFFFu;
+  b4.x = 0 < nmd ? evb[0] : 0u;
+  b4.y = 1 < nmd ? evb[1] : 0u;
+  b4.z = 2 < nmd ? evb[2] : 0u;
+  b4.w = 3 < nmd ? evb[3] : 0u;
+  const int32_t a = s > L0 ? s : L0;
+  const int32_t b = e < L1 ? e : L1;
+  if (lead >= 0) {  // [S|H]* (M|=|X) [S|H]*: every element is a Match/Mismatch
+    bases_run(R, a, b, seq_off + lead + (a - s), L0, fl, sink, sv);
+    events_run(ev, evb, e4, b4, nmd, s, a, b, L0, fl, sink);
     return;
   }
-
-  // general CIGAR
-  int32_t ref = s;
-  int32_t rpos = 0;
+  // general CIGAR: operator by operator
+  const int64_t cig_off = R.cigar_off[r];
+  const int32_t ncig = R.n_cigar[r];
+  const int32_t slen = R.seq_len[r];
+  auto md_at = [&](int32_t l) -> int {  // MD event at locus l: base, or -1
+    const int32_t off = l - s;
+    for (int k = 0; k < nmd; ++k) {
+      const uint32_t v = k < 4 ? (k == 0 ? e4.x : k == 1 ? e4.y : k == 2 ? e4.z : e4.w) : ev[k];
+      const int32_t o = (int32_t)(v >> 8);
+      if (o == off) return (int)(v & 0xFFu);
+      if (o > off) break;
+    }
+    return -1;
+  };
+  int32_t ref = s, rpos = 0;
   bool lead_ins = false;  // I before any reference-consuming op on a read at locus 0 (PileupElement.scala:102-103, 240-245)
   bool seen_ref = false;
-  int kev = 0;
+  uint32_t cc = ncig > 0 ? R.cigar[cig_off] : 0u;
   for (int k = 0; k < ncig; ++k) {
-    const uint32_t c = R.cigar[cig_off + k];
-    const int op = (int)(c & 15u);
-    const int32_t len = (int32_t)(c >> 4);
-    const int nextop = (k + 1 < ncig) ? (int)(R.cigar[cig_off + k + 1] & 15u) : -1;
+    const int op = (int)(cc & 15u);
+    const int32_t len = (int32_t)(cc >> 4);
+    const uint32_t cn = (k + 1 < ncig) ? R.cigar[cig_off + k + 1] : 0u;
+    const int nextop = (k + 1 < ncig) ? (int)(cn & 15u) : -1;
     if (op == OP_I && !seen_ref && s == 0) lead_ins = true;
     if (op == OP_P) sink.error(1 /*GQ_E_ASSERT*/, (int64_t)ref);
     if (consumes_ref(op)) {
       seen_ref = true;
-      const int32_t a = ref > L0 ? ref : L0;
-      const int32_t b = (ref + len) < L1 ? (ref + len) : L1;
-      while (kev < nmd && (int32_t)(ev[kev] >> 8) < a - s) ++kev;
-      for (int32_t l = a; l < b; ++l) {
-        const int32_t off = l - s;
-        int mdv = -1;
-        if (kev < nmd && (int32_t)(ev[kev] >> 8) == off) {
-          mdv = (int)(ev[kev] & 0xFFu);
-          ++kev;
-        }
+      const int32_t ra = ref, rb = ref + len;
+      const int32_t xa = ra > L0 ? ra : L0, xb = rb < L1 ? rb : L1;
+      if (xa < xb) {
         if (op == OP_M || op == OP_EQ || op == OP_X) {
-          const int32_t rp = rpos + (l - ref);
-          uint8_t base = 0;
-          if (rp < slen) base = R.seq[seq_off + rp];
-          else sink.error(1, (int64_t)l);
-          const bool fin = (l == ref + len - 1);
-          int kind = K_SNV;
-          if (lead_ins && l == 0) kind = K_INS;
-          else if (fin && (op == OP_M || op == OP_EQ) && nextop == OP_I) kind = K_INS;
-          else if (fin && nextop == OP_D) kind = K_DEL;
-          sink.elem(l, kind, base, mdv >= 0 ? (uint8_t)mdv : base, mdv >= 0, fl);
+          const bool first_ins = lead_ins && ra == 0;  // the element at locus 0 is an insertion
+          const bool ins_anchor = (op == OP_M || op == OP_EQ) && nextop == OP_I;
+          const bool del_anchor = nextop == OP_D;
+          int32_t lo = first_ins ? ra + 1 : ra;
+          int32_t hi = (ins_anchor || del_anchor) ? rb - 1 : rb;
+          lo = lo > xa ? lo : xa;
+          hi = hi < xb ? hi : xb;
+          // bases past the end of the sequence: assertion in the reference (Seq index)
+          const int32_t rend = ra + (slen - rpos);  // first locus without a sequenced base
+          if (xb > rend) sink.error(1 /*GQ_E_ASSERT*/, (int64_t)rend);
+          bases_run(R, lo, hi < rend ? hi : rend, seq_off + rpos + (lo - ra), L0, fl, sink, sv);
+          events_run(ev, evb, e4, b4, nmd, s, lo, hi, L0, fl, sink);
+          auto special = [&](int32_t l, int kind) {  // an anchor element at l
+            if (l < xa || l >= xb || rpos + (l - ra) >= slen) return;
+            const uint8_t base = R.seq[seq_off + rpos + (l - ra)];
+            const int v = md_at(l);
+            sink.elem(l, kind, base, v >= 0 ? (uint8_t)v : base, v >= 0, fl);
+          };
+          if (first_ins) special(ra, K_INS);
+          if ((ins_anchor || del_anchor) && !(first_ins && rb - 1 == ra)) special(rb - 1, ins_anchor ? K_INS : K_DEL);
         } else if (op == OP_D) {
-          if (mdv < 0) sink.error(3 /*GQ_E_MD*/, (int64_t)l);
-          sink.elem(l, K_MID, (uint8_t)0, mdv >= 0 ? (uint8_t)mdv : (uint8_t)'N', true, fl);
+          for (int32_t l = xa; l < xb; ++l) {  // mid-deletions
+            const int v = md_at(l);
+            if (v < 0) sink.error(3 /*GQ_E_MD*/, (int64_t)l);
+            sink.elem(l, K_MID, (uint8_t)0, v >= 0 ? (uint8_t)v : (uint8_t)'N', true, fl);
+          }
         } else {  // N: Clipped, MD-derived reference 'N'
-          sink.elem(l, K_CLIP, (uint8_t)0, (uint8_t)'N', false, fl);
+          sink.clip_run(xa - L0, xb - L0, fl);
         }
       }
       ref += len;
     }
     if (consumes_read(op)) rpos += len;
     if (ref >= L1) break;
+    cc = cn;
   }
 }
 
-// LDS histogram: seven u32 words per locus (SoA: word * S + guard + i, so consecutive loci
+
+// LDS histogram: six u32 words per locus (SoA: word * S + guard + i, so consecutive loci
 // sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has
 // code (b >> 1) & 7, distinct for A 0, C 1, T 2, G 3, N 7; a base whose code does not
 // map back to it is "other" (slot 4).  slot = word * 2 + half:
-//   W_AC = A | C << 16, W_TG = T | G << 16, W_OX = other | complex << 16, W_NN = N << 16,
-//   W_EAC / W_ETG = A C / T G counts of Match/Mismatch elements carrying an MD mismatch
-//   event, W_MASK = OR of MD-derived standard reference bases of event / complex elements.
+//   W_AC = A | C << 16, W_TG = T | G << 16, W_OX = other | complex << 16,
+//   W_NN = N << 16 | mask (bits 0-3: OR of the MD-derived standard reference bases of
+//   event / complex elements; W_MASK aliases W_NN, read it with & 0xF),
+//   W_EAC / W_ETG = A C / T G counts of Match/Mismatch elements carrying an MD mismatch event.
 // Tiles whose read window could exceed 65535 reads never use this path (wide tiles).
-enum : int { W_AC = 0, W_TG, W_OX, W_NN, W_EAC, W_ETG, W_MASK, W_N };
+enum : int { W_AC = 0, W_TG, W_OX, W_NN, W_EAC, W_ETG, W_N, W_MASK = W_NN };
 // LDS arrays carry a 16-entry guard band on each side (stride T + 32, index 16 + i), so
 // the branch-free base pass may address i in [-16, T + 16) with a zero increment.
 constexpr int kGuard = 16;
@@ -338,6 +369,10 @@ struct GermSink {
   }
   __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
     elem_i(l - L0, kind, base, mdb, ev, fl);
+  }
+  // Clipped elements (CIGAR N) at tile indices [i0, i1): complex, MD-derived reference 'N'
+  __device__ __forceinline__ void clip_run(int i0, int i1, uint8_t) {
+    for (int i = i0; i < i1; ++i) atomicAdd(at(W_OX, i), 1u << 16);
   }
   __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
 };

@@ -174,20 +174,22 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 //   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
 //   8 = skip the MD-event pass.
 template <int T, int ABL = 0, int STAGE = 0>
-__global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : T <= 768 ? 8 : T <= 1024 ? 6 : 3))) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
                                                         int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
                                                         unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
                                                         unsigned long long cplx_cap, Counters *ctr) {
   constexpr int S = T + 2 * kGuard;
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ __attribute__((aligned(16))) uint4 stage[STAGE ? STAGE / 16 : 1];
+  const uint64_t pt0 = (ABL & 32) ? __builtin_readcyclecounter() : 0;
+  uint64_t pt1 = 0, pt2 = 0, pt3 = 0;
   const Tile tl = tiles[blockIdx.x];
   const int32_t L0 = tl.L0, L1 = tl.L1;
   // a window of >= 65535 reads could overflow the 16-bit counters: queue every locus of
   // the tile for the exact (32-bit) kernel instead
   const bool wide = (tl.re - tl.rb) >= 65535;
   if (!wide) {
-    GermSink<T, ABL> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+    GermSink<T, (ABL & 31)> sink{cnt, L0, &ctr->err, &ctr->err_pos};
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     // Reads are walked in batches of up to blockDim.x (one per lane).  A batch's reads
     // sit in one contiguous byte range of the sequence pool (reads are stored in
@@ -214,12 +216,15 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
       if (STAGE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       const StageView sv{stage, B0, B0 + n1k * 1024};
+      if ((ABL & 32) && r0 == tl.rb) pt1 = __builtin_readcyclecounter();
       if (!(ABL & 1) && (int64_t)threadIdx.x < nb) walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink, sv);
+      if (ABL & 32) pt2 = __builtin_readcyclecounter();
       __syncthreads();  // counters complete / stage free for the next batch
       if (nb <= 0) break;
     }
   }
   __syncthreads();
+  if (ABL & 32) pt3 = __builtin_readcyclecounter();
   if (ABL & 2) {
     if (threadIdx.x == 0) atomicAdd(&ctr->visited, (unsigned long long)cnt[kGuard + (blockIdx.x & 63)]);
     return;
@@ -244,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
       const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
       if (depth > 0) {
         ++visited;
-        uint32_t mask = cnt[W_MASK * S + kGuard + i];
+        uint32_t mask = cnt[W_MASK * S + kGuard + i] & 0xFu;
         const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
         const uint32_t ev[4] = {eac & 0xFFFFu, eac >> 16, etg & 0xFFFFu, etg >> 16};
 #pragma unroll
@@ -367,6 +372,14 @@ __global__ __launch_bounds__(kBlock) void germline_tile(const Tile *__restrict__
     if (red[0]) atomicAdd(&ctr->spread[0][sl], (unsigned long long)red[0]);
     if (red[1]) atomicAdd(&ctr->spread[1][sl], (unsigned long long)red[1]);
     if (red[2]) atomicAdd(&ctr->spread[2][sl], (unsigned long long)red[2]);
+  }
+  if ((ABL & 32) && (threadIdx.x & 63) == 0) {  // per-wave phase clocks
+    const uint64_t pt4 = __builtin_readcyclecounter();
+    atomicAdd(&ctr->prof[0], (unsigned long long)(pt1 - pt0));  // tile load + LDS zero + barrier
+    atomicAdd(&ctr->prof[1], (unsigned long long)(pt2 - pt1));  // this wave's read walk
+    atomicAdd(&ctr->prof[2], (unsigned long long)(pt3 - pt2));  // waiting for the other waves
+    atomicAdd(&ctr->prof[3], (unsigned long long)(pt4 - pt3));  // decision + output
+    atomicAdd(&ctr->prof[4], 1ull);
   }
 }
 
@@ -696,6 +709,9 @@ struct CountSink {
     }
     if (b) atomicOr(&cnt[K2_MASK * T + i], b);
   }
+  __device__ __forceinline__ void clip_run(int i0, int i1, uint8_t fl) {
+    for (int i = i0; i < i1; ++i) elem_i(i, K_CLIP, 0, (uint8_t)'N', false, fl);
+  }
   __device__ __forceinline__ void error(int code, int64_t where) { raise_error(err, (int64_t *)err_pos, code, where); }
 };
 
@@ -845,7 +861,7 @@ gq_status gq_get_timings(const gq_ctx *c, gq_timings *out) {
 gq_status gq_set_tile(gq_ctx *c, int32_t t) {
   if (!c) return set_err(GQ_E_ARG, "null ctx");
   if (t == 0) t = kGermT;
-  if (t != 512 && t != 1024 && t != 2048) return set_err(GQ_E_ARG, "tile must be 512, 1024 or 2048");
+  if (t != 512 && t != 768 && t != 1024 && t != 2048) return set_err(GQ_E_ARG, "tile must be 512, 768, 1024 or 2048");
   c->germ_tile = t;
   return GQ_OK;
 }
@@ -1081,6 +1097,12 @@ static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const g
                        cplx_cap, ctr);
     return;
   }
+  if (stg == 2) {  // smaller stage (for T = 512 / 768 tiles)
+    hipLaunchKernelGGL((germline_tile<T, 0, 24 * 1024>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
+                       cplx_cap, ctr);
+    return;
+  }
   if (stg) {
     hipLaunchKernelGGL((germline_tile<T, 0, kStageBytes>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
                        (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
@@ -1098,6 +1120,7 @@ static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const g
     case 8: GQ_LAUNCH(8); break;
     case 12: GQ_LAUNCH(12); break;
     case 14: GQ_LAUNCH(14); break;
+    case 32: GQ_LAUNCH(32); break;
     default: GQ_LAUNCH(0); break;
   }
 #undef GQ_LAUNCH
@@ -1137,6 +1160,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
     if (attempt == 0) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     switch (T) {
       case 512: launch_germline<512>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
+      case 768: launch_germline<768>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
       case 2048: launch_germline<2048>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
       default: launch_germline<1024>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
     }
@@ -1169,6 +1193,10 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
       return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
     }
   }
+  if (getenv("GQ_PROF") && hc.prof[4])
+    fprintf(stderr, "gq prof (cycles/wave): setup %.0f walk %.0f wait %.0f decide %.0f  (waves %llu)\n",
+            (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4], (double)hc.prof[2] / hc.prof[4],
+            (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
   for (int k = 0; k < kSpread; ++k) {
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];

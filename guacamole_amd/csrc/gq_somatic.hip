@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ 
     const uint32_t depth = cA + cC + cT + cG + cN + cx;
     if (depth == 0) continue;
     tflag |= 1u << k;
-    uint32_t mask = cnt[W_MASK * S + kGuard + i];
+    uint32_t mask = cnt[W_MASK * S + kGuard + i] & 0xFu;
     const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
     if (cA > (eac & 0xFFFFu)) mask |= 1u;
     if (cC > (eac >> 16)) mask |= 2u;
@@ -121,10 +121,11 @@ __global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ 
     if (i < nloci) {
       uint32_t dn = 0;
 #pragma unroll
-      for (int w = W_AC; w <= W_NN; ++w) {
+      for (int w = W_AC; w < W_NN; ++w) {
         const uint32_t v = cnt[w * S + kGuard + i];
         dn += (v & 0xFFFFu) + (v >> 16);
       }
+      dn += cnt[W_NN * S + kGuard + i] >> 16;  // low bits of W_NN hold the reference mask
       if (((tflag >> k) & 1u) || dn > 0) ++visited;
       q = ((tflag >> (8 + k)) & 1u) && dn > 0;
     }

@@ -112,9 +112,11 @@ def lib():
     """Load the HIP library (raises if it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError("libgqpileup.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
-        L = C.CDLL(LIB_PATH)
+        # GQ_LIB: an alternative in-tree build of the same library (kernel A/B experiments)
+        path = os.environ.get("GQ_LIB", LIB_PATH)
+        if not os.path.exists(path):
+            raise RuntimeError("libgqpileup.so not built (%s); run __graft_entry__.build()" % path)
+        L = C.CDLL(path)
         L.gq_version.restype = C.c_char_p
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device",
