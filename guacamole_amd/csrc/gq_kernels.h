@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace gq {
 
 enum : int { OP_M = 0, OP_I = 1, OP_D = 2, OP_N = 3, OP_S = 4, OP_H = 5, OP_P = 6, OP_EQ = 7, OP_X = 8 };
@@ -43,6 +45,7 @@ struct DevReads {
   // derived at upload (read_shape):
   const int16_t *lead;   // leading soft clip of a [S|H]*(M|=|X)[S|H]* CIGAR, -1 otherwise
   const uint8_t *ev_rb;  // per MD event: the read's sequenced base at that position (0 for deletions)
+  const uint8_t *clean;  // 1 if every sequenced byte of the read is one of A C G T N
 };
 
 // One locus tile: contiguous loci [L0, L1) of one contig, plus the index range
@@ -121,7 +124,7 @@ struct StageView {
 // add nothing; i may fall in the sink's guard band).
 template <class Sink>
 __device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t b, int64_t p0, int32_t L0, uint8_t fl,
-                                          Sink &sink, const StageView &sv) {
+                                          Sink &sink, const StageView &sv, bool clean = false) {
   if (b <= a) return;
   const int64_t p1 = p0 + (b - a);
   const int64_t cb0 = p0 & ~(int64_t)15;
@@ -129,7 +132,8 @@ __device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t 
   const int32_t ioff = (a - L0) - (int32_t)(p0 - cb0);  // tile index of byte cb0
   const int64_t cend = cb0 + 16 * (int64_t)nchunks;
   constexpr int kChunkGroup = 6;
-  auto run = [&](auto ld) {  // ld(q): chunk q, clamped to the last chunk (every load in bounds)
+  auto run = [&](auto ld, auto clean_tag) {  // ld(q): chunk q, clamped to the last chunk (every load in bounds)
+    constexpr bool CLEAN = decltype(clean_tag)::value;
     const int32_t lo0 = (int32_t)(p0 - cb0);  // first valid byte of chunk 0
     for (int g = 0; g < nchunks; g += kChunkGroup) {
       uint4 c[kChunkGroup];
@@ -144,17 +148,29 @@ __device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t 
           const int32_t hi = rem < 16 ? (int32_t)rem : 16;
           const uint32_t vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);  // valid bytes [lo, hi)
           const int32_t ib = ioff + 16 * q;
-          sink.bases4(ib, c[u].x, vm & 15u, fl);
-          sink.bases4(ib + 4, c[u].y, (vm >> 4) & 15u, fl);
-          sink.bases4(ib + 8, c[u].z, (vm >> 8) & 15u, fl);
-          sink.bases4(ib + 12, c[u].w, (vm >> 12) & 15u, fl);
+          if (CLEAN) {  // A C G T N only (checked once per read at upload): no category checks
+            sink.bases4_clean(ib, c[u].x, vm & 15u, fl);
+            sink.bases4_clean(ib + 4, c[u].y, (vm >> 4) & 15u, fl);
+            sink.bases4_clean(ib + 8, c[u].z, (vm >> 8) & 15u, fl);
+            sink.bases4_clean(ib + 12, c[u].w, (vm >> 12) & 15u, fl);
+          } else {
+            sink.bases4(ib, c[u].x, vm & 15u, fl);
+            sink.bases4(ib + 4, c[u].y, (vm >> 4) & 15u, fl);
+            sink.bases4(ib + 8, c[u].z, (vm >> 8) & 15u, fl);
+            sink.bases4(ib + 12, c[u].w, (vm >> 12) & 15u, fl);
+          }
         }
       }
     }
   };
+  // the clean / checked choice is per read (a wave pays for both only where its lanes' reads differ)
+  auto run2 = [&](auto ld) {
+    if (clean) run(ld, std::true_type{});
+    else run(ld, std::false_type{});
+  };
   if (cb0 >= sv.b0 && cend <= sv.b1) {  // staged in LDS
     const uint4 *base = sv.lds + ((cb0 - sv.b0) >> 4);
-    run([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
+    run2([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
   } else if (cend > R.seq_cap) {  // last read of an unpadded pool: byte loads
     for (int64_t p = p0; p < p1; ++p) {
       const int32_t i = ioff + (int32_t)(p - cb0);
@@ -163,7 +179,7 @@ __device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t 
     }
   } else {
     const uint4 *base = reinterpret_cast<const uint4 *>(R.seq + cb0);
-    run([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
+    run2([&](int q) -> uint4 { return base[q < nchunks ? q : nchunks - 1]; });
   }
 }
 
@@ -217,6 +233,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   const int64_t seq_off = R.seq_off[r];
   const uint8_t fl = R.flags[r];
   const int32_t lead = R.lead[r];
+  const bool clean = R.clean[r] != 0;
   const uint32_t *ev = R.md_ev + md_off;
   const uint8_t *evb = R.ev_rb + md_off;
   uint4 e4, b4;  // first four MD events and the read bases under them, loaded with the metadata
@@ -231,7 +248,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   const int32_t a = s > L0 ? s : L0;
   const int32_t b = e < L1 ? e : L1;
   if (lead >= 0) {  // [S|H]* (M|=|X) [S|H]*: every element is a Match/Mismatch
-    bases_run(R, a, b, seq_off + lead + (a - s), L0, fl, sink, sv);
+    bases_run(R, a, b, seq_off + lead + (a - s), L0, fl, sink, sv, clean);
     events_run(ev, evb, e4, b4, nmd, s, a, b, L0, fl, sink);
     return;
   }
@@ -276,7 +293,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
           // bases past the end of the sequence: assertion in the reference (Seq index)
           const int32_t rend = ra + (slen - rpos);  // first locus without a sequenced base
           if (xb > rend) sink.error(1 /*GQ_E_ASSERT*/, (int64_t)rend);
-          bases_run(R, lo, hi < rend ? hi : rend, seq_off + rpos + (lo - ra), L0, fl, sink, sv);
+          bases_run(R, lo, hi < rend ? hi : rend, seq_off + rpos + (lo - ra), L0, fl, sink, sv, clean);
           events_run(ev, evb, e4, b4, nmd, s, lo, hi, L0, fl, sink);
           auto special = [&](int32_t l, int kind) {  // an anchor element at l
             if (l < xa || l >= xb || rpos + (l - ra) >= slen) return;
@@ -304,6 +321,124 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   }
 }
 
+
+// Chunk-major walk of one batch of up to blockDim.x start-sorted reads (the default).
+// Lane-per-read loads of 16-byte chunks hit a different cache line per lane; here the
+// batch's sequence bytes, which are one contiguous range of the pool, are read as
+// consecutive 16-byte chunks by consecutive threads (1 KiB per wave-instruction).
+//   A. thread t fills row t of an LDS table for read r0 + t: the pool byte range [lo, hi)
+//      of its Match/Mismatch elements on the tile, and base = tile index - byte offset;
+//   B. every thread takes chunks k = t, t + blockDim.x, ...; each chunk's bytes are
+//      counted for the reads whose ranges intersect it (found from a guess + short scan);
+//   C. thread t adds its own read's MD events, or walks the read itself if it is not a
+//      simple CIGAR in pool order.
+// Returns false (nothing counted) if the batch's reads are not laid out in pool order; the
+// caller then walks it lane-per-read.
+struct ChunkRows {
+  int32_t *lo, *hi, *base;
+  uint8_t *info;  // bit0 reverse strand, bit1 clean bases
+};
+
+template <class Sink>
+__device__ __forceinline__ bool walk_batch_chunked(const DevReads &R, int64_t r0, int nb, int32_t L0, int32_t L1,
+                                                   Sink &sink, ChunkRows rows, int *flag) {
+  const int t = threadIdx.x;
+  const int64_t last = r0 + nb - 1;
+  const int64_t B0 = R.seq_off[r0] & ~(int64_t)15;
+  const int64_t Bend = R.seq_off[last] + R.seq_len[last];
+  const int n16 = (int)((Bend - B0 + 15) >> 4);
+  if (t == 0) *flag = 0;
+  __syncthreads();
+  // ---- A: table rows
+  int32_t s = 0, e = 0, a = 0, b = 0, nmd = 0;
+  int64_t md_off = 0;
+  uint8_t fl = 0;
+  bool mine = false;  // this thread's read needs phase C
+  bool simple_in = false;
+  uint4 e4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), b4 = make_uint4(0u, 0u, 0u, 0u);
+  if (t < nb) {
+    const int64_t r = r0 + t;
+    s = R.start[r];
+    e = R.end[r];
+    const int64_t so = R.seq_off[r];
+    const int32_t sl = R.seq_len[r];
+    const int32_t lead = R.lead[r];
+    nmd = R.n_md[r];
+    md_off = R.md_off[r];
+    fl = R.flags[r];
+    const bool clean = R.clean[r] != 0;
+    bool ordered = so >= B0 && so + sl <= Bend;
+    if (t > 0) ordered = ordered && so >= R.seq_off[r - 1] + R.seq_len[r - 1];
+    if (!ordered) atomicOr(flag, 1);
+    a = s > L0 ? s : L0;
+    b = e < L1 ? e : L1;
+    const bool overlaps = a < b;
+    simple_in = overlaps && lead >= 0 && nmd >= 0;
+    mine = overlaps;
+    int32_t lo = (int32_t)(so - B0), hi = lo, base = 0;
+    if (simple_in) {
+      lo = (int32_t)(so + lead + (a - s) - B0);
+      hi = lo + (b - a);
+      base = (a - L0) - lo;
+      const uint32_t *ev = R.md_ev + md_off;
+      const uint8_t *evb = R.ev_rb + md_off;
+      e4.x = 0 < nmd ? ev[0] : 0xFFFFFFFFu;
+      e4.y = 1 < nmd ? ev[1] : 0xFFFFFFFFu;
+      e4.z = 2 < nmd ? ev[2] : 0xFFFFFFFFu;
+      e4.w = 3 < nmd ? ev[3] : 0xFFFFFFFFu;
+      b4.x = 0 < nmd ? evb[0] : 0u;
+      b4.y = 1 < nmd ? evb[1] : 0u;
+      b4.z = 2 < nmd ? evb[2] : 0u;
+      b4.w = 3 < nmd ? evb[3] : 0u;
+    }
+    rows.lo[t] = lo;
+    rows.hi[t] = hi;
+    rows.base[t] = base;
+    rows.info[t] = (uint8_t)((fl & 1) | (clean ? 2 : 0));
+  }
+  __syncthreads();
+  if (*flag) return false;
+  // ---- B: chunks
+  const int avg = max(16, (n16 * 16) / nb);
+  int g = 0;
+  for (int k = t; k < n16; k += blockDim.x) {
+    const int cb = 16 * k;
+    const uint4 c = *reinterpret_cast<const uint4 *>(R.seq + B0 + cb);
+    int j = cb / avg;
+    j = j < g ? g : (j > nb - 1 ? nb - 1 : j);
+    while (j > 0 && rows.hi[j - 1] > cb) --j;
+    while (j < nb && rows.hi[j] <= cb) ++j;
+    g = j;
+    for (; j < nb; ++j) {
+      const int32_t lo = rows.lo[j];
+      if (lo >= cb + 16) break;
+      const int32_t hi = rows.hi[j];
+      const int32_t f = lo > cb ? lo - cb : 0, u = hi < cb + 16 ? hi - cb : 16;
+      if (f >= u) continue;
+      const uint32_t vm = ((u >= 16 ? 0x10000u : (1u << u)) - 1u) & ~((1u << f) - 1u);
+      const int32_t i0 = cb + rows.base[j];
+      const uint8_t inf = rows.info[j];
+      const uint8_t rfl = inf & 1;
+      if (inf & 2) {
+        sink.bases4_clean(i0, c.x, vm & 15u, rfl);
+        sink.bases4_clean(i0 + 4, c.y, (vm >> 4) & 15u, rfl);
+        sink.bases4_clean(i0 + 8, c.z, (vm >> 8) & 15u, rfl);
+        sink.bases4_clean(i0 + 12, c.w, (vm >> 12) & 15u, rfl);
+      } else {
+        sink.bases4(i0, c.x, vm & 15u, rfl);
+        sink.bases4(i0 + 4, c.y, (vm >> 4) & 15u, rfl);
+        sink.bases4(i0 + 8, c.z, (vm >> 8) & 15u, rfl);
+        sink.bases4(i0 + 12, c.w, (vm >> 12) & 15u, rfl);
+      }
+    }
+  }
+  // ---- C: MD events of simple reads; other reads walked by their own thread
+  if (mine) {
+    if (simple_in) events_run(R.md_ev + md_off, R.ev_rb + md_off, e4, b4, nmd, s, a, b, L0, fl, sink);
+    else walk_read_lane(R, r0 + t, L0, L1, sink);
+  }
+  return true;
+}
 
 // LDS histogram: six u32 words per locus (SoA: word * S + guard + i, so consecutive loci
 // sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has
@@ -344,6 +479,22 @@ struct GermSink {
         acc ^= slot;
       } else {
         atomicAdd(at((int)(slot >> 1), i + j), ((valid4 >> j) & 1u) << ((slot & 1u) << 4));
+      }
+    }
+  }
+  // four Match/Mismatch elements whose bytes are all A C G T N (checked once per read at
+  // upload): counter word (b >> 2) & 3 (A C -> W_AC, T G -> W_TG, N -> W_NN), half (b >> 1) & 1;
+  // the increment is valid << (16 * half)
+  __device__ __forceinline__ void bases4_clean(int i, uint32_t w, uint32_t valid4, uint8_t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t ws = (w >> (8 * j + 2)) & 3u, hb = (w >> (8 * j + 1)) & 1u;
+      const uint32_t inc = ((valid4 >> j) & 1u) << (hb << 4);
+      if (ABL & 4) {
+        acc += inc;
+        acc ^= ws;
+      } else {
+        atomicAdd(cnt + ws * S + kGuard + i + j, inc);
       }
     }
   }

@@ -101,9 +101,19 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
 
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
 // [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
-__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
+__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb,
+                           uint8_t *__restrict__ clean) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
+  {  // every sequenced byte one of A C G T N (the germline fast path's precondition)
+    const uint8_t *q = R.seq + R.seq_off[r];
+    bool ok = true;
+    for (int32_t k = 0; k < R.seq_len[r]; ++k) {
+      const uint8_t b = q[k];
+      ok = ok && (b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'N');
+    }
+    clean[r] = ok ? 1 : 0;
+  }
   const int64_t off = R.cigar_off[r];
   const int32_t n = R.n_cigar[r];
   int32_t ld = 0, mlen = 0;
@@ -173,14 +183,18 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ABL (diagnostic builds only, selected by env GQ_ABLATE; results are wrong when != 0):
 //   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
 //   8 = skip the MD-event pass.
-template <int T, int ABL = 0, int STAGE = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : T <= 768 ? 8 : T <= 1024 ? 6 : 3))) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
+template <int T, int ABL = 0, int STAGE = 0, int CH = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : T <= 768 ? 8 : T <= 1024 ? (CH ? 5 : 6) : 3))) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
                                                         int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
                                                         unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
                                                         unsigned long long cplx_cap, Counters *ctr) {
   constexpr int S = T + 2 * kGuard;
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ __attribute__((aligned(16))) uint4 stage[STAGE ? STAGE / 16 : 1];
+  constexpr int NR = (CH && !STAGE) ? kBlock : 1;  // chunk-major walk: one table row per read of a batch
+  __shared__ int32_t ch_lo[NR], ch_hi[NR], ch_base[NR];
+  __shared__ uint8_t ch_info[NR];
+  __shared__ int ch_flag;
   const uint64_t pt0 = (ABL & 32) ? __builtin_readcyclecounter() : 0;
   uint64_t pt1 = 0, pt2 = 0, pt3 = 0;
   const Tile tl = tiles[blockIdx.x];
@@ -217,7 +231,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 
       __syncthreads();
       const StageView sv{stage, B0, B0 + n1k * 1024};
       if ((ABL & 32) && r0 == tl.rb) pt1 = __builtin_readcyclecounter();
-      if (!(ABL & 1) && (int64_t)threadIdx.x < nb) walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink, sv);
+      if (CH && !STAGE && nb > 0 && !(ABL & 1)) {
+        if (!walk_batch_chunked(R, r0, (int)nb, L0, L1, sink, ChunkRows{ch_lo, ch_hi, ch_base, ch_info}, &ch_flag) &&
+            (int64_t)threadIdx.x < nb)
+          walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink);  // reads not in pool order: lane per read
+      } else if (!(ABL & 1) && (int64_t)threadIdx.x < nb) {
+        walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink, sv);
+      }
       if (ABL & 32) pt2 = __builtin_readcyclecounter();
       __syncthreads();  // counters complete / stage free for the next batch
       if (nb <= 0) break;
@@ -680,6 +700,9 @@ struct CountSink {
   __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
     elem_i(l - L0, kind, base, mdb, ev, fl);
   }
+  __device__ __forceinline__ void bases4_clean(int i, uint32_t w, uint32_t valid4, uint8_t fl) {
+    bases4(i, w, valid4, fl);
+  }
   __device__ __forceinline__ void bases4(int i, uint32_t w, uint32_t valid4, uint8_t fl) {
     for (int j = 0; j < 4; ++j)
       if (((valid4 >> j) & 1u) && i + j >= 0 && i + j < T) elem_i(i + j, K_SNV, (uint8_t)(w >> (8 * j)), 0, false, fl);
@@ -874,16 +897,20 @@ static gq_status validate_reads(const gq_reads *h) {
 }
 
 static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
-  void *p = nullptr, *q = nullptr;
+  void *p = nullptr, *q = nullptr, *cl = nullptr;
   HIP_TRY(hipMalloc(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
   d->owned.push_back(p);
+  HIP_TRY(hipMalloc(&cl, (size_t)std::max<int64_t>(d->d.n_reads, 1)));
+  d->owned.push_back(cl);
+  d->d.clean = (const uint8_t *)cl;
   HIP_TRY(hipMalloc(&q, (size_t)std::max<int64_t>(md_len, 16)));
   d->owned.push_back(q);
   d->d.lead = (const int16_t *)p;
   d->d.ev_rb = (const uint8_t *)q;
   if (d->d.n_reads > 0) {
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q);
+    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q,
+                       (uint8_t *)cl);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1105,6 +1132,13 @@ static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const g
   }
   if (stg) {
     hipLaunchKernelGGL((germline_tile<T, 0, kStageBytes>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
+                       cplx_cap, ctr);
+    return;
+  }
+  static const int chunked = getenv("GQ_CHUNKED") ? atoi(getenv("GQ_CHUNKED")) : 0;
+  if (chunked) {  // chunk-major walk (experimental: coalesced loads, more VALU per element)
+    hipLaunchKernelGGL((germline_tile<T, 0, 0, 1>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
                        (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
                        cplx_cap, ctr);
     return;
