@@ -1,0 +1,585 @@
+// gq_germline_cols.h — germline_cols<T>: the germline-threshold pileup kernel.
+//
+// One workgroup per tile of T loci (XCD-aware tile order).  The tile's reads are
+// start-sorted and their sequence bytes are one contiguous range of the pool, so the
+// workgroup copies that range into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction, fully coalesced) and then counts it COLUMN-MAJOR: lane j owns the
+// four loci [4j, 4j + 4) of the tile and walks the reads covering them, reading one
+// dword (4 bases) per read from LDS.  Counts live in registers as SWAR nibble fields
+// (A|C and T|G per byte, one byte per locus) folded into byte counters every 15 reads,
+// so the hot loop has no atomics and no histogram re-read:
+//
+//     w    = alignbyte(stage[a+1], stage[a], a)       4 bases at loci 4j..4j+3
+//     sel  = w & 0x07070707                           A 1, C 3, T 4, N 6, G 7
+//     n_ac += perm(0, 0x10000100, sel)                A -> 0x01, C -> 0x10 per byte
+//     n_tg += perm(0x10000001, 0, sel)                T -> 0x01, G -> 0x10 per byte
+//
+// N = (reads fully covering the column) - A - C - T - G.  Everything the column pass does
+// not cover goes through the LDS histogram (GermSink atomics) in a lane-per-read pass:
+//   * the <= 3 + 3 loci of a read that only partially cover a column (its two ends),
+//   * MD mismatch events (for the MD-derived reference base, Pileup.scala:157-165),
+//   * reads that are not a single (M|=|X) block with A/C/G/T/N bases, or whose bytes are
+//     not staged: the general per-read walker (walk_read_lane, PileupElement.scala:68-248).
+// Tiles whose reads do not fit the stage are processed in several read chunks.  Then one
+// thread per locus makes the GermlineThreshold decision (GermlineThresholdCaller.scala:90-179)
+// for single-base pileups and queues the rest for germline_complex.
+#pragma once
+
+#include "gq_kernels.h"
+
+// (included inside gq_pileup.hip's anonymous namespace, after `using namespace gq`)
+
+// tile index of block b: blocks b, b + 8, b + 16, ... run on one XCD (round-robin
+// dispatch), so give each XCD a contiguous run of tiles (reads straddling neighbouring
+// tiles are then re-read from that XCD's L2).  A bijection on [0, n).
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t n) {
+  const int64_t q = n >> 3, rem = n & 7;
+  const int64_t x = b & 7, j = b >> 3;
+  return x * q + (x < rem ? x : rem) + j;
+}
+
+// GermlineThresholdCaller.scala:100-177 for the loci of a tile whose histogram is complete
+// in `cnt` (GermSink layout).  One thread per locus; loci needing exact alleles (indels,
+// clips, other bases, several samples, ambiguous reference) are queued as ComplexItems.
+// Output slots of germline_decide.  reserve(which, n) gives this lane's first slot for n
+// records (which = 0) or complex items (1), wave-aggregated, relative to partition `part`
+// of capacity cap[which]; slots >= cap are dropped (the host retries with more room).
+struct LdsOut {  // germline_cols: one partition per workgroup, counters in LDS
+  unsigned *lds;  // [2]
+  unsigned long long base[2], cap[2];
+  __device__ __forceinline__ unsigned long long reserve(int which, unsigned n) {
+    return wave_reserve_lds(lds + which, n);
+  }
+};
+struct GlobalOut {  // germline_walk: a partition per wave, counters in device memory
+  Counters *ctr;
+  int part;
+  unsigned long long base[2], cap[2];
+  __device__ __forceinline__ unsigned long long reserve(int which, unsigned n) {
+    return wave_reserve(&ctr->part[which][part], n);
+  }
+};
+
+template <int T, class Out>
+__device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile &tl, int64_t tile_id, bool wide,
+                                                const DevReads &R, int threshold, int emit_ref, int emit_no_call,
+                                                CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx,
+                                                Out &out, unsigned &visited, unsigned &amb, unsigned &ties) {
+  constexpr int S = T + 2 * kGuard;
+  const int32_t L0 = tl.L0;
+  const bool multi_sample = R.n_samples > 1;
+  const int nloci = tl.L1 - L0;
+  // count * 100 / depth > threshold  <=>  count * 100 >= (threshold + 1) * depth  (integers, depth > 0)
+  const int64_t thr1 = (int64_t)threshold + 1;
+  auto passes = [thr1](uint32_t count, uint32_t depth) { return (int64_t)count * 100 >= thr1 * (int64_t)depth; };
+  // uniform trip count so every wave reaches the wave-level reservations together
+  for (int i0 = 0; i0 < nloci; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    CallRec out0, out1;  // named (not an array): no scratch
+    unsigned nout = 0;
+    bool to_complex = false;
+    if (wide && i < nloci) {
+      to_complex = true;
+    } else if (i < nloci) {
+      const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
+                     wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
+      const uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
+      const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
+      const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
+      if (depth > 0) {
+        ++visited;
+        uint32_t mask = wnn & 0xFu;  // W_MASK aliases W_NN's low bits
+        const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
+        const uint32_t ev[4] = {eac & 0xFFFFu, eac >> 16, etg & 0xFFFFu, etg >> 16};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c[k] > ev[k]) mask |= 1u << k;
+        const bool ambiguous = __popc(mask) > 1;
+        if (ambiguous) ++amb;
+        if (ambiguous || cx > 0 || multi_sample) {
+          to_complex = true;
+        } else {
+          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+          const int rc = mask ? (__ffs((int)mask) - 1) : 4;  // select chain: no dynamic register indexing
+          const uint32_t c_ref = rc == 0 ? c[0] : rc == 1 ? c[1] : rc == 2 ? c[2] : rc == 3 ? c[3] : c[4];
+          const int32_t pos = L0 + i;
+          const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
+          constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                                       ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+          if (!passes(depth - c_ref, depth)) {
+            // every non-reference allele has count <= depth - c_ref, so none passes the
+            // threshold: HomRef if the reference allele passes, else NoCall (the same
+            // outcome as the general case split below)
+            const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+            if (ref_pass ? emit_ref : emit_no_call) {
+              CallRec rr;
+              rr.key = ord << 12;
+              rr.contig = tl.contig;
+              rr.pos = pos;
+              rr.sample = 0;
+              rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
+              rr.flags = 0;
+              rr.ref_len = 1;
+              rr.alt_len = 5;
+              rr.allele = (uint64_t)ref | kAltSym;
+              if (nout == 0) out0 = rr;
+              else out1 = rr;
+              ++nout;
+            }
+          } else {
+            // Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of
+            // Allele(ref, alt) for one ref is the alt byte order A < C < G < N < T, i.e. the
+            // categories 0, 1, 3, 4, 2.  Sorting keys descending = sortBy(-count), ties canonical.
+            uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
+            int npass = 0;
+#pragma unroll
+            for (int rank = 0; rank < 5; ++rank) {
+              const int cat = (0x24310 >> (4 * rank)) & 0xF;
+              const uint32_t cc = c[cat];
+              if (cc == 0 || !passes(cc, depth)) continue;
+              ++npass;
+              uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
+              if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
+              if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
+              if (key > k2) { k2 = key; }
+            }
+            auto key_base = [](uint32_t key) -> uint8_t {
+              const int rank = 255 - (int)(key & 0xFFu);
+              return cat_base((0x24310 >> (4 * rank)) & 0xF);
+            };
+            const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
+            if (tie) ++ties;
+            const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
+            auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
+              CallRec rr;
+              rr.key = (ord << 12) | (uint64_t)sub;
+              rr.contig = tl.contig;
+              rr.pos = pos;
+              rr.sample = 0;
+              rr.gt0 = g0;
+              rr.gt1 = g1;
+              rr.flags = fl;
+              rr.ref_len = 1;
+              rr.alt_len = alt_sym ? 5 : 1;
+              rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
+              return rr;
+            };
+            const uint8_t b0 = key_base(k0), b1 = key_base(k1);
+            auto push = [&](const CallRec &rr) {
+              if (nout == 0) out0 = rr;
+              else out1 = rr;
+              ++nout;
+            };
+            if (npass == 0) {
+              if (emit_no_call) push(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
+            } else if (npass == 1 && b0 == ref) {
+              if (emit_ref) push(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
+            } else if (npass == 1) {
+              push(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
+            } else {
+              const bool v1 = b0 != ref, v2 = b1 != ref;
+              if (v1 != v2) {
+                push(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
+              } else if (v1 && v2) {
+                push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
+                push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
+              }
+              // two non-variant single-base alleles cannot occur (all Match alleles share ref)
+            }
+          }
+        }
+      }
+    }
+    // reserve + write records (wave-aggregated, in the writer's partition)
+    const unsigned long long base = out.reserve(0, nout);
+    CallRec *prec = recs + out.base[0];
+    if (nout > 0 && base < out.cap[0]) prec[base] = out0;
+    if (nout > 1 && base + 1 < out.cap[0]) prec[base + 1] = out1;
+    const unsigned long long cb = out.reserve(1, to_complex ? 1u : 0u);
+    if (to_complex && cb < out.cap[1])
+      cplx[out.base[1] + cb] = ComplexItem{(int32_t)tile_id, L0 + i, wide ? 1 : 0};
+  }
+}
+
+// Run counters (visited / ambiguous / tie loci) of a workgroup, added once at its end.
+__device__ __forceinline__ void add_run_counters(Counters *ctr, unsigned visited, unsigned amb, unsigned ties,
+                                                 int slot) {
+  __shared__ unsigned red[3];
+  if (threadIdx.x < 3) red[threadIdx.x] = 0;
+  __syncthreads();
+  if (visited) atomicAdd(&red[0], visited);
+  if (amb) atomicAdd(&red[1], amb);
+  if (ties) atomicAdd(&red[2], ties);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int sl = slot & (kSpread - 1);
+    if (red[0]) atomicAdd(&ctr->spread[0][sl], (unsigned long long)red[0]);
+    if (red[1]) atomicAdd(&ctr->spread[1][sl], (unsigned long long)red[1]);
+    if (red[2]) atomicAdd(&ctr->spread[2][sl], (unsigned long long)red[2]);
+  }
+}
+
+// Geometry of the column kernel (T = 512 loci per tile, two lanes per 4-locus column).
+// Per workgroup: two LDS buffers of {sequence stage, ColDesc rows, MD events} (the next
+// tile's are DMA'd while this one is counted), the histogram words, the column buckets:
+// about 80 KiB, two workgroups per CU.  plan_tiles marks tiles whose window fits.
+struct ColsCfg {
+  static constexpr int kT = 512;
+  static constexpr int kThreads = 512;
+  static constexpr int kLanesPerCol = kThreads / (kT / 4);  // rows of a column split over 4 lanes
+  static constexpr int kStage = 24 * 1024;  // sequence bytes (1 KiB DMA pieces)
+  static constexpr int kMeta = 256;         // reads (ColDesc rows, one per thread)
+  static constexpr int kEv = 512;           // MD events
+  // one buffer: stage | rows (+16 B alignment, +256 B dword-DMA tail) | events (same)
+  static constexpr int kRowsOff = kStage + 16;  // + 16 zero bytes after the stage (kZero)
+  static constexpr int kEvOff = kRowsOff + kMeta * 24 + 16 + 256;
+  static constexpr int kBuf = kEvOff + kEv * 4 + 16 + 256;
+};
+
+// Byte counters of one lane's column: c_a c_c c_t c_g hold one byte per locus; nf8 reads
+// fully covering the column since the last flush (<= 255).  Flushed into the LDS words with
+// atomics (the other lane of the column and the per-read pass add to the same words).
+struct ColCounts {
+  uint32_t ca = 0, cc = 0, ct = 0, cg = 0, nf8 = 0;
+  __device__ __forceinline__ void flush(uint32_t *cnt, int S, int c) {
+    if (nf8 == 0) return;
+    const uint32_t cn = nf8 * 0x01010101u - (ca + cc + ct + cg);  // bytewise, no borrow
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t sel = 0x0C000C00u | ((uint32_t)(4 + b) << 16) | (uint32_t)b;  // [x_b, 0, y_b, 0]
+      const uint32_t ac = __builtin_amdgcn_perm(cc, ca, sel), tg = __builtin_amdgcn_perm(cg, ct, sel);
+      const uint32_t nn = ((cn >> (8 * b)) & 0xFFu) << 16;
+      if (ac) atomicAdd(cnt + W_AC * S + kGuard + c + b, ac);
+      if (tg) atomicAdd(cnt + W_TG * S + kGuard + c + b, tg);
+      if (nn) atomicAdd(cnt + W_NN * S + kGuard + c + b, nn);
+    }
+    ca = cc = ct = cg = nf8 = 0;
+  }
+};
+
+// LDS-DMA of the global byte range [g, g + n) into LDS at `l` (16-B aligned g), by wave
+// `wave` of NW, as 1 KiB (dwordx4) or 256 B (dword) pieces.
+template <int NW, int WIDTH>
+__device__ __forceinline__ void dma_range(const uint8_t *g, uint8_t *l, int n, int wave, int lane) {
+  constexpr int P = 64 * WIDTH;
+  const int np = (n + P - 1) / P;
+  for (int q = wave; q < np; q += NW) {
+    const void *src = (const void *)(g + q * P + lane * WIDTH);
+    __attribute__((address_space(3))) void *dst = (__attribute__((address_space(3))) void *)(l + q * P);
+    if constexpr (WIDTH == 16) __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(src, dst, 4, 0, 0);
+  }
+}
+
+// germline_cols: persistent workgroups, each over a contiguous run of tiles (XCD-local
+// neighbours: reads straddling two tiles are re-read from L2).  Per tile:
+//   A  wait for this tile's DMA (issued one tile earlier), then DMA the next tile
+//   B  thread per read: the column row (clamped s | e << 16, LDS address of tile locus 0,
+//      written over the ColDesc's pmax_end / seq_lo words) and the column-bucket histogram
+//   C  scan of the buckets -> each lane's row range [lo, hi)
+//   D  column pass (lanes t and t + 128 take alternate rows of column t % 128)
+//   E  per-read pass: column ends and MD events into the LDS histogram (GermSink)
+//   F  flush, decision (germline_decide), histogram zeroed for the next tile
+// Tiles that do not fit (plan_tiles: sbytes == 0) or hold a read the column path cannot
+// count are listed in `slow` for germline_walk.
+__global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
+    const Tile *__restrict__ tiles, int64_t n_tiles, DevReads R, int threshold, int emit_ref, int emit_no_call,
+    CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
+    int32_t *__restrict__ slow, int dbg) {
+  // dbg (diagnostics, env GQ_DBG; results are wrong when bits 0-3 are set): 1 skip the column
+  // pass, 2 skip the per-read pass, 4 skip the decision, 8 skip the DMA; 16 phase clocks
+  using C = ColsCfg;
+  constexpr int T = C::kT, NT = C::kThreads, NW = NT / 64, NCOL = T / 4;
+  constexpr int S = T + 2 * kGuard;
+  constexpr int kNever = (int)(0x7FFFu | 0x80000000u);  // s = 32767, e = -32768: covers no column
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[2][C::kBuf];
+  __shared__ uint32_t hist[NCOL];  // per column bucket: rows starting (lo 16) / prefix-max end reaching (hi 16)
+  __shared__ uint32_t crng[NCOL];  // per column: lo << 16 | hi (its row range)
+  __shared__ unsigned outn[2];  // records / complex items of this workgroup's partition
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // this workgroup's tiles [i0, i1)
+  const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
+  const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
+  const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
+  uint64_t clk[5] = {0, 0, 0, 0, 0};
+
+  auto issue = [&](const Tile &tn, int b) {  // DMA of a tile's window into buffer b
+    if (tn.sbytes <= 0 || (dbg & 8)) return;
+    uint8_t *L = buf[b];
+    dma_range<NW, 16>(R.seq + tn.sb0, L, tn.sbytes, wave, lane);
+    const int64_t d0 = (tn.rb * 24) & ~(int64_t)15;
+    dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(R.cdesc) + d0, L + C::kRowsOff,
+                     (int)(tn.re * 24 - d0), wave, lane);
+    if (tn.mcnt > 0)
+      dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(R.cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, wave, lane);
+  };
+  {  // zero the histogram words, the buckets and the 16 zero bytes after each stage
+    uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+    for (int i = t; i < W_N * S / 4; i += NT) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (t < NCOL) hist[t] = 0;
+    if (t < 2) *reinterpret_cast<uint4 *>(buf[t] + C::kStage) = make_uint4(0u, 0u, 0u, 0u);
+    if (t < 2) outn[t] = 0;
+  }
+  LdsOut out{outn, {og.slot(0, (int)blockIdx.x, 0), og.slot(1, (int)blockIdx.x, 0)}, {og.capA[0], og.capA[1]}};
+  unsigned visited = 0, amb = 0, ties = 0;
+  Tile tn = i0 < i1 ? tiles[i0] : Tile{};
+  if (i0 < i1) issue(tn, 0);
+  const uint32_t *ev_unused = nullptr;
+  (void)ev_unused;
+  for (int64_t i = i0; i < i1; ++i) {
+    const int b = (int)((i - i0) & 1);
+    const Tile tl = tn;
+    const int64_t tid_tile = i;
+    // ---- A: this tile's DMA (issued one tile ago) has landed everywhere; next tile's DMA
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (i + 1 < i1) {
+      tn = tiles[i + 1];
+      issue(tn, b ^ 1);
+    }
+    const uint64_t ta = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    const int32_t L0 = tl.L0, L1 = tl.L1;
+    uint8_t *L = buf[b];
+    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L);
+    const int64_t d0 = (tl.rb * 24) & ~(int64_t)15;
+    uint32_t *rows = reinterpret_cast<uint32_t *>(L + C::kRowsOff + (tl.rb * 24 - d0));  // 6 words per read
+    const uint32_t *evs = reinterpret_cast<const uint32_t *>(L + C::kEvOff);
+    const int nch = (int)(tl.re - tl.rb);
+    const uint32_t sb_lo = (uint32_t)(uint64_t)tl.sb0, mb_lo = (uint32_t)(uint64_t)tl.mb0;
+    // ---- B: rows (thread per read) and buckets
+    int not_col = tl.sbytes <= 0;
+    int32_t my_s = 0, my_e = 0, my_base = 0;
+    bool mine = false;
+    if (!not_col && t < nch) {
+      const uint32_t *d = rows + 6 * t;
+      const int32_t s = (int32_t)d[0], e = (int32_t)d[1], pe = (int32_t)d[2];
+      const uint32_t info = d[3];
+      const int32_t srel = s - L0, erel = e - L0, perel = pe - L0;
+      const uint32_t sa = d[4] - sb_lo;  // stage address of the base at `start`
+      const uint32_t ea = d[5] - mb_lo;  // staged index of the first MD event
+      const int32_t nmd = (int32_t)(info & 0xFFFFu);
+      uint32_t rx = (uint32_t)kNever, ry = 0;
+      if (e > L0 && s < L1) {
+        const bool ok = (info & kColEligible) && sa + (uint32_t)(e - s) <= (uint32_t)tl.sbytes &&
+                        ea + (uint32_t)nmd <= (uint32_t)tl.mcnt;
+        if (!ok) {
+          not_col = 1;
+        } else {
+          const int32_t sc = srel > -4 ? srel : -4, ec = erel < T + 4 ? erel : T + 4;
+          rx = (uint32_t)((sc & 0xFFFF) | (ec << 16));
+          ry = sa - (uint32_t)srel;  // LDS address of tile locus 0
+          mine = true;
+          my_s = srel;
+          my_e = erel;
+          my_base = (int32_t)ry;
+        }
+      }
+      // rows [0, hi(col)) start at or before the column's last locus; rows [0, lo(col))
+      // have prefix-max end at or before its first locus (so cover none of it)
+      const int bs = srel < 0 ? 0 : srel >> 2, bp = perel < 0 ? 0 : (perel + 3) >> 2;
+      if (bs < NCOL) atomicAdd(&hist[bs], 1u);
+      if (bp < NCOL) atomicAdd(&hist[bp], 1u << 16);
+      // rows keep: d0 start, d1 end, d5 md_lo; d2 d3 <- the column row (rx, ry);
+      // d4 <- n_md | 1 << 31 if the read's events go to the histogram (mine)
+      *reinterpret_cast<uint2 *>(const_cast<uint32_t *>(d) + 2) = make_uint2(rx, ry);
+      const_cast<uint32_t *>(d)[4] = (uint32_t)nmd | (mine ? 0x80000000u : 0u);
+    }
+    if (__syncthreads_or(not_col)) {  // uniform: the tile goes to the walker kernel
+      if (t < NCOL) hist[t] = 0;
+      if (t == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_slow, 1ull);
+        slow[k] = (int32_t)tid_tile;
+      }
+      continue;  // the next iteration's barrier orders the bucket reset
+    }
+    // ---- C: inclusive scan of the packed buckets over the columns (wave 0, two columns per
+    //      lane) -> crng[col] = (lo << 16 | hi) of every column
+    if (wave == 0) {
+      const uint32_t x0 = hist[2 * lane], x1 = hist[2 * lane + 1];
+      const uint32_t sc = wave_incl_scan(x0 + x1);
+      crng[2 * lane] = sc - x1;
+      crng[2 * lane + 1] = sc;
+      hist[2 * lane] = 0;  // ready for the next tile (its atomics follow this tile's barriers)
+      hist[2 * lane + 1] = 0;
+    }
+    __syncthreads();
+    // lanes 4q .. 4q + 3 share column q and take alternate rows
+    const int col = t >> 2, par = t & 3;
+    const uint32_t v = crng[col];
+    const int lo = (int)(v >> 16), hi = (int)(v & 0xFFFFu);
+    const uint64_t tc = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch,
+    //      all loads of a batch issued before use
+    constexpr int P = C::kLanesPerCol, U = 8;
+    const int c = 4 * col;
+    ColCounts cc;
+    if (!(dbg & 1)) {
+      for (int k0 = lo + par; k0 < hi; k0 += P * U) {
+        uint2 m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          m[u] = *reinterpret_cast<const uint2 *>(rows + 6 * min(k0 + P * u, hi - 1) + 2);
+        uint32_t a[U];
+        uint32_t nf = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu), e = (int32_t)m[u].x >> 16;
+          const bool full = k0 + P * u < hi && s <= c && e >= c + 4;
+          a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 8 zero bytes
+          nf += full ? 1u : 0u;
+        }
+        uint32_t w0[U], w1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          w0[u] = st32[a[u] >> 2];
+          w1[u] = st32[(a[u] >> 2) + 1];
+        }
+        uint32_t n_ac = 0, n_tg = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t w = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]);
+          const uint32_t sel = w & 0x07070707u;  // A 1, C 3, T 4, N 6, G 7 (0 for the zero dword)
+          n_ac += __builtin_amdgcn_perm(0u, 0x10000100u, sel);
+          n_tg += __builtin_amdgcn_perm(0x10000001u, 0u, sel);
+        }
+        if (cc.nf8 + nf > 255) cc.flush(cnt, S, c);
+        cc.ca += n_ac & 0x0F0F0F0Fu;
+        cc.cc += (n_ac >> 4) & 0x0F0F0F0Fu;
+        cc.ct += n_tg & 0x0F0F0F0Fu;
+        cc.cg += (n_tg >> 4) & 0x0F0F0F0Fu;
+        cc.nf8 += nf;
+      }
+    }
+    {  // quad sums of the column's four lanes (bytes cannot overflow while the reads sum to <= 255)
+      auto qsum = [](uint32_t x) {
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1 0 3 2
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2 3 0 1
+        return x;
+      };
+      const uint32_t nq = qsum(cc.nf8);
+      const uint32_t sa_ = qsum(cc.ca), sc_ = qsum(cc.cc), st_ = qsum(cc.ct), sg_ = qsum(cc.cg);
+      if (nq <= 255) {
+        cc.ca = sa_;
+        cc.cc = sc_;
+        cc.ct = st_;
+        cc.cg = sg_;
+        cc.nf8 = par == 0 ? nq : 0u;  // one lane of the four adds the column's counts
+      }
+      cc.flush(cnt, S, c);
+    }
+    const uint64_t te = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    // ---- E: threads t < 256 the column ends of read t, threads t >= 256 the MD events of
+    //      read t - 256 (into the LDS histogram, GermSink)
+    if (!(dbg & 2)) {
+      GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+      if (mine) {
+        const int32_t s = my_s, e = my_e;
+        const int32_t cs = s & ~3, ce = (e - 1) & ~3;
+        const bool ps = s != cs || e < cs + 4, pe = (e & 3) != 0 || s > ce;
+        // the <= 3 + 3 bytes of the two partial columns: both dwords loaded, then one atomic per byte
+        int32_t ea0 = s, ea1 = e < cs + 4 ? e : cs + 4;  // first partial column's loci
+        int32_t eb0 = ce, eb1 = e;                       // last partial column's loci
+        if (!ps) ea1 = ea0;
+        if (!pe || ce == cs) eb1 = eb0;
+        ea0 = ea0 > 0 ? ea0 : 0;
+        ea1 = ea1 < T ? ea1 : T;
+        eb0 = eb0 > 0 ? eb0 : 0;
+        eb1 = eb1 < T ? eb1 : T;
+        const uint32_t pa = (uint32_t)my_base + (uint32_t)ea0, pb = (uint32_t)my_base + (uint32_t)eb0;
+        const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1];
+        const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1];
+        const uint32_t wa = __builtin_amdgcn_alignbyte(wa1, wa0, pa), wb = __builtin_amdgcn_alignbyte(wb1, wb0, pb);
+        for (int32_t l = ea0; l < ea1; ++l) sink.bases4_clean(l, (wa >> (8 * (l - ea0))) & 0xFFu, 1u, 0);
+        for (int32_t l = eb0; l < eb1; ++l) sink.bases4_clean(l, (wb >> (8 * (l - eb0))) & 0xFFu, 1u, 0);
+      }
+      const int k = t - C::kMeta;
+      if (k >= 0 && k < nch) {
+        const uint32_t *d = rows + 6 * k;
+        const uint32_t d4 = d[4];
+        const int32_t nmd = (int32_t)(d4 & 0xFFFFu);
+        if ((d4 & 0x80000000u) && nmd > 0) {
+          const int32_t s = (int32_t)d[0] - L0, x1 = L1 - L0;
+          const int32_t e0 = (int32_t)(d[5] - mb_lo);
+          for (int32_t k0 = 0; k0 < nmd; k0 += 4) {  // events are sorted by offset; 4 loads in flight
+            uint32_t w4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w4[u] = evs[e0 + min(k0 + u, nmd - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int32_t l = s + (int32_t)(w4[u] >> 16);
+              if (k0 + u < nmd && l >= 0 && l < x1) sink.event_i(l, (uint8_t)w4[u], (uint8_t)(w4[u] >> 8), 0);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // histogram complete
+    const uint64_t tf = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    // ---- F: decision, then the histogram words are zeroed for the next tile
+    if (!(dbg & 4))
+      germline_decide<T>(cnt, tl, tid_tile, false, R, threshold, emit_ref, emit_no_call, recs, cplx, out, visited,
+                         amb, ties);
+    __syncthreads();  // decision reads done before the words are zeroed
+    {
+      uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+      for (int k = t; k < W_N * S / 4; k += NT) c4[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (dbg & 16) {
+      const uint64_t now = __builtin_readcyclecounter();
+      clk[0] += now - ta;  // tile total from after the A barrier
+      clk[1] += te - tc;   // scan + column pass
+      clk[2] += tf - te;   // per-read pass + barrier
+      clk[3] += now - tf;  // decision
+      clk[4] += 1;
+    }
+  }
+  add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
+  if (t == 0) {  // this workgroup's partition counts (may exceed the capacity: host retry)
+    ctr->part[0][blockIdx.x] = outn[0];
+    ctr->part[1][blockIdx.x] = outn[1];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((dbg & 16) && lane == 0 && clk[4]) {
+    atomicAdd(&ctr->prof[0], (unsigned long long)clk[0]);
+    atomicAdd(&ctr->prof[1], (unsigned long long)clk[1]);
+    atomicAdd(&ctr->prof[2], (unsigned long long)clk[2]);
+    atomicAdd(&ctr->prof[3], (unsigned long long)clk[3]);
+    atomicAdd(&ctr->prof[7], (unsigned long long)clk[4]);
+  }
+}
+
+// The tiles germline_cols handed over: every read walked lane-per-read (walk_read_lane,
+// PileupElement.scala:68-248) into the LDS histogram, bases from HBM.  A grid-stride loop
+// over the list ctr->n_slow long.
+template <int T>
+__global__ __launch_bounds__(kBlock) void germline_walk(const Tile *__restrict__ tiles, const int32_t *__restrict__ slow,
+                                                        DevReads R, int threshold, int emit_ref, int emit_no_call,
+                                                        CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx,
+                                                        OutGeom og,
+                                                        Counters *ctr) {
+  constexpr int S = T + 2 * kGuard;
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
+  const int64_t n = (int64_t)ctr->n_slow;
+  const int part = kPartsCols + (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kPartsCols - 1));
+  GlobalOut out{ctr, part, {og.slot(0, part, 0), og.slot(1, part, 0)}, {og.capB[0], og.capB[1]}};
+  unsigned visited = 0, amb = 0, ties = 0;
+  for (int64_t q = blockIdx.x; q < n; q += gridDim.x) {
+    const int64_t tid_tile = slow[q];
+    const Tile tl = tiles[tid_tile];
+    const bool wide = (tl.re - tl.rb) >= 65535;
+    uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+    for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    if (!wide) {
+      GermSink<T, 0> sink{cnt, tl.L0, &ctr->err, &ctr->err_pos};
+      for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, tl.L0, tl.L1, sink);
+    }
+    __syncthreads();
+    germline_decide<T>(cnt, tl, tid_tile, wide, R, threshold, emit_ref, emit_no_call, recs, cplx, out, visited, amb,
+                       ties);
+    __syncthreads();
+  }
+  add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
+}

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -25,10 +26,13 @@ gq_status set_err(gq_status s, const char *fmt, ...);  // thread-local message f
   } while (0)
 
 constexpr int kBlock = 256;
-constexpr int kGermT = 1024;  // loci per germline tile
+constexpr int kGermT = 512;  // loci per germline tile
 constexpr int kCountT = 512;  // loci per counts tile
-constexpr int kStageBytes = 40 * 1024;
 constexpr size_t kSeqPad = 2048;  // zeroed tail of the uploaded sequence pool  // LDS staging of a read batch's sequence bytes
+
+constexpr int kSpread = 64;
+constexpr int kParts = 2048;      // output partitions (see Counters::part)
+constexpr int kPartsCols = 1024;  // [0, 1024): one per germline_cols workgroup; the rest: walker / complex waves
 
 struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_rec;
@@ -40,11 +44,19 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   int err;
   int pad;
   long long err_pos;
-  // per-tile run counters of germline_tile, spread over kSpread addresses (summed on the host)
+  unsigned long long n_slow;       // tiles germline_cols handed to germline_walk
+  unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
+  // per-tile run counters, spread over kSpread addresses (summed on the host)
   unsigned long long spread[3][64];
-  unsigned long long prof[8];  // diagnostic phase clocks (GQ_ABLATE=32 builds only)
+  unsigned long long prof[8];  // diagnostic phase clocks (GQ_DBG=16 only)
+  // ---- device-only tail (the host copies the head, up to `part`)
+  // germline outputs: records (0) and complex items (1) are reserved per partition — a
+  // writer appends to partition p at slot p * capacity + k — so no single counter serialises
+  // every writer on the chip.  part_off = exclusive offsets of the kept counts (part_scan).
+  unsigned long long part[2][kParts];
+  unsigned long long part_off[2][kParts + 1];
 };
-constexpr int kSpread = 64;
+constexpr size_t kCountersHead = offsetof(Counters, part);
 
 // Wave-aggregated reservation of `n` slots on a global counter.
 __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *ctr, unsigned n) {
@@ -62,6 +74,66 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *c
   if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
   base = __shfl(base, 63, 64);
   return base + (x - n);
+}
+
+// Geometry of the partitioned germline outputs (records: which = 0, complex items: 1).
+// Partitions [0, ncols) belong to germline_cols workgroups (capacity capA each), partitions
+// [kPartsCols, kParts) to walker / complex-kernel waves (capacity capB each); the others are
+// unused.  slot(which, p, k) is the buffer index of element k of partition p.
+struct OutGeom {
+  int ncols;
+  int pad_;
+  unsigned long long capA[2], capB[2];
+  __host__ __device__ __forceinline__ unsigned long long cap(int which, int p) const {
+    return p < kPartsCols ? capA[which] : capB[which];
+  }
+  __host__ __device__ __forceinline__ unsigned long long slot(int which, int p, unsigned long long k) const {
+    return p < kPartsCols ? (unsigned long long)p * capA[which] + k
+                          : (unsigned long long)ncols * capA[which] + (unsigned long long)(p - kPartsCols) * capB[which] + k;
+  }
+  __host__ __device__ __forceinline__ unsigned long long total(int which) const {
+    return (unsigned long long)ncols * capA[which] + (unsigned long long)(kParts - kPartsCols) * capB[which];
+  }
+};
+
+// Buffer index of the k-th kept element of a partitioned output: the partition q with
+// off[q] <= k < off[q + 1] (off = part_off[which], kParts + 1 entries), then its slot.
+__device__ __forceinline__ unsigned long long part_slot(const unsigned long long *off, unsigned long long k,
+                                                        const OutGeom &g, int which) {
+  int lo = 0, hi = kParts - 1;  // last q with off[q] <= k
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (off[m] <= k) lo = m;
+    else hi = m - 1;
+  }
+  return g.slot(which, lo, k - off[lo]);
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave with DPP row shifts and row broadcasts
+// (no LDS round trips).  Every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Wave-aggregated reservation of n <= 3 slots per lane on an LDS counter: lane prefixes
+// from two ballots, one returning LDS atomic by the first active lane (a few hundred
+// cycles, not the microseconds of a returning device-scope atomic).
+__device__ __forceinline__ unsigned wave_reserve_lds(unsigned *ctr, unsigned n) {
+  const uint64_t b1 = __ballot(n & 1u), b2 = __ballot(n & 2u);
+  if ((b1 | b2) == 0) return 0;
+  const uint64_t lt = __builtin_amdgcn_read_exec() & ((1ull << (threadIdx.x & 63)) - 1ull);
+  const unsigned pre = (unsigned)__popcll(b1 & lt) + 2u * (unsigned)__popcll(b2 & lt);
+  const unsigned total = (unsigned)__popcll(b1) + 2u * (unsigned)__popcll(b2);
+  unsigned base = 0;
+  if (lt == 0) base = atomicAdd(ctr, total);  // the first active lane
+  base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+  return base + pre;
 }
 
 struct Plan {
@@ -102,8 +174,9 @@ struct gq_ctx {
   hipEvent_t ev[6] = {};
   gq_timings timings{};
   int germ_tile = gq::kGermT;
+  int n_cu = 0;
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
-  gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb;
+  gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
 };
 
 struct gq_dev_reads {
@@ -116,7 +189,8 @@ struct gq_dev_reads {
 
 namespace gq {
 // Loci ranges -> locus tiles of T loci with each tile's read window in `rd`, written to `tiles`.
-gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles);
+gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,
+               int stage_cap = 0, int meta_cap = 0, int ev_cap = 0);
 gq_status check_device_error(gq_ctx *c, const Counters &h);
 }  // namespace gq
 

@@ -46,7 +46,22 @@ struct DevReads {
   const int16_t *lead;   // leading soft clip of a [S|H]*(M|=|X)[S|H]* CIGAR, -1 otherwise
   const uint8_t *ev_rb;  // per MD event: the read's sequenced base at that position (0 for deletions)
   const uint8_t *clean;  // 1 if every sequenced byte of the read is one of A C G T N
+  int32_t pool_ordered;  // reads' sequence bytes are disjoint and in read order in the pool
+  // derived at upload for the germline column kernel (LDS-DMA'd per tile, see ColDesc)
+  const struct ColDesc *cdesc;  // one per read
+  const uint32_t *cev;          // one per MD event: offset << 16 | MD base << 8 | read base
 };
+
+// Packed per-read record of the germline column kernel (24 bytes, DMA'd into LDS per tile).
+struct ColDesc {
+  int32_t start, end, pmax_end;
+  uint32_t info;    // bits 0-15 n_md, bit 16: column-eligible (single (M|=|X) block, A/C/G/T/N bases,
+                    // MD present, span < 32768, n_md < 65536)
+  uint32_t seq_lo;  // low 32 bits of the pool offset of the base at `start` (seq_off + leading clip)
+  uint32_t md_lo;   // low 32 bits of md_off
+};
+static_assert(sizeof(ColDesc) == 24, "ColDesc layout");
+constexpr uint32_t kColEligible = 1u << 16;
 
 // One locus tile: contiguous loci [L0, L1) of one contig, plus the index range
 // [rb, re) of reads that can overlap it (pmax_end > L0, start < L1).
@@ -54,7 +69,12 @@ struct Tile {
   int64_t ordinal0;  // output ordinal of L0 (position in the concatenated loci ranges)
   int64_t rb, re;
   int32_t contig, L0, L1, range;
+  int64_t sb0;     // germline column kernel: 16-aligned pool offset of the tile's sequence bytes
+  int32_t sbytes;  // bytes to stage from sb0 when the whole read window fits one LDS stage, else 0
+  int32_t mcnt;    // MD events to stage from mb0
+  int64_t mb0;     // first MD event index to stage (a multiple of 4)
 };
+static_assert(sizeof(Tile) == 64, "Tile layout");
 
 // Per-call record written by the germline kernels, sorted by `key` afterwards.
 struct CallRec {
@@ -321,124 +341,6 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   }
 }
 
-
-// Chunk-major walk of one batch of up to blockDim.x start-sorted reads (the default).
-// Lane-per-read loads of 16-byte chunks hit a different cache line per lane; here the
-// batch's sequence bytes, which are one contiguous range of the pool, are read as
-// consecutive 16-byte chunks by consecutive threads (1 KiB per wave-instruction).
-//   A. thread t fills row t of an LDS table for read r0 + t: the pool byte range [lo, hi)
-//      of its Match/Mismatch elements on the tile, and base = tile index - byte offset;
-//   B. every thread takes chunks k = t, t + blockDim.x, ...; each chunk's bytes are
-//      counted for the reads whose ranges intersect it (found from a guess + short scan);
-//   C. thread t adds its own read's MD events, or walks the read itself if it is not a
-//      simple CIGAR in pool order.
-// Returns false (nothing counted) if the batch's reads are not laid out in pool order; the
-// caller then walks it lane-per-read.
-struct ChunkRows {
-  int32_t *lo, *hi, *base;
-  uint8_t *info;  // bit0 reverse strand, bit1 clean bases
-};
-
-template <class Sink>
-__device__ __forceinline__ bool walk_batch_chunked(const DevReads &R, int64_t r0, int nb, int32_t L0, int32_t L1,
-                                                   Sink &sink, ChunkRows rows, int *flag) {
-  const int t = threadIdx.x;
-  const int64_t last = r0 + nb - 1;
-  const int64_t B0 = R.seq_off[r0] & ~(int64_t)15;
-  const int64_t Bend = R.seq_off[last] + R.seq_len[last];
-  const int n16 = (int)((Bend - B0 + 15) >> 4);
-  if (t == 0) *flag = 0;
-  __syncthreads();
-  // ---- A: table rows
-  int32_t s = 0, e = 0, a = 0, b = 0, nmd = 0;
-  int64_t md_off = 0;
-  uint8_t fl = 0;
-  bool mine = false;  // this thread's read needs phase C
-  bool simple_in = false;
-  uint4 e4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), b4 = make_uint4(0u, 0u, 0u, 0u);
-  if (t < nb) {
-    const int64_t r = r0 + t;
-    s = R.start[r];
-    e = R.end[r];
-    const int64_t so = R.seq_off[r];
-    const int32_t sl = R.seq_len[r];
-    const int32_t lead = R.lead[r];
-    nmd = R.n_md[r];
-    md_off = R.md_off[r];
-    fl = R.flags[r];
-    const bool clean = R.clean[r] != 0;
-    bool ordered = so >= B0 && so + sl <= Bend;
-    if (t > 0) ordered = ordered && so >= R.seq_off[r - 1] + R.seq_len[r - 1];
-    if (!ordered) atomicOr(flag, 1);
-    a = s > L0 ? s : L0;
-    b = e < L1 ? e : L1;
-    const bool overlaps = a < b;
-    simple_in = overlaps && lead >= 0 && nmd >= 0;
-    mine = overlaps;
-    int32_t lo = (int32_t)(so - B0), hi = lo, base = 0;
-    if (simple_in) {
-      lo = (int32_t)(so + lead + (a - s) - B0);
-      hi = lo + (b - a);
-      base = (a - L0) - lo;
-      const uint32_t *ev = R.md_ev + md_off;
-      const uint8_t *evb = R.ev_rb + md_off;
-      e4.x = 0 < nmd ? ev[0] : 0xFFFFFFFFu;
-      e4.y = 1 < nmd ? ev[1] : 0xFFFFFFFFu;
-      e4.z = 2 < nmd ? ev[2] : 0xFFFFFFFFu;
-      e4.w = 3 < nmd ? ev[3] : 0xFFFFFFFFu;
-      b4.x = 0 < nmd ? evb[0] : 0u;
-      b4.y = 1 < nmd ? evb[1] : 0u;
-      b4.z = 2 < nmd ? evb[2] : 0u;
-      b4.w = 3 < nmd ? evb[3] : 0u;
-    }
-    rows.lo[t] = lo;
-    rows.hi[t] = hi;
-    rows.base[t] = base;
-    rows.info[t] = (uint8_t)((fl & 1) | (clean ? 2 : 0));
-  }
-  __syncthreads();
-  if (*flag) return false;
-  // ---- B: chunks
-  const int avg = max(16, (n16 * 16) / nb);
-  int g = 0;
-  for (int k = t; k < n16; k += blockDim.x) {
-    const int cb = 16 * k;
-    const uint4 c = *reinterpret_cast<const uint4 *>(R.seq + B0 + cb);
-    int j = cb / avg;
-    j = j < g ? g : (j > nb - 1 ? nb - 1 : j);
-    while (j > 0 && rows.hi[j - 1] > cb) --j;
-    while (j < nb && rows.hi[j] <= cb) ++j;
-    g = j;
-    for (; j < nb; ++j) {
-      const int32_t lo = rows.lo[j];
-      if (lo >= cb + 16) break;
-      const int32_t hi = rows.hi[j];
-      const int32_t f = lo > cb ? lo - cb : 0, u = hi < cb + 16 ? hi - cb : 16;
-      if (f >= u) continue;
-      const uint32_t vm = ((u >= 16 ? 0x10000u : (1u << u)) - 1u) & ~((1u << f) - 1u);
-      const int32_t i0 = cb + rows.base[j];
-      const uint8_t inf = rows.info[j];
-      const uint8_t rfl = inf & 1;
-      if (inf & 2) {
-        sink.bases4_clean(i0, c.x, vm & 15u, rfl);
-        sink.bases4_clean(i0 + 4, c.y, (vm >> 4) & 15u, rfl);
-        sink.bases4_clean(i0 + 8, c.z, (vm >> 8) & 15u, rfl);
-        sink.bases4_clean(i0 + 12, c.w, (vm >> 12) & 15u, rfl);
-      } else {
-        sink.bases4(i0, c.x, vm & 15u, rfl);
-        sink.bases4(i0 + 4, c.y, (vm >> 4) & 15u, rfl);
-        sink.bases4(i0 + 8, c.z, (vm >> 8) & 15u, rfl);
-        sink.bases4(i0 + 12, c.w, (vm >> 12) & 15u, rfl);
-      }
-    }
-  }
-  // ---- C: MD events of simple reads; other reads walked by their own thread
-  if (mine) {
-    if (simple_in) events_run(R.md_ev + md_off, R.ev_rb + md_off, e4, b4, nmd, s, a, b, L0, fl, sink);
-    else walk_read_lane(R, r0 + t, L0, L1, sink);
-  }
-  return true;
-}
 
 // LDS histogram: six u32 words per locus (SoA: word * S + guard + i, so consecutive loci
 // sit on consecutive banks), each holding two 16-bit counters.  A sequenced base b has

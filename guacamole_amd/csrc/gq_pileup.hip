@@ -59,7 +59,7 @@ namespace {
 __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *__restrict__ r_start,
                            const int64_t *__restrict__ r_end, const int64_t *__restrict__ r_ord,
                            const int64_t *__restrict__ r_tile0, int64_t n_ranges, int64_t n_tiles, int T,
-                           DevReads R, Tile *__restrict__ tiles) {
+                           DevReads R, Tile *__restrict__ tiles, int stage_cap, int meta_cap, int ev_cap) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tiles) return;
   int64_t lo = 0, hi = n_ranges - 1;  // largest r with r_tile0[r] <= t
@@ -96,15 +96,63 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   tl.L0 = (int32_t)L0;
   tl.L1 = (int32_t)L1;
   tl.range = (int32_t)r;
+  // the germline column kernel stages the whole read window of a tile in LDS: at most
+  // meta_cap reads, sequence bytes within stage_cap (1 KiB pieces), at most ev_cap MD events
+  // (4-event aligned).  Otherwise sbytes = 0 and the tile goes to the walker kernel.
+  tl.sb0 = 0;
+  tl.sbytes = 0;
+  tl.mb0 = 0;
+  tl.mcnt = 0;
+  if (stage_cap > 0 && a0 > rb && a0 - rb <= meta_cap) {
+    const int64_t B0 = R.seq_off[rb] & ~(int64_t)15;
+    const int64_t nb = R.seq_off[a0 - 1] + R.seq_len[a0 - 1] - B0;
+    const int64_t M0 = R.md_off[rb] & ~(int64_t)3;
+    const int64_t nm = R.md_off[a0 - 1] + (R.n_md[a0 - 1] > 0 ? R.n_md[a0 - 1] : 0) - M0;
+    if (nb > 0 && ((nb + 1023) >> 10) * 1024 <= stage_cap && B0 + ((nb + 1023) >> 10) * 1024 <= R.seq_cap &&
+        nm >= 0 && nm <= ev_cap) {
+      tl.sb0 = B0;
+      tl.sbytes = (int32_t)nb;
+      tl.mb0 = M0;
+      tl.mcnt = (int32_t)nm;
+    }
+  }
   tiles[t] = tl;
+}
+
+// Column-kernel records (derived once at upload, after read_shape): the packed ColDesc of
+// each read and one u32 per MD event (offset << 16 | MD base << 8 | read base).
+__global__ void col_derive(DevReads R, ColDesc *__restrict__ cd, uint32_t *__restrict__ cev) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const int32_t s = R.start[r], e = R.end[r], nmd = R.n_md[r], lead = R.lead[r];
+  const bool ok = lead >= 0 && R.clean[r] && nmd >= 0 && nmd < 65536 && e - s < 32768 && e > s;
+  ColDesc d;
+  d.start = s;
+  d.end = e;
+  d.pmax_end = R.pmax_end[r];
+  d.info = (uint32_t)(nmd > 0 ? (nmd < 65536 ? nmd : 65535) : 0) | (ok ? kColEligible : 0u);
+  d.seq_lo = (uint32_t)(uint64_t)(R.seq_off[r] + (lead > 0 ? lead : 0));
+  d.md_lo = (uint32_t)(uint64_t)R.md_off[r];
+  cd[r] = d;
+  if (nmd > 0) {
+    const uint32_t *ev = R.md_ev + R.md_off[r];
+    const uint8_t *rb = R.ev_rb + R.md_off[r];
+    uint32_t *o = cev + R.md_off[r];
+    for (int32_t k = 0; k < nmd; ++k) {
+      const uint32_t off = ev[k] >> 8;
+      o[k] = off < 32768u ? (off << 16) | ((ev[k] & 0xFFu) << 8) | rb[k] : 0xFFFFFFFFu;
+    }
+  }
 }
 
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
 // [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
 __global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb,
-                           uint8_t *__restrict__ clean) {
+                           uint8_t *__restrict__ clean, int *__restrict__ unordered) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
+  // pool order: read r's bytes start at or after the end of read r - 1's
+  if (r > 0 && R.seq_off[r] < R.seq_off[r - 1] + R.seq_len[r - 1]) atomicOr(unordered, 1);
   {  // every sequenced byte one of A C G T N (the germline fast path's precondition)
     const uint8_t *q = R.seq + R.seq_off[r];
     bool ok = true;
@@ -171,237 +219,8 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ------------------------------------------------------------------------------------------
 // germline_tile: LDS histogram + on-device decision for simple loci
 // ------------------------------------------------------------------------------------------
-#define PUSH_OUT(rec)             \
-  do {                            \
-    if (nout == 0) out0 = (rec);  \
-    else out1 = (rec);            \
-    ++nout;                       \
-  } while (0)
 
-#include "gq_germline_v2.h"
-
-// ABL (diagnostic builds only, selected by env GQ_ABLATE; results are wrong when != 0):
-//   1 = skip the read walk, 2 = skip the decision phase, 4 = base pass without LDS atomics,
-//   8 = skip the MD-event pass.
-template <int T, int ABL = 0, int STAGE = 0, int CH = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : T <= 768 ? 8 : T <= 1024 ? (CH ? 5 : 6) : 3))) void germline_tile(const Tile *__restrict__ tiles, DevReads R, int threshold,
-                                                        int emit_ref, int emit_no_call, CallRec *__restrict__ recs,
-                                                        unsigned long long rec_cap, ComplexItem *__restrict__ cplx,
-                                                        unsigned long long cplx_cap, Counters *ctr) {
-  constexpr int S = T + 2 * kGuard;
-  __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
-  __shared__ __attribute__((aligned(16))) uint4 stage[STAGE ? STAGE / 16 : 1];
-  constexpr int NR = (CH && !STAGE) ? kBlock : 1;  // chunk-major walk: one table row per read of a batch
-  __shared__ int32_t ch_lo[NR], ch_hi[NR], ch_base[NR];
-  __shared__ uint8_t ch_info[NR];
-  __shared__ int ch_flag;
-  const uint64_t pt0 = (ABL & 32) ? __builtin_readcyclecounter() : 0;
-  uint64_t pt1 = 0, pt2 = 0, pt3 = 0;
-  const Tile tl = tiles[blockIdx.x];
-  const int32_t L0 = tl.L0, L1 = tl.L1;
-  // a window of >= 65535 reads could overflow the 16-bit counters: queue every locus of
-  // the tile for the exact (32-bit) kernel instead
-  const bool wide = (tl.re - tl.rb) >= 65535;
-  if (!wide) {
-    GermSink<T, (ABL & 31)> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-    // Reads are walked in batches of up to blockDim.x (one per lane).  A batch's reads
-    // sit in one contiguous byte range of the sequence pool (reads are stored in
-    // alignment order), which is copied into LDS by LDS-DMA (global_load_lds_dwordx4,
-    // 1 KiB per wave-instruction, fully coalesced) while the counters are zeroed; the
-    // lanes then read their bases from LDS instead of issuing scattered 16-byte loads.
-    for (int64_t r0 = tl.rb; r0 < tl.re || r0 == tl.rb; r0 += blockDim.x) {
-      const int64_t nb = min((int64_t)blockDim.x, tl.re - r0);
-      int64_t B0 = 0, n1k = 0;
-      if (STAGE && nb > 0) {
-        B0 = R.seq_off[r0] & ~(int64_t)15;
-        const int64_t B1 = R.seq_off[r0 + nb - 1] + R.seq_len[r0 + nb - 1];
-        n1k = B1 > B0 ? (B1 - B0 + 1023) >> 10 : 0;
-        if (n1k * 1024 > STAGE || B0 + n1k * 1024 > R.seq_cap) n1k = 0;  // not staged: HBM loads
-      }
-      if (!(ABL & 1))
-        for (int64_t q = wave; q < n1k; q += nwaves)
-          __builtin_amdgcn_global_load_lds((const void *)(R.seq + B0 + q * 1024 + lane * 16),
-                                           (__attribute__((address_space(3))) void *)(stage + q * 64), 16, 0, 0);
-      if (r0 == tl.rb) {
-        uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
-        for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
-      if (STAGE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const StageView sv{stage, B0, B0 + n1k * 1024};
-      if ((ABL & 32) && r0 == tl.rb) pt1 = __builtin_readcyclecounter();
-      if (CH && !STAGE && nb > 0 && !(ABL & 1)) {
-        if (!walk_batch_chunked(R, r0, (int)nb, L0, L1, sink, ChunkRows{ch_lo, ch_hi, ch_base, ch_info}, &ch_flag) &&
-            (int64_t)threadIdx.x < nb)
-          walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink);  // reads not in pool order: lane per read
-      } else if (!(ABL & 1) && (int64_t)threadIdx.x < nb) {
-        walk_read_lane(R, r0 + threadIdx.x, L0, L1, sink, sv);
-      }
-      if (ABL & 32) pt2 = __builtin_readcyclecounter();
-      __syncthreads();  // counters complete / stage free for the next batch
-      if (nb <= 0) break;
-    }
-  }
-  __syncthreads();
-  if (ABL & 32) pt3 = __builtin_readcyclecounter();
-  if (ABL & 2) {
-    if (threadIdx.x == 0) atomicAdd(&ctr->visited, (unsigned long long)cnt[kGuard + (blockIdx.x & 63)]);
-    return;
-  }
-
-  const bool multi_sample = R.n_samples > 1;
-  unsigned visited = 0, amb = 0, ties = 0;
-  const int nloci = L1 - L0;
-  // uniform trip count so every wave reaches the wave-level reservations together
-  for (int i0 = 0; i0 < nloci; i0 += blockDim.x) {
-    const int i = i0 + threadIdx.x;
-    CallRec out0, out1;  // named (not an array): no scratch
-    unsigned nout = 0;
-    bool to_complex = false;
-    if (wide && i < nloci) {
-      to_complex = true;
-    } else if (i < nloci) {
-      const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
-                     wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
-      const uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
-      const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
-      const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
-      if (depth > 0) {
-        ++visited;
-        uint32_t mask = cnt[W_MASK * S + kGuard + i] & 0xFu;
-        const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
-        const uint32_t ev[4] = {eac & 0xFFFFu, eac >> 16, etg & 0xFFFFu, etg >> 16};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (c[k] > ev[k]) mask |= 1u << k;
-        const bool ambiguous = __popc(mask) > 1;
-        if (ambiguous) ++amb;
-        if (ambiguous || cx > 0 || multi_sample) {
-          to_complex = true;
-        } else {
-          // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles.
-          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-          const int rc = mask ? (__ffs((int)mask) - 1) : 4;  // select chain: no dynamic register indexing
-          const uint32_t c_ref = rc == 0 ? c[0] : rc == 1 ? c[1] : rc == 2 ? c[2] : rc == 3 ? c[3] : c[4];
-          if ((long long)(depth - c_ref) * 100 / (long long)depth <= threshold) {
-            // fast path: every non-reference allele has count <= depth - c_ref, so none
-            // passes the threshold; the call is HomRef if the reference allele passes,
-            // else NoCall (same outcome as the general case split below)
-            const int32_t pos = L0 + i;
-            const bool ref_pass = c_ref > 0 && (long long)c_ref * 100 / (long long)depth > threshold;
-            if (ref_pass ? emit_ref : emit_no_call) {
-              CallRec rr;
-              rr.key = (uint64_t)(tl.ordinal0 + i) << 12;
-              rr.contig = tl.contig;
-              rr.pos = pos;
-              rr.sample = 0;
-              rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
-              rr.flags = 0;
-              rr.ref_len = 1;
-              rr.alt_len = 5;
-              rr.allele = (uint64_t)ref | ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
-                          ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
-              PUSH_OUT(rr);
-            }
-          } else {
-          // Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of
-          // Allele(ref, alt) for one ref is the alt byte order A < C < G < N < T, i.e. the
-          // categories 0, 1, 3, 4, 2.  Sorting keys descending = sortBy(-count), ties canonical.
-          uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
-          int npass = 0;
-#pragma unroll
-          for (int rank = 0; rank < 5; ++rank) {
-            const int cat = (0x24310 >> (4 * rank)) & 0xF;
-            const uint32_t cc = c[cat];
-            if (cc == 0 || (long long)cc * 100 / (long long)depth <= threshold) continue;
-            ++npass;
-            uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
-            // insert into (k0 >= k1 >= k2)
-            if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
-            if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
-            if (key > k2) { k2 = key; }
-          }
-          auto key_base = [](uint32_t key) -> uint8_t {
-            const int rank = 255 - (int)(key & 0xFFu);
-            return cat_base((0x24310 >> (4 * rank)) & 0xF);
-          };
-          const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
-          if (tie) ++ties;
-          const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
-          const int32_t pos = L0 + i;
-          const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
-          auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
-            CallRec rr;
-            rr.key = (ord << 12) | (uint64_t)sub;
-            rr.contig = tl.contig;
-            rr.pos = pos;
-            rr.sample = 0;
-            rr.gt0 = g0;
-            rr.gt1 = g1;
-            rr.flags = fl;
-            rr.ref_len = 1;
-            if (alt_sym) {  // (ref, "<ALT>")
-              rr.alt_len = 5;
-              rr.allele = (uint64_t)ref | ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
-                          ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
-            } else {
-              rr.alt_len = 1;
-              rr.allele = (uint64_t)ref | ((uint64_t)alt1 << 8);
-            }
-            return rr;
-          };
-          const uint8_t b0 = key_base(k0), b1 = key_base(k1);
-          if (npass == 0) {
-            if (emit_no_call) PUSH_OUT(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
-          } else if (npass == 1 && b0 == ref) {
-            if (emit_ref) PUSH_OUT(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
-          } else if (npass == 1) {
-            PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
-          } else {
-            const bool v1 = b0 != ref, v2 = b1 != ref;
-            if (v1 != v2) {
-              PUSH_OUT(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
-            } else if (v1 && v2) {
-              PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
-              PUSH_OUT(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
-            }
-            // two non-variant single-base alleles cannot occur (all Match alleles share ref)
-          }
-          }
-        }
-      }
-    }
-    // reserve + write records (wave-aggregated)
-    const unsigned long long base = wave_reserve(&ctr->n_rec, nout);
-    if (nout > 0 && base < rec_cap) recs[base] = out0;
-    if (nout > 1 && base + 1 < rec_cap) recs[base + 1] = out1;
-    const unsigned long long cb = wave_reserve(&ctr->n_complex, to_complex ? 1u : 0u);
-    if (to_complex && cb < cplx_cap) cplx[cb] = ComplexItem{(int32_t)blockIdx.x, L0 + i, wide ? 1 : 0};
-  }
-  // block-level reduction of run counters
-  __shared__ unsigned red[3];
-  if (threadIdx.x < 3) red[threadIdx.x] = 0;
-  __syncthreads();
-  if (visited) atomicAdd(&red[0], visited);
-  if (amb) atomicAdd(&red[1], amb);
-  if (ties) atomicAdd(&red[2], ties);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int sl = blockIdx.x & (kSpread - 1);
-    if (red[0]) atomicAdd(&ctr->spread[0][sl], (unsigned long long)red[0]);
-    if (red[1]) atomicAdd(&ctr->spread[1][sl], (unsigned long long)red[1]);
-    if (red[2]) atomicAdd(&ctr->spread[2][sl], (unsigned long long)red[2]);
-  }
-  if ((ABL & 32) && (threadIdx.x & 63) == 0) {  // per-wave phase clocks
-    const uint64_t pt4 = __builtin_readcyclecounter();
-    atomicAdd(&ctr->prof[0], (unsigned long long)(pt1 - pt0));  // tile load + LDS zero + barrier
-    atomicAdd(&ctr->prof[1], (unsigned long long)(pt2 - pt1));  // this wave's read walk
-    atomicAdd(&ctr->prof[2], (unsigned long long)(pt3 - pt2));  // waiting for the other waves
-    atomicAdd(&ctr->prof[3], (unsigned long long)(pt4 - pt3));  // decision + output
-    atomicAdd(&ctr->prof[4], 1ull);
-  }
-}
+#include "gq_germline_cols.h"
 
 // ------------------------------------------------------------------------------------------
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
@@ -410,16 +229,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(STAGE ? 
 __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
                                                            int threshold, int emit_ref, int emit_no_call,
-                                                           CallRec *__restrict__ recs, unsigned long long rec_cap,
+                                                           CallRec *__restrict__ recs, OutGeom og,
                                                            uint8_t *__restrict__ pool, unsigned long long pool_cap,
-                                                           unsigned long long cplx_cap, Counters *ctr) {
+                                                           Counters *ctr) {
   const int lane = threadIdx.x & 63;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // items beyond the queue's capacity were never written (the host retries with a larger queue)
-  const unsigned long long n_items = ctr->n_complex < cplx_cap ? ctr->n_complex : cplx_cap;
+  // items beyond a partition's capacity were never written (the host retries with larger ones)
+  const unsigned long long n_items = ctr->part_off[1][kParts];
+  const int rpart = kPartsCols + (int)(gwave & (kPartsCols - 1));  // this wave's record partition
   for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
-    const ComplexItem item = items[it];
+    const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
     const int32_t pos = item.pos;
     // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
@@ -644,8 +464,8 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
           rr.allele = off;
         }
         if (lane == 0) {
-          const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
-          if (k < rec_cap) recs[k] = rr;
+          const unsigned long long k = atomicAdd(&ctr->part[0][rpart], 1ull);
+          if (k < og.capB[0]) recs[og.slot(0, rpart, k)] = rr;
         }
       };
       if (npass == 0) {
@@ -798,6 +618,58 @@ static CallsLayout calls_layout(int64_t n, int64_t dev_pool_used) {
   return L;
 }
 
+// Exclusive offsets of the per-partition counts (clamped to the capacity) of one output kind,
+// their total (n_rec / n_complex) and the largest count (part_max); one block of 1024
+// threads, kParts / 1024 partitions each.
+__global__ __launch_bounds__(1024) void part_scan(Counters *ctr, int which, OutGeom og) {
+  constexpr int PER = kParts / 1024;
+  __shared__ unsigned long long s[1024];
+  __shared__ unsigned long long mx;
+  const int t = threadIdx.x;
+  unsigned long long v[PER], sum = 0, m = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const unsigned long long x = ctr->part[which][t * PER + j];
+    const unsigned long long cap = og.cap(which, t * PER + j);
+    m = x > cap && x - cap > m ? x - cap : m;  // largest overflow
+    v[j] = x < cap ? x : cap;
+    sum += v[j];
+  }
+  if (t == 0) mx = 0;
+  s[t] = sum;
+  __syncthreads();
+  if (m) atomicMax(&mx, m);
+  for (int d = 1; d < 1024; d <<= 1) {
+    const unsigned long long y = t >= d ? s[t - d] : 0ull;
+    __syncthreads();
+    s[t] += y;
+    __syncthreads();
+  }
+  unsigned long long o = s[t] - sum;  // exclusive
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    ctr->part_off[which][t * PER + j] = o;
+    o += v[j];
+  }
+  if (t == 1023) {
+    ctr->part_off[which][kParts] = s[t];
+    if (which == 0) ctr->n_rec = s[t];
+    else ctr->n_complex = s[t];
+    ctr->part_max[which] = mx;  // 0: every partition within its capacity
+  }
+}
+
+// Dense (key, slot) pairs of the partitioned records, for the radix sort.
+__global__ void gather_keys(const CallRec *__restrict__ recs, const Counters *__restrict__ ctr, OutGeom og,
+                            int64_t n, uint64_t *__restrict__ keys,
+                            int32_t *__restrict__ slot) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const unsigned long long src = part_slot(ctr->part_off[0], (unsigned long long)k, og, 0);
+  keys[k] = recs[src].key;
+  slot[k] = (int32_t)src;
+}
+
 __global__ void iota_i32(int32_t *__restrict__ v, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) v[i] = (int32_t)i;
@@ -868,7 +740,7 @@ void gq_close(gq_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
                     &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
-                    &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb})
+                    &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -884,7 +756,7 @@ gq_status gq_get_timings(const gq_ctx *c, gq_timings *out) {
 gq_status gq_set_tile(gq_ctx *c, int32_t t) {
   if (!c) return set_err(GQ_E_ARG, "null ctx");
   if (t == 0) t = kGermT;
-  if (t != 512 && t != 768 && t != 1024 && t != 2048) return set_err(GQ_E_ARG, "tile must be 512, 768, 1024 or 2048");
+  if (t != 512) return set_err(GQ_E_ARG, "tile must be 512 (the germline column kernel's geometry)");
   c->germ_tile = t;
   return GQ_OK;
 }
@@ -907,13 +779,38 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   d->owned.push_back(q);
   d->d.lead = (const int16_t *)p;
   d->d.ev_rb = (const uint8_t *)q;
+  int unordered = 0;
   if (d->d.n_reads > 0) {
+    void *flag = nullptr;
+    HIP_TRY(hipMalloc(&flag, sizeof(int)));
+    d->owned.push_back(flag);
+    HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q,
-                       (uint8_t *)cl);
+                       (uint8_t *)cl, (int *)flag);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&unordered, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  }
+  {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds
+    void *cd = nullptr, *ce = nullptr;
+    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(d->d.n_reads, 1) + 1024;
+    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(md_len, 1) + 1024;
+    HIP_TRY(hipMalloc(&cd, ncd));
+    d->owned.push_back(cd);
+    HIP_TRY(hipMalloc(&ce, nce));
+    d->owned.push_back(ce);
+    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
+    HIP_TRY(hipMemsetAsync(ce, 0, nce, c->stream));
+    d->d.cdesc = (const ColDesc *)cd;
+    d->d.cev = (const uint32_t *)ce;
+    if (d->d.n_reads > 0) {
+      const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
+      hipLaunchKernelGGL(col_derive, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (ColDesc *)cd, (uint32_t *)ce);
+      HIP_TRY(hipGetLastError());
+    }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  d->d.pool_ordered = unordered ? 0 : 1;
   return GQ_OK;
 }
 
@@ -949,6 +846,35 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   enum : size_t { pad_contig_read_begin = 0, pad_start = 0, pad_end = 0, pad_pmax_end = 0, pad_mapq = 0, pad_flags = 0,
                   pad_sample = 0, pad_seq_off = 0, pad_seq_len = 0, pad_cigar_off = 0, pad_n_cigar = 0, pad_md_off = 0,
                   pad_n_md = 0, pad_n_mismatch = 0, pad_seq = kSeqPad, pad_qual = 0, pad_cigar = 0, pad_md_ev = 0 };
+  // HBM layout: the sequence / quality pools in read order (each read's bytes after the
+  // previous read's), so a tile's reads are one contiguous byte range for the LDS stage.
+  // A host pool in another order is re-laid out here (the caller's buffers are untouched).
+  gq_reads hh = *h;
+  std::vector<int64_t> off2;
+  std::vector<uint8_t> seq2, qual2;
+  {
+    bool ordered = true;
+    for (int64_t r = 1; r < n && ordered; ++r) ordered = h->seq_off[r] >= h->seq_off[r - 1] + h->seq_len[r - 1];
+    if (!ordered) {
+      off2.resize((size_t)n);
+      int64_t o = 0;
+      for (int64_t r = 0; r < n; ++r) {
+        off2[(size_t)r] = o;
+        o += h->seq_len[r];
+      }
+      seq2.resize((size_t)std::max<int64_t>(o, 1));
+      qual2.resize((size_t)std::max<int64_t>(o, 1));
+      for (int64_t r = 0; r < n; ++r) {
+        memcpy(seq2.data() + off2[(size_t)r], h->seq + h->seq_off[r], (size_t)h->seq_len[r]);
+        if (h->qual) memcpy(qual2.data() + off2[(size_t)r], h->qual + h->seq_off[r], (size_t)h->seq_len[r]);
+      }
+      hh.seq_off = off2.data();
+      hh.seq = seq2.data();
+      hh.qual = h->qual ? qual2.data() : nullptr;
+      hh.seq_bytes = o;
+    }
+  }
+  h = &hh;
   UP(contig_read_begin, h->n_contigs + 1, int64_t);
   UP(start, n, int32_t);
   UP(end, n, int32_t);
@@ -1039,7 +965,8 @@ void gq_reads_free(gq_dev_reads *d) {
 }  // extern "C"
 
 // ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
-gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles_buf) {
+gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles_buf,
+                   int stage_cap, int meta_cap, int ev_cap) {
   if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
   const int64_t R = loci->n_ranges;
   std::vector<int32_t> rc;
@@ -1077,7 +1004,7 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   HIP_TRY(tiles_buf.ensure((size_t)tiles * sizeof(Tile)));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
-                     tiles, T, rd->d, (Tile *)tiles_buf.p);
+                     tiles, T, rd->d, (Tile *)tiles_buf.p, stage_cap, meta_cap, ev_cap);
   HIP_TRY(hipGetLastError());
   return GQ_OK;
 }
@@ -1095,69 +1022,27 @@ gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
 
 extern "C" {
 
-extern "C++" template <int T>
-static void launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p, CallRec *recs,
-                            unsigned long long rec_cap, ComplexItem *cplx, unsigned long long cplx_cap,
-                            Counters *ctr) {
-  static const int abl = getenv("GQ_ABLATE") ? atoi(getenv("GQ_ABLATE")) : 0;
-  static const int stg = getenv("GQ_STAGE") ? atoi(getenv("GQ_STAGE")) : 0;
-  static const int v2 = getenv("GQ_V2") ? atoi(getenv("GQ_V2")) : 0;
-  static const int abl2 = getenv("GQ_V2ABL") ? atoi(getenv("GQ_V2ABL")) : 0;
-  if (abl2) {  // diagnostic ablations of the locus-major kernel (results are wrong)
-#define GQ_V2A(A)                                                                                                  \
-  hipLaunchKernelGGL((germline_tile_v2<T / 256, A>), dim3((unsigned)tiles), dim3(T / 4), 0, c->stream,              \
-                     (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, \
-                     cplx_cap, ctr)
-    switch (abl2) {
-      case 1: GQ_V2A(1); break;
-      case 2: GQ_V2A(2); break;
-      case 4: GQ_V2A(4); break;
-      case 7: GQ_V2A(7); break;
-      default: GQ_V2A(0); break;
-    }
-#undef GQ_V2A
-    return;
-  }
-  if (v2 && !abl && !stg) {  // locus-major kernel (experimental: more VALU per element than v1)
-    hipLaunchKernelGGL((germline_tile_v2<T / 256>), dim3((unsigned)tiles), dim3(T / 4), 0, c->stream,
-                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
-                       cplx_cap, ctr);
-    return;
-  }
-  if (stg == 2) {  // smaller stage (for T = 512 / 768 tiles)
-    hipLaunchKernelGGL((germline_tile<T, 0, 24 * 1024>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
-                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
-                       cplx_cap, ctr);
-    return;
-  }
-  if (stg) {
-    hipLaunchKernelGGL((germline_tile<T, 0, kStageBytes>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
-                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
-                       cplx_cap, ctr);
-    return;
-  }
-  static const int chunked = getenv("GQ_CHUNKED") ? atoi(getenv("GQ_CHUNKED")) : 0;
-  if (chunked) {  // chunk-major walk (experimental: coalesced loads, more VALU per element)
-    hipLaunchKernelGGL((germline_tile<T, 0, 0, 1>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,
-                       (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx,
-                       cplx_cap, ctr);
-    return;
-  }
-#define GQ_LAUNCH(A)                                                                                             \
-  hipLaunchKernelGGL((germline_tile<T, A>), dim3((unsigned)tiles), dim3(kBlock), 0, c->stream,                   \
-                     (const Tile *)c->tiles.p, R, p->threshold, p->emit_ref, p->emit_no_call, recs, rec_cap, cplx, \
-                     cplx_cap, ctr)
-  switch (abl) {
-    case 1: GQ_LAUNCH(1); break;
-    case 2: GQ_LAUNCH(2); break;
-    case 4: GQ_LAUNCH(4); break;
-    case 8: GQ_LAUNCH(8); break;
-    case 12: GQ_LAUNCH(12); break;
-    case 14: GQ_LAUNCH(14); break;
-    case 32: GQ_LAUNCH(32); break;
-    default: GQ_LAUNCH(0); break;
-  }
-#undef GQ_LAUNCH
+static unsigned germline_grid(gq_ctx *c, int64_t tiles) {
+  if (c->n_cu <= 0 && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+    c->n_cu = 256;
+  // persistent: two workgroups per CU (LDS-bound), each over a contiguous run of tiles
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>({tiles, 2 * (int64_t)c->n_cu, (int64_t)kPartsCols}));
+}
+
+static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p,
+                                 CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr) {
+  static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
+  HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
+  hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,
+                     (const Tile *)c->tiles.p, tiles, R, p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og,
+                     ctr, (int32_t *)c->slow.p, dbg);
+  HIP_TRY(hipGetLastError());
+  const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
+  hipLaunchKernelGGL((germline_walk<ColsCfg::kT>), dim3(wblocks), dim3(kBlock), 0, c->stream,
+                     (const Tile *)c->tiles.p, (const int32_t *)c->slow.p, R, p->threshold, p->emit_ref,
+                     p->emit_no_call, recs, cplx, og, ctr);
+  HIP_TRY(hipGetLastError());
+  return GQ_OK;
 }
 
 gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,
@@ -1169,7 +1054,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = plan(c, rd, loci, T, pl, c->tiles);
+  gq_status st = plan(c, rd, loci, T, pl, c->tiles, ColsCfg::kStage, ColsCfg::kMeta, ColsCfg::kEv);
   if (st) return st;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
@@ -1179,44 +1064,50 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
     return GQ_OK;
   }
   const int ns = rd->d.n_samples;
-  unsigned long long rec_cap = (p->emit_ref || p->emit_no_call) ? (unsigned long long)(2 * ns) * pl.n_loci + 1024
-                                                                 : std::max<unsigned long long>(1 << 16, pl.n_loci / 8);
-  unsigned long long cplx_cap = std::max<unsigned long long>(1 << 16, pl.n_loci / 8);
+  // output partitions: per germline_cols workgroup (capA, its share of the loci) and per
+  // walker / complex-kernel wave (capB); grown on overflow
+  OutGeom og{};
+  og.ncols = (int)germline_grid(c, pl.n_tiles);
+  const bool dense = p->emit_ref || p->emit_no_call;
+  const unsigned long long wg_loci = (unsigned long long)((pl.n_tiles + og.ncols - 1) / og.ncols) * T;
+  og.capA[0] = dense ? 2ull * ns * wg_loci + 64 : wg_loci / 32 + 256;
+  og.capA[1] = wg_loci / 32 + 256;
+  og.capB[0] = dense ? 2ull * ns * (unsigned long long)pl.n_loci / 8192 + 256 : (unsigned long long)pl.n_loci / 16384 + 256;
+  og.capB[1] = (unsigned long long)pl.n_loci / 16384 + 256;
   unsigned long long pool_cap = 1 << 22;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
-    HIP_TRY(c->recs.ensure(rec_cap * sizeof(CallRec)));
-    HIP_TRY(c->cplx.ensure(cplx_cap * sizeof(ComplexItem)));
+    HIP_TRY(c->recs.ensure(og.total(0) * sizeof(CallRec)));
+    HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
     HIP_TRY(c->pool.ensure(pool_cap));
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     if (attempt == 0) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    switch (T) {
-      case 512: launch_germline<512>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
-      case 768: launch_germline<768>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
-      case 2048: launch_germline<2048>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
-      default: launch_germline<1024>(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, rec_cap, (ComplexItem *)c->cplx.p, cplx_cap, ctr); break;
+    st = launch_germline(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, (ComplexItem *)c->cplx.p, og, ctr);
+    if (st) {
+      free(res);
+      return st;
     }
-    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), 4096);
+    hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 1, og);
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                       (CallRec *)c->recs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cplx_cap, ctr);
+                       (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr);
     HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     bool retry = false;
-    if (hc.n_complex > cplx_cap) {
-      cplx_cap = hc.n_complex + 1024;
-      retry = true;
-    }
-    if (hc.n_rec > rec_cap) {
-      rec_cap = hc.n_rec + 1024;
-      retry = true;
-    }
+    // part_max = the largest overflow of a partition: grow both capacities by it
+    for (int w = 0; w < 2; ++w)
+      if (hc.part_max[w]) {
+        og.capA[w] += hc.part_max[w] + 64;
+        og.capB[w] += hc.part_max[w] + 64;
+        retry = true;
+      }
     if (hc.pool_used > pool_cap) {
       pool_cap = hc.pool_used + 4096;
       retry = true;
@@ -1227,10 +1118,10 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
       return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
     }
   }
-  if (getenv("GQ_PROF") && hc.prof[4])
-    fprintf(stderr, "gq prof (cycles/wave): setup %.0f walk %.0f wait %.0f decide %.0f  (waves %llu)\n",
-            (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4], (double)hc.prof[2] / hc.prof[4],
-            (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
+  if (getenv("GQ_DBG") && hc.prof[7])
+    fprintf(stderr, "gq prof (cycles/tile/wave): tile %.0f scan+column %.0f per-read %.0f decide %.0f (%llu)\n",
+            (double)hc.prof[0] / hc.prof[7], (double)hc.prof[1] / hc.prof[7], (double)hc.prof[2] / hc.prof[7],
+            (double)hc.prof[3] / hc.prof[7], hc.prof[7]);
   for (int k = 0; k < kSpread; ++k) {
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];
@@ -1253,10 +1144,9 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   HIP_TRY(c->image.ensure(lay.bytes));
   if (n > 0) {
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
-    // keys are the first 8 bytes of each record: strided copy into a dense key array
-    HIP_TRY(hipMemcpy2DAsync(c->keys.p, 8, c->recs.p, sizeof(CallRec), 8, (size_t)n, hipMemcpyDeviceToDevice,
-                             c->stream));
-    hipLaunchKernelGGL(iota_i32, dim3(nb), dim3(kBlock), 0, c->stream, (int32_t *)c->idx.p, n);
+    // keys and record slots of the partitioned records, densely
+    hipLaunchKernelGGL(gather_keys, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const Counters *)c->counters.p, og, n, (uint64_t *)c->keys.p, (int32_t *)c->idx.p);
     HIP_TRY(hipGetLastError());
     int end_bit = 12;
     while (end_bit < 64 && ((uint64_t)pl.n_loci >> (end_bit - 12)) != 0) ++end_bit;
