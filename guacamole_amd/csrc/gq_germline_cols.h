@@ -229,7 +229,8 @@ struct ColsCfg {
   static constexpr int kLanesPerCol = kThreads / (kT / 4);  // rows of a column split over 4 lanes
   static constexpr int kStage = 24 * 1024;  // sequence bytes (1 KiB DMA pieces)
   static constexpr int kMeta = 256;         // reads (ColDesc rows, one per thread)
-  static constexpr int kEv = 512;           // MD events
+  static constexpr int kEv = 512;           // auxiliary words (MD events, segments of general reads)
+  static constexpr int kExtra = 64;         // column rows of general reads' count segments
   // one buffer: stage | rows (+16 B alignment, +256 B dword-DMA tail) | events (same)
   static constexpr int kRowsOff = kStage + 16;  // + 16 zero bytes after the stage (kZero)
   static constexpr int kEvOff = kRowsOff + kMeta * 24 + 16 + 256;
@@ -271,6 +272,8 @@ __device__ __forceinline__ void dma_range(const uint8_t *g, uint8_t *l, int n, i
   }
 }
 
+constexpr uint32_t kSegCountK = 0;  // segment kinds of the auxiliary list (col_derive): count / complex
+
 // germline_cols: persistent workgroups, each over a contiguous run of tiles (XCD-local
 // neighbours: reads straddling two tiles are re-read from L2).  Per tile:
 //   A  wait for this tile's DMA (issued one tile earlier), then DMA the next tile
@@ -296,6 +299,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   __shared__ __attribute__((aligned(16))) uint8_t buf[2][C::kBuf];
   __shared__ uint32_t hist[NCOL];  // per column bucket: rows starting (lo 16) / prefix-max end reaching (hi 16)
   __shared__ uint32_t crng[NCOL];  // per column: lo << 16 | hi (its row range)
+  __shared__ __attribute__((aligned(8))) uint2 xrow[C::kExtra];  // rows of general reads' count segments
+  __shared__ unsigned n_xrow;
   __shared__ unsigned outn[2];  // records / complex items of this workgroup's partition
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -321,6 +326,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     if (t < NCOL) hist[t] = 0;
     if (t < 2) *reinterpret_cast<uint4 *>(buf[t] + C::kStage) = make_uint4(0u, 0u, 0u, 0u);
     if (t < 2) outn[t] = 0;
+    if (t == 0) n_xrow = 0;
   }
   LdsOut out{outn, {og.slot(0, (int)blockIdx.x, 0), og.slot(1, (int)blockIdx.x, 0)}, {og.capA[0], og.capA[1]}};
   unsigned visited = 0, amb = 0, ties = 0;
@@ -350,8 +356,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const uint32_t sb_lo = (uint32_t)(uint64_t)tl.sb0, mb_lo = (uint32_t)(uint64_t)tl.mb0;
     // ---- B: rows (thread per read) and buckets
     int not_col = tl.sbytes <= 0;
-    int32_t my_s = 0, my_e = 0, my_base = 0;
-    bool mine = false;
+    int32_t my_s = 0, my_e = 0, my_base = 0, my_seg = 0, my_nseg = 0;
+    bool mine = false, general = false;
     if (!not_col && t < nch) {
       const uint32_t *d = rows + 6 * t;
       const int32_t s = (int32_t)d[0], e = (int32_t)d[1], pe = (int32_t)d[2];
@@ -362,9 +368,33 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const int32_t nmd = (int32_t)(info & 0xFFFFu);
       uint32_t rx = (uint32_t)kNever, ry = 0;
       if (e > L0 && s < L1) {
-        const bool ok = (info & kColEligible) && sa + (uint32_t)(e - s) <= (uint32_t)tl.sbytes &&
-                        ea + (uint32_t)nmd <= (uint32_t)tl.mcnt;
-        if (!ok) {
+        const uint32_t nseg = (info >> 18) & 0xFFu;
+        const bool evs_in = ea + (uint32_t)nmd + 2u * nseg <= (uint32_t)tl.mcnt;
+        const bool ok = (info & kColEligible) && sa + (uint32_t)(e - s) <= (uint32_t)tl.sbytes && evs_in;
+        const bool gen = (info & kColGeneral) && evs_in;
+        if (gen) {  // its count segments become extra column rows
+          general = true;
+          mine = true;
+          my_s = srel;
+          my_base = (int32_t)sa;
+          my_seg = (int32_t)(ea + (uint32_t)nmd);
+          my_nseg = (int32_t)nseg;
+          for (uint32_t q = 0; q < nseg; ++q) {
+            const uint32_t w0 = evs[ea + nmd + 2 * q], w1 = evs[ea + nmd + 2 * q + 1];
+            if ((w1 >> 16) != kSegCountK) continue;
+            const int32_t a = srel + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
+            const uint32_t so = sa + (w1 & 0xFFFFu);  // stage address of the segment's first base
+            if (so + (uint32_t)(b - a) > (uint32_t)tl.sbytes) not_col = 1;
+            if (b <= 0 || a >= L1 - L0) continue;
+            const unsigned x = atomicAdd(&n_xrow, 1u);
+            if (x >= (unsigned)C::kExtra) {
+              not_col = 1;
+              continue;
+            }
+            const int32_t sc = a > -4 ? a : -4, ec = b < T + 4 ? b : T + 4;
+            xrow[x] = make_uint2((uint32_t)((sc & 0xFFFF) | (ec << 16)), so - (uint32_t)a);
+          }
+        } else if (!ok) {
           not_col = 1;
         } else {
           const int32_t sc = srel > -4 ? srel : -4, ec = erel < T + 4 ? erel : T + 4;
@@ -389,6 +419,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     if (__syncthreads_or(not_col)) {  // uniform: the tile goes to the walker kernel
       if (t < NCOL) hist[t] = 0;
       if (t == 0) {
+        n_xrow = 0;
         const unsigned long long k = atomicAdd(&ctr->n_slow, 1ull);
         slow[k] = (int32_t)tid_tile;
       }
@@ -415,42 +446,45 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     constexpr int P = C::kLanesPerCol, U = 8;
     const int c = 4 * col;
     ColCounts cc;
-    if (!(dbg & 1)) {
-      for (int k0 = lo + par; k0 < hi; k0 += P * U) {
-        uint2 m[U];
+    // rows k0, k0 + P, ... (< kend) of a row table (uint2 {rx, ry} at word stride ws)
+    auto batch = [&](const uint32_t *tab, int ws, int k0, int kend) {
+      uint2 m[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          m[u] = *reinterpret_cast<const uint2 *>(rows + 6 * min(k0 + P * u, hi - 1) + 2);
-        uint32_t a[U];
-        uint32_t nf = 0;
+      for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(tab + ws * min(k0 + P * u, kend - 1));
+      uint32_t a[U];
+      uint32_t nf = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu), e = (int32_t)m[u].x >> 16;
-          const bool full = k0 + P * u < hi && s <= c && e >= c + 4;
-          a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 8 zero bytes
-          nf += full ? 1u : 0u;
-        }
-        uint32_t w0[U], w1[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          w0[u] = st32[a[u] >> 2];
-          w1[u] = st32[(a[u] >> 2) + 1];
-        }
-        uint32_t n_ac = 0, n_tg = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t w = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]);
-          const uint32_t sel = w & 0x07070707u;  // A 1, C 3, T 4, N 6, G 7 (0 for the zero dword)
-          n_ac += __builtin_amdgcn_perm(0u, 0x10000100u, sel);
-          n_tg += __builtin_amdgcn_perm(0x10000001u, 0u, sel);
-        }
-        if (cc.nf8 + nf > 255) cc.flush(cnt, S, c);
-        cc.ca += n_ac & 0x0F0F0F0Fu;
-        cc.cc += (n_ac >> 4) & 0x0F0F0F0Fu;
-        cc.ct += n_tg & 0x0F0F0F0Fu;
-        cc.cg += (n_tg >> 4) & 0x0F0F0F0Fu;
-        cc.nf8 += nf;
+      for (int u = 0; u < U; ++u) {
+        const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu), e = (int32_t)m[u].x >> 16;
+        const bool full = k0 + P * u < kend && s <= c && e >= c + 4;
+        a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 8 zero bytes
+        nf += full ? 1u : 0u;
       }
+      uint32_t w0[U], w1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        w0[u] = st32[a[u] >> 2];
+        w1[u] = st32[(a[u] >> 2) + 1];
+      }
+      uint32_t n_ac = 0, n_tg = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t w = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]);
+        const uint32_t sel = w & 0x07070707u;  // A 1, C 3, T 4, N 6, G 7 (0 for the zero dword)
+        n_ac += __builtin_amdgcn_perm(0u, 0x10000100u, sel);
+        n_tg += __builtin_amdgcn_perm(0x10000001u, 0u, sel);
+      }
+      if (cc.nf8 + nf > 255) cc.flush(cnt, S, c);
+      cc.ca += n_ac & 0x0F0F0F0Fu;
+      cc.cc += (n_ac >> 4) & 0x0F0F0F0Fu;
+      cc.ct += n_tg & 0x0F0F0F0Fu;
+      cc.cg += (n_tg >> 4) & 0x0F0F0F0Fu;
+      cc.nf8 += nf;
+    };
+    if (!(dbg & 1)) {
+      for (int k0 = lo + par; k0 < hi; k0 += P * U) batch(rows + 2, 6, k0, hi);
+      const int nx = (int)min(n_xrow, (unsigned)C::kExtra);
+      for (int k0 = par; k0 < nx; k0 += P * U) batch(reinterpret_cast<const uint32_t *>(xrow), 2, k0, nx);
     }
     {  // quad sums of the column's four lanes (bytes cannot overflow while the reads sum to <= 255)
       auto qsum = [](uint32_t x) {
@@ -474,11 +508,11 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     //      read t - 256 (into the LDS histogram, GermSink)
     if (!(dbg & 2)) {
       GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-      if (mine) {
-        const int32_t s = my_s, e = my_e;
+      // the <= 3 + 3 bytes of the two partial columns of a row over tile loci [s, e) whose
+      // base at tile locus l sits at stage address base + l: both dwords loaded, one atomic per byte
+      auto edges = [&](int32_t s, int32_t e, uint32_t base) {
         const int32_t cs = s & ~3, ce = (e - 1) & ~3;
         const bool ps = s != cs || e < cs + 4, pe = (e & 3) != 0 || s > ce;
-        // the <= 3 + 3 bytes of the two partial columns: both dwords loaded, then one atomic per byte
         int32_t ea0 = s, ea1 = e < cs + 4 ? e : cs + 4;  // first partial column's loci
         int32_t eb0 = ce, eb1 = e;                       // last partial column's loci
         if (!ps) ea1 = ea0;
@@ -487,12 +521,26 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         ea1 = ea1 < T ? ea1 : T;
         eb0 = eb0 > 0 ? eb0 : 0;
         eb1 = eb1 < T ? eb1 : T;
-        const uint32_t pa = (uint32_t)my_base + (uint32_t)ea0, pb = (uint32_t)my_base + (uint32_t)eb0;
+        const uint32_t pa = base + (uint32_t)ea0, pb = base + (uint32_t)eb0;
         const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1];
         const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1];
         const uint32_t wa = __builtin_amdgcn_alignbyte(wa1, wa0, pa), wb = __builtin_amdgcn_alignbyte(wb1, wb0, pb);
         for (int32_t l = ea0; l < ea1; ++l) sink.bases4_clean(l, (wa >> (8 * (l - ea0))) & 0xFFu, 1u, 0);
         for (int32_t l = eb0; l < eb1; ++l) sink.bases4_clean(l, (wb >> (8 * (l - eb0))) & 0xFFu, 1u, 0);
+      };
+      if (general) {  // segments: ends of the count segments, complex loci
+        for (int32_t q = 0; q < my_nseg; ++q) {
+          const uint32_t w0 = evs[my_seg + 2 * q], w1 = evs[my_seg + 2 * q + 1];
+          const int32_t a = my_s + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
+          if (b <= 0 || a >= T) continue;
+          if ((w1 >> 16) == kSegCountK) {
+            edges(a, b, (uint32_t)my_base + (w1 & 0xFFFFu) - (uint32_t)a);
+          } else {
+            for (int32_t l = a > 0 ? a : 0; l < (b < T ? b : T); ++l) sink.complex_i(l);
+          }
+        }
+      } else if (mine) {
+        edges(my_s, my_e, (uint32_t)my_base);
       }
       const int k = t - C::kMeta;
       if (k >= 0 && k < nch) {
@@ -516,6 +564,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       }
     }
     __syncthreads();  // histogram complete
+    if (t == 0) n_xrow = 0;  // the next tile's row-build follows this tile's barriers
     const uint64_t tf = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- F: decision, then the histogram words are zeroed for the next tile
     if (!(dbg & 4))

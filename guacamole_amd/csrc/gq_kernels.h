@@ -49,19 +49,23 @@ struct DevReads {
   int32_t pool_ordered;  // reads' sequence bytes are disjoint and in read order in the pool
   // derived at upload for the germline column kernel (LDS-DMA'd per tile, see ColDesc)
   const struct ColDesc *cdesc;  // one per read
-  const uint32_t *cev;          // one per MD event: offset << 16 | MD base << 8 | read base
+  const uint32_t *cev;          // per read: MD events (offset << 16 | MD base << 8 | read base), segments
+  const int64_t *caux_off;      // n_reads + 1 offsets into cev
 };
 
 // Packed per-read record of the germline column kernel (24 bytes, DMA'd into LDS per tile).
 struct ColDesc {
   int32_t start, end, pmax_end;
-  uint32_t info;    // bits 0-15 n_md, bit 16: column-eligible (single (M|=|X) block, A/C/G/T/N bases,
-                    // MD present, span < 32768, n_md < 65536)
-  uint32_t seq_lo;  // low 32 bits of the pool offset of the base at `start` (seq_off + leading clip)
-  uint32_t md_lo;   // low 32 bits of md_off
+  uint32_t info;    // bits 0-15 n_md; bit 16 column-eligible: a single (M|=|X) block, A/C/G/T/N
+                    // bases, MD present, span < 32768, n_md < 65536; bit 17 general: another CIGAR
+                    // as segments (validated at upload), their number in bits 18-25
+  uint32_t seq_lo;  // low 32 bits of the pool offset of the base at `start` (seq_off + leading clip;
+                    // seq_off for a general read)
+  uint32_t md_lo;   // low 32 bits of the read's offset in the auxiliary list (cev)
 };
 static_assert(sizeof(ColDesc) == 24, "ColDesc layout");
 constexpr uint32_t kColEligible = 1u << 16;
+constexpr uint32_t kColGeneral = 1u << 17;
 
 // One locus tile: contiguous loci [L0, L1) of one contig, plus the index range
 // [rb, re) of reads that can overlap it (pmax_end > L0, start < L1).
@@ -71,8 +75,8 @@ struct Tile {
   int32_t contig, L0, L1, range;
   int64_t sb0;     // germline column kernel: 16-aligned pool offset of the tile's sequence bytes
   int32_t sbytes;  // bytes to stage from sb0 when the whole read window fits one LDS stage, else 0
-  int32_t mcnt;    // MD events to stage from mb0
-  int64_t mb0;     // first MD event index to stage (a multiple of 4)
+  int32_t mcnt;    // auxiliary-list words (MD events, segments) to stage from mb0
+  int64_t mb0;     // first auxiliary word to stage (a multiple of 4)
 };
 static_assert(sizeof(Tile) == 64, "Tile layout");
 
@@ -423,6 +427,9 @@ struct GermSink {
   __device__ __forceinline__ void elem(int32_t l, int kind, uint8_t base, uint8_t mdb, bool ev, uint8_t fl) {
     elem_i(l - L0, kind, base, mdb, ev, fl);
   }
+  // a complex element (insertion / deletion anchor, mid-deletion) at tile index i; its locus
+  // is decided by the exact kernel, so no reference-base bit is needed
+  __device__ __forceinline__ void complex_i(int i) { atomicAdd(at(W_OX, i), 1u << 16); }
   // Clipped elements (CIGAR N) at tile indices [i0, i1): complex, MD-derived reference 'N'
   __device__ __forceinline__ void clip_run(int i0, int i1, uint8_t) {
     for (int i = i0; i < i1; ++i) atomicAdd(at(W_OX, i), 1u << 16);

@@ -106,8 +106,8 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   if (stage_cap > 0 && a0 > rb && a0 - rb <= meta_cap) {
     const int64_t B0 = R.seq_off[rb] & ~(int64_t)15;
     const int64_t nb = R.seq_off[a0 - 1] + R.seq_len[a0 - 1] - B0;
-    const int64_t M0 = R.md_off[rb] & ~(int64_t)3;
-    const int64_t nm = R.md_off[a0 - 1] + (R.n_md[a0 - 1] > 0 ? R.n_md[a0 - 1] : 0) - M0;
+    const int64_t M0 = R.caux_off[rb] & ~(int64_t)3;
+    const int64_t nm = R.caux_off[a0] - M0;
     if (nb > 0 && ((nb + 1023) >> 10) * 1024 <= stage_cap && B0 + ((nb + 1023) >> 10) * 1024 <= R.seq_cap &&
         nm >= 0 && nm <= ev_cap) {
       tl.sb0 = B0;
@@ -119,25 +119,110 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   tiles[t] = tl;
 }
 
-// Column-kernel records (derived once at upload, after read_shape): the packed ColDesc of
-// each read and one u32 per MD event (offset << 16 | MD base << 8 | read base).
-__global__ void col_derive(DevReads R, ColDesc *__restrict__ cd, uint32_t *__restrict__ cev) {
+// Column-kernel records (derived once at upload, after read_shape).  A general-CIGAR read
+// (not a single (M|=|X) block) becomes segments for the in-kernel path, PileupElement's rules
+// (PileupElement.scala:68-248, as walk_read_lane) over the whole read:
+//   count   loci [ref_off, ref_off + len) are Match/Mismatch elements whose bases start at
+//           sequence offset seq_off;
+//   complex loci [ref_off, ref_off + len) hold an insertion / deletion anchor, mid-deletions
+//           or clipped (N) elements: the exact kernel decides them.
+// Returns false if the in-kernel path cannot take the read (P op, M bases past the sequence,
+// a deleted locus without its MD base, sizes beyond the packed fields): such reads keep the
+// exact walker, which raises the reference's error where it applies.
+constexpr uint32_t kSegCount = 0, kSegComplex = 1;
+template <class Emit>
+__device__ bool general_segments(const DevReads &R, int64_t r, Emit emit) {
+  const int32_t s = R.start[r], nmd = R.n_md[r], slen = R.seq_len[r], ncig = R.n_cigar[r];
+  if (ncig < 1 || ncig > 32 || slen >= 16384) return false;
+  const uint32_t *cg = R.cigar + R.cigar_off[r];
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  int32_t ref = 0, rpos = 0, k = 0, nseg = 0;
+  bool lead_ins = false, seen_ref = false;
+  for (int32_t q = 0; q < ncig; ++q) {
+    const int op = (int)(cg[q] & 15u);
+    const int32_t len = (int32_t)(cg[q] >> 4);
+    const int nextop = q + 1 < ncig ? (int)(cg[q + 1] & 15u) : -1;
+    if (op == OP_P || op > OP_X) return false;
+    if (op == OP_I && !seen_ref && s == 0) lead_ins = true;
+    if (consumes_ref(op)) {
+      seen_ref = true;
+      const int32_t ra = ref, rb = ref + len;
+      if (op == OP_M || op == OP_EQ || op == OP_X) {
+        if (rpos + len > slen) return false;
+        const bool first_ins = lead_ins && s + ra == 0;
+        const bool anchor = ((op == OP_M || op == OP_EQ) && nextop == OP_I) || nextop == OP_D;
+        const int32_t lo = first_ins ? ra + 1 : ra, hi = anchor ? rb - 1 : rb;
+        if (hi > lo) emit(kSegCount, lo, hi - lo, rpos + (lo - ra), nseg++);
+        if (first_ins) emit(kSegComplex, ra, 1, 0, nseg++);
+        if (anchor && !(first_ins && rb - 1 == ra)) emit(kSegComplex, rb - 1, 1, 0, nseg++);
+      } else {
+        if (op == OP_D)
+          for (int32_t l = ra; l < rb; ++l) {
+            while (k < nmd && (int32_t)(ev[k] >> 8) < l) ++k;
+            if (k >= nmd || (int32_t)(ev[k] >> 8) != l) return false;
+          }
+        emit(kSegComplex, ra, len, 0, nseg++);
+      }
+      ref += len;
+    }
+    if (consumes_read(op)) rpos += len;
+  }
+  return nseg <= 255;
+}
+
+__device__ __forceinline__ bool col_base_ok(const DevReads &R, int64_t r) {
+  const int32_t s = R.start[r], e = R.end[r], nmd = R.n_md[r];
+  return R.clean[r] && nmd >= 0 && nmd < 65536 && e - s < 32768 && e > s;
+}
+
+// Words of each read's auxiliary list (MD events, then two per segment of a general read).
+__global__ void col_count(DevReads R, int64_t *__restrict__ n_aux) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R.n_reads) return;
+  if (r == R.n_reads) {
+    n_aux[r] = 0;
+    return;
+  }
+  int32_t nseg = 0;
+  if (R.lead[r] < 0 && col_base_ok(R, r) &&
+      !general_segments(R, r, [&](uint32_t, int32_t, int32_t, int32_t, int32_t) { ++nseg; }))
+    nseg = 0;
+  n_aux[r] = (int64_t)(R.n_md[r] > 0 ? R.n_md[r] : 0) + 2 * nseg;
+}
+
+// The packed ColDesc of each read and its auxiliary list at aux_off[r]: one u32 per MD event
+// (offset << 16 | MD base << 8 | read base), then per segment (ref_off | len << 16,
+// seq_off | kind << 16).
+__global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColDesc *__restrict__ cd,
+                           uint32_t *__restrict__ aux) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
   const int32_t s = R.start[r], e = R.end[r], nmd = R.n_md[r], lead = R.lead[r];
-  const bool ok = lead >= 0 && R.clean[r] && nmd >= 0 && nmd < 65536 && e - s < 32768 && e > s;
+  const bool base_ok = col_base_ok(R, r);
+  const bool ok = lead >= 0 && base_ok;
+  uint32_t *o = aux + aux_off[r];
+  const int32_t nev = nmd > 0 ? nmd : 0;
+  int32_t nseg = 0;
+  bool gen = false;
+  if (lead < 0 && base_ok && aux_off[r + 1] - aux_off[r] > nev) {  // col_count found segments
+    gen = general_segments(R, r, [&](uint32_t kind, int32_t ref_off, int32_t len, int32_t seq_off, int32_t q) {
+      o[nev + 2 * q] = (uint32_t)ref_off | ((uint32_t)len << 16);
+      o[nev + 2 * q + 1] = (uint32_t)seq_off | (kind << 16);
+      nseg = q + 1;
+    });
+  }
   ColDesc d;
   d.start = s;
   d.end = e;
   d.pmax_end = R.pmax_end[r];
-  d.info = (uint32_t)(nmd > 0 ? (nmd < 65536 ? nmd : 65535) : 0) | (ok ? kColEligible : 0u);
+  d.info = (uint32_t)(nmd > 0 ? (nmd < 65536 ? nmd : 65535) : 0) | (ok ? kColEligible : 0u) |
+           (gen ? kColGeneral | ((uint32_t)nseg << 18) : 0u);
   d.seq_lo = (uint32_t)(uint64_t)(R.seq_off[r] + (lead > 0 ? lead : 0));
-  d.md_lo = (uint32_t)(uint64_t)R.md_off[r];
+  d.md_lo = (uint32_t)(uint64_t)aux_off[r];
   cd[r] = d;
   if (nmd > 0) {
     const uint32_t *ev = R.md_ev + R.md_off[r];
     const uint8_t *rb = R.ev_rb + R.md_off[r];
-    uint32_t *o = cev + R.md_off[r];
     for (int32_t k = 0; k < nmd; ++k) {
       const uint32_t off = ev[k] >> 8;
       o[k] = off < 32768u ? (off << 16) | ((ev[k] & 0xFFu) << 8) | rb[k] : 0xFFFFFFFFu;
@@ -792,20 +877,37 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     HIP_TRY(hipMemcpyAsync(&unordered, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   }
   {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds
-    void *cd = nullptr, *ce = nullptr;
-    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(d->d.n_reads, 1) + 1024;
-    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(md_len, 1) + 1024;
+    const int64_t n = d->d.n_reads;
+    void *cd = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr, *tmp = nullptr;
+    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
     HIP_TRY(hipMalloc(&cd, ncd));
     d->owned.push_back(cd);
+    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
+    HIP_TRY(hipMalloc(&ao, sizeof(int64_t) * (size_t)(n + 1)));
+    d->owned.push_back(ao);
+    HIP_TRY(hipMalloc(&na, sizeof(int64_t) * (size_t)(n + 1)));
+    const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int64_t *)na);
+    HIP_TRY(hipGetLastError());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    int64_t aux_len = 0;
+    HIP_TRY(hipMemcpyAsync(&aux_len, (int64_t *)ao + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(tmp);
+    (void)hipFree(na);
+    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_len, 1) + 1024;
     HIP_TRY(hipMalloc(&ce, nce));
     d->owned.push_back(ce);
-    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
     HIP_TRY(hipMemsetAsync(ce, 0, nce, c->stream));
     d->d.cdesc = (const ColDesc *)cd;
     d->d.cev = (const uint32_t *)ce;
-    if (d->d.n_reads > 0) {
-      const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
-      hipLaunchKernelGGL(col_derive, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (ColDesc *)cd, (uint32_t *)ce);
+    d->d.caux_off = (const int64_t *)ao;
+    if (n > 0) {
+      hipLaunchKernelGGL(col_derive, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (const int64_t *)ao, (ColDesc *)cd, (uint32_t *)ce);
       HIP_TRY(hipGetLastError());
     }
   }
