@@ -62,12 +62,15 @@ struct GlobalOut {  // germline_walk: a partition per wave, counters in device m
 
 template <int T, class Out>
 __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile &tl, int64_t tile_id, bool wide,
-                                                const DevReads &R, int threshold, int emit_ref, int emit_no_call,
+                                                int n_samples, int threshold, int emit_ref, int emit_no_call,
                                                 CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx,
-                                                Out &out, unsigned &visited, unsigned &amb, unsigned &ties) {
+                                                Out &out, unsigned &visited, unsigned &amb, unsigned &ties,
+                                                const uint32_t *reg = nullptr) {
+  // reg (germline_cols, one locus per thread): this thread's locus's A C T G N counts held in
+  // registers, added to the LDS words
   constexpr int S = T + 2 * kGuard;
   const int32_t L0 = tl.L0;
-  const bool multi_sample = R.n_samples > 1;
+  const bool multi_sample = n_samples > 1;
   const int nloci = tl.L1 - L0;
   // count * 100 / depth > threshold  <=>  count * 100 >= (threshold + 1) * depth  (integers, depth > 0)
   const int64_t thr1 = (int64_t)threshold + 1;
@@ -83,7 +86,11 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
     } else if (i < nloci) {
       const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
                      wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
-      const uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
+      uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
+      if (reg) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c[k] += reg[k];
+      }
       const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
       const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
       if (depth > 0) {
@@ -237,24 +244,29 @@ struct ColsCfg {
   static constexpr int kBuf = kEvOff + kEv * 4 + 16 + 256;
 };
 
-// Byte counters of one lane's column: c_a c_c c_t c_g hold one byte per locus; nf8 reads
-// fully covering the column since the last flush (<= 255).  Flushed into the LDS words with
-// atomics (the other lane of the column and the per-read pass add to the same words).
+// Byte counters of one lane's 8-locus column: c_x[0] for loci c..c+3, c_x[1] for c+4..c+7,
+// one byte per locus; nf8 = reads fully covering the column since the last flush (<= 255).
+// Flushed into the LDS words with atomics (other lanes of the column and the per-read pass
+// add to the same words).
 struct ColCounts {
-  uint32_t ca = 0, cc = 0, ct = 0, cg = 0, nf8 = 0;
+  uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0}, nf8 = 0;
   __device__ __forceinline__ void flush(uint32_t *cnt, int S, int c) {
     if (nf8 == 0) return;
-    const uint32_t cn = nf8 * 0x01010101u - (ca + cc + ct + cg);  // bytewise, no borrow
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t sel = 0x0C000C00u | ((uint32_t)(4 + b) << 16) | (uint32_t)b;  // [x_b, 0, y_b, 0]
-      const uint32_t ac = __builtin_amdgcn_perm(cc, ca, sel), tg = __builtin_amdgcn_perm(cg, ct, sel);
-      const uint32_t nn = ((cn >> (8 * b)) & 0xFFu) << 16;
-      if (ac) atomicAdd(cnt + W_AC * S + kGuard + c + b, ac);
-      if (tg) atomicAdd(cnt + W_TG * S + kGuard + c + b, tg);
-      if (nn) atomicAdd(cnt + W_NN * S + kGuard + c + b, nn);
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t cn = nf8 * 0x01010101u - (ca[h] + cc[h] + ct[h] + cg[h]);  // bytewise, no borrow
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t sel = 0x0C000C00u | ((uint32_t)(4 + b) << 16) | (uint32_t)b;  // [x_b, 0, y_b, 0]
+        const uint32_t ac = __builtin_amdgcn_perm(cc[h], ca[h], sel), tg = __builtin_amdgcn_perm(cg[h], ct[h], sel);
+        const uint32_t nn = ((cn >> (8 * b)) & 0xFFu) << 16;
+        const int i = kGuard + c + 4 * h + b;
+        if (ac) atomicAdd(cnt + W_AC * S + i, ac);
+        if (tg) atomicAdd(cnt + W_TG * S + i, tg);
+        if (nn) atomicAdd(cnt + W_NN * S + i, nn);
+      }
     }
-    ca = cc = ct = cg = nf8 = 0;
+    ca[0] = ca[1] = cc[0] = cc[1] = ct[0] = ct[1] = cg[0] = cg[1] = nf8 = 0;
   }
 };
 
@@ -286,13 +298,15 @@ constexpr uint32_t kSegCountK = 0;  // segment kinds of the auxiliary list (col_
 // Tiles that do not fit (plan_tiles: sbytes == 0) or hold a read the column path cannot
 // count are listed in `slow` for germline_walk.
 __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
-    const Tile *__restrict__ tiles, int64_t n_tiles, DevReads R, int threshold, int emit_ref, int emit_no_call,
-    CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
+    const Tile *__restrict__ tiles, int64_t n_tiles, const uint8_t *__restrict__ seq,
+    const ColDesc *__restrict__ cdesc, const uint32_t *__restrict__ cev, int n_samples, int threshold, int emit_ref,
+    int emit_no_call, CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
   // dbg (diagnostics, env GQ_DBG; results are wrong when bits 0-3 are set): 1 skip the column
   // pass, 2 skip the per-read pass, 4 skip the decision, 8 skip the DMA; 16 phase clocks
   using C = ColsCfg;
-  constexpr int T = C::kT, NT = C::kThreads, NW = NT / 64, NCOL = T / 4;
+  constexpr int T = C::kT, NT = C::kThreads, NW = NT / 64, W = 8, NCOL = T / W;
+  static_assert(NCOL == 64 && NT == 8 * NCOL, "one wave scans the columns; eight lanes per column");
   constexpr int S = T + 2 * kGuard;
   constexpr int kNever = (int)(0x7FFFu | 0x80000000u);  // s = 32767, e = -32768: covers no column
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
@@ -313,12 +327,12 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   auto issue = [&](const Tile &tn, int b) {  // DMA of a tile's window into buffer b
     if (tn.sbytes <= 0 || (dbg & 8)) return;
     uint8_t *L = buf[b];
-    dma_range<NW, 16>(R.seq + tn.sb0, L, tn.sbytes, wave, lane);
+    dma_range<NW, 16>(seq + tn.sb0, L, tn.sbytes, wave, lane);
     const int64_t d0 = (tn.rb * 24) & ~(int64_t)15;
-    dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(R.cdesc) + d0, L + C::kRowsOff,
-                     (int)(tn.re * 24 - d0), wave, lane);
+    dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(cdesc) + d0, L + C::kRowsOff, (int)(tn.re * 24 - d0), wave,
+                     lane);
     if (tn.mcnt > 0)
-      dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(R.cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, wave, lane);
+      dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, wave, lane);
   };
   {  // zero the histogram words, the buckets and the 16 zero bytes after each stage
     uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
@@ -332,8 +346,6 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   unsigned visited = 0, amb = 0, ties = 0;
   Tile tn = i0 < i1 ? tiles[i0] : Tile{};
   if (i0 < i1) issue(tn, 0);
-  const uint32_t *ev_unused = nullptr;
-  (void)ev_unused;
   for (int64_t i = i0; i < i1; ++i) {
     const int b = (int)((i - i0) & 1);
     const Tile tl = tn;
@@ -391,13 +403,13 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
               not_col = 1;
               continue;
             }
-            const int32_t sc = a > -4 ? a : -4, ec = b < T + 4 ? b : T + 4;
+            const int32_t sc = a > -W ? a : -W, ec = b < T + W ? b : T + W;
             xrow[x] = make_uint2((uint32_t)((sc & 0xFFFF) | (ec << 16)), so - (uint32_t)a);
           }
         } else if (!ok) {
           not_col = 1;
         } else {
-          const int32_t sc = srel > -4 ? srel : -4, ec = erel < T + 4 ? erel : T + 4;
+          const int32_t sc = srel > -W ? srel : -W, ec = erel < T + W ? erel : T + W;
           rx = (uint32_t)((sc & 0xFFFF) | (ec << 16));
           ry = sa - (uint32_t)srel;  // LDS address of tile locus 0
           mine = true;
@@ -408,7 +420,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       }
       // rows [0, hi(col)) start at or before the column's last locus; rows [0, lo(col))
       // have prefix-max end at or before its first locus (so cover none of it)
-      const int bs = srel < 0 ? 0 : srel >> 2, bp = perel < 0 ? 0 : (perel + 3) >> 2;
+      const int bs = srel < 0 ? 0 : srel >> 3, bp = perel < 0 ? 0 : (perel + 7) >> 3;
       if (bs < NCOL) atomicAdd(&hist[bs], 1u);
       if (bp < NCOL) atomicAdd(&hist[bp], 1u << 16);
       // rows keep: d0 start, d1 end, d5 md_lo; d2 d3 <- the column row (rx, ry);
@@ -425,27 +437,37 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       }
       continue;  // the next iteration's barrier orders the bucket reset
     }
-    // ---- C: inclusive scan of the packed buckets over the columns (wave 0, two columns per
-    //      lane) -> crng[col] = (lo << 16 | hi) of every column
+    // ---- C: inclusive scan of the packed buckets over the 64 columns (wave 0) -> crng[col] =
+    //      (lo << 16 | hi) of every column
     if (wave == 0) {
-      const uint32_t x0 = hist[2 * lane], x1 = hist[2 * lane + 1];
-      const uint32_t sc = wave_incl_scan(x0 + x1);
-      crng[2 * lane] = sc - x1;
-      crng[2 * lane + 1] = sc;
-      hist[2 * lane] = 0;  // ready for the next tile (its atomics follow this tile's barriers)
-      hist[2 * lane + 1] = 0;
+      crng[lane] = wave_incl_scan(hist[lane]);
+      hist[lane] = 0;  // ready for the next tile (its atomics follow this tile's barriers)
     }
     __syncthreads();
-    // lanes 4q .. 4q + 3 share column q and take alternate rows
-    const int col = t >> 2, par = t & 3;
+    // lanes 8q .. 8q + 7 share column q and take every eighth row
+    const int col = t >> 3, par = t & 7;
     const uint32_t v = crng[col];
     const int lo = (int)(v >> 16), hi = (int)(v & 0xFFFFu);
     const uint64_t tc = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch,
-    //      all loads of a batch issued before use
-    constexpr int P = C::kLanesPerCol, U = 8;
-    const int c = 4 * col;
+    // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch, all
+    //      loads of a batch issued before use.  Per row: 3 LDS dwords -> 8 bases (2 dwords),
+    //      code = byte & 7 (A 1, C 3, T 4, N 6, G 7), two v_perm tables per dword into
+    //      A|C / T|G nibble fields, folded into byte counters before they can overflow.
+    constexpr int P = 8, U = 4;
+    const int c = W * col;
     ColCounts cc;
+    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nnib = 0;  // nibble fields and the reads in them
+    auto fold = [&]() {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        cc.ca[h] += nac[h] & 0x0F0F0F0Fu;
+        cc.cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
+        cc.ct[h] += ntg[h] & 0x0F0F0F0Fu;
+        cc.cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
+        nac[h] = ntg[h] = 0;
+      }
+      nnib = 0;
+    };
     // rows k0, k0 + P, ... (< kend) of a row table (uint2 {rx, ry} at word stride ws)
     auto batch = [&](const uint32_t *tab, int ws, int k0, int kend) {
       uint2 m[U];
@@ -456,29 +478,32 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu), e = (int32_t)m[u].x >> 16;
-        const bool full = k0 + P * u < kend && s <= c && e >= c + 4;
-        a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 8 zero bytes
+        const bool full = k0 + P * u < kend && s <= c && e >= c + W;
+        a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
         nf += full ? 1u : 0u;
       }
-      uint32_t w0[U], w1[U];
+      uint32_t w0[U], w1[U], w2[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         w0[u] = st32[a[u] >> 2];
         w1[u] = st32[(a[u] >> 2) + 1];
+        w2[u] = st32[(a[u] >> 2) + 2];
       }
-      uint32_t n_ac = 0, n_tg = 0;
+      if (nnib + nf > 15) fold();
+      if (cc.nf8 + nf > 255) {
+        fold();
+        cc.flush(cnt, S, c);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t w = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]);
-        const uint32_t sel = w & 0x07070707u;  // A 1, C 3, T 4, N 6, G 7 (0 for the zero dword)
-        n_ac += __builtin_amdgcn_perm(0u, 0x10000100u, sel);
-        n_tg += __builtin_amdgcn_perm(0x10000001u, 0u, sel);
+        const uint32_t s0 = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]) & 0x07070707u;
+        const uint32_t s1 = __builtin_amdgcn_alignbyte(w2[u], w1[u], a[u]) & 0x07070707u;
+        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, s0);
+        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, s0);
+        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, s1);
+        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, s1);
       }
-      if (cc.nf8 + nf > 255) cc.flush(cnt, S, c);
-      cc.ca += n_ac & 0x0F0F0F0Fu;
-      cc.cc += (n_ac >> 4) & 0x0F0F0F0Fu;
-      cc.ct += n_tg & 0x0F0F0F0Fu;
-      cc.cg += (n_tg >> 4) & 0x0F0F0F0Fu;
+      nnib += nf;
       cc.nf8 += nf;
     };
     if (!(dbg & 1)) {
@@ -486,22 +511,32 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const int nx = (int)min(n_xrow, (unsigned)C::kExtra);
       for (int k0 = par; k0 < nx; k0 += P * U) batch(reinterpret_cast<const uint32_t *>(xrow), 2, k0, nx);
     }
-    {  // quad sums of the column's four lanes (bytes cannot overflow while the reads sum to <= 255)
-      auto qsum = [](uint32_t x) {
-        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1 0 3 2
-        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2 3 0 1
+    fold();
+    // the column's totals in all eight of its lanes (quad sums, then + the half-row mirror:
+    // lane i <-> 7 - i); lane par keeps locus c + par (= t) for the decision.  Bytes cannot
+    // overflow while the column's reads sum to <= 255; otherwise (deep pileups) each lane
+    // flushes its own counts into the LDS words.
+    uint32_t regc[5] = {0, 0, 0, 0, 0};  // A C T G N of locus t from the column pass
+    {
+      auto csum = [](uint32_t x) {
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1 0 3 2
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2 3 0 1
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
         return x;
       };
-      const uint32_t nq = qsum(cc.nf8);
-      const uint32_t sa_ = qsum(cc.ca), sc_ = qsum(cc.cc), st_ = qsum(cc.ct), sg_ = qsum(cc.cg);
-      if (nq <= 255) {
-        cc.ca = sa_;
-        cc.cc = sc_;
-        cc.ct = st_;
-        cc.cg = sg_;
-        cc.nf8 = par == 0 ? nq : 0u;  // one lane of the four adds the column's counts
+      const uint32_t nq = csum(cc.nf8);
+      if (nq > 255) {
+        cc.flush(cnt, S, c);
+      } else {
+        const int h = par >> 2, sh = 8 * (par & 3);
+        const uint32_t a0 = csum(cc.ca[0]), a1 = csum(cc.ca[1]), c0 = csum(cc.cc[0]), c1 = csum(cc.cc[1]);
+        const uint32_t t0 = csum(cc.ct[0]), t1 = csum(cc.ct[1]), g0 = csum(cc.cg[0]), g1 = csum(cc.cg[1]);
+        regc[0] = ((h ? a1 : a0) >> sh) & 0xFFu;
+        regc[1] = ((h ? c1 : c0) >> sh) & 0xFFu;
+        regc[2] = ((h ? t1 : t0) >> sh) & 0xFFu;
+        regc[3] = ((h ? g1 : g0) >> sh) & 0xFFu;
+        regc[4] = nq - regc[0] - regc[1] - regc[2] - regc[3];
       }
-      cc.flush(cnt, S, c);
     }
     const uint64_t te = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- E: threads t < 256 the column ends of read t, threads t >= 256 the MD events of
@@ -511,9 +546,9 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       // the <= 3 + 3 bytes of the two partial columns of a row over tile loci [s, e) whose
       // base at tile locus l sits at stage address base + l: both dwords loaded, one atomic per byte
       auto edges = [&](int32_t s, int32_t e, uint32_t base) {
-        const int32_t cs = s & ~3, ce = (e - 1) & ~3;
-        const bool ps = s != cs || e < cs + 4, pe = (e & 3) != 0 || s > ce;
-        int32_t ea0 = s, ea1 = e < cs + 4 ? e : cs + 4;  // first partial column's loci
+        const int32_t cs = s & ~(W - 1), ce = (e - 1) & ~(W - 1);
+        const bool ps = s != cs || e < cs + W, pe = (e & (W - 1)) != 0 || s > ce;
+        int32_t ea0 = s, ea1 = e < cs + W ? e : cs + W;  // first partial column's loci
         int32_t eb0 = ce, eb1 = e;                       // last partial column's loci
         if (!ps) ea1 = ea0;
         if (!pe || ce == cs) eb1 = eb0;
@@ -522,11 +557,14 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         eb0 = eb0 > 0 ? eb0 : 0;
         eb1 = eb1 < T ? eb1 : T;
         const uint32_t pa = base + (uint32_t)ea0, pb = base + (uint32_t)eb0;
-        const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1];
-        const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1];
-        const uint32_t wa = __builtin_amdgcn_alignbyte(wa1, wa0, pa), wb = __builtin_amdgcn_alignbyte(wb1, wb0, pb);
-        for (int32_t l = ea0; l < ea1; ++l) sink.bases4_clean(l, (wa >> (8 * (l - ea0))) & 0xFFu, 1u, 0);
-        for (int32_t l = eb0; l < eb1; ++l) sink.bases4_clean(l, (wb >> (8 * (l - eb0))) & 0xFFu, 1u, 0);
+        const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1], wa2 = st32[(pa >> 2) + 2];
+        const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1], wb2 = st32[(pb >> 2) + 2];
+        const uint64_t va = (uint64_t)__builtin_amdgcn_alignbyte(wa1, wa0, pa) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(wa2, wa1, pa) << 32);
+        const uint64_t vb = (uint64_t)__builtin_amdgcn_alignbyte(wb1, wb0, pb) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(wb2, wb1, pb) << 32);
+        for (int32_t l = ea0; l < ea1; ++l) sink.bases4_clean(l, (uint32_t)(va >> (8 * (l - ea0))) & 0xFFu, 1u, 0);
+        for (int32_t l = eb0; l < eb1; ++l) sink.bases4_clean(l, (uint32_t)(vb >> (8 * (l - eb0))) & 0xFFu, 1u, 0);
       };
       if (general) {  // segments: ends of the count segments, complex loci
         for (int32_t q = 0; q < my_nseg; ++q) {
@@ -568,8 +606,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const uint64_t tf = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- F: decision, then the histogram words are zeroed for the next tile
     if (!(dbg & 4))
-      germline_decide<T>(cnt, tl, tid_tile, false, R, threshold, emit_ref, emit_no_call, recs, cplx, out, visited,
-                         amb, ties);
+      germline_decide<T>(cnt, tl, tid_tile, false, n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
+                         visited, amb, ties, regc);
     __syncthreads();  // decision reads done before the words are zeroed
     {
       uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
@@ -626,8 +664,8 @@ __global__ __launch_bounds__(kBlock) void germline_walk(const Tile *__restrict__
       for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, tl.L0, tl.L1, sink);
     }
     __syncthreads();
-    germline_decide<T>(cnt, tl, tid_tile, wide, R, threshold, emit_ref, emit_no_call, recs, cplx, out, visited, amb,
-                       ties);
+    germline_decide<T>(cnt, tl, tid_tile, wide, R.n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
+                       visited, amb, ties);
     __syncthreads();
   }
   add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);

@@ -1136,8 +1136,8 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,
-                     (const Tile *)c->tiles.p, tiles, R, p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og,
-                     ctr, (int32_t *)c->slow.p, dbg);
+                     (const Tile *)c->tiles.p, tiles, R.seq, R.cdesc, R.cev, R.n_samples, p->threshold, p->emit_ref,
+                     p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   HIP_TRY(hipGetLastError());
   const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
   hipLaunchKernelGGL((germline_walk<ColsCfg::kT>), dim3(wblocks), dim3(kBlock), 0, c->stream,
