@@ -60,7 +60,7 @@ struct GlobalOut {  // germline_walk: a partition per wave, counters in device m
   }
 };
 
-template <int T, class Out>
+template <int T, bool ZERO = false, class Out>
 __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile &tl, int64_t tile_id, bool wide,
                                                 int n_samples, int threshold, int emit_ref, int emit_no_call,
                                                 CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx,
@@ -72,129 +72,139 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
   const int32_t L0 = tl.L0;
   const bool multi_sample = n_samples > 1;
   const int nloci = tl.L1 - L0;
-  // count * 100 / depth > threshold  <=>  count * 100 >= (threshold + 1) * depth  (integers, depth > 0)
+  // count * 100 / depth > threshold  <=>  count * 100 >= (threshold + 1) * depth  (integers, depth > 0);
+  // 32-bit products when they cannot overflow (counts < 2^19, threshold <= 1000)
   const int64_t thr1 = (int64_t)threshold + 1;
-  auto passes = [thr1](uint32_t count, uint32_t depth) { return (int64_t)count * 100 >= thr1 * (int64_t)depth; };
+  const bool narrow = thr1 >= 0 && thr1 <= 1001;
+  const uint32_t thr1u = (uint32_t)thr1;
+  auto passes = [=](uint32_t count, uint32_t depth) {
+    return narrow ? count * 100u >= thr1u * depth : (int64_t)count * 100 >= thr1 * (int64_t)depth;
+  };
+  constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                               ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
   // uniform trip count so every wave reaches the wave-level reservations together
   for (int i0 = 0; i0 < nloci; i0 += blockDim.x) {
     const int i = i0 + threadIdx.x;
+    const bool in = i < nloci;
+    // ---- summary of the locus, branch-free
+    uint32_t wac = 0, wtg = 0, wox = 0, wnn = 0, eac = 0, etg = 0;
+    if (in) {
+      wac = cnt[W_AC * S + kGuard + i];
+      wtg = cnt[W_TG * S + kGuard + i];
+      wox = cnt[W_OX * S + kGuard + i];
+      wnn = cnt[W_NN * S + kGuard + i];
+      eac = cnt[W_EAC * S + kGuard + i];
+      etg = cnt[W_ETG * S + kGuard + i];
+    }
+    if (ZERO && i < T) {  // ready for the next tile (one thread per locus: its own words)
+      uint32_t *z = const_cast<uint32_t *>(cnt) + kGuard + i;
+#pragma unroll
+      for (int w = 0; w < W_N; ++w) z[w * S] = 0u;
+    }
+    uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
+    if (reg) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) c[k] += in ? reg[k] : 0u;
+    }
+    const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
+    const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
+    // MD-derived reference bases present: event / complex bits, plus every base with more
+    // reads than reads carrying a mismatch event there (those read the base as reference)
+    const uint32_t mask = (wnn & 0xFu) | (c[0] > (eac & 0xFFFFu) ? 1u : 0u) | (c[1] > (eac >> 16) ? 2u : 0u) |
+                          (c[2] > (etg & 0xFFFFu) ? 4u : 0u) | (c[3] > (etg >> 16) ? 8u : 0u);
+    const bool live = in && depth > 0;
+    const bool ambiguous = (mask & (mask - 1)) != 0;
+    const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit
+    const uint32_t c_ref = low == 1u ? c[0] : low == 2u ? c[1] : low == 4u ? c[2] : low == 8u ? c[3] : c[4];
+    const bool to_complex = (wide && in) || (live && (ambiguous || cx > 0 || multi_sample));
+    // every non-reference allele has count <= depth - c_ref: if that does not pass, no
+    // alternate allele does (HomRef if the reference passes, else NoCall)
+    const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
+    const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+    const bool emit_hr = homref && (ref_pass ? emit_ref : emit_no_call);
+    const bool general = live && !to_complex && !homref;
+    visited += (live && !(wide && in)) ? 1u : 0u;
+    amb += (live && ambiguous && !wide) ? 1u : 0u;
+    if (__ballot(to_complex || emit_hr || general) == 0) continue;  // the common case: nothing to write
+    // ---- records
     CallRec out0, out1;  // named (not an array): no scratch
     unsigned nout = 0;
-    bool to_complex = false;
-    if (wide && i < nloci) {
-      to_complex = true;
-    } else if (i < nloci) {
-      const uint32_t wac = cnt[W_AC * S + kGuard + i], wtg = cnt[W_TG * S + kGuard + i],
-                     wox = cnt[W_OX * S + kGuard + i], wnn = cnt[W_NN * S + kGuard + i];
-      uint32_t c[5] = {wac & 0xFFFFu, wac >> 16, wtg & 0xFFFFu, wtg >> 16, wnn >> 16};  // A C T G N
-      if (reg) {
+    const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+    const int32_t pos = L0 + i;
+    const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
+    auto push = [&](const CallRec &rr) {
+      if (nout == 0) out0 = rr;
+      else out1 = rr;
+      ++nout;
+    };
+    if (emit_hr) {
+      CallRec rr;
+      rr.key = ord << 12;
+      rr.contig = tl.contig;
+      rr.pos = pos;
+      rr.sample = 0;
+      rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
+      rr.flags = 0;
+      rr.ref_len = 1;
+      rr.alt_len = 5;
+      rr.allele = (uint64_t)ref | kAltSym;
+      push(rr);
+    }
+    if (general) {
+      // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles.  Allele
+      // (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of Allele(ref, alt)
+      // for one ref is the alt byte order A < C < G < N < T, i.e. the categories 0, 1, 3, 4, 2.
+      // Sorting keys descending = sortBy(-count), ties canonical.
+      uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
+      int npass = 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) c[k] += reg[k];
+      for (int rank = 0; rank < 5; ++rank) {
+        const int cat = (0x24310 >> (4 * rank)) & 0xF;
+        const uint32_t cc = c[cat];
+        if (cc == 0 || !passes(cc, depth)) continue;
+        ++npass;
+        uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
+        if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
+        if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
+        if (key > k2) { k2 = key; }
       }
-      const uint32_t cx = (wox & 0xFFFFu) + (wox >> 16);  // other bases + complex elements
-      const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + cx;
-      if (depth > 0) {
-        ++visited;
-        uint32_t mask = wnn & 0xFu;  // W_MASK aliases W_NN's low bits
-        const uint32_t eac = cnt[W_EAC * S + kGuard + i], etg = cnt[W_ETG * S + kGuard + i];
-        const uint32_t ev[4] = {eac & 0xFFFFu, eac >> 16, etg & 0xFFFFu, etg >> 16};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (c[k] > ev[k]) mask |= 1u << k;
-        const bool ambiguous = __popc(mask) > 1;
-        if (ambiguous) ++amb;
-        if (ambiguous || cx > 0 || multi_sample) {
-          to_complex = true;
-        } else {
-          const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-          const int rc = mask ? (__ffs((int)mask) - 1) : 4;  // select chain: no dynamic register indexing
-          const uint32_t c_ref = rc == 0 ? c[0] : rc == 1 ? c[1] : rc == 2 ? c[2] : rc == 3 ? c[3] : c[4];
-          const int32_t pos = L0 + i;
-          const uint64_t ord = (uint64_t)(tl.ordinal0 + i);
-          constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
-                                       ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
-          if (!passes(depth - c_ref, depth)) {
-            // every non-reference allele has count <= depth - c_ref, so none passes the
-            // threshold: HomRef if the reference allele passes, else NoCall (the same
-            // outcome as the general case split below)
-            const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
-            if (ref_pass ? emit_ref : emit_no_call) {
-              CallRec rr;
-              rr.key = ord << 12;
-              rr.contig = tl.contig;
-              rr.pos = pos;
-              rr.sample = 0;
-              rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
-              rr.flags = 0;
-              rr.ref_len = 1;
-              rr.alt_len = 5;
-              rr.allele = (uint64_t)ref | kAltSym;
-              if (nout == 0) out0 = rr;
-              else out1 = rr;
-              ++nout;
-            }
-          } else {
-            // Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of
-            // Allele(ref, alt) for one ref is the alt byte order A < C < G < N < T, i.e. the
-            // categories 0, 1, 3, 4, 2.  Sorting keys descending = sortBy(-count), ties canonical.
-            uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
-            int npass = 0;
-#pragma unroll
-            for (int rank = 0; rank < 5; ++rank) {
-              const int cat = (0x24310 >> (4 * rank)) & 0xF;
-              const uint32_t cc = c[cat];
-              if (cc == 0 || !passes(cc, depth)) continue;
-              ++npass;
-              uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
-              if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
-              if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
-              if (key > k2) { k2 = key; }
-            }
-            auto key_base = [](uint32_t key) -> uint8_t {
-              const int rank = 255 - (int)(key & 0xFFu);
-              return cat_base((0x24310 >> (4 * rank)) & 0xF);
-            };
-            const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
-            if (tie) ++ties;
-            const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
-            auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
-              CallRec rr;
-              rr.key = (ord << 12) | (uint64_t)sub;
-              rr.contig = tl.contig;
-              rr.pos = pos;
-              rr.sample = 0;
-              rr.gt0 = g0;
-              rr.gt1 = g1;
-              rr.flags = fl;
-              rr.ref_len = 1;
-              rr.alt_len = alt_sym ? 5 : 1;
-              rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
-              return rr;
-            };
-            const uint8_t b0 = key_base(k0), b1 = key_base(k1);
-            auto push = [&](const CallRec &rr) {
-              if (nout == 0) out0 = rr;
-              else out1 = rr;
-              ++nout;
-            };
-            if (npass == 0) {
-              if (emit_no_call) push(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
-            } else if (npass == 1 && b0 == ref) {
-              if (emit_ref) push(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
-            } else if (npass == 1) {
-              push(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
-            } else {
-              const bool v1 = b0 != ref, v2 = b1 != ref;
-              if (v1 != v2) {
-                push(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
-              } else if (v1 && v2) {
-                push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
-                push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
-              }
-              // two non-variant single-base alleles cannot occur (all Match alleles share ref)
-            }
-          }
+      auto key_base = [](uint32_t key) -> uint8_t {
+        const int rank = 255 - (int)(key & 0xFFu);
+        return cat_base((0x24310 >> (4 * rank)) & 0xF);
+      };
+      const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
+      if (tie) ++ties;
+      const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
+      auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
+        CallRec rr;
+        rr.key = (ord << 12) | (uint64_t)sub;
+        rr.contig = tl.contig;
+        rr.pos = pos;
+        rr.sample = 0;
+        rr.gt0 = g0;
+        rr.gt1 = g1;
+        rr.flags = fl;
+        rr.ref_len = 1;
+        rr.alt_len = alt_sym ? 5 : 1;
+        rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
+        return rr;
+      };
+      const uint8_t b0 = key_base(k0), b1 = key_base(k1);
+      if (npass == 0) {
+        if (emit_no_call) push(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
+      } else if (npass == 1 && b0 == ref) {
+        if (emit_ref) push(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
+      } else if (npass == 1) {
+        push(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
+      } else {
+        const bool v1 = b0 != ref, v2 = b1 != ref;
+        if (v1 != v2) {
+          push(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
+        } else if (v1 && v2) {
+          push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
+          push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
         }
+        // two non-variant single-base alleles cannot occur (all Match alleles share ref)
       }
     }
     // reserve + write records (wave-aggregated, in the writer's partition)
@@ -235,12 +245,16 @@ struct ColsCfg {
   static constexpr int kThreads = 512;
   static constexpr int kLanesPerCol = kThreads / (kT / 4);  // rows of a column split over 4 lanes
   static constexpr int kStage = 24 * 1024;  // sequence bytes (1 KiB DMA pieces)
-  static constexpr int kMeta = 256;         // reads (ColDesc rows, one per thread)
+  static constexpr int kBatch = 6;          // rows per lane per column-pass batch (8 lanes per column)
+  static constexpr int kMeta = 208;         // reads per tile (ColDesc rows); the row buffer holds
+                                            // kRowCap rows: 8 * kBatch zero rows pad the batches
+  static constexpr int kRowCap = 256;
+  static_assert(kMeta + 8 * kBatch <= kRowCap, "row padding");
   static constexpr int kEv = 512;           // auxiliary words (MD events, segments of general reads)
   static constexpr int kExtra = 64;         // column rows of general reads' count segments
   // one buffer: stage | rows (+16 B alignment, +256 B dword-DMA tail) | events (same)
   static constexpr int kRowsOff = kStage + 16;  // + 16 zero bytes after the stage (kZero)
-  static constexpr int kEvOff = kRowsOff + kMeta * 24 + 16 + 256;
+  static constexpr int kEvOff = kRowsOff + kRowCap * 24 + 16 + 256;
   static constexpr int kBuf = kEvOff + kEv * 4 + 16 + 256;
 };
 
@@ -284,7 +298,25 @@ __device__ __forceinline__ void dma_range(const uint8_t *g, uint8_t *l, int n, i
   }
 }
 
-constexpr uint32_t kSegCountK = 0;  // segment kinds of the auxiliary list (col_derive): count / complex
+constexpr uint32_t kSegCountK = 0;
+
+// Column row of tile loci [a, b): the 64 8-locus columns it covers completely, as a bit mask,
+// laid out {mask lo, base, mask hi, base} so a lane reads the dword pair of its half with one
+// ds_read_b64; base = LDS address of tile locus 0 in the read's bytes.
+__device__ __forceinline__ uint4 col_row(int32_t a, int32_t b, uint32_t base, int T) {
+  const int32_t fc = a <= 0 ? 0 : (a + 7) >> 3;
+  const int32_t lc = (b >= T ? T : (b < 0 ? 0 : b)) >> 3;
+  auto below = [](int32_t n, int h) -> uint32_t {  // bits [0, n) of the 64, half h
+    const int32_t m = n - 32 * h;
+    return m <= 0 ? 0u : (m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u);
+  };
+  uint32_t lo = 0, hi = 0;
+  if (lc > fc) {
+    lo = below(lc, 0) & ~below(fc, 0);
+    hi = below(lc, 1) & ~below(fc, 1);
+  }
+  return make_uint4(lo, base, hi, base);
+}  // segment kinds of the auxiliary list (col_derive): count / complex
 
 // germline_cols: persistent workgroups, each over a contiguous run of tiles (XCD-local
 // neighbours: reads straddling two tiles are re-read from L2).  Per tile:
@@ -302,8 +334,9 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const ColDesc *__restrict__ cdesc, const uint32_t *__restrict__ cev, int n_samples, int threshold, int emit_ref,
     int emit_no_call, CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
-  // dbg (diagnostics, env GQ_DBG; results are wrong when bits 0-3 are set): 1 skip the column
-  // pass, 2 skip the per-read pass, 4 skip the decision, 8 skip the DMA; 16 phase clocks
+  // dbg (diagnostics, env GQ_DBG; results are wrong when bits 0-3, 5, 6 are set): 1 skip the
+  // column pass, 2 skip the per-read pass, 4 skip the decision, 8 skip the DMA; 16 phase
+  // clocks; 32 skip the column ends, 64 skip the MD events
   using C = ColsCfg;
   constexpr int T = C::kT, NT = C::kThreads, NW = NT / 64, W = 8, NCOL = T / W;
   static_assert(NCOL == 64 && NT == 8 * NCOL, "one wave scans the columns; eight lanes per column");
@@ -312,8 +345,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ __attribute__((aligned(16))) uint8_t buf[2][C::kBuf];
   __shared__ uint32_t hist[NCOL];  // per column bucket: rows starting (lo 16) / prefix-max end reaching (hi 16)
-  __shared__ uint32_t crng[NCOL];  // per column: lo << 16 | hi (its row range)
-  __shared__ __attribute__((aligned(8))) uint2 xrow[C::kExtra];  // rows of general reads' count segments
+  __shared__ __attribute__((aligned(16))) uint4 xrow[C::kExtra];  // rows of general reads' count segments
   __shared__ unsigned n_xrow;
   __shared__ unsigned outn[2];  // records / complex items of this workgroup's partition
 
@@ -324,15 +356,17 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
   uint64_t clk[5] = {0, 0, 0, 0, 0};
 
-  auto issue = [&](const Tile &tn, int b) {  // DMA of a tile's window into buffer b
-    if (tn.sbytes <= 0 || (dbg & 8)) return;
+  // DMA of a tile's window into buffer b, by waves 4-7 (waves 0-3 build rows meanwhile)
+  auto issue = [&](const Tile &tn, int b) {
+    if (tn.sbytes <= 0 || (dbg & 8) || wave < 4) return;
     uint8_t *L = buf[b];
-    dma_range<NW, 16>(seq + tn.sb0, L, tn.sbytes, wave, lane);
+    const int w4 = wave - 4;
+    dma_range<4, 16>(seq + tn.sb0, L, tn.sbytes, w4, lane);
     const int64_t d0 = (tn.rb * 24) & ~(int64_t)15;
-    dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(cdesc) + d0, L + C::kRowsOff, (int)(tn.re * 24 - d0), wave,
-                     lane);
+    dma_range<4, 4>(reinterpret_cast<const uint8_t *>(cdesc) + d0, L + C::kRowsOff, (int)(tn.re * 24 - d0), w4,
+                    lane);
     if (tn.mcnt > 0)
-      dma_range<NW, 4>(reinterpret_cast<const uint8_t *>(cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, wave, lane);
+      dma_range<4, 4>(reinterpret_cast<const uint8_t *>(cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, w4, lane);
   };
   {  // zero the histogram words, the buckets and the 16 zero bytes after each stage
     uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
@@ -346,8 +380,9 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   unsigned visited = 0, amb = 0, ties = 0;
   Tile tn = i0 < i1 ? tiles[i0] : Tile{};
   if (i0 < i1) issue(tn, 0);
-  for (int64_t i = i0; i < i1; ++i) {
-    const int b = (int)((i - i0) & 1);
+  int it = 0;
+  for (int64_t i = i0; i < i1; ++i, ++it) {
+    const int b = it & 1;
     const Tile tl = tn;
     const int64_t tid_tile = i;
     // ---- A: this tile's DMA (issued one tile ago) has landed everywhere; next tile's DMA
@@ -366,19 +401,20 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const uint32_t *evs = reinterpret_cast<const uint32_t *>(L + C::kEvOff);
     const int nch = (int)(tl.re - tl.rb);
     const uint32_t sb_lo = (uint32_t)(uint64_t)tl.sb0, mb_lo = (uint32_t)(uint64_t)tl.mb0;
-    // ---- B: rows (thread per read) and buckets
+    // ---- B: rows (thread per read) and buckets; threads nch .. nch + 8 * kBatch - 1 write zero rows
+    //      (padding for the column pass's fixed batches), waves 4-7 issue the next tile's DMA
     int not_col = tl.sbytes <= 0;
     int32_t my_s = 0, my_e = 0, my_base = 0, my_seg = 0, my_nseg = 0;
     bool mine = false, general = false;
     if (!not_col && t < nch) {
-      const uint32_t *d = rows + 6 * t;
+      uint32_t *d = rows + 6 * t;
       const int32_t s = (int32_t)d[0], e = (int32_t)d[1], pe = (int32_t)d[2];
       const uint32_t info = d[3];
       const int32_t srel = s - L0, erel = e - L0, perel = pe - L0;
       const uint32_t sa = d[4] - sb_lo;  // stage address of the base at `start`
       const uint32_t ea = d[5] - mb_lo;  // staged index of the first MD event
       const int32_t nmd = (int32_t)(info & 0xFFFFu);
-      uint32_t rx = (uint32_t)kNever, ry = 0;
+      uint4 row = make_uint4(0u, 0u, 0u, 0u);
       if (e > L0 && s < L1) {
         const uint32_t nseg = (info >> 18) & 0xFFu;
         const bool evs_in = ea + (uint32_t)nmd + 2u * nseg <= (uint32_t)tl.mcnt;
@@ -403,19 +439,16 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
               not_col = 1;
               continue;
             }
-            const int32_t sc = a > -W ? a : -W, ec = b < T + W ? b : T + W;
-            xrow[x] = make_uint2((uint32_t)((sc & 0xFFFF) | (ec << 16)), so - (uint32_t)a);
+            xrow[x] = col_row(a, b, so - (uint32_t)a, T);
           }
         } else if (!ok) {
           not_col = 1;
         } else {
-          const int32_t sc = srel > -W ? srel : -W, ec = erel < T + W ? erel : T + W;
-          rx = (uint32_t)((sc & 0xFFFF) | (ec << 16));
-          ry = sa - (uint32_t)srel;  // LDS address of tile locus 0
+          row = col_row(srel, erel, sa - (uint32_t)srel, T);
           mine = true;
           my_s = srel;
           my_e = erel;
-          my_base = (int32_t)ry;
+          my_base = (int32_t)(sa - (uint32_t)srel);
         }
       }
       // rows [0, hi(col)) start at or before the column's last locus; rows [0, lo(col))
@@ -423,10 +456,16 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const int bs = srel < 0 ? 0 : srel >> 3, bp = perel < 0 ? 0 : (perel + 7) >> 3;
       if (bs < NCOL) atomicAdd(&hist[bs], 1u);
       if (bp < NCOL) atomicAdd(&hist[bp], 1u << 16);
-      // rows keep: d0 start, d1 end, d5 md_lo; d2 d3 <- the column row (rx, ry);
-      // d4 <- n_md | 1 << 31 if the read's events go to the histogram (mine)
-      *reinterpret_cast<uint2 *>(const_cast<uint32_t *>(d) + 2) = make_uint2(rx, ry);
-      const_cast<uint32_t *>(d)[4] = (uint32_t)nmd | (mine ? 0x80000000u : 0u);
+      // the row's words become: d0..d3 the column row, d4 = n_md | first event << 16 | mine << 31,
+      // d5 = tile-relative start (for the MD-event pass)
+      *reinterpret_cast<uint2 *>(d) = make_uint2(row.x, row.y);
+      *reinterpret_cast<uint2 *>(d + 2) = make_uint2(row.z, row.w);
+      *reinterpret_cast<uint2 *>(d + 4) =
+          make_uint2((uint32_t)nmd | (ea << 16) | (mine ? 0x80000000u : 0u), (uint32_t)srel);
+    } else if (!not_col && t < nch + 8 * C::kBatch && t < C::kRowCap) {
+      uint32_t *d = rows + 6 * t;
+      *reinterpret_cast<uint2 *>(d) = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2 *>(d + 2) = make_uint2(0u, 0u);
     }
     if (__syncthreads_or(not_col)) {  // uniform: the tile goes to the walker kernel
       if (t < NCOL) hist[t] = 0;
@@ -437,23 +476,17 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       }
       continue;  // the next iteration's barrier orders the bucket reset
     }
-    // ---- C: inclusive scan of the packed buckets over the 64 columns (wave 0) -> crng[col] =
-    //      (lo << 16 | hi) of every column
-    if (wave == 0) {
-      crng[lane] = wave_incl_scan(hist[lane]);
-      hist[lane] = 0;  // ready for the next tile (its atomics follow this tile's barriers)
-    }
-    __syncthreads();
-    // lanes 8q .. 8q + 7 share column q and take every eighth row
-    const int col = t >> 3, par = t & 7;
-    const uint32_t v = crng[col];
+    // ---- C: inclusive scan of the packed buckets over the 64 columns, by every wave (no
+    //      barrier): lane l scans column l, then each lane fetches its own column's value
+    const int col = t >> 3, par = t & 7;  // lanes 8q .. 8q + 7 share column q, every eighth row
+    const uint32_t v = (uint32_t)__shfl((int)wave_incl_scan(hist[lane]), col, 64);
     const int lo = (int)(v >> 16), hi = (int)(v & 0xFFFFu);
     const uint64_t tc = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch, all
     //      loads of a batch issued before use.  Per row: 3 LDS dwords -> 8 bases (2 dwords),
     //      code = byte & 7 (A 1, C 3, T 4, N 6, G 7), two v_perm tables per dword into
     //      A|C / T|G nibble fields, folded into byte counters before they can overflow.
-    constexpr int P = 8, U = 4;
+    constexpr int P = 8, U = C::kBatch;  // lanes per column, rows per batch (a column has ~31 rows at 30x)
     const int c = W * col;
     ColCounts cc;
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nnib = 0;  // nibble fields and the reads in them
@@ -468,26 +501,30 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       }
       nnib = 0;
     };
-    // rows k0, k0 + P, ... (< kend) of a row table (uint2 {rx, ry} at word stride ws)
-    auto batch = [&](const uint32_t *tab, int ws, int k0, int kend) {
+    // rows k0, k0 + P, ... of a row table at byte stride bs (rows past the range are zero
+    //   rows): the lane's half of the column mask and the base, at immediate offsets
+    const int half = col >> 5, cb = col & 31;
+    auto batch = [&](const uint8_t *tab, int bs, int k0, auto uu) {
+      constexpr int U = decltype(uu)::value;
+      const uint8_t *rp = tab + bs * k0 + 8 * half;
       uint2 m[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(tab + ws * min(k0 + P * u, kend - 1));
+      for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(rp + bs * P * u);
       uint32_t a[U];
       uint32_t nf = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu), e = (int32_t)m[u].x >> 16;
-        const bool full = k0 + P * u < kend && s <= c && e >= c + W;
+        const uint32_t full = (m[u].x >> cb) & 1u;
         a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
-        nf += full ? 1u : 0u;
+        nf += full;
       }
       uint32_t w0[U], w1[U], w2[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        w0[u] = st32[a[u] >> 2];
-        w1[u] = st32[(a[u] >> 2) + 1];
-        w2[u] = st32[(a[u] >> 2) + 2];
+        const uint32_t *q = st32 + (a[u] >> 2);
+        w0[u] = q[0];
+        w1[u] = q[1];
+        w2[u] = q[2];
       }
       if (nnib + nf > 15) fold();
       if (cc.nf8 + nf > 255) {
@@ -507,9 +544,12 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       cc.nf8 += nf;
     };
     if (!(dbg & 1)) {
-      for (int k0 = lo + par; k0 < hi; k0 += P * U) batch(rows + 2, 6, k0, hi);
+      for (int k0 = lo + par; k0 < hi; k0 += P * U)
+        batch(reinterpret_cast<const uint8_t *>(rows), 24, k0, std::integral_constant<int, U>{});
+      // extra rows (rare): one at a time, no padding
       const int nx = (int)min(n_xrow, (unsigned)C::kExtra);
-      for (int k0 = par; k0 < nx; k0 += P * U) batch(reinterpret_cast<const uint32_t *>(xrow), 2, k0, nx);
+      for (int k0 = par; k0 < nx; k0 += P)
+        batch(reinterpret_cast<const uint8_t *>(xrow), 16, k0, std::integral_constant<int, 1>{});
     }
     fold();
     // the column's totals in all eight of its lanes (quad sums, then + the half-row mirror:
@@ -559,14 +599,18 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         const uint32_t pa = base + (uint32_t)ea0, pb = base + (uint32_t)eb0;
         const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1], wa2 = st32[(pa >> 2) + 2];
         const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1], wb2 = st32[(pb >> 2) + 2];
-        const uint64_t va = (uint64_t)__builtin_amdgcn_alignbyte(wa1, wa0, pa) |
-                            ((uint64_t)__builtin_amdgcn_alignbyte(wa2, wa1, pa) << 32);
-        const uint64_t vb = (uint64_t)__builtin_amdgcn_alignbyte(wb1, wb0, pb) |
-                            ((uint64_t)__builtin_amdgcn_alignbyte(wb2, wb1, pb) << 32);
-        for (int32_t l = ea0; l < ea1; ++l) sink.bases4_clean(l, (uint32_t)(va >> (8 * (l - ea0))) & 0xFFu, 1u, 0);
-        for (int32_t l = eb0; l < eb1; ++l) sink.bases4_clean(l, (uint32_t)(vb >> (8 * (l - eb0))) & 0xFFu, 1u, 0);
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(wa1, wa0, pa), a1 = __builtin_amdgcn_alignbyte(wa2, wa1, pa);
+        const uint32_t b0 = __builtin_amdgcn_alignbyte(wb1, wb0, pb), b1 = __builtin_amdgcn_alignbyte(wb2, wb1, pb);
+        // at most W - 1 bytes per side: fixed, predicated steps (no data-dependent loop)
+#pragma unroll
+        for (int j = 0; j < W - 1; ++j) {
+          const uint32_t ba = ((j < 4 ? a0 : a1) >> (8 * (j & 3))) & 0xFFu;
+          const uint32_t bb = ((j < 4 ? b0 : b1) >> (8 * (j & 3))) & 0xFFu;
+          if (ea0 + j < ea1) sink.base1_clean(ea0 + j, ba);
+          if (eb0 + j < eb1) sink.base1_clean(eb0 + j, bb);
+        }
       };
-      if (general) {  // segments: ends of the count segments, complex loci
+      if (general && !(dbg & 32)) {  // segments: ends of the count segments, complex loci
         for (int32_t q = 0; q < my_nseg; ++q) {
           const uint32_t w0 = evs[my_seg + 2 * q], w1 = evs[my_seg + 2 * q + 1];
           const int32_t a = my_s + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
@@ -577,17 +621,17 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
             for (int32_t l = a > 0 ? a : 0; l < (b < T ? b : T); ++l) sink.complex_i(l);
           }
         }
-      } else if (mine) {
+      } else if (mine && !(dbg & 32)) {
         edges(my_s, my_e, (uint32_t)my_base);
       }
       const int k = t - C::kMeta;
-      if (k >= 0 && k < nch) {
+      if (k >= 0 && k < nch && !(dbg & 64)) {
         const uint32_t *d = rows + 6 * k;
         const uint32_t d4 = d[4];
         const int32_t nmd = (int32_t)(d4 & 0xFFFFu);
         if ((d4 & 0x80000000u) && nmd > 0) {
-          const int32_t s = (int32_t)d[0] - L0, x1 = L1 - L0;
-          const int32_t e0 = (int32_t)(d[5] - mb_lo);
+          const int32_t s = (int32_t)d[5], x1 = L1 - L0;
+          const int32_t e0 = (int32_t)((d4 >> 16) & 0x7FFFu);
           for (int32_t k0 = 0; k0 < nmd; k0 += 4) {  // events are sorted by offset; 4 loads in flight
             uint32_t w4[4];
 #pragma unroll
@@ -603,16 +647,12 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     }
     __syncthreads();  // histogram complete
     if (t == 0) n_xrow = 0;  // the next tile's row-build follows this tile's barriers
+    if (t < NCOL) hist[t] = 0;
     const uint64_t tf = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- F: decision, then the histogram words are zeroed for the next tile
-    if (!(dbg & 4))
-      germline_decide<T>(cnt, tl, tid_tile, false, n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
-                         visited, amb, ties, regc);
-    __syncthreads();  // decision reads done before the words are zeroed
-    {
-      uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
-      for (int k = t; k < W_N * S / 4; k += NT) c4[k] = make_uint4(0u, 0u, 0u, 0u);
-    }
+    // (each thread zeroes the words of its own locus after reading them: no barrier)
+    germline_decide<T, true>(cnt, tl, tid_tile, false, n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
+                             visited, amb, ties, regc);
     if (dbg & 16) {
       const uint64_t now = __builtin_readcyclecounter();
       clk[0] += now - ta;  // tile total from after the A barrier

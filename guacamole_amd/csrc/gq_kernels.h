@@ -391,6 +391,10 @@ struct GermSink {
   // four Match/Mismatch elements whose bytes are all A C G T N (checked once per read at
   // upload): counter word (b >> 2) & 3 (A C -> W_AC, T G -> W_TG, N -> W_NN), half (b >> 1) & 1;
   // the increment is valid << (16 * half)
+  // one Match/Mismatch element with an A/C/G/T/N base b at tile index i (one atomic)
+  __device__ __forceinline__ void base1_clean(int i, uint32_t b) {
+    atomicAdd(cnt + ((b >> 2) & 3u) * S + kGuard + i, 1u << (((b >> 1) & 1u) << 4));
+  }
   __device__ __forceinline__ void bases4_clean(int i, uint32_t w, uint32_t valid4, uint8_t) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
