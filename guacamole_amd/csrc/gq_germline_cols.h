@@ -259,16 +259,16 @@ struct ColsCfg {
 };
 
 // Byte counters of one lane's 8-locus column: c_x[0] for loci c..c+3, c_x[1] for c+4..c+7,
-// one byte per locus; nf8 = reads fully covering the column since the last flush (<= 255).
-// Flushed into the LDS words with atomics (other lanes of the column and the per-read pass
-// add to the same words).
+// one byte per locus (A C T G and cv = reads with a base there); nrow = rows added since the
+// last flush (bounds every byte, <= 255).  Flushed into the LDS words with atomics only when a
+// column is deeper than 255 reads.
 struct ColCounts {
-  uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0}, nf8 = 0;
+  uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0}, cv[2] = {0, 0}, nrow = 0;
   __device__ __forceinline__ void flush(uint32_t *cnt, int S, int c) {
-    if (nf8 == 0) return;
+    if (nrow == 0) return;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint32_t cn = nf8 * 0x01010101u - (ca[h] + cc[h] + ct[h] + cg[h]);  // bytewise, no borrow
+      const uint32_t cn = cv[h] - (ca[h] + cc[h] + ct[h] + cg[h]);  // bytewise, no borrow
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t sel = 0x0C000C00u | ((uint32_t)(4 + b) << 16) | (uint32_t)b;  // [x_b, 0, y_b, 0]
@@ -280,7 +280,7 @@ struct ColCounts {
         if (nn) atomicAdd(cnt + W_NN * S + i, nn);
       }
     }
-    ca[0] = ca[1] = cc[0] = cc[1] = ct[0] = ct[1] = cg[0] = cg[1] = nf8 = 0;
+    ca[0] = ca[1] = cc[0] = cc[1] = ct[0] = ct[1] = cg[0] = cg[1] = cv[0] = cv[1] = nrow = 0;
   }
 };
 
@@ -300,23 +300,12 @@ __device__ __forceinline__ void dma_range(const uint8_t *g, uint8_t *l, int n, i
 
 constexpr uint32_t kSegCountK = 0;
 
-// Column row of tile loci [a, b): the 64 8-locus columns it covers completely, as a bit mask,
-// laid out {mask lo, base, mask hi, base} so a lane reads the dword pair of its half with one
-// ds_read_b64; base = LDS address of tile locus 0 in the read's bytes.
-__device__ __forceinline__ uint4 col_row(int32_t a, int32_t b, uint32_t base, int T) {
-  const int32_t fc = a <= 0 ? 0 : (a + 7) >> 3;
-  const int32_t lc = (b >= T ? T : (b < 0 ? 0 : b)) >> 3;
-  auto below = [](int32_t n, int h) -> uint32_t {  // bits [0, n) of the 64, half h
-    const int32_t m = n - 32 * h;
-    return m <= 0 ? 0u : (m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u);
-  };
-  uint32_t lo = 0, hi = 0;
-  if (lc > fc) {
-    lo = below(lc, 0) & ~below(fc, 0);
-    hi = below(lc, 1) & ~below(fc, 1);
-  }
-  return make_uint4(lo, base, hi, base);
-}  // segment kinds of the auxiliary list (col_derive): count / complex
+// Column row of tile loci [a, b) (clamped to 16 bits) and base = LDS address of tile locus 0
+// in the row's bytes.
+__device__ __forceinline__ uint2 col_row(int32_t a, int32_t b, uint32_t base, int T) {
+  const int32_t sc = a > -8 ? a : -8, ec = b < T + 8 ? b : T + 8;
+  return make_uint2((uint32_t)((sc & 0xFFFF) | (ec << 16)), base);
+}
 
 // germline_cols: persistent workgroups, each over a contiguous run of tiles (XCD-local
 // neighbours: reads straddling two tiles are re-read from L2).  Per tile:
@@ -345,7 +334,9 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ __attribute__((aligned(16))) uint8_t buf[2][C::kBuf];
   __shared__ uint32_t hist[NCOL];  // per column bucket: rows starting (lo 16) / prefix-max end reaching (hi 16)
-  __shared__ __attribute__((aligned(16))) uint4 xrow[C::kExtra];  // rows of general reads' count segments
+  __shared__ __attribute__((aligned(8))) uint2 xrow[C::kExtra];  // rows of general reads' count segments
+  // byte masks of the bases [lo, hi) of an 8-locus column, lo, hi in 0..8: 0x07 per base
+  __shared__ __attribute__((aligned(8))) uint2 bmask[81];
   __shared__ unsigned n_xrow;
   __shared__ unsigned outn[2];  // records / complex items of this workgroup's partition
 
@@ -354,7 +345,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
   const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
-  uint64_t clk[5] = {0, 0, 0, 0, 0};
+  uint64_t clk[7] = {0, 0, 0, 0, 0, 0, 0};
 
   // DMA of a tile's window into buffer b, by waves 4-7 (waves 0-3 build rows meanwhile)
   auto issue = [&](const Tile &tn, int b) {
@@ -375,10 +366,44 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     if (t < 2) *reinterpret_cast<uint4 *>(buf[t] + C::kStage) = make_uint4(0u, 0u, 0u, 0u);
     if (t < 2) outn[t] = 0;
     if (t == 0) n_xrow = 0;
+    if (t < 81) {
+      const int lo = t / 9, hi = t % 9;
+      uint32_t m0 = 0, m1 = 0;
+      for (int j = 0; j < 8; ++j)
+        if (j >= lo && j < hi) {
+          if (j < 4) m0 |= 0x07u << (8 * j);
+          else m1 |= 0x07u << (8 * (j - 4));
+        }
+      bmask[t] = make_uint2(m0, m1);
+    }
   }
   LdsOut out{outn, {og.slot(0, (int)blockIdx.x, 0), og.slot(1, (int)blockIdx.x, 0)}, {og.capA[0], og.capA[1]}};
   unsigned visited = 0, amb = 0, ties = 0;
-  Tile tn = i0 < i1 ? tiles[i0] : Tile{};
+  // tile descriptors travel as one dword per lane (lanes 0-15) loaded two tiles ahead with a
+  // vector load: a scalar load would share lgkmcnt with the LDS traffic and stall it
+  auto load_desc = [&](int64_t k) -> uint32_t {
+    return (k < i1 && lane < 16) ? reinterpret_cast<const uint32_t *>(tiles + k)[lane] : 0u;
+  };
+  auto unpack = [](uint32_t v) {
+    Tile x;
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+    x.ordinal0 = (int64_t)((uint64_t)w[0] | ((uint64_t)w[1] << 32));
+    x.rb = (int64_t)((uint64_t)w[2] | ((uint64_t)w[3] << 32));
+    x.re = (int64_t)((uint64_t)w[4] | ((uint64_t)w[5] << 32));
+    x.contig = (int32_t)w[6];
+    x.L0 = (int32_t)w[7];
+    x.L1 = (int32_t)w[8];
+    x.range = (int32_t)w[9];
+    x.sb0 = (int64_t)((uint64_t)w[10] | ((uint64_t)w[11] << 32));
+    x.sbytes = (int32_t)w[12];
+    x.mcnt = (int32_t)w[13];
+    x.mb0 = (int64_t)((uint64_t)w[14] | ((uint64_t)w[15] << 32));
+    return x;
+  };
+  Tile tn = unpack(load_desc(i0));   // tile i0 (waited for once)
+  uint32_t dn2 = load_desc(i0 + 1);  // tile i0 + 1, in flight
   if (i0 < i1) issue(tn, 0);
   int it = 0;
   for (int64_t i = i0; i < i1; ++i, ++it) {
@@ -386,10 +411,13 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const Tile tl = tn;
     const int64_t tid_tile = i;
     // ---- A: this tile's DMA (issued one tile ago) has landed everywhere; next tile's DMA
+    const uint64_t tw = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t tv = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     __syncthreads();
     if (i + 1 < i1) {
-      tn = tiles[i + 1];
+      tn = unpack(dn2);  // loaded one tile ago
+      dn2 = load_desc(i + 2);
       issue(tn, b ^ 1);
     }
     const uint64_t ta = (dbg & 16) ? __builtin_readcyclecounter() : 0;
@@ -414,7 +442,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const uint32_t sa = d[4] - sb_lo;  // stage address of the base at `start`
       const uint32_t ea = d[5] - mb_lo;  // staged index of the first MD event
       const int32_t nmd = (int32_t)(info & 0xFFFFu);
-      uint4 row = make_uint4(0u, 0u, 0u, 0u);
+      uint2 row = make_uint2(0u, 0u);  // empty: s = e = 0
       if (e > L0 && s < L1) {
         const uint32_t nseg = (info >> 18) & 0xFFu;
         const bool evs_in = ea + (uint32_t)nmd + 2u * nseg <= (uint32_t)tl.mcnt;
@@ -456,16 +484,14 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const int bs = srel < 0 ? 0 : srel >> 3, bp = perel < 0 ? 0 : (perel + 7) >> 3;
       if (bs < NCOL) atomicAdd(&hist[bs], 1u);
       if (bp < NCOL) atomicAdd(&hist[bp], 1u << 16);
-      // the row's words become: d0..d3 the column row, d4 = n_md | first event << 16 | mine << 31,
+      // the row's words become: d0 d1 the column row, d4 = n_md | first event << 16 | mine << 31,
       // d5 = tile-relative start (for the MD-event pass)
-      *reinterpret_cast<uint2 *>(d) = make_uint2(row.x, row.y);
-      *reinterpret_cast<uint2 *>(d + 2) = make_uint2(row.z, row.w);
+      *reinterpret_cast<uint2 *>(d) = row;
       *reinterpret_cast<uint2 *>(d + 4) =
           make_uint2((uint32_t)nmd | (ea << 16) | (mine ? 0x80000000u : 0u), (uint32_t)srel);
     } else if (!not_col && t < nch + 8 * C::kBatch && t < C::kRowCap) {
       uint32_t *d = rows + 6 * t;
       *reinterpret_cast<uint2 *>(d) = make_uint2(0u, 0u);
-      *reinterpret_cast<uint2 *>(d + 2) = make_uint2(0u, 0u);
     }
     if (__syncthreads_or(not_col)) {  // uniform: the tile goes to the walker kernel
       if (t < NCOL) hist[t] = 0;
@@ -489,7 +515,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     constexpr int P = 8, U = C::kBatch;  // lanes per column, rows per batch (a column has ~31 rows at 30x)
     const int c = W * col;
     ColCounts cc;
-    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nnib = 0;  // nibble fields and the reads in them
+    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nv[2] = {0, 0}, nnib = 0;  // nibble / byte fields, rows in them
     auto fold = [&]() {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -497,26 +523,29 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         cc.cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
         cc.ct[h] += ntg[h] & 0x0F0F0F0Fu;
         cc.cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
-        nac[h] = ntg[h] = 0;
+        cc.cv[h] += nv[h];
+        nac[h] = ntg[h] = nv[h] = 0;
       }
       nnib = 0;
     };
-    // rows k0, k0 + P, ... of a row table at byte stride bs (rows past the range are zero
-    //   rows): the lane's half of the column mask and the base, at immediate offsets
-    const int half = col >> 5, cb = col & 31;
+    // rows k0, k0 + P, ... of a row table at byte stride bs (rows past the range are empty
+    //   rows): the bases of [max(s, c), min(e, c + 8)) via a byte-mask lookup, so rows that
+    //   cover the column only partly (read ends) are counted here too
     auto batch = [&](const uint8_t *tab, int bs, int k0, auto uu) {
       constexpr int U = decltype(uu)::value;
-      const uint8_t *rp = tab + bs * k0 + 8 * half;
+      const uint8_t *rp = tab + bs * k0;
       uint2 m[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(rp + bs * P * u);
       uint32_t a[U];
-      uint32_t nf = 0;
+      uint2 bm[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t full = (m[u].x >> cb) & 1u;
-        a[u] = full ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
-        nf += full;
+        const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu) - c, e = ((int32_t)m[u].x >> 16) - c;
+        const int32_t l = s < 0 ? 0 : (s > 8 ? 8 : s), h = e < 0 ? 0 : (e > 8 ? 8 : e);
+        const bool ov = h > l;
+        a[u] = ov ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
+        bm[u] = bmask[ov ? 9 * l + h : 0];
       }
       uint32_t w0[U], w1[U], w2[U];
 #pragma unroll
@@ -526,22 +555,24 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         w1[u] = q[1];
         w2[u] = q[2];
       }
-      if (nnib + nf > 15) fold();
-      if (cc.nf8 + nf > 255) {
+      if (nnib + U > 15) fold();
+      if (cc.nrow + U > 255) {
         fold();
         cc.flush(cnt, S, c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t s0 = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]) & 0x07070707u;
-        const uint32_t s1 = __builtin_amdgcn_alignbyte(w2[u], w1[u], a[u]) & 0x07070707u;
+        const uint32_t s0 = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]) & bm[u].x;
+        const uint32_t s1 = __builtin_amdgcn_alignbyte(w2[u], w1[u], a[u]) & bm[u].y;
         nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, s0);
         ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, s0);
         nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, s1);
         ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, s1);
+        nv[0] += bm[u].x & 0x01010101u;
+        nv[1] += bm[u].y & 0x01010101u;
       }
-      nnib += nf;
-      cc.nf8 += nf;
+      nnib += U;
+      cc.nrow += U;
     };
     if (!(dbg & 1)) {
       for (int k0 = lo + par; k0 < hi; k0 += P * U)
@@ -549,7 +580,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       // extra rows (rare): one at a time, no padding
       const int nx = (int)min(n_xrow, (unsigned)C::kExtra);
       for (int k0 = par; k0 < nx; k0 += P)
-        batch(reinterpret_cast<const uint8_t *>(xrow), 16, k0, std::integral_constant<int, 1>{});
+        batch(reinterpret_cast<const uint8_t *>(xrow), 8, k0, std::integral_constant<int, 1>{});
     }
     fold();
     // the column's totals in all eight of its lanes (quad sums, then + the half-row mirror:
@@ -564,18 +595,20 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
         return x;
       };
-      const uint32_t nq = csum(cc.nf8);
+      // a column deeper than 255 rows: each lane flushes its own counts instead
+      const uint32_t nq = csum(cc.nrow);
       if (nq > 255) {
         cc.flush(cnt, S, c);
       } else {
         const int h = par >> 2, sh = 8 * (par & 3);
         const uint32_t a0 = csum(cc.ca[0]), a1 = csum(cc.ca[1]), c0 = csum(cc.cc[0]), c1 = csum(cc.cc[1]);
         const uint32_t t0 = csum(cc.ct[0]), t1 = csum(cc.ct[1]), g0 = csum(cc.cg[0]), g1 = csum(cc.cg[1]);
+        const uint32_t v0 = csum(cc.cv[0]), v1 = csum(cc.cv[1]);
         regc[0] = ((h ? a1 : a0) >> sh) & 0xFFu;
         regc[1] = ((h ? c1 : c0) >> sh) & 0xFFu;
         regc[2] = ((h ? t1 : t0) >> sh) & 0xFFu;
         regc[3] = ((h ? g1 : g0) >> sh) & 0xFFu;
-        regc[4] = nq - regc[0] - regc[1] - regc[2] - regc[3];
+        regc[4] = (((h ? v1 : v0) >> sh) & 0xFFu) - regc[0] - regc[1] - regc[2] - regc[3];
       }
     }
     const uint64_t te = (dbg & 16) ? __builtin_readcyclecounter() : 0;
@@ -583,46 +616,13 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     //      read t - 256 (into the LDS histogram, GermSink)
     if (!(dbg & 2)) {
       GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-      // the <= 3 + 3 bytes of the two partial columns of a row over tile loci [s, e) whose
-      // base at tile locus l sits at stage address base + l: both dwords loaded, one atomic per byte
-      auto edges = [&](int32_t s, int32_t e, uint32_t base) {
-        const int32_t cs = s & ~(W - 1), ce = (e - 1) & ~(W - 1);
-        const bool ps = s != cs || e < cs + W, pe = (e & (W - 1)) != 0 || s > ce;
-        int32_t ea0 = s, ea1 = e < cs + W ? e : cs + W;  // first partial column's loci
-        int32_t eb0 = ce, eb1 = e;                       // last partial column's loci
-        if (!ps) ea1 = ea0;
-        if (!pe || ce == cs) eb1 = eb0;
-        ea0 = ea0 > 0 ? ea0 : 0;
-        ea1 = ea1 < T ? ea1 : T;
-        eb0 = eb0 > 0 ? eb0 : 0;
-        eb1 = eb1 < T ? eb1 : T;
-        const uint32_t pa = base + (uint32_t)ea0, pb = base + (uint32_t)eb0;
-        const uint32_t wa0 = st32[pa >> 2], wa1 = st32[(pa >> 2) + 1], wa2 = st32[(pa >> 2) + 2];
-        const uint32_t wb0 = st32[pb >> 2], wb1 = st32[(pb >> 2) + 1], wb2 = st32[(pb >> 2) + 2];
-        const uint32_t a0 = __builtin_amdgcn_alignbyte(wa1, wa0, pa), a1 = __builtin_amdgcn_alignbyte(wa2, wa1, pa);
-        const uint32_t b0 = __builtin_amdgcn_alignbyte(wb1, wb0, pb), b1 = __builtin_amdgcn_alignbyte(wb2, wb1, pb);
-        // at most W - 1 bytes per side: fixed, predicated steps (no data-dependent loop)
-#pragma unroll
-        for (int j = 0; j < W - 1; ++j) {
-          const uint32_t ba = ((j < 4 ? a0 : a1) >> (8 * (j & 3))) & 0xFFu;
-          const uint32_t bb = ((j < 4 ? b0 : b1) >> (8 * (j & 3))) & 0xFFu;
-          if (ea0 + j < ea1) sink.base1_clean(ea0 + j, ba);
-          if (eb0 + j < eb1) sink.base1_clean(eb0 + j, bb);
-        }
-      };
-      if (general && !(dbg & 32)) {  // segments: ends of the count segments, complex loci
+      if (general) {  // segments: the complex loci (count segments are column rows)
         for (int32_t q = 0; q < my_nseg; ++q) {
           const uint32_t w0 = evs[my_seg + 2 * q], w1 = evs[my_seg + 2 * q + 1];
           const int32_t a = my_s + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
-          if (b <= 0 || a >= T) continue;
-          if ((w1 >> 16) == kSegCountK) {
-            edges(a, b, (uint32_t)my_base + (w1 & 0xFFFFu) - (uint32_t)a);
-          } else {
-            for (int32_t l = a > 0 ? a : 0; l < (b < T ? b : T); ++l) sink.complex_i(l);
-          }
+          if (b <= 0 || a >= T || (w1 >> 16) == kSegCountK) continue;
+          for (int32_t l = a > 0 ? a : 0; l < (b < T ? b : T); ++l) sink.complex_i(l);
         }
-      } else if (mine && !(dbg & 32)) {
-        edges(my_s, my_e, (uint32_t)my_base);
       }
       const int k = t - C::kMeta;
       if (k >= 0 && k < nch && !(dbg & 64)) {
@@ -660,6 +660,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       clk[2] += tf - te;   // per-read pass + barrier
       clk[3] += now - tf;  // decision
       clk[4] += 1;
+      clk[5] += tv - tw;   // vmcnt wait at A
+      clk[6] += ta - tv;   // barrier A + next DMA issue
     }
   }
   add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
@@ -674,6 +676,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     atomicAdd(&ctr->prof[2], (unsigned long long)clk[2]);
     atomicAdd(&ctr->prof[3], (unsigned long long)clk[3]);
     atomicAdd(&ctr->prof[7], (unsigned long long)clk[4]);
+    atomicAdd(&ctr->prof[4], (unsigned long long)clk[5]);
+    atomicAdd(&ctr->prof[5], (unsigned long long)clk[6]);
   }
 }
 
