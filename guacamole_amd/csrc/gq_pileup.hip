@@ -1139,6 +1139,7 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
                      (const Tile *)c->tiles.p, tiles, R.seq, R.cdesc, R.cev, R.n_samples, p->threshold, p->emit_ref,
                      p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // column kernel | walker kernel
   const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
   hipLaunchKernelGGL((germline_walk<ColsCfg::kT>), dim3(wblocks), dim3(kBlock), 0, c->stream,
                      (const Tile *)c->tiles.p, (const int32_t *)c->slow.p, R, p->threshold, p->emit_ref,
@@ -1310,8 +1311,11 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   float ms = 0;
   (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
   c->timings.plan_ms = ms;
-  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[5]);
   c->timings.pileup_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[2]);
+  c->timings.walk_ms = ms;
+  c->timings.walk_tiles = (int64_t)hc.n_slow;
   (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
   c->timings.complex_ms = ms;
   (void)hipEventElapsedTime(&ms, c->ev[3], c->ev[4]);

@@ -64,7 +64,8 @@ class gq_counts(C.Structure):
 class gq_timings(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("pileup_ms", C.c_float), ("complex_ms", C.c_float),
                 ("finalize_ms", C.c_float), ("total_ms", C.c_float), ("pileup_launches", C.c_int64),
-                ("tiles", C.c_int64), ("host_ms", C.c_float), ("marshal_ms", C.c_float)]
+                ("tiles", C.c_int64), ("host_ms", C.c_float), ("marshal_ms", C.c_float),
+                ("walk_ms", C.c_float), ("walk_tiles", C.c_int64)]
 
 
 class gq_somatic_params(C.Structure):

@@ -148,6 +148,9 @@ typedef struct {
   int64_t tiles;
   float host_ms;     /* host wall time of the whole call (enqueue + waits + marshalling) */
   float marshal_ms;  /* host time spent building the output arrays                      */
+  float walk_ms;     /* germline: the walker kernel over the tiles the column kernel     */
+                     /* handed over (pileup_ms is then the column kernel alone)          */
+  int64_t walk_tiles;
 } gq_timings;
 
 const char *gq_version(void);
