@@ -151,61 +151,23 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
       push(rr);
     }
     if (general) {
-      // GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles.  Allele
-      // (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of Allele(ref, alt)
-      // for one ref is the alt byte order A < C < G < N < T, i.e. the categories 0, 1, 3, 4, 2.
-      // Sorting keys descending = sortBy(-count), ties canonical.
-      uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
-      int npass = 0;
-#pragma unroll
-      for (int rank = 0; rank < 5; ++rank) {
-        const int cat = (0x24310 >> (4 * rank)) & 0xF;
-        const uint32_t cc = c[cat];
-        if (cc == 0 || !passes(cc, depth)) continue;
-        ++npass;
-        uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
-        if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
-        if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
-        if (key > k2) { k2 = key; }
-      }
-      auto key_base = [](uint32_t key) -> uint8_t {
-        const int rank = 255 - (int)(key & 0xFFu);
-        return cat_base((0x24310 >> (4 * rank)) & 0xF);
-      };
-      const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
-      if (tie) ++ties;
-      const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
-      auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
-        CallRec rr;
-        rr.key = (ord << 12) | (uint64_t)sub;
-        rr.contig = tl.contig;
-        rr.pos = pos;
-        rr.sample = 0;
-        rr.gt0 = g0;
-        rr.gt1 = g1;
-        rr.flags = fl;
-        rr.ref_len = 1;
-        rr.alt_len = alt_sym ? 5 : 1;
-        rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
-        return rr;
-      };
-      const uint8_t b0 = key_base(k0), b1 = key_base(k1);
-      if (npass == 0) {
-        if (emit_no_call) push(mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0));
-      } else if (npass == 1 && b0 == ref) {
-        if (emit_ref) push(mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0));
-      } else if (npass == 1) {
-        push(mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0));
-      } else {
-        const bool v1 = b0 != ref, v2 = b1 != ref;
-        if (v1 != v2) {
-          push(mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0));
-        } else if (v1 && v2) {
-          push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0));
-          push(mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1));
-        }
-        // two non-variant single-base alleles cannot occur (all Match alleles share ref)
-      }
+      // a variant candidate: its counts travel in a placeholder record pair (two slots), which
+      // germline_expand turns into the 0-2 Genotype records (GermlineThresholdCaller.scala:100-177)
+      // after the kernel: the long case split stays out of this loop
+      CallRec rr;
+      rr.key = ord << 12;
+      rr.contig = tl.contig;
+      rr.pos = pos;
+      rr.sample = 0;
+      rr.gt0 = ref;
+      rr.gt1 = 0;
+      rr.flags = kCandidate;
+      rr.ref_len = (uint16_t)c[4];
+      rr.alt_len = 0;
+      rr.allele = (uint64_t)c[0] | ((uint64_t)c[1] << 16) | ((uint64_t)c[2] << 32) | ((uint64_t)c[3] << 48);
+      push(rr);
+      rr.flags = kCandidateSlot;
+      push(rr);
     }
     // reserve + write records (wave-aggregated, in the writer's partition)
     const unsigned long long base = out.reserve(0, nout);
@@ -216,6 +178,100 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
     if (to_complex && cb < out.cap[1])
       cplx[out.base[1] + cb] = ComplexItem{(int32_t)tile_id, L0 + i, wide ? 1 : 0};
   }
+}
+
+// The variant candidates of germline_decide -> Genotype records, one thread per record slot
+// (GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles; counts < 2^16).
+// Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of Allele(ref, alt)
+// for one ref is the alt byte order A < C < G < N < T, i.e. the categories 0, 1, 3, 4, 2.
+// Sorting keys descending = sortBy(-count), ties canonical.  Unused slots get a key past
+// every ordinal (dead_key) and are counted in n_dead; they sort behind the live records.
+__global__ void germline_expand(CallRec *__restrict__ recs, Counters *ctr, OutGeom og, int threshold,
+                                int emit_ref, int emit_no_call, uint64_t dead_key) {
+  const unsigned long long n = ctr->n_rec;
+  const int64_t thr1 = (int64_t)threshold + 1;
+  auto passes = [=](uint32_t count, uint32_t depth) { return (int64_t)count * 100 >= thr1 * (int64_t)depth; };
+  constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                               ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+  unsigned dead = 0, ties = 0;
+  (void)n;
+  // partition by partition (block per partition): its slots [0, kept count)
+  for (int p = blockIdx.x; p < kParts; p += gridDim.x) {
+   const unsigned long long cnt = ctr->part_off[0][p + 1] - ctr->part_off[0][p];
+   for (unsigned long long k = threadIdx.x; k < cnt; k += blockDim.x) {
+    const unsigned long long slot = og.slot(0, p, k);
+    const CallRec cand = recs[slot];
+    if (cand.flags != kCandidate) continue;  // an ordinary record, or the second slot of a pair
+    const uint32_t c[5] = {(uint32_t)(cand.allele & 0xFFFFu), (uint32_t)((cand.allele >> 16) & 0xFFFFu),
+                           (uint32_t)((cand.allele >> 32) & 0xFFFFu), (uint32_t)(cand.allele >> 48), cand.ref_len};
+    const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4];
+    const uint8_t ref = cand.gt0;
+    uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
+    int npass = 0;
+#pragma unroll
+    for (int rank = 0; rank < 5; ++rank) {
+      const int cat = (0x24310 >> (4 * rank)) & 0xF;
+      const uint32_t cc = c[cat];
+      if (cc == 0 || !passes(cc, depth)) continue;
+      ++npass;
+      uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
+      if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
+      if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
+      if (key > k2) { k2 = key; }
+    }
+    auto key_base = [](uint32_t key) -> uint8_t {
+      const int rank = 255 - (int)(key & 0xFFu);
+      return cat_base((0x24310 >> (4 * rank)) & 0xF);
+    };
+    const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
+    if (tie) ++ties;
+    const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
+    CallRec out[2];
+    int nout = 0;
+    auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
+      CallRec rr = cand;
+      rr.key = cand.key | (uint64_t)sub;
+      rr.gt0 = g0;
+      rr.gt1 = g1;
+      rr.flags = fl;
+      rr.ref_len = 1;
+      rr.alt_len = alt_sym ? 5 : 1;
+      rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
+      out[nout++] = rr;
+    };
+    const uint8_t b0 = key_base(k0), b1 = key_base(k1);
+    if (npass == 0) {
+      if (emit_no_call) mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0);
+    } else if (npass == 1 && b0 == ref) {
+      if (emit_ref) mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0);
+    } else if (npass == 1) {
+      mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0);
+    } else {
+      const bool v1 = b0 != ref, v2 = b1 != ref;
+      if (v1 != v2) {
+        mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0);
+      } else if (v1 && v2) {
+        mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0);
+        mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1);
+      }
+      // two non-variant single-base alleles cannot occur (all Match alleles share ref)
+    }
+    // the pair's two slots are consecutive in the partition (reserved together)
+    for (int q = 0; q < 2; ++q) {
+      if (q < nout) {
+        recs[slot + q] = out[q];
+      } else {
+        CallRec d = cand;
+        d.key = dead_key;
+        d.flags = 0;
+        recs[slot + q] = d;
+        ++dead;
+      }
+    }
+   }
+  }
+  if (dead) atomicAdd(&ctr->n_dead, (unsigned long long)dead);
+  if (ties) atomicAdd(&ctr->spread[2][threadIdx.x & (kSpread - 1)], (unsigned long long)ties);
 }
 
 // Run counters (visited / ambiguous / tie loci) of a workgroup, added once at its end.

@@ -45,6 +45,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   int pad;
   long long err_pos;
   unsigned long long n_slow;       // tiles germline_cols handed to germline_walk
+  unsigned long long n_dead;       // record slots germline_expand left unused
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
   // per-tile run counters, spread over kSpread addresses (summed on the host)
   unsigned long long spread[3][64];

@@ -90,6 +90,9 @@ struct CallRec {
   uint64_t allele;  // inline bytes (ref then alt) if ref_len + alt_len <= 8, else pool offset
 };
 static_assert(sizeof(CallRec) == 32, "CallRec layout");
+// CallRec.flags of a germline variant candidate (counts in allele / ref_len, expanded by
+// germline_expand) and of the second slot reserved with it
+constexpr uint8_t kCandidate = 0xC0, kCandidateSlot = 0xC1;
 
 struct ComplexItem {
   int32_t tile;

@@ -1200,6 +1200,12 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
                        (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
+    {  // variant candidates -> records; unused slots get a key behind every ordinal
+      const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
+      hipLaunchKernelGGL(germline_expand, dim3(1024), dim3(kBlock), 0, c->stream, (CallRec *)c->recs.p, ctr, og,
+                         p->threshold, p->emit_ref, p->emit_no_call, dead_key);
+      HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1240,8 +1246,9 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   }
   // ---- sort records by key (output order), then build the host result image on device:
   //      one D2H copy of [header | SoA arrays | allele pool] instead of per-record marshalling
-  const int64_t n = (int64_t)hc.n_rec;
-  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  const int64_t n_all = (int64_t)hc.n_rec;         // record slots, including unused candidate slots
+  const int64_t n = n_all - (int64_t)hc.n_dead;    // records (the unused slots sort last)
+  const size_t nn = (size_t)std::max<int64_t>(n_all, 1);
   HIP_TRY(c->keys.ensure(nn * 8));
   HIP_TRY(c->keys_sorted.ensure(nn * 8));
   HIP_TRY(c->idx.ensure(nn * 8));
@@ -1249,23 +1256,23 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   const CallsLayout lay = calls_layout(n, (int64_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
   HIP_TRY(c->image.ensure(lay.bytes));
   if (n > 0) {
-    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock), nb_all = (unsigned)((n_all + kBlock - 1) / kBlock);
     // keys and record slots of the partitioned records, densely
-    hipLaunchKernelGGL(gather_keys, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const Counters *)c->counters.p, og, n, (uint64_t *)c->keys.p, (int32_t *)c->idx.p);
+    hipLaunchKernelGGL(gather_keys, dim3(nb_all), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const Counters *)c->counters.p, og, n_all, (uint64_t *)c->keys.p, (int32_t *)c->idx.p);
     HIP_TRY(hipGetLastError());
     int end_bit = 12;
     while (end_bit < 64 && ((uint64_t)pl.n_loci >> (end_bit - 12)) != 0) ++end_bit;
     size_t tmp = 0, tmp2 = 0;
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t *)c->keys.p, (uint64_t *)c->keys_sorted.p,
-                                               (const int32_t *)c->idx.p, (int32_t *)c->idx_sorted.p, (int)n, 0,
+                                               (const int32_t *)c->idx.p, (int32_t *)c->idx_sorted.p, (int)n_all, 0,
                                                end_bit, c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p, (int)n,
                                              c->stream));
     HIP_TRY(c->sort_tmp.ensure(std::max(tmp, tmp2)));
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (const uint64_t *)c->keys.p,
                                                (uint64_t *)c->keys_sorted.p, (const int32_t *)c->idx.p,
-                                               (int32_t *)c->idx_sorted.p, (int)n, 0, end_bit, c->stream));
+                                               (int32_t *)c->idx_sorted.p, (int)n_all, 0, end_bit, c->stream));
     // allele byte lengths in output order -> exclusive offsets into the pool
     hipLaunchKernelGGL(calls_lengths, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
                        (const int32_t *)c->idx_sorted.p, n, (int64_t *)c->idx.p);
