@@ -116,3 +116,84 @@ def test_cli_germline_vcf_and_somatic_json(tmp_path):
                  fixture("normal.chr20.tough.sam"), "--out", js, "--min-tumor-read-depth", "8"]) == 0
     rows = [json.loads(l) for l in open(js)]
     assert rows and all(r["alleles"] == ["Ref", "Alt"] and r["readDepth"] >= 8 for r in rows)
+
+
+def test_synthetic_column_path_dense_outputs(gpu_ctx):
+    """emit_ref / emit_no_call through the column kernel (HomRef / NoCall rows inline,
+    variant candidates through germline_expand); the column kernel keeps nearly every tile."""
+    g = generate(60_000, 30, seed=7, indel_rate=3e-4)
+    rs = g.to_read_set()
+    loci = _loci(rs)
+    for t, er, enc in ((8, True, False), (30, False, True), (0, True, True)):
+        got = germline_threshold_reads(gpu_ctx, rs, loci, t, er, enc)
+        want = O.germline_threshold(rs, loci, t, er, enc)
+        assert got == want, (t, er, enc)
+        tm = gpu_ctx.timings()
+        assert tm["walk_tiles"] <= 0.05 * tm["tiles"], tm
+
+
+def test_chrm_subsampled_column_path(gpu_ctx, chrm):
+    """Real reads (29-80 bp, real MD tags) at a depth whose tiles fit the column kernel's stage
+    (every 8th read of chrM.sorted.bam: about 18x)."""
+    from guacamole_amd.reads import ReadSet
+    sub = chrm.subset(np.arange(0, chrm.n, 8))
+    loci = _loci(sub)
+    for t, er, enc in ((8, False, False), (0, True, True)):
+        got = germline_threshold_reads(gpu_ctx, sub, loci, t, er, enc)
+        want = O.germline_threshold(sub, loci, t, er, enc)
+        ge, ga = _split(got)
+        we, wa = _split(want)
+        assert ge == we
+        assert sorted(set(r[1] for r in ga)) == sorted(set(r[1] for r in wa))
+    tm = gpu_ctx.timings()
+    assert tm["walk_tiles"] < tm["tiles"] // 2, tm  # most tiles through the column kernel
+
+
+class _DeviceArray:
+    """A numpy array copied to device memory with the HIP runtime the library links (hipMalloc /
+    hipMemcpy through ctypes), exposing what native._ptr needs."""
+    _hip = None
+
+    def __init__(self, a):
+        import ctypes as C
+        if _DeviceArray._hip is None:
+            _DeviceArray._hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+        a = np.ascontiguousarray(a)
+        self.shape, self.dtype, self.nbytes = a.shape, a.dtype, max(a.nbytes, 16)
+        self.ptr = C.c_void_p()
+        assert _DeviceArray._hip.hipMalloc(C.byref(self.ptr), C.c_size_t(self.nbytes)) == 0
+        assert _DeviceArray._hip.hipMemcpy(self.ptr, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), 1) == 0
+
+    def data_ptr(self):
+        return self.ptr.value
+
+    def __del__(self):
+        if self.ptr and _DeviceArray._hip is not None:
+            _DeviceArray._hip.hipFree(self.ptr)
+
+
+def test_wrapped_device_reads_unordered_pool(gpu_ctx):
+    """gq_reads_wrap_device over device buffers whose sequence pool is NOT in read order: the
+    column kernel's per-read stage check sends such reads' tiles to the walker, results equal."""
+    g = generate(40_000, 30, seed=11, indel_rate=3e-4)
+    a = {k: np.asarray(v) for k, v in g.arrays.items()}
+    n = a["start"].shape[0]
+    # reverse the pool: read r's bytes move to the mirrored offset
+    L = a["seq_len"].astype(np.int64)
+    total = int(a["seq"].shape[0])
+    new_off = total - a["seq_off"] - L
+    seq2 = np.empty_like(a["seq"])
+    qual2 = np.empty_like(a["qual"])
+    for r in range(n):
+        o, no, l = int(a["seq_off"][r]), int(new_off[r]), int(L[r])
+        seq2[no:no + l] = a["seq"][o:o + l]
+        qual2[no:no + l] = a["qual"][o:o + l]
+    host = dict(a, seq=seq2, qual=qual2, seq_off=new_off.astype(np.int64))
+    dev = {k: (_DeviceArray(v) if v.ndim else int(v)) for k, v in host.items()}
+    dr = gpu_ctx.wrap_device(dev)
+    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([39_999], np.int64), np.array([0], np.int64))
+    got = gpu_ctx.germline_threshold(dr, loci, 8)
+    ref = gpu_ctx.germline_threshold(gpu_ctx.upload(a), loci, 8)
+    assert got.tuples(g.contig_names) == ref.tuples(g.contig_names)
+    want = O.germline_threshold(g.to_read_set(), loci, 8)
+    assert ref.tuples(g.contig_names) == want
