@@ -85,6 +85,7 @@ def main() -> int:
         step()
     barrier()
     pileup_ms, walk_ms, total_ms, host_ms, marshal_ms = [], [], [], [], []
+    stage_ms = {"plan_ms": [], "complex_ms": [], "finalize_ms": []}
     walk_frac = []
     t = time.perf_counter()
     for _ in range(args.steps):
@@ -92,6 +93,8 @@ def main() -> int:
         tm = ctx.timings()
         pileup_ms.append(tm["pileup_ms"])
         walk_ms.append(tm["walk_ms"])
+        for k in stage_ms:
+            stage_ms[k].append(tm[k])
         walk_frac.append(tm["walk_tiles"] / max(1, tm["tiles"]))
         total_ms.append(tm["total_ms"])
         host_ms.append(tm["host_ms"])
@@ -154,6 +157,7 @@ def main() -> int:
                      "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
         "device_total_ms": float(np.mean(total_ms)),
+        "device_stages_ms": {k: float(np.mean(v)) for k, v in stage_ms.items()},
         "host_call_ms": float(np.mean(host_ms)),
         "host_marshal_ms": float(np.mean(marshal_ms)),
         "calls": len(calls),
