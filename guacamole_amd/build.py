@@ -47,6 +47,19 @@ def build_synth(force: bool = False) -> str:
     return SYNTH_LIB
 
 
+INGEST_SRC = os.path.join(CSRC, "gq_ingest.cpp")
+INGEST_LIB = os.path.join(LIB_DIR, "libgqingest.so")
+
+
+def build_ingest(force: bool = False) -> str:
+    """Host read ingest (BGZF/BAM decode, MD events), g++ -O3 -pthread, zlib."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _stale(INGEST_LIB, [INGEST_SRC, os.path.join(ROOT, "include", "gqingest.h")]):
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", INGEST_LIB,
+                               INGEST_SRC, "-lz"])
+    return INGEST_LIB
+
+
 def build_oracle() -> str:
     d = os.path.join(ROOT, "oracle")
     subprocess.check_call(["make", "-s", "-C", d])

@@ -10,15 +10,16 @@ Host side of the path; restates the reference's loading + filtering semantics
 * ``ReadSet.mappedReads``                                ReadSet.scala:47-53
 * ``MappedRead.end = start + paddedReferenceLength``      reads/MappedRead.scala:87
 
-The BAM decoder (BGZF = concatenated gzip members, then BAM records) is
-written here from the SAM/BAM specification; it is ingest plumbing (SURVEY §8f
-rank 1 "next"), kept simple and exact rather than fast.
+BAM input goes through the native loader (``ingest.load_bam``, libgqingest: parallel
+BGZF inflate + record decode).  ``_load_bam_py`` states the same
+rules in Python and is the checker of the native loader in tests/test_ingest.py.
 """
 from __future__ import annotations
 
 import gzip
 import io
 import struct
+import zlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -251,9 +252,14 @@ def load_reads(path: str, filters: InputFilters = InputFilters()) -> ReadSet:
     with open(path, "rb") as fh:
         head = fh.read(2)
     if head == b"\x1f\x8b":  # BGZF (BAM) or a gzip-compressed SAM
-        with gzip.open(path, "rb") as fh:
-            if fh.read(4) == b"BAM\x01":
-                return _load_bam(path, filters)
+        try:
+            with gzip.open(path, "rb") as fh:
+                is_bam = fh.read(4) == b"BAM\x01"
+        except (OSError, EOFError, zlib.error):
+            is_bam = True  # a damaged first block: the BAM decoder names the fault
+        if is_bam:
+            from .ingest import load_bam  # native (libgqingest); raises if not built
+            return load_bam(path, filters)
     return _load_sam(path, filters)
 
 
@@ -314,7 +320,8 @@ def _load_sam(path: str, filters: InputFilters) -> ReadSet:
     return _finish(b, contig_names, contig_lengths, samples)
 
 
-def _load_bam(path: str, filters: InputFilters) -> ReadSet:
+def _load_bam_py(path: str, filters: InputFilters) -> ReadSet:
+    """The same BAM rules in Python: the checker of the native loader (tests/test_ingest.py)."""
     with gzip.open(path, "rb") as fh:
         data = fh.read()
     if data[:4] != b"BAM\x01":

@@ -84,27 +84,13 @@ def md_events(md: bytes, start: int, cigar_ops: List[Tuple[int, int]]) -> Tuple[
 
 
 def pack(rs: ReadSet) -> Dict[str, np.ndarray]:
-    """Build the gq_reads host arrays for a ReadSet (cached on the ReadSet)."""
+    """Build the gq_reads host arrays for a ReadSet (cached on the ReadSet).  MD events come
+    from libgqingest (gq_md_count / gq_md_fill); md_events above is their Python statement,
+    the checker in tests/test_ingest.py."""
     if rs._gq is not None:
         return rs._gq
-    n = rs.n
-    ev_lists, n_md, n_mm = [], np.zeros(n, np.int32), np.zeros(n, np.uint16)
-    for i in range(n):
-        if rs.md_len[i] < 0:
-            ev_lists.append([])
-            n_md[i] = -1
-            continue
-        ops = [(int(c) & 15, int(c) >> 4) for c in rs.cigar[rs.cigar_off[i]:rs.cigar_off[i] + rs.n_cigar[i]]]
-        md = rs.md[rs.md_off[i]:rs.md_off[i] + rs.md_len[i]].tobytes()
-        ev, mm = md_events(md, int(rs.start[i]), ops)
-        ev_lists.append(ev)
-        n_md[i] = len(ev)
-        n_mm[i] = min(mm, 65535)
-    md_off = np.zeros(n, np.int64)
-    lens = np.maximum(n_md, 0).astype(np.int64)
-    if n:
-        md_off[1:] = np.cumsum(lens)[:-1]
-    md_ev = np.array([e for lst in ev_lists for e in lst], dtype=np.uint32)
+    from .ingest import md_events as native_md_events  # libgqingest; raises if not built
+    n_md, n_mm, md_off, md_ev = native_md_events(rs.cigar_off, rs.n_cigar, rs.cigar, rs.md_off, rs.md_len, rs.md)
     out = assemble(rs.contig, rs.start, rs.end, rs.mapq, rs.flags, rs.sample, rs.seq_off, rs.seq_len, rs.seq,
                    rs.qual, rs.cigar_off, rs.n_cigar, rs.cigar, md_off, n_md, n_mm, md_ev, len(rs.contig_names),
                    max(1, len(rs.sample_names)))
