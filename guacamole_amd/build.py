@@ -43,7 +43,8 @@ def build_synth(force: bool = False) -> str:
     """Host-side synthetic read generator (bench / test data), g++ -O3 -pthread."""
     os.makedirs(LIB_DIR, exist_ok=True)
     if force or _stale(SYNTH_LIB, [SYNTH_SRC]):
-        subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", SYNTH_LIB, SYNTH_SRC])
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", SYNTH_LIB, SYNTH_SRC,
+                               "-lz"])
     return SYNTH_LIB
 
 
@@ -56,7 +57,7 @@ def build_ingest(force: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     if force or _stale(INGEST_LIB, [INGEST_SRC, os.path.join(ROOT, "include", "gqingest.h")]):
         subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", INGEST_LIB,
-                               INGEST_SRC, "-lz"])
+                               INGEST_SRC, "-lz", "-ldl"])
     return INGEST_LIB
 
 

@@ -14,9 +14,12 @@
 // Layout of the work: the file is mapped; BGZF block boundaries are found by hopping over
 // BSIZE fields; every block is inflated (raw deflate) in parallel straight into its slot of
 // one contiguous buffer (ISIZE prefix sums), CRC32 checked.  Record boundaries are a
-// sequential hop over block_size fields; records are then decoded in parallel chunks into
-// chunk-local SoA vectors, and gq_bam_fill copies the chunks into the caller's arrays
-// (chunk prefix sums when the file is coordinate-sorted, a stable permutation otherwise).
+// sequential hop over block_size fields.  gq_bam_scan parses and filters the records in
+// parallel chunks and keeps, per kept read, its record offset, MD position and read group;
+// gq_bam_fill decodes the kept records straight into the caller's arrays (pool offsets from
+// a per-block pre-pass), in file order when the file is coordinate-sorted and through a
+// stable permutation otherwise.
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -168,34 +171,56 @@ gqi_status inflate_stream(const uint8_t *p, int64_t n, std::vector<uint8_t> &out
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
-struct Chunk {  // decoded records of one range of the file, chunk-local pools
-  std::vector<int32_t> contig, rg, seq_len, n_cigar, md_len, name_len;
-  std::vector<int64_t> start, end;
-  std::vector<uint8_t> mapq, flags, seq, qual, md, names;
-  std::vector<uint32_t> cigar;
+struct Kept {  // a record that passed the filters
+  int64_t rec;    // offset of its block_size field in the inflated stream
+  int64_t md_at;  // offset of its MD value, -1: no MD tag
+  int32_t md_len;
+  int32_t rg;     // chunk-local RG id (global after gq_bam_scan), -1: none
+};
+
+struct Chunk {  // the records of one range of the file
+  std::vector<Kept> kept;
   std::vector<std::string> rg_vals;  // chunk-local RG values, first appearance order
-  std::vector<int32_t> rg_map;       // chunk-local -> global
-  std::vector<int64_t> rg_first;     // chunk-local read index of each RG value's first read
-  int64_t none_first = -1;           // ... and of the first read without an RG tag
-  int64_t err_rec = -1;              // first failing record (file order) of this chunk
+  std::vector<int64_t> rg_first;     // chunk-local kept index of each RG value's first read
+  int64_t none_first = -1;           // ... and of the first kept read without an RG tag
+  int64_t seq = 0, cigar = 0, md = 0, names = 0;  // pool totals of the kept reads
+  bool sorted = true;                // kept reads in (contig, start) order within the chunk
+  int32_t c0 = 0, c1 = 0;            // (contig, start) of the first and last kept read
+  int64_t s0 = 0, s1 = 0;
   gqi_status err = GQI_OK;
   std::string err_msg;
-  // prefix offsets inside the chunk (gq_bam_fill)
-  std::vector<int64_t> seq_o, cig_o, md_o, name_o;
 };
 
 struct gq_bam {
   int fd = -1;
   const uint8_t *map = nullptr;
   size_t map_len = 0;
-  std::vector<uint8_t> data;  // inflated BAM stream
+  struct Bytes {  // inflated BAM stream: anonymous mapping on huge pages, faulted in by the inflate threads
+    uint8_t *p = nullptr;
+    int64_t n = 0;
+    size_t cap = 0;
+    bool alloc(int64_t len) {
+      cap = (size_t)std::max<int64_t>(len, 1);
+      void *m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m == MAP_FAILED) return false;
+      madvise(m, cap, MADV_HUGEPAGE);
+      p = (uint8_t *)m;
+      n = len;
+      return true;
+    }
+    ~Bytes() {
+      if (p) munmap(p, cap);
+    }
+    uint8_t *data() { return p; }
+    const uint8_t *data() const { return p; }
+    size_t size() const { return (size_t)n; }
+  } data;
   std::string text;
   std::vector<std::string> contig_names;
   std::vector<int64_t> contig_lengths;
   int64_t rec0 = 0;  // first alignment record
   // last scan
-  std::vector<Chunk> chunks;
-  std::vector<int64_t> chunk_read0;  // first output read of each chunk (file order)
+  std::vector<Kept> kept;  // every kept read, file order
   std::vector<std::string> rgs;
   std::vector<int64_t> rg_first;  // [1 + n_rg]: first kept read (file order) without RG, with RG k
   std::vector<int64_t> order;  // output read -> file-order read (empty: already sorted)
@@ -204,6 +229,30 @@ struct gq_bam {
 };
 
 namespace {
+
+// Raw-deflate backend for BGZF blocks: libdeflate when the system has it (a whole-buffer
+// decoder, ~2x zlib's inflate here, and a folded CRC32), else zlib.  Both decode the same
+// bytes; the choice only changes speed.  libdeflate ships without a header in this image,
+// so its four entry points (stable since libdeflate 1.0) are resolved with dlsym.
+struct Deflate {
+  void *(*alloc)() = nullptr;
+  int (*dec)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+  uint32_t (*crc)(uint32_t, const void *, size_t) = nullptr;
+};
+const Deflate &deflate_lib() {
+  static const Deflate lz = []() {
+    Deflate x;
+    if (getenv("GQ_INGEST_ZLIB")) return x;
+    void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.alloc = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+    x.dec = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_deflate_decompress");
+    x.crc = (uint32_t(*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
+    if (!x.alloc || !x.dec || !x.crc) x = Deflate();
+    return x;
+  }();
+  return lz;
+}
 
 gqi_status inflate_bgzf(gq_bam *b, int nt) {
   const uint8_t *p = b->map;
@@ -231,25 +280,42 @@ gqi_status inflate_bgzf(gq_bam *b, int nt) {
     blocks.push_back(k);
     off += bsize;
   }
-  if (!bgzf) return inflate_stream(p, n, b->data);
-  b->data.resize((size_t)out);
+  if (!bgzf) {
+    std::vector<uint8_t> v;
+    const gqi_status s = inflate_stream(p, n, v);
+    if (s != GQI_OK) return s;
+    if (!b->data.alloc((int64_t)v.size())) return fail(GQI_E_NOMEM, "inflated stream of %zu bytes", v.size());
+    memcpy(b->data.p, v.data(), v.size());
+    return GQI_OK;
+  }
+  if (!b->data.alloc(out)) return fail(GQI_E_NOMEM, "inflated stream of %lld bytes", (long long)out);
+  const Deflate &lz = deflate_lib();
   std::atomic<int64_t> bad{-1};
   parallel_for((int64_t)blocks.size(), nt, [&](int64_t i) {
     const Block &k = blocks[i];
     uint8_t *dst = b->data.data() + k.out_off;
-    z_stream z;
-    memset(&z, 0, sizeof(z));
-    bool ok = inflateInit2(&z, -15) == Z_OK;
-    if (ok) {
-      z.next_in = const_cast<uint8_t *>(p + k.in_off);
-      z.avail_in = (uInt)k.in_len;
-      z.next_out = dst;
-      z.avail_out = k.isize;
-      const int rc = inflate(&z, Z_FINISH);
-      ok = rc == Z_STREAM_END && z.total_out == k.isize;
-      inflateEnd(&z);
+    bool ok;
+    if (lz.dec) {  // libdeflate: whole-buffer decoder, no stream state
+      thread_local void *d = nullptr;
+      if (!d) d = lz.alloc();
+      size_t got = 0;
+      ok = d && lz.dec(d, p + k.in_off, (size_t)k.in_len, dst, k.isize, &got) == 0 && got == k.isize;
+      if (ok) ok = lz.crc(0, dst, k.isize) == k.crc;
+    } else {
+      z_stream z;
+      memset(&z, 0, sizeof(z));
+      ok = inflateInit2(&z, -15) == Z_OK;
+      if (ok) {
+        z.next_in = const_cast<uint8_t *>(p + k.in_off);
+        z.avail_in = (uInt)k.in_len;
+        z.next_out = dst;
+        z.avail_out = k.isize;
+        const int rc = inflate(&z, Z_FINISH);
+        ok = rc == Z_STREAM_END && z.total_out == k.isize;
+        inflateEnd(&z);
+      }
+      if (ok) ok = (uint32_t)crc32(0L, dst, k.isize) == k.crc;
     }
-    if (ok) ok = (uint32_t)crc32(0L, dst, k.isize) == k.crc;
     if (!ok) {
       int64_t cur = bad.load();
       while ((cur < 0 || i < cur) && !bad.compare_exchange_weak(cur, i)) {
@@ -310,44 +376,121 @@ bool loci_intersect(const gq_bam_filters *f, int32_t contig, int64_t s, int64_t 
   return k < b1 && f->loci_start[k] < e;
 }
 
-// decode records [r0, r1) of the record-offset list into c
-void decode_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0, int64_t r1, const gq_bam_filters *f,
-                  Chunk &c) {
+// plausible alignment record at o (every length field consistent with block_size)?
+inline bool record_at(const uint8_t *d, int64_t n, int64_t o, int32_t n_ref) {
+  if (o + 40 > n) return false;
+  const int32_t bs = rd32s(d + o);
+  if (bs < 32 || o + 4 + bs > n) return false;
+  const uint8_t *p = d + o + 4;
+  const int32_t ref_id = rd32s(p), pos = rd32s(p + 4), l_seq = rd32s(p + 16), next_ref = rd32s(p + 20);
+  const uint32_t l_name = p[8], n_cig = rd16(p + 12);
+  if (ref_id < -1 || ref_id >= n_ref || next_ref < -1 || next_ref >= n_ref || pos < -1 || l_seq < 0 || l_name < 1)
+    return false;
+  if (32 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + l_seq > bs) return false;
+  return p[32 + l_name - 1] == 0;
+}
+
+// Record boundaries: a hop over block_size fields is a dependent chain of cache misses, so
+// the stream is cut into segments, each segment finds its first record by validating
+// candidate offsets (a record must chain into 8 more plausible records) and hops to its end
+// in parallel; a segment whose first record is not where the previous segment's chain lands
+// (a false sync) is re-hopped from that landing point.  Segment 0 starts at the first record.
+gqi_status record_offsets(const gq_bam *b, int nt, std::vector<int64_t> &recs) {
+  const uint8_t *d = b->data.data();
+  const int64_t n = (int64_t)b->data.size(), r0 = b->rec0;
+  const int32_t n_ref = (int32_t)b->contig_names.size();
+  const int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(4 * nt, (n - r0) / (1 << 20)));
+  const int64_t len = (n - r0 + nseg - 1) / std::max<int64_t>(nseg, 1);
+  std::vector<std::vector<int64_t>> seg((size_t)nseg);
+  std::vector<int64_t> land((size_t)nseg, -1);  // first offset >= the segment's end reached by its chain
+  std::vector<int> bad((size_t)nseg, 0);
+  auto hop = [&](int64_t o, int64_t stop, std::vector<int64_t> &out, int64_t *landed) -> bool {
+    while (o < stop) {
+      if (o + 4 > n) return false;
+      const int32_t bs = rd32s(d + o);
+      if (bs < 32 || o + 4 + bs > n) return false;
+      out.push_back(o);
+      o += 4 + bs;
+    }
+    *landed = o;
+    return true;
+  };
+  parallel_for(nseg, nt, [&](int64_t k) {
+    const int64_t a = r0 + k * len, e = std::min(n, a + len);
+    if (a >= e) {
+      land[k] = a;
+      return;
+    }
+    int64_t o = a;
+    if (k > 0) {  // sync: the first offset that chains into 8 more plausible records
+      for (; o < e; ++o) {
+        int64_t q = o;
+        int ok = 0;
+        while (ok < 9 && q < n && record_at(d, n, q, n_ref)) {
+          q += 4 + rd32s(d + q);
+          ++ok;
+        }
+        if (ok == 9 || (ok > 0 && q == n)) break;
+      }
+    }
+    seg[k].reserve((size_t)((e - a) / 256 + 16));
+    if (!hop(o, e, seg[k], &land[k])) bad[k] = 1;
+  });
+  recs.clear();
+  int64_t at = r0;  // where the true chain stands
+  for (int64_t k = 0; k < nseg; ++k) {
+    const int64_t a = r0 + k * len, e = std::min(n, a + len);
+    if (at >= e) continue;  // the previous chain already covered this segment
+    if (!bad[k] && !seg[k].empty() && seg[k][0] == at) {
+      recs.insert(recs.end(), seg[k].begin(), seg[k].end());
+      at = land[k];
+    } else if (!bad[k] && seg[k].empty() && land[k] == at) {
+      continue;
+    } else {  // false sync (or none): hop this segment from the true chain
+      std::vector<int64_t> v;
+      int64_t l = -1;
+      if (!hop(at, e, v, &l))
+        return fail(GQI_E_FORMAT, "truncated BAM record %lld", (long long)(recs.size() + v.size()));
+      recs.insert(recs.end(), v.begin(), v.end());
+      at = l;
+    }
+  }
+  if (at != n) return fail(GQI_E_FORMAT, "truncated BAM record %lld", (long long)recs.size());
+  return GQI_OK;
+}
+
+// scan pass over records [r0, r1): parse, filter, remember the kept ones and their sizes
+void scan_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0, int64_t r1, const gq_bam_filters *f,
+                Chunk &c) {
   const uint8_t *d = b->data.data();
   const int32_t n_ref = (int32_t)b->contig_names.size();
   std::unordered_map<std::string, int32_t> rg_local;
-  auto error = [&](int64_t r, gqi_status s, const char *fmt, auto... args) {
+  auto error = [&](gqi_status s, const char *fmt, auto... args) {
     char buf[400];
     snprintf(buf, sizeof(buf), fmt, args...);
     c.err = s;
-    c.err_rec = r;
     c.err_msg = buf;
   };
+  c.kept.reserve((size_t)(r1 - r0));
   for (int64_t r = r0; r < r1; ++r) {
     const int64_t o = recs[r], end = recs[r + 1];
     const uint8_t *p = d + o + 4;
     const int32_t ref_id = rd32s(p), pos = rd32s(p + 4);
-    const uint32_t l_read_name = p[8], mapq = p[9];
+    const uint32_t l_read_name = p[8];
     const uint32_t n_cig = rd16(p + 12), flag = rd16(p + 14);
     const int32_t l_seq = rd32s(p + 16);
-    int64_t q = o + 36;
-    const int64_t name_at = q;
-    q += l_read_name;
-    const int64_t cig_at = q;
-    q += 4 * (int64_t)n_cig;
-    const int64_t seq_at = q;
-    q += ((int64_t)l_seq + 1) / 2;
-    const int64_t qual_at = q;
-    q += l_seq;
+    const int64_t cig_at = o + 36 + l_read_name;
+    const int64_t qual_at = cig_at + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2;
+    int64_t q = qual_at + l_seq;
     if (l_seq < 0 || l_read_name < 1 || q > end) {
-      error(r, GQI_E_FORMAT, "truncated BAM record %lld", (long long)r);
+      error(GQI_E_FORMAT, "truncated BAM record %lld", (long long)r);
       return;
     }
     // aux fields: MD and RG (every record's aux is parsed, as the Python statement does)
     int64_t md_at = -1, md_n = 0, rg_at = -1, rg_n = 0;
     while (q < end) {
       if (q + 3 > end) {
-        error(r, GQI_E_FORMAT, "truncated aux field in BAM record %lld", (long long)r);
+        error(GQI_E_FORMAT, "truncated aux field in BAM record %lld", (long long)r);
         return;
       }
       const uint8_t t0 = d[q], t1 = d[q + 1], ty = d[q + 2];
@@ -359,7 +502,7 @@ void decode_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0,
         case 'Z': case 'H': {
           const uint8_t *z = (const uint8_t *)memchr(d + q, 0, (size_t)(end - q));
           if (!z) {
-            error(r, GQI_E_FORMAT, "unterminated aux string in BAM record %lld", (long long)r);
+            error(GQI_E_FORMAT, "unterminated aux string in BAM record %lld", (long long)r);
             return;
           }
           const int64_t len = z - (d + q);
@@ -370,7 +513,7 @@ void decode_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0,
         }
         case 'B': {
           if (q + 5 > end) {
-            error(r, GQI_E_FORMAT, "truncated aux array in BAM record %lld", (long long)r);
+            error(GQI_E_FORMAT, "truncated aux array in BAM record %lld", (long long)r);
             return;
           }
           const uint8_t sub = d[q];
@@ -381,43 +524,38 @@ void decode_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0,
             case 's': case 'S': w = 2; break;
             case 'i': case 'I': case 'f': w = 4; break;
             default:
-              error(r, GQI_E_RECORD, "bad aux array type '%c'", (char)sub);
+              error(GQI_E_RECORD, "bad aux array type '%c'", (char)sub);
               return;
           }
           q += 5 + cnt * w;
           break;
         }
         default:
-          error(r, GQI_E_RECORD, "bad aux type '%c'", (char)ty);
+          error(GQI_E_RECORD, "bad aux type '%c'", (char)ty);
           return;
       }
     }
     // Read.scala:411-418 record filters, then isMapped / hasMdTag (Read.scala:421-428)
     const bool unmapped = (flag & 0x4) || ref_id < 0;
     if (unmapped || pos < 0 || ref_id >= n_ref) continue;
-    int64_t ref_len = 0, padded = 0;
-    const uint8_t *cg = d + cig_at;
-    for (uint32_t k = 0; k < n_cig; ++k) {
-      const uint32_t v = rd32(cg + 4 * k), op = v & 15, ln = v >> 4;
-      if (op < 9 && (kConsumesRef >> op) & 1) ref_len += ln;
-      if (op < 9 && (kPaddedRef >> op) & 1) padded += ln;
+    if (f->use_loci) {
+      int64_t ref_len = 0;
+      for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t v = rd32(d + cig_at + 4 * k), op = v & 15;
+        if (op < 9 && (kConsumesRef >> op) & 1) ref_len += v >> 4;
+      }
+      if (!loci_intersect(f, ref_id, pos, pos + ref_len)) continue;
     }
-    if (f->use_loci && !loci_intersect(f, ref_id, pos, pos + ref_len)) continue;
     if (f->non_duplicate && (flag & 0x400)) continue;
     if (f->passed_vendor_quality_checks && (flag & 0x200)) continue;
     if (f->is_paired && !(flag & 0x1)) continue;
     if (f->has_md_tag && md_at < 0) continue;
     // htsjdk: missing qualities (0xFF) -> empty array -> MappedRead's length assertion
-    const bool no_qual = l_seq > 0 && d[qual_at] == 0xFF;
-    if (no_qual) {
-      error(r, GQI_E_RECORD, "Base qualities have length 0 but sequence has length %d", l_seq);
+    if (l_seq > 0 && d[qual_at] == 0xFF) {
+      error(GQI_E_RECORD, "Base qualities have length 0 but sequence has length %d", l_seq);
       return;
     }
-    c.contig.push_back(ref_id);
-    c.start.push_back(pos);
-    c.end.push_back(pos + padded);
-    c.mapq.push_back((uint8_t)mapq);
-    c.flags.push_back((flag & 0x10) ? 1 : 0);
+    const int64_t k = (int64_t)c.kept.size();
     int32_t rg = -1;
     if (rg_at >= 0) {
       std::string v((const char *)d + rg_at, (size_t)rg_n);
@@ -425,36 +563,25 @@ void decode_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0,
       if (it == rg_local.end()) {
         it = rg_local.emplace(v, (int32_t)c.rg_vals.size()).first;
         c.rg_vals.push_back(v);
-        c.rg_first.push_back((int64_t)c.contig.size() - 1);
+        c.rg_first.push_back(k);
       }
       rg = it->second;
     } else if (c.none_first < 0) {
-      c.none_first = (int64_t)c.contig.size() - 1;
+      c.none_first = k;
     }
-    c.rg.push_back(rg);
-    c.seq_len.push_back(l_seq);
-    const size_t s0 = c.seq.size();
-    c.seq.resize(s0 + (size_t)l_seq + 1);
-    {
-      const uint8_t *sp = d + seq_at;
-      uint8_t *o2 = c.seq.data() + s0;
-      for (int32_t k = 0; k < l_seq / 2; ++k) memcpy(o2 + 2 * k, &kSeq.t[sp[k]], 2);
-      if (l_seq & 1) o2[l_seq - 1] = (uint8_t)(kSeq.t[sp[l_seq / 2]] & 0xFF);
+    if (k == 0) {
+      c.c0 = ref_id;
+      c.s0 = pos;
+    } else if (ref_id < c.c1 || (ref_id == c.c1 && pos < c.s1)) {
+      c.sorted = false;
     }
-    c.seq.resize(s0 + (size_t)l_seq);
-    c.qual.insert(c.qual.end(), d + qual_at, d + qual_at + l_seq);
-    c.n_cigar.push_back((int32_t)n_cig);
-    const size_t c0 = c.cigar.size();
-    c.cigar.resize(c0 + n_cig);
-    memcpy(c.cigar.data() + c0, d + cig_at, 4 * (size_t)n_cig);
-    if (md_at >= 0) {
-      c.md_len.push_back((int32_t)md_n);
-      c.md.insert(c.md.end(), d + md_at, d + md_at + md_n);
-    } else {
-      c.md_len.push_back(-1);
-    }
-    c.name_len.push_back((int32_t)l_read_name - 1);
-    c.names.insert(c.names.end(), d + name_at, d + name_at + l_read_name - 1);
+    c.c1 = ref_id;
+    c.s1 = pos;
+    c.kept.push_back(Kept{o, md_at, (int32_t)md_n, rg});
+    c.seq += l_seq;
+    c.cigar += n_cig;
+    c.md += md_at >= 0 ? md_n : 0;
+    c.names += l_read_name - 1;
   }
 }
 
@@ -480,7 +607,7 @@ gqi_status gq_bam_open(const char *path, int32_t n_threads, gq_bam **out) {
     return fail(GQI_E_IO, "cannot stat (or empty) %s", path);
   }
   b->map_len = (size_t)st.st_size;
-  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE, b->fd, 0);
+  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, b->fd, 0);
   if (m == MAP_FAILED) {
     close(b->fd);
     delete b;
@@ -526,43 +653,38 @@ gqi_status gq_bam_scan(gq_bam *b, const gq_bam_filters *f, int32_t n_threads, gq
     return fail(GQI_E_ARG, "use_loci without loci arrays");
   const int nt = threads_of(n_threads);
   b->scanned = false;
-  // record boundaries (sequential hop over block_size)
   const uint8_t *d = b->data.data();
   const int64_t n = (int64_t)b->data.size();
   std::vector<int64_t> recs;
-  recs.reserve((size_t)(n / 300 + 16));
-  int64_t o = b->rec0;
-  while (o < n) {
-    if (o + 4 > n) return fail(GQI_E_FORMAT, "truncated BAM record at offset %lld", (long long)o);
-    const int32_t bs = rd32s(d + o);
-    if (bs < 32 || o + 4 + bs > n)
-      return fail(GQI_E_FORMAT, "truncated BAM record %lld", (long long)recs.size());
-    recs.push_back(o);
-    o += 4 + bs;
-  }
+  gqi_status st = record_offsets(b, nt, recs);
+  if (st != GQI_OK) return st;
   const int64_t nrec = (int64_t)recs.size();
   recs.push_back(n);
-  const int64_t per = 1 << 15;
+  const int64_t per = 1 << 14;
   const int64_t nch = std::max<int64_t>(1, (nrec + per - 1) / per);
-  b->chunks.assign((size_t)nch, Chunk());
+  std::vector<Chunk> chunks((size_t)nch);
   parallel_for(nch, nt, [&](int64_t k) {
-    decode_chunk(b, recs, k * per, std::min(nrec, (k + 1) * per), f, b->chunks[k]);
+    scan_chunk(b, recs, k * per, std::min(nrec, (k + 1) * per), f, chunks[k]);
   });
-  for (auto &c : b->chunks)
+  for (auto &c : chunks)
     if (c.err != GQI_OK) {  // the first failing record in file order (chunks are in order)
       g_err = c.err_msg;
-      b->chunks.clear();
       return c.err;
     }
-  // global RG table (first appearance) and sizes
+  // global RG table (first appearance), sizes, sortedness, kept-read offsets per chunk
   gq_bam_sizes z{};
   b->rgs.clear();
   b->rg_first.assign(1, -1);
   std::unordered_map<std::string, int32_t> rg_glob;
-  b->chunk_read0.assign((size_t)nch + 1, 0);
+  std::vector<int64_t> k0((size_t)nch + 1, 0);
+  std::vector<std::vector<int32_t>> rg_map((size_t)nch);
+  bool sorted = true;
+  bool any = false;
+  int32_t pc = 0;
+  int64_t ps = 0;
   for (int64_t k = 0; k < nch; ++k) {
-    Chunk &c = b->chunks[k];
-    c.rg_map.resize(c.rg_vals.size());
+    const Chunk &c = chunks[k];
+    rg_map[k].resize(c.rg_vals.size());
     for (size_t j = 0; j < c.rg_vals.size(); ++j) {
       auto it = rg_glob.find(c.rg_vals[j]);
       if (it == rg_glob.end()) {
@@ -570,64 +692,44 @@ gqi_status gq_bam_scan(gq_bam *b, const gq_bam_filters *f, int32_t n_threads, gq
         b->rgs.push_back(c.rg_vals[j]);
         b->rg_first.push_back(z.n_reads + c.rg_first[j]);
       }
-      c.rg_map[j] = it->second;
+      rg_map[k][j] = it->second;
     }
     if (b->rg_first[0] < 0 && c.none_first >= 0) b->rg_first[0] = z.n_reads + c.none_first;
-    b->chunk_read0[k] = z.n_reads;
-    z.n_reads += (int64_t)c.contig.size();
-    z.seq_bytes += (int64_t)c.seq.size();
-    z.cigar_len += (int64_t)c.cigar.size();
-    z.md_bytes += (int64_t)c.md.size();
-    z.name_bytes += (int64_t)c.names.size();
+    if (!c.kept.empty()) {
+      if (!c.sorted || (any && (c.c0 < pc || (c.c0 == pc && c.s0 < ps)))) sorted = false;
+      any = true;
+      pc = c.c1;
+      ps = c.s1;
+    }
+    k0[k] = z.n_reads;
+    z.n_reads += (int64_t)c.kept.size();
+    z.seq_bytes += c.seq;
+    z.cigar_len += c.cigar;
+    z.md_bytes += c.md;
+    z.name_bytes += c.names;
   }
-  b->chunk_read0[nch] = z.n_reads;
+  k0[nch] = z.n_reads;
   z.n_rg = (int32_t)b->rgs.size();
-  // chunk-local pool offsets
+  b->kept.resize((size_t)z.n_reads);
   parallel_for(nch, nt, [&](int64_t k) {
-    Chunk &c = b->chunks[k];
-    const size_t m = c.contig.size();
-    c.seq_o.resize(m + 1);
-    c.cig_o.resize(m + 1);
-    c.md_o.resize(m + 1);
-    c.name_o.resize(m + 1);
-    c.seq_o[0] = c.cig_o[0] = c.md_o[0] = c.name_o[0] = 0;
-    for (size_t i = 0; i < m; ++i) {
-      c.seq_o[i + 1] = c.seq_o[i] + c.seq_len[i];
-      c.cig_o[i + 1] = c.cig_o[i] + c.n_cigar[i];
-      c.md_o[i + 1] = c.md_o[i] + std::max(c.md_len[i], 0);
-      c.name_o[i + 1] = c.name_o[i] + c.name_len[i];
+    const Chunk &c = chunks[k];
+    for (size_t i = 0; i < c.kept.size(); ++i) {
+      Kept x = c.kept[i];
+      x.rg = x.rg < 0 ? -1 : rg_map[k][x.rg];
+      b->kept[k0[k] + i] = x;
     }
   });
-  // sorted by (contig, start)?  else a stable permutation (ties keep file order)
-  bool sorted = true;
-  {
-    int32_t pc = INT32_MIN;
-    int64_t ps = INT64_MIN;
-    for (const Chunk &c : b->chunks) {
-      for (size_t i = 0; i < c.contig.size() && sorted; ++i) {
-        if (c.contig[i] < pc || (c.contig[i] == pc && c.start[i] < ps)) sorted = false;
-        pc = c.contig[i];
-        ps = c.start[i];
-      }
-      if (!sorted) break;
-    }
-  }
+  // not coordinate-sorted: a stable permutation (ties keep file order)
   b->order.clear();
   if (!sorted) {
-    std::vector<int32_t> kc((size_t)z.n_reads);
-    std::vector<int64_t> ks((size_t)z.n_reads);
-    for (int64_t k = 0; k < nch; ++k) {
-      const Chunk &c = b->chunks[k];
-      for (size_t i = 0; i < c.contig.size(); ++i) {
-        kc[b->chunk_read0[k] + i] = c.contig[i];
-        ks[b->chunk_read0[k] + i] = c.start[i];
-      }
-    }
+    std::vector<std::pair<int32_t, int32_t>> key((size_t)z.n_reads);
+    parallel_for(z.n_reads, nt, [&](int64_t i) {
+      const uint8_t *p = d + b->kept[i].rec + 4;
+      key[i] = {rd32s(p), rd32s(p + 4)};
+    });
     b->order.resize((size_t)z.n_reads);
     std::iota(b->order.begin(), b->order.end(), 0);
-    std::stable_sort(b->order.begin(), b->order.end(), [&](int64_t x, int64_t y) {
-      return kc[x] != kc[y] ? kc[x] < kc[y] : ks[x] < ks[y];
-    });
+    std::stable_sort(b->order.begin(), b->order.end(), [&](int64_t x, int64_t y) { return key[x] < key[y]; });
   }
   z.sorted = sorted ? 1 : 0;
   b->sizes = z;
@@ -640,42 +742,22 @@ gqi_status gq_bam_fill(gq_bam *b, int32_t n_threads, const gq_bam_reads *R) {
   if (!b || !R) return fail(GQI_E_ARG, "null argument");
   if (!b->scanned) return fail(GQI_E_ARG, "gq_bam_fill before gq_bam_scan");
   const int nt = threads_of(n_threads);
-  const int64_t nch = (int64_t)b->chunks.size();
   const int64_t N = b->sizes.n_reads;
-  // output read -> (chunk, index): file order when sorted, else via the permutation
-  auto locate = [&](int64_t file_i, int64_t *k, int64_t *i) {
-    const int64_t c = std::upper_bound(b->chunk_read0.begin(), b->chunk_read0.end(), file_i) - b->chunk_read0.begin() - 1;
-    *k = c;
-    *i = file_i - b->chunk_read0[c];
-  };
-  // pool offsets of output reads: exclusive scans over output order
-  std::vector<int64_t> fi;  // file index of output read r (only when unsorted)
-  if (!b->order.empty()) fi = b->order;
-  auto file_of = [&](int64_t r) { return fi.empty() ? r : fi[r]; };
-  // per-read fields + lengths
-  const int64_t per = 1 << 16;
+  const uint8_t *d = b->data.data();
+  auto kept_of = [&](int64_t r) -> const Kept & { return b->kept[b->order.empty() ? r : b->order[r]]; };
+  // pass 1: pool sizes per block of output reads; pass 2: every field, straight from the records
+  const int64_t per = 1 << 14;
   const int64_t nblk = (N + per - 1) / per;
   std::vector<int64_t> bs(nblk + 1, 0), bc(nblk + 1, 0), bm(nblk + 1, 0), bn(nblk + 1, 0);
   parallel_for(nblk, nt, [&](int64_t q) {
     int64_t s = 0, cg = 0, m = 0, nm = 0;
     for (int64_t r = q * per; r < std::min(N, (q + 1) * per); ++r) {
-      int64_t k, i;
-      locate(file_of(r), &k, &i);
-      const Chunk &c = b->chunks[k];
-      R->contig[r] = c.contig[i];
-      R->start[r] = c.start[i];
-      R->end[r] = c.end[i];
-      R->mapq[r] = c.mapq[i];
-      R->flags[r] = c.flags[i];
-      R->rg[r] = c.rg[i] < 0 ? -1 : c.rg_map[c.rg[i]];
-      R->seq_len[r] = c.seq_len[i];
-      R->n_cigar[r] = c.n_cigar[i];
-      R->md_len[r] = c.md_len[i];
-      R->name_len[r] = c.name_len[i];
-      s += c.seq_len[i];
-      cg += c.n_cigar[i];
-      m += std::max(c.md_len[i], 0);
-      nm += c.name_len[i];
+      const Kept &x = kept_of(r);
+      const uint8_t *p = d + x.rec + 4;
+      s += rd32s(p + 16);
+      cg += rd16(p + 12);
+      m += x.md_at >= 0 ? x.md_len : 0;
+      nm += p[8] - 1;
     }
     bs[q + 1] = s;
     bc[q + 1] = cg;
@@ -691,26 +773,44 @@ gqi_status gq_bam_fill(gq_bam *b, int32_t n_threads, const gq_bam_reads *R) {
   parallel_for(nblk, nt, [&](int64_t q) {
     int64_t s = bs[q], cg = bc[q], m = bm[q], nm = bn[q];
     for (int64_t r = q * per; r < std::min(N, (q + 1) * per); ++r) {
-      int64_t k, i;
-      locate(file_of(r), &k, &i);
-      const Chunk &c = b->chunks[k];
+      const Kept &x = kept_of(r);
+      const uint8_t *p = d + x.rec + 4;
+      const int32_t ref_id = rd32s(p), pos = rd32s(p + 4);
+      const uint32_t l_name = p[8] - 1u, mapq = p[9], n_cig = rd16(p + 12), flag = rd16(p + 14);
+      const int32_t l_seq = rd32s(p + 16);
+      const uint8_t *name = p + 32, *cg_p = name + l_name + 1, *sq = cg_p + 4 * n_cig, *ql = sq + (l_seq + 1) / 2;
+      int64_t padded = 0;
+      for (uint32_t k = 0; k < n_cig; ++k) {
+        const uint32_t v = rd32(cg_p + 4 * k), op = v & 15;
+        if (op < 9 && (kPaddedRef >> op) & 1) padded += v >> 4;
+      }
+      R->contig[r] = ref_id;
+      R->start[r] = pos;
+      R->end[r] = pos + padded;
+      R->mapq[r] = (uint8_t)mapq;
+      R->flags[r] = (flag & 0x10) ? 1 : 0;
+      R->rg[r] = x.rg;
       R->seq_off[r] = s;
+      R->seq_len[r] = l_seq;
       R->cigar_off[r] = cg;
+      R->n_cigar[r] = (int32_t)n_cig;
       R->md_off[r] = m;
+      R->md_len[r] = x.md_at >= 0 ? x.md_len : -1;
       R->name_off[r] = nm;
-      const int64_t ls = c.seq_len[i], lc = c.n_cigar[i], lm = std::max(c.md_len[i], 0), ln = c.name_len[i];
-      memcpy(R->seq + s, c.seq.data() + c.seq_o[i], (size_t)ls);
-      memcpy(R->qual + s, c.qual.data() + c.seq_o[i], (size_t)ls);
-      memcpy(R->cigar + cg, c.cigar.data() + c.cig_o[i], 4 * (size_t)lc);
-      if (lm) memcpy(R->md + m, c.md.data() + c.md_o[i], (size_t)lm);
-      if (ln) memcpy(R->names + nm, c.names.data() + c.name_o[i], (size_t)ln);
-      s += ls;
-      cg += lc;
-      m += lm;
-      nm += ln;
+      R->name_len[r] = (int32_t)l_name;
+      uint8_t *os = R->seq + s;
+      for (int32_t k = 0; k < l_seq / 2; ++k) memcpy(os + 2 * k, &kSeq.t[sq[k]], 2);
+      if (l_seq & 1) os[l_seq - 1] = (uint8_t)(kSeq.t[sq[l_seq / 2]] & 0xFF);
+      memcpy(R->qual + s, ql, (size_t)l_seq);
+      memcpy(R->cigar + cg, cg_p, 4 * (size_t)n_cig);
+      if (x.md_at >= 0 && x.md_len) memcpy(R->md + m, d + x.md_at, (size_t)x.md_len);
+      if (l_name) memcpy(R->names + nm, name, l_name);
+      s += l_seq;
+      cg += n_cig;
+      m += x.md_at >= 0 ? x.md_len : 0;
+      nm += l_name;
     }
   });
-  (void)nch;
   return GQI_OK;
 }
 

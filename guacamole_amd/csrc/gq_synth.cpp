@@ -14,12 +14,15 @@
 // 10^(-q/10).  Reads crossing an indel carry the corresponding I/D CIGAR op
 // (reads are error-free through an indel to keep the alignment canonical).
 #include <stdint.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -415,6 +418,147 @@ int gq_synth_generate(const gq_synth_params *P, gq_synth_out *o) {
   free(hap0);
   free(hap1);
   return 0;
+}
+
+// Write the read set as a coordinate-sorted BAM (one contig, no read groups, read names
+// "r<index>"), BGZF level `level`: the input of the native ingest measurement
+// (scripts/bench_ingest.py).  MD strings are rebuilt from the MD events the way
+// synthetic.md_string does (a deleted base without an event is written as N).
+int gq_synth_write_bam(const gq_synth_out *o, const char *path, const char *contig, int64_t contig_len,
+                       int32_t level) {
+  const int64_t N = o->n_reads;
+  const int T = nthreads();
+  const int64_t per = std::max<int64_t>(1, (N + T - 1) / T);
+  std::vector<std::string> parts((size_t)T);
+  auto put32 = [](std::string &b, uint32_t v) { b.append((const char *)&v, 4); };
+  parallel_for(N, [&](int t, int64_t a, int64_t e) {
+    (void)per;
+    std::string &b = parts[(size_t)t];
+    std::string md;
+    static const char kNib[] = "=ACMGRSVTWYHKDBN";
+    uint8_t code[256];
+    memset(code, 15, sizeof(code));
+    for (int k = 0; k < 16; ++k) code[(uint8_t)kNib[k]] = (uint8_t)k;
+    for (int64_t r = a; r < e; ++r) {
+      const uint32_t *cg = o->cigar + o->cigar_off[r];
+      const int32_t nc = o->n_cigar[r], ls = o->seq_len[r];
+      const uint32_t *ev = o->md_ev + o->md_off[r];
+      const int32_t ne = std::max(o->n_md[r], 0);
+      // MD string
+      md.clear();
+      int64_t run = 0, ref = 0;
+      int32_t k = 0;
+      for (int32_t c = 0; c < nc; ++c) {
+        const uint32_t op = cg[c] & 15, ln = cg[c] >> 4;
+        if (op == 0 || op == 7 || op == 8) {
+          const int64_t end = ref + ln;
+          while (k < ne && (int64_t)(ev[k] >> 8) < end) {
+            const int64_t off = ev[k] >> 8;
+            run += off - ref;
+            md += std::to_string(run);
+            md += (char)(ev[k] & 0xFF);
+            run = 0;
+            ref = off + 1;
+            ++k;
+          }
+          run += end - ref;
+          ref = end;
+        } else if (op == 2) {
+          md += std::to_string(run);
+          md += '^';
+          for (uint32_t j = 0; j < ln; ++j) {
+            if (k < ne && (int64_t)(ev[k] >> 8) == ref + j) md += (char)(ev[k++] & 0xFF);
+            else md += 'N';
+          }
+          run = 0;
+          ref += ln;
+        } else if (op == 3) {
+          ref += ln;
+        }
+      }
+      md += std::to_string(run);
+      const std::string name = "r" + std::to_string(r);
+      const uint32_t l_name = (uint32_t)name.size() + 1;
+      const uint32_t block = 32 + l_name + 4 * (uint32_t)nc + (uint32_t)(ls + 1) / 2 + (uint32_t)ls +
+                             3 + (uint32_t)md.size() + 1;
+      put32(b, block);
+      put32(b, 0);  // ref_id
+      put32(b, (uint32_t)o->start[r]);
+      b += (char)l_name;
+      b += (char)o->mapq[r];
+      b.append("\0\0", 2);  // bin (unused by readers here)
+      const uint16_t ncig = (uint16_t)nc, flag = (o->flags[r] & 1) ? 16 : 0;
+      b.append((const char *)&ncig, 2);
+      b.append((const char *)&flag, 2);
+      put32(b, (uint32_t)ls);
+      put32(b, 0xFFFFFFFFu);
+      put32(b, 0xFFFFFFFFu);
+      put32(b, 0);
+      b.append(name.c_str(), l_name);
+      b.append((const char *)cg, 4 * (size_t)nc);
+      const uint8_t *sq = o->seq + o->seq_off[r];
+      for (int32_t j = 0; j < ls; j += 2) {
+        const uint8_t hi = code[sq[j]], lo = j + 1 < ls ? code[sq[j + 1]] : 0;
+        b += (char)((hi << 4) | lo);
+      }
+      b.append((const char *)(o->qual + o->seq_off[r]), (size_t)ls);
+      b.append("MDZ", 3);
+      b.append(md.c_str(), md.size() + 1);
+    }
+  });
+  std::string data("BAM\1", 4);
+  const std::string text = std::string("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:") + contig + "\tLN:" +
+                           std::to_string(contig_len) + "\n";
+  put32(data, (uint32_t)text.size());
+  data += text;
+  put32(data, 1);
+  put32(data, (uint32_t)strlen(contig) + 1);
+  data.append(contig, strlen(contig) + 1);
+  put32(data, (uint32_t)contig_len);
+  for (auto &x : parts) {
+    data += x;
+    std::string().swap(x);
+  }
+  // BGZF blocks of 65280 input bytes, compressed in parallel
+  const int64_t kBlk = 65280;
+  const int64_t nb = ((int64_t)data.size() + kBlk - 1) / kBlk;
+  std::vector<std::string> comp((size_t)nb + 1);
+  auto block = [&](const uint8_t *src, int64_t len, std::string &out) {
+    z_stream z;
+    memset(&z, 0, sizeof(z));
+    deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+    std::string buf(deflateBound(&z, (uLong)len) + 64, '\0');
+    z.next_in = const_cast<uint8_t *>(src);
+    z.avail_in = (uInt)len;
+    z.next_out = (Bytef *)&buf[18];
+    z.avail_out = (uInt)(buf.size() - 26);
+    deflate(&z, Z_FINISH);
+    const size_t clen = z.total_out;
+    deflateEnd(&z);
+    const uint32_t bsize = (uint32_t)(18 + clen + 8);
+    const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                             (uint8_t)((bsize - 1) & 0xFF), (uint8_t)((bsize - 1) >> 8)};
+    memcpy(&buf[0], hdr, 18);
+    const uint32_t crc = (uint32_t)crc32(0L, src, (uInt)len), isz = (uint32_t)len;
+    memcpy(&buf[18 + clen], &crc, 4);
+    memcpy(&buf[18 + clen + 4], &isz, 4);
+    buf.resize(bsize);
+    out.swap(buf);
+  };
+  parallel_for(nb, [&](int, int64_t a, int64_t e) {
+    for (int64_t i = a; i < e; ++i)
+      block((const uint8_t *)data.data() + i * kBlk, std::min<int64_t>(kBlk, (int64_t)data.size() - i * kBlk),
+            comp[(size_t)i]);
+  });
+  block(nullptr, 0, comp[(size_t)nb]);  // EOF marker block
+  FILE *f = fopen(path, "wb");
+  if (!f) return 1;
+  for (auto &c : comp)
+    if (fwrite(c.data(), 1, c.size(), f) != c.size()) {
+      fclose(f);
+      return 2;
+    }
+  return fclose(f) == 0 ? 0 : 2;
 }
 
 }  // extern "C"

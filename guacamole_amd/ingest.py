@@ -114,13 +114,17 @@ class NamePool:
         raise ValueError("%r is not in the read names" % name)
 
 
-def load_bam(path: str, filters) -> "ReadSet":
-    """BAM -> ReadSet through libgqingest (reads._load_bam_py states the same rules)."""
+def load_bam(path: str, filters, timings: Optional[Dict[str, float]] = None) -> "ReadSet":
+    """BAM -> ReadSet through libgqingest (reads._load_bam_py states the same rules).
+    ``timings`` (optional) receives the seconds of open+inflate, scan and fill."""
+    import time
     from .reads import ReadLoadError, ReadSet, _header_read_groups, _sample_of
     L = lib()
     nt = n_threads()
     h = C.c_void_p()
+    t0 = time.perf_counter()
     st = L.gq_bam_open(os.fsencode(path), nt, C.byref(h))
+    t1 = time.perf_counter()
     if st:
         raise ReadLoadError(_err(L))
     try:
@@ -145,15 +149,19 @@ def load_bam(path: str, filters) -> "ReadSet":
             if not starts:
                 f.loci_start = f.loci_end = None
         z = _Sizes()
+        t2 = time.perf_counter()
         st = L.gq_bam_scan(h, C.byref(f), nt, C.byref(z))
         if st:
             raise ReadLoadError(_err(L))
+        t3 = time.perf_counter()
         sizes = {"n": z.n_reads, "seq": z.seq_bytes, "cigar": z.cigar_len, "md": z.md_bytes, "name": z.name_bytes}
         arrs = {name: np.empty(sizes[kind], dt) for name, dt, kind in _READ_FIELDS}
         R = _Reads(*[_ptr(arrs[name]) for name, _, _ in _READ_FIELDS])
         st = L.gq_bam_fill(h, nt, C.byref(R))
         if st:
             raise ReadLoadError(_err(L))
+        if timings is not None:
+            timings.update(open_inflate_s=t1 - t0, scan_s=t3 - t2, fill_s=time.perf_counter() - t3, threads=nt)
         # samples: RG -> SM (else "default"), numbered by first appearance in file order
         rg_samples = _header_read_groups(text)
         rg_vals = [L.gq_bam_rg(h, k).decode("utf-8", "replace") for k in range(z.n_rg)]

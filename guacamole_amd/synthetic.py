@@ -87,6 +87,15 @@ class SyntheticReads:
         idx = np.arange(lo, hi)
         return idx[a["end"][idx] > start]
 
+    def write_bam(self, path: str, level: int = 6) -> None:
+        """Coordinate-sorted BAM of every read (native writer; read names r<index>, no RG)."""
+        L = _load()
+        L.gq_synth_write_bam.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int64, C.c_int32]
+        rc = L.gq_synth_write_bam(C.byref(self._owner.out), os.fsencode(path), self.contig_names[0].encode(),
+                                  int(self.contig_lengths[0]), int(level))
+        if rc != 0:
+            raise OSError("gq_synth_write_bam failed (%d) for %s" % (rc, path))
+
     def to_read_set(self, sel: Optional[np.ndarray] = None) -> ReadSet:
         """Raw ReadSet (MD strings) for the reads `sel` (default: all) — oracle input."""
         a = self.arrays
