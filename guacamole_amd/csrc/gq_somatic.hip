@@ -16,6 +16,9 @@
 //                     sample are counted; loci with a tumor non-Match and normal depth > 0
 //                     are queued (a superset of the loci the caller can emit at: filters
 //                     only remove elements).
+//                     A queued locus whose tumor pileup provably has the hom-ref genotype as
+//                     its maximum-likelihood genotype is dropped (hom_ref_margin below): the
+//                     caller returns nothing there whatever the odds and filters.
 //   somatic_call      one wave per queued locus: exact elements of both pileups
 //                     (classify), per-sample distinct-allele table in registers with the
 //                     FP64 per-allele sums of log(2pc), log(pc + (1 - pc)), log(2(1 - pc)),
@@ -52,17 +55,91 @@ struct SomRec {  // one emitted CalledSomaticAllele
 };
 
 // ------------------------------------------------------------------------------------------
+// Hom-ref bound (the tumor side of findPotentialVariantAtLocus, SomaticStandardCaller.scala:
+// 196-206).  The caller computes, over the filtered tumor pileup, genotype likelihoods
+//   L(a1, a2) = sum_e log(P(e, a1) + P(e, a2)) (- D ln 2, common),  P(e, a) = pc_e if the
+//   element's allele is a else 1 - pc_e,  pc_e = phredSuccess(base quality) * phredSuccess(mapq)
+// (Likelihood.scala:149-201, IncludingAlignment) and emits nothing unless the maximum-likelihood
+// genotype holds a variant allele.  At a locus whose elements are all single-base Match /
+// Mismatch elements against one reference base r:
+//   L(r, r)  = sum_match log(2 pc) + sum_mismatch log(2 (1 - pc))
+//   L(g)    <= ln2 * n_mismatch + sum_match max(0, log(2 (1 - pc)))  for every other genotype g
+// (each term is at most log 2; a Match element adds log 1 = 0 to (r, v) and log(2 (1 - pc)) to
+// (v, w)).  So margin = sum_match [log(2 pc) - max(0, log(2 (1 - pc)))] + sum_mismatch
+// [log(2 (1 - pc)) - ln 2] > 0 proves (r, r) is the unique maximum: no call at any odds.  The
+// sum runs in FP32 (error far below the eps the test applies) over the reads the mapq filter
+// keeps (QualityAlignedReadsFilter, PileupElementsFilter.scala:25-36).
+__device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1,
+                                                    int min_mapq, const float *eq, float *marg) {
+  const int32_t s = R.start[r], e = R.end[r];
+  if (e <= L0 || s >= L1) return;
+  const int mq = (int)R.mapq[r];
+  if (min_mapq > 0 && mq < min_mapq) return;
+  const int32_t nmd = R.n_md[r];
+  if (nmd < 0) return;  // GQ_E_NO_MD is raised by the histogram pass
+  const float em = exp2f(-0.33219281f * (float)mq);  // 10^(-mapq/10)
+  const uint8_t *sq = R.seq + R.seq_off[r];
+  const uint8_t *ql = R.qual + R.seq_off[r];
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  int k = 0;  // MD event cursor (events sorted by offset; runs visited in reference order)
+  constexpr float kLn2 = 0.69314718f;
+  auto run = [&](int32_t ra, int32_t rp0, int32_t len) {
+    const int32_t a = ra > L0 ? ra : L0, b = (ra + len) < L1 ? (ra + len) : L1;
+    for (int32_t l = a; l < b; ++l) {
+      const int32_t rp = rp0 + (l - ra);
+      const uint8_t base = sq[rp];
+      const int q = (int)(int8_t)ql[rp];
+      while (k < nmd && (int32_t)(ev[k] >> 8) < l - s) ++k;
+      const uint8_t m = (k < nmd && (int32_t)(ev[k] >> 8) == l - s) ? (uint8_t)(ev[k] & 0xFFu) : base;
+      float t;
+      if (q < 0 || q > 127) {
+        t = -1e30f;  // outside the table: the exact kernel decides
+      } else {
+        const float eb = eq[q];
+        const float f = eb + em - eb * em;  // 1 - pc
+        if (base == m) t = kLn2 + __logf(1.0f - f) - fmaxf(0.0f, kLn2 + __logf(f));
+        else t = __logf(f);  // log(2 (1 - pc)) - ln 2
+      }
+      atomicAdd(&marg[l - L0], t);
+    }
+  };
+  const int32_t lead = R.lead[r];
+  if (lead >= 0) {
+    run(s, lead, e - s);
+    return;
+  }
+  const uint32_t *cg = R.cigar + R.cigar_off[r];
+  const int32_t nc = R.n_cigar[r];
+  int32_t ref = s, rp = 0;
+  for (int c = 0; c < nc && ref < L1; ++c) {
+    const int op = (int)(cg[c] & 15u);
+    const int32_t len = (int32_t)(cg[c] >> 4);
+    if (op == OP_M || op == OP_EQ || op == OP_X) {
+      run(ref, rp, len);
+      ref += len;
+      rp += len;
+    } else if (op == OP_I || op == OP_S) {
+      rp += len;
+    } else if (op == OP_D || op == OP_N) {
+      ref += len;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // somatic_tile: candidate loci
 // ------------------------------------------------------------------------------------------
 template <int T>
 __global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ tiles_t,
                                                        const Tile *__restrict__ tiles_n, DevReads RT, DevReads RN,
                                                        ComplexItem *__restrict__ cand, unsigned long long cand_cap,
-                                                       Counters *ctr) {
+                                                       int min_mapq, Counters *ctr) {
   constexpr int S = T + 2 * kGuard;
   constexpr int KPT = T / kBlock;  // loci per thread
   static_assert(KPT <= 8, "per-thread flag bits");
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
+  __shared__ float marg[T];  // hom-ref margin of the tumor pileup
+  __shared__ float eq[128];  // 10^(-q/10)
   const Tile tt = tiles_t[blockIdx.x], tn = tiles_n[blockIdx.x];
   const int32_t L0 = tt.L0, L1 = tt.L1;
   const int nloci = L1 - L0;
@@ -78,10 +155,15 @@ __global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ 
   }
   uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
   for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = threadIdx.x; i < T; i += blockDim.x) marg[i] = 0.0f;
+  if (threadIdx.x < 128) eq[threadIdx.x] = exp2f(-0.33219281f * (float)threadIdx.x);
   __syncthreads();
   {
     GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-    for (int64_t r = tt.rb + threadIdx.x; r < tt.re; r += blockDim.x) walk_read_lane(RT, r, L0, L1, sink);
+    for (int64_t r = tt.rb + threadIdx.x; r < tt.re; r += blockDim.x) {
+      walk_read_lane(RT, r, L0, L1, sink);
+      hom_ref_margin_lane(RT, r, L0, L1, min_mapq, eq, marg);
+    }
   }
   __syncthreads();
   uint32_t tflag = 0;  // bit k: tumor depth > 0 at locus tid + k * kBlock; bit 8 + k: tumor candidate
@@ -104,7 +186,11 @@ __global__ __launch_bounds__(kBlock) void somatic_tile(const Tile *__restrict__ 
     if (cG > (etg >> 16)) mask |= 8u;
     const int rc = mask ? (__ffs((int)mask) - 1) : 4;
     const uint32_t c_ref = rc == 0 ? cA : rc == 1 ? cC : rc == 2 ? cT : rc == 3 ? cG : cN;
-    if (__popc(mask) > 1 || cx > 0 || depth > c_ref) tflag |= 1u << (8 + k);
+    if (__popc(mask) > 1 || cx > 0 || depth > c_ref) {
+      // single-base elements only, one standard reference base, no N: the hom-ref bound applies
+      const bool bound = __popc(mask) == 1 && cx == 0 && cN == 0 && marg[i] > 0.02f + 2e-4f * (float)depth;
+      if (!bound) tflag |= 1u << (8 + k);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -765,9 +851,22 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL((somatic_tile<kSomT>), dim3((unsigned)pt.n_tiles), dim3(kBlock), 0, c->stream,
                        (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, t->d, n->d, (ComplexItem *)c->cplx.p,
-                       cand_cap, ctr);
+                       cand_cap, (int)p->min_mapq, ctr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    {  // candidate overflow: grow and re-run the tile kernel before the (costly) caller runs
+      unsigned long long nc = 0;
+      HIP_TRY(hipMemcpyAsync(&nc, &ctr->n_complex, sizeof(nc), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (nc > cand_cap) {
+        cand_cap = nc + 1024;
+        if (attempt == 2) {
+          free(res);
+          return set_err(GQ_E_CAPACITY, "candidate capacity retries exhausted");
+        }
+        continue;
+      }
+    }
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
     hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
