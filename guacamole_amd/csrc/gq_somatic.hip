@@ -78,29 +78,47 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
   const int32_t nmd = R.n_md[r];
   if (nmd < 0) return;  // GQ_E_NO_MD is raised by the histogram pass
   const float em = exp2f(-0.33219281f * (float)mq);  // 10^(-mapq/10)
-  const uint8_t *sq = R.seq + R.seq_off[r];
-  const uint8_t *ql = R.qual + R.seq_off[r];
+  const int64_t so = R.seq_off[r];
   const uint32_t *ev = R.md_ev + R.md_off[r];
   int k = 0;  // MD event cursor (events sorted by offset; runs visited in reference order)
+  int32_t ev_off = nmd > 0 ? (int32_t)(ev[0] >> 8) : 0x7FFFFFFF;
+  uint32_t ev_b = nmd > 0 ? (ev[0] & 0xFFu) : 0u;
   constexpr float kLn2 = 0.69314718f;
+  // bases and qualities share offsets: both come in aligned 16-byte chunks (the pools are
+  // device allocations, so the aligned chunk around a read's first / last byte is readable)
   auto run = [&](int32_t ra, int32_t rp0, int32_t len) {
     const int32_t a = ra > L0 ? ra : L0, b = (ra + len) < L1 ? (ra + len) : L1;
-    for (int32_t l = a; l < b; ++l) {
-      const int32_t rp = rp0 + (l - ra);
-      const uint8_t base = sq[rp];
-      const int q = (int)(int8_t)ql[rp];
-      while (k < nmd && (int32_t)(ev[k] >> 8) < l - s) ++k;
-      const uint8_t m = (k < nmd && (int32_t)(ev[k] >> 8) == l - s) ? (uint8_t)(ev[k] & 0xFFu) : base;
-      float t;
-      if (q < 0 || q > 127) {
-        t = -1e30f;  // outside the table: the exact kernel decides
-      } else {
-        const float eb = eq[q];
-        const float f = eb + em - eb * em;  // 1 - pc
-        if (base == m) t = kLn2 + __logf(1.0f - f) - fmaxf(0.0f, kLn2 + __logf(f));
-        else t = __logf(f);  // log(2 (1 - pc)) - ln 2
+    for (int32_t l = a; l < b;) {
+      const int64_t gp = so + rp0 + (l - ra);
+      const int sh = (int)(gp & 15);
+      const uint4 ws = *reinterpret_cast<const uint4 *>(R.seq + (gp - sh));
+      const uint4 wq = *reinterpret_cast<const uint4 *>(R.qual + (gp - sh));
+      const int nb = min(16 - sh, b - l);
+      for (int j = 0; j < nb; ++j) {
+        const int bi = sh + j, wi = bi >> 2, bs = 8 * (bi & 3);
+        const uint32_t w_s = wi == 0 ? ws.x : wi == 1 ? ws.y : wi == 2 ? ws.z : ws.w;
+        const uint32_t w_q = wi == 0 ? wq.x : wi == 1 ? wq.y : wi == 2 ? wq.z : wq.w;
+        const uint32_t base = (w_s >> bs) & 0xFFu;
+        const int q = (int)(int8_t)(uint8_t)(w_q >> bs);
+        const int32_t off = l + j - s;
+        while (ev_off < off) {
+          ++k;
+          ev_off = k < nmd ? (int32_t)(ev[k] >> 8) : 0x7FFFFFFF;
+          ev_b = k < nmd ? (ev[k] & 0xFFu) : 0u;
+        }
+        const uint32_t m = ev_off == off ? ev_b : base;
+        float t;
+        if (q < 0) {
+          t = -1e30f;  // outside the table: the exact kernel decides
+        } else {
+          const float eb = eq[q];
+          const float f = eb + em - eb * em;  // 1 - pc
+          if (base == m) t = kLn2 + __logf(1.0f - f) - fmaxf(0.0f, kLn2 + __logf(f));
+          else t = __logf(f);  // log(2 (1 - pc)) - ln 2
+        }
+        atomicAdd(&marg[l + j - L0], t);
       }
-      atomicAdd(&marg[l - L0], t);
+      l += nb;
     }
   };
   const int32_t lead = R.lead[r];

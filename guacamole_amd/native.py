@@ -334,23 +334,37 @@ class GermlineCalls:
 
 
 class SomaticCalls:
-    """CalledSomaticAllele records in output order."""
+    """CalledSomaticAllele records in output order: numpy columns copied out of the library's
+    result (one copy per column), row dicts built on first use of ``rows``."""
 
-    def __init__(self, rows: List[dict], visited: int, candidates: int):
-        self.rows, self.visited_loci, self.candidate_loci = rows, visited, candidates
+    def __init__(self, cols: Dict[str, np.ndarray], pool: bytes, visited: int, candidates: int):
+        self.cols, self.pool, self.visited_loci, self.candidate_loci = cols, pool, visited, candidates
+        self._rows: Optional[List[dict]] = None
 
     @staticmethod
     def from_struct(c: gq_somatic_calls) -> "SomaticCalls":
+        n = int(c.n)
+
+        def col(ptr):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0)
+        cols = {k: col(getattr(c, k)) for k in ("contig", "pos", "sample", "ref_off", "ref_len", "alt_off", "alt_len",
+                                                "log_odds", "gq", "tumor", "normal", "flags")}
         pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
-        rows = []
-        for i in range(c.n):
-            ro, rl, ao, al = c.ref_off[i], c.ref_len[i], c.alt_off[i], c.alt_len[i]
-            ev = lambda e: tuple(getattr(e, k) for k in EVIDENCE_FIELDS)
-            rows.append(dict(contig=int(c.contig[i]), locus=int(c.pos[i]), sample=int(c.sample[i]),
-                             ref=pool[ro:ro + rl].decode("latin-1"), alt=pool[ao:ao + al].decode("latin-1"),
-                             log_odds=float(c.log_odds[i]), gq=int(c.gq[i]), tumor=ev(c.tumor[i]),
-                             normal=ev(c.normal[i]), flags=int(c.flags[i])))
-        return SomaticCalls(rows, int(c.visited_loci), int(c.candidate_loci))
+        return SomaticCalls(cols, pool, int(c.visited_loci), int(c.candidate_loci))
+
+    @property
+    def rows(self) -> List[dict]:
+        if self._rows is None:
+            c, pool = self.cols, self.pool
+            n = len(self)
+            ev = lambda e: tuple(e[k].item() for k in EVIDENCE_FIELDS)
+            self._rows = [dict(contig=int(c["contig"][i]), locus=int(c["pos"][i]), sample=int(c["sample"][i]),
+                               ref=pool[c["ref_off"][i]:c["ref_off"][i] + c["ref_len"][i]].decode("latin-1"),
+                               alt=pool[c["alt_off"][i]:c["alt_off"][i] + c["alt_len"][i]].decode("latin-1"),
+                               log_odds=float(c["log_odds"][i]), gq=int(c["gq"][i]), tumor=ev(c["tumor"][i]),
+                               normal=ev(c["normal"][i]), flags=int(c["flags"][i])) for i in range(n)]
+        return self._rows
 
     def __len__(self) -> int:
-        return len(self.rows)
+        return int(self.cols["pos"].shape[0])
+
