@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--length", type=int, default=CHR20)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--tumor-depth", type=float, default=60.0)
+    ap.add_argument("--normal-depth", type=float, default=30.0)
+    ap.add_argument("--somatic-rate", type=float, default=2e-4)
     ap.add_argument("--cpu-window", type=int, default=200_000)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -37,8 +40,10 @@ def main():
     from guacamole_amd import native, synthetic
     t0 = time.time()
     seed = synthetic.SEED + 3
-    tg = synthetic.generate(args.length, 60.0, seed=seed, somatic_rate=2e-4, tumor=True, read_seed=11)
-    ng = synthetic.generate(args.length, 30.0, seed=seed, somatic_rate=2e-4, tumor=False, read_seed=12)
+    tg = synthetic.generate(args.length, args.tumor_depth, seed=seed, somatic_rate=args.somatic_rate, tumor=True,
+                            read_seed=11)
+    ng = synthetic.generate(args.length, args.normal_depth, seed=seed, somatic_rate=args.somatic_rate, tumor=False,
+                            read_seed=12)
     gen_s = time.time() - t0
     ctx = native.Context(0)
     t = ctx.upload(tg.arrays)
@@ -57,10 +62,13 @@ def main():
     el = time.perf_counter() - t1
     visited = int(calls.visited_loci)
     line = {
-        "metric": "somatic-standard loci/sec, tumor 60x / normal 30x", "value": visited * args.steps / el,
+        "metric": "somatic-standard loci/sec, tumor %gx / normal %gx" % (args.tumor_depth, args.normal_depth),
+        "value": visited * args.steps / el,
         "unit": "loci/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps,
-        "dtype": "u8 counts + f64 likelihoods", "data": "synthetic (native generator, somatic SNV rate 2e-4)",
-        "config": {"workload": "somatic-standard, synthetic tumor/normal 60x/30x, %d loci" % args.length,
+        "dtype": "u8 counts + f64 likelihoods",
+        "data": "synthetic (native generator, somatic SNV rate %g)" % args.somatic_rate,
+        "config": {"workload": "somatic-standard, synthetic tumor/normal %gx/%gx, %d loci" % (
+                       args.tumor_depth, args.normal_depth, args.length),
                    "tumor_reads": tg.n, "normal_reads": ng.n, "visited_loci": visited},
         "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items()},
         "candidate_loci": int(calls.candidate_loci),
@@ -73,7 +81,7 @@ def main():
         from guacamole_amd.loci import LociSet, flatten_partitions, partition_loci_uniformly
         from oracle import oracle as O
         from test_gpu_somatic import assert_rows_match
-        w0 = args.length // 3
+        w0 = args.length // 3 if args.length > 3 * args.cpu_window else 0
         w1 = min(args.length - 1, w0 + args.cpu_window)
         sel_t, sel_n = tg.window(w0, w1), ng.window(w0, w1)
         rt, rn = tg.to_read_set(sel_t), ng.to_read_set(sel_n)

@@ -197,3 +197,17 @@ def test_wrapped_device_reads_unordered_pool(gpu_ctx):
     assert got.tuples(g.contig_names) == ref.tuples(g.contig_names)
     want = O.germline_threshold(g.to_read_set(), loci, 8)
     assert ref.tuples(g.contig_names) == want
+
+
+def test_deep_panel_500x_germline(gpu_ctx):
+    """BASELINE configs[4] depth (500x, a targeted-panel region): deep tiles (thousands of reads
+    per tile, beyond the column kernel's stage) go through the walker; calls and per-locus
+    counts identical to the oracle."""
+    g = generate(12_000, 500.0, seed=5, indel_rate=3e-4)
+    rs = g.to_read_set()
+    loci = _loci(rs)
+    for t in (2, 8):
+        got = germline_threshold_reads(gpu_ctx, rs, loci, t)
+        want = O.germline_threshold(rs, loci, t)
+        assert got == want
+        assert len(want) > 10
