@@ -323,16 +323,49 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
   // items beyond a partition's capacity were never written (the host retries with larger ones)
   const unsigned long long n_items = ctr->part_off[1][kParts];
   const int rpart = kPartsCols + (int)(gwave & (kPartsCols - 1));  // this wave's record partition
+  // the reads covering the locus, compacted (tile-relative indices): the two per-read passes
+  // then run over ~depth lanes instead of every read of the tile (one latency chain, not three)
+  constexpr int kCover = 256;
+  __shared__ int32_t cover_buf[kBlock / 64][kCover];
+  int32_t *cover = cover_buf[threadIdx.x >> 6];
   for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
     const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
     const int32_t pos = item.pos;
+    int ncov = 0;
+    bool compact = true;
+    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
+      const int64_t r = r0 + lane;
+      const bool c = r < tl.re && R.start[r] <= pos && pos < R.end[r];
+      const unsigned long long b = __ballot(c);
+      const int at = ncov + (int)__popcll(b & ((1ull << lane) - 1ull));
+      if (c && at < kCover) cover[at] = (int32_t)(r - tl.rb);
+      ncov += (int)__popcll(b);
+    }
+    if (ncov > kCover) compact = false;  // deeper than the buffer: walk the tile's reads
+    __builtin_amdgcn_wave_barrier();
+    // read slot k of a pass: the k-th covering read (compact) or read rb + k (every read)
+    const int64_t n_slots = compact ? ncov : (tl.re - tl.rb);
+    auto slot_read = [&](int64_t k, bool *act) -> int64_t {
+      if (k >= n_slots) {
+        *act = false;
+        return tl.rb;
+      }
+      if (compact) {
+        *act = true;
+        return tl.rb + cover[k];
+      }
+      const int64_t r = tl.rb + k;
+      *act = R.start[r] <= pos && pos < R.end[r];
+      return r;
+    };
     // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
     uint32_t mask = 0;
     uint64_t best = ~0ull;  // (end, read) of the heap-root proxy among standard-base reads
-    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
-      const int64_t r = r0 + lane;
-      if (r < tl.re && R.start[r] <= pos && pos < R.end[r]) {
+    for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
+      bool cv;
+      const int64_t r = slot_read(k0 + lane, &cv);
+      if (cv) {
         const int v = md_ref_at(R, r, pos);
         if (v < 0) {
           raise_error(&ctr->err, (int64_t *)&ctr->err_pos, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT,
@@ -370,9 +403,9 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
     int nt = 0;  // used slots (uniform)
     bool overflow = false;
     uint32_t sample_total[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
-      const int64_t r = r0 + lane;
-      bool act = r < tl.re && R.start[r] <= pos && pos < R.end[r];
+    for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
+      bool act;
+      const int64_t r = slot_read(k0 + lane, &act);
       AlleleDesc d;
       Key128 key{0, 0};
       int smp = 0;
