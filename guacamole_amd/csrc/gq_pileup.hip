@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
     }
     int nt = 0;  // used slots (uniform)
     bool overflow = false;
-    uint32_t sample_total[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t st_lane = 0;  // lane s < 8: elements of sample s (read back with readlane: no scratch array)
     for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
       bool act;
       const int64_t r = slot_read(k0 + lane, &act);
@@ -420,9 +420,9 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
         }
       }
       // per-sample totals
-      for (int sm = 0; sm < 8; ++sm) {
+      for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
         const unsigned long long b = __ballot(act && smp == sm);
-        sample_total[sm] += (uint32_t)__popcll(b);
+        if (lane == sm) st_lane += (uint32_t)__popcll(b);
       }
       unsigned long long pending = __ballot(act);
       while (pending) {
@@ -479,8 +479,7 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
       continue;
     }
     if (item.flags & 1) {  // queued from a wide tile: count the visit here
-      uint32_t tot = 0;
-      for (int sm = 0; sm < 8; ++sm) tot += sample_total[sm];
+      const uint32_t tot = (uint32_t)__ballot(lane < 8 && st_lane > 0);
       if (tot == 0) continue;
       if (lane == 0) {
         atomicAdd(&ctr->visited, 1ull);
@@ -489,11 +488,11 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
     }
     // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
     const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
-    for (int sm = 0; sm < 8; ++sm) {
-      const uint32_t total = sample_total[sm];
+    for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)st_lane, sm);
       if (total == 0) continue;
-      // select top-3 passing entries by (count desc, allele asc)
-      int top[3] = {-1, -1, -1};
+      // select top-3 passing entries by (count desc, allele asc); three named slots, not an
+      // indexed array (a dynamically indexed array would live in scratch)
       uint32_t topc[3] = {0, 0, 0};
       AlleleDesc topd[3];
       int npass = 0;
@@ -515,20 +514,31 @@ __global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restric
           }
         if (dj.pad != sm) continue;
         if ((long long)cj * 100 / (long long)total <= threshold) continue;
+        const int f = npass < 3 ? npass : 3;  // entries held before this one (sorted)
         ++npass;
-        int p = npass - 1 < 3 ? npass - 1 : 3;
-        while (p > 0 && (topc[p - 1] < cj || (topc[p - 1] == cj && allele_cmp(R, dj, topd[p - 1], pos) < 0))) {
-          if (p < 3) {
-            top[p] = top[p - 1];
-            topc[p] = topc[p - 1];
-            topd[p] = topd[p - 1];
-          }
-          --p;
-        }
-        if (p < 3) {
-          top[p] = j;
-          topc[p] = cj;
-          topd[p] = dj;
+        auto better = [&](uint32_t ce, const AlleleDesc &de) {
+          return ce < cj || (ce == cj && allele_cmp(R, dj, de, pos) < 0);
+        };
+        // insertion position: past every held entry this one does not beat
+        const bool b2 = f > 2 && better(topc[2], topd[2]);
+        const bool b1 = f > 1 && (b2 || f == 2) && better(topc[1], topd[1]);
+        const bool b0 = f > 0 && (b1 || f == 1) && better(topc[0], topd[0]);
+        const int p = b0 ? 0 : b1 ? 1 : (b2 || f == 2) ? 2 : f;
+        if (p == 0) {
+          topc[2] = topc[1];
+          topd[2] = topd[1];
+          topc[1] = topc[0];
+          topd[1] = topd[0];
+          topc[0] = cj;
+          topd[0] = dj;
+        } else if (p == 1) {
+          topc[2] = topc[1];
+          topd[2] = topd[1];
+          topc[1] = cj;
+          topd[1] = dj;
+        } else if (p == 2) {
+          topc[2] = cj;
+          topd[2] = dj;
         }
       }
       const bool tie = npass >= 2 && (topc[0] == topc[1] || (npass >= 3 && topc[1] == topc[2]));
