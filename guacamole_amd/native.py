@@ -54,6 +54,10 @@ class gq_calls(C.Structure):
                 ("block_", C.c_void_p)]
 
 
+class gq_calls_device(C.Structure):
+    _fields_ = [("calls", gq_calls), ("image", C.c_void_p), ("image_bytes", C.c_int64)]
+
+
 class gq_counts(C.Structure):
     _fields_ = [("n_loci", C.c_int64), ("depth", C.POINTER(C.c_int32)), ("pos_depth", C.POINTER(C.c_int32)),
                 ("base_counts", C.POINTER(C.c_int32)), ("indel_counts", C.POINTER(C.c_int32)),
@@ -105,7 +109,8 @@ class gq_somatic_calls(C.Structure):
 
 
 EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
-            "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_free_calls", "gq_pileup_counts",
+            "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
+            "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic")
 
 
@@ -121,10 +126,12 @@ def lib():
         L.gq_version.restype = C.c_char_p
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device",
-                  "gq_germline_threshold", "gq_pileup_counts", "gq_somatic_standard"):
+                  "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
                                             C.POINTER(C.POINTER(gq_calls))]
+        L.gq_germline_threshold_device.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
+                                                   C.POINTER(gq_germline_params), C.POINTER(gq_calls_device)]
         L.gq_pileup_counts.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(C.POINTER(gq_counts))]
         L.gq_somatic_standard.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
                                           C.POINTER(gq_somatic_params), C.POINTER(C.POINTER(gq_somatic_calls))]
@@ -214,6 +221,15 @@ class Context:
         _check(lib().gq_germline_threshold(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
         return GermlineCalls.from_result(out)
 
+    def germline_threshold_device(self, reads: "DeviceReads", loci, threshold: int = 8, emit_ref: bool = False,
+                                  emit_no_call: bool = False) -> "DeviceCalls":
+        """gq_germline_threshold_device: the records stay in HBM (valid until the next call)."""
+        L, keep = make_gq_loci(*loci)
+        p = gq_germline_params(int(threshold), int(bool(emit_ref)), int(bool(emit_no_call)))
+        out = gq_calls_device()
+        _check(lib().gq_germline_threshold_device(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
+        return DeviceCalls(out)
+
     def somatic_standard(self, tumor: "DeviceReads", normal: "DeviceReads", loci, **params) -> "SomaticCalls":
         """somatic-standard over the loci ranges (gq_somatic_standard).  params: the
         gq_somatic_params fields; defaults SOMATIC_DEFAULTS (the CLI defaults)."""
@@ -260,6 +276,41 @@ class DeviceReads:
             self.free()
         except Exception:
             pass
+
+
+class DeviceCalls:
+    """Germline records left in HBM by gq_germline_threshold_device: one contiguous device image
+    (``image`` address, ``image_bytes``), its array offsets, and the run counters."""
+
+    NAMES = ("contig", "pos", "sample", "gt0", "gt1", "flags", "ref_off", "ref_len", "alt_off", "alt_len")
+
+    def __init__(self, d: gq_calls_device):
+        c = d.calls
+        self.n, self.image, self.image_bytes = int(c.n), int(d.image or 0), int(d.image_bytes)
+        self.pool_len = int(c.pool_len)
+        self.visited_loci, self.complex_loci = int(c.visited_loci), int(c.complex_loci)
+        self.ambiguous_loci, self.tie_loci = int(c.ambiguous_loci), int(c.tie_loci)
+        base = self.image
+        self.offsets = {k: (C.cast(getattr(c, k), C.c_void_p).value or base) - base for k in self.NAMES}
+        self.offsets["pool"] = (C.cast(c.allele_pool, C.c_void_p).value or base) - base
+        self._types = {k: np.dtype(getattr(c, k)._type_) for k in self.NAMES}
+
+    def __len__(self) -> int:
+        return self.n
+
+    def to_host(self) -> "GermlineCalls":
+        """Copy the image over PCIe (hipMemcpy) and view it as GermlineCalls (test / export)."""
+        host = np.zeros(max(self.image_bytes, 1), np.uint8)
+        if self.image_bytes:
+            hip = C.CDLL("libamdhip64.so")
+            hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+            rc = hip.hipMemcpy(host.ctypes.data, C.c_void_p(self.image), self.image_bytes, 2)  # DeviceToHost
+            if rc != 0:
+                raise GQError(8, "hipMemcpy of the result image failed (%d)" % rc)
+        a = {k: host[self.offsets[k]:self.offsets[k] + self.n * self._types[k].itemsize].view(self._types[k])
+             for k in self.NAMES}
+        pool = host[self.offsets["pool"]:self.offsets["pool"] + self.pool_len].tobytes()
+        return GermlineCalls(a, pool, self.visited_loci, self.complex_loci, self.ambiguous_loci, self.tie_loci)
 
 
 class GermlineCalls:

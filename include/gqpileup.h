@@ -133,6 +133,18 @@ typedef struct {
   void *block_;           /* owner of the arrays above (freed by gq_free_calls) */
 } gq_calls;
 
+/* The same records left in HBM (gq_germline_threshold_device): `calls` holds DEVICE pointers
+ * into one contiguous image owned by the context and valid until its next call (do not pass
+ * it to gq_free_calls).  Image layout: int64 pool_len at byte 0, then the arrays of `calls`
+ * in the order contig, pos, ref_off, alt_off, ref_len, alt_len, sample, gt0, gt1, flags, pool,
+ * each starting on a 64-byte boundary (the first at byte 64); image_bytes covers the pool's
+ * used bytes.  One buffer per rank is what the multi-GPU gather moves over xGMI.           */
+typedef struct {
+  gq_calls calls;
+  const void *image;
+  int64_t image_bytes;
+} gq_calls_device;
+
 typedef struct gq_ctx gq_ctx;
 typedef struct gq_dev_reads gq_dev_reads;
 
@@ -173,6 +185,10 @@ void gq_reads_free(gq_dev_reads *r);
 gq_status gq_germline_threshold(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
                                 const gq_germline_params *params, gq_calls **out);
 void gq_free_calls(gq_calls *c);
+/* gq_germline_threshold with the records left in HBM (no PCIe copy; the multi-GPU driver
+ * gathers the images over xGMI).  Same decisions, same record order.                      */
+gq_status gq_germline_threshold_device(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
+                                       const gq_germline_params *p, gq_calls_device *out);
 
 /* Raw per-locus pileup histogram for every locus of `loci` (dense, in range
  * order).  Categories: Match/Mismatch by sequenced base A,C,G,T,N,other; then

@@ -211,3 +211,22 @@ def test_deep_panel_500x_germline(gpu_ctx):
         want = O.germline_threshold(rs, loci, t)
         assert got == want
         assert len(want) > 10
+
+
+def test_device_results_equal_host_results(gpu_ctx, chrm):
+    """gq_germline_threshold_device leaves the same records in HBM as gq_germline_threshold
+    copies to the host (the bench's timed path vs the API the parity tests use)."""
+    from guacamole_amd.commands import device_reads
+    g = generate(80_000, 30, seed=3, indel_rate=3e-4)
+    for rs in (chrm, g.to_read_set()):
+        d = device_reads(gpu_ctx, rs)
+        loci = _loci(rs)
+        for args in ((8, False, False), (0, True, True), (25, False, True)):
+            h = gpu_ctx.germline_threshold(d, loci, *args)
+            dv = gpu_ctx.germline_threshold_device(d, loci, *args)
+            assert len(dv) == len(h) and dv.visited_loci == h.visited_loci
+            x = dv.to_host()
+            for k in h.a:
+                assert np.array_equal(x.a[k], h.a[k]), k
+            assert x.pool == h.pool
+            assert x.tuples(rs.contig_names) == h.tuples(rs.contig_names)
