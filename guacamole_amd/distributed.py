@@ -64,7 +64,7 @@ def gather_images_to_rank0(calls, device: str):
     mine = torch.empty(cap, dtype=torch.uint8, device=dev)
     if calls.image_bytes:
         torch.cuda.synchronize(dev)
-        hip = C.CDLL("libamdhip64.so")
+        hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
         hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         rc = hip.hipMemcpy(C.c_void_p(mine.data_ptr()), C.c_void_p(calls.image), int(calls.image_bytes), 3)
         if rc != 0:

@@ -302,7 +302,7 @@ class DeviceCalls:
         """Copy the image over PCIe (hipMemcpy) and view it as GermlineCalls (test / export)."""
         host = np.zeros(max(self.image_bytes, 1), np.uint8)
         if self.image_bytes:
-            hip = C.CDLL("libamdhip64.so")
+            hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
             hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
             rc = hip.hipMemcpy(host.ctypes.data, C.c_void_p(self.image), self.image_bytes, 2)  # DeviceToHost
             if rc != 0:

@@ -29,7 +29,7 @@ def main():
     got = parts[0].cpu().numpy()
     host = np.zeros(d.image_bytes, np.uint8)
     import ctypes as C
-    hip = C.CDLL("libamdhip64.so")
+    hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
     hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
     assert hip.hipMemcpy(host.ctypes.data, C.c_void_p(d.image), d.image_bytes, 2) == 0
     assert got.shape == host.shape and np.array_equal(got, host), "gathered image differs"

@@ -157,7 +157,7 @@ class _DeviceArray:
     def __init__(self, a):
         import ctypes as C
         if _DeviceArray._hip is None:
-            _DeviceArray._hip = C.CDLL("/opt/rocm/lib/libamdhip64.so")
+            _DeviceArray._hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the runtime libgqpileup.so already uses
         a = np.ascontiguousarray(a)
         self.shape, self.dtype, self.nbytes = a.shape, a.dtype, max(a.nbytes, 16)
         self.ptr = C.c_void_p()
