@@ -54,11 +54,22 @@ def main() -> int:
 
     rank, world, local = rank_info()
     dist = None
+    # GQ_DIST_BACKEND=gloo: a rehearsal of the N > 1 flow on fewer GPUs (ranks share devices,
+    # the gather goes through host memory); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("GQ_DIST_BACKEND", "nccl")
+    gather_dev = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            gather_dev = "cuda:%d" % local
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend)
+            gather_dev = "cpu"
 
     t0 = time.time()
     g = synthetic.generate(args.length, args.depth, seed=synthetic.SEED + 2 + rank)
@@ -80,7 +91,7 @@ def main() -> int:
     def step():
         calls = ctx.germline_threshold_device(reads, loci, args.threshold)
         if dist is not None:
-            gather_images_to_rank0(calls, "cuda:%d" % local)
+            gather_images_to_rank0(calls, gather_dev)
         return calls
 
     for _ in range(args.warmup):

@@ -45,6 +45,7 @@ def unpack_rows(buf: np.ndarray) -> List[tuple]:
 
 
 def gather_images_to_rank0(calls, device: str):
+    # device "cpu": the images are staged in host memory (a gloo rehearsal of the flow)
     """The terminal gather of the multi-GPU bench: every rank's germline result image (left in
     HBM by gq_germline_threshold_device) goes to rank 0's HBM with one RCCL gather over xGMI
     (sizes all-gathered first).  Returns rank 0's list of per-rank uint8 device tensors
@@ -63,12 +64,16 @@ def gather_images_to_rank0(calls, device: str):
     cap = max(1, max(sizes))
     mine = torch.empty(cap, dtype=torch.uint8, device=dev)
     if calls.image_bytes:
-        torch.cuda.synchronize(dev)
+        on_gpu = dev.type == "cuda"
+        if on_gpu:
+            torch.cuda.synchronize(dev)
         hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
         hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        rc = hip.hipMemcpy(C.c_void_p(mine.data_ptr()), C.c_void_p(calls.image), int(calls.image_bytes), 3)
+        # device to device (RCCL) or device to host (a gloo rehearsal)
+        rc = hip.hipMemcpy(C.c_void_p(mine.data_ptr()), C.c_void_p(calls.image), int(calls.image_bytes),
+                           3 if on_gpu else 2)
         if rc != 0:
-            raise RuntimeError("hipMemcpy (device to device) of the result image failed (%d)" % rc)
+            raise RuntimeError("hipMemcpy of the result image failed (%d)" % rc)
     if rank == 0:
         parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
         dist.gather(mine, gather_list=parts, dst=0)
