@@ -301,7 +301,10 @@ struct ColsCfg {
   static constexpr int kThreads = 512;
   static constexpr int kLanesPerCol = kThreads / (kT / 4);  // rows of a column split over 4 lanes
   static constexpr int kStage = 24 * 1024;  // sequence bytes (1 KiB DMA pieces)
-  static constexpr int kBatch = 6;          // rows per lane per column-pass batch (8 lanes per column)
+#ifndef GQ_COLS_BATCH
+#define GQ_COLS_BATCH 5
+#endif
+  static constexpr int kBatch = GQ_COLS_BATCH;  // rows per lane per column-pass batch (8 lanes per column)
   static constexpr int kMeta = 208;         // reads per tile (ColDesc rows); the row buffer holds
                                             // kRowCap rows: 8 * kBatch zero rows pad the batches
   static constexpr int kRowCap = 256;
