@@ -392,11 +392,14 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   constexpr int kNever = (int)(0x7FFFu | 0x80000000u);  // s = 32767, e = -32768: covers no column
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ __attribute__((aligned(16))) uint8_t buf[2][C::kBuf];
-  __shared__ uint32_t hist[NCOL];  // per column bucket: rows starting (lo 16) / prefix-max end reaching (hi 16)
-  __shared__ __attribute__((aligned(8))) uint2 xrow[C::kExtra];  // rows of general reads' count segments
+  // per buffer parity: column buckets (rows starting (lo 16) / prefix-max end reaching (hi 16))
+  // and the count of extra rows; the extra rows (general reads' count segments) themselves are
+  // written by B(i + 1) only after D(i) has read them (barrier 1), so one array serves
+  __shared__ uint32_t hist[2][NCOL];
+  __shared__ __attribute__((aligned(8))) uint2 xrow[C::kExtra];
   // byte masks of the bases [lo, hi) of an 8-locus column, lo, hi in 0..8: 0x07 per base
   __shared__ __attribute__((aligned(8))) uint2 bmask[81];
-  __shared__ unsigned n_xrow;
+  __shared__ unsigned n_xrow[2];
   __shared__ unsigned outn[2];  // records / complex items of this workgroup's partition
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -421,10 +424,10 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   {  // zero the histogram words, the buckets and the 16 zero bytes after each stage
     uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
     for (int i = t; i < W_N * S / 4; i += NT) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (t < NCOL) hist[t] = 0;
+    if (t < 2 * NCOL) hist[t >> 6][t & (NCOL - 1)] = 0;
     if (t < 2) *reinterpret_cast<uint4 *>(buf[t] + C::kStage) = make_uint4(0u, 0u, 0u, 0u);
     if (t < 2) outn[t] = 0;
-    if (t == 0) n_xrow = 0;
+    if (t < 2) n_xrow[t] = 0;
     if (t < 81) {
       const int lo = t / 9, hi = t % 9;
       uint32_t m0 = 0, m1 = 0;
@@ -461,40 +464,29 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     x.mb0 = (int64_t)((uint64_t)w[14] | ((uint64_t)w[15] << 32));
     return x;
   };
-  Tile tn = unpack(load_desc(i0));   // tile i0 (waited for once)
-  uint32_t dn2 = load_desc(i0 + 1);  // tile i0 + 1, in flight
-  if (i0 < i1) issue(tn, 0);
-  int it = 0;
-  for (int64_t i = i0; i < i1; ++i, ++it) {
-    const int b = it & 1;
-    const Tile tl = tn;
-    const int64_t tid_tile = i;
-    // ---- A: this tile's DMA (issued one tile ago) has landed everywhere; next tile's DMA
-    const uint64_t tw = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint64_t tv = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    __syncthreads();
-    if (i + 1 < i1) {
-      tn = unpack(dn2);  // loaded one tile ago
-      dn2 = load_desc(i + 2);
-      issue(tn, b ^ 1);
-    }
-    const uint64_t ta = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    const int32_t L0 = tl.L0, L1 = tl.L1;
-    uint8_t *L = buf[b];
-    const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L);
-    const int64_t d0 = (tl.rb * 24) & ~(int64_t)15;
-    uint32_t *rows = reinterpret_cast<uint32_t *>(L + C::kRowsOff + (tl.rb * 24 - d0));  // 6 words per read
+  // Row state a thread keeps from building a tile's rows (B) to its per-read pass (E)
+  struct RowState {
+    int32_t s = 0, base = 0, seg = 0, nseg = 0;
+    bool general = false;
+  };
+  // ---- B: rows of tile tb in buffer bb (thread per read) and its column buckets; threads
+  //      nch .. nch + 8 * kBatch - 1 write the zero rows that pad the column pass's batches.
+  //      Returns this thread's "the tile cannot take the column path" vote.
+  auto build = [&](const Tile &tb, int bb, RowState &rs) -> int {
+    rs = RowState{};
+    int not_col = tb.sbytes <= 0;
+    if (not_col) return 1;
+    const int32_t L0 = tb.L0, L1 = tb.L1;
+    uint8_t *L = buf[bb];
+    const int64_t d0 = (tb.rb * 24) & ~(int64_t)15;
+    uint32_t *rows = reinterpret_cast<uint32_t *>(L + C::kRowsOff + (tb.rb * 24 - d0));  // 6 words per read
     const uint32_t *evs = reinterpret_cast<const uint32_t *>(L + C::kEvOff);
-    const int nch = (int)(tl.re - tl.rb);
-    const uint32_t sb_lo = (uint32_t)(uint64_t)tl.sb0, mb_lo = (uint32_t)(uint64_t)tl.mb0;
-    // ---- B: rows (thread per read) and buckets; threads nch .. nch + 8 * kBatch - 1 write zero rows
-    //      (padding for the column pass's fixed batches), waves 4-7 issue the next tile's DMA
-    int not_col = tl.sbytes <= 0;
-    int32_t my_s = 0, my_e = 0, my_base = 0, my_seg = 0, my_nseg = 0;
-    bool mine = false, general = false;
-    if (!not_col && t < nch) {
-      uint32_t *d = rows + 6 * t;
+    const int nch = (int)(tb.re - tb.rb);
+    const uint32_t sb_lo = (uint32_t)(uint64_t)tb.sb0, mb_lo = (uint32_t)(uint64_t)tb.mb0;
+    uint32_t *hb = hist[bb];
+    const int k = t;  // thread per read
+    if (k < nch) {
+      uint32_t *d = rows + 6 * k;
       const int32_t s = (int32_t)d[0], e = (int32_t)d[1], pe = (int32_t)d[2];
       const uint32_t info = d[3];
       const int32_t srel = s - L0, erel = e - L0, perel = pe - L0;
@@ -502,26 +494,27 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       const uint32_t ea = d[5] - mb_lo;  // staged index of the first MD event
       const int32_t nmd = (int32_t)(info & 0xFFFFu);
       uint2 row = make_uint2(0u, 0u);  // empty: s = e = 0
+      bool mine = false;
       if (e > L0 && s < L1) {
         const uint32_t nseg = (info >> 18) & 0xFFu;
-        const bool evs_in = ea + (uint32_t)nmd + 2u * nseg <= (uint32_t)tl.mcnt;
-        const bool ok = (info & kColEligible) && sa + (uint32_t)(e - s) <= (uint32_t)tl.sbytes && evs_in;
+        const bool evs_in = ea + (uint32_t)nmd + 2u * nseg <= (uint32_t)tb.mcnt;
+        const bool ok = (info & kColEligible) && sa + (uint32_t)(e - s) <= (uint32_t)tb.sbytes && evs_in;
         const bool gen = (info & kColGeneral) && evs_in;
         if (gen) {  // its count segments become extra column rows
-          general = true;
+          rs.general = true;
           mine = true;
-          my_s = srel;
-          my_base = (int32_t)sa;
-          my_seg = (int32_t)(ea + (uint32_t)nmd);
-          my_nseg = (int32_t)nseg;
+          rs.s = srel;
+          rs.base = (int32_t)sa;
+          rs.seg = (int32_t)(ea + (uint32_t)nmd);
+          rs.nseg = (int32_t)nseg;
           for (uint32_t q = 0; q < nseg; ++q) {
             const uint32_t w0 = evs[ea + nmd + 2 * q], w1 = evs[ea + nmd + 2 * q + 1];
             if ((w1 >> 16) != kSegCountK) continue;
             const int32_t a = srel + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
             const uint32_t so = sa + (w1 & 0xFFFFu);  // stage address of the segment's first base
-            if (so + (uint32_t)(b - a) > (uint32_t)tl.sbytes) not_col = 1;
+            if (so + (uint32_t)(b - a) > (uint32_t)tb.sbytes) not_col = 1;
             if (b <= 0 || a >= L1 - L0) continue;
-            const unsigned x = atomicAdd(&n_xrow, 1u);
+            const unsigned x = atomicAdd(&n_xrow[bb], 1u);
             if (x >= (unsigned)C::kExtra) {
               not_col = 1;
               continue;
@@ -533,195 +526,239 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
         } else {
           row = col_row(srel, erel, sa - (uint32_t)srel, T);
           mine = true;
-          my_s = srel;
-          my_e = erel;
-          my_base = (int32_t)(sa - (uint32_t)srel);
         }
       }
       // rows [0, hi(col)) start at or before the column's last locus; rows [0, lo(col))
       // have prefix-max end at or before its first locus (so cover none of it)
       const int bs = srel < 0 ? 0 : srel >> 3, bp = perel < 0 ? 0 : (perel + 7) >> 3;
-      if (bs < NCOL) atomicAdd(&hist[bs], 1u);
-      if (bp < NCOL) atomicAdd(&hist[bp], 1u << 16);
+      if (bs < NCOL) atomicAdd(&hb[bs], 1u);
+      if (bp < NCOL) atomicAdd(&hb[bp], 1u << 16);
       // the row's words become: d0 d1 the column row, d4 = n_md | first event << 16 | mine << 31,
       // d5 = tile-relative start (for the MD-event pass)
       *reinterpret_cast<uint2 *>(d) = row;
       *reinterpret_cast<uint2 *>(d + 4) =
           make_uint2((uint32_t)nmd | (ea << 16) | (mine ? 0x80000000u : 0u), (uint32_t)srel);
-    } else if (!not_col && t < nch + 8 * C::kBatch && t < C::kRowCap) {
-      uint32_t *d = rows + 6 * t;
+    } else if (k < nch + 8 * C::kBatch && k < C::kRowCap) {
+      uint32_t *d = rows + 6 * k;
       *reinterpret_cast<uint2 *>(d) = make_uint2(0u, 0u);
     }
-    if (__syncthreads_or(not_col)) {  // uniform: the tile goes to the walker kernel
-      if (t < NCOL) hist[t] = 0;
-      if (t == 0) {
-        n_xrow = 0;
-        const unsigned long long k = atomicAdd(&ctr->n_slow, 1ull);
-        slow[k] = (int32_t)tid_tile;
-      }
-      continue;  // the next iteration's barrier orders the bucket reset
+    return not_col;
+  };
+
+  // Software pipeline over this workgroup's tiles, two barriers per tile.  Iteration i:
+  //   C/D/E(i)   bucket scan, column pass, per-read pass of tile i (buffer i & 1)
+  //   barrier 1  tile i's histogram complete; DMA(i + 1) landed (issued one iteration ago)
+  //   DMA(i + 2) into buffer i & 1 (free now); B(i + 1) on buffer (i + 1) & 1; decide(i)
+  //   barrier 2  tile i + 1's rows / buckets complete (its column-path vote); tile i's
+  //              histogram words zeroed by its decision
+  // Buckets (hist) and extra rows (xrow, n_xrow) are kept per buffer parity.
+  Tile tc{}, tn{};  // tile i (rows built) and tile i + 1
+  uint32_t d2 = 0;  // raw descriptor of tile i + 2 (one dword per lane, loaded ahead)
+  RowState rs_c, rs_n;
+  int slow_c = 1;
+  if (i0 < i1) {
+    tc = unpack(load_desc(i0));
+    issue(tc, 0);
+    if (i0 + 1 < i1) {
+      tn = unpack(load_desc(i0 + 1));
+      issue(tn, 1);
     }
-    // ---- C: inclusive scan of the packed buckets over the 64 columns, by every wave (no
-    //      barrier): lane l scans column l, then each lane fetches its own column's value
-    const int col = t >> 3, par = t & 7;  // lanes 8q .. 8q + 7 share column q, every eighth row
-    const uint32_t v = (uint32_t)__shfl((int)wave_incl_scan(hist[lane]), col, 64);
-    const int lo = (int)(v >> 16), hi = (int)(v & 0xFFFFu);
-    const uint64_t tc = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch, all
-    //      loads of a batch issued before use.  Per row: 3 LDS dwords -> 8 bases (2 dwords),
-    //      code = byte & 7 (A 1, C 3, T 4, N 6, G 7), two v_perm tables per dword into
-    //      A|C / T|G nibble fields, folded into byte counters before they can overflow.
-    constexpr int P = 8, U = C::kBatch;  // lanes per column, rows per batch (a column has ~31 rows at 30x)
-    const int c = W * col;
-    ColCounts cc;
-    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nv[2] = {0, 0}, nnib = 0;  // nibble / byte fields, rows in them
-    auto fold = [&]() {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        cc.ca[h] += nac[h] & 0x0F0F0F0Fu;
-        cc.cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
-        cc.ct[h] += ntg[h] & 0x0F0F0F0Fu;
-        cc.cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
-        cc.cv[h] += nv[h];
-        nac[h] = ntg[h] = nv[h] = 0;
-      }
-      nnib = 0;
-    };
-    // rows k0, k0 + P, ... of a row table at byte stride bs (rows past the range are empty
-    //   rows): the bases of [max(s, c), min(e, c + 8)) via a byte-mask lookup, so rows that
-    //   cover the column only partly (read ends) are counted here too
-    auto batch = [&](const uint8_t *tab, int bs, int k0, auto uu) {
-      constexpr int U = decltype(uu)::value;
-      const uint8_t *rp = tab + bs * k0;
-      uint2 m[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(rp + bs * P * u);
-      uint32_t a[U];
-      uint2 bm[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu) - c, e = ((int32_t)m[u].x >> 16) - c;
-        const int32_t l = s < 0 ? 0 : (s > 8 ? 8 : s), h = e < 0 ? 0 : (e > 8 ? 8 : e);
-        const bool ov = h > l;
-        a[u] = ov ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
-        bm[u] = bmask[ov ? 9 * l + h : 0];
-      }
-      uint32_t w0[U], w1[U], w2[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t *q = st32 + (a[u] >> 2);
-        w0[u] = q[0];
-        w1[u] = q[1];
-        w2[u] = q[2];
-      }
-      if (nnib + U > 15) fold();
-      if (cc.nrow + U > 255) {
-        fold();
-        cc.flush(cnt, S, c);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t s0 = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]) & bm[u].x;
-        const uint32_t s1 = __builtin_amdgcn_alignbyte(w2[u], w1[u], a[u]) & bm[u].y;
-        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, s0);
-        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, s0);
-        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, s1);
-        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, s1);
-        nv[0] += bm[u].x & 0x01010101u;
-        nv[1] += bm[u].y & 0x01010101u;
-      }
-      nnib += U;
-      cc.nrow += U;
-    };
-    if (!(dbg & 1)) {
-      for (int k0 = lo + par; k0 < hi; k0 += P * U)
-        batch(reinterpret_cast<const uint8_t *>(rows), 24, k0, std::integral_constant<int, U>{});
-      // extra rows (rare): one at a time, no padding
-      const int nx = (int)min(n_xrow, (unsigned)C::kExtra);
-      for (int k0 = par; k0 < nx; k0 += P)
-        batch(reinterpret_cast<const uint8_t *>(xrow), 8, k0, std::integral_constant<int, 1>{});
-    }
-    fold();
-    // the column's totals in all eight of its lanes (quad sums, then + the half-row mirror:
-    // lane i <-> 7 - i); lane par keeps locus c + par (= t) for the decision.  Bytes cannot
-    // overflow while the column's reads sum to <= 255; otherwise (deep pileups) each lane
-    // flushes its own counts into the LDS words.
+    d2 = load_desc(i0 + 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // the zeroing above, and tile i0's DMA
+    slow_c = __syncthreads_or(build(tc, 0, rs_c));
+    if (slow_c && t == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i0;
+  }
+  int it = 0;
+  for (int64_t i = i0; i < i1; ++i, ++it) {
+    const int b = it & 1;
+    const uint64_t ta = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     uint32_t regc[5] = {0, 0, 0, 0, 0};  // A C T G N of locus t from the column pass
-    {
-      auto csum = [](uint32_t x) {
-        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1 0 3 2
-        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2 3 0 1
-        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-        return x;
+    if (!slow_c) {
+      const Tile &tl = tc;
+      const int32_t L0 = tl.L0, L1 = tl.L1;
+      uint8_t *L = buf[b];
+      const uint32_t *st32 = reinterpret_cast<const uint32_t *>(L);
+      const int64_t d0 = (tl.rb * 24) & ~(int64_t)15;
+      uint32_t *rows = reinterpret_cast<uint32_t *>(L + C::kRowsOff + (tl.rb * 24 - d0));
+      const uint32_t *evs = reinterpret_cast<const uint32_t *>(L + C::kEvOff);
+      const int nch = (int)(tl.re - tl.rb);
+      // ---- C: inclusive scan of the packed buckets over the 64 columns, by every wave (no
+      //      barrier): lane l scans column l, then each lane fetches its own column's value
+      const int col = t >> 3, par = t & 7;  // lanes 8q .. 8q + 7 share column q, every eighth row
+      const uint32_t v = (uint32_t)__shfl((int)wave_incl_scan(hist[b][lane]), col, 64);
+      const int lo = (int)(v >> 16), hi = (int)(v & 0xFFFFu);
+      // ---- D: column pass: lanes par, par + P, ... of the column's rows, U rows per batch, all
+      //      loads of a batch issued before use.  Per row: 3 LDS dwords -> 8 bases (2 dwords),
+      //      code = byte & 7 (A 1, C 3, T 4, N 6, G 7), two v_perm tables per dword into
+      //      A|C / T|G nibble fields, folded into byte counters before they can overflow.
+      constexpr int P = 8, U = C::kBatch;  // lanes per column, rows per batch (a column has ~31 rows at 30x)
+      const int c = W * col;
+      ColCounts cc;
+      uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0}, nv[2] = {0, 0}, nnib = 0;  // nibble / byte fields, rows in them
+      auto fold = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          cc.ca[h] += nac[h] & 0x0F0F0F0Fu;
+          cc.cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
+          cc.ct[h] += ntg[h] & 0x0F0F0F0Fu;
+          cc.cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
+          cc.cv[h] += nv[h];
+          nac[h] = ntg[h] = nv[h] = 0;
+        }
+        nnib = 0;
       };
-      // a column deeper than 255 rows: each lane flushes its own counts instead
-      const uint32_t nq = csum(cc.nrow);
-      if (nq > 255) {
-        cc.flush(cnt, S, c);
-      } else {
-        const int h = par >> 2, sh = 8 * (par & 3);
-        const uint32_t a0 = csum(cc.ca[0]), a1 = csum(cc.ca[1]), c0 = csum(cc.cc[0]), c1 = csum(cc.cc[1]);
-        const uint32_t t0 = csum(cc.ct[0]), t1 = csum(cc.ct[1]), g0 = csum(cc.cg[0]), g1 = csum(cc.cg[1]);
-        const uint32_t v0 = csum(cc.cv[0]), v1 = csum(cc.cv[1]);
-        regc[0] = ((h ? a1 : a0) >> sh) & 0xFFu;
-        regc[1] = ((h ? c1 : c0) >> sh) & 0xFFu;
-        regc[2] = ((h ? t1 : t0) >> sh) & 0xFFu;
-        regc[3] = ((h ? g1 : g0) >> sh) & 0xFFu;
-        regc[4] = (((h ? v1 : v0) >> sh) & 0xFFu) - regc[0] - regc[1] - regc[2] - regc[3];
+      // rows k0, k0 + P, ... of a row table at byte stride bs (rows past the range are empty
+      //   rows): the bases of [max(s, c), min(e, c + 8)) via a byte-mask lookup, so rows that
+      //   cover the column only partly (read ends) are counted here too
+      auto batch = [&](const uint8_t *tab, int bs, int k0, auto uu) {
+        constexpr int U = decltype(uu)::value;
+        const uint8_t *rp = tab + bs * k0;
+        uint2 m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] = *reinterpret_cast<const uint2 *>(rp + bs * P * u);
+        uint32_t a[U];
+        uint2 bm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int32_t s = (int32_t)(int16_t)(m[u].x & 0xFFFFu) - c, e = ((int32_t)m[u].x >> 16) - c;
+          const int32_t l = s < 0 ? 0 : (s > 8 ? 8 : s), h = e < 0 ? 0 : (e > 8 ? 8 : e);
+          const bool ov = h > l;
+          a[u] = ov ? m[u].y + (uint32_t)c : (uint32_t)C::kStage;  // 12 zero bytes
+          bm[u] = bmask[ov ? 9 * l + h : 0];
+        }
+        uint32_t w0[U], w1[U], w2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t *q = st32 + (a[u] >> 2);
+          w0[u] = q[0];
+          w1[u] = q[1];
+          w2[u] = q[2];
+        }
+        if (nnib + U > 15) fold();
+        if (cc.nrow + U > 255) {
+          fold();
+          cc.flush(cnt, S, c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t s0 = __builtin_amdgcn_alignbyte(w1[u], w0[u], a[u]) & bm[u].x;
+          const uint32_t s1 = __builtin_amdgcn_alignbyte(w2[u], w1[u], a[u]) & bm[u].y;
+          nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, s0);
+          ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, s0);
+          nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, s1);
+          ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, s1);
+          nv[0] += bm[u].x & 0x01010101u;
+          nv[1] += bm[u].y & 0x01010101u;
+        }
+        nnib += U;
+        cc.nrow += U;
+      };
+      if (!(dbg & 1)) {
+        for (int k0 = lo + par; k0 < hi; k0 += P * U)
+          batch(reinterpret_cast<const uint8_t *>(rows), 24, k0, std::integral_constant<int, U>{});
+        // extra rows (rare): one at a time, no padding
+        const int nx = (int)min(n_xrow[b], (unsigned)C::kExtra);
+        for (int k0 = par; k0 < nx; k0 += P)
+          batch(reinterpret_cast<const uint8_t *>(xrow), 8, k0, std::integral_constant<int, 1>{});
       }
-    }
-    const uint64_t te = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // ---- E: threads t < 256 the column ends of read t, threads t >= 256 the MD events of
-    //      read t - 256 (into the LDS histogram, GermSink)
-    if (!(dbg & 2)) {
-      GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
-      if (general) {  // segments: the complex loci (count segments are column rows)
-        for (int32_t q = 0; q < my_nseg; ++q) {
-          const uint32_t w0 = evs[my_seg + 2 * q], w1 = evs[my_seg + 2 * q + 1];
-          const int32_t a = my_s + (int32_t)(w0 & 0xFFFFu), b = a + (int32_t)(w0 >> 16);
-          if (b <= 0 || a >= T || (w1 >> 16) == kSegCountK) continue;
-          for (int32_t l = a > 0 ? a : 0; l < (b < T ? b : T); ++l) sink.complex_i(l);
+      fold();
+      // the column's totals in all eight of its lanes (quad sums, then + the half-row mirror:
+      // lane i <-> 7 - i); lane par keeps locus c + par (= t) for the decision.  Bytes cannot
+      // overflow while the column's reads sum to <= 255; otherwise (deep pileups) each lane
+      // flushes its own counts into the LDS words.
+      {
+        auto csum = [](uint32_t x) {
+          x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1 0 3 2
+          x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2 3 0 1
+          x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+          return x;
+        };
+        // a column deeper than 255 rows: each lane flushes its own counts instead
+        const uint32_t nq = csum(cc.nrow);
+        if (nq > 255) {
+          cc.flush(cnt, S, c);
+        } else {
+          const int h = par >> 2, sh = 8 * (par & 3);
+          const uint32_t a0 = csum(cc.ca[0]), a1 = csum(cc.ca[1]), c0 = csum(cc.cc[0]), c1 = csum(cc.cc[1]);
+          const uint32_t t0 = csum(cc.ct[0]), t1 = csum(cc.ct[1]), g0 = csum(cc.cg[0]), g1 = csum(cc.cg[1]);
+          const uint32_t v0 = csum(cc.cv[0]), v1 = csum(cc.cv[1]);
+          regc[0] = ((h ? a1 : a0) >> sh) & 0xFFu;
+          regc[1] = ((h ? c1 : c0) >> sh) & 0xFFu;
+          regc[2] = ((h ? t1 : t0) >> sh) & 0xFFu;
+          regc[3] = ((h ? g1 : g0) >> sh) & 0xFFu;
+          regc[4] = (((h ? v1 : v0) >> sh) & 0xFFu) - regc[0] - regc[1] - regc[2] - regc[3];
         }
       }
-      const int k = t - C::kMeta;
-      if (k >= 0 && k < nch && !(dbg & 64)) {
-        const uint32_t *d = rows + 6 * k;
-        const uint32_t d4 = d[4];
-        const int32_t nmd = (int32_t)(d4 & 0xFFFFu);
-        if ((d4 & 0x80000000u) && nmd > 0) {
-          const int32_t s = (int32_t)d[5], x1 = L1 - L0;
-          const int32_t e0 = (int32_t)((d4 >> 16) & 0x7FFFu);
-          for (int32_t k0 = 0; k0 < nmd; k0 += 4) {  // events are sorted by offset; 4 loads in flight
-            uint32_t w4[4];
+      // ---- E: threads t >= kMeta: the MD events of read t - kMeta; the builders of general
+      //      reads: their complex segment loci (into the LDS histogram, GermSink)
+      if (!(dbg & 2)) {
+        GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+        if (rs_c.general) {  // segments: the complex loci (count segments are column rows)
+          for (int32_t q = 0; q < rs_c.nseg; ++q) {
+            const uint32_t w0 = evs[rs_c.seg + 2 * q], w1 = evs[rs_c.seg + 2 * q + 1];
+            const int32_t a = rs_c.s + (int32_t)(w0 & 0xFFFFu), bq = a + (int32_t)(w0 >> 16);
+            if (bq <= 0 || a >= T || (w1 >> 16) == kSegCountK) continue;
+            for (int32_t l = a > 0 ? a : 0; l < (bq < T ? bq : T); ++l) sink.complex_i(l);
+          }
+        }
+        const int k = t - C::kMeta;
+        if (k >= 0 && k < nch && !(dbg & 64)) {
+          const uint32_t *d = rows + 6 * k;
+          const uint32_t d4 = d[4];
+          const int32_t nmd = (int32_t)(d4 & 0xFFFFu);
+          if ((d4 & 0x80000000u) && nmd > 0) {
+            const int32_t s = (int32_t)d[5], x1 = L1 - L0;
+            const int32_t e0 = (int32_t)((d4 >> 16) & 0x7FFFu);
+            for (int32_t k0 = 0; k0 < nmd; k0 += 4) {  // events are sorted by offset; 4 loads in flight
+              uint32_t w4[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) w4[u] = evs[e0 + min(k0 + u, nmd - 1)];
+              for (int u = 0; u < 4; ++u) w4[u] = evs[e0 + min(k0 + u, nmd - 1)];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int32_t l = s + (int32_t)(w4[u] >> 16);
-              if (k0 + u < nmd && l >= 0 && l < x1) sink.event_i(l, (uint8_t)w4[u], (uint8_t)(w4[u] >> 8), 0);
+              for (int u = 0; u < 4; ++u) {
+                const int32_t l = s + (int32_t)(w4[u] >> 16);
+                if (k0 + u < nmd && l >= 0 && l < x1) sink.event_i(l, (uint8_t)w4[u], (uint8_t)(w4[u] >> 8), 0);
+              }
             }
           }
         }
       }
     }
-    __syncthreads();  // histogram complete
-    if (t == 0) n_xrow = 0;  // the next tile's row-build follows this tile's barriers
-    if (t < NCOL) hist[t] = 0;
+    const uint64_t te = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMA(i + 1) has landed (this wave's part)
+    __syncthreads();                                   // 1: histogram of tile i complete
+    const uint64_t tb = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    if (t < NCOL) hist[b][t] = 0;  // buffer parity b is next built for tile i + 2
+    if (t == 0) n_xrow[b] = 0;
+    Tile t2{};
+    const bool has2 = i + 2 < i1, has1 = i + 1 < i1;
+    if (has2) {
+      t2 = unpack(d2);
+      d2 = load_desc(i + 3);
+      issue(t2, b);
+    }
+    const int vote = has1 ? build(tn, b ^ 1, rs_n) : 0;
+    // ---- F: decision of tile i, then its histogram words are zeroed for tile i + 1
+    // (each thread zeroes the words of its own locus after reading them)
+    if (!slow_c)
+      germline_decide<T, true>(cnt, tc, i, false, n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
+                               visited, amb, ties, regc);
     const uint64_t tf = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // ---- F: decision, then the histogram words are zeroed for the next tile
-    // (each thread zeroes the words of its own locus after reading them: no barrier)
-    germline_decide<T, true>(cnt, tl, tid_tile, false, n_samples, threshold, emit_ref, emit_no_call, recs, cplx, out,
-                             visited, amb, ties, regc);
+    const int slow_n = __syncthreads_or(vote);  // 2: rows of tile i + 1 complete
+    if (has1 && slow_n && t == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)(i + 1);
     if (dbg & 16) {
       const uint64_t now = __builtin_readcyclecounter();
-      clk[0] += now - ta;  // tile total from after the A barrier
-      clk[1] += te - tc;   // scan + column pass
-      clk[2] += tf - te;   // per-read pass + barrier
-      clk[3] += now - tf;  // decision
+      clk[0] += now - ta;  // tile total
+      clk[1] += te - ta;   // scan + column pass + per-read pass
+      clk[2] += tb - te;   // vmcnt + barrier 1
+      clk[3] += tf - tb;   // DMA issue + next tile's rows + decision
       clk[4] += 1;
-      clk[5] += tv - tw;   // vmcnt wait at A
-      clk[6] += ta - tv;   // barrier A + next DMA issue
+      clk[5] += now - tf;  // barrier 2
     }
+    tc = tn;
+    tn = t2;
+    rs_c = rs_n;
+    slow_c = has1 ? slow_n : 1;
   }
   add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
   if (t == 0) {  // this workgroup's partition counts (may exceed the capacity: host retry)

@@ -1275,11 +1275,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   }
   if (getenv("GQ_DBG") && hc.prof[7])
     fprintf(stderr,
-            "gq prof (cycles/tile/wave): tile %.0f scan+column %.0f per-read %.0f decide %.0f | vmcnt-wait %.0f "
-            "barrier+issue %.0f (%llu)\n",
+            "gq prof (cycles/tile/wave): tile %.0f scan+column+per-read %.0f vmcnt+barrier1 %.0f "
+            "dma+rows+decide %.0f barrier2 %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[7], (double)hc.prof[1] / hc.prof[7], (double)hc.prof[2] / hc.prof[7],
-            (double)hc.prof[3] / hc.prof[7], (double)hc.prof[4] / hc.prof[7], (double)hc.prof[5] / hc.prof[7],
-            hc.prof[7]);
+            (double)hc.prof[3] / hc.prof[7], (double)hc.prof[4] / hc.prof[7], hc.prof[7]);
   for (int k = 0; k < kSpread; ++k) {
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];
