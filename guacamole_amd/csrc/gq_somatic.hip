@@ -329,17 +329,62 @@ __device__ void raise_at(Counters *ctr, int code, int64_t where) {
   raise_error(&ctr->err, (int64_t *)&ctr->err_pos, code, where);
 }
 
+// The reads of a tile window [rb, re) covering pos, compacted into a per-wave LDS list (tile-
+// relative indices, in read order) so the per-read passes below run over ~depth lanes rather
+// than every read of the window; deeper than the list: the passes walk the window instead.
+constexpr int kCover = 768;
+struct Cover {
+  const int32_t *lst;
+  int64_t rb, n;  // slots
+  bool compact;
+  // read of slot k and whether it covers pos
+  __device__ __forceinline__ int64_t read(const DevReads &R, int64_t k, int32_t pos, bool *act) const {
+    if (k >= n) {
+      *act = false;
+      return rb;
+    }
+    if (compact) {
+      *act = true;
+      return rb + lst[k];
+    }
+    const int64_t r = rb + k;
+    *act = R.start[r] <= pos && pos < R.end[r];
+    return r;
+  }
+};
+__device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst) {
+  const int lane = threadIdx.x & 63;
+  int64_t n = 0;
+  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+    const int64_t r = r0 + lane;
+    const bool c = r < re && R.start[r] <= pos && pos < R.end[r];
+    const unsigned long long b = __ballot(c);
+    const int64_t at = n + (int64_t)__popcll(b & ((1ull << lane) - 1ull));
+    if (c && at < kCover) lst[at] = (int32_t)(r - rb);
+    n += (int64_t)__popcll(b);
+  }
+  __builtin_amdgcn_wave_barrier();
+  Cover cv;
+  cv.lst = lst;
+  cv.rb = rb;
+  cv.compact = n <= kCover;
+  cv.n = cv.compact ? n : (re - rb);
+  return cv;
+}
+
 // Pileup.referenceBaseAtLocus over the reads of window [rb, re) covering pos (as in
 // germline_complex: first standard MD-derived base; heap order approximated by the minimum
 // (end, index) read when the bases disagree, flagged ambiguous).
-__device__ void pileup_ref(const DevReads &R, int64_t rb, int64_t re, int32_t pos, Counters *ctr, uint8_t &refbase,
+__device__ void pileup_ref(const DevReads &R, const Cover &cv, int32_t pos, Counters *ctr, uint8_t &refbase,
                            bool &ambiguous) {
   const int lane = threadIdx.x & 63;
+  const int64_t rb = cv.rb;
   uint32_t mask = 0;
   uint64_t best = ~0ull;
-  for (int64_t r0 = rb; r0 < re; r0 += 64) {
-    const int64_t r = r0 + lane;
-    if (r < re && R.start[r] <= pos && pos < R.end[r]) {
+  for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
+    bool cov;
+    const int64_t r = cv.read(R, k0 + lane, pos, &cov);
+    if (cov) {
       const int v = md_ref_at(R, r, pos);
       if (v < 0) {
         raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
@@ -363,9 +408,10 @@ __device__ void pileup_ref(const DevReads &R, int64_t rb, int64_t re, int32_t po
 
 // Build the allele table of one sample's pileup at pos.
 __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
-                              bool include_alignment, Counters *ctr, SamplePile &P) {
+                              bool include_alignment, Counters *ctr, SamplePile &P, int32_t *cover_lds) {
   const int lane = threadIdx.x & 63;
-  pileup_ref(R, rb, re, pos, ctr, P.refbase, P.ambiguous);
+  const Cover cv = make_cover(R, rb, re, pos, cover_lds);
+  pileup_ref(R, cv, pos, ctr, P.refbase, P.ambiguous);
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
     P.klo[s] = P.khi[s] = 0;
@@ -375,9 +421,9 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
   P.nt = 0;
   P.depth_all = P.depth_f = P.fwd_f = 0;
   P.overflow = false;
-  for (int64_t r0 = rb; r0 < re; r0 += 64) {
-    const int64_t r = r0 + lane;
-    bool act = r < re && R.start[r] <= pos && pos < R.end[r];
+  for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
+    bool act;
+    const int64_t r = cv.read(R, k0 + lane, pos, &act);
     AlleleDesc d;
     Key128 key{0, 0};
     bool pass = false;
@@ -406,7 +452,7 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
     const unsigned long long actb = __ballot(act), passb = __ballot(act && pass);
     P.depth_all += (uint32_t)__popcll(actb);
     P.depth_f += (uint32_t)__popcll(passb);
-    P.fwd_f += (uint32_t)__popcll(__ballot(act && pass && !(R.flags[r < re ? r : rb] & 1)));
+    P.fwd_f += (uint32_t)__popcll(__ballot(act && pass && !(R.flags[r] & 1)));
     unsigned long long pending = actb;
     while (pending) {
       const int leader = __ffsll((long long)pending) - 1;
@@ -614,14 +660,16 @@ __device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, int32_t 
 // in element order for the running mean and the medians.
 __device__ void allele_evidence(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
                                 const SamplePile &P, Key128 target, double likelihood, uint32_t *ev_lds,
-                                Counters *ctr, gq_evidence &ev) {
+                                Counters *ctr, gq_evidence &ev, int32_t *cover_lds) {
   const int lane = threadIdx.x & 63;
+  const Cover cv = make_cover(R, rb, re, pos, cover_lds);
   uint32_t n = 0, fwd = 0;
-  for (int64_t r0 = rb; r0 < re; r0 += 64) {
-    const int64_t r = r0 + lane;
+  for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
+    bool cov;
+    const int64_t r = cv.read(R, k0 + lane, pos, &cov);
     bool hit = false;
     uint32_t packed = 0;
-    if (r < re && R.start[r] <= pos && pos < R.end[r]) {
+    if (cov) {
       const int mq = (int)R.mapq[r];
       if (min_mapq <= 0 || mq >= min_mapq) {
         AlleleDesc d;
@@ -709,6 +757,7 @@ __global__ __launch_bounds__(kBlock) void somatic_call(const Tile *__restrict__ 
   __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
   __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
   __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
+  __shared__ int32_t cover_lds[kSomWaves][kCover];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -718,8 +767,8 @@ __global__ __launch_bounds__(kBlock) void somatic_call(const Tile *__restrict__ 
     const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
     const int32_t pos = item.pos;
     SamplePile PT, PN;
-    gather_sample(RT, tt.rb, tt.re, pos, prm.min_mapq, true, ctr, PT);
-    gather_sample(RN, tn.rb, tn.re, pos, prm.min_mapq, false, ctr, PN);
+    gather_sample(RT, tt.rb, tt.re, pos, prm.min_mapq, true, ctr, PT, cover_lds[wv]);
+    gather_sample(RN, tn.rb, tn.re, pos, prm.min_mapq, false, ctr, PN, cover_lds[wv]);
     if (PT.overflow || PN.overflow) {
       raise_at(ctr, GQ_E_CAPACITY, pos);
       continue;
@@ -765,8 +814,8 @@ __global__ __launch_bounds__(kBlock) void somatic_call(const Tile *__restrict__ 
     const Key128 tkey = allele_key(RT, al, pos, 0);
     const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
     gq_evidence tev, nev;
-    allele_evidence(RT, tt.rb, tt.re, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev);
-    allele_evidence(RN, tn.rb, tn.re, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev);
+    allele_evidence(RT, tt.rb, tt.re, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev, cover_lds[wv]);
+    allele_evidence(RN, tn.rb, tn.re, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev, cover_lds[wv]);
     const double log_odds = log(odds);
     const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
     if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
