@@ -296,6 +296,12 @@ __device__ __forceinline__ void add_run_counters(Counters *ctr, unsigned visited
 // Per workgroup: two LDS buffers of {sequence stage, ColDesc rows, MD events} (the next
 // tile's are DMA'd while this one is counted), the histogram words, the column buckets:
 // about 80 KiB, two workgroups per CU.  plan_tiles marks tiles whose window fits.
+#ifndef GQ_DMA_W0
+#define GQ_DMA_W0 5   // waves GQ_DMA_W0 .. 7 issue the DMA (measured: 5 beats 4 and 6)
+#endif
+#ifndef GQ_EV_T0
+#define GQ_EV_T0 96   // thread GQ_EV_T0 + k takes the MD events of read k (waves 1-4)
+#endif
 struct ColsCfg {
   static constexpr int kT = 512;
   static constexpr int kThreads = 512;
@@ -409,17 +415,17 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
   uint64_t clk[7] = {0, 0, 0, 0, 0, 0, 0};
 
-  // DMA of a tile's window into buffer b, by waves 4-7 (waves 0-3 build rows meanwhile)
+  // DMA of a tile's window into buffer b, by waves GQ_DMA_W0 .. 7 (waves 0-2 build rows meanwhile)
   auto issue = [&](const Tile &tn, int b) {
-    if (tn.sbytes <= 0 || (dbg & 8) || wave < 4) return;
+    if (tn.sbytes <= 0 || (dbg & 8) || wave < GQ_DMA_W0) return;
     uint8_t *L = buf[b];
-    const int w4 = wave - 4;
-    dma_range<4, 16>(seq + tn.sb0, L, tn.sbytes, w4, lane);
+    const int w4 = wave - GQ_DMA_W0;
+    dma_range<NW - GQ_DMA_W0, 16>(seq + tn.sb0, L, tn.sbytes, w4, lane);
     const int64_t d0 = (tn.rb * 24) & ~(int64_t)15;
-    dma_range<4, 4>(reinterpret_cast<const uint8_t *>(cdesc) + d0, L + C::kRowsOff, (int)(tn.re * 24 - d0), w4,
+    dma_range<NW - GQ_DMA_W0, 4>(reinterpret_cast<const uint8_t *>(cdesc) + d0, L + C::kRowsOff, (int)(tn.re * 24 - d0), w4,
                     lane);
     if (tn.mcnt > 0)
-      dma_range<4, 4>(reinterpret_cast<const uint8_t *>(cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, w4, lane);
+      dma_range<NW - GQ_DMA_W0, 4>(reinterpret_cast<const uint8_t *>(cev + tn.mb0), L + C::kEvOff, tn.mcnt * 4, w4, lane);
   };
   {  // zero the histogram words, the buckets and the 16 zero bytes after each stage
     uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
           regc[4] = (((h ? v1 : v0) >> sh) & 0xFFu) - regc[0] - regc[1] - regc[2] - regc[3];
         }
       }
-      // ---- E: threads t >= kMeta: the MD events of read t - kMeta; the builders of general
+      // ---- E: thread GQ_EV_T0 + k: the MD events of read k; the builders of general
       //      reads: their complex segment loci (into the LDS histogram, GermSink)
       if (!(dbg & 2)) {
         GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
             for (int32_t l = a > 0 ? a : 0; l < (bq < T ? bq : T); ++l) sink.complex_i(l);
           }
         }
-        const int k = t - C::kMeta;
+        const int k = t - GQ_EV_T0;
         if (k >= 0 && k < nch && !(dbg & 64)) {
           const uint32_t *d = rows + 6 * k;
           const uint32_t d4 = d[4];
