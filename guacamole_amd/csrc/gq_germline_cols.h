@@ -299,6 +299,9 @@ __device__ __forceinline__ void add_run_counters(Counters *ctr, unsigned visited
 #ifndef GQ_DMA_W0
 #define GQ_DMA_W0 5   // waves GQ_DMA_W0 .. 7 issue the DMA (measured: 5 beats 4 and 6)
 #endif
+#ifndef GQ_B_T0
+#define GQ_B_T0 0     // thread GQ_B_T0 + k builds the row of read k
+#endif
 #ifndef GQ_EV_T0
 #define GQ_EV_T0 96   // thread GQ_EV_T0 + k takes the MD events of read k (waves 1-4)
 #endif
@@ -490,8 +493,8 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
     const int nch = (int)(tb.re - tb.rb);
     const uint32_t sb_lo = (uint32_t)(uint64_t)tb.sb0, mb_lo = (uint32_t)(uint64_t)tb.mb0;
     uint32_t *hb = hist[bb];
-    const int k = t;  // thread per read
-    if (k < nch) {
+    const int k = t - GQ_B_T0;  // thread per read
+    if (k >= 0 && k < nch) {
       uint32_t *d = rows + 6 * k;
       const int32_t s = (int32_t)d[0], e = (int32_t)d[1], pe = (int32_t)d[2];
       const uint32_t info = d[3];
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(ColsCfg::kThreads) void germline_cols(
       *reinterpret_cast<uint2 *>(d) = row;
       *reinterpret_cast<uint2 *>(d + 4) =
           make_uint2((uint32_t)nmd | (ea << 16) | (mine ? 0x80000000u : 0u), (uint32_t)srel);
-    } else if (k < nch + 8 * C::kBatch && k < C::kRowCap) {
+    } else if (k >= 0 && k < nch + 8 * C::kBatch && k < C::kRowCap) {
       uint32_t *d = rows + 6 * k;
       *reinterpret_cast<uint2 *>(d) = make_uint2(0u, 0u);
     }
