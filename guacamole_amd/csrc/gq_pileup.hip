@@ -311,7 +311,8 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
 // ------------------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(kBlock) void germline_complex(const Tile *__restrict__ tiles,
+// four waves per SIMD (128 VGPRs; a few spills) beat three without spills: the kernel is latency-bound
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
                                                            int threshold, int emit_ref, int emit_no_call,
                                                            CallRec *__restrict__ recs, OutGeom og,
