@@ -47,6 +47,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_slow;       // tiles germline_cols handed to germline_walk
   unsigned long long n_dead;       // record slots germline_expand left unused
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
+  unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
   // per-tile run counters, spread over kSpread addresses (summed on the host)
   unsigned long long spread[3][64];
   unsigned long long prof[8];  // diagnostic phase clocks (GQ_DBG=16 only)
@@ -140,6 +141,28 @@ __device__ __forceinline__ unsigned wave_reserve_lds(unsigned *ctr, unsigned n) 
 struct Plan {
   int64_t n_tiles = 0;
   int64_t n_loci = 0;
+  int T = 0;
+  // the non-empty loci ranges in call order (host copies): contig, [start, end), first tile,
+  // task, and the window each belongs to.  A window = a maximal run of ranges of one (task,
+  // contig): one SlidingWindow per task and contig (DistributedUtil.scala:473-486).
+  std::vector<int32_t> rc, rwin;
+  std::vector<int64_t> rs, re, rt, rtask;
+  struct Win {
+    int32_t contig;
+    int64_t r0, r1;  // ranges [r0, r1)
+  };
+  std::vector<Win> wins;
+  int64_t range_of_tile(int64_t t) const {  // last range whose first tile <= t
+    return (int64_t)(std::upper_bound(rt.begin(), rt.end(), t) - rt.begin()) - 1;
+  }
+  int64_t tiles_of(int64_t r) const { return (re[(size_t)r] - rs[(size_t)r] + T - 1) / T; }
+};
+
+// A locus whose pileup reference base depends on the queue's heap order (the reads' MD tags
+// disagree there): listed by the kernels, resolved by heap_ref_bases.
+struct AmbItem {
+  int32_t tile, pos;
+  int64_t item;  // the kernel's own item index (complex item / candidate)
 };
 
 }  // namespace gq
@@ -178,6 +201,7 @@ struct gq_ctx {
   int n_cu = 0;
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
+  gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
 };
 
 struct gq_dev_reads {
@@ -193,5 +217,13 @@ namespace gq {
 gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,
                int stage_cap = 0, int meta_cap = 0, int ev_cap = 0);
 gq_status check_device_error(gq_ctx *c, const Counters &h);
+// Pileup.referenceBaseAtLocus in the reference's heap order at each listed locus, for each of
+// the read sets (advanced together, as the somatic caller's two windows are): the queues are
+// replayed on the host (gq_replay.h) and the bases read on the device.  out_ref (device,
+// n * sets.size() bytes) receives item i's base for set k at i * sets.size() + k.  `tiles`
+// are the plan's device tiles (the same loci plan for every set).
+gq_status heap_ref_bases(gq_ctx *c, const Plan &pl, const DevBuf &tiles_buf,
+                         const std::vector<const gq_dev_reads *> &sets, const std::vector<AmbItem> &items,
+                         uint8_t *out_ref);
 }  // namespace gq
 

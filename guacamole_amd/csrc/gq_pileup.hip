@@ -317,19 +317,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                            int threshold, int emit_ref, int emit_no_call,
                                                            CallRec *__restrict__ recs, OutGeom og,
                                                            uint8_t *__restrict__ pool, unsigned long long pool_cap,
-                                                           Counters *ctr) {
+                                                           Counters *ctr, AmbItem *__restrict__ amb_out,
+                                                           unsigned long long amb_cap,
+                                                           const AmbItem *__restrict__ amb_in,
+                                                           const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+  // amb_in == nullptr: every queued item; a locus whose reads' MD-derived bases disagree
+  // (Pileup.referenceBaseAtLocus then depends on the queue's heap order) is only listed in
+  // amb_out.  amb_in != nullptr: the listed loci again, with their reference base resolved
+  // in heap order (heap_ref_bases) in amb_ref.
   const int lane = threadIdx.x & 63;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // items beyond a partition's capacity were never written (the host retries with larger ones)
-  const unsigned long long n_items = ctr->part_off[1][kParts];
+  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
   const int rpart = kPartsCols + (int)(gwave & (kPartsCols - 1));  // this wave's record partition
   // the reads covering the locus, compacted (tile-relative indices): the two per-read passes
   // then run over ~depth lanes instead of every read of the tile (one latency chain, not three)
   constexpr int kCover = 256;
   __shared__ int32_t cover_buf[kBlock / 64][kCover];
   int32_t *cover = cover_buf[threadIdx.x >> 6];
-  for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
+  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    const int64_t it = amb_in ? amb_in[li].item : li;
     const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
     const int32_t pos = item.pos;
@@ -361,8 +369,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       return r;
     };
     // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
-    uint32_t mask = 0;
-    uint64_t best = ~0ull;  // (end, read) of the heap-root proxy among standard-base reads
+    uint32_t mask = 0;  // standard MD-derived bases present
     for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
       bool cv;
       const int64_t r = slot_read(k0 + lane, &cv);
@@ -371,24 +378,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (v < 0) {
           raise_error(&ctr->err, (int64_t *)&ctr->err_pos, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT,
                       pos);
-        } else if (std_bit((uint8_t)v)) {
+        } else {
           mask |= std_bit((uint8_t)v);
-          const uint64_t key = ((uint64_t)(uint32_t)R.end[r] << 32) | (uint64_t)(r - tl.rb);
-          best = key < best ? key : best;
         }
       }
     }
-    for (int d = 1; d < 64; d <<= 1) {
-      mask |= __shfl_xor(mask, d, 64);
-      const uint64_t o = __shfl_xor(best, d, 64);
-      best = o < best ? o : best;
-    }
+    for (int d = 1; d < 64; d <<= 1) mask |= __shfl_xor(mask, d, 64);
     const bool ambiguous = __popc(mask) > 1;
     uint8_t refbase = 'N';
-    if (ambiguous) {
-      const int64_t rr = tl.rb + (int64_t)(best & 0xFFFFFFFFull);
-      const int v = md_ref_at(R, rr, pos);
-      refbase = (uint8_t)v;
+    if (amb_in) {
+      refbase = amb_ref[li];
+    } else if (ambiguous) {
+      // listed for the heap-order replay; a wide tile's visit is counted here, once
+      if (lane == 0) {
+        if (item.flags & 1) {
+          atomicAdd(&ctr->visited, 1ull);
+          atomicAdd(&ctr->ambiguous, 1ull);
+        }
+        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+      }
+      continue;
     } else if (mask) {
       refbase = bit_base(mask);
     }
@@ -479,7 +489,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_CAPACITY, pos);
       continue;
     }
-    if (item.flags & 1) {  // queued from a wide tile: count the visit here
+    if ((item.flags & 1) && !amb_in) {  // queued from a wide tile: count the visit here
       const uint32_t tot = (uint32_t)__ballot(lane < 8 && st_lane > 0);
       if (tot == 0) continue;
       if (lane == 0) {
@@ -869,7 +879,8 @@ void gq_close(gq_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
                     &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
-                    &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow})
+                    &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow, &c->amb, &c->amb_ref,
+                    &c->heap_off, &c->heap_reads})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1115,8 +1126,10 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
                    int stage_cap, int meta_cap, int ev_cap) {
   if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
   const int64_t R = loci->n_ranges;
-  std::vector<int32_t> rc;
-  std::vector<int64_t> rs, re, ro, rt;
+  pl = Plan{};
+  pl.T = T;
+  std::vector<int32_t> &rc = pl.rc;
+  std::vector<int64_t> &rs = pl.rs, &re = pl.re, &rt = pl.rt, ro;
   int64_t ord = 0, tiles = 0;
   for (int64_t i = 0; i < R; ++i) {
     const int32_t cc = loci->contig[i];
@@ -1124,6 +1137,17 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
     if (cc < 0 || cc >= rd->d.n_contigs) return set_err(GQ_E_ARG, "loci range %lld: contig %d out of range", (long long)i, cc);
     if (s < 0 || e < s || e > INT32_MAX) return set_err(GQ_E_ARG, "loci range %lld: bad interval", (long long)i);
     if (e == s) continue;
+    const int64_t task = loci->task ? loci->task[i] : 0;
+    // a new window at each change of (task, contig); within one, ranges must ascend
+    if (pl.wins.empty() || pl.rtask.back() != task || rc.back() != cc) {
+      pl.wins.push_back(Plan::Win{cc, (int64_t)rc.size(), (int64_t)rc.size()});
+    } else if (s < re.back()) {
+      return set_err(GQ_E_ARG, "loci range %lld: ranges of one task and contig must be sorted and disjoint",
+                     (long long)i);
+    }
+    pl.wins.back().r1 = (int64_t)rc.size() + 1;
+    pl.rwin.push_back((int32_t)(pl.wins.size() - 1));
+    pl.rtask.push_back(task);
     rc.push_back(cc);
     rs.push_back(s);
     re.push_back(e);
@@ -1224,9 +1248,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   og.capA[1] = wg_loci / 32 + 256;
   og.capB[0] = dense ? 2ull * ns * (unsigned long long)pl.n_loci / 8192 + 256 : (unsigned long long)pl.n_loci / 16384 + 256;
   og.capB[1] = (unsigned long long)pl.n_loci / 16384 + 256;
-  unsigned long long pool_cap = 1 << 22;
+  unsigned long long pool_cap = 1 << 22, amb_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->recs.ensure(og.total(0) * sizeof(CallRec)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
     HIP_TRY(c->pool.ensure(pool_cap));
@@ -1244,7 +1269,8 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 1, og);
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                       (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr);
+                       (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap,
+                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
@@ -1267,6 +1293,43 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     if (hc.pool_used > pool_cap) {
       pool_cap = hc.pool_used + 4096;
       retry = true;
+    }
+    if (hc.n_amb > amb_cap) {
+      amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (!retry && hc.n_amb > 0 && !hc.err) {
+      // loci whose reference base depends on heap order: replay the window's queue, then the
+      // complex kernel again over just those loci with the resolved base
+      std::vector<AmbItem> amb((size_t)hc.n_amb);
+      HIP_TRY(hipMemcpyAsync(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(c->amb_ref.ensure(amb.size()));
+      st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
+      if (st) {
+        free(res);
+        return st;
+      }
+      const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 4096);
+      hipLaunchKernelGGL(germline_complex, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
+                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
+                         (unsigned long long)0, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p,
+                         (int64_t)amb.size());
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (hc.part_max[0]) {
+        og.capA[0] += hc.part_max[0] + 64;
+        og.capB[0] += hc.part_max[0] + 64;
+        retry = true;
+      }
+      if (hc.pool_used > pool_cap) {
+        pool_cap = hc.pool_used + 4096;
+        retry = true;
+      }
     }
     if (!retry) break;
     if (attempt == 2) {
@@ -1470,6 +1533,43 @@ gq_status gq_pileup_counts(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loc
   if (st) {
     gq_free_counts(res);
     return st;
+  }
+  {  // loci whose reference base depends on the queue's heap order: replayed (gq_replay.h)
+    std::vector<AmbItem> amb;
+    std::vector<int64_t> ords;
+    int64_t o = 0;
+    for (size_t r = 0; r < pl.rs.size(); ++r) {
+      const int64_t len = pl.re[r] - pl.rs[r];
+      for (int64_t i = 0; i < len; ++i)
+        if (res->ambiguous[o + i]) {
+          amb.push_back(AmbItem{(int32_t)(pl.rt[r] + i / kCountT), (int32_t)(pl.rs[r] + i), (int64_t)amb.size()});
+          ords.push_back(o + i);
+        }
+      o += len;
+    }
+    if (!amb.empty()) {
+      HIP_TRY(c->amb_ref.ensure(amb.size()));
+      st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
+      if (st) {
+        gq_free_counts(res);
+        return st;
+      }
+      std::vector<uint8_t> rb(amb.size());
+      HIP_TRY(hipMemcpy(rb.data(), c->amb_ref.p, rb.size(), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost));
+      st = check_device_error(c, hc);
+      if (st) {
+        gq_free_counts(res);
+        return st;
+      }
+      for (size_t k = 0; k < amb.size(); ++k) {
+        const int64_t x = ords[k];
+        const uint8_t b = rb[k];
+        const int cat = b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : 4;  // base_counts: A C G T N other
+        res->ref_base[x] = b;
+        res->ref_depth[x] = res->base_counts[x * 6 + cat];
+      }
+    }
   }
   *out = res;
   return GQ_OK;

@@ -14,9 +14,11 @@
  * file.  Third-party behaviour restated from the published algorithms (not in
  * /root/reference): ADAM 0.18.1 MdTag / PhredUtils, htsjdk 1.118 CigarOperator,
  * Colt 1.2.0 DoubleMatrix1D.aggregate (folds last->first), Scala 2.10
- * mutable.PriorityQueue (heap array order), Breeze 0.11 mean/median.
+ * mutable.PriorityQueue (heap array order), Breeze 0.11 mean/median, java.lang.StrictMath
+ * log / exp / log10 (fdlibm 5.3, strictmath.h).
  */
 #include "oracle.h"
+#include "strictmath.h"
 
 #include <algorithm>
 #include <cmath>
@@ -206,7 +208,7 @@ double phredToErrorProbability(int phred) {
 }
 double phredToSuccessProbability(int phred) { return 1.0 - phredToErrorProbability(phred); }
 int probabilityToPhred(double p) {
-  double x = -10.0 * std::log10(p);
+  double x = -10.0 * strictmath::log10(p);
   // java Math.round(double) = floor(x + 0.5), saturating; .toInt truncates the long
   if (std::isnan(x)) return 0;
   double r = std::floor(x + 0.5);
@@ -268,7 +270,7 @@ struct Elem {
     int readPositionOffset = consumesRead(c.op) ? c.len - indexWithinCigarElement : 0;
     int64_t nextLocus = locus + (cigarRefLength(c) - indexWithinCigarElement);
     Elem e{read, nextLocus, (uint8_t)'N', readPosition + readPositionOffset, cigarElementIndex + 1,
-           cigarElementLocus + cigarRefLength(c), 0};
+           cigarElementLocus + cigarRefLength(c), 0, false, {}};
     return e;
   }
   Elem advanceToLocus(int64_t newLocus, uint8_t newReferenceBase) const {  // :220-248
@@ -294,7 +296,7 @@ struct Elem {
   }
   static Elem create(const Read *read, int64_t locus, uint8_t referenceBase) {  // :264-274
     if (!(read->start < read->end)) fail(E_ASSERT, "assumption failed: locus < read.end");
-    Elem e{read, read->start, (uint8_t)'N', 0, 0, read->start, 0};
+    Elem e{read, read->start, (uint8_t)'N', 0, 0, read->start, 0, false, {}};
     return e.advanceToLocus(locus, referenceBase);
   }
 
@@ -851,19 +853,19 @@ std::vector<double> likelihoodsOfGenotypes(const std::vector<const Elem *> &elem
     double agg;
     if (depth == 0) agg = NAN;  // Colt aggregate of an empty vector
     else {
-      agg = std::log(r1[depth - 1] + r2[depth - 1]);
-      for (size_t i = depth - 1; i-- > 0;) agg = agg + std::log(r1[i] + r2[i]);
+      agg = strictmath::log(r1[depth - 1] + r2[depth - 1]);
+      for (size_t i = depth - 1; i-- > 0;) agg = agg + strictmath::log(r1[i] + r2[i]);
     }
-    ll.push_back(agg + std::log(1.0) - std::log(2.0) * (double)depth);
+    ll.push_back(agg + strictmath::log(1.0) - strictmath::log(2.0) * (double)depth);
   }
   if (normalize) {
     double tot = 0.0;
-    for (double x : ll) tot += std::exp(x);
-    double lt = std::log(tot);
+    for (double x : ll) tot += strictmath::exp(x);
+    double lt = strictmath::log(tot);
     for (double &x : ll) x = x - lt;
   }
   if (!logSpace)
-    for (double &x : ll) x = std::exp(x);
+    for (double &x : ll) x = strictmath::exp(x);
   return ll;
 }
 
@@ -1026,10 +1028,10 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
       if (!allele) return;
       Evidence tev = alleleEvidence(mll, *allele, ft);
       Evidence nev = alleleEvidence(1 - nvs, Allele{allele->ref, allele->ref}, fn);
-      double logOdds = std::log(odds);
+      double logOdds = strictmath::log(odds);
       int gq = successProbabilityToPhred(tev.likelihood * nev.likelihood - 1e-10);
       {
-        double x = -10.0 * std::log10(1.0 - (tev.likelihood * nev.likelihood - 1e-10));
+        double x = -10.0 * strictmath::log10(1.0 - (tev.likelihood * nev.likelihood - 1e-10));
         if (std::isfinite(x) && std::fabs((x - std::floor(x)) - 0.5) <= 1e-6) flags |= 4;
       }
       if (filterMode == 1) {
@@ -1111,6 +1113,40 @@ int or_pileup_stats(const or_reads *reads, const or_loci *loci, char **o, int64_
               (long long)p.locus, (char)p.referenceBase, p.depth(), pos, base[0], base[1], base[2], base[3], base[4],
               base[5], ins, del, mid, clip, refDepth, amb[0] ? 1 : 0);
     });
+  });
+}
+
+int or_heap_orders(const or_reads *const *reads, int32_t n_sets, const or_loci *loci, int64_t every, char **o,
+                   int64_t *olen) {
+  std::string out;
+  return guard(out, o, olen, [&]() {
+    std::vector<ReadSet> rs((size_t)n_sets);
+    std::vector<ContigIndex> idx;
+    for (int32_t s = 0; s < n_sets; ++s) {
+      buildReads(reads[s], rs[(size_t)s]);
+      idx.emplace_back(rs[(size_t)s]);
+    }
+    for (const TaskContig &tc : taskContigs(loci)) {
+      std::vector<Window> windows((size_t)n_sets);
+      std::vector<Window *> wp;
+      for (int32_t s = 0; s < n_sets; ++s) {
+        windows[(size_t)s].sorted = taskReads(rs[(size_t)s], idx[(size_t)s].get(tc.contig), tc);
+        windows[(size_t)s].checkSorted();
+        wp.push_back(&windows[(size_t)s]);
+      }
+      LociIter it;
+      it.ranges = tc.ranges;
+      int64_t locus;
+      while (advanceMultipleWindows(wp, it, locus)) {
+        if (every > 1 && locus % every != 0) continue;
+        for (int32_t s = 0; s < n_sets; ++s) {
+          appendf(out, "%d\t%lld\t%d\t", tc.contig, (long long)locus, s);
+          const auto regions = windows[(size_t)s].currentRegions();
+          for (size_t k = 0; k < regions.size(); ++k) appendf(out, k ? ",%lld" : "%lld", (long long)regions[k]->index);
+          out.push_back('\n');
+        }
+      }
+    }
   });
 }
 

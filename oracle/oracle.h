@@ -54,6 +54,13 @@ typedef struct {
  * where A..other count Match/Mismatch elements by sequenced base.            */
 int or_pileup_stats(const or_reads *reads, const or_loci *loci, char **out, int64_t *out_len);
 
+/* SlidingWindow.currentRegions() (the priority queue's heap array) of each read set's
+ * window at every visited locus with locus % every == 0 (every <= 1: all), the sets'
+ * windows advanced together (advanceMultipleWindows).  Lines:
+ *   contig \t locus \t set \t read,read,...   (indices into the set's input arrays)     */
+int or_heap_orders(const or_reads *const *reads, int32_t n_sets, const or_loci *loci, int64_t every, char **out,
+                   int64_t *out_len);
+
 /* germline-threshold (GermlineThresholdCaller.scala:58-179).  Lines:
  *   contig \t locus \t sample \t gt0,gt1 \t ref \t alt \t flags
  * flags bit0 = pileup reference base depends on heap order (MD disagreement),

@@ -219,3 +219,18 @@ def somatic_at(tumor, normal, contig: str, locus: int, **params):
         f = line.split("\t")
         out.append(dict(locus=int(f[1]), ref=f[3], alt=f[4], log_odds=float(f[5]), gq=int(f[6])))
     return out
+
+
+def heap_orders(sets, loci, every: int = 1):
+    """SlidingWindow.currentRegions() of each set's window at visited loci with locus % every == 0:
+    {(contig, locus): [[read indices of set 0 in heap order], [set 1], ...]}."""
+    ms = [_Marshalled(rs) for rs in sets]
+    arr = (C.POINTER(or_reads) * len(ms))(*[C.pointer(m.s) for m in ms])
+    L = _Loci(sets[0].contig_names, *loci)
+    text = _call(lib().or_heap_orders, arr, C.c_int32(len(ms)), C.byref(L.s), C.c_int64(every))
+    out = {}
+    for line in text.splitlines():
+        f = line.split("\t")
+        key = (int(f[0]), int(f[1]))
+        out.setdefault(key, [None] * len(sets))[int(f[2])] = [int(x) for x in f[3].split(",")] if f[3] else []
+    return out

@@ -18,10 +18,8 @@ def _loci(rs, expr="all", tasks=1):
     return flatten_partitions(partition_loci_uniformly(tasks, ls), rs.contig_index())
 
 
-def _split(rows):
-    exact = [r for r in rows if not (r[6] & native.FLAG_AMBIGUOUS_REF)]
-    amb = [r for r in rows if r[6] & native.FLAG_AMBIGUOUS_REF]
-    return exact, amb
+def _ambiguous(rows):
+    return [r for r in rows if r[6] & native.FLAG_AMBIGUOUS_REF]
 
 
 @pytest.fixture(scope="module")
@@ -35,11 +33,10 @@ def test_chrm_germline_matches_oracle(gpu_ctx, chrm, threshold, emit_ref, emit_n
     loci = _loci(chrm)
     got = germline_threshold_reads(gpu_ctx, chrm, loci, threshold, emit_ref, emit_no_call)
     want = O.germline_threshold(chrm, loci, threshold, emit_ref, emit_no_call)
-    ge, ga = _split(got)
-    we, wa = _split(want)
-    assert ge == we
-    # heap-order-dependent loci are reported separately; same loci flagged on both sides
-    assert sorted(set(r[1] for r in ga)) == sorted(set(r[1] for r in wa))
+    # every record, including those at loci whose reference base the reference takes from the
+    # SlidingWindow queue's heap order (the reads' MD tags disagree there: replayed on the host)
+    assert got == want
+    assert _ambiguous(want), "chrM holds heap-order-dependent loci"
 
 
 def test_chrm_counts_match_oracle(gpu_ctx, chrm):
@@ -57,17 +54,22 @@ def test_chrm_counts_match_oracle(gpu_ctx, chrm):
         assert tuple(c["base_counts"][i]) == row[5]
         assert tuple(c["indel_counts"][i]) == row[6]
         assert c["ambiguous"][i] == row[8]
-        if not row[8]:
-            assert chr(c["ref_base"][i]) == row[2]
-            assert c["ref_depth"][i] == row[7]
+        assert chr(c["ref_base"][i]) == row[2]
+        assert c["ref_depth"][i] == row[7]
+    assert any(row[8] for row in stats)
 
 
 def test_parallelism_partitions_agree(gpu_ctx, chrm):
-    """Same calls whatever the task split (DistributedUtilSuite: 1 vs 5 vs 800 tasks)."""
+    """DistributedUtilSuite (1 vs 5 vs 800 tasks): identical calls wherever the reads' MD tags
+    agree; at heap-order-dependent loci each split gives what the reference gives for that
+    split (each task starts its own SlidingWindow queue)."""
     base = germline_threshold_reads(gpu_ctx, chrm, _loci(chrm, tasks=1), 8)
+    firm = lambda rows: [r for r in rows if not (r[6] & native.FLAG_AMBIGUOUS_REF)]
     for tasks in (5, 800):
-        got = germline_threshold_reads(gpu_ctx, chrm, _loci(chrm, tasks=tasks), 8)
-        assert _split(got)[0] == _split(base)[0]
+        loci = _loci(chrm, tasks=tasks)
+        got = germline_threshold_reads(gpu_ctx, chrm, loci, 8)
+        assert firm(got) == firm(base)
+        assert got == O.germline_threshold(chrm, loci, 8)
 
 
 @pytest.mark.parametrize("seed", [1, 2])
@@ -141,10 +143,7 @@ def test_chrm_subsampled_column_path(gpu_ctx, chrm):
     for t, er, enc in ((8, False, False), (0, True, True)):
         got = germline_threshold_reads(gpu_ctx, sub, loci, t, er, enc)
         want = O.germline_threshold(sub, loci, t, er, enc)
-        ge, ga = _split(got)
-        we, wa = _split(want)
-        assert ge == we
-        assert sorted(set(r[1] for r in ga)) == sorted(set(r[1] for r in wa))
+        assert got == want
     tm = gpu_ctx.timings()
     assert tm["walk_tiles"] < tm["tiles"] // 2, tm  # most tiles through the column kernel
 
