@@ -202,6 +202,7 @@ struct gq_ctx {
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
+  gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
 };
 
 struct gq_dev_reads {

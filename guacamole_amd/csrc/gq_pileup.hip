@@ -880,7 +880,7 @@ void gq_close(gq_ctx *c) {
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
                     &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
                     &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow, &c->amb, &c->amb_ref,
-                    &c->heap_off, &c->heap_reads})
+                    &c->heap_off, &c->heap_reads, &c->win_meta, &c->win_grp})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);

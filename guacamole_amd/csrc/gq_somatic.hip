@@ -35,6 +35,11 @@
 
 #include "gq_alleles.h"
 #include "gq_host.h"
+#include "gq_strictmath.h"
+
+// The caller's FP64 arithmetic must round like the reference's: no fused multiply-add
+// anywhere in this file (e.g. (agg + 0) - ln2 * depth would otherwise contract).
+#pragma clang fp contract(off)
 
 using namespace gq;
 
@@ -254,13 +259,24 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// ADAM PhredUtils (restated in oracle/oracle.cpp:201-219)
-__device__ __forceinline__ double phred_success(int q) {
-  if (q > 255) q = 255;
-  return 1.0 - pow(10.0, -(double)q / 10.0);
+// Value of lane j (wave-uniform j) broadcast to every lane, for 64-bit types.
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+__device__ __forceinline__ double lane_f64(double v, int j) {
+  return __builtin_bit_cast(double, lane_u64(__builtin_bit_cast(uint64_t, v), j));
+}
+
+// ADAM PhredUtils.phredToSuccessProbability, 1 - 10^(-q/10) for q in [0, 255] (restated in
+// oracle/oracle.cpp:201-207): a table filled on the host with the host's pow, so the device
+// starts from the very bits the reference's arithmetic starts from.
+__constant__ double g_succ[256];
+__device__ __forceinline__ double phred_success(int q) { return g_succ[q > 255 ? 255 : (q < 0 ? 0 : q)]; }
+
 __device__ int success_to_phred(double p) {  // successProbabilityToPhred: round(-10 log10(1 - p)) (Math.round)
-  const double x = -10.0 * log10(1.0 - p);
+  const double x = -10.0 * sm::log10(1.0 - p);
   if (isnan(x)) return 0;
   const double r = floor(x + 0.5);
   long long l;
@@ -270,11 +286,12 @@ __device__ int success_to_phred(double p) {  // successProbabilityToPhred: round
   return (int)(int32_t)(uint32_t)(uint64_t)l;
 }
 
-// |a - b| within FP rounding noise of the reference's own (order-dependent) arithmetic
+// |a - b| within FP rounding noise of the threshold: reported as GQ_FLAG_KNIFE_EDGE (the
+// outcome there depends on the exact bits of every term, which this kernel reproduces)
 __device__ __forceinline__ bool near_edge(double a, double b) { return fabs(a - b) <= 1e-9 * fmax(1.0, fabs(b)); }
 // successProbabilityToPhred(p) rounds -10 log10(1 - p); flag values within 1e-6 of a .5 step
 __device__ __forceinline__ bool phred_rounding_edge(double p) {
-  const double x = -10.0 * log10(1.0 - p);
+  const double x = -10.0 * sm::log10(1.0 - p);
   if (!isfinite(x)) return false;
   return fabs((x - floor(x)) - 0.5) <= 1e-6;
 }
@@ -311,28 +328,125 @@ __device__ bool allele_std_alt(const DevReads &R, const AlleleDesc &a, int32_t p
   return true;
 }
 
-// Per-sample pileup summary held by one wave: a distinct-allele table (slot s * 64 + lane
-// lives in lane `lane`, register slot s) with per-allele counts and FP64 log sums.
-struct SamplePile {
-  uint64_t klo[kSlots], khi[kSlots];
-  AlleleDesc desc[kSlots];
-  uint32_t n_all[kSlots], n_f[kSlots];
-  double s1[kSlots], s0[kSlots], sh[kSlots];
-  int nt;             // used table entries (wave-uniform)
-  uint32_t depth_all; // elements
-  uint32_t depth_f;   // elements passing the mapping-quality filter
-  uint32_t fwd_f;     // ... on the positive strand
-  uint8_t refbase;
-  bool ambiguous, overflow;
-};
-
 __device__ void raise_at(Counters *ctr, int code, int64_t where) {
   raise_error(&ctr->err, (int64_t *)&ctr->err_pos, code, where);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pileup element order.  Pileup.atGreaterLocus (Pileup.scala:103-132) keeps the surviving
+// elements in order and appends new reads in start order, and the first pileup of a window
+// (one per task and contig) takes the reads in SlidingWindow.currentRegions() order: the
+// priority queue's heap array after enqueueing, in start order, the reads that overlap the
+// window's first visited locus F (DistributedUtil.scala:260-274).  So at any locus the
+// elements are the reads of that initial group still covering it, in heap order, then the
+// other covering reads in read order.  The order matters for the FP sums (Likelihood,
+// AlleleEvidence mean); it is restored here from the per-window initial ranks.
+// ------------------------------------------------------------------------------------------
+struct WinInit {
+  int32_t F;    // first visited locus of the window (INT32_MAX: none)
+  int32_t E;    // largest end of this set's initial-group reads (loci >= E hold none of them)
+  int64_t off;  // the group's reads (ascending) and heap ranks at init_reads / init_rank [off, off + n)
+  int32_t n, cap;
+};
+
+// F of each window over both read sets (the first locus of its ranges covered by a read of
+// either set), and each set's candidate reads for the group (prefix-max end past F, start at
+// or before F): their count is the group's capacity.  One thread per window.
+__global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t *__restrict__ w_roff,
+                             const int64_t *__restrict__ r_s, const int64_t *__restrict__ r_e, int64_t n_win,
+                             DevReads RT, DevReads RN, WinInit *__restrict__ wi, int64_t *__restrict__ wi_lo) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n_win) return;
+  const int32_t c = w_contig[w];
+  int64_t F = INT32_MAX;
+  for (int s = 0; s < 2; ++s) {
+    const DevReads &R = s ? RN : RT;
+    const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
+    for (int64_t k = w_roff[w]; k < w_roff[w + 1]; ++k) {
+      const int64_t a = r_s[k];
+      if (a >= F) break;
+      int64_t lo = cb, hi = ce;  // first read with pmax_end > a: it covers max(a, its start)
+      while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if ((int64_t)R.pmax_end[m] > a) hi = m;
+        else lo = m + 1;
+      }
+      if (lo < ce) {
+        const int64_t f = max(a, (int64_t)R.start[lo]);
+        if (f < r_e[k]) {
+          F = min(F, f);
+          break;
+        }
+      }
+    }
+  }
+  for (int s = 0; s < 2; ++s) {
+    const DevReads &R = s ? RN : RT;
+    WinInit x{(int32_t)F, INT32_MIN, 0, 0, 0};
+    int64_t lo = 0;
+    if (F < INT32_MAX) {
+      const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
+      int64_t a = cb, b = ce;
+      while (a < b) {  // first read with pmax_end > F
+        const int64_t m = (a + b) >> 1;
+        if ((int64_t)R.pmax_end[m] > F) b = m;
+        else a = m + 1;
+      }
+      lo = a;
+      b = ce;
+      while (a < b) {  // first read with start > F
+        const int64_t m = (a + b) >> 1;
+        if ((int64_t)R.start[m] > F) b = m;
+        else a = m + 1;
+      }
+      x.cap = (int32_t)min<int64_t>(a - lo, INT32_MAX);
+    }
+    wi[2 * w + s] = x;
+    wi_lo[2 * w + s] = lo;
+  }
+}
+
+// The initial group of each (window, set): reads [lo, lo + cap) that overlap F, enqueued in
+// read order into an empty Scala PriorityQueue (fixUp while the parent's end is larger,
+// SlidingWindow.scala:62-68); rank = position in the heap array.  One thread per (window, set).
+__global__ void window_group(WinInit *__restrict__ wi, const int64_t *__restrict__ wi_lo, int64_t n,
+                             DevReads RT, DevReads RN, int64_t *__restrict__ init_reads,
+                             int32_t *__restrict__ init_rank, int32_t *__restrict__ heap) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  WinInit x = wi[k];
+  const DevReads &R = (k & 1) ? RN : RT;
+  int64_t *rd = init_reads + x.off;
+  int32_t *rk = init_rank + x.off;
+  int32_t *h = heap + x.off;  // heap of group positions, 0-based (h[i] <-> Scala index i + 1)
+  int32_t m = 0;
+  int32_t E = INT32_MIN;
+  for (int64_t i = 0; i < x.cap; ++i) {
+    const int64_t r = wi_lo[k] + i;
+    if (R.end[r] <= x.F) continue;
+    rd[m] = r;
+    E = max(E, R.end[r]);
+    int32_t q = m++;
+    h[q] = q;
+    while (q > 0) {
+      const int32_t p = (q + 1) / 2 - 1;
+      if (!(R.end[rd[h[q]]] < R.end[rd[h[p]]])) break;
+      const int32_t t = h[q];
+      h[q] = h[p];
+      h[p] = t;
+      q = p;
+    }
+  }
+  for (int32_t i = 0; i < m; ++i) rk[h[i]] = i;
+  x.n = m;
+  x.E = E;
+  wi[k] = x;
+}
+
 // The reads of a tile window [rb, re) covering pos, compacted into a per-wave LDS list (tile-
-// relative indices, in read order) so the per-read passes below run over ~depth lanes rather
-// than every read of the window; deeper than the list: the passes walk the window instead.
+// relative indices) in pileup element order, so the per-read passes below run over ~depth
+// lanes rather than every read of the window; deeper than the list: the passes walk the
+// window in read order instead (with an initial group there: a capacity error).
 constexpr int kCover = 768;
 struct Cover {
   const int32_t *lst;
@@ -353,7 +467,9 @@ struct Cover {
     return r;
   }
 };
-__device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst) {
+__device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst, uint32_t *tmp,
+                            const WinInit &w, const int64_t *__restrict__ init_reads,
+                            const int32_t *__restrict__ init_rank, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   int64_t n = 0;
   for (int64_t r0 = rb; r0 < re; r0 += 64) {
@@ -370,54 +486,95 @@ __device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t p
   cv.rb = rb;
   cv.compact = n <= kCover;
   cv.n = cv.compact ? n : (re - rb);
+  if (w.n > 0 && pos < w.E) {
+    if (!cv.compact) {
+      raise_at(ctr, GQ_E_CAPACITY, pos);
+      return cv;
+    }
+    // the initial group's reads covering pos are a prefix of the list (they start at or
+    // before F, every other covering read after F): reorder that prefix by heap rank
+    int p = 0;
+    for (int k0 = 0; k0 < (int)n; k0 += 64) {
+      const int k = k0 + lane;
+      p += (int)__popcll(__ballot(k < (int)n && R.start[rb + lst[k]] <= w.F));
+    }
+    if (p > 512) {
+      raise_at(ctr, GQ_E_CAPACITY, pos);
+      return cv;
+    }
+    for (int k = lane; k < p; k += 64) {
+      const int64_t r = rb + lst[k];
+      int lo = 0, hi = w.n;  // r in the group's ascending read list
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (init_reads[w.off + m] < r) lo = m + 1;
+        else hi = m;
+      }
+      tmp[k] = (uint32_t)init_rank[w.off + lo];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < p; k += 64) {
+      int before = 0;
+      for (int j = 0; j < p; ++j) before += tmp[j] < tmp[k] ? 1 : 0;
+      tmp[512 + before] = (uint32_t)lst[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < p; k += 64) lst[k] = (int32_t)tmp[512 + k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
   return cv;
 }
 
-// Pileup.referenceBaseAtLocus over the reads of window [rb, re) covering pos (as in
-// germline_complex: first standard MD-derived base; heap order approximated by the minimum
-// (end, index) read when the bases disagree, flagged ambiguous).
-__device__ void pileup_ref(const DevReads &R, const Cover &cv, int32_t pos, Counters *ctr, uint8_t &refbase,
-                           bool &ambiguous) {
+// Pileup.referenceBaseAtLocus over the covering reads: the standard MD-derived bases present
+// (ambiguous = more than one); the base itself when they agree.  Where they disagree the
+// reference takes the first in heap order: the first pass lists the locus and the second
+// receives the base from heap_ref_bases (ref_override >= 0).
+__device__ void pileup_ref(const DevReads &R, const Cover &cv, int32_t pos, Counters *ctr, int ref_override,
+                           uint8_t &refbase, bool &ambiguous) {
   const int lane = threadIdx.x & 63;
-  const int64_t rb = cv.rb;
   uint32_t mask = 0;
-  uint64_t best = ~0ull;
   for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
     bool cov;
     const int64_t r = cv.read(R, k0 + lane, pos, &cov);
     if (cov) {
       const int v = md_ref_at(R, r, pos);
-      if (v < 0) {
-        raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
-      } else if (std_bit((uint8_t)v)) {
-        mask |= std_bit((uint8_t)v);
-        const uint64_t key = ((uint64_t)(uint32_t)R.end[r] << 32) | (uint64_t)(r - rb);
-        best = key < best ? key : best;
-      }
+      if (v < 0) raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
+      else mask |= std_bit((uint8_t)v);
     }
   }
-  for (int d = 1; d < 64; d <<= 1) {
-    mask |= __shfl_xor(mask, d, 64);
-    const uint64_t o = __shfl_xor(best, d, 64);
-    best = o < best ? o : best;
-  }
+  for (int d = 1; d < 64; d <<= 1) mask |= __shfl_xor(mask, d, 64);
   ambiguous = __popc(mask) > 1;
   refbase = 'N';
-  if (ambiguous) refbase = (uint8_t)md_ref_at(R, rb + (int64_t)(best & 0xFFFFFFFFull), pos);
+  if (ref_override >= 0) refbase = (uint8_t)ref_override;
   else if (mask) refbase = bit_base(mask);
 }
 
-// Build the allele table of one sample's pileup at pos.
-__device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
-                              bool include_alignment, Counters *ctr, SamplePile &P, int32_t *cover_lds) {
+// Per-sample pileup summary held by one wave: a distinct-allele table (slot s * 64 + lane
+// lives in lane `lane`, register slot s) with per-allele element counts.
+struct SamplePile {
+  uint64_t klo[kSlots], khi[kSlots];
+  AlleleDesc desc[kSlots];
+  uint32_t n_all[kSlots], n_f[kSlots];
+  int nt;             // used table entries (wave-uniform)
+  uint32_t depth_all; // elements
+  uint32_t depth_f;   // elements passing the mapping-quality filter
+  uint32_t fwd_f;     // ... on the positive strand
+  uint8_t refbase;
+  bool ambiguous, overflow;
+};
+
+// Build the allele table of one sample's pileup at pos (counts only: order-free).
+__device__ void gather_sample(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, int ref_override,
+                              Counters *ctr, SamplePile &P) {
   const int lane = threadIdx.x & 63;
-  const Cover cv = make_cover(R, rb, re, pos, cover_lds);
-  pileup_ref(R, cv, pos, ctr, P.refbase, P.ambiguous);
+  pileup_ref(R, cv, pos, ctr, ref_override, P.refbase, P.ambiguous);
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
     P.klo[s] = P.khi[s] = 0;
     P.n_all[s] = P.n_f[s] = 0;
-    P.s1[s] = P.s0[s] = P.sh[s] = 0.0;
   }
   P.nt = 0;
   P.depth_all = P.depth_f = P.fwd_f = 0;
@@ -428,7 +585,6 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
     AlleleDesc d;
     Key128 key{0, 0};
     bool pass = false;
-    double l1 = 0.0, l0 = 0.0, lh = 0.0;
     if (act) {
       int errc = 0;
       if (!classify(R, r, pos, P.refbase, d, &errc)) {
@@ -438,16 +594,6 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
         key = allele_key(R, d, pos, 0);
         const int mq = (int)R.mapq[r];
         pass = min_mapq <= 0 || mq >= min_mapq;  // QualityAlignedReadsFilter (PileupElementsFilter.scala:25-36)
-        if (pass) {
-          const int q = elem_quality(R, d);
-          if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
-          double pc = phred_success(q < 0 ? 0 : q);
-          if (include_alignment) pc = pc * phred_success(mq);  // probabilityCorrectIncludingAlignment
-          // Likelihood.scala:166-188: log(P(e, a1) + P(e, a2)) with P = pc if e's allele is a, else 1 - pc
-          l1 = log(pc + pc);
-          lh = log(pc + (1.0 - pc));
-          l0 = log((1.0 - pc) + (1.0 - pc));
-        }
       }
     }
     const unsigned long long actb = __ballot(act), passb = __ballot(act && pass);
@@ -461,8 +607,6 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
       const bool match = act && key.lo == klo && key.hi == khi;
       const unsigned long long mb = __ballot(match);
       const uint32_t na = (uint32_t)__popcll(mb), nf = (uint32_t)__popcll(mb & passb);
-      const bool mf = match && pass;
-      const double a1 = wave_sum(mf ? l1 : 0.0), a0 = wave_sum(mf ? l0 : 0.0), ah = wave_sum(mf ? lh : 0.0);
       int found = -1;
 #pragma unroll
       for (int s = 0; s < kSlots; ++s) {
@@ -500,22 +644,12 @@ __device__ void gather_sample(const DevReads &R, int64_t rb, int64_t re, int32_t
           if (s == sl && lane == owner) {
             P.n_all[s] += na;
             P.n_f[s] += nf;
-            P.s1[s] += a1;
-            P.s0[s] += a0;
-            P.sh[s] += ah;
           }
       }
       pending &= ~mb;
     }
   }
 }
-
-// Broadcast table entry j (owner lane j & 63, register slot j >> 6) of a SamplePile field.
-#define PILE_GET(P, field, j, out)                                  \
-  do {                                                              \
-    _Pragma("unroll") for (int _s = 0; _s < kSlots; ++_s) if (_s == ((j) >> 6)) \
-      out = __shfl(P.field[_s], (j) & 63, 64);                      \
-  } while (0)
 
 __device__ AlleleDesc pile_desc(const SamplePile &P, int j) {
   AlleleDesc d{};
@@ -536,8 +670,7 @@ __device__ AlleleDesc pile_desc(const SamplePile &P, int j) {
 // Genotype likelihoods of one sample (Likelihood.likelihoodsOfAllPossibleGenotypesFromPileup,
 // normalised, not log space).  Eligible alleles (filtered count > 0, standard alt bases) are
 // ranked by Allele order into `order[0..n)` (LDS, per wave); genotype g <-> (i <= j) in the
-// reference's enumeration order.  Returns n; per lane: likelihoods of genotypes lane, lane+64..
-// are reduced by the caller through the two callbacks.
+// reference's enumeration order.
 struct GenoResult {
   int n;          // eligible alleles
   int G;          // genotypes
@@ -557,8 +690,66 @@ __device__ void genotype_index(int g, int n, int &i, int &j) {  // g -> (i, j), 
   j = row + rem;
 }
 
-__device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, int32_t pos, int16_t *order,
-                                uint8_t *is_var) {
+constexpr int kMaxG = 128;  // genotypes held per sample for the normalisation (15 eligible alleles)
+
+// sum_e log(P(e, a1) + P(e, a2)) over the mapq-filtered elements of the pileup for the
+// genotype (k1, k2) of each lane, P(e, a) = pc_e if e's allele is a else 1 - pc_e
+// (Likelihood.scala:166-188).  The reference fills a Colt matrix and folds each genotype's row
+// with DoubleMatrix1D.aggregate(plus, chain(log, plus)), which starts from the LAST element and
+// adds the earlier ones in turn; the fold below runs in exactly that order over the elements
+// in pileup order, with java.lang.StrictMath's log, so every genotype gets the reference's
+// bits.  Lanes = elements compute the three possible terms log(pc + pc), log(pc + (1 - pc)),
+// log((1 - pc) + (1 - pc)); then the wave walks the elements backwards, each lane (genotype)
+// adding the term its alleles select.
+__device__ double fold_genotypes(const DevReads &R, const Cover &cv, int32_t pos, uint8_t refbase, int min_mapq,
+                                 bool include_alignment, Key128 k1, Key128 k2, Counters *ctr) {
+  const int lane = threadIdx.x & 63;
+  double agg = 0.0;
+  bool started = false;
+  if (cv.n == 0) return agg;
+  for (int64_t c0 = ((cv.n - 1) / 64) * 64; c0 >= 0; c0 -= 64) {
+    bool act;
+    const int64_t r = cv.read(R, c0 + lane, pos, &act);
+    Key128 key{0, 0};
+    double t2 = 0.0, th = 0.0, t0 = 0.0;
+    bool pass = false;
+    if (act) {
+      AlleleDesc d;
+      int errc = 0;
+      if (classify(R, r, pos, refbase, d, &errc)) {
+        const int mq = (int)R.mapq[r];
+        pass = min_mapq <= 0 || mq >= min_mapq;
+        if (pass) {
+          key = allele_key(R, d, pos, 0);
+          const int q = elem_quality(R, d);
+          if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
+          double pc = phred_success(q);
+          if (include_alignment) pc = pc * phred_success(mq);  // probabilityCorrectIncludingAlignment
+          const double pw = 1.0 - pc;
+          t2 = sm::log(pc + pc);
+          th = sm::log(pc + pw);
+          t0 = sm::log(pw + pw);
+        }
+      }
+    }
+    unsigned long long pb = __ballot(act && pass);
+    while (pb) {
+      const int j = 63 - __clzll((long long)pb);  // the chunk's last element first
+      pb &= ~(1ull << j);
+      const uint64_t klo = lane_u64(key.lo, j), khi = lane_u64(key.hi, j);
+      const double a2 = lane_f64(t2, j), ah = lane_f64(th, j), a0 = lane_f64(t0, j);
+      const bool m1 = k1.lo == klo && k1.hi == khi, m2 = k2.lo == klo && k2.hi == khi;
+      const double term = (m1 && m2) ? a2 : (m1 || m2) ? ah : a0;
+      agg = started ? agg + term : term;
+      started = true;
+    }
+  }
+  return agg;
+}
+
+__device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Cover &cv, int32_t pos,
+                                int min_mapq, bool include_alignment, int16_t *order, uint8_t *is_var,
+                                double *ll_lds, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   GenoResult res{};
   // eligibility + variant flag per entry (entry j on lane j & 63, slot j >> 6)
@@ -591,64 +782,66 @@ __device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, int32_t 
   const int G = n * (n + 1) / 2;
   res.G = G;
   if (G == 0) return res;
-  const double ln2d = log(2.0) * (double)P.depth_f;
-  // log-likelihood of this lane's genotype in chunk g0 (wave-uniform call: the table
-  // broadcasts below need every lane)
-  auto ll_chunk = [&](int g0) -> double {
+  if (G > kMaxG) {
+    raise_at(ctr, GQ_E_CAPACITY, pos);
+    res.G = 0;
+    return res;
+  }
+  // log-likelihood per genotype: the Colt fold, + log(prior = 1) - ln 2 * depth (Likelihood.scala:189)
+  const double ln2d = sm::log(2.0) * (double)P.depth_f;
+  for (int g0 = 0; g0 < G; g0 += 64) {
     const int g = g0 + lane;
-    int ei = -1, ej = -1;
-    if (g < G) {
-      int i, j;
-      genotype_index(g, n, i, j);
-      ei = order[i];
-      ej = order[j];
+    int i = 0, j = 0;
+    if (g < G) genotype_index(g, n, i, j);
+    const int ei = g < G ? order[i] : 0, ej = g < G ? order[j] : 0;
+    // the table keys live on their owner lanes (entry e: lane e & 63, slot e >> 6)
+    Key128 k1{~0ull, ~0ull}, k2{~0ull, ~0ull};
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const uint64_t lo1 = __shfl(P.klo[s], ei & 63, 64), hi1 = __shfl(P.khi[s], ei & 63, 64);
+      const uint64_t lo2 = __shfl(P.klo[s], ej & 63, 64), hi2 = __shfl(P.khi[s], ej & 63, 64);
+      if (g < G && s == (ei >> 6)) k1 = Key128{lo1, hi1};
+      if (g < G && s == (ej >> 6)) k2 = Key128{lo2, hi2};
     }
-    double agg = 0.0;
-    for (int x = 0; x < P.nt; ++x) {
-      uint32_t nf = 0;
-      PILE_GET(P, n_f, x, nf);
-      if (nf == 0) continue;  // uniform
-      double a1 = 0, a0 = 0, ah = 0;
-      PILE_GET(P, s1, x, a1);
-      PILE_GET(P, s0, x, a0);
-      PILE_GET(P, sh, x, ah);
-      agg += (x == ei && x == ej) ? a1 : (x == ei || x == ej) ? ah : a0;
-    }
-    return agg + log(1.0) - ln2d;
-  };
+    const double agg = fold_genotypes(R, cv, pos, P.refbase, min_mapq, include_alignment, k1, k2, ctr);
+    if (g < G) ll_lds[g] = agg + sm::log(1.0) - ln2d;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // normalisation in the reference's order (Likelihood.scala:190-199): total = the exp(ll)
+  // added genotype by genotype, then exp(ll - log(total)); maxBy keeps the first maximum, the
+  // normal's variant mass adds the variant genotypes in turn (SomaticStandardCaller.scala:206-217)
   double tot = 0.0;
   for (int g0 = 0; g0 < G; g0 += 64) {
-    const double ll = ll_chunk(g0);
-    if (g0 + lane < G) tot += exp(ll);
+    const double e = (g0 + lane < G) ? sm::exp(ll_lds[g0 + lane]) : 0.0;
+    for (int j = 0; j < 64 && g0 + j < G; ++j) tot = tot + lane_f64(e, j);
   }
-  const double lt = log(wave_sum(tot));
-  double best = -1.0, vsum = 0.0;
-  int bestg = 0x7FFFFFFF;
+  const double lt = sm::log(tot);
+  double best = 0.0, vsum = 0.0;
+  int bestg = -1;
   for (int g0 = 0; g0 < G; g0 += 64) {
-    const double ll = ll_chunk(g0);
     const int g = g0 + lane;
-    if (g >= G) continue;
-    const double L = exp(ll - lt);
-    int i, j;
-    genotype_index(g, n, i, j);
-    if (is_var[order[i]] || is_var[order[j]]) vsum += L;
-    if (L > best) {
-      best = L;
-      bestg = g;
+    double L = 0.0;
+    bool v = false;
+    if (g < G) {
+      L = sm::exp(ll_lds[g] - lt);
+      int i, j;
+      genotype_index(g, n, i, j);
+      v = is_var[order[i]] || is_var[order[j]];
     }
-  }
-  // wave argmax with first-maximum tie break (maxBy)
-  for (int d = 1; d < 64; d <<= 1) {
-    const double ob = __shfl_xor(best, d, 64);
-    const int og = __shfl_xor(bestg, d, 64);
-    if (ob > best || (ob == best && og < bestg)) {
-      best = ob;
-      bestg = og;
+    const unsigned long long vb = __ballot(v);
+    for (int j = 0; j < 64 && g0 + j < G; ++j) {
+      const double Lj = lane_f64(L, j);
+      if (bestg < 0 || Lj > best) {
+        best = Lj;
+        bestg = g0 + j;
+      }
+      if ((vb >> j) & 1ull) vsum = vsum + Lj;
     }
   }
   res.best_g = bestg;
   res.best_l = best;
-  res.var_sum = wave_sum(vsum);
+  res.var_sum = vsum;
   int i, j;
   genotype_index(bestg, n, i, j);
   res.bi = order[i];
@@ -658,12 +851,10 @@ __device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, int32_t 
 
 // AlleleEvidence.apply (AlleleEvidence.scala:58-101) for the elements of one sample whose
 // allele key is `target`.  Supporting elements' (mapq, quality, mismatches) go to `ev_lds`
-// in element order for the running mean and the medians.
-__device__ void allele_evidence(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int min_mapq,
-                                const SamplePile &P, Key128 target, double likelihood, uint32_t *ev_lds,
-                                Counters *ctr, gq_evidence &ev, int32_t *cover_lds) {
+// in element order for the running mean (Breeze, in element order) and the medians.
+__device__ void allele_evidence(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, const SamplePile &P,
+                                Key128 target, double likelihood, uint32_t *ev_lds, Counters *ctr, gq_evidence &ev) {
   const int lane = threadIdx.x & 63;
-  const Cover cv = make_cover(R, rb, re, pos, cover_lds);
   uint32_t n = 0, fwd = 0;
   for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
     bool cov;
@@ -689,7 +880,7 @@ __device__ void allele_evidence(const DevReads &R, int64_t rb, int64_t re, int32
     const unsigned long long hb = __ballot(hit);
     const uint32_t before = (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
     if (hit && n + before < (uint32_t)kEvCap) ev_lds[n + before] = packed;
-    fwd += (uint32_t)__popcll(__ballot(hit && !(R.flags[r < re ? r : rb] & 1)));
+    fwd += (uint32_t)__popcll(__ballot(hit && !(R.flags[r] & 1)));
     n += (uint32_t)__popcll(hb);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -748,35 +939,63 @@ __device__ void allele_evidence(const DevReads &R, int64_t rb, int64_t re, int32
 
 constexpr int kSomWaves = kBlock / 64;
 
-// three waves per SIMD (<= 168 VGPRs) instead of one at the unconstrained 298: 13.6 -> 8.5 ms
+// Per-window data of the element order (window_first / window_group), by tile range.
+struct SomWin {
+  const int32_t *range_win;  // plan range -> window
+  const WinInit *wi;         // [window * 2 + set]
+  const int64_t *init_reads;
+  const int32_t *init_rank;
+};
+
+// three waves per SIMD (<= 168 VGPRs)
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void somatic_call(const Tile *__restrict__ tiles_t,
                                                        const Tile *__restrict__ tiles_n,
                                                        const ComplexItem *__restrict__ items, DevReads RT,
                                                        DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
                                                        unsigned long long rec_cap, uint8_t *__restrict__ pool,
                                                        unsigned long long pool_cap, unsigned long long cand_cap,
-                                                       Counters *ctr) {
+                                                       Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out,
+                                                       unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
+                                                       const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+  // amb_in == nullptr: every candidate; where a sample's reads' MD-derived bases disagree the
+  // locus is only listed (amb_out) for the heap-order replay.  amb_in != nullptr: the listed
+  // loci, with both samples' reference bases resolved in heap order (amb_ref[2 i + set]).
   __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
   __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
   __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
-  __shared__ int32_t cover_lds[kSomWaves][kCover];
+  __shared__ int32_t cover_t[kSomWaves][kCover], cover_n[kSomWaves][kCover];
+  __shared__ double ll_lds[kSomWaves][kMaxG];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const unsigned long long n_items = ctr->n_complex < cand_cap ? ctr->n_complex : cand_cap;
-  for (int64_t it = gwave; it < (int64_t)n_items; it += nwaves_total) {
+  const unsigned long long n_items =
+      amb_in ? (unsigned long long)n_amb_in : (ctr->n_complex < cand_cap ? ctr->n_complex : cand_cap);
+  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    const int64_t it = amb_in ? amb_in[li].item : li;
     const ComplexItem item = items[it];
     const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
     const int32_t pos = item.pos;
+    const int32_t win = sw.range_win[tt.range];
+    const Cover ct = make_cover(RT, tt.rb, tt.re, pos, cover_t[wv], ev_lds[wv], sw.wi[2 * win], sw.init_reads,
+                                sw.init_rank, ctr);
+    const Cover cn = make_cover(RN, tn.rb, tn.re, pos, cover_n[wv], ev_lds[wv], sw.wi[2 * win + 1], sw.init_reads,
+                                sw.init_rank, ctr);
     SamplePile PT, PN;
-    gather_sample(RT, tt.rb, tt.re, pos, prm.min_mapq, true, ctr, PT, cover_lds[wv]);
-    gather_sample(RN, tn.rb, tn.re, pos, prm.min_mapq, false, ctr, PN, cover_lds[wv]);
+    gather_sample(RT, ct, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li] : -1, ctr, PT);
+    gather_sample(RN, cn, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li + 1] : -1, ctr, PN);
     if (PT.overflow || PN.overflow) {
       raise_at(ctr, GQ_E_CAPACITY, pos);
       continue;
     }
-    if ((item.flags & 1) && (PT.depth_all + PN.depth_all) > 0 && lane == 0)
+    if ((item.flags & 1) && !amb_in && (PT.depth_all + PN.depth_all) > 0 && lane == 0)
       atomicAdd(&ctr->spread[0][it & (kSpread - 1)], 1ull);
+    if (!amb_in && (PT.ambiguous || PN.ambiguous)) {  // heap order decides a reference base: list it
+      if (lane == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+      }
+      continue;
+    }
     // MultiAllelicPileupFilter (PileupFilter.scala:29-44): > 2 distinct alleles => no elements
     if (prm.filter_multi_allelic) {
       if (PT.nt > 2) PT.depth_f = 0;
@@ -795,19 +1014,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       }
       if (ref_match == PT.depth_f) continue;
     }
-    const GenoResult tg = genotypes(RT, PT, pos, order_lds[wv], var_lds[wv]);
+    const GenoResult tg = genotypes(RT, PT, ct, pos, prm.min_mapq, true, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
     if (tg.G == 0) continue;
     const bool t_var = var_lds[wv][tg.bi] || var_lds[wv][tg.bj];
     if (!t_var) continue;
-    const GenoResult ng = genotypes(RN, PN, pos, order_lds[wv], var_lds[wv]);
+    const AlleleDesc a1 = pile_desc(PT, tg.bi), a2 = pile_desc(PT, tg.bj);
+    const GenoResult ng = genotypes(RN, PN, cn, pos, prm.min_mapq, false, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
     const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
     const double odds = tg.best_l / nvs;
     if (!(odds * 100.0 >= (double)prm.odds)) continue;
-    // decisions taken within FP rounding of a threshold are flagged (GQ_FLAG_KNIFE_EDGE):
-    // their outcome depends on summation order in the reference too
+    // decisions taken within FP rounding of a threshold are flagged (GQ_FLAG_KNIFE_EDGE)
     uint8_t knife = near_edge(odds * 100.0, (double)prm.odds) ? GQ_FLAG_KNIFE_EDGE : 0;
     // first variant allele of the ML genotype with a non-empty alt (SomaticStandardCaller.scala:227)
-    const AlleleDesc a1 = pile_desc(PT, tg.bi), a2 = pile_desc(PT, tg.bj);
     const bool v1 = allele_is_variant(RT, a1, pos) && allele_alt_len(a1) > 0;
     const bool v2 = allele_is_variant(RT, a2, pos) && allele_alt_len(a2) > 0;
     if (!v1 && !v2) continue;
@@ -816,9 +1034,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     const Key128 tkey = allele_key(RT, al, pos, 0);
     const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
     gq_evidence tev, nev;
-    allele_evidence(RT, tt.rb, tt.re, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev, cover_lds[wv]);
-    allele_evidence(RN, tn.rb, tn.re, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev, cover_lds[wv]);
-    const double log_odds = log(odds);
+    allele_evidence(RT, ct, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev);
+    allele_evidence(RN, cn, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev);
+    const double log_odds = sm::log(odds);
     const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
     if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
     const float vaf = (float)tev.allele_read_depth / (float)tev.read_depth;
@@ -907,10 +1125,66 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     *out = res;
     return GQ_OK;
   }
+  // PhredUtils.phredToSuccessProbability table: the host's pow, the bits the reference starts from
+  {
+    static_assert(sizeof(double) == 8, "FP64");
+    double succ[256];
+    for (int q = 0; q < 256; ++q) succ[q] = 1.0 - std::pow(10.0, -q / 10.0);
+    HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_succ), succ, sizeof succ, 0, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  // pileup element order: each window's first visited locus and initial (heap-ordered) group
+  SomWin sw{};
+  {
+    const int64_t nw = (int64_t)pt.wins.size(), nr = (int64_t)pt.rs.size();
+    std::vector<int32_t> w_contig((size_t)nw);
+    std::vector<int64_t> w_roff((size_t)nw + 1);
+    for (int64_t w = 0; w < nw; ++w) {
+      w_contig[(size_t)w] = pt.wins[(size_t)w].contig;
+      w_roff[(size_t)w] = pt.wins[(size_t)w].r0;
+    }
+    w_roff[(size_t)nw] = nr;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_roff = al(4 * (size_t)nw), o_rs = o_roff + al(8 * ((size_t)nw + 1)), o_re = o_rs + al(8 * (size_t)nr),
+                 o_rw = o_re + al(8 * (size_t)nr), o_wi = o_rw + al(4 * (size_t)nr),
+                 o_lo = o_wi + al(sizeof(WinInit) * 2 * (size_t)nw), o_end = o_lo + al(8 * 2 * (size_t)nw);
+    HIP_TRY(c->win_meta.ensure(o_end));
+    char *b = (char *)c->win_meta.p;
+    HIP_TRY(hipMemcpyAsync(b, w_contig.data(), 4 * (size_t)nw, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_roff, w_roff.data(), 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_rs, pt.rs.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_re, pt.re.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_rw, pt.rwin.data(), 4 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    WinInit *d_wi = (WinInit *)(b + o_wi);
+    int64_t *d_lo = (int64_t *)(b + o_lo);
+    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       (const int32_t *)b, (const int64_t *)(b + o_roff), (const int64_t *)(b + o_rs),
+                       (const int64_t *)(b + o_re), nw, t->d, n->d, d_wi, d_lo);
+    HIP_TRY(hipGetLastError());
+    std::vector<WinInit> wi((size_t)(2 * nw));
+    HIP_TRY(hipMemcpyAsync(wi.data(), d_wi, sizeof(WinInit) * wi.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int64_t tot = 0;
+    for (WinInit &x : wi) {
+      x.off = tot;
+      tot += x.cap;
+    }
+    HIP_TRY(hipMemcpyAsync(d_wi, wi.data(), sizeof(WinInit) * wi.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c->win_grp.ensure((size_t)std::max<int64_t>(tot, 1) * 16));
+    int64_t *d_reads = (int64_t *)c->win_grp.p;
+    int32_t *d_rank = (int32_t *)(d_reads + std::max<int64_t>(tot, 1));
+    int32_t *d_heap = d_rank + std::max<int64_t>(tot, 1);
+    hipLaunchKernelGGL(window_group, dim3((unsigned)((2 * nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       d_wi, (const int64_t *)d_lo, 2 * nw, t->d, n->d, d_reads, d_rank, d_heap);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // wi (host) outlives its copy
+    sw = SomWin{(const int32_t *)(b + o_rw), d_wi, d_reads, d_rank};
+  }
   unsigned long long cand_cap = std::max<unsigned long long>(1 << 16, pt.n_loci / 4);
-  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20;
+  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->cplx.ensure(cand_cap * sizeof(ComplexItem)));
     HIP_TRY(c->srecs.ensure(rec_cap * sizeof(SomRec)));
     HIP_TRY(c->pool.ensure(pool_cap));
@@ -939,7 +1213,8 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
     hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
-                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr);
+                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr, sw,
+                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -948,6 +1223,33 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     if (hc.n_complex > cand_cap) {
       cand_cap = hc.n_complex + 1024;
       retry = true;
+    }
+    if (hc.n_amb > amb_cap) {
+      amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (!retry && hc.n_amb > 0 && !hc.err) {
+      // loci where a sample's reference base depends on heap order: replay both windows'
+      // queues, then the caller again over just those loci with the resolved bases
+      std::vector<AmbItem> amb((size_t)hc.n_amb);
+      HIP_TRY(hipMemcpyAsync(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(c->amb_ref.ensure(2 * amb.size()));
+      st = heap_ref_bases(c, pt, c->tiles, {t, n}, amb, (uint8_t *)c->amb_ref.p);
+      if (st) {
+        free(res);
+        return st;
+      }
+      const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 8192);
+      hipLaunchKernelGGL(somatic_call, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr, sw,
+                         (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
+                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
     }
     if (hc.n_rec > rec_cap) {
       rec_cap = hc.n_rec + 1024;
