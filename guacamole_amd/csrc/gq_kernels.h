@@ -42,6 +42,7 @@ struct DevReads {
   const uint32_t *cigar, *md_ev;
   int64_t seq_bytes;
   int64_t seq_cap;  // readable bytes of the device seq allocation (>= seq_bytes; padded on upload)
+  int64_t cigar_len, md_len;  // pool sizes (upload-time bounds checks)
   // derived at upload (read_shape):
   const int16_t *lead;   // leading soft clip of a [S|H]*(M|=|X)[S|H]* CIGAR, -1 otherwise
   const uint8_t *ev_rb;  // per MD event: the read's sequenced base at that position (0 for deletions)

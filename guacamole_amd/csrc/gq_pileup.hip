@@ -230,23 +230,80 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
   }
 }
 
-// CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
-// [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
-__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb,
-                           uint8_t *__restrict__ clean, int *__restrict__ unordered) {
+// Upload-time checks, one thread per read (bits of *bad): 1 = reads not sorted by start within
+// their contig, or pmax_end not the running maximum of end (SlidingWindow.scala:55-56 "Regions
+// must be sorted"; plan_tiles binary-searches both); 2 = an offset / length outside its pool or
+// a sample slot >= n_samples (would read out of bounds); 4 = the sequence pool is not in read
+// order (flags only: such tiles take the walker).
+__global__ void validate_reads(DevReads R, int *__restrict__ bad) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
-  // pool order: read r's bytes start at or after the end of read r - 1's
-  if (r > 0 && R.seq_off[r] < R.seq_off[r - 1] + R.seq_len[r - 1]) atomicOr(unordered, 1);
-  {  // every sequenced byte one of A C G T N (the germline fast path's precondition)
-    const uint8_t *q = R.seq + R.seq_off[r];
-    bool ok = true;
-    for (int32_t k = 0; k < R.seq_len[r]; ++k) {
-      const uint8_t b = q[k];
-      ok = ok && (b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'N');
-    }
-    clean[r] = ok ? 1 : 0;
+  int lo = 0, hi = R.n_contigs;  // contig of r: last c with contig_read_begin[c] <= r
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (R.contig_read_begin[m] <= r) lo = m;
+    else hi = m - 1;
   }
+  const bool first = R.contig_read_begin[lo] == r;
+  const int32_t s = R.start[r], e = R.end[r], pm = R.pmax_end[r];
+  int b = 0;
+  if (e < s || s < 0) b |= 1;
+  if (first ? pm != e : (s < R.start[r - 1] || pm != max(R.pmax_end[r - 1], e))) b |= 1;
+  if (R.seq_off[r] < 0 || R.seq_len[r] < 0 || R.seq_off[r] + R.seq_len[r] > R.seq_bytes) b |= 2;
+  if (R.cigar_off[r] < 0 || R.n_cigar[r] < 0 || R.cigar_off[r] + R.n_cigar[r] > R.cigar_len) b |= 2;
+  if (R.n_md[r] > 0 && (R.md_off[r] < 0 || R.md_off[r] + R.n_md[r] > R.md_len)) b |= 2;
+  if ((int)R.sample[r] >= R.n_samples) b |= 2;
+  if (r > 0 && R.seq_off[r] < R.seq_off[r - 1] + R.seq_len[r - 1]) b |= 4;
+  if (b) atomicOr(bad, b);
+}
+
+// clean[r] = every sequenced byte of read r is one of A C G T N (the germline column path's
+// precondition).  Pool in read order: 16 bytes per thread, coalesced; the rare other bytes
+// find their read by binary search of seq_off and clear its flag (clean preset to 1).
+__global__ void pool_clean(DevReads R, uint8_t *__restrict__ clean) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte chunk
+  const int64_t b0 = c * 16;
+  if (b0 >= R.seq_bytes) return;
+  uint32_t ws[4] = {0, 0, 0, 0};
+  if (b0 + 16 <= R.seq_cap) {  // uploaded pools have a zeroed tail; a wrapped one may end anywhere
+    const uint4 w = *reinterpret_cast<const uint4 *>(R.seq + b0);
+    ws[0] = w.x, ws[1] = w.y, ws[2] = w.z, ws[3] = w.w;
+  } else {
+    for (int k = 0; k < 16 && b0 + k < R.seq_bytes; ++k) ws[k >> 2] |= (uint32_t)R.seq[b0 + k] << (8 * (k & 3));
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint8_t x = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
+    if (b0 + k >= R.seq_bytes || x == 'A' || x == 'C' || x == 'G' || x == 'T' || x == 'N') continue;
+    int64_t lo = 0, hi = R.n_reads - 1;  // last read with seq_off <= b0 + k
+    while (lo < hi) {
+      const int64_t m = (lo + hi + 1) >> 1;
+      if (R.seq_off[m] <= b0 + k) lo = m;
+      else hi = m - 1;
+    }
+    // zero-length reads share an offset with their neighbour: clear every read holding the byte
+    for (int64_t r = lo; r >= 0 && R.seq_off[r] + R.seq_len[r] > b0 + k; --r)
+      if (R.seq_off[r] <= b0 + k) clean[r] = 0;
+  }
+}
+// The same per read (a wrapped pool in another order), one thread per read.
+__global__ void read_clean(DevReads R, uint8_t *__restrict__ clean) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const uint8_t *q = R.seq + R.seq_off[r];
+  bool ok = true;
+  for (int32_t k = 0; k < R.seq_len[r]; ++k) {
+    const uint8_t b = q[k];
+    ok = ok && (b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'N');
+  }
+  clean[r] = ok ? 1 : 0;
+}
+
+// CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
+// [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
+__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
   const int64_t off = R.cigar_off[r];
   const int32_t n = R.n_cigar[r];
   int32_t ld = 0, mlen = 0;
@@ -909,6 +966,12 @@ static gq_status validate_reads(const gq_reads *h) {
 }
 
 static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
+  {  // contig_read_begin: 0, non-decreasing, n_reads (host copy)
+    const auto &b = d->contig_read_begin;
+    bool ok = !b.empty() && b.front() == 0 && b.back() == d->d.n_reads;
+    for (size_t i = 1; i < b.size() && ok; ++i) ok = b[i] >= b[i - 1];
+    if (!ok) return set_err(GQ_E_UNSORTED, "contig_read_begin must run from 0 to n_reads, non-decreasing");
+  }
   void *p = nullptr, *q = nullptr, *cl = nullptr;
   HIP_TRY(hipMalloc(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
   d->owned.push_back(p);
@@ -926,10 +989,29 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->owned.push_back(flag);
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q,
-                       (uint8_t *)cl, (int *)flag);
+    hipLaunchKernelGGL(validate_reads, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&unordered, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    int bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad & 1)
+      return set_err(GQ_E_UNSORTED, "Regions must be sorted by start locus: reads are not sorted by (contig, start), "
+                                    "or pmax_end is not the running maximum of end within each contig");
+    if (bad & 2)
+      return set_err(GQ_E_ARG, "read set: an offset or length lies outside its pool, or a sample slot >= n_samples");
+    unordered = (bad & 4) ? 1 : 0;
+    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q);
+    HIP_TRY(hipGetLastError());
+    if (!unordered) {
+      HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->stream));
+      const int64_t chunks = (d->d.seq_bytes + 15) / 16;
+      if (chunks > 0)
+        hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                           d->d, (uint8_t *)cl);
+    } else {
+      hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl);
+    }
+    HIP_TRY(hipGetLastError());
   }
   {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds
     const int64_t n = d->d.n_reads;
@@ -1002,7 +1084,8 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   // past the last read stay inside the allocation (DevReads::seq_cap)
   enum : size_t { pad_contig_read_begin = 0, pad_start = 0, pad_end = 0, pad_pmax_end = 0, pad_mapq = 0, pad_flags = 0,
                   pad_sample = 0, pad_seq_off = 0, pad_seq_len = 0, pad_cigar_off = 0, pad_n_cigar = 0, pad_md_off = 0,
-                  pad_n_md = 0, pad_n_mismatch = 0, pad_seq = kSeqPad, pad_qual = 0, pad_cigar = 0, pad_md_ev = 0 };
+                  pad_n_md = 0, pad_n_mismatch = 0, pad_seq = kSeqPad, pad_qual = kSeqPad, pad_cigar = 0,
+                  pad_md_ev = 0 };
   // HBM layout: the sequence / quality pools in read order (each read's bytes after the
   // previous read's), so a tile's reads are one contiguous byte range for the LDS stage.
   // A host pool in another order is re-laid out here (the caller's buffers are untouched).
@@ -1054,6 +1137,8 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   d->d.n_reads = n;
   d->d.seq_bytes = h->seq_bytes;
   d->d.seq_cap = h->seq_bytes + kSeqPad;
+  d->d.cigar_len = h->cigar_len;
+  d->d.md_len = h->md_len;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
@@ -1076,6 +1161,8 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   d->d.n_reads = h->n_reads;
   d->d.seq_bytes = h->seq_bytes;
   d->d.seq_cap = h->seq_bytes;  // caller-owned buffer: no readable tail assumed
+  d->d.cigar_len = h->cigar_len;
+  d->d.md_len = h->md_len;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
   d->d.contig_read_begin = h->contig_read_begin;

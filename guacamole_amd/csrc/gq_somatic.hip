@@ -75,7 +75,7 @@ struct SomRec {  // one emitted CalledSomaticAllele
 // sum runs in FP32 (error far below the eps the test applies) over the reads the mapq filter
 // keeps (QualityAlignedReadsFilter, PileupElementsFilter.scala:25-36).
 __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r, int32_t L0, int32_t L1,
-                                                    int min_mapq, const float *eq, float *marg) {
+                                                    int min_mapq, const float *eq, const float *lsq, float *marg) {
   const int32_t s = R.start[r], e = R.end[r];
   if (e <= L0 || s >= L1) return;
   const int mq = (int)R.mapq[r];
@@ -83,6 +83,10 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
   const int32_t nmd = R.n_md[r];
   if (nmd < 0) return;  // GQ_E_NO_MD is raised by the histogram pass
   const float em = exp2f(-0.33219281f * (float)mq);  // 10^(-mapq/10)
+  // log phredSuccess(mapq) = log(1 - em), -inf at mapq 0: taken from log1p, not from 1 - f below
+  // (1 - f cancels catastrophically when pc -> 0 and would turn log(2 pc) = -inf into a finite
+  // value, proving hom-ref where a mapq-0 Match read makes L(ref, ref) = -inf)
+  const float lsm = log1pf(-em);
   const int64_t so = R.seq_off[r];
   const uint32_t *ev = R.md_ev + R.md_off[r];
   int k = 0;  // MD event cursor (events sorted by offset; runs visited in reference order)
@@ -96,8 +100,19 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
     for (int32_t l = a; l < b;) {
       const int64_t gp = so + rp0 + (l - ra);
       const int sh = (int)(gp & 15);
-      const uint4 ws = *reinterpret_cast<const uint4 *>(R.seq + (gp - sh));
-      const uint4 wq = *reinterpret_cast<const uint4 *>(R.qual + (gp - sh));
+      uint4 ws, wq;
+      if (gp - sh + 16 <= R.seq_cap) {  // uploaded pools carry a zeroed tail (seq and qual)
+        ws = *reinterpret_cast<const uint4 *>(R.seq + (gp - sh));
+        wq = *reinterpret_cast<const uint4 *>(R.qual + (gp - sh));
+      } else {  // the end of a wrapped (caller-allocated) pool: byte loads only inside it
+        uint32_t s4[4] = {0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16 && gp - sh + k < R.seq_bytes; ++k) {
+          s4[k >> 2] |= (uint32_t)R.seq[gp - sh + k] << (8 * (k & 3));
+          q4[k >> 2] |= (uint32_t)R.qual[gp - sh + k] << (8 * (k & 3));
+        }
+        ws = make_uint4(s4[0], s4[1], s4[2], s4[3]);
+        wq = make_uint4(q4[0], q4[1], q4[2], q4[3]);
+      }
       const int nb = min(16 - sh, b - l);
       for (int j = 0; j < nb; ++j) {
         const int bi = sh + j, wi = bi >> 2, bs = 8 * (bi & 3);
@@ -118,7 +133,7 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
         } else {
           const float eb = eq[q];
           const float f = eb + em - eb * em;  // 1 - pc
-          if (base == m) t = kLn2 + __logf(1.0f - f) - fmaxf(0.0f, kLn2 + __logf(f));
+          if (base == m) t = kLn2 + lsq[q] + lsm - fmaxf(0.0f, kLn2 + __logf(f));
           else t = __logf(f);  // log(2 (1 - pc)) - ln 2
         }
         atomicAdd(&marg[l + j - L0], t);
@@ -163,7 +178,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   static_assert(KPT <= 8, "per-thread flag bits");
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   __shared__ float marg[T];  // hom-ref margin of the tumor pileup
-  __shared__ float eq[128];  // 10^(-q/10)
+  __shared__ float eq[128];   // 10^(-q/10)
+  __shared__ float lsq[128];  // log(1 - 10^(-q/10)) = log phredSuccess(q), -inf at q = 0
   const Tile tt = tiles_t[blockIdx.x], tn = tiles_n[blockIdx.x];
   const int32_t L0 = tt.L0, L1 = tt.L1;
   const int nloci = L1 - L0;
@@ -180,13 +196,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
   for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int i = threadIdx.x; i < T; i += blockDim.x) marg[i] = 0.0f;
-  if (threadIdx.x < 128) eq[threadIdx.x] = exp2f(-0.33219281f * (float)threadIdx.x);
+  if (threadIdx.x < 128) {
+    eq[threadIdx.x] = exp2f(-0.33219281f * (float)threadIdx.x);
+    lsq[threadIdx.x] = log1pf(-eq[threadIdx.x]);
+  }
   __syncthreads();
   {
     GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
     for (int64_t r = tt.rb + threadIdx.x; r < tt.re; r += blockDim.x) {
       walk_read_lane(RT, r, L0, L1, sink);
-      hom_ref_margin_lane(RT, r, L0, L1, min_mapq, eq, marg);
+      hom_ref_margin_lane(RT, r, L0, L1, min_mapq, eq, lsq, marg);
     }
   }
   __syncthreads();

@@ -30,20 +30,6 @@ def split_loci(loci: LociSet, world: int) -> List[LociSet]:
     return [inv.get(r, LociSet()) for r in range(world)]
 
 
-def pack_rows(rows: Sequence[tuple]) -> np.ndarray:
-    """Genotype rows -> one uint8 buffer (tab-separated lines)."""
-    text = "".join("%s\t%d\t%d\t%s,%s\t%s\t%s\t%d\n" % (c, l, s, g[0], g[1], r, a, f) for c, l, s, g, r, a, f in rows)
-    return np.frombuffer(text.encode("latin-1"), dtype=np.uint8).copy()
-
-
-def unpack_rows(buf: np.ndarray) -> List[tuple]:
-    out = []
-    for line in bytes(buf).decode("latin-1").splitlines():
-        c, l, s, g, r, a, f = line.split("\t")
-        out.append((c, int(l), int(s), tuple(g.split(",")), r, a, int(f)))
-    return out
-
-
 def gather_images_to_rank0(calls, device: str):
     # device "cpu": the images are staged in host memory (a gloo rehearsal of the flow)
     """The terminal gather of the multi-GPU bench: every rank's germline result image (left in
@@ -55,6 +41,7 @@ def gather_images_to_rank0(calls, device: str):
     import torch
     import torch.distributed as dist
 
+    calls.check_current()
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = torch.device(device)
     n = torch.tensor([int(calls.image_bytes)], dtype=torch.int64, device=dev)

@@ -181,6 +181,9 @@ class Context:
         self.h = C.c_void_p()
         _check(lib().gq_open(int(device), C.byref(self.h)))
         self.device = device
+        # germline calls reuse the context's result image: a DeviceCalls is valid until the
+        # next germline call on this context (gqpileup.h, gq_calls_device)
+        self.image_epoch = 0
 
     def close(self) -> None:
         if self.h:
@@ -218,6 +221,7 @@ class Context:
         L, keep = make_gq_loci(*loci)
         p = gq_germline_params(int(threshold), int(bool(emit_ref)), int(bool(emit_no_call)))
         out = C.POINTER(gq_calls)()
+        self.image_epoch += 1
         _check(lib().gq_germline_threshold(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
         return GermlineCalls.from_result(out)
 
@@ -227,8 +231,9 @@ class Context:
         L, keep = make_gq_loci(*loci)
         p = gq_germline_params(int(threshold), int(bool(emit_ref)), int(bool(emit_no_call)))
         out = gq_calls_device()
+        self.image_epoch += 1
         _check(lib().gq_germline_threshold_device(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
-        return DeviceCalls(out)
+        return DeviceCalls(out, self)
 
     def somatic_standard(self, tumor: "DeviceReads", normal: "DeviceReads", loci, **params) -> "SomaticCalls":
         """somatic-standard over the loci ranges (gq_somatic_standard).  params: the
@@ -284,7 +289,8 @@ class DeviceCalls:
 
     NAMES = ("contig", "pos", "sample", "gt0", "gt1", "flags", "ref_off", "ref_len", "alt_off", "alt_len")
 
-    def __init__(self, d: gq_calls_device):
+    def __init__(self, d: gq_calls_device, ctx: Optional["Context"] = None):
+        self.ctx, self.epoch = ctx, (ctx.image_epoch if ctx is not None else None)
         c = d.calls
         self.n, self.image, self.image_bytes = int(c.n), int(d.image or 0), int(d.image_bytes)
         self.pool_len = int(c.pool_len)
@@ -298,8 +304,15 @@ class DeviceCalls:
     def __len__(self) -> int:
         return self.n
 
+    def check_current(self) -> None:
+        """Raise if a later germline call on the context has replaced the image."""
+        if self.ctx is not None and self.ctx.image_epoch != self.epoch:
+            raise GQError(7, "DeviceCalls used after a later germline call on its context (the result image "
+                             "is reused; copy it first with to_host())")
+
     def to_host(self) -> "GermlineCalls":
         """Copy the image over PCIe (hipMemcpy) and view it as GermlineCalls (test / export)."""
+        self.check_current()
         host = np.zeros(max(self.image_bytes, 1), np.uint8)
         if self.image_bytes:
             hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
@@ -356,25 +369,6 @@ class GermlineCalls:
     def alt(self, i: int) -> str:
         o = int(self.a["alt_off"][i])
         return self.pool[o:o + int(self.a["alt_len"][i])].decode("latin-1")
-
-    def pack(self) -> np.ndarray:
-        """Flat uint8 buffer (fixed-width fields + allele pool) for the multi-GPU gather."""
-        parts = [np.array([len(self), len(self.pool)], np.int64).view(np.uint8)]
-        parts += [np.ascontiguousarray(self.a[k]).view(np.uint8) for k in sorted(self.a)]
-        parts.append(np.frombuffer(self.pool, dtype=np.uint8))
-        return np.concatenate(parts)
-
-    @staticmethod
-    def unpack(buf: np.ndarray) -> "GermlineCalls":
-        n, pl = (int(x) for x in buf[:16].view(np.int64))
-        dt = {"contig": np.int32, "pos": np.int64, "sample": np.uint8, "gt0": np.uint8, "gt1": np.uint8,
-              "flags": np.uint8, "ref_off": np.int64, "ref_len": np.int32, "alt_off": np.int64, "alt_len": np.int32}
-        off, a = 16, {}
-        for k in sorted(dt):
-            nb = n * np.dtype(dt[k]).itemsize
-            a[k] = buf[off:off + nb].copy().view(dt[k])
-            off += nb
-        return GermlineCalls(a, bytes(buf[off:off + pl]), 0, 0, 0, 0)
 
     def tuples(self, contig_names: Sequence[str]) -> List[tuple]:
         """(contig, locus, sample, (gt0, gt1), ref, alt, flags) — same shape as the oracle's rows."""
