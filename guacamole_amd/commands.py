@@ -4,39 +4,45 @@ Reference surface (paths relative to /root/reference/src/main/scala/org/hammerla
   * command registry + args       Guacamole.scala:37-77, Command.scala:33-62, Common.scala:48-136
   * germline-threshold            commands/GermlineThresholdCaller.scala:40-88
         --threshold (8), --emit-ref, --emit-no-call, + --reads/--loci/--out/--parallelism/...
-  * somatic-standard              commands/SomaticStandardCaller.scala:228-160
+  * somatic-standard              commands/SomaticStandardCaller.scala:40-160
         --tumor-reads, --normal-reads, --odds (20), --min-mapq (1), --filter-multi-allelic, ...
   * loci partitioning             DistributedUtil.scala:55-69 (--parallelism, --partition-accuracy)
 
 The per-locus work (pileupFlatMap + callVariantsAtLocus / findPotentialVariantAtLocus)
 runs in libgqpileup on the GPU; this module only loads reads, builds LociSets and
 partitions, and formats output.
+
+Launched under torch.distributed.run (WORLD_SIZE > 1) the commands run one rank per GPU:
+the reference's task partition is split into contiguous blocks of tasks per rank, each rank
+uploads the reads overlapping its tasks' loci and calls its share, and rank 0 gathers the
+records (over RCCL) and writes the output (distributed.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import sys
+import weakref
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
 from . import native, soa
+from .distributed import (assign_tasks_to_ranks, gather_germline, gather_somatic, init_from_env, rank_share,
+                          reads_overlapping)
 from .loci import (LociSet, LociSetBuilder, flatten_partitions, partition_loci_by_approximate_depth,
                    partition_loci_uniformly)
 from .reads import InputFilters, ReadSet, load_reads
 
-_UPLOADED: Dict[int, tuple] = {}
-
-
 def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
-    """Upload a ReadSet once per context and keep it resident."""
-    key = (id(ctx), id(rs))
-    hit = _UPLOADED.get(key)
-    if hit is not None and hit[0] is rs:
+    """Upload a ReadSet once per context and keep it resident for as long as the ReadSet lives
+    (the HBM copy is held by the ReadSet object itself and freed with it)."""
+    cache = rs.__dict__.setdefault("_device", {})
+    hit = cache.get(id(ctx))
+    if hit is not None and hit[0]() is ctx:
         return hit[1]
     d = ctx.upload(soa.pack(rs))
-    _UPLOADED[key] = (rs, d)
+    cache[id(ctx)] = (weakref.ref(ctx), d)
     return d
 
 
@@ -56,17 +62,23 @@ def germline_threshold_reads(ctx: native.Context, rs: ReadSet, loci, threshold: 
     return calls.tuples(rs.contig_names)
 
 
-def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet, loci, **params) -> List[dict]:
+def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet, loci, _gather=None,
+                           **params) -> Optional[List[dict]]:
     """pileupFlatMapTwoRDDs(tumor, normal, partitions, skipEmpty=true, findPotentialVariantAtLocus)
-    + the driver's filters on the GPU.  Rows as the oracle's somatic_standard (contig by name)."""
+    + the driver's filters on the GPU.  Rows as the oracle's somatic_standard (contig by name).
+    _gather: the gather device of a multi-GPU run (rank 0 gets every rank's rows, others None)."""
     if tumor.contig_names != normal.contig_names:
         raise ValueError("tumor and normal reads must share the contig list")
     calls = ctx.somatic_standard(device_reads(ctx, tumor), device_reads(ctx, normal), loci, **params)
+    per_rank = [calls] if _gather is None else gather_somatic(calls, _gather)
+    if per_rank is None:
+        return None
     rows = []
-    for r in calls.rows:
-        r = dict(r)
-        r["contig"] = tumor.contig_names[r["contig"]]
-        rows.append(r)
+    for c in per_rank:
+        for r in c.rows:
+            r = dict(r)
+            r["contig"] = tumor.contig_names[r["contig"]]
+            rows.append(r)
     return rows
 
 
@@ -112,19 +124,30 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     p.add_argument("--emit-no-call", action="store_true", help="Output no call calls.")
     _common_args(p)
     args = p.parse_args(argv)
+    rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
     rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True))
     loci = builder.result(rs.contig_lengths_map)
-    parts = partition(loci, args.parallelism, args.partition_accuracy, rs)
-    ctx = native.Context(args.device)
-    rows = germline_threshold_reads(ctx, rs, flatten_partitions(parts, rs.contig_index()), args.threshold,
-                                    args.emit_ref, args.emit_no_call)
+    parts = partition(loci, args.parallelism if args.parallelism > 0 else world, args.partition_accuracy, rs)
+    flat = flatten_partitions(parts, rs.contig_index())
+    ctx = native.Context(local if world > 1 else args.device)
+    if world > 1:
+        rr = assign_tasks_to_ranks(flat, world, [rs], len(rs.contig_names))
+        mine_rs, mine = rank_share(rs, flat, rr, rank)
+        calls = ctx.germline_threshold_device(device_reads(ctx, mine_rs), mine, args.threshold, args.emit_ref,
+                                              args.emit_no_call)
+        per_rank = gather_germline(calls, gdev)
+        if per_rank is None:
+            return _finish_rank(0)
+        rows = [t for c in per_rank for t in c.tuples(rs.contig_names)]
+    else:
+        rows = germline_threshold_reads(ctx, rs, flat, args.threshold, args.emit_ref, args.emit_no_call)
     from .output import germline_genotype
     out = [germline_genotype(c, l, rs.sample_names[s] if s < len(rs.sample_names) else "default", gt, ref, alt)
            for c, l, s, gt, ref, alt, fl in rows]
     _write_genotypes(args.out, out, rs.contig_lengths_map)
     print("Called %d genotypes." % len(out), file=sys.stderr)
-    return 0
+    return _finish_rank(0)
 
 
 def somatic_standard_main(argv: Sequence[str]) -> int:
@@ -149,6 +172,7 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     p.add_argument("--max-median-mismatches", type=int, default=2 ** 31 - 1)
     _common_args(p)
     args = p.parse_args(argv)
+    rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
     f = InputFilters.make(overlaps_loci=builder, non_duplicate=True, passed_vendor_quality_checks=True,
                           has_md_tag=True)
@@ -156,10 +180,15 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     if tumor.contig_lengths_map != normal.contig_lengths_map:
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
     loci = builder.result(normal.contig_lengths_map)
-    parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal)
-    ctx = native.Context(args.device)
+    parts = partition(loci, args.parallelism if args.parallelism > 0 else world, args.partition_accuracy, tumor, normal)
+    flat = flatten_partitions(parts, tumor.contig_index())
+    ctx = native.Context(local if world > 1 else args.device)
+    if world > 1:
+        rr = assign_tasks_to_ranks(flat, world, [tumor, normal], len(tumor.contig_names))
+        tumor, flat = rank_share(tumor, flat, rr, rank)
+        normal = normal.subset(reads_overlapping(normal, *flat[:3]))
     rows = somatic_standard_reads(
-        ctx, tumor, normal, flatten_partitions(parts, tumor.contig_index()), odds=args.odds, min_mapq=args.min_mapq,
+        ctx, tumor, normal, flat, odds=args.odds, min_mapq=args.min_mapq,
         filter_multi_allelic=int(args.filter_multi_allelic), max_read_depth=args.max_tumor_read_depth,
         min_tumor_read_depth=args.min_tumor_read_depth, max_tumor_read_depth=args.max_tumor_read_depth,
         min_normal_read_depth=args.min_normal_read_depth,
@@ -167,13 +196,26 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         min_likelihood=args.min_likelihood, min_vaf=args.min_vaf,
         min_average_mapping_quality=args.min_average_mapping_quality,
         min_average_base_quality=args.min_average_base_quality, max_median_mismatches=args.max_median_mismatches,
-        apply_filters=1)
+        apply_filters=1, _gather=gdev if world > 1 else None)
+    if rows is None:
+        return _finish_rank(0)
     from .output import somatic_genotype
     sample = tumor.sample_names[0] if tumor.sample_names else "default"
     out = [somatic_genotype(r["contig"], r, sample) for r in rows]
     _write_genotypes(args.out, out, tumor.contig_lengths_map)
     print("Called %d somatic genotypes." % len(out), file=sys.stderr)
-    return 0
+    return _finish_rank(0)
+
+
+def _finish_rank(rc: int) -> int:
+    """Leave the process group (multi-GPU runs) after every rank has finished."""
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+    return rc
 
 
 COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main}

@@ -1,12 +1,16 @@
-"""Multi-GPU driver pieces: static LociSet split across ranks + one terminal gather.
+"""Multi-GPU driver: one process per GPU, a static split of the loci tasks, one terminal gather.
 
-Loci ranges shard embarrassingly (each locus depends only on reads overlapping it,
-DistributedUtil.scala:585-597 with halfWindowSize = 0), so every rank runs the
-pileup engine on its own contiguous loci range with no data-path collective.
-The single exchange is the end-of-job gather of the per-rank genotype buffers to
-rank 0: sizes are all-gathered, then each rank's packed
-buffer goes to rank 0 over RCCL (backend "nccl" on ROCm) — or gloo on CPU tests.
-Rank 0 concatenates in rank order = partition order.
+Loci shard embarrassingly: each locus depends only on the reads overlapping it
+(DistributedUtil.scala:584-597 with halfWindowSize = 0), and the reference already runs its
+tasks independently (:621-633).  The multi-GPU driver therefore keeps the reference's own task
+partition (``--parallelism`` tasks from partitionLociUniformly / ByApproximateDepth,
+DistributedUtil.scala:55-251) and hands each rank a contiguous block of tasks, balanced by read
+count.  Every task keeps its own SlidingWindow on its rank, so a run on N GPUs gives exactly the
+records of the same task partition on one GPU.  Each rank uploads only the reads overlapping its
+tasks' loci, reads straddling a cut going to both sides (the reference's "expanded regions",
+:584-597).  There is no data-path collective: the single exchange is the end-of-job gather of
+the per-rank result buffers to rank 0 over RCCL (backend "nccl" on ROCm) — or gloo in tests —
+where they are concatenated in rank order, which is task order.
 """
 from __future__ import annotations
 
@@ -15,12 +19,31 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .loci import LociMapBuilder, LociSet, partition_loci_uniformly
+from .loci import LociSet, partition_loci_uniformly
 
 
 def rank_info() -> Tuple[int, int, int]:
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_from_env():
+    """Join the process group torch.distributed.run set up (one rank per GPU).  Returns
+    (rank, world, local GPU, gather device): the gather device is "cuda:<local>" for RCCL, or
+    "cpu" when GQ_DIST_BACKEND=gloo (ranks may then share GPUs: a rehearsal of the flow)."""
+    rank, world, local = rank_info()
+    if world == 1:
+        return rank, world, local, None
+    import torch
+    import torch.distributed as dist
+    backend = os.environ.get("GQ_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return rank, world, local, "cuda:%d" % local
+    local = local % max(1, torch.cuda.device_count())
+    dist.init_process_group(backend)
+    return rank, world, local, "cpu"
 
 
 def split_loci(loci: LociSet, world: int) -> List[LociSet]:
@@ -30,12 +53,72 @@ def split_loci(loci: LociSet, world: int) -> List[LociSet]:
     return [inv.get(r, LociSet()) for r in range(world)]
 
 
+def _starts_by_contig(read_sets, n_contigs: int):
+    out = [[] for _ in range(n_contigs)]
+    for rs in read_sets:
+        for c in range(n_contigs):
+            m = rs.contig == c
+            if m.any():
+                out[c].append(np.asarray(rs.start[m], np.int64))
+    return [np.sort(np.concatenate(x)) if x else np.zeros(0, np.int64) for x in out]
+
+
+def assign_tasks_to_ranks(flat_loci, world: int, read_sets: Sequence, n_contigs: int) -> np.ndarray:
+    """Rank of each flattened loci range (flatten_partitions order: task, contig, start): tasks in
+    contiguous blocks, cut where the running weight crosses k / world of the total.  Weight of a
+    range = reads starting in it (all read sets) + 1e-3 per locus (so empty stretches still spread)."""
+    contig, start, end, task = (np.asarray(a) for a in flat_loci)
+    n = len(task)
+    if n == 0 or world == 1:
+        return np.zeros(n, np.int64)
+    starts = _starts_by_contig(read_sets, n_contigs)
+    w = np.empty(n, np.float64)
+    for i in range(n):
+        s = starts[int(contig[i])]
+        w[i] = (np.searchsorted(s, end[i], "left") - np.searchsorted(s, start[i], "left")) + 1e-3 * (end[i] - start[i])
+    tasks = np.unique(task)
+    tw = np.zeros(len(tasks))
+    np.add.at(tw, np.searchsorted(tasks, task), w)
+    cum = np.cumsum(tw)
+    total = cum[-1] if cum[-1] > 0 else 1.0
+    rank_of_task = np.minimum(world - 1, np.floor((cum - tw / 2) * world / total)).astype(np.int64)
+    rank_of_task = np.maximum.accumulate(rank_of_task)  # contiguous blocks, rank order = task order
+    return rank_of_task[np.searchsorted(tasks, task)]
+
+
+def reads_overlapping(rs, contig, start, end) -> np.ndarray:
+    """Indices (ascending) of the reads overlapping any of the ranges (contig, [start, end)):
+    the reads the reference shuffles to those loci's tasks (DistributedUtil.scala:585-597)."""
+    contig = np.asarray(contig)
+    keep = []
+    for c in np.unique(contig):
+        m = contig == c
+        s, e = np.asarray(start, np.int64)[m], np.asarray(end, np.int64)[m]
+        o = np.argsort(s, kind="stable")
+        s, e = s[o], e[o]
+        idx = np.nonzero(rs.contig == c)[0]
+        if len(idx) == 0:
+            continue
+        rst, ren = np.asarray(rs.start[idx], np.int64), np.asarray(rs.end[idx], np.int64)
+        k = np.searchsorted(e, rst, "right")  # first range ending after the read's start
+        hit = k < len(e)
+        hit[hit] = s[k[hit]] < ren[hit]
+        keep.append(idx[hit])
+    return np.sort(np.concatenate(keep)) if keep else np.zeros(0, np.int64)
+
+
+def rank_share(rs, flat_loci, rank_of_range: np.ndarray, rank: int):
+    """(this rank's reads, its flattened loci ranges with their original task ids)."""
+    sel = rank_of_range == rank
+    loci = tuple(np.ascontiguousarray(np.asarray(a)[sel]) for a in flat_loci)
+    return rs.subset(reads_overlapping(rs, loci[0], loci[1], loci[2])), loci
+
+
 def gather_images_to_rank0(calls, device: str):
-    # device "cpu": the images are staged in host memory (a gloo rehearsal of the flow)
-    """The terminal gather of the multi-GPU bench: every rank's germline result image (left in
-    HBM by gq_germline_threshold_device) goes to rank 0's HBM with one RCCL gather over xGMI
-    (sizes all-gathered first).  Returns rank 0's list of per-rank uint8 device tensors
-    (partition order), None elsewhere."""
+    """Every rank's germline result image (left in HBM by gq_germline_threshold_device) to rank 0:
+    sizes all-gathered, then one gather over RCCL / xGMI (device "cuda:k"), or through host
+    memory with gloo (device "cpu").  Returns rank 0's list of per-rank uint8 tensors (rank
+    order), None elsewhere."""
     import ctypes as C
 
     import torch
@@ -56,7 +139,7 @@ def gather_images_to_rank0(calls, device: str):
             torch.cuda.synchronize(dev)
         hip = C.CDLL("libamdhip64.so.7")  # by SONAME: the HIP runtime already loaded in this process
         hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-        # device to device (RCCL) or device to host (a gloo rehearsal)
+        # device to device (RCCL) or device to host (gloo)
         rc = hip.hipMemcpy(C.c_void_p(mine.data_ptr()), C.c_void_p(calls.image), int(calls.image_bytes),
                            3 if on_gpu else 2)
         if rc != 0:
@@ -67,6 +150,28 @@ def gather_images_to_rank0(calls, device: str):
         return [parts[r][:sizes[r]] for r in range(world)]
     dist.gather(mine, dst=0)
     return None
+
+
+def gather_germline(calls, device: str):
+    """gather_images_to_rank0 plus each rank's record count and run counters; rank 0 gets one
+    GermlineCalls per rank (rank order), other ranks None."""
+    import torch
+    import torch.distributed as dist
+
+    from .native import GermlineCalls
+    world = dist.get_world_size()
+    meta = torch.tensor([len(calls), calls.visited_loci, calls.complex_loci, calls.ambiguous_loci, calls.tie_loci],
+                        dtype=torch.int64, device=torch.device(device))
+    metas = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta)
+    images = gather_images_to_rank0(calls, device)
+    if images is None:
+        return None
+    out = []
+    for img, m in zip(images, metas):
+        m = [int(x) for x in m.cpu().tolist()]
+        out.append(GermlineCalls.from_image(img.cpu().numpy(), m[0], *m[1:]))
+    return out
 
 
 def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[List[np.ndarray]]:
@@ -94,3 +199,10 @@ def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[L
         return [parts[r][:sizes[r]].cpu().numpy() for r in range(world)]
     dist.gather(mine, dst=0)
     return None
+
+
+def gather_somatic(calls, device: Optional[str]):
+    """Each rank's SomaticCalls (host arrays) to rank 0 (rank order), packed as raw columns."""
+    from .native import SomaticCalls
+    parts = gather_to_rank0(calls.pack(), device)
+    return None if parts is None else [SomaticCalls.unpack(p) for p in parts]

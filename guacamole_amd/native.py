@@ -95,6 +95,11 @@ SOMATIC_DEFAULTS = dict(odds=20, min_mapq=1, filter_multi_allelic=0, max_read_de
                         min_average_mapping_quality=0, min_average_base_quality=0,
                         max_median_mismatches=2 ** 31 - 1, apply_filters=1)
 
+_EVIDENCE_DTYPE = np.dtype([("likelihood", np.float64), ("read_depth", np.int32), ("allele_read_depth", np.int32),
+                            ("forward_depth", np.int32), ("allele_forward_depth", np.int32), ("mean_mq", np.float64),
+                            ("median_mq", np.float64), ("mean_bq", np.float64), ("median_bq", np.float64),
+                            ("median_mismatches", np.float64)])
+
 EVIDENCE_FIELDS = ("likelihood", "read_depth", "allele_read_depth", "forward_depth", "allele_forward_depth",
                    "mean_mq", "median_mq", "mean_bq", "median_bq", "median_mismatches")
 
@@ -359,6 +364,24 @@ class GermlineCalls:
             a[k] = np.frombuffer(buf, dtype=np.dtype(t), count=n, offset=C.cast(getattr(c, k), C.c_void_p).value - c.block_)
         return GermlineCalls(a, pool, c.visited_loci, c.complex_loci, c.ambiguous_loci, c.tie_loci)
 
+    IMAGE_FIELDS = (("contig", np.int32), ("pos", np.int64), ("ref_off", np.int64), ("alt_off", np.int64),
+                    ("ref_len", np.int32), ("alt_len", np.int32), ("sample", np.uint8), ("gt0", np.uint8),
+                    ("gt1", np.uint8), ("flags", np.uint8))
+
+    @staticmethod
+    def from_image(img: np.ndarray, n: int, visited=0, complex_loci=0, ambiguous=0, ties=0) -> "GermlineCalls":
+        """Decode a result image of n records (gqpileup.h, gq_calls_device: int64 pool_len at byte
+        0, then the arrays in IMAGE_FIELDS order and the pool, each on a 64-byte boundary from 64)."""
+        img = np.asarray(img, np.uint8)
+        al = lambda x: (x + 63) & ~63
+        off, a = 64, {}
+        for k, dt in GermlineCalls.IMAGE_FIELDS:
+            nb = n * np.dtype(dt).itemsize
+            a[k] = img[off:off + nb].view(dt).copy() if n else np.zeros(0, dt)
+            off = al(off + nb)
+        pool_len = int(img[:8].view(np.int64)[0]) if n else 0
+        return GermlineCalls(a, img[off:off + pool_len].tobytes(), visited, complex_loci, ambiguous, ties)
+
     def __len__(self) -> int:
         return int(self.a["pos"].shape[0])
 
@@ -412,4 +435,30 @@ class SomaticCalls:
 
     def __len__(self) -> int:
         return int(self.cols["pos"].shape[0])
+
+    COLS = ("contig", "pos", "sample", "ref_off", "ref_len", "alt_off", "alt_len", "log_odds", "gq", "tumor", "normal",
+            "flags")
+
+    def pack(self) -> np.ndarray:
+        """One uint8 buffer (n, pool length, visited, candidates, the columns' raw bytes, the
+        pool) for the multi-GPU gather."""
+        head = np.array([len(self), len(self.pool), self.visited_loci, self.candidate_loci], np.int64)
+        parts = [head.view(np.uint8)] + [np.ascontiguousarray(self.cols[k]).view(np.uint8).ravel() for k in self.COLS]
+        parts.append(np.frombuffer(self.pool, np.uint8))
+        return np.concatenate(parts)
+
+    @staticmethod
+    def unpack(buf: np.ndarray) -> "SomaticCalls":
+        buf = np.asarray(buf, np.uint8)
+        n, pl, visited, cands = (int(x) for x in buf[:32].view(np.int64))
+        dts = dict(contig=np.int32, pos=np.int64, sample=np.uint8, ref_off=np.int64, ref_len=np.int32,
+                   alt_off=np.int64, alt_len=np.int32, log_odds=np.float64, gq=np.int32, tumor=_EVIDENCE_DTYPE,
+                   normal=_EVIDENCE_DTYPE, flags=np.uint8)
+        off, cols = 32, {}
+        for k in SomaticCalls.COLS:
+            dt = np.dtype(dts[k])
+            nb = n * dt.itemsize
+            cols[k] = buf[off:off + nb].copy().view(dt)
+            off += nb
+        return SomaticCalls(cols, buf[off:off + pl].tobytes(), visited, cands)
 

@@ -1,0 +1,118 @@
+"""Multi-GPU driver pieces on the CPU: the task-to-rank split, the reads each rank receives
+(halo duplication, DistributedUtil.scala:584-597), the record buffers' packing and the
+world-size-2 gather over gloo."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+
+from conftest import fixture
+from guacamole_amd import native
+from guacamole_amd.distributed import assign_tasks_to_ranks, rank_share, reads_overlapping
+from guacamole_amd.loci import LociSet, flatten_partitions, partition_loci_uniformly
+from guacamole_amd.reads import InputFilters, load_reads
+
+
+def _chrm():
+    return load_reads(fixture("chrM.sorted.bam"),
+                      InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True))
+
+
+def test_tasks_to_ranks_contiguous_and_balanced():
+    rs = _chrm()
+    flat = flatten_partitions(partition_loci_uniformly(16, LociSet.parse("all").result(rs.contig_lengths_map)),
+                              rs.contig_index())
+    for world in (2, 3, 4, 8):
+        rr = assign_tasks_to_ranks(flat, world, [rs], len(rs.contig_names))
+        assert np.all(np.diff(rr) >= 0) and rr[0] == 0 and rr[-1] == world - 1
+        # ranks own whole tasks
+        for t in np.unique(flat[3]):
+            assert len(set(rr[flat[3] == t].tolist())) == 1
+        # read starts per rank within a factor 2 of the mean (16 tasks of chrM over <= 8 ranks)
+        counts = [len(rank_share(rs, flat, rr, r)[0].start) for r in range(world)]
+        assert max(counts) <= 2.2 * (sum(counts) / world), counts
+
+
+def test_reads_overlapping_is_the_halo():
+    rs = _chrm()
+    cut = 8000
+    left = reads_overlapping(rs, np.array([0]), np.array([0]), np.array([cut]))
+    right = reads_overlapping(rs, np.array([0]), np.array([cut]), np.array([16570]))
+    brute_l = np.nonzero(rs.start < cut)[0]
+    brute_r = np.nonzero(rs.end > cut)[0]
+    assert np.array_equal(left, brute_l) and np.array_equal(right, brute_r)
+    straddle = np.intersect1d(left, right)
+    assert len(straddle) > 50  # reads crossing the cut go to both sides
+    assert np.array_equal(np.union1d(left, right), np.arange(rs.n))
+
+
+def _somatic_calls(n, seed):
+    rng = np.random.default_rng(seed)
+    ev = np.zeros(n, native._EVIDENCE_DTYPE)
+    for k in native.EVIDENCE_FIELDS:
+        ev[k] = rng.integers(0, 100, n) if "depth" in k else rng.random(n)
+    cols = dict(contig=rng.integers(0, 5, n).astype(np.int32), pos=rng.integers(0, 10 ** 9, n).astype(np.int64),
+                sample=np.zeros(n, np.uint8), ref_off=(2 * np.arange(n)).astype(np.int64), ref_len=np.ones(n, np.int32),
+                alt_off=(2 * np.arange(n) + 1).astype(np.int64), alt_len=np.ones(n, np.int32),
+                log_odds=rng.random(n), gq=rng.integers(0, 99, n).astype(np.int32), tumor=ev, normal=ev.copy(),
+                flags=np.zeros(n, np.uint8))
+    return native.SomaticCalls(cols, bytes(rng.choice(list(b"ACGT"), 2 * n).tolist()), 1000 + n, 7 * n)
+
+
+def test_somatic_pack_roundtrip():
+    for n in (0, 1, 17):
+        c = _somatic_calls(n, n)
+        d = native.SomaticCalls.unpack(c.pack())
+        assert len(d) == n and d.pool == c.pool and d.visited_loci == c.visited_loci
+        assert d.rows == c.rows
+
+
+def test_germline_image_decoder():
+    """GermlineCalls.from_image reads the image layout gqpileup.h documents."""
+    n = 5
+    al = lambda x: (x + 63) & ~63
+    vals = {"contig": np.arange(n, dtype=np.int32), "pos": np.arange(n, dtype=np.int64) * 10,
+            "ref_off": np.arange(n, dtype=np.int64) * 2, "alt_off": np.arange(n, dtype=np.int64) * 2 + 1,
+            "ref_len": np.ones(n, np.int32), "alt_len": np.ones(n, np.int32), "sample": np.zeros(n, np.uint8),
+            "gt0": np.zeros(n, np.uint8), "gt1": np.ones(n, np.uint8), "flags": np.zeros(n, np.uint8)}
+    pool = b"ACGTACGTAC"
+    img = bytearray(4096)
+    img[:8] = np.array([len(pool)], np.int64).tobytes()
+    off = 64
+    for k, dt in native.GermlineCalls.IMAGE_FIELDS:
+        b = vals[k].astype(dt).tobytes()
+        img[off:off + len(b)] = b
+        off = al(off + len(b))
+    img[off:off + len(pool)] = pool
+    g = native.GermlineCalls.from_image(np.frombuffer(bytes(img), np.uint8), n)
+    rows = g.tuples(["c%d" % i for i in range(n)])
+    assert rows[3] == ("c3", 30, 0, ("Ref", "Alt"), "G", "T", 0)
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from guacamole_amd.distributed import gather_somatic
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = gather_somatic(_somatic_calls(3 + 4 * rank, rank), None)
+    if rank == 0:
+        q.put([c.rows for c in out])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_somatic_gloo_world2():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [_somatic_calls(3, 0).rows, _somatic_calls(7, 1).rows]
