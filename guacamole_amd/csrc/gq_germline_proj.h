@@ -1,0 +1,324 @@
+// gq_germline_proj.h — germline_proj: the germline-threshold pileup kernel over the read
+// projections derived at upload (ProjRec, proj, pev: gq_pileup.hip proj_count / proj_fill /
+// pev_fill).
+//
+// One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
+// (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
+// block B0 and the projection word of any read at that column sits at base + 8 * column.
+// Lanes 16g .. 16g + 15 (group g) own the 128-locus sub-span [B0 + 128g, B0 + 128g + 128) and
+// walk the reads that can overlap it, one read per group per step:
+//
+//     on  = col0 <= column < col1                         (the read covers the column)
+//     w   = buffer_load_b64(tile window, on ? base + 8 * column : out of range -> 0)
+//     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
+//     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
+//
+// (the projection holds base codes A 1, C 3, T 4, G 7 and 0 where the read has no
+// Match/Mismatch element, so neither the read's ends nor its deletions need a mask).  Counts
+// are SWAR nibbles folded into byte counters every 15 reads, in registers.  The sparse rest —
+// MD mismatch events (PileupElement.scala:108-118, Pileup.scala:157-165: the MD-derived
+// reference base), N bases, complex ranges (insertion / deletion anchors, mid-deletions,
+// N-skips) — comes from the tile's pev entries, one lane per entry, into two LDS words per
+// locus.  Then each lane makes the GermlineThreshold decision (GermlineThresholdCaller.scala:
+// 90-179) for its eight loci; variant candidates, Ref/NoCall records and complex items leave
+// as in germline_decide.  Tiles holding a read the projection cannot take, or more than 255
+// reads over one sub-span, or a read window of >= 65535 reads, go to germline_walk.
+#pragma once
+
+#include "gq_kernels.h"
+
+// (included inside gq_pileup.hip's anonymous namespace, after gq_germline_cols.h)
+
+struct ProjCfg {
+  static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
+  static constexpr int kWaves = 8;     // waves per workgroup, each on its own tiles
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kU = 5;         // reads per group per batch (all loads issued before use)
+  static constexpr int kMaxRows = 255;  // reads per group (byte counters); deeper tiles: walker
+};
+
+// Wave-aggregated reservation of n slots per lane on an LDS counter (every lane active).
+__device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n) {
+  const uint32_t x = wave_incl_scan(n);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  unsigned base = 0;
+  if ((threadIdx.x & 63) == 63 && total) base = atomicAdd(ctr, total);
+  base = (unsigned)__builtin_amdgcn_readlane((int)base, 63);
+  return base + x - n;
+}
+
+__global__ __launch_bounds__(ProjCfg::kThreads) void germline_proj(
+    const Tile *__restrict__ tiles, int64_t n_tiles, const ProjRec *__restrict__ prec,
+    const int32_t *__restrict__ pmax_end, const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev,
+    const int64_t *__restrict__ pev_off, int n_samples, int threshold, int emit_ref, int emit_no_call,
+    CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
+    int32_t *__restrict__ slow, int dbg) {
+  // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the counting loop,
+  // 2 skip the entry pass, 4 skip the decision
+  using C = ProjCfg;
+  constexpr int T = C::kT, U = C::kU;
+  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // event read bases: A C T G bytes
+  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
+  __shared__ unsigned outn[2];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint32_t *ev = evw[wave], *mk = mkw[wave];
+  {
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (threadIdx.x < 2) outn[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
+  const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
+  const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
+  LdsOut out{outn, {og.slot(0, (int)blockIdx.x, 0), og.slot(1, (int)blockIdx.x, 0)}, {og.capA[0], og.capA[1]}};
+  unsigned visited = 0, amb = 0, ties = 0;
+  const int g = lane >> 4;
+  const bool multi_sample = n_samples > 1;
+  const int64_t thr1 = (int64_t)threshold + 1;
+  const bool narrow = thr1 >= 0 && thr1 <= 1001;
+  const uint32_t thr1u = (uint32_t)thr1;
+  auto passes = [=](uint32_t count, uint32_t depth) {  // count * 100 / depth > threshold (depth > 0)
+    return narrow ? count * 100u >= thr1u * depth : (int64_t)count * 100 >= thr1 * (int64_t)depth;
+  };
+  const uint4 *prec4 = reinterpret_cast<const uint4 *>(prec);
+  for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
+    const Tile tl = tiles[i];
+    const int32_t L0 = tl.L0, L1 = tl.L1;
+    const int64_t rb = tl.rb, re = tl.re;
+    const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
+    const int32_t myc = C0 + lane;
+    // ---- the read range of each group: reads [rb + lo_g, rb + hi_g) can overlap sub-span g
+    //      (pmax_end > its first locus, start < its end); any read the projection cannot take
+    //      sends the tile to the walker
+    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+    bool bad = (re - rb) >= 65535;
+    for (int64_t q = rb; q < re && !bad; q += 64) {
+      const int64_t r = q + lane;
+      const bool v = r < re;
+      int32_t pe = 0x7FFFFFFF, c0 = 0x7FFFFFFF, c1 = 0;
+      if (v) {
+        pe = pmax_end[r];
+        const int2 cc = *reinterpret_cast<const int2 *>(prec + r);
+        c0 = cc.x;
+        c1 = cc.y;
+      }
+      bad = bad || __ballot(c1 == kProjNone) != 0;
+      lo0 += (int)__popcll(__ballot(pe <= B0));
+      lo1 += (int)__popcll(__ballot(pe <= B0 + 128));
+      lo2 += (int)__popcll(__ballot(pe <= B0 + 256));
+      lo3 += (int)__popcll(__ballot(pe <= B0 + 384));
+      hi0 += (int)__popcll(__ballot(c0 < C0 + 16));
+      hi1 += (int)__popcll(__ballot(c0 < C0 + 32));
+      hi2 += (int)__popcll(__ballot(c0 < C0 + 48));
+      hi3 += (int)__popcll(__ballot(c0 < C0 + 64));
+    }
+    const int n0 = hi0 - lo0, n1 = hi1 - lo1, n2 = hi2 - lo2, n3 = hi3 - lo3;
+    const int nmax = max(max(n0, n1), max(n2, n3));
+    if (bad || nmax > C::kMaxRows) {
+      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
+      continue;
+    }
+    if (nmax <= 0) continue;  // no reads: nothing visited
+    const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
+    const int n_me = g == 0 ? n0 : g == 1 ? n1 : g == 2 ? n2 : n3;
+    // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1])
+    uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
+    if (!(dbg & 1)) {
+      // the tile's projection window [tb, te): every read of [rb, re) lies inside
+      const uint4 pr0 = prec4[rb], pr1 = prec4[re];
+      const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
+      const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
+      const uint8_t *wp = proj + tb;
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)wp, (short)0, (int)(te - tb), 0x00020000);
+      const uint32_t K = (uint32_t)(8 * myc) - (uint32_t)tb;  // + a read's base: its word at this column
+      // the tile's read records [rb, re] through a buffer descriptor too (32-bit offsets)
+      const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(prec + rb), (short)0, (int)((re - rb + 1) * 16), 0x00020000);
+      uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
+      int nn = 0;
+      auto fold = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ca[h] += nac[h] & 0x0F0F0F0Fu;
+          cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
+          ct[h] += ntg[h] & 0x0F0F0F0Fu;
+          cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
+          nac[h] = ntg[h] = 0;
+        }
+        nn = 0;
+      };
+      const int last = lo_me + (n_me > 0 ? n_me - 1 : 0);  // record index (from rb) of the group's last read
+      for (int k0 = 0; k0 < nmax; k0 += U) {
+        uint32_t rx[U], ry[U], rz[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // every load issued (clamped index), then used
+          const auto v = __builtin_amdgcn_raw_buffer_load_b96(rrec, 16 * min(lo_me + k0 + u, last), 0, 0);
+          rx[u] = v[0];
+          ry[u] = v[1];
+          rz[u] = v[2];
+        }
+        uint32_t w0[U], w1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // the read covers this column (col0 <= myc < col1) and is one of the group's
+          const uint32_t rel = (uint32_t)(myc - (int32_t)rx[u]), span = ry[u] - rx[u];
+          const bool on = (rel < span) & (k0 + u < n_me);
+          const uint32_t voff = on ? rz[u] + K : 0x80000000u;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
+          w0[u] = w[0];
+          w1[u] = w[1];
+        }
+        if (nn + U > 15) fold();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w0[u]);
+          ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w0[u]);
+          nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w1[u]);
+          ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w1[u]);
+        }
+        nn += U;
+      }
+      fold();
+    }
+    // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
+    if (!(dbg & 2)) {
+      const int64_t e0 = pev_off[rb], e1 = pev_off[re];
+      for (int64_t q = e0; q < e1; q += 64) {
+        const int64_t k = q + lane;
+        if (k < e1) {
+          const uint2 p = pev[k];
+          const int32_t l = (int32_t)p.x;
+          if (p.y & kPevComplex) {
+            const int64_t a = max((int64_t)l, (int64_t)B0);
+            const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+            if (a < b) {
+              atomicAdd(&mk[a - B0], 1u << 16);
+              if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
+            }
+          } else if (l >= B0 && l < B0 + T) {
+            const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
+            if (m) atomicOr(&mk[l - B0], m);
+            if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
+            else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t e8[8], m8[8];
+    {
+      uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+      const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1];
+      e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // ready for the next tile
+      e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
+      m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
+    }
+    if (dbg & 4) continue;
+    // complex elements per locus: prefix of the range differences over the block
+    int32_t pc[8];
+    int32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      run += (int32_t)m8[j] >> 16;
+      pc[j] = run;
+    }
+    const int32_t exs = (int32_t)wave_incl_scan((uint32_t)run) - run;
+    // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci:
+    //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
+    uint32_t kinds = 0, nrec = 0, ncpx = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int32_t l = B0 + 8 * lane + j;
+      const bool in = l >= L0 && l < L1;
+      const int h = j >> 2, sh = 8 * (j & 3);
+      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
+      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
+      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+      const int32_t ncx_s = exs + pc[j];
+      const uint32_t ncx = ncx_s > 0 ? (uint32_t)ncx_s : 0u;
+      const uint32_t depth = cA + cC + cT + cG + nN + ncx;
+      const uint32_t ew = e8[j];
+      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
+                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+      const bool live = in && depth > 0;
+      const bool ambiguous = (mask & (mask - 1u)) != 0;
+      const uint32_t low = mask & (0u - mask);
+      const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
+      const bool to_complex = live && (ambiguous || ncx > 0 || multi_sample);
+      const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
+      const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+      const bool emit_hr = homref && (ref_pass ? emit_ref : emit_no_call);
+      const bool general = live && !to_complex && !homref;
+      visited += live ? 1u : 0u;
+      amb += (live && ambiguous) ? 1u : 0u;
+      const uint32_t kind = to_complex ? 3u : general ? 2u : emit_hr ? 1u : 0u;
+      kinds |= kind << (2 * j);
+      nrec += emit_hr ? 1u : general ? 2u : 0u;
+      ncpx += to_complex ? 1u : 0u;
+    }
+    if (__ballot(kinds != 0) == 0) continue;  // the common case: nothing to write
+    const unsigned rbase = wave_reserve_lds_n(out.lds + 0, nrec);
+    const unsigned cbase = wave_reserve_lds_n(out.lds + 1, ncpx);
+    CallRec *prec_out = recs + out.base[0];
+    unsigned kr = rbase, kc = cbase;
+    constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                                 ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t kind = (kinds >> (2 * j)) & 3u;
+      if (kind == 0) continue;
+      const int32_t pos = B0 + 8 * lane + j;
+      if (kind == 3) {
+        if (kc < out.cap[1]) cplx[out.base[1] + kc] = ComplexItem{(int32_t)i, pos, 0};
+        ++kc;
+        continue;
+      }
+      const int h = j >> 2, sh = 8 * (j & 3);
+      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
+      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
+      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+      const uint32_t ew = e8[j];
+      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
+                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+      const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+      const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - L0));
+      CallRec rr;
+      rr.key = ord << 12;
+      rr.contig = tl.contig;
+      rr.pos = pos;
+      rr.sample = 0;
+      if (kind == 1) {
+        const uint32_t depth = cA + cC + cT + cG + nN;
+        const uint32_t low = mask & (0u - mask);
+        const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
+        const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+        rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
+        rr.flags = 0;
+        rr.ref_len = 1;
+        rr.alt_len = 5;
+        rr.allele = (uint64_t)ref | kAltSym;
+        if (kr < out.cap[0]) prec_out[kr] = rr;
+        ++kr;
+      } else {
+        // a variant candidate: counts in a placeholder record pair, expanded by germline_expand
+        rr.gt0 = ref;
+        rr.gt1 = 0;
+        rr.flags = kCandidate;
+        rr.ref_len = (uint16_t)nN;
+        rr.alt_len = 0;
+        rr.allele = (uint64_t)cA | ((uint64_t)cC << 16) | ((uint64_t)cT << 32) | ((uint64_t)cG << 48);
+        if (kr < out.cap[0]) prec_out[kr] = rr;
+        rr.flags = kCandidateSlot;
+        if (kr + 1 < out.cap[0]) prec_out[kr + 1] = rr;
+        kr += 2;
+      }
+    }
+  }
+  add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
+  if (threadIdx.x == 0) {  // this workgroup's partition counts (may exceed the capacity: host retry)
+    ctr->part[0][blockIdx.x] = outn[0];
+    ctr->part[1][blockIdx.x] = outn[1];
+  }
+}

@@ -142,6 +142,7 @@ struct Plan {
   int64_t n_tiles = 0;
   int64_t n_loci = 0;
   int T = 0;
+  bool aligned = false;  // tiles are pieces of T-aligned locus blocks (germline_proj)
   // the non-empty loci ranges in call order (host copies): contig, [start, end), first tile,
   // task, and the window each belongs to.  A window = a maximal run of ranges of one (task,
   // contig): one SlidingWindow per task and contig (DistributedUtil.scala:473-486).
@@ -155,7 +156,10 @@ struct Plan {
   int64_t range_of_tile(int64_t t) const {  // last range whose first tile <= t
     return (int64_t)(std::upper_bound(rt.begin(), rt.end(), t) - rt.begin()) - 1;
   }
-  int64_t tiles_of(int64_t r) const { return (re[(size_t)r] - rs[(size_t)r] + T - 1) / T; }
+  int64_t tiles_of(int64_t r) const {
+    const int64_t s = rs[(size_t)r], e = re[(size_t)r];
+    return aligned ? (e - 1) / T - s / T + 1 : (e - s + T - 1) / T;
+  }
 };
 
 // A locus whose pileup reference base depends on the queue's heap order (the reads' MD tags
@@ -199,6 +203,7 @@ struct gq_ctx {
   gq_timings timings{};
   int germ_tile = gq::kGermT;
   int n_cu = 0;
+  int proj_wg_per_cu = 0;  // resident germline_proj workgroups per CU (occupancy query, once)
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
@@ -211,12 +216,13 @@ struct gq_dev_reads {
   std::vector<int64_t> contig_read_begin;  // host copy
   std::vector<void *> owned;               // device allocations owned by this handle
   int64_t seq_bytes = 0;
+  int64_t proj_bytes = 0, pev_count = 0;  // germline projection pool sizes (derive_shape)
 };
 
 namespace gq {
 // Loci ranges -> locus tiles of T loci with each tile's read window in `rd`, written to `tiles`.
 gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,
-               int stage_cap = 0, int meta_cap = 0, int ev_cap = 0);
+               int stage_cap = 0, int meta_cap = 0, int ev_cap = 0, bool aligned = false);
 gq_status check_device_error(gq_ctx *c, const Counters &h);
 // Pileup.referenceBaseAtLocus in the reference's heap order at each listed locus, for each of
 // the read sets (advanced together, as the somatic caller's two windows are): the queues are

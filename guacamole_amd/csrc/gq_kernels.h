@@ -52,7 +52,34 @@ struct DevReads {
   const struct ColDesc *cdesc;  // one per read
   const uint32_t *cev;          // per read: MD events (offset << 16 | MD base << 8 | read base), segments
   const int64_t *caux_off;      // n_reads + 1 offsets into cev
+  // derived at upload for the germline projection kernel (germline_proj, see ProjRec)
+  const struct ProjRec *prec;   // n_reads + 1 (the last: end of the projection pool)
+  const uint8_t *proj;          // locus-aligned base codes, 8 loci per word
+  const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
+  const int64_t *pev_off;       // n_reads + 1 offsets into pev
 };
+
+// Per-read record of the germline projection kernel (16 bytes).  The read's projection is
+// the words of 8 loci [8 * col0, 8 * col1) at byte offset base + 8 * col in `proj`: one byte
+// per locus, the read's base there as a code (A 1, C 3, T 4, G 7: ASCII & 7) where the
+// element is a Match/Mismatch (PileupElement.scala:68-135), 0 elsewhere (outside the read,
+// deleted / skipped loci, insertion and deletion anchors, N bases).  col1 = kProjNone marks a
+// read the projection path cannot take (bases other than A C G T N, no MD tag, a P op ...).
+struct ProjRec {
+  int32_t col0, col1;
+  int64_t base;
+};
+static_assert(sizeof(ProjRec) == 16, "ProjRec layout");
+constexpr int32_t kProjNone = (int32_t)0x80000000;
+// Sparse entries of a read (uint2 {x = locus, y}), in any order:
+//   y bit 31 clear: MD event / N base at locus x: bits 0-3 the MD reference base's std_bit
+//     (0 for an N base without an MD event), bits 4-6 the read base's category there (0-3 A C
+//     T G: a Match/Mismatch element carrying an MD event; 4: an N base; 7: none, e.g. an event
+//     on a deleted base);
+//   y bit 31 set: loci [x, x + (y & 0x7FFFFFFF)) hold complex elements (insertion / deletion
+//     anchors, mid-deletions, clipped N-skips): the exact kernel decides them.
+constexpr uint32_t kPevComplex = 0x80000000u;
+constexpr uint32_t kPevNone = 7u << 4;  // a padding entry (no effect)
 
 // Packed per-read record of the germline column kernel (24 bytes, DMA'd into LDS per tile).
 struct ColDesc {

@@ -59,7 +59,8 @@ namespace {
 __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *__restrict__ r_start,
                            const int64_t *__restrict__ r_end, const int64_t *__restrict__ r_ord,
                            const int64_t *__restrict__ r_tile0, int64_t n_ranges, int64_t n_tiles, int T,
-                           DevReads R, Tile *__restrict__ tiles, int stage_cap, int meta_cap, int ev_cap) {
+                           DevReads R, Tile *__restrict__ tiles, int stage_cap, int meta_cap, int ev_cap,
+                           int aligned) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tiles) return;
   int64_t lo = 0, hi = n_ranges - 1;  // largest r with r_tile0[r] <= t
@@ -69,8 +70,10 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
     else hi = mid - 1;
   }
   const int64_t r = lo;
-  const int64_t L0 = r_start[r] + (t - r_tile0[r]) * (int64_t)T;
-  const int64_t L1 = min(L0 + (int64_t)T, r_end[r]);
+  // aligned: tiles are the range's pieces of the T-aligned blocks it meets (T a power of two)
+  const int64_t blk = (r_start[r] / T + (t - r_tile0[r])) * (int64_t)T;
+  const int64_t L0 = aligned ? max(r_start[r], blk) : r_start[r] + (t - r_tile0[r]) * (int64_t)T;
+  const int64_t L1 = aligned ? min(blk + (int64_t)T, r_end[r]) : min(L0 + (int64_t)T, r_end[r]);
   const int32_t c = r_contig[r];
   int64_t b = R.contig_read_begin[c], e = R.contig_read_begin[c + 1];
   // rb: first read with pmax_end > L0 (pmax_end non-decreasing within the contig)
@@ -230,6 +233,144 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
   }
 }
 
+// ---- Projections (germline_proj, ProjRec in gq_kernels.h), derived after col_derive -------
+__device__ __forceinline__ uint32_t proj_code(uint8_t b) {  // A 1, C 3, T 4, G 7; N and the rest 0
+  return (b == 'A' || b == 'C' || b == 'G' || b == 'T') ? (uint32_t)(b & 7u) : 0u;
+}
+__device__ __forceinline__ bool proj_ok(uint32_t info) { return (info & (kColEligible | kColGeneral)) != 0; }
+
+// Words (8-locus columns) and sparse entries of each read's projection; entry n is 0.
+__global__ void proj_count(DevReads R, const uint32_t *__restrict__ n_nbase, int64_t *__restrict__ nwords,
+                           int64_t *__restrict__ nents) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R.n_reads) return;
+  int64_t w = 0, e = 0;
+  if (r < R.n_reads) {
+    const ColDesc d = R.cdesc[r];
+    if (proj_ok(d.info)) {
+      w = (int64_t)((d.end + 7) >> 3) - (int64_t)(d.start >> 3);
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+      e = nmd + (int64_t)n_nbase[r];
+      if (d.info & kColGeneral) {
+        const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+        const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+        for (int32_t q = 0; q < nseg; ++q) e += (sg[2 * q + 1] >> 16) != kSegCount ? 1 : 0;
+      }
+    }
+  }
+  nwords[r] = w;
+  nents[r] = e;
+}
+
+// ProjRec of each read from the word offsets; record n closes the pool.
+__global__ void prec_fill(DevReads R, const int64_t *__restrict__ woff, ProjRec *__restrict__ prec) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R.n_reads) return;
+  ProjRec p;
+  if (r == R.n_reads) {
+    p.col0 = p.col1 = 0;
+    p.base = 8 * woff[r];
+  } else {
+    const ColDesc d = R.cdesc[r];
+    p.col0 = d.start >> 3;
+    p.col1 = proj_ok(d.info) ? (d.end + 7) >> 3 : kProjNone;
+    p.base = 8 * woff[r] - 8 * (int64_t)p.col0;
+  }
+  prec[r] = p;
+}
+
+// The projection words of 256 reads per block (thread per word, coalesced in the pool).
+__global__ __launch_bounds__(256) void proj_fill(DevReads R, const int64_t *__restrict__ woff,
+                                                 uint8_t *__restrict__ proj) {
+  __shared__ int64_t wb[257];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int t = threadIdx.x;
+  const int64_t w0 = woff[r0];
+  wb[t] = woff[min(r0 + t, R.n_reads)] - w0;
+  if (t == 0) wb[256] = woff[min(r0 + 256, R.n_reads)] - w0;
+  __syncthreads();
+  const int64_t W = wb[256];
+  for (int64_t w = t; w < W; w += 256) {
+    int lo = 0, hi = 255;  // the last read whose words start at or before w
+    while (lo < hi) {
+      const int m = (lo + hi + 1) >> 1;
+      if (wb[m] <= w) lo = m;
+      else hi = m - 1;
+    }
+    const int64_t r = r0 + lo, j = w - wb[lo];
+    const ColDesc d = R.cdesc[r];
+    const int32_t s = d.start, e = d.end;
+    const int32_t lb = 8 * ((s >> 3) + (int32_t)j);  // locus of byte 0
+    uint32_t v[2] = {0, 0};
+    if (d.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base seq_lo + (l - s)
+      const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int32_t l = lb + q;
+        if (l >= s && l < e) v[q >> 2] |= proj_code(R.seq[p0 + l]) << (8 * (q & 3));
+      }
+    } else {  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu), nseg = (int32_t)((d.info >> 18) & 0xFFu);
+      const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+      const int64_t so = R.seq_off[r];
+      for (int32_t q2 = 0; q2 < nseg; ++q2) {
+        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+        if ((b >> 16) != kSegCount) continue;
+        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
+        for (int q = 0; q < 8; ++q) {
+          const int32_t l = lb + q;
+          if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
+        }
+      }
+    }
+    *reinterpret_cast<uint2 *>(proj + 8 * (w0 + w)) = make_uint2(v[0], v[1]);
+  }
+}
+
+// The sparse entries of each read (thread per read): MD events, N bases (without an event),
+// complex segments; unused slots of the N bound are padding.
+__global__ void pev_fill(DevReads R, const int64_t *__restrict__ eoff, uint2 *__restrict__ pev) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const ColDesc d = R.cdesc[r];
+  if (!proj_ok(d.info)) return;
+  int64_t o = eoff[r];
+  const int64_t o1 = eoff[r + 1];
+  const int32_t s = d.start, nmd = (int32_t)(d.info & 0xFFFFu);
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  const uint8_t *evb = R.ev_rb + R.md_off[r];
+  for (int32_t k = 0; k < nmd; ++k) {
+    const uint32_t x = ev[k];
+    const uint8_t rb = evb[k];
+    const int c = rb == 0 ? 7 : base_cat(rb);
+    pev[o++] = make_uint2((uint32_t)(s + (int32_t)(x >> 8)), std_bit((uint8_t)(x & 0xFFu)) | ((uint32_t)(c <= 4 ? c : 7) << 4));
+  }
+  // N bases of the Match/Mismatch elements that carry no MD event (an event entry counts those)
+  auto n_run = [&](int32_t ra, int32_t len, int64_t p) {  // loci [ra, ra + len) at pool offset p
+    int32_t k = 0;
+    for (int32_t i = 0; i < len && o < o1; ++i) {
+      if (R.seq[p + i] != 'N') continue;
+      const int32_t off = ra + i - s;
+      while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
+      if (k < nmd && (int32_t)(ev[k] >> 8) == off) continue;
+      pev[o++] = make_uint2((uint32_t)(ra + i), 4u << 4);
+    }
+  };
+  if (d.info & kColGeneral) {
+    const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+    for (int32_t q = 0; q < nseg; ++q) {
+      const uint32_t a = sg[2 * q], b = sg[2 * q + 1];
+      const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
+      if ((b >> 16) != kSegCount) pev[o++] = make_uint2((uint32_t)ra, kPevComplex | (uint32_t)rl);
+      else if (o < o1) n_run(ra, rl, R.seq_off[r] + (int32_t)(b & 0xFFFFu));
+    }
+  } else if (o < o1) {
+    n_run(s, d.end - s, R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0));
+  }
+  for (; o < o1; ++o) pev[o] = make_uint2(0x80000000u, kPevNone);
+}
+
 // Upload-time checks, one thread per read (bits of *bad): 1 = reads not sorted by start within
 // their contig, or pmax_end not the running maximum of end (SlidingWindow.scala:55-56 "Regions
 // must be sorted"; plan_tiles binary-searches both); 2 = an offset / length outside its pool or
@@ -260,7 +401,7 @@ __global__ void validate_reads(DevReads R, int *__restrict__ bad) {
 // clean[r] = every sequenced byte of read r is one of A C G T N (the germline column path's
 // precondition).  Pool in read order: 16 bytes per thread, coalesced; the rare other bytes
 // find their read by binary search of seq_off and clear its flag (clean preset to 1).
-__global__ void pool_clean(DevReads R, uint8_t *__restrict__ clean) {
+__global__ void pool_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__restrict__ n_nbase) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte chunk
   const int64_t b0 = c * 16;
   if (b0 >= R.seq_bytes) return;
@@ -274,29 +415,36 @@ __global__ void pool_clean(DevReads R, uint8_t *__restrict__ clean) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const uint8_t x = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
-    if (b0 + k >= R.seq_bytes || x == 'A' || x == 'C' || x == 'G' || x == 'T' || x == 'N') continue;
+    if (b0 + k >= R.seq_bytes || x == 'A' || x == 'C' || x == 'G' || x == 'T') continue;
     int64_t lo = 0, hi = R.n_reads - 1;  // last read with seq_off <= b0 + k
     while (lo < hi) {
       const int64_t m = (lo + hi + 1) >> 1;
       if (R.seq_off[m] <= b0 + k) lo = m;
       else hi = m - 1;
     }
-    // zero-length reads share an offset with their neighbour: clear every read holding the byte
+    // zero-length reads share an offset with their neighbour: every read holding the byte.
+    // An N keeps the read clean and is counted (the projection's N-base entries).
     for (int64_t r = lo; r >= 0 && R.seq_off[r] + R.seq_len[r] > b0 + k; --r)
-      if (R.seq_off[r] <= b0 + k) clean[r] = 0;
+      if (R.seq_off[r] <= b0 + k) {
+        if (x == 'N') atomicAdd(&n_nbase[r], 1u);
+        else clean[r] = 0;
+      }
   }
 }
 // The same per read (a wrapped pool in another order), one thread per read.
-__global__ void read_clean(DevReads R, uint8_t *__restrict__ clean) {
+__global__ void read_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__restrict__ n_nbase) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
   const uint8_t *q = R.seq + R.seq_off[r];
   bool ok = true;
+  uint32_t nn = 0;
   for (int32_t k = 0; k < R.seq_len[r]; ++k) {
     const uint8_t b = q[k];
     ok = ok && (b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'N');
+    nn += b == 'N' ? 1u : 0u;
   }
   clean[r] = ok ? 1 : 0;
+  n_nbase[r] = nn;
 }
 
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
@@ -363,6 +511,7 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ------------------------------------------------------------------------------------------
 
 #include "gq_germline_cols.h"
+#include "gq_germline_proj.h"
 
 // ------------------------------------------------------------------------------------------
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
@@ -983,6 +1132,9 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   d->d.lead = (const int16_t *)p;
   d->d.ev_rb = (const uint8_t *)q;
   int unordered = 0;
+  void *nnb = nullptr;  // N bytes per read (pool_clean / read_clean), for the projection entries
+  HIP_TRY(hipMalloc(&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
+  HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1), c->stream));
   if (d->d.n_reads > 0) {
     void *flag = nullptr;
     HIP_TRY(hipMalloc(&flag, sizeof(int)));
@@ -1007,9 +1159,9 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       const int64_t chunks = (d->d.seq_bytes + 15) / 16;
       if (chunks > 0)
         hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                           d->d, (uint8_t *)cl);
+                           d->d, (uint8_t *)cl, (uint32_t *)nnb);
     } else {
-      hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl);
+      hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl, (uint32_t *)nnb);
     }
     HIP_TRY(hipGetLastError());
   }
@@ -1048,7 +1200,52 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       HIP_TRY(hipGetLastError());
     }
   }
+  {  // projections (germline_proj): per-read word / entry counts, offsets, records, pools
+    const int64_t n = d->d.n_reads;
+    void *cnt = nullptr, *off = nullptr, *tmp = nullptr, *pr = nullptr, *pj = nullptr, *pe = nullptr;
+    HIP_TRY(hipMalloc(&cnt, sizeof(int64_t) * 2 * (size_t)(n + 1)));
+    HIP_TRY(hipMalloc(&off, sizeof(int64_t) * 2 * (size_t)(n + 1)));
+    d->owned.push_back(off);
+    int64_t *nw = (int64_t *)cnt, *ne = nw + (n + 1), *wo = (int64_t *)off, *eo = wo + (n + 1);
+    const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, nw, ne);
+    HIP_TRY(hipGetLastError());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nw, wo, (int)(n + 1), c->stream));
+    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nw, wo, (int)(n + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ne, eo, (int)(n + 1), c->stream));
+    int64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], wo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tot[1], eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(tmp);
+    (void)hipFree(cnt);
+    HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
+    d->owned.push_back(pr);
+    HIP_TRY(hipMalloc(&pj, (size_t)(8 * tot[0] + 16)));
+    d->owned.push_back(pj);
+    HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
+    d->owned.push_back(pe);
+    hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const int64_t *)wo, (ProjRec *)pr);
+    HIP_TRY(hipGetLastError());
+    if (n > 0) {
+      hipLaunchKernelGGL(proj_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->d,
+                         (const int64_t *)wo, (uint8_t *)pj);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (const int64_t *)eo, (uint2 *)pe);
+      HIP_TRY(hipGetLastError());
+    }
+    d->d.prec = (const ProjRec *)pr;
+    d->d.proj = (const uint8_t *)pj;
+    d->d.pev = (const uint2 *)pe;
+    d->d.pev_off = (const int64_t *)eo;
+    d->proj_bytes = 8 * tot[0];
+    d->pev_count = tot[1];
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(nnb);
   d->d.pool_ordered = unordered ? 0 : 1;
   return GQ_OK;
 }
@@ -1210,11 +1407,12 @@ void gq_reads_free(gq_dev_reads *d) {
 
 // ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
 gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles_buf,
-                   int stage_cap, int meta_cap, int ev_cap) {
+                   int stage_cap, int meta_cap, int ev_cap, bool aligned) {
   if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
   const int64_t R = loci->n_ranges;
   pl = Plan{};
   pl.T = T;
+  pl.aligned = aligned;
   std::vector<int32_t> &rc = pl.rc;
   std::vector<int64_t> &rs = pl.rs, &re = pl.re, &rt = pl.rt, ro;
   int64_t ord = 0, tiles = 0;
@@ -1241,7 +1439,7 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
     ro.push_back(ord);
     rt.push_back(tiles);
     ord += e - s;
-    tiles += (e - s + T - 1) / T;
+    tiles += aligned ? (e - 1) / T - s / T + 1 : (e - s + T - 1) / T;
   }
   pl.n_tiles = tiles;
   pl.n_loci = ord;
@@ -1261,7 +1459,7 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   HIP_TRY(tiles_buf.ensure((size_t)tiles * sizeof(Tile)));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
-                     tiles, T, rd->d, (Tile *)tiles_buf.p, stage_cap, meta_cap, ev_cap);
+                     tiles, T, rd->d, (Tile *)tiles_buf.p, stage_cap, meta_cap, ev_cap, aligned ? 1 : 0);
   HIP_TRY(hipGetLastError());
   return GQ_OK;
 }
@@ -1279,20 +1477,42 @@ gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
 
 extern "C" {
 
+// GQ_GERM=cols: the LDS-staged column kernel of round 1 (diagnostics / A-B); default: germline_proj
+static bool germline_use_proj() {
+  static const bool proj = !(getenv("GQ_GERM") && strcmp(getenv("GQ_GERM"), "cols") == 0);
+  return proj;
+}
+
 static unsigned germline_grid(gq_ctx *c, int64_t tiles) {
   if (c->n_cu <= 0 && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
     c->n_cu = 256;
-  // persistent: two workgroups per CU (LDS-bound), each over a contiguous run of tiles
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>({tiles, 2 * (int64_t)c->n_cu, (int64_t)kPartsCols}));
+  if (!germline_use_proj())  // persistent: two workgroups per CU (LDS-bound), each over a contiguous run of tiles
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>({tiles, 2 * (int64_t)c->n_cu, (int64_t)kPartsCols}));
+  // persistent: every resident workgroup (8 waves, a tile per wave at a time) over a contiguous run
+  if (c->proj_wg_per_cu <= 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, germline_proj, ProjCfg::kThreads, 0) != hipSuccess || nb <= 0)
+      nb = 2;
+    c->proj_wg_per_cu = nb;
+  }
+  const int64_t want = (tiles + ProjCfg::kWaves - 1) / ProjCfg::kWaves;
+  return (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>({want, (int64_t)c->proj_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
 }
 
 static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p,
                                  CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr) {
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
-  hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,
-                     (const Tile *)c->tiles.p, tiles, R.seq, R.cdesc, R.cev, R.n_samples, p->threshold, p->emit_ref,
-                     p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
+  if (germline_use_proj()) {
+    hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, tiles, R.prec, R.pmax_end, R.proj, R.pev, R.pev_off, R.n_samples,
+                       p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
+  } else {
+    hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, tiles, R.seq, R.cdesc, R.cev, R.n_samples, p->threshold,
+                       p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // column kernel | walker kernel
   const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
@@ -1315,7 +1535,8 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = plan(c, rd, loci, T, pl, c->tiles, ColsCfg::kStage, ColsCfg::kMeta, ColsCfg::kEv);
+  gq_status st = germline_use_proj() ? plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true)
+                                      : plan(c, rd, loci, T, pl, c->tiles, ColsCfg::kStage, ColsCfg::kMeta, ColsCfg::kEv);
   if (st) return st;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
