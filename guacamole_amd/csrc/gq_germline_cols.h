@@ -799,7 +799,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   constexpr int S = T + 2 * kGuard;
   __shared__ __attribute__((aligned(16))) uint32_t cnt[W_N * S];
   const int64_t n = (int64_t)ctr->n_slow;
-  const int part = kPartsCols + (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kPartsCols - 1));
+  const int part = kPartsCols + (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kPartsWalk - 1));
   GlobalOut out{ctr, part, {og.slot(0, part, 0), og.slot(1, part, 0)}, {og.capB[0], og.capB[1]}};
   unsigned visited = 0, amb = 0, ties = 0;
   for (int64_t q = blockIdx.x; q < n; q += gridDim.x) {

@@ -29,12 +29,24 @@
 
 // (included inside gq_pileup.hip's anonymous namespace, after gq_germline_cols.h)
 
+#ifndef GQ_PROJ_U
+#define GQ_PROJ_U 5
+#endif
+#ifndef GQ_PROJ_WPE
+#define GQ_PROJ_WPE 5  // waves per SIMD the register budget must allow
+#endif
+#ifndef GQ_PROJ_WAVES
+#define GQ_PROJ_WAVES 4
+#endif
 struct ProjCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
-  static constexpr int kWaves = 8;     // waves per workgroup, each on its own tiles
+  static constexpr int kWaves = GQ_PROJ_WAVES;  // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kU = 5;         // reads per group per batch (all loads issued before use)
+  static constexpr int kU = GQ_PROJ_U;  // reads per group per batch (all loads issued before use)
   static constexpr int kMaxRows = 255;  // reads per group (byte counters); deeper tiles: walker
+  static constexpr int kRecCap = 256;   // reads per tile window (LDS records); more: walker
+  static constexpr int kRecBuf = kRecCap + 1;  // + one padding record
+  static constexpr int kEnt = 6;  // sparse entries per lane loaded with the records (the rest: a loop)
 };
 
 // Wave-aggregated reservation of n slots per lane on an LDS counter (every lane active).
@@ -47,22 +59,24 @@ __device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n
   return base + x - n;
 }
 
-__global__ __launch_bounds__(ProjCfg::kThreads) void germline_proj(
+__global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_PROJ_WPE))) void germline_proj(
     const Tile *__restrict__ tiles, int64_t n_tiles, const ProjRec *__restrict__ prec,
     const int32_t *__restrict__ pmax_end, const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev,
     const int64_t *__restrict__ pev_off, int n_samples, int threshold, int emit_ref, int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
-  // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the counting loop,
-  // 2 skip the entry pass, 4 skip the decision
+  // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the projection loads,
+  // 2 skip the sparse entries, 4 skip the decision
   using C = ProjCfg;
   constexpr int T = C::kT, U = C::kU;
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // event read bases: A C T G bytes
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
+  __shared__ __attribute__((aligned(16))) uint2 recw[C::kWaves][C::kRecBuf];  // the tile's read records
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave];
+  uint2 *rec = recw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
@@ -74,6 +88,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) void germline_proj(
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
   LdsOut out{outn, {og.slot(0, (int)blockIdx.x, 0), og.slot(1, (int)blockIdx.x, 0)}, {og.capA[0], og.capA[1]}};
   unsigned visited = 0, amb = 0, ties = 0;
+  uint64_t clk[6] = {0, 0, 0, 0, 0, 0};
   const int g = lane >> 4;
   const bool multi_sample = n_samples > 1;
   const int64_t thr1 = (int64_t)threshold + 1;
@@ -84,238 +99,282 @@ __global__ __launch_bounds__(ProjCfg::kThreads) void germline_proj(
   };
   const uint4 *prec4 = reinterpret_cast<const uint4 *>(prec);
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
+    const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const Tile tl = tiles[i];
     const int32_t L0 = tl.L0, L1 = tl.L1;
     const int64_t rb = tl.rb, re = tl.re;
     const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
     const int32_t myc = C0 + lane;
     // ---- the read range of each group: reads [rb + lo_g, rb + hi_g) can overlap sub-span g
-    //      (pmax_end > its first locus, start < its end); any read the projection cannot take
-    //      sends the tile to the walker
-    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
-    bool bad = (re - rb) >= 65535;
-    for (int64_t q = rb; q < re && !bad; q += 64) {
-      const int64_t r = q + lane;
-      const bool v = r < re;
-      int32_t pe = 0x7FFFFFFF, c0 = 0x7FFFFFFF, c1 = 0;
-      if (v) {
-        pe = pmax_end[r];
-        const int2 cc = *reinterpret_cast<const int2 *>(prec + r);
-        c0 = cc.x;
-        c1 = cc.y;
+    //      (pmax_end > its first locus, start < its end).  The window's read records go to
+    //      LDS as {col0 - C0 (16 bits) | span << 16, word offset of column C0 in the tile's
+    //      projection window}.  A read the projection cannot take, or a window of more than
+    //      kRecCap reads, sends the tile to the walker.  The window's records and the first
+    //      kEnt sparse entries per lane are loaded together, before any is used.
+    const int64_t nwin = re - rb;
+    if (nwin > C::kRecCap) {
+      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
+      continue;
+    }
+    if (nwin <= 0) continue;  // no reads: nothing visited
+    const int nrd = (int)nwin;
+    const uint4 pr0 = prec4[rb], pr1 = prec4[re];
+    const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
+    const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
+    const int64_t e0 = pev_off[rb], e1 = pev_off[re];
+    const uint32_t ybias = (uint32_t)(8 * C0) - (uint32_t)tb;
+    constexpr int NQ = C::kRecCap / 64, NE = C::kEnt;
+    int32_t pe[NQ];
+    uint4 pp[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      pe[q] = 0x7FFFFFFF;
+      pp[q] = make_uint4(0x7FFFFFFFu, 0u, 0u, 0u);
+      if (64 * q + lane < nrd) {
+        pe[q] = pmax_end[rb + 64 * q + lane];
+        pp[q] = prec4[rb + 64 * q + lane];
       }
-      bad = bad || __ballot(c1 == kProjNone) != 0;
-      lo0 += (int)__popcll(__ballot(pe <= B0));
-      lo1 += (int)__popcll(__ballot(pe <= B0 + 128));
-      lo2 += (int)__popcll(__ballot(pe <= B0 + 256));
-      lo3 += (int)__popcll(__ballot(pe <= B0 + 384));
+    }
+    uint2 ent[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int64_t k = e0 + 64 * j + lane;
+      ent[j] = make_uint2(0x80000000u, kPevNone);
+      if (!(dbg & 2) && k < e1) ent[j] = pev[k];
+    }
+    bool bad = false;
+    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (64 * q >= nrd) break;
+      const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
+      if (64 * q + lane < nrd)
+        rec[64 * q + lane] = make_uint2((uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16), pp[q].z + ybias);
+      bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
+      lo0 += (int)__popcll(__ballot(pe[q] <= B0));
+      lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
+      lo2 += (int)__popcll(__ballot(pe[q] <= B0 + 256));
+      lo3 += (int)__popcll(__ballot(pe[q] <= B0 + 384));
       hi0 += (int)__popcll(__ballot(c0 < C0 + 16));
       hi1 += (int)__popcll(__ballot(c0 < C0 + 32));
       hi2 += (int)__popcll(__ballot(c0 < C0 + 48));
       hi3 += (int)__popcll(__ballot(c0 < C0 + 64));
     }
-    const int n0 = hi0 - lo0, n1 = hi1 - lo1, n2 = hi2 - lo2, n3 = hi3 - lo3;
-    const int nmax = max(max(n0, n1), max(n2, n3));
+    const int nmax = max(max(hi0 - lo0, hi1 - lo1), max(hi2 - lo2, hi3 - lo3));
     if (bad || nmax > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
     }
-    if (nmax <= 0) continue;  // no reads: nothing visited
+    const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
-    const int n_me = g == 0 ? n0 : g == 1 ? n1 : g == 2 ? n2 : n3;
-    // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1])
+    const int hi_me = g == 0 ? hi0 : g == 1 ? hi1 : g == 2 ? hi2 : hi3;
+    // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]).
+    //      Group g reads records lo_g, lo_g + 1, ..., clamped to hi_g: a read starting at or
+    //      after the sub-span's end (start-sorted), which covers none of its columns, or the
+    //      padding record (span 0) at the window's end.  Two batches of loads stay in flight
+    //      while a third is counted; the sparse entries are applied while the first two land.
+    if (lane == 0) rec[nrd] = make_uint2(0u, 0u);
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
-    if (!(dbg & 1)) {
-      // the tile's projection window [tb, te): every read of [rb, re) lies inside
-      const uint4 pr0 = prec4[rb], pr1 = prec4[re];
-      const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
-      const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
-      const uint8_t *wp = proj + tb;
-      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)wp, (short)0, (int)(te - tb), 0x00020000);
-      const uint32_t K = (uint32_t)(8 * myc) - (uint32_t)tb;  // + a read's base: its word at this column
-      // the tile's read records [rb, re] through a buffer descriptor too (32-bit offsets)
-      const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(prec + rb), (short)0, (int)((re - rb + 1) * 16), 0x00020000);
-      uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
-      int nn = 0;
-      auto fold = [&]() {
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(proj + tb), (short)0, (int)(te - tb), 0x00020000);
+    const uint32_t l8 = 8u * (uint32_t)lane;
+    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
+    int nn = 0;
+    auto fold = [&]() {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          ca[h] += nac[h] & 0x0F0F0F0Fu;
-          cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
-          ct[h] += ntg[h] & 0x0F0F0F0Fu;
-          cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
-          nac[h] = ntg[h] = 0;
-        }
-        nn = 0;
-      };
-      const int last = lo_me + (n_me > 0 ? n_me - 1 : 0);  // record index (from rb) of the group's last read
-      for (int k0 = 0; k0 < nmax; k0 += U) {
-        uint32_t rx[U], ry[U], rz[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // every load issued (clamped index), then used
-          const auto v = __builtin_amdgcn_raw_buffer_load_b96(rrec, 16 * min(lo_me + k0 + u, last), 0, 0);
-          rx[u] = v[0];
-          ry[u] = v[1];
-          rz[u] = v[2];
-        }
-        uint32_t w0[U], w1[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          // the read covers this column (col0 <= myc < col1) and is one of the group's
-          const uint32_t rel = (uint32_t)(myc - (int32_t)rx[u]), span = ry[u] - rx[u];
-          const bool on = (rel < span) & (k0 + u < n_me);
-          const uint32_t voff = on ? rz[u] + K : 0x80000000u;
-          const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
-          w0[u] = w[0];
-          w1[u] = w[1];
-        }
-        if (nn + U > 15) fold();
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w0[u]);
-          ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w0[u]);
-          nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w1[u]);
-          ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w1[u]);
-        }
-        nn += U;
+      for (int h = 0; h < 2; ++h) {
+        ca[h] += nac[h] & 0x0F0F0F0Fu;
+        cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
+        ct[h] += ntg[h] & 0x0F0F0F0Fu;
+        cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
+        nac[h] = ntg[h] = 0;
       }
-      fold();
-    }
+      nn = 0;
+    };
+    auto issue = [&](int k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
+      uint2 rv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];  // all LDS reads first
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint2 rr = rv[u];
+        const int32_t d = lane - (int32_t)(int16_t)(rr.x & 0xFFFFu);  // column - col0
+        const uint32_t voff = (uint32_t)d < (rr.x >> 16) && !(dbg & 1) ? rr.y + l8 : 0x80000000u;
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
+        w0[u] = w[0];
+        w1[u] = w[1];
+      }
+    };
+    auto count = [&](const uint32_t (&w0)[U], const uint32_t (&w1)[U]) {
+      if (nn + U > 15) fold();
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w0[u]);
+        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w0[u]);
+        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w1[u]);
+        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w1[u]);
+      }
+      nn += U;
+    };
+    uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U];
+    issue(0, a0, a1);
+    issue(U, b0, b1);
     // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
-    if (!(dbg & 2)) {
-      const int64_t e0 = pev_off[rb], e1 = pev_off[re];
-      for (int64_t q = e0; q < e1; q += 64) {
-        const int64_t k = q + lane;
-        if (k < e1) {
-          const uint2 p = pev[k];
-          const int32_t l = (int32_t)p.x;
-          if (p.y & kPevComplex) {
-            const int64_t a = max((int64_t)l, (int64_t)B0);
-            const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
-            if (a < b) {
-              atomicAdd(&mk[a - B0], 1u << 16);
-              if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
-            }
-          } else if (l >= B0 && l < B0 + T) {
-            const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
-            if (m) atomicOr(&mk[l - B0], m);
-            if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
-            else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
-          }
+    auto apply = [&](uint2 p) {
+      const int32_t l = (int32_t)p.x;
+      if (p.y & kPevComplex) {
+        const int64_t a = max((int64_t)l, (int64_t)B0);
+        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+        if (a < b) {
+          atomicAdd(&mk[a - B0], 1u << 16);
+          if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
         }
+      } else if (l >= B0 && l < B0 + T) {
+        const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
+        if (m) atomicOr(&mk[l - B0], m);
+        if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
+        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
       }
+    };
+    const uint64_t t_c = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) apply(ent[j]);
+    if (!(dbg & 2))
+      for (int64_t q = e0 + 64 * NE; q < e1; q += 64) {  // the rest (rare)
+        const int64_t k = q + lane;
+        if (k < e1) apply(pev[k]);
+      }
+    const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    for (int k0 = 0;; k0 += 3 * U) {  // rows past the group's are clamped (zero words)
+      issue(k0 + 2 * U, c0, c1);
+      count(a0, a1);
+      issue(k0 + 3 * U, a0, a1);
+      count(b0, b1);
+      issue(k0 + 4 * U, b0, b1);
+      count(c0, c1);
+      if (k0 + 3 * U >= nmax) break;
     }
+    fold();
+    const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint32_t e8[8], m8[8];
-    {
-      uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-      const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1];
-      e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // ready for the next tile
-      e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
-      m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
-    }
-    if (dbg & 4) continue;
-    // complex elements per locus: prefix of the range differences over the block
-    int32_t pc[8];
-    int32_t run = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      run += (int32_t)m8[j] >> 16;
-      pc[j] = run;
-    }
-    const int32_t exs = (int32_t)wave_incl_scan((uint32_t)run) - run;
-    // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci:
-    //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     uint32_t kinds = 0, nrec = 0, ncpx = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int32_t l = B0 + 8 * lane + j;
-      const bool in = l >= L0 && l < L1;
-      const int h = j >> 2, sh = 8 * (j & 3);
-      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
-      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
-      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
-      const int32_t ncx_s = exs + pc[j];
-      const uint32_t ncx = ncx_s > 0 ? (uint32_t)ncx_s : 0u;
-      const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-      const uint32_t ew = e8[j];
-      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
-                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
-      const bool live = in && depth > 0;
-      const bool ambiguous = (mask & (mask - 1u)) != 0;
-      const uint32_t low = mask & (0u - mask);
-      const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
-      const bool to_complex = live && (ambiguous || ncx > 0 || multi_sample);
-      const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
-      const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
-      const bool emit_hr = homref && (ref_pass ? emit_ref : emit_no_call);
-      const bool general = live && !to_complex && !homref;
-      visited += live ? 1u : 0u;
-      amb += (live && ambiguous) ? 1u : 0u;
-      const uint32_t kind = to_complex ? 3u : general ? 2u : emit_hr ? 1u : 0u;
-      kinds |= kind << (2 * j);
-      nrec += emit_hr ? 1u : general ? 2u : 0u;
-      ncpx += to_complex ? 1u : 0u;
-    }
-    if (__ballot(kinds != 0) == 0) continue;  // the common case: nothing to write
-    const unsigned rbase = wave_reserve_lds_n(out.lds + 0, nrec);
-    const unsigned cbase = wave_reserve_lds_n(out.lds + 1, ncpx);
-    CallRec *prec_out = recs + out.base[0];
-    unsigned kr = rbase, kc = cbase;
-    constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
-                                 ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t kind = (kinds >> (2 * j)) & 3u;
-      if (kind == 0) continue;
-      const int32_t pos = B0 + 8 * lane + j;
-      if (kind == 3) {
-        if (kc < out.cap[1]) cplx[out.base[1] + kc] = ComplexItem{(int32_t)i, pos, 0};
-        ++kc;
-        continue;
+    if (!(dbg & 4)) {
+      uint32_t e8[8], m8[8];
+      {
+        const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1];
+        e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
+        m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
       }
-      const int h = j >> 2, sh = 8 * (j & 3);
-      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
-      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
-      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
-      const uint32_t ew = e8[j];
-      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
-                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
-      const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-      const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - L0));
-      CallRec rr;
-      rr.key = ord << 12;
-      rr.contig = tl.contig;
-      rr.pos = pos;
-      rr.sample = 0;
-      if (kind == 1) {
-        const uint32_t depth = cA + cC + cT + cG + nN;
+      // complex elements per locus: prefix of the range differences over the block
+      int32_t run = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) run += (int32_t)m8[j] >> 16;
+      int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
+      // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci:
+      //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int32_t l = B0 + 8 * lane + j;
+        const bool in = l >= L0 && l < L1;
+        const int h = j >> 2, sh = 8 * (j & 3);
+        const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
+        const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
+        const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+        ncx_run += (int32_t)m8[j] >> 16;
+        const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
+        const uint32_t depth = cA + cC + cT + cG + nN + ncx;
+        const uint32_t ew = e8[j];
+        const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
+                              (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+        const bool live = in && depth > 0;
+        const bool ambiguous = (mask & (mask - 1u)) != 0;
         const uint32_t low = mask & (0u - mask);
         const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
+        const bool to_complex = live && (ambiguous || ncx > 0 || multi_sample);
+        const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
         const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
-        rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
-        rr.flags = 0;
-        rr.ref_len = 1;
-        rr.alt_len = 5;
-        rr.allele = (uint64_t)ref | kAltSym;
-        if (kr < out.cap[0]) prec_out[kr] = rr;
-        ++kr;
-      } else {
-        // a variant candidate: counts in a placeholder record pair, expanded by germline_expand
-        rr.gt0 = ref;
-        rr.gt1 = 0;
-        rr.flags = kCandidate;
-        rr.ref_len = (uint16_t)nN;
-        rr.alt_len = 0;
-        rr.allele = (uint64_t)cA | ((uint64_t)cC << 16) | ((uint64_t)cT << 32) | ((uint64_t)cG << 48);
-        if (kr < out.cap[0]) prec_out[kr] = rr;
-        rr.flags = kCandidateSlot;
-        if (kr + 1 < out.cap[0]) prec_out[kr + 1] = rr;
-        kr += 2;
+        const bool emit_hr = homref && (ref_pass ? emit_ref : emit_no_call);
+        const bool general = live && !to_complex && !homref;
+        visited += live ? 1u : 0u;
+        amb += (live && ambiguous) ? 1u : 0u;
+        const uint32_t kind = to_complex ? 3u : general ? 2u : emit_hr ? 1u : 0u;
+        kinds |= kind << (2 * j);
+        nrec += emit_hr ? 1u : general ? 2u : 0u;
+        ncpx += to_complex ? 1u : 0u;
       }
     }
+    if (__ballot(kinds != 0) != 0) {  // rare: records / complex items to write
+      const unsigned rbase = wave_reserve_lds_n(out.lds + 0, nrec);
+      const unsigned cbase = wave_reserve_lds_n(out.lds + 1, ncpx);
+      CallRec *prec_out = recs + out.base[0];
+      unsigned kr = rbase, kc = cbase;
+      constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
+                                   ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t kind = (kinds >> (2 * j)) & 3u;
+        if (kind == 0) continue;
+        const int32_t pos = B0 + 8 * lane + j;
+        if (kind == 3) {
+          if (kc < out.cap[1]) cplx[out.base[1] + kc] = ComplexItem{(int32_t)i, pos, 0};
+          ++kc;
+          continue;
+        }
+        const int sh = 8 * (j & 3);
+        const bool hi = j >= 4;
+        const uint32_t cA = ((hi ? ca[1] : ca[0]) >> sh) & 0xFFu, cC = ((hi ? cc[1] : cc[0]) >> sh) & 0xFFu;
+        const uint32_t cT = ((hi ? ct[1] : ct[0]) >> sh) & 0xFFu, cG = ((hi ? cg[1] : cg[0]) >> sh) & 0xFFu;
+        const uint32_t mw = mk[8 * lane + j], ew = ev[8 * lane + j];
+        const uint32_t nN = (mw >> 8) & 0xFFu;
+        const uint32_t mask = (mw & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
+                              (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+        const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
+        const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - L0));
+        CallRec rr;
+        rr.key = ord << 12;
+        rr.contig = tl.contig;
+        rr.pos = pos;
+        rr.sample = 0;
+        if (kind == 1) {
+          const uint32_t depth = cA + cC + cT + cG + nN;
+          const uint32_t low = mask & (0u - mask);
+          const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
+          const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+          rr.gt0 = rr.gt1 = ref_pass ? GQ_GT_REF : GQ_GT_NOCALL;
+          rr.flags = 0;
+          rr.ref_len = 1;
+          rr.alt_len = 5;
+          rr.allele = (uint64_t)ref | kAltSym;
+          if (kr < out.cap[0]) prec_out[kr] = rr;
+          ++kr;
+        } else {
+          // a variant candidate: counts in a placeholder record pair, expanded by germline_expand
+          rr.gt0 = ref;
+          rr.gt1 = 0;
+          rr.flags = kCandidate;
+          rr.ref_len = (uint16_t)nN;
+          rr.alt_len = 0;
+          rr.allele = (uint64_t)cA | ((uint64_t)cC << 16) | ((uint64_t)cT << 32) | ((uint64_t)cG << 48);
+          if (kr < out.cap[0]) prec_out[kr] = rr;
+          rr.flags = kCandidateSlot;
+          if (kr + 1 < out.cap[0]) prec_out[kr + 1] = rr;
+          kr += 2;
+        }
+      }
+    }
+    e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
+    if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup, first loads, entries, counting, decision
+      const uint64_t t_f = __builtin_readcyclecounter();
+      clk[0] += t_b - t_a;
+      clk[1] += t_c - t_b;
+      clk[2] += t_d - t_c;
+      clk[3] += t_e - t_d;
+      clk[4] += t_f - t_e;
+      clk[5] += 1;
+    }
   }
+  if ((dbg & 16) && lane == 0 && clk[5])
+    for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
   add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
   if (threadIdx.x == 0) {  // this workgroup's partition counts (may exceed the capacity: host retry)
     ctr->part[0][blockIdx.x] = outn[0];

@@ -31,8 +31,9 @@ constexpr int kCountT = 512;  // loci per counts tile
 constexpr size_t kSeqPad = 2048;  // zeroed tail of the uploaded sequence pool  // LDS staging of a read batch's sequence bytes
 
 constexpr int kSpread = 64;
-constexpr int kParts = 2048;      // output partitions (see Counters::part)
-constexpr int kPartsCols = 1024;  // [0, 1024): one per germline_cols workgroup; the rest: walker / complex waves
+constexpr int kPartsCols = 2048;  // [0, 2048): one output partition per germline workgroup
+constexpr int kPartsWalk = 1024;  // then one per walker / complex-kernel wave (modulo)
+constexpr int kParts = kPartsCols + kPartsWalk;  // output partitions (see Counters::part)
 
 struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_rec;

@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // items beyond a partition's capacity were never written (the host retries with larger ones)
   const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
-  const int rpart = kPartsCols + (int)(gwave & (kPartsCols - 1));  // this wave's record partition
+  const int rpart = kPartsCols + (int)(gwave & (kPartsWalk - 1));  // this wave's record partition
   // the reads covering the locus, compacted (tile-relative indices): the two per-read passes
   // then run over ~depth lanes instead of every read of the tile (one latency chain, not three)
   constexpr int kCover = 256;
@@ -1645,7 +1645,12 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
     }
   }
-  if (getenv("GQ_DBG") && hc.prof[7])
+  if (getenv("GQ_DBG") && germline_use_proj() && hc.prof[5])
+    fprintf(stderr,
+            "gq prof (cycles/tile/wave): setup %.0f first-loads %.0f entries %.0f counting %.0f decision %.0f (%llu)\n",
+            (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
+            (double)hc.prof[3] / hc.prof[5], (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
+  if (getenv("GQ_DBG") && !germline_use_proj() && hc.prof[7])
     fprintf(stderr,
             "gq prof (cycles/tile/wave): tile %.0f scan+column+per-read %.0f vmcnt+barrier1 %.0f "
             "dma+rows+decide %.0f barrier2 %.0f (%llu)\n",

@@ -6,7 +6,7 @@ OUT=$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
 for A in "$@"; do
-  GQ_DBG=$A timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM --kernel-include-regex "germline_cols" --output-format csv -d $OUT/a$A -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/a$A.log 2>&1
+  GQ_DBG=$A timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM --kernel-include-regex "${GQ_KRE:-germline_proj}" --output-format csv -d $OUT/a$A -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/a$A.log 2>&1
   python3 - $OUT/a$A/run_counter_collection.csv $A <<'PY'
 import csv, sys, collections
 v = collections.defaultdict(list)
