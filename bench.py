@@ -2,22 +2,30 @@
 """bench.py — pileup loci/s for germline-threshold on synthetic 30x reads (BASELINE.json configs[1]).
 
 A "step" = one germline-threshold pass (gq_germline_threshold_device: tile planning, the
-column pileup kernel, the walker and general-allele kernels, record sort, the result image
-built in HBM) over every locus of the rank's shard, reads already resident in HBM, plus
-(N > 1) the terminal RCCL gather of the per-rank result images to rank 0 over xGMI.  The
-PCIe copy of the results to the host (gq_germline_threshold) is not part of `value`; its
+projection pileup kernel germline_proj, the walker and general-allele kernels, record sort,
+the result image built in HBM) over every locus of the rank's loci, reads already resident in
+HBM, plus (N > 1) the terminal RCCL gather of the per-rank result images to rank 0 over xGMI.
+The PCIe copy of the results to the host (gq_germline_threshold) is not part of `value`; its
 rate is reported beside it as host_results_loci_per_s.
 
-Workload per GPU: one chr20-sized contig (63,025,520 loci, b37 length —
-T/DistributedUtilSuite.scala:72), 30x, L = 150, seed 20261015 + 2 (+ rank).
-`--gpus N` under torch.distributed.run gives each rank its own chr20-sized
-shard (weak scaling; the static LociSet split of a WGS run).
+Workload
+  N = 1   one chr20-sized contig (63,025,520 loci, b37 length — T/DistributedUtilSuite.scala:72),
+          30x, L = 150, seed 20261015 + 2 (configs[1]).
+  N > 1   the b37 genome (lexicographic contig order, LociMap.scala:39-42) cut to N x 63,025,520
+          loci and split into N contiguous parts by partitionLociUniformly (DistributedUtil.scala:
+          83-108); each rank generates the reads of its part (halo included) and calls its loci
+          (weak scaling: the same loci per GPU as N = 1).  --wgs splits the whole 3.1 G-locus
+          genome instead (configs[3]: ~390 M loci per GPU at N = 8).
 
 Also reported:
-  roofline     the pileup (column) kernel's algorithmic bytes / its HIP-event time vs 8 TB/s
-  cpu_baseline the CPU oracle (single-threaded restatement) on a bounded window of
-               the same workload; its calls are also compared to the GPU's on that
-               window (parity_window).
+  roofline      germline_proj's algorithmic bytes / its HIP-event time vs 8 TB/s
+  end_to_end    SoA upload (H2D + upload-time derivation), the step, the results' D2H, and
+                BAM ingest (native libgqingest, rate measured on a sample BAM) for the shard
+  cpu_baseline  the CPU oracle (restatement, not the JVM reference) on a bounded window of the
+                same workload at 1 thread and at `cores` threads; its calls are compared to the
+                GPU's on that window (parity_window)
+  somatic       somatic-standard on tumor/normal 60x/30x at chr1 length (configs[2]), rank 0,
+                N = 1 only (--somatic-length 0 skips it)
 """
 import argparse
 import json
@@ -31,7 +39,32 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 CHR20 = 63_025_520
+CHR1 = 249_250_621
 HBM_PEAK_GBS = 8000.0
+
+
+def rank_pieces(world: int, rank: int, wgs: bool):
+    """This rank's loci of the split genome: [(contig, contig_length, start, end)]."""
+    from guacamole_amd.genomes import B37
+    from guacamole_amd.loci import LociSet, partition_loci_uniformly
+    budget = None if wgs else world * CHR20
+    b = LociSet.parse("all")
+    lengths = {}
+    ranges = []
+    for name, ln in B37:  # already lexicographic
+        lengths[name] = ln
+        span = ln - 1  # "all" drops each contig's last base (LociSet.scala:205-207)
+        if budget is not None:
+            span = min(span, budget)
+            budget -= span
+        if span > 0:
+            ranges.append("%s:0-%d" % (name, span))
+        if budget == 0:
+            break
+    ls = LociSet.parse(",".join(ranges)).result(lengths)
+    parts = partition_loci_uniformly(world, ls)
+    mine = [(c, lengths[c], s, e) for c, s, e, t in parts.entries() if t == rank]
+    return mine, ls.count
 
 
 def main() -> int:
@@ -39,13 +72,14 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--length", type=int, default=CHR20, help="loci per GPU shard")
+    ap.add_argument("--length", type=int, default=CHR20, help="loci of the N = 1 shard")
     ap.add_argument("--depth", type=float, default=30.0)
     ap.add_argument("--threshold", type=int, default=8)
-    ap.add_argument("--tile", type=int, default=0)
-    ap.add_argument("--cpu-window", type=int, default=4_000_000, help="loci in the CPU-oracle sample window")
+    ap.add_argument("--wgs", action="store_true", help="N > 1: split the whole b37 genome (configs[3])")
+    ap.add_argument("--cpu-window", type=int, default=2_000_000, help="loci in the CPU-oracle sample window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+    ap.add_argument("--somatic-length", type=int, default=CHR1, help="somatic sub-run loci (0: skip)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
@@ -72,15 +106,24 @@ def main() -> int:
             gather_dev = "cpu"
 
     t0 = time.time()
-    g = synthetic.generate(args.length, args.depth, seed=synthetic.SEED + 2 + rank)
+    if world == 1:
+        g = synthetic.generate(args.length, args.depth, seed=synthetic.SEED + 2)
+        loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([args.length - 1], np.int64),
+                np.array([0], np.int64))
+        genome_loci = args.length - 1
+        workload = "germline-threshold, synthetic 30x chr20-length shard per GPU (configs[1])"
+    else:
+        pieces, genome_loci = rank_pieces(world, rank, args.wgs)
+        g = synthetic.generate_pieces(pieces, args.depth, seed=synthetic.SEED + 4 + 1000 * rank)
+        loci = (np.arange(len(pieces), dtype=np.int32), np.array([p[2] for p in pieces], np.int64),
+                np.array([p[3] for p in pieces], np.int64), np.zeros(len(pieces), np.int64))
+        workload = ("germline-threshold, synthetic 30x b37 genome (%s) split over %d GPUs (configs[3])"
+                    % ("whole" if args.wgs else "first %d loci" % genome_loci, world))
     gen_s = time.time() - t0
     ctx = native.Context(local)
-    if args.tile:
-        ctx.set_tile(args.tile)
+    t = time.perf_counter()
     reads = ctx.upload(g.arrays)
-    # loci "all" on the shard's contig: [0, length - 1) (LociSet.scala:205-207)
-    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([args.length - 1], np.int64),
-            np.array([0], np.int64))
+    upload_ms = (time.perf_counter() - t) * 1e3
 
     def barrier():
         if dist is not None:
@@ -97,7 +140,7 @@ def main() -> int:
     for _ in range(args.warmup):
         step()
     barrier()
-    pileup_ms, walk_ms, total_ms, host_ms, marshal_ms = [], [], [], [], []
+    pileup_ms, walk_ms = [], []
     stage_ms = {"plan_ms": [], "complex_ms": [], "finalize_ms": []}
     walk_frac = []
     t = time.perf_counter()
@@ -109,9 +152,6 @@ def main() -> int:
         for k in stage_ms:
             stage_ms[k].append(tm[k])
         walk_frac.append(tm["walk_tiles"] / max(1, tm["tiles"]))
-        total_ms.append(tm["total_ms"])
-        host_ms.append(tm["host_ms"])
-        marshal_ms.append(tm["marshal_ms"])
     barrier()
     elapsed = time.perf_counter() - t
     if dist is not None:
@@ -119,8 +159,12 @@ def main() -> int:
         x = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         elapsed = float(x.item())
+        v = torch.tensor([int(calls.visited_loci)], dtype=torch.int64, device="cuda:%d" % local)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        loci_total = int(v.item())
+    else:
+        loci_total = int(calls.visited_loci)
     visited = int(calls.visited_loci)
-    loci_total = visited * world
     # the same pass with the records copied to the host (PCIe-inclusive), a few steps, rank-local
     hc = ctx.germline_threshold(reads, loci, args.threshold)  # warm-up of the host-block path
     n_host = 5
@@ -130,18 +174,18 @@ def main() -> int:
     host_ms_step = (time.perf_counter() - t) / n_host * 1e3
     assert len(hc) == len(calls)
 
-    # ---- roofline for the pileup kernel (germline_cols): algorithmic bytes per launch.  The
-    #      column kernel counts every tile except the few it hands to the walker kernel
-    #      (walk_tiles: reads it cannot stage or count), so its share of the bytes is the
-    #      tiles it kept.
+    # ---- roofline for the pileup kernel (germline_proj): algorithmic bytes per launch.  The
+    #      kernel reads each read's projection (1 B per locus it spans, 8-locus aligned), its
+    #      16-B record and pmax_end, and the sparse entries (8 B); it writes 32 B per record and
+    #      12 B per queued locus.  Its share is the tiles it kept (walk_tiles go to the walker).
+    st = ctx.proj_stats(reads)
     a = g.arrays
     n_reads = int(a["start"].shape[0])
-    bytes_seq = int(a["seq"].shape[0])            # 1 B per aligned/inserted base (no qualities: not read by this caller)
-    bytes_meta = 16 * n_reads                     # start/end/offsets/counts/flags minimum per read
-    bytes_cigar = 4 * int(a["cigar"].shape[0])
-    bytes_md = 4 * int(a["md_ev"].shape[0])
-    bytes_out = 32 * len(calls) + 8 * int(calls.complex_loci)
-    b_all = bytes_seq + bytes_meta + bytes_cigar + bytes_md + bytes_out
+    bytes_proj = int(st["proj_bytes"])
+    bytes_meta = 20 * n_reads
+    bytes_ent = 8 * int(st["pev_count"])
+    bytes_out = 32 * len(calls) + 12 * int(calls.complex_loci)
+    b_all = bytes_proj + bytes_meta + bytes_ent + bytes_out
     kept = 1.0 - float(np.mean(walk_frac))
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))
@@ -150,7 +194,7 @@ def main() -> int:
     try:
         with open(args.traffic) as fh:
             tr = json.load(fh)
-        if tr.get("length") == args.length and tr.get("depth") == args.depth:
+        if tr.get("length") == args.length and tr.get("depth") == args.depth and world == 1:
             traffic = tr.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -168,39 +212,79 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (native generator: 30x, L=150, GC 0.41, het/hom SNV + indels + Phred errors)",
-        "config": {"workload": "germline-threshold, synthetic 30x chr20-length shard per GPU (configs[1])",
-                   "loci_per_gpu": args.length - 1, "visited_loci_per_gpu": visited, "reads_per_gpu": n_reads,
-                   "depth": args.depth, "read_len": 150, "threshold": args.threshold,
-                   "parallelism": "loci-sharded x%d" % world},
+        "config": {"workload": workload, "genome_loci": genome_loci, "visited_loci_per_gpu": visited,
+                   "reads_per_gpu": n_reads, "contigs_per_gpu": len(g.contig_names), "depth": args.depth,
+                   "read_len": 150, "threshold": args.threshold, "parallelism": "loci-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "germline_cols", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
+                     "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
                      "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
-        "device_total_ms": float(np.mean(total_ms)),
         "device_stages_ms": {k: float(np.mean(v)) for k, v in stage_ms.items()},
         "host_results_loci_per_s": visited / (host_ms_step * 1e-3),
         "host_results_ms_per_step": host_ms_step,
-        "host_call_ms": float(np.mean(host_ms)),
-        "host_marshal_ms": float(np.mean(marshal_ms)),
         "calls": len(calls),
         "complex_loci": int(calls.complex_loci),
         "ambiguous_loci": int(calls.ambiguous_loci),
         "gen_s": gen_s,
     }
-
-    if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"], line["parity_window"] = cpu_baseline(g, ctx, reads, args)
     if rank == 0:
-        print(json.dumps(line))
+        e2e = {"upload_ms": upload_ms, "step_ms": line["ms_per_step"], "step_with_d2h_ms": host_ms_step,
+               "reads": n_reads}
+        e2e.update(ingest_rate(args.depth))
+        e2e["ingest_s_est"] = n_reads / e2e["ingest_reads_per_s"]
+        e2e["single_pass_s_est"] = e2e["ingest_s_est"] + (upload_ms + host_ms_step) / 1e3
+        e2e["single_pass_loci_per_s_est"] = visited / e2e["single_pass_s_est"]
+        line["end_to_end"] = e2e
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"], line["parity_window"] = cpu_baseline(g, ctx, reads, args)
     if dist is not None:
         dist.destroy_process_group()
+    del reads, g
+    if rank == 0 and world == 1 and args.somatic_length > 0:
+        line["somatic"] = somatic_run(ctx, args)
+    if rank == 0:
+        print(json.dumps(line))
     return 0
 
 
+def ingest_rate(depth: float):
+    """BAM -> SoA (native libgqingest: parallel BGZF inflate, decode, the germline filters, MD
+    events) on a synthetic sample BAM of the same model, best of 3."""
+    from guacamole_amd import ingest, soa, synthetic
+    from guacamole_amd.loci import LociSet
+    from guacamole_amd.reads import InputFilters
+    gs = synthetic.generate(4_000_000, depth, seed=synthetic.SEED + 9)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gq_bench_ingest_%d.bam" % os.getpid())
+    gs.write_bam(path)
+    filters = InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True)
+    best = None
+    try:
+        for _ in range(3):
+            t = time.perf_counter()
+            rs = ingest.load_bam(path, filters)
+            soa.pack(rs)
+            s = time.perf_counter() - t
+            best = s if best is None else min(best, s)
+        size = os.path.getsize(path)
+    finally:
+        os.remove(path)
+    return {"ingest_reads_per_s": rs.n / best, "ingest_threads": ingest.n_threads(),
+            "ingest_sample": "BGZF level-6 BAM of %d synthetic reads (%.0f MB), best of 3" % (rs.n, size / 1e6)}
+
+
+def _oracle_threads() -> int:
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() else (os.cpu_count() or 1)
+    return max(1, min(n, 16, os.cpu_count() or 1))
+
+
 def cpu_baseline(g, ctx, reads, args):
-    """Single-threaded CPU oracle on a window of the same workload, timed; its calls
-    are compared with the GPU's calls over the same loci window."""
+    """The CPU oracle on a window of the same workload, timed at 1 thread and at `cores`
+    threads (the window cut into `cores` contiguous parts, one oracle call per thread, as
+    Spark local[*] runs one task per core; ctypes releases the GIL); its calls are compared
+    with the GPU's calls over the same loci window."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
 
     w0 = args.length // 3
@@ -214,10 +298,68 @@ def cpu_baseline(g, ctx, reads, args):
     gpu = ctx.germline_threshold(reads, loci, args.threshold)
     parity = gpu.tuples(g.contig_names) == want
     visited = int(gpu.visited_loci)  # loci with depth > 0 in the window (same set the oracle visits)
-    return ({"value": visited / cpu_s, "unit": "loci/s", "cores": 1, "kind": "port",
-             "sample": "CPU oracle (oracle/oracle.cpp, 1 thread, not the JVM reference) on loci [%d, %d) of the "
-                       "same synthetic shard: %d visited loci, %d reads, %.1f s" % (w0, w1, visited, len(idx), cpu_s)},
+    # the window split over `cores` threads, each with its own reads
+    cores = _oracle_threads()
+    cuts = np.linspace(w0, w1, cores + 1).astype(np.int64)
+    jobs = []
+    for k in range(cores):
+        a, b = int(cuts[k]), int(cuts[k + 1])
+        jobs.append((g.to_read_set(g.window(a, b)),
+                     (np.array([0], np.int32), np.array([a], np.int64), np.array([b], np.int64),
+                      np.array([0], np.int64))))
+    t = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        parts = list(ex.map(lambda j: O.germline_threshold(j[0], j[1], args.threshold), jobs))
+    par_s = time.perf_counter() - t
+    par_same = [r for p in parts for r in p] == want
+    return ({"value": visited / par_s, "unit": "loci/s", "cores": cores, "kind": "port",
+             "value_1_thread": visited / cpu_s,
+             "sample": "CPU oracle (oracle/oracle.cpp, not the JVM reference) on loci [%d, %d) of the same synthetic "
+                       "shard: %d visited loci, %d reads; 1 thread %.1f s, %d threads %.1f s (calls identical: %s)"
+                       % (w0, w1, visited, len(idx), cpu_s, cores, par_s, par_same)},
             {"loci": [w0, w1], "calls": len(want), "identical": bool(parity)})
+
+
+def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
+    """somatic-standard on synthetic tumor 60x / normal 30x over one chr1-length contig
+    (configs[2]), reads resident in HBM; a step = one gq_somatic_standard call (CLI defaults,
+    driver filters on).  Roofline of somatic_tile from its algorithmic bytes (tumor bases +
+    qualities + normal bases + 16 B per read of metadata + MD events)."""
+    from guacamole_amd import synthetic
+    L = args.somatic_length
+    t0 = time.time()
+    seed = synthetic.SEED + 3
+    tg = synthetic.generate(L, 60.0, seed=seed, somatic_rate=2e-4, tumor=True, read_seed=11)
+    ng = synthetic.generate(L, 30.0, seed=seed, somatic_rate=2e-4, tumor=False, read_seed=12)
+    gen_s = time.time() - t0
+    t = ctx.upload(tg.arrays)
+    n = ctx.upload(ng.arrays)
+    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([L - 1], np.int64), np.array([0], np.int64))
+    for _ in range(warmup):
+        ctx.somatic_standard(t, n, loci)
+    stages = {"pileup_ms": [], "complex_ms": [], "finalize_ms": [], "total_ms": []}
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        calls = ctx.somatic_standard(t, n, loci)
+        tm = ctx.timings()
+        for k in stages:
+            stages[k].append(tm[k])
+    el = time.perf_counter() - t1
+    ta, na = tg.arrays, ng.arrays
+    b_alg = (2 * int(ta["seq"].shape[0]) + int(na["seq"].shape[0]) + 16 * (tg.n + ng.n)
+             + 4 * (int(ta["md_ev"].shape[0]) + int(na["md_ev"].shape[0])))
+    k_ms = float(np.mean(stages["pileup_ms"]))
+    ach = b_alg / (k_ms * 1e-3) / 1e9
+    visited = int(calls.visited_loci)
+    return {"metric": "somatic-standard loci/sec, tumor 60x / normal 30x", "value": visited * steps / el,
+            "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": warmup,
+            "config": {"workload": "somatic-standard, synthetic tumor/normal 60x/30x, chr1-length contig (configs[2])",
+                       "loci": L - 1, "visited_loci": visited, "tumor_reads": tg.n, "normal_reads": ng.n},
+            "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items()},
+            "roofline": {"bound": "hbm", "kernel": "somatic_tile", "kernel_ms": k_ms, "achieved": ach,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": b_alg},
+            "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s}
 
 
 if __name__ == "__main__":

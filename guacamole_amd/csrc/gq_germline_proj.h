@@ -91,12 +91,11 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   uint64_t clk[6] = {0, 0, 0, 0, 0, 0};
   const int g = lane >> 4;
   const bool multi_sample = n_samples > 1;
+  // count * 100 / depth > threshold <=> count * 100 >= (threshold + 1) * depth (integers, depth > 0);
+  // with count <= depth < 2^16 the factor clamps to [0, 101] (101: never; 0: always) in 32 bits
   const int64_t thr1 = (int64_t)threshold + 1;
-  const bool narrow = thr1 >= 0 && thr1 <= 1001;
-  const uint32_t thr1u = (uint32_t)thr1;
-  auto passes = [=](uint32_t count, uint32_t depth) {  // count * 100 / depth > threshold (depth > 0)
-    return narrow ? count * 100u >= thr1u * depth : (int64_t)count * 100 >= thr1 * (int64_t)depth;
-  };
+  const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
+  auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
   const uint4 *prec4 = reinterpret_cast<const uint4 *>(prec);
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
@@ -287,21 +286,25 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const uint32_t ew = e8[j];
         const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
                               (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
-        const bool live = in && depth > 0;
-        const bool ambiguous = (mask & (mask - 1u)) != 0;
-        const uint32_t low = mask & (0u - mask);
-        const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
-        const bool to_complex = live && (ambiguous || ncx > 0 || multi_sample);
-        const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
-        const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
-        const bool emit_hr = homref && (ref_pass ? emit_ref : emit_no_call);
-        const bool general = live && !to_complex && !homref;
-        visited += live ? 1u : 0u;
-        amb += (live && ambiguous) ? 1u : 0u;
-        const uint32_t kind = to_complex ? 3u : general ? 2u : emit_hr ? 1u : 0u;
+        // branch-free (0/1 integers): the common hom-ref locus writes nothing
+        const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
+        const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
+        const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit (or 0: N)
+        const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
+                               nN * (low == 0u ? 1u : 0u);
+        const uint32_t to_complex = live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u));
+        const uint32_t simple = live & (to_complex ^ 1u);
+        const uint32_t alt_pass = passes(depth - c_ref, depth) ? 1u : 0u;  // some other allele may pass
+        const uint32_t homref = simple & (alt_pass ^ 1u);
+        const uint32_t ref_pass = (c_ref > 0 && passes(c_ref, depth)) ? 1u : 0u;
+        const uint32_t emit_hr = homref & (ref_pass ? (uint32_t)(emit_ref != 0) : (uint32_t)(emit_no_call != 0));
+        const uint32_t general = simple & alt_pass;
+        visited += live;
+        amb += live & ambiguous;
+        const uint32_t kind = to_complex * 3u + general * 2u + emit_hr;  // at most one is set
         kinds |= kind << (2 * j);
-        nrec += emit_hr ? 1u : general ? 2u : 0u;
-        ncpx += to_complex ? 1u : 0u;
+        nrec += emit_hr + 2u * general;
+        ncpx += to_complex;
       }
     }
     if (__ballot(kinds != 0) != 0) {  // rare: records / complex items to write
@@ -313,6 +316,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
                                    ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
       for (int j = 0; j < 8; ++j) {
         const uint32_t kind = (kinds >> (2 * j)) & 3u;
+        if (__ballot(kind != 0) == 0) continue;  // no lane writes for locus j (uniform skip)
         if (kind == 0) continue;
         const int32_t pos = B0 + 8 * lane + j;
         if (kind == 3) {

@@ -217,7 +217,7 @@ struct gq_dev_reads {
   std::vector<int64_t> contig_read_begin;  // host copy
   std::vector<void *> owned;               // device allocations owned by this handle
   int64_t seq_bytes = 0;
-  int64_t proj_bytes = 0, pev_count = 0;  // germline projection pool sizes (derive_shape)
+  int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // germline projection sizes (derive_shape)
 };
 
 namespace gq {

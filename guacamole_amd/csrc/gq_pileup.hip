@@ -279,6 +279,13 @@ __global__ void prec_fill(DevReads R, const int64_t *__restrict__ woff, ProjRec 
   prec[r] = p;
 }
 
+__global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, int64_t *__restrict__ n_ok) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = r < R.n_reads && prec[r].col1 != kProjNone;
+  const unsigned long long b = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd((unsigned long long *)n_ok, (unsigned long long)__popcll(b));
+}
+
 // The projection words of 256 reads per block (thread per word, coalesced in the pool).
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, const int64_t *__restrict__ woff,
                                                  uint8_t *__restrict__ proj) {
@@ -1243,6 +1250,17 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.pev_off = (const int64_t *)eo;
     d->proj_bytes = 8 * tot[0];
     d->pev_count = tot[1];
+    if (n > 0) {  // reads the projection takes (words > 0 or an empty span)
+      int64_t *nok = nullptr;
+      HIP_TRY(hipMalloc(&nok, sizeof(int64_t)));
+      HIP_TRY(hipMemsetAsync(nok, 0, sizeof(int64_t), c->stream));
+      hipLaunchKernelGGL(proj_count_ok, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                         d->d, (const ProjRec *)pr, nok);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&d->proj_reads, nok, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      (void)hipFree(nok);
+    }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   (void)hipFree(nnb);
@@ -1394,6 +1412,16 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
     return st2;
   }
   *out = d;
+  return GQ_OK;
+}
+
+gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
+  if (!d || !out) return set_err(GQ_E_ARG, "gq_reads_get_info: null argument");
+  out->n_reads = d->d.n_reads;
+  out->seq_bytes = d->seq_bytes;
+  out->proj_bytes = d->proj_bytes;
+  out->pev_count = d->pev_count;
+  out->proj_reads = d->proj_reads;
   return GQ_OK;
 }
 

@@ -72,6 +72,10 @@ class gq_timings(C.Structure):
                 ("walk_ms", C.c_float), ("walk_tiles", C.c_int64)]
 
 
+class gq_reads_info(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads")]
+
+
 class gq_somatic_params(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "odds", "min_mapq", "filter_multi_allelic", "max_read_depth", "min_tumor_read_depth",
@@ -116,7 +120,7 @@ class gq_somatic_calls(C.Structure):
 EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
             "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
             "gq_free_calls", "gq_pileup_counts",
-            "gq_free_counts", "gq_somatic_standard", "gq_free_somatic")
+            "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info")
 
 
 def lib():
@@ -130,7 +134,7 @@ def lib():
         L = C.CDLL(path)
         L.gq_version.restype = C.c_char_p
         L.gq_last_error.restype = C.c_char_p
-        for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device",
+        for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
                   "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
@@ -208,6 +212,12 @@ class Context:
         t = gq_timings()
         _check(lib().gq_get_timings(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in gq_timings._fields_}
+
+    def proj_stats(self, reads: "DeviceReads") -> Dict[str, int]:
+        """Sizes of a resident read set and of its upload-time projection (gq_reads_get_info)."""
+        info = gq_reads_info()
+        _check(lib().gq_reads_get_info(reads.h, C.byref(info)))
+        return {k: int(getattr(info, k)) for k, _ in gq_reads_info._fields_}
 
     def upload(self, arrs: Dict[str, object]) -> "DeviceReads":
         s, keep = make_gq_reads(arrs)

@@ -172,6 +172,52 @@ def md_string(cigar: np.ndarray, events: np.ndarray) -> str:
     return "".join(out)
 
 
+def generate_pieces(pieces, depth: float, seed: int = SEED, L: int = 150) -> SyntheticReads:
+    """Reads for loci ranges of several contigs: pieces = [(contig, contig_length, start, end)],
+    one range per contig, in the caller's contig order (local contig ids 0, 1, ...).  Each piece
+    is generated as its own stretch [start - L, end) (seed + piece index) and shifted into place,
+    so the reads straddling a piece's start are present (the halo of DistributedUtil.scala:
+    584-597); the arrays are concatenated in contig order."""
+    parts, names, lengths = [], [], []
+    for k, (contig, clen, s, e) in enumerate(pieces):
+        s0 = max(0, int(s) - L)
+        g = generate(int(e) - s0, depth, seed=seed + 7919 * k, L=L, contig=contig)
+        parts.append((g, s0))
+        names.append(contig)
+        lengths.append(int(clen))
+    keys_pos = ("start", "end", "pmax_end")
+    out: Dict[str, np.ndarray] = {}
+    n_tot, seq_tot, cig_tot, md_tot = 0, 0, 0, 0
+    begin = [0]
+    cols = {k: [] for k in ("start", "end", "pmax_end", "mapq", "flags", "sample", "seq_off", "seq_len", "cigar_off",
+                            "n_cigar", "md_off", "n_md", "n_mismatch", "seq", "qual", "cigar", "md_ev")}
+    for g, s0 in parts:
+        a = g.arrays
+        for k in cols:
+            v = a[k]
+            if k in keys_pos:
+                v = v + np.int32(s0)
+            elif k == "seq_off":
+                v = v + seq_tot
+            elif k == "cigar_off":
+                v = v + cig_tot
+            elif k == "md_off":
+                v = v + md_tot
+            cols[k].append(np.asarray(v))
+        n_tot += g.n
+        seq_tot += int(a["seq"].shape[0])
+        cig_tot += int(a["cigar"].shape[0])
+        md_tot += int(a["md_ev"].shape[0])
+        begin.append(n_tot)
+    for k, v in cols.items():
+        out[k] = np.concatenate(v) if v else np.zeros(0)
+    out["contig_read_begin"] = np.array(begin, np.int64)
+    out["n_contigs"] = np.int64(len(parts))
+    out["n_samples"] = np.int64(1)
+    stats = {k: sum(g.stats[k] for g, _ in parts) for k in ("n_snv", "n_indel", "n_somatic")}
+    return SyntheticReads(names, lengths, out, np.zeros(0, np.uint8), stats, None)
+
+
 def generate(length: int, depth: float, seed: int = SEED, L: int = 150, contig: str = "20",
              het: float = 1e-3, hom: float = 5e-4, indel_rate: float = 1e-4, somatic_rate: float = 0.0,
              tumor: bool = False, read_seed: Optional[int] = None) -> SyntheticReads:

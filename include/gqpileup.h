@@ -180,6 +180,12 @@ gq_status gq_reads_upload(gq_ctx *ctx, const gq_reads *host, gq_dev_reads **out)
 /* the caller keeps them alive.                                              */
 gq_status gq_reads_wrap_device(gq_ctx *ctx, const gq_reads *device_ptrs, gq_dev_reads **out);
 void gq_reads_free(gq_dev_reads *r);
+/* Sizes of a resident read set and of what the upload derived from it (the germline         */
+/* projection pool and its sparse entries): for measurement and capacity planning.             */
+typedef struct gq_reads_info {
+  int64_t n_reads, seq_bytes, proj_bytes, pev_count, proj_reads;  /* proj_reads: reads the projection takes */
+} gq_reads_info;
+gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
 /* germline-threshold over the given loci partitions.                         */
 gq_status gq_germline_threshold(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
