@@ -226,52 +226,53 @@ __global__ void germline_expand(CallRec *__restrict__ recs, Counters *ctr, OutGe
     const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
     if (tie) ++ties;
     const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
-    CallRec out[2];
-    int nout = 0;
-    auto mk = [&](uint8_t g0, uint8_t g1, uint8_t alt1, bool alt_sym, int sub) {
-      CallRec rr = cand;
-      rr.key = cand.key | (uint64_t)sub;
-      rr.gt0 = g0;
-      rr.gt1 = g1;
-      rr.flags = fl;
-      rr.ref_len = 1;
-      rr.alt_len = alt_sym ? 5 : 1;
-      rr.allele = alt_sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt1 << 8));
-      out[nout++] = rr;
-    };
+    // the case split -> up to two records (g0, g1, alt base or the symbolic <ALT>)
     const uint8_t b0 = key_base(k0), b1 = key_base(k1);
+    int nout = 0;
+    uint8_t ga0 = 0, ga1 = 0, aa = 0, gb0 = 0, gb1 = 0, ab = 0;
+    bool syma = false;
     if (npass == 0) {
-      if (emit_no_call) mk(GQ_GT_NOCALL, GQ_GT_NOCALL, 0, true, 0);
+      if (emit_no_call) nout = 1, ga0 = ga1 = GQ_GT_NOCALL, syma = true;
     } else if (npass == 1 && b0 == ref) {
-      if (emit_ref) mk(GQ_GT_REF, GQ_GT_REF, 0, true, 0);
+      if (emit_ref) nout = 1, ga0 = ga1 = GQ_GT_REF, syma = true;
     } else if (npass == 1) {
-      mk(GQ_GT_ALT, GQ_GT_ALT, b0, false, 0);
+      nout = 1, ga0 = ga1 = GQ_GT_ALT, aa = b0;
     } else {
       const bool v1 = b0 != ref, v2 = b1 != ref;
       if (v1 != v2) {
-        mk(GQ_GT_REF, GQ_GT_ALT, v1 ? b0 : b1, false, 0);
+        nout = 1, ga0 = GQ_GT_REF, ga1 = GQ_GT_ALT, aa = v1 ? b0 : b1;
       } else if (v1 && v2) {
-        mk(GQ_GT_ALT, GQ_GT_OTHERALT, b0, false, 0);
-        mk(GQ_GT_ALT, GQ_GT_OTHERALT, b1, false, 1);
+        nout = 2, ga0 = gb0 = GQ_GT_ALT, ga1 = gb1 = GQ_GT_OTHERALT, aa = b0, ab = b1;
       }
       // two non-variant single-base alleles cannot occur (all Match alleles share ref)
     }
-    // the pair's two slots are consecutive in the partition (reserved together)
-    for (int q = 0; q < 2; ++q) {
-      if (q < nout) {
-        recs[slot + q] = out[q];
-      } else {
-        CallRec d = cand;
-        d.key = dead_key;
-        d.flags = 0;
-        recs[slot + q] = d;
-        ++dead;
-      }
-    }
+    // the pair's two slots are consecutive in the partition (reserved together); an unused
+    // slot gets the dead key.  Records are written as two 16-byte halves (CallRec layout).
+    auto put = [&](unsigned long long at, bool live, int sub, uint8_t g0, uint8_t g1, uint8_t alt, bool sym) {
+      const uint64_t key = live ? (cand.key | (uint64_t)sub) : dead_key;
+      const uint64_t allele = sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt << 8));
+      const uint32_t w3 = (uint32_t)cand.sample | ((uint32_t)g0 << 8) | ((uint32_t)g1 << 16) |
+                          ((uint32_t)(live ? fl : 0) << 24);
+      const uint32_t w4 = 1u | ((uint32_t)(sym ? 5 : 1) << 16);  // ref_len 1, alt_len
+      uint4 *d = reinterpret_cast<uint4 *>(recs + at);
+      d[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)cand.contig, (uint32_t)cand.pos);
+      d[1] = make_uint4(w3, w4, (uint32_t)allele, (uint32_t)(allele >> 32));
+    };
+    put(slot, nout > 0, 0, ga0, ga1, aa, syma);
+    put(slot + 1, nout > 1, 1, gb0, gb1, ab, false);
+    dead += nout > 1 ? 0u : nout > 0 ? 1u : 2u;
    }
   }
-  if (dead) atomicAdd(&ctr->n_dead, (unsigned long long)dead);
-  if (ties) atomicAdd(&ctr->spread[2][threadIdx.x & (kSpread - 1)], (unsigned long long)ties);
+  // one atomic per wave (a per-thread add on one word serialises ~10^5 threads at the L2)
+  for (int d = 32; d >= 1; d >>= 1) {
+    dead += __shfl_xor(dead, d, 64);
+    ties += __shfl_xor(ties, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {  // spread over kSpread words (one word serialises ~10 ns per add)
+    const int sl = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1));
+    if (dead) atomicAdd(&ctr->spread[3][sl], (unsigned long long)dead);
+    if (ties) atomicAdd(&ctr->spread[2][sl], (unsigned long long)ties);
+  }
 }
 
 // Run counters (visited / ambiguous / tie loci) of a workgroup, added once at its end.

@@ -50,7 +50,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
   // per-tile run counters, spread over kSpread addresses (summed on the host)
-  unsigned long long spread[3][64];
+  unsigned long long spread[4][64];  // visited, ambiguous, ties, dead record slots
   unsigned long long prof[8];  // diagnostic phase clocks (GQ_DBG=16 only)
   // ---- device-only tail (the host copies the head, up to `part`)
   // germline outputs: records (0) and complex items (1) are reserved per partition — a
@@ -209,6 +209,19 @@ struct gq_ctx {
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
+  gq::DevBuf bkt;                                  // germline output order: bucket counts / offsets / fill
+  void *pin = nullptr;                             // pinned host staging for the small per-call copies
+  size_t pin_n = 0;
+  hipError_t pinned(size_t bytes) {                // pin has >= bytes (contents not kept)
+    if (bytes <= pin_n) return hipSuccess;
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_n = 0;
+    const size_t want = std::max(bytes, (size_t)65536);
+    hipError_t e = hipHostMalloc(&pin, want, hipHostMallocDefault);
+    if (e == hipSuccess) pin_n = want;
+    return e;
+  }
 };
 
 struct gq_dev_reads {

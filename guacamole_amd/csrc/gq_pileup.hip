@@ -279,11 +279,14 @@ __global__ void prec_fill(DevReads R, const int64_t *__restrict__ woff, ProjRec 
   prec[r] = p;
 }
 
-__global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, int64_t *__restrict__ n_ok) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ok = r < R.n_reads && prec[r].col1 != kProjNone;
-  const unsigned long long b = __ballot(ok);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd((unsigned long long *)n_ok, (unsigned long long)__popcll(b));
+// Reads the projection takes, into kSpread words (summed on the host): a grid-stride count per
+// thread, one add per wave.
+__global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ n_ok) {
+  unsigned long long k = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R.n_reads; r += (int64_t)gridDim.x * blockDim.x)
+    k += prec[r].col1 != kProjNone ? 1u : 0u;
+  for (int d = 32; d >= 1; d >>= 1) k += __shfl_xor(k, d, 64);
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
 }
 
 // The projection words of 256 reads per block (thread per word, coalesced in the pool).
@@ -1022,6 +1025,48 @@ __global__ void gather_keys(const CallRec *__restrict__ recs, const Counters *__
   slot[k] = (int32_t)src;
 }
 
+// Output order without a comparison sort.  Records fall into buckets of 2^bshift output
+// ordinals (key >> (12 + bshift)); the buckets are scanned, and a record's place inside its
+// bucket is the number of the bucket's records with a smaller key (keys of live records are
+// unique).  Buckets hold few records: 512 loci of a sparse call set (bshift 9), one locus when
+// every locus emits (bshift 0).  Unused candidate slots (dead_key) are dropped.
+__global__ void bucket_count(const CallRec *__restrict__ recs, const Counters *__restrict__ ctr, OutGeom og,
+                             int64_t n_all, uint64_t dead_key, int bshift, uint64_t *__restrict__ keys,
+                             int32_t *__restrict__ slot, int64_t *__restrict__ bkt, uint32_t *__restrict__ cnt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_all) return;
+  const unsigned long long src = part_slot(ctr->part_off[0], (unsigned long long)k, og, 0);
+  const uint64_t key = recs[src].key;
+  keys[k] = key;
+  slot[k] = (int32_t)src;
+  const int64_t b = key == dead_key ? -1 : (int64_t)(key >> (12 + bshift));
+  bkt[k] = b;
+  if (b >= 0) atomicAdd(&cnt[b], 1u);
+}
+
+__global__ void bucket_scatter(int64_t n_all, const int64_t *__restrict__ bkt, const uint32_t *__restrict__ off,
+                               uint32_t *__restrict__ fill, int32_t *__restrict__ members) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_all) return;
+  const int64_t b = bkt[k];
+  if (b < 0) return;
+  members[off[b] + atomicAdd(&fill[b], 1u)] = (int32_t)k;
+}
+
+__global__ void bucket_rank(int64_t n, const uint32_t *__restrict__ off, const int32_t *__restrict__ members,
+                            const uint64_t *__restrict__ keys, const int32_t *__restrict__ slot,
+                            const int64_t *__restrict__ bkt, int32_t *__restrict__ order) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t k = members[p];
+  const int64_t b = bkt[k];
+  const uint32_t lo = off[b], hi = off[b + 1];
+  const uint64_t key = keys[k];
+  uint32_t rank = 0;
+  for (uint32_t q = lo; q < hi; ++q) rank += keys[members[q]] < key ? 1u : 0u;
+  order[lo + rank] = slot[k];
+}
+
 __global__ void iota_i32(int32_t *__restrict__ v, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) v[i] = (int32_t)i;
@@ -1093,9 +1138,10 @@ void gq_close(gq_ctx *c) {
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
                     &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
                     &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow, &c->amb, &c->amb_ref,
-                    &c->heap_off, &c->heap_reads, &c->win_meta, &c->win_grp})
+                    &c->heap_off, &c->heap_reads, &c->win_meta, &c->win_grp, &c->bkt})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
+  if (c->pin) (void)hipHostFree(c->pin);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1250,16 +1296,17 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.pev_off = (const int64_t *)eo;
     d->proj_bytes = 8 * tot[0];
     d->pev_count = tot[1];
-    if (n > 0) {  // reads the projection takes (words > 0 or an empty span)
-      int64_t *nok = nullptr;
-      HIP_TRY(hipMalloc(&nok, sizeof(int64_t)));
-      HIP_TRY(hipMemsetAsync(nok, 0, sizeof(int64_t), c->stream));
-      hipLaunchKernelGGL(proj_count_ok, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                         d->d, (const ProjRec *)pr, nok);
+    if (n > 0) {  // reads the projection takes
+      unsigned long long *nok = nullptr, hk[kSpread];
+      HIP_TRY(hipMalloc(&nok, sizeof(hk)));
+      HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
+      hipLaunchKernelGGL(proj_count_ok, dim3(1024), dim3(kBlock), 0, c->stream, d->d, (const ProjRec *)pr, nok);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(&d->proj_reads, nok, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       (void)hipFree(nok);
+      d->proj_reads = 0;
+      for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
     }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1479,11 +1526,17 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   int64_t *d_rs = (int64_t *)(base + ((nr * 4 + 15) & ~(size_t)15));
   int64_t *d_re = d_rs + nr, *d_ro = d_re + nr, *d_rt = d_ro + nr;
   HIP_TRY(c->ranges.ensure((size_t)((char *)(d_rt + nr) - base)));
-  HIP_TRY(hipMemcpyAsync(d_rc, rc.data(), nr * 4, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_rs, rs.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_re, re.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_ro, ro.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(d_rt, rt.data(), nr * 8, hipMemcpyHostToDevice, c->stream));
+  {  // one H2D copy from pinned staging (the previous call's copy has completed: every call syncs)
+    const size_t bytes = (size_t)((char *)(d_rt + nr) - base);
+    HIP_TRY(c->pinned(bytes));
+    char *hb = (char *)c->pin;
+    memcpy(hb + ((char *)d_rc - base), rc.data(), nr * 4);
+    memcpy(hb + ((char *)d_rs - base), rs.data(), nr * 8);
+    memcpy(hb + ((char *)d_re - base), re.data(), nr * 8);
+    memcpy(hb + ((char *)d_ro - base), ro.data(), nr * 8);
+    memcpy(hb + ((char *)d_rt - base), rt.data(), nr * 8);
+    HIP_TRY(hipMemcpyAsync(base, hb, bytes, hipMemcpyHostToDevice, c->stream));
+  }
   HIP_TRY(tiles_buf.ensure((size_t)tiles * sizeof(Tile)));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
@@ -1616,8 +1669,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c->pinned(kCountersHead));
+    HIP_TRY(hipMemcpyAsync(c->pin, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(&hc, c->pin, kCountersHead);
     bool retry = false;
     // part_max = the largest overflow of a partition: grow both capacities by it
     for (int w = 0; w < 2; ++w)
@@ -1688,6 +1743,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];
     hc.ties += hc.spread[2][k];
+    hc.n_dead += hc.spread[3][k];
   }
   st = check_device_error(c, hc);
   if (st) {
@@ -1707,30 +1763,42 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   HIP_TRY(c->image.ensure(lay.bytes));
   if (n > 0) {
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock), nb_all = (unsigned)((n_all + kBlock - 1) / kBlock);
-    // keys and record slots of the partitioned records, densely
-    hipLaunchKernelGGL(gather_keys, dim3(nb_all), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const Counters *)c->counters.p, og, n_all, (uint64_t *)c->keys.p, (int32_t *)c->idx.p);
+    // output order: bucket counts, their scan, the members of each bucket, ranks inside it
+    const bool dense = p->emit_ref || p->emit_no_call;
+    const int bshift = dense ? 0 : 9;
+    const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
+    const int64_t nbk = (pl.n_loci >> bshift) + 1;
+    HIP_TRY(c->bkt.ensure(sizeof(uint32_t) * (size_t)(3 * (nbk + 1))));
+    uint32_t *cnt = (uint32_t *)c->bkt.p, *off = cnt + (nbk + 1), *fill = off + (nbk + 1);
+    HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (size_t)(nbk + 1), c->stream));
+    HIP_TRY(hipMemsetAsync(fill, 0, sizeof(uint32_t) * (size_t)(nbk + 1), c->stream));
+    hipLaunchKernelGGL(bucket_count, dim3(nb_all), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const Counters *)c->counters.p, og, n_all, dead_key, bshift, (uint64_t *)c->keys.p,
+                       (int32_t *)c->idx_sorted.p, (int64_t *)c->idx.p, cnt);
     HIP_TRY(hipGetLastError());
-    int end_bit = 12;
-    while (end_bit < 64 && ((uint64_t)pl.n_loci >> (end_bit - 12)) != 0) ++end_bit;
     size_t tmp = 0, tmp2 = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t *)c->keys.p, (uint64_t *)c->keys_sorted.p,
-                                               (const int32_t *)c->idx.p, (int32_t *)c->idx_sorted.p, (int)n_all, 0,
-                                               end_bit, c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, off, (int)(nbk + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p, (int)n,
                                              c->stream));
     HIP_TRY(c->sort_tmp.ensure(std::max(tmp, tmp2)));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (const uint64_t *)c->keys.p,
-                                               (uint64_t *)c->keys_sorted.p, (const int32_t *)c->idx.p,
-                                               (int32_t *)c->idx_sorted.p, (int)n_all, 0, end_bit, c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, cnt, off, (int)(nbk + 1), c->stream));
+    hipLaunchKernelGGL(bucket_scatter, dim3(nb_all), dim3(kBlock), 0, c->stream, n_all, (const int64_t *)c->idx.p,
+                       (const uint32_t *)off, fill, (int32_t *)c->keys_sorted.p);
+    HIP_TRY(hipGetLastError());
+    // order -> the record slot of each output position (c->recs_sorted as int32)
+    HIP_TRY(c->recs_sorted.ensure(nn * 4));
+    hipLaunchKernelGGL(bucket_rank, dim3(nb), dim3(kBlock), 0, c->stream, n, (const uint32_t *)off,
+                       (const int32_t *)c->keys_sorted.p, (const uint64_t *)c->keys.p, (const int32_t *)c->idx_sorted.p,
+                       (const int64_t *)c->idx.p, (int32_t *)c->recs_sorted.p);
+    HIP_TRY(hipGetLastError());
     // allele byte lengths in output order -> exclusive offsets into the pool
     hipLaunchKernelGGL(calls_lengths, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const int32_t *)c->idx_sorted.p, n, (int64_t *)c->idx.p);
+                       (const int32_t *)c->recs_sorted.p, n, (int64_t *)c->idx.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p,
                                              (int)n, c->stream));
     hipLaunchKernelGGL(calls_image, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const int32_t *)c->idx_sorted.p, (const int64_t *)c->keys.p, (const uint8_t *)c->pool.p, n,
+                       (const int32_t *)c->recs_sorted.p, (const int64_t *)c->keys.p, (const uint8_t *)c->pool.p, n,
                        lay, (uint8_t *)c->image.p);
     HIP_TRY(hipGetLastError());
   } else {
@@ -1739,9 +1807,11 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   uint8_t *blk = nullptr;
   int64_t pool_len = 0;
   if (dev) {  // the image stays in HBM: only its pool length comes back
-    HIP_TRY(hipMemcpyAsync(&pool_len, c->image.p, sizeof(pool_len), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c->pinned(sizeof(pool_len)));
+    HIP_TRY(hipMemcpyAsync(c->pin, c->image.p, sizeof(pool_len), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev[4], c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(&pool_len, c->pin, sizeof(pool_len));
     blk = (uint8_t *)c->image.p;
     dev->image = c->image.p;
     dev->image_bytes = (int64_t)lay.pool + pool_len;
