@@ -174,18 +174,22 @@ def main() -> int:
     host_ms_step = (time.perf_counter() - t) / n_host * 1e3
     assert len(hc) == len(calls)
 
-    # ---- roofline for the pileup kernel (germline_proj): algorithmic bytes per launch.  The
-    #      kernel reads each read's projection (1 B per locus it spans, 8-locus aligned), its
-    #      16-B record and pmax_end, and the sparse entries (8 B); it writes 32 B per record and
-    #      12 B per queued locus.  Its share is the tiles it kept (walk_tiles go to the walker).
+    # ---- roofline for the pileup kernel (germline_proj): algorithmic bytes per launch,
+    #      SURVEY §8(d) without qualities (germline-threshold never reads them): 1 B per read
+    #      base, 16 B of metadata per read, 4 B per CIGAR op and per MD event, 32 B per record
+    #      and 12 B per queued locus written.  Its share is the tiles it kept (walk_tiles go to
+    #      the walker).  The bytes it actually reads are reported beside it (`read_bytes`: the
+    #      8-locus-aligned projection, 16-B records + pmax_end, 8-B sparse entries).
     st = ctx.proj_stats(reads)
     a = g.arrays
     n_reads = int(a["start"].shape[0])
-    bytes_proj = int(st["proj_bytes"])
-    bytes_meta = 20 * n_reads
-    bytes_ent = 8 * int(st["pev_count"])
+    bytes_seq = int(a["seq"].shape[0])
+    bytes_meta = 16 * n_reads
+    bytes_cigar = 4 * int(a["cigar"].shape[0])
+    bytes_md = 4 * int(a["md_ev"].shape[0])
     bytes_out = 32 * len(calls) + 12 * int(calls.complex_loci)
-    b_all = bytes_proj + bytes_meta + bytes_ent + bytes_out
+    b_all = bytes_seq + bytes_meta + bytes_cigar + bytes_md + bytes_out
+    read_bytes = int(st["proj_bytes"]) + 20 * n_reads + 8 * int(st["pev_count"])
     kept = 1.0 - float(np.mean(walk_frac))
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))
@@ -218,7 +222,7 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
-                     "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
+                     "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
         "device_stages_ms": {k: float(np.mean(v)) for k, v in stage_ms.items()},
         "host_results_loci_per_s": visited / (host_ms_step * 1e-3),
@@ -323,8 +327,10 @@ def cpu_baseline(g, ctx, reads, args):
 def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
     """somatic-standard on synthetic tumor 60x / normal 30x over one chr1-length contig
     (configs[2]), reads resident in HBM; a step = one gq_somatic_standard call (CLI defaults,
-    driver filters on).  Roofline of somatic_tile from its algorithmic bytes (tumor bases +
-    qualities + normal bases + 16 B per read of metadata + MD events)."""
+    driver filters on).  Roofline of the candidate kernel somatic_proj from its algorithmic bytes:
+    tumor bases + qualities, 16 B per tumor read, 4 B per tumor CIGAR op and MD event, 8 B per
+    normal read (the normal's depth needs its reads' intervals only); the bytes it reads
+    (projection, 16-bit margin terms, records, sparse entries, normal intervals) beside it."""
     from guacamole_amd import synthetic
     L = args.somatic_length
     t0 = time.time()
@@ -345,9 +351,11 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
         for k in stages:
             stages[k].append(tm[k])
     el = time.perf_counter() - t1
-    ta, na = tg.arrays, ng.arrays
-    b_alg = (2 * int(ta["seq"].shape[0]) + int(na["seq"].shape[0]) + 16 * (tg.n + ng.n)
-             + 4 * (int(ta["md_ev"].shape[0]) + int(na["md_ev"].shape[0])))
+    ta = tg.arrays
+    b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
+             + 8 * ng.n)
+    st = ctx.proj_stats(t)
+    read_bytes = 3 * int(st["proj_bytes"]) + 20 * tg.n + 8 * int(st["pev_count"]) + 8 * ng.n
     k_ms = float(np.mean(stages["pileup_ms"]))
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)
@@ -356,9 +364,9 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
             "config": {"workload": "somatic-standard, synthetic tumor/normal 60x/30x, chr1-length contig (configs[2])",
                        "loci": L - 1, "visited_loci": visited, "tumor_reads": tg.n, "normal_reads": ng.n},
             "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items()},
-            "roofline": {"bound": "hbm", "kernel": "somatic_tile", "kernel_ms": k_ms, "achieved": ach,
+            "roofline": {"bound": "hbm", "kernel": "somatic_proj", "kernel_ms": k_ms, "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_launch": b_alg},
+                         "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes},
             "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s}
 
 

@@ -205,6 +205,7 @@ struct gq_ctx {
   int germ_tile = gq::kGermT;
   int n_cu = 0;
   int proj_wg_per_cu = 0;  // resident germline_proj workgroups per CU (occupancy query, once)
+  int som_wg_per_cu = 0;   // resident somatic_proj workgroups per CU
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
@@ -231,6 +232,8 @@ struct gq_dev_reads {
   std::vector<void *> owned;               // device allocations owned by this handle
   int64_t seq_bytes = 0;
   int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // germline projection sizes (derive_shape)
+  mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
+  mutable int mproj_mapq = -1;
 };
 
 namespace gq {

@@ -1475,6 +1475,7 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
 void gq_reads_free(gq_dev_reads *d) {
   if (!d) return;
   for (void *p : d->owned) (void)hipFree(p);
+  if (d->mproj) (void)hipFree(d->mproj);
   delete d;
 }
 

@@ -164,15 +164,18 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
   }
 }
 
+#include "gq_somatic_proj.h"
+
 // ------------------------------------------------------------------------------------------
-// somatic_tile: candidate loci
+// somatic_tile: candidate loci (the tiles somatic_proj cannot take)
 // ------------------------------------------------------------------------------------------
 template <int T>
-// four waves per SIMD (<= 128 VGPRs)
+// four waves per SIMD (<= 128 VGPRs).  The tiles somatic_proj hands over (list), a block per
+// tile at a time; candidates go to the block's output partition (kPartsCols + block).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void somatic_tile(const Tile *__restrict__ tiles_t,
                                                        const Tile *__restrict__ tiles_n, DevReads RT, DevReads RN,
-                                                       ComplexItem *__restrict__ cand, unsigned long long cand_cap,
-                                                       int min_mapq, Counters *ctr) {
+                                                       ComplexItem *__restrict__ cand, OutGeom og,
+                                                       const int32_t *__restrict__ list, int min_mapq, Counters *ctr) {
   constexpr int S = T + 2 * kGuard;
   constexpr int KPT = T / kBlock;  // loci per thread
   static_assert(KPT <= 8, "per-thread flag bits");
@@ -180,26 +183,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   __shared__ float marg[T];  // hom-ref margin of the tumor pileup
   __shared__ float eq[128];   // 10^(-q/10)
   __shared__ float lsq[128];  // log(1 - 10^(-q/10)) = log phredSuccess(q), -inf at q = 0
-  const Tile tt = tiles_t[blockIdx.x], tn = tiles_n[blockIdx.x];
-  const int32_t L0 = tt.L0, L1 = tt.L1;
-  const int nloci = L1 - L0;
-  const bool wide = (tt.re - tt.rb) >= 65535 || (tn.re - tn.rb) >= 65535;
-  unsigned visited = 0;
-  if (wide) {  // 16-bit counters could overflow: every locus goes to the exact kernel
-    for (int k = 0; k < KPT; ++k) {
-      const int i = threadIdx.x + k * kBlock;
-      const unsigned long long b = wave_reserve(&ctr->n_complex, i < nloci ? 1u : 0u);
-      if (i < nloci && b < cand_cap) cand[b] = ComplexItem{(int32_t)blockIdx.x, L0 + i, 1};
-    }
-    return;
-  }
-  uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
-  for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int i = threadIdx.x; i < T; i += blockDim.x) marg[i] = 0.0f;
+  const int part = kPartsCols + (int)(blockIdx.x & (kPartsWalk - 1));
+  const unsigned long long pbase = og.slot(1, part, 0), pcap = og.capB[1];
   if (threadIdx.x < 128) {
     eq[threadIdx.x] = exp2f(-0.33219281f * (float)threadIdx.x);
     lsq[threadIdx.x] = log1pf(-eq[threadIdx.x]);
   }
+  const int64_t n_list = (int64_t)ctr->n_slow;
+  unsigned visited = 0;
+  for (int64_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+  const int32_t tile = list[li];
+  const Tile tt = tiles_t[tile], tn = tiles_n[tile];
+  const int32_t L0 = tt.L0, L1 = tt.L1;
+  const int nloci = L1 - L0;
+  const bool wide = (tt.re - tt.rb) >= 65535 || (tn.re - tn.rb) >= 65535;
+  if (wide) {  // 16-bit counters could overflow: every locus goes to the exact kernel
+    for (int k = 0; k < KPT; ++k) {
+      const int i = threadIdx.x + k * kBlock;
+      const unsigned long long b = wave_reserve(&ctr->part[1][part], i < nloci ? 1u : 0u);
+      if (i < nloci && b < pcap) cand[pbase + b] = ComplexItem{tile, L0 + i, 1};
+    }
+    continue;
+  }
+  uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
+  __syncthreads();  // the previous tile's readers are done
+  for (int i = threadIdx.x; i < W_N * S / 4; i += blockDim.x) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = threadIdx.x; i < T; i += blockDim.x) marg[i] = 0.0f;
   __syncthreads();
   {
     GermSink<T, 0> sink{cnt, L0, &ctr->err, &ctr->err_pos};
@@ -258,8 +267,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       if (((tflag >> k) & 1u) || dn > 0) ++visited;
       q = ((tflag >> (8 + k)) & 1u) && dn > 0;
     }
-    const unsigned long long b = wave_reserve(&ctr->n_complex, q ? 1u : 0u);
-    if (q && b < cand_cap) cand[b] = ComplexItem{(int32_t)blockIdx.x, L0 + i, 0};
+    const unsigned long long b = wave_reserve(&ctr->part[1][part], q ? 1u : 0u);
+    if (q && b < pcap) cand[pbase + b] = ComplexItem{tile, L0 + i, 0};
+  }
   }
   __shared__ unsigned red;
   if (threadIdx.x == 0) red = 0;
@@ -972,7 +982,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
                                                        const ComplexItem *__restrict__ items, DevReads RT,
                                                        DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
                                                        unsigned long long rec_cap, uint8_t *__restrict__ pool,
-                                                       unsigned long long pool_cap, unsigned long long cand_cap,
+                                                       unsigned long long pool_cap, OutGeom og,
                                                        Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out,
                                                        unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
                                                        const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
@@ -987,11 +997,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const unsigned long long n_items =
-      amb_in ? (unsigned long long)n_amb_in : (ctr->n_complex < cand_cap ? ctr->n_complex : cand_cap);
+  // candidates: the partitioned items of somatic_proj / somatic_tile (part_scan: kept counts)
+  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
   for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
     const int64_t it = amb_in ? amb_in[li].item : li;
-    const ComplexItem item = items[it];
+    const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
     const int32_t pos = item.pos;
     const int32_t win = sw.range_win[tt.range];
@@ -1119,6 +1129,60 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   }
 }
 
+// Exclusive offsets of the candidate partitions (clamped to their capacities), the total in
+// n_complex and the largest overflow in part_max[1] (part_scan of gq_pileup.hip, which = 1).
+__global__ __launch_bounds__(1024) void part_scan_som(Counters *ctr, OutGeom og) {
+  constexpr int PER = kParts / 1024;
+  __shared__ unsigned long long s[1024];
+  __shared__ unsigned long long mx;
+  const int t = threadIdx.x;
+  unsigned long long v[PER], sum = 0, m = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const unsigned long long x = ctr->part[1][t * PER + j];
+    const unsigned long long cap = og.cap(1, t * PER + j);
+    m = x > cap && x - cap > m ? x - cap : m;
+    v[j] = x < cap ? x : cap;
+    sum += v[j];
+  }
+  if (t == 0) mx = 0;
+  s[t] = sum;
+  __syncthreads();
+  if (m) atomicMax(&mx, m);
+  for (int d = 1; d < 1024; d <<= 1) {
+    const unsigned long long y = t >= d ? s[t - d] : 0ull;
+    __syncthreads();
+    s[t] += y;
+    __syncthreads();
+  }
+  unsigned long long o = s[t] - sum;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    ctr->part_off[1][t * PER + j] = o;
+    o += v[j];
+  }
+  if (t == 1023) {
+    ctr->part_off[1][kParts] = s[t];
+    ctr->n_complex = s[t];
+    ctr->part_max[1] = mx;
+  }
+}
+
+gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq) {
+  if (t->mproj && t->mproj_mapq == min_mapq) return GQ_OK;
+  if (!t->mproj) {
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)(2 * t->proj_bytes + 32)));
+    t->mproj = p;
+  }
+  if (t->d.n_reads > 0)
+    hipLaunchKernelGGL(mproj_fill, dim3((unsigned)((t->d.n_reads + 255) / 256)), dim3(256), 0, c->stream, t->d, min_mapq,
+                       (int16_t *)t->mproj);
+  HIP_TRY(hipGetLastError());
+  t->mproj_mapq = min_mapq;
+  return GQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1133,10 +1197,11 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
   const auto h0 = std::chrono::steady_clock::now();
   c->timings = gq_timings{};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  // one loci plan per sample, 512-locus tiles aligned to 512-locus blocks (somatic_proj)
   Plan pt, pn;
-  gq_status st = plan(c, t, loci, kSomT, pt, c->tiles);
+  gq_status st = plan(c, t, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;
-  st = plan(c, n, loci, kSomT, pn, c->tiles2);
+  st = plan(c, n, loci, SomProjCfg::kT, pn, c->tiles2, 0, 0, 0, true);
   if (st) return st;
   gq_somatic_calls *res = (gq_somatic_calls *)calloc(1, sizeof(gq_somatic_calls));
   if (!res) return set_err(GQ_E_NOMEM, "calloc");
@@ -1199,29 +1264,62 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     HIP_TRY(hipStreamSynchronize(c->stream));  // wi (host) outlives its copy
     sw = SomWin{(const int32_t *)(b + o_rw), d_wi, d_reads, d_rank};
   }
-  unsigned long long cand_cap = std::max<unsigned long long>(1 << 16, pt.n_loci / 4);
+  // the tumor's margin projection for this mapq filter (derived once per read set and filter)
+  st = ensure_margin_projection(c, t, (int)p->min_mapq);
+  if (st) {
+    free(res);
+    return st;
+  }
+  // candidates: one output partition per somatic_proj workgroup (capA) and per somatic_tile
+  // block (capB), grown on overflow (part_scan's part_max)
+  OutGeom og{};
+  {
+    if (c->n_cu <= 0 &&
+        hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+      c->n_cu = 256;
+    if (c->som_wg_per_cu <= 0) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj, SomProjCfg::kThreads, 0) != hipSuccess || nb <= 0)
+        nb = 4;
+      c->som_wg_per_cu = nb;
+    }
+    og.ncols = (int)std::max<int64_t>(1, std::min<int64_t>({(pt.n_tiles + SomProjCfg::kWaves - 1) / SomProjCfg::kWaves,
+                                                           (int64_t)c->som_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
+    const unsigned long long wg_loci = (unsigned long long)((pt.n_tiles + og.ncols - 1) / og.ncols) * SomProjCfg::kT;
+    og.capA[1] = wg_loci / 16 + 256;
+    og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;
+  }
   unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
-    HIP_TRY(c->cplx.ensure(cand_cap * sizeof(ComplexItem)));
+    HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
     HIP_TRY(c->srecs.ensure(rec_cap * sizeof(SomRec)));
     HIP_TRY(c->pool.ensure(pool_cap));
+    HIP_TRY(c->slow.ensure((size_t)pt.n_tiles * sizeof(int32_t)));
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL((somatic_tile<kSomT>), dim3((unsigned)pt.n_tiles), dim3(kBlock), 0, c->stream,
-                       (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, t->d, n->d, (ComplexItem *)c->cplx.p,
-                       cand_cap, (int)p->min_mapq, ctr);
+    hipLaunchKernelGGL(somatic_proj, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
+                       (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                       (int32_t *)c->slow.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((somatic_tile<SomProjCfg::kT>), dim3((unsigned)std::min<int64_t>(pt.n_tiles, 2048)), dim3(kBlock), 0,
+                       c->stream, (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, t->d, n->d,
+                       (ComplexItem *)c->cplx.p, og, (const int32_t *)c->slow.p, (int)p->min_mapq, ctr);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(part_scan_som, dim3(1), dim3(1024), 0, c->stream, ctr, og);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    {  // candidate overflow: grow and re-run the tile kernel before the (costly) caller runs
-      unsigned long long nc = 0;
-      HIP_TRY(hipMemcpyAsync(&nc, &ctr->n_complex, sizeof(nc), hipMemcpyDeviceToHost, c->stream));
+    {  // candidate overflow: grow and re-run the tile kernels before the (costly) caller runs
+      unsigned long long pm = 0;
+      HIP_TRY(hipMemcpyAsync(&pm, &ctr->part_max[1], sizeof(pm), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
-      if (nc > cand_cap) {
-        cand_cap = nc + 1024;
+      if (pm) {
+        og.capA[1] += pm + 64;
+        og.capB[1] += pm + 64;
         if (attempt == 2) {
           free(res);
           return set_err(GQ_E_CAPACITY, "candidate capacity retries exhausted");
@@ -1232,17 +1330,13 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
     hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
-                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr, sw,
+                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                        (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     bool retry = false;
-    if (hc.n_complex > cand_cap) {
-      cand_cap = hc.n_complex + 1024;
-      retry = true;
-    }
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;
       retry = true;
@@ -1262,7 +1356,7 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
       const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 8192);
       hipLaunchKernelGGL(somatic_call, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                          (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
-                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, cand_cap, ctr, sw,
+                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                          (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
                          (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
       HIP_TRY(hipGetLastError());

@@ -1,0 +1,398 @@
+// gq_somatic_proj.h — somatic candidate loci over the read projections (somatic_proj), and
+// the tumor's margin projection it reads (mproj_fill).  Included inside gq_somatic.hip's
+// anonymous namespace.
+//
+// somatic_proj restates somatic_tile's per-locus test (SomaticStandardCaller.scala:184-206: the
+// tumor pileup must hold a non-Match element, the normal pileup must be non-empty; loci whose
+// tumor pileup provably has the hom-ref genotype as its maximum-likelihood genotype are dropped,
+// hom_ref_margin_lane) on germline_proj's machinery: one wave per 512-locus tile, lane l owns the
+// 8-locus column [B0 + 8l, B0 + 8l + 8), groups of 16 lanes walk the tumor reads of their
+// 128-locus sub-span and add, per read and column, the projection's base codes (SWAR nibble
+// counts) and the margin projection's 16-bit terms (saturating packed adds).  The tumor's MD
+// events, N bases and complex ranges come from its sparse entries, the normal's depth from its
+// reads' [start, end) intervals (every locus a read spans holds one of its elements,
+// PileupElement.scala:68-135) as a difference array.  Tiles the projection cannot take go to
+// somatic_tile (lane-per-read walker).
+#pragma once
+
+#include "gq_kernels.h"
+
+// The margin term of one tumor element (hom_ref_margin_lane's t, in units of 1/256, rounded
+// down; INT16_MIN when it is below -127 or -inf), so that a sum of terms never exceeds the
+// margin it stands for: a sum that passes the bound proves what the FP32 sum proved.
+__device__ __forceinline__ int16_t margin_term(bool match, int q, float em, float lsm) {
+  constexpr float kLn2 = 0.69314718f;
+  if (q < 0) return (int16_t)-32768;  // outside the quality table: no bound
+  const float eb = exp2f(-0.33219281f * (float)q);
+  const float lsq = log1pf(-eb);
+  const float f = eb + em - eb * em;  // 1 - pc
+  const float t = match ? kLn2 + lsq + lsm - fmaxf(0.0f, kLn2 + __logf(f)) : __logf(f);
+  if (!(t > -127.0f)) return (int16_t)-32768;
+  const float v = floorf(t * 256.0f) - 1.0f;  // -1: room for the FP32 rounding of t
+  return (int16_t)(v > 32767.0f ? 32767.0f : v);
+}
+
+// The margin projection of the tumor reads, laid out as `proj` (int16 per locus): thread per
+// 8-locus word, 256 reads per block.  Reads the mapq filter drops (QualityAlignedReadsFilter,
+// PileupElementsFilter.scala:25-36) and non-Match/Mismatch loci hold 0.
+__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int min_mapq, int16_t *__restrict__ mproj) {
+  __shared__ int64_t wb[257];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int t = threadIdx.x;
+  // word offsets of the block's reads (their projections are consecutive in the pool)
+  const int64_t w0 = (R.prec[min(r0, R.n_reads)].base + 8 * (int64_t)R.prec[min(r0, R.n_reads)].col0) >> 3;
+  {
+    const int64_t r = min(r0 + t, R.n_reads);
+    wb[t] = ((R.prec[r].base + 8 * (int64_t)R.prec[r].col0) >> 3) - w0;
+    if (t == 0) {
+      const int64_t rl = min(r0 + 256, R.n_reads);
+      wb[256] = ((R.prec[rl].base + 8 * (int64_t)R.prec[rl].col0) >> 3) - w0;
+    }
+  }
+  __syncthreads();
+  const int64_t W = wb[256];
+  for (int64_t w = t; w < W; w += 256) {
+    int lo = 0, hi = 255;
+    while (lo < hi) {
+      const int m = (lo + hi + 1) >> 1;
+      if (wb[m] <= w) lo = m;
+      else hi = m - 1;
+    }
+    const int64_t r = r0 + lo, j = w - wb[lo];
+    const ColDesc d = R.cdesc[r];
+    const int32_t s = d.start;
+    const int32_t lb = 8 * ((s >> 3) + (int32_t)j);
+    int16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int mq = (int)R.mapq[r];
+    if (!(min_mapq > 0 && mq < min_mapq)) {
+      const float em = exp2f(-0.33219281f * (float)mq);
+      const float lsm = log1pf(-em);
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+      const uint32_t *ev = R.md_ev + R.md_off[r];
+      // MD events at offsets >= lb - s (sorted)
+      int k = 0, hi2 = nmd;
+      while (k < hi2) {
+        const int m = (k + hi2) >> 1;
+        if ((int32_t)(ev[m] >> 8) < lb - s) k = m + 1;
+        else hi2 = m;
+      }
+      auto term_at = [&](int q8, int32_t l, int64_t p) {  // element at locus l, base / quality at pool offset p
+        const int32_t off = l - s;
+        while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
+        const bool event = k < nmd && (int32_t)(ev[k] >> 8) == off;
+        const int q = (int)(int8_t)R.qual[p];
+        v[q8] = margin_term(!event, q, em, lsm);
+      };
+      if (d.info & kColEligible) {
+        const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+        for (int q8 = 0; q8 < 8; ++q8) {
+          const int32_t l = lb + q8;
+          if (l >= s && l < d.end) term_at(q8, l, p0 + l);
+        }
+      } else {  // general CIGAR: the count segments
+        const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+        const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+        const int64_t so = R.seq_off[r];
+        for (int q8 = 0; q8 < 8; ++q8) {
+          const int32_t l = lb + q8;
+          for (int32_t q2 = 0; q2 < nseg; ++q2) {
+            const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+            const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
+            if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
+              term_at(q8, l, so + (int32_t)(b & 0xFFFFu) + (l - ra));
+              break;
+            }
+          }
+        }
+      }
+    }
+    uint4 o;
+    o.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
+    o.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
+    o.z = (uint32_t)(uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16);
+    o.w = (uint32_t)(uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16);
+    *reinterpret_cast<uint4 *>(mproj + 8 * (w0 + w)) = o;
+  }
+}
+
+struct SomProjCfg {
+  static constexpr int kT = 512;
+  static constexpr int kWaves = 4;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kU = 4;
+  static constexpr int kMaxRows = 255;
+  static constexpr int kRecCap = 384;  // tumor reads per tile window (60x: ~270)
+  static constexpr int kRecBuf = kRecCap + 1;
+  static constexpr int kEnt = 6;
+};
+
+__device__ __forceinline__ unsigned som_reserve_lds(unsigned *ctr, unsigned n) {  // every lane active
+  const uint32_t x = wave_incl_scan(n);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  unsigned base = 0;
+  if ((threadIdx.x & 63) == 63 && total) base = atomicAdd(ctr, total);
+  base = (unsigned)__builtin_amdgcn_readlane((int)base, 63);
+  return base + x - n;
+}
+
+typedef short gq_short2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t add_sat2(uint32_t a, uint32_t b) {  // v_pk_add_i16 clamp
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(__builtin_bit_cast(gq_short2, a),
+                                                                     __builtin_bit_cast(gq_short2, b)));
+}
+
+__global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void somatic_proj(
+    const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, int64_t n_tiles, DevReads RT,
+    const int16_t *__restrict__ mproj, const int32_t *__restrict__ n_start, const int32_t *__restrict__ n_end,
+    ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow) {
+  using C = SomProjCfg;
+  constexpr int T = C::kT, U = C::kU;
+  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // tumor event read bases: A C T G bytes
+  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
+  __shared__ __attribute__((aligned(16))) uint32_t cvw[C::kWaves][T];  // normal coverage differences
+  __shared__ __attribute__((aligned(16))) uint2 recw[C::kWaves][C::kRecBuf];
+  __shared__ unsigned outn[2];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint32_t *ev = evw[wave], *mk = mkw[wave], *cv = cvw[wave];
+  uint2 *rec = recw[wave];
+  {
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+          *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
+    e4[0] = e4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (threadIdx.x < 2) outn[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
+  const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
+  const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
+  const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
+  unsigned visited = 0;
+  const int g = lane >> 4;
+  const uint4 *prec4 = reinterpret_cast<const uint4 *>(RT.prec);
+  for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
+    const Tile tt = tiles_t[i], tn = tiles_n[i];
+    const int32_t L0 = tt.L0, L1 = tt.L1;
+    const int64_t rb = tt.rb, re = tt.re;
+    const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
+    const int64_t nwin = re - rb;
+    if (nwin > C::kRecCap || (tn.re - tn.rb) >= 65535) {
+      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
+      continue;
+    }
+    const int nrd = (int)nwin;
+    // ---- tumor: read records (LDS), group ranges, the first sparse entries (as germline_proj)
+    const uint4 pr0 = prec4[rb], pr1 = prec4[re];
+    const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
+    const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
+    const int64_t e0 = RT.pev_off[rb], e1 = RT.pev_off[re];
+    const uint32_t ybias = (uint32_t)(8 * C0) - (uint32_t)tb;
+    constexpr int NQ = (C::kRecCap + 63) / 64, NE = C::kEnt;
+    int32_t pe[NQ];
+    uint4 pp[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      pe[q] = 0x7FFFFFFF;
+      pp[q] = make_uint4(0x7FFFFFFFu, 0u, 0u, 0u);
+      if (64 * q + lane < nrd) {
+        pe[q] = RT.pmax_end[rb + 64 * q + lane];
+        pp[q] = prec4[rb + 64 * q + lane];
+      }
+    }
+    uint2 ent[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int64_t k = e0 + 64 * j + lane;
+      ent[j] = make_uint2(0x80000000u, kPevNone);
+      if (k < e1) ent[j] = RT.pev[k];
+    }
+    bool bad = false;
+    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (64 * q >= nrd) break;
+      const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
+      if (64 * q + lane < nrd)
+        rec[64 * q + lane] = make_uint2((uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16), pp[q].z + ybias);
+      bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
+      lo0 += (int)__popcll(__ballot(pe[q] <= B0));
+      lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
+      lo2 += (int)__popcll(__ballot(pe[q] <= B0 + 256));
+      lo3 += (int)__popcll(__ballot(pe[q] <= B0 + 384));
+      hi0 += (int)__popcll(__ballot(c0 < C0 + 16));
+      hi1 += (int)__popcll(__ballot(c0 < C0 + 32));
+      hi2 += (int)__popcll(__ballot(c0 < C0 + 48));
+      hi3 += (int)__popcll(__ballot(c0 < C0 + 64));
+    }
+    const int nmax = max(max(hi0 - lo0, hi1 - lo1), max(hi2 - lo2, hi3 - lo3));
+    if (bad || nmax > C::kMaxRows) {
+      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
+      continue;
+    }
+    const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
+    const int hi_me = g == 0 ? hi0 : g == 1 ? hi1 : g == 2 ? hi2 : hi3;
+    if (lane == 0) rec[nrd] = make_uint2(0u, 0u);
+    // ---- tumor column counts and margin sums (16-bit pairs, loci 2k, 2k + 1 in msum[k])
+    uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
+    uint32_t msum[4] = {0, 0, 0, 0};
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(RT.proj + tb), (short)0, (int)(te - tb), 0x00020000);
+    const __amdgpu_buffer_rsrc_t msrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(mproj + tb), (short)0, (int)(2 * (te - tb)), 0x00020000);
+    const uint32_t l8 = 8u * (uint32_t)lane;
+    uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
+    int nn = 0;
+    auto fold = [&]() {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ca[h] += nac[h] & 0x0F0F0F0Fu;
+        cc[h] += (nac[h] >> 4) & 0x0F0F0F0Fu;
+        ct[h] += ntg[h] & 0x0F0F0F0Fu;
+        cg[h] += (ntg[h] >> 4) & 0x0F0F0F0Fu;
+        nac[h] = ntg[h] = 0;
+      }
+      nn = 0;
+    };
+    auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {
+      uint2 rv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t d = lane - (int32_t)(int16_t)(rv[u].x & 0xFFFFu);
+        const uint32_t voff = (uint32_t)d < (rv[u].x >> 16) ? rv[u].y + l8 : 0x80000000u;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(voff == 0x80000000u ? voff : 2 * voff), 0, 0);
+        w[u] = make_uint2(a[0], a[1]);
+        m[u] = make_uint4(b[0], b[1], b[2], b[3]);
+      }
+    };
+    auto count = [&](const uint2 (&w)[U], const uint4 (&m)[U]) {
+      if (nn + U > 15) fold();
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].x);
+        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].x);
+        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].y);
+        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].y);
+        msum[0] = add_sat2(msum[0], m[u].x);
+        msum[1] = add_sat2(msum[1], m[u].y);
+        msum[2] = add_sat2(msum[2], m[u].z);
+        msum[3] = add_sat2(msum[3], m[u].w);
+      }
+      nn += U;
+    };
+    uint2 aw[U], bw[U];
+    uint4 am[U], bm[U];
+    issue(0, aw, am);
+    // ---- tumor sparse entries, one lane per entry (germline_proj's encoding)
+    auto apply = [&](uint2 p) {
+      const int32_t l = (int32_t)p.x;
+      if (p.y & kPevComplex) {
+        const int64_t a = max((int64_t)l, (int64_t)B0);
+        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+        if (a < b) {
+          atomicAdd(&mk[a - B0], 1u << 16);
+          if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
+        }
+      } else if (l >= B0 && l < B0 + T) {
+        const uint32_t mm = p.y & 15u, c = (p.y >> 4) & 7u;
+        if (mm) atomicOr(&mk[l - B0], mm);
+        if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
+        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < NE; ++j) apply(ent[j]);
+    for (int64_t q = e0 + 64 * NE; q < e1; q += 64) {
+      const int64_t k = q + lane;
+      if (k < e1) apply(RT.pev[k]);
+    }
+    // ---- normal depth: each read spans [start, end) (any element), as +1 / -1 differences
+    for (int64_t q = tn.rb; q < tn.re; q += 64) {
+      const int64_t r = q + lane;
+      if (r < tn.re) {
+        const int32_t a = max(n_start[r], B0), b = min(n_end[r], B0 + T);
+        if (a < b) {
+          atomicAdd(&cv[a - B0], 1u);
+          if (b < B0 + T) atomicAdd(&cv[b - B0], 0xFFFFFFFFu);
+        }
+      }
+    }
+    for (int k0 = 0;; k0 += 2 * U) {  // rows past the group's are clamped (zero words)
+      issue(k0 + U, bw, bm);
+      count(aw, am);
+      issue(k0 + 2 * U, aw, am);
+      count(bw, bm);
+      if (k0 + 2 * U >= nmax) break;
+    }
+    fold();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- decision: candidate loci (somatic_tile's test)
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+          *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
+    uint32_t e8[8], m8[8], v8[8];
+    {
+      const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1], va = c4[0], vb = c4[1];
+      e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
+      m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
+      v8[0] = va.x, v8[1] = va.y, v8[2] = va.z, v8[3] = va.w, v8[4] = vb.x, v8[5] = vb.y, v8[6] = vb.z, v8[7] = vb.w;
+      e4[0] = e4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    int32_t run_c = 0, run_n = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      run_c += (int32_t)m8[j] >> 16;
+      run_n += (int32_t)v8[j];
+    }
+    int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run_c) - run_c;
+    int32_t dn_run = (int32_t)wave_incl_scan((uint32_t)run_n) - run_n;
+    uint32_t qmask = 0, nq = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int32_t l = B0 + 8 * lane + j;
+      const bool in = l >= L0 && l < L1;
+      const int h = j >> 2, sh = 8 * (j & 3);
+      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
+      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
+      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+      ncx_run += (int32_t)m8[j] >> 16;
+      dn_run += (int32_t)v8[j];
+      const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
+      const uint32_t depth = cA + cC + cT + cG + nN + ncx;
+      const uint32_t ew = e8[j];
+      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
+                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+      const uint32_t low = mask & (0u - mask);
+      const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
+                             nN * (low == 0u ? 1u : 0u);
+      const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
+      const bool nonmatch = (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
+      const int16_t m16 = (int16_t)((msum[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+      const bool bound = single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
+      const bool tcand = depth > 0 && nonmatch && !bound;
+      visited += (in && (depth > 0 || dn_run > 0)) ? 1u : 0u;
+      const bool q = in && tcand && dn_run > 0;
+      qmask |= q ? 1u << j : 0u;
+      nq += q ? 1u : 0u;
+    }
+    if (__ballot(qmask != 0) != 0) {
+      unsigned kq = som_reserve_lds(&outn[1], nq);
+      for (int j = 0; j < 8; ++j)
+        if ((qmask >> j) & 1u) {
+          if (kq < ccap) cand[cbase + kq] = ComplexItem{(int32_t)i, B0 + 8 * lane + j, 0};
+          ++kq;
+        }
+    }
+  }
+  // visited loci into the spread counters, this workgroup's candidate count
+  __shared__ unsigned red;
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  if (visited) atomicAdd(&red, visited);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (red) atomicAdd(&ctr->spread[0][blockIdx.x & (kSpread - 1)], (unsigned long long)red);
+    ctr->part[1][blockIdx.x] = outn[1];
+  }
+}
