@@ -48,7 +48,6 @@ def rank_pieces(world: int, rank: int, wgs: bool):
     from guacamole_amd.genomes import B37
     from guacamole_amd.loci import LociSet, partition_loci_uniformly
     budget = None if wgs else world * CHR20
-    b = LociSet.parse("all")
     lengths = {}
     ranges = []
     for name, ln in B37:  # already lexicographic
@@ -156,10 +155,11 @@ def main() -> int:
     elapsed = time.perf_counter() - t
     if dist is not None:
         import torch
-        x = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
+        dev = "cuda:%d" % local if backend == "nccl" else "cpu"
+        x = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         elapsed = float(x.item())
-        v = torch.tensor([int(calls.visited_loci)], dtype=torch.int64, device="cuda:%d" % local)
+        v = torch.tensor([int(calls.visited_loci)], dtype=torch.int64, device=dev)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
         loci_total = int(v.item())
     else:
