@@ -63,13 +63,20 @@ def germline_threshold_reads(ctx: native.Context, rs: ReadSet, loci, threshold: 
 
 
 def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet, loci, _gather=None,
-                           **params) -> Optional[List[dict]]:
-    """pileupFlatMapTwoRDDs(tumor, normal, partitions, skipEmpty=true, findPotentialVariantAtLocus)
-    + the driver's filters on the GPU.  Rows as the oracle's somatic_standard (contig by name).
+                           reference=None, **params) -> Optional[List[dict]]:
+    """pileupFlatMapTwoRDDs(tumor, normal, partitions, skipEmpty=true, findPotentialVariantAtLocus,
+    referenceGenome) + the driver's filters on the GPU.  Rows as the oracle's somatic_standard
+    (contig by name).  reference: a reference.ReferenceGenome (--reference-fasta) or None.
     _gather: the gather device of a multi-GPU run (rank 0 gets every rank's rows, others None)."""
     if tumor.contig_names != normal.contig_names:
         raise ValueError("tumor and normal reads must share the contig list")
-    calls = ctx.somatic_standard(device_reads(ctx, tumor), device_reads(ctx, normal), loci, **params)
+    dref = None if reference is None else ctx.upload_reference(reference.for_contigs(tumor.contig_names))
+    try:
+        calls = ctx.somatic_standard(device_reads(ctx, tumor), device_reads(ctx, normal), loci, reference=dref,
+                                     **params)
+    finally:
+        if dref is not None:
+            dref.free()
     per_rank = [calls] if _gather is None else gather_somatic(calls, _gather)
     if per_rank is None:
         return None
@@ -85,6 +92,18 @@ def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet,
 # ---------------------------------------------------------------------------------------------
 # CLI
 def _common_args(p: argparse.ArgumentParser) -> None:
+    """Common.Arguments (Common.scala:48-136): Base, Loci, NoSequenceDictionary,
+    ReadLoadingConfigArgs, GenotypeOutput, DistributedUtil.Arguments."""
+    p.add_argument("--debug", action="store_true", help="If set, prints a higher level of debug output.")
+    p.add_argument("--no-sequence-dictionary", action="store_true",
+                   help="If set, get contigs and lengths directly from reads instead of from sequence dictionary.")
+    p.add_argument("--recompute-md-tags", action="store_true",
+                   help="Use the reference fasta to recompute the MD Tags on all mapped reads")
+    p.add_argument("--bam-reader-api", default="best", help="(accepted; the native reader is always used)")
+    p.add_argument("--out-chunks", type=int, default=1,
+                   help="When writing out to json format, number of chunks to coalesce the genotypes into.")
+    p.add_argument("--max-genotypes", type=int, default=0,
+                   help="Maximum number of genotypes to output. 0 (default) means output all genotypes.")
     p.add_argument("--loci", default="", help="Loci at which to call variants (e.g. 'all', 'chr1:0-1000,chr2')")
     p.add_argument("--loci-from-file", default="", help="Path to file giving loci")
     p.add_argument("--out", default="", help="Output path (.vcf or .json; empty = JSON to stdout)")
@@ -106,9 +125,15 @@ def _loci_builder(args) -> LociSetBuilder:
     return LociSet.parse("all")
 
 
-def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None) -> None:
-    """Common.writeVariantsFromArguments (Common.scala:246-304): JSON for "" / .json, else VCF."""
+def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None, max_genotypes: int = 0) -> None:
+    """Common.writeVariantsFromArguments (Common.scala:246-304): JSON for "" / .json, else VCF.
+    --max-genotypes reaches RDD.sample(false, maxGenotypes, 0) as the sampling FRACTION
+    (Common.scala:247-249): 1 keeps every genotype, larger values are refused by Spark's
+    Bernoulli sampler ("must be on interval [0, 1]"), as here.  --out-chunks only coalesces
+    partitions (order-preserving), so it does not change what is written."""
     from .output import write_json, write_vcf
+    if max_genotypes > 1:
+        raise ValueError("Sampling fraction (%s) must be on interval [0, 1]" % float(max_genotypes))
     if path.lower().endswith(".vcf"):
         write_vcf(path, genotypes, contig_lengths)
     else:
@@ -126,7 +151,11 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     args = p.parse_args(argv)
     rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
-    rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True))
+    # germline-threshold takes no reference (GermlineThresholdCaller.scala:64-70): with
+    # --recompute-md-tags read loading fails (Read.scala:223-225)
+    rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True),
+                    recompute_md=args.recompute_md_tags,
+                    contig_lengths_from_dictionary=not args.no_sequence_dictionary)
     loci = builder.result(rs.contig_lengths_map)
     parts = partition(loci, args.parallelism if args.parallelism > 0 else world, args.partition_accuracy, rs)
     flat = flatten_partitions(parts, rs.contig_index())
@@ -145,7 +174,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     from .output import germline_genotype
     out = [germline_genotype(c, l, rs.sample_names[s] if s < len(rs.sample_names) else "default", gt, ref, alt)
            for c, l, s, gt, ref, alt, fl in rows]
-    _write_genotypes(args.out, out, rs.contig_lengths_map)
+    _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
     print("Called %d genotypes." % len(out), file=sys.stderr)
     return _finish_rank(0)
 
@@ -170,13 +199,21 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     p.add_argument("--max-tumor-read-depth", type=int, default=2 ** 31 - 1)
     p.add_argument("--min-tumor-alternate-read-depth", type=int, default=0)
     p.add_argument("--max-median-mismatches", type=int, default=2 ** 31 - 1)
+    p.add_argument("--reference-fasta", default="", help="Local path to a reference FASTA file")
+    p.add_argument("--dbsnp-vcf", default="", help="VCF file to identify DBSNP variants")
     _common_args(p)
     args = p.parse_args(argv)
     rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
     f = InputFilters.make(overlaps_loci=builder, non_duplicate=True, passed_vendor_quality_checks=True,
                           has_md_tag=True)
-    tumor, normal = load_reads(args.tumor_reads, f), load_reads(args.normal_reads, f)
+    reference = None
+    if args.reference_fasta:  # SomaticStandardCaller.scala:75
+        from .reference import ReferenceGenome
+        reference = ReferenceGenome.load_fasta(args.reference_fasta)
+    tumor, normal = [load_reads(path, f, reference=reference, recompute_md=args.recompute_md_tags,
+                                contig_lengths_from_dictionary=not args.no_sequence_dictionary)
+                     for path in (args.tumor_reads, args.normal_reads)]
     if tumor.contig_lengths_map != normal.contig_lengths_map:
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
     loci = builder.result(normal.contig_lengths_map)
@@ -196,13 +233,16 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         min_likelihood=args.min_likelihood, min_vaf=args.min_vaf,
         min_average_mapping_quality=args.min_average_mapping_quality,
         min_average_base_quality=args.min_average_base_quality, max_median_mismatches=args.max_median_mismatches,
-        apply_filters=1, _gather=gdev if world > 1 else None)
+        apply_filters=1, _gather=gdev if world > 1 else None, reference=reference)
     if rows is None:
         return _finish_rank(0)
+    if args.dbsnp_vcf:  # SomaticStandardCaller.scala:139-149
+        from .output import dbsnp_join, read_dbsnp_vcf
+        rows = dbsnp_join(rows, read_dbsnp_vcf(args.dbsnp_vcf))
     from .output import somatic_genotype
     sample = tumor.sample_names[0] if tumor.sample_names else "default"
     out = [somatic_genotype(r["contig"], r, sample) for r in rows]
-    _write_genotypes(args.out, out, tumor.contig_lengths_map)
+    _write_genotypes(args.out, out, tumor.contig_lengths_map, args.max_genotypes)
     print("Called %d somatic genotypes." % len(out), file=sys.stderr)
     return _finish_rank(0)
 

@@ -175,7 +175,8 @@ template <int T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void somatic_tile(const Tile *__restrict__ tiles_t,
                                                        const Tile *__restrict__ tiles_n, DevReads RT, DevReads RN,
                                                        ComplexItem *__restrict__ cand, OutGeom og,
-                                                       const int32_t *__restrict__ list, int min_mapq, Counters *ctr) {
+                                                       const int32_t *__restrict__ list, int min_mapq, Counters *ctr,
+                                                       RefView ref) {
   constexpr int S = T + 2 * kGuard;
   constexpr int KPT = T / kBlock;  // loci per thread
   static_assert(KPT <= 8, "per-thread flag bits");
@@ -238,9 +239,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (cG > (etg >> 16)) mask |= 8u;
     const int rc = mask ? (__ffs((int)mask) - 1) : 4;
     const uint32_t c_ref = rc == 0 ? cA : rc == 1 ? cC : rc == 2 ? cT : rc == 3 ? cG : cN;
-    if (__popc(mask) > 1 || cx > 0 || depth > c_ref) {
+    const bool agree = !ref.b || ref_agrees(mask, ref.b[ref.off[tt.contig] + L0 + i]);
+    if (!agree || __popc(mask) > 1 || cx > 0 || depth > c_ref) {
       // single-base elements only, one standard reference base, no N: the hom-ref bound applies
-      const bool bound = __popc(mask) == 1 && cx == 0 && cN == 0 && marg[i] > 0.02f + 2e-4f * (float)depth;
+      const bool bound = agree && __popc(mask) == 1 && cx == 0 && cN == 0 && marg[i] > 0.02f + 2e-4f * (float)depth;
       if (!bound) tflag |= 1u << (8 + k);
     }
   }
@@ -985,10 +987,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
                                                        unsigned long long pool_cap, OutGeom og,
                                                        Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out,
                                                        unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
-                                                       const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+                                                       const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
+                                                       RefView ref) {
   // amb_in == nullptr: every candidate; where a sample's reads' MD-derived bases disagree the
   // locus is only listed (amb_out) for the heap-order replay.  amb_in != nullptr: the listed
   // loci, with both samples' reference bases resolved in heap order (amb_ref[2 i + set]).
+  // ref.b != nullptr: every pileup's reference base is the reference genome's (nothing listed).
   __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
   __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
   __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
@@ -1010,8 +1014,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     const Cover cn = make_cover(RN, tn.rb, tn.re, pos, cover_n[wv], ev_lds[wv], sw.wi[2 * win + 1], sw.init_reads,
                                 sw.init_rank, ctr);
     SamplePile PT, PN;
-    gather_sample(RT, ct, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li] : -1, ctr, PT);
-    gather_sample(RN, cn, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li + 1] : -1, ctr, PN);
+    const int fb = ref.b ? (int)ref.b[ref.off[tt.contig] + pos] : -1;
+    gather_sample(RT, ct, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li] : fb, ctr, PT);
+    gather_sample(RN, cn, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li + 1] : fb, ctr, PN);
+    if (fb >= 0) PT.ambiguous = PN.ambiguous = false;
     if (PT.overflow || PN.overflow) {
       raise_at(ctr, GQ_E_CAPACITY, pos);
       continue;
@@ -1185,14 +1191,132 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
 
 }  // namespace
 
+// A reference genome resident in HBM (ReferenceBroadcast.scala:39-55): the contigs of a read
+// set's contig list, each at a 512-aligned offset and padded with 'N' to a whole 512-locus block
+// past its end (somatic_proj reads 8 bases per lane of an aligned block).
+struct gq_reference {
+  int device = 0;
+  int32_t n_contigs = 0;
+  void *bytes = nullptr;
+  int64_t *d_off = nullptr;
+  std::vector<int64_t> off, len;  // host copies; off = -1 for a contig the reference lacks
+};
+
 extern "C" {
+
+gq_status gq_reference_upload(gq_ctx *c, int32_t n_contigs, const uint8_t *const *bases, const int64_t *lengths,
+                              gq_reference **out) {
+  if (!c || n_contigs < 0 || (n_contigs > 0 && (!bases || !lengths)) || !out)
+    return set_err(GQ_E_ARG, "gq_reference_upload: bad argument");
+  HIP_TRY(hipSetDevice(c->device));
+  gq_reference *r = new gq_reference();
+  r->device = c->device;
+  r->n_contigs = n_contigs;
+  r->off.assign((size_t)n_contigs, -1);
+  r->len.assign((size_t)n_contigs, -1);
+  int64_t tot = 0;
+  for (int32_t k = 0; k < n_contigs; ++k) {
+    if (!bases[k] || lengths[k] < 0) continue;
+    r->off[(size_t)k] = tot;
+    r->len[(size_t)k] = lengths[k];
+    tot += (lengths[k] + 1023) / 512 * 512;
+  }
+  auto fail = [&](gq_status st) {
+    gq_reference_free(r);
+    return st;
+  };
+  if (hipMalloc(&r->bytes, (size_t)std::max<int64_t>(tot, 512)) != hipSuccess ||
+      hipMalloc((void **)&r->d_off, sizeof(int64_t) * (size_t)std::max(n_contigs, 1)) != hipSuccess)
+    return fail(set_err(GQ_E_HIP, "gq_reference_upload: hipMalloc of %lld bytes failed", (long long)tot));
+  if (hipMemsetAsync(r->bytes, 'N', (size_t)std::max<int64_t>(tot, 512), c->stream) != hipSuccess)
+    return fail(set_err(GQ_E_HIP, "gq_reference_upload: memset failed"));
+  for (int32_t k = 0; k < n_contigs; ++k)
+    if (r->off[(size_t)k] >= 0 && lengths[k] > 0 &&
+        hipMemcpyAsync((uint8_t *)r->bytes + r->off[(size_t)k], bases[k], (size_t)lengths[k], hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess)
+      return fail(set_err(GQ_E_HIP, "gq_reference_upload: copy of contig %d failed", k));
+  if (n_contigs > 0 && hipMemcpyAsync(r->d_off, r->off.data(), sizeof(int64_t) * (size_t)n_contigs,
+                                      hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return fail(set_err(GQ_E_HIP, "gq_reference_upload: offsets copy failed"));
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(set_err(GQ_E_HIP, "gq_reference_upload: sync failed"));
+  *out = r;
+  return GQ_OK;
+}
+
+void gq_reference_free(gq_reference *r) {
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  if (r->bytes) (void)hipFree(r->bytes);
+  if (r->d_off) (void)hipFree(r->d_off);
+  delete r;
+}
 
 gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_reads *n, const gq_loci *loci,
                               const gq_somatic_params *p, gq_somatic_calls **out) {
+  return gq_somatic_standard_ref(c, t, n, loci, nullptr, p, out);
+}
+
+gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev_reads *n, const gq_loci *loci,
+                                  const gq_reference *ref, const gq_somatic_params *p, gq_somatic_calls **out) {
   if (!c || !t || !n || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_somatic_standard: null argument");
   if (t->d.n_contigs != n->d.n_contigs)
     return set_err(GQ_E_ARG, "tumor and normal read sets must share the contig list (%d vs %d contigs)",
                    t->d.n_contigs, n->d.n_contigs);
+  RefView rv{nullptr, nullptr};
+  std::vector<int32_t> lc;
+  std::vector<int64_t> ls, le, lt;
+  gq_loci trimmed{};
+  if (ref) {
+    // The reference looks a base up for every pileup (getReferenceBase, ReferenceBroadcast.scala:
+    // 26-30): a contig it lacks, or a locus past its end, fails the job where a read covers it.
+    // Loci no read reaches are trimmed away (no pileup forms there).
+    if (ref->n_contigs != t->d.n_contigs)
+      return set_err(GQ_E_ARG, "reference covers %d contigs, the read sets %d", ref->n_contigs, t->d.n_contigs);
+    if (ref->device != c->device) return set_err(GQ_E_ARG, "reference uploaded to another device");
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<int64_t> max_end((size_t)ref->n_contigs, -2);
+    auto reach = [&](int32_t ci) -> int64_t {  // largest read end on contig ci over both samples
+      if (max_end[(size_t)ci] != -2) return max_end[(size_t)ci];
+      int64_t m = -1;
+      for (const gq_dev_reads *sr : {t, n}) {
+        const int64_t b = sr->contig_read_begin[(size_t)ci], e = sr->contig_read_begin[(size_t)ci + 1];
+        if (e > b) {
+          int32_t v = 0;
+          if (hipMemcpy(&v, sr->d.pmax_end + (e - 1), sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+          m = std::max<int64_t>(m, v);
+        }
+      }
+      return max_end[(size_t)ci] = m;
+    };
+    for (int64_t k = 0; k < loci->n_ranges; ++k) {
+      const int32_t ci = loci->contig[k];
+      const int64_t s0 = loci->start[k];
+      int64_t e0 = loci->end[k];
+      if (e0 <= s0) continue;
+      if (ci < 0 || ci >= ref->n_contigs) return set_err(GQ_E_ARG, "loci range on contig %d: no such contig", ci);
+      const int64_t m = reach(ci);
+      if (m == -3) return set_err(GQ_E_HIP, "gq_somatic_standard_ref: read-extent copy failed");
+      if (ref->off[(size_t)ci] < 0) {
+        if (m > s0) return set_err(GQ_E_ARG, "contig %d does not exist in the current reference", ci);
+        continue;
+      }
+      const int64_t len = ref->len[(size_t)ci];
+      if (e0 > len) {
+        if (m > std::max(len, s0))
+          return set_err(GQ_E_ARG, "locus %lld of contig %d is past the end of the reference contig (length %lld)",
+                         (long long)std::max(len, s0), ci, (long long)len);
+        e0 = len;
+        if (e0 <= s0) continue;
+      }
+      lc.push_back(ci);
+      ls.push_back(s0);
+      le.push_back(e0);
+      lt.push_back(loci->task ? loci->task[k] : 0);
+    }
+    trimmed = gq_loci{(int64_t)lc.size(), lc.data(), ls.data(), le.data(), loci->task ? lt.data() : nullptr};
+    loci = &trimmed;
+    rv = RefView{(const uint8_t *)ref->bytes, ref->d_off};
+  }
   HIP_TRY(hipSetDevice(c->device));
   const auto h0 = std::chrono::steady_clock::now();
   c->timings = gq_timings{};
@@ -1279,7 +1403,8 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
       c->n_cu = 256;
     if (c->som_wg_per_cu <= 0) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj, SomProjCfg::kThreads, 0) != hipSuccess || nb <= 0)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0) != hipSuccess ||
+          nb <= 0)
         nb = 4;
       c->som_wg_per_cu = nb;
     }
@@ -1301,14 +1426,20 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(somatic_proj, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
-                       (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
-                       (int32_t *)c->slow.p);
+    if (rv.b)
+      hipLaunchKernelGGL(somatic_proj<true>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
+                         (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
+                         (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (int32_t *)c->slow.p, rv);
+    else
+      hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
+                         (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
+                         (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (int32_t *)c->slow.p, rv);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((somatic_tile<SomProjCfg::kT>), dim3((unsigned)std::min<int64_t>(pt.n_tiles, 2048)), dim3(kBlock), 0,
                        c->stream, (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, t->d, n->d,
-                       (ComplexItem *)c->cplx.p, og, (const int32_t *)c->slow.p, (int)p->min_mapq, ctr);
+                       (ComplexItem *)c->cplx.p, og, (const int32_t *)c->slow.p, (int)p->min_mapq, ctr, rv);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan_som, dim3(1), dim3(1024), 0, c->stream, ctr, og);
     HIP_TRY(hipGetLastError());
@@ -1331,7 +1462,8 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
     hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                        (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
-                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
+                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
+                       rv);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -1358,7 +1490,7 @@ gq_status gq_somatic_standard(gq_ctx *c, const gq_dev_reads *t, const gq_dev_rea
                          (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                          (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
-                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), RefView{nullptr, nullptr});
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
       HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

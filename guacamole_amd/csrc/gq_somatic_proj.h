@@ -141,10 +141,27 @@ __device__ __forceinline__ uint32_t add_sat2(uint32_t a, uint32_t b) {  // v_pk_
                                                                      __builtin_bit_cast(gq_short2, b)));
 }
 
+// A reference genome in HBM (gq_reference): contig c's base at locus l is b[off[c] + l]; each
+// contig starts on a 512-byte boundary and is padded past its end to the next 512-locus block.
+// b == nullptr: no reference, the pileup's base is the reads' MD-derived one.
+struct RefView {
+  const uint8_t *b;
+  const int64_t *off;
+};
+
+// With a reference (DistributedUtil.scala:266-267) the MD-derived candidate test stands where the
+// reference base is the one the reads' MD gives (the same pileup reference base); anywhere else
+// the locus is a candidate and somatic_call decides it with the reference base.
+__device__ __forceinline__ bool ref_agrees(uint32_t md_mask, uint32_t base) {
+  const uint32_t bit = std_bit((uint8_t)base);
+  return bit ? md_mask == bit : (md_mask == 0 && base == 'N');
+}
+
+template <bool kRef>
 __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void somatic_proj(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, int64_t n_tiles, DevReads RT,
     const int16_t *__restrict__ mproj, const int32_t *__restrict__ n_start, const int32_t *__restrict__ n_end,
-    ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow) {
+    ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref) {
   using C = SomProjCfg;
   constexpr int T = C::kT, U = C::kU;
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // tumor event read bases: A C T G bytes
@@ -348,6 +365,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run_c) - run_c;
     int32_t dn_run = (int32_t)wave_incl_scan((uint32_t)run_n) - run_n;
     uint32_t qmask = 0, nq = 0;
+    uint2 fb8 = make_uint2(0u, 0u);  // the reference bases of this lane's 8 loci
+    if constexpr (kRef) fb8 = *reinterpret_cast<const uint2 *>(ref.b + ref.off[tt.contig] + B0 + 8 * lane);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int32_t l = B0 + 8 * lane + j;
@@ -366,10 +385,12 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       const uint32_t low = mask & (0u - mask);
       const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
                              nN * (low == 0u ? 1u : 0u);
+      bool agree = true;
+      if constexpr (kRef) agree = ref_agrees(mask, ((j < 4 ? fb8.x : fb8.y) >> (8 * (j & 3))) & 0xFFu);
       const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
-      const bool nonmatch = (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
+      const bool nonmatch = !agree || (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
       const int16_t m16 = (int16_t)((msum[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-      const bool bound = single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
+      const bool bound = agree && single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
       const bool tcand = depth > 0 && nonmatch && !bound;
       visited += (in && (depth > 0 || dn_run > 0)) ? 1u : 0u;
       const bool q = in && tcand && dn_run > 0;

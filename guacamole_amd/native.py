@@ -120,7 +120,8 @@ class gq_somatic_calls(C.Structure):
 EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
             "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
             "gq_free_calls", "gq_pileup_counts",
-            "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info")
+            "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
+            "gq_reference_free", "gq_somatic_standard_ref")
 
 
 def lib():
@@ -135,7 +136,8 @@ def lib():
         L.gq_version.restype = C.c_char_p
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
-                  "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard"):
+                  "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard",
+                  "gq_reference_upload", "gq_somatic_standard_ref"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
                                             C.POINTER(C.POINTER(gq_calls))]
@@ -144,6 +146,11 @@ def lib():
         L.gq_pileup_counts.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(C.POINTER(gq_counts))]
         L.gq_somatic_standard.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
                                           C.POINTER(gq_somatic_params), C.POINTER(C.POINTER(gq_somatic_calls))]
+        L.gq_somatic_standard_ref.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.c_void_p,
+                                              C.POINTER(gq_somatic_params), C.POINTER(C.POINTER(gq_somatic_calls))]
+        L.gq_reference_upload.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.c_void_p,
+                                          C.POINTER(C.c_void_p)]
+        L.gq_reference_free.argtypes = [C.c_void_p]
         L.gq_free_calls.argtypes = [C.POINTER(gq_calls)]
         L.gq_free_counts.argtypes = [C.POINTER(gq_counts)]
         L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
@@ -250,15 +257,33 @@ class Context:
         _check(lib().gq_germline_threshold_device(self.h, reads.h, C.byref(L), C.byref(p), C.byref(out)))
         return DeviceCalls(out, self)
 
-    def somatic_standard(self, tumor: "DeviceReads", normal: "DeviceReads", loci, **params) -> "SomaticCalls":
-        """somatic-standard over the loci ranges (gq_somatic_standard).  params: the
-        gq_somatic_params fields; defaults SOMATIC_DEFAULTS (the CLI defaults)."""
+    def upload_reference(self, contigs: List[Optional[np.ndarray]]) -> "DeviceReference":
+        """A reference genome in HBM (gq_reference_upload): contigs[k] = the unmasked bases of
+        contig k of the read sets' contig list (None where the reference lacks it)."""
+        keep = [None if a is None else np.ascontiguousarray(a, np.uint8) for a in contigs]
+        n = len(keep)
+        ptrs = (C.c_void_p * max(n, 1))(*[None if a is None else a.ctypes.data for a in keep])
+        lens = np.array([-1 if a is None else len(a) for a in keep] or [0], np.int64)
+        h = C.c_void_p()
+        _check(lib().gq_reference_upload(self.h, n, C.cast(ptrs, C.POINTER(C.c_void_p)), lens.ctypes.data,
+                                         C.byref(h)))
+        return DeviceReference(h)
+
+    def somatic_standard(self, tumor: "DeviceReads", normal: "DeviceReads", loci, reference=None,
+                         **params) -> "SomaticCalls":
+        """somatic-standard over the loci ranges (gq_somatic_standard, or gq_somatic_standard_ref
+        with a DeviceReference).  params: the gq_somatic_params fields; defaults SOMATIC_DEFAULTS
+        (the CLI defaults)."""
         L, keep = make_gq_loci(*loci)
         p = dict(SOMATIC_DEFAULTS)
         p.update(params)
         ps = gq_somatic_params(**{k: int(v) for k, v in p.items()})
         out = C.POINTER(gq_somatic_calls)()
-        _check(lib().gq_somatic_standard(self.h, tumor.h, normal.h, C.byref(L), C.byref(ps), C.byref(out)))
+        if reference is None:
+            _check(lib().gq_somatic_standard(self.h, tumor.h, normal.h, C.byref(L), C.byref(ps), C.byref(out)))
+        else:
+            _check(lib().gq_somatic_standard_ref(self.h, tumor.h, normal.h, C.byref(L), reference.h, C.byref(ps),
+                                                 C.byref(out)))
         try:
             return SomaticCalls.from_struct(out.contents)
         finally:
@@ -280,6 +305,24 @@ class Context:
                         ref_base=arr(c.ref_base), ambiguous=arr(c.ambiguous))
         finally:
             lib().gq_free_counts(out)
+
+
+class DeviceReference:
+    """A gq_reference handle (freed with the object)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def free(self) -> None:
+        if self.h:
+            lib().gq_reference_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class DeviceReads:

@@ -1,48 +1,169 @@
-"""Genotype output: bdg-formats Genotype records as JSON lines and a VCF writer.
+"""Genotype output: bdg-formats Genotype records, Avro-JSON and VCF writers, dbSNP join.
 
-Restates the record builders the two callers use:
-  * germline: Genotype{alleles, sampleId, variant{contig, start, end, ref, alt}}
-    (commands/GermlineThresholdCaller.scala:106-117)
+Restates the record builders the two callers use (paths relative to
+/root/reference/src/main/scala/org/hammerlab/guacamole/):
+  * germline: Genotype{alleles, sampleId, variant{start, referenceAllele, alternateAllele,
+    contig{contigName}}} — no `end`, no depths (commands/GermlineThresholdCaller.scala:106-117)
   * somatic: AlleleConversions.calledSomaticAlleleToADAMGenotype
-    (variants/AlleleConversions.scala:47-62): GQ = phredScaledSomaticLikelihood, DP / AD
-    from the tumor evidence, expectedAlleleDosage = alt / DP (float32).
+    (variants/AlleleConversions.scala:47-62): alleles [Ref, Alt], GQ = phredScaledSomaticLikelihood,
+    readDepth / alternateReadDepth from the tumor evidence, referenceReadDepth = DP - alt,
+    expectedAlleleDosage = alt / DP (float32), variant = CalledSomaticAllele.adamVariant
+    (variants/ReferenceVariant.scala:42-48) whose end is start + 1 (CalledSomaticAllele.scala:46)
+  * dbSNP join: SomaticStandardCaller.scala:139-149 (leftOuterJoin on the ADAM Variant)
 The writer path (Common.writeVariantsFromArguments, Common.scala:246-304) picks JSON for
-"" / ".json" and VCF for ".vcf".  ADAM's exact VCF rendering (saveAsVcf) and the Avro
-JSON encoder's field order are third-party behaviour that is parity unpinned;
-the fields and values written here are the reference's.
+"" / ".json" and VCF for ".vcf".  JSON is what Avro's JsonEncoder writes for the Genotype schema
+through Jackson's default pretty printer: every schema field in schema order, nullable fields as
+unions ({"<type>": value} or null).  The schema is bdg-formats 0.6.1 (pom.xml:20), a dependency
+absent from /root/reference: its field lists are restated below from the published schema and are
+parity unpinned, as is ADAM 0.18's VCF rendering (saveAsVcf).
 """
 from __future__ import annotations
 
 import json
+import math
 import sys
-from typing import Dict, Iterable, List, Optional, TextIO
+from typing import Dict, Iterable, List, Optional, TextIO, Tuple
+
+import numpy as np
 
 GT_CODE = {"Ref": "0", "Alt": "1", "OtherAlt": ".", "NoCall": "."}
 
+_NS = "org.bdgenomics.formats.avro."
+# bdg-formats 0.6.1 records (field, Avro type, default); "?T" = union {null, T} default null,
+# "T?" = union {T, null} with the default shown, "[T]" = array (default [])
+CONTIG_SCHEMA: List[Tuple[str, str, object]] = [
+    ("contigName", "?string", None), ("contigLength", "?long", None), ("contigMD5", "?string", None),
+    ("referenceURL", "?string", None), ("assembly", "?string", None), ("species", "?string", None),
+    ("referenceIndex", "?int", None)]
+VARIANT_SCHEMA: List[Tuple[str, str, object]] = [
+    ("contig", "?Contig", None), ("start", "?long", None), ("end", "?long", None),
+    ("referenceAllele", "?string", None), ("alternateAllele", "?string", None),
+    ("svAllele", "?StructuralVariant", None), ("isSomatic", "boolean?", False)]
+GENOTYPE_SCHEMA: List[Tuple[str, str, object]] = [
+    ("variant", "?Variant", None), ("variantCallingAnnotations", "?VariantCallingAnnotations", None),
+    ("sampleId", "?string", None), ("sampleDescription", "?string", None),
+    ("processingDescription", "?string", None), ("alleles", "[GenotypeAllele]", []),
+    ("expectedAlleleDosage", "?float", None), ("referenceReadDepth", "?int", None),
+    ("alternateReadDepth", "?int", None), ("readDepth", "?int", None), ("minReadDepth", "?int", None),
+    ("genotypeQuality", "?int", None), ("genotypeLikelihoods", "[float]", []),
+    ("nonReferenceLikelihoods", "[float]", []), ("strandBiasComponents", "[int]", []),
+    ("splitFromMultiAllelic", "boolean?", False), ("isPhased", "?boolean", None), ("phaseSetId", "?int", None),
+    ("phaseQuality", "?int", None)]
+_RECORDS = {"Contig": CONTIG_SCHEMA, "Variant": VARIANT_SCHEMA, "Genotype": GENOTYPE_SCHEMA}
+
 
 def germline_genotype(contig: str, start: int, sample: str, alleles, ref: str, alt: str) -> Dict:
+    """GermlineThresholdCaller.scala:106-117 (the fields the builder sets)."""
     return dict(alleles=list(alleles), sampleId=sample,
-                variant=dict(contig=dict(contigName=contig), start=int(start), end=int(start) + len(ref),
-                             referenceAllele=ref, alternateAllele=alt))
+                variant=dict(start=int(start), referenceAllele=ref, alternateAllele=alt,
+                             contig=dict(contigName=contig)))
 
 
 def somatic_genotype(contig: str, row: Dict, sample: str) -> Dict:
+    """AlleleConversions.calledSomaticAlleleToADAMGenotype (AlleleConversions.scala:47-62)."""
     t = row["tumor"]  # (likelihood, readDepth, alleleReadDepth, forwardDepth, alleleForwardDepth, ...)
     depth, alt_depth = int(t[1]), int(t[2])
-    import numpy as np
+    with np.errstate(divide="ignore", invalid="ignore"):
+        dosage = float(np.float32(alt_depth) / np.float32(depth))
     return dict(alleles=["Ref", "Alt"], sampleId=sample, genotypeQuality=int(row["gq"]), readDepth=depth,
-                expectedAlleleDosage=float(np.float32(alt_depth) / np.float32(depth)) if depth else float("nan"),
-                referenceReadDepth=depth - alt_depth, alternateReadDepth=alt_depth,
-                variant=dict(contig=dict(contigName=contig), start=int(row["locus"]),
-                             end=int(row["locus"]) + len(row["ref"]), referenceAllele=row["ref"],
-                             alternateAllele=row["alt"]))
+                expectedAlleleDosage=dosage, referenceReadDepth=depth - alt_depth, alternateReadDepth=alt_depth,
+                variant=dict(start=int(row["locus"]), end=int(row["locus"]) + 1, referenceAllele=row["ref"],
+                             alternateAllele=row["alt"], contig=dict(contigName=contig)))
+
+
+# ---- Avro JSON encoding -------------------------------------------------------------------
+def java_float(x: float) -> str:
+    """Float.toString of a float32 (what Jackson writes for JsonEncoder.writeFloat): the shortest
+    repr that round-trips the float32, "d.ddd" for 1e-3 <= |x| < 1e7, else "d.dddE<exp>"."""
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    f = np.float32(x)
+    if f == 0:
+        return "-0.0" if math.copysign(1.0, float(f)) < 0 else "0.0"
+    s = np.format_float_scientific(f, unique=True, trim="-")  # e.g. '2e-01', '1.2345e+07'
+    mant, exp = s.split("e")
+    e = int(exp)
+    neg = mant.startswith("-")
+    digits = mant.lstrip("-").replace(".", "")
+    if 1e-3 <= abs(float(f)) < 1e7:
+        if e >= 0:
+            ip = digits[:e + 1].ljust(e + 1, "0")
+            fp = digits[e + 1:] or "0"
+        else:
+            ip, fp = "0", "0" * (-e - 1) + digits
+        out = ip + "." + fp
+    else:
+        out = digits[0] + "." + (digits[1:] or "0") + "E" + str(e)
+    return ("-" if neg else "") + out
+
+
+def avro_datum(record: str, value: Optional[Dict]) -> Dict:
+    """The JsonEncoder's view of a record: every schema field in order, unions wrapped."""
+    value = value or {}
+    out: Dict = {}
+    for name, typ, default in _RECORDS[record]:
+        v = value.get(name, default)
+        if typ.startswith("["):
+            out[name] = list(v)
+        elif v is None:
+            out[name] = None
+        else:
+            base = typ.strip("?")
+            if base in _RECORDS:
+                out[name] = {_NS + base: avro_datum(base, v)}
+            else:
+                out[name] = {base: v}
+    return out
+
+
+def _pretty(v, ind: int, float_fields: bool = False) -> str:
+    """Jackson 1.x DefaultPrettyPrinter: objects one field a line ("name" : value) at two-space
+    indents, arrays inline ([ a, b ]), empty containers "{ }" / "[ ]"."""
+    if isinstance(v, dict):
+        if not v:
+            return "{ }"
+        pad = "  " * (ind + 1)
+        items = []
+        for k, x in v.items():
+            items.append(pad + json.dumps(k) + " : " + _pretty(x, ind + 1, k == "float"))
+        return "{\n" + ",\n".join(items) + "\n" + "  " * ind + "}"
+    if isinstance(v, list):
+        return "[ " + ", ".join(_pretty(x, ind) for x in v) + " ]" if v else "[ ]"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if v is None:
+        return "null"
+    if float_fields or isinstance(v, float):
+        return java_float(float(v))
+    return json.dumps(v)
+
+
+def avro_json(genotypes: Iterable[Dict]) -> str:
+    """The bytes Common.writeVariantsFromArguments writes for JSON output (Common.scala:263-285):
+    the records, pretty-printed and separated by Jackson's root separator (one space), then a
+    newline."""
+    return " ".join(_pretty(avro_datum("Genotype", g), 0) for g in genotypes) + "\n"
+
+
+def read_avro_json(text: str) -> List[Dict]:
+    """The records of an avro_json text (whitespace-separated JSON objects)."""
+    dec, i, out = json.JSONDecoder(), 0, []
+    n = len(text)
+    while True:
+        while i < n and text[i] in " \t\r\n":
+            i += 1
+        if i >= n:
+            return out
+        obj, i = dec.raw_decode(text, i)
+        out.append(obj)
 
 
 def write_json(path: str, genotypes: Iterable[Dict]) -> None:
     out: TextIO = open(path, "w") if path else sys.stdout
     try:
-        for g in genotypes:
-            out.write(json.dumps(g) + "\n")
+        out.write(avro_json(genotypes))
     finally:
         if path:
             out.close()
@@ -74,3 +195,48 @@ def write_vcf(path: str, genotypes: List[Dict], contig_lengths: Optional[Dict[st
             cols[samples.index(g["sampleId"])] = ":".join(vals)
             fh.write("\t".join([v["contig"]["contigName"], str(v["start"] + 1), ".", v["referenceAllele"],
                                 v["alternateAllele"], ".", ".", ".", ":".join(fmt)] + cols) + "\n")
+
+
+# ---- dbSNP annotation join ----------------------------------------------------------------
+def read_dbsnp_vcf(path: str) -> List[Dict]:
+    """ADAMContext.loadVariantAnnotations over a VCF, restated as what the join reads: one
+    entry per (record, ALT allele) with the variant key (contig, 0-based start, end = start +
+    len(REF), REF, ALT) and the numeric dbSNP id of an "rs<N>" ID column (None otherwise)."""
+    import gzip
+    with open(path, "rb") as fh:
+        gz = fh.read(2) == b"\x1f\x8b"
+    out: List[Dict] = []
+    with (gzip.open(path, "rt") if gz else open(path)) as fh:
+        for line in fh:
+            if not line.strip() or line.startswith("#"):
+                continue
+            f = line.rstrip("\n").split("\t")
+            if len(f) < 5:
+                raise ValueError("%s: malformed VCF line: %r" % (path, line[:80]))
+            contig, pos, vid, ref = f[0], int(f[1]) - 1, f[2], f[3]
+            rs = None
+            for tok in vid.split(";"):
+                if tok.startswith("rs") and tok[2:].isdigit():
+                    rs = int(tok[2:])
+                    break
+            for alt in f[4].split(","):
+                out.append(dict(contig=contig, start=pos, end=pos + len(ref), ref=ref, alt=alt, rs_id=rs))
+    return out
+
+
+def dbsnp_join(rows: List[Dict], dbsnp: List[Dict]) -> List[Dict]:
+    """potentialGenotypes.keyBy(_.adamVariant).leftOuterJoin(dbSnp.keyBy(_.getVariant))
+    (SomaticStandardCaller.scala:141-147): each call gets rs_id from every dbSNP entry with its
+    variant key (the call repeated once per match, as a join does), None when none matches.
+    The reference's post-shuffle record order is Spark hash-partition order; calls keep theirs."""
+    index: Dict[tuple, List[Optional[int]]] = {}
+    for d in dbsnp:
+        index.setdefault((d["contig"], d["start"], d["end"], d["ref"], d["alt"]), []).append(d["rs_id"])
+    out = []
+    for r in rows:
+        key = (r["contig"], int(r["locus"]), int(r["locus"]) + 1, r["ref"], r["alt"])
+        for rs in index.get(key, [None]):
+            x = dict(r)
+            x["rs_id"] = rs
+            out.append(x)
+    return out

@@ -20,7 +20,7 @@ import gzip
 import io
 import struct
 import zlib
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -246,9 +246,25 @@ def _header_read_groups(text: str) -> Dict[str, str]:
     return out
 
 
-def load_reads(path: str, filters: InputFilters = InputFilters()) -> ReadSet:
+def load_reads(path: str, filters: InputFilters = InputFilters(), reference=None, recompute_md: bool = False,
+               contig_lengths_from_dictionary: bool = True) -> ReadSet:
     """Load mapped reads of a SAM/BAM file (Read.loadReadRDDAndSequenceDictionaryFromBAM,
-    samtools path, then ReadSet.mappedReads)."""
+    samtools path, then ReadSet.mappedReads).  `reference` (reference.ReferenceGenome) supplies
+    MD tags for reads without one, or for every read with `recompute_md` (Read.scala:223-247);
+    the hasMdTag filter then sees the rebuilt tags (Read.scala:422).  With
+    `contig_lengths_from_dictionary` False (--no-sequence-dictionary) contig lengths are the
+    largest read end per contig, and contigs without reads are dropped (ReadSet.scala:69-80)."""
+    if recompute_md and reference is None:
+        raise ValueError("To recompute MD tags, a reference genome fasta must be provided.")
+    if reference is not None:
+        from .reference import rebuild_md_tags
+        rs = load_reads(path, replace(filters, has_md_tag=False), None, False, contig_lengths_from_dictionary)
+        rs = rebuild_md_tags(rs, reference, recompute_md)
+        if filters.has_md_tag and (rs.md_len < 0).any():
+            rs = rs.subset(np.flatnonzero(rs.md_len >= 0))
+        return rs
+    if not contig_lengths_from_dictionary:
+        return contig_lengths_from_reads(load_reads(path, filters))
     with open(path, "rb") as fh:
         head = fh.read(2)
     if head == b"\x1f\x8b":  # BGZF (BAM) or a gzip-compressed SAM
@@ -261,6 +277,19 @@ def load_reads(path: str, filters: InputFilters = InputFilters()) -> ReadSet:
             from .ingest import load_bam  # native (libgqingest); raises if not built
             return load_bam(path, filters)
     return _load_sam(path, filters)
+
+
+def contig_lengths_from_reads(rs: ReadSet) -> ReadSet:
+    """ReadSet.contigLengths with contigLengthsFromDictionary = false (ReadSet.scala:75-79):
+    contig -> max read end over the mapped reads; contigs without reads are absent."""
+    if rs.n == 0:
+        raise ValueError("no mapped reads to take contig lengths from (--no-sequence-dictionary)")
+    keep = sorted(set(int(c) for c in np.unique(rs.contig)))
+    remap = np.full(len(rs.contig_names), -1, np.int32)
+    remap[keep] = np.arange(len(keep), dtype=np.int32)
+    lengths = [int(rs.end[rs.contig == c].max()) for c in keep]
+    return replace(rs, contig_names=[rs.contig_names[c] for c in keep], contig_lengths=lengths,
+                   contig=remap[rs.contig].astype(np.int32), _gq=None)
 
 
 def _finish(b: _Builder, contig_names, contig_lengths, samples: List[str]) -> ReadSet:

@@ -256,6 +256,23 @@ gq_status gq_somatic_standard(gq_ctx *ctx, const gq_dev_reads *tumor, const gq_d
                               const gq_loci *loci, const gq_somatic_params *params, gq_somatic_calls **out);
 void gq_free_somatic(gq_somatic_calls *c);
 
+/* --reference-fasta (SomaticStandardCaller.scala:57, :75).  A reference genome resident in HBM
+ * (replaces ReferenceBroadcast.apply, reference/ReferenceBroadcast.scala:39-55): bases[k] /
+ * lengths[k] are the unmasked bases of contig k of the read sets' contig list (bases[k] == NULL
+ * for a contig the FASTA lacks).  Bytes are copied; the caller's buffers may be freed after. */
+typedef struct gq_reference gq_reference;
+gq_status gq_reference_upload(gq_ctx *ctx, int32_t n_contigs, const uint8_t *const *bases, const int64_t *lengths,
+                              gq_reference **out);
+void gq_reference_free(gq_reference *ref);
+/* gq_somatic_standard with pileupFlatMapTwoRDDs' referenceGenome argument
+ * (DistributedUtil.scala:316-335): every pileup's reference base is the reference's
+ * (DistributedUtil.scala:266-268) instead of the reads' MD-derived one.  ref == NULL is
+ * gq_somatic_standard.  GQ_E_ARG when a loci range lies on a contig the reference lacks
+ * (ContigNotFound, ReferenceBroadcast.scala:26-30) or runs past its end.               */
+gq_status gq_somatic_standard_ref(gq_ctx *ctx, const gq_dev_reads *tumor, const gq_dev_reads *normal,
+                                  const gq_loci *loci, const gq_reference *ref, const gq_somatic_params *params,
+                                  gq_somatic_calls **out);
+
 #ifdef __cplusplus
 }
 #endif

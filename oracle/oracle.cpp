@@ -534,10 +534,17 @@ uint8_t referenceBaseAtLocus(const std::vector<const Read *> &reads, int64_t loc
 }
 
 // DistributedUtil.initOrMovePileup (DistributedUtil.scala:260-274) + Pileup.atGreaterLocus (Pileup.scala:103-132)
-void initOrMovePileup(Pileup &p, bool exists, const Window &w, bool *ambiguous) {
+// ref_base >= 0: the reference genome's base (DistributedUtil.scala:266-267)
+void initOrMovePileup(Pileup &p, bool exists, const Window &w, bool *ambiguous, int ref_base = -1) {
   int64_t locus = w.currentLocus;
   std::vector<const Read *> regions = w.currentRegions();
-  uint8_t ref = referenceBaseAtLocus(regions, locus, ambiguous);
+  uint8_t ref;
+  if (ref_base >= 0) {
+    ref = (uint8_t)ref_base;
+    if (ambiguous) *ambiguous = false;
+  } else {
+    ref = referenceBaseAtLocus(regions, locus, ambiguous);
+  }
   if (!exists) {
     p.locus = locus;
     p.referenceBase = ref;
@@ -752,8 +759,20 @@ void germlineCallAtLocus(const Pileup &p, const char *contig, int threshold, boo
 }
 
 // Drives pileupFlatMap / pileupFlatMapTwoRDDs (DistributedUtil.scala:288-335, 388-418, 473-486)
+// ReferenceBroadcast.getReferenceBase (ReferenceBroadcast.scala:26-37): ContigNotFound for a
+// contig the reference lacks, an index failure past its end
+int referenceBase(const or_reference *ref, const or_loci *loci, int32_t contig, int64_t locus) {
+  if (contig < 0 || contig >= ref->n_contigs || !ref->bases[contig])
+    fail(E_ARG, std::string("Contig ") + loci->contig_names[contig] + " does not exist in the current reference");
+  if (locus < 0 || locus >= ref->lengths[contig])
+    fail(E_ARG, std::string("locus ") + std::to_string(locus) + " is past the end of reference contig " +
+                    loci->contig_names[contig]);
+  return ref->bases[contig][locus];
+}
+
 template <class F>
-void forEachPileup(const std::vector<ReadSet *> &sets, const or_loci *loci, F &&fn) {
+void forEachPileup(const std::vector<ReadSet *> &sets, const or_loci *loci, F &&fn,
+                   const or_reference *reference = nullptr) {
   std::vector<ContigIndex> idx;
   for (ReadSet *rs : sets) idx.emplace_back(*rs);
   for (const TaskContig &tc : taskContigs(loci)) {
@@ -771,9 +790,10 @@ void forEachPileup(const std::vector<ReadSet *> &sets, const or_loci *loci, F &&
     int64_t locus;
     while (advanceMultipleWindows(wp, it, locus)) {
       std::vector<bool> amb(sets.size(), false);
+      const int rb = reference ? referenceBase(reference, loci, tc.contig, locus) : -1;
       for (size_t s = 0; s < sets.size(); ++s) {
         bool a = false;
-        initOrMovePileup(pileups[s], have, windows[s], &a);
+        initOrMovePileup(pileups[s], have, windows[s], &a, rb);
         amb[s] = a;
       }
       have = true;
@@ -1164,18 +1184,27 @@ int or_germline_threshold(const or_reads *reads, const or_loci *loci, int32_t th
   });
 }
 
-int or_somatic_standard(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
-                        const or_somatic_params *prm, char **o, int64_t *olen) {
+int or_somatic_standard_ref(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
+                            const or_reference *ref, const or_somatic_params *prm, char **o, int64_t *olen) {
   std::string out;
   return guard(out, o, olen, [&]() {
     ReadSet trs, nrs;
     buildReads(tumor, trs);
     buildReads(normal, nrs);
     std::vector<ReadSet *> sets{&trs, &nrs};
-    forEachPileup(sets, loci, [&](const TaskContig &tc, std::vector<Pileup> &ps, std::vector<bool> &amb) {
-      somaticAtLocus(ps[0], ps[1], loci->contig_names[tc.contig], prm, prm->apply_filters, (amb[0] ? 1 : 0) | (amb[1] ? 2 : 0), out);
-    });
+    forEachPileup(
+        sets, loci,
+        [&](const TaskContig &tc, std::vector<Pileup> &ps, std::vector<bool> &amb) {
+          somaticAtLocus(ps[0], ps[1], loci->contig_names[tc.contig], prm, prm->apply_filters,
+                         (amb[0] ? 1 : 0) | (amb[1] ? 2 : 0), out);
+        },
+        ref);
   });
+}
+
+int or_somatic_standard(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
+                        const or_somatic_params *prm, char **o, int64_t *olen) {
+  return or_somatic_standard_ref(tumor, normal, loci, nullptr, prm, o, olen);
 }
 
 int or_elements_at(const or_reads *reads, int32_t contig, int64_t locus, int32_t own_ref, char **o, int64_t *olen) {

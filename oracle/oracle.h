@@ -89,6 +89,19 @@ typedef struct {
 int or_somatic_standard(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
                         const or_somatic_params *p, char **out, int64_t *out_len);
 
+/* A reference genome (ReferenceBroadcast.scala:39-55): unmasked bases of each contig of
+ * the loci's contig list, in that order; bases[i] == NULL => contig absent (ContigNotFound). */
+typedef struct {
+  int32_t n_contigs;
+  const uint8_t *const *bases;
+  const int64_t *lengths;
+} or_reference;
+
+/* somatic-standard with --reference-fasta: every pileup's reference base is the reference's
+ * (DistributedUtil.scala:266-268); flags bits 0/1 are then never set.                    */
+int or_somatic_standard_ref(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
+                            const or_reference *ref, const or_somatic_params *p, char **out, int64_t *out_len);
+
 /* ---- single-locus entry points used to pin the oracle with the reference's unit
  * KATs.  They build the pileup with Pileup.apply(reads, contig, locus)
  * (Pileup.scala:181-186): reads in input order, reference base from

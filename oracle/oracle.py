@@ -59,7 +59,7 @@ def lib():
             build()
         _lib = C.CDLL(_LIB_PATH)
         _lib.or_last_error.restype = C.c_char_p
-        for fn in ("or_pileup_stats", "or_germline_threshold", "or_somatic_standard"):
+        for fn in ("or_pileup_stats", "or_germline_threshold", "or_somatic_standard", "or_somatic_standard_ref"):
             getattr(_lib, fn).restype = C.c_int
     return _lib
 
@@ -136,13 +136,33 @@ SOMATIC_DEFAULTS = dict(odds=20, min_mapq=1, filter_multi_allelic=0, max_read_de
                         max_median_mismatches=2 ** 31 - 1, apply_filters=1)
 
 
-def somatic_standard(tumor, normal, loci, **params):
+class or_reference(C.Structure):
+    _fields_ = [("n_contigs", C.c_int32), ("bases", C.POINTER(C.c_void_p)), ("lengths", C.c_void_p)]
+
+
+class _Reference:
+    """The reference genome's bytes for each contig of `contig_names` (None = absent)."""
+
+    def __init__(self, reference, contig_names: List[str]):
+        self.keep = [reference.contigs.get(n) for n in contig_names]
+        self.ptrs = (C.c_void_p * max(len(contig_names), 1))(*[None if a is None else a.ctypes.data for a in self.keep])
+        self.lens = np.array([-1 if a is None else len(a) for a in self.keep], np.int64)
+        self.s = or_reference(len(contig_names), C.cast(self.ptrs, C.POINTER(C.c_void_p)), _ptr(self.lens))
+
+
+def somatic_standard(tumor, normal, loci, reference=None, **params):
+    """reference: a guacamole_amd.reference.ReferenceGenome (--reference-fasta) or None."""
     p = dict(SOMATIC_DEFAULTS)
     p.update(params)
     ps = or_somatic_params(**{k: int(v) for k, v in p.items()})
     mt, mn = _Marshalled(tumor), _Marshalled(normal)
     L = _Loci(tumor.contig_names, *loci)
-    text = _call(lib().or_somatic_standard, C.byref(mt.s), C.byref(mn.s), C.byref(L.s), C.byref(ps))
+    if reference is None:
+        text = _call(lib().or_somatic_standard, C.byref(mt.s), C.byref(mn.s), C.byref(L.s), C.byref(ps))
+    else:
+        R = _Reference(reference, tumor.contig_names)
+        text = _call(lib().or_somatic_standard_ref, C.byref(mt.s), C.byref(mn.s), C.byref(L.s), C.byref(R.s),
+                     C.byref(ps))
     out = []
     for line in text.splitlines():
         f = line.split("\t")

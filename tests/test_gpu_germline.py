@@ -106,7 +106,6 @@ def test_kat_pileups(gpu_ctx):
 
 def test_cli_germline_vcf_and_somatic_json(tmp_path):
     """End-to-end CLI (python -m guacamole_amd ...) writes the callers' outputs."""
-    import json
     from guacamole_amd.commands import main
     vcf = str(tmp_path / "g.vcf")
     assert main(["germline-threshold", "--reads", fixture("chrM.sorted.bam"), "--loci", "chrM:0-16570",
@@ -116,8 +115,9 @@ def test_cli_germline_vcf_and_somatic_json(tmp_path):
     js = str(tmp_path / "s.json")
     assert main(["somatic-standard", "--tumor-reads", fixture("tumor.chr20.tough.sam"), "--normal-reads",
                  fixture("normal.chr20.tough.sam"), "--out", js, "--min-tumor-read-depth", "8"]) == 0
-    rows = [json.loads(l) for l in open(js)]
-    assert rows and all(r["alleles"] == ["Ref", "Alt"] and r["readDepth"] >= 8 for r in rows)
+    from guacamole_amd.output import read_avro_json
+    rows = read_avro_json(open(js).read())
+    assert rows and all(r["alleles"] == ["Ref", "Alt"] and r["readDepth"]["int"] >= 8 for r in rows)
 
 
 def test_synthetic_column_path_dense_outputs(gpu_ctx):
