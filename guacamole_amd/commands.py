@@ -247,6 +247,69 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     return _finish_rank(0)
 
 
+def variant_loci(vcf_path: str) -> LociSet:
+    """LociSet.union of the variants' [start, end) (VariantSupport.scala:82-87) over ADAM's VCF
+    variants (loadVariants: one Variant per ALT allele, start = POS - 1, end = start + len(REF))."""
+    from .output import read_dbsnp_vcf
+    b = LociSetBuilder()
+    for v in read_dbsnp_vcf(vcf_path):
+        b.put(v["contig"], v["start"], v["end"])
+    return b.result()
+
+
+def variant_support_reads(ctx: native.Context, rs: ReadSet, loci) -> List[tuple]:
+    """pileupFlatMap(reads, partitions, skipEmpty=true, pileupToAlleleCounts) on the GPU
+    (VariantSupport.scala:93-100, 110-118).  Rows (sample name, contig, locus, ref, alt, count,
+    flags), in the loci's call order, a locus's alleles by (ref, alt)."""
+    rows = ctx.variant_support(device_reads(ctx, rs), loci)
+    return [(rs.sample_names[s] if s < len(rs.sample_names) else "default", rs.contig_names[c], l, ref, alt, n, f)
+            for s, c, l, ref, alt, n, f in rows]
+
+
+def variant_support_main(argv: Sequence[str]) -> int:
+    """VariantSupport.Caller.run (commands/VariantSupport.scala:62-103): allele counts at each
+    variant of --input-variant in every BAM; saveAsTextFile layout (one part file per BAM and
+    task, lines "sample, contig, locus, ref, alt, count", AlleleCount.toString :58-60)."""
+    import os
+    p = argparse.ArgumentParser(prog="variant-support",
+                                description="Find number of reads that support each variant across BAMs")
+    p.add_argument("-v", "--input-variant", required=True, help="VCF of the variants")
+    p.add_argument("-o", "--output", required=True, help="Output path for CSV")
+    p.add_argument("bams", nargs="+", help="Retrieve read data from BAMs at each variant position")
+    p.add_argument("--parallelism", type=int, default=0, help="Num variant calling tasks")
+    p.add_argument("--partition-accuracy", type=int, default=250, help="(accepted; partitioning is uniform)")
+    p.add_argument("--bam-reader-api", default="best", help="(accepted; the native reader is always used)")
+    p.add_argument("--recompute-md-tags", action="store_true")
+    p.add_argument("--device", type=int, default=0, help="GPU index")
+    args = p.parse_args(argv)
+    loci = variant_loci(args.input_variant)
+    # partitionLociUniformly(args.parallelism, ...) takes the flag as given (VariantSupport.scala:89)
+    parts = partition_loci_uniformly(args.parallelism, loci)
+    ctx = native.Context(args.device)
+    os.makedirs(args.output, exist_ok=False)
+    tasks = args.parallelism
+    for b, bam in enumerate(args.bams):
+        rs = load_reads(bam, InputFilters(), recompute_md=args.recompute_md_tags, contig_lengths_from_dictionary=False)
+        idx = rs.contig_index()
+        contig, start, end, task = flatten_partitions(parts, {c: idx.get(c, -1) for c in loci.contigs})
+        keep = contig >= 0  # contigs without reads hold no pileups
+        flat = (contig[keep], start[keep], end[keep], task[keep])
+        rows = variant_support_reads(ctx, rs, flat)
+        # the task of each row: its loci range's
+        by_task: Dict[int, List[str]] = {t: [] for t in range(tasks)}
+        r = 0
+        for sample, cname, locus, ref, alt, n, _ in rows:
+            ci = idx[cname]
+            while not (flat[0][r] == ci and flat[1][r] <= locus < flat[2][r]):
+                r += 1
+            by_task[int(flat[3][r])].append("%s, %s, %d, %s, %s, %d" % (sample, cname, locus, ref, alt, n))
+        for t in range(tasks):
+            with open(os.path.join(args.output, "part-%05d" % (b * tasks + t)), "w") as fh:
+                fh.writelines(line + "\n" for line in by_task[t])
+    open(os.path.join(args.output, "_SUCCESS"), "w").close()
+    return 0
+
+
 def _finish_rank(rc: int) -> int:
     """Leave the process group (multi-GPU runs) after every rank has finished."""
     import os
@@ -258,7 +321,8 @@ def _finish_rank(rc: int) -> int:
     return rc
 
 
-COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main}
+COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main,
+            "variant-support": variant_support_main}
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

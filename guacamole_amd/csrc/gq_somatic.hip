@@ -1174,6 +1174,120 @@ __global__ __launch_bounds__(1024) void part_scan_som(Counters *ctr, OutGeom og)
   }
 }
 
+// ---- variant-support: VariantSupport.pileupToAlleleCounts (commands/VariantSupport.scala:110-118)
+struct VsRec {
+  uint64_t key;  // locus ordinal (position in the concatenated loci ranges)
+  int32_t contig, pos;
+  int32_t count;
+  uint16_t ref_len, alt_len;
+  uint8_t flags, sample, pad[6];
+  uint64_t allele;  // ref then alt bytes: inline when they fit 8 bytes, else a pool offset
+};
+static_assert(sizeof(VsRec) == 40, "VsRec layout");
+
+// One wave per locus of the loci set: the covering reads' pileup (every element, no filter),
+// its distinct alleles and their element counts (gather_sample's table).  Loci whose reference
+// base depends on heap order are listed first (amb_out) and redone with the replayed base.
+__global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__restrict__ tiles, int64_t n_tiles,
+                                                               int64_t n_items, DevReads R, VsRec *__restrict__ recs,
+                                                               unsigned long long rec_cap, uint8_t *__restrict__ pool,
+                                                               unsigned long long pool_cap, Counters *ctr,
+                                                               AmbItem *__restrict__ amb_out, unsigned long long amb_cap,
+                                                               const AmbItem *__restrict__ amb_in,
+                                                               const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+  __shared__ int32_t cover[kSomWaves][kCover];
+  __shared__ uint32_t tmp[kSomWaves][kEvCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t n = amb_in ? n_amb_in : n_items;
+  for (int64_t li = gwave; li < n; li += nwaves_total) {
+    const int64_t k = amb_in ? amb_in[li].item : li;
+    int64_t t;
+    if (amb_in) {
+      t = amb_in[li].tile;
+    } else {  // last tile whose first ordinal <= k
+      int64_t lo = 0, hi = n_tiles - 1;
+      while (lo < hi) {
+        const int64_t m = (lo + hi + 1) >> 1;
+        if (tiles[m].ordinal0 <= k) lo = m;
+        else hi = m - 1;
+      }
+      t = lo;
+    }
+    const Tile tt = tiles[t];
+    const int64_t pos64 = (int64_t)tt.L0 + (k - tt.ordinal0);
+    if (k < tt.ordinal0 || pos64 >= tt.L1) continue;
+    const int32_t pos = (int32_t)pos64;
+    WinInit w0{};
+    const Cover cv = make_cover(R, tt.rb, tt.re, pos, cover[wv], tmp[wv], w0, nullptr, nullptr, ctr);
+    SamplePile P;
+    gather_sample(R, cv, pos, 0, amb_in ? (int)amb_ref[li] : -1, ctr, P);
+    if (P.depth_all == 0) continue;  // skipEmpty
+    if (P.overflow) {
+      raise_at(ctr, GQ_E_CAPACITY, pos);
+      continue;
+    }
+    if (!amb_in && P.ambiguous) {
+      if (lane == 0) {
+        const unsigned long long a = atomicAdd(&ctr->n_amb, 1ull);
+        if (a < amb_cap) amb_out[a] = AmbItem{(int32_t)t, pos, k};
+      }
+      continue;
+    }
+    // Pileup.sampleName = the head element's sample (Pileup.scala:51): the reads' one sample,
+    // or (flag bit 1) the first covering read's where the pileup mixes samples
+    int first = -1;
+    bool mixed = false;
+    for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
+      bool act;
+      const int64_t r = cv.read(R, k0 + lane, pos, &act);
+      const int smp = act ? (int)R.sample[r] : -1;
+      const unsigned long long b = __ballot(act);
+      if (!b) continue;
+      if (first < 0) first = __shfl(smp, __ffsll((long long)b) - 1, 64);
+      mixed |= __ballot(act && smp != first) != 0;
+    }
+    const uint8_t flags = (uint8_t)((amb_in ? 1 : 0) | (mixed ? 2 : 0));
+    for (int j = 0; j < P.nt; ++j) {
+      const AlleleDesc d = pile_desc(P, j);
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int s2 = 0; s2 < kSlots; ++s2)
+        if (s2 == (j >> 6)) cnt = (uint32_t)__shfl((int)P.n_all[s2], j & 63, 64);
+      const int rl = allele_ref_len(d), al = allele_alt_len(d);
+      VsRec rr;
+      rr.key = (uint64_t)k;
+      rr.contig = tt.contig;
+      rr.pos = pos;
+      rr.count = (int32_t)cnt;
+      rr.ref_len = (uint16_t)rl;
+      rr.alt_len = (uint16_t)al;
+      rr.flags = flags;
+      rr.sample = (uint8_t)first;
+      for (int q = 0; q < 6; ++q) rr.pad[q] = 0;
+      if (rl + al <= 8) {
+        uint64_t v = 0;
+        for (int i = 0; i < rl; ++i) v |= (uint64_t)allele_byte(R, d, pos, 0, i) << (8 * i);
+        for (int i = 0; i < al; ++i) v |= (uint64_t)allele_byte(R, d, pos, 1, i) << (8 * (rl + i));
+        rr.allele = v;
+      } else {
+        unsigned long long off = 0;
+        if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + al));
+        off = __shfl(off, 0, 64);
+        if (off + rl + al <= pool_cap)
+          for (int i = lane; i < rl + al; i += 64)
+            pool[off + i] = i < rl ? allele_byte(R, d, pos, 0, i) : allele_byte(R, d, pos, 1, i - rl);
+        rr.allele = off;
+      }
+      if (lane == 0) {
+        const unsigned long long q = atomicAdd(&ctr->n_rec, 1ull);
+        if (q < rec_cap) recs[q] = rr;
+      }
+    }
+  }
+}
+
 gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq) {
   if (t->mproj && t->mproj_mapq == min_mapq) return GQ_OK;
   if (!t->mproj) {
@@ -1577,6 +1691,153 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
   *out = res;
   return GQ_OK;
+}
+
+gq_status gq_variant_support(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, gq_allele_counts **out) {
+  if (!c || !rd || !loci || !out) return set_err(GQ_E_ARG, "gq_variant_support: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const auto h0 = std::chrono::steady_clock::now();
+  c->timings = gq_timings{};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  Plan pl;
+  gq_status st = plan(c, rd, loci, 512, pl, c->tiles);
+  if (st) return st;
+  gq_allele_counts *res = (gq_allele_counts *)calloc(1, sizeof(gq_allele_counts));
+  if (!res) return set_err(GQ_E_NOMEM, "calloc");
+  auto fail = [&](gq_status e) {
+    gq_free_allele_counts(res);
+    return e;
+  };
+  unsigned long long rec_cap = (unsigned long long)std::max<int64_t>(pl.n_loci * 2, 1024), pool_cap = 1 << 16,
+                     amb_cap = 4096;
+  Counters hc{};
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((pl.n_loci + kSomWaves - 1) / kSomWaves, 1), 8192);
+  for (int attempt = 0; pl.n_tiles > 0; ++attempt) {
+    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
+    HIP_TRY(c->srecs.ensure(rec_cap * sizeof(VsRec)));
+    HIP_TRY(c->pool.ensure(pool_cap));
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    Counters *ctr = (Counters *)c->counters.p;
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(variant_support_call, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                       pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, ctr,
+                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bool retry = false;
+    if (hc.n_amb > amb_cap) {
+      amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (!retry && hc.n_amb > 0 && !hc.err) {  // heap-order reference bases: replay, then redo those loci
+      std::vector<AmbItem> amb((size_t)hc.n_amb);
+      HIP_TRY(hipMemcpyAsync(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(c->amb_ref.ensure(amb.size()));
+      st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
+      if (st) return fail(st);
+      const int ab = (int)std::min<int64_t>(((int64_t)amb.size() + kSomWaves - 1) / kSomWaves, 8192);
+      hipLaunchKernelGGL(variant_support_call, dim3((unsigned)ab), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap,
+                         ctr, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
+                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (hc.n_rec > rec_cap) {
+      rec_cap = hc.n_rec + 1024;
+      retry = true;
+    }
+    if (hc.pool_used > pool_cap) {
+      pool_cap = hc.pool_used + 4096;
+      retry = true;
+    }
+    if (!retry || hc.err) break;
+    if (attempt == 2) return fail(set_err(GQ_E_CAPACITY, "variant-support output capacity retries exhausted"));
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  st = check_device_error(c, hc);
+  if (st) return fail(st);
+  const int64_t nr = pl.n_tiles > 0 ? (int64_t)hc.n_rec : 0;
+  std::vector<VsRec> recs((size_t)nr);
+  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(VsRec), hipMemcpyDeviceToHost, c->stream));
+  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  // loci in call order; a locus's alleles by (ref, alt) bytes (the reference iterates a HashMap)
+  auto bytes = [&](const VsRec &r) {
+    std::string b((size_t)(r.ref_len + r.alt_len), '\0');
+    for (int i = 0; i < r.ref_len + r.alt_len; ++i)
+      b[(size_t)i] = (char)(r.ref_len + r.alt_len <= 8 ? (uint8_t)(r.allele >> (8 * i)) : hpool[(size_t)r.allele + (size_t)i]);
+    return b;
+  };
+  std::vector<std::string> ab((size_t)nr);
+  for (int64_t k = 0; k < nr; ++k) ab[(size_t)k] = bytes(recs[(size_t)k]);
+  std::vector<int64_t> ord((size_t)nr);
+  for (int64_t k = 0; k < nr; ++k) ord[(size_t)k] = k;
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    const VsRec &a = recs[(size_t)x], &b = recs[(size_t)y];
+    if (a.key != b.key) return a.key < b.key;
+    const std::string ra = ab[(size_t)x].substr(0, a.ref_len), rb2 = ab[(size_t)y].substr(0, b.ref_len);
+    if (ra != rb2) return ra < rb2;
+    return ab[(size_t)x].substr(a.ref_len) < ab[(size_t)y].substr(b.ref_len);
+  });
+  const size_t N = (size_t)std::max<int64_t>(nr, 1);
+  res->n = nr;
+  res->contig = (int32_t *)malloc(N * 4);
+  res->pos = (int64_t *)malloc(N * 8);
+  res->sample = (int32_t *)malloc(N * 4);
+  res->count = (int32_t *)malloc(N * 4);
+  res->ref_off = (int64_t *)malloc(N * 8);
+  res->alt_off = (int64_t *)malloc(N * 8);
+  res->ref_len = (int32_t *)malloc(N * 4);
+  res->alt_len = (int32_t *)malloc(N * 4);
+  res->flags = (uint8_t *)malloc(N);
+  std::string apool;
+  for (int64_t q = 0; q < nr; ++q) {
+    const int64_t k = ord[(size_t)q];
+    const VsRec &r = recs[(size_t)k];
+    res->contig[q] = r.contig;
+    res->pos[q] = r.pos;
+    res->sample[q] = r.sample;
+    res->count[q] = r.count;
+    res->ref_len[q] = r.ref_len;
+    res->alt_len[q] = r.alt_len;
+    res->ref_off[q] = (int64_t)apool.size();
+    res->alt_off[q] = (int64_t)apool.size() + r.ref_len;
+    res->flags[q] = r.flags;
+    apool += ab[(size_t)k];
+  }
+  res->pool_len = (int64_t)apool.size();
+  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
+  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timings.pileup_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[2]);
+  c->timings.total_ms = ms;
+  c->timings.tiles = pl.n_tiles;
+  c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
+  *out = res;
+  return GQ_OK;
+}
+
+void gq_free_allele_counts(gq_allele_counts *r) {
+  if (!r) return;
+  free(r->contig);
+  free(r->pos);
+  free(r->sample);
+  free(r->count);
+  free(r->ref_off);
+  free(r->alt_off);
+  free(r->ref_len);
+  free(r->alt_len);
+  free(r->allele_pool);
+  free(r->flags);
+  free(r);
 }
 
 void gq_free_somatic(gq_somatic_calls *r) {

@@ -58,6 +58,14 @@ class gq_calls_device(C.Structure):
     _fields_ = [("calls", gq_calls), ("image", C.c_void_p), ("image_bytes", C.c_int64)]
 
 
+class gq_allele_counts(C.Structure):
+    _fields_ = [("n", C.c_int64), ("contig", C.POINTER(C.c_int32)), ("pos", C.POINTER(C.c_int64)),
+                ("sample", C.POINTER(C.c_int32)), ("count", C.POINTER(C.c_int32)),
+                ("ref_off", C.POINTER(C.c_int64)), ("ref_len", C.POINTER(C.c_int32)),
+                ("alt_off", C.POINTER(C.c_int64)), ("alt_len", C.POINTER(C.c_int32)),
+                ("allele_pool", C.c_void_p), ("pool_len", C.c_int64), ("flags", C.POINTER(C.c_uint8))]
+
+
 class gq_counts(C.Structure):
     _fields_ = [("n_loci", C.c_int64), ("depth", C.POINTER(C.c_int32)), ("pos_depth", C.POINTER(C.c_int32)),
                 ("base_counts", C.POINTER(C.c_int32)), ("indel_counts", C.POINTER(C.c_int32)),
@@ -121,7 +129,7 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
             "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
-            "gq_reference_free", "gq_somatic_standard_ref")
+            "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts")
 
 
 def lib():
@@ -137,7 +145,7 @@ def lib():
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
                   "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard",
-                  "gq_reference_upload", "gq_somatic_standard_ref"):
+                  "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
                                             C.POINTER(C.POINTER(gq_calls))]
@@ -151,6 +159,9 @@ def lib():
         L.gq_reference_upload.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.c_void_p,
                                           C.POINTER(C.c_void_p)]
         L.gq_reference_free.argtypes = [C.c_void_p]
+        L.gq_variant_support.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
+                                         C.POINTER(C.POINTER(gq_allele_counts))]
+        L.gq_free_allele_counts.argtypes = [C.POINTER(gq_allele_counts)]
         L.gq_free_calls.argtypes = [C.POINTER(gq_calls)]
         L.gq_free_counts.argtypes = [C.POINTER(gq_counts)]
         L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
@@ -288,6 +299,25 @@ class Context:
             return SomaticCalls.from_struct(out.contents)
         finally:
             lib().gq_free_somatic(out)
+
+    def variant_support(self, reads: "DeviceReads", loci) -> List[tuple]:
+        """gq_variant_support: rows (sample index, contig index, locus, ref, alt, count, flags)."""
+        L, keep = make_gq_loci(*loci)
+        out = C.POINTER(gq_allele_counts)()
+        _check(lib().gq_variant_support(self.h, reads.h, C.byref(L), C.byref(out)))
+        try:
+            c = out.contents
+            n = c.n
+            if n == 0:
+                return []
+            arr = lambda p: np.ctypeslib.as_array(p, shape=(n,)).copy()
+            pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
+            contig, pos, smp, cnt = arr(c.contig), arr(c.pos), arr(c.sample), arr(c.count)
+            ro, rl, ao, al, fl = arr(c.ref_off), arr(c.ref_len), arr(c.alt_off), arr(c.alt_len), arr(c.flags)
+            return [(int(smp[i]), int(contig[i]), int(pos[i]), pool[ro[i]:ro[i] + rl[i]].decode("latin-1"),
+                     pool[ao[i]:ao[i] + al[i]].decode("latin-1"), int(cnt[i]), int(fl[i])) for i in range(n)]
+        finally:
+            lib().gq_free_allele_counts(out)
 
     def pileup_counts(self, reads: "DeviceReads", loci) -> Dict[str, np.ndarray]:
         L, keep = make_gq_loci(*loci)

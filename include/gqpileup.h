@@ -256,6 +256,28 @@ gq_status gq_somatic_standard(gq_ctx *ctx, const gq_dev_reads *tumor, const gq_d
                               const gq_loci *loci, const gq_somatic_params *params, gq_somatic_calls **out);
 void gq_free_somatic(gq_somatic_calls *c);
 
+/* variant-support: VariantSupport.pileupToAlleleCounts (commands/VariantSupport.scala:110-118)
+ * over pileupFlatMap(reads, partitions, skipEmpty = true, ...) (:93-100).  One row per
+ * (visited locus, distinct allele of its pileup): every element counts (no filter).  Rows in
+ * call order of the loci, a locus's alleles by (ref, alt) bytes (the reference iterates a Scala
+ * HashMap there: order unpinned).  sample = the pileup's head-element read sample
+ * (Pileup.scala:51); flags bit0 = reference base from heap order (MD tags disagree), bit1 =
+ * the pileup mixes samples (the head element, hence `sample`, is then heap-order dependent). */
+typedef struct {
+  int64_t n;
+  int32_t *contig;
+  int64_t *pos;
+  int32_t *sample;
+  int32_t *count;
+  int64_t *ref_off;  int32_t *ref_len;
+  int64_t *alt_off;  int32_t *alt_len;
+  uint8_t *allele_pool;
+  int64_t pool_len;
+  uint8_t *flags;
+} gq_allele_counts;
+gq_status gq_variant_support(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci, gq_allele_counts **out);
+void gq_free_allele_counts(gq_allele_counts *c);
+
 /* --reference-fasta (SomaticStandardCaller.scala:57, :75).  A reference genome resident in HBM
  * (replaces ReferenceBroadcast.apply, reference/ReferenceBroadcast.scala:39-55): bases[k] /
  * lengths[k] are the unmasked bases of contig k of the read sets' contig list (bases[k] == NULL

@@ -1207,6 +1207,33 @@ int or_somatic_standard(const or_reads *tumor, const or_reads *normal, const or_
   return or_somatic_standard_ref(tumor, normal, loci, nullptr, prm, o, olen);
 }
 
+// VariantSupport.pileupToAlleleCounts (commands/VariantSupport.scala:110-118) over
+// pileupFlatMap(reads, partitions, skipEmpty = true) (:93-100): per pileup, the elements
+// grouped by allele.  Rows: sample of the head element (Pileup.sampleName, Pileup.scala:51),
+// contig, locus, ref, alt, count, flags (bit0: heap-order reference base); within a locus by
+// (ref, alt) — the reference iterates a Scala HashMap there (order unpinned).
+int or_variant_support(const or_reads *reads, const or_loci *loci, char **o, int64_t *olen) {
+  std::string out;
+  return guard(out, o, olen, [&]() {
+    ReadSet rs;
+    buildReads(reads, rs);
+    std::vector<ReadSet *> sets{&rs};
+    forEachPileup(sets, loci, [&](const TaskContig &tc, std::vector<Pileup> &ps, std::vector<bool> &amb) {
+      const Pileup &p = ps[0];
+      if (p.elements.empty()) return;
+      std::map<std::pair<std::string, std::string>, int> counts;
+      for (const Elem &e : p.elements) {
+        const Evaluated &ev = e.evaluate();
+        ++counts[{ev.allele.ref, ev.allele.alt}];
+      }
+      for (const auto &kv : counts)
+        appendf(out, "%d\t%s\t%lld\t%s\t%s\t%d\t%d\n", p.elements.front().read->sample,
+                loci->contig_names[tc.contig], (long long)p.locus, kv.first.first.c_str(), kv.first.second.c_str(),
+                kv.second, amb[0] ? 1 : 0);
+    });
+  });
+}
+
 int or_elements_at(const or_reads *reads, int32_t contig, int64_t locus, int32_t own_ref, char **o, int64_t *olen) {
   std::string out;
   return guard(out, o, olen, [&]() {

@@ -102,6 +102,12 @@ typedef struct {
 int or_somatic_standard_ref(const or_reads *tumor, const or_reads *normal, const or_loci *loci,
                             const or_reference *ref, const or_somatic_params *p, char **out, int64_t *out_len);
 
+/* variant-support (VariantSupport.scala:110-118).  Lines:
+ *   sample \t contig \t locus \t ref \t alt \t count \t flags
+ * sample = index of the head element's read sample; flags bit0 = pileup reference base
+ * depends on heap order; within a locus rows by (ref, alt).                            */
+int or_variant_support(const or_reads *reads, const or_loci *loci, char **out, int64_t *out_len);
+
 /* ---- single-locus entry points used to pin the oracle with the reference's unit
  * KATs.  They build the pileup with Pileup.apply(reads, contig, locus)
  * (Pileup.scala:181-186): reads in input order, reference base from

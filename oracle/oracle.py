@@ -172,6 +172,18 @@ def somatic_standard(tumor, normal, loci, reference=None, **params):
     return out
 
 
+def variant_support(rs, loci):
+    """Rows (sample index, contig, locus, ref, alt, count, flags) — see oracle.h."""
+    m = _Marshalled(rs)
+    L = _Loci(rs.contig_names, *loci)
+    text = _call(lib().or_variant_support, C.byref(m.s), C.byref(L.s))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        out.append((int(f[0]), f[1], int(f[2]), f[3], f[4], int(f[5]), int(f[6])))
+    return out
+
+
 # ---- single-locus entry points (Pileup.apply semantics), used by the KAT tests
 def _contig_id(rs, contig: str) -> int:
     return rs.contig_names.index(contig)
