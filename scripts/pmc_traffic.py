@@ -60,7 +60,8 @@ def main():
         out = {"kernel": a.kernel.rstrip("<"), "length": a.length, "depth": a.depth,
                "hbm_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
                "raw_FETCH_SIZE_KiB": pm["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": pm["WRITE_SIZE"],
-               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), KiB->bytes; WRITE_SIZE as is",
+               "correction": ("FETCH_SIZE x2 (gfx950 tallies the kernel's 128-B coalesced requests at 64 B: raw "
+                              "FETCH_SIZE is below the launch's compulsory read bytes), KiB->bytes; WRITE_SIZE as is"),
                "source": "profiles/%s_pmc.csv" % a.tag}
         with open(os.path.join(prof, "traffic_%s.json" % a.round), "w") as fh:
             json.dump(out, fh, indent=1)
