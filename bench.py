@@ -189,7 +189,7 @@ def main() -> int:
     bytes_md = 4 * int(a["md_ev"].shape[0])
     bytes_out = 32 * len(calls) + 12 * int(calls.complex_loci)
     b_all = bytes_seq + bytes_meta + bytes_cigar + bytes_md + bytes_out
-    read_bytes = int(st["proj_bytes"]) + 20 * n_reads + 8 * int(st["pev_count"])
+    read_bytes = int(st["proj_bytes"]) + 12 * n_reads + 8 * int(st["pev_count"])
     kept = 1.0 - float(np.mean(walk_frac))
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))
@@ -355,7 +355,7 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
     b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
              + 8 * ng.n)
     st = ctx.proj_stats(t)
-    read_bytes = 3 * int(st["proj_bytes"]) + 20 * tg.n + 8 * int(st["pev_count"]) + 8 * ng.n
+    read_bytes = 3 * int(st["proj_bytes"]) + 12 * tg.n + 8 * int(st["pev_count"]) + 8 * ng.n
     k_ms = float(np.mean(stages["pileup_ms"]))
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)

@@ -4,12 +4,13 @@
 //
 // One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
 // (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
-// block B0 and the projection word of any read at that column sits at base + 8 * column.
-// Lanes 16g .. 16g + 15 (group g) own the 128-locus sub-span [B0 + 128g, B0 + 128g + 128) and
-// walk the reads that can overlap it, one read per group per step:
+// block B0.  Lanes 16g .. 16g + 15 (group g) own the 128-locus slice [B0 + 128g, B0 + 128g +
+// 128), whose projection words are one contiguous run in the slice-major pool (ProjRec), and
+// walk the reads that can overlap it in read order, one read per group per step:
 //
-//     on  = col0 <= column < col1                         (the read covers the column)
-//     w   = buffer_load_b64(tile window, on ? base + 8 * column : out of range -> 0)
+//     [s0, e0) = the read's columns inside the slice, off = the words of the earlier reads
+//     w   = buffer_load_b64(slice run, column in [s0, e0) ? 8 (off + column - s0) : out of range -> 0)
+//     off += e0 - s0
 //     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
 //     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
 //
@@ -61,7 +62,8 @@ __device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n
 
 __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_PROJ_WPE))) void germline_proj(
     const Tile *__restrict__ tiles, int64_t n_tiles, const ProjRec *__restrict__ prec,
-    const int32_t *__restrict__ pmax_end, const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev,
+    const int32_t *__restrict__ pmax_end, const uint8_t *__restrict__ proj, const int64_t *__restrict__ qoff,
+    const int64_t *__restrict__ sbase, const uint2 *__restrict__ pev,
     const int64_t *__restrict__ pev_off, int n_samples, int threshold, int emit_ref, int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
@@ -71,12 +73,12 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   constexpr int T = C::kT, U = C::kU;
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // event read bases: A C T G bytes
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
-  __shared__ __attribute__((aligned(16))) uint2 recw[C::kWaves][C::kRecBuf];  // the tile's read records
+  __shared__ __attribute__((aligned(16))) uint32_t recw[C::kWaves][C::kRecBuf];  // the tile's read records
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave];
-  uint2 *rec = recw[wave];
+  uint32_t *rec = recw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
@@ -96,7 +98,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
   auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
-  const uint4 *prec4 = reinterpret_cast<const uint4 *>(prec);
+  const uint2 *prec2 = reinterpret_cast<const uint2 *>(prec);
+  const int32_t g16 = 16 * g;
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const Tile tl = tiles[i];
@@ -104,12 +107,12 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const int64_t rb = tl.rb, re = tl.re;
     const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
     const int32_t myc = C0 + lane;
-    // ---- the read range of each group: reads [rb + lo_g, rb + hi_g) can overlap sub-span g
-    //      (pmax_end > its first locus, start < its end).  The window's read records go to
-    //      LDS as {col0 - C0 (16 bits) | span << 16, word offset of column C0 in the tile's
-    //      projection window}.  A read the projection cannot take, or a window of more than
-    //      kRecCap reads, sends the tile to the walker.  The window's records and the first
-    //      kEnt sparse entries per lane are loaded together, before any is used.
+    // ---- the read range of each group: reads [rb + lo_g, rb + hi_g) can overlap slice g
+    //      (pmax_end > its first locus, start < its end).  The window (every read with words
+    //      in the block: plan_tiles starts it at B0) goes to LDS as {col0 - C0 (16 bits) |
+    //      span << 16}.  A read the projection cannot take, or a window of more than kRecCap
+    //      reads, sends the tile to the walker.  The window's records, the slices' word
+    //      offsets and the first kEnt sparse entries per lane are loaded together.
     const int64_t nwin = re - rb;
     if (nwin > C::kRecCap) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
@@ -117,21 +120,20 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     }
     if (nwin <= 0) continue;  // no reads: nothing visited
     const int nrd = (int)nwin;
-    const uint4 pr0 = prec4[rb], pr1 = prec4[re];
-    const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
-    const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
+    const int64_t qs = qoff[tl.contig] + (B0 >> 7);  // the block's first slice
+    const int64_t sb0 = sbase[qs], sb4 = sbase[qs + 4];
+    const uint32_t gb = (uint32_t)(sbase[qs + g] - sb0);  // this group's slice run, in words
     const int64_t e0 = pev_off[rb], e1 = pev_off[re];
-    const uint32_t ybias = (uint32_t)(8 * C0) - (uint32_t)tb;
     constexpr int NQ = C::kRecCap / 64, NE = C::kEnt;
     int32_t pe[NQ];
-    uint4 pp[NQ];
+    uint2 pp[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       pe[q] = 0x7FFFFFFF;
-      pp[q] = make_uint4(0x7FFFFFFFu, 0u, 0u, 0u);
+      pp[q] = make_uint2(0x7FFFFFFFu, 0u);
       if (64 * q + lane < nrd) {
         pe[q] = pmax_end[rb + 64 * q + lane];
-        pp[q] = prec4[rb + 64 * q + lane];
+        pp[q] = prec2[rb + 64 * q + lane];
       }
     }
     uint2 ent[NE];
@@ -147,8 +149,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     for (int q = 0; q < NQ; ++q) {
       if (64 * q >= nrd) break;
       const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
-      if (64 * q + lane < nrd)
-        rec[64 * q + lane] = make_uint2((uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16), pp[q].z + ybias);
+      if (64 * q + lane < nrd) rec[64 * q + lane] = (uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16);
       bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
       lo0 += (int)__popcll(__ballot(pe[q] <= B0));
       lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
@@ -172,11 +173,11 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     //      after the sub-span's end (start-sorted), which covers none of its columns, or the
     //      padding record (span 0) at the window's end.  Two batches of loads stay in flight
     //      while a third is counted; the sparse entries are applied while the first two land.
-    if (lane == 0) rec[nrd] = make_uint2(0u, 0u);
+    if (lane == 0) rec[nrd] = 0u;
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(proj + tb), (short)0, (int)(te - tb), 0x00020000);
-    const uint32_t l8 = 8u * (uint32_t)lane;
+        (void *)(proj + 8 * sb0), (short)0, (int)(8 * (sb4 - sb0)), 0x00020000);
+    uint32_t off = gb;  // this group's slice run + the words of its earlier reads there
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -191,14 +192,18 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       nn = 0;
     };
     auto issue = [&](int k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
-      uint2 rv[U];
+      uint32_t rv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];  // all LDS reads first
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint2 rr = rv[u];
-        const int32_t d = lane - (int32_t)(int16_t)(rr.x & 0xFFFFu);  // column - col0
-        const uint32_t voff = (uint32_t)d < (rr.x >> 16) && !(dbg & 1) ? rr.y + l8 : 0x80000000u;
+        const uint32_t rr = rv[u];
+        const int32_t c0 = (int32_t)(int16_t)(rr & 0xFFFFu);  // the read's columns, tile-relative
+        const int32_t s0 = max(c0, g16), se = min(c0 + (int32_t)(rr >> 16), g16 + 16);
+        const uint32_t sl = (uint32_t)max(se - s0, 0);  // its words in this group's slice
+        const uint32_t d = (uint32_t)(lane - s0);
+        const uint32_t voff = d < sl && !(dbg & 1) ? 8u * (off + d) : 0x80000000u;
+        off += sl;
         const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
         w0[u] = w[0];
         w1[u] = w[1];

@@ -124,6 +124,65 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// One wave over the words of projection slice `slot` (the slice-major pool, ProjRec in
+// gq_kernels.h): its reads are those of the slice's contig with pmax_end > the slice's first
+// locus and start < its end, in read order; each contributes its columns inside the slice.
+// put(active, read, column, word index in the slice) runs with every lane of the wave
+// (uniform control flow), active for lanes that hold a word.
+template <class F>
+__device__ __forceinline__ void walk_slice_words(const DevReads &R, int64_t slot, F &&put) {
+  const int lane = threadIdx.x & 63;
+  int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (R.qoff[m] <= slot) lo = m;
+    else hi = m - 1;
+  }
+  const int c = lo;
+  const int32_t q = (int32_t)(slot - R.qoff[c]);
+  const int32_t L = 128 * q, qc0 = 16 * q, qc1 = qc0 + 16;
+  const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
+  int64_t a0 = cb, a1 = ce;
+  while (a0 < a1) {  // first read with pmax_end > L
+    const int64_t m = (a0 + a1) >> 1;
+    if (R.pmax_end[m] > L) a1 = m;
+    else a0 = m + 1;
+  }
+  const int64_t ra = a0;
+  a1 = ce;
+  while (a0 < a1) {  // first read with start >= L + 128
+    const int64_t m = (a0 + a1) >> 1;
+    if (R.start[m] >= L + 128) a1 = m;
+    else a0 = m + 1;
+  }
+  const int64_t rz = a0;
+  uint32_t run = 0;
+  for (int64_t r0 = ra; r0 < rz; r0 += 64) {
+    const int64_t r = r0 + lane;
+    int32_t s0 = 0, sl = 0;
+    if (r < rz) {
+      const ProjRec p = R.prec[r];
+      if (p.col1 != kProjNone) {
+        s0 = p.col0 > qc0 ? p.col0 : qc0;
+        const int32_t e = p.col1 < qc1 ? p.col1 : qc1;
+        sl = e > s0 ? e - s0 : 0;
+      }
+    }
+    const uint32_t incl = wave_incl_scan((uint32_t)sl), ex = incl - (uint32_t)sl;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
+      const uint32_t w = w0 + (uint32_t)lane;
+      int k = 0;  // the last lane whose words start at or before w
+#pragma unroll
+      for (int b = 32; b >= 1; b >>= 1)
+        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+      const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
+      put(w < tot, r0 + k, col, (int64_t)run + w);
+    }
+    run += tot;
+  }
+}
+
 // Wave-aggregated reservation of n <= 3 slots per lane on an LDS counter: lane prefixes
 // from two ballots, one returning LDS atomic by the first active lane (a few hundred
 // cycles, not the microseconds of a returning device-scope atomic).
@@ -231,7 +290,8 @@ struct gq_dev_reads {
   std::vector<int64_t> contig_read_begin;  // host copy
   std::vector<void *> owned;               // device allocations owned by this handle
   int64_t seq_bytes = 0;
-  int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // germline projection sizes (derive_shape)
+  int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // projection sizes (derive_shape)
+  int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
   mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
   mutable int mproj_mapq = -1;
 };

@@ -52,24 +52,30 @@ struct DevReads {
   const struct ColDesc *cdesc;  // one per read
   const uint32_t *cev;          // per read: MD events (offset << 16 | MD base << 8 | read base), segments
   const int64_t *caux_off;      // n_reads + 1 offsets into cev
-  // derived at upload for the germline projection kernel (germline_proj, see ProjRec)
-  const struct ProjRec *prec;   // n_reads + 1 (the last: end of the projection pool)
-  const uint8_t *proj;          // locus-aligned base codes, 8 loci per word
+  // derived at upload for the projection kernels (germline_proj / somatic_proj, see ProjRec)
+  const struct ProjRec *prec;   // n_reads + 1 (the last: a zero record)
+  const uint8_t *proj;          // base codes, 8 loci per word, slice-major (see ProjRec)
+  const int64_t *qoff;          // n_contigs + 1: each contig's first slice (slice = 128 loci)
+  const int64_t *sbase;         // qoff[n_contigs] + 1: each slice's first word in proj
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
   const int64_t *pev_off;       // n_reads + 1 offsets into pev
 };
 
-// Per-read record of the germline projection kernel (16 bytes).  The read's projection is
-// the words of 8 loci [8 * col0, 8 * col1) at byte offset base + 8 * col in `proj`: one byte
-// per locus, the read's base there as a code (A 1, C 3, T 4, G 7: ASCII & 7) where the
-// element is a Match/Mismatch (PileupElement.scala:68-135), 0 elsewhere (outside the read,
-// deleted / skipped loci, insertion and deletion anchors, N bases).  col1 = kProjNone marks a
-// read the projection path cannot take (bases other than A C G T N, no MD tag, a P op ...).
+// Per-read record of the projection kernels (8 bytes): the read spans the 8-locus columns
+// [col0, col1).  Its projection holds one byte per locus, the read's base there as a code
+// (A 1, C 3, T 4, G 7: ASCII & 7) where the element is a Match/Mismatch
+// (PileupElement.scala:68-135), 0 elsewhere (outside the read, deleted / skipped loci,
+// insertion and deletion anchors, N bases).  The pool is SLICE-MAJOR: slice q of contig c
+// (loci [128 q, 128 q + 128), columns [16 q, 16 q + 16)) holds, from word sbase[qoff[c] + q],
+// the words of every read with columns in the slice, in read order, each read's columns
+// [max(col0, 16 q), min(col1, 16 q + 16)).  So the 16 lanes that own a slice stream one
+// contiguous run of words over their reads (a read's offset in the run = the sum of the
+// earlier reads' pieces).  col1 = kProjNone marks a read the projection path cannot take
+// (bases other than A C G T N, no MD tag, a P op ...); it has no words.
 struct ProjRec {
   int32_t col0, col1;
-  int64_t base;
 };
-static_assert(sizeof(ProjRec) == 16, "ProjRec layout");
+static_assert(sizeof(ProjRec) == 8, "ProjRec layout");
 constexpr int32_t kProjNone = (int32_t)0x80000000;
 // Sparse entries of a read (uint2 {x = locus, y}), in any order:
 //   y bit 31 clear: MD event / N base at locus x: bits 0-3 the MD reference base's std_bit

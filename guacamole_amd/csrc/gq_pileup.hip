@@ -76,11 +76,14 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   const int64_t L1 = aligned ? min(blk + (int64_t)T, r_end[r]) : min(L0 + (int64_t)T, r_end[r]);
   const int32_t c = r_contig[r];
   int64_t b = R.contig_read_begin[c], e = R.contig_read_begin[c + 1];
-  // rb: first read with pmax_end > L0 (pmax_end non-decreasing within the contig)
+  // rb: first read with pmax_end > L0 (pmax_end non-decreasing within the contig); aligned
+  // tiles start their window at the block (every read with words in the block's projection
+  // slices, so that a read's place in a slice is the sum of the window's earlier pieces)
+  const int64_t W0 = aligned ? blk : L0;
   int64_t a0 = b, a1 = e;
   while (a0 < a1) {
     int64_t m = (a0 + a1) >> 1;
-    if ((int64_t)R.pmax_end[m] > L0) a1 = m;
+    if ((int64_t)R.pmax_end[m] > W0) a1 = m;
     else a0 = m + 1;
   }
   const int64_t rb = a0;
@@ -239,16 +242,14 @@ __device__ __forceinline__ uint32_t proj_code(uint8_t b) {  // A 1, C 3, T 4, G 
 }
 __device__ __forceinline__ bool proj_ok(uint32_t info) { return (info & (kColEligible | kColGeneral)) != 0; }
 
-// Words (8-locus columns) and sparse entries of each read's projection; entry n is 0.
-__global__ void proj_count(DevReads R, const uint32_t *__restrict__ n_nbase, int64_t *__restrict__ nwords,
-                           int64_t *__restrict__ nents) {
+// Sparse entries of each read's projection; entry n is 0.
+__global__ void proj_count(DevReads R, const uint32_t *__restrict__ n_nbase, int64_t *__restrict__ nents) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R.n_reads) return;
-  int64_t w = 0, e = 0;
+  int64_t e = 0;
   if (r < R.n_reads) {
     const ColDesc d = R.cdesc[r];
     if (proj_ok(d.info)) {
-      w = (int64_t)((d.end + 7) >> 3) - (int64_t)(d.start >> 3);
       const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
       e = nmd + (int64_t)n_nbase[r];
       if (d.info & kColGeneral) {
@@ -258,25 +259,39 @@ __global__ void proj_count(DevReads R, const uint32_t *__restrict__ n_nbase, int
       }
     }
   }
-  nwords[r] = w;
   nents[r] = e;
 }
 
-// ProjRec of each read from the word offsets; record n closes the pool.
-__global__ void prec_fill(DevReads R, const int64_t *__restrict__ woff, ProjRec *__restrict__ prec) {
+// ProjRec of each read (record n: zero).
+__global__ void prec_fill(DevReads R, ProjRec *__restrict__ prec) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R.n_reads) return;
-  ProjRec p;
-  if (r == R.n_reads) {
-    p.col0 = p.col1 = 0;
-    p.base = 8 * woff[r];
-  } else {
+  ProjRec p{0, 0};
+  if (r < R.n_reads) {
     const ColDesc d = R.cdesc[r];
     p.col0 = d.start >> 3;
     p.col1 = proj_ok(d.info) ? (d.end + 7) >> 3 : kProjNone;
-    p.base = 8 * woff[r] - 8 * (int64_t)p.col0;
   }
   prec[r] = p;
+}
+
+// Words per slice (thread per read: each slice it meets gets its piece), for the slice offsets.
+__global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ scnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const ProjRec p = prec[r];
+  if (p.col1 == kProjNone || p.col1 <= p.col0) return;
+  int lo = 0, hi = R.n_contigs - 1;  // contig of r: last c with contig_read_begin[c] <= r
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (R.contig_read_begin[m] <= r) lo = m;
+    else hi = m - 1;
+  }
+  const int64_t q0 = R.qoff[lo];
+  for (int32_t q = p.col0 >> 4; q <= (p.col1 - 1) >> 4; ++q) {
+    const int32_t a = max(p.col0, 16 * q), b = min(p.col1, 16 * q + 16);
+    atomicAdd(&scnt[q0 + q], (unsigned long long)(b - a));
+  }
 }
 
 // Reads the projection takes, into kSpread words (summed on the host): a grid-stride count per
@@ -289,51 +304,45 @@ __global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, unsi
   if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
 }
 
-// The projection words of 256 reads per block (thread per word, coalesced in the pool).
-__global__ __launch_bounds__(256) void proj_fill(DevReads R, const int64_t *__restrict__ woff,
-                                                 uint8_t *__restrict__ proj) {
-  __shared__ int64_t wb[257];
-  const int64_t r0 = (int64_t)blockIdx.x * 256;
-  const int t = threadIdx.x;
-  const int64_t w0 = woff[r0];
-  wb[t] = woff[min(r0 + t, R.n_reads)] - w0;
-  if (t == 0) wb[256] = woff[min(r0 + 256, R.n_reads)] - w0;
-  __syncthreads();
-  const int64_t W = wb[256];
-  for (int64_t w = t; w < W; w += 256) {
-    int lo = 0, hi = 255;  // the last read whose words start at or before w
-    while (lo < hi) {
-      const int m = (lo + hi + 1) >> 1;
-      if (wb[m] <= w) lo = m;
-      else hi = m - 1;
-    }
-    const int64_t r = r0 + lo, j = w - wb[lo];
-    const ColDesc d = R.cdesc[r];
-    const int32_t s = d.start, e = d.end;
-    const int32_t lb = 8 * ((s >> 3) + (int32_t)j);  // locus of byte 0
-    uint32_t v[2] = {0, 0};
-    if (d.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base seq_lo + (l - s)
-      const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+// The projection word of read r at column col (loci [8 col, 8 col + 8)).
+__device__ uint2 proj_word(const DevReads &R, int64_t r, int32_t col) {
+  const ColDesc d = R.cdesc[r];
+  const int32_t s = d.start, e = d.end;
+  const int32_t lb = 8 * col;  // locus of byte 0
+  uint32_t v[2] = {0, 0};
+  if (d.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base seq_lo + (l - s)
+    const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
 #pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int32_t l = lb + q;
+      if (l >= s && l < e) v[q >> 2] |= proj_code(R.seq[p0 + l]) << (8 * (q & 3));
+    }
+  } else {  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
+    const int32_t nmd = (int32_t)(d.info & 0xFFFFu), nseg = (int32_t)((d.info >> 18) & 0xFFu);
+    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+    const int64_t so = R.seq_off[r];
+    for (int32_t q2 = 0; q2 < nseg; ++q2) {
+      const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+      if ((b >> 16) != kSegCount) continue;
+      const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
       for (int q = 0; q < 8; ++q) {
         const int32_t l = lb + q;
-        if (l >= s && l < e) v[q >> 2] |= proj_code(R.seq[p0 + l]) << (8 * (q & 3));
-      }
-    } else {  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
-      const int32_t nmd = (int32_t)(d.info & 0xFFFFu), nseg = (int32_t)((d.info >> 18) & 0xFFu);
-      const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-      const int64_t so = R.seq_off[r];
-      for (int32_t q2 = 0; q2 < nseg; ++q2) {
-        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-        if ((b >> 16) != kSegCount) continue;
-        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
-        for (int q = 0; q < 8; ++q) {
-          const int32_t l = lb + q;
-          if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
-        }
+        if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
       }
     }
-    *reinterpret_cast<uint2 *>(proj + 8 * (w0 + w)) = make_uint2(v[0], v[1]);
+  }
+  return make_uint2(v[0], v[1]);
+}
+
+// The projection pool, one wave per slice (walk_slice_words): coalesced word stores.
+__global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = w0; slot < n_slices; slot += nw) {
+    const int64_t base = R.sbase[slot];
+    walk_slice_words(R, slot, [&](bool act, int64_t r, int32_t col, int64_t w) {
+      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + w)) = proj_word(R, r, col);
+    });
   }
 }
 
@@ -1253,48 +1262,84 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       HIP_TRY(hipGetLastError());
     }
   }
-  {  // projections (germline_proj): per-read word / entry counts, offsets, records, pools
+  {  // projections: records, the slice-major pool (slices of whole 512-locus blocks up to each
+     // contig's largest read end), sparse entries
     const int64_t n = d->d.n_reads;
-    void *cnt = nullptr, *off = nullptr, *tmp = nullptr, *pr = nullptr, *pj = nullptr, *pe = nullptr;
-    HIP_TRY(hipMalloc(&cnt, sizeof(int64_t) * 2 * (size_t)(n + 1)));
-    HIP_TRY(hipMalloc(&off, sizeof(int64_t) * 2 * (size_t)(n + 1)));
-    d->owned.push_back(off);
-    int64_t *nw = (int64_t *)cnt, *ne = nw + (n + 1), *wo = (int64_t *)off, *eo = wo + (n + 1);
-    const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, nw, ne);
-    HIP_TRY(hipGetLastError());
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nw, wo, (int)(n + 1), c->stream));
-    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nw, wo, (int)(n + 1), c->stream));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ne, eo, (int)(n + 1), c->stream));
-    int64_t tot[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&tot[0], wo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&tot[1], eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(tmp);
-    (void)hipFree(cnt);
+    const int nc = d->d.n_contigs;
+    std::vector<int64_t> qoff((size_t)nc + 1, 0);
+    {
+      std::vector<int32_t> last((size_t)nc, 0);
+      const auto &crb = d->contig_read_begin;
+      for (int k = 0; k < nc; ++k)
+        if (crb[(size_t)k + 1] > crb[(size_t)k])
+          HIP_TRY(hipMemcpyAsync(&last[(size_t)k], d->d.pmax_end + (crb[(size_t)k + 1] - 1), sizeof(int32_t),
+                                 hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (int k = 0; k < nc; ++k) {
+        const int64_t col1 = ((int64_t)std::max(last[(size_t)k], 0) + 7) >> 3;
+        qoff[(size_t)k + 1] = qoff[(size_t)k] + 4 * ((col1 + 63) >> 6);
+      }
+    }
+    const int64_t n_sl = qoff[(size_t)nc];
+    void *qo = nullptr, *pr = nullptr, *sc = nullptr, *sb = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
+         *eo = nullptr, *pe = nullptr;
+    HIP_TRY(hipMalloc(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
+    d->owned.push_back(qo);
+    HIP_TRY(hipMemcpyAsync(qo, qoff.data(), sizeof(int64_t) * ((size_t)nc + 1), hipMemcpyHostToDevice, c->stream));
+    d->d.qoff = (const int64_t *)qo;
     HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
     d->owned.push_back(pr);
+    const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
+    HIP_TRY(hipGetLastError());
+    d->d.prec = (const ProjRec *)pr;
+    HIP_TRY(hipMalloc(&sc, sizeof(int64_t) * (size_t)(n_sl + 1)));
+    HIP_TRY(hipMemsetAsync(sc, 0, sizeof(int64_t) * (size_t)(n_sl + 1), c->stream));
+    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
+    d->owned.push_back(sb);
+    if (n > 0) {
+      hipLaunchKernelGGL(slice_count, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (const ProjRec *)pr, (unsigned long long *)sc);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
+    HIP_TRY(hipMalloc(&eo, sizeof(int64_t) * (size_t)(n + 1)));
+    d->owned.push_back(eo);
+    hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, (int64_t *)ne);
+    HIP_TRY(hipGetLastError());
+    size_t tb = 0, tb2 = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)sc, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)sc, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+    int64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(tmp);
+    (void)hipFree(sc);
+    (void)hipFree(ne);
+    d->d.sbase = (const int64_t *)sb;
     HIP_TRY(hipMalloc(&pj, (size_t)(8 * tot[0] + 16)));
     d->owned.push_back(pj);
     HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
     d->owned.push_back(pe);
-    hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const int64_t *)wo, (ProjRec *)pr);
-    HIP_TRY(hipGetLastError());
-    if (n > 0) {
-      hipLaunchKernelGGL(proj_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->d,
-                         (const int64_t *)wo, (uint8_t *)pj);
+    if (n_sl > 0) {
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(proj_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
       HIP_TRY(hipGetLastError());
+    }
+    if (n > 0) {
       hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
                          (const int64_t *)eo, (uint2 *)pe);
       HIP_TRY(hipGetLastError());
     }
-    d->d.prec = (const ProjRec *)pr;
     d->d.proj = (const uint8_t *)pj;
     d->d.pev = (const uint2 *)pe;
     d->d.pev_off = (const int64_t *)eo;
     d->proj_bytes = 8 * tot[0];
+    d->n_slices = n_sl;
     d->pev_count = tot[1];
     if (n > 0) {  // reads the projection takes
       unsigned long long *nok = nullptr, hk[kSpread];
@@ -1588,7 +1633,7 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   if (germline_use_proj()) {
     hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, tiles, R.prec, R.pmax_end, R.proj, R.pev, R.pev_off, R.n_samples,
+                       (const Tile *)c->tiles.p, tiles, R.prec, R.pmax_end, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
                        p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   } else {
     hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,

@@ -1295,9 +1295,9 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
     HIP_TRY(hipMalloc(&p, (size_t)(2 * t->proj_bytes + 32)));
     t->mproj = p;
   }
-  if (t->d.n_reads > 0)
-    hipLaunchKernelGGL(mproj_fill, dim3((unsigned)((t->d.n_reads + 255) / 256)), dim3(256), 0, c->stream, t->d, min_mapq,
-                       (int16_t *)t->mproj);
+  if (t->n_slices > 0)
+    hipLaunchKernelGGL(mproj_fill, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
+                       c->stream, t->d, t->n_slices, min_mapq, (int16_t *)t->mproj);
   HIP_TRY(hipGetLastError());
   t->mproj_mapq = min_mapq;
   return GQ_OK;

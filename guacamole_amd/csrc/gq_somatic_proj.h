@@ -32,86 +32,76 @@ __device__ __forceinline__ int16_t margin_term(bool match, int q, float em, floa
   return (int16_t)(v > 32767.0f ? 32767.0f : v);
 }
 
-// The margin projection of the tumor reads, laid out as `proj` (int16 per locus): thread per
-// 8-locus word, 256 reads per block.  Reads the mapq filter drops (QualityAlignedReadsFilter,
-// PileupElementsFilter.scala:25-36) and non-Match/Mismatch loci hold 0.
-__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int min_mapq, int16_t *__restrict__ mproj) {
-  __shared__ int64_t wb[257];
-  const int64_t r0 = (int64_t)blockIdx.x * 256;
-  const int t = threadIdx.x;
-  // word offsets of the block's reads (their projections are consecutive in the pool)
-  const int64_t w0 = (R.prec[min(r0, R.n_reads)].base + 8 * (int64_t)R.prec[min(r0, R.n_reads)].col0) >> 3;
-  {
-    const int64_t r = min(r0 + t, R.n_reads);
-    wb[t] = ((R.prec[r].base + 8 * (int64_t)R.prec[r].col0) >> 3) - w0;
-    if (t == 0) {
-      const int64_t rl = min(r0 + 256, R.n_reads);
-      wb[256] = ((R.prec[rl].base + 8 * (int64_t)R.prec[rl].col0) >> 3) - w0;
+// The margin word of tumor read r at column col (8 loci, int16 each; hom_ref_margin_lane's
+// terms).  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
+// 25-36) and non-Match/Mismatch loci hold 0.
+__device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq) {
+  const ColDesc d = R.cdesc[r];
+  const int32_t s = d.start;
+  const int32_t lb = 8 * col;
+  int16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int mq = (int)R.mapq[r];
+  if (!(min_mapq > 0 && mq < min_mapq)) {
+    const float em = exp2f(-0.33219281f * (float)mq);
+    const float lsm = log1pf(-em);
+    const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+    const uint32_t *ev = R.md_ev + R.md_off[r];
+    // MD events at offsets >= lb - s (sorted)
+    int k = 0, hi2 = nmd;
+    while (k < hi2) {
+      const int m = (k + hi2) >> 1;
+      if ((int32_t)(ev[m] >> 8) < lb - s) k = m + 1;
+      else hi2 = m;
     }
-  }
-  __syncthreads();
-  const int64_t W = wb[256];
-  for (int64_t w = t; w < W; w += 256) {
-    int lo = 0, hi = 255;
-    while (lo < hi) {
-      const int m = (lo + hi + 1) >> 1;
-      if (wb[m] <= w) lo = m;
-      else hi = m - 1;
-    }
-    const int64_t r = r0 + lo, j = w - wb[lo];
-    const ColDesc d = R.cdesc[r];
-    const int32_t s = d.start;
-    const int32_t lb = 8 * ((s >> 3) + (int32_t)j);
-    int16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int mq = (int)R.mapq[r];
-    if (!(min_mapq > 0 && mq < min_mapq)) {
-      const float em = exp2f(-0.33219281f * (float)mq);
-      const float lsm = log1pf(-em);
-      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
-      const uint32_t *ev = R.md_ev + R.md_off[r];
-      // MD events at offsets >= lb - s (sorted)
-      int k = 0, hi2 = nmd;
-      while (k < hi2) {
-        const int m = (k + hi2) >> 1;
-        if ((int32_t)(ev[m] >> 8) < lb - s) k = m + 1;
-        else hi2 = m;
+    auto term_at = [&](int q8, int32_t l, int64_t p) {  // element at locus l, base / quality at pool offset p
+      const int32_t off = l - s;
+      while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
+      const bool event = k < nmd && (int32_t)(ev[k] >> 8) == off;
+      const int q = (int)(int8_t)R.qual[p];
+      v[q8] = margin_term(!event, q, em, lsm);
+    };
+    if (d.info & kColEligible) {
+      const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+      for (int q8 = 0; q8 < 8; ++q8) {
+        const int32_t l = lb + q8;
+        if (l >= s && l < d.end) term_at(q8, l, p0 + l);
       }
-      auto term_at = [&](int q8, int32_t l, int64_t p) {  // element at locus l, base / quality at pool offset p
-        const int32_t off = l - s;
-        while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
-        const bool event = k < nmd && (int32_t)(ev[k] >> 8) == off;
-        const int q = (int)(int8_t)R.qual[p];
-        v[q8] = margin_term(!event, q, em, lsm);
-      };
-      if (d.info & kColEligible) {
-        const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
-        for (int q8 = 0; q8 < 8; ++q8) {
-          const int32_t l = lb + q8;
-          if (l >= s && l < d.end) term_at(q8, l, p0 + l);
-        }
-      } else {  // general CIGAR: the count segments
-        const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
-        const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-        const int64_t so = R.seq_off[r];
-        for (int q8 = 0; q8 < 8; ++q8) {
-          const int32_t l = lb + q8;
-          for (int32_t q2 = 0; q2 < nseg; ++q2) {
-            const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-            const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
-            if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
-              term_at(q8, l, so + (int32_t)(b & 0xFFFFu) + (l - ra));
-              break;
-            }
+    } else {  // general CIGAR: the count segments
+      const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+      const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+      const int64_t so = R.seq_off[r];
+      for (int q8 = 0; q8 < 8; ++q8) {
+        const int32_t l = lb + q8;
+        for (int32_t q2 = 0; q2 < nseg; ++q2) {
+          const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+          const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
+          if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
+            term_at(q8, l, so + (int32_t)(b & 0xFFFFu) + (l - ra));
+            break;
           }
         }
       }
     }
-    uint4 o;
-    o.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
-    o.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
-    o.z = (uint32_t)(uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16);
-    o.w = (uint32_t)(uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16);
-    *reinterpret_cast<uint4 *>(mproj + 8 * (w0 + w)) = o;
+  }
+  uint4 o;
+  o.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
+  o.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
+  o.z = (uint32_t)(uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16);
+  o.w = (uint32_t)(uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16);
+  return o;
+}
+
+// The margin projection of the tumor reads, laid out as `proj` (an int16 per projection byte:
+// word w of the pool at mproj + 16 w), one wave per slice.
+__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
+                                                  int16_t *__restrict__ mproj) {
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = w0; slot < n_slices; slot += nw) {
+    const int64_t base = R.sbase[slot];
+    walk_slice_words(R, slot, [&](bool act, int64_t r, int32_t col, int64_t w) {
+      if (act) *reinterpret_cast<uint4 *>(mproj + 8 * (base + w)) = margin_word(R, r, col, min_mapq);
+    });
   }
 }
 
@@ -167,12 +157,12 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // tumor event read bases: A C T G bytes
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
   __shared__ __attribute__((aligned(16))) uint32_t cvw[C::kWaves][T];  // normal coverage differences
-  __shared__ __attribute__((aligned(16))) uint2 recw[C::kWaves][C::kRecBuf];
+  __shared__ __attribute__((aligned(16))) uint32_t recw[C::kWaves][C::kRecBuf];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave], *cv = cvw[wave];
-  uint2 *rec = recw[wave];
+  uint32_t *rec = recw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
@@ -186,7 +176,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
   const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
   unsigned visited = 0;
   const int g = lane >> 4;
-  const uint4 *prec4 = reinterpret_cast<const uint4 *>(RT.prec);
+  const uint2 *prec2 = reinterpret_cast<const uint2 *>(RT.prec);
+  const int32_t g16 = 16 * g;
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const Tile tt = tiles_t[i], tn = tiles_n[i];
     const int32_t L0 = tt.L0, L1 = tt.L1;
@@ -199,21 +190,23 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     }
     const int nrd = (int)nwin;
     // ---- tumor: read records (LDS), group ranges, the first sparse entries (as germline_proj)
-    const uint4 pr0 = prec4[rb], pr1 = prec4[re];
-    const int64_t tb = (int64_t)(((uint64_t)pr0.w << 32) | pr0.z) + 8 * (int64_t)(int32_t)pr0.x;
-    const int64_t te = (int64_t)(((uint64_t)pr1.w << 32) | pr1.z) + 8 * (int64_t)(int32_t)pr1.x;
+    // the block's first slice: it exists only where tumor reads reach the block (a tile may
+    // hold normal reads alone, past the tumor's last read)
+    const bool tumor = nrd > 0;
+    const int64_t qs = tumor ? RT.qoff[tt.contig] + (B0 >> 7) : 0;
+    const int64_t sb0 = tumor ? RT.sbase[qs] : 0, sb4 = tumor ? RT.sbase[qs + 4] : 0;
+    const uint32_t gb = tumor ? (uint32_t)(RT.sbase[qs + g] - sb0) : 0u;  // this group's slice run, in words
     const int64_t e0 = RT.pev_off[rb], e1 = RT.pev_off[re];
-    const uint32_t ybias = (uint32_t)(8 * C0) - (uint32_t)tb;
     constexpr int NQ = (C::kRecCap + 63) / 64, NE = C::kEnt;
     int32_t pe[NQ];
-    uint4 pp[NQ];
+    uint2 pp[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       pe[q] = 0x7FFFFFFF;
-      pp[q] = make_uint4(0x7FFFFFFFu, 0u, 0u, 0u);
+      pp[q] = make_uint2(0x7FFFFFFFu, 0u);
       if (64 * q + lane < nrd) {
         pe[q] = RT.pmax_end[rb + 64 * q + lane];
-        pp[q] = prec4[rb + 64 * q + lane];
+        pp[q] = prec2[rb + 64 * q + lane];
       }
     }
     uint2 ent[NE];
@@ -229,8 +222,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     for (int q = 0; q < NQ; ++q) {
       if (64 * q >= nrd) break;
       const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
-      if (64 * q + lane < nrd)
-        rec[64 * q + lane] = make_uint2((uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16), pp[q].z + ybias);
+      if (64 * q + lane < nrd) rec[64 * q + lane] = (uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16);
       bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
       lo0 += (int)__popcll(__ballot(pe[q] <= B0));
       lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
@@ -248,15 +240,15 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     }
     const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
     const int hi_me = g == 0 ? hi0 : g == 1 ? hi1 : g == 2 ? hi2 : hi3;
-    if (lane == 0) rec[nrd] = make_uint2(0u, 0u);
+    if (lane == 0) rec[nrd] = 0u;
     // ---- tumor column counts and margin sums (16-bit pairs, loci 2k, 2k + 1 in msum[k])
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t msum[4] = {0, 0, 0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(RT.proj + tb), (short)0, (int)(te - tb), 0x00020000);
+        (void *)(RT.proj + 8 * sb0), (short)0, (int)(8 * (sb4 - sb0)), 0x00020000);
     const __amdgpu_buffer_rsrc_t msrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(mproj + tb), (short)0, (int)(2 * (te - tb)), 0x00020000);
-    const uint32_t l8 = 8u * (uint32_t)lane;
+        (void *)(mproj + 8 * sb0), (short)0, (int)(16 * (sb4 - sb0)), 0x00020000);
+    uint32_t off = gb;  // this group's slice run + the words of its earlier reads there
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -271,13 +263,17 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       nn = 0;
     };
     auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {
-      uint2 rv[U];
+      uint32_t rv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int32_t d = lane - (int32_t)(int16_t)(rv[u].x & 0xFFFFu);
-        const uint32_t voff = (uint32_t)d < (rv[u].x >> 16) ? rv[u].y + l8 : 0x80000000u;
+        const int32_t c0 = (int32_t)(int16_t)(rv[u] & 0xFFFFu);
+        const int32_t s0 = max(c0, g16), se = min(c0 + (int32_t)(rv[u] >> 16), g16 + 16);
+        const uint32_t sl = (uint32_t)max(se - s0, 0);
+        const uint32_t d = (uint32_t)(lane - s0);
+        const uint32_t voff = d < sl ? 8u * (off + d) : 0x80000000u;
+        off += sl;
         const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
         const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(voff == 0x80000000u ? voff : 2 * voff), 0, 0);
         w[u] = make_uint2(a[0], a[1]);
