@@ -37,7 +37,7 @@ __device__ __forceinline__ int allele_alt_len(const AlleleDesc &d) {
 }
 // Byte i of the ref (which=0) / alt (which=1) allele.  DEL bytes 1.. come from the
 // read's MD deletion events at pos+1.. (PileupElement.scala:108-114).
-__device__ uint8_t allele_byte(const DevReads &R, const AlleleDesc &d, int32_t pos, int which, int i) {
+__device__ __forceinline__ uint8_t allele_byte(const DevReads &R, const AlleleDesc &d, int32_t pos, int which, int i) {
   switch (d.kind) {
     case K_SNV: return which == 0 ? d.rb : d.base;
     case K_INS: {
@@ -89,13 +89,13 @@ __device__ __forceinline__ Key128 key_from(int rl, int al, int sample, F byte) {
   }
   return k;
 }
-__device__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
+__device__ __forceinline__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
   return key_from(allele_ref_len(d), allele_alt_len(d), sample,
                   [&](int which, int i) { return allele_byte(R, d, pos, which, i); });
 }
 
 // Allele ordering (variants/Allele.scala:31-36): ref string, then alt string.
-__device__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDesc &b, int32_t pos) {
+__device__ __forceinline__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDesc &b, int32_t pos) {
   for (int which = 0; which < 2; ++which) {
     const int la = which ? allele_alt_len(a) : allele_ref_len(a);
     const int lb = which ? allele_alt_len(b) : allele_ref_len(b);
@@ -111,7 +111,7 @@ __device__ int allele_cmp(const DevReads &R, const AlleleDesc &a, const AlleleDe
 
 // Locate the PileupElement of read r at `pos` (PileupElement.apply + advanceToLocus) and
 // classify it (PileupElement.alignment).  Returns false and sets *errc on a reference error.
-__device__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
+__device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
   const int32_t s = R.start[r];
   const int64_t cig_off = R.cigar_off[r];
   const int32_t ncig = R.n_cigar[r];
@@ -227,7 +227,7 @@ __device__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refb
 }
 
 // MD-derived reference base of read r at pos (MappedRead.getReferenceBaseAtLocus) or -1 on error.
-__device__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
+__device__ __forceinline__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
   const int32_t s = R.start[r];
   const int64_t cig_off = R.cigar_off[r];
   const int32_t ncig = R.n_cigar[r];

@@ -112,6 +112,46 @@ __device__ __forceinline__ unsigned long long part_slot(const unsigned long long
   return g.slot(which, lo, k - off[lo]);
 }
 
+// First index in [lo, hi) whose monotone predicate (false ... true) holds, hi if none: 64
+// probes per round (wave-uniform bounds; every lane active).  A window of n reads takes
+// ceil(log64 n) dependent loads.
+template <class P>
+__device__ __forceinline__ int64_t wave_first_true(int64_t lo, int64_t hi, P &&pred) {
+  const int lane = threadIdx.x & 63;
+  while (hi - lo > 64) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t p = lo + (int64_t)lane * step;
+    const unsigned long long b = __ballot(p >= hi || pred(p));
+    if (!b) {
+      lo = lo + 63 * step + 1;
+      continue;
+    }
+    const int f = __ffsll((long long)b) - 1;
+    if (f == 0) return lo;
+    const int64_t nhi = lo + (int64_t)f * step;  // true there (or hi)
+    lo = lo + (int64_t)(f - 1) * step + 1;
+    hi = nhi < hi ? nhi : hi;
+  }
+  const int64_t p = lo + lane;
+  const unsigned long long b = __ballot(p >= hi || pred(p));
+  return b ? lo + (__ffsll((long long)b) - 1) : hi;
+}
+
+// part_slot for a wave-uniform k, the search spread over the lanes: two rounds of 64 probes
+// (two dependent loads instead of a twelve-step binary search).  Every lane must be active.
+__device__ __forceinline__ unsigned long long part_slot_wave(const unsigned long long *off, unsigned long long k,
+                                                             const OutGeom &g, int which) {
+  constexpr int kStep = (kParts + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int q1 = lane * kStep;
+  const bool le1 = q1 < kParts && off[q1 < kParts ? q1 : 0] <= k;
+  const int base = (63 - __clzll((long long)__ballot(le1))) * kStep;  // off[0] = 0 <= k: lane 0 always
+  const int q2 = base + lane;
+  const bool le2 = lane < kStep && q2 < kParts && off[q2 < kParts ? q2 : 0] <= k;
+  const int q = base + (63 - __clzll((long long)__ballot(le2)));
+  return g.slot(which, q, k - off[q]);
+}
+
 // Inclusive prefix sum over the 64 lanes of a wave with DPP row shifts and row broadcasts
 // (no LDS round trips).  Every lane must be active.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {

@@ -563,14 +563,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   int32_t *cover = cover_buf[threadIdx.x >> 6];
   for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
     const int64_t it = amb_in ? amb_in[li].item : li;
-    const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
     const int32_t pos = item.pos;
     int ncov = 0;
     bool compact = true;
-    for (int64_t r0 = tl.rb; r0 < tl.re; r0 += 64) {
+    // the covering reads lie in [first pmax_end > pos, first start > pos)
+    const int64_t ra = wave_first_true(tl.rb, tl.re, [&](int64_t r) { return R.pmax_end[r] > pos; });
+    const int64_t rz = wave_first_true(ra, tl.re, [&](int64_t r) { return R.start[r] > pos; });
+    for (int64_t r0 = ra; r0 < rz; r0 += 64) {
       const int64_t r = r0 + lane;
-      const bool c = r < tl.re && R.start[r] <= pos && pos < R.end[r];
+      const bool c = r < rz && R.start[r] <= pos && pos < R.end[r];
       const unsigned long long b = __ballot(c);
       const int at = ncov + (int)__popcll(b & ((1ull << lane) - 1ull));
       if (c && at < kCover) cover[at] = (int32_t)(r - tl.rb);

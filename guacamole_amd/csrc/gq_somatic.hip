@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -330,7 +331,7 @@ __device__ __forceinline__ bool phred_rounding_edge(double p) {
 // Element quality (PileupElement.qualityScore, PileupElement.scala:166-171; quality bytes are
 // signed JVM bytes): SNV / Deletion = the base quality at the element's read position,
 // Insertion = min over its bases, MidDeletion / Clipped = the read's mapping quality.
-__device__ int elem_quality(const DevReads &R, const AlleleDesc &d) {
+__device__ __forceinline__ int elem_quality(const DevReads &R, const AlleleDesc &d) {
   const int64_t r = d.read;
   const uint8_t *q = R.qual + R.seq_off[r];
   switch (d.kind) {
@@ -345,14 +346,14 @@ __device__ int elem_quality(const DevReads &R, const AlleleDesc &d) {
   }
 }
 
-__device__ bool allele_is_variant(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Allele.isVariant
+__device__ __forceinline__ bool allele_is_variant(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Allele.isVariant
   const int rl = allele_ref_len(a), al = allele_alt_len(a);
   if (rl != al) return true;
   for (int i = 0; i < rl; ++i)
     if (allele_byte(R, a, pos, 0, i) != allele_byte(R, a, pos, 1, i)) return true;
   return false;
 }
-__device__ bool allele_std_alt(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Likelihood.scala:106
+__device__ __forceinline__ bool allele_std_alt(const DevReads &R, const AlleleDesc &a, int32_t pos) {  // Likelihood.scala:106
   const int al = allele_alt_len(a);
   for (int i = 0; i < al; ++i)
     if (!std_bit(allele_byte(R, a, pos, 1, i))) return false;
@@ -498,14 +499,17 @@ struct Cover {
     return r;
   }
 };
-__device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst, uint32_t *tmp,
+__device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst, uint32_t *tmp,
                             const WinInit &w, const int64_t *__restrict__ init_reads,
                             const int32_t *__restrict__ init_rank, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   int64_t n = 0;
-  for (int64_t r0 = rb; r0 < re; r0 += 64) {
+  // the covering reads lie in [first pmax_end > pos, first start > pos)
+  const int64_t ra = wave_first_true(rb, re, [&](int64_t r) { return R.pmax_end[r] > pos; });
+  const int64_t rz = wave_first_true(ra, re, [&](int64_t r) { return R.start[r] > pos; });
+  for (int64_t r0 = ra; r0 < rz; r0 += 64) {
     const int64_t r = r0 + lane;
-    const bool c = r < re && R.start[r] <= pos && pos < R.end[r];
+    const bool c = r < rz && R.start[r] <= pos && pos < R.end[r];
     const unsigned long long b = __ballot(c);
     const int64_t at = n + (int64_t)__popcll(b & ((1ull << lane) - 1ull));
     if (c && at < kCover) lst[at] = (int32_t)(r - rb);
@@ -563,7 +567,7 @@ __device__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t p
 // (ambiguous = more than one); the base itself when they agree.  Where they disagree the
 // reference takes the first in heap order: the first pass lists the locus and the second
 // receives the base from heap_ref_bases (ref_override >= 0).
-__device__ void pileup_ref(const DevReads &R, const Cover &cv, int32_t pos, Counters *ctr, int ref_override,
+__device__ __forceinline__ void pileup_ref(const DevReads &R, const Cover &cv, int32_t pos, Counters *ctr, int ref_override,
                            uint8_t &refbase, bool &ambiguous) {
   const int lane = threadIdx.x & 63;
   uint32_t mask = 0;
@@ -598,7 +602,7 @@ struct SamplePile {
 };
 
 // Build the allele table of one sample's pileup at pos (counts only: order-free).
-__device__ void gather_sample(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, int ref_override,
+__device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, int ref_override,
                               Counters *ctr, SamplePile &P) {
   const int lane = threadIdx.x & 63;
   pileup_ref(R, cv, pos, ctr, ref_override, P.refbase, P.ambiguous);
@@ -682,7 +686,7 @@ __device__ void gather_sample(const DevReads &R, const Cover &cv, int32_t pos, i
   }
 }
 
-__device__ AlleleDesc pile_desc(const SamplePile &P, int j) {
+__device__ __forceinline__ AlleleDesc pile_desc(const SamplePile &P, int j) {
   AlleleDesc d{};
 #pragma unroll
   for (int s = 0; s < kSlots; ++s)
@@ -711,7 +715,7 @@ struct GenoResult {
   int bi, bj;     // table entries of the best genotype's alleles
 };
 
-__device__ void genotype_index(int g, int n, int &i, int &j) {  // g -> (i, j), i <= j, row-major
+__device__ __forceinline__ void genotype_index(int g, int n, int &i, int &j) {  // g -> (i, j), i <= j, row-major
   int row = 0, rem = g;
   while (rem >= n - row) {
     rem -= n - row;
@@ -732,7 +736,7 @@ constexpr int kMaxG = 128;  // genotypes held per sample for the normalisation (
 // bits.  Lanes = elements compute the three possible terms log(pc + pc), log(pc + (1 - pc)),
 // log((1 - pc) + (1 - pc)); then the wave walks the elements backwards, each lane (genotype)
 // adding the term its alleles select.
-__device__ double fold_genotypes(const DevReads &R, const Cover &cv, int32_t pos, uint8_t refbase, int min_mapq,
+__device__ __forceinline__ double fold_genotypes(const DevReads &R, const Cover &cv, int32_t pos, uint8_t refbase, int min_mapq,
                                  bool include_alignment, Key128 k1, Key128 k2, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   double agg = 0.0;
@@ -778,7 +782,7 @@ __device__ double fold_genotypes(const DevReads &R, const Cover &cv, int32_t pos
   return agg;
 }
 
-__device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Cover &cv, int32_t pos,
+__device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Cover &cv, int32_t pos,
                                 int min_mapq, bool include_alignment, int16_t *order, uint8_t *is_var,
                                 double *ll_lds, Counters *ctr) {
   const int lane = threadIdx.x & 63;
@@ -883,7 +887,7 @@ __device__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Co
 // AlleleEvidence.apply (AlleleEvidence.scala:58-101) for the elements of one sample whose
 // allele key is `target`.  Supporting elements' (mapq, quality, mismatches) go to `ev_lds`
 // in element order for the running mean (Breeze, in element order) and the medians.
-__device__ void allele_evidence(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, const SamplePile &P,
+__device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, const SamplePile &P,
                                 Key128 target, double likelihood, uint32_t *ev_lds, Counters *ctr, gq_evidence &ev) {
   const int lane = threadIdx.x & 63;
   uint32_t n = 0, fwd = 0;
@@ -978,8 +982,10 @@ struct SomWin {
   const int32_t *init_rank;
 };
 
-// three waves per SIMD (<= 168 VGPRs)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void somatic_call(const Tile *__restrict__ tiles_t,
+#ifndef GQ_CALL_WPE
+#define GQ_CALL_WPE 3  // waves per SIMD the register budget must allow
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_WPE))) void somatic_call(const Tile *__restrict__ tiles_t,
                                                        const Tile *__restrict__ tiles_n,
                                                        const ComplexItem *__restrict__ items, DevReads RT,
                                                        DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
@@ -988,7 +994,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
                                                        Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out,
                                                        unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
                                                        const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
-                                                       RefView ref) {
+                                                       RefView ref, int dbg) {
   // amb_in == nullptr: every candidate; where a sample's reads' MD-derived bases disagree the
   // locus is only listed (amb_out) for the heap-order replay.  amb_in != nullptr: the listed
   // loci, with both samples' reference bases resolved in heap order (amb_ref[2 i + set]).
@@ -1003,9 +1009,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // candidates: the partitioned items of somatic_proj / somatic_tile (part_scan: kept counts)
   const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
+  // dbg & 16: phase clocks per candidate (covers, pileups, tumor genotypes, normal genotypes,
+  // evidence + record, candidates) into ctr->prof
+  uint64_t clk[6] = {0, 0, 0, 0, 0, 0}, tk = 0;
+  auto tick = [&](int k) {
+    if (dbg & 16) {
+      const uint64_t t = __builtin_readcyclecounter();
+      if (k >= 0) clk[k] += t - tk;
+      tk = t;
+    }
+  };
   for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    tick(-1);
+    if (dbg & 16) clk[5] += 1;
     const int64_t it = amb_in ? amb_in[li].item : li;
-    const ComplexItem item = items[part_slot(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
     const int32_t pos = item.pos;
     const int32_t win = sw.range_win[tt.range];
@@ -1013,11 +1031,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
                                 sw.init_rank, ctr);
     const Cover cn = make_cover(RN, tn.rb, tn.re, pos, cover_n[wv], ev_lds[wv], sw.wi[2 * win + 1], sw.init_reads,
                                 sw.init_rank, ctr);
+    tick(0);
     SamplePile PT, PN;
     const int fb = ref.b ? (int)ref.b[ref.off[tt.contig] + pos] : -1;
     gather_sample(RT, ct, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li] : fb, ctr, PT);
     gather_sample(RN, cn, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li + 1] : fb, ctr, PN);
     if (fb >= 0) PT.ambiguous = PN.ambiguous = false;
+    tick(1);
     if (PT.overflow || PN.overflow) {
       raise_at(ctr, GQ_E_CAPACITY, pos);
       continue;
@@ -1050,11 +1070,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       if (ref_match == PT.depth_f) continue;
     }
     const GenoResult tg = genotypes(RT, PT, ct, pos, prm.min_mapq, true, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
+    tick(2);
     if (tg.G == 0) continue;
     const bool t_var = var_lds[wv][tg.bi] || var_lds[wv][tg.bj];
     if (!t_var) continue;
     const AlleleDesc a1 = pile_desc(PT, tg.bi), a2 = pile_desc(PT, tg.bj);
     const GenoResult ng = genotypes(RN, PN, cn, pos, prm.min_mapq, false, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
+    tick(3);
     const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
     const double odds = tg.best_l / nvs;
     if (!(odds * 100.0 >= (double)prm.odds)) continue;
@@ -1132,7 +1154,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
       const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
       if (k < rec_cap) recs[k] = rr;
     }
+    tick(4);
   }
+  if ((dbg & 16) && lane == 0 && clk[5])
+    for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
 }
 
 // Exclusive offsets of the candidate partitions (clamped to their capacities), the total in
@@ -1376,6 +1401,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   if (t->d.n_contigs != n->d.n_contigs)
     return set_err(GQ_E_ARG, "tumor and normal read sets must share the contig list (%d vs %d contigs)",
                    t->d.n_contigs, n->d.n_contigs);
+  static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   RefView rv{nullptr, nullptr};
   std::vector<int32_t> lc;
   std::vector<int64_t> ls, le, lt;
@@ -1577,7 +1603,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                        (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                        (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
-                       rv);
+                       rv, dbg);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -1604,7 +1630,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
                          (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                          (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
-                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), RefView{nullptr, nullptr});
+                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), RefView{nullptr, nullptr}, dbg);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
       HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -1625,6 +1651,11 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     }
   }
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
+  if ((dbg & 16) && hc.prof[5])
+    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): covers %.0f pileups %.0f tumor-genotypes %.0f "
+            "normal-genotypes %.0f evidence %.0f (%llu candidates reached)\n", (double)hc.prof[0] / hc.prof[5],
+            (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5], (double)hc.prof[3] / hc.prof[5],
+            (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
   st = check_device_error(c, hc);
   if (st) {
     free(res);
