@@ -310,6 +310,74 @@ def variant_support_main(argv: Sequence[str]) -> int:
     return 0
 
 
+def vaf_histogram_reads(ctx: native.Context, rs: ReadSet, loci, bins: int = 20, min_read_depth: int = 0,
+                        min_vaf: int = 0) -> Dict[str, object]:
+    """VAFHistogram.variantLociFromReads + generateVAFHistogram (commands/VAFHistogram.scala:
+    188-229) on the GPU: {bin start: loci}, variant and visited locus counts."""
+    return ctx.vaf_histogram(device_reads(ctx, rs), loci, bins, min_read_depth, min_vaf)
+
+
+def vaf_histogram_main(argv: Sequence[str]) -> int:
+    """VAFHistogram.Caller.run (commands/VAFHistogram.scala:89-184).  The Gaussian mixture fit
+    (--cluster, Spark MLlib) is outside the pileup path and refused."""
+    import os
+    p = argparse.ArgumentParser(prog="vaf-histogram", description="Compute and cluster the variant allele frequencies")
+    p.add_argument("bams", nargs="+", help="BAMs")
+    p.add_argument("--loci", default="", help="Loci at which to compute VAFs")
+    p.add_argument("--loci-from-file", default="", help="Path to file giving loci")
+    p.add_argument("--out", default="", help="Path to save the histogram (saveAsTextFile layout)")
+    p.add_argument("--local-out", default="", help="Local file path to save the histogram")
+    p.add_argument("--bins", type=int, default=20, help="Number of bins (Default: 20)")
+    p.add_argument("--cluster", action="store_true", help="(Gaussian mixture model: not supported)")
+    p.add_argument("--num-clusters", type=int, default=3)
+    p.add_argument("--min-read-depth", type=int, default=0, help="Minimum read depth to include variant allele frequency")
+    p.add_argument("--min-vaf", type=int, default=0, help="Minimum variant allele frequency to include")
+    p.add_argument("--print-stats", action="store_true", help="(accepted; statistics are not printed)")
+    p.add_argument("--sample-percent", type=int, default=25)
+    p.add_argument("--parallelism", type=int, default=0, help="Num variant calling tasks (loci partitions)")
+    p.add_argument("--partition-accuracy", type=int, default=250)
+    p.add_argument("--bam-reader-api", default="best", help="(accepted; the native reader is always used)")
+    p.add_argument("--recompute-md-tags", action="store_true")
+    p.add_argument("--device", type=int, default=0, help="GPU index")
+    args = p.parse_args(argv)
+    if args.out and args.local_out:
+        raise ValueError("--out and --local-out are exclusive")
+    if args.cluster:
+        raise ValueError("--cluster (Gaussian mixture model over Spark MLlib) is not supported")
+    builder = _loci_builder(args)
+    # ReadSet(..., InputFilters.empty, contigLengthsFromDictionary = true) (:98-109)
+    read_sets = [load_reads(b, InputFilters(), recompute_md=args.recompute_md_tags) for b in args.bams]
+    rs0 = read_sets[0]
+    loci = builder.result(rs0.contig_lengths_map)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, rs0)
+    ctx = native.Context(args.device)
+    bin_size = 100 // args.bins if 1 <= args.bins <= 100 else 1
+    lines, plain = [], []
+    for path, rs in zip(args.bams, read_sets):
+        flat = flatten_partitions(parts, {c: rs.contig_index().get(c, -1) for c in loci.contigs})
+        keep = flat[0] >= 0
+        flat = tuple(a[keep] for a in flat)
+        h = vaf_histogram_reads(ctx, rs, flat, args.bins, args.min_read_depth, args.min_vaf)["histogram"]
+        sample = rs.sample_names[int(rs.sample[0])] if rs.n else "default"
+        for b in sorted(h):
+            row = "%d, %d, %d" % (b, min(b + bin_size, 100), h[b])
+            lines.append("%s, %s, %s" % (path, sample, row))
+            plain.append(row)
+    if args.local_out:
+        with open(args.local_out, "w") as fh:
+            fh.write("Filename, SampleName, BinStart, BinEnd, Size\n")
+            fh.writelines(l + "\n" for l in lines)
+    elif args.out:
+        os.makedirs(args.out, exist_ok=False)
+        with open(os.path.join(args.out, "part-00000"), "w") as fh:
+            fh.writelines(l + "\n" for l in lines)
+        open(os.path.join(args.out, "_SUCCESS"), "w").close()
+    else:
+        for row in plain:
+            print(row)
+    return 0
+
+
 def _finish_rank(rc: int) -> int:
     """Leave the process group (multi-GPU runs) after every rank has finished."""
     import os
@@ -322,7 +390,7 @@ def _finish_rank(rc: int) -> int:
 
 
 COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main,
-            "variant-support": variant_support_main}
+            "variant-support": variant_support_main, "vaf-histogram": vaf_histogram_main}
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

@@ -959,6 +959,74 @@ __global__ __launch_bounds__(kBlock) void counts_tile(const Tile *__restrict__ t
   }
 }
 
+// vaf_tile: VAFHistogram's per-locus variant allele frequency (VariantLocus.apply,
+// commands/VAFHistogram.scala:31-37) binned on the device (generateVAFHistogram, :188-196).
+// Loci whose reference base depends on heap order are listed with their counts (the host
+// bins them after the replay).  hist: 64 spread copies of the 101 bins.
+struct VafAmb {
+  int32_t depth, base[6];  // depth, Match/Mismatch elements by base (A C G T N other)
+};
+template <int T>
+__global__ __launch_bounds__(kBlock) void vaf_tile(const Tile *__restrict__ tiles, DevReads R, int bins,
+                                                   int min_depth, int min_vaf, unsigned long long *__restrict__ hist,
+                                                   AmbItem *__restrict__ amb, VafAmb *__restrict__ amb_cnt,
+                                                   unsigned long long amb_cap, Counters *ctr) {
+  __shared__ uint32_t cnt[K2_NCAT * T];
+  __shared__ uint32_t h[101];
+  const Tile tl = tiles[blockIdx.x];
+  const int32_t L0 = tl.L0, L1 = tl.L1;
+  for (int i = threadIdx.x; i < K2_NCAT * T; i += blockDim.x) cnt[i] = 0u;
+  for (int i = threadIdx.x; i < 101; i += blockDim.x) h[i] = 0u;
+  __syncthreads();
+  CountSink<T> sink{cnt, L0, &ctr->err, &ctr->err_pos};
+  for (int64_t r = tl.rb + threadIdx.x; r < tl.re; r += blockDim.x) walk_read_lane(R, r, L0, L1, sink);
+  __syncthreads();
+  const int bin_size = 100 / bins;
+  unsigned visited = 0, variant = 0;
+  for (int i = threadIdx.x; i < L1 - L0; i += blockDim.x) {
+    uint32_t dsum = 0;
+    for (int k = 0; k <= K2_CLIP; ++k) dsum += cnt[k * T + i];
+    if (dsum == 0) continue;  // skipEmpty
+    ++visited;
+    uint32_t mask = cnt[K2_MASK * T + i];
+    for (int k = 0; k < 4; ++k)
+      if (cnt[k * T + i] > cnt[(K2_EVA + k) * T + i]) mask |= 1u << k;
+    if (__popc(mask) > 1) {  // the reference base comes from heap order: the host bins it
+      const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+      if (k < amb_cap) {
+        amb[k] = AmbItem{(int32_t)blockIdx.x, L0 + i, (int64_t)k};
+        VafAmb v;
+        v.depth = (int32_t)dsum;
+        const int out_order[6] = {K2_A, K2_C, K2_G, K2_T, K2_N, K2_O};
+        for (int q = 0; q < 6; ++q) v.base[q] = (int32_t)cnt[out_order[q] * T + i];
+        amb_cnt[k] = v;
+      }
+      continue;
+    }
+    const uint8_t rb = mask ? bit_base(mask) : (uint8_t)'N';
+    const uint32_t ref = cnt[base_cat(rb) * T + i];
+    if (ref == dsum) continue;  // no VariantLocus
+    // (depth - referenceDepth).toFloat / depth; depth >= minReadDepth; vaf >= minVAF / 100.0
+    const float vaf = (float)(int32_t)(dsum - ref) / (float)(int32_t)dsum;
+    if (!((int32_t)dsum >= min_depth) || !((double)vaf >= (double)min_vaf / 100.0)) continue;
+    ++variant;
+    const int pct = (int)(vaf * 100.0f);
+    atomicAdd(&h[pct - pct % bin_size], 1u);
+  }
+  __syncthreads();
+  unsigned long long *hh = hist + (size_t)(blockIdx.x & 63) * 101;
+  for (int i = threadIdx.x; i < 101; i += blockDim.x)
+    if (h[i]) atomicAdd(&hh[i], (unsigned long long)h[i]);
+  for (int d = 32; d >= 1; d >>= 1) {
+    visited += __shfl_xor(visited, d, 64);
+    variant += __shfl_xor(variant, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (visited) atomicAdd(&ctr->spread[0][blockIdx.x & (kSpread - 1)], (unsigned long long)visited);
+    if (variant) atomicAdd(&ctr->spread[1][blockIdx.x & (kSpread - 1)], (unsigned long long)variant);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Result image: the gq_calls arrays built on device in output order (one D2H copy)
 // ------------------------------------------------------------------------------------------
@@ -2032,6 +2100,75 @@ gq_status gq_pileup_counts(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loc
     }
   }
   *out = res;
+  return GQ_OK;
+}
+
+gq_status gq_vaf_histogram(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, const gq_vaf_params *p,
+                           gq_vaf_hist *out) {
+  if (!c || !rd || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_vaf_histogram: null argument");
+  if (p->bins < 1 || p->bins > 100) return set_err(GQ_E_ASSERT, "assumption failed: Bins should be between 1 and 100");
+  HIP_TRY(hipSetDevice(c->device));
+  memset(out, 0, sizeof(*out));
+  Plan pl;
+  gq_status st = plan(c, rd, loci, kCountT, pl, c->tiles);
+  if (st) return st;
+  if (pl.n_tiles == 0) return GQ_OK;
+  unsigned long long amb_cap = 4096;
+  Counters hc{};
+  for (int attempt = 0;; ++attempt) {
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    HIP_TRY(c->c_depth.ensure(sizeof(unsigned long long) * 64 * 101));
+    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
+    HIP_TRY(c->c_base.ensure(amb_cap * sizeof(VafAmb)));
+    Counters *ctr = (Counters *)c->counters.p;
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+    HIP_TRY(hipMemsetAsync(c->c_depth.p, 0, sizeof(unsigned long long) * 64 * 101, c->stream));
+    hipLaunchKernelGGL((vaf_tile<kCountT>), dim3((unsigned)pl.n_tiles), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, rd->d, (int)p->bins, (int)p->min_read_depth, (int)p->min_vaf,
+                       (unsigned long long *)c->c_depth.p, (AmbItem *)c->amb.p, (VafAmb *)c->c_base.p, amb_cap, ctr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (hc.n_amb <= amb_cap || hc.err) break;
+    if (attempt == 2) return set_err(GQ_E_CAPACITY, "vaf-histogram: listed-locus capacity retries exhausted");
+    amb_cap = hc.n_amb + 1024;
+  }
+  st = check_device_error(c, hc);
+  if (st) return st;
+  std::vector<unsigned long long> h(64 * 101);
+  HIP_TRY(hipMemcpy(h.data(), c->c_depth.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 64; ++k)
+    for (int b = 0; b < 101; ++b) out->counts[b] += (int64_t)h[(size_t)k * 101 + (size_t)b];
+  for (int k = 0; k < kSpread; ++k) {
+    out->visited_loci += (int64_t)hc.spread[0][k];
+    out->variant_loci += (int64_t)hc.spread[1][k];
+  }
+  if (hc.n_amb > 0) {  // heap-order reference bases (gq_replay.h), binned here as on the device
+    std::vector<AmbItem> amb((size_t)hc.n_amb);
+    std::vector<VafAmb> cnt((size_t)hc.n_amb);
+    HIP_TRY(hipMemcpy(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cnt.data(), c->c_base.p, cnt.size() * sizeof(VafAmb), hipMemcpyDeviceToHost));
+    HIP_TRY(c->amb_ref.ensure(amb.size()));
+    st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
+    if (st) return st;
+    std::vector<uint8_t> rb(amb.size());
+    HIP_TRY(hipMemcpy(rb.data(), c->amb_ref.p, rb.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&hc, c->counters.p, sizeof(Counters), hipMemcpyDeviceToHost));
+    st = check_device_error(c, hc);
+    if (st) return st;
+    const int bin_size = 100 / p->bins;
+    for (size_t k = 0; k < amb.size(); ++k) {
+      const uint8_t b = rb[k];
+      const int cat = b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : b == 'N' ? 4 : 5;
+      const int32_t depth = cnt[k].depth, ref = cnt[k].base[cat];
+      if (ref == depth) continue;
+      const float vaf = (float)(depth - ref) / (float)depth;
+      if (!(depth >= p->min_read_depth) || !((double)vaf >= (double)p->min_vaf / 100.0)) continue;
+      const int pct = (int)(vaf * 100.0f);
+      out->counts[pct - pct % bin_size] += 1;
+      out->variant_loci += 1;
+    }
+  }
   return GQ_OK;
 }
 

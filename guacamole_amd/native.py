@@ -66,6 +66,14 @@ class gq_allele_counts(C.Structure):
                 ("allele_pool", C.c_void_p), ("pool_len", C.c_int64), ("flags", C.POINTER(C.c_uint8))]
 
 
+class gq_vaf_params(C.Structure):
+    _fields_ = [("bins", C.c_int32), ("min_read_depth", C.c_int32), ("min_vaf", C.c_int32)]
+
+
+class gq_vaf_hist(C.Structure):
+    _fields_ = [("counts", C.c_int64 * 101), ("variant_loci", C.c_int64), ("visited_loci", C.c_int64)]
+
+
 class gq_counts(C.Structure):
     _fields_ = [("n_loci", C.c_int64), ("depth", C.POINTER(C.c_int32)), ("pos_depth", C.POINTER(C.c_int32)),
                 ("base_counts", C.POINTER(C.c_int32)), ("indel_counts", C.POINTER(C.c_int32)),
@@ -129,7 +137,8 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
             "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
-            "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts")
+            "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts",
+            "gq_vaf_histogram")
 
 
 def lib():
@@ -145,7 +154,7 @@ def lib():
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
                   "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard",
-                  "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support"):
+                  "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support", "gq_vaf_histogram"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
                                             C.POINTER(C.POINTER(gq_calls))]
@@ -162,6 +171,8 @@ def lib():
         L.gq_variant_support.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
                                          C.POINTER(C.POINTER(gq_allele_counts))]
         L.gq_free_allele_counts.argtypes = [C.POINTER(gq_allele_counts)]
+        L.gq_vaf_histogram.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_vaf_params),
+                                       C.POINTER(gq_vaf_hist)]
         L.gq_free_calls.argtypes = [C.POINTER(gq_calls)]
         L.gq_free_counts.argtypes = [C.POINTER(gq_counts)]
         L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
@@ -318,6 +329,16 @@ class Context:
                      pool[ao[i]:ao[i] + al[i]].decode("latin-1"), int(cnt[i]), int(fl[i])) for i in range(n)]
         finally:
             lib().gq_free_allele_counts(out)
+
+    def vaf_histogram(self, reads: "DeviceReads", loci, bins: int = 20, min_read_depth: int = 0,
+                      min_vaf: int = 0) -> Dict[str, object]:
+        """gq_vaf_histogram: {bin start: loci} (non-empty bins), plus variant / visited locus counts."""
+        L, keep = make_gq_loci(*loci)
+        prm = gq_vaf_params(int(bins), int(min_read_depth), int(min_vaf))
+        h = gq_vaf_hist()
+        _check(lib().gq_vaf_histogram(self.h, reads.h, C.byref(L), C.byref(prm), C.byref(h)))
+        return dict(histogram={b: int(h.counts[b]) for b in range(101) if h.counts[b]},
+                    variant_loci=int(h.variant_loci), visited_loci=int(h.visited_loci))
 
     def pileup_counts(self, reads: "DeviceReads", loci) -> Dict[str, np.ndarray]:
         L, keep = make_gq_loci(*loci)

@@ -278,6 +278,25 @@ typedef struct {
 gq_status gq_variant_support(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci, gq_allele_counts **out);
 void gq_free_allele_counts(gq_allele_counts *c);
 
+/* vaf-histogram: VAFHistogram.variantLociFromReads + generateVAFHistogram
+ * (commands/VAFHistogram.scala:208-229, 188-196): at every visited locus whose pileup holds a
+ * non-Match element (VariantLocus.apply, :31-37), VAF = (depth - referenceDepth).toFloat /
+ * depth; kept when depth >= min_read_depth and VAF >= min_vaf / 100.0; binned as
+ * pct - pct % (100 / bins) with pct = (int)(VAF * 100).  counts[b] = loci in the bin starting
+ * at b.  GQ_E_ASSERT unless 1 <= bins <= 100 (the reference's assume).                      */
+typedef struct {
+  int32_t bins;            /* --bins (20)          */
+  int32_t min_read_depth;  /* --min-read-depth (0) */
+  int32_t min_vaf;         /* --min-vaf (0)        */
+} gq_vaf_params;
+typedef struct {
+  int64_t counts[101];
+  int64_t variant_loci;  /* loci binned          */
+  int64_t visited_loci;  /* non-empty pileups    */
+} gq_vaf_hist;
+gq_status gq_vaf_histogram(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci, const gq_vaf_params *params,
+                           gq_vaf_hist *out);
+
 /* --reference-fasta (SomaticStandardCaller.scala:57, :75).  A reference genome resident in HBM
  * (replaces ReferenceBroadcast.apply, reference/ReferenceBroadcast.scala:39-55): bases[k] /
  * lengths[k] are the unmasked bases of contig k of the read sets' contig list (bases[k] == NULL

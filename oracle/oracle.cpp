@@ -1234,6 +1234,40 @@ int or_variant_support(const or_reads *reads, const or_loci *loci, char **o, int
   });
 }
 
+// VAFHistogram (commands/VAFHistogram.scala:31-37, 188-229): per non-empty pileup with a
+// non-Match element, VAF = (depth - referenceDepth).toFloat / depth (referenceDepth = Match
+// elements, Pileup.scala:86-91), kept for depth >= minReadDepth and VAF >= minVAF / 100.0,
+// binned as pct - pct % (100 / bins), pct = (VAF * 100).toInt.  Lines: bin \t loci, then
+// "variant \t N".
+int or_vaf_histogram(const or_reads *reads, const or_loci *loci, int32_t bins, int32_t min_read_depth,
+                     int32_t min_vaf, char **o, int64_t *olen) {
+  std::string out;
+  return guard(out, o, olen, [&]() {
+    if (!(bins <= 100 && bins >= 1)) fail(E_ASSERT, "assumption failed: Bins should be between 1 and 100");
+    ReadSet rs;
+    buildReads(reads, rs);
+    std::vector<ReadSet *> sets{&rs};
+    std::map<int, int64_t> hist;
+    int64_t variant = 0;
+    const int bin_size = 100 / bins;
+    forEachPileup(sets, loci, [&](const TaskContig &, std::vector<Pileup> &ps, std::vector<bool> &) {
+      const Pileup &p = ps[0];
+      const int depth = p.depth();
+      int ref = 0;
+      for (const Elem &e : p.elements)
+        if (e.evaluate().kind == K_MATCH) ++ref;
+      if (ref == depth) return;
+      const float vaf = (float)(depth - ref) / (float)depth;
+      if (!(depth >= min_read_depth) || !((double)vaf >= (double)min_vaf / 100.0)) return;
+      const int pct = (int)(vaf * 100.0f);
+      ++hist[pct - pct % bin_size];
+      ++variant;
+    });
+    for (const auto &kv : hist) appendf(out, "%d\t%lld\n", kv.first, (long long)kv.second);
+    appendf(out, "variant\t%lld\n", (long long)variant);
+  });
+}
+
 int or_elements_at(const or_reads *reads, int32_t contig, int64_t locus, int32_t own_ref, char **o, int64_t *olen) {
   std::string out;
   return guard(out, o, olen, [&]() {

@@ -108,6 +108,11 @@ int or_somatic_standard_ref(const or_reads *tumor, const or_reads *normal, const
  * depends on heap order; within a locus rows by (ref, alt).                            */
 int or_variant_support(const or_reads *reads, const or_loci *loci, char **out, int64_t *out_len);
 
+/* vaf-histogram (VAFHistogram.scala:31-37, 188-229).  Lines: bin \t loci; then
+ * "variant \t N".                                                            */
+int or_vaf_histogram(const or_reads *reads, const or_loci *loci, int32_t bins, int32_t min_read_depth,
+                     int32_t min_vaf, char **out, int64_t *out_len);
+
 /* ---- single-locus entry points used to pin the oracle with the reference's unit
  * KATs.  They build the pileup with Pileup.apply(reads, contig, locus)
  * (Pileup.scala:181-186): reads in input order, reference base from

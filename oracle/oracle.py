@@ -184,6 +184,22 @@ def variant_support(rs, loci):
     return out
 
 
+def vaf_histogram(rs, loci, bins: int = 20, min_read_depth: int = 0, min_vaf: int = 0):
+    """({bin start: loci}, variant loci) — see oracle.h."""
+    m = _Marshalled(rs)
+    L = _Loci(rs.contig_names, *loci)
+    text = _call(lib().or_vaf_histogram, C.byref(m.s), C.byref(L.s), C.c_int32(bins), C.c_int32(min_read_depth),
+                 C.c_int32(min_vaf))
+    hist, variant = {}, 0
+    for line in text.splitlines():
+        a, b = line.split("\t")
+        if a == "variant":
+            variant = int(b)
+        else:
+            hist[int(a)] = int(b)
+    return hist, variant
+
+
 # ---- single-locus entry points (Pileup.apply semantics), used by the KAT tests
 def _contig_id(rs, contig: str) -> int:
     return rs.contig_names.index(contig)
