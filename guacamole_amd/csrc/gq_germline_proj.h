@@ -36,6 +36,9 @@
 #ifndef GQ_PROJ_WPE
 #define GQ_PROJ_WPE 5  // waves per SIMD the register budget must allow
 #endif
+#ifndef GQ_PROJ_NBUF
+#define GQ_PROJ_NBUF 3  // load batches in registers: NBUF - 1 in flight while one is counted
+#endif
 #ifndef GQ_PROJ_WAVES
 #define GQ_PROJ_WAVES 4
 #endif
@@ -221,8 +224,14 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       nn += U;
     };
     uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U];
+#if GQ_PROJ_NBUF == 4
+    uint32_t d0[U], d1[U];
+#endif
     issue(0, a0, a1);
     issue(U, b0, b1);
+#if GQ_PROJ_NBUF == 4
+    issue(2 * U, c0, c1);
+#endif
     // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
     auto apply = [&](uint2 p) {
       const int32_t l = (int32_t)p.x;
@@ -249,6 +258,19 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         if (k < e1) apply(pev[k]);
       }
     const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+#if GQ_PROJ_NBUF == 4
+    for (int k0 = 0;; k0 += 4 * U) {  // rows past the group's are clamped (zero words)
+      issue(k0 + 3 * U, d0, d1);
+      count(a0, a1);
+      issue(k0 + 4 * U, a0, a1);
+      count(b0, b1);
+      issue(k0 + 5 * U, b0, b1);
+      count(c0, c1);
+      issue(k0 + 6 * U, c0, c1);
+      count(d0, d1);
+      if (k0 + 4 * U >= nmax) break;
+    }
+#else
     for (int k0 = 0;; k0 += 3 * U) {  // rows past the group's are clamped (zero words)
       issue(k0 + 2 * U, c0, c1);
       count(a0, a1);
@@ -258,6 +280,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       count(c0, c1);
       if (k0 + 3 * U >= nmax) break;
     }
+#endif
     fold();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

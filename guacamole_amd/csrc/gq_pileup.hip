@@ -545,7 +545,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                            Counters *ctr, AmbItem *__restrict__ amb_out,
                                                            unsigned long long amb_cap,
                                                            const AmbItem *__restrict__ amb_in,
-                                                           const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+                                                           const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
+                                                           int dbg) {
   // amb_in == nullptr: every queued item; a locus whose reads' MD-derived bases disagree
   // (Pileup.referenceBaseAtLocus then depends on the queue's heap order) is only listed in
   // amb_out.  amb_in != nullptr: the listed loci again, with their reference base resolved
@@ -561,7 +562,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   constexpr int kCover = 256;
   __shared__ int32_t cover_buf[kBlock / 64][kCover];
   int32_t *cover = cover_buf[threadIdx.x >> 6];
+  // dbg & 32: phase clocks per item (cover, reference base, elements, decision + records, items)
+  uint64_t clk[5] = {0, 0, 0, 0, 0}, tk = 0;
+  auto tick = [&](int k) {
+    if (dbg & 32) {
+      const uint64_t t = __builtin_readcyclecounter();
+      if (k >= 0) clk[k] += t - tk;
+      tk = t;
+    }
+  };
   for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    tick(-1);
+    if (dbg & 32) clk[4] += 1;
     const int64_t it = amb_in ? amb_in[li].item : li;
     const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
@@ -596,6 +608,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       *act = R.start[r] <= pos && pos < R.end[r];
       return r;
     };
+    tick(0);
     // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
     uint32_t mask = 0;  // standard MD-derived bases present
     for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
@@ -630,6 +643,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     } else if (mask) {
       refbase = bit_base(mask);
     }
+    tick(1);
     // ---- pass 2: classify elements, group alleles per (sample, allele) in registers
     uint64_t tlo[kSlots], thi[kSlots];
     uint32_t tcnt[kSlots];
@@ -725,6 +739,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (ambiguous) atomicAdd(&ctr->ambiguous, 1ull);
       }
     }
+    tick(2);
     // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
     const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
     for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
@@ -869,7 +884,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
       }
     }
+    tick(3);
   }
+  if ((dbg & 32) && (threadIdx.x & 63) == 0 && clk[4])
+    for (int k = 0; k < 5; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1598,6 +1616,11 @@ void gq_reads_free(gq_dev_reads *d) {
 }  // extern "C"
 
 // ---- shared planning: validate loci, upload ranges, plan tiles -----------------------------
+static int gq_dbg() {  // GQ_DBG: diagnostics only (phase clocks, ablations)
+  static const int d = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;
+  return d;
+}
+
 gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles_buf,
                    int stage_cap, int meta_cap, int ev_cap, bool aligned) {
   if (!loci || loci->n_ranges < 0) return set_err(GQ_E_ARG, "bad loci");
@@ -1776,7 +1799,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
                        (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap,
-                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
+                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg());
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
@@ -1823,7 +1846,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
                          (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
                          (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
                          (unsigned long long)0, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p,
-                         (int64_t)amb.size());
+                         (int64_t)amb.size(), gq_dbg());
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -1845,7 +1868,11 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       return set_err(GQ_E_CAPACITY, "output capacity retries exhausted");
     }
   }
-  if (getenv("GQ_DBG") && germline_use_proj() && hc.prof[5])
+  if ((gq_dbg() & 32) && hc.prof[4])
+    fprintf(stderr, "gq germline_complex prof (cycles/item/wave): cover %.0f reference-base %.0f elements %.0f "
+            "decision %.0f (%llu items)\n", (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
+            (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
+  if ((gq_dbg() & 16) && germline_use_proj() && hc.prof[5])
     fprintf(stderr,
             "gq prof (cycles/tile/wave): setup %.0f first-loads %.0f entries %.0f counting %.0f decision %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
