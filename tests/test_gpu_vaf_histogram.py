@@ -46,3 +46,13 @@ def test_cli_vaf_histogram(tmp_path):
     want_h, _ = O.vaf_histogram(rs, _loci(rs, "chrM"), 10)
     sample = rs.sample_names[int(rs.sample[0])]
     assert lines[1:] == ["%s, %s, %d, %d, %d" % (bam, sample, b, min(b + 10, 100), n) for b, n in sorted(want_h.items())]
+
+
+@pytest.mark.parametrize("bins", [10, 20, 100])
+def test_vaf_histogram_suite_gpu(gpu_ctx, bins):
+    """VAFHistogramSuite.scala:8-43 through the device binning."""
+    from test_vaf_histogram import SUITE_HIST, suite_reads
+    rs = suite_reads()
+    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([8], np.int64), np.array([0], np.int64))
+    got = vaf_histogram_reads(gpu_ctx, rs, loci, bins)
+    assert got["histogram"] == SUITE_HIST[bins] and got["variant_loci"] == 5
