@@ -310,6 +310,59 @@ def variant_support_main(argv: Sequence[str]) -> int:
     return 0
 
 
+def germline_standard_reads(ctx: native.Context, rs: ReadSet, loci, **params) -> List[dict]:
+    """pileupFlatMap(reads, partitions, skipEmpty=true, callVariantsAtLocus) + GenotypeFilter
+    (commands/GermlineStandardCaller.scala:63-72) on the GPU.  Rows as somatic_standard_reads'
+    (contig by name; sample = the sample slot; tumor = the allele's evidence)."""
+    calls = ctx.germline_standard(device_reads(ctx, rs), loci, **params)
+    rows = []
+    for r in calls.rows:
+        r = dict(r)
+        r["contig"] = rs.contig_names[r["contig"]]
+        rows.append(r)
+    return rows
+
+
+def germline_standard_main(argv: Sequence[str]) -> int:
+    """GermlineStandard.Caller.run (commands/GermlineStandardCaller.scala:48-76).  The truth-set
+    concordance report (--truth-genotypes) is outside the pileup path and refused."""
+    p = argparse.ArgumentParser(prog="germline-standard",
+                                description="call variants using a simple quality-based probability")
+    p.add_argument("--reads", required=True)
+    p.add_argument("--min-mapq", type=int, default=1, help="Minimum read mapping quality for a read (Phred-scaled)")
+    p.add_argument("--min-read-depth", type=int, default=0, help="Minimum number of reads for a genotype call")
+    p.add_argument("--max-read-depth", type=int, default=2 ** 31 - 1, help="Maximum number of reads for a genotype call")
+    p.add_argument("--min-alternate-read-depth", type=int, default=0)
+    p.add_argument("--min-likelihood", type=int, default=0, help="Minimum Phred-scaled likelihood. Default: 0 (off)")
+    p.add_argument("--emit-ref", action="store_true", help="(accepted; callVariantsAtLocus is called without it)")
+    p.add_argument("--filter-multi-allelic", action="store_true", help="(accepted, unused by this caller)")
+    p.add_argument("--min-edge-distance", type=int, default=0, help="(accepted, unused by this caller)")
+    p.add_argument("--debug-genotype-filters", action="store_true")
+    p.add_argument("--truth-genotypes", default="", help="(concordance report: not supported)")
+    _common_args(p)
+    args = p.parse_args(argv)
+    if args.truth_genotypes:
+        raise ValueError("--truth-genotypes (concordance report) is not supported")
+    builder = _loci_builder(args)
+    rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True),
+                    recompute_md=args.recompute_md_tags,
+                    contig_lengths_from_dictionary=not args.no_sequence_dictionary)
+    loci = builder.result(rs.contig_lengths_map)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, rs)
+    flat = flatten_partitions(parts, rs.contig_index())
+    ctx = native.Context(args.device)
+    rows = germline_standard_reads(ctx, rs, flat, min_mapq=args.min_mapq, min_read_depth=args.min_read_depth,
+                                   max_read_depth=args.max_read_depth,
+                                   min_alternate_read_depth=args.min_alternate_read_depth,
+                                   min_likelihood=args.min_likelihood, apply_filters=1)
+    from .output import called_allele_genotype
+    out = [called_allele_genotype(r["contig"], r, rs.sample_names[r["sample"]] if r["sample"] < len(rs.sample_names)
+                                  else "default") for r in rows]
+    _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
+    print("Called %d genotypes." % len(out), file=sys.stderr)
+    return 0
+
+
 def vaf_histogram_reads(ctx: native.Context, rs: ReadSet, loci, bins: int = 20, min_read_depth: int = 0,
                         min_vaf: int = 0) -> Dict[str, object]:
     """VAFHistogram.variantLociFromReads + generateVAFHistogram (commands/VAFHistogram.scala:
@@ -390,7 +443,8 @@ def _finish_rank(rc: int) -> int:
 
 
 COMMANDS = {"germline-threshold": germline_threshold_main, "somatic-standard": somatic_standard_main,
-            "variant-support": variant_support_main, "vaf-histogram": vaf_histogram_main}
+            "variant-support": variant_support_main, "vaf-histogram": vaf_histogram_main,
+            "germline-standard": germline_standard_main}
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                        const Tile *__restrict__ tiles_n, DevReads RT, DevReads RN,
                                                        ComplexItem *__restrict__ cand, OutGeom og,
                                                        const int32_t *__restrict__ list, int min_mapq, Counters *ctr,
-                                                       RefView ref) {
+                                                       RefView ref, int no_bound = 0) {
   constexpr int S = T + 2 * kGuard;
   constexpr int KPT = T / kBlock;  // loci per thread
   static_assert(KPT <= 8, "per-thread flag bits");
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const bool agree = !ref.b || ref_agrees(mask, ref.b[ref.off[tt.contig] + L0 + i]);
     if (!agree || __popc(mask) > 1 || cx > 0 || depth > c_ref) {
       // single-base elements only, one standard reference base, no N: the hom-ref bound applies
-      const bool bound = agree && __popc(mask) == 1 && cx == 0 && cN == 0 && marg[i] > 0.02f + 2e-4f * (float)depth;
+      const bool bound = !no_bound && agree && __popc(mask) == 1 && cx == 0 && cN == 0 && marg[i] > 0.02f + 2e-4f * (float)depth;
       if (!bound) tflag |= 1u << (8 + k);
     }
   }
@@ -484,6 +484,7 @@ struct Cover {
   const int32_t *lst;
   int64_t rb, n;  // slots
   bool compact;
+  int sel;  // sample filter (-1: every read)
   // read of slot k and whether it covers pos
   __device__ __forceinline__ int64_t read(const DevReads &R, int64_t k, int32_t pos, bool *act) const {
     if (k >= n) {
@@ -495,13 +496,13 @@ struct Cover {
       return rb + lst[k];
     }
     const int64_t r = rb + k;
-    *act = R.start[r] <= pos && pos < R.end[r];
+    *act = R.start[r] <= pos && pos < R.end[r] && (sel < 0 || (int)R.sample[r] == sel);
     return r;
   }
 };
 __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst, uint32_t *tmp,
                             const WinInit &w, const int64_t *__restrict__ init_reads,
-                            const int32_t *__restrict__ init_rank, Counters *ctr) {
+                            const int32_t *__restrict__ init_rank, Counters *ctr, int sel = -1) {
   const int lane = threadIdx.x & 63;
   int64_t n = 0;
   // the covering reads lie in [first pmax_end > pos, first start > pos)
@@ -509,7 +510,7 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
   const int64_t rz = wave_first_true(ra, re, [&](int64_t r) { return R.start[r] > pos; });
   for (int64_t r0 = ra; r0 < rz; r0 += 64) {
     const int64_t r = r0 + lane;
-    const bool c = r < rz && R.start[r] <= pos && pos < R.end[r];
+    const bool c = r < rz && R.start[r] <= pos && pos < R.end[r] && (sel < 0 || (int)R.sample[r] == sel);
     const unsigned long long b = __ballot(c);
     const int64_t at = n + (int64_t)__popcll(b & ((1ull << lane) - 1ull));
     if (c && at < kCover) lst[at] = (int32_t)(r - rb);
@@ -521,6 +522,7 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
   cv.rb = rb;
   cv.compact = n <= kCover;
   cv.n = cv.compact ? n : (re - rb);
+  cv.sel = sel;
   if (w.n > 0 && pos < w.E) {
     if (!cv.compact) {
       raise_at(ctr, GQ_E_CAPACITY, pos);
@@ -784,7 +786,7 @@ __device__ __forceinline__ double fold_genotypes(const DevReads &R, const Cover 
 
 __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Cover &cv, int32_t pos,
                                 int min_mapq, bool include_alignment, int16_t *order, uint8_t *is_var,
-                                double *ll_lds, Counters *ctr) {
+                                double *ll_lds, Counters *ctr, bool by_log = false) {
   const int lane = threadIdx.x & 63;
   GenoResult res{};
   // eligibility + variant flag per entry (entry j on lane j & 63, slot j >> 6)
@@ -852,14 +854,17 @@ __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SampleP
     for (int j = 0; j < 64 && g0 + j < G; ++j) tot = tot + lane_f64(e, j);
   }
   const double lt = sm::log(tot);
-  double best = 0.0, vsum = 0.0;
+  // by_log: the first maximum of the normalized log-likelihoods (logSpace = true,
+  // GermlineStandardCaller.scala:105-111), its exp as the likelihood
+  double best = 0.0, bestx = 0.0, vsum = 0.0;
   int bestg = -1;
   for (int g0 = 0; g0 < G; g0 += 64) {
     const int g = g0 + lane;
-    double L = 0.0;
+    double L = 0.0, X = 0.0;
     bool v = false;
     if (g < G) {
-      L = sm::exp(ll_lds[g] - lt);
+      X = ll_lds[g] - lt;
+      L = sm::exp(X);
       int i, j;
       genotype_index(g, n, i, j);
       v = is_var[order[i]] || is_var[order[j]];
@@ -867,8 +872,10 @@ __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SampleP
     const unsigned long long vb = __ballot(v);
     for (int j = 0; j < 64 && g0 + j < G; ++j) {
       const double Lj = lane_f64(L, j);
-      if (bestg < 0 || Lj > best) {
+      const double Xj = by_log ? lane_f64(X, j) : 0.0;
+      if (bestg < 0 || (by_log ? Xj > bestx : Lj > best)) {
         best = Lj;
+        bestx = Xj;
         bestg = g0 + j;
       }
       if ((vb >> j) & 1ull) vsum = vsum + Lj;
@@ -1160,6 +1167,119 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_
     for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
 }
 
+// ---- germline-standard: GermlineStandard.Caller.callVariantsAtLocus
+// (commands/GermlineStandardCaller.scala:90-124) + GenotypeFilter (filters/GenotypeFilter.scala:
+// 140-154) at the candidate loci somatic_proj / somatic_tile leave (the reads as both "tumor"
+// and "normal"; the hom-ref bound with probabilityCorrectIgnoringAlignment).  One wave per
+// locus: the pileup's reference base over every read, then per sample (bySample, in sample
+// order) the QualityAlignedReadsFilter pileup's genotype likelihoods in log space, normalized,
+// the first maximum, and each non-reference allele of that genotype (twice for a hom-alt) with
+// its evidence over the sample's unfiltered pileup.  Records keep the sample in key bits 4-11.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_WPE))) void germline_standard_call(
+    const Tile *__restrict__ tiles, const ComplexItem *__restrict__ items, DevReads R, gq_germline_std_params prm,
+    SomRec *__restrict__ recs, unsigned long long rec_cap, uint8_t *__restrict__ pool, unsigned long long pool_cap,
+    OutGeom og, Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out, unsigned long long amb_cap,
+    const AmbItem *__restrict__ amb_in, const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+  __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
+  __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
+  __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
+  __shared__ int32_t cover_a[kSomWaves][kCover], cover_s[kSomWaves][kCover];
+  __shared__ double ll_lds[kSomWaves][kMaxG];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
+  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    const int64_t it = amb_in ? amb_in[li].item : li;
+    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    const Tile tt = tiles[item.tile];
+    const int32_t pos = item.pos;
+    const int32_t win = sw.range_win[tt.range];
+    // the pileup's reference base (Pileup.referenceBaseAtLocus over every read)
+    const Cover ca = make_cover(R, tt.rb, tt.re, pos, cover_a[wv], ev_lds[wv], sw.wi[2 * win], sw.init_reads,
+                                sw.init_rank, ctr);
+    uint8_t refbase;
+    bool ambiguous;
+    pileup_ref(R, ca, pos, ctr, amb_in ? (int)amb_ref[li] : -1, refbase, ambiguous);
+    if (!amb_in && ambiguous) {  // heap order decides the reference base: list it
+      if (lane == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+      }
+      continue;
+    }
+    for (int smp = 0; smp < R.n_samples; ++smp) {
+      const Cover cs = R.n_samples == 1 ? ca
+                                        : make_cover(R, tt.rb, tt.re, pos, cover_s[wv], ev_lds[wv], sw.wi[2 * win],
+                                                     sw.init_reads, sw.init_rank, ctr, smp);
+      SamplePile PF;
+      gather_sample(R, cs, pos, prm.min_mapq, refbase, ctr, PF);
+      if (PF.overflow) {
+        raise_at(ctr, GQ_E_CAPACITY, pos);
+        continue;
+      }
+      if (PF.depth_f == 0) continue;  // no sample pileup, or nothing left after the mapq filter
+      const GenoResult g =
+          genotypes(R, PF, cs, pos, prm.min_mapq, false, order_lds[wv], var_lds[wv], ll_lds[wv], ctr, true);
+      if (g.G == 0) {
+        raise_at(ctr, GQ_E_ASSERT, pos);  // empty.maxBy: no allele with standard bases
+        continue;
+      }
+      const AlleleDesc a1 = pile_desc(PF, g.bi), a2 = pile_desc(PF, g.bj);
+      const bool v1 = allele_is_variant(R, a1, pos), v2 = allele_is_variant(R, a2, pos);
+      if (!v1 && !v2) continue;
+      SamplePile PA;  // the sample's unfiltered pileup: AlleleEvidence's
+      gather_sample(R, cs, pos, 0, refbase, ctr, PA);
+      for (int sub = 0; sub < 2; ++sub) {
+        if (!(sub == 0 ? v1 : v2)) continue;
+        const AlleleDesc al = sub == 0 ? a1 : a2;
+        const Key128 key = allele_key(R, al, pos, 0);
+        gq_evidence ev;
+        allele_evidence(R, cs, pos, 0, PA, key, g.best_l, ev_lds[wv], ctr, ev);
+        const int gqv = success_to_phred(ev.likelihood - 1e-10);
+        if (prm.apply_filters) {
+          if (!(ev.read_depth >= prm.min_read_depth && ev.read_depth < prm.max_read_depth)) continue;
+          if (prm.min_alternate_read_depth > 0 && !(ev.allele_read_depth >= prm.min_alternate_read_depth)) continue;
+          if (prm.min_likelihood > 0 && !(gqv >= prm.min_likelihood)) continue;
+        }
+        const int rl = allele_ref_len(al), alt_l = allele_alt_len(al);
+        SomRec rr;
+        rr.key = ((uint64_t)(tt.ordinal0 + (pos - tt.L0)) << 12) | ((uint64_t)smp << 4) | (uint64_t)sub;
+        rr.contig = tt.contig;
+        rr.pos = pos;
+        rr.ref_len = (uint16_t)rl;
+        rr.alt_len = (uint16_t)alt_l;
+        rr.flags = amb_in ? 1 : 0;
+        rr.pad[0] = rr.pad[1] = rr.pad[2] = 0;
+        rr.log_odds = 0.0;
+        rr.gq = gqv;
+        rr.pad2 = 0;
+        rr.tumor = ev;
+        rr.normal = gq_evidence{};
+        if (rl + alt_l <= 8) {
+          uint64_t v = 0;
+          int j = 0;
+          for (int i = 0; i < rl; ++i) v |= (uint64_t)allele_byte(R, al, pos, 0, i) << (8 * j++);
+          for (int i = 0; i < alt_l; ++i) v |= (uint64_t)allele_byte(R, al, pos, 1, i) << (8 * j++);
+          rr.allele = v;
+        } else {
+          unsigned long long off = 0;
+          if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + alt_l));
+          off = __shfl(off, 0, 64);
+          if (off + rl + alt_l <= pool_cap)
+            for (int i = lane; i < rl + alt_l; i += 64)
+              pool[off + i] = i < rl ? allele_byte(R, al, pos, 0, i) : allele_byte(R, al, pos, 1, i - rl);
+          rr.allele = off;
+        }
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
+          if (k < rec_cap) recs[k] = rr;
+        }
+      }
+    }
+  }
+}
+
 // Exclusive offsets of the candidate partitions (clamped to their capacities), the total in
 // n_complex and the largest overflow in part_max[1] (part_scan of gq_pileup.hip, which = 1).
 __global__ __launch_bounds__(1024) void part_scan_som(Counters *ctr, OutGeom og) {
@@ -1313,8 +1433,60 @@ __global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__res
   }
 }
 
-gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq) {
-  if (t->mproj && t->mproj_mapq == min_mapq) return GQ_OK;
+// The pileup element order of a plan's windows (SomWin): each window's first visited locus and
+// its initial (heap-ordered) group of reads, for the two read sets t and n.
+gq_status build_somwin(gq_ctx *c, const Plan &pt, const gq_dev_reads *t, const gq_dev_reads *n, SomWin &sw) {
+  {
+    const int64_t nw = (int64_t)pt.wins.size(), nr = (int64_t)pt.rs.size();
+    std::vector<int32_t> w_contig((size_t)nw);
+    std::vector<int64_t> w_roff((size_t)nw + 1);
+    for (int64_t w = 0; w < nw; ++w) {
+      w_contig[(size_t)w] = pt.wins[(size_t)w].contig;
+      w_roff[(size_t)w] = pt.wins[(size_t)w].r0;
+    }
+    w_roff[(size_t)nw] = nr;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_roff = al(4 * (size_t)nw), o_rs = o_roff + al(8 * ((size_t)nw + 1)), o_re = o_rs + al(8 * (size_t)nr),
+                 o_rw = o_re + al(8 * (size_t)nr), o_wi = o_rw + al(4 * (size_t)nr),
+                 o_lo = o_wi + al(sizeof(WinInit) * 2 * (size_t)nw), o_end = o_lo + al(8 * 2 * (size_t)nw);
+    HIP_TRY(c->win_meta.ensure(o_end));
+    char *b = (char *)c->win_meta.p;
+    HIP_TRY(hipMemcpyAsync(b, w_contig.data(), 4 * (size_t)nw, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_roff, w_roff.data(), 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_rs, pt.rs.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_re, pt.re.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_rw, pt.rwin.data(), 4 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
+    WinInit *d_wi = (WinInit *)(b + o_wi);
+    int64_t *d_lo = (int64_t *)(b + o_lo);
+    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       (const int32_t *)b, (const int64_t *)(b + o_roff), (const int64_t *)(b + o_rs),
+                       (const int64_t *)(b + o_re), nw, t->d, n->d, d_wi, d_lo);
+    HIP_TRY(hipGetLastError());
+    std::vector<WinInit> wi((size_t)(2 * nw));
+    HIP_TRY(hipMemcpyAsync(wi.data(), d_wi, sizeof(WinInit) * wi.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int64_t tot = 0;
+    for (WinInit &x : wi) {
+      x.off = tot;
+      tot += x.cap;
+    }
+    HIP_TRY(hipMemcpyAsync(d_wi, wi.data(), sizeof(WinInit) * wi.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c->win_grp.ensure((size_t)std::max<int64_t>(tot, 1) * 16));
+    int64_t *d_reads = (int64_t *)c->win_grp.p;
+    int32_t *d_rank = (int32_t *)(d_reads + std::max<int64_t>(tot, 1));
+    int32_t *d_heap = d_rank + std::max<int64_t>(tot, 1);
+    hipLaunchKernelGGL(window_group, dim3((unsigned)((2 * nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       d_wi, (const int64_t *)d_lo, 2 * nw, t->d, n->d, d_reads, d_rank, d_heap);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // wi (host) outlives its copy
+    sw = SomWin{(const int32_t *)(b + o_rw), d_wi, d_reads, d_rank};
+  }
+  return GQ_OK;
+}
+
+gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq, bool incl_align = true) {
+  const int key = 2 * min_mapq + (incl_align ? 1 : 0);  // the projection's filter and probability model
+  if (t->mproj && t->mproj_mapq == key) return GQ_OK;
   if (!t->mproj) {
     void *p = nullptr;
     HIP_TRY(hipMalloc(&p, (size_t)(2 * t->proj_bytes + 32)));
@@ -1322,9 +1494,9 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   }
   if (t->n_slices > 0)
     hipLaunchKernelGGL(mproj_fill, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
-                       c->stream, t->d, t->n_slices, min_mapq, (int16_t *)t->mproj);
+                       c->stream, t->d, t->n_slices, min_mapq, incl_align ? 1 : 0, (int16_t *)t->mproj);
   HIP_TRY(hipGetLastError());
-  t->mproj_mapq = min_mapq;
+  t->mproj_mapq = key;
   return GQ_OK;
 }
 
@@ -1483,50 +1655,10 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   // pileup element order: each window's first visited locus and initial (heap-ordered) group
   SomWin sw{};
-  {
-    const int64_t nw = (int64_t)pt.wins.size(), nr = (int64_t)pt.rs.size();
-    std::vector<int32_t> w_contig((size_t)nw);
-    std::vector<int64_t> w_roff((size_t)nw + 1);
-    for (int64_t w = 0; w < nw; ++w) {
-      w_contig[(size_t)w] = pt.wins[(size_t)w].contig;
-      w_roff[(size_t)w] = pt.wins[(size_t)w].r0;
-    }
-    w_roff[(size_t)nw] = nr;
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t o_roff = al(4 * (size_t)nw), o_rs = o_roff + al(8 * ((size_t)nw + 1)), o_re = o_rs + al(8 * (size_t)nr),
-                 o_rw = o_re + al(8 * (size_t)nr), o_wi = o_rw + al(4 * (size_t)nr),
-                 o_lo = o_wi + al(sizeof(WinInit) * 2 * (size_t)nw), o_end = o_lo + al(8 * 2 * (size_t)nw);
-    HIP_TRY(c->win_meta.ensure(o_end));
-    char *b = (char *)c->win_meta.p;
-    HIP_TRY(hipMemcpyAsync(b, w_contig.data(), 4 * (size_t)nw, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_roff, w_roff.data(), 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_rs, pt.rs.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_re, pt.re.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_rw, pt.rwin.data(), 4 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    WinInit *d_wi = (WinInit *)(b + o_wi);
-    int64_t *d_lo = (int64_t *)(b + o_lo);
-    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                       (const int32_t *)b, (const int64_t *)(b + o_roff), (const int64_t *)(b + o_rs),
-                       (const int64_t *)(b + o_re), nw, t->d, n->d, d_wi, d_lo);
-    HIP_TRY(hipGetLastError());
-    std::vector<WinInit> wi((size_t)(2 * nw));
-    HIP_TRY(hipMemcpyAsync(wi.data(), d_wi, sizeof(WinInit) * wi.size(), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    int64_t tot = 0;
-    for (WinInit &x : wi) {
-      x.off = tot;
-      tot += x.cap;
-    }
-    HIP_TRY(hipMemcpyAsync(d_wi, wi.data(), sizeof(WinInit) * wi.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c->win_grp.ensure((size_t)std::max<int64_t>(tot, 1) * 16));
-    int64_t *d_reads = (int64_t *)c->win_grp.p;
-    int32_t *d_rank = (int32_t *)(d_reads + std::max<int64_t>(tot, 1));
-    int32_t *d_heap = d_rank + std::max<int64_t>(tot, 1);
-    hipLaunchKernelGGL(window_group, dim3((unsigned)((2 * nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                       d_wi, (const int64_t *)d_lo, 2 * nw, t->d, n->d, d_reads, d_rank, d_heap);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));  // wi (host) outlives its copy
-    sw = SomWin{(const int32_t *)(b + o_rw), d_wi, d_reads, d_rank};
+  st = build_somwin(c, pt, t, n, sw);
+  if (st) {
+    free(res);
+    return st;
   }
   // the tumor's margin projection for this mapq filter (derived once per read set and filter)
   st = ensure_margin_projection(c, t, (int)p->min_mapq);
@@ -1869,6 +2001,201 @@ void gq_free_allele_counts(gq_allele_counts *r) {
   free(r->allele_pool);
   free(r->flags);
   free(r);
+}
+
+gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, const gq_germline_std_params *p,
+                               gq_somatic_calls **out) {
+  if (!c || !rd || !loci || !p || !out) return set_err(GQ_E_ARG, "gq_germline_standard: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const auto h0 = std::chrono::steady_clock::now();
+  c->timings = gq_timings{};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  Plan pt;
+  gq_status st = plan(c, rd, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
+  if (st) return st;
+  gq_somatic_calls *res = (gq_somatic_calls *)calloc(1, sizeof(gq_somatic_calls));
+  if (!res) return set_err(GQ_E_NOMEM, "calloc");
+  auto fail = [&](gq_status e) {
+    free(res);
+    return e;
+  };
+  if (pt.n_tiles == 0) {
+    *out = res;
+    return GQ_OK;
+  }
+  {
+    double succ[256];
+    for (int q = 0; q < 256; ++q) succ[q] = 1.0 - std::pow(10.0, -q / 10.0);
+    HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_succ), succ, sizeof succ, 0, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  SomWin sw{};
+  st = build_somwin(c, pt, rd, rd, sw);
+  if (st) return fail(st);
+  // the hom-ref bound with probabilityCorrectIgnoringAlignment; with several samples the bound
+  // over the pooled elements proves nothing per sample, so every non-Match locus is a candidate
+  st = ensure_margin_projection(c, rd, (int)p->min_mapq, false);
+  if (st) return fail(st);
+  const int no_bound = rd->d.n_samples > 1 ? 1 : 0;
+  OutGeom og{};
+  {
+    if (c->n_cu <= 0 &&
+        hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+      c->n_cu = 256;
+    if (c->som_wg_per_cu <= 0) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0) != hipSuccess ||
+          nb <= 0)
+        nb = 4;
+      c->som_wg_per_cu = nb;
+    }
+    og.ncols = (int)std::max<int64_t>(1, std::min<int64_t>({(pt.n_tiles + SomProjCfg::kWaves - 1) / SomProjCfg::kWaves,
+                                                           (int64_t)c->som_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
+    const unsigned long long wg_loci = (unsigned long long)((pt.n_tiles + og.ncols - 1) / og.ncols) * SomProjCfg::kT;
+    og.capA[1] = wg_loci / 16 + 256;
+    og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;
+  }
+  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096;
+  Counters hc{};
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
+    HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
+    HIP_TRY(c->srecs.ensure(rec_cap * sizeof(SomRec)));
+    HIP_TRY(c->pool.ensure(pool_cap));
+    HIP_TRY(c->slow.ensure((size_t)pt.n_tiles * sizeof(int32_t)));
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    Counters *ctr = (Counters *)c->counters.p;
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, pt.n_tiles, rd->d, (const int16_t *)rd->mproj,
+                       rd->d.start, rd->d.end, (ComplexItem *)c->cplx.p, og, ctr, (int32_t *)c->slow.p,
+                       RefView{nullptr, nullptr}, no_bound);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((somatic_tile<SomProjCfg::kT>), dim3((unsigned)std::min<int64_t>(pt.n_tiles, 2048)), dim3(kBlock), 0,
+                       c->stream, (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, rd->d, rd->d, (ComplexItem *)c->cplx.p,
+                       og, (const int32_t *)c->slow.p, (int)p->min_mapq, ctr, RefView{nullptr, nullptr}, 1);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(part_scan_som, dim3(1), dim3(1024), 0, c->stream, ctr, og);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    {
+      unsigned long long pm = 0;
+      HIP_TRY(hipMemcpyAsync(&pm, &ctr->part_max[1], sizeof(pm), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (pm) {
+        og.capA[1] += pm + 64;
+        og.capB[1] += pm + 64;
+        if (attempt == 2) return fail(set_err(GQ_E_CAPACITY, "candidate capacity retries exhausted"));
+        continue;
+      }
+    }
+    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
+    hipLaunchKernelGGL(germline_standard_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                       (const ComplexItem *)c->cplx.p, rd->d, *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p,
+                       pool_cap, og, ctr, sw, (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr,
+                       (const uint8_t *)nullptr, (int64_t)0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bool retry = false;
+    if (hc.n_amb > amb_cap) {
+      amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (!retry && hc.n_amb > 0 && !hc.err) {  // heap-order reference bases: replay, then those loci again
+      std::vector<AmbItem> amb((size_t)hc.n_amb);
+      HIP_TRY(hipMemcpyAsync(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(c->amb_ref.ensure(amb.size()));
+      st = heap_ref_bases(c, pt, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
+      if (st) return fail(st);
+      const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 8192);
+      hipLaunchKernelGGL(germline_standard_call, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const ComplexItem *)c->cplx.p, rd->d, *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p,
+                         pool_cap, og, ctr, sw, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
+                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (hc.n_rec > rec_cap) {
+      rec_cap = hc.n_rec + 1024;
+      retry = true;
+    }
+    if (hc.pool_used > pool_cap) {
+      pool_cap = hc.pool_used + 4096;
+      retry = true;
+    }
+    if (!retry) break;
+    if (attempt == 2) return fail(set_err(GQ_E_CAPACITY, "output capacity retries exhausted"));
+  }
+  for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
+  st = check_device_error(c, hc);
+  if (st) return fail(st);
+  const int64_t nr = (int64_t)hc.n_rec;
+  std::vector<SomRec> recs((size_t)nr);
+  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
+  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::sort(recs.begin(), recs.end(), [](const SomRec &a, const SomRec &b) { return a.key < b.key; });
+  const size_t N = (size_t)std::max<int64_t>(nr, 1);
+  res->n = nr;
+  res->contig = (int32_t *)malloc(N * 4);
+  res->pos = (int64_t *)malloc(N * 8);
+  res->sample = (uint8_t *)calloc(N, 1);
+  res->ref_off = (int64_t *)malloc(N * 8);
+  res->alt_off = (int64_t *)malloc(N * 8);
+  res->ref_len = (int32_t *)malloc(N * 4);
+  res->alt_len = (int32_t *)malloc(N * 4);
+  res->log_odds = (double *)malloc(N * 8);
+  res->gq = (int32_t *)malloc(N * 4);
+  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->flags = (uint8_t *)malloc(N);
+  std::vector<uint8_t> apool;
+  for (int64_t k = 0; k < nr; ++k) {
+    const SomRec &r = recs[(size_t)k];
+    res->contig[k] = r.contig;
+    res->pos[k] = r.pos;
+    res->sample[k] = (uint8_t)((r.key >> 4) & 0xFFu);
+    res->ref_len[k] = r.ref_len;
+    res->alt_len[k] = r.alt_len;
+    res->ref_off[k] = (int64_t)apool.size();
+    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
+    const int tot = r.ref_len + r.alt_len;
+    if (tot <= 8)
+      for (int i = 0; i < tot; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
+    else
+      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele, hpool.begin() + (ptrdiff_t)(r.allele + tot));
+    res->log_odds[k] = r.log_odds;
+    res->gq[k] = r.gq;
+    res->tumor[k] = r.tumor;
+    res->normal[k] = r.normal;
+    res->flags[k] = r.flags;
+  }
+  res->pool_len = (int64_t)apool.size();
+  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
+  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  res->visited_loci = (int64_t)hc.visited;
+  res->candidate_loci = (int64_t)hc.n_complex;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timings.pileup_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+  c->timings.complex_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[3], c->ev[4]);
+  c->timings.finalize_ms = ms;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[4]);
+  c->timings.total_ms = ms;
+  c->timings.tiles = pt.n_tiles;
+  c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
+  *out = res;
+  return GQ_OK;
 }
 
 void gq_free_somatic(gq_somatic_calls *r) {

@@ -35,14 +35,15 @@ __device__ __forceinline__ int16_t margin_term(bool match, int q, float em, floa
 // The margin word of tumor read r at column col (8 loci, int16 each; hom_ref_margin_lane's
 // terms).  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
 // 25-36) and non-Match/Mismatch loci hold 0.
-__device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq) {
+__device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq, bool incl_align) {
   const ColDesc d = R.cdesc[r];
   const int32_t s = d.start;
   const int32_t lb = 8 * col;
   int16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int mq = (int)R.mapq[r];
   if (!(min_mapq > 0 && mq < min_mapq)) {
-    const float em = exp2f(-0.33219281f * (float)mq);
+    // probabilityCorrectIncludingAlignment (somatic tumor) or IgnoringAlignment (germline-standard)
+    const float em = incl_align ? exp2f(-0.33219281f * (float)mq) : 0.0f;
     const float lsm = log1pf(-em);
     const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
     const uint32_t *ev = R.md_ev + R.md_off[r];
@@ -93,14 +94,14 @@ __device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_
 
 // The margin projection of the tumor reads, laid out as `proj` (an int16 per projection byte:
 // word w of the pool at mproj + 16 w), one wave per slice.
-__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
+__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq, int incl_align,
                                                   int16_t *__restrict__ mproj) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     const int64_t base = R.sbase[slot];
     walk_slice_words(R, slot, [&](bool act, int64_t r, int32_t col, int64_t w) {
-      if (act) *reinterpret_cast<uint4 *>(mproj + 8 * (base + w)) = margin_word(R, r, col, min_mapq);
+      if (act) *reinterpret_cast<uint4 *>(mproj + 8 * (base + w)) = margin_word(R, r, col, min_mapq, incl_align != 0);
     });
   }
 }
@@ -151,7 +152,8 @@ template <bool kRef>
 __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void somatic_proj(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, int64_t n_tiles, DevReads RT,
     const int16_t *__restrict__ mproj, const int32_t *__restrict__ n_start, const int32_t *__restrict__ n_end,
-    ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref) {
+    ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref,
+    int no_bound = 0) {
   using C = SomProjCfg;
   constexpr int T = C::kT, U = C::kU;
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // tumor event read bases: A C T G bytes
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
       const bool nonmatch = !agree || (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
       const int16_t m16 = (int16_t)((msum[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-      const bool bound = agree && single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
+      const bool bound = !no_bound && agree && single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
       const bool tcand = depth > 0 && nonmatch && !bound;
       visited += (in && (depth > 0 || dn_run > 0)) ? 1u : 0u;
       const bool q = in && tcand && dn_run > 0;

@@ -66,6 +66,15 @@ class gq_allele_counts(C.Structure):
                 ("allele_pool", C.c_void_p), ("pool_len", C.c_int64), ("flags", C.POINTER(C.c_uint8))]
 
 
+class gq_germline_std_params(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("min_mapq", "min_read_depth", "max_read_depth", "min_alternate_read_depth",
+                                         "min_likelihood", "apply_filters")]
+
+
+GERMLINE_STD_DEFAULTS = dict(min_mapq=1, min_read_depth=0, max_read_depth=2 ** 31 - 1, min_alternate_read_depth=0,
+                             min_likelihood=0, apply_filters=1)
+
+
 class gq_vaf_params(C.Structure):
     _fields_ = [("bins", C.c_int32), ("min_read_depth", C.c_int32), ("min_vaf", C.c_int32)]
 
@@ -138,7 +147,7 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
             "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts",
-            "gq_vaf_histogram")
+            "gq_vaf_histogram", "gq_germline_standard")
 
 
 def lib():
@@ -154,7 +163,8 @@ def lib():
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
                   "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard",
-                  "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support", "gq_vaf_histogram"):
+                  "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support", "gq_vaf_histogram",
+                  "gq_germline_standard"):
             getattr(L, f).restype = C.c_int
         L.gq_germline_threshold.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_params),
                                             C.POINTER(C.POINTER(gq_calls))]
@@ -171,6 +181,8 @@ def lib():
         L.gq_variant_support.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci),
                                          C.POINTER(C.POINTER(gq_allele_counts))]
         L.gq_free_allele_counts.argtypes = [C.POINTER(gq_allele_counts)]
+        L.gq_germline_standard.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_germline_std_params),
+                                           C.POINTER(C.POINTER(gq_somatic_calls))]
         L.gq_vaf_histogram.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(gq_loci), C.POINTER(gq_vaf_params),
                                        C.POINTER(gq_vaf_hist)]
         L.gq_free_calls.argtypes = [C.POINTER(gq_calls)]
@@ -329,6 +341,21 @@ class Context:
                      pool[ao[i]:ao[i] + al[i]].decode("latin-1"), int(cnt[i]), int(fl[i])) for i in range(n)]
         finally:
             lib().gq_free_allele_counts(out)
+
+    def germline_standard(self, reads: "DeviceReads", loci, **params) -> "SomaticCalls":
+        """germline-standard (gq_germline_standard): CalledAllele rows in the SomaticCalls layout
+        (tumor = the allele's evidence, sample = its sample slot).  params: the
+        gq_germline_std_params fields; defaults GERMLINE_STD_DEFAULTS (the CLI defaults)."""
+        L, keep = make_gq_loci(*loci)
+        p = dict(GERMLINE_STD_DEFAULTS)
+        p.update(params)
+        ps = gq_germline_std_params(**{k: int(v) for k, v in p.items()})
+        out = C.POINTER(gq_somatic_calls)()
+        _check(lib().gq_germline_standard(self.h, reads.h, C.byref(L), C.byref(ps), C.byref(out)))
+        try:
+            return SomaticCalls.from_struct(out.contents)
+        finally:
+            lib().gq_free_somatic(out)
 
     def vaf_histogram(self, reads: "DeviceReads", loci, bins: int = 20, min_read_depth: int = 0,
                       min_vaf: int = 0) -> Dict[str, object]:

@@ -71,6 +71,13 @@ def somatic_genotype(contig: str, row: Dict, sample: str) -> Dict:
                              alternateAllele=row["alt"], contig=dict(contigName=contig)))
 
 
+def called_allele_genotype(contig: str, row: Dict, sample: str) -> Dict:
+    """AlleleConversions.calledAlleleToADAMGenotype (AlleleConversions.scala:30-45): as the
+    somatic builder with GQ = the evidence's phredScaledLikelihood (CalledAllele.scala:39: end
+    = start + 1)."""
+    return somatic_genotype(contig, row, sample)
+
+
 # ---- Avro JSON encoding -------------------------------------------------------------------
 def java_float(x: float) -> str:
     """Float.toString of a float32 (what Jackson writes for JsonEncoder.writeFloat): the shortest

@@ -278,6 +278,24 @@ typedef struct {
 gq_status gq_variant_support(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci, gq_allele_counts **out);
 void gq_free_allele_counts(gq_allele_counts *c);
 
+/* germline-standard: GermlineStandard.Caller.callVariantsAtLocus (commands/GermlineStandardCaller
+ * .scala:90-124) over pileupFlatMap(reads, partitions, skipEmpty = true) (:63-68), then
+ * GenotypeFilter (filters/GenotypeFilter.scala:140-154) when apply_filters.  Results in a
+ * gq_somatic_calls: one row per CalledAllele, `sample` its sample slot, `tumor` its
+ * AlleleEvidence, `gq` its phredScaledLikelihood, `normal` and `log_odds` zero; flags bit0 =
+ * the pileup reference base came from heap order.  A sample's rows follow sample order (the
+ * reference iterates a Scala Map there: unpinned for > 1 sample).                          */
+typedef struct {
+  int32_t min_mapq;                 /* --min-mapq (1): QualityAlignedReadsFilter        */
+  int32_t min_read_depth;           /* --min-read-depth (0)                             */
+  int32_t max_read_depth;           /* --max-read-depth (Int.MaxValue)                  */
+  int32_t min_alternate_read_depth; /* --min-alternate-read-depth (0)                   */
+  int32_t min_likelihood;           /* --min-likelihood (0)                             */
+  int32_t apply_filters;            /* 0 => raw callVariantsAtLocus output              */
+} gq_germline_std_params;
+gq_status gq_germline_standard(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
+                               const gq_germline_std_params *params, gq_somatic_calls **out);
+
 /* vaf-histogram: VAFHistogram.variantLociFromReads + generateVAFHistogram
  * (commands/VAFHistogram.scala:208-229, 188-196): at every visited locus whose pileup holds a
  * non-Match element (VariantLocus.apply, :31-37), VAF = (depth - referenceDepth).toFloat /

@@ -1093,9 +1093,65 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
       appendEvidence(out, nev);
       appendf(out, "\t%d\n", flags);
 }
+// GermlineStandard.Caller.callVariantsAtLocus (commands/GermlineStandardCaller.scala:90-124) +
+// GenotypeFilter (filters/GenotypeFilter.scala:140-154) when apply_filters.  Per sample of the
+// pileup (bySample: a Scala Map; here by sample index, unpinned for > 1 sample): the elements
+// passing QualityAlignedReadsFilter, the ML genotype over likelihoodsOfAllPossibleGenotypes
+// (log space, normalized; maxBy keeps the first maximum), probability = exp of it, and for each
+// non-reference allele of the genotype (both, for a hom-alt) the allele's evidence over the
+// sample's unfiltered elements.  Lines as somatic-standard's (normal evidence zero, log-odds 0,
+// gq = the evidence's phredScaledLikelihood).
+void germlineStandardAtLocus(const Pileup &p, const char *contigName, const or_germline_std_params *prm,
+                             bool ambiguousRef, std::string &out) {
+  if (p.elements.empty()) return;
+  std::map<int, std::vector<const Elem *>> bySample;
+  for (const Elem &e : p.elements) bySample[e.read->sample].push_back(&e);
+  for (auto &kv : bySample) {
+    const std::vector<const Elem *> &all = kv.second;
+    std::vector<const Elem *> filt;
+    for (const Elem *e : all)
+      if (e->read->mapq >= prm->min_mapq) filt.push_back(e);  // QualityAlignedReadsFilter
+    if (filt.empty()) continue;
+    auto gl = likelihoodsOfAllPossibleGenotypes(filt, false, true, true);
+    if (gl.empty()) fail(E_ASSERT, "empty.maxBy");
+    size_t best = 0;
+    for (size_t i = 1; i < gl.size(); ++i)
+      if (gl[i].second > gl[best].second) best = i;
+    const double probability = strictmath::exp(gl[best].second);
+    const Genotype &g = gl[best].first;
+    for (const Allele *a : {&g.a1, &g.a2}) {
+      if (!a->isVariant()) continue;
+      Evidence ev = alleleEvidence(probability, *a, all);
+      const int gq = successProbabilityToPhred(ev.likelihood - 1e-10);
+      if (prm->apply_filters) {
+        if (!(ev.readDepth >= prm->min_read_depth && ev.readDepth < prm->max_read_depth)) continue;
+        if (prm->min_alternate_read_depth > 0 && !(ev.alleleReadDepth >= prm->min_alternate_read_depth)) continue;
+        if (prm->min_likelihood > 0 && !(gq >= prm->min_likelihood)) continue;
+      }
+      appendf(out, "%s\t%lld\t%d\t%s\t%s\t%.17g\t%d", contigName, (long long)p.locus, kv.first, a->ref.c_str(),
+              a->alt.c_str(), 0.0, gq);
+      appendEvidence(out, ev);
+      appendEvidence(out, Evidence{});
+      appendf(out, "\t%d\n", ambiguousRef ? 1 : 0);  // bit0: heap-order reference base
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
+
+int or_germline_standard(const or_reads *reads, const or_loci *loci, const or_germline_std_params *prm, char **o,
+                         int64_t *olen) {
+  std::string out;
+  return guard(out, o, olen, [&]() {
+    ReadSet rs;
+    buildReads(reads, rs);
+    std::vector<ReadSet *> sets{&rs};
+    forEachPileup(sets, loci, [&](const TaskContig &tc, std::vector<Pileup> &ps, std::vector<bool> &amb) {
+      germlineStandardAtLocus(ps[0], loci->contig_names[tc.contig], prm, amb[0], out);
+    });
+  });
+}
 
 const char *or_last_error(void) { return g_err.c_str(); }
 void or_free(char *p) { free(p); }

@@ -113,6 +113,19 @@ int or_variant_support(const or_reads *reads, const or_loci *loci, char **out, i
 int or_vaf_histogram(const or_reads *reads, const or_loci *loci, int32_t bins, int32_t min_read_depth,
                      int32_t min_vaf, char **out, int64_t *out_len);
 
+/* germline-standard (GermlineStandardCaller.scala:90-124, GenotypeFilter.scala:140-154). */
+typedef struct {
+  int32_t min_mapq;                 /* --min-mapq (1)                        */
+  int32_t min_read_depth;           /* --min-read-depth (0)                  */
+  int32_t max_read_depth;           /* --max-read-depth (Int.MaxValue)       */
+  int32_t min_alternate_read_depth; /* --min-alternate-read-depth (0)        */
+  int32_t min_likelihood;           /* --min-likelihood (0)                  */
+  int32_t apply_filters;            /* 0 => raw callVariantsAtLocus output   */
+} or_germline_std_params;
+/* Lines as or_somatic_standard's (normal evidence zero).                     */
+int or_germline_standard(const or_reads *reads, const or_loci *loci, const or_germline_std_params *p, char **out,
+                         int64_t *out_len);
+
 /* ---- single-locus entry points used to pin the oracle with the reference's unit
  * KATs.  They build the pileup with Pileup.apply(reads, contig, locus)
  * (Pileup.scala:181-186): reads in input order, reference base from

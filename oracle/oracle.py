@@ -200,6 +200,32 @@ def vaf_histogram(rs, loci, bins: int = 20, min_read_depth: int = 0, min_vaf: in
     return hist, variant
 
 
+class or_germline_std_params(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("min_mapq", "min_read_depth", "max_read_depth", "min_alternate_read_depth",
+                                         "min_likelihood", "apply_filters")]
+
+
+GERMLINE_STD_DEFAULTS = dict(min_mapq=1, min_read_depth=0, max_read_depth=2 ** 31 - 1, min_alternate_read_depth=0,
+                             min_likelihood=0, apply_filters=1)
+
+
+def germline_standard(rs, loci, **params):
+    """Rows as somatic_standard's (sample = sample index; normal evidence zero)."""
+    p = dict(GERMLINE_STD_DEFAULTS)
+    p.update(params)
+    ps = or_germline_std_params(**{k: int(v) for k, v in p.items()})
+    m = _Marshalled(rs)
+    L = _Loci(rs.contig_names, *loci)
+    text = _call(lib().or_germline_standard, C.byref(m.s), C.byref(L.s), C.byref(ps))
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        ev = lambda a: (float(a[0]), int(a[1]), int(a[2]), int(a[3]), int(a[4])) + tuple(float(x) for x in a[5:10])
+        out.append(dict(contig=f[0], locus=int(f[1]), sample=int(f[2]), ref=f[3], alt=f[4], log_odds=float(f[5]),
+                        gq=int(f[6]), tumor=ev(f[7:17]), normal=ev(f[17:27]), flags=int(f[27])))
+    return out
+
+
 # ---- single-locus entry points (Pileup.apply semantics), used by the KAT tests
 def _contig_id(rs, contig: str) -> int:
     return rs.contig_names.index(contig)
