@@ -179,7 +179,7 @@ def main() -> int:
     #      base, 16 B of metadata per read, 4 B per CIGAR op and per MD event, 32 B per record
     #      and 12 B per queued locus written.  Its share is the tiles it kept (walk_tiles go to
     #      the walker).  The bytes it actually reads are reported beside it (`read_bytes`: the
-    #      8-locus-aligned projection, 16-B records + pmax_end, 8-B sparse entries).
+    #      8-locus-aligned projection, 4-B piece records, 8-B sparse entries).
     st = ctx.proj_stats(reads)
     a = g.arrays
     n_reads = int(a["start"].shape[0])
@@ -189,7 +189,7 @@ def main() -> int:
     bytes_md = 4 * int(a["md_ev"].shape[0])
     bytes_out = 32 * len(calls) + 12 * int(calls.complex_loci)
     b_all = bytes_seq + bytes_meta + bytes_cigar + bytes_md + bytes_out
-    read_bytes = int(st["proj_bytes"]) + 12 * n_reads + 8 * int(st["pev_count"])
+    read_bytes = int(st["proj_bytes"]) + 4 * int(st["n_pieces"]) + 8 * int(st["pev_count"])
     kept = 1.0 - float(np.mean(walk_frac))
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))

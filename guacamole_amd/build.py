@@ -27,11 +27,24 @@ def _stale(target: str, deps) -> bool:
 def build_hip(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     if force or _stale(LIB, DEPS):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I" + os.path.join(ROOT, "include"), "-o", LIB] + SOURCES
+        # one hipcc per translation unit, in parallel, then one link
+        objs = [os.path.join(LIB_DIR, os.path.basename(s) + ".o") for s in SOURCES]
+        procs = []
+        for src, obj in zip(SOURCES, objs):
+            cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-c",
+                   "-I" + os.path.join(ROOT, "include"), "-o", obj, src]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((cmd, subprocess.Popen(cmd)))
+        for cmd, p in procs:
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, cmd)
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
+        for obj in objs:
+            os.remove(obj)
     return LIB
 
 

@@ -1,16 +1,17 @@
 // gq_germline_proj.h — germline_proj: the germline-threshold pileup kernel over the read
-// projections derived at upload (ProjRec, proj, pev: gq_pileup.hip proj_count / proj_fill /
+// projections derived at upload (proj, pieces, pev: gq_pileup.hip proj_fill / piece_fill /
 // pev_fill).
 //
 // One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
 // (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
 // block B0.  Lanes 16g .. 16g + 15 (group g) own the 128-locus slice [B0 + 128g, B0 + 128g +
 // 128), whose projection words are one contiguous run in the slice-major pool (ProjRec), and
-// walk the reads that can overlap it in read order, one read per group per step:
+// walk the slice's pieces (the reads with words there, in read order; PieceRec), one piece per
+// group per step:
 //
-//     [s0, e0) = the read's columns inside the slice, off = the words of the earlier reads
-//     w   = buffer_load_b64(slice run, column in [s0, e0) ? 8 (off + column - s0) : out of range -> 0)
-//     off += e0 - s0
+//     rec = piece k's record (16 per stage, one per lane, shared in the group by ds_bpermute)
+//     d   = l16 - s0(rec)
+//     w   = buffer_load_b64(block's words, d < len(rec) ? 8 (base(rec) + d) : out of range -> 0)
 //     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
 //     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
 //
@@ -22,22 +23,16 @@
 // N-skips) — comes from the tile's pev entries, one lane per entry, into two LDS words per
 // locus.  Then each lane makes the GermlineThreshold decision (GermlineThresholdCaller.scala:
 // 90-179) for its eight loci; variant candidates, Ref/NoCall records and complex items leave
-// as in germline_decide.  Tiles holding a read the projection cannot take, or more than 255
-// reads over one sub-span, or a read window of >= 65535 reads, go to germline_walk.
+// as in germline_decide.  Blocks a read the projection cannot take overlaps (pbad), or with
+// more than 255 pieces in one slice, go to germline_walk.
 #pragma once
 
 #include "gq_kernels.h"
 
 // (included inside gq_pileup.hip's anonymous namespace, after gq_germline_cols.h)
 
-#ifndef GQ_PROJ_U
-#define GQ_PROJ_U 5
-#endif
 #ifndef GQ_PROJ_WPE
 #define GQ_PROJ_WPE 5  // waves per SIMD the register budget must allow
-#endif
-#ifndef GQ_PROJ_NBUF
-#define GQ_PROJ_NBUF 3  // load batches in registers: NBUF - 1 in flight while one is counted
 #endif
 #ifndef GQ_PROJ_WAVES
 #define GQ_PROJ_WAVES 4
@@ -46,10 +41,8 @@ struct ProjCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = GQ_PROJ_WAVES;  // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kU = GQ_PROJ_U;  // reads per group per batch (all loads issued before use)
-  static constexpr int kMaxRows = 255;  // reads per group (byte counters); deeper tiles: walker
-  static constexpr int kRecCap = 256;   // reads per tile window (LDS records); more: walker
-  static constexpr int kRecBuf = kRecCap + 1;  // + one padding record
+  static constexpr int kU = 4;  // pieces per group per batch (all loads issued before use); 4 batches per stage
+  static constexpr int kMaxRows = 255;  // pieces per slice (byte counters); deeper blocks: walker
   static constexpr int kEnt = 6;  // sparse entries per lane loaded with the records (the rest: a loop)
 };
 
@@ -64,8 +57,9 @@ __device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n
 }
 
 __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_PROJ_WPE))) void germline_proj(
-    const Tile *__restrict__ tiles, int64_t n_tiles, const ProjRec *__restrict__ prec,
-    const int32_t *__restrict__ pmax_end, const uint8_t *__restrict__ proj, const int64_t *__restrict__ qoff,
+    const Tile *__restrict__ tiles, int64_t n_tiles, const uint32_t *__restrict__ pcs,
+    const int64_t *__restrict__ pbase, const uint8_t *__restrict__ pbad, const uint8_t *__restrict__ proj,
+    const int64_t *__restrict__ qoff,
     const int64_t *__restrict__ sbase, const uint2 *__restrict__ pev,
     const int64_t *__restrict__ pev_off, int n_samples, int threshold, int emit_ref, int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
@@ -76,12 +70,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   constexpr int T = C::kT, U = C::kU;
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // event read bases: A C T G bytes
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
-  __shared__ __attribute__((aligned(16))) uint32_t recw[C::kWaves][C::kRecBuf];  // the tile's read records
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave];
-  uint32_t *rec = recw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
@@ -101,44 +93,24 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
   auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
-  const uint2 *prec2 = reinterpret_cast<const uint2 *>(prec);
-  const int32_t g16 = 16 * g;
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const Tile tl = tiles[i];
     const int32_t L0 = tl.L0, L1 = tl.L1;
     const int64_t rb = tl.rb, re = tl.re;
-    const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
-    const int32_t myc = C0 + lane;
-    // ---- the read range of each group: reads [rb + lo_g, rb + hi_g) can overlap slice g
-    //      (pmax_end > its first locus, start < its end).  The window (every read with words
-    //      in the block: plan_tiles starts it at B0) goes to LDS as {col0 - C0 (16 bits) |
-    //      span << 16}.  A read the projection cannot take, or a window of more than kRecCap
-    //      reads, sends the tile to the walker.  The window's records, the slices' word
-    //      offsets and the first kEnt sparse entries per lane are loaded together.
-    const int64_t nwin = re - rb;
-    if (nwin > C::kRecCap) {
-      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
-      continue;
-    }
-    if (nwin <= 0) continue;  // no reads: nothing visited
-    const int nrd = (int)nwin;
-    const int64_t qs = qoff[tl.contig] + (B0 >> 7);  // the block's first slice
+    const int32_t B0 = L0 & ~(T - 1);
+    if (re <= rb) continue;  // no reads: nothing visited
+    // ---- the block's slices (one per group): their piece ranges and pbad flags, the first
+    //      kEnt sparse entries per lane of the window's reads, and the first three 16-piece
+    //      stages of each group's piece records, loaded together.  A pbad slice (a read the
+    //      projection cannot take) or more than kMaxRows pieces in a slice: the walker.
+    const int64_t qs = qoff[tl.contig] + (B0 >> 7);  // the block's first slice (a multiple of 4)
     const int64_t sb0 = sbase[qs], sb4 = sbase[qs + 4];
-    const uint32_t gb = (uint32_t)(sbase[qs + g] - sb0);  // this group's slice run, in words
+    const int64_t pbg = pbase[qs + g];
+    const int32_t ng = (int32_t)(pbase[qs + g + 1] - pbg);
+    const uint32_t badg = pbad[qs + g];
     const int64_t e0 = pev_off[rb], e1 = pev_off[re];
-    constexpr int NQ = C::kRecCap / 64, NE = C::kEnt;
-    int32_t pe[NQ];
-    uint2 pp[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      pe[q] = 0x7FFFFFFF;
-      pp[q] = make_uint2(0x7FFFFFFFu, 0u);
-      if (64 * q + lane < nrd) {
-        pe[q] = pmax_end[rb + 64 * q + lane];
-        pp[q] = prec2[rb + 64 * q + lane];
-      }
-    }
+    constexpr int NE = C::kEnt;
     uint2 ent[NE];
 #pragma unroll
     for (int j = 0; j < NE; ++j) {
@@ -146,41 +118,26 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       ent[j] = make_uint2(0x80000000u, kPevNone);
       if (!(dbg & 2) && k < e1) ent[j] = pev[k];
     }
-    bool bad = false;
-    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      if (64 * q >= nrd) break;
-      const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
-      if (64 * q + lane < nrd) rec[64 * q + lane] = (uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16);
-      bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
-      lo0 += (int)__popcll(__ballot(pe[q] <= B0));
-      lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
-      lo2 += (int)__popcll(__ballot(pe[q] <= B0 + 256));
-      lo3 += (int)__popcll(__ballot(pe[q] <= B0 + 384));
-      hi0 += (int)__popcll(__ballot(c0 < C0 + 16));
-      hi1 += (int)__popcll(__ballot(c0 < C0 + 32));
-      hi2 += (int)__popcll(__ballot(c0 < C0 + 48));
-      hi3 += (int)__popcll(__ballot(c0 < C0 + 64));
-    }
-    const int nmax = max(max(hi0 - lo0, hi1 - lo1), max(hi2 - lo2, hi3 - lo3));
-    if (bad || nmax > C::kMaxRows) {
+    const int32_t l16 = lane & 15;
+    auto stage = [&](int32_t k) -> uint32_t {  // piece record of row k + l16 of this group (0: none)
+      return k + l16 < ng ? pcs[pbg + k + l16] : 0u;
+    };
+    uint32_t P0 = stage(0), P1 = stage(16), P2 = stage(32);
+    const int32_t nmax = max(max(__builtin_amdgcn_readlane(ng, 0), __builtin_amdgcn_readlane(ng, 16)),
+                             max(__builtin_amdgcn_readlane(ng, 32), __builtin_amdgcn_readlane(ng, 48)));
+    if (__ballot(badg != 0) != 0 || nmax > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
     }
     const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
-    const int hi_me = g == 0 ? hi0 : g == 1 ? hi1 : g == 2 ? hi2 : hi3;
     // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]).
-    //      Group g reads records lo_g, lo_g + 1, ..., clamped to hi_g: a read starting at or
-    //      after the sub-span's end (start-sorted), which covers none of its columns, or the
-    //      padding record (span 0) at the window's end.  Two batches of loads stay in flight
-    //      while a third is counted; the sparse entries are applied while the first two land.
-    if (lane == 0) rec[nrd] = 0u;
+    //      Row k of group g is piece k of its slice: record from the 16-piece stage in a
+    //      register (ds_bpermute within the group), word (rec >> 9) + l16 - s0 when this
+    //      lane's column is inside the piece, else an out-of-range offset (the load returns
+    //      0).  Three batches of loads stay in flight while a fourth is counted.
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(proj + 8 * sb0), (short)0, (int)(8 * (sb4 - sb0)), 0x00020000);
-    uint32_t off = gb;  // this group's slice run + the words of its earlier reads there
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -194,19 +151,16 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       }
       nn = 0;
     };
-    auto issue = [&](int k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
+    const int32_t bp = (lane & 48) << 2;  // ds_bpermute address of the group's lane 0
+    auto issue = [&](uint32_t P, int u0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
       uint32_t rv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];  // all LDS reads first
+      for (int u = 0; u < U; ++u) rv[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(bp + 4 * (u0 + u), (int)P);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t rr = rv[u];
-        const int32_t c0 = (int32_t)(int16_t)(rr & 0xFFFFu);  // the read's columns, tile-relative
-        const int32_t s0 = max(c0, g16), se = min(c0 + (int32_t)(rr >> 16), g16 + 16);
-        const uint32_t sl = (uint32_t)max(se - s0, 0);  // its words in this group's slice
-        const uint32_t d = (uint32_t)(lane - s0);
-        const uint32_t voff = d < sl && !(dbg & 1) ? 8u * (off + d) : 0x80000000u;
-        off += sl;
+        const uint32_t d = (uint32_t)l16 - (rr & 15u);
+        const uint32_t voff = d < ((rr >> 4) & 31u) && !(dbg & 1) ? ((rr >> 9) + d) << 3 : 0x80000000u;
         const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
         w0[u] = w[0];
         w1[u] = w[1];
@@ -223,15 +177,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       }
       nn += U;
     };
-    uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U];
-#if GQ_PROJ_NBUF == 4
-    uint32_t d0[U], d1[U];
-#endif
-    issue(0, a0, a1);
-    issue(U, b0, b1);
-#if GQ_PROJ_NBUF == 4
-    issue(2 * U, c0, c1);
-#endif
+    uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U], d0[U], d1[U];
+    issue(P0, 0, a0, a1);
+    issue(P0, U, b0, b1);
+    issue(P0, 2 * U, c0, c1);
     // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
     auto apply = [&](uint2 p) {
       const int32_t l = (int32_t)p.x;
@@ -258,29 +207,22 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         if (k < e1) apply(pev[k]);
       }
     const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-#if GQ_PROJ_NBUF == 4
-    for (int k0 = 0;; k0 += 4 * U) {  // rows past the group's are clamped (zero words)
-      issue(k0 + 3 * U, d0, d1);
+    static_assert(4 * U == 16, "a loop iteration is one 16-piece stage");
+    for (int32_t k0 = 0;; k0 += 16) {  // P0: rows k0 .. k0 + 15, P1: the next 16, P2: the 16 after
+      issue(P0, 3 * U, d0, d1);
+      const bool more = k0 + 16 < nmax;  // wave-uniform
       count(a0, a1);
-      issue(k0 + 4 * U, a0, a1);
+      if (more) issue(P1, 0, a0, a1);
       count(b0, b1);
-      issue(k0 + 5 * U, b0, b1);
+      if (more) issue(P1, U, b0, b1);
       count(c0, c1);
-      issue(k0 + 6 * U, c0, c1);
+      if (more) issue(P1, 2 * U, c0, c1);
       count(d0, d1);
-      if (k0 + 4 * U >= nmax) break;
+      if (!more) break;
+      P0 = P1;
+      P1 = P2;
+      P2 = stage(k0 + 48);
     }
-#else
-    for (int k0 = 0;; k0 += 3 * U) {  // rows past the group's are clamped (zero words)
-      issue(k0 + 2 * U, c0, c1);
-      count(a0, a1);
-      issue(k0 + 3 * U, a0, a1);
-      count(b0, b1);
-      issue(k0 + 4 * U, b0, b1);
-      count(c0, c1);
-      if (k0 + 3 * U >= nmax) break;
-    }
-#endif
     fold();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -59,6 +59,10 @@ struct DevReads {
   const int64_t *sbase;         // qoff[n_contigs] + 1: each slice's first word in proj
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
   const int64_t *pev_off;       // n_reads + 1 offsets into pev
+  // derived at upload for germline_proj: the pieces of each slice (see PieceRec)
+  const uint32_t *pcs;          // per slice, in read order: one PieceRec word per read with words there
+  const int64_t *pbase;         // qoff[n_contigs] + 1: each slice's first piece
+  const uint8_t *pbad;          // per slice: 1 if a read the projection cannot take overlaps it
 };
 
 // Per-read record of the projection kernels (8 bytes): the read spans the 8-locus columns
@@ -84,6 +88,15 @@ constexpr int32_t kProjNone = (int32_t)0x80000000;
 //     on a deleted base);
 //   y bit 31 set: loci [x, x + (y & 0x7FFFFFFF)) hold complex elements (insertion / deletion
 //     anchors, mid-deletions, clipped N-skips): the exact kernel decides them.
+// A PIECE is one read's run of words inside one slice.  Its record (PieceRec, one u32) lets
+// the 16 lanes owning the slice find their word without any per-read arithmetic beyond a
+// subtract and a compare:
+//   bits 0-3  s0: the piece's first column inside the slice (0-15)
+//   bits 4-8  len: its columns (1-16)
+//   bits 9-31 the word of its first column, counted from the first word of the slice's
+//             512-locus block (sbase[slot & ~3]); a block of more than 2^23 words is pbad
+// Lane l16 of the slice's group reads word (rec >> 9) + (l16 - s0) when 0 <= l16 - s0 < len.
+constexpr int kPieceBaseBits = 23;
 constexpr uint32_t kPevComplex = 0x80000000u;
 constexpr uint32_t kPevNone = 7u << 4;  // a padding entry (no effect)
 

@@ -276,11 +276,13 @@ __global__ void prec_fill(DevReads R, ProjRec *__restrict__ prec) {
 }
 
 // Words per slice (thread per read: each slice it meets gets its piece), for the slice offsets.
-__global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ scnt) {
+// Also the pieces per slice (pcnt), and pbad = 1 on every slice a read the projection cannot
+// take overlaps (germline_proj hands such blocks to the walker).
+__global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ scnt,
+                            unsigned long long *__restrict__ pcnt, uint8_t *__restrict__ pbad) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
   const ProjRec p = prec[r];
-  if (p.col1 == kProjNone || p.col1 <= p.col0) return;
   int lo = 0, hi = R.n_contigs - 1;  // contig of r: last c with contig_read_begin[c] <= r
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
@@ -288,9 +290,77 @@ __global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsign
     else hi = m - 1;
   }
   const int64_t q0 = R.qoff[lo];
+  if (p.col1 == kProjNone) {
+    const int32_t s = R.start[r], e = R.end[r];
+    if (e > s && s >= 0)
+      for (int32_t q = s >> 7; q <= (e - 1) >> 7; ++q) pbad[q0 + q] = 1;
+    return;
+  }
+  if (p.col1 <= p.col0) return;
   for (int32_t q = p.col0 >> 4; q <= (p.col1 - 1) >> 4; ++q) {
     const int32_t a = max(p.col0, 16 * q), b = min(p.col1, 16 * q + 16);
     atomicAdd(&scnt[q0 + q], (unsigned long long)(b - a));
+    atomicAdd(&pcnt[q0 + q], 1ull);
+  }
+}
+
+// The piece records (PieceRec), one wave per slice: the slice's reads in read order, each with
+// words there gets {s0, len, its first word from the block's first word}.
+__global__ __launch_bounds__(256) void piece_fill(DevReads R, int64_t n_slices, uint32_t *__restrict__ pcs,
+                                                  uint8_t *__restrict__ pbad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = w0; slot < n_slices; slot += nw) {
+    int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
+    while (lo < hi) {
+      const int m = (lo + hi + 1) >> 1;
+      if (R.qoff[m] <= slot) lo = m;
+      else hi = m - 1;
+    }
+    const int32_t q = (int32_t)(slot - R.qoff[lo]);
+    const int32_t L = 128 * q, qc0 = 16 * q, qc1 = qc0 + 16;
+    const int64_t cb = R.contig_read_begin[lo], ce = R.contig_read_begin[lo + 1];
+    int64_t a0 = cb, a1 = ce;
+    while (a0 < a1) {  // first read with pmax_end > L
+      const int64_t m = (a0 + a1) >> 1;
+      if (R.pmax_end[m] > L) a1 = m;
+      else a0 = m + 1;
+    }
+    const int64_t ra = a0;
+    a1 = ce;
+    while (a0 < a1) {  // first read with start >= L + 128
+      const int64_t m = (a0 + a1) >> 1;
+      if (R.start[m] >= L + 128) a1 = m;
+      else a0 = m + 1;
+    }
+    const int64_t rz = a0;
+    const int64_t wb = R.sbase[slot] - R.sbase[slot & ~(int64_t)3];  // the slice run in its block
+    const int64_t pb = R.pbase[slot];
+    int64_t run = 0, np = 0;
+    bool over = false;
+    for (int64_t r0 = ra; r0 < rz; r0 += 64) {
+      const int64_t r = r0 + lane;
+      int32_t s0 = 0, sl = 0;
+      if (r < rz) {
+        const ProjRec p = R.prec[r];
+        if (p.col1 != kProjNone) {
+          s0 = max(p.col0, qc0);
+          sl = max(min(p.col1, qc1) - s0, 0);
+        }
+      }
+      const uint32_t ex = wave_incl_scan((uint32_t)sl) - (uint32_t)sl;
+      const uint64_t has = __ballot(sl > 0);
+      const int64_t k = np + (int64_t)__popcll(has & ((1ull << lane) - 1ull));
+      const int64_t w = wb + run + (int64_t)ex;
+      if (sl > 0) {
+        over = over || w >= (1ll << kPieceBaseBits);
+        pcs[pb + k] = ((uint32_t)w << 9) | ((uint32_t)sl << 4) | (uint32_t)(s0 - qc0);
+      }
+      run += (int64_t)__builtin_amdgcn_readlane((int)(ex + (uint32_t)sl), 63);
+      np += (int64_t)__popcll(has);
+    }
+    if (__ballot(over) && lane == 0) pbad[slot] = 1;
   }
 }
 
@@ -1386,9 +1456,17 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     HIP_TRY(hipMemsetAsync(sc, 0, sizeof(int64_t) * (size_t)(n_sl + 1), c->stream));
     HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
     d->owned.push_back(sb);
+    void *pcn = nullptr, *pbs = nullptr, *pbd = nullptr, *pcs = nullptr;
+    HIP_TRY(hipMalloc(&pcn, sizeof(int64_t) * (size_t)(n_sl + 1)));
+    HIP_TRY(hipMemsetAsync(pcn, 0, sizeof(int64_t) * (size_t)(n_sl + 1), c->stream));
+    HIP_TRY(hipMalloc(&pbs, sizeof(int64_t) * (size_t)(n_sl + 1)));
+    d->owned.push_back(pbs);
+    HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
+    d->owned.push_back(pbd);
+    HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
     if (n > 0) {
       hipLaunchKernelGGL(slice_count, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const ProjRec *)pr, (unsigned long long *)sc);
+                         (const ProjRec *)pr, (unsigned long long *)sc, (unsigned long long *)pcn, (uint8_t *)pbd);
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
@@ -1401,15 +1479,30 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
     HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)sc, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)pcn, (int64_t *)pbs, (int)(n_sl + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
-    int64_t tot[2] = {0, 0};
+    int64_t tot[3] = {0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tot[2], (int64_t *)pbs + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(tmp);
     (void)hipFree(sc);
     (void)hipFree(ne);
+    (void)hipFree(pcn);
     d->d.sbase = (const int64_t *)sb;
+    d->d.pbase = (const int64_t *)pbs;
+    d->d.pbad = (const uint8_t *)pbd;
+    HIP_TRY(hipMalloc(&pcs, sizeof(uint32_t) * (size_t)(tot[2] + 64)));
+    d->owned.push_back(pcs);
+    d->d.pcs = (const uint32_t *)pcs;
+    d->n_pieces = tot[2];
+    if (n_sl > 0) {
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(piece_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint32_t *)pcs,
+                         (uint8_t *)pbd);
+      HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipMalloc(&pj, (size_t)(8 * tot[0] + 16)));
     d->owned.push_back(pj);
     HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
@@ -1602,6 +1695,7 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->seq_bytes = d->seq_bytes;
   out->proj_bytes = d->proj_bytes;
   out->pev_count = d->pev_count;
+  out->n_pieces = d->n_pieces;
   out->proj_reads = d->proj_reads;
   return GQ_OK;
 }
@@ -1727,7 +1821,7 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   if (germline_use_proj()) {
     hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, tiles, R.prec, R.pmax_end, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
+                       (const Tile *)c->tiles.p, tiles, R.pcs, R.pbase, R.pbad, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
                        p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   } else {
     hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,

@@ -98,7 +98,7 @@ class gq_timings(C.Structure):
 
 
 class gq_reads_info(C.Structure):
-    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads")]
+    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_pieces")]
 
 
 class gq_somatic_params(C.Structure):

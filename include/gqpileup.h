@@ -184,6 +184,7 @@ void gq_reads_free(gq_dev_reads *r);
 /* projection pool and its sparse entries): for measurement and capacity planning.             */
 typedef struct gq_reads_info {
   int64_t n_reads, seq_bytes, proj_bytes, pev_count, proj_reads;  /* proj_reads: reads the projection takes */
+  int64_t n_pieces;  /* germline_proj piece records (4 bytes each) */
 } gq_reads_info;
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
