@@ -37,13 +37,16 @@
 #ifndef GQ_PROJ_WAVES
 #define GQ_PROJ_WAVES 4
 #endif
+#ifndef GQ_PROJ_ENT
+#define GQ_PROJ_ENT 6
+#endif
 struct ProjCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = GQ_PROJ_WAVES;  // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
   static constexpr int kU = 4;  // pieces per group per batch (all loads issued before use); 4 batches per stage
   static constexpr int kMaxRows = 255;  // pieces per slice (byte counters); deeper blocks: walker
-  static constexpr int kEnt = 6;  // sparse entries per lane loaded with the records (the rest: a loop)
+  static constexpr int kEnt = GQ_PROJ_ENT;  // sparse entries per lane loaded with the records (the rest: a loop)
 };
 
 // Wave-aggregated reservation of n slots per lane on an LDS counter (every lane active).

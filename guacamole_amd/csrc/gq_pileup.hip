@@ -608,7 +608,10 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // ------------------------------------------------------------------------------------------
 
 // four waves per SIMD (128 VGPRs; a few spills) beat three without spills: the kernel is latency-bound
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void germline_complex(const Tile *__restrict__ tiles,
+#ifndef GQ_CPLX_WPE
+#define GQ_CPLX_WPE 4  // waves per SIMD the register budget must allow
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_WPE))) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
                                                            int threshold, int emit_ref, int emit_no_call,
                                                            CallRec *__restrict__ recs, OutGeom og,
@@ -1543,6 +1546,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   return GQ_OK;
 }
 
+extern "C++" {
 namespace {
 // H2D of large pageable host arrays at PCIe rate: a copy from pageable memory goes through the
 // runtime's own small bounce buffer (≈ 3 GB/s measured for the 4 GB bench shard); here the host
@@ -1578,29 +1582,32 @@ struct H2DStager {
     }
     return hipSuccess;
   }
-  void fill(void *dst, const void *src, size_t bytes) const {
-    const unsigned t = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, bytes >> 22));  // >= 4 MiB / thread
+  // out[0, k) <- bytes [o, o + k) of the logical source, split over the threads
+  template <class F>
+  void fill(uint8_t *out, size_t o, size_t k, const F &src_range) const {
+    const unsigned t = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, k >> 22));  // >= 4 MiB / thread
     if (t <= 1) {
-      memcpy(dst, src, bytes);
+      src_range(out, o, k);
       return;
     }
     std::vector<std::thread> th;
-    const size_t per = (bytes + t - 1) / t;
+    const size_t per = (k + t - 1) / t;
     for (unsigned i = 0; i < t; ++i) {
-      const size_t o = (size_t)i * per;
-      if (o >= bytes) break;
-      th.emplace_back([=] { memcpy((char *)dst + o, (const char *)src + o, std::min(per, bytes - o)); });
+      const size_t a = (size_t)i * per;
+      if (a >= k) break;
+      th.emplace_back([&, a] { src_range(out + a, o + a, std::min(per, k - a)); });
     }
     for (auto &x : th) x.join();
   }
-  hipError_t copy(void *dst, const void *src, size_t bytes) {
+  template <class F>
+  hipError_t copy_from(void *dst, size_t bytes, const F &src_range) {
     for (size_t o = 0; o < bytes; o += kChunk) {
       const size_t k = std::min(kChunk, bytes - o);
       if (used[slot]) {
         hipError_t e = hipEventSynchronize(done[slot]);
         if (e != hipSuccess) return e;
       }
-      fill(buf[slot], (const char *)src + o, k);
+      fill((uint8_t *)buf[slot], o, k, src_range);
       hipError_t e = hipMemcpyAsync((char *)dst + o, buf[slot], k, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) e = hipEventRecord(done[slot], stream);
       if (e != hipSuccess) return e;
@@ -1609,8 +1616,12 @@ struct H2DStager {
     }
     return hipSuccess;
   }
+  hipError_t copy(void *dst, const void *src, size_t bytes) {
+    return copy_from(dst, bytes, [src](uint8_t *out, size_t o, size_t k) { memcpy(out, (const uint8_t *)src + o, k); });
+  }
 };
 }  // namespace
+}  // extern "C++"
 
 gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   if (!c || !out) return set_err(GQ_E_ARG, "gq_reads_upload: null argument");
@@ -1628,28 +1639,41 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
       return set_err(GQ_E_HIP, "upload: pinned staging: %s", hipGetErrorString(e));
     }
   }
-  auto up = [&](const void *src, size_t bytes, void **dst, size_t pad) -> hipError_t {
+  // src_range(out, o, k): bytes [o, o + k) of the array in its device layout
+  auto up_from = [&](size_t bytes, void **dst, size_t pad, const auto &src_range) -> hipError_t {
     *dst = nullptr;
     hipError_t e = hipMalloc(dst, std::max(bytes + pad, (size_t)16));
     if (e != hipSuccess) return e;
     d->owned.push_back(*dst);
-    if (bytes >= (size_t(1) << 20))
-      e = stager.copy(*dst, src, bytes);
-    else if (bytes)
-      e = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    if (bytes) e = stager.copy_from(*dst, bytes, src_range);
+    if (e == hipSuccess && pad) e = hipMemsetAsync((char *)*dst + bytes, 0, pad, c->stream);
+    return e;
+  };
+  auto up = [&](const void *src, size_t bytes, void **dst, size_t pad) -> hipError_t {
+    if (bytes >= (size_t(1) << 20) || (!src && bytes))  // (a null source reads as zeros)
+      return up_from(bytes, dst, pad, [src](uint8_t *out, size_t o, size_t k) {
+        if (src) memcpy(out, (const uint8_t *)src + o, k);
+        else memset(out, 0, k);
+      });
+    *dst = nullptr;
+    hipError_t e = hipMalloc(dst, std::max(bytes + pad, (size_t)16));
+    if (e != hipSuccess) return e;
+    d->owned.push_back(*dst);
+    if (bytes) e = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess && pad) e = hipMemsetAsync((char *)*dst + bytes, 0, pad, c->stream);
     return e;
   };
   void *p;
-#define UP(field, count, T)                                                     \
+#define UP_CHECK(field, T, expr)                                                \
   do {                                                                          \
-    hipError_t _e = up(h->field, (size_t)(count) * sizeof(T), &p, pad_##field); \
+    hipError_t _e = (expr);                                                     \
     if (_e != hipSuccess) {                                                     \
       gq_reads_free(d);                                                         \
       return set_err(GQ_E_HIP, "upload %s: %s", #field, hipGetErrorString(_e)); \
     }                                                                           \
     d->d.field = (const T *)p;                                                  \
   } while (0)
+#define UP(field, count, T) UP_CHECK(field, T, up(h->field, (size_t)(count) * sizeof(T), &p, pad_##field))
   // the sequence pool gets a zeroed tail so 1 KiB LDS-DMA pieces and 16-byte chunk loads
   // past the last read stay inside the allocation (DevReads::seq_cap)
   enum : size_t { pad_contig_read_begin = 0, pad_start = 0, pad_end = 0, pad_pmax_end = 0, pad_mapq = 0, pad_flags = 0,
@@ -1658,32 +1682,41 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
                   pad_md_ev = 0 };
   // HBM layout: the sequence / quality pools in read order (each read's bytes after the
   // previous read's), so a tile's reads are one contiguous byte range for the LDS stage.
-  // A host pool in another order is re-laid out here (the caller's buffers are untouched).
+  // A host pool in another order is gathered into that order on its way through the pinned
+  // staging chunks (the caller's buffers are untouched; no host copy of the pool is made).
+  const gq_reads *h0 = h;
   gq_reads hh = *h;
   std::vector<int64_t> off2;
-  std::vector<uint8_t> seq2, qual2;
-  {
-    bool ordered = true;
-    for (int64_t r = 1; r < n && ordered; ++r) ordered = h->seq_off[r] >= h->seq_off[r - 1] + h->seq_len[r - 1];
-    if (!ordered) {
-      off2.resize((size_t)n);
-      int64_t o = 0;
-      for (int64_t r = 0; r < n; ++r) {
-        off2[(size_t)r] = o;
-        o += h->seq_len[r];
-      }
-      seq2.resize((size_t)std::max<int64_t>(o, 1));
-      qual2.resize((size_t)std::max<int64_t>(o, 1));
-      for (int64_t r = 0; r < n; ++r) {
-        memcpy(seq2.data() + off2[(size_t)r], h->seq + h->seq_off[r], (size_t)h->seq_len[r]);
-        if (h->qual) memcpy(qual2.data() + off2[(size_t)r], h->qual + h->seq_off[r], (size_t)h->seq_len[r]);
-      }
-      hh.seq_off = off2.data();
-      hh.seq = seq2.data();
-      hh.qual = h->qual ? qual2.data() : nullptr;
-      hh.seq_bytes = o;
+  bool ordered = true;
+  for (int64_t r = 1; r < n && ordered; ++r) ordered = h->seq_off[r] >= h->seq_off[r - 1] + h->seq_len[r - 1];
+  if (!ordered) {
+    off2.resize((size_t)n);
+    int64_t o = 0;
+    for (int64_t r = 0; r < n; ++r) {
+      off2[(size_t)r] = o;
+      o += h->seq_len[r];
     }
+    hh.seq_off = off2.data();
+    hh.seq_bytes = o;
   }
+  // pool bytes [o, o + k) in read order, from a caller pool at h0->seq_off
+  auto gather = [&](const uint8_t *src) {
+    return [&, src](uint8_t *out, size_t o, size_t k) {
+      if (!src) {
+        memset(out, 0, k);
+        return;
+      }
+      int64_t r = (int64_t)(std::upper_bound(off2.begin(), off2.end(), (int64_t)o) - off2.begin()) - 1;
+      size_t done = 0;
+      while (done < k) {
+        const size_t a = o + done - (size_t)off2[(size_t)r];
+        const size_t m = std::min((size_t)h0->seq_len[r] - a, k - done);
+        memcpy(out + done, src + h0->seq_off[r] + a, m);
+        done += m;
+        ++r;
+      }
+    };
+  };
   h = &hh;
   UP(contig_read_begin, h->n_contigs + 1, int64_t);
   UP(start, n, int32_t);
@@ -1699,11 +1732,17 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   UP(md_off, n, int64_t);
   UP(n_md, n, int32_t);
   UP(n_mismatch, n, uint16_t);
-  UP(seq, h->seq_bytes, uint8_t);
-  UP(qual, h->seq_bytes, uint8_t);
+  if (ordered) {
+    UP(seq, h->seq_bytes, uint8_t);
+    UP(qual, h->seq_bytes, uint8_t);
+  } else {
+    UP_CHECK(seq, uint8_t, up_from((size_t)h->seq_bytes, &p, pad_seq, gather(h0->seq)));
+    UP_CHECK(qual, uint8_t, up_from((size_t)h->seq_bytes, &p, pad_qual, gather(h0->qual)));
+  }
   UP(cigar, h->cigar_len, uint32_t);
   UP(md_ev, h->md_len, uint32_t);
 #undef UP
+#undef UP_CHECK
   d->d.n_reads = n;
   d->d.seq_bytes = h->seq_bytes;
   d->d.seq_cap = h->seq_bytes + kSeqPad;
