@@ -32,7 +32,7 @@
 // (included inside gq_pileup.hip's anonymous namespace, after gq_germline_cols.h)
 
 #ifndef GQ_PROJ_WPE
-#define GQ_PROJ_WPE 5  // waves per SIMD the register budget must allow
+#define GQ_PROJ_WPE 4  // waves per SIMD the register budget must allow (5: 72 B/lane of spills, 4 % slower)
 #endif
 #ifndef GQ_PROJ_WAVES
 #define GQ_PROJ_WAVES 4

@@ -609,7 +609,7 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 
 // four waves per SIMD (128 VGPRs; a few spills) beat three without spills: the kernel is latency-bound
 #ifndef GQ_CPLX_WPE
-#define GQ_CPLX_WPE 4  // waves per SIMD the register budget must allow
+#define GQ_CPLX_WPE 3  // waves per SIMD the register budget must allow (4: 120 B/lane of spills)
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_WPE))) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
