@@ -115,6 +115,8 @@ __device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t p
   const int32_t s = R.start[r];
   const int64_t cig_off = R.cigar_off[r];
   const int32_t ncig = R.n_cigar[r];
+  const int32_t slen = R.seq_len[r];  // loaded with the other scalars: the base load below
+  const int64_t so = R.seq_off[r];    // then waits for the CIGAR walk only
   int ci = 0;
   int32_t ci_locus = s, within = 0, rp = 0;
   for (;;) {
@@ -146,7 +148,6 @@ __device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t p
   const bool has_next = ci + 1 < ncig;
   const uint32_t cn = has_next ? R.cigar[cig_off + ci + 1] : 0u;
   const int nextop = fin ? (has_next ? (int)(cn & 15u) : -1) : op;
-  const int32_t slen = R.seq_len[r];
   d.read = r;
   d.rb = refbase;
   d.pad = 0;
@@ -211,7 +212,7 @@ __device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t p
       return false;
     }
     d.kind = K_SNV;
-    d.base = R.seq[R.seq_off[r] + rp];
+    d.base = R.seq[so + rp];
     d.aux = 0;
     d.rp = rp;
   } else if (op == OP_S || op == OP_N || op == OP_H) {
@@ -228,9 +229,15 @@ __device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t p
 
 // MD-derived reference base of read r at pos (MappedRead.getReferenceBaseAtLocus) or -1 on error.
 __device__ __forceinline__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos) {
+  // the read's scalars are loaded together up front, and the read base at pos is loaded beside
+  // the MD search: one latency round each instead of a chain
   const int32_t s = R.start[r];
   const int64_t cig_off = R.cigar_off[r];
   const int32_t ncig = R.n_cigar[r];
+  const int32_t nmd = R.n_md[r];
+  const int64_t mdo = R.md_off[r];
+  const int64_t so = R.seq_off[r];
+  const int32_t sl = R.seq_len[r];
   int32_t ref = s, rp = 0;
   for (int k = 0; k < ncig; ++k) {
     const uint32_t c = R.cigar[cig_off + k];
@@ -238,14 +245,15 @@ __device__ __forceinline__ int md_ref_at(const DevReads &R, int64_t r, int32_t p
     const int32_t len = (int32_t)(c >> 4);
     if (consumes_ref(op)) {
       if (pos < ref + len) {
-        if (R.n_md[r] < 0) return -4;
-        const int v = md_find(R.md_ev + R.md_off[r], R.n_md[r], pos - s);
+        if (nmd < 0) return -4;
+        const int32_t q = rp + (pos - ref);
+        const bool seq_elem = op != OP_D && op != OP_N && q < sl;
+        const int b = seq_elem ? (int)R.seq[so + q] : -1;
+        const int v = md_find(R.md_ev + mdo, nmd, pos - s);
         if (op == OP_D) return v < 0 ? -3 : v;
         if (op == OP_N) return 'N';
         if (v >= 0) return v;
-        const int32_t q = rp + (pos - ref);
-        if (q >= R.seq_len[r]) return -1;
-        return R.seq[R.seq_off[r] + q];
+        return b;  // -1 past the read's bases
       }
       ref += len;
     }

@@ -137,6 +137,50 @@ __device__ __forceinline__ int64_t wave_first_true(int64_t lo, int64_t hi, P &&p
   return b ? lo + (__ffsll((long long)b) - 1) : hi;
 }
 
+// Two wave_first_true searches over the same [lo, hi) in lockstep: each round issues both
+// searches' probes before either ballot is read, so the two dependent-load chains overlap.
+template <class P1, class P2>
+__device__ __forceinline__ void wave_first_true2(int64_t lo, int64_t hi, P1 &&pred1, P2 &&pred2, int64_t &out1,
+                                                 int64_t &out2) {
+  const int lane = threadIdx.x & 63;
+  int64_t lo1 = lo, hi1 = hi, lo2 = lo, hi2 = hi;
+  bool done1 = false, done2 = false;
+  // one round of one search: narrows [l, h) or finishes it (wave-uniform)
+  auto round = [&](int64_t &l, int64_t &h, bool &done, int64_t &out, bool hit) {
+    if (done) return;
+    if (h - l > 64) {
+      const int64_t step = (h - l + 63) / 64;
+      const unsigned long long b = __ballot(hit);
+      if (!b) {
+        l = l + 63 * step + 1;
+        return;
+      }
+      const int f = __ffsll((long long)b) - 1;
+      if (f == 0) {
+        out = l;
+        done = true;
+        return;
+      }
+      const int64_t nh = l + (int64_t)f * step;
+      l = l + (int64_t)(f - 1) * step + 1;
+      h = nh < h ? nh : h;
+    } else {
+      const unsigned long long b = __ballot(hit);
+      out = b ? l + (__ffsll((long long)b) - 1) : h;
+      done = true;
+    }
+  };
+  while (!(done1 && done2)) {
+    // this round's probe of each unfinished search (both loads in flight together)
+    const int64_t s1 = hi1 - lo1 > 64 ? (hi1 - lo1 + 63) / 64 : 1, s2 = hi2 - lo2 > 64 ? (hi2 - lo2 + 63) / 64 : 1;
+    const int64_t p1 = lo1 + (int64_t)lane * s1, p2 = lo2 + (int64_t)lane * s2;
+    const bool h1 = !done1 && (p1 >= hi1 || pred1(p1));
+    const bool h2 = !done2 && (p2 >= hi2 || pred2(p2));
+    round(lo1, hi1, done1, out1, h1);
+    round(lo2, hi2, done2, out2, h2);
+  }
+}
+
 // part_slot for a wave-uniform k, the search spread over the lanes: two rounds of 64 probes
 // (two dependent loads instead of a twelve-step binary search).  Every lane must be active.
 __device__ __forceinline__ unsigned long long part_slot_wave(const unsigned long long *off, unsigned long long k,

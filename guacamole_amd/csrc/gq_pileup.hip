@@ -655,8 +655,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     int ncov = 0;
     bool compact = true;
     // the covering reads lie in [first pmax_end > pos, first start > pos)
-    const int64_t ra = wave_first_true(tl.rb, tl.re, [&](int64_t r) { return R.pmax_end[r] > pos; });
-    const int64_t rz = wave_first_true(ra, tl.re, [&](int64_t r) { return R.start[r] > pos; });
+    //  (both searched over the window together: every read before the first is also before the
+    //  second, as start < end <= pmax_end)
+    int64_t ra, rz;
+    wave_first_true2(tl.rb, tl.re, [&](int64_t r) { return R.pmax_end[r] > pos; },
+                     [&](int64_t r) { return R.start[r] > pos; }, ra, rz);
     for (int64_t r0 = ra; r0 < rz; r0 += 64) {
       const int64_t r = r0 + lane;
       const bool c = r < rz && R.start[r] <= pos && pos < R.end[r];

@@ -506,8 +506,10 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
   const int lane = threadIdx.x & 63;
   int64_t n = 0;
   // the covering reads lie in [first pmax_end > pos, first start > pos)
-  const int64_t ra = wave_first_true(rb, re, [&](int64_t r) { return R.pmax_end[r] > pos; });
-  const int64_t rz = wave_first_true(ra, re, [&](int64_t r) { return R.start[r] > pos; });
+  //  (searched together: every read before the first is also before the second)
+  int64_t ra, rz;
+  wave_first_true2(rb, re, [&](int64_t r) { return R.pmax_end[r] > pos; }, [&](int64_t r) { return R.start[r] > pos; },
+                   ra, rz);
   for (int64_t r0 = ra; r0 < rz; r0 += 64) {
     const int64_t r = r0 + lane;
     const bool c = r < rz && R.start[r] <= pos && pos < R.end[r] && (sel < 0 || (int)R.sample[r] == sel);
