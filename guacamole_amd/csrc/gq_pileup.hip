@@ -738,14 +738,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       const int64_t r = slot_read(k0 + lane, &act);
       AlleleDesc d;
       Key128 key{0, 0};
-      int smp = 0;
+      int smp = act ? (R.sample[r] & 7) : 0;  // issued with classify's loads
       if (act) {
         int errc = 0;
         if (!classify(R, r, pos, refbase, d, &errc)) {
           raise_error(&ctr->err, (int64_t *)&ctr->err_pos, errc, pos);
           act = false;
+          smp = 0;
         } else {
-          smp = R.sample[r] & 7;
           key = allele_key(R, d, pos, smp);
         }
       }

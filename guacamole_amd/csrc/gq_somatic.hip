@@ -331,9 +331,9 @@ __device__ __forceinline__ bool phred_rounding_edge(double p) {
 // Element quality (PileupElement.qualityScore, PileupElement.scala:166-171; quality bytes are
 // signed JVM bytes): SNV / Deletion = the base quality at the element's read position,
 // Insertion = min over its bases, MidDeletion / Clipped = the read's mapping quality.
-__device__ __forceinline__ int elem_quality(const DevReads &R, const AlleleDesc &d) {
-  const int64_t r = d.read;
-  const uint8_t *q = R.qual + R.seq_off[r];
+// (so, mapq: the read's seq_off and mapq, loaded by the caller beside its classify)
+__device__ __forceinline__ int elem_quality(const DevReads &R, const AlleleDesc &d, int64_t so, int mapq) {
+  const uint8_t *q = R.qual + so;
   switch (d.kind) {
     case K_SNV:
     case K_DEL: return (int)(int8_t)q[d.rp];
@@ -342,7 +342,7 @@ __device__ __forceinline__ int elem_quality(const DevReads &R, const AlleleDesc 
       for (int i = 0; i < d.aux; ++i) m = min(m, (int)(int8_t)q[d.rp + i]);
       return m;
     }
-    default: return (int)R.mapq[r];
+    default: return mapq;
   }
 }
 
@@ -624,6 +624,8 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
     AlleleDesc d;
     Key128 key{0, 0};
     bool pass = false;
+    const int mq = act ? (int)R.mapq[r] : 0;  // issued with classify's loads
+    const bool fwd = act && !(R.flags[r] & 1);
     if (act) {
       int errc = 0;
       if (!classify(R, r, pos, P.refbase, d, &errc)) {
@@ -631,14 +633,13 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
         act = false;
       } else {
         key = allele_key(R, d, pos, 0);
-        const int mq = (int)R.mapq[r];
         pass = min_mapq <= 0 || mq >= min_mapq;  // QualityAlignedReadsFilter (PileupElementsFilter.scala:25-36)
       }
     }
     const unsigned long long actb = __ballot(act), passb = __ballot(act && pass);
     P.depth_all += (uint32_t)__popcll(actb);
     P.depth_f += (uint32_t)__popcll(passb);
-    P.fwd_f += (uint32_t)__popcll(__ballot(act && pass && !(R.flags[r] & 1)));
+    P.fwd_f += (uint32_t)__popcll(__ballot(act && pass && fwd));
     unsigned long long pending = actb;
     while (pending) {
       const int leader = __ffsll((long long)pending) - 1;
@@ -755,12 +756,13 @@ __device__ __forceinline__ double fold_genotypes(const DevReads &R, const Cover 
     if (act) {
       AlleleDesc d;
       int errc = 0;
+      const int mq = (int)R.mapq[r];  // issued with classify's loads
+      const int64_t so = R.seq_off[r];
       if (classify(R, r, pos, refbase, d, &errc)) {
-        const int mq = (int)R.mapq[r];
         pass = min_mapq <= 0 || mq >= min_mapq;
         if (pass) {
           key = allele_key(R, d, pos, 0);
-          const int q = elem_quality(R, d);
+          const int q = elem_quality(R, d, so, mq);
           if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
           double pc = phred_success(q);
           if (include_alignment) pc = pc * phred_success(mq);  // probabilityCorrectIncludingAlignment
@@ -907,6 +909,9 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
     uint32_t packed = 0;
     if (cov) {
       const int mq = (int)R.mapq[r];
+      const int64_t so = R.seq_off[r];  // the read's scalars issued with classify's loads
+      const int32_t nmd = R.n_md[r];
+      const uint32_t nmm = (uint32_t)R.n_mismatch[r];
       if (min_mapq <= 0 || mq >= min_mapq) {
         AlleleDesc d;
         int errc = 0;
@@ -914,9 +919,8 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
           const Key128 k = allele_key(R, d, pos, 0);
           if (k.lo == target.lo && k.hi == target.hi) {
             hit = true;
-            if (R.n_md[r] < 0) raise_at(ctr, GQ_E_NO_MD, pos);
-            packed = (uint32_t)mq | ((uint32_t)(uint8_t)(int8_t)elem_quality(R, d) << 8) |
-                     ((uint32_t)R.n_mismatch[r] << 16);
+            if (nmd < 0) raise_at(ctr, GQ_E_NO_MD, pos);
+            packed = (uint32_t)mq | ((uint32_t)(uint8_t)(int8_t)elem_quality(R, d, so, mq) << 8) | (nmm << 16);
           }
         }
       }
