@@ -63,6 +63,10 @@ struct DevReads {
   const uint32_t *pcs;          // per slice, in read order: one PieceRec word per read with words there
   const int64_t *pbase;         // qoff[n_contigs] + 1: each slice's first piece
   const uint8_t *pbad;          // per slice: 1 if a read the projection cannot take overlaps it
+  // derived at upload for plan_tiles: per 512-locus block g (qoff[c] / 4 + block in contig c),
+  // the first read with pmax_end > the block's first locus and the first read starting at or
+  // after it (a block index of the reads, so aligned tiles need no search over the contig)
+  const int64_t *blk_rb, *blk_rs;
 };
 
 // Per-read record of the projection kernels (8 bytes): the read spans the 8-locus columns

@@ -57,6 +57,35 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // Tile planning
 // ------------------------------------------------------------------------------------------
+// The block index of the reads (DevReads::blk_rb / blk_rs): one thread per 512-locus block.
+__global__ void block_index(DevReads R, int64_t n_blocks, int64_t *__restrict__ blk_rb, int64_t *__restrict__ blk_rs) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_blocks) return;
+  int lo = 0, hi = R.n_contigs - 1;  // the contig: last c with qoff[c] / 4 <= g
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if ((R.qoff[m] >> 2) <= g) lo = m;
+    else hi = m - 1;
+  }
+  const int c = lo;
+  const int64_t blk = (g - (R.qoff[c] >> 2)) * 512;
+  const int64_t b = R.contig_read_begin[c], e = R.contig_read_begin[c + 1];
+  int64_t a0 = b, a1 = e;
+  while (a0 < a1) {
+    const int64_t m = (a0 + a1) >> 1;
+    if ((int64_t)R.pmax_end[m] > blk) a1 = m;
+    else a0 = m + 1;
+  }
+  blk_rb[g] = a0;
+  a1 = e;
+  while (a0 < a1) {
+    const int64_t m = (a0 + a1) >> 1;
+    if ((int64_t)R.start[m] >= blk) a1 = m;
+    else a0 = m + 1;
+  }
+  blk_rs[g] = a0;
+}
+
 __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *__restrict__ r_start,
                            const int64_t *__restrict__ r_end, const int64_t *__restrict__ r_ord,
                            const int64_t *__restrict__ r_tile0, int64_t n_ranges, int64_t n_tiles, int T,
@@ -82,18 +111,43 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   // slices, so that a read's place in a slice is the sum of the window's earlier pieces)
   const int64_t W0 = aligned ? blk : L0;
   int64_t a0 = b, a1 = e;
-  while (a0 < a1) {
-    int64_t m = (a0 + a1) >> 1;
-    if ((int64_t)R.pmax_end[m] > W0) a1 = m;
-    else a0 = m + 1;
+  // aligned tiles: the window from the upload-time block index (blocks past the contig's
+  // last read end hold no reads: [e, e))
+  const int64_t g0 = aligned && T == 512 && R.blk_rb ? (R.qoff[c] >> 2) + blk / 512 : -1, g1 = aligned ? (R.qoff[c + 1] >> 2) : -1;
+  if (g0 >= 0) {
+    if (g0 >= g1) {
+      a0 = a1 = e;
+    } else {
+      a0 = R.blk_rb[g0];
+      // re in [first start >= blk, first start >= blk + 512]
+      a1 = g0 + 1 < g1 ? R.blk_rs[g0 + 1] : e;
+      if (L1 < blk + (int64_t)T) {
+        int64_t s0 = max(a0, R.blk_rs[g0]);
+        while (s0 < a1) {
+          int64_t m = (s0 + a1) >> 1;
+          if ((int64_t)R.start[m] >= L1) a1 = m;
+          else s0 = m + 1;
+        }
+      }
+    }
+  } else {
+    while (a0 < a1) {
+      int64_t m = (a0 + a1) >> 1;
+      if ((int64_t)R.pmax_end[m] > W0) a1 = m;
+      else a0 = m + 1;
+    }
   }
   const int64_t rb = a0;
-  a0 = rb;
-  a1 = e;  // re: first read with start >= L1
-  while (a0 < a1) {
-    int64_t m = (a0 + a1) >> 1;
-    if ((int64_t)R.start[m] >= L1) a1 = m;
-    else a0 = m + 1;
+  if (g0 >= 0) {
+    a0 = a1;  // re
+  } else {
+    a0 = rb;
+    a1 = e;  // re: first read with start >= L1
+    while (a0 < a1) {
+      int64_t m = (a0 + a1) >> 1;
+      if ((int64_t)R.start[m] >= L1) a1 = m;
+      else a0 = m + 1;
+    }
   }
   Tile tl;
   tl.ordinal0 = r_ord[r] + (L0 - r_start[r]);
@@ -1453,6 +1507,20 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->owned.push_back(qo);
     HIP_TRY(hipMemcpyAsync(qo, qoff.data(), sizeof(int64_t) * ((size_t)nc + 1), hipMemcpyHostToDevice, c->stream));
     d->d.qoff = (const int64_t *)qo;
+    {  // the block index of the reads (plan_tiles' windows of aligned tiles)
+      const int64_t n_blk = qoff[(size_t)nc] / 4;
+      void *bi = nullptr;
+      HIP_TRY(hipMalloc(&bi, sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_blk, 1)));
+      d->owned.push_back(bi);
+      int64_t *brb = (int64_t *)bi, *brs = brb + std::max<int64_t>(n_blk, 1);
+      if (n_blk > 0) {
+        hipLaunchKernelGGL(block_index, dim3((unsigned)((n_blk + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                           n_blk, brb, brs);
+        HIP_TRY(hipGetLastError());
+      }
+      d->d.blk_rb = brb;
+      d->d.blk_rs = brs;
+    }
     HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
     d->owned.push_back(pr);
     const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
