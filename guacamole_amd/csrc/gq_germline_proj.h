@@ -107,7 +107,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     //      kEnt sparse entries per lane of the window's reads, and the first three 16-piece
     //      stages of each group's piece records, loaded together.  A pbad slice (a read the
     //      projection cannot take) or more than kMaxRows pieces in a slice: the walker.
-    const int64_t qs = qoff[tl.contig] + (B0 >> 7);  // the block's first slice (a multiple of 4)
+    const int64_t qs = tl.qs;  // the block's first slice (a multiple of 4; qoff[contig] + (B0 >> 7))
     const int64_t sb0 = sbase[qs], sb4 = sbase[qs + 4];
     const int64_t pbg = pbase[qs + g];
     const int32_t ng = (int32_t)(pbase[qs + g + 1] - pbg);

@@ -127,7 +127,10 @@ struct Tile {
   int64_t sb0;     // germline column kernel: 16-aligned pool offset of the tile's sequence bytes
   int32_t sbytes;  // bytes to stage from sb0 when the whole read window fits one LDS stage, else 0
   int32_t mcnt;    // auxiliary-list words (MD events, segments) to stage from mb0
-  int64_t mb0;     // first auxiliary word to stage (a multiple of 4)
+  union {
+    int64_t mb0;  // germline column kernel: first auxiliary word to stage (a multiple of 4)
+    int64_t qs;   // aligned (projection) tiles: the block's first slice, qoff[contig] + (block >> 7)
+  };
 };
 static_assert(sizeof(Tile) == 64, "Tile layout");
 

@@ -177,6 +177,9 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
       tl.mcnt = (int32_t)nm;
     }
   }
+  // (the projection kernels' aligned tiles are planned without staging: mb0 is free for qs, so
+  //  their setup skips a dependent qoff load)
+  if (aligned && stage_cap == 0 && R.qoff) tl.qs = R.qoff[c] + blk / 128;
   tiles[t] = tl;
 }
 

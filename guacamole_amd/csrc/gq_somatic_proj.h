@@ -195,7 +195,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     // the block's first slice: it exists only where tumor reads reach the block (a tile may
     // hold normal reads alone, past the tumor's last read)
     const bool tumor = nrd > 0;
-    const int64_t qs = tumor ? RT.qoff[tt.contig] + (B0 >> 7) : 0;
+    const int64_t qs = tumor ? tt.qs : 0;  // qoff[contig] + (B0 >> 7), from the plan
     const int64_t sb0 = tumor ? RT.sbase[qs] : 0, sb4 = tumor ? RT.sbase[qs + 4] : 0;
     const uint32_t gb = tumor ? (uint32_t)(RT.sbase[qs + g] - sb0) : 0u;  // this group's slice run, in words
     const int64_t e0 = RT.pev_off[rb], e1 = RT.pev_off[re];
