@@ -693,11 +693,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
   constexpr int kCover = 256;
   __shared__ int32_t cover_buf[kBlock / 64][kCover];
   int32_t *cover = cover_buf[threadIdx.x >> 6];
-  // the complex items' partition offsets in LDS (one coalesced round per workgroup): an item's
-  // slot is then an LDS search, not two dependent global rounds per item
-  __shared__ unsigned long long poff[kParts + 1];
-  for (int i = threadIdx.x; i <= kParts; i += blockDim.x) poff[i] = ctr->part_off[1][i];
-  __syncthreads();
   // dbg & 32: phase clocks per item (cover, reference base, elements, decision + records, items)
   uint64_t clk[5] = {0, 0, 0, 0, 0}, tk = 0;
   auto tick = [&](int k) {
@@ -711,7 +706,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     tick(-1);
     if (dbg & 32) clk[4] += 1;
     const int64_t it = amb_in ? amb_in[li].item : li;
-    const ComplexItem item = items[part_slot(poff, (unsigned long long)it, og, 1)];
+    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
     const int32_t pos = item.pos;
     int ncov = 0;
@@ -1271,14 +1266,9 @@ __global__ __launch_bounds__(kBlock) void bucket_count(const CallRec *__restrict
                                                         OutGeom og, int64_t n_all, uint64_t dead_key, int bshift,
                                                         uint64_t *__restrict__ keys, int32_t *__restrict__ slot,
                                                         int64_t *__restrict__ bkt, uint32_t *__restrict__ cnt) {
-  // the partition offsets in LDS (one coalesced round), so part_slot's search is an LDS walk
-  // instead of twelve dependent global loads per record
-  __shared__ unsigned long long so[kParts + 1];
-  for (int i = threadIdx.x; i <= kParts; i += blockDim.x) so[i] = ctr->part_off[0][i];
-  __syncthreads();
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_all) return;
-  const unsigned long long src = part_slot(so, (unsigned long long)k, og, 0);
+  const unsigned long long src = part_slot(ctr->part_off[0], (unsigned long long)k, og, 0);
   const uint64_t key = recs[src].key;
   keys[k] = key;
   slot[k] = (int32_t)src;
@@ -2093,7 +2083,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       return st;
     }
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), 4096);
+#ifndef GQ_CPLX_BLOCKS
+#define GQ_CPLX_BLOCKS 4096
+#endif
+    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), GQ_CPLX_BLOCKS);
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 1, og);
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
