@@ -2096,7 +2096,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
       const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
-      hipLaunchKernelGGL(germline_expand, dim3(1024), dim3(kBlock), 0, c->stream, (CallRec *)c->recs.p, ctr, og,
+#ifndef GQ_EXPAND_BLOCKS
+#define GQ_EXPAND_BLOCKS 1024  // workgroups of germline_expand (each walks kParts / this many partitions)
+#endif
+      hipLaunchKernelGGL(germline_expand, dim3(GQ_EXPAND_BLOCKS), dim3(kBlock), 0, c->stream, (CallRec *)c->recs.p, ctr, og,
                          p->threshold, p->emit_ref, p->emit_no_call, dead_key);
       HIP_TRY(hipGetLastError());
     }
