@@ -46,9 +46,20 @@ def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
     return d
 
 
-def partition(loci: LociSet, parallelism: int, accuracy: int, *read_sets: ReadSet):
+def task_count(parallelism: int, world: int = 1) -> int:
+    """`--parallelism` or, at 0, Spark's sc.defaultParallelism (DistributedUtil.scala:59).  The
+    default parallelism of a Spark job is the number of its workers' cores; here it is the
+    number of ranks (1 for a single process, N under torch.distributed.run with N GPUs).  So, as
+    between Spark local[1] and local[N], a run with the default and a different rank count
+    cuts the loci into different tasks, and the records at heap-order loci (the first pileup of
+    every task) may differ; identical output across rank counts needs
+    the same explicit --parallelism."""
+    return parallelism if parallelism > 0 else max(1, world)
+
+
+def partition(loci: LociSet, parallelism: int, accuracy: int, *read_sets: ReadSet, world: int = 1):
     """DistributedUtil.partitionLociAccordingToArgs (DistributedUtil.scala:55-69)."""
-    tasks = parallelism if parallelism > 0 else 1
+    tasks = task_count(parallelism, world)
     if accuracy == 0:
         return partition_loci_uniformly(tasks, loci)
     return partition_loci_by_approximate_depth(tasks, loci, accuracy, *[r.regions() for r in read_sets])
@@ -125,19 +136,46 @@ def _loci_builder(args) -> LociSetBuilder:
     return LociSet.parse("all")
 
 
+class OutputFormatError(ValueError):
+    """An --out path the reference would write in a format this build does not produce."""
+
+
 def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None, max_genotypes: int = 0) -> None:
-    """Common.writeVariantsFromArguments (Common.scala:246-304): JSON for "" / .json, else VCF.
+    """Common.writeVariantsFromArguments (Common.scala:246-304), by the path's extension
+    (lower-cased, after stripMargin):
+      * "" or .json: Avro-JSON, serially, to stdout or to the file (overwritten, :254-289);
+      * .vcf: toVariantContext.coalesce(1).saveAsVcf (:290-293), a Hadoop output DIRECTORY
+        holding one part-r-00000 and the committer's _SUCCESS marker (README.md:49-51); an
+        existing path is refused, as Hadoop's checkOutputSpecs refuses it;
+      * anything else: adamParquetSave (:294-302).  ADAM Parquet is not produced here, so such
+        a path is refused up front rather than silently written in another format.
     --max-genotypes reaches RDD.sample(false, maxGenotypes, 0) as the sampling FRACTION
     (Common.scala:247-249): 1 keeps every genotype, larger values are refused by Spark's
     Bernoulli sampler ("must be on interval [0, 1]"), as here.  --out-chunks only coalesces
     partitions (order-preserving), so it does not change what is written."""
-    from .output import write_json, write_vcf
+    from .output import write_json, write_vcf_dir
+    check_output_path(path)
     if max_genotypes > 1:
         raise ValueError("Sampling fraction (%s) must be on interval [0, 1]" % float(max_genotypes))
     if path.lower().endswith(".vcf"):
-        write_vcf(path, genotypes, contig_lengths)
+        write_vcf_dir(path, genotypes, contig_lengths)
     else:
         write_json(path, genotypes)
+
+
+def check_output_path(path: str) -> None:
+    """Refuse, before any work, an --out the reference would write as ADAM Parquet or a VCF
+    directory that already exists (Common.scala:254, 290, 294)."""
+    import os
+    low = path.lower()
+    if path == "" or low.endswith(".json"):
+        return
+    if low.endswith(".vcf"):
+        if os.path.exists(path):
+            raise OutputFormatError("Output directory %s already exists" % path)
+        return
+    raise OutputFormatError("--out %s: the reference writes this as ADAM Parquet (adamParquetSave, Common.scala:"
+                            "294-302), which this build does not produce; use a .vcf or .json path" % path)
 
 
 def germline_threshold_main(argv: Sequence[str]) -> int:
@@ -149,6 +187,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     p.add_argument("--emit-no-call", action="store_true", help="Output no call calls.")
     _common_args(p)
     args = p.parse_args(argv)
+    check_output_path(args.out)
     rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
     # germline-threshold takes no reference (GermlineThresholdCaller.scala:64-70): with
@@ -157,7 +196,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
                     recompute_md=args.recompute_md_tags,
                     contig_lengths_from_dictionary=not args.no_sequence_dictionary)
     loci = builder.result(rs.contig_lengths_map)
-    parts = partition(loci, args.parallelism if args.parallelism > 0 else world, args.partition_accuracy, rs)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, rs, world=world)
     flat = flatten_partitions(parts, rs.contig_index())
     ctx = native.Context(local if world > 1 else args.device)
     if world > 1:
@@ -203,6 +242,7 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     p.add_argument("--dbsnp-vcf", default="", help="VCF file to identify DBSNP variants")
     _common_args(p)
     args = p.parse_args(argv)
+    check_output_path(args.out)
     rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
     f = InputFilters.make(overlaps_loci=builder, non_duplicate=True, passed_vendor_quality_checks=True,
@@ -217,7 +257,7 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     if tumor.contig_lengths_map != normal.contig_lengths_map:
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
     loci = builder.result(normal.contig_lengths_map)
-    parts = partition(loci, args.parallelism if args.parallelism > 0 else world, args.partition_accuracy, tumor, normal)
+    parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal, world=world)
     flat = flatten_partitions(parts, tumor.contig_index())
     ctx = native.Context(local if world > 1 else args.device)
     if world > 1:
@@ -282,6 +322,7 @@ def variant_support_main(argv: Sequence[str]) -> int:
     p.add_argument("--recompute-md-tags", action="store_true")
     p.add_argument("--device", type=int, default=0, help="GPU index")
     args = p.parse_args(argv)
+    single_process_only("variant-support")
     loci = variant_loci(args.input_variant)
     # partitionLociUniformly(args.parallelism, ...) takes the flag as given (VariantSupport.scala:89)
     parts = partition_loci_uniformly(args.parallelism, loci)
@@ -341,6 +382,8 @@ def germline_standard_main(argv: Sequence[str]) -> int:
     p.add_argument("--truth-genotypes", default="", help="(concordance report: not supported)")
     _common_args(p)
     args = p.parse_args(argv)
+    single_process_only("germline-standard")
+    check_output_path(args.out)
     if args.truth_genotypes:
         raise ValueError("--truth-genotypes (concordance report) is not supported")
     builder = _loci_builder(args)
@@ -393,6 +436,7 @@ def vaf_histogram_main(argv: Sequence[str]) -> int:
     p.add_argument("--recompute-md-tags", action="store_true")
     p.add_argument("--device", type=int, default=0, help="GPU index")
     args = p.parse_args(argv)
+    single_process_only("vaf-histogram")
     if args.out and args.local_out:
         raise ValueError("--out and --local-out are exclusive")
     if args.cluster:
@@ -429,6 +473,16 @@ def vaf_histogram_main(argv: Sequence[str]) -> int:
         for row in plain:
             print(row)
     return 0
+
+
+def single_process_only(command: str) -> None:
+    """germline-standard, variant-support and vaf-histogram run as one process on --device: under
+    torch.distributed.run every rank would repeat the whole job and write the same output, so a
+    multi-rank launch is refused."""
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise RuntimeError("%s runs as a single process (WORLD_SIZE=%s): launch it without torch.distributed.run "
+                           "and pick the GPU with --device" % (command, os.environ["WORLD_SIZE"]))
 
 
 def _finish_rank(rc: int) -> int:

@@ -29,7 +29,7 @@
 
 #include "gq_kernels.h"
 
-// (included inside gq_pileup.hip's anonymous namespace, after gq_germline_cols.h)
+// (included inside gq_pileup.hip's anonymous namespace, after gq_germline_common.h)
 
 #ifndef GQ_PROJ_WPE
 #define GQ_PROJ_WPE 4  // waves per SIMD the register budget must allow (5: 72 B/lane of spills, 4 % slower)

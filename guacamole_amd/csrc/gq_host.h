@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gqpileup.h"
@@ -45,7 +46,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   int err;
   int pad;
   long long err_pos;
-  unsigned long long n_slow;       // tiles germline_cols handed to germline_walk
+  unsigned long long n_slow;       // tiles germline_proj handed to germline_walk
   unsigned long long n_dead;       // record slots germline_expand left unused
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
@@ -80,7 +81,7 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *c
 }
 
 // Geometry of the partitioned germline outputs (records: which = 0, complex items: 1).
-// Partitions [0, ncols) belong to germline_cols workgroups (capacity capA each), partitions
+// Partitions [0, ncols) belong to germline_proj workgroups (capacity capA each), partitions
 // [kPartsCols, kParts) to walker / complex-kernel waves (capacity capB each); the others are
 // unused.  slot(which, p, k) is the buffer index of element k of partition p.
 struct OutGeom {
@@ -394,5 +395,11 @@ gq_status check_device_error(gq_ctx *c, const Counters &h);
 gq_status heap_ref_bases(gq_ctx *c, const Plan &pl, const DevBuf &tiles_buf,
                          const std::vector<const gq_dev_reads *> &sets, const std::vector<AmbItem> &items,
                          uint8_t *out_ref);
+
+// For each locus range [a, b) of `ranges` on contig `contig`: does a read of `set` overlap it
+// (out[i] = 1)?  A device search: the first read with pmax_end > a is the first read ending
+// past a, and a read overlaps [a, b) iff that one starts before b.
+gq_status reads_overlap(gq_ctx *c, const gq_dev_reads *set, int32_t contig,
+                        const std::vector<std::pair<int64_t, int64_t>> &ranges, std::vector<char> &out);
 }  // namespace gq
 

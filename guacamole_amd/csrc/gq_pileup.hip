@@ -657,7 +657,7 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // germline_tile: LDS histogram + on-device decision for simple loci
 // ------------------------------------------------------------------------------------------
 
-#include "gq_germline_cols.h"
+#include "gq_germline_common.h"
 #include "gq_germline_proj.h"
 
 // ------------------------------------------------------------------------------------------
@@ -1987,17 +1987,9 @@ gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
 
 extern "C" {
 
-// GQ_GERM=cols: the LDS-staged column kernel of round 1 (diagnostics / A-B); default: germline_proj
-static bool germline_use_proj() {
-  static const bool proj = !(getenv("GQ_GERM") && strcmp(getenv("GQ_GERM"), "cols") == 0);
-  return proj;
-}
-
 static unsigned germline_grid(gq_ctx *c, int64_t tiles) {
   if (c->n_cu <= 0 && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
     c->n_cu = 256;
-  if (!germline_use_proj())  // persistent: two workgroups per CU (LDS-bound), each over a contiguous run of tiles
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>({tiles, 2 * (int64_t)c->n_cu, (int64_t)kPartsCols}));
   // persistent: every resident workgroup (8 waves, a tile per wave at a time) over a contiguous run
   if (c->proj_wg_per_cu <= 0) {
     int nb = 0;
@@ -2014,19 +2006,13 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
                                  CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr) {
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
-  if (germline_use_proj()) {
-    hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, tiles, R.pcs, R.pbase, R.pbad, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
-                       p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
-  } else {
-    hipLaunchKernelGGL(germline_cols, dim3((unsigned)og.ncols), dim3(ColsCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, tiles, R.seq, R.cdesc, R.cev, R.n_samples, p->threshold,
-                       p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
-  }
+  hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
+                     (const Tile *)c->tiles.p, tiles, R.pcs, R.pbase, R.pbad, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
+                     p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // column kernel | walker kernel
   const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
-  hipLaunchKernelGGL((germline_walk<ColsCfg::kT>), dim3(wblocks), dim3(kBlock), 0, c->stream,
+  hipLaunchKernelGGL((germline_walk<ProjCfg::kT>), dim3(wblocks), dim3(kBlock), 0, c->stream,
                      (const Tile *)c->tiles.p, (const int32_t *)c->slow.p, R, p->threshold, p->emit_ref,
                      p->emit_no_call, recs, cplx, og, ctr);
   HIP_TRY(hipGetLastError());
@@ -2045,8 +2031,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = germline_use_proj() ? plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true)
-                                      : plan(c, rd, loci, T, pl, c->tiles, ColsCfg::kStage, ColsCfg::kMeta, ColsCfg::kEv);
+  gq_status st = plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true);
   if (st) return st;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
@@ -2056,7 +2041,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     return GQ_OK;
   }
   const int ns = rd->d.n_samples;
-  // output partitions: per germline_cols workgroup (capA, its share of the loci) and per
+  // output partitions: per germline_proj workgroup (capA, its share of the loci) and per
   // walker / complex-kernel wave (capB); grown on overflow
   OutGeom og{};
   og.ncols = (int)germline_grid(c, pl.n_tiles);
@@ -2167,17 +2152,11 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     fprintf(stderr, "gq germline_complex prof (cycles/item/wave): cover %.0f reference-base %.0f elements %.0f "
             "decision %.0f (%llu items)\n", (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
             (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
-  if ((gq_dbg() & 16) && germline_use_proj() && hc.prof[5])
+  if ((gq_dbg() & 16) && hc.prof[5])
     fprintf(stderr,
             "gq prof (cycles/tile/wave): setup %.0f first-loads %.0f entries %.0f counting %.0f decision %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
             (double)hc.prof[3] / hc.prof[5], (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
-  if (getenv("GQ_DBG") && !germline_use_proj() && hc.prof[7])
-    fprintf(stderr,
-            "gq prof (cycles/tile/wave): tile %.0f scan+column+per-read %.0f vmcnt+barrier1 %.0f "
-            "dma+rows+decide %.0f barrier2 %.0f (%llu)\n",
-            (double)hc.prof[0] / hc.prof[7], (double)hc.prof[1] / hc.prof[7], (double)hc.prof[2] / hc.prof[7],
-            (double)hc.prof[3] / hc.prof[7], (double)hc.prof[4] / hc.prof[7], hc.prof[7]);
   for (int k = 0; k < kSpread; ++k) {
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];

@@ -1592,19 +1592,16 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       return set_err(GQ_E_ARG, "reference covers %d contigs, the read sets %d", ref->n_contigs, t->d.n_contigs);
     if (ref->device != c->device) return set_err(GQ_E_ARG, "reference uploaded to another device");
     HIP_TRY(hipSetDevice(c->device));
-    std::vector<int64_t> max_end((size_t)ref->n_contigs, -2);
-    auto reach = [&](int32_t ci) -> int64_t {  // largest read end on contig ci over both samples
-      if (max_end[(size_t)ci] != -2) return max_end[(size_t)ci];
-      int64_t m = -1;
+    // does a read of either sample overlap [a, b) of contig ci (a pileup forms there)?
+    auto covered = [&](int32_t ci, int64_t a, int64_t b, bool *hit) -> gq_status {
+      *hit = false;
       for (const gq_dev_reads *sr : {t, n}) {
-        const int64_t b = sr->contig_read_begin[(size_t)ci], e = sr->contig_read_begin[(size_t)ci + 1];
-        if (e > b) {
-          int32_t v = 0;
-          if (hipMemcpy(&v, sr->d.pmax_end + (e - 1), sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -3;
-          m = std::max<int64_t>(m, v);
-        }
+        std::vector<char> o;
+        const gq_status s2 = reads_overlap(c, sr, ci, {{a, b}}, o);
+        if (s2) return s2;
+        if (o[0]) *hit = true;
       }
-      return max_end[(size_t)ci] = m;
+      return GQ_OK;
     };
     for (int64_t k = 0; k < loci->n_ranges; ++k) {
       const int32_t ci = loci->contig[k];
@@ -1612,15 +1609,19 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       int64_t e0 = loci->end[k];
       if (e0 <= s0) continue;
       if (ci < 0 || ci >= ref->n_contigs) return set_err(GQ_E_ARG, "loci range on contig %d: no such contig", ci);
-      const int64_t m = reach(ci);
-      if (m == -3) return set_err(GQ_E_HIP, "gq_somatic_standard_ref: read-extent copy failed");
+      bool hit = false;
       if (ref->off[(size_t)ci] < 0) {
-        if (m > s0) return set_err(GQ_E_ARG, "contig %d does not exist in the current reference", ci);
+        const gq_status s2 = covered(ci, s0, e0, &hit);
+        if (s2) return s2;
+        if (hit) return set_err(GQ_E_ARG, "contig %d does not exist in the current reference", ci);
         continue;
       }
       const int64_t len = ref->len[(size_t)ci];
       if (e0 > len) {
-        if (m > std::max(len, s0))
+        // only a pileup at a locus of THIS range past the contig's end fails (getReferenceBase)
+        const gq_status s2 = covered(ci, std::max(len, s0), e0, &hit);
+        if (s2) return s2;
+        if (hit)
           return set_err(GQ_E_ARG, "locus %lld of contig %d is past the end of the reference contig (length %lld)",
                          (long long)std::max(len, s0), ci, (long long)len);
         e0 = len;

@@ -176,8 +176,23 @@ def write_json(path: str, genotypes: Iterable[Dict]) -> None:
             out.close()
 
 
+VCF_PART = "part-r-00000"
+
+
+def write_vcf_dir(path: str, genotypes: List[Dict], contig_lengths: Optional[Dict[str, int]] = None) -> str:
+    """saveAsVcf after coalesce(1, shuffle = true) (Common.scala:293): Hadoop's new-API output
+    layout — the directory `path` holding the single part file part-r-00000 and the committer's
+    empty _SUCCESS marker.  Returns the part file's path."""
+    import os
+    os.makedirs(path, exist_ok=False)
+    part = os.path.join(path, VCF_PART)
+    write_vcf(part, genotypes, contig_lengths)
+    open(os.path.join(path, "_SUCCESS"), "w").close()
+    return part
+
+
 def write_vcf(path: str, genotypes: List[Dict], contig_lengths: Optional[Dict[str, int]] = None) -> None:
-    """One VCF line per Genotype (VCF 4.1; POS is 1-based = start + 1)."""
+    """One VCF line per Genotype (VCF 4.1; POS is 1-based = start + 1) into the file `path`."""
     samples: List[str] = []
     for g in genotypes:
         if g["sampleId"] not in samples:

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import gzip
 from dataclasses import replace
-from typing import Dict, Iterable, List, Optional
+from typing import Tuple, Dict, Iterable, List, Optional
 
 import numpy as np
 
@@ -168,25 +168,38 @@ def rebuild_md_tags(rs: ReadSet, reference: Optional[ReferenceGenome], recompute
     todo = np.arange(rs.n) if recompute else np.flatnonzero(rs.md_len < 0)
     if len(todo) == 0:
         return rs
-    new_md: Dict[int, bytes] = {}
-    for i in todo:
-        i = int(i)
-        so, sl = int(rs.seq_off[i]), int(rs.seq_len[i])
-        co, nc = int(rs.cigar_off[i]), int(rs.n_cigar[i])
-        new_md[i] = reference.build_md_tag(rs.seq[so:so + sl], rs.contig_names[int(rs.contig[i])], int(rs.start[i]),
-                                           rs.cigar[co:co + nc]).encode()
-    parts, lens = [], np.empty(rs.n, np.int32)
-    for i in range(rs.n):
-        m = new_md.get(i)
-        if m is None:
-            ln = int(rs.md_len[i])
-            m = rs.md[int(rs.md_off[i]):int(rs.md_off[i]) + ln].tobytes() if ln >= 0 else None
-        lens[i] = -1 if m is None else len(m)
-        if m:
-            parts.append(m)
-    md_off = np.zeros(rs.n, np.int64)
-    md_off[1:] = np.cumsum(np.maximum(lens, 0))[:-1]
-    md = np.frombuffer(b"".join(parts), np.uint8).copy()
+    new_md = [reference.build_md_tag(rs.seq[int(rs.seq_off[i]):int(rs.seq_off[i]) + int(rs.seq_len[i])],
+                                     rs.contig_names[int(rs.contig[i])], int(rs.start[i]),
+                                     rs.cigar[int(rs.cigar_off[i]):int(rs.cigar_off[i]) + int(rs.n_cigar[i])]).encode()
+              for i in todo]
+    md_off, lens, md = repack_md(rs.md, np.asarray(rs.md_off, np.int64), np.asarray(rs.md_len, np.int32), todo, new_md)
     out = replace(rs, md_off=md_off, md_len=lens, md=md)
     out._gq = None
     return out
+
+
+def repack_md(pool: np.ndarray, md_off: np.ndarray, md_len: np.ndarray, todo: np.ndarray,
+              new_md: List[bytes]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The MD pool with the reads `todo` given the strings `new_md`, packed in read order, in
+    vectorised numpy (no per-read Python work for the reads that keep their tag): each read's
+    bytes are gathered from the old pool or from the new strings appended behind it."""
+    n = len(md_len)
+    todo = np.asarray(todo, np.int64)
+    new_lens = np.fromiter((len(m) for m in new_md), np.int64, len(new_md))
+    src_off = np.asarray(md_off, np.int64).copy()
+    lens = np.asarray(md_len, np.int64).copy()
+    base = len(pool)
+    if len(todo):
+        noff = np.zeros(len(todo), np.int64)
+        noff[1:] = np.cumsum(new_lens)[:-1]
+        src_off[todo] = base + noff
+        lens[todo] = new_lens
+    src = np.concatenate([np.asarray(pool, np.uint8), np.frombuffer(b"".join(new_md), np.uint8)])
+    take = np.maximum(lens, 0)
+    out_off = np.zeros(n, np.int64)
+    if n:
+        out_off[1:] = np.cumsum(take)[:-1]
+    total = int(take.sum())
+    # byte k of read i comes from src[src_off[i] + k]
+    idx = np.repeat(src_off - out_off, take) + np.arange(total, dtype=np.int64)
+    return out_off, lens.astype(np.int32), src[idx].copy()

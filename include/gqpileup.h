@@ -18,7 +18,7 @@
  * fixed-function entry points (gq_germline_threshold, gq_somatic_standard) and
  * a raw per-locus histogram (gq_pileup_counts).  skipEmpty = true is the only
  * mode (both callers pass true: GermlineThresholdCaller.scala:76,
- * SomaticStandardCaller.scala:289).
+ * SomaticStandardCaller.scala:108).
  *
  * Conventions: plain pointers + sizes, no exceptions across the ABI.  Every
  * function returns a gq_status; gq_last_error() gives the thread-local message.

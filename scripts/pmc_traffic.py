@@ -6,7 +6,7 @@
 writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary of the trace pass
   profiles/<tag>_pmc.csv            per-kernel averages of every PMC counter collected
-  profiles/traffic_<round>.json     HBM bytes per germline_cols launch (read by bench.py)
+  profiles/traffic_<round>.json     HBM bytes per pileup-kernel launch (read by bench.py)
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 come from separate --pmc passes (they cannot share one on gfx950), both in KiB; on gfx950
@@ -38,7 +38,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--length", type=int, required=True)
     ap.add_argument("--depth", type=float, required=True)
-    ap.add_argument("--kernel", default="germline_cols")
+    ap.add_argument("--kernel", default="germline_proj")
     ap.add_argument("--round", default="r01")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")

@@ -110,7 +110,10 @@ def test_cli_germline_vcf_and_somatic_json(tmp_path):
     vcf = str(tmp_path / "g.vcf")
     assert main(["germline-threshold", "--reads", fixture("chrM.sorted.bam"), "--loci", "chrM:0-16570",
                  "--out", vcf]) == 0
-    lines = [l for l in open(vcf) if not l.startswith("#")]
+    # saveAsVcf's Hadoop layout: a directory with one part file (Common.scala:290-293)
+    import os
+    assert sorted(os.listdir(vcf)) == ["_SUCCESS", "part-r-00000"]
+    lines = [l for l in open(os.path.join(vcf, "part-r-00000")) if not l.startswith("#")]
     assert len(lines) > 100 and all(l.split("\t")[0] == "chrM" for l in lines)
     js = str(tmp_path / "s.json")
     assert main(["somatic-standard", "--tumor-reads", fixture("tumor.chr20.tough.sam"), "--normal-reads",

@@ -90,3 +90,18 @@ def test_reference_errors(gpu_ctx):
     far = (np.array([0], np.int32), np.array([0], np.int64), np.array([400], np.int64), np.array([0], np.int64))
     full = ReferenceGenome({t.contig_names[0]: np.frombuffer(b"TCGATCGA" + b"A" * 100, np.uint8)})
     assert somatic_standard_reads(gpu_ctx, t, n, far, reference=full) == []
+
+
+def test_read_past_the_range_is_not_looked_up(gpu_ctx):
+    """A read beyond the FASTA contig's end but outside the loci range forms no pileup in the
+    range, so nothing fails (getReferenceBase is only called at visited loci of the range,
+    ReferenceBroadcast.scala:26-30); the same read inside the range does fail."""
+    reads = [mr("TCGATCGA", "8M", "8", 0)] * 2 + [mr("AAAAAAAA", "8M", "8", 200)]
+    t, n = make_read_set(reads), make_read_set(reads)
+    ref = ReferenceGenome({t.contig_names[0]: np.frombuffer(b"TCGATCGA" + b"A" * 92, np.uint8)})  # length 100
+    inside = (np.array([0], np.int32), np.array([0], np.int64), np.array([150], np.int64), np.array([0], np.int64))
+    assert somatic_standard_reads(gpu_ctx, t, n, inside, reference=ref) == O.somatic_standard(
+        t, n, inside, reference=ref)
+    reach = (np.array([0], np.int32), np.array([0], np.int64), np.array([205], np.int64), np.array([0], np.int64))
+    with pytest.raises(native.GQError, match="past the end of the reference contig"):
+        somatic_standard_reads(gpu_ctx, t, n, reach, reference=ref)

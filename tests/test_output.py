@@ -4,7 +4,8 @@ import json
 import pytest
 
 from guacamole_amd.output import (GENOTYPE_SCHEMA, VARIANT_SCHEMA, dbsnp_join, germline_genotype, java_float,
-                                  read_avro_json, read_dbsnp_vcf, somatic_genotype, write_json, write_vcf)
+                                  read_avro_json, read_dbsnp_vcf, somatic_genotype, write_json, write_vcf,
+                                  write_vcf_dir)
 
 
 def test_vcf_lines(tmp_path):
@@ -72,3 +73,49 @@ def test_max_genotypes_and_dbsnp(tmp_path):
             dict(contig="20", locus=6, ref="C", alt="G")]
     out = dbsnp_join(rows, db)
     assert [(r["alt"], r["rs_id"]) for r in out] == [("A", 42), ("A", 43), ("C", None), ("G", None)]
+
+
+def test_vcf_output_is_a_hadoop_directory(tmp_path):
+    """--out X.vcf: saveAsVcf after coalesce(1) writes the directory X.vcf holding part-r-00000
+    and _SUCCESS (Common.scala:290-293, README.md:49-51); an existing X.vcf is refused."""
+    import os
+    from guacamole_amd.commands import OutputFormatError, _write_genotypes
+    g = [germline_genotype("1", 5, "default", ("Alt", "Alt"), "C", "G")]
+    out = tmp_path / "calls.VCF"
+    _write_genotypes(str(out), g, {"1": 100})
+    assert sorted(os.listdir(out)) == ["_SUCCESS", "part-r-00000"]
+    body = [l for l in open(out / "part-r-00000") if not l.startswith("#")]
+    assert body == ["1\t6\t.\tC\tG\t.\t.\t.\tGT\t1/1\n"]
+    with pytest.raises(OutputFormatError, match="already exists"):
+        _write_genotypes(str(out), g)
+    assert write_vcf_dir(str(tmp_path / "b.vcf"), g).endswith("part-r-00000")
+
+
+@pytest.mark.parametrize("name", ["calls.adam", "calls.parquet", "calls", "calls.vcf.gz"])
+def test_parquet_paths_are_refused(tmp_path, name):
+    """Every other extension is ADAM Parquet in the reference (Common.scala:294-302): refused
+    before anything is written, not silently written as JSON."""
+    from guacamole_amd.commands import OutputFormatError, _write_genotypes, check_output_path
+    with pytest.raises(OutputFormatError, match="Parquet"):
+        check_output_path(str(tmp_path / name))
+    with pytest.raises(OutputFormatError):
+        _write_genotypes(str(tmp_path / name), [])
+    assert not (tmp_path / name).exists()
+
+
+def test_cli_refuses_parquet_before_loading(tmp_path):
+    """The CLI checks --out before reading its inputs (the reads path need not exist)."""
+    from guacamole_amd.commands import OutputFormatError, main
+    with pytest.raises(OutputFormatError):
+        main(["germline-threshold", "--reads", str(tmp_path / "missing.bam"), "--out", str(tmp_path / "x.adam")])
+    with pytest.raises(OutputFormatError):
+        main(["somatic-standard", "--tumor-reads", "t.bam", "--normal-reads", "n.bam", "--out", str(tmp_path / "y")])
+
+
+def test_default_parallelism_is_the_rank_count(monkeypatch):
+    """--parallelism 0 = sc.defaultParallelism (DistributedUtil.scala:59): the rank count here."""
+    from guacamole_amd.commands import single_process_only, task_count
+    assert task_count(0, 1) == 1 and task_count(0, 4) == 4 and task_count(7, 4) == 7
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(RuntimeError, match="single process"):
+        single_process_only("variant-support")

@@ -146,3 +146,30 @@ def test_oracle_reference_changes_calls():
     with pytest.raises(O.OracleError, match="does not exist in the current reference"):
         O.somatic_standard(t, n, loci, reference=ReferenceGenome({"other": ref.get_contig(t.contig_names[0])}),
                            apply_filters=0)
+
+
+def test_repack_md_matches_the_per_read_layout():
+    """repack_md (vectorised) = the straightforward per-read repack: reads keep their MD bytes
+    unless listed, listed reads take the new strings, MD-less reads (length -1) stay MD-less."""
+    import numpy as np
+    from guacamole_amd.reference import repack_md
+    rng = np.random.default_rng(5)
+    n = 200
+    lens = rng.integers(-1, 9, n).astype(np.int32)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(np.maximum(lens, 0))[:-1]
+    pool = rng.integers(48, 58, int(np.maximum(lens, 0).sum())).astype(np.uint8)
+    todo = np.sort(rng.choice(n, 37, replace=False))
+    new = [bytes(rng.integers(65, 70, int(k))) for k in rng.integers(0, 7, len(todo))]
+    got_off, got_len, got = repack_md(pool, off, lens, todo, new)
+    want = []
+    want_len = []
+    nm = dict(zip(todo.tolist(), new))
+    for i in range(n):
+        m = nm.get(i)
+        if m is None:
+            m = pool[off[i]:off[i] + lens[i]].tobytes() if lens[i] >= 0 else None
+        want_len.append(-1 if m is None else len(m))
+        want.append(m or b"")
+    assert got_len.tolist() == want_len and got.tobytes() == b"".join(want)
+    assert all(got[got_off[i]:got_off[i] + max(got_len[i], 0)].tobytes() == want[i] for i in range(n))
