@@ -4,6 +4,7 @@
 // general-allele germline kernel and the somatic candidate kernel.
 #pragma once
 #include "gq_kernels.h"
+#include "gq_scala_order.h"
 
 namespace gq {
 namespace {
@@ -263,6 +264,35 @@ __device__ __forceinline__ int md_ref_at(const DevReads &R, int64_t r, int32_t p
 }
 
 constexpr int kSlots = 2;  // table capacity = 64 * kSlots distinct (sample, allele) keys per locus
+
+// Scala hash (Allele(refBases, altBases).hashCode, gq_scala_order.h) of an allele from its bytes
+__device__ __forceinline__ uint32_t allele_scala_hash(const DevReads &R, const AlleleDesc &a, int32_t pos) {
+  scala::SeqHasher hr, ha;
+  const int rl = allele_ref_len(a), al = allele_alt_len(a);
+  for (int i = 0; i < rl; ++i) hr.add_byte(allele_byte(R, a, pos, 0, i));
+  for (int i = 0; i < al; ++i) ha.add_byte(allele_byte(R, a, pos, 1, i));
+  return scala::allele_hash(hr.result(), ha.result());
+}
+
+// Value of lane j (wave-uniform j) broadcast to every lane, for 64-bit types.
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ double lane_f64(double v, int j) {
+  return __builtin_bit_cast(double, lane_u64(__builtin_bit_cast(uint64_t, v), j));
+}
+// Minimum over the wave (every lane active).
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = (int64_t)(((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)v, d, 64)) |
+                                ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)v >> 32), d, 64) << 32));
+    v = o < v ? o : v;
+  }
+  return v;
+}
 
 }  // namespace
 }  // namespace gq

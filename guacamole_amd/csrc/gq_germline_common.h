@@ -95,7 +95,10 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
     const bool ambiguous = (mask & (mask - 1)) != 0;
     const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit
     const uint32_t c_ref = low == 1u ? c[0] : low == 2u ? c[1] : low == 4u ? c[2] : low == 8u ? c[3] : c[4];
-    const bool to_complex = (wide && in) || (live && (ambiguous || cx > 0 || multi_sample));
+    // (ref C with G and N alleles present: their Scala map order depends on first occurrences,
+    // gq_scala_order.h; germline_complex decides those)
+    const bool cgn = low == 2u && c[3] > 0 && c[4] > 0;
+    const bool to_complex = (wide && in) || (live && (ambiguous || cx > 0 || multi_sample || cgn));
     // every non-reference allele has count <= depth - c_ref: if that does not pass, no
     // alternate allele does (HomRef if the reference passes, else NoCall)
     const bool homref = live && !to_complex && !passes(depth - c_ref, depth);
@@ -161,9 +164,9 @@ __device__ __forceinline__ void germline_decide(const uint32_t *cnt, const Tile 
 
 // The variant candidates of germline_decide -> Genotype records, one thread per record slot
 // (GermlineThresholdCaller.scala:100-177 for a pileup of single-base alleles; counts < 2^16).
-// Allele (ref, b) keys: count << 8 | (255 - canonical rank); canonical order of Allele(ref, alt)
-// for one ref is the alt byte order A < C < G < N < T, i.e. the categories 0, 1, 3, 4, 2.
-// Sorting keys descending = sortBy(-count), ties canonical.  Unused slots get a key past
+// Allele (ref, b) keys: count << 16 | (255 - Scala map rank) << 8 | category: sorting the keys
+// descending = sortBy(-count), a stable sort of the counts map's iteration order
+// (GermlineThresholdCaller.scala:103-104, gq_scala_order.h).  Unused slots get a key past
 // every ordinal (dead_key) and are counted in n_dead; they sort behind the live records.
 __global__ void germline_expand(CallRec *__restrict__ recs, Counters *ctr, OutGeom og, int threshold,
                                 int emit_ref, int emit_no_call, uint64_t dead_key) {
@@ -185,24 +188,39 @@ __global__ void germline_expand(CallRec *__restrict__ recs, Counters *ctr, OutGe
                            (uint32_t)((cand.allele >> 32) & 0xFFFFu), (uint32_t)(cand.allele >> 48), cand.ref_len};
     const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4];
     const uint8_t ref = cand.gt0;
-    uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys
+    // the counts map's Scala order over the alleles present (ref, b): up to four, the mutable
+    // map's (bucket descending; no two share a bucket here: the one pair that could, ref C with
+    // G and N, went to germline_complex), five: the HashTrieMap's (gq_scala_order.h)
+    int npres = 0;
+#pragma unroll
+    for (int cat = 0; cat < 5; ++cat) npres += c[cat] > 0 ? 1 : 0;
+    uint64_t sk[5];
+#pragma unroll
+    for (int cat = 0; cat < 5; ++cat) {
+      scala::SeqHasher hr, ha;
+      hr.add_byte(ref);
+      ha.add_byte(cat_base(cat));
+      const uint32_t h = scala::allele_hash(hr.result(), ha.result());
+      sk[cat] = npres <= 4 ? (uint64_t)(15u - scala::mutable_bucket(h, 4)) : scala::trie_key(h);
+    }
+    uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys: count << 16 | (255 - map rank) << 8 | category
     int npass = 0;
 #pragma unroll
-    for (int rank = 0; rank < 5; ++rank) {
-      const int cat = (0x24310 >> (4 * rank)) & 0xF;
+    for (int cat = 0; cat < 5; ++cat) {
       const uint32_t cc = c[cat];
       if (cc == 0 || !passes(cc, depth)) continue;
       ++npass;
-      uint32_t key = (cc << 8) | (uint32_t)(255 - rank);
+      int rank = 0;
+#pragma unroll
+      for (int o = 0; o < 5; ++o)
+        if (o != cat && c[o] > 0 && (sk[o] < sk[cat] || (sk[o] == sk[cat] && o < cat))) ++rank;
+      uint32_t key = (cc << 16) | ((uint32_t)(255 - rank) << 8) | (uint32_t)cat;
       if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
       if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
       if (key > k2) { k2 = key; }
     }
-    auto key_base = [](uint32_t key) -> uint8_t {
-      const int rank = 255 - (int)(key & 0xFFu);
-      return cat_base((0x24310 >> (4 * rank)) & 0xF);
-    };
-    const bool tie = npass >= 2 && ((k0 >> 8) == (k1 >> 8) || (npass >= 3 && (k1 >> 8) == (k2 >> 8)));
+    auto key_base = [](uint32_t key) -> uint8_t { return cat_base((int)(key & 0xFFu)); };
+    const bool tie = npass >= 2 && ((k0 >> 16) == (k1 >> 16) || (npass >= 3 && (k1 >> 16) == (k2 >> 16)));
     if (tie) ++ties;
     const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
     // the case split -> up to two records (g0, g1, alt base or the symbolic <ALT>)

@@ -265,7 +265,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit (or 0: N)
         const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
                                nN * (low == 0u ? 1u : 0u);
-        const uint32_t to_complex = live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u));
+        // ref C with G and N present: Scala map order by first occurrence (germline_complex)
+        const uint32_t cgn = (low == 2u ? 1u : 0u) & (cG > 0 ? 1u : 0u) & (nN > 0 ? 1u : 0u);
+        const uint32_t to_complex = live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u) | cgn);
         const uint32_t simple = live & (to_complex ^ 1u);
         const uint32_t alt_pass = passes(depth - c_ref, depth) ? 1u : 0u;  // some other allele may pass
         const uint32_t homref = simple & (alt_pass ^ 1u);

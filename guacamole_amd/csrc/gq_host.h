@@ -50,6 +50,8 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_dead;       // record slots germline_expand left unused
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
+  unsigned long long n_deep;       // somatic candidates handed to the deep caller
+  unsigned long long deep_max;     // deepest per-sample pileup among them and the listed loci
   // per-tile run counters, spread over kSpread addresses (summed on the host)
   unsigned long long spread[4][64];  // visited, ambiguous, ties, dead record slots
   unsigned long long prof[8];  // diagnostic phase clocks (GQ_DBG=16 only)
@@ -354,6 +356,7 @@ struct gq_ctx {
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
+  gq::DevBuf deep_list, deep_scratch;              // somatic: the deep caller's list and per-wave scratch
   gq::DevBuf bkt;                                  // germline output order: bucket counts / offsets / fill
   void *pin = nullptr;                             // pinned host staging for the small per-call copies
   size_t pin_n = 0;

@@ -67,6 +67,8 @@ struct DevReads {
   // the first read with pmax_end > the block's first locus and the first read starting at or
   // after it (a block index of the reads, so aligned tiles need no search over the contig)
   const int64_t *blk_rb, *blk_rs;
+  // Scala String.hashCode of each sample slot's name (gq_reads.sample_hash; nullptr: slot order)
+  const uint32_t *sample_hash;
 };
 
 // Per-read record of the projection kernels (8 bytes): the read spans the 8-locus columns

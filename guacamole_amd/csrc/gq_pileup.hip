@@ -659,6 +659,7 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 
 #include "gq_germline_common.h"
 #include "gq_germline_proj.h"
+#include "gq_winorder.h"
 
 // ------------------------------------------------------------------------------------------
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
@@ -677,11 +678,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
                                                            unsigned long long amb_cap,
                                                            const AmbItem *__restrict__ amb_in,
                                                            const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
-                                                           int dbg) {
+                                                           int dbg, SomWin sw) {
   // amb_in == nullptr: every queued item; a locus whose reads' MD-derived bases disagree
   // (Pileup.referenceBaseAtLocus then depends on the queue's heap order) is only listed in
   // amb_out.  amb_in != nullptr: the listed loci again, with their reference base resolved
-  // in heap order (heap_ref_bases) in amb_ref.
+  // in heap order (heap_ref_bases) in amb_ref, and the element order of each window (sw: the
+  // initial group's heap ranks) for the Scala map orders below.
+  //
+  // Output order (GermlineThresholdCaller.scala:100-104): the per-sample records come in the
+  // order of Pileup.bySample (a groupBy over sample names, Pileup.scala:57-61) and count ties
+  // among passing alleles keep the order of the counts' groupBy map (sortBy is stable): the
+  // Scala 2.10 Map iteration orders restated in gq_scala_order.h.  Both depend on the first
+  // occurrence of a key in pileup element order only where two keys share a mutable.HashMap
+  // bucket (up to four keys); such loci are listed with the heap-order ones (amb_out) and
+  // redone with the windows' element order.
   const int lane = threadIdx.x & 63;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -781,15 +791,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     // ---- pass 2: classify elements, group alleles per (sample, allele) in registers
     uint64_t tlo[kSlots], thi[kSlots];
     uint32_t tcnt[kSlots];
+    int64_t tfirst[kSlots];  // first occurrence (element-order key) of each entry
     AlleleDesc tdesc[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
       tlo[s] = thi[s] = 0;
       tcnt[s] = 0;
+      tfirst[s] = INT64_MAX;
     }
     int nt = 0;  // used slots (uniform)
     bool overflow = false;
     uint32_t st_lane = 0;  // lane s < 8: elements of sample s (read back with readlane: no scratch array)
+    int64_t st_first = INT64_MAX;  // lane s < 8: the first element of sample s (element-order key)
+    const WinInit wio = sw.wi ? sw.wi[2 * sw.range_win[tl.range]] : WinInit{INT32_MAX, INT32_MIN, 0, 0, 0};
     for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
       bool act;
       const int64_t r = slot_read(k0 + lane, &act);
@@ -806,10 +820,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
           key = allele_key(R, d, pos, smp);
         }
       }
-      // per-sample totals
+      const int64_t okey = act ? element_order_key(R, r, pos, wio, sw.init_reads, sw.init_rank) : INT64_MAX;
+      // per-sample totals and first elements
       for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
         const unsigned long long b = __ballot(act && smp == sm);
-        if (lane == sm) st_lane += (uint32_t)__popcll(b);
+        if (!b) continue;  // uniform
+        const int64_t f = wave_min_i64(act && smp == sm ? okey : INT64_MAX);
+        if (lane == sm) {
+          st_lane += (uint32_t)__popcll(b);
+          st_first = f < st_first ? f : st_first;
+        }
       }
       unsigned long long pending = __ballot(act);
       while (pending) {
@@ -854,9 +874,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         }
         if (found >= 0) {
           const int owner = found & 63, sl = found >> 6;
+          const int64_t f = wave_min_i64(match ? okey : INT64_MAX);
 #pragma unroll
           for (int s = 0; s < kSlots; ++s)
-            if (s == sl && lane == owner) tcnt[s] += n;
+            if (s == sl && lane == owner) {
+              tcnt[s] += n;
+              tfirst[s] = f < tfirst[s] ? f : tfirst[s];
+            }
         }
         pending &= ~mb;
       }
@@ -874,23 +898,112 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       }
     }
     tick(2);
+    // ---- Scala map orders (gq_scala_order.h): each entry's order key within its sample's
+    //      counts map, each present sample's within bySample, and whether either depends on
+    //      first occurrences (two keys in one mutable.HashMap bucket, up to four keys)
+    const int ns_all = R.n_samples < 8 ? R.n_samples : 8;
+    uint64_t tkey[kSlots];
+    bool dep = false;
+    {
+      uint32_t tb[kSlots];
+      int tsm[kSlots];
+      bool tpass[kSlots];
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        const bool live = s * 64 + lane < nt;
+        const uint32_t h = live ? allele_scala_hash(R, tdesc[s], pos) : 0u;
+        tb[s] = scala::mutable_bucket(h, 4);
+        tsm[s] = live ? (int)tdesc[s].pad : -1;
+        const uint32_t tot = (uint32_t)__shfl((int)st_lane, tsm[s] < 0 ? 0 : tsm[s], 64);
+        tpass[s] = live && tot > 0 && (long long)tcnt[s] * 100 / (long long)tot > threshold;
+        tkey[s] = scala::trie_key(h);  // five or more alleles in the sample: HashTrieMap order
+      }
+      // entries of the same sample, and same-bucket ties among passing ones
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        int n_same = 0;
+        bool pair = false;
+        for (int k = 0; k < nt; ++k) {
+          const int ow = k & 63, sl = k >> 6;
+          int ksm = -1;
+          uint32_t kb = 0, kc = 0;
+          bool kp = false;
+#pragma unroll
+          for (int t = 0; t < kSlots; ++t)
+            if (t == sl) {
+              ksm = __shfl(tsm[t], ow, 64);
+              kb = (uint32_t)__shfl((int)tb[t], ow, 64);
+              kc = (uint32_t)__shfl((int)tcnt[t], ow, 64);
+              kp = __shfl((int)tpass[t], ow, 64) != 0;
+            }
+          if (ksm == tsm[s] && tsm[s] >= 0) {
+            ++n_same;
+            if (k != s * 64 + lane && kb == tb[s] && kp && tpass[s] && kc == tcnt[s]) pair = true;
+          }
+        }
+        // up to four keys: Map1..Map4 in the mutable map's order (bucket descending, a chain
+        // newest first = the later first occurrence first)
+        if (tsm[s] >= 0 && n_same <= 4)
+          tkey[s] = ((uint64_t)(15u - tb[s]) << 42) | (((1ull << 42) - 1ull) - (uint64_t)tfirst[s]);
+        if (tsm[s] >= 0 && n_same <= 4 && pair) dep = true;
+      }
+    }
+    // samples: lane sm < 8 holds its rank among the present samples
+    int srank = lane;
+    {
+      const bool present = lane < ns_all && st_lane > 0;
+      const int np = __popcll(__ballot(present));
+      uint64_t sk = ~0ull;
+      uint32_t sb = 16u + (uint32_t)lane;
+      if (R.sample_hash && present) {
+        const uint32_t h = R.sample_hash[lane];
+        sb = scala::mutable_bucket(h, 4);
+        sk = np <= 4 ? (((uint64_t)(15u - sb) << 42) | (((1ull << 42) - 1ull) - (uint64_t)st_first)) : scala::trie_key(h);
+      } else if (present) {
+        sk = (uint64_t)lane;  // no sample names given: slot order
+      }
+      int rk = 0;
+      bool same_bucket = false;
+      for (int t = 0; t < 8; ++t) {
+        const uint64_t tk2 = lane_u64(sk, t);
+        const uint32_t tb2 = (uint32_t)__builtin_amdgcn_readlane((int)sb, t);
+        if (t != lane && tk2 != ~0ull && present) {
+          if (tk2 < sk || (tk2 == sk && t < lane)) ++rk;
+          if (R.sample_hash && np <= 4 && tb2 == sb) same_bucket = true;
+        }
+      }
+      srank = rk;
+      if (__ballot(same_bucket) != 0) dep = true;
+    }
+    if (__ballot(dep) != 0 && !amb_in) {
+      // the order depends on first occurrences: redone with the windows' element order
+      if (lane == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+      }
+      continue;
+    }
     // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
     const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
     for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
       const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)st_lane, sm);
       if (total == 0) continue;
-      // select top-3 passing entries by (count desc, allele asc); three named slots, not an
+      const int rank_sm = __builtin_amdgcn_readlane(srank, sm);
+      // select top-3 passing entries by (count desc, map order); three named slots, not an
       // indexed array (a dynamically indexed array would live in scratch)
       uint32_t topc[3] = {0, 0, 0};
+      uint64_t topk[3] = {0, 0, 0};
       AlleleDesc topd[3];
       int npass = 0;
       for (int j = 0; j < nt; ++j) {
         const int owner = j & 63, sl = j >> 6;
         uint32_t cj = 0;
+        uint64_t kj = 0;
         AlleleDesc dj;
 #pragma unroll
         for (int s = 0; s < kSlots; ++s)
           if (s == sl) {
+            kj = lane_u64(tkey[s], owner);
             cj = (uint32_t)__shfl((int)tcnt[s], owner, 64);
             dj.read = __shfl(tdesc[s].read, owner, 64);
             dj.aux = __shfl(tdesc[s].aux, owner, 64);
@@ -904,28 +1017,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         if ((long long)cj * 100 / (long long)total <= threshold) continue;
         const int f = npass < 3 ? npass : 3;  // entries held before this one (sorted)
         ++npass;
-        auto better = [&](uint32_t ce, const AlleleDesc &de) {
-          return ce < cj || (ce == cj && allele_cmp(R, dj, de, pos) < 0);
-        };
+        auto better = [&](uint32_t ce, uint64_t ke) { return ce < cj || (ce == cj && kj < ke); };
         // insertion position: past every held entry this one does not beat
-        const bool b2 = f > 2 && better(topc[2], topd[2]);
-        const bool b1 = f > 1 && (b2 || f == 2) && better(topc[1], topd[1]);
-        const bool b0 = f > 0 && (b1 || f == 1) && better(topc[0], topd[0]);
+        const bool b2 = f > 2 && better(topc[2], topk[2]);
+        const bool b1 = f > 1 && (b2 || f == 2) && better(topc[1], topk[1]);
+        const bool b0 = f > 0 && (b1 || f == 1) && better(topc[0], topk[0]);
         const int p = b0 ? 0 : b1 ? 1 : (b2 || f == 2) ? 2 : f;
         if (p == 0) {
           topc[2] = topc[1];
+          topk[2] = topk[1];
           topd[2] = topd[1];
           topc[1] = topc[0];
+          topk[1] = topk[0];
           topd[1] = topd[0];
           topc[0] = cj;
+          topk[0] = kj;
           topd[0] = dj;
         } else if (p == 1) {
           topc[2] = topc[1];
+          topk[2] = topk[1];
           topd[2] = topd[1];
           topc[1] = cj;
+          topk[1] = kj;
           topd[1] = dj;
         } else if (p == 2) {
           topc[2] = cj;
+          topk[2] = kj;
           topd[2] = dj;
         }
       }
@@ -954,7 +1071,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
           return allele_byte(R, *ref_src, pos, 0, i);
         };
         CallRec rr;
-        rr.key = (ord << 12) | ((uint64_t)sm << 4) | (uint64_t)sub;
+        rr.key = (ord << 12) | ((uint64_t)rank_sm << 4) | (uint64_t)sub;  // bySample order
         rr.contig = tl.contig;
         rr.pos = pos;
         rr.sample = (uint8_t)sm;
@@ -1825,6 +1942,17 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   d->d.md_len = h->md_len;
   d->d.n_contigs = h->n_contigs;
   d->d.n_samples = h->n_samples;
+  if (h->sample_hash && h->n_samples > 0) {  // a few words: one synchronous copy
+    void *sh = nullptr;
+    if (hipMalloc(&sh, sizeof(uint32_t) * (size_t)h->n_samples) != hipSuccess ||
+        hipMemcpy(sh, h->sample_hash, sizeof(uint32_t) * (size_t)h->n_samples, hipMemcpyHostToDevice) != hipSuccess) {
+      if (sh) (void)hipFree(sh);
+      gq_reads_free(d);
+      return set_err(GQ_E_HIP, "gq_reads_upload: sample hashes");
+    }
+    d->owned.push_back(sh);
+    d->d.sample_hash = (const uint32_t *)sh;
+  }
   d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
   d->seq_bytes = h->seq_bytes;
   gq_status st2 = derive_shape(c, d, h->md_len);
@@ -1867,6 +1995,7 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   d->d.qual = h->qual;
   d->d.cigar = h->cigar;
   d->d.md_ev = h->md_ev;
+  d->d.sample_hash = h->sample_hash;  // device pointer (or NULL), as every array here
   d->contig_read_begin.resize((size_t)h->n_contigs + 1);
   hipError_t e = hipMemcpy(d->contig_read_begin.data(), h->contig_read_begin,
                            sizeof(int64_t) * ((size_t)h->n_contigs + 1), hipMemcpyDeviceToHost);
@@ -2076,7 +2205,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
                        (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap,
-                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg());
+                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg(), SomWin{});
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
@@ -2121,12 +2250,20 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
         free(res);
         return st;
       }
+      // the windows' element order (initial groups in heap order), for the first occurrences
+      // the Scala map orders of the listed loci depend on
+      SomWin sw{};
+      st = build_somwin(c, pl, rd, rd, sw);
+      if (st) {
+        free(res);
+        return st;
+      }
       const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 4096);
       hipLaunchKernelGGL(germline_complex, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                          (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
                          (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
                          (unsigned long long)0, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p,
-                         (int64_t)amb.size(), gq_dbg());
+                         (int64_t)amb.size(), gq_dbg(), sw);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));

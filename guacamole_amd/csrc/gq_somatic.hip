@@ -37,6 +37,7 @@
 #include "gq_alleles.h"
 #include "gq_host.h"
 #include "gq_strictmath.h"
+#include "gq_scala_order.h"
 
 // The caller's FP64 arithmetic must round like the reference's: no fused multiply-add
 // anywhere in this file (e.g. (agg + 0) - ln2 * depth would otherwise contract).
@@ -45,6 +46,8 @@
 using namespace gq;
 
 namespace {
+
+#include "gq_winorder.h"
 
 constexpr int kSomT = 1024;
 constexpr int kEvCap = 1024;  // allele-supporting elements per sample held in LDS for medians
@@ -291,15 +294,6 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Value of lane j (wave-uniform j) broadcast to every lane, for 64-bit types.
-__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int j) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-__device__ __forceinline__ double lane_f64(double v, int j) {
-  return __builtin_bit_cast(double, lane_u64(__builtin_bit_cast(uint64_t, v), j));
-}
 
 // ADAM PhredUtils.phredToSuccessProbability, 1 - 10^(-q/10) for q in [0, 255] (restated in
 // oracle/oracle.cpp:201-207): a table filled on the host with the host's pow, so the device
@@ -362,117 +356,6 @@ __device__ __forceinline__ bool allele_std_alt(const DevReads &R, const AlleleDe
 
 __device__ void raise_at(Counters *ctr, int code, int64_t where) {
   raise_error(&ctr->err, (int64_t *)&ctr->err_pos, code, where);
-}
-
-// ------------------------------------------------------------------------------------------
-// Pileup element order.  Pileup.atGreaterLocus (Pileup.scala:103-132) keeps the surviving
-// elements in order and appends new reads in start order, and the first pileup of a window
-// (one per task and contig) takes the reads in SlidingWindow.currentRegions() order: the
-// priority queue's heap array after enqueueing, in start order, the reads that overlap the
-// window's first visited locus F (DistributedUtil.scala:260-274).  So at any locus the
-// elements are the reads of that initial group still covering it, in heap order, then the
-// other covering reads in read order.  The order matters for the FP sums (Likelihood,
-// AlleleEvidence mean); it is restored here from the per-window initial ranks.
-// ------------------------------------------------------------------------------------------
-struct WinInit {
-  int32_t F;    // first visited locus of the window (INT32_MAX: none)
-  int32_t E;    // largest end of this set's initial-group reads (loci >= E hold none of them)
-  int64_t off;  // the group's reads (ascending) and heap ranks at init_reads / init_rank [off, off + n)
-  int32_t n, cap;
-};
-
-// F of each window over both read sets (the first locus of its ranges covered by a read of
-// either set), and each set's candidate reads for the group (prefix-max end past F, start at
-// or before F): their count is the group's capacity.  One thread per window.
-__global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t *__restrict__ w_roff,
-                             const int64_t *__restrict__ r_s, const int64_t *__restrict__ r_e, int64_t n_win,
-                             DevReads RT, DevReads RN, WinInit *__restrict__ wi, int64_t *__restrict__ wi_lo) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= n_win) return;
-  const int32_t c = w_contig[w];
-  int64_t F = INT32_MAX;
-  for (int s = 0; s < 2; ++s) {
-    const DevReads &R = s ? RN : RT;
-    const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
-    for (int64_t k = w_roff[w]; k < w_roff[w + 1]; ++k) {
-      const int64_t a = r_s[k];
-      if (a >= F) break;
-      int64_t lo = cb, hi = ce;  // first read with pmax_end > a: it covers max(a, its start)
-      while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if ((int64_t)R.pmax_end[m] > a) hi = m;
-        else lo = m + 1;
-      }
-      if (lo < ce) {
-        const int64_t f = max(a, (int64_t)R.start[lo]);
-        if (f < r_e[k]) {
-          F = min(F, f);
-          break;
-        }
-      }
-    }
-  }
-  for (int s = 0; s < 2; ++s) {
-    const DevReads &R = s ? RN : RT;
-    WinInit x{(int32_t)F, INT32_MIN, 0, 0, 0};
-    int64_t lo = 0;
-    if (F < INT32_MAX) {
-      const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
-      int64_t a = cb, b = ce;
-      while (a < b) {  // first read with pmax_end > F
-        const int64_t m = (a + b) >> 1;
-        if ((int64_t)R.pmax_end[m] > F) b = m;
-        else a = m + 1;
-      }
-      lo = a;
-      b = ce;
-      while (a < b) {  // first read with start > F
-        const int64_t m = (a + b) >> 1;
-        if ((int64_t)R.start[m] > F) b = m;
-        else a = m + 1;
-      }
-      x.cap = (int32_t)min<int64_t>(a - lo, INT32_MAX);
-    }
-    wi[2 * w + s] = x;
-    wi_lo[2 * w + s] = lo;
-  }
-}
-
-// The initial group of each (window, set): reads [lo, lo + cap) that overlap F, enqueued in
-// read order into an empty Scala PriorityQueue (fixUp while the parent's end is larger,
-// SlidingWindow.scala:62-68); rank = position in the heap array.  One thread per (window, set).
-__global__ void window_group(WinInit *__restrict__ wi, const int64_t *__restrict__ wi_lo, int64_t n,
-                             DevReads RT, DevReads RN, int64_t *__restrict__ init_reads,
-                             int32_t *__restrict__ init_rank, int32_t *__restrict__ heap) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  WinInit x = wi[k];
-  const DevReads &R = (k & 1) ? RN : RT;
-  int64_t *rd = init_reads + x.off;
-  int32_t *rk = init_rank + x.off;
-  int32_t *h = heap + x.off;  // heap of group positions, 0-based (h[i] <-> Scala index i + 1)
-  int32_t m = 0;
-  int32_t E = INT32_MIN;
-  for (int64_t i = 0; i < x.cap; ++i) {
-    const int64_t r = wi_lo[k] + i;
-    if (R.end[r] <= x.F) continue;
-    rd[m] = r;
-    E = max(E, R.end[r]);
-    int32_t q = m++;
-    h[q] = q;
-    while (q > 0) {
-      const int32_t p = (q + 1) / 2 - 1;
-      if (!(R.end[rd[h[q]]] < R.end[rd[h[p]]])) break;
-      const int32_t t = h[q];
-      h[q] = h[p];
-      h[p] = t;
-      q = p;
-    }
-  }
-  for (int32_t i = 0; i < m; ++i) rk[h[i]] = i;
-  x.n = m;
-  x.E = E;
-  wi[k] = x;
 }
 
 // The reads of a tile window [rb, re) covering pos, compacted into a per-wave LDS list (tile-
@@ -987,191 +870,11 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
 
 constexpr int kSomWaves = kBlock / 64;
 
-// Per-window data of the element order (window_first / window_group), by tile range.
-struct SomWin {
-  const int32_t *range_win;  // plan range -> window
-  const WinInit *wi;         // [window * 2 + set]
-  const int64_t *init_reads;
-  const int32_t *init_rank;
-};
-
 #ifndef GQ_CALL_WPE
 #define GQ_CALL_WPE 3  // waves per SIMD the register budget must allow
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_WPE))) void somatic_call(const Tile *__restrict__ tiles_t,
-                                                       const Tile *__restrict__ tiles_n,
-                                                       const ComplexItem *__restrict__ items, DevReads RT,
-                                                       DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
-                                                       unsigned long long rec_cap, uint8_t *__restrict__ pool,
-                                                       unsigned long long pool_cap, OutGeom og,
-                                                       Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out,
-                                                       unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
-                                                       const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
-                                                       RefView ref, int dbg) {
-  // amb_in == nullptr: every candidate; where a sample's reads' MD-derived bases disagree the
-  // locus is only listed (amb_out) for the heap-order replay.  amb_in != nullptr: the listed
-  // loci, with both samples' reference bases resolved in heap order (amb_ref[2 i + set]).
-  // ref.b != nullptr: every pileup's reference base is the reference genome's (nothing listed).
-  __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
-  __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
-  __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
-  __shared__ int32_t cover_t[kSomWaves][kCover], cover_n[kSomWaves][kCover];
-  __shared__ double ll_lds[kSomWaves][kMaxG];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // candidates: the partitioned items of somatic_proj / somatic_tile (part_scan: kept counts)
-  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
-  // dbg & 16: phase clocks per candidate (covers, pileups, tumor genotypes, normal genotypes,
-  // evidence + record, candidates) into ctr->prof
-  uint64_t clk[6] = {0, 0, 0, 0, 0, 0}, tk = 0;
-  auto tick = [&](int k) {
-    if (dbg & 16) {
-      const uint64_t t = __builtin_readcyclecounter();
-      if (k >= 0) clk[k] += t - tk;
-      tk = t;
-    }
-  };
-  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
-    tick(-1);
-    if (dbg & 16) clk[5] += 1;
-    const int64_t it = amb_in ? amb_in[li].item : li;
-    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
-    const Tile tt = tiles_t[item.tile], tn = tiles_n[item.tile];
-    const int32_t pos = item.pos;
-    const int32_t win = sw.range_win[tt.range];
-    const Cover ct = make_cover(RT, tt.rb, tt.re, pos, cover_t[wv], ev_lds[wv], sw.wi[2 * win], sw.init_reads,
-                                sw.init_rank, ctr);
-    const Cover cn = make_cover(RN, tn.rb, tn.re, pos, cover_n[wv], ev_lds[wv], sw.wi[2 * win + 1], sw.init_reads,
-                                sw.init_rank, ctr);
-    tick(0);
-    SamplePile PT, PN;
-    const int fb = ref.b ? (int)ref.b[ref.off[tt.contig] + pos] : -1;
-    gather_sample(RT, ct, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li] : fb, ctr, PT);
-    gather_sample(RN, cn, pos, prm.min_mapq, amb_in ? (int)amb_ref[2 * li + 1] : fb, ctr, PN);
-    if (fb >= 0) PT.ambiguous = PN.ambiguous = false;
-    tick(1);
-    if (PT.overflow || PN.overflow) {
-      raise_at(ctr, GQ_E_CAPACITY, pos);
-      continue;
-    }
-    if ((item.flags & 1) && !amb_in && (PT.depth_all + PN.depth_all) > 0 && lane == 0)
-      atomicAdd(&ctr->spread[0][it & (kSpread - 1)], 1ull);
-    if (!amb_in && (PT.ambiguous || PN.ambiguous)) {  // heap order decides a reference base: list it
-      if (lane == 0) {
-        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
-        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
-      }
-      continue;
-    }
-    // MultiAllelicPileupFilter (PileupFilter.scala:29-44): > 2 distinct alleles => no elements
-    if (prm.filter_multi_allelic) {
-      if (PT.nt > 2) PT.depth_f = 0;
-      if (PN.nt > 2) PN.depth_f = 0;
-    }
-    // SomaticStandardCaller.scala:184-190
-    if (PT.depth_f == 0 || PN.depth_f == 0 || (int64_t)PT.depth_f > (int64_t)prm.max_read_depth ||
-        (int64_t)PN.depth_f > (int64_t)prm.max_read_depth)
-      continue;
-    {  // tumor pileup must hold a non-Match element: Match = allele (ref, ref) of one byte
-      uint32_t ref_match = 0;
-#pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
-        const bool m = (s * 64 + lane) < PT.nt && PT.desc[s].kind == K_SNV && PT.desc[s].base == PT.refbase;
-        ref_match += (uint32_t)wave_sum(m ? (double)PT.n_f[s] : 0.0);
-      }
-      if (ref_match == PT.depth_f) continue;
-    }
-    const GenoResult tg = genotypes(RT, PT, ct, pos, prm.min_mapq, true, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
-    tick(2);
-    if (tg.G == 0) continue;
-    const bool t_var = var_lds[wv][tg.bi] || var_lds[wv][tg.bj];
-    if (!t_var) continue;
-    const AlleleDesc a1 = pile_desc(PT, tg.bi), a2 = pile_desc(PT, tg.bj);
-    const GenoResult ng = genotypes(RN, PN, cn, pos, prm.min_mapq, false, order_lds[wv], var_lds[wv], ll_lds[wv], ctr);
-    tick(3);
-    const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
-    const double odds = tg.best_l / nvs;
-    if (!(odds * 100.0 >= (double)prm.odds)) continue;
-    // decisions taken within FP rounding of a threshold are flagged (GQ_FLAG_KNIFE_EDGE)
-    uint8_t knife = near_edge(odds * 100.0, (double)prm.odds) ? GQ_FLAG_KNIFE_EDGE : 0;
-    // first variant allele of the ML genotype with a non-empty alt (SomaticStandardCaller.scala:227)
-    const bool v1 = allele_is_variant(RT, a1, pos) && allele_alt_len(a1) > 0;
-    const bool v2 = allele_is_variant(RT, a2, pos) && allele_alt_len(a2) > 0;
-    if (!v1 && !v2) continue;
-    const AlleleDesc al = v1 ? a1 : a2;
-    const int rl = allele_ref_len(al), alt_l = allele_alt_len(al);
-    const Key128 tkey = allele_key(RT, al, pos, 0);
-    const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
-    gq_evidence tev, nev;
-    allele_evidence(RT, ct, pos, prm.min_mapq, PT, tkey, tg.best_l, ev_lds[wv], ctr, tev);
-    allele_evidence(RN, cn, pos, prm.min_mapq, PN, nkey, 1.0 - nvs, ev_lds[wv], ctr, nev);
-    const double log_odds = sm::log(odds);
-    const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
-    if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
-    const float vaf = (float)tev.allele_read_depth / (float)tev.read_depth;
-    if (prm.apply_filters == 1) {  // SomaticStandardCaller.scala:124-137 then SomaticGenotypeFilter.apply (:285-307)
-      const bool depth_ok = tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
-                            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF;
-      if (!depth_ok) continue;
-      if (!(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth)) continue;
-      if (!(log_odds > (double)prm.min_lod)) continue;
-      if (near_edge(log_odds, (double)prm.min_lod)) knife |= GQ_FLAG_KNIFE_EDGE;
-      if (!(gqv >= prm.min_likelihood)) continue;
-      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
-      if (!(tev.mean_mq >= prm.min_average_mapping_quality && nev.mean_mq >= prm.min_average_mapping_quality)) continue;
-      if (near_edge(tev.mean_mq, prm.min_average_mapping_quality) || near_edge(nev.mean_mq, prm.min_average_mapping_quality) ||
-          near_edge(tev.mean_mq, prm.min_average_base_quality) || near_edge(nev.mean_mq, prm.min_average_base_quality))
-        knife |= GQ_FLAG_KNIFE_EDGE;
-      // the "average base quality" filter tests mean mapping quality (SomaticGenotypeFilter.scala:194-195)
-      if (!(tev.mean_mq >= prm.min_average_base_quality && nev.mean_mq >= prm.min_average_base_quality)) continue;
-      if (!(tev.median_mismatches <= (double)prm.max_median_mismatches)) continue;
-    } else if (prm.apply_filters == 2) {  // SomaticGenotypeFilter(Seq, ...) as the caller suite uses it
-      if (!(tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
-            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF))
-        continue;
-      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
-      if (!(gqv >= prm.min_likelihood)) continue;
-      if (prm.min_tumor_alternate_read_depth > 0 && !(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth))
-        continue;
-    }
-    SomRec rr;
-    rr.key = (uint64_t)(tt.ordinal0 + (pos - tt.L0)) << 12;
-    rr.contig = tt.contig;
-    rr.pos = pos;
-    rr.ref_len = (uint16_t)rl;
-    rr.alt_len = (uint16_t)alt_l;
-    rr.flags = (PT.ambiguous ? 1 : 0) | (PN.ambiguous ? 2 : 0) | knife;
-    rr.pad[0] = rr.pad[1] = rr.pad[2] = 0;
-    rr.log_odds = log_odds;
-    rr.gq = gqv;
-    rr.pad2 = 0;
-    rr.tumor = tev;
-    rr.normal = nev;
-    if (rl + alt_l <= 8) {
-      uint64_t v = 0;
-      int j = 0;
-      for (int i = 0; i < rl; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 0, i) << (8 * j++);
-      for (int i = 0; i < alt_l; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 1, i) << (8 * j++);
-      rr.allele = v;
-    } else {
-      unsigned long long off = 0;
-      if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + alt_l));
-      off = __shfl(off, 0, 64);
-      if (off + rl + alt_l <= pool_cap)
-        for (int i = lane; i < rl + alt_l; i += 64)
-          pool[off + i] = i < rl ? allele_byte(RT, al, pos, 0, i) : allele_byte(RT, al, pos, 1, i - rl);
-      rr.allele = off;
-    }
-    if (lane == 0) {
-      const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
-      if (k < rec_cap) recs[k] = rr;
-    }
-    tick(4);
-  }
-  if ((dbg & 16) && lane == 0 && clk[5])
-    for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
-}
+
+#include "gq_somatic_call.h"
 
 // ---- germline-standard: GermlineStandard.Caller.callVariantsAtLocus
 // (commands/GermlineStandardCaller.scala:90-124) + GenotypeFilter (filters/GenotypeFilter.scala:
@@ -1439,57 +1142,6 @@ __global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__res
   }
 }
 
-// The pileup element order of a plan's windows (SomWin): each window's first visited locus and
-// its initial (heap-ordered) group of reads, for the two read sets t and n.
-gq_status build_somwin(gq_ctx *c, const Plan &pt, const gq_dev_reads *t, const gq_dev_reads *n, SomWin &sw) {
-  {
-    const int64_t nw = (int64_t)pt.wins.size(), nr = (int64_t)pt.rs.size();
-    std::vector<int32_t> w_contig((size_t)nw);
-    std::vector<int64_t> w_roff((size_t)nw + 1);
-    for (int64_t w = 0; w < nw; ++w) {
-      w_contig[(size_t)w] = pt.wins[(size_t)w].contig;
-      w_roff[(size_t)w] = pt.wins[(size_t)w].r0;
-    }
-    w_roff[(size_t)nw] = nr;
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t o_roff = al(4 * (size_t)nw), o_rs = o_roff + al(8 * ((size_t)nw + 1)), o_re = o_rs + al(8 * (size_t)nr),
-                 o_rw = o_re + al(8 * (size_t)nr), o_wi = o_rw + al(4 * (size_t)nr),
-                 o_lo = o_wi + al(sizeof(WinInit) * 2 * (size_t)nw), o_end = o_lo + al(8 * 2 * (size_t)nw);
-    HIP_TRY(c->win_meta.ensure(o_end));
-    char *b = (char *)c->win_meta.p;
-    HIP_TRY(hipMemcpyAsync(b, w_contig.data(), 4 * (size_t)nw, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_roff, w_roff.data(), 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_rs, pt.rs.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_re, pt.re.data(), 8 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(b + o_rw, pt.rwin.data(), 4 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
-    WinInit *d_wi = (WinInit *)(b + o_wi);
-    int64_t *d_lo = (int64_t *)(b + o_lo);
-    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                       (const int32_t *)b, (const int64_t *)(b + o_roff), (const int64_t *)(b + o_rs),
-                       (const int64_t *)(b + o_re), nw, t->d, n->d, d_wi, d_lo);
-    HIP_TRY(hipGetLastError());
-    std::vector<WinInit> wi((size_t)(2 * nw));
-    HIP_TRY(hipMemcpyAsync(wi.data(), d_wi, sizeof(WinInit) * wi.size(), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    int64_t tot = 0;
-    for (WinInit &x : wi) {
-      x.off = tot;
-      tot += x.cap;
-    }
-    HIP_TRY(hipMemcpyAsync(d_wi, wi.data(), sizeof(WinInit) * wi.size(), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c->win_grp.ensure((size_t)std::max<int64_t>(tot, 1) * 16));
-    int64_t *d_reads = (int64_t *)c->win_grp.p;
-    int32_t *d_rank = (int32_t *)(d_reads + std::max<int64_t>(tot, 1));
-    int32_t *d_heap = d_rank + std::max<int64_t>(tot, 1);
-    hipLaunchKernelGGL(window_group, dim3((unsigned)((2 * nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
-                       d_wi, (const int64_t *)d_lo, 2 * nw, t->d, n->d, d_reads, d_rank, d_heap);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));  // wi (host) outlives its copy
-    sw = SomWin{(const int32_t *)(b + o_rw), d_wi, d_reads, d_rank};
-  }
-  return GQ_OK;
-}
-
 gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq, bool incl_align = true) {
   const int key = 2 * min_mapq + (incl_align ? 1 : 0);  // the projection's filter and probability model
   if (t->mproj && t->mproj_mapq == key) return GQ_OK;
@@ -1579,7 +1231,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   if (t->d.n_contigs != n->d.n_contigs)
     return set_err(GQ_E_ARG, "tumor and normal read sets must share the contig list (%d vs %d contigs)",
                    t->d.n_contigs, n->d.n_contigs);
-  static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
+  const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only (read per call)
   RefView rv{nullptr, nullptr};
   std::vector<int32_t> lc;
   std::vector<int64_t> ls, le, lt;
@@ -1693,7 +1345,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     og.capA[1] = wg_loci / 16 + 256;
     og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;
   }
-  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096;
+  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096, deep_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
@@ -1737,24 +1389,60 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
         continue;
       }
     }
+    // the exact caller: the fast kernel (pileups up to kFastCap reads per sample, element
+    // records in LDS), then the deep kernel over the deeper candidates it listed, then the
+    // deep kernel again over the loci whose reference base heap order decides
+    HIP_TRY(c->deep_list.ensure(deep_cap * sizeof(int64_t)));
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
-    hipLaunchKernelGGL(somatic_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+    hipLaunchKernelGGL(somatic_call_k<false>, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                        (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                        (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
-                       rv, dbg);
+                       rv, dbg, DeepIO{(int64_t *)c->deep_list.p, deep_cap, 0, nullptr, 0, 0});
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     bool retry = false;
+    if (hc.n_deep > deep_cap) {
+      deep_cap = hc.n_deep + 1024;
+      retry = true;
+    }
+    // the deep kernel's per-wave scratch: the deepest listed pileup (at least kFastCap: the
+    // genotype keys share its evidence words)
+    auto run_deep = [&](int64_t n_items, const AmbItem *ain, const uint8_t *aref) -> gq_status {
+      const int scap = (int)std::max<unsigned long long>(hc.deep_max, (unsigned long long)kFastCap);
+      const int64_t nw = std::min<int64_t>(n_items, 4096);
+      const size_t wb = deep_wave_bytes(scap, kMaxG);
+      HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
+      const unsigned blocks = (unsigned)((nw + kSomWaves - 1) / kSomWaves);
+      hipLaunchKernelGGL(somatic_call_k<true>, dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
+                         (AmbItem *)(ain ? nullptr : c->amb.p), ain ? (unsigned long long)0 : amb_cap, ain, aref,
+                         ain ? n_items : (int64_t)0, ain ? RefView{nullptr, nullptr} : rv, dbg,
+                         DeepIO{(int64_t *)c->deep_list.p, 0, ain ? 0 : n_items, (uint8_t *)c->deep_scratch.p, scap,
+                                kMaxG});
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      return GQ_OK;
+    };
+    if (!retry && hc.n_deep > 0 && !hc.err) {
+      st = run_deep((int64_t)hc.n_deep, nullptr, nullptr);
+      if (st) {
+        free(res);
+        return st;
+      }
+    }
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;
       retry = true;
     }
     if (!retry && hc.n_amb > 0 && !hc.err) {
       // loci where a sample's reference base depends on heap order: replay both windows'
-      // queues, then the caller again over just those loci with the resolved bases
+      // queues, then the deep caller over just those loci with the resolved bases
       std::vector<AmbItem> amb((size_t)hc.n_amb);
       HIP_TRY(hipMemcpyAsync(amb.data(), c->amb.p, amb.size() * sizeof(AmbItem), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1764,16 +1452,11 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
         free(res);
         return st;
       }
-      const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 8192);
-      hipLaunchKernelGGL(somatic_call, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
-                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
-                         (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
-                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), RefView{nullptr, nullptr}, dbg);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      st = run_deep((int64_t)amb.size(), (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p);
+      if (st) {
+        free(res);
+        return st;
+      }
     }
     if (hc.n_rec > rec_cap) {
       rec_cap = hc.n_rec + 1024;
@@ -1791,8 +1474,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
   if ((dbg & 16) && hc.prof[5])
-    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): covers %.0f pileups %.0f tumor-genotypes %.0f "
-            "normal-genotypes %.0f evidence %.0f (%llu candidates reached)\n", (double)hc.prof[0] / hc.prof[5],
+    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): covers %.0f elements %.0f tables %.0f "
+            "tumor-genotypes %.0f normal-genotypes+evidence %.0f (%llu candidates reached)\n", (double)hc.prof[0] / hc.prof[5],
             (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5], (double)hc.prof[3] / hc.prof[5],
             (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
   st = check_device_error(c, hc);
@@ -2062,7 +1745,7 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
     og.capA[1] = wg_loci / 16 + 256;
     og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;
   }
-  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096;
+  unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096, deep_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));

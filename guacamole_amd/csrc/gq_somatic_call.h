@@ -1,0 +1,932 @@
+// gq_somatic_call.h — somatic_call: the exact per-candidate caller of somatic-standard
+// (SomaticStandard.Caller.findPotentialVariantAtLocus + the driver's filters,
+// commands/SomaticStandardCaller.scala:124-245; Likelihood.scala:99-201; AlleleEvidence.scala:
+// 58-101), one wave per candidate locus.  Included by gq_somatic.hip inside its anonymous
+// namespace, after the helpers it uses (WinInit, SomWin, phred_success, success_to_phred).
+//
+// Each covering read is classified ONCE: the wave walks both samples' covering reads together
+// (the two samples' searches, scans and per-read loads in the same latency rounds), stores one
+// 16-byte element record per read in pileup element order, and every later step — the
+// pileup reference base, the allele table, the filters, both likelihood folds, the evidence —
+// reads those records instead of re-walking CIGARs and MD tags.
+//
+// Two instantiations:
+//   DEEP = false  records in LDS, kFastCap elements per sample; a candidate whose pileup is
+//                 deeper is appended to the deep list (counted visit and all, it is wholly the
+//                 deep kernel's);
+//   DEEP = true   records in a global scratch slice per wave sized on the host from the deepest
+//                 listed pileup: no depth limit.  Also runs the heap-order loci (amb_in).
+#pragma once
+
+constexpr int kFastCap = 128;  // elements per sample held in LDS by the fast kernel
+
+// Element record (16 bytes), one per covering read in pileup element order:
+//   x  rp    read position of the element (SNV / DEL: its base; INS: its first alt byte)
+//   y  aux   INS: alt bytes; DEL: deleted length
+//   z  base | kind << 8 | quality (as a signed byte) << 16 | mapq << 24
+//   w  n_mismatch | flags << 16 | table index << 24
+constexpr uint32_t kElAct = 1u, kElPass = 2u, kElFwd = 4u;
+__device__ __forceinline__ int el_q(const uint4 &e) { return (int)(int8_t)(uint8_t)(e.z >> 16); }
+__device__ __forceinline__ int el_mq(const uint4 &e) { return (int)(e.z >> 24); }
+__device__ __forceinline__ uint32_t el_flags(const uint4 &e) { return (e.w >> 16) & 0xFFu; }
+__device__ __forceinline__ int el_tidx(const uint4 &e) { return (int)(e.w >> 24); }
+
+// Per-wave working memory (LDS for the fast kernel, a global scratch slice for the deep one).
+struct CallMem {
+  int32_t *cov[2];  // [cap] covering reads (offset from the tile's rb), pileup element order
+  uint4 *el[2];     // [cap] element records
+  uint32_t *tmp;    // [2 cap] heap-order reorder / evidence values
+  int16_t *order;   // [64 kSlots]
+  uint8_t *is_var;  // [64 kSlots]
+  double *ll;       // [maxG]
+  double *terms;    // [3 cap] per element: log(2(1 - pc)), log(pc + (1 - pc)), log(2 pc) (0 when filtered out)
+  int cap, maxG;
+};
+
+// Deep-kernel scratch geometry: bytes per wave for `cap` elements per sample.
+__host__ __device__ __forceinline__ size_t deep_wave_bytes(int cap, int maxG) {
+  return (size_t)cap * (2 * 4 + 2 * 16 + 2 * 4 + 3 * 8) + 64 * kSlots * 3 + (size_t)maxG * 8 + 64;
+}
+__device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
+  CallMem m;
+  uint8_t *p = base;
+  m.el[0] = (uint4 *)p;
+  p += (size_t)cap * 16;
+  m.el[1] = (uint4 *)p;
+  p += (size_t)cap * 16;
+  m.ll = (double *)p;
+  p += (size_t)maxG * 8;
+  m.terms = (double *)p;
+  p += (size_t)cap * 24;
+  m.cov[0] = (int32_t *)p;
+  p += (size_t)cap * 4;
+  m.cov[1] = (int32_t *)p;
+  p += (size_t)cap * 4;
+  m.tmp = (uint32_t *)p;
+  p += (size_t)cap * 8;
+  m.order = (int16_t *)p;
+  p += 64 * kSlots * 2;
+  m.is_var = p;
+  m.cap = cap;
+  m.maxG = maxG;
+  return m;
+}
+
+// K lockstep wave_first_true searches (each over its own [lo, hi)): every round issues all
+// unfinished searches' probes before any ballot is read.  pred(k, index) is monotone.
+template <int K, class P>
+__device__ __forceinline__ void wave_first_true_k(const int64_t (&lo0)[K], const int64_t (&hi0)[K], P &&pred,
+                                                  int64_t (&out)[K]) {
+  const int lane = threadIdx.x & 63;
+  int64_t lo[K], hi[K];
+  bool done[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    lo[k] = lo0[k];
+    hi[k] = hi0[k];
+    done[k] = false;
+    out[k] = hi0[k];
+  }
+  for (;;) {
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) all = all && done[k];
+    if (all) break;
+    bool hit[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t s = hi[k] - lo[k] > 64 ? (hi[k] - lo[k] + 63) / 64 : 1;
+      const int64_t p = lo[k] + (int64_t)lane * s;
+      hit[k] = !done[k] && (p >= hi[k] || pred(k, p));
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (done[k]) continue;
+      const unsigned long long b = __ballot(hit[k]);
+      if (hi[k] - lo[k] > 64) {
+        const int64_t step = (hi[k] - lo[k] + 63) / 64;
+        if (!b) {
+          lo[k] = lo[k] + 63 * step + 1;
+          continue;
+        }
+        const int f = __ffsll((long long)b) - 1;
+        if (f == 0) {
+          out[k] = lo[k];
+          done[k] = true;
+          continue;
+        }
+        const int64_t nh = lo[k] + (int64_t)f * step;
+        lo[k] = lo[k] + (int64_t)(f - 1) * step + 1;
+        hi[k] = nh < hi[k] ? nh : hi[k];
+      } else {
+        out[k] = b ? lo[k] + (__ffsll((long long)b) - 1) : hi[k];
+        done[k] = true;
+      }
+    }
+  }
+}
+
+// The pileup's allele table (a sample's distinct alleles; entry j on lane j & 63, register
+// slot j >> 6) and its totals.
+template <int NS>
+struct Pile {
+  static constexpr int kNS = NS;
+  uint64_t klo[NS], khi[NS];
+  AlleleDesc desc[NS];
+  uint32_t n_all[NS], n_f[NS];
+  int nt;
+  uint32_t depth_all, depth_f, fwd_f;
+  uint8_t refbase;
+  bool ambiguous, overflow;
+};
+
+template <int NS>
+__device__ __forceinline__ AlleleDesc pile_entry(const Pile<NS> &P, int j) {
+  AlleleDesc d{};
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s == (j >> 6)) {
+      const int o = j & 63;
+      d.read = __shfl(P.desc[s].read, o, 64);
+      d.aux = __shfl(P.desc[s].aux, o, 64);
+      d.rp = __shfl(P.desc[s].rp, o, 64);
+      d.kind = (uint8_t)__shfl((int)P.desc[s].kind, o, 64);
+      d.rb = (uint8_t)__shfl((int)P.desc[s].rb, o, 64);
+      d.base = (uint8_t)__shfl((int)P.desc[s].base, o, 64);
+    }
+  return d;
+}
+
+// Table index of `key` in P (-1: absent).
+template <int NS>
+__device__ __forceinline__ int pile_find(const Pile<NS> &P, Key128 key) {
+  const int lane = threadIdx.x & 63;
+  int found = -1;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const unsigned long long hb = __ballot((s * 64 + lane) < P.nt && P.klo[s] == key.lo && P.khi[s] == key.hi);
+    if (found < 0 && hb) found = s * 64 + (__ffsll((long long)hb) - 1);
+  }
+  return found;
+}
+
+
+struct GenoOut {
+  int n, G, best_g, bi, bj;
+  double best_l, var_sum;
+  bool order_tie;  // two variant genotypes with equal immutable-map keys (insertion order used)
+};
+
+// Likelihood.likelihoodsOfAllPossibleGenotypesFromPileup (normalised, not log space) over the
+// sample's filtered elements (records in `el`, n of them).  Eligible alleles (filtered count
+// > 0, standard alt bases, Likelihood.scala:106) ranked by Allele order; genotype g <-> (i <= j)
+// in the reference's enumeration order; the per-genotype row fold is Colt's aggregate (the LAST
+// element first, Likelihood.scala:185) with StrictMath log; normalisation in the reference's
+// order (:190-199); maxBy = the first maximum.  The normal's variant mass (with_var_sum) adds
+// the variant genotypes' likelihoods in the iteration order of the immutable Map `toMap`
+// builds (SomaticStandardCaller.scala:206-217): generation order up to four genotypes, the
+// HashTrieMap's beyond (gq_scala_order.h).
+template <int NS>
+__device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS> &P, const uint4 *el, int n_el, int32_t pos,
+                                                bool include_alignment, bool with_var_sum, CallMem &m, Counters *ctr) {
+  const int lane = threadIdx.x & 63;
+  GenoOut res{};
+  bool elig[NS], var[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int j = s * 64 + lane;
+    elig[s] = j < P.nt && P.n_f[s] > 0 && allele_std_alt(R, P.desc[s], pos);
+    var[s] = j < P.nt && allele_is_variant(R, P.desc[s], pos);
+  }
+  int n = 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) n += __popcll(__ballot(elig[s]));
+  res.n = n;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int rank = 0;
+    for (int k = 0; k < P.nt; ++k) {
+      bool ek = false;
+#pragma unroll
+      for (int t = 0; t < NS; ++t)
+        if (t == (k >> 6)) ek = __shfl((int)elig[t], k & 63, 64);
+      if (!ek) continue;  // uniform
+      const AlleleDesc dk = pile_entry(P, k);
+      if (elig[s] && k != s * 64 + lane && allele_cmp(R, dk, P.desc[s], pos) < 0) ++rank;
+    }
+    if (elig[s]) m.order[rank] = (int16_t)(s * 64 + lane);
+    if (s * 64 + lane < 64 * NS) m.is_var[s * 64 + lane] = var[s] ? 1 : 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const int G = n * (n + 1) / 2;
+  res.G = G;
+  if (G == 0) return res;
+  if (G > m.maxG) {
+    raise_at(ctr, GQ_E_CAPACITY, pos);
+    res.G = 0;
+    return res;
+  }
+  const double ln2d = sm::log(2.0) * (double)P.depth_f;
+  // the three possible log terms of each element (lanes = elements), 0 for an element the
+  // mapq filter drops: starting the fold at +0.0 and adding 0.0 for those is bit-identical
+  // to Colt's fold over the filtered elements (no term is -0.0)
+  for (int c0 = 0; c0 < n_el; c0 += 64) {
+    const int k = c0 + lane;
+    if (k >= n_el) continue;
+    const uint4 e = el[k];
+    const uint32_t fl = el_flags(e);
+    double t2 = 0.0, th = 0.0, t0 = 0.0;
+    if ((fl & kElAct) && (fl & kElPass)) {
+      const int q = el_q(e);
+      if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
+      double pc = phred_success(q);
+      if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
+      const double pw = 1.0 - pc;
+      t2 = sm::log(pc + pc);
+      th = sm::log(pc + pw);
+      t0 = sm::log(pw + pw);
+    }
+    m.terms[3 * k] = t0;
+    m.terms[3 * k + 1] = th;
+    m.terms[3 * k + 2] = t2;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const int g = g0 + lane;
+    int i = 0, j = 0;
+    if (g < G) genotype_index(g, n, i, j);
+    const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
+    double agg = 0.0;
+#pragma unroll 4
+    for (int k = n_el - 1; k >= 0; --k) {
+      const int tj = el_tidx(el[k]);
+      const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
+      agg = agg + m.terms[3 * k + sel];
+    }
+    if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  double tot = 0.0;
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const double e = (g0 + lane < G) ? sm::exp(m.ll[g0 + lane]) : 0.0;
+    for (int j = 0; j < 64 && g0 + j < G; ++j) tot = tot + lane_f64(e, j);
+  }
+  const double lt = sm::log(tot);
+  double best = 0.0;
+  int bestg = -1;
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const int g = g0 + lane;
+    double L = 0.0;
+    if (g < G) {
+      L = sm::exp(m.ll[g] - lt);
+      m.ll[g] = L;  // the normalised likelihood, for the variant mass below
+    }
+    for (int j = 0; j < 64 && g0 + j < G; ++j) {
+      const double Lj = lane_f64(L, j);
+      if (bestg < 0 || Lj > best) {
+        best = Lj;
+        bestg = g0 + j;
+      }
+    }
+  }
+  res.best_g = bestg;
+  res.best_l = best;
+  int i, j;
+  genotype_index(bestg, n, i, j);
+  res.bi = m.order[i];
+  res.bj = m.order[j];
+  if (!with_var_sum) return res;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // the variant genotypes' mass in the immutable Map's order
+  double vsum = 0.0;
+  if (G <= 4) {  // Map1..Map4: insertion (= generation) order
+    for (int g = 0; g < G; ++g) {
+      int a, b;
+      genotype_index(g, n, a, b);
+      if (m.is_var[m.order[a]] || m.is_var[m.order[b]]) vsum = vsum + m.ll[g];
+    }
+  } else {
+    // HashTrieMap: ascending trie key of each genotype's Scala hash; equal keys (a full 32-bit
+    // hash collision, a ListMap there) keep insertion order and are flagged.  G <= kMaxG = 128:
+    // two genotype chunks, the keys in tmp (2 words per genotype: 2 * kFastCap >= 2 * 128).
+    static_assert(kMaxG <= 128 && 2 * kFastCap >= 2 * kMaxG, "genotype key scratch");
+    const uint32_t ah = lane < n ? allele_scala_hash(R, pile_entry(P, m.order[lane < n ? lane : 0]), pos) : 0u;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int g = 64 * c + lane;
+      int a = 0, b = 0;
+      if (g < G) genotype_index(g, n, a, b);
+      const uint32_t ha = (uint32_t)__shfl((int)ah, a & 63, 64), hb = (uint32_t)__shfl((int)ah, b & 63, 64);
+      if (g < G) {
+        const bool v = m.is_var[m.order[a]] || m.is_var[m.order[b]];
+        const uint64_t key = scala::trie_key(scala::genotype_hash(ha, hb));
+        m.tmp[2 * g] = (uint32_t)key;
+        m.tmp[2 * g + 1] = (uint32_t)(key >> 32) | (v ? 0x80000000u : 0u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int rank[2];
+    double Lr[2];
+    bool tie = false;
+    int nvar = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int g = 64 * c + lane;
+      rank[c] = -1;
+      Lr[c] = 0.0;
+      const bool vg = g < G && (m.tmp[2 * g + 1] & 0x80000000u);
+      if (vg) {
+        const uint64_t kg = (uint64_t)m.tmp[2 * g] | ((uint64_t)(m.tmp[2 * g + 1] & 0x7FFFFFFFu) << 32);
+        int r = 0;
+        for (int h = 0; h < G; ++h) {
+          const uint32_t hi = m.tmp[2 * h + 1];
+          if (!(hi & 0x80000000u)) continue;
+          const uint64_t kh = (uint64_t)m.tmp[2 * h] | ((uint64_t)(hi & 0x7FFFFFFFu) << 32);
+          if (kh < kg || (kh == kg && h < g)) ++r;
+          if (kh == kg && h != g) tie = true;
+        }
+        rank[c] = r;
+        Lr[c] = m.ll[g];
+      }
+      nvar += __popcll(__ballot(vg));
+    }
+    for (int r = 0; r < nvar; ++r) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const unsigned long long b = __ballot(rank[c] == r);
+        if (b) vsum = vsum + lane_f64(Lr[c], __ffsll((long long)b) - 1);
+      }
+    }
+    res.order_tie = __ballot(tie) != 0;
+  }
+  res.var_sum = vsum;
+  return res;
+}
+
+// k-th smallest (0-based) of the n values val(tmp[base + e]) by bisection over the value range
+// [lo, hi]: each round counts the values <= mid with ballots (n <= 64: one ballot).
+template <class V>
+__device__ __forceinline__ int kth_bisect(const uint32_t *tmp, int base, uint32_t n, uint32_t k, int lo, int hi, V val) {
+  const int lane = threadIdx.x & 63;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;  // floor (arithmetic shift)
+    uint32_t c = 0;
+    for (uint32_t e0 = 0; e0 < n; e0 += 64) {
+      const uint32_t e = e0 + lane;
+      c += (uint32_t)__popcll(__ballot(e < n && val(tmp[base + e]) <= mid));
+    }
+    if (c > k) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// Evidence of the called allele in both samples (AlleleEvidence.apply, AlleleEvidence.scala:
+// 58-101): per sample the filtered elements whose table index is its target (-1: none), their
+// (mapq, quality, mismatches) gathered in element order into tmp (sample s at s * cap); the
+// four running means (Breeze, element order) on lanes 0-3 together; medians by bisection.
+template <int NS>
+__device__ __forceinline__ void evidence_pair(const Pile<NS> &PT, const Pile<NS> &PN, const uint4 *elT, int nT,
+                                              const uint4 *elN, int nN, int tgtT, int tgtN, double likT, double likN,
+                                              int32_t pos, CallMem &m, gq_evidence &evT, gq_evidence &evN) {
+  const int lane = threadIdx.x & 63;
+  uint32_t n[2] = {0, 0}, fwd[2] = {0, 0};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint4 *el = s ? elN : elT;
+    const int ne = s ? nN : nT, target = s ? tgtN : tgtT;
+    for (int c0 = 0; c0 < ne; c0 += 64) {
+      const int k = c0 + lane;
+      bool hit = false;
+      uint32_t packed = 0, fl = 0;
+      if (k < ne && target >= 0) {
+        const uint4 e = el[k];
+        fl = el_flags(e);
+        hit = (fl & kElAct) && (fl & kElPass) && el_tidx(e) == target;
+        packed = (uint32_t)el_mq(e) | (((e.z >> 16) & 0xFFu) << 8) | ((e.w & 0xFFFFu) << 16);
+      }
+      const unsigned long long hb = __ballot(hit);
+      const uint32_t before = (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
+      if (hit) m.tmp[s * m.cap + n[s] + before] = packed;
+      fwd[s] += (uint32_t)__popcll(__ballot(hit && (fl & kElFwd)));
+      n[s] += (uint32_t)__popcll(hb);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // breeze.stats.mean, running mean in element order: lane 2 s + f = sample s, field f (0 mapq, 1 quality)
+  double mu = 0.0;
+  {
+    const int s = (lane >> 1) & 1, f = lane & 1;
+    const uint32_t ns = s ? n[1] : n[0];
+    const uint32_t nmax = n[0] > n[1] ? n[0] : n[1];
+    for (uint32_t k = 0; k < nmax; ++k) {
+      if (lane < 4 && k < ns) {
+        const uint32_t v = m.tmp[s * m.cap + k];
+        const double x = f ? (double)(int8_t)((v >> 8) & 0xFFu) : (double)(v & 0xFFu);
+        mu += (x - mu) / (double)(k + 1);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    gq_evidence &ev = s ? evN : evT;
+    const Pile<NS> &P = s ? PN : PT;
+    ev.likelihood = s ? likN : likT;
+    ev.read_depth = (int32_t)P.depth_f;
+    ev.forward_depth = (int32_t)P.fwd_f;
+    ev.allele_read_depth = (int32_t)n[s];
+    ev.allele_forward_depth = (int32_t)fwd[s];
+    if (n[s] == 0) {
+      ev.mean_mq = ev.median_mq = ev.mean_bq = ev.median_bq = ev.median_mismatches = __builtin_nan("");
+      continue;
+    }
+    ev.mean_mq = lane_f64(mu, 2 * s);
+    ev.mean_bq = lane_f64(mu, 2 * s + 1);
+    const int base = s * m.cap;
+    const uint32_t ns = n[s];
+    auto f_mq = [](uint32_t v) { return (int)(v & 0xFFu); };
+    auto f_bq = [](uint32_t v) { return (int)(int8_t)((v >> 8) & 0xFFu); };
+    auto f_mm = [](uint32_t v) { return (int)(v >> 16); };
+    if (ns & 1) {
+      const uint32_t k = (ns - 1) / 2;
+      ev.median_mq = (double)kth_bisect(m.tmp, base, ns, k, 0, 255, f_mq);
+      ev.median_bq = (double)kth_bisect(m.tmp, base, ns, k, -128, 127, f_bq);
+      ev.median_mismatches = (double)kth_bisect(m.tmp, base, ns, k, 0, 65535, f_mm);
+    } else {
+      const uint32_t k = ns / 2 - 1;
+      ev.median_mq = ((double)kth_bisect(m.tmp, base, ns, k, 0, 255, f_mq) +
+                      (double)kth_bisect(m.tmp, base, ns, k + 1, 0, 255, f_mq)) / 2.0;
+      ev.median_bq = ((double)kth_bisect(m.tmp, base, ns, k, -128, 127, f_bq) +
+                      (double)kth_bisect(m.tmp, base, ns, k + 1, -128, 127, f_bq)) / 2.0;
+      ev.median_mismatches = (double)((kth_bisect(m.tmp, base, ns, k, 0, 65535, f_mm) +
+                                       kth_bisect(m.tmp, base, ns, k + 1, 0, 65535, f_mm)) / 2);  // Int median (parity unpinned)
+    }
+  }
+}
+
+// The deep list: candidates the fast kernel hands over (their item index), and the deepest
+// pileup among them and the heap-order loci (sizes the deep kernel's scratch).
+struct DeepIO {
+  int64_t *list;             // fast kernel: out; deep kernel: in
+  unsigned long long cap;    // list capacity (fast kernel)
+  int64_t n_in;              // deep kernel: list length
+  uint8_t *scratch;          // deep kernel: per-wave slices
+  int scap, maxG;            // deep kernel: elements per sample per wave, genotypes
+};
+
+#ifndef GQ_CALL_WPE2
+#define GQ_CALL_WPE2 3  // fast kernel: waves per SIMD the register budget must allow (4: 69 VGPRs spilled)
+#endif
+template <bool DEEP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : GQ_CALL_WPE2))) void somatic_call_k(
+    const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
+    DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs, unsigned long long rec_cap,
+    uint8_t *__restrict__ pool, unsigned long long pool_cap, OutGeom og, Counters *ctr, SomWin sw,
+    AmbItem *__restrict__ amb_out, unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
+    const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, RefView ref, int dbg, DeepIO dio) {
+  // amb_in == nullptr: the candidates (fast kernel) or the deep list (deep kernel); loci where a
+  // sample's MD-derived reference bases disagree are listed (amb_out) for the heap-order replay.
+  // amb_in != nullptr (deep kernel only): the listed loci with both samples' bases resolved
+  // (amb_ref[2 i + set]).  ref.b != nullptr: every pileup's base is the reference genome's.
+  constexpr int FW = kSomWaves;
+  constexpr int NS = DEEP ? kSlots : 1;  // allele-table slots: 64 NS distinct alleles per sample
+  __shared__ int32_t s_cov[DEEP ? 1 : FW][2][kFastCap];
+  __shared__ uint4 s_el[DEEP ? 1 : FW][2][kFastCap];
+  __shared__ uint32_t s_tmp[DEEP ? 1 : FW][2 * kFastCap];
+  __shared__ int16_t s_order[DEEP ? 1 : FW][64 * NS];
+  __shared__ uint8_t s_var[DEEP ? 1 : FW][64 * NS];
+  __shared__ double s_ll[DEEP ? 1 : FW][kMaxG];
+  __shared__ double s_terms[DEEP ? 1 : FW][3 * kFastCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  CallMem m;
+  if constexpr (DEEP) {
+    m = deep_mem(dio.scratch + (size_t)gwave * deep_wave_bytes(dio.scap, dio.maxG), dio.scap, dio.maxG);
+  } else {
+    m.cov[0] = s_cov[wv][0];
+    m.cov[1] = s_cov[wv][1];
+    m.el[0] = s_el[wv][0];
+    m.el[1] = s_el[wv][1];
+    m.tmp = s_tmp[wv];
+    m.order = s_order[wv];
+    m.is_var = s_var[wv];
+    m.ll = s_ll[wv];
+    m.terms = s_terms[wv];
+    m.cap = kFastCap;
+    m.maxG = kMaxG;
+  }
+  const unsigned long long n_items =
+      amb_in ? (unsigned long long)n_amb_in : DEEP ? (unsigned long long)dio.n_in : ctr->part_off[1][kParts];
+  // dbg & 16: phase clocks per candidate and wave (covers, elements, tables, tumor genotypes,
+  // normal genotypes + evidence + record, candidates), summed per workgroup in LDS (a global
+  // atomic per phase would queue every wave on one address) and added to ctr->prof at the end
+  __shared__ unsigned long long s_clk[6];
+  if (threadIdx.x < 6) s_clk[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t tk = 0;
+  auto tick = [&](int k) {
+    if (dbg & 16) {
+      const uint64_t t = __builtin_readcyclecounter();
+      if (k >= 0 && lane == 0) atomicAdd(&s_clk[k], (unsigned long long)(t - tk));
+      tk = t;
+    }
+  };
+  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+    tick(-1);
+    if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[5], 1ull);
+    const int64_t it = amb_in ? amb_in[li].item : DEEP ? dio.list[li] : li;
+    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    const Tile &tt_ = tiles_t[item.tile], &tn_ = tiles_n[item.tile];
+    const int32_t pos = item.pos;
+    const int32_t t_contig = tt_.contig, t_L0 = tt_.L0;
+    const int64_t t_ord0 = tt_.ordinal0;
+    const int64_t rb[2] = {tt_.rb, tn_.rb}, re[2] = {tt_.re, tn_.re};
+    const int32_t win = sw.range_win[tt_.range];
+    const WinInit wi[2] = {sw.wi[2 * win], sw.wi[2 * win + 1]};
+    // ---- covering reads of both samples: [first pmax_end > pos, first start > pos) of each
+    //      tile window, the four searches in lockstep
+    int64_t ra[2], rz[2];
+    {
+      const int64_t lo[4] = {rb[0], rb[0], rb[1], rb[1]}, hi[4] = {re[0], re[0], re[1], re[1]};
+      int64_t out[4];
+      wave_first_true_k<4>(lo, hi, [&](int k, int64_t r) {
+        const DevReads &R = k < 2 ? RT : RN;
+        return (k & 1) ? R.start[r] > pos : R.pmax_end[r] > pos;
+      }, out);
+      ra[0] = out[0], rz[0] = out[1], ra[1] = out[2], rz[1] = out[3];
+    }
+    uint32_t nc[2] = {0, 0};
+    {
+      const int64_t span = max(rz[0] - ra[0], rz[1] - ra[1]);
+      for (int64_t c0 = 0; c0 < span; c0 += 64) {
+        bool c[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const DevReads &R = s ? RN : RT;
+          const int64_t r = ra[s] + c0 + lane;
+          c[s] = r < rz[s] && R.start[r] <= pos && pos < R.end[r];
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const unsigned long long b = __ballot(c[s]);
+          const uint32_t at = nc[s] + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+          if (c[s] && at < (uint32_t)m.cap) m.cov[s][at] = (int32_t)(ra[s] + c0 + lane - rb[s]);
+          nc[s] += (uint32_t)__popcll(b);
+        }
+      }
+    }
+    if (nc[0] > (uint32_t)m.cap || nc[1] > (uint32_t)m.cap || (!DEEP && (dbg & 64))) {
+      if constexpr (!DEEP) {  // deeper than the LDS records (or GQ_DBG & 64, tests): the deep kernel's, whole
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
+          if (k < dio.cap) dio.list[k] = it;
+          atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
+        }
+      } else {
+        raise_at(ctr, GQ_E_CAPACITY, pos);  // the host sized the scratch from deep_max
+      }
+      continue;
+    }
+    // ---- pileup element order: where the window's initial (heap-ordered) group still covers
+    //      pos, its reads are a prefix of the list, reordered by heap rank (SlidingWindow
+    //      currentRegions(), DistributedUtil.scala:260-274; Pile.atGreaterLocus keeps them first)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const WinInit &w = wi[s];
+      if (!(w.n > 0 && pos < w.E)) continue;  // uniform
+      const DevReads &R = s ? RN : RT;
+      int p = 0;
+      for (int k0 = 0; k0 < (int)nc[s]; k0 += 64) {
+        const int k = k0 + lane;
+        p += (int)__popcll(__ballot(k < (int)nc[s] && R.start[rb[s] + m.cov[s][k]] <= w.F));
+      }
+      for (int k = lane; k < p; k += 64) {
+        const int64_t r = rb[s] + m.cov[s][k];
+        int lo = 0, hi = w.n;
+        while (lo < hi) {
+          const int md = (lo + hi) >> 1;
+          if (sw.init_reads[w.off + md] < r) lo = md + 1;
+          else hi = md;
+        }
+        m.tmp[k] = (uint32_t)sw.init_rank[w.off + lo];
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int k = lane; k < p; k += 64) {
+        int before = 0;
+        for (int j = 0; j < p; ++j) before += m.tmp[j] < m.tmp[k] ? 1 : 0;
+        m.tmp[m.cap + before] = (uint32_t)m.cov[s][k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int k = lane; k < p; k += 64) m.cov[s][k] = (int32_t)m.tmp[m.cap + k];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    tick(0);
+    // ---- elements, both samples' chunks together: each covering read's scalars in one round,
+    //      then (a single aligned block, the common read) its base, quality and MD event at
+    //      pos; other reads take the general CIGAR walk (classify) and md_ref_at
+    uint32_t mask[2] = {0, 0};
+    {
+      const uint32_t span = max(nc[0], nc[1]);
+      for (uint32_t c0 = 0; c0 < span; c0 += 64) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const DevReads &R = s ? RN : RT;
+          const uint32_t k = c0 + lane;
+          if (k >= nc[s]) continue;
+          const int64_t r = rb[s] + m.cov[s][k];
+          const int32_t st = R.start[r];
+          const int ld = (int)R.lead[r];
+          const int64_t so = R.seq_off[r];
+          const int mq = (int)R.mapq[r];
+          const uint8_t rfl = R.flags[r];
+          const int32_t nmd = R.n_md[r];
+          const int64_t mdo = R.md_off[r];
+          const uint32_t nmm = (uint32_t)R.n_mismatch[r];
+          uint32_t fl = 0;
+          int32_t rp = 0, aux = 0;
+          uint32_t base = 0, kind = K_SNV;
+          int q = 0;
+          if (ld >= 0) {
+            const int32_t off = pos - st;
+            rp = ld + off;
+            base = R.seq[so + rp];
+            q = (int)(int8_t)R.qual[so + rp];
+            if (nmd < 0) {
+              raise_at(ctr, GQ_E_NO_MD, pos);
+            } else {
+              const int v = nmd > 0 ? md_find(R.md_ev + mdo, nmd, off) : -1;
+              mask[s] |= std_bit((uint8_t)(v >= 0 ? v : (int)base));
+              fl = kElAct;
+            }
+          } else {
+            const int v = md_ref_at(R, r, pos);
+            if (v < 0) {
+              raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
+            } else {
+              mask[s] |= std_bit((uint8_t)v);
+              AlleleDesc d;
+              int errc = 0;
+              if (!classify(R, r, pos, 0, d, &errc)) {
+                raise_at(ctr, errc, pos);
+              } else {
+                fl = kElAct;
+                kind = d.kind;
+                base = d.base;
+                rp = d.rp;
+                aux = d.aux;
+                q = elem_quality(R, d, so, mq);
+              }
+            }
+          }
+          if (prm.min_mapq <= 0 || mq >= prm.min_mapq) fl |= kElPass;  // QualityAlignedReadsFilter
+          if (!(rfl & 1)) fl |= kElFwd;
+          m.el[s][k] = make_uint4((uint32_t)rp, (uint32_t)aux,
+                                  base | (kind << 8) | ((uint32_t)(uint8_t)(int8_t)q << 16) | ((uint32_t)mq << 24),
+                                  (nmm & 0xFFFFu) | (fl << 16));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    Pile<NS> PS[2];
+    const int fb = ref.b ? (int)ref.b[ref.off[t_contig] + pos] : -1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint32_t mk = mask[s];
+      for (int d = 1; d < 64; d <<= 1) mk |= __shfl_xor(mk, d, 64);
+      PS[s].ambiguous = fb < 0 && __popc(mk) > 1;
+      PS[s].refbase = amb_in ? amb_ref[2 * li + s] : fb >= 0 ? (uint8_t)fb : mk ? bit_base(mk) : (uint8_t)'N';
+    }
+    tick(1);
+    // ---- allele tables (the records now get their pileup reference base: SNV / DEL keys)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const DevReads &R = s ? RN : RT;
+      Pile<NS> &P = PS[s];
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        P.klo[t] = P.khi[t] = 0;
+        P.n_all[t] = P.n_f[t] = 0;
+      }
+      P.nt = 0;
+      P.depth_all = P.depth_f = P.fwd_f = 0;
+      P.overflow = false;
+      for (uint32_t c0 = 0; c0 < nc[s]; c0 += 64) {
+        const uint32_t k = c0 + lane;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        if (k < nc[s]) e = m.el[s][k];
+        const uint32_t fl = el_flags(e);
+        const bool act = k < nc[s] && (fl & kElAct);
+        const bool pass = act && (fl & kElPass);
+        AlleleDesc d;
+        d.read = rb[s] + (k < nc[s] ? m.cov[s][k] : 0);
+        d.rp = (int32_t)e.x;
+        d.aux = (int32_t)e.y;
+        d.base = (uint8_t)(e.z & 0xFFu);
+        d.kind = (uint8_t)((e.z >> 8) & 0xFFu);
+        d.rb = P.refbase;
+        d.pad = 0;
+        Key128 key{0, 0};
+        if (act) key = allele_key(R, d, pos, 0);
+        const unsigned long long actb = __ballot(act), passb = __ballot(pass);
+        P.depth_all += (uint32_t)__popcll(actb);
+        P.depth_f += (uint32_t)__popcll(passb);
+        P.fwd_f += (uint32_t)__popcll(__ballot(pass && (fl & kElFwd)));
+        int mine = -1;
+        unsigned long long pending = actb;
+        while (pending) {
+          const int leader = __ffsll((long long)pending) - 1;
+          const uint64_t klo = __shfl(key.lo, leader, 64), khi = __shfl(key.hi, leader, 64);
+          const bool match = act && key.lo == klo && key.hi == khi;
+          const unsigned long long mb = __ballot(match);
+          const uint32_t na = (uint32_t)__popcll(mb), nf = (uint32_t)__popcll(mb & passb);
+          int found = -1;
+#pragma unroll
+          for (int t = 0; t < NS; ++t) {
+            const unsigned long long hb = __ballot((t * 64 + lane) < P.nt && P.klo[t] == klo && P.khi[t] == khi);
+            if (found < 0 && hb) found = t * 64 + (__ffsll((long long)hb) - 1);
+          }
+          if (found < 0) {
+            if (P.nt >= 64 * NS) {
+              P.overflow = true;
+            } else {
+              found = P.nt++;
+              const int owner = found & 63, sl = found >> 6;
+              AlleleDesc ldsc;
+              ldsc.read = __shfl(d.read, leader, 64);
+              ldsc.aux = __shfl(d.aux, leader, 64);
+              ldsc.rp = __shfl(d.rp, leader, 64);
+              ldsc.kind = (uint8_t)__shfl((int)d.kind, leader, 64);
+              ldsc.rb = P.refbase;
+              ldsc.base = (uint8_t)__shfl((int)d.base, leader, 64);
+              ldsc.pad = 0;
+#pragma unroll
+              for (int t = 0; t < NS; ++t)
+                if (t == sl && lane == owner) {
+                  P.klo[t] = klo;
+                  P.khi[t] = khi;
+                  P.desc[t] = ldsc;
+                }
+            }
+          }
+          if (found >= 0) {
+            const int owner = found & 63, sl = found >> 6;
+#pragma unroll
+            for (int t = 0; t < NS; ++t)
+              if (t == sl && lane == owner) {
+                P.n_all[t] += na;
+                P.n_f[t] += nf;
+              }
+            if (match) mine = found;
+          }
+          pending &= ~mb;
+        }
+        if (act && mine >= 0) m.el[s][k].w = (e.w & 0x00FFFFFFu) | ((uint32_t)mine << 24);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    Pile<NS> &PT = PS[0], &PN = PS[1];
+    if (PT.overflow || PN.overflow) {
+      if constexpr (!DEEP) {  // more distinct alleles than the fast table: the deep kernel's
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
+          if (k < dio.cap) dio.list[k] = it;
+          atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
+        }
+      } else {
+        raise_at(ctr, GQ_E_CAPACITY, pos);
+      }
+      continue;
+    }
+    if ((item.flags & 1) && !amb_in && (PT.depth_all + PN.depth_all) > 0 && lane == 0)
+      atomicAdd(&ctr->spread[0][it & (kSpread - 1)], 1ull);
+    if (!amb_in && (PT.ambiguous || PN.ambiguous)) {  // heap order decides a reference base: list it
+      if (lane == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
+        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+        atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
+      }
+      continue;
+    }
+    tick(2);
+    if (prm.filter_multi_allelic) {  // MultiAllelicPileupFilter (PileupFilter.scala:29-44)
+      if (PT.nt > 2) PT.depth_f = 0;
+      if (PN.nt > 2) PN.depth_f = 0;
+    }
+    // SomaticStandardCaller.scala:184-190
+    if (PT.depth_f == 0 || PN.depth_f == 0 || (int64_t)PT.depth_f > (int64_t)prm.max_read_depth ||
+        (int64_t)PN.depth_f > (int64_t)prm.max_read_depth)
+      continue;
+    {  // the tumor pileup must hold a non-Match element: Match = allele (ref, ref) of one byte
+      uint32_t ref_match = 0;
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        const bool mt = (t * 64 + lane) < PT.nt && PT.desc[t].kind == K_SNV && PT.desc[t].base == PT.refbase;
+        ref_match += (uint32_t)wave_sum(mt ? (double)PT.n_f[t] : 0.0);
+      }
+      if (ref_match == PT.depth_f) continue;
+    }
+    // the multi-allelic filter empties a pileup: no element passes then
+    const int nT = PT.depth_f ? (int)nc[0] : 0, nN = PN.depth_f ? (int)nc[1] : 0;
+    const GenoOut tg = genotypes_el(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
+    tick(3);
+    if (tg.G == 0) continue;
+    const bool t_var = m.is_var[tg.bi] || m.is_var[tg.bj];
+    if (!t_var) continue;
+    const AlleleDesc a1 = pile_entry(PT, tg.bi), a2 = pile_entry(PT, tg.bj);
+    const GenoOut ng = genotypes_el(RN, PN, m.el[1], nN, pos, false, true, m, ctr);
+    const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
+    const double odds = tg.best_l / nvs;
+    if (!(odds * 100.0 >= (double)prm.odds)) continue;
+    uint8_t knife = near_edge(odds * 100.0, (double)prm.odds) ? GQ_FLAG_KNIFE_EDGE : 0;
+    // first variant allele of the ML genotype with a non-empty alt (SomaticStandardCaller.scala:227)
+    const bool v1 = allele_is_variant(RT, a1, pos) && allele_alt_len(a1) > 0;
+    const bool v2 = allele_is_variant(RT, a2, pos) && allele_alt_len(a2) > 0;
+    if (!v1 && !v2) continue;
+    const AlleleDesc al = v1 ? a1 : a2;
+    const int t_idx = v1 ? tg.bi : tg.bj;
+    const int rl = allele_ref_len(al), alt_l = allele_alt_len(al);
+    const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
+    const int n_idx = PN.depth_f ? pile_find(PN, nkey) : -1;
+    gq_evidence tev, nev;
+    evidence_pair(PT, PN, m.el[0], nT, m.el[1], nN, t_idx, n_idx, tg.best_l, 1.0 - nvs, pos, m, tev, nev);
+    const double log_odds = sm::log(odds);
+    const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
+    if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
+    const float vaf = (float)tev.allele_read_depth / (float)tev.read_depth;
+    if (prm.apply_filters == 1) {  // SomaticStandardCaller.scala:124-137 then SomaticGenotypeFilter.apply (:285-307)
+      const bool depth_ok = tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
+                            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF;
+      if (!depth_ok) continue;
+      if (!(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth)) continue;
+      if (!(log_odds > (double)prm.min_lod)) continue;
+      if (near_edge(log_odds, (double)prm.min_lod)) knife |= GQ_FLAG_KNIFE_EDGE;
+      if (!(gqv >= prm.min_likelihood)) continue;
+      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
+      if (!(tev.mean_mq >= prm.min_average_mapping_quality && nev.mean_mq >= prm.min_average_mapping_quality)) continue;
+      if (near_edge(tev.mean_mq, prm.min_average_mapping_quality) || near_edge(nev.mean_mq, prm.min_average_mapping_quality) ||
+          near_edge(tev.mean_mq, prm.min_average_base_quality) || near_edge(nev.mean_mq, prm.min_average_base_quality))
+        knife |= GQ_FLAG_KNIFE_EDGE;
+      // the "average base quality" filter tests mean mapping quality (SomaticGenotypeFilter.scala:194-195)
+      if (!(tev.mean_mq >= prm.min_average_base_quality && nev.mean_mq >= prm.min_average_base_quality)) continue;
+      if (!(tev.median_mismatches <= (double)prm.max_median_mismatches)) continue;
+    } else if (prm.apply_filters == 2) {  // SomaticGenotypeFilter(Seq, ...) as the caller suite uses it
+      if (!(tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&
+            nev.read_depth >= prm.min_normal_read_depth && nev.read_depth < 0x7FFFFFFF))
+        continue;
+      if (!((double)vaf * 100.0 > (double)prm.min_vaf)) continue;
+      if (!(gqv >= prm.min_likelihood)) continue;
+      if (prm.min_tumor_alternate_read_depth > 0 && !(tev.allele_read_depth >= prm.min_tumor_alternate_read_depth))
+        continue;
+    }
+    SomRec rr;
+    rr.key = (uint64_t)(t_ord0 + (pos - t_L0)) << 12;
+    rr.contig = t_contig;
+    rr.pos = pos;
+    rr.ref_len = (uint16_t)rl;
+    rr.alt_len = (uint16_t)alt_l;
+    rr.flags = (PT.ambiguous ? 1 : 0) | (PN.ambiguous ? 2 : 0) | knife;
+    rr.pad[0] = rr.pad[1] = rr.pad[2] = 0;
+    rr.log_odds = log_odds;
+    rr.gq = gqv;
+    rr.pad2 = 0;
+    rr.tumor = tev;
+    rr.normal = nev;
+    if (rl + alt_l <= 8) {
+      uint64_t v = 0;
+      int j = 0;
+      for (int i = 0; i < rl; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 0, i) << (8 * j++);
+      for (int i = 0; i < alt_l; ++i) v |= (uint64_t)allele_byte(RT, al, pos, 1, i) << (8 * j++);
+      rr.allele = v;
+    } else {
+      unsigned long long off = 0;
+      if (lane == 0) off = atomicAdd(&ctr->pool_used, (unsigned long long)(rl + alt_l));
+      off = __shfl(off, 0, 64);
+      if (off + rl + alt_l <= pool_cap)
+        for (int i = lane; i < rl + alt_l; i += 64)
+          pool[off + i] = i < rl ? allele_byte(RT, al, pos, 0, i) : allele_byte(RT, al, pos, 1, i - rl);
+      rr.allele = off;
+    }
+    if (lane == 0) {
+      const unsigned long long k = atomicAdd(&ctr->n_rec, 1ull);
+      if (k < rec_cap) recs[k] = rr;
+    }
+    tick(4);
+  }
+  if (dbg & 16) {
+    __syncthreads();
+    if (threadIdx.x < 6 && s_clk[threadIdx.x]) atomicAdd(&ctr->prof[threadIdx.x], s_clk[threadIdx.x]);
+  }
+}

@@ -32,7 +32,7 @@ class gq_reads(C.Structure):
         (n, C.c_void_p) for n in ("contig_read_begin", "start", "end", "pmax_end", "mapq", "flags", "sample",
                                   "seq_off", "seq_len", "cigar_off", "n_cigar", "md_off", "n_md", "n_mismatch")] + [
         ("seq_bytes", C.c_int64), ("cigar_len", C.c_int64), ("md_len", C.c_int64)] + [
-        (n, C.c_void_p) for n in ("seq", "qual", "cigar", "md_ev")]
+        (n, C.c_void_p) for n in ("seq", "qual", "cigar", "md_ev", "sample_hash")]
 
 
 class gq_loci(C.Structure):
@@ -214,7 +214,8 @@ def make_gq_reads(arrs: Dict[str, object]) -> Tuple[gq_reads, list]:
                                            "sample", "seq_off", "seq_len", "cigar_off", "n_cigar", "md_off", "n_md",
                                            "n_mismatch")],
                  int(arrs["seq"].shape[0]), int(arrs["cigar"].shape[0]), int(arrs["md_ev"].shape[0]),
-                 *[_ptr(arrs[k]) for k in ("seq", "qual", "cigar", "md_ev")])
+                 *[_ptr(arrs[k]) for k in ("seq", "qual", "cigar", "md_ev")],
+                 _ptr(arrs["sample_hash"]) if "sample_hash" in arrs else None)
     return s, keep
 
 

@@ -94,8 +94,26 @@ def pack(rs: ReadSet) -> Dict[str, np.ndarray]:
     out = assemble(rs.contig, rs.start, rs.end, rs.mapq, rs.flags, rs.sample, rs.seq_off, rs.seq_len, rs.seq,
                    rs.qual, rs.cigar_off, rs.n_cigar, rs.cigar, md_off, n_md, n_mm, md_ev, len(rs.contig_names),
                    max(1, len(rs.sample_names)))
+    out["sample_hash"] = sample_hashes(rs.sample_names, int(out["n_samples"]))
     rs._gq = out
     return out
+
+
+def java_string_hash(s: str) -> int:
+    """java.lang.String.hashCode (over UTF-16 code units), as an unsigned 32-bit value."""
+    h = 0
+    u = s.encode("utf-16-be")
+    for i in range(0, len(u), 2):
+        h = (31 * h + ((u[i] << 8) | u[i + 1])) & 0xFFFFFFFF
+    return h
+
+
+def sample_hashes(sample_names, n_samples: int) -> np.ndarray:
+    """gq_reads.sample_hash: the Scala ## (String.hashCode) of each sample slot's name; a slot
+    past the names is the reference's "default" sample (Pileup.scala:58)."""
+    names = list(sample_names)
+    return np.array([java_string_hash(names[k] if k < len(names) else "default") for k in range(n_samples)],
+                    np.uint32)
 
 
 def assemble(contig, start, end, mapq, flags, sample, seq_off, seq_len, seq, qual, cigar_off, n_cigar, cigar,

@@ -83,6 +83,11 @@ typedef struct {
   const uint8_t *qual;              /* phred, same offsets as seq                      */
   const uint32_t *cigar;
   const uint32_t *md_ev;
+  /* [n_samples] java.lang.String.hashCode of each slot's sample name (the JVM host passes
+   * name.hashCode(); a read without a read group is sample "default", Pileup.scala:58), or
+   * NULL.  It orders the per-sample records of a locus as Pileup.bySample's Scala Map iterates
+   * (GermlineThresholdCaller.scala:100); NULL keeps slot order.                            */
+  const uint32_t *sample_hash;
 } gq_reads;
 
 /* LociMap[Long] as flat ranges in partition order (task ascending, contigs
@@ -107,7 +112,8 @@ enum { GQ_GT_REF = 0, GQ_GT_ALT = 1, GQ_GT_OTHERALT = 2, GQ_GT_NOCALL = 3 };
  * ambiguous, plus GQ_FLAG_KNIFE_EDGE) */
 enum {
   GQ_FLAG_AMBIGUOUS_REF = 1, /* pileup ref base decided by JVM heap order (MD tags disagree) */
-  GQ_FLAG_TIE = 2,           /* count tie among passing alleles (JVM hash order unpinned)   */
+  GQ_FLAG_TIE = 2,           /* count tie among passing alleles, ordered as the reference's
+                                Scala 2.10 groupBy map iterates (restated, parity unpinned) */
   GQ_FLAG_KNIFE_EDGE = 4     /* somatic: a test or filter decided within FP rounding of its
                                 threshold (outcome depends on summation order)              */
 };

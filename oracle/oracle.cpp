@@ -137,6 +137,7 @@ struct Read {
   int mapq;
   bool positive;
   int sample;
+  std::string sampleName;  // Option(read.sampleName).getOrElse("default") (Pileup.scala:58)
   const uint8_t *seq;
   const uint8_t *qual;
   int len;
@@ -235,6 +236,100 @@ struct Allele {
 struct AlleleHash {
   size_t operator()(const Allele &a) const { return std::hash<std::string>()(a.ref) * 1000003u ^ std::hash<std::string>()(a.alt); }
 };
+
+// ---- Scala 2.10.3 hash-collection iteration order (scala-library 2.10.3, pom.xml:22;
+// restated from its published sources: MurmurHash3, mutable.HashTable, immutable.HashMap,
+// TraversableLike.groupBy).  Parity unpinned: no JVM here to observe it.
+namespace scala_order {
+uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+uint32_t mix(uint32_t h, uint32_t k) {  // MurmurHash3.mix
+  k *= 0xcc9e2d51u;
+  k = rotl(k, 15);
+  k *= 0x1b873593u;
+  h ^= k;
+  h = rotl(h, 13);
+  return h * 5u + 0xe6546b64u;
+}
+uint32_t finalizeHash(uint32_t h, uint32_t len) {  // MurmurHash3.finalizeHash (avalanche(h ^ len))
+  h ^= len;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+uint32_t javaStringHash(const std::string &s) {  // java.lang.String.hashCode
+  uint32_t h = 0;
+  for (unsigned char c : s) h = 31u * h + c;
+  return h;
+}
+const uint32_t kSeqSeed = javaStringHash("Seq"), kProductSeed = 0xcafebabeu;
+uint32_t byteSeqHash(const std::string &bytes) {  // MurmurHash3.seqHash of a Seq[Byte] (## = signed value)
+  uint32_t h = kSeqSeed;
+  for (unsigned char c : bytes) h = mix(h, (uint32_t)(int32_t)(int8_t)c);
+  return finalizeHash(h, (uint32_t)bytes.size());
+}
+uint32_t alleleHash(const Allele &a) {  // case class Allele(refBases, altBases): productHash
+  return finalizeHash(mix(mix(kProductSeed, byteSeqHash(a.ref)), byteSeqHash(a.alt)), 2);
+}
+uint32_t genotypeHash(const Allele &a1, const Allele &a2) {  // case class Genotype(alleles: Allele*)
+  const uint32_t seq = finalizeHash(mix(mix(kSeqSeed, alleleHash(a1)), alleleHash(a2)), 2);
+  return finalizeHash(mix(kProductSeed, seq), 1);
+}
+// mutable.HashTable.index: the top log2(size) bits of improve(hash, seed), improve =
+// byteswap32(hash) rotated right by seed (the initial 16-bucket table's bitCount(15) = 4)
+uint32_t mutableIndex(uint32_t hash, int bits) {
+  uint32_t hc = hash * 0x9e3775cdu;
+  hc = (hc >> 24) | ((hc >> 8) & 0xFF00u) | ((hc << 8) & 0xFF0000u) | (hc << 24);
+  const uint32_t i = hc * 0x9e3775cdu;
+  const uint32_t improved = (i >> 4) | (i << 28);
+  return (improved >> (32 - bits)) & ((1u << bits) - 1u);
+}
+// immutable.HashMap.improve, and the HashTrieMap iteration key: 5-bit chunks, lowest first
+uint64_t trieKey(uint32_t h) {
+  h = h + ~(h << 9);
+  h = h ^ (h >> 14);
+  h = h + (h << 4);
+  h = h ^ (h >> 10);
+  uint64_t k = 0;
+  for (int c = 0; c < 7; ++c) k = (k << 5) | (uint64_t)((h >> (5 * c)) & 31u);
+  return k;
+}
+// Iteration order of the immutable Map groupBy returns for keys with these hashes, given in
+// first-occurrence (insertion) order: positions into `hashes`.
+//   mutable.HashMap filled in that order: 16 buckets, entry prepended to its chain, resize x2
+//   when more than size * 3/4 entries (old buckets last to first, chains from the head);
+//   iterated from the last populated bucket down, chains from the head;
+//   immutable.Map built from that iteration: Map1..Map4 keep it; five or more keys form a
+//   HashTrieMap (ascending trieKey; equal keys in insertion order, a ListMap).
+std::vector<int> groupByOrder(const std::vector<uint32_t> &hashes) {
+  int bits = 4;
+  std::vector<std::vector<int>> table(16);
+  size_t n = 0;
+  for (int i = 0; i < (int)hashes.size(); ++i) {
+    auto &chain = table[mutableIndex(hashes[(size_t)i], bits)];
+    chain.insert(chain.begin(), i);
+    if (++n > table.size() * 3 / 4) {
+      std::vector<std::vector<int>> nt(table.size() * 2);
+      ++bits;
+      for (size_t b = table.size(); b-- > 0;)
+        for (int e : table[b]) {
+          auto &c2 = nt[mutableIndex(hashes[(size_t)e], bits)];
+          c2.insert(c2.begin(), e);
+        }
+      table.swap(nt);
+    }
+  }
+  std::vector<int> order;
+  for (size_t b = table.size(); b-- > 0;)
+    for (int e : table[b]) order.push_back(e);
+  if (order.size() > 4)
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return trieKey(hashes[(size_t)a]) < trieKey(hashes[(size_t)b]); });
+  return order;
+}
+}  // namespace scala_order
 
 // pileup/Alignment.scala:32-94
 enum Kind { K_MATCH, K_MISMATCH, K_INSERTION, K_DELETION, K_MIDDELETION, K_CLIPPED };
@@ -586,6 +681,9 @@ void buildReads(const or_reads *in, ReadSet &rs) {
     r.mapq = in->mapq[i];
     r.positive = !(in->flags[i] & 1);
     r.sample = in->sample[i];
+    r.sampleName = (r.sample >= 0 && r.sample < in->n_sample_names && in->sample_names && in->sample_names[r.sample])
+                       ? std::string(in->sample_names[r.sample])
+                       : std::string("default");
     r.seq = in->seq + in->seq_off[i];
     r.qual = in->qual + in->seq_off[i];
     r.len = in->seq_len[i];
@@ -701,32 +799,65 @@ void appendf(std::string &s, const char *fmt, ...) {
   }
 }
 
+// Pileup.bySample (Pileup.scala:57-61): elements.groupBy(sample name) then .map(...), so the
+// samples come in the Scala Map's iteration order over their names (String.hashCode; the
+// first occurrence in element order is the insertion order).  (sample slot, elements) pairs.
+std::vector<std::pair<int, std::vector<const Elem *>>> bySampleOrdered(const Pileup &p) {
+  std::vector<std::string> names;
+  std::vector<std::pair<int, std::vector<const Elem *>>> groups;
+  for (const Elem &e : p.elements) {
+    size_t k = 0;
+    while (k < names.size() && names[k] != e.read->sampleName) ++k;
+    if (k == names.size()) {
+      names.push_back(e.read->sampleName);
+      groups.push_back({e.read->sample, {}});
+    }
+    groups[k].second.push_back(&e);
+  }
+  std::vector<uint32_t> hashes;
+  for (const std::string &n : names) hashes.push_back(scala_order::javaStringHash(n));
+  std::vector<std::pair<int, std::vector<const Elem *>>> out;
+  for (int k : scala_order::groupByOrder(hashes)) out.push_back(groups[(size_t)k]);
+  return out;
+}
+
 // GermlineThreshold.Caller.callVariantsAtLocus (GermlineThresholdCaller.scala:90-179)
 void germlineCallAtLocus(const Pileup &p, const char *contig, int threshold, bool emitRef, bool emitNoCall,
                          bool ambiguousRef, std::string &out) {
   if (p.elements.empty()) return;
-  // bySample (Pileup.scala:57-61); sample slots in ascending order (hash order unpinned)
-  std::map<int, std::vector<const Elem *>> bySample;
-  for (const Elem &e : p.elements) bySample[e.read->sample].push_back(&e);
-  for (auto &kv : bySample) {
-    const auto &elems = kv.second;
+  // bySample (Pileup.scala:57-61): groupBy over the sample names, iterated in the Scala Map's order
+  for (const auto &grp : bySampleOrdered(p)) {
+    const int sampleSlot = grp.first;
+    const auto &elems = grp.second;
     int total = (int)elems.size();
-    std::unordered_map<Allele, int, AlleleHash> counts;
-    for (const Elem *e : elems) counts[e->evaluate().allele]++;
+    // counts = elements.map(_.allele).groupBy(x => x).mapValues(_.length) (:103): the distinct
+    // alleles in first-occurrence order, then the groupBy map's iteration order
+    std::vector<Allele> distinct;
+    std::vector<int> cnt;
+    for (const Elem *e : elems) {
+      const Allele &a = e->evaluate().allele;
+      size_t k = 0;
+      while (k < distinct.size() && !(distinct[k] == a)) ++k;
+      if (k == distinct.size()) {
+        distinct.push_back(a);
+        cnt.push_back(0);
+      }
+      ++cnt[k];
+    }
+    std::vector<uint32_t> hashes;
+    for (const Allele &a : distinct) hashes.push_back(scala_order::alleleHash(a));
     std::vector<std::pair<Allele, int>> sorted;
-    for (auto &c : counts)
-      if ((int64_t)c.second * 100 / total > threshold) sorted.push_back(c);
-    // sortBy(-count): ties resolved canonically by Allele ordering (Scala hash order unpinned)
-    std::sort(sorted.begin(), sorted.end(), [](const std::pair<Allele, int> &a, const std::pair<Allele, int> &b) {
-      if (a.second != b.second) return a.second > b.second;
-      return a.first < b.first;
-    });
+    for (int k : scala_order::groupByOrder(hashes))
+      if ((int64_t)cnt[(size_t)k] * 100 / total > threshold) sorted.push_back({distinct[(size_t)k], cnt[(size_t)k]});
+    // sortBy(-count) (:104): a stable sort, count ties keep the map's order
+    std::stable_sort(sorted.begin(), sorted.end(),
+                     [](const std::pair<Allele, int> &a, const std::pair<Allele, int> &b) { return a.second > b.second; });
     int flags = ambiguousRef ? 1 : 0;
     if (sorted.size() >= 2 && (sorted[0].second == sorted[1].second ||
                                (sorted.size() >= 3 && sorted[1].second == sorted[2].second)))
       flags |= 2;
     auto emit = [&](const std::string &ref, const std::string &alt, int g0, int g1) {
-      appendf(out, "%s\t%lld\t%d\t%s,%s\t%s\t%s\t%d\n", contig, (long long)p.locus, kv.first, gtName(g0), gtName(g1),
+      appendf(out, "%s\t%lld\t%d\t%s,%s\t%s\t%s\t%d\n", contig, (long long)p.locus, sampleSlot, gtName(g0), gtName(g1),
               ref.c_str(), alt.c_str(), flags);
     };
     std::string refStr(1, (char)p.referenceBase);
@@ -1030,9 +1161,18 @@ void somaticAtLocus(const Pileup &tp, const Pileup &np, const char *contigName, 
       double mll = tg[best].second;
       if (!mlg.hasVariantAllele()) return;
       auto ng = likelihoodsOfAllPossibleGenotypes(fn, false);
+      // normalLikelihoods.toMap.filter(_._1.hasVariantAllele).map(_._2).sum (:206-217): the
+      // genotypes in the immutable Map's order (insertion order up to four, else HashTrieMap)
+      std::vector<size_t> gorder(ng.size());
+      for (size_t i = 0; i < ng.size(); ++i) gorder[i] = i;
+      if (ng.size() > 4)
+        std::stable_sort(gorder.begin(), gorder.end(), [&](size_t a, size_t b) {
+          return scala_order::trieKey(scala_order::genotypeHash(ng[a].first.a1, ng[a].first.a2)) <
+                 scala_order::trieKey(scala_order::genotypeHash(ng[b].first.a1, ng[b].first.a2));
+        });
       double nvs = 0.0;
-      for (auto &g : ng)
-        if (g.first.hasVariantAllele()) nvs += g.second;
+      for (size_t i : gorder)
+        if (ng[i].first.hasVariantAllele()) nvs += ng[i].second;
       double odds = mll / nvs;
       if (!(odds * 100 >= prm->odds)) return;
       // test-infrastructure flag (same rule as the device, GQ_FLAG_KNIFE_EDGE = 4): a decision
@@ -1154,6 +1294,18 @@ int or_germline_standard(const or_reads *reads, const or_loci *loci, const or_ge
 }
 
 const char *or_last_error(void) { return g_err.c_str(); }
+void or_scala_group_order(const uint32_t *hashes, int32_t n, int32_t *out) {
+  std::vector<uint32_t> h(hashes, hashes + n);
+  const std::vector<int> o = scala_order::groupByOrder(h);
+  for (int32_t i = 0; i < n; ++i) out[i] = o[(size_t)i];
+}
+uint32_t or_scala_allele_hash(const char *ref, const char *alt) {
+  return scala_order::alleleHash(Allele{ref, alt});
+}
+uint32_t or_scala_genotype_hash(const char *r1, const char *a1, const char *r2, const char *a2) {
+  return scala_order::genotypeHash(Allele{r1, a1}, Allele{r2, a2});
+}
+
 void or_free(char *p) { free(p); }
 
 int or_pileup_stats(const or_reads *reads, const or_loci *loci, char **o, int64_t *olen) {

@@ -35,6 +35,8 @@ typedef struct {
   const int64_t *md_off;
   const int32_t *md_len;     /* < 0 => read has no MD tag                      */
   const char *md;            /* MD strings pool                                 */
+  int32_t n_sample_names;    /* sample slot -> read-group sample name; a slot    */
+  const char *const *sample_names; /* past the list: "default" (Pileup.scala:58) */
 } or_reads;
 
 typedef struct {
@@ -156,6 +158,13 @@ int or_germline_at(const or_reads *reads, int32_t contig, int64_t locus, int32_t
  * applies the Seq form SomaticGenotypeFilter.apply (SomaticGenotypeFilter.scala:314-337). */
 int or_somatic_at(const or_reads *tumor, const or_reads *normal, int32_t contig, int64_t locus,
                   const or_somatic_params *p, char **out, int64_t *out_len);
+
+/* The Scala 2.10 iteration-order restatement (test hooks): groupBy's Map order of n keys with
+ * these hashes given in first-occurrence order (out[i] = position of the i-th key iterated);
+ * Allele(ref, alt).hashCode; Genotype(Allele(r1, a1), Allele(r2, a2)).hashCode.          */
+void or_scala_group_order(const uint32_t *hashes, int32_t n, int32_t *out);
+uint32_t or_scala_allele_hash(const char *ref, const char *alt);
+uint32_t or_scala_genotype_hash(const char *r1, const char *a1, const char *r2, const char *a2);
 
 void or_free(char *p);
 const char *or_last_error(void);

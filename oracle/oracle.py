@@ -28,7 +28,8 @@ class or_reads(C.Structure):
     _fields_ = [("n_reads", C.c_int64), ("contig", C.c_void_p), ("start", C.c_void_p), ("mapq", C.c_void_p),
                 ("flags", C.c_void_p), ("sample", C.c_void_p), ("seq_off", C.c_void_p), ("seq_len", C.c_void_p),
                 ("seq", C.c_void_p), ("qual", C.c_void_p), ("cigar_off", C.c_void_p), ("n_cigar", C.c_void_p),
-                ("cigar", C.c_void_p), ("md_off", C.c_void_p), ("md_len", C.c_void_p), ("md", C.c_void_p)]
+                ("cigar", C.c_void_p), ("md_off", C.c_void_p), ("md_len", C.c_void_p), ("md", C.c_void_p),
+                ("n_sample_names", C.c_int32), ("sample_names", C.POINTER(C.c_char_p))]
 
 
 class or_loci(C.Structure):
@@ -79,7 +80,9 @@ class _Marshalled:
                      np.ascontiguousarray(rs.md_off, np.int64), np.ascontiguousarray(rs.md_len, np.int32),
                      np.ascontiguousarray(rs.md, np.uint8)]
         k = self.keep
-        self.s = or_reads(rs.n, *[_ptr(a) for a in k])
+        names = list(getattr(rs, "sample_names", []) or [])
+        self.names = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+        self.s = or_reads(rs.n, *[_ptr(a) for a in k], len(names), C.cast(self.names, C.POINTER(C.c_char_p)))
 
 
 class _Loci:
@@ -308,3 +311,24 @@ def heap_orders(sets, loci, every: int = 1):
         key = (int(f[0]), int(f[1]))
         out.setdefault(key, [None] * len(sets))[int(f[2])] = [int(x) for x in f[3].split(",")] if f[3] else []
     return out
+
+
+def scala_group_order(hashes) -> List[int]:
+    """or_scala_group_order: groupBy's Map iteration order over keys with these hashes."""
+    n = len(hashes)
+    h = np.ascontiguousarray(np.array(hashes, np.uint64).astype(np.uint32))
+    out = np.zeros(max(n, 1), np.int32)
+    lib().or_scala_group_order(C.c_void_p(_ptr(h)), n, C.c_void_p(out.ctypes.data))
+    return out[:n].tolist()
+
+
+def scala_allele_hash(ref: str, alt: str) -> int:
+    f = lib().or_scala_allele_hash
+    f.restype = C.c_uint32
+    return int(f(ref.encode("latin-1"), alt.encode("latin-1")))
+
+
+def scala_genotype_hash(a1, a2) -> int:
+    f = lib().or_scala_genotype_hash
+    f.restype = C.c_uint32
+    return int(f(*[x.encode("latin-1") for x in (a1[0], a1[1], a2[0], a2[1])]))

@@ -126,3 +126,50 @@ def test_deep_panel_500x_tumor_normal(gpu_ctx):
         want = O.somatic_standard(t, n, loci, **params)
         assert_rows_match(got, want)
     assert len(want) > 0
+
+
+@pytest.fixture
+def deep_everywhere(monkeypatch):
+    """GQ_DBG=64: the fast caller hands every candidate to the deep caller (global-memory
+    element records, no depth limit), so the deep kernel runs over every ordinary case too."""
+    monkeypatch.setenv("GQ_DBG", "64")
+    yield
+
+
+@pytest.mark.parametrize("tumor,normal", PAIRS, ids=["tough", "simplefp", "syn1fp", "complexvar"])
+def test_deep_caller_on_fixture_pairs(gpu_ctx, deep_everywhere, tumor, normal):
+    t = load_reads(fixture(tumor), TN_FILTERS)
+    n = load_reads(fixture(normal), TN_FILTERS)
+    loci = _loci(t)
+    for params in (dict(apply_filters=0), dict(SUITE, apply_filters=1)):
+        got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+        assert_rows_match(got, O.somatic_standard(t, n, loci, **params))
+
+
+def test_deep_caller_on_synthetic_window(gpu_ctx, deep_everywhere):
+    L = 60_000
+    tg = generate(L, 60.0, seed=20261015 + 3, somatic_rate=1e-3, tumor=True, read_seed=31)
+    ng = generate(L, 30.0, seed=20261015 + 3, somatic_rate=1e-3, tumor=False, read_seed=32)
+    t, n = tg.to_read_set(), ng.to_read_set()
+    loci = _loci(t)
+    got = somatic_standard_reads(gpu_ctx, t, n, loci, apply_filters=1)
+    want = O.somatic_standard(t, n, loci, apply_filters=1)
+    assert len(want) > 0
+    assert_rows_match(got, want)
+
+
+def test_1000x_panel_over_several_tasks(gpu_ctx):
+    """1000x tumor / 1000x normal over 3 kb split into 4 tasks: every task's first pileup is a
+    heap-ordered group of ~1000 reads per sample (no capacity limit: the deep caller), and the
+    likelihood normalisation underflows as the reference's does (Likelihood.scala:191-193,
+    SURVEY Appendix A #15)."""
+    L = 3_000
+    tg = generate(L, 1000.0, seed=20261015 + 5, somatic_rate=2e-3, tumor=True, read_seed=41)
+    ng = generate(L, 1000.0, seed=20261015 + 5, somatic_rate=2e-3, tumor=False, read_seed=42)
+    t, n = tg.to_read_set(), ng.to_read_set()
+    ls = LociSet.parse("all").result(t.contig_lengths_map)
+    loci = flatten_partitions(partition_loci_uniformly(4, ls), t.contig_index())
+    for params in (dict(apply_filters=0), dict(apply_filters=1, max_tumor_read_depth=100000)):
+        got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+        want = O.somatic_standard(t, n, loci, **params)
+        assert_rows_match(got, want)
