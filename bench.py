@@ -230,11 +230,15 @@ def main() -> int:
         "calls": len(calls),
         "complex_loci": int(calls.complex_loci),
         "ambiguous_loci": int(calls.ambiguous_loci),
+        # loci with a count tie among passing alleles (their order is the restated Scala map
+        # order), and loci whose order also depends on first occurrences (redone in element order)
+        "tie_loci": int(calls.tie_loci),
+        "order_loci": int(ctx.timings()["order_loci"]),
         "gen_s": gen_s,
     }
     if rank == 0:
-        e2e = {"upload_ms": upload_ms, "step_ms": line["ms_per_step"], "step_with_d2h_ms": host_ms_step,
-               "reads": n_reads}
+        e2e = {"upload_ms": upload_ms, "upload_h2d_ms": st["h2d_ms"], "upload_derive_ms": st["derive_ms"],
+               "step_ms": line["ms_per_step"], "step_with_d2h_ms": host_ms_step, "reads": n_reads}
         e2e.update(ingest_rate(args.depth))
         e2e["ingest_s_est"] = n_reads / e2e["ingest_reads_per_s"]
         e2e["single_pass_s_est"] = e2e["ingest_s_est"] + (upload_ms + host_ms_step) / 1e3
@@ -343,7 +347,8 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
     loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([L - 1], np.int64), np.array([0], np.int64))
     for _ in range(warmup):
         ctx.somatic_standard(t, n, loci)
-    stages = {"pileup_ms": [], "complex_ms": [], "finalize_ms": [], "total_ms": []}
+    stages = {"pileup_ms": [], "complex_ms": [], "call_ms": [], "deep_ms": [], "finalize_ms": [], "total_ms": [],
+              "host_ms": [], "marshal_ms": []}
     t1 = time.perf_counter()
     for _ in range(steps):
         calls = ctx.somatic_standard(t, n, loci)
@@ -351,6 +356,7 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
         for k in stages:
             stages[k].append(tm[k])
     el = time.perf_counter() - t1
+    tm = ctx.timings()
     ta = tg.arrays
     b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
              + 8 * ng.n)
@@ -363,7 +369,18 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
             "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": warmup,
             "config": {"workload": "somatic-standard, synthetic tumor/normal 60x/30x, chr1-length contig (configs[2])",
                        "loci": L - 1, "visited_loci": visited, "tumor_reads": tg.n, "normal_reads": ng.n},
-            "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items()},
+            "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items() if k not in ("host_ms", "marshal_ms")},
+            # the step's wall time beyond the device span: the C-ABI call's own host time (launch
+            # gaps at its capacity checks, the results' D2H, sort and marshalling) and the ctypes
+            # wrapping of the arrays
+            "host_ms": {"call_wall_ms": float(np.mean(stages["host_ms"])),
+                        "beyond_device_ms": float(np.mean(stages["host_ms"]) - np.mean(stages["total_ms"])),
+                        "marshal_ms": float(np.mean(stages["marshal_ms"])),
+                        "python_ms": 1e3 * el / steps - float(np.mean(stages["host_ms"]))},
+            "caller": {"kernel": "somatic_call", "fast_ms": float(np.mean(stages["call_ms"])),
+                       "deep_ms": float(np.mean(stages["deep_ms"])), "candidates": int(calls.candidate_loci),
+                       "deep_candidates": int(tm["deep_loci"]), "deep_max_depth": int(tm["deep_max"]),
+                       "ns_per_candidate": 1e6 * float(np.mean(stages["call_ms"])) / max(1, int(calls.candidate_loci))},
             "roofline": {"bound": "hbm", "kernel": "somatic_proj", "kernel_ms": k_ms, "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes},

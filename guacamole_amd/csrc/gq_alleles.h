@@ -283,7 +283,17 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, int j) {
 __device__ __forceinline__ double lane_f64(double v, int j) {
   return __builtin_bit_cast(double, lane_u64(__builtin_bit_cast(uint64_t, v), j));
 }
-// Minimum over the wave (every lane active).
+// Minimum / maximum over the wave (every lane active).
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v = min(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d, 64));
+  return v;
+}
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {

@@ -60,11 +60,9 @@ __device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n
 }
 
 __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_PROJ_WPE))) void germline_proj(
-    const Tile *__restrict__ tiles, int64_t n_tiles, const uint32_t *__restrict__ pcs,
-    const int64_t *__restrict__ pbase, const uint8_t *__restrict__ pbad, const uint8_t *__restrict__ proj,
-    const int64_t *__restrict__ qoff,
-    const int64_t *__restrict__ sbase, const uint2 *__restrict__ pev,
-    const int64_t *__restrict__ pev_off, int n_samples, int threshold, int emit_ref, int emit_no_call,
+    const Tile *__restrict__ tiles, const TileX *__restrict__ tilex, int64_t n_tiles, const uint32_t *__restrict__ pcs,
+    const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev, int n_samples, int threshold, int emit_ref,
+    int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
   // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the projection loads,
@@ -96,23 +94,39 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
   auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
+  // the tile record (Tile + TileX: dword d on lane d < 32) of the wave's next tile, loaded one
+  // tile ahead: its fields are in a register when the tile starts (no dependent setup rounds)
+  auto fetch = [&](int64_t t) -> uint32_t {
+    const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tiles + t);
+    const uint32_t *x32 = reinterpret_cast<const uint32_t *>(tilex + t);
+    return lane < 16 ? t32[lane] : lane < 32 ? x32[lane - 16] : 0u;
+  };
+  auto f32 = [](uint32_t rec, int d) { return (uint32_t)__builtin_amdgcn_readlane((int)rec, d); };
+  auto f64 = [&](uint32_t rec, int d) { return (int64_t)((uint64_t)f32(rec, d) | ((uint64_t)f32(rec, d + 1) << 32)); };
+  uint32_t next_rec = i0 + wave < i1 ? fetch(i0 + wave) : 0u;
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    const Tile tl = tiles[i];
-    const int32_t L0 = tl.L0, L1 = tl.L1;
-    const int64_t rb = tl.rb, re = tl.re;
+    const uint32_t rec = next_rec;
+    if (i + C::kWaves < i1) next_rec = fetch(i + C::kWaves);
+    // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8; TileX from dw 16: sb0, sb4,
+    // e0, e1, pb0 (16-25), pbd[4] (26-29), pbad4 (30)
+    const int32_t L0 = (int32_t)f32(rec, 7), L1 = (int32_t)f32(rec, 8);
+    const int64_t rb = f64(rec, 2), re = f64(rec, 4);
     const int32_t B0 = L0 & ~(T - 1);
     if (re <= rb) continue;  // no reads: nothing visited
-    // ---- the block's slices (one per group): their piece ranges and pbad flags, the first
-    //      kEnt sparse entries per lane of the window's reads, and the first three 16-piece
-    //      stages of each group's piece records, loaded together.  A pbad slice (a read the
-    //      projection cannot take) or more than kMaxRows pieces in a slice: the walker.
-    const int64_t qs = tl.qs;  // the block's first slice (a multiple of 4; qoff[contig] + (B0 >> 7))
-    const int64_t sb0 = sbase[qs], sb4 = sbase[qs + 4];
-    const int64_t pbg = pbase[qs + g];
-    const int32_t ng = (int32_t)(pbase[qs + g + 1] - pbg);
-    const uint32_t badg = pbad[qs + g];
-    const int64_t e0 = pev_off[rb], e1 = pev_off[re];
+    // ---- the block's slices (one per group): their piece ranges and pbad flags (from the
+    //      record), the first kEnt sparse entries per lane of the window's reads and the first
+    //      three 16-piece stages of each group's piece records, loaded together.  A pbad slice
+    //      (a read the projection cannot take) or more than kMaxRows pieces in a slice: the walker.
+    const int64_t sb0 = f64(rec, 16), sb4 = f64(rec, 18);
+    const int32_t pd0 = (int32_t)f32(rec, 26), pd1 = (int32_t)f32(rec, 27), pd2 = (int32_t)f32(rec, 28),
+                  pd3 = (int32_t)f32(rec, 29);
+    const int32_t plo = g == 0 ? 0 : g == 1 ? pd0 : g == 2 ? pd1 : pd2;
+    const int32_t phi = g == 0 ? pd0 : g == 1 ? pd1 : g == 2 ? pd2 : pd3;
+    const int64_t pbg = f64(rec, 24) + plo;
+    const int32_t ng = phi - plo;
+    const uint32_t badg = (f32(rec, 30) >> (8 * g)) & 0xFFu;
+    const int64_t e0 = f64(rec, 20), e1 = f64(rec, 22);
     constexpr int NE = C::kEnt;
     uint2 ent[NE];
 #pragma unroll
@@ -122,12 +136,11 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       if (!(dbg & 2) && k < e1) ent[j] = pev[k];
     }
     const int32_t l16 = lane & 15;
-    auto stage = [&](int32_t k) -> uint32_t {  // piece record of row k + l16 of this group (0: none)
-      return k + l16 < ng ? pcs[pbg + k + l16] : 0u;
+    auto stage = [&](int32_t k) -> uint32_t {  // piece record of row k + l16 of this group
+      return k + l16 < ng ? pcs[pbg + k + l16] : kPieceNone;
     };
     uint32_t P0 = stage(0), P1 = stage(16), P2 = stage(32);
-    const int32_t nmax = max(max(__builtin_amdgcn_readlane(ng, 0), __builtin_amdgcn_readlane(ng, 16)),
-                             max(__builtin_amdgcn_readlane(ng, 32), __builtin_amdgcn_readlane(ng, 48)));
+    const int32_t nmax = max(max(pd0, pd1 - pd0), max(pd2 - pd1, pd3 - pd2));
     if (__ballot(badg != 0) != 0 || nmax > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
@@ -155,6 +168,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       nn = 0;
     };
     const int32_t bp = (lane & 48) << 2;  // ds_bpermute address of the group's lane 0
+    // lane offset B + l16 - 16 (dbg & 1, diagnostics: every load out of range)
+    const uint32_t lm16 = (dbg & 1) ? 0x10000000u : (uint32_t)l16 - 16u, ibit = 16u + (uint32_t)l16;
     auto issue = [&](uint32_t P, int u0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
       uint32_t rv[U];
 #pragma unroll
@@ -162,8 +177,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t rr = rv[u];
-        const uint32_t d = (uint32_t)l16 - (rr & 15u);
-        const uint32_t voff = d < ((rr >> 4) & 31u) && !(dbg & 1) ? ((rr >> 9) + d) << 3 : 0x80000000u;
+        // (B + l16 - 16) * 8 | (lane invalid) << 31 (PieceRec)
+        const uint32_t inv = (rr >> ibit) & 1u;
+        const uint32_t voff = (((rr & 0xFFFFu) + lm16) << 3) | (inv << 31);
         const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
         w0[u] = w[0];
         w1[u] = w[1];
@@ -214,12 +230,12 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     for (int32_t k0 = 0;; k0 += 16) {  // P0: rows k0 .. k0 + 15, P1: the next 16, P2: the 16 after
       issue(P0, 3 * U, d0, d1);
       const bool more = k0 + 16 < nmax;  // wave-uniform
-      count(a0, a1);
-      if (more) issue(P1, 0, a0, a1);
+      count(a0, a1);  // past the last stage P1 is all kPieceNone: the loads fall out of range
+      issue(P1, 0, a0, a1);
       count(b0, b1);
-      if (more) issue(P1, U, b0, b1);
+      issue(P1, U, b0, b1);
       count(c0, c1);
-      if (more) issue(P1, 2 * U, c0, c1);
+      issue(P1, 2 * U, c0, c1);
       count(d0, d1);
       if (!more) break;
       P0 = P1;
@@ -308,10 +324,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const uint32_t mask = (mw & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
                               (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
         const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-        const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - L0));
+        const uint64_t ord = (uint64_t)(f64(rec, 0) + (pos - L0));
         CallRec rr;
         rr.key = ord << 12;
-        rr.contig = tl.contig;
+        rr.contig = (int32_t)f32(rec, 6);
         rr.pos = pos;
         rr.sample = 0;
         if (kind == 1) {

@@ -50,6 +50,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_dead;       // record slots germline_expand left unused
   unsigned long long part_max[2];  // largest partition count of records / complex items (part_scan)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
+  unsigned long long n_ord;        // germline loci whose Scala map order depends on element order
   unsigned long long n_deep;       // somatic candidates handed to the deep caller
   unsigned long long deep_max;     // deepest per-sample pileup among them and the listed loci
   // per-tile run counters, spread over kSpread addresses (summed on the host)
@@ -300,6 +301,10 @@ struct Plan {
     int64_t r0, r1;  // ranges [r0, r1)
   };
   std::vector<Win> wins;
+  // device copies (plan(), in the context's ranges buffer: valid until its next plan()): the
+  // ranges' starts / ends, each range's window, each window's contig and first range (+ end)
+  const int64_t *d_rs = nullptr, *d_re = nullptr, *d_wroff = nullptr;
+  const int32_t *d_rwin = nullptr, *d_wcontig = nullptr;
   int64_t range_of_tile(int64_t t) const {  // last range whose first tile <= t
     return (int64_t)(std::upper_bound(rt.begin(), rt.end(), t) - rt.begin()) - 1;
   }
@@ -357,6 +362,7 @@ struct gq_ctx {
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
   gq::DevBuf deep_list, deep_scratch;              // somatic: the deep caller's list and per-wave scratch
+  gq::DevBuf win_bound;                            // germline: window bounds (window_bounds)
   gq::DevBuf bkt;                                  // germline output order: bucket counts / offsets / fill
   void *pin = nullptr;                             // pinned host staging for the small per-call copies
   size_t pin_n = 0;
@@ -381,6 +387,7 @@ struct gq_dev_reads {
   int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // projection sizes (derive_shape)
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
   int64_t n_pieces = 0;                                    // germline_proj piece records (PieceRec)
+  float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
   mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
   mutable int mproj_mapq = -1;
 };

@@ -94,15 +94,17 @@ constexpr int32_t kProjNone = (int32_t)0x80000000;
 //     on a deleted base);
 //   y bit 31 set: loci [x, x + (y & 0x7FFFFFFF)) hold complex elements (insertion / deletion
 //     anchors, mid-deletions, clipped N-skips): the exact kernel decides them.
-// A PIECE is one read's run of words inside one slice.  Its record (PieceRec, one u32) lets
-// the 16 lanes owning the slice find their word without any per-read arithmetic beyond a
-// subtract and a compare:
-//   bits 0-3  s0: the piece's first column inside the slice (0-15)
-//   bits 4-8  len: its columns (1-16)
-//   bits 9-31 the word of its first column, counted from the first word of the slice's
-//             512-locus block (sbase[slot & ~3]); a block of more than 2^23 words is pbad
-// Lane l16 of the slice's group reads word (rec >> 9) + (l16 - s0) when 0 <= l16 - s0 < len.
-constexpr int kPieceBaseBits = 23;
+// A PIECE is one read's run of words inside one slice.  Its record (PieceRec, one u32) gives
+// each of the 16 lanes owning the slice its word in four ALU ops, with no compare or select:
+//   bits 0-15   B = (the word of the piece's first column, counted from the first word of the
+//               slice's 512-locus block) - s0 + 16, s0 = the piece's first column in the slice
+//               (0-15); lane l16 of the group reads word B + l16 - 16
+//   bits 16-31  the lanes NOT in the piece: bit j set unless s0 <= j < s0 + len
+// so voff = ((B + l16 - 16) << 3) | (bit (16 + l16) << 31): an invalid lane's offset is out of
+// the buffer's range and its load returns 0.  kPieceNone (every lane invalid) pads a stage.  A
+// block of more than kPieceBaseMax words is pbad (the walker takes it).
+constexpr uint32_t kPieceNone = 0xFFFF0000u;
+constexpr int64_t kPieceBaseMax = 65535 - 16;
 constexpr uint32_t kPevComplex = 0x80000000u;
 constexpr uint32_t kPevNone = 7u << 4;  // a padding entry (no effect)
 
@@ -135,6 +137,20 @@ struct Tile {
   };
 };
 static_assert(sizeof(Tile) == 64, "Tile layout");
+
+// Setup record of an aligned projection tile (plan_tiles, beside its Tile): the slice and
+// sparse-entry offsets germline_proj would otherwise load in two dependent rounds per tile.
+// germline_proj holds the next tile's Tile + TileX in one VGPR (a dword per lane 0-31) while it
+// counts the current one.
+struct TileX {
+  int64_t sb0, sb4;   // sbase[qs], sbase[qs + 4]: the block's projection words
+  int64_t e0, e1;     // pev_off[rb], pev_off[re]: the window's sparse entries
+  int64_t pb0;        // pbase[qs]: the block's first piece record
+  int32_t pbd[4];     // pbase[qs + g + 1] - pbase[qs]: end of slice g's pieces
+  uint32_t pbad4;     // byte g: pbad[qs + g]
+  uint32_t pad;
+};
+static_assert(sizeof(TileX) == 64, "TileX layout");
 
 // Per-call record written by the germline kernels, sorted by `key` afterwards.
 struct CallRec {

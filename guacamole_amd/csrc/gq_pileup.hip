@@ -90,7 +90,7 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
                            const int64_t *__restrict__ r_end, const int64_t *__restrict__ r_ord,
                            const int64_t *__restrict__ r_tile0, int64_t n_ranges, int64_t n_tiles, int T,
                            DevReads R, Tile *__restrict__ tiles, int stage_cap, int meta_cap, int ev_cap,
-                           int aligned) {
+                           int aligned, TileX *__restrict__ tilex) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tiles) return;
   int64_t lo = 0, hi = n_ranges - 1;  // largest r with r_tile0[r] <= t
@@ -181,6 +181,25 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   //  their setup skips a dependent qoff load)
   if (aligned && stage_cap == 0 && R.qoff) tl.qs = R.qoff[c] + blk / 128;
   tiles[t] = tl;
+  if (tilex) {  // aligned projection tiles: germline_proj's per-tile setup, resolved here
+    TileX x{};
+    if (R.sbase && R.qoff && a0 > rb) {
+      const int64_t qs = tl.qs;
+      x.sb0 = R.sbase[qs];
+      x.sb4 = R.sbase[qs + 4];
+      x.e0 = R.pev_off[rb];
+      x.e1 = R.pev_off[a0];
+      x.pb0 = R.pbase[qs];
+      uint32_t bad = 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        x.pbd[g] = (int32_t)min<int64_t>(R.pbase[qs + g + 1] - x.pb0, INT32_MAX);
+        bad |= (R.pbad[qs + g] ? 1u : 0u) << (8 * g);
+      }
+      x.pbad4 = bad;
+    }
+    tilex[t] = x;
+  }
 }
 
 // Column-kernel records (derived once at upload, after read_shape).  A general-CIGAR read
@@ -363,7 +382,7 @@ __global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsign
 }
 
 // The piece records (PieceRec), one wave per slice: the slice's reads in read order, each with
-// words there gets {s0, len, its first word from the block's first word}.
+// words there gets {its first word from the block's first word - s0 + 16, its invalid lanes}.
 __global__ __launch_bounds__(256) void piece_fill(DevReads R, int64_t n_slices, uint32_t *__restrict__ pcs,
                                                   uint8_t *__restrict__ pbad) {
   const int lane = threadIdx.x & 63;
@@ -412,8 +431,10 @@ __global__ __launch_bounds__(256) void piece_fill(DevReads R, int64_t n_slices, 
       const int64_t k = np + (int64_t)__popcll(has & ((1ull << lane) - 1ull));
       const int64_t w = wb + run + (int64_t)ex;
       if (sl > 0) {
-        over = over || w >= (1ll << kPieceBaseBits);
-        pcs[pb + k] = ((uint32_t)w << 9) | ((uint32_t)sl << 4) | (uint32_t)(s0 - qc0);
+        over = over || w > kPieceBaseMax;
+        const uint32_t s0r = (uint32_t)(s0 - qc0);
+        const uint32_t valid = ((1u << sl) - 1u) << s0r;  // lanes s0 .. s0 + len - 1 (sl <= 16 - s0r)
+        pcs[pb + k] = ((~valid & 0xFFFFu) << 16) | (((uint32_t)w + 16u - s0r) & 0xFFFFu);
       }
       run += (int64_t)__builtin_amdgcn_readlane((int)(ex + (uint32_t)sl), 63);
       np += (int64_t)__popcll(has);
@@ -771,9 +792,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     for (int d = 1; d < 64; d <<= 1) mask |= __shfl_xor(mask, d, 64);
     const bool ambiguous = __popc(mask) > 1;
     uint8_t refbase = 'N';
-    if (amb_in) {
+    if (amb_in && amb_ref) {
       refbase = amb_ref[li];
-    } else if (ambiguous) {
+    } else if (ambiguous && !amb_in) {
       // listed for the heap-order replay; a wide tile's visit is counted here, once
       if (lane == 0) {
         if (item.flags & 1) {
@@ -821,11 +842,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         }
       }
       const int64_t okey = act ? element_order_key(R, r, pos, wio, sw.init_reads, sw.init_rank) : INT64_MAX;
+      // slots run in read order, so with no initial-group read in the batch the first element
+      // of a group is its lowest lane (no wave reduction)
+      const bool by_lane = __ballot(act && okey < (1ll << 40)) == 0;
       // per-sample totals and first elements
       for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
         const unsigned long long b = __ballot(act && smp == sm);
         if (!b) continue;  // uniform
-        const int64_t f = wave_min_i64(act && smp == sm ? okey : INT64_MAX);
+        const int64_t f = by_lane ? lane_u64(okey, __ffsll((long long)b) - 1)
+                                  : wave_min_i64(act && smp == sm ? okey : INT64_MAX);
         if (lane == sm) {
           st_lane += (uint32_t)__popcll(b);
           st_first = f < st_first ? f : st_first;
@@ -874,7 +899,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         }
         if (found >= 0) {
           const int owner = found & 63, sl = found >> 6;
-          const int64_t f = wave_min_i64(match ? okey : INT64_MAX);
+          const int64_t f = by_lane ? lane_u64(okey, leader) : wave_min_i64(match ? okey : INT64_MAX);
 #pragma unroll
           for (int s = 0; s < kSlots; ++s)
             if (s == sl && lane == owner) {
@@ -904,18 +929,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     const int ns_all = R.n_samples < 8 ? R.n_samples : 8;
     uint64_t tkey[kSlots];
     bool dep = false;
-    {
+    int tsm[kSlots];
+    bool tpass[kSlots];
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const bool live = s * 64 + lane < nt;
+      tsm[s] = live ? (int)tdesc[s].pad : -1;
+      const uint32_t tot = (uint32_t)__shfl((int)st_lane, tsm[s] < 0 ? 0 : tsm[s], 64);
+      tpass[s] = live && tot > 0 && (long long)tcnt[s] * 100 / (long long)tot > threshold;
+      tkey[s] = 0;
+    }
+    // the map order only decides between passing entries of one sample with equal counts
+    bool tie_any = false;
+#pragma unroll
+    for (int s2 = 0; s2 < kSlots; ++s2) {
+      unsigned long long pb = __ballot(tpass[s2]);
+      while (pb && !tie_any) {
+        const int ow = __ffsll((long long)pb) - 1;
+        pb &= pb - 1;
+        const int smj = __builtin_amdgcn_readlane(tsm[s2], ow);
+        const int cj = __builtin_amdgcn_readlane((int)tcnt[s2], ow);
+        bool hit = false;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+          hit |= tpass[s] && tsm[s] == smj && (int)tcnt[s] == cj && !(s == s2 && lane == ow);
+        tie_any = __ballot(hit) != 0;
+      }
+    }
+    if (tie_any) {
       uint32_t tb[kSlots];
-      int tsm[kSlots];
-      bool tpass[kSlots];
 #pragma unroll
       for (int s = 0; s < kSlots; ++s) {
-        const bool live = s * 64 + lane < nt;
-        const uint32_t h = live ? allele_scala_hash(R, tdesc[s], pos) : 0u;
+        const uint32_t h = tsm[s] >= 0 ? allele_scala_hash(R, tdesc[s], pos) : 0u;
         tb[s] = scala::mutable_bucket(h, 4);
-        tsm[s] = live ? (int)tdesc[s].pad : -1;
-        const uint32_t tot = (uint32_t)__shfl((int)st_lane, tsm[s] < 0 ? 0 : tsm[s], 64);
-        tpass[s] = live && tot > 0 && (long long)tcnt[s] * 100 / (long long)tot > threshold;
         tkey[s] = scala::trie_key(h);  // five or more alleles in the sample: HashTrieMap order
       }
       // entries of the same sample, and same-bucket ties among passing ones
@@ -949,10 +995,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       }
     }
     // samples: lane sm < 8 holds its rank among the present samples
-    int srank = lane;
-    {
-      const bool present = lane < ns_all && st_lane > 0;
-      const int np = __popcll(__ballot(present));
+    int srank = 0;
+    const bool present = lane < ns_all && st_lane > 0;
+    const int np = __popcll(__ballot(present));
+    if (np > 1) {
       uint64_t sk = ~0ull;
       uint32_t sb = 16u + (uint32_t)lane;
       if (R.sample_hash && present) {
@@ -975,11 +1021,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       srank = rk;
       if (__ballot(same_bucket) != 0) dep = true;
     }
-    if (__ballot(dep) != 0 && !amb_in) {
-      // the order depends on first occurrences: redone with the windows' element order
+    // (sw without init_reads: window bounds only; past a window's initial group the elements
+    //  are in read order, which the keys above already used)
+    if (__ballot(dep) != 0 && !amb_in && (sw.init_reads || !sw.wi || pos < wio.E)) {
+      // the order depends on first occurrences: listed (after the amb list's capacity) and
+      // redone with the windows' element order (amb_ref == nullptr: the base is not ambiguous)
       if (lane == 0) {
-        const unsigned long long k = atomicAdd(&ctr->n_amb, 1ull);
-        if (k < amb_cap) amb_out[k] = AmbItem{item.tile, pos, it};
+        const unsigned long long k = atomicAdd(&ctr->n_ord, 1ull);
+        if (k < amb_cap) amb_out[amb_cap + k] = AmbItem{item.tile, pos, it};
       }
       continue;
     }
@@ -1823,6 +1872,7 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   gq_dev_reads *d = new gq_dev_reads();
   d->ctx = c;
   const int64_t n = h->n_reads;
+  const auto t0 = std::chrono::steady_clock::now();
   H2DStager stager(c->stream);
   {
     hipError_t e = stager.init();
@@ -1955,7 +2005,14 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   }
   d->contig_read_begin.assign(h->contig_read_begin, h->contig_read_begin + h->n_contigs + 1);
   d->seq_bytes = h->seq_bytes;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    gq_reads_free(d);
+    return set_err(GQ_E_HIP, "gq_reads_upload: copies");
+  }
+  const auto t1 = std::chrono::steady_clock::now();
+  d->h2d_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   gq_status st2 = derive_shape(c, d, h->md_len);
+  d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
   if (st2) {
     gq_reads_free(d);
     return st2;
@@ -2004,7 +2061,9 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
     return set_err(GQ_E_HIP, "wrap: contig_read_begin D2H: %s", hipGetErrorString(e));
   }
   d->seq_bytes = h->seq_bytes;
+  const auto t1 = std::chrono::steady_clock::now();
   gq_status st2 = derive_shape(c, d, h->md_len);
+  d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
   if (st2) {
     gq_reads_free(d);
     return st2;
@@ -2021,6 +2080,8 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->pev_count = d->pev_count;
   out->n_pieces = d->n_pieces;
   out->proj_reads = d->proj_reads;
+  out->h2d_ms = d->h2d_ms;
+  out->derive_ms = d->derive_ms;
   return GQ_OK;
 }
 
@@ -2077,28 +2138,45 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   pl.n_tiles = tiles;
   pl.n_loci = ord;
   if (tiles == 0) return GQ_OK;
-  const size_t nr = rc.size();
-  HIP_TRY(c->ranges.ensure(nr * (4 + 8 * 4) + 64));
+  const size_t nr = rc.size(), nw = pl.wins.size();
+  // device layout: rc | rs re ro rt | w_roff (nw + 1) | rwin | w_contig
+  const size_t o_rs = (nr * 4 + 15) & ~(size_t)15, o_wroff = o_rs + 4 * 8 * nr, o_rwin = o_wroff + 8 * (nw + 1),
+               o_wc = o_rwin + ((4 * nr + 15) & ~(size_t)15), bytes = o_wc + 4 * nw;
+  HIP_TRY(c->ranges.ensure(bytes + 64));
   char *base = (char *)c->ranges.p;
   int32_t *d_rc = (int32_t *)base;
-  int64_t *d_rs = (int64_t *)(base + ((nr * 4 + 15) & ~(size_t)15));
+  int64_t *d_rs = (int64_t *)(base + o_rs);
   int64_t *d_re = d_rs + nr, *d_ro = d_re + nr, *d_rt = d_ro + nr;
-  HIP_TRY(c->ranges.ensure((size_t)((char *)(d_rt + nr) - base)));
   {  // one H2D copy from pinned staging (the previous call's copy has completed: every call syncs)
-    const size_t bytes = (size_t)((char *)(d_rt + nr) - base);
     HIP_TRY(c->pinned(bytes));
     char *hb = (char *)c->pin;
-    memcpy(hb + ((char *)d_rc - base), rc.data(), nr * 4);
-    memcpy(hb + ((char *)d_rs - base), rs.data(), nr * 8);
-    memcpy(hb + ((char *)d_re - base), re.data(), nr * 8);
-    memcpy(hb + ((char *)d_ro - base), ro.data(), nr * 8);
-    memcpy(hb + ((char *)d_rt - base), rt.data(), nr * 8);
+    memcpy(hb, rc.data(), nr * 4);
+    memcpy(hb + o_rs, rs.data(), nr * 8);
+    memcpy(hb + o_rs + 8 * nr, re.data(), nr * 8);
+    memcpy(hb + o_rs + 16 * nr, ro.data(), nr * 8);
+    memcpy(hb + o_rs + 24 * nr, rt.data(), nr * 8);
+    int64_t *wroff = (int64_t *)(hb + o_wroff);
+    int32_t *wc = (int32_t *)(hb + o_wc);
+    for (size_t w = 0; w < nw; ++w) {
+      wroff[w] = pl.wins[w].r0;
+      wc[w] = pl.wins[w].contig;
+    }
+    wroff[nw] = (int64_t)nr;
+    memcpy(hb + o_rwin, pl.rwin.data(), nr * 4);
     HIP_TRY(hipMemcpyAsync(base, hb, bytes, hipMemcpyHostToDevice, c->stream));
   }
-  HIP_TRY(tiles_buf.ensure((size_t)tiles * sizeof(Tile)));
+  pl.d_rs = d_rs;
+  pl.d_re = d_re;
+  pl.d_wroff = (const int64_t *)(base + o_wroff);
+  pl.d_rwin = (const int32_t *)(base + o_rwin);
+  pl.d_wcontig = (const int32_t *)(base + o_wc);
+  // aligned 512-locus plans over projected reads carry a TileX per tile after the Tiles
+  const bool with_x = aligned && T == 512 && rd->d.sbase != nullptr;
+  HIP_TRY(tiles_buf.ensure((size_t)tiles * (sizeof(Tile) + (with_x ? sizeof(TileX) : 0))));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
-                     tiles, T, rd->d, (Tile *)tiles_buf.p, stage_cap, meta_cap, ev_cap, aligned ? 1 : 0);
+                     tiles, T, rd->d, (Tile *)tiles_buf.p, stage_cap, meta_cap, ev_cap, aligned ? 1 : 0,
+                     with_x ? (TileX *)((Tile *)tiles_buf.p + tiles) : (TileX *)nullptr);
   HIP_TRY(hipGetLastError());
   return GQ_OK;
 }
@@ -2136,7 +2214,8 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                     (const Tile *)c->tiles.p, tiles, R.pcs, R.pbase, R.pbad, R.proj, R.qoff, R.sbase, R.pev, R.pev_off, R.n_samples,
+                     (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.pcs, R.proj,
+                     R.pev, R.n_samples,
                      p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // column kernel | walker kernel
@@ -2183,7 +2262,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   unsigned long long pool_cap = 1 << 22, amb_cap = 4096;
   Counters hc{};
   for (int attempt = 0; attempt < 3; ++attempt) {
-    HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
+    HIP_TRY(c->amb.ensure(2 * amb_cap * sizeof(AmbItem)));  // heap-order loci, then order-dependent loci
     HIP_TRY(c->recs.ensure(og.total(0) * sizeof(CallRec)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
     HIP_TRY(c->pool.ensure(pool_cap));
@@ -2201,11 +2280,18 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
 #define GQ_CPLX_BLOCKS 4096
 #endif
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pl.n_tiles, 1), GQ_CPLX_BLOCKS);
+    // each window's initial-group bound: an order-dependent locus past it needs no re-run
+    SomWin wb{};
+    st = window_bounds(c, pl, rd, wb);
+    if (st) {
+      free(res);
+      return st;
+    }
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 1, og);
     hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
                        (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap,
-                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg(), SomWin{});
+                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg(), wb);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
@@ -2234,9 +2320,42 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       pool_cap = hc.pool_used + 4096;
       retry = true;
     }
-    if (hc.n_amb > amb_cap) {
-      amb_cap = hc.n_amb + 1024;
+    if (hc.n_amb > amb_cap || hc.n_ord > amb_cap) {
+      amb_cap = std::max(hc.n_amb, hc.n_ord) + 1024;
       retry = true;
+    }
+    // the windows' element order (initial groups in heap order) for the re-runs below: the
+    // first occurrences the Scala map orders of those loci depend on
+    SomWin sw{};
+    if (!retry && (hc.n_amb > 0 || hc.n_ord > 0) && !hc.err) {
+      st = build_somwin(c, pl, rd, rd, sw);
+      if (st) {
+        free(res);
+        return st;
+      }
+    }
+    if (!retry && hc.n_ord > 0 && !hc.err) {
+      // loci whose output order depends on first occurrences in element order
+      const int oblocks = (int)std::min<int64_t>(((int64_t)hc.n_ord + 3) / 4, 4096);
+      hipLaunchKernelGGL(germline_complex, dim3(oblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
+                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
+                         (unsigned long long)0, (const AmbItem *)c->amb.p + amb_cap, (const uint8_t *)nullptr,
+                         (int64_t)hc.n_ord, gq_dbg(), sw);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (hc.part_max[0]) {
+        og.capA[0] += hc.part_max[0] + 64;
+        og.capB[0] += hc.part_max[0] + 64;
+        retry = true;
+      }
+      if (hc.pool_used > pool_cap) {
+        pool_cap = hc.pool_used + 4096;
+        retry = true;
+      }
     }
     if (!retry && hc.n_amb > 0 && !hc.err) {
       // loci whose reference base depends on heap order: replay the window's queue, then the
@@ -2246,14 +2365,6 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       HIP_TRY(hipStreamSynchronize(c->stream));
       HIP_TRY(c->amb_ref.ensure(amb.size()));
       st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
-      if (st) {
-        free(res);
-        return st;
-      }
-      // the windows' element order (initial groups in heap order), for the first occurrences
-      // the Scala map orders of the listed loci depend on
-      SomWin sw{};
-      st = build_somwin(c, pl, rd, rd, sw);
       if (st) {
         free(res);
         return st;
@@ -2410,6 +2521,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[2]);
   c->timings.walk_ms = ms;
   c->timings.walk_tiles = (int64_t)hc.n_slow;
+  c->timings.order_loci = (int64_t)hc.n_ord;
   (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
   c->timings.complex_ms = ms;
   (void)hipEventElapsedTime(&ms, c->ev[3], c->ev[4]);

@@ -1158,6 +1158,91 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   return GQ_OK;
 }
 
+// The records of a somatic / germline-standard pass (device SomRec array + allele pool) ->
+// the caller's result arrays in output (key) order.  The keys are sorted as (key, index) pairs
+// by an LSD radix sort (11-bit digits over the bits the largest key uses; skipped when the
+// records already come in order), then the fields are gathered once: the 176-byte records are
+// never moved.  ev[4] marks the end of the D2H; timings.marshal_ms is the host time after it.
+gq_status fetch_somatic_records(gq_ctx *c, const Counters &hc, unsigned long long pool_cap, gq_somatic_calls *res) {
+  const int64_t nr = (int64_t)hc.n_rec;
+  std::vector<SomRec> recs((size_t)nr);
+  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
+  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const auto m0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> idx((size_t)nr), tmp((size_t)nr);
+  uint64_t mx = 0;
+  bool sorted = true;
+  for (int64_t k = 0; k < nr; ++k) {
+    idx[(size_t)k] = (uint32_t)k;
+    mx = std::max(mx, recs[(size_t)k].key);
+    if (k && recs[(size_t)k].key < recs[(size_t)k - 1].key) sorted = false;
+  }
+  if (!sorted) {
+    constexpr int kD = 11;
+    std::vector<uint32_t> cnt(1u << kD);
+    for (int sh = 0; sh < 64 && (mx >> sh) != 0; sh += kD) {
+      std::fill(cnt.begin(), cnt.end(), 0u);
+      for (int64_t k = 0; k < nr; ++k) ++cnt[(recs[idx[(size_t)k]].key >> sh) & ((1u << kD) - 1)];
+      uint32_t o = 0;
+      for (uint32_t &x : cnt) {
+        const uint32_t t = x;
+        x = o;
+        o += t;
+      }
+      for (int64_t k = 0; k < nr; ++k) tmp[cnt[(recs[idx[(size_t)k]].key >> sh) & ((1u << kD) - 1)]++] = idx[(size_t)k];
+      idx.swap(tmp);
+    }
+  }
+  const size_t N = (size_t)std::max<int64_t>(nr, 1);
+  res->n = nr;
+  res->contig = (int32_t *)malloc(N * 4);
+  res->pos = (int64_t *)malloc(N * 8);
+  res->sample = (uint8_t *)calloc(N, 1);
+  res->ref_off = (int64_t *)malloc(N * 8);
+  res->alt_off = (int64_t *)malloc(N * 8);
+  res->ref_len = (int32_t *)malloc(N * 4);
+  res->alt_len = (int32_t *)malloc(N * 4);
+  res->log_odds = (double *)malloc(N * 8);
+  res->gq = (int32_t *)malloc(N * 4);
+  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
+  res->flags = (uint8_t *)malloc(N);
+  size_t pool_bytes = 0;
+  for (int64_t k = 0; k < nr; ++k) pool_bytes += (size_t)recs[(size_t)k].ref_len + recs[(size_t)k].alt_len;
+  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(pool_bytes, 1));
+  if (!res->contig || !res->pos || !res->sample || !res->ref_off || !res->alt_off || !res->ref_len || !res->alt_len ||
+      !res->log_odds || !res->gq || !res->tumor || !res->normal || !res->flags || !res->allele_pool)
+    return set_err(GQ_E_NOMEM, "somatic result arrays");
+  size_t at = 0;
+  for (int64_t k = 0; k < nr; ++k) {
+    const SomRec &r = recs[idx[(size_t)k]];
+    res->contig[k] = r.contig;
+    res->pos[k] = r.pos;
+    res->sample[k] = (uint8_t)((r.key >> 4) & 0xFFu);  // germline-standard: the sample slot (somatic: 0)
+    res->ref_len[k] = r.ref_len;
+    res->alt_len[k] = r.alt_len;
+    res->ref_off[k] = (int64_t)at;
+    res->alt_off[k] = (int64_t)at + r.ref_len;
+    const int tot = r.ref_len + r.alt_len;
+    if (tot <= 8)
+      for (int i = 0; i < tot; ++i) res->allele_pool[at + (size_t)i] = (uint8_t)(r.allele >> (8 * i));
+    else
+      memcpy(res->allele_pool + at, hpool.data() + r.allele, (size_t)tot);
+    at += (size_t)tot;
+    res->log_odds[k] = r.log_odds;
+    res->gq[k] = r.gq;
+    res->tumor[k] = r.tumor;
+    res->normal[k] = r.normal;
+    res->flags[k] = r.flags;
+  }
+  res->pool_len = (int64_t)at;
+  c->timings.marshal_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - m0).count();
+  return GQ_OK;
+}
+
 }  // namespace
 
 // A reference genome resident in HBM (ReferenceBroadcast.scala:39-55): the contigs of a read
@@ -1347,6 +1432,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096, deep_cap = 4096;
   Counters hc{};
+  float call_ms = 0, deep_ms = 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
@@ -1403,6 +1489,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipEventElapsedTime(&call_ms, c->ev[2], c->ev[3]);
+    deep_ms = 0;
     bool retry = false;
     if (hc.n_deep > deep_cap) {
       deep_cap = hc.n_deep + 1024;
@@ -1415,6 +1503,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       const int64_t nw = std::min<int64_t>(n_items, 4096);
       const size_t wb = deep_wave_bytes(scap, kMaxG);
       HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
+      HIP_TRY(hipEventRecord(c->ev[5], c->stream));
       const unsigned blocks = (unsigned)((nw + kSomWaves - 1) / kSomWaves);
       hipLaunchKernelGGL(somatic_call_k<true>, dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                          (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
@@ -1427,6 +1516,9 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
       HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[3]);
+      deep_ms += ms;
       return GQ_OK;
     };
     if (!retry && hc.n_deep > 0 && !hc.err) {
@@ -1483,51 +1575,11 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     free(res);
     return st;
   }
-  const int64_t nr = (int64_t)hc.n_rec;
-  std::vector<SomRec> recs((size_t)nr);
-  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
-  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
-  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  std::sort(recs.begin(), recs.end(), [](const SomRec &a, const SomRec &b) { return a.key < b.key; });
-  const size_t N = (size_t)std::max<int64_t>(nr, 1);
-  res->n = nr;
-  res->contig = (int32_t *)malloc(N * 4);
-  res->pos = (int64_t *)malloc(N * 8);
-  res->sample = (uint8_t *)calloc(N, 1);
-  res->ref_off = (int64_t *)malloc(N * 8);
-  res->alt_off = (int64_t *)malloc(N * 8);
-  res->ref_len = (int32_t *)malloc(N * 4);
-  res->alt_len = (int32_t *)malloc(N * 4);
-  res->log_odds = (double *)malloc(N * 8);
-  res->gq = (int32_t *)malloc(N * 4);
-  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->flags = (uint8_t *)malloc(N);
-  std::vector<uint8_t> apool;
-  for (int64_t k = 0; k < nr; ++k) {
-    const SomRec &r = recs[(size_t)k];
-    res->contig[k] = r.contig;
-    res->pos[k] = r.pos;
-    res->ref_len[k] = r.ref_len;
-    res->alt_len[k] = r.alt_len;
-    res->ref_off[k] = (int64_t)apool.size();
-    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
-    const int tot = r.ref_len + r.alt_len;
-    if (tot <= 8)
-      for (int i = 0; i < tot; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
-    else
-      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele, hpool.begin() + (ptrdiff_t)(r.allele + tot));
-    res->log_odds[k] = r.log_odds;
-    res->gq[k] = r.gq;
-    res->tumor[k] = r.tumor;
-    res->normal[k] = r.normal;
-    res->flags[k] = r.flags;
+  st = fetch_somatic_records(c, hc, pool_cap, res);
+  if (st) {
+    free(res);
+    return st;
   }
-  res->pool_len = (int64_t)apool.size();
-  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
-  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
   res->visited_loci = (int64_t)hc.visited;
   res->candidate_loci = (int64_t)hc.n_complex;
   float ms = 0;
@@ -1541,6 +1593,10 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   c->timings.total_ms = ms;
   c->timings.pileup_launches = 1;
   c->timings.tiles = pt.n_tiles;
+  c->timings.deep_loci = (int64_t)hc.n_deep;
+  c->timings.deep_max = (int64_t)hc.deep_max;
+  c->timings.call_ms = call_ms;
+  c->timings.deep_ms = deep_ms;
   c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
   *out = res;
   return GQ_OK;
@@ -1825,52 +1881,8 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
   st = check_device_error(c, hc);
   if (st) return fail(st);
-  const int64_t nr = (int64_t)hc.n_rec;
-  std::vector<SomRec> recs((size_t)nr);
-  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
-  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
-  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  std::sort(recs.begin(), recs.end(), [](const SomRec &a, const SomRec &b) { return a.key < b.key; });
-  const size_t N = (size_t)std::max<int64_t>(nr, 1);
-  res->n = nr;
-  res->contig = (int32_t *)malloc(N * 4);
-  res->pos = (int64_t *)malloc(N * 8);
-  res->sample = (uint8_t *)calloc(N, 1);
-  res->ref_off = (int64_t *)malloc(N * 8);
-  res->alt_off = (int64_t *)malloc(N * 8);
-  res->ref_len = (int32_t *)malloc(N * 4);
-  res->alt_len = (int32_t *)malloc(N * 4);
-  res->log_odds = (double *)malloc(N * 8);
-  res->gq = (int32_t *)malloc(N * 4);
-  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->flags = (uint8_t *)malloc(N);
-  std::vector<uint8_t> apool;
-  for (int64_t k = 0; k < nr; ++k) {
-    const SomRec &r = recs[(size_t)k];
-    res->contig[k] = r.contig;
-    res->pos[k] = r.pos;
-    res->sample[k] = (uint8_t)((r.key >> 4) & 0xFFu);
-    res->ref_len[k] = r.ref_len;
-    res->alt_len[k] = r.alt_len;
-    res->ref_off[k] = (int64_t)apool.size();
-    res->alt_off[k] = (int64_t)apool.size() + r.ref_len;
-    const int tot = r.ref_len + r.alt_len;
-    if (tot <= 8)
-      for (int i = 0; i < tot; ++i) apool.push_back((uint8_t)(r.allele >> (8 * i)));
-    else
-      apool.insert(apool.end(), hpool.begin() + (ptrdiff_t)r.allele, hpool.begin() + (ptrdiff_t)(r.allele + tot));
-    res->log_odds[k] = r.log_odds;
-    res->gq[k] = r.gq;
-    res->tumor[k] = r.tumor;
-    res->normal[k] = r.normal;
-    res->flags[k] = r.flags;
-  }
-  res->pool_len = (int64_t)apool.size();
-  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(apool.size(), 1));
-  if (!apool.empty()) memcpy(res->allele_pool, apool.data(), apool.size());
+  st = fetch_somatic_records(c, hc, pool_cap, res);
+  if (st) return fail(st);
   res->visited_loci = (int64_t)hc.visited;
   res->candidate_loci = (int64_t)hc.n_complex;
   float ms = 0;

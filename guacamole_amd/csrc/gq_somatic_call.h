@@ -454,13 +454,36 @@ __device__ __forceinline__ void evidence_pair(const Pile<NS> &PT, const Pile<NS>
     auto f_mq = [](uint32_t v) { return (int)(v & 0xFFu); };
     auto f_bq = [](uint32_t v) { return (int)(int8_t)((v >> 8) & 0xFFu); };
     auto f_mm = [](uint32_t v) { return (int)(v >> 16); };
-    if (ns & 1) {
-      const uint32_t k = (ns - 1) / 2;
+    const uint32_t k = (ns & 1) ? (ns - 1) / 2 : ns / 2 - 1;
+    if (ns <= 64) {
+      // one value per lane: bisection over [min, max] with ballots only (no memory in the
+      // rounds), and for an even count the next order statistic from one more count
+      const bool valid = (uint32_t)lane < ns;
+      const uint32_t v = valid ? m.tmp[base + lane] : 0u;
+      auto med = [&](int x, bool half_int, double *outd) {
+        int lo = wave_min_i32(valid ? x : INT32_MAX), hi = wave_max_i32(valid ? x : INT32_MIN);
+        while (lo < hi) {
+          const int mid = (int)(((int64_t)lo + (int64_t)hi) >> 1);
+          if ((uint32_t)__popcll(__ballot(valid && x <= mid)) > k) hi = mid;
+          else lo = mid + 1;
+        }
+        const int a = lo;
+        if (ns & 1) {
+          *outd = (double)a;
+          return;
+        }
+        const bool more = (uint32_t)__popcll(__ballot(valid && x <= a)) > k + 1;
+        const int b = more ? a : wave_min_i32(valid && x > a ? x : INT32_MAX);
+        *outd = half_int ? (double)((a + b) / 2) : ((double)a + (double)b) / 2.0;  // Int median (parity unpinned)
+      };
+      med(f_mq(v), false, &ev.median_mq);
+      med(f_bq(v), false, &ev.median_bq);
+      med(f_mm(v), true, &ev.median_mismatches);
+    } else if (ns & 1) {
       ev.median_mq = (double)kth_bisect(m.tmp, base, ns, k, 0, 255, f_mq);
       ev.median_bq = (double)kth_bisect(m.tmp, base, ns, k, -128, 127, f_bq);
       ev.median_mismatches = (double)kth_bisect(m.tmp, base, ns, k, 0, 65535, f_mm);
     } else {
-      const uint32_t k = ns / 2 - 1;
       ev.median_mq = ((double)kth_bisect(m.tmp, base, ns, k, 0, 255, f_mq) +
                       (double)kth_bisect(m.tmp, base, ns, k + 1, 0, 255, f_mq)) / 2.0;
       ev.median_bq = ((double)kth_bisect(m.tmp, base, ns, k, -128, 127, f_bq) +
@@ -632,6 +655,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     tick(0);
+    if (dbg & 1024) continue;  // ablation (diagnostics only): covers alone
     // ---- elements, both samples' chunks together: each covering read's scalars in one round,
     //      then (a single aligned block, the common read) its base, quality and MD event at
     //      pos; other reads take the general CIGAR walk (classify) and md_ref_at
@@ -709,6 +733,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       PS[s].refbase = amb_in ? amb_ref[2 * li + s] : fb >= 0 ? (uint8_t)fb : mk ? bit_base(mk) : (uint8_t)'N';
     }
     tick(1);
+    if (dbg & 2048) continue;  // ablation: covers + elements
     // ---- allele tables (the records now get their pileup reference base: SNV / DEL keys)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -821,6 +846,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       continue;
     }
     tick(2);
+    if (dbg & 4096) continue;  // ablation: up to the tables
     if (prm.filter_multi_allelic) {  // MultiAllelicPileupFilter (PileupFilter.scala:29-44)
       if (PT.nt > 2) PT.depth_f = 0;
       if (PN.nt > 2) PN.depth_f = 0;
@@ -842,6 +868,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     const int nT = PT.depth_f ? (int)nc[0] : 0, nN = PN.depth_f ? (int)nc[1] : 0;
     const GenoOut tg = genotypes_el(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
     tick(3);
+    if (dbg & 8192) continue;  // ablation: up to the tumor genotypes
     if (tg.G == 0) continue;
     const bool t_var = m.is_var[tg.bi] || m.is_var[tg.bj];
     if (!t_var) continue;

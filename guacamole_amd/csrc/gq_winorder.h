@@ -70,6 +70,9 @@ __global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t
         else a = m + 1;
       }
       x.cap = (int32_t)min<int64_t>(a - lo, INT32_MAX);
+      // a bound on the group's largest end until window_group sets it exactly: the prefix
+      // max of end over the reads starting at or before F
+      if (a > lo) x.E = R.pmax_end[a - 1];
     }
     wi[2 * w + s] = x;
     wi_lo[2 * w + s] = lo;
@@ -120,6 +123,26 @@ struct SomWin {
   const int64_t *init_reads;
   const int32_t *init_rank;
 };
+
+// Window bounds only (germline first pass): window_first over the plan's device copies of its
+// ranges (valid until the next plan() on the context), no host round trip.  SomWin without
+// init_reads: every WinInit has n = 0 (element order = read order) and E = an upper bound on
+// the initial group's ends, so a locus at or past E is known to have read-order elements.
+gq_status window_bounds(gq_ctx *c, const Plan &pl, const gq_dev_reads *t, SomWin &sw) {
+  const int64_t nw = (int64_t)pl.wins.size();
+  if (nw == 0 || !pl.d_rwin) {
+    sw = SomWin{};
+    return GQ_OK;
+  }
+  HIP_TRY(c->win_bound.ensure((size_t)nw * (2 * sizeof(WinInit) + 2 * sizeof(int64_t)) + 64));
+  WinInit *d_wi = (WinInit *)c->win_bound.p;
+  int64_t *d_lo = (int64_t *)(d_wi + 2 * nw);
+  hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                     pl.d_wcontig, pl.d_wroff, pl.d_rs, pl.d_re, nw, t->d, t->d, d_wi, d_lo);
+  HIP_TRY(hipGetLastError());
+  sw = SomWin{pl.d_rwin, d_wi, nullptr, nullptr};
+  return GQ_OK;
+}
 
 // The pileup element order of a plan's windows (SomWin): each window's first visited locus and
 // its initial (heap-ordered) group of reads, for the two read sets t and n.

@@ -94,11 +94,13 @@ class gq_timings(C.Structure):
     _fields_ = [("plan_ms", C.c_float), ("pileup_ms", C.c_float), ("complex_ms", C.c_float),
                 ("finalize_ms", C.c_float), ("total_ms", C.c_float), ("pileup_launches", C.c_int64),
                 ("tiles", C.c_int64), ("host_ms", C.c_float), ("marshal_ms", C.c_float),
-                ("walk_ms", C.c_float), ("walk_tiles", C.c_int64)]
+                ("walk_ms", C.c_float), ("walk_tiles", C.c_int64), ("order_loci", C.c_int64),
+                ("deep_loci", C.c_int64), ("deep_max", C.c_int64), ("call_ms", C.c_float), ("deep_ms", C.c_float)]
 
 
 class gq_reads_info(C.Structure):
-    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_pieces")]
+    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_pieces")] + [
+        ("h2d_ms", C.c_float), ("derive_ms", C.c_float)]
 
 
 class gq_somatic_params(C.Structure):
@@ -259,7 +261,7 @@ class Context:
         """Sizes of a resident read set and of its upload-time projection (gq_reads_get_info)."""
         info = gq_reads_info()
         _check(lib().gq_reads_get_info(reads.h, C.byref(info)))
-        return {k: int(getattr(info, k)) for k, _ in gq_reads_info._fields_}
+        return {k: (float if t is C.c_float else int)(getattr(info, k)) for k, t in gq_reads_info._fields_}
 
     def upload(self, arrs: Dict[str, object]) -> "DeviceReads":
         s, keep = make_gq_reads(arrs)

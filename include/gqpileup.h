@@ -169,6 +169,11 @@ typedef struct {
   float walk_ms;     /* germline: the walker kernel over the tiles the column kernel     */
                      /* handed over (pileup_ms is then the column kernel alone)          */
   int64_t walk_tiles;
+  int64_t order_loci;  /* germline: loci whose records depend on the restated Scala map order */
+  int64_t deep_loci;   /* somatic: candidates the deep caller took (pileup past the fast path) */
+  int64_t deep_max;    /* somatic: deepest per-sample pileup among them                     */
+  float call_ms;       /* somatic: the fast exact-caller kernel alone (inside complex_ms)    */
+  float deep_ms;       /* somatic: the deep caller launches (inside complex_ms)              */
 } gq_timings;
 
 const char *gq_version(void);
@@ -191,6 +196,8 @@ void gq_reads_free(gq_dev_reads *r);
 typedef struct gq_reads_info {
   int64_t n_reads, seq_bytes, proj_bytes, pev_count, proj_reads;  /* proj_reads: reads the projection takes */
   int64_t n_pieces;  /* germline_proj piece records (4 bytes each) */
+  float h2d_ms;      /* gq_reads_upload: host wall time of the copies (pinned staging, PCIe) */
+  float derive_ms;   /* gq_reads_upload / wrap: the upload-time derivation on the device    */
 } gq_reads_info;
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
