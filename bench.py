@@ -43,11 +43,13 @@ CHR1 = 249_250_621
 HBM_PEAK_GBS = 8000.0
 
 
-def rank_pieces(world: int, rank: int, wgs: bool):
-    """This rank's loci of the split genome: [(contig, contig_length, start, end)]."""
+def genome_parts(parts: int, wgs: bool, length: int = CHR20):
+    """The split genome: [(contig, contig_length, start, end, part)] in partition order, and the
+    genome's locus count.  The b37 genome (lexicographic contig order) cut to parts x length loci
+    (whole with wgs), split into `parts` contiguous parts by partitionLociUniformly."""
     from guacamole_amd.genomes import B37
     from guacamole_amd.loci import LociSet, partition_loci_uniformly
-    budget = None if wgs else world * CHR20
+    budget = None if wgs else parts * length
     lengths = {}
     ranges = []
     for name, ln in B37:  # already lexicographic
@@ -61,9 +63,25 @@ def rank_pieces(world: int, rank: int, wgs: bool):
         if budget == 0:
             break
     ls = LociSet.parse(",".join(ranges)).result(lengths)
-    parts = partition_loci_uniformly(world, ls)
-    mine = [(c, lengths[c], s, e) for c, s, e, t in parts.entries() if t == rank]
-    return mine, ls.count
+    split = partition_loci_uniformly(parts, ls)
+    return [(c, lengths[c], s, e, t) for c, s, e, t in split.entries()], ls.count
+
+
+def rank_pieces(world: int, rank: int, wgs: bool, length: int = CHR20):
+    """This rank's loci of the split genome: [(contig, contig_length, start, end)]."""
+    parts, count = genome_parts(world, wgs, length)
+    return [p[:4] for p in parts if p[4] == rank], count
+
+
+def merged_pieces(parts):
+    """One (contig, contig_length, start, end) per contig spanning all of its parts."""
+    out = []
+    for c, ln, s, e, _ in parts:
+        if out and out[-1][0] == c:
+            out[-1] = (c, ln, out[-1][2], e)
+        else:
+            out.append((c, ln, s, e))
+    return out
 
 
 def main() -> int:
@@ -78,6 +96,14 @@ def main() -> int:
     ap.add_argument("--cpu-window", type=int, default=2_000_000, help="loci in the CPU-oracle sample window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--somatic-length", type=int, default=CHR1, help="somatic sub-run loci (0: skip)")
+    ap.add_argument("--genome-ranks", type=int, default=0,
+                    help="split the genome into this many parts (default: the world size); with one "
+                         "process, one task per part (the N-rank job's task partition on one GPU)")
+    ap.add_argument("--shared-reads", action="store_true",
+                    help="generate the whole split genome's reads once (same seed on every rank) and give "
+                         "each rank the reads overlapping its loci (DistributedUtil.scala:584-597), so N ranks "
+                         "reproduce the 1-process records of the same task partition")
+    ap.add_argument("--calls-out", default=None, help="rank 0 writes the gathered records (rank order) as JSON")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
@@ -105,19 +131,30 @@ def main() -> int:
             gather_dev = "cpu"
 
     t0 = time.time()
-    if world == 1:
+    n_parts = args.genome_ranks or world
+    if world == 1 and n_parts == 1:
         g = synthetic.generate(args.length, args.depth, seed=synthetic.SEED + 2)
         loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([args.length - 1], np.int64),
                 np.array([0], np.int64))
         genome_loci = args.length - 1
         workload = "germline-threshold, synthetic 30x chr20-length shard per GPU (configs[1])"
     else:
-        pieces, genome_loci = rank_pieces(world, rank, args.wgs)
-        g = synthetic.generate_pieces(pieces, args.depth, seed=synthetic.SEED + 4 + 1000 * rank)
-        loci = (np.arange(len(pieces), dtype=np.int32), np.array([p[2] for p in pieces], np.int64),
-                np.array([p[3] for p in pieces], np.int64), np.zeros(len(pieces), np.int64))
-        workload = ("germline-threshold, synthetic 30x b37 genome (%s) split over %d GPUs (configs[3])"
-                    % ("whole" if args.wgs else "first %d loci" % genome_loci, world))
+        parts, genome_loci = genome_parts(n_parts, args.wgs, args.length)
+        # this process's parts: its rank's (one task), or every part (one task each) in one process
+        mine = [p for p in parts if world == 1 or p[4] == rank]
+        pieces = merged_pieces(mine)
+        if args.shared_reads:
+            every = merged_pieces(parts)
+            g = synthetic.subset_pieces(synthetic.generate_pieces(every, args.depth, seed=synthetic.SEED + 4),
+                                        every, pieces)
+        else:
+            g = synthetic.generate_pieces(pieces, args.depth, seed=synthetic.SEED + 4 + 1000 * rank)
+        names = [p[0] for p in pieces]
+        loci = (np.array([names.index(p[0]) for p in mine], np.int32), np.array([p[2] for p in mine], np.int64),
+                np.array([p[3] for p in mine], np.int64),
+                np.array([p[4] if world == 1 else 0 for p in mine], np.int64))
+        workload = ("germline-threshold, synthetic 30x b37 genome (%s) split into %d parts over %d GPUs (configs[3])"
+                    % ("whole" if args.wgs else "first %d loci" % genome_loci, n_parts, world))
     gen_s = time.time() - t0
     ctx = native.Context(local)
     t = time.perf_counter()
@@ -165,6 +202,8 @@ def main() -> int:
     else:
         loci_total = int(calls.visited_loci)
     visited = int(calls.visited_loci)
+    if args.calls_out:  # (before the next germline call on the context reuses the result image)
+        write_calls(args, calls, g, gather_dev, world, rank)
     # the same pass with the records copied to the host (PCIe-inclusive), a few steps, rank-local
     hc = ctx.germline_threshold(reads, loci, args.threshold)  # warm-up of the host-block path
     n_host = 5
@@ -244,7 +283,7 @@ def main() -> int:
         e2e["single_pass_s_est"] = e2e["ingest_s_est"] + (upload_ms + host_ms_step) / 1e3
         e2e["single_pass_loci_per_s_est"] = visited / e2e["single_pass_s_est"]
         line["end_to_end"] = e2e
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and n_parts == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], line["parity_window"] = cpu_baseline(g, ctx, reads, args)
     if dist is not None:
         dist.destroy_process_group()
@@ -254,6 +293,24 @@ def main() -> int:
     if rank == 0:
         print(json.dumps(line))
     return 0
+
+
+def write_calls(args, calls, g, gather_dev, world: int, rank: int):
+    """Rank 0 writes every rank's records (rank order = task order) as JSON rows."""
+    if world > 1:
+        from guacamole_amd.distributed import gather_germline
+        per_rank = gather_germline(calls, gather_dev)
+        if rank != 0:
+            return
+        parts, _ = genome_parts(args.genome_ranks or world, args.wgs, args.length)
+        rows = []
+        for r, c in enumerate(per_rank):
+            names = [p[0] for p in merged_pieces([p for p in parts if p[4] == r])]
+            rows += c.tuples(names)
+    else:
+        rows = calls.to_host().tuples(g.contig_names)
+    with open(args.calls_out, "w") as fh:
+        json.dump([list(x) for x in rows], fh)
 
 
 def ingest_rate(depth: float):

@@ -110,18 +110,26 @@ __device__ __forceinline__ int allele_cmp(const DevReads &R, const AlleleDesc &a
   return 0;
 }
 
+__device__ __forceinline__ int md_ref_at(const DevReads &R, int64_t r, int32_t pos);
+
 // Locate the PileupElement of read r at `pos` (PileupElement.apply + advanceToLocus) and
 // classify it (PileupElement.alignment).  Returns false and sets *errc on a reference error.
-__device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc) {
+// With mdv != nullptr the same CIGAR walk also yields md_ref_at(R, r, pos) in *mdv (always
+// set, also when classify fails).
+__device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t pos, uint8_t refbase, AlleleDesc &d, int *errc,
+                                         int *mdv = nullptr) {
   const int32_t s = R.start[r];
   const int64_t cig_off = R.cigar_off[r];
   const int32_t ncig = R.n_cigar[r];
   const int32_t slen = R.seq_len[r];  // loaded with the other scalars: the base load below
   const int64_t so = R.seq_off[r];    // then waits for the CIGAR walk only
+  const int32_t nmd = mdv ? R.n_md[r] : 0;
+  const int64_t mdo = mdv ? R.md_off[r] : 0;
   int ci = 0;
   int32_t ci_locus = s, within = 0, rp = 0;
   for (;;) {
     if (ci >= ncig) {
+      if (mdv) *mdv = -1;
       *errc = 1;
       return false;
     }
@@ -145,6 +153,18 @@ __device__ __forceinline__ bool classify(const DevReads &R, int64_t r, int32_t p
   const uint32_t c = R.cigar[cig_off + ci];
   const int op = (int)(c & 15u);
   const int32_t len = (int32_t)(c >> 4);
+  if (mdv) {  // md_ref_at's answer from this walk (rp is the read offset at pos in a read op)
+    if (op == OP_I) {
+      *mdv = md_ref_at(R, r, pos);  // (pos 0 behind a leading insertion)
+    } else if (nmd < 0) {
+      *mdv = -4;
+    } else {
+      const bool seq_elem = op != OP_D && op != OP_N && rp < slen;
+      const int b = seq_elem ? (int)R.seq[so + rp] : -1;
+      const int v = md_find(R.md_ev + mdo, nmd, pos - s);
+      *mdv = op == OP_D ? (v < 0 ? -3 : v) : op == OP_N ? (int)'N' : v >= 0 ? v : b;
+    }
+  }
   const bool fin = within == len - 1;
   const bool has_next = ci + 1 < ncig;
   const uint32_t cn = has_next ? R.cigar[cig_off + ci + 1] : 0u;

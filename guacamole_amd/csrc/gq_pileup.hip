@@ -774,13 +774,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       return r;
     };
     tick(0);
-    // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus)
+    // ---- pass 1: pileup reference base (Pileup.referenceBaseAtLocus).  When every covering
+    //      read fits one batch, the same CIGAR walk classifies the element too (pass 2 then
+    //      only sets its reference base): one latency chain instead of two
+    const bool fused = n_slots <= 64;  // uniform
+    AlleleDesc fd;
+    fd.rb = 0;
+    int ferr = 0, fsmp = 0;
+    bool fact = false, fok = false;
+    int64_t fr = tl.rb;
     uint32_t mask = 0;  // standard MD-derived bases present
     for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
       bool cv;
       const int64_t r = slot_read(k0 + lane, &cv);
       if (cv) {
-        const int v = md_ref_at(R, r, pos);
+        int v;
+        if (fused) {
+          fsmp = R.sample[r] & 7;
+          fok = classify(R, r, pos, 0, fd, &ferr, &v);
+          fact = true;
+          fr = r;
+        } else {
+          v = md_ref_at(R, r, pos);
+        }
         if (v < 0) {
           raise_error(&ctr->err, (int64_t *)&ctr->err_pos, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT,
                       pos);
@@ -824,23 +840,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     bool overflow = false;
     uint32_t st_lane = 0;  // lane s < 8: elements of sample s (read back with readlane: no scratch array)
     int64_t st_first = INT64_MAX;  // lane s < 8: the first element of sample s (element-order key)
-    const WinInit wio = sw.wi ? sw.wi[2 * sw.range_win[tl.range]] : WinInit{INT32_MAX, INT32_MIN, 0, 0, 0};
-    for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
-      bool act;
-      const int64_t r = slot_read(k0 + lane, &act);
-      AlleleDesc d;
-      Key128 key{0, 0};
-      int smp = act ? (R.sample[r] & 7) : 0;  // issued with classify's loads
-      if (act) {
-        int errc = 0;
-        if (!classify(R, r, pos, refbase, d, &errc)) {
-          raise_error(&ctr->err, (int64_t *)&ctr->err_pos, errc, pos);
-          act = false;
-          smp = 0;
-        } else {
-          key = allele_key(R, d, pos, smp);
-        }
-      }
+    // the window's initial group (element order): only the re-runs carry it
+    const WinInit wio = sw.init_reads ? sw.wi[2 * sw.range_win[tl.range]] : WinInit{INT32_MAX, INT32_MIN, 0, 0, 0};
+    // one batch of elements (up to 64, in read order) into the table and the per-sample totals
+    auto add_batch = [&](bool act, int64_t r, const AlleleDesc &d, int smp, const Key128 &key) {
       const int64_t okey = act ? element_order_key(R, r, pos, wio, sw.init_reads, sw.init_rank) : INT64_MAX;
       // slots run in read order, so with no initial-group read in the batch the first element
       // of a group is its lowest lane (no wave reduction)
@@ -908,6 +911,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
             }
         }
         pending &= ~mb;
+      }
+    };
+    if (fused) {
+      bool act = fact;
+      AlleleDesc d = fd;
+      d.rb = refbase;
+      int smp = act ? fsmp : 0;
+      Key128 key{0, 0};
+      if (act && !fok) {
+        raise_error(&ctr->err, (int64_t *)&ctr->err_pos, ferr, pos);
+        act = false;
+        smp = 0;
+      }
+      if (act) key = allele_key(R, d, pos, smp);
+      add_batch(act, fr, d, smp, key);
+    } else {
+      for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
+        bool act;
+        const int64_t r = slot_read(k0 + lane, &act);
+        AlleleDesc d;
+        Key128 key{0, 0};
+        int smp = act ? (R.sample[r] & 7) : 0;  // issued with classify's loads
+        if (act) {
+          int errc = 0;
+          if (!classify(R, r, pos, refbase, d, &errc)) {
+            raise_error(&ctr->err, (int64_t *)&ctr->err_pos, errc, pos);
+            act = false;
+            smp = 0;
+          } else {
+            key = allele_key(R, d, pos, smp);
+          }
+        }
+        add_batch(act, r, d, smp, key);
       }
     }
     if (overflow) {
@@ -1023,7 +1059,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     }
     // (sw without init_reads: window bounds only; past a window's initial group the elements
     //  are in read order, which the keys above already used)
-    if (__ballot(dep) != 0 && !amb_in && (sw.init_reads || !sw.wi || pos < wio.E)) {
+    // (a first pass has the window bounds only: past E the read order above is the element order)
+    if (__ballot(dep) != 0 && !amb_in && (sw.init_reads || !sw.wi || pos < sw.wi[2 * sw.range_win[tl.range]].E)) {
       // the order depends on first occurrences: listed (after the amb list's capacity) and
       // redone with the windows' element order (amb_ref == nullptr: the base is not ambiguous)
       if (lane == 0) {

@@ -21,12 +21,14 @@ struct WinInit {
 
 // F of each window over both read sets (the first locus of its ranges covered by a read of
 // either set), and each set's candidate reads for the group (prefix-max end past F, start at
-// or before F): their count is the group's capacity.  One thread per window.
+// or before F): their count is the group's capacity.  One wave per window: every search is a
+// 64-way wave_first_true (a few dependent loads over a whole contig, not ~24).
 __global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t *__restrict__ w_roff,
                              const int64_t *__restrict__ r_s, const int64_t *__restrict__ r_e, int64_t n_win,
                              DevReads RT, DevReads RN, WinInit *__restrict__ wi, int64_t *__restrict__ wi_lo) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= n_win) return;
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w >= n_win) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
   const int32_t c = w_contig[w];
   int64_t F = INT32_MAX;
   for (int s = 0; s < 2; ++s) {
@@ -35,12 +37,8 @@ __global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t
     for (int64_t k = w_roff[w]; k < w_roff[w + 1]; ++k) {
       const int64_t a = r_s[k];
       if (a >= F) break;
-      int64_t lo = cb, hi = ce;  // first read with pmax_end > a: it covers max(a, its start)
-      while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if ((int64_t)R.pmax_end[m] > a) hi = m;
-        else lo = m + 1;
-      }
+      // the first read with pmax_end > a covers max(a, its start)
+      const int64_t lo = wave_first_true(cb, ce, [&](int64_t m) { return (int64_t)R.pmax_end[m] > a; });
       if (lo < ce) {
         const int64_t f = max(a, (int64_t)R.start[lo]);
         if (f < r_e[k]) {
@@ -56,26 +54,17 @@ __global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t
     int64_t lo = 0;
     if (F < INT32_MAX) {
       const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
-      int64_t a = cb, b = ce;
-      while (a < b) {  // first read with pmax_end > F
-        const int64_t m = (a + b) >> 1;
-        if ((int64_t)R.pmax_end[m] > F) b = m;
-        else a = m + 1;
-      }
-      lo = a;
-      b = ce;
-      while (a < b) {  // first read with start > F
-        const int64_t m = (a + b) >> 1;
-        if ((int64_t)R.start[m] > F) b = m;
-        else a = m + 1;
-      }
+      lo = wave_first_true(cb, ce, [&](int64_t m) { return (int64_t)R.pmax_end[m] > F; });
+      const int64_t a = wave_first_true(lo, ce, [&](int64_t m) { return (int64_t)R.start[m] > F; });
       x.cap = (int32_t)min<int64_t>(a - lo, INT32_MAX);
       // a bound on the group's largest end until window_group sets it exactly: the prefix
       // max of end over the reads starting at or before F
       if (a > lo) x.E = R.pmax_end[a - 1];
     }
-    wi[2 * w + s] = x;
-    wi_lo[2 * w + s] = lo;
+    if (lane == 0) {
+      wi[2 * w + s] = x;
+      wi_lo[2 * w + s] = lo;
+    }
   }
 }
 
@@ -137,7 +126,7 @@ gq_status window_bounds(gq_ctx *c, const Plan &pl, const gq_dev_reads *t, SomWin
   HIP_TRY(c->win_bound.ensure((size_t)nw * (2 * sizeof(WinInit) + 2 * sizeof(int64_t)) + 64));
   WinInit *d_wi = (WinInit *)c->win_bound.p;
   int64_t *d_lo = (int64_t *)(d_wi + 2 * nw);
-  hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+  hipLaunchKernelGGL(window_first, dim3((unsigned)((nw * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                      pl.d_wcontig, pl.d_wroff, pl.d_rs, pl.d_re, nw, t->d, t->d, d_wi, d_lo);
   HIP_TRY(hipGetLastError());
   sw = SomWin{pl.d_rwin, d_wi, nullptr, nullptr};
@@ -169,7 +158,7 @@ gq_status build_somwin(gq_ctx *c, const Plan &pt, const gq_dev_reads *t, const g
     HIP_TRY(hipMemcpyAsync(b + o_rw, pt.rwin.data(), 4 * (size_t)nr, hipMemcpyHostToDevice, c->stream));
     WinInit *d_wi = (WinInit *)(b + o_wi);
     int64_t *d_lo = (int64_t *)(b + o_lo);
-    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+    hipLaunchKernelGGL(window_first, dim3((unsigned)((nw * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                        (const int32_t *)b, (const int64_t *)(b + o_roff), (const int64_t *)(b + o_rs),
                        (const int64_t *)(b + o_re), nw, t->d, n->d, d_wi, d_lo);
     HIP_TRY(hipGetLastError());

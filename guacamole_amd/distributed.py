@@ -114,25 +114,51 @@ def rank_share(rs, flat_loci, rank_of_range: np.ndarray, rank: int):
     return rs.subset(reads_overlapping(rs, loci[0], loci[1], loci[2])), loci
 
 
-def gather_images_to_rank0(calls, device: str):
-    """Every rank's germline result image (left in HBM by gq_germline_threshold_device) to rank 0:
-    sizes all-gathered, then one gather over RCCL / xGMI (device "cuda:k"), or through host
-    memory with gloo (device "cpu").  Returns rank 0's list of per-rank uint8 tensors (rank
-    order), None elsewhere."""
-    import ctypes as C
-
+def _gatherv_to_rank0(mine, sizes: List[int], device):
+    """Variable-size gather of one uint8 tensor per rank (``mine``: exactly ``sizes[rank]``
+    bytes, on ``device``) to rank 0, rank order.  Every rank's bytes travel once, at their own
+    size: rank 0 posts one receive per non-empty rank and the others one send, batched into a
+    single group (``batch_isend_irecv``: one RCCL group call, so the transfers run concurrently,
+    each over its own xGMI link into rank 0 — no ring, no padding to the largest rank)."""
     import torch
     import torch.distributed as dist
 
-    calls.check_current()
     world, rank = dist.get_world_size(), dist.get_rank()
+    if rank == 0:
+        parts = [mine] + [torch.empty(max(0, sizes[r]), dtype=torch.uint8, device=device) for r in range(1, world)]
+        ops = [dist.P2POp(dist.irecv, parts[r], r) for r in range(1, world) if sizes[r] > 0]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return parts
+    if sizes[rank] > 0:
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, mine, 0)]):
+            w.wait()
+    return None
+
+
+def _all_sizes(n: int, device) -> List[int]:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(n)], dtype=torch.int64, device=device)
+    out = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
+
+
+def gather_images_to_rank0(calls, device: str):
+    """Every rank's germline result image (left in HBM by gq_germline_threshold_device) to rank 0:
+    sizes all-gathered, then the images gathered at their own sizes (_gatherv_to_rank0) over
+    RCCL / xGMI (device "cuda:k"), or through host memory with gloo (device "cpu").  Returns
+    rank 0's list of per-rank uint8 tensors (rank order), None elsewhere."""
+    import ctypes as C
+
+    import torch
+
+    calls.check_current()
     dev = torch.device(device)
-    n = torch.tensor([int(calls.image_bytes)], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(x.item()) for x in sizes]
-    cap = max(1, max(sizes))
-    mine = torch.empty(cap, dtype=torch.uint8, device=dev)
+    sizes = _all_sizes(int(calls.image_bytes), dev)
+    mine = torch.empty(int(calls.image_bytes), dtype=torch.uint8, device=dev)
     if calls.image_bytes:
         on_gpu = dev.type == "cuda"
         if on_gpu:
@@ -144,12 +170,7 @@ def gather_images_to_rank0(calls, device: str):
                            3 if on_gpu else 2)
         if rc != 0:
             raise RuntimeError("hipMemcpy of the result image failed (%d)" % rc)
-    if rank == 0:
-        parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
-        dist.gather(mine, gather_list=parts, dst=0)
-        return [parts[r][:sizes[r]] for r in range(world)]
-    dist.gather(mine, dst=0)
-    return None
+    return _gatherv_to_rank0(mine, sizes, dev)
 
 
 def gather_germline(calls, device: str):
@@ -175,7 +196,7 @@ def gather_germline(calls, device: str):
 
 
 def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[List[np.ndarray]]:
-    """Variable-size gather of one uint8 buffer per rank to rank 0.
+    """Variable-size gather of one uint8 buffer per rank to rank 0 (_gatherv_to_rank0).
 
     device: torch device for the collective ("cuda:k" => RCCL over xGMI; None => CPU/gloo)."""
     import torch
@@ -183,22 +204,11 @@ def gather_to_rank0(buf: np.ndarray, device: Optional[str] = None) -> Optional[L
 
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return [buf]
-    world, rank = dist.get_world_size(), dist.get_rank()
     dev = torch.device(device) if device else torch.device("cpu")
-    n = torch.tensor([int(buf.size)], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
-    cap = max(1, max(sizes))
-    mine = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    if buf.size:
-        mine[:buf.size] = torch.from_numpy(buf).to(dev)
-    if rank == 0:
-        parts = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
-        dist.gather(mine, gather_list=parts, dst=0)
-        return [parts[r][:sizes[r]].cpu().numpy() for r in range(world)]
-    dist.gather(mine, dst=0)
-    return None
+    sizes = _all_sizes(int(buf.size), dev)
+    mine = torch.from_numpy(np.ascontiguousarray(buf, np.uint8)).to(dev)
+    parts = _gatherv_to_rank0(mine, sizes, dev)
+    return None if parts is None else [p.cpu().numpy() for p in parts]
 
 
 def gather_somatic(calls, device: Optional[str]):

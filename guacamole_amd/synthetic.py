@@ -218,6 +218,55 @@ def generate_pieces(pieces, depth: float, seed: int = SEED, L: int = 150) -> Syn
     return SyntheticReads(names, lengths, out, np.zeros(0, np.uint8), stats, None)
 
 
+def _gather_pool(pool: np.ndarray, off: np.ndarray, ln: np.ndarray):
+    """(new pool, new offsets): the slices pool[off[i] : off[i] + ln[i]] packed in order."""
+    ln = np.asarray(ln, np.int64)
+    new_off = np.zeros(len(ln), np.int64)
+    if len(ln) > 1:
+        np.cumsum(ln[:-1], out=new_off[1:])
+    tot = int(ln.sum())
+    if tot == 0:
+        return pool[:0].copy(), new_off
+    src = np.repeat(np.asarray(off, np.int64) - new_off, ln) + np.arange(tot, dtype=np.int64)
+    return pool[src], new_off
+
+
+def subset_pieces(g: "SyntheticReads", pieces, mine) -> "SyntheticReads":
+    """The reads of `g` (generate_pieces over `pieces`) overlapping the ranges `mine` (a sub-list
+    of (contig, contig_length, start, end), one per contig, in `pieces`' contig order): what a
+    task over those loci receives (DistributedUtil.scala:584-597), with local contig ids in
+    `mine`'s order.  Reads straddling a cut are in both sides' subsets."""
+    a = g.arrays
+    crb = np.asarray(a["contig_read_begin"], np.int64)
+    names = [p[0] for p in pieces]
+    sel, begin = [], [0]
+    for contig, clen, s0, e0 in mine:
+        k = names.index(contig)
+        idx = np.arange(crb[k], crb[k + 1])
+        keep = idx[(a["start"][idx] < e0) & (a["end"][idx] > s0)]
+        sel.append(keep)
+        begin.append(begin[-1] + len(keep))
+    idx = np.concatenate(sel) if sel else np.zeros(0, np.int64)
+    out: Dict[str, np.ndarray] = {}
+    for k in ("start", "end", "mapq", "flags", "sample", "seq_len", "n_cigar", "n_md", "n_mismatch"):
+        out[k] = np.ascontiguousarray(a[k][idx])
+    # prefix max of end within each contig block (SoA invariant)
+    pm = out["end"].copy()
+    for b0, b1 in zip(begin[:-1], begin[1:]):
+        if b1 > b0:
+            pm[b0:b1] = np.maximum.accumulate(pm[b0:b1])
+    out["pmax_end"] = pm
+    out["seq"], out["seq_off"] = _gather_pool(a["seq"], a["seq_off"][idx], a["seq_len"][idx])
+    out["qual"], _ = _gather_pool(a["qual"], a["seq_off"][idx], a["seq_len"][idx])
+    out["cigar"], out["cigar_off"] = _gather_pool(a["cigar"], a["cigar_off"][idx], a["n_cigar"][idx])
+    out["md_ev"], out["md_off"] = _gather_pool(a["md_ev"], a["md_off"][idx], a["n_md"][idx])
+    out["contig_read_begin"] = np.array(begin, np.int64)
+    out["n_contigs"] = np.int64(len(mine))
+    out["n_samples"] = np.int64(1)
+    return SyntheticReads([m[0] for m in mine], [int(m[1]) for m in mine], out, np.zeros(0, np.uint8),
+                          dict(g.stats), None)
+
+
 def generate(length: int, depth: float, seed: int = SEED, L: int = 150, contig: str = "20",
              het: float = 1e-3, hom: float = 5e-4, indel_rate: float = 1e-4, somatic_rate: float = 0.0,
              tumor: bool = False, read_seed: Optional[int] = None) -> SyntheticReads:

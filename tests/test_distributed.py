@@ -116,3 +116,35 @@ def test_gather_somatic_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == [_somatic_calls(3, 0).rows, _somatic_calls(7, 1).rows]
+
+
+def _gatherv_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from guacamole_amd.distributed import gather_to_rank0
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = [5, 0, 17][rank]  # an empty rank sends nothing
+    out = gather_to_rank0(np.arange(n, dtype=np.uint8) + rank, None)
+    if rank == 0:
+        q.put([o.tolist() for o in out])
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gatherv_gloo_world3_exact_sizes():
+    """Sizes all-gathered, then one grouped send/recv per non-empty rank (no padding)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gatherv_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [list(range(5)), [], [2 + i for i in range(17)]]

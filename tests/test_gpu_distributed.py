@@ -49,3 +49,30 @@ def test_somatic_two_ranks_equal_one(tmp_path):
     one = _run(args, 1, str(tmp_path / "one.json"))
     two = _run(args, 2, str(tmp_path / "two.json"))
     assert one == two and one.count("\n") > 10
+
+
+def _bench(world, out, extra):
+    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    args = ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "0", "--somatic-length", "0",
+            "--no-cpu-baseline", "--shared-reads", "--calls-out", out] + extra
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    with open(out) as fh:
+        return fh.read(), r.stdout
+
+
+def test_bench_two_ranks_equal_one(tmp_path):
+    """bench.py's N = 2 flow (weak scaling: 2 x L loci of b37 split by partitionLociUniformly, each
+    rank holding the reads overlapping its part, records gathered to rank 0 by sizes + grouped
+    send/recv) against one process over the same 2 x L loci with the same two tasks
+    (DistributedUtil.scala:584-597, 621-633): identical records."""
+    L = "3000000"
+    two, out2 = _bench(2, str(tmp_path / "two.json"), ["--length", L])
+    one, _ = _bench(1, str(tmp_path / "one.json"), ["--length", L, "--genome-ranks", "2"])
+    assert one == two and one.count("], [") > 100
+    assert '"n_gpus": 2' in out2
