@@ -26,6 +26,7 @@ Also reported:
                 GPU's on that window (parity_window)
   somatic       somatic-standard on tumor/normal 60x/30x at chr1 length (configs[2]), rank 0,
                 N = 1 only (--somatic-length 0 skips it)
+  configs4      somatic-standard on a 500x/500x panel (configs[4], 1 GPU; --panel-length 0 skips it)
 """
 import argparse
 import json
@@ -96,6 +97,8 @@ def main() -> int:
     ap.add_argument("--cpu-window", type=int, default=2_000_000, help="loci in the CPU-oracle sample window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--somatic-length", type=int, default=CHR1, help="somatic sub-run loci (0: skip)")
+    ap.add_argument("--panel-length", type=int, default=1_000_000,
+                    help="configs[4] sub-run: 500x/500x panel loci (0: skip)")
     ap.add_argument("--genome-ranks", type=int, default=0,
                     help="split the genome into this many parts (default: the world size); with one "
                          "process, one task per part (the N-rank job's task partition on one GPU)")
@@ -228,7 +231,7 @@ def main() -> int:
     bytes_md = 4 * int(a["md_ev"].shape[0])
     bytes_out = 32 * len(calls) + 12 * int(calls.complex_loci)
     b_all = bytes_seq + bytes_meta + bytes_cigar + bytes_md + bytes_out
-    read_bytes = int(st["proj_bytes"]) + 4 * int(st["n_pieces"]) + 8 * int(st["pev_count"])
+    read_bytes = int(st["proj_bytes"]) + 8 * int(st["pev_count"])
     kept = 1.0 - float(np.mean(walk_frac))
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))
@@ -290,6 +293,10 @@ def main() -> int:
     del reads, g
     if rank == 0 and world == 1 and args.somatic_length > 0:
         line["somatic"] = somatic_run(ctx, args)
+    if rank == 0 and world == 1 and args.panel_length > 0:
+        line["configs4"] = somatic_run(ctx, args, steps=5, warmup=2, L=args.panel_length, tdepth=500.0, ndepth=500.0,
+                                       rate=1e-3, workload="%d-locus targeted panel (configs[4], 1 GPU)"
+                                       % args.panel_length)
     if rank == 0:
         print(json.dumps(line))
     return 0
@@ -385,19 +392,21 @@ def cpu_baseline(g, ctx, reads, args):
             {"loci": [w0, w1], "calls": len(want), "identical": bool(parity)})
 
 
-def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
+def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: float = 60.0, ndepth: float = 30.0,
+                rate: float = 2e-4, workload: str = "chr1-length contig (configs[2])"):
     """somatic-standard on synthetic tumor 60x / normal 30x over one chr1-length contig
-    (configs[2]), reads resident in HBM; a step = one gq_somatic_standard call (CLI defaults,
-    driver filters on).  Roofline of the candidate kernel somatic_proj from its algorithmic bytes:
-    tumor bases + qualities, 16 B per tumor read, 4 B per tumor CIGAR op and MD event, 8 B per
-    normal read (the normal's depth needs its reads' intervals only); the bytes it reads
-    (projection, 16-bit margin terms, records, sparse entries, normal intervals) beside it."""
+    (configs[2]; the panel sub-run: 500x / 500x over a short contig, configs[4]), reads resident
+    in HBM; a step = one gq_somatic_standard call (CLI defaults, driver filters on).  Roofline of
+    the candidate kernel somatic_proj from its algorithmic bytes: tumor bases + qualities, 16 B
+    per tumor read, 4 B per tumor CIGAR op and MD event, 8 B per normal read (the normal's depth
+    needs its reads' intervals only); the bytes it reads (projection rows, 16-bit margin terms,
+    sparse entries, normal intervals) beside it."""
     from guacamole_amd import synthetic
-    L = args.somatic_length
+    L = L or args.somatic_length
     t0 = time.time()
     seed = synthetic.SEED + 3
-    tg = synthetic.generate(L, 60.0, seed=seed, somatic_rate=2e-4, tumor=True, read_seed=11)
-    ng = synthetic.generate(L, 30.0, seed=seed, somatic_rate=2e-4, tumor=False, read_seed=12)
+    tg = synthetic.generate(L, tdepth, seed=seed, somatic_rate=rate, tumor=True, read_seed=11)
+    ng = synthetic.generate(L, ndepth, seed=seed, somatic_rate=rate, tumor=False, read_seed=12)
     gen_s = time.time() - t0
     t = ctx.upload(tg.arrays)
     n = ctx.upload(ng.arrays)
@@ -418,14 +427,17 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1):
     b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
              + 8 * ng.n)
     st = ctx.proj_stats(t)
-    read_bytes = 3 * int(st["proj_bytes"]) + 12 * tg.n + 8 * int(st["pev_count"]) + 8 * ng.n
+    read_bytes = 3 * int(st["proj_bytes"]) + 8 * int(st["pev_count"]) + 8 * ng.n
     k_ms = float(np.mean(stages["pileup_ms"]))
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)
-    return {"metric": "somatic-standard loci/sec, tumor 60x / normal 30x", "value": visited * steps / el,
-            "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": warmup,
-            "config": {"workload": "somatic-standard, synthetic tumor/normal 60x/30x, chr1-length contig (configs[2])",
-                       "loci": L - 1, "visited_loci": visited, "tumor_reads": tg.n, "normal_reads": ng.n},
+    return {"metric": "somatic-standard loci/sec, tumor %gx / normal %gx" % (tdepth, ndepth),
+            "value": visited * steps / el, "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
+            "warmup": warmup,
+            "config": {"workload": "somatic-standard, synthetic tumor/normal %gx/%gx, %s" % (tdepth, ndepth, workload),
+                       "loci": L - 1, "visited_loci": visited, "tumor_reads": tg.n, "normal_reads": ng.n,
+                       "somatic_rate": rate},
+            "walker_tiles_frac": float(tm["walk_tiles"]) / max(1, int(tm["tiles"])),
             "device_stages_ms": {k: float(np.mean(v)) for k, v in stages.items() if k not in ("host_ms", "marshal_ms")},
             # the step's wall time beyond the device span: the C-ABI call's own host time (launch
             # gaps at its capacity checks, the results' D2H, sort and marshalling) and the ctypes

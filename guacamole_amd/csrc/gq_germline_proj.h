@@ -4,27 +4,24 @@
 //
 // One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
 // (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
-// block B0.  Lanes 16g .. 16g + 15 (group g) own the 128-locus slice [B0 + 128g, B0 + 128g +
-// 128), whose projection words are one contiguous run in the slice-major pool (ProjRec), and
-// walk the slice's pieces (the reads with words there, in read order; PieceRec), one piece per
-// group per step:
+// block B0, and the block's projection rows (ProjRec: 64 words each, word l = column l, the
+// reads packed into rows by interval partitioning) are read one row per load, 512 contiguous
+// bytes per wave, with no per-row address arithmetic:
 //
-//     rec = piece k's record (16 per stage, one per lane, shared in the group by ds_bpermute)
-//     d   = l16 - s0(rec)
-//     w   = buffer_load_b64(block's words, d < len(rec) ? 8 (base(rec) + d) : out of range -> 0)
+//     w    = buffer_load_b64(row k of the block, lane l)          (rows past the block's: 0)
 //     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
 //     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
 //
 // (the projection holds base codes A 1, C 3, T 4, G 7 and 0 where the read has no
 // Match/Mismatch element, so neither the read's ends nor its deletions need a mask).  Counts
-// are SWAR nibbles folded into byte counters every 15 reads, in registers.  The sparse rest —
+// are SWAR nibbles folded into byte counters every 15 rows, in registers.  The sparse rest —
 // MD mismatch events (PileupElement.scala:108-118, Pileup.scala:157-165: the MD-derived
 // reference base), N bases, complex ranges (insertion / deletion anchors, mid-deletions,
 // N-skips) — comes from the tile's pev entries, one lane per entry, into two LDS words per
 // locus.  Then each lane makes the GermlineThreshold decision (GermlineThresholdCaller.scala:
 // 90-179) for its eight loci; variant candidates, Ref/NoCall records and complex items leave
 // as in germline_decide.  Blocks a read the projection cannot take overlaps (pbad), or with
-// more than 255 pieces in one slice, go to germline_walk.
+// more than 255 rows (byte counters), go to germline_walk.
 #pragma once
 
 #include "gq_kernels.h"
@@ -44,8 +41,8 @@ struct ProjCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = GQ_PROJ_WAVES;  // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kU = 4;  // pieces per group per batch (all loads issued before use); 4 batches per stage
-  static constexpr int kMaxRows = 255;  // pieces per slice (byte counters); deeper blocks: walker
+  static constexpr int kU = 4;  // rows per batch (all loads issued before use); 3 batches in flight
+  static constexpr int kMaxRows = kSliceRowsMax;  // rows per block (16-bit counts past 240 rows)
   static constexpr int kEnt = GQ_PROJ_ENT;  // sparse entries per lane loaded with the records (the rest: a loop)
 };
 
@@ -60,8 +57,7 @@ __device__ __forceinline__ unsigned wave_reserve_lds_n(unsigned *ctr, unsigned n
 }
 
 __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_PROJ_WPE))) void germline_proj(
-    const Tile *__restrict__ tiles, const TileX *__restrict__ tilex, int64_t n_tiles, const uint32_t *__restrict__ pcs,
-    const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev, int n_samples, int threshold, int emit_ref,
+    const Tile *__restrict__ tiles, const TileX *__restrict__ tilex, int64_t n_tiles, const uint8_t *__restrict__ proj, const uint2 *__restrict__ pev, int n_samples, int threshold, int emit_ref,
     int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
@@ -69,15 +65,17 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // 2 skip the sparse entries, 4 skip the decision
   using C = ProjCfg;
   constexpr int T = C::kT, U = C::kU;
-  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // event read bases: A C T G bytes
-  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
+  // per locus: event read bases (2 words: A | C << 16, T | G << 16); MD bits 0-3 | N << 4 |
+  // complex diff << 16
+  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
+  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave];
   {
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-    e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -108,25 +106,23 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const uint32_t rec = next_rec;
     if (i + C::kWaves < i1) next_rec = fetch(i + C::kWaves);
-    // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8; TileX from dw 16: sb0, sb4,
-    // e0, e1, pb0 (16-25), pbd[4] (26-29), pbad4 (30)
+    // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8; TileX from dw 16: row0 16-17,
+    // nrows 18, pbad4 19, e0 20-21, e1 22-23
     const int32_t L0 = (int32_t)f32(rec, 7), L1 = (int32_t)f32(rec, 8);
     const int64_t rb = f64(rec, 2), re = f64(rec, 4);
     const int32_t B0 = L0 & ~(T - 1);
     if (re <= rb) continue;  // no reads: nothing visited
-    // ---- the block's slices (one per group): their piece ranges and pbad flags (from the
-    //      record), the first kEnt sparse entries per lane of the window's reads and the first
-    //      three 16-piece stages of each group's piece records, loaded together.  A pbad slice
-    //      (a read the projection cannot take) or more than kMaxRows pieces in a slice: the walker.
-    const int64_t sb0 = f64(rec, 16), sb4 = f64(rec, 18);
-    const int32_t pd0 = (int32_t)f32(rec, 26), pd1 = (int32_t)f32(rec, 27), pd2 = (int32_t)f32(rec, 28),
-                  pd3 = (int32_t)f32(rec, 29);
-    const int32_t plo = g == 0 ? 0 : g == 1 ? pd0 : g == 2 ? pd1 : pd2;
-    const int32_t phi = g == 0 ? pd0 : g == 1 ? pd1 : g == 2 ? pd2 : pd3;
-    const int64_t pbg = f64(rec, 24) + plo;
-    const int32_t ng = phi - plo;
-    const uint32_t badg = (f32(rec, 30) >> (8 * g)) & 0xFFu;
+    // ---- the block's rows and pbad flags (from the record), the first kEnt sparse entries per
+    //      lane of the window's reads and the first rows, loaded together.  A pbad slice (a read
+    //      the projection cannot take) or more than kMaxRows rows: the walker.
+    const int64_t row0 = f64(rec, 16);
+    const int32_t nrows = (int32_t)f32(rec, 18);
+    const uint32_t bad4 = f32(rec, 19);
     const int64_t e0 = f64(rec, 20), e1 = f64(rec, 22);
+    if (bad4 != 0 || nrows > C::kMaxRows) {
+      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
+      continue;
+    }
     constexpr int NE = C::kEnt;
     uint2 ent[NE];
 #pragma unroll
@@ -135,25 +131,16 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       ent[j] = make_uint2(0x80000000u, kPevNone);
       if (!(dbg & 2) && k < e1) ent[j] = pev[k];
     }
-    const int32_t l16 = lane & 15;
-    auto stage = [&](int32_t k) -> uint32_t {  // piece record of row k + l16 of this group
-      return k + l16 < ng ? pcs[pbg + k + l16] : kPieceNone;
-    };
-    uint32_t P0 = stage(0), P1 = stage(16), P2 = stage(32);
-    const int32_t nmax = max(max(pd0, pd1 - pd0), max(pd2 - pd1, pd3 - pd2));
-    if (__ballot(badg != 0) != 0 || nmax > C::kMaxRows) {
-      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
-      continue;
-    }
     const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]).
-    //      Row k of group g is piece k of its slice: record from the 16-piece stage in a
-    //      register (ds_bpermute within the group), word (rec >> 9) + l16 - s0 when this
-    //      lane's column is inside the piece, else an out-of-range offset (the load returns
-    //      0).  Three batches of loads stay in flight while a fourth is counted.
+    // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]),
+    //      widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 rows and at the end.
+    //      Row k: one 512-byte load at lane offset 8 lane + 512 k (rows past the block's fall
+    //      out of the buffer's range and read 0; dbg & 1, diagnostics: every load).  Three
+    //      batches of loads stay in flight while a fourth is counted.
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
+    uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(proj + 8 * sb0), (short)0, (int)(8 * (sb4 - sb0)), 0x00020000);
+        (void *)(proj + 512 * row0), (short)0, (dbg & 1) ? 0 : 512 * nrows, 0x00020000);
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -167,20 +154,26 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       }
       nn = 0;
     };
-    const int32_t bp = (lane & 48) << 2;  // ds_bpermute address of the group's lane 0
-    // lane offset B + l16 - 16 (dbg & 1, diagnostics: every load out of range)
-    const uint32_t lm16 = (dbg & 1) ? 0x10000000u : (uint32_t)l16 - 16u, ibit = 16u + (uint32_t)l16;
-    auto issue = [&](uint32_t P, int u0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
-      uint32_t rv[U];
+    auto widen = [&]() {
+      auto w2 = [](uint32_t (&w)[4], uint32_t (&c)[2]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) rv[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(bp + 4 * (u0 + u), (int)P);
+        for (int h = 0; h < 2; ++h) {
+          w[2 * h] += __builtin_amdgcn_perm(0u, c[h], 0x0c010c00u);  // bytes 0, 1 -> halves
+          w[2 * h + 1] += __builtin_amdgcn_perm(0u, c[h], 0x0c030c02u);
+          c[h] = 0;
+        }
+      };
+      w2(wA, ca);
+      w2(wC, cc);
+      w2(wT, ct);
+      w2(wG, cg);
+    };
+    const uint32_t vl = 8u * (uint32_t)lane;
+    auto issue = [&](int32_t k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {  // rows k0 .. k0 + U - 1
+      const uint32_t vb = vl + 512u * (uint32_t)k0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t rr = rv[u];
-        // (B + l16 - 16) * 8 | (lane invalid) << 31 (PieceRec)
-        const uint32_t inv = (rr >> ibit) & 1u;
-        const uint32_t voff = (((rr & 0xFFFFu) + lm16) << 3) | (inv << 31);
-        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(vb + 512u * u), 0, 0);
         w0[u] = w[0];
         w1[u] = w[1];
       }
@@ -197,9 +190,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       nn += U;
     };
     uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U], d0[U], d1[U];
-    issue(P0, 0, a0, a1);
-    issue(P0, U, b0, b1);
-    issue(P0, 2 * U, c0, c1);
+    issue(0, a0, a1);
+    issue(U, b0, b1);
+    issue(2 * U, c0, c1);
     // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
     auto apply = [&](uint2 p) {
       const int32_t l = (int32_t)p.x;
@@ -213,8 +206,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
         if (m) atomicOr(&mk[l - B0], m);
-        if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
-        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
+        if (c < 4) atomicAdd(&ev[2 * (l - B0) + (c >> 1)], 1u << (16 * (c & 1)));
+        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
       }
     };
     const uint64_t t_c = (dbg & 16) ? __builtin_readcyclecounter() : 0;
@@ -226,32 +219,50 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         if (k < e1) apply(pev[k]);
       }
     const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    static_assert(4 * U == 16, "a loop iteration is one 16-piece stage");
-    for (int32_t k0 = 0;; k0 += 16) {  // P0: rows k0 .. k0 + 15, P1: the next 16, P2: the 16 after
-      issue(P0, 3 * U, d0, d1);
-      const bool more = k0 + 16 < nmax;  // wave-uniform
-      count(a0, a1);  // past the last stage P1 is all kPieceNone: the loads fall out of range
-      issue(P1, 0, a0, a1);
+    // rows k0 .. k0 + 4U - 1 per iteration, three batches in flight; one exit (the rows past
+    // the block's read 0 and count nothing)
+    for (int32_t k0 = 0, since = 0;; k0 += 4 * U) {
+      issue(k0 + 3 * U, d0, d1);
+      count(a0, a1);
+      issue(k0 + 4 * U, a0, a1);
       count(b0, b1);
-      issue(P1, U, b0, b1);
+      issue(k0 + 5 * U, b0, b1);
       count(c0, c1);
-      issue(P1, 2 * U, c0, c1);
+      issue(k0 + 6 * U, c0, c1);
       count(d0, d1);
-      if (!more) break;
-      P0 = P1;
-      P1 = P2;
-      P2 = stage(k0 + 48);
+      if (k0 + 4 * U >= nrows) break;
+      since += 4 * U;
+      if (since == 240) {  // uniform: bytes hold 240 rows at most
+        fold();
+        widen();
+        since = 0;
+      }
     }
     fold();
+    widen();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     uint32_t kinds = 0, nrec = 0, ncpx = 0;
+    // locus j's 16-bit count of base w (a dynamic j selects among four registers)
+    auto cnt16 = [](const uint32_t (&w)[4], int j) {
+      const int q = j >> 1;
+      const uint32_t x = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+      return (x >> (16 * (j & 1))) & 0xFFFFu;
+    };
+    // the reference-base mask of a locus: MD bits, plus each base with more Match/Mismatch
+    // elements than events (an element without an event reads the reference)
+    auto ref_mask = [](uint32_t mw, uint32_t eac, uint32_t etg, uint32_t cA, uint32_t cC, uint32_t cT, uint32_t cG) {
+      return (mw & 15u) | (cA > (eac & 0xFFFFu) ? 1u : 0u) | (cC > (eac >> 16) ? 2u : 0u) |
+             (cT > (etg & 0xFFFFu) ? 4u : 0u) | (cG > (etg >> 16) ? 8u : 0u);
+    };
     if (!(dbg & 4)) {
-      uint32_t e8[8], m8[8];
+      uint32_t e16[16], m8[8];
       {
-        const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1];
-        e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
+        const uint4 ea = e4[0], eb = e4[1], ec = e4[2], ed = e4[3], ma = m4[0], mb = m4[1];
+        e16[0] = ea.x, e16[1] = ea.y, e16[2] = ea.z, e16[3] = ea.w, e16[4] = eb.x, e16[5] = eb.y, e16[6] = eb.z;
+        e16[7] = eb.w, e16[8] = ec.x, e16[9] = ec.y, e16[10] = ec.z, e16[11] = ec.w, e16[12] = ed.x, e16[13] = ed.y;
+        e16[14] = ed.z, e16[15] = ed.w;
         m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
       }
       // complex elements per locus: prefix of the range differences over the block
@@ -265,16 +276,12 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       for (int j = 0; j < 8; ++j) {
         const int32_t l = B0 + 8 * lane + j;
         const bool in = l >= L0 && l < L1;
-        const int h = j >> 2, sh = 8 * (j & 3);
-        const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
-        const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
-        const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+        const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
+        const uint32_t nN = (m8[j] >> 4) & 0xFFFu;
         ncx_run += (int32_t)m8[j] >> 16;
         const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
         const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-        const uint32_t ew = e8[j];
-        const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
-                              (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+        const uint32_t mask = ref_mask(m8[j], e16[2 * j], e16[2 * j + 1], cA, cC, cT, cG);
         // branch-free (0/1 integers): the common hom-ref locus writes nothing
         const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
         const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
@@ -315,14 +322,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
           ++kc;
           continue;
         }
-        const int sh = 8 * (j & 3);
-        const bool hi = j >= 4;
-        const uint32_t cA = ((hi ? ca[1] : ca[0]) >> sh) & 0xFFu, cC = ((hi ? cc[1] : cc[0]) >> sh) & 0xFFu;
-        const uint32_t cT = ((hi ? ct[1] : ct[0]) >> sh) & 0xFFu, cG = ((hi ? cg[1] : cg[0]) >> sh) & 0xFFu;
-        const uint32_t mw = mk[8 * lane + j], ew = ev[8 * lane + j];
-        const uint32_t nN = (mw >> 8) & 0xFFu;
-        const uint32_t mask = (mw & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
-                              (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+        const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
+        const uint32_t mw = mk[8 * lane + j];
+        const uint32_t nN = (mw >> 4) & 0xFFFu;
+        const uint32_t mask = ref_mask(mw, ev[16 * lane + 2 * j], ev[16 * lane + 2 * j + 1], cA, cC, cT, cG);
         const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
         const uint64_t ord = (uint64_t)(f64(rec, 0) + (pos - L0));
         CallRec rr;
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         }
       }
     }
-    e4[0] = e4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
+    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
     if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup, first loads, entries, counting, decision
       const uint64_t t_f = __builtin_readcyclecounter();
       clk[0] += t_b - t_a;

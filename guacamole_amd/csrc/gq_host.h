@@ -212,13 +212,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// One wave over the words of projection slice `slot` (the slice-major pool, ProjRec in
-// gq_kernels.h): its reads are those of the slice's contig with pmax_end > the slice's first
-// locus and start < its end, in read order; each contributes its columns inside the slice.
-// put(active, read, column, word index in the slice) runs with every lane of the wave
-// (uniform control flow), active for lanes that hold a word.
-template <class F>
-__device__ __forceinline__ void walk_slice_words(const DevReads &R, int64_t slot, F &&put) {
+// One wave over projection slice `slot` (the block-row pool, ProjRec in gq_kernels.h): its
+// reads are those of the slice's contig with pmax_end > the slice's first locus and start <
+// its end, in read order; each piece (a read's columns inside the slice) takes the first row
+// that is free from its first column (greedy interval partitioning over pieces sorted by first
+// column: as many rows as the slice's deepest column has reads).  Returns the slice's rows,
+// or -1 past kSliceRowsMax.  With kWords, put(active, read, column, row) then runs once per
+// word with every lane of the wave (uniform control flow), active for lanes that hold a word.
+template <bool kWords, class F>
+__device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t slot, F &&put) {
   const int lane = threadIdx.x & 63;
   int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
   while (lo < hi) {
@@ -244,7 +246,14 @@ __device__ __forceinline__ void walk_slice_words(const DevReads &R, int64_t slot
     else a0 = m + 1;
   }
   const int64_t rz = a0;
-  uint32_t run = 0;
+  // row k's first free column (0-16) is byte k & 3 of rend[k >> 8] on lane (k >> 2) & 63;
+  // 0x7F: not opened.  A free row: byte <= s, tested four at a time without borrows.
+  constexpr int kRD = kSliceRowsMax / 256;
+  uint32_t rend[kRD];
+#pragma unroll
+  for (int j = 0; j < kRD; ++j) rend[j] = 0x7F7F7F7Fu;
+  int32_t nrows = 0;
+  bool over = false;
   for (int64_t r0 = ra; r0 < rz; r0 += 64) {
     const int64_t r = r0 + lane;
     int32_t s0 = 0, sl = 0;
@@ -256,19 +265,55 @@ __device__ __forceinline__ void walk_slice_words(const DevReads &R, int64_t slot
         sl = e > s0 ? e - s0 : 0;
       }
     }
-    const uint32_t incl = wave_incl_scan((uint32_t)sl), ex = incl - (uint32_t)sl;
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
-      const uint32_t w = w0 + (uint32_t)lane;
-      int k = 0;  // the last lane whose words start at or before w
+    int32_t myrow = -1;
+    unsigned long long pend = __ballot(sl > 0);
+    while (pend) {  // the batch's pieces in read order (uniform)
+      const int pl = __ffsll((long long)pend) - 1;
+      pend &= pend - 1;
+      const uint32_t ps = (uint32_t)__builtin_amdgcn_readlane(s0 - qc0, pl);
+      const uint32_t pe = ps + (uint32_t)__builtin_amdgcn_readlane(sl, pl);
+      const uint32_t lim = (ps + 1u) * 0x01010101u;
+      int32_t k = -1;
 #pragma unroll
-      for (int b = 32; b >= 1; b >>= 1)
-        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
-      const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
-      put(w < tot, r0 + k, col, (int64_t)run + w);
+      for (int j = 0; j < kRD; ++j) {
+        if (k >= 0 || 256 * j >= nrows) continue;  // uniform
+        const uint32_t fr = ~((rend[j] | 0x80808080u) - lim) & 0x80808080u;
+        const unsigned long long b = __ballot(fr != 0);
+        if (b) {
+          const int ln = __ffsll((long long)b) - 1;
+          const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fr, ln);
+          k = 256 * j + 4 * ln + (__builtin_ctz(f) >> 3);
+        }
+      }
+      if (k < 0) {
+        if (nrows >= kSliceRowsMax) {
+          over = true;
+          continue;
+        }
+        k = nrows++;
+      }
+      const int kl = (k >> 2) & 63, sh = 8 * (k & 3);
+#pragma unroll
+      for (int j = 0; j < kRD; ++j)
+        if (j == (k >> 8) && lane == kl) rend[j] = (rend[j] & ~(0xFFu << sh)) | (pe << sh);
+      if (lane == pl) myrow = k;
     }
-    run += tot;
+    if constexpr (kWords) {
+      const uint32_t len = myrow >= 0 ? (uint32_t)sl : 0u;
+      const uint32_t incl = wave_incl_scan(len), ex = incl - len;
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
+        const uint32_t w = w0 + (uint32_t)lane;
+        int k = 0;  // the last lane whose words start at or before w
+#pragma unroll
+        for (int b = 32; b >= 1; b >>= 1)
+          if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+        const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
+        put(w < tot, r0 + k, col, __shfl(myrow, k, 64));
+      }
+    }
   }
+  return over ? -1 : nrows;
 }
 
 // Wave-aggregated reservation of n <= 3 slots per lane on an LDS counter: lane prefixes
@@ -386,10 +431,11 @@ struct gq_dev_reads {
   int64_t seq_bytes = 0;
   int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // projection sizes (derive_shape)
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
-  int64_t n_pieces = 0;                                    // germline_proj piece records (PieceRec)
+  int64_t n_rows = 0;                                      // projection rows (512 B each, ProjRec)
   float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
   mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
   mutable int mproj_mapq = -1;
+  mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMarginNone (no bound)
 };
 
 namespace gq {

@@ -54,14 +54,11 @@ struct DevReads {
   const int64_t *caux_off;      // n_reads + 1 offsets into cev
   // derived at upload for the projection kernels (germline_proj / somatic_proj, see ProjRec)
   const struct ProjRec *prec;   // n_reads + 1 (the last: a zero record)
-  const uint8_t *proj;          // base codes, 8 loci per word, slice-major (see ProjRec)
+  const uint8_t *proj;          // base codes, 8 loci per word, in block rows (see ProjRec)
   const int64_t *qoff;          // n_contigs + 1: each contig's first slice (slice = 128 loci)
-  const int64_t *sbase;         // qoff[n_contigs] + 1: each slice's first word in proj
+  const int64_t *brow;          // qoff[n_contigs] / 4 + 1: each 512-locus block's first row in proj
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
   const int64_t *pev_off;       // n_reads + 1 offsets into pev
-  // derived at upload for germline_proj: the pieces of each slice (see PieceRec)
-  const uint32_t *pcs;          // per slice, in read order: one PieceRec word per read with words there
-  const int64_t *pbase;         // qoff[n_contigs] + 1: each slice's first piece
   const uint8_t *pbad;          // per slice: 1 if a read the projection cannot take overlaps it
   // derived at upload for plan_tiles: per 512-locus block g (qoff[c] / 4 + block in contig c),
   // the first read with pmax_end > the block's first locus and the first read starting at or
@@ -75,13 +72,17 @@ struct DevReads {
 // [col0, col1).  Its projection holds one byte per locus, the read's base there as a code
 // (A 1, C 3, T 4, G 7: ASCII & 7) where the element is a Match/Mismatch
 // (PileupElement.scala:68-135), 0 elsewhere (outside the read, deleted / skipped loci,
-// insertion and deletion anchors, N bases).  The pool is SLICE-MAJOR: slice q of contig c
-// (loci [128 q, 128 q + 128), columns [16 q, 16 q + 16)) holds, from word sbase[qoff[c] + q],
-// the words of every read with columns in the slice, in read order, each read's columns
-// [max(col0, 16 q), min(col1, 16 q + 16)).  So the 16 lanes that own a slice stream one
-// contiguous run of words over their reads (a read's offset in the run = the sum of the
-// earlier reads' pieces).  col1 = kProjNone marks a read the projection path cannot take
-// (bases other than A C G T N, no MD tag, a P op ...); it has no words.
+// insertion and deletion anchors, N bases).  A PIECE is one read's run of columns inside one
+// 128-locus slice (16 columns).  The pool is in BLOCK ROWS: a 512-locus block (4 slices, 64
+// columns) owns rows [brow[b], brow[b + 1]) of 64 words (512 bytes), word l of a row = column l
+// of the block.  Each slice's pieces are packed into its rows by greedy interval partitioning
+// in read order (a piece takes the first row that is free from its first column: as few rows
+// as the slice's deepest column holds reads), and the block has as many rows as its fullest
+// slice; the words no piece covers are zero.  So a wave that owns the block reads row k with
+// one 512-byte load (lane l: word l) and no per-row address math, and the rows are fewer than
+// the pieces (a read ending in a slice shares a row with one starting there).  col1 =
+// kProjNone marks a read the projection path cannot take (bases other than A C G T N, no MD
+// tag, a P op ...); it has no words.
 struct ProjRec {
   int32_t col0, col1;
 };
@@ -94,17 +95,7 @@ constexpr int32_t kProjNone = (int32_t)0x80000000;
 //     on a deleted base);
 //   y bit 31 set: loci [x, x + (y & 0x7FFFFFFF)) hold complex elements (insertion / deletion
 //     anchors, mid-deletions, clipped N-skips): the exact kernel decides them.
-// A PIECE is one read's run of words inside one slice.  Its record (PieceRec, one u32) gives
-// each of the 16 lanes owning the slice its word in four ALU ops, with no compare or select:
-//   bits 0-15   B = (the word of the piece's first column, counted from the first word of the
-//               slice's 512-locus block) - s0 + 16, s0 = the piece's first column in the slice
-//               (0-15); lane l16 of the group reads word B + l16 - 16
-//   bits 16-31  the lanes NOT in the piece: bit j set unless s0 <= j < s0 + len
-// so voff = ((B + l16 - 16) << 3) | (bit (16 + l16) << 31): an invalid lane's offset is out of
-// the buffer's range and its load returns 0.  kPieceNone (every lane invalid) pads a stage.  A
-// block of more than kPieceBaseMax words is pbad (the walker takes it).
-constexpr uint32_t kPieceNone = 0xFFFF0000u;
-constexpr int64_t kPieceBaseMax = 65535 - 16;
+constexpr int32_t kSliceRowsMax = 2048;  // rows of one slice (its deepest column); deeper: pbad
 constexpr uint32_t kPevComplex = 0x80000000u;
 constexpr uint32_t kPevNone = 7u << 4;  // a padding entry (no effect)
 
@@ -138,17 +129,16 @@ struct Tile {
 };
 static_assert(sizeof(Tile) == 64, "Tile layout");
 
-// Setup record of an aligned projection tile (plan_tiles, beside its Tile): the slice and
+// Setup record of an aligned projection tile (plan_tiles, beside its Tile): the row and
 // sparse-entry offsets germline_proj would otherwise load in two dependent rounds per tile.
 // germline_proj holds the next tile's Tile + TileX in one VGPR (a dword per lane 0-31) while it
 // counts the current one.
 struct TileX {
-  int64_t sb0, sb4;   // sbase[qs], sbase[qs + 4]: the block's projection words
-  int64_t e0, e1;     // pev_off[rb], pev_off[re]: the window's sparse entries
-  int64_t pb0;        // pbase[qs]: the block's first piece record
-  int32_t pbd[4];     // pbase[qs + g + 1] - pbase[qs]: end of slice g's pieces
+  int64_t row0;       // brow[qs / 4]: the block's first projection row
+  int32_t nrows;      // its rows
   uint32_t pbad4;     // byte g: pbad[qs + g]
-  uint32_t pad;
+  int64_t e0, e1;     // pev_off[rb], pev_off[re]: the window's sparse entries
+  int64_t pad[4];
 };
 static_assert(sizeof(TileX) == 64, "TileX layout");
 

@@ -183,19 +183,15 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   tiles[t] = tl;
   if (tilex) {  // aligned projection tiles: germline_proj's per-tile setup, resolved here
     TileX x{};
-    if (R.sbase && R.qoff && a0 > rb) {
+    if (R.brow && R.qoff && a0 > rb) {
       const int64_t qs = tl.qs;
-      x.sb0 = R.sbase[qs];
-      x.sb4 = R.sbase[qs + 4];
+      x.row0 = R.brow[qs >> 2];
+      x.nrows = (int32_t)(R.brow[(qs >> 2) + 1] - x.row0);
       x.e0 = R.pev_off[rb];
       x.e1 = R.pev_off[a0];
-      x.pb0 = R.pbase[qs];
       uint32_t bad = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        x.pbd[g] = (int32_t)min<int64_t>(R.pbase[qs + g + 1] - x.pb0, INT32_MAX);
-        bad |= (R.pbad[qs + g] ? 1u : 0u) << (8 * g);
-      }
+      for (int g = 0; g < 4; ++g) bad |= (R.pbad[qs + g] ? 1u : 0u) << (8 * g);
       x.pbad4 = bad;
     }
     tilex[t] = x;
@@ -352,14 +348,12 @@ __global__ void prec_fill(DevReads R, ProjRec *__restrict__ prec) {
   prec[r] = p;
 }
 
-// Words per slice (thread per read: each slice it meets gets its piece), for the slice offsets.
-// Also the pieces per slice (pcnt), and pbad = 1 on every slice a read the projection cannot
-// take overlaps (germline_proj hands such blocks to the walker).
-__global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ scnt,
-                            unsigned long long *__restrict__ pcnt, uint8_t *__restrict__ pbad) {
+// pbad = 1 on every slice a read the projection cannot take overlaps (the projection
+// kernels hand such blocks to the walkers), thread per read.
+__global__ void slice_bad(DevReads R, const ProjRec *__restrict__ prec, uint8_t *__restrict__ pbad) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
-  const ProjRec p = prec[r];
+  if (prec[r].col1 != kProjNone) return;
   int lo = 0, hi = R.n_contigs - 1;  // contig of r: last c with contig_read_begin[c] <= r
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
@@ -367,80 +361,29 @@ __global__ void slice_count(DevReads R, const ProjRec *__restrict__ prec, unsign
     else hi = m - 1;
   }
   const int64_t q0 = R.qoff[lo];
-  if (p.col1 == kProjNone) {
-    const int32_t s = R.start[r], e = R.end[r];
-    if (e > s && s >= 0)
-      for (int32_t q = s >> 7; q <= (e - 1) >> 7; ++q) pbad[q0 + q] = 1;
-    return;
-  }
-  if (p.col1 <= p.col0) return;
-  for (int32_t q = p.col0 >> 4; q <= (p.col1 - 1) >> 4; ++q) {
-    const int32_t a = max(p.col0, 16 * q), b = min(p.col1, 16 * q + 16);
-    atomicAdd(&scnt[q0 + q], (unsigned long long)(b - a));
-    atomicAdd(&pcnt[q0 + q], 1ull);
-  }
+  const int32_t s = R.start[r], e = R.end[r];
+  if (e > s && s >= 0)
+    for (int32_t q = s >> 7; q <= (e - 1) >> 7; ++q) pbad[q0 + q] = 1;
 }
 
-// The piece records (PieceRec), one wave per slice: the slice's reads in read order, each with
-// words there gets {its first word from the block's first word - s0 + 16, its invalid lanes}.
-__global__ __launch_bounds__(256) void piece_fill(DevReads R, int64_t n_slices, uint32_t *__restrict__ pcs,
-                                                  uint8_t *__restrict__ pbad) {
-  const int lane = threadIdx.x & 63;
+// Rows of each slice (walk_slice_rows, one wave per slice); past kSliceRowsMax the slice is
+// pbad.  Then each block's rows = its fullest slice's.
+__global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, int32_t *__restrict__ srows,
+                                                 uint8_t *__restrict__ pbad) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
-    int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
-    while (lo < hi) {
-      const int m = (lo + hi + 1) >> 1;
-      if (R.qoff[m] <= slot) lo = m;
-      else hi = m - 1;
+    const int32_t n = walk_slice_rows<false>(R, slot, [](bool, int64_t, int32_t, int32_t) {});
+    if ((threadIdx.x & 63) == 0) {
+      srows[slot] = n < 0 ? 0 : n;
+      if (n < 0) pbad[slot] = 1;
     }
-    const int32_t q = (int32_t)(slot - R.qoff[lo]);
-    const int32_t L = 128 * q, qc0 = 16 * q, qc1 = qc0 + 16;
-    const int64_t cb = R.contig_read_begin[lo], ce = R.contig_read_begin[lo + 1];
-    int64_t a0 = cb, a1 = ce;
-    while (a0 < a1) {  // first read with pmax_end > L
-      const int64_t m = (a0 + a1) >> 1;
-      if (R.pmax_end[m] > L) a1 = m;
-      else a0 = m + 1;
-    }
-    const int64_t ra = a0;
-    a1 = ce;
-    while (a0 < a1) {  // first read with start >= L + 128
-      const int64_t m = (a0 + a1) >> 1;
-      if (R.start[m] >= L + 128) a1 = m;
-      else a0 = m + 1;
-    }
-    const int64_t rz = a0;
-    const int64_t wb = R.sbase[slot] - R.sbase[slot & ~(int64_t)3];  // the slice run in its block
-    const int64_t pb = R.pbase[slot];
-    int64_t run = 0, np = 0;
-    bool over = false;
-    for (int64_t r0 = ra; r0 < rz; r0 += 64) {
-      const int64_t r = r0 + lane;
-      int32_t s0 = 0, sl = 0;
-      if (r < rz) {
-        const ProjRec p = R.prec[r];
-        if (p.col1 != kProjNone) {
-          s0 = max(p.col0, qc0);
-          sl = max(min(p.col1, qc1) - s0, 0);
-        }
-      }
-      const uint32_t ex = wave_incl_scan((uint32_t)sl) - (uint32_t)sl;
-      const uint64_t has = __ballot(sl > 0);
-      const int64_t k = np + (int64_t)__popcll(has & ((1ull << lane) - 1ull));
-      const int64_t w = wb + run + (int64_t)ex;
-      if (sl > 0) {
-        over = over || w > kPieceBaseMax;
-        const uint32_t s0r = (uint32_t)(s0 - qc0);
-        const uint32_t valid = ((1u << sl) - 1u) << s0r;  // lanes s0 .. s0 + len - 1 (sl <= 16 - s0r)
-        pcs[pb + k] = ((~valid & 0xFFFFu) << 16) | (((uint32_t)w + 16u - s0r) & 0xFFFFu);
-      }
-      run += (int64_t)__builtin_amdgcn_readlane((int)(ex + (uint32_t)sl), 63);
-      np += (int64_t)__popcll(has);
-    }
-    if (__ballot(over) && lane == 0) pbad[slot] = 1;
   }
+}
+__global__ void block_rows(int64_t n_blocks, const int32_t *__restrict__ srows, int64_t *__restrict__ brows) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > n_blocks) return;
+  brows[b] = b < n_blocks ? max(max(srows[4 * b], srows[4 * b + 1]), max(srows[4 * b + 2], srows[4 * b + 3])) : 0;
 }
 
 // Reads the projection takes, into kSpread words (summed on the host): a grid-stride count per
@@ -483,14 +426,16 @@ __device__ uint2 proj_word(const DevReads &R, int64_t r, int32_t col) {
   return make_uint2(v[0], v[1]);
 }
 
-// The projection pool, one wave per slice (walk_slice_words): coalesced word stores.
+// The projection pool in block rows, one wave per slice (walk_slice_rows; pbad slices stay
+// zero: their blocks go to the walker).
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
-    const int64_t base = R.sbase[slot];
-    walk_slice_words(R, slot, [&](bool act, int64_t r, int32_t col, int64_t w) {
-      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + w)) = proj_word(R, r, col);
+    if (R.pbad[slot]) continue;  // uniform
+    const int64_t base = 64 * R.brow[slot >> 2] + 16 * (slot & 3);
+    walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
+      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + 64 * (int64_t)row + (col & 15))) = proj_word(R, r, col);
     });
   }
 }
@@ -1708,8 +1653,8 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       }
     }
     const int64_t n_sl = qoff[(size_t)nc];
-    void *qo = nullptr, *pr = nullptr, *sc = nullptr, *sb = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
-         *eo = nullptr, *pe = nullptr;
+    void *qo = nullptr, *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr,
+         *ne = nullptr, *eo = nullptr, *pe = nullptr, *pbd = nullptr;
     HIP_TRY(hipMalloc(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
     d->owned.push_back(qo);
     HIP_TRY(hipMemcpyAsync(qo, qoff.data(), sizeof(int64_t) * ((size_t)nc + 1), hipMemcpyHostToDevice, c->stream));
@@ -1734,59 +1679,57 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
     HIP_TRY(hipGetLastError());
     d->d.prec = (const ProjRec *)pr;
-    HIP_TRY(hipMalloc(&sc, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    HIP_TRY(hipMemsetAsync(sc, 0, sizeof(int64_t) * (size_t)(n_sl + 1), c->stream));
-    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    d->owned.push_back(sb);
-    void *pcn = nullptr, *pbs = nullptr, *pbd = nullptr, *pcs = nullptr;
-    HIP_TRY(hipMalloc(&pcn, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    HIP_TRY(hipMemsetAsync(pcn, 0, sizeof(int64_t) * (size_t)(n_sl + 1), c->stream));
-    HIP_TRY(hipMalloc(&pbs, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    d->owned.push_back(pbs);
+    // sparse-entry offsets; slices a read the projection cannot take touches (pbad); each
+    // slice's rows, each block's (its fullest slice's), the blocks' first rows (scan)
+    const int64_t n_blk = n_sl / 4;
     HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
     d->owned.push_back(pbd);
     HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
     if (n > 0) {
-      hipLaunchKernelGGL(slice_count, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const ProjRec *)pr, (unsigned long long *)sc, (unsigned long long *)pcn, (uint8_t *)pbd);
+      hipLaunchKernelGGL(slice_bad, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (const ProjRec *)pr, (uint8_t *)pbd);
       HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipMalloc(&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
+    HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_blk + 1)));
+    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_blk + 1)));
+    d->owned.push_back(sb);
+    if (n_sl > 0) {
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(row_count, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (int32_t *)sc,
+                         (uint8_t *)pbd);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(block_rows, dim3((unsigned)((n_blk + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_blk,
+                       (const int32_t *)sc, (int64_t *)br);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
     HIP_TRY(hipMalloc(&eo, sizeof(int64_t) * (size_t)(n + 1)));
     d->owned.push_back(eo);
     hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, (int64_t *)ne);
     HIP_TRY(hipGetLastError());
     size_t tb = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)sc, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_blk + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
     HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)sc, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)pcn, (int64_t *)pbs, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_blk + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
-    int64_t tot[3] = {0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    int64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_blk, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&tot[2], (int64_t *)pbs + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(tmp);
     (void)hipFree(sc);
+    (void)hipFree(br);
     (void)hipFree(ne);
-    (void)hipFree(pcn);
-    d->d.sbase = (const int64_t *)sb;
-    d->d.pbase = (const int64_t *)pbs;
+    d->d.brow = (const int64_t *)sb;
     d->d.pbad = (const uint8_t *)pbd;
-    HIP_TRY(hipMalloc(&pcs, sizeof(uint32_t) * (size_t)(tot[2] + 64)));
-    d->owned.push_back(pcs);
-    d->d.pcs = (const uint32_t *)pcs;
-    d->n_pieces = tot[2];
-    if (n_sl > 0) {
-      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-      hipLaunchKernelGGL(piece_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint32_t *)pcs,
-                         (uint8_t *)pbd);
-      HIP_TRY(hipGetLastError());
-    }
-    HIP_TRY(hipMalloc(&pj, (size_t)(8 * tot[0] + 16)));
+    d->n_rows = tot[0];
+    // the pool: rows of 64 words, zero where no piece lies
+    const size_t pool_bytes = (size_t)512 * (size_t)tot[0] + 16;
+    HIP_TRY(hipMalloc(&pj, pool_bytes));
     d->owned.push_back(pj);
+    HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
     HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
     d->owned.push_back(pe);
     if (n_sl > 0) {
@@ -1802,7 +1745,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.proj = (const uint8_t *)pj;
     d->d.pev = (const uint2 *)pe;
     d->d.pev_off = (const int64_t *)eo;
-    d->proj_bytes = 8 * tot[0];
+    d->proj_bytes = 512 * tot[0];
     d->n_slices = n_sl;
     d->pev_count = tot[1];
     if (n > 0) {  // reads the projection takes
@@ -2115,7 +2058,7 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->seq_bytes = d->seq_bytes;
   out->proj_bytes = d->proj_bytes;
   out->pev_count = d->pev_count;
-  out->n_pieces = d->n_pieces;
+  out->n_rows = d->n_rows;
   out->proj_reads = d->proj_reads;
   out->h2d_ms = d->h2d_ms;
   out->derive_ms = d->derive_ms;
@@ -2126,6 +2069,7 @@ void gq_reads_free(gq_dev_reads *d) {
   if (!d) return;
   for (void *p : d->owned) (void)hipFree(p);
   if (d->mproj) (void)hipFree(d->mproj);
+  if (d->mnb) (void)hipFree(d->mnb);
   delete d;
 }
 
@@ -2208,7 +2152,7 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   pl.d_rwin = (const int32_t *)(base + o_rwin);
   pl.d_wcontig = (const int32_t *)(base + o_wc);
   // aligned 512-locus plans over projected reads carry a TileX per tile after the Tiles
-  const bool with_x = aligned && T == 512 && rd->d.sbase != nullptr;
+  const bool with_x = aligned && T == 512 && rd->d.brow != nullptr;
   HIP_TRY(tiles_buf.ensure((size_t)tiles * (sizeof(Tile) + (with_x ? sizeof(TileX) : 0))));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,
@@ -2251,7 +2195,7 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                     (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.pcs, R.proj,
+                     (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.proj,
                      R.pev, R.n_samples,
                      p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
   HIP_TRY(hipGetLastError());

@@ -35,6 +35,8 @@
 #include <vector>
 
 #include "gq_alleles.h"
+#include <hipcub/hipcub.hpp>
+
 #include "gq_host.h"
 #include "gq_strictmath.h"
 #include "gq_scala_order.h"
@@ -1149,96 +1151,157 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
     void *p = nullptr;
     HIP_TRY(hipMalloc(&p, (size_t)(2 * t->proj_bytes + 32)));
     t->mproj = p;
+    HIP_TRY(hipMemsetAsync(p, 0, (size_t)(2 * t->proj_bytes + 32), c->stream));  // the words no piece covers
+    void *q = nullptr;
+    HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
+    t->mnb = q;
+    HIP_TRY(hipMemsetAsync(q, 0, (size_t)t->n_slices + 16, c->stream));
   }
   if (t->n_slices > 0)
     hipLaunchKernelGGL(mproj_fill, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
-                       c->stream, t->d, t->n_slices, min_mapq, incl_align ? 1 : 0, (int16_t *)t->mproj);
+                       c->stream, t->d, t->n_slices, min_mapq, incl_align ? 1 : 0, (int16_t *)t->mproj,
+                       (uint8_t *)t->mnb);
   HIP_TRY(hipGetLastError());
   t->mproj_mapq = key;
   return GQ_OK;
 }
 
 // The records of a somatic / germline-standard pass (device SomRec array + allele pool) ->
-// the caller's result arrays in output (key) order.  The keys are sorted as (key, index) pairs
-// by an LSD radix sort (11-bit digits over the bits the largest key uses; skipped when the
-// records already come in order), then the fields are gathered once: the 176-byte records are
-// never moved.  ev[4] marks the end of the D2H; timings.marshal_ms is the host time after it.
-gq_status fetch_somatic_records(gq_ctx *c, const Counters &hc, unsigned long long pool_cap, gq_somatic_calls *res) {
-  const int64_t nr = (int64_t)hc.n_rec;
-  std::vector<SomRec> recs((size_t)nr);
-  std::vector<uint8_t> hpool((size_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
-  if (nr) HIP_TRY(hipMemcpyAsync(recs.data(), c->srecs.p, (size_t)nr * sizeof(SomRec), hipMemcpyDeviceToHost, c->stream));
-  if (!hpool.empty()) HIP_TRY(hipMemcpyAsync(hpool.data(), c->pool.p, hpool.size(), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+// the caller's result arrays in output (key) order, built on the device: the (key, slot) pairs
+// radix-sorted (hipcub, only the bits a key can use), the allele lengths scanned into pool
+// offsets, then one kernel writes the result image [pool_len | SoA columns | allele pool] and
+// one D2H copy brings it into the result block.  ev[4] marks the end of the D2H;
+// timings.marshal_ms is the host time after it.
+struct SomLayout {  // byte offsets inside the image; header = int64 pool_len
+  size_t contig, pos, sample, ref_off, ref_len, alt_off, alt_len, log_odds, gq, tumor, normal, flags, pool, bytes;
+};
+SomLayout som_layout(int64_t n, int64_t dev_pool_used) {
+  auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+  const size_t N = (size_t)n;
+  SomLayout L;
+  L.contig = 64;
+  L.pos = al(L.contig + 4 * N);
+  L.sample = al(L.pos + 8 * N);
+  L.ref_off = al(L.sample + N);
+  L.ref_len = al(L.ref_off + 8 * N);
+  L.alt_off = al(L.ref_len + 4 * N);
+  L.alt_len = al(L.alt_off + 8 * N);
+  L.log_odds = al(L.alt_len + 4 * N);
+  L.gq = al(L.log_odds + 8 * N);
+  L.tumor = al(L.gq + 4 * N);
+  L.normal = al(L.tumor + sizeof(gq_evidence) * N);
+  L.flags = al(L.normal + sizeof(gq_evidence) * N);
+  L.pool = al(L.flags + N);
+  // inline alleles hold <= 8 bytes; longer ones live in the device pool (each used once)
+  L.bytes = al(L.pool + 8 * N + (size_t)dev_pool_used + 1);
+  return L;
+}
+
+__global__ void som_keys(const SomRec *__restrict__ recs, int64_t n, uint64_t *__restrict__ keys,
+                         uint32_t *__restrict__ slot) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  keys[k] = recs[k].key;
+  slot[k] = (uint32_t)k;
+}
+
+__global__ void som_lengths(const SomRec *__restrict__ recs, const uint32_t *__restrict__ order, int64_t n,
+                            int64_t *__restrict__ len) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const SomRec &r = recs[order[k]];
+  len[k] = (int64_t)r.ref_len + r.alt_len;
+}
+
+// Record k of the output (slot order[k]) into the image; its allele bytes at pool offset off[k].
+__global__ void som_image(const SomRec *__restrict__ recs, const uint32_t *__restrict__ order,
+                          const int64_t *__restrict__ off, const uint8_t *__restrict__ dpool, int64_t n, SomLayout L,
+                          uint8_t *__restrict__ img) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const SomRec &r = recs[order[k]];
+  const int64_t at = off[k];
+  const int tot = r.ref_len + r.alt_len;
+  ((int32_t *)(img + L.contig))[k] = r.contig;
+  ((int64_t *)(img + L.pos))[k] = r.pos;
+  img[L.sample + k] = (uint8_t)((r.key >> 4) & 0xFFu);  // germline-standard: the sample slot (somatic: 0)
+  ((int64_t *)(img + L.ref_off))[k] = at;
+  ((int32_t *)(img + L.ref_len))[k] = r.ref_len;
+  ((int64_t *)(img + L.alt_off))[k] = at + r.ref_len;
+  ((int32_t *)(img + L.alt_len))[k] = r.alt_len;
+  ((double *)(img + L.log_odds))[k] = r.log_odds;
+  ((int32_t *)(img + L.gq))[k] = r.gq;
+  ((gq_evidence *)(img + L.tumor))[k] = r.tumor;
+  ((gq_evidence *)(img + L.normal))[k] = r.normal;
+  img[L.flags + k] = r.flags;
+  uint8_t *o = img + L.pool + at;
+  if (tot <= 8)
+    for (int i = 0; i < tot; ++i) o[i] = (uint8_t)(r.allele >> (8 * i));
+  else
+    for (int i = 0; i < tot; ++i) o[i] = dpool[r.allele + (uint64_t)i];
+  if (k == n - 1) *(int64_t *)img = at + tot;
+}
+
+gq_status fetch_somatic_records(gq_ctx *c, const Counters &hc, unsigned long long pool_cap, uint64_t key_bound,
+                                gq_somatic_calls *res) {
+  const int64_t n = (int64_t)hc.n_rec;
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  const SomLayout lay = som_layout(n, (int64_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
+  HIP_TRY(c->image.ensure(lay.bytes));
+  if (n > 0) {
+    HIP_TRY(c->keys.ensure(nn * 8));
+    HIP_TRY(c->keys_sorted.ensure(nn * 8));
+    HIP_TRY(c->idx.ensure(nn * 8));
+    HIP_TRY(c->idx_sorted.ensure(nn * 8));
+    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+    uint64_t *keys = (uint64_t *)c->keys.p, *keys2 = (uint64_t *)c->keys_sorted.p;
+    uint32_t *slot = (uint32_t *)c->idx.p, *order = (uint32_t *)c->idx_sorted.p;
+    int64_t *len = (int64_t *)c->keys.p, *off = (int64_t *)c->idx.p;  // reused once the sort is done
+    hipLaunchKernelGGL(som_keys, dim3(nb), dim3(kBlock), 0, c->stream, (const SomRec *)c->srecs.p, n, keys, slot);
+    HIP_TRY(hipGetLastError());
+    const int end_bit = key_bound ? 64 - __builtin_clzll(key_bound) : 64;
+    size_t tmp = 0, tmp2 = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys, keys2, slot, order, (int)n, 0, end_bit, c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, len, off, (int)n, c->stream));
+    HIP_TRY(c->sort_tmp.ensure(std::max(tmp, tmp2)));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, keys, keys2, slot, order, (int)n, 0, end_bit,
+                                               c->stream));
+    hipLaunchKernelGGL(som_lengths, dim3(nb), dim3(kBlock), 0, c->stream, (const SomRec *)c->srecs.p,
+                       (const uint32_t *)order, n, len);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp2, len, off, (int)n, c->stream));
+    hipLaunchKernelGGL(som_image, dim3(nb), dim3(kBlock), 0, c->stream, (const SomRec *)c->srecs.p,
+                       (const uint32_t *)order, (const int64_t *)off, (const uint8_t *)c->pool.p, n, lay,
+                       (uint8_t *)c->image.p);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemsetAsync(c->image.p, 0, 64, c->stream));
+  }
+  uint8_t *blk = (uint8_t *)malloc(lay.bytes);
+  if (!blk) return set_err(GQ_E_NOMEM, "somatic result block of %zu bytes", lay.bytes);
+  const hipError_t e = hipMemcpyAsync(blk, c->image.p, lay.bytes, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) (void)hipEventRecord(c->ev[4], c->stream);
+  if (e != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+    free(blk);
+    return set_err(GQ_E_HIP, "somatic result image D2H");
+  }
   const auto m0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> idx((size_t)nr), tmp((size_t)nr);
-  uint64_t mx = 0;
-  bool sorted = true;
-  for (int64_t k = 0; k < nr; ++k) {
-    idx[(size_t)k] = (uint32_t)k;
-    mx = std::max(mx, recs[(size_t)k].key);
-    if (k && recs[(size_t)k].key < recs[(size_t)k - 1].key) sorted = false;
-  }
-  if (!sorted) {
-    constexpr int kD = 11;
-    std::vector<uint32_t> cnt(1u << kD);
-    for (int sh = 0; sh < 64 && (mx >> sh) != 0; sh += kD) {
-      std::fill(cnt.begin(), cnt.end(), 0u);
-      for (int64_t k = 0; k < nr; ++k) ++cnt[(recs[idx[(size_t)k]].key >> sh) & ((1u << kD) - 1)];
-      uint32_t o = 0;
-      for (uint32_t &x : cnt) {
-        const uint32_t t = x;
-        x = o;
-        o += t;
-      }
-      for (int64_t k = 0; k < nr; ++k) tmp[cnt[(recs[idx[(size_t)k]].key >> sh) & ((1u << kD) - 1)]++] = idx[(size_t)k];
-      idx.swap(tmp);
-    }
-  }
-  const size_t N = (size_t)std::max<int64_t>(nr, 1);
-  res->n = nr;
-  res->contig = (int32_t *)malloc(N * 4);
-  res->pos = (int64_t *)malloc(N * 8);
-  res->sample = (uint8_t *)calloc(N, 1);
-  res->ref_off = (int64_t *)malloc(N * 8);
-  res->alt_off = (int64_t *)malloc(N * 8);
-  res->ref_len = (int32_t *)malloc(N * 4);
-  res->alt_len = (int32_t *)malloc(N * 4);
-  res->log_odds = (double *)malloc(N * 8);
-  res->gq = (int32_t *)malloc(N * 4);
-  res->tumor = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->normal = (gq_evidence *)malloc(N * sizeof(gq_evidence));
-  res->flags = (uint8_t *)malloc(N);
-  size_t pool_bytes = 0;
-  for (int64_t k = 0; k < nr; ++k) pool_bytes += (size_t)recs[(size_t)k].ref_len + recs[(size_t)k].alt_len;
-  res->allele_pool = (uint8_t *)malloc(std::max<size_t>(pool_bytes, 1));
-  if (!res->contig || !res->pos || !res->sample || !res->ref_off || !res->alt_off || !res->ref_len || !res->alt_len ||
-      !res->log_odds || !res->gq || !res->tumor || !res->normal || !res->flags || !res->allele_pool)
-    return set_err(GQ_E_NOMEM, "somatic result arrays");
-  size_t at = 0;
-  for (int64_t k = 0; k < nr; ++k) {
-    const SomRec &r = recs[idx[(size_t)k]];
-    res->contig[k] = r.contig;
-    res->pos[k] = r.pos;
-    res->sample[k] = (uint8_t)((r.key >> 4) & 0xFFu);  // germline-standard: the sample slot (somatic: 0)
-    res->ref_len[k] = r.ref_len;
-    res->alt_len[k] = r.alt_len;
-    res->ref_off[k] = (int64_t)at;
-    res->alt_off[k] = (int64_t)at + r.ref_len;
-    const int tot = r.ref_len + r.alt_len;
-    if (tot <= 8)
-      for (int i = 0; i < tot; ++i) res->allele_pool[at + (size_t)i] = (uint8_t)(r.allele >> (8 * i));
-    else
-      memcpy(res->allele_pool + at, hpool.data() + r.allele, (size_t)tot);
-    at += (size_t)tot;
-    res->log_odds[k] = r.log_odds;
-    res->gq[k] = r.gq;
-    res->tumor[k] = r.tumor;
-    res->normal[k] = r.normal;
-    res->flags[k] = r.flags;
-  }
-  res->pool_len = (int64_t)at;
+  res->n = n;
+  res->block_ = blk;
+  res->contig = (int32_t *)(blk + lay.contig);
+  res->pos = (int64_t *)(blk + lay.pos);
+  res->sample = blk + lay.sample;
+  res->ref_off = (int64_t *)(blk + lay.ref_off);
+  res->ref_len = (int32_t *)(blk + lay.ref_len);
+  res->alt_off = (int64_t *)(blk + lay.alt_off);
+  res->alt_len = (int32_t *)(blk + lay.alt_len);
+  res->log_odds = (double *)(blk + lay.log_odds);
+  res->gq = (int32_t *)(blk + lay.gq);
+  res->tumor = (gq_evidence *)(blk + lay.tumor);
+  res->normal = (gq_evidence *)(blk + lay.normal);
+  res->flags = blk + lay.flags;
+  res->allele_pool = blk + lay.pool;
+  res->pool_len = n > 0 ? *(const int64_t *)blk : 0;
   c->timings.marshal_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - m0).count();
   return GQ_OK;
 }
@@ -1446,12 +1509,12 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     if (rv.b)
       hipLaunchKernelGGL(somatic_proj<true>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
-                         (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (const int16_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
                          (int32_t *)c->slow.p, rv);
     else
       hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
-                         (const int16_t *)t->mproj, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (const int16_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
                          (int32_t *)c->slow.p, rv);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((somatic_tile<SomProjCfg::kT>), dim3((unsigned)std::min<int64_t>(pt.n_tiles, 2048)), dim3(kBlock), 0,
@@ -1575,7 +1638,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     free(res);
     return st;
   }
-  st = fetch_somatic_records(c, hc, pool_cap, res);
+  st = fetch_somatic_records(c, hc, pool_cap, (uint64_t)std::max<int64_t>(pt.n_loci, 1) << 12, res);
   if (st) {
     free(res);
     return st;
@@ -1593,6 +1656,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   c->timings.total_ms = ms;
   c->timings.pileup_launches = 1;
   c->timings.tiles = pt.n_tiles;
+  c->timings.walk_tiles = (int64_t)hc.n_slow;
   c->timings.deep_loci = (int64_t)hc.n_deep;
   c->timings.deep_max = (int64_t)hc.deep_max;
   c->timings.call_ms = call_ms;
@@ -1814,7 +1878,7 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, pt.n_tiles, rd->d, (const int16_t *)rd->mproj,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, pt.n_tiles, rd->d, (const int16_t *)rd->mproj, (const uint8_t *)rd->mnb,
                        rd->d.start, rd->d.end, (ComplexItem *)c->cplx.p, og, ctr, (int32_t *)c->slow.p,
                        RefView{nullptr, nullptr}, no_bound);
     HIP_TRY(hipGetLastError());
@@ -1881,7 +1945,7 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
   st = check_device_error(c, hc);
   if (st) return fail(st);
-  st = fetch_somatic_records(c, hc, pool_cap, res);
+  st = fetch_somatic_records(c, hc, pool_cap, (uint64_t)std::max<int64_t>(pt.n_loci, 1) << 12, res);
   if (st) return fail(st);
   res->visited_loci = (int64_t)hc.visited;
   res->candidate_loci = (int64_t)hc.n_complex;
@@ -1902,6 +1966,11 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
 
 void gq_free_somatic(gq_somatic_calls *r) {
   if (!r) return;
+  if (r->block_) {  // one block holds every array (fetch_somatic_records)
+    free(r->block_);
+    free(r);
+    return;
+  }
   free(r->contig);
   free(r->pos);
   free(r->sample);

@@ -18,18 +18,21 @@
 #include "gq_kernels.h"
 
 // The margin term of one tumor element (hom_ref_margin_lane's t, in units of 1/256, rounded
-// down; INT16_MIN when it is below -127 or -inf), so that a sum of terms never exceeds the
-// margin it stands for: a sum that passes the bound proves what the FP32 sum proved.
+// down; kMarginNone when it is below -8191/256 or -inf), so that a sum of terms never exceeds
+// the margin it stands for: a sum that passes the bound proves what the FP32 sum proved.
+// Four terms >= -8191 sum exactly in 16 bits (somatic_proj folds every four rows into 32
+// bits); a slice holding kMarginNone gets no bound at all (mnb).
+constexpr int16_t kMarginNone = -8192;
 __device__ __forceinline__ int16_t margin_term(bool match, int q, float em, float lsm) {
   constexpr float kLn2 = 0.69314718f;
-  if (q < 0) return (int16_t)-32768;  // outside the quality table: no bound
+  if (q < 0) return kMarginNone;  // outside the quality table: no bound
   const float eb = exp2f(-0.33219281f * (float)q);
   const float lsq = log1pf(-eb);
   const float f = eb + em - eb * em;  // 1 - pc
   const float t = match ? kLn2 + lsq + lsm - fmaxf(0.0f, kLn2 + __logf(f)) : __logf(f);
-  if (!(t > -127.0f)) return (int16_t)-32768;
   const float v = floorf(t * 256.0f) - 1.0f;  // -1: room for the FP32 rounding of t
-  return (int16_t)(v > 32767.0f ? 32767.0f : v);
+  if (!(v >= -8191.0f)) return kMarginNone;
+  return (int16_t)(v > 8191.0f ? 8191.0f : v);
 }
 
 // The margin word of tumor read r at column col (8 loci, int16 each; hom_ref_margin_lane's
@@ -93,16 +96,28 @@ __device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_
 }
 
 // The margin projection of the tumor reads, laid out as `proj` (an int16 per projection byte:
-// word w of the pool at mproj + 16 w), one wave per slice.
+// word w of the row pool at mproj + 8 w, 16 bytes), one wave per slice (the same rows:
+// walk_slice_rows packs a slice's pieces the same way every time).
 __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq, int incl_align,
-                                                  int16_t *__restrict__ mproj) {
+                                                  int16_t *__restrict__ mproj, uint8_t *__restrict__ mnb) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
-    const int64_t base = R.sbase[slot];
-    walk_slice_words(R, slot, [&](bool act, int64_t r, int32_t col, int64_t w) {
-      if (act) *reinterpret_cast<uint4 *>(mproj + 8 * (base + w)) = margin_word(R, r, col, min_mapq, incl_align != 0);
+    if (R.pbad[slot]) continue;  // uniform
+    const int64_t base = 64 * R.brow[slot >> 2] + 16 * (slot & 3);
+    bool none = false;
+    walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
+      if (act) {
+        const uint4 w = margin_word(R, r, col, min_mapq, incl_align != 0);
+        *reinterpret_cast<uint4 *>(mproj + 8 * (base + 64 * (int64_t)row + (col & 15))) = w;
+        auto has = [](uint32_t x) {
+          return (int16_t)(x & 0xFFFFu) == kMarginNone || (int16_t)(x >> 16) == kMarginNone;
+        };
+        none = none || has(w.x) || has(w.y) || has(w.z) || has(w.w);
+      }
     });
+    const bool any = __ballot(none) != 0;
+    if ((threadIdx.x & 63) == 0) mnb[slot] = any ? 1 : 0;
   }
 }
 
@@ -111,9 +126,7 @@ struct SomProjCfg {
   static constexpr int kWaves = 4;
   static constexpr int kThreads = 64 * kWaves;
   static constexpr int kU = 4;
-  static constexpr int kMaxRows = 255;
-  static constexpr int kRecCap = 384;  // tumor reads per tile window (60x: ~270)
-  static constexpr int kRecBuf = kRecCap + 1;
+  static constexpr int kMaxRows = kSliceRowsMax;  // rows per block (16-bit counts past 240 rows)
   static constexpr int kEnt = 6;
 };
 
@@ -151,24 +164,25 @@ __device__ __forceinline__ bool ref_agrees(uint32_t md_mask, uint32_t base) {
 template <bool kRef>
 __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void somatic_proj(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, int64_t n_tiles, DevReads RT,
-    const int16_t *__restrict__ mproj, const int32_t *__restrict__ n_start, const int32_t *__restrict__ n_end,
+    const int16_t *__restrict__ mproj, const uint8_t *__restrict__ mnb, const int32_t *__restrict__ n_start,
+    const int32_t *__restrict__ n_end,
     ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref,
     int no_bound = 0) {
   using C = SomProjCfg;
   constexpr int T = C::kT, U = C::kU;
-  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][T];  // tumor event read bases: A C T G bytes
-  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];  // MD bits 0-3 | N << 8 | complex diff << 16
+  // per locus: tumor event read bases (2 words: A | C << 16, T | G << 16); MD bits 0-3 | N << 4 |
+  // complex diff << 16
+  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
+  __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ __attribute__((aligned(16))) uint32_t cvw[C::kWaves][T];  // normal coverage differences
-  __shared__ __attribute__((aligned(16))) uint32_t recw[C::kWaves][C::kRecBuf];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave], *cv = cvw[wave];
-  uint32_t *rec = recw[wave];
   {
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
-    e4[0] = e4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -177,40 +191,27 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
   const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
   unsigned visited = 0;
-  const int g = lane >> 4;
-  const uint2 *prec2 = reinterpret_cast<const uint2 *>(RT.prec);
-  const int32_t g16 = 16 * g;
   for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
     const Tile tt = tiles_t[i], tn = tiles_n[i];
     const int32_t L0 = tt.L0, L1 = tt.L1;
     const int64_t rb = tt.rb, re = tt.re;
     const int32_t B0 = L0 & ~(T - 1), C0 = B0 >> 3;
-    const int64_t nwin = re - rb;
-    if (nwin > C::kRecCap || (tn.re - tn.rb) >= 65535) {
+    if ((tn.re - tn.rb) >= 65535) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
     }
-    const int nrd = (int)nwin;
-    // ---- tumor: read records (LDS), group ranges, the first sparse entries (as germline_proj)
-    // the block's first slice: it exists only where tumor reads reach the block (a tile may
-    // hold normal reads alone, past the tumor's last read)
-    const bool tumor = nrd > 0;
+    // ---- tumor: the block's projection rows (ProjRec) and the first sparse entries.  The
+    // block exists only where tumor reads reach it (a tile may hold normal reads alone, past
+    // the tumor's last read).  A pbad slice (a read the projection cannot take) or more than
+    // kMaxRows rows (byte counters): somatic_tile.
+    const bool tumor = re > rb;
     const int64_t qs = tumor ? tt.qs : 0;  // qoff[contig] + (B0 >> 7), from the plan
-    const int64_t sb0 = tumor ? RT.sbase[qs] : 0, sb4 = tumor ? RT.sbase[qs + 4] : 0;
-    const uint32_t gb = tumor ? (uint32_t)(RT.sbase[qs + g] - sb0) : 0u;  // this group's slice run, in words
+    const int64_t row0 = tumor ? RT.brow[qs >> 2] : 0;
+    const int32_t nrows = tumor ? (int32_t)(RT.brow[(qs >> 2) + 1] - row0) : 0;
+    const uint32_t bad4 = tumor ? *reinterpret_cast<const uint32_t *>(RT.pbad + qs) : 0u;
+    const bool nb = tumor && *reinterpret_cast<const uint32_t *>(mnb + qs) != 0u;  // a slice without bounds
     const int64_t e0 = RT.pev_off[rb], e1 = RT.pev_off[re];
-    constexpr int NQ = (C::kRecCap + 63) / 64, NE = C::kEnt;
-    int32_t pe[NQ];
-    uint2 pp[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      pe[q] = 0x7FFFFFFF;
-      pp[q] = make_uint2(0x7FFFFFFFu, 0u);
-      if (64 * q + lane < nrd) {
-        pe[q] = RT.pmax_end[rb + 64 * q + lane];
-        pp[q] = prec2[rb + 64 * q + lane];
-      }
-    }
+    constexpr int NE = C::kEnt;
     uint2 ent[NE];
 #pragma unroll
     for (int j = 0; j < NE; ++j) {
@@ -218,39 +219,21 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       ent[j] = make_uint2(0x80000000u, kPevNone);
       if (k < e1) ent[j] = RT.pev[k];
     }
-    bool bad = false;
-    int lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0, hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      if (64 * q >= nrd) break;
-      const int32_t c0 = (int32_t)pp[q].x, c1 = (int32_t)pp[q].y;
-      if (64 * q + lane < nrd) rec[64 * q + lane] = (uint32_t)(c0 - C0) & 0xFFFFu | ((uint32_t)(c1 - c0) << 16);
-      bad = bad || __ballot(c1 == kProjNone || c0 - C0 < -32768) != 0;
-      lo0 += (int)__popcll(__ballot(pe[q] <= B0));
-      lo1 += (int)__popcll(__ballot(pe[q] <= B0 + 128));
-      lo2 += (int)__popcll(__ballot(pe[q] <= B0 + 256));
-      lo3 += (int)__popcll(__ballot(pe[q] <= B0 + 384));
-      hi0 += (int)__popcll(__ballot(c0 < C0 + 16));
-      hi1 += (int)__popcll(__ballot(c0 < C0 + 32));
-      hi2 += (int)__popcll(__ballot(c0 < C0 + 48));
-      hi3 += (int)__popcll(__ballot(c0 < C0 + 64));
-    }
-    const int nmax = max(max(hi0 - lo0, hi1 - lo1), max(hi2 - lo2, hi3 - lo3));
-    if (bad || nmax > C::kMaxRows) {
+    if (bad4 != 0 || nrows > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
     }
-    const int lo_me = g == 0 ? lo0 : g == 1 ? lo1 : g == 2 ? lo2 : lo3;
-    const int hi_me = g == 0 ? hi0 : g == 1 ? hi1 : g == 2 ? hi2 : hi3;
-    if (lane == 0) rec[nrd] = 0u;
-    // ---- tumor column counts and margin sums (16-bit pairs, loci 2k, 2k + 1 in msum[k])
+    // ---- tumor column counts (bytes, widened into 16-bit pairs every 240 rows and at the end)
+    //      and margin sums (exact 16-bit pairs over one batch of four rows, loci 2k, 2k + 1 in
+    //      msum[k], folded into 32 bits per locus after each batch): row k is one 512-byte load
+    //      of base codes and one 1 KiB load of margin terms
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
-    uint32_t msum[4] = {0, 0, 0, 0};
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(RT.proj + 8 * sb0), (short)0, (int)(8 * (sb4 - sb0)), 0x00020000);
-    const __amdgpu_buffer_rsrc_t msrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(mproj + 8 * sb0), (short)0, (int)(16 * (sb4 - sb0)), 0x00020000);
-    uint32_t off = gb;  // this group's slice run + the words of its earlier reads there
+    uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
+    int32_t m32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(RT.proj + 512 * row0), (short)0, 512 * nrows, 0x00020000);
+    const __amdgpu_buffer_rsrc_t msrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 512 * row0), (short)0, 1024 * nrows, 0x00020000);
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -264,36 +247,48 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       }
       nn = 0;
     };
-    auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {
-      uint32_t rv[U];
+    auto widen = [&]() {
+      auto w2 = [](uint32_t (&w)[4], uint32_t (&c)[2]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) rv[u] = rec[min(lo_me + k0 + u, hi_me)];
+        for (int h = 0; h < 2; ++h) {
+          w[2 * h] += __builtin_amdgcn_perm(0u, c[h], 0x0c010c00u);  // bytes 0, 1 -> halves
+          w[2 * h + 1] += __builtin_amdgcn_perm(0u, c[h], 0x0c030c02u);
+          c[h] = 0;
+        }
+      };
+      w2(wA, ca);
+      w2(wC, cc);
+      w2(wT, ct);
+      w2(wG, cg);
+    };
+    auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {  // rows k0 .. k0 + U - 1
+      const uint32_t va = 8u * (uint32_t)lane + 512u * (uint32_t)k0, vm = 2u * va;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int32_t c0 = (int32_t)(int16_t)(rv[u] & 0xFFFFu);
-        const int32_t s0 = max(c0, g16), se = min(c0 + (int32_t)(rv[u] >> 16), g16 + 16);
-        const uint32_t sl = (uint32_t)max(se - s0, 0);
-        const uint32_t d = (uint32_t)(lane - s0);
-        const uint32_t voff = d < sl ? 8u * (off + d) : 0x80000000u;
-        off += sl;
-        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)voff, 0, 0);
-        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(voff == 0x80000000u ? voff : 2 * voff), 0, 0);
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(va + 512u * u), 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(vm + 1024u * u), 0, 0);
         w[u] = make_uint2(a[0], a[1]);
         m[u] = make_uint4(b[0], b[1], b[2], b[3]);
       }
     };
     auto count = [&](const uint2 (&w)[U], const uint4 (&m)[U]) {
       if (nn + U > 15) fold();
+      uint32_t msum[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].x);
         ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].x);
         nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].y);
         ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].y);
-        msum[0] = add_sat2(msum[0], m[u].x);
+        msum[0] = add_sat2(msum[0], m[u].x);  // exact: four terms >= -8191
         msum[1] = add_sat2(msum[1], m[u].y);
         msum[2] = add_sat2(msum[2], m[u].z);
         msum[3] = add_sat2(msum[3], m[u].w);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        m32[2 * q] += (int32_t)(int16_t)(msum[q] & 0xFFFFu);
+        m32[2 * q + 1] += (int32_t)msum[q] >> 16;
       }
       nn += U;
     };
@@ -313,8 +308,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t mm = p.y & 15u, c = (p.y >> 4) & 7u;
         if (mm) atomicOr(&mk[l - B0], mm);
-        if (c < 4) atomicAdd(&ev[l - B0], 1u << (8 * c));
-        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 8);
+        if (c < 4) atomicAdd(&ev[2 * (l - B0) + (c >> 1)], 1u << (16 * (c & 1)));
+        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
       }
     };
 #pragma unroll
@@ -334,25 +329,34 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
         }
       }
     }
-    for (int k0 = 0;; k0 += 2 * U) {  // rows past the group's are clamped (zero words)
+    for (int k0 = 0, since = 0;; k0 += 2 * U) {  // rows past the block's read 0 (out of the buffers' range)
       issue(k0 + U, bw, bm);
       count(aw, am);
       issue(k0 + 2 * U, aw, am);
       count(bw, bm);
-      if (k0 + 2 * U >= nmax) break;
+      if (k0 + 2 * U >= nrows) break;
+      since += 2 * U;
+      if (since == 240) {  // uniform: bytes hold 240 rows at most
+        fold();
+        widen();
+        since = 0;
+      }
     }
     fold();
+    widen();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // ---- decision: candidate loci (somatic_tile's test)
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
-    uint32_t e8[8], m8[8], v8[8];
+    uint32_t e16[16], m8[8], v8[8];
     {
-      const uint4 ea = e4[0], eb = e4[1], ma = m4[0], mb = m4[1], va = c4[0], vb = c4[1];
-      e8[0] = ea.x, e8[1] = ea.y, e8[2] = ea.z, e8[3] = ea.w, e8[4] = eb.x, e8[5] = eb.y, e8[6] = eb.z, e8[7] = eb.w;
+      const uint4 ea = e4[0], eb = e4[1], ec = e4[2], ed = e4[3], ma = m4[0], mb = m4[1], va = c4[0], vb = c4[1];
+      e16[0] = ea.x, e16[1] = ea.y, e16[2] = ea.z, e16[3] = ea.w, e16[4] = eb.x, e16[5] = eb.y, e16[6] = eb.z;
+      e16[7] = eb.w, e16[8] = ec.x, e16[9] = ec.y, e16[10] = ec.z, e16[11] = ec.w, e16[12] = ed.x, e16[13] = ed.y;
+      e16[14] = ed.z, e16[15] = ed.w;
       m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
       v8[0] = va.x, v8[1] = va.y, v8[2] = va.z, v8[3] = va.w, v8[4] = vb.x, v8[5] = vb.y, v8[6] = vb.z, v8[7] = vb.w;
-      e4[0] = e4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+      e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
     }
     int32_t run_c = 0, run_n = 0;
 #pragma unroll
@@ -369,17 +373,17 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     for (int j = 0; j < 8; ++j) {
       const int32_t l = B0 + 8 * lane + j;
       const bool in = l >= L0 && l < L1;
-      const int h = j >> 2, sh = 8 * (j & 3);
-      const uint32_t cA = (ca[h] >> sh) & 0xFFu, cC = (cc[h] >> sh) & 0xFFu;
-      const uint32_t cT = (ct[h] >> sh) & 0xFFu, cG = (cg[h] >> sh) & 0xFFu;
-      const uint32_t nN = (m8[j] >> 8) & 0xFFu;
+      const int q2 = j >> 1, sh = 16 * (j & 1);
+      const uint32_t cA = (wA[q2] >> sh) & 0xFFFFu, cC = (wC[q2] >> sh) & 0xFFFFu;
+      const uint32_t cT = (wT[q2] >> sh) & 0xFFFFu, cG = (wG[q2] >> sh) & 0xFFFFu;
+      const uint32_t nN = (m8[j] >> 4) & 0xFFFu;
       ncx_run += (int32_t)m8[j] >> 16;
       dn_run += (int32_t)v8[j];
       const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
       const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-      const uint32_t ew = e8[j];
-      const uint32_t mask = (m8[j] & 15u) | (cA > (ew & 0xFFu) ? 1u : 0u) | (cC > ((ew >> 8) & 0xFFu) ? 2u : 0u) |
-                            (cT > ((ew >> 16) & 0xFFu) ? 4u : 0u) | (cG > (ew >> 24) ? 8u : 0u);
+      const uint32_t eac = e16[2 * j], etg = e16[2 * j + 1];
+      const uint32_t mask = (m8[j] & 15u) | (cA > (eac & 0xFFFFu) ? 1u : 0u) | (cC > (eac >> 16) ? 2u : 0u) |
+                            (cT > (etg & 0xFFFFu) ? 4u : 0u) | (cG > (etg >> 16) ? 8u : 0u);
       const uint32_t low = mask & (0u - mask);
       const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
                              nN * (low == 0u ? 1u : 0u);
@@ -387,8 +391,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       if constexpr (kRef) agree = ref_agrees(mask, ((j < 4 ? fb8.x : fb8.y) >> (8 * (j & 3))) & 0xFFu);
       const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
       const bool nonmatch = !agree || (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
-      const int16_t m16 = (int16_t)((msum[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
-      const bool bound = !no_bound && agree && single && ncx == 0 && nN == 0 && (float)m16 * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
+      const bool bound = !no_bound && !nb && agree && single && ncx == 0 && nN == 0 &&
+                         (float)m32[j] * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
       const bool tcand = depth > 0 && nonmatch && !bound;
       visited += (in && (depth > 0 || dn_run > 0)) ? 1u : 0u;
       const bool q = in && tcand && dn_run > 0;

@@ -99,7 +99,7 @@ class gq_timings(C.Structure):
 
 
 class gq_reads_info(C.Structure):
-    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_pieces")] + [
+    _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_rows")] + [
         ("h2d_ms", C.c_float), ("derive_ms", C.c_float)]
 
 
@@ -141,7 +141,8 @@ class gq_somatic_calls(C.Structure):
                 ("alt_off", C.POINTER(C.c_int64)), ("alt_len", C.POINTER(C.c_int32)),
                 ("allele_pool", C.POINTER(C.c_uint8)), ("pool_len", C.c_int64), ("log_odds", C.POINTER(C.c_double)),
                 ("gq", C.POINTER(C.c_int32)), ("tumor", C.POINTER(gq_evidence)), ("normal", C.POINTER(gq_evidence)),
-                ("flags", C.POINTER(C.c_uint8)), ("visited_loci", C.c_int64), ("candidate_loci", C.c_int64)]
+                ("flags", C.POINTER(C.c_uint8)), ("visited_loci", C.c_int64), ("candidate_loci", C.c_int64),
+                ("block_", C.c_void_p)]
 
 
 EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
@@ -321,10 +322,7 @@ class Context:
         else:
             _check(lib().gq_somatic_standard_ref(self.h, tumor.h, normal.h, C.byref(L), reference.h, C.byref(ps),
                                                  C.byref(out)))
-        try:
-            return SomaticCalls.from_struct(out.contents)
-        finally:
-            lib().gq_free_somatic(out)
+        return SomaticCalls.from_result(out)
 
     def variant_support(self, reads: "DeviceReads", loci) -> List[tuple]:
         """gq_variant_support: rows (sample index, contig index, locus, ref, alt, count, flags)."""
@@ -355,10 +353,7 @@ class Context:
         ps = gq_germline_std_params(**{k: int(v) for k, v in p.items()})
         out = C.POINTER(gq_somatic_calls)()
         _check(lib().gq_germline_standard(self.h, reads.h, C.byref(L), C.byref(ps), C.byref(out)))
-        try:
-            return SomaticCalls.from_struct(out.contents)
-        finally:
-            lib().gq_free_somatic(out)
+        return SomaticCalls.from_result(out)
 
     def vaf_histogram(self, reads: "DeviceReads", loci, bins: int = 20, min_read_depth: int = 0,
                       min_vaf: int = 0) -> Dict[str, object]:
@@ -543,15 +538,41 @@ class SomaticCalls:
         self.cols, self.pool, self.visited_loci, self.candidate_loci = cols, pool, visited, candidates
         self._rows: Optional[List[dict]] = None
 
+    COLUMNS = ("contig", "pos", "sample", "ref_off", "ref_len", "alt_off", "alt_len", "log_odds", "gq", "tumor",
+               "normal", "flags")
+
     @staticmethod
-    def from_struct(c: gq_somatic_calls) -> "SomaticCalls":
+    def from_result(ptr) -> "SomaticCalls":
+        """Zero-copy numpy views over the result block (gq_somatic_calls.block_), kept alive by a
+        ctypes buffer whose finalizer calls gq_free_somatic; results without a block are copied
+        and freed at once."""
+        import weakref
+
+        c = ptr.contents
+        n = int(c.n)
+        pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
+        if n == 0 or not c.block_:
+            try:
+                return SomaticCalls.from_struct(c, pool)
+            finally:
+                lib().gq_free_somatic(ptr)
+        types = {k: getattr(c, k)._type_ for k in SomaticCalls.COLUMNS}
+        ends = [C.cast(getattr(c, k), C.c_void_p).value + n * C.sizeof(types[k]) for k in SomaticCalls.COLUMNS]
+        buf = (C.c_uint8 * (max(ends) - c.block_)).from_address(c.block_)
+        weakref.finalize(buf, lib().gq_free_somatic, ptr)
+        cols = {}
+        for k in SomaticCalls.COLUMNS:
+            dt = np.dtype(_EVIDENCE_DTYPE) if types[k] is gq_evidence else np.dtype(types[k])
+            cols[k] = np.frombuffer(buf, dtype=dt, count=n, offset=C.cast(getattr(c, k), C.c_void_p).value - c.block_)
+        return SomaticCalls(cols, pool, int(c.visited_loci), int(c.candidate_loci))
+
+    @staticmethod
+    def from_struct(c: gq_somatic_calls, pool: bytes) -> "SomaticCalls":
         n = int(c.n)
 
         def col(ptr):
             return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0)
-        cols = {k: col(getattr(c, k)) for k in ("contig", "pos", "sample", "ref_off", "ref_len", "alt_off", "alt_len",
-                                                "log_odds", "gq", "tumor", "normal", "flags")}
-        pool = C.string_at(c.allele_pool, c.pool_len) if c.pool_len else b""
+        cols = {k: col(getattr(c, k)) for k in SomaticCalls.COLUMNS}
         return SomaticCalls(cols, pool, int(c.visited_loci), int(c.candidate_loci))
 
     @property

@@ -195,7 +195,7 @@ void gq_reads_free(gq_dev_reads *r);
 /* projection pool and its sparse entries): for measurement and capacity planning.             */
 typedef struct gq_reads_info {
   int64_t n_reads, seq_bytes, proj_bytes, pev_count, proj_reads;  /* proj_reads: reads the projection takes */
-  int64_t n_pieces;  /* germline_proj piece records (4 bytes each) */
+  int64_t n_rows;    /* projection rows (512 bytes each: proj_bytes = 512 n_rows) */
   float h2d_ms;      /* gq_reads_upload: host wall time of the copies (pinned staging, PCIe) */
   float derive_ms;   /* gq_reads_upload / wrap: the upload-time derivation on the device    */
 } gq_reads_info;
@@ -264,6 +264,7 @@ typedef struct {
   uint8_t *flags;
   int64_t visited_loci;
   int64_t candidate_loci;    /* loci that reached the likelihood kernel      */
+  void *block_;              /* owner of the arrays above when non-NULL (freed by gq_free_somatic) */
 } gq_somatic_calls;
 
 gq_status gq_somatic_standard(gq_ctx *ctx, const gq_dev_reads *tumor, const gq_dev_reads *normal,

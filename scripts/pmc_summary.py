@@ -20,6 +20,7 @@ def main():
         for row in csv.DictReader(open(p)):
             k = row["Kernel_Name"]
             if re.search(kre, k):
+                k = k.replace("(anonymous namespace)::", "")
                 v[k.split("(")[0][-60:]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     rows = []
     for k, cs in v.items():

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--length", type=int, required=True)
     ap.add_argument("--depth", type=float, required=True)
     ap.add_argument("--kernel", default="germline_proj")
-    ap.add_argument("--round", default="r01")
+    ap.add_argument("--round", required=True)
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)

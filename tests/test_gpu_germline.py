@@ -202,14 +202,15 @@ def test_wrapped_device_reads_unordered_pool(gpu_ctx):
 
 
 def test_deep_panel_500x_germline(gpu_ctx):
-    """BASELINE configs[4] depth (500x, a targeted-panel region): deep tiles (thousands of reads
-    per tile, beyond the column kernel's stage) go through the walker; calls and per-locus
-    counts identical to the oracle."""
+    """BASELINE configs[4] depth (500x, a targeted-panel region): blocks of ~550 projection rows
+    (16-bit counts past 240 rows) stay on germline_proj, none goes to the walker; calls
+    identical to the oracle."""
     g = generate(12_000, 500.0, seed=5, indel_rate=3e-4)
     rs = g.to_read_set()
     loci = _loci(rs)
     for t in (2, 8):
         got = germline_threshold_reads(gpu_ctx, rs, loci, t)
+        assert gpu_ctx.timings()["walk_tiles"] == 0
         want = O.germline_threshold(rs, loci, t)
         assert got == want
         assert len(want) > 10

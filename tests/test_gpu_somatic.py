@@ -115,7 +115,9 @@ def test_synthetic_tumor_normal_window(gpu_ctx):
 
 def test_deep_panel_500x_tumor_normal(gpu_ctx):
     """BASELINE configs[4]: 500x tumor / 500x normal over a panel-sized region (deep-pileup LDS
-    stress; tiles of ~7000 reads per sample), every locus, three parameter sets."""
+    stress; tiles of ~7000 reads per sample), every locus, three parameter sets.  The candidate
+    pass stays on somatic_proj (~550 projection rows a block, 16-bit counts, 32-bit margin
+    sums): no tile goes to the walker."""
     L = 12_000
     tg = generate(L, 500.0, seed=20261015 + 5, somatic_rate=1e-3, tumor=True, read_seed=21)
     ng = generate(L, 500.0, seed=20261015 + 5, somatic_rate=1e-3, tumor=False, read_seed=22)
@@ -123,6 +125,7 @@ def test_deep_panel_500x_tumor_normal(gpu_ctx):
     loci = _loci(t)
     for params in (dict(apply_filters=0), dict(apply_filters=1), dict(SUITE, apply_filters=1, max_tumor_read_depth=5000)):
         got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+        assert gpu_ctx.timings()["walk_tiles"] == 0
         want = O.somatic_standard(t, n, loci, **params)
         assert_rows_match(got, want)
     assert len(want) > 0
