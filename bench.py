@@ -107,7 +107,9 @@ def main() -> int:
                          "each rank the reads overlapping its loci (DistributedUtil.scala:584-597), so N ranks "
                          "reproduce the 1-process records of the same task partition")
     ap.add_argument("--calls-out", default=None, help="rank 0 writes the gathered records (rank order) as JSON")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
+    ap.add_argument("--no-single-pass", dest="single_pass", action="store_false",
+                    help="skip the measured single pass (the shard as a BAM through the CLI)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
@@ -286,6 +288,8 @@ def main() -> int:
         e2e["single_pass_s_est"] = e2e["ingest_s_est"] + (upload_ms + host_ms_step) / 1e3
         e2e["single_pass_loci_per_s_est"] = visited / e2e["single_pass_s_est"]
         line["end_to_end"] = e2e
+    if rank == 0 and world == 1 and n_parts == 1 and args.single_pass:
+        line["end_to_end"]["single_pass"] = single_pass(g, visited)
     if rank == 0 and world == 1 and n_parts == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], line["parity_window"] = cpu_baseline(g, ctx, reads, args)
     if dist is not None:
@@ -318,6 +322,40 @@ def write_calls(args, calls, g, gather_dev, world: int, rank: int):
         rows = calls.to_host().tuples(g.contig_names)
     with open(args.calls_out, "w") as fh:
         json.dump([list(x) for x in rows], fh)
+
+
+def single_pass(g, visited: int):
+    """Measured single pass on configs[1]: the shard's reads written as a BGZF level-6 BAM
+    (native writer), then `python -m guacamole_amd germline-threshold --reads X.bam --out Y.vcf`
+    timed in a fresh process: BAM ingest with the command's filters, loci partitioning (the CLI
+    defaults), upload + derivation, the call, the VCF writer (stage wall times from GQ_TIMING)."""
+    import shutil
+    import subprocess
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    bam = os.path.join(tmp, "gq_single_pass_%d.bam" % os.getpid())
+    out = os.path.join(tmp, "gq_single_pass_%d.vcf" % os.getpid())
+    try:
+        t = time.perf_counter()
+        g.write_bam(bam)
+        write_s = time.perf_counter() - t
+        env = dict(os.environ, GQ_TIMING="1", PYTHONPATH=ROOT)
+        cmd = [sys.executable, "-m", "guacamole_amd", "germline-threshold", "--reads", bam, "--out", out]
+        t = time.perf_counter()
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t
+        if r.returncode != 0:
+            return {"error": r.stderr[-2000:]}
+        stages = {}
+        for ln in r.stderr.splitlines():
+            if ln.startswith("GQ_TIMING "):
+                stages = json.loads(ln[len("GQ_TIMING "):])
+        return {"wall_s": wall, "loci_per_s": visited / wall, "bam_bytes": os.path.getsize(bam),
+                "bam_write_s": write_s, "stages_s": stages,
+                "command": "python -m guacamole_amd germline-threshold --reads <shard>.bam --out <out>.vcf"}
+    finally:
+        if os.path.exists(bam):
+            os.remove(bam)
+        shutil.rmtree(out, ignore_errors=True)
 
 
 def ingest_rate(depth: float):

@@ -46,6 +46,27 @@ def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
     return d
 
 
+class StageClock:
+    """Wall time per stage of a command (GQ_TIMING=1: one JSON line on stderr at the end)."""
+
+    def __init__(self):
+        import os
+        import time
+        self.on = os.environ.get("GQ_TIMING") == "1"
+        self.t = time.perf_counter
+        self.t0 = self.last = self.t()
+        self.stages: Dict[str, float] = {}
+
+    def mark(self, name: str) -> None:
+        now = self.t()
+        self.stages[name] = self.stages.get(name, 0.0) + (now - self.last)
+        self.last = now
+
+    def report(self, **extra) -> None:
+        if self.on:
+            print("GQ_TIMING " + json.dumps(dict(self.stages, total_s=self.t() - self.t0, **extra)), file=sys.stderr)
+
+
 def task_count(parallelism: int, world: int = 1) -> int:
     """`--parallelism` or, at 0, Spark's sc.defaultParallelism (DistributedUtil.scala:59).  The
     default parallelism of a Spark job is the number of its workers' cores; here it is the
@@ -187,6 +208,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     p.add_argument("--emit-no-call", action="store_true", help="Output no call calls.")
     _common_args(p)
     args = p.parse_args(argv)
+    clock = StageClock()
     check_output_path(args.out)
     rank, world, local, gdev = init_from_env()
     builder = _loci_builder(args)
@@ -195,10 +217,15 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True),
                     recompute_md=args.recompute_md_tags,
                     contig_lengths_from_dictionary=not args.no_sequence_dictionary)
+    clock.mark("load_reads")
     loci = builder.result(rs.contig_lengths_map)
     parts = partition(loci, args.parallelism, args.partition_accuracy, rs, world=world)
     flat = flatten_partitions(parts, rs.contig_index())
+    clock.mark("partition")
     ctx = native.Context(local if world > 1 else args.device)
+    if world == 1:
+        device_reads(ctx, rs)
+        clock.mark("upload")
     if world > 1:
         rr = assign_tasks_to_ranks(flat, world, [rs], len(rs.contig_names))
         mine_rs, mine = rank_share(rs, flat, rr, rank)
@@ -210,11 +237,14 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
         rows = [t for c in per_rank for t in c.tuples(rs.contig_names)]
     else:
         rows = germline_threshold_reads(ctx, rs, flat, args.threshold, args.emit_ref, args.emit_no_call)
+    clock.mark("call")
     from .output import germline_genotype
     out = [germline_genotype(c, l, rs.sample_names[s] if s < len(rs.sample_names) else "default", gt, ref, alt)
            for c, l, s, gt, ref, alt, fl in rows]
     _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
+    clock.mark("write")
     print("Called %d genotypes." % len(out), file=sys.stderr)
+    clock.report(reads=int(rs.n), genotypes=len(out), loci=int(loci.count))
     return _finish_rank(0)
 
 

@@ -1,27 +1,28 @@
 // gq_germline_proj.h — germline_proj: the germline-threshold pileup kernel over the read
-// projections derived at upload (proj, pieces, pev: gq_pileup.hip proj_fill / piece_fill /
+// projections derived at upload (proj rows, pev: gq_pileup.hip row_count / proj_fill /
 // pev_fill).
 //
 // One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
 // (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
-// block B0, and the block's projection rows (ProjRec: 64 words each, word l = column l, the
-// reads packed into rows by interval partitioning) are read one row per load, 512 contiguous
-// bytes per wave, with no per-row address arithmetic:
+// block B0, and lanes 16g .. 16g + 15 own slice g's projection rows (ProjRec: 16 words each,
+// word c = column c of the slice, the reads packed into rows by interval partitioning), one
+// 128-byte row per group and load, no per-row address arithmetic beyond the slice's bound:
 //
-//     w    = buffer_load_b64(row k of the block, lane l)          (rows past the block's: 0)
+//     w    = buffer_load_b64(row k of slice g, lane l16)          (rows past the slice's: 0)
 //     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
 //     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
 //
 // (the projection holds base codes A 1, C 3, T 4, G 7 and 0 where the read has no
 // Match/Mismatch element, so neither the read's ends nor its deletions need a mask).  Counts
-// are SWAR nibbles folded into byte counters every 15 rows, in registers.  The sparse rest —
+// are SWAR nibbles folded into byte counters every 12 rows and into 16-bit pairs every 240, in
+// registers (so 500x blocks stay here).  The sparse rest —
 // MD mismatch events (PileupElement.scala:108-118, Pileup.scala:157-165: the MD-derived
 // reference base), N bases, complex ranges (insertion / deletion anchors, mid-deletions,
-// N-skips) — comes from the tile's pev entries, one lane per entry, into two LDS words per
+// N-skips) — comes from the tile's pev entries, one lane per entry, into three LDS words per
 // locus.  Then each lane makes the GermlineThreshold decision (GermlineThresholdCaller.scala:
 // 90-179) for its eight loci; variant candidates, Ref/NoCall records and complex items leave
-// as in germline_decide.  Blocks a read the projection cannot take overlaps (pbad), or with
-// more than 255 rows (byte counters), go to germline_walk.
+// as in germline_decide.  Blocks a read the projection cannot take overlaps (pbad: also slices
+// past kSliceRowsMax rows) go to germline_walk.
 #pragma once
 
 #include "gq_kernels.h"
@@ -65,8 +66,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // 2 skip the sparse entries, 4 skip the decision
   using C = ProjCfg;
   constexpr int T = C::kT, U = C::kU;
-  // per locus: event read bases (2 words: A | C << 16, T | G << 16); MD bits 0-3 | N << 4 |
-  // complex diff << 16
+  // per locus: event read bases (A | C << 16 at [i], T | G << 16 at [T + i]); MD bits 0-3 |
+  // N << 4 | complex diff << 16
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ unsigned outn[2];
@@ -74,8 +75,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave];
   {
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const uint32_t rec = next_rec;
     if (i + C::kWaves < i1) next_rec = fetch(i + C::kWaves);
     // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8; TileX from dw 16: row0 16-17,
-    // nrows 18, pbad4 19, e0 20-21, e1 22-23
+    // nr[4] 18-21, pbad4 22, e0 24-25, e1 26-27
     const int32_t L0 = (int32_t)f32(rec, 7), L1 = (int32_t)f32(rec, 8);
     const int64_t rb = f64(rec, 2), re = f64(rec, 4);
     const int32_t B0 = L0 & ~(T - 1);
@@ -116,9 +117,14 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     //      lane of the window's reads and the first rows, loaded together.  A pbad slice (a read
     //      the projection cannot take) or more than kMaxRows rows: the walker.
     const int64_t row0 = f64(rec, 16);
-    const int32_t nrows = (int32_t)f32(rec, 18);
-    const uint32_t bad4 = f32(rec, 19);
-    const int64_t e0 = f64(rec, 20), e1 = f64(rec, 22);
+    const int32_t nr0 = (int32_t)f32(rec, 18), nr1 = (int32_t)f32(rec, 19), nr2 = (int32_t)f32(rec, 20),
+                  nr3 = (int32_t)f32(rec, 21);
+    const int32_t nrows = max(max(nr0, nr1), max(nr2, nr3));  // the block's fullest slice
+    const uint32_t bad4 = f32(rec, 22);
+    const int64_t e0 = f64(rec, 24), e1 = f64(rec, 26);
+    // this group's slice: its first row (from the block's) and its rows
+    const int32_t gbase = g == 0 ? 0 : g == 1 ? nr0 : g == 2 ? nr0 + nr1 : nr0 + nr1 + nr2;
+    const int32_t gn = g == 0 ? nr0 : g == 1 ? nr1 : g == 2 ? nr2 : nr3;
     if (bad4 != 0 || nrows > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
@@ -134,13 +140,14 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]),
     //      widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 rows and at the end.
-    //      Row k: one 512-byte load at lane offset 8 lane + 512 k (rows past the block's fall
-    //      out of the buffer's range and read 0; dbg & 1, diagnostics: every load).  Three
-    //      batches of loads stay in flight while a fourth is counted.
+    //      Row k of each group's slice: one 128-byte load per group at lane offset 8 l16 + 128
+    //      (gbase + k); a group past its slice's rows loads at an out-of-range offset and reads
+    //      0 (no bytes move; dbg & 1, diagnostics: every load).  Three batches of loads stay in
+    //      flight while a fourth is counted.
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(proj + 512 * row0), (short)0, (dbg & 1) ? 0 : 512 * nrows, 0x00020000);
+        (void *)(proj + 128 * row0), (short)0, (dbg & 1) ? 0 : 128 * (nr0 + nr1 + nr2 + nr3), 0x00020000);
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -168,12 +175,16 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       w2(wT, ct);
       w2(wG, cg);
     };
-    const uint32_t vl = 8u * (uint32_t)lane;
+    const uint32_t vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
     auto issue = [&](int32_t k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {  // rows k0 .. k0 + U - 1
-      const uint32_t vb = vl + 512u * (uint32_t)k0;
+      const uint32_t vb = vl + 128u * (uint32_t)k0;
+      const int32_t rem = gn - k0;  // this group's rows left
+      // row k0 + u: the lane offset, or an out-of-range one past the slice's rows; + 128 u in
+      // the scalar offset (in range whenever the lane offset is)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(vb + 512u * u), 0, 0);
+        const uint32_t v = u < rem ? vb : 0x80000000u;
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)v, 128 * u, 0);
         w0[u] = w[0];
         w1[u] = w[1];
       }
@@ -206,7 +217,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
         if (m) atomicOr(&mk[l - B0], m);
-        if (c < 4) atomicAdd(&ev[2 * (l - B0) + (c >> 1)], 1u << (16 * (c & 1)));
+        if (c < 4) atomicAdd(&ev[(c >> 1) * T + (l - B0)], 1u << (16 * (c & 1)));
         else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
       }
     };
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     widen();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     uint32_t kinds = 0, nrec = 0, ncpx = 0;
     // locus j's 16-bit count of base w (a dynamic j selects among four registers)
     auto cnt16 = [](const uint32_t (&w)[4], int j) {
@@ -259,7 +270,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     if (!(dbg & 4)) {
       uint32_t e16[16], m8[8];
       {
-        const uint4 ea = e4[0], eb = e4[1], ec = e4[2], ed = e4[3], ma = m4[0], mb = m4[1];
+        const uint4 ea = e4[0], eb = e4[1], ec = f4[0], ed = f4[1], ma = m4[0], mb = m4[1];
         e16[0] = ea.x, e16[1] = ea.y, e16[2] = ea.z, e16[3] = ea.w, e16[4] = eb.x, e16[5] = eb.y, e16[6] = eb.z;
         e16[7] = eb.w, e16[8] = ec.x, e16[9] = ec.y, e16[10] = ec.z, e16[11] = ec.w, e16[12] = ed.x, e16[13] = ed.y;
         e16[14] = ed.z, e16[15] = ed.w;
@@ -281,7 +292,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         ncx_run += (int32_t)m8[j] >> 16;
         const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
         const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-        const uint32_t mask = ref_mask(m8[j], e16[2 * j], e16[2 * j + 1], cA, cC, cT, cG);
+        const uint32_t mask = ref_mask(m8[j], e16[j], e16[8 + j], cA, cC, cT, cG);
         // branch-free (0/1 integers): the common hom-ref locus writes nothing
         const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
         const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
@@ -325,7 +336,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
         const uint32_t mw = mk[8 * lane + j];
         const uint32_t nN = (mw >> 4) & 0xFFFu;
-        const uint32_t mask = ref_mask(mw, ev[16 * lane + 2 * j], ev[16 * lane + 2 * j + 1], cA, cC, cT, cG);
+        const uint32_t mask = ref_mask(mw, ev[8 * lane + j], ev[T + 8 * lane + j], cA, cC, cT, cG);
         const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
         const uint64_t ord = (uint64_t)(f64(rec, 0) + (pos - L0));
         CallRec rr;
@@ -360,7 +371,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         }
       }
     }
-    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
+    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
     if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup, first loads, entries, counting, decision
       const uint64_t t_f = __builtin_readcyclecounter();
       clk[0] += t_b - t_a;

@@ -402,6 +402,7 @@ struct gq_ctx {
   int n_cu = 0;
   int proj_wg_per_cu = 0;  // resident germline_proj workgroups per CU (occupancy query, once)
   int som_wg_per_cu = 0;   // resident somatic_proj workgroups per CU
+  int call_wg_per_cu = 0;  // resident somatic_call_k<false> workgroups per CU
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)

@@ -56,7 +56,7 @@ struct DevReads {
   const struct ProjRec *prec;   // n_reads + 1 (the last: a zero record)
   const uint8_t *proj;          // base codes, 8 loci per word, in block rows (see ProjRec)
   const int64_t *qoff;          // n_contigs + 1: each contig's first slice (slice = 128 loci)
-  const int64_t *brow;          // qoff[n_contigs] / 4 + 1: each 512-locus block's first row in proj
+  const int64_t *srow;          // qoff[n_contigs] + 1: each slice's first row in proj
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
   const int64_t *pev_off;       // n_reads + 1 offsets into pev
   const uint8_t *pbad;          // per slice: 1 if a read the projection cannot take overlaps it
@@ -73,14 +73,13 @@ struct DevReads {
 // (A 1, C 3, T 4, G 7: ASCII & 7) where the element is a Match/Mismatch
 // (PileupElement.scala:68-135), 0 elsewhere (outside the read, deleted / skipped loci,
 // insertion and deletion anchors, N bases).  A PIECE is one read's run of columns inside one
-// 128-locus slice (16 columns).  The pool is in BLOCK ROWS: a 512-locus block (4 slices, 64
-// columns) owns rows [brow[b], brow[b + 1]) of 64 words (512 bytes), word l of a row = column l
-// of the block.  Each slice's pieces are packed into its rows by greedy interval partitioning
-// in read order (a piece takes the first row that is free from its first column: as few rows
-// as the slice's deepest column holds reads), and the block has as many rows as its fullest
-// slice; the words no piece covers are zero.  So a wave that owns the block reads row k with
-// one 512-byte load (lane l: word l) and no per-row address math, and the rows are fewer than
-// the pieces (a read ending in a slice shares a row with one starting there).  col1 =
+// 128-locus slice (16 columns).  The pool is in SLICE ROWS: slice q owns rows [srow[q],
+// srow[q + 1]) of 16 words (128 bytes), word c of a row = column c of the slice.  The slice's
+// pieces are packed into its rows by greedy interval partitioning in read order (a piece takes
+// the first row that is free from its first column: as few rows as the slice's deepest column
+// holds reads); the words no piece covers are zero.  So the 16 lanes that own a slice read row
+// k with one 128-byte load (lane l16: word l16), and the rows are fewer than the pieces (a read
+// ending in a slice shares a row with one starting there).  col1 =
 // kProjNone marks a read the projection path cannot take (bases other than A C G T N, no MD
 // tag, a P op ...); it has no words.
 struct ProjRec {
@@ -134,11 +133,12 @@ static_assert(sizeof(Tile) == 64, "Tile layout");
 // germline_proj holds the next tile's Tile + TileX in one VGPR (a dword per lane 0-31) while it
 // counts the current one.
 struct TileX {
-  int64_t row0;       // brow[qs / 4]: the block's first projection row
-  int32_t nrows;      // its rows
+  int64_t row0;       // srow[qs]: the block's first projection row (its first slice's)
+  int32_t nr[4];      // rows of slice qs + g
   uint32_t pbad4;     // byte g: pbad[qs + g]
+  uint32_t pad0;
   int64_t e0, e1;     // pev_off[rb], pev_off[re]: the window's sparse entries
-  int64_t pad[4];
+  int64_t pad[2];
 };
 static_assert(sizeof(TileX) == 64, "TileX layout");
 

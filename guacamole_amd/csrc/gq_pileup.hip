@@ -183,10 +183,11 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   tiles[t] = tl;
   if (tilex) {  // aligned projection tiles: germline_proj's per-tile setup, resolved here
     TileX x{};
-    if (R.brow && R.qoff && a0 > rb) {
+    if (R.srow && R.qoff && a0 > rb) {
       const int64_t qs = tl.qs;
-      x.row0 = R.brow[qs >> 2];
-      x.nrows = (int32_t)(R.brow[(qs >> 2) + 1] - x.row0);
+      x.row0 = R.srow[qs];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) x.nr[g] = (int32_t)(R.srow[qs + g + 1] - R.srow[qs + g]);
       x.e0 = R.pev_off[rb];
       x.e1 = R.pev_off[a0];
       uint32_t bad = 0;
@@ -367,7 +368,7 @@ __global__ void slice_bad(DevReads R, const ProjRec *__restrict__ prec, uint8_t 
 }
 
 // Rows of each slice (walk_slice_rows, one wave per slice); past kSliceRowsMax the slice is
-// pbad.  Then each block's rows = its fullest slice's.
+// pbad (and gets no rows).
 __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, int32_t *__restrict__ srows,
                                                  uint8_t *__restrict__ pbad) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -380,10 +381,9 @@ __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, i
     }
   }
 }
-__global__ void block_rows(int64_t n_blocks, const int32_t *__restrict__ srows, int64_t *__restrict__ brows) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > n_blocks) return;
-  brows[b] = b < n_blocks ? max(max(srows[4 * b], srows[4 * b + 1]), max(srows[4 * b + 2], srows[4 * b + 3])) : 0;
+__global__ void rows64(int64_t n, const int32_t *__restrict__ srows, int64_t *__restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q <= n) out[q] = q < n ? srows[q] : 0;
 }
 
 // Reads the projection takes, into kSpread words (summed on the host): a grid-stride count per
@@ -433,9 +433,9 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
-    const int64_t base = 64 * R.brow[slot >> 2] + 16 * (slot & 3);
+    const int64_t base = 16 * R.srow[slot];  // words
     walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
-      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + 64 * (int64_t)row + (col & 15))) = proj_word(R, r, col);
+      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + 16 * (int64_t)row + (col & 15))) = proj_word(R, r, col);
     });
   }
 }
@@ -1680,8 +1680,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     HIP_TRY(hipGetLastError());
     d->d.prec = (const ProjRec *)pr;
     // sparse-entry offsets; slices a read the projection cannot take touches (pbad); each
-    // slice's rows, each block's (its fullest slice's), the blocks' first rows (scan)
-    const int64_t n_blk = n_sl / 4;
+    // slice's rows and first row (scan)
     HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
     d->owned.push_back(pbd);
     HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
@@ -1691,8 +1690,8 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMalloc(&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
-    HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_blk + 1)));
-    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_blk + 1)));
+    HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_sl + 1)));
+    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
     d->owned.push_back(sb);
     if (n_sl > 0) {
       const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
@@ -1700,7 +1699,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
                          (uint8_t *)pbd);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(block_rows, dim3((unsigned)((n_blk + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_blk,
+    hipLaunchKernelGGL(rows64, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_sl,
                        (const int32_t *)sc, (int64_t *)br);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
@@ -1709,24 +1708,24 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, (int64_t *)ne);
     HIP_TRY(hipGetLastError());
     size_t tb = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_blk + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
     HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_blk + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
     int64_t tot[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_blk, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(tmp);
     (void)hipFree(sc);
     (void)hipFree(br);
     (void)hipFree(ne);
-    d->d.brow = (const int64_t *)sb;
+    d->d.srow = (const int64_t *)sb;
     d->d.pbad = (const uint8_t *)pbd;
     d->n_rows = tot[0];
-    // the pool: rows of 64 words, zero where no piece lies
-    const size_t pool_bytes = (size_t)512 * (size_t)tot[0] + 16;
+    // the pool: rows of 16 words, zero where no piece lies
+    const size_t pool_bytes = (size_t)128 * (size_t)tot[0] + 16;
     HIP_TRY(hipMalloc(&pj, pool_bytes));
     d->owned.push_back(pj);
     HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
@@ -1745,7 +1744,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.proj = (const uint8_t *)pj;
     d->d.pev = (const uint2 *)pe;
     d->d.pev_off = (const int64_t *)eo;
-    d->proj_bytes = 512 * tot[0];
+    d->proj_bytes = 128 * tot[0];
     d->n_slices = n_sl;
     d->pev_count = tot[1];
     if (n > 0) {  // reads the projection takes
@@ -2152,7 +2151,7 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
   pl.d_rwin = (const int32_t *)(base + o_rwin);
   pl.d_wcontig = (const int32_t *)(base + o_wc);
   // aligned 512-locus plans over projected reads carry a TileX per tile after the Tiles
-  const bool with_x = aligned && T == 512 && rd->d.brow != nullptr;
+  const bool with_x = aligned && T == 512 && rd->d.srow != nullptr;
   HIP_TRY(tiles_buf.ensure((size_t)tiles * (sizeof(Tile) + (with_x ? sizeof(TileX) : 0))));
   const int nb = (int)((tiles + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(plan_tiles, dim3(nb), dim3(kBlock), 0, c->stream, d_rc, d_rs, d_re, d_ro, d_rt, (int64_t)nr,

@@ -1542,7 +1542,17 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     // records in LDS), then the deep kernel over the deeper candidates it listed, then the
     // deep kernel again over the loci whose reference base heap order decides
     HIP_TRY(c->deep_list.ensure(deep_cap * sizeof(int64_t)));
-    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
+    // persistent: the resident workgroups, each wave over every (grid)-th candidate (a grid of
+    // many generations leaves a tail of idle SIMDs behind the last ones)
+    if (c->call_wg_per_cu <= 0) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_call_k<false>, kBlock, 0) != hipSuccess || nb <= 0)
+        nb = 3;
+      c->call_wg_per_cu = nb;
+    }
+    static const int grid_env = getenv("GQ_CALL_GRID") ? atoi(getenv("GQ_CALL_GRID")) : 0;  // A/B: 0 = resident
+    const int64_t grid_cap = grid_env > 0 ? (int64_t)grid_env : (int64_t)c->call_wg_per_cu * c->n_cu;
+    const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), grid_cap);
     hipLaunchKernelGGL(somatic_call_k<false>, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                        (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,

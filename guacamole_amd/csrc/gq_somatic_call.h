@@ -562,11 +562,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       tk = t;
     }
   };
+  // the next candidate's record is loaded one candidate ahead (it lands while this one runs)
+  auto fetch_item = [&](int64_t li, int64_t &it) -> ComplexItem {
+    it = amb_in ? amb_in[li].item : DEEP ? dio.list[li] : li;
+    return items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
+  };
+  int64_t it_next = 0;
+  ComplexItem item_next{0, 0, 0};
+  if (gwave < (int64_t)n_items) item_next = fetch_item(gwave, it_next);
   for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
     tick(-1);
     if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[5], 1ull);
-    const int64_t it = amb_in ? amb_in[li].item : DEEP ? dio.list[li] : li;
-    const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    const int64_t it = it_next;
+    const ComplexItem item = item_next;
+    if (li + nwaves_total < (int64_t)n_items) item_next = fetch_item(li + nwaves_total, it_next);
     const Tile &tt_ = tiles_t[item.tile], &tn_ = tiles_n[item.tile];
     const int32_t pos = item.pos;
     const int32_t t_contig = tt_.contig, t_L0 = tt_.L0;
@@ -887,11 +896,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     const int rl = allele_ref_len(al), alt_l = allele_alt_len(al);
     const Key128 nkey = key_from(rl, rl, 0, [&](int, int i) { return allele_byte(RT, al, pos, 0, i); });
     const int n_idx = PN.depth_f ? pile_find(PN, nkey) : -1;
+    // log-odds and the phred likelihood need no evidence (its likelihoods are tg.best_l and
+    // 1 - nvs): a candidate the driver's filters drop on them skips the evidence pass
+    const double log_odds = sm::log(odds);
+    const double lik = tg.best_l * (1.0 - nvs) - 1e-10;
+    const int gqv = success_to_phred(lik);
+    if (prm.apply_filters == 1 && (!(log_odds > (double)prm.min_lod) || !(gqv >= prm.min_likelihood))) continue;
     gq_evidence tev, nev;
     evidence_pair(PT, PN, m.el[0], nT, m.el[1], nN, t_idx, n_idx, tg.best_l, 1.0 - nvs, pos, m, tev, nev);
-    const double log_odds = sm::log(odds);
-    const int gqv = success_to_phred(tev.likelihood * nev.likelihood - 1e-10);
-    if (phred_rounding_edge(tev.likelihood * nev.likelihood - 1e-10)) knife |= GQ_FLAG_KNIFE_EDGE;
+    if (phred_rounding_edge(lik)) knife |= GQ_FLAG_KNIFE_EDGE;
     const float vaf = (float)tev.allele_read_depth / (float)tev.read_depth;
     if (prm.apply_filters == 1) {  // SomaticStandardCaller.scala:124-137 then SomaticGenotypeFilter.apply (:285-307)
       const bool depth_ok = tev.read_depth >= prm.min_tumor_read_depth && tev.read_depth < prm.max_tumor_read_depth &&

@@ -104,12 +104,12 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
-    const int64_t base = 64 * R.brow[slot >> 2] + 16 * (slot & 3);
+    const int64_t base = 16 * R.srow[slot];  // words
     bool none = false;
     walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
       if (act) {
         const uint4 w = margin_word(R, r, col, min_mapq, incl_align != 0);
-        *reinterpret_cast<uint4 *>(mproj + 8 * (base + 64 * (int64_t)row + (col & 15))) = w;
+        *reinterpret_cast<uint4 *>(mproj + 8 * (base + 16 * (int64_t)row + (col & 15))) = w;
         auto has = [](uint32_t x) {
           return (int16_t)(x & 0xFFFFu) == kMarginNone || (int16_t)(x >> 16) == kMarginNone;
         };
@@ -170,8 +170,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     int no_bound = 0) {
   using C = SomProjCfg;
   constexpr int T = C::kT, U = C::kU;
-  // per locus: tumor event read bases (2 words: A | C << 16, T | G << 16); MD bits 0-3 | N << 4 |
-  // complex diff << 16
+  // per locus: tumor event read bases (A | C << 16 at [i], T | G << 16 at [T + i]); MD bits
+  // 0-3 | N << 4 | complex diff << 16
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ __attribute__((aligned(16))) uint32_t cvw[C::kWaves][T];  // normal coverage differences
@@ -180,9 +180,9 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave], *cv = cvw[wave];
   {
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
-    e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -206,8 +206,16 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     // kMaxRows rows (byte counters): somatic_tile.
     const bool tumor = re > rb;
     const int64_t qs = tumor ? tt.qs : 0;  // qoff[contig] + (B0 >> 7), from the plan
-    const int64_t row0 = tumor ? RT.brow[qs >> 2] : 0;
-    const int32_t nrows = tumor ? (int32_t)(RT.brow[(qs >> 2) + 1] - row0) : 0;
+    const int64_t row0 = tumor ? RT.srow[qs] : 0;
+    const int32_t g = lane >> 4;
+    // this group's slice: its first row (from the block's first) and its rows; the loop runs to
+    // the block's fullest slice
+    const int32_t gbase = tumor ? (int32_t)(RT.srow[qs + g] - row0) : 0;
+    const int32_t gn = tumor ? (int32_t)(RT.srow[qs + g + 1] - RT.srow[qs + g]) : 0;
+    const int32_t ntot = tumor ? (int32_t)(RT.srow[qs + 4] - row0) : 0;
+    int32_t nrows = gn;
+#pragma unroll
+    for (int d = 16; d < 64; d <<= 1) nrows = max(nrows, __shfl_xor(nrows, d, 64));
     const uint32_t bad4 = tumor ? *reinterpret_cast<const uint32_t *>(RT.pbad + qs) : 0u;
     const bool nb = tumor && *reinterpret_cast<const uint32_t *>(mnb + qs) != 0u;  // a slice without bounds
     const int64_t e0 = RT.pev_off[rb], e1 = RT.pev_off[re];
@@ -225,15 +233,17 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     }
     // ---- tumor column counts (bytes, widened into 16-bit pairs every 240 rows and at the end)
     //      and margin sums (exact 16-bit pairs over one batch of four rows, loci 2k, 2k + 1 in
-    //      msum[k], folded into 32 bits per locus after each batch): row k is one 512-byte load
-    //      of base codes and one 1 KiB load of margin terms
+    //      msum[k], folded into 32 bits per locus after each batch): row k of each group's slice
+    //      is one 128-byte load of base codes and one 256-byte load of margin terms (past the
+    //      slice's rows: out-of-range offsets, 0)
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
     int32_t m32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(RT.proj + 512 * row0), (short)0, 512 * nrows, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(RT.proj + 128 * row0), (short)0, 128 * ntot, 0x00020000);
     const __amdgpu_buffer_rsrc_t msrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 512 * row0), (short)0, 1024 * nrows, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 128 * row0), (short)0, 256 * ntot, 0x00020000);
+    const uint32_t vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -262,11 +272,14 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       w2(wG, cg);
     };
     auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {  // rows k0 .. k0 + U - 1
-      const uint32_t va = 8u * (uint32_t)lane + 512u * (uint32_t)k0, vm = 2u * va;
+      const uint32_t va = vl + 128u * (uint32_t)k0;
+      const int32_t rem = gn - k0;  // this group's rows left
+      const uint32_t vm = 2u * va;
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(va + 512u * u), 0, 0);
-        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(vm + 1024u * u), 0, 0);
+      for (int u = 0; u < U; ++u) {  // past the slice's rows: out-of-range lane offsets
+        const bool ok = u < rem;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(ok ? va : 0x80000000u), 128 * u, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(ok ? vm : 0x80000000u), 256 * u, 0);
         w[u] = make_uint2(a[0], a[1]);
         m[u] = make_uint4(b[0], b[1], b[2], b[3]);
       }
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t mm = p.y & 15u, c = (p.y >> 4) & 7u;
         if (mm) atomicOr(&mk[l - B0], mm);
-        if (c < 4) atomicAdd(&ev[2 * (l - B0) + (c >> 1)], 1u << (16 * (c & 1)));
+        if (c < 4) atomicAdd(&ev[(c >> 1) * T + (l - B0)], 1u << (16 * (c & 1)));
         else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
       }
     };
@@ -346,17 +359,17 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     widen();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // ---- decision: candidate loci (somatic_tile's test)
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 16 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
     uint32_t e16[16], m8[8], v8[8];
     {
-      const uint4 ea = e4[0], eb = e4[1], ec = e4[2], ed = e4[3], ma = m4[0], mb = m4[1], va = c4[0], vb = c4[1];
+      const uint4 ea = e4[0], eb = e4[1], ec = f4[0], ed = f4[1], ma = m4[0], mb = m4[1], va = c4[0], vb = c4[1];
       e16[0] = ea.x, e16[1] = ea.y, e16[2] = ea.z, e16[3] = ea.w, e16[4] = eb.x, e16[5] = eb.y, e16[6] = eb.z;
       e16[7] = eb.w, e16[8] = ec.x, e16[9] = ec.y, e16[10] = ec.z, e16[11] = ec.w, e16[12] = ed.x, e16[13] = ed.y;
       e16[14] = ed.z, e16[15] = ed.w;
       m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
       v8[0] = va.x, v8[1] = va.y, v8[2] = va.z, v8[3] = va.w, v8[4] = vb.x, v8[5] = vb.y, v8[6] = vb.z, v8[7] = vb.w;
-      e4[0] = e4[1] = e4[2] = e4[3] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+      e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
     }
     int32_t run_c = 0, run_n = 0;
 #pragma unroll
@@ -381,7 +394,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       dn_run += (int32_t)v8[j];
       const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
       const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-      const uint32_t eac = e16[2 * j], etg = e16[2 * j + 1];
+      const uint32_t eac = e16[j], etg = e16[8 + j];
       const uint32_t mask = (m8[j] & 15u) | (cA > (eac & 0xFFFFu) ? 1u : 0u) | (cC > (eac >> 16) ? 2u : 0u) |
                             (cT > (etg & 0xFFFFu) ? 4u : 0u) | (cG > (etg >> 16) ? 8u : 0u);
       const uint32_t low = mask & (0u - mask);

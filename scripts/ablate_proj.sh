@@ -6,6 +6,6 @@ set -e
 OUT=$1; shift
 mkdir -p $OUT
 for A in "$@"; do
-  GQ_DBG=$A timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --somatic-length 0 --panel-length 0 > $OUT/d$A.json 2> $OUT/d$A.err || true
+  GQ_DBG=$A timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --somatic-length 0 --panel-length 0 --no-single-pass > $OUT/d$A.json 2> $OUT/d$A.err || true
   python3 -c "import json; d=json.load(open('$OUT/d$A.json')); print('dbg $A', round(d['roofline']['kernel_ms'],4))" || echo "dbg $A failed"
 done

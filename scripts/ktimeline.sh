@@ -6,7 +6,7 @@ set -e
 OUT=$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --somatic-length 0 --panel-length 0 "$@" > $OUT/bench.log 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --somatic-length 0 --panel-length 0 --no-single-pass "$@" > $OUT/bench.log 2>&1
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_trace.csv", recursive=True)[0]

@@ -7,7 +7,7 @@ OUT=$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
 for A in "$@"; do
-  GQ_DBG=$A timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "${GQ_KRE:-germline_proj}" --output-format csv -d $OUT/f$A -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --somatic-length 0 --panel-length 0 > $OUT/f$A.log 2>&1
+  GQ_DBG=$A timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "${GQ_KRE:-germline_proj}" --output-format csv -d $OUT/f$A -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --somatic-length 0 --panel-length 0 --no-single-pass > $OUT/f$A.log 2>&1
   python3 - $OUT/f$A/run_counter_collection.csv $A <<'PY'
 import csv, sys, collections
 v = collections.defaultdict(list)

@@ -54,6 +54,7 @@ def test_somatic_two_ranks_equal_one(tmp_path):
 def _bench(world, out, extra):
     env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
     args = ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "0", "--somatic-length", "0", "--panel-length", "0",
+            "--no-single-pass",
             "--no-cpu-baseline", "--shared-reads", "--calls-out", out] + extra
     if world == 1:
         cmd = [sys.executable] + args
