@@ -76,7 +76,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   uint32_t *ev = evw[wave], *mk = mkw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);
+    {  // separate stores (a chained assignment re-reads each word from LDS)
+      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4;
+    }
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -95,59 +98,151 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
   // the tile record (Tile + TileX: dword d on lane d < 32) of the wave's next tile, loaded one
   // tile ahead: its fields are in a register when the tile starts (no dependent setup rounds)
+  // (TileX array follows the Tiles: one buffer over both, lane d < 16 reads Tile dword d,
+  // lanes 16-31 TileX dword d - 16, the rest an out-of-range offset; the tile in the scalar
+  // offset.  plan sizes the arrays below 2^31 bytes.)
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)tiles, (short)0, (int)(128 * n_tiles), 0x00020000);
+  const uint32_t tvo = lane < 16 ? 4u * (uint32_t)lane
+                       : lane < 32 ? (uint32_t)(64 * n_tiles) + 4u * (uint32_t)(lane - 16)
+                                   : 0x80000000u;
   auto fetch = [&](int64_t t) -> uint32_t {
-    const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tiles + t);
-    const uint32_t *x32 = reinterpret_cast<const uint32_t *>(tilex + t);
-    return lane < 16 ? t32[lane] : lane < 32 ? x32[lane - 16] : 0u;
+    return __builtin_amdgcn_raw_buffer_load_b32(trs, (int)tvo, (int)(64 * t), 0);
   };
   auto f32 = [](uint32_t rec, int d) { return (uint32_t)__builtin_amdgcn_readlane((int)rec, d); };
   auto f64 = [&](uint32_t rec, int d) { return (int64_t)((uint64_t)f32(rec, d) | ((uint64_t)f32(rec, d + 1) << 32)); };
-  uint32_t next_rec = i0 + wave < i1 ? fetch(i0 + wave) : 0u;
-  for (int64_t i = i0 + wave; i < i1; i += C::kWaves) {
+  // A tile's row context: the buffer over its block's rows, this lane's offset in its slice's
+  // first row, and its slice's rows (gn = 0: every load of the tile reads 0).  Rows past the
+  // slice's, and (dbg & 1, diagnostics) every row, fall out of the buffer's range and read 0.
+  struct RowCtx {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t vl;
+    int32_t gn;
+  };
+  auto row_ctx = [&](uint32_t rec) -> RowCtx {
+    const int64_t row0 = f64(rec, 16);
+    const int32_t nr0 = (int32_t)f32(rec, 18), nr1 = (int32_t)f32(rec, 19), nr2 = (int32_t)f32(rec, 20),
+                  nr3 = (int32_t)f32(rec, 21);
+    // (masks, not selects: nested selects on the lane's group compile to divergent branches)
+    const int32_t gbase = (nr0 & -(int32_t)(g >= 1)) + (nr1 & -(int32_t)(g >= 2)) + (nr2 & -(int32_t)(g >= 3));
+    RowCtx x;
+    x.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(proj + 128 * row0), (short)0,
+                                               (dbg & 1) ? 0 : 128 * (nr0 + nr1 + nr2 + nr3), 0x00020000);
+    x.vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
+    x.gn = (nr0 & -(int32_t)(g == 0)) | (nr1 & -(int32_t)(g == 1)) | (nr2 & -(int32_t)(g == 2)) |
+           (nr3 & -(int32_t)(g == 3));
+    return x;
+  };
+  // the block's fullest slice, and whether the tile runs here (reads, no pbad slice, rows in range)
+  auto rec_rows = [&](uint32_t rec) {
+    return max(max((int32_t)f32(rec, 18), (int32_t)f32(rec, 19)), max((int32_t)f32(rec, 20), (int32_t)f32(rec, 21)));
+  };
+  auto rec_runs = [&](uint32_t rec) {
+    return f64(rec, 4) > f64(rec, 2) && f32(rec, 22) == 0u && rec_rows(rec) <= C::kMaxRows;
+  };
+  // rows k0 .. k0 + U - 1 of each group's slice: the lane offset, or an out-of-range one past
+  // the slice's rows; + 128 u in the scalar offset (in range whenever the lane offset is)
+  auto issue = [&](const RowCtx &x, int32_t k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
+    const uint32_t vb = x.vl + 128u * (uint32_t)k0;
+    const int32_t rem = x.gn - k0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t v = u < rem ? vb : 0x80000000u;
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(x.rsrc, (int)v, 128 * u, 0);
+      w0[u] = w[0];
+      w1[u] = w[1];
+    }
+  };
+  // Tiles are software-pipelined: the Tile + TileX records arrive two tiles ahead, and a tile's
+  // last counting round issues the NEXT tile's first three row batches, so those loads are in
+  // flight while this tile's sparse entries and decision run (no loads past the rows are
+  // issued, and nothing waits for them).  primed: rows 0 .. 3U - 1 of the tile starting now are
+  // already in a, b, c.
+  uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U], d0[U], d1[U];
+  // the first kEnt sparse entries per lane of a tile's reads (the rest: a loop), applied before
+  // its counting (the entry loads' latency overlaps the primed row batches')
+  constexpr int NE = C::kEnt;
+  auto load_ent = [&](uint2 (&ent)[NE], int64_t e0, int64_t e1) {
+    // a buffer over the window's first entries (32-bit lane offsets).  Past them the load
+    // reads 0 and the locus becomes INT_MIN, outside every block: no effect.
+    const uint32_t nb = (dbg & 2) ? 0u : 8u * (uint32_t)min(e1 - e0, (int64_t)NE * 64);
+    const __amdgpu_buffer_rsrc_t ers =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(pev + e0), (short)0, (int)nb, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const uint32_t o = 8u * (uint32_t)lane + 512u * j;
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(ers, (int)o, 0, 0);
+      ent[j] = make_uint2(w[0] | (o < nb ? 0u : 0x80000000u), w[1]);
+    }
+  };
+  bool primed = false;
+  int64_t i = i0 + wave;
+  uint32_t rec_c = i < i1 ? fetch(i) : 0u;
+  uint32_t rec_n = i + C::kWaves < i1 ? fetch(i + C::kWaves) : 0u;
+  for (; i < i1; i += C::kWaves) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    const uint32_t rec = next_rec;
-    if (i + C::kWaves < i1) next_rec = fetch(i + C::kWaves);
+    const uint32_t rec = rec_c;
+    rec_c = rec_n;
+    if (i + 2 * C::kWaves < i1) rec_n = fetch(i + 2 * C::kWaves);
+    const bool was_primed = primed;
+    primed = false;
     // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8; TileX from dw 16: row0 16-17,
     // nr[4] 18-21, pbad4 22, e0 24-25, e1 26-27
     const int32_t L0 = (int32_t)f32(rec, 7), L1 = (int32_t)f32(rec, 8);
     const int64_t rb = f64(rec, 2), re = f64(rec, 4);
     const int32_t B0 = L0 & ~(T - 1);
     if (re <= rb) continue;  // no reads: nothing visited
-    // ---- the block's rows and pbad flags (from the record), the first kEnt sparse entries per
-    //      lane of the window's reads and the first rows, loaded together.  A pbad slice (a read
-    //      the projection cannot take) or more than kMaxRows rows: the walker.
-    const int64_t row0 = f64(rec, 16);
-    const int32_t nr0 = (int32_t)f32(rec, 18), nr1 = (int32_t)f32(rec, 19), nr2 = (int32_t)f32(rec, 20),
-                  nr3 = (int32_t)f32(rec, 21);
-    const int32_t nrows = max(max(nr0, nr1), max(nr2, nr3));  // the block's fullest slice
-    const uint32_t bad4 = f32(rec, 22);
-    const int64_t e0 = f64(rec, 24), e1 = f64(rec, 26);
-    // this group's slice: its first row (from the block's) and its rows
-    const int32_t gbase = g == 0 ? 0 : g == 1 ? nr0 : g == 2 ? nr0 + nr1 : nr0 + nr1 + nr2;
-    const int32_t gn = g == 0 ? nr0 : g == 1 ? nr1 : g == 2 ? nr2 : nr3;
-    if (bad4 != 0 || nrows > C::kMaxRows) {
+    // A pbad slice (a read the projection cannot take) or more than kMaxRows rows: the walker.
+    const int32_t nrows = rec_rows(rec);
+    if (f32(rec, 22) != 0u || nrows > C::kMaxRows) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)i;
       continue;
     }
-    constexpr int NE = C::kEnt;
-    uint2 ent[NE];
-#pragma unroll
-    for (int j = 0; j < NE; ++j) {
-      const int64_t k = e0 + 64 * j + lane;
-      ent[j] = make_uint2(0x80000000u, kPevNone);
-      if (!(dbg & 2) && k < e1) ent[j] = pev[k];
+    const RowCtx cur = row_ctx(rec);
+    if (!was_primed) {
+      issue(cur, 0, a0, a1);
+      issue(cur, U, b0, b1);
+      issue(cur, 2 * U, c0, c1);
     }
+    const int64_t e0 = f64(rec, 24), e1 = f64(rec, 26);
+    uint2 ent[NE];
+    load_ent(ent, e0, e1);
     const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
+    auto apply = [&](uint2 p) {
+      const int32_t l = (int32_t)p.x;
+      if (p.y & kPevComplex) {
+        const int64_t a = max((int64_t)l, (int64_t)B0);
+        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+        if (a < b) {
+          atomicAdd(&mk[a - B0], 1u << 16);
+          if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
+        }
+      } else if (l >= B0 && l < B0 + T) {
+        const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
+        if (m) atomicOr(&mk[l - B0], m);
+        if (c < 4) atomicAdd(&ev[(c >> 1) * T + (l - B0)], 1u << (16 * (c & 1)));
+        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < NE; ++j) apply(ent[j]);
+    if (!(dbg & 2))
+      for (int64_t q = e0 + 64 * NE; q < e1; q += 64) {  // the rest (rare)
+        const int64_t k = q + lane;
+        if (k < e1) apply(pev[k]);
+      }
+    // the next tile of this wave: its first batches leave with this tile's last round
+    const bool next_ok = i + C::kWaves < i1 && rec_runs(rec_c);
+    RowCtx nxt = cur;
+    nxt.gn = 0;
+    if (next_ok) nxt = row_ctx(rec_c);
     // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]),
     //      widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 rows and at the end.
-    //      Row k of each group's slice: one 128-byte load per group at lane offset 8 l16 + 128
-    //      (gbase + k); a group past its slice's rows loads at an out-of-range offset and reads
-    //      0 (no bytes move; dbg & 1, diagnostics: every load).  Three batches of loads stay in
-    //      flight while a fourth is counted.
+    //      Row k of each group's slice: one 128-byte load per group.  Three batches of loads
+    //      stay in flight while a fourth is counted.
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(proj + 128 * row0), (short)0, (dbg & 1) ? 0 : 128 * (nr0 + nr1 + nr2 + nr3), 0x00020000);
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -175,20 +270,6 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       w2(wT, ct);
       w2(wG, cg);
     };
-    const uint32_t vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
-    auto issue = [&](int32_t k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {  // rows k0 .. k0 + U - 1
-      const uint32_t vb = vl + 128u * (uint32_t)k0;
-      const int32_t rem = gn - k0;  // this group's rows left
-      // row k0 + u: the lane offset, or an out-of-range one past the slice's rows; + 128 u in
-      // the scalar offset (in range whenever the lane offset is)
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t v = u < rem ? vb : 0x80000000u;
-        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)v, 128 * u, 0);
-        w0[u] = w[0];
-        w1[u] = w[1];
-      }
-    };
     auto count = [&](const uint32_t (&w0)[U], const uint32_t (&w1)[U]) {
       if (nn + U > 15) fold();
 #pragma unroll
@@ -200,48 +281,19 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       }
       nn += U;
     };
-    uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U], d0[U], d1[U];
-    issue(0, a0, a1);
-    issue(U, b0, b1);
-    issue(2 * U, c0, c1);
-    // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
-    auto apply = [&](uint2 p) {
-      const int32_t l = (int32_t)p.x;
-      if (p.y & kPevComplex) {
-        const int64_t a = max((int64_t)l, (int64_t)B0);
-        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
-        if (a < b) {
-          atomicAdd(&mk[a - B0], 1u << 16);
-          if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
-        }
-      } else if (l >= B0 && l < B0 + T) {
-        const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
-        if (m) atomicOr(&mk[l - B0], m);
-        if (c < 4) atomicAdd(&ev[(c >> 1) * T + (l - B0)], 1u << (16 * (c & 1)));
-        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
-      }
-    };
-    const uint64_t t_c = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-#pragma unroll
-    for (int j = 0; j < NE; ++j) apply(ent[j]);
-    if (!(dbg & 2))
-      for (int64_t q = e0 + 64 * NE; q < e1; q += 64) {  // the rest (rare)
-        const int64_t k = q + lane;
-        if (k < e1) apply(pev[k]);
-      }
-    const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // rows k0 .. k0 + 4U - 1 per iteration, three batches in flight; one exit (the rows past
-    // the block's read 0 and count nothing)
+    // rows k0 .. k0 + 4U - 1 per round; the last round (uniform) issues the next tile's rows
+    // 0 .. 3U - 1 instead of this tile's past its end
     for (int32_t k0 = 0, since = 0;; k0 += 4 * U) {
-      issue(k0 + 3 * U, d0, d1);
+      const bool last = k0 + 4 * U >= nrows;
+      issue(cur, k0 + 3 * U, d0, d1);
       count(a0, a1);
-      issue(k0 + 4 * U, a0, a1);
+      issue(last ? nxt : cur, last ? 0 : k0 + 4 * U, a0, a1);
       count(b0, b1);
-      issue(k0 + 5 * U, b0, b1);
+      issue(last ? nxt : cur, last ? U : k0 + 5 * U, b0, b1);
       count(c0, c1);
-      issue(k0 + 6 * U, c0, c1);
+      issue(last ? nxt : cur, last ? 2 * U : k0 + 6 * U, c0, c1);
       count(d0, d1);
-      if (k0 + 4 * U >= nrows) break;
+      if (last) break;
       since += 4 * U;
       if (since == 240) {  // uniform: bytes hold 240 rows at most
         fold();
@@ -249,6 +301,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         since = 0;
       }
     }
+    primed = next_ok;
+    const uint64_t t_c = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+    const uint64_t t_d = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     fold();
     widen();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
@@ -268,31 +323,38 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
              (cT > (etg & 0xFFFFu) ? 4u : 0u) | (cG > (etg >> 16) ? 8u : 0u);
     };
     if (!(dbg & 4)) {
-      uint32_t e16[16], m8[8];
-      {
-        const uint4 ea = e4[0], eb = e4[1], ec = f4[0], ed = f4[1], ma = m4[0], mb = m4[1];
-        e16[0] = ea.x, e16[1] = ea.y, e16[2] = ea.z, e16[3] = ea.w, e16[4] = eb.x, e16[5] = eb.y, e16[6] = eb.z;
-        e16[7] = eb.w, e16[8] = ec.x, e16[9] = ec.y, e16[10] = ec.z, e16[11] = ec.w, e16[12] = ed.x, e16[13] = ed.y;
-        e16[14] = ed.z, e16[15] = ed.w;
-        m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
-      }
       // complex elements per locus: prefix of the range differences over the block
       int32_t run = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) run += (int32_t)m8[j] >> 16;
+      {
+        const uint4 ma = m4[0], mb = m4[1];
+        run = ((int32_t)ma.x >> 16) + ((int32_t)ma.y >> 16) + ((int32_t)ma.z >> 16) + ((int32_t)ma.w >> 16) +
+              ((int32_t)mb.x >> 16) + ((int32_t)mb.y >> 16) + ((int32_t)mb.z >> 16) + ((int32_t)mb.w >> 16);
+      }
       int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
-      // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci:
-      //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
+      // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci
+      //      in two halves (the LDS words of four loci at a time: the next tile's row batches
+      //      are in flight in registers meanwhile): kind 0 nothing, 1 a Ref/NoCall record, 2 a
+      //      variant candidate (record pair), 3 complex
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int h = 0; h < 2; ++h) {
+        uint32_t eac[4], etg[4], m8[4];
+        {
+          const uint4 ea = e4[h], ec = f4[h], ma = m4[h];
+          eac[0] = ea.x, eac[1] = ea.y, eac[2] = ea.z, eac[3] = ea.w;
+          etg[0] = ec.x, etg[1] = ec.y, etg[2] = ec.z, etg[3] = ec.w;
+          m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * h + jj;
         const int32_t l = B0 + 8 * lane + j;
         const bool in = l >= L0 && l < L1;
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
-        const uint32_t nN = (m8[j] >> 4) & 0xFFFu;
-        ncx_run += (int32_t)m8[j] >> 16;
+        const uint32_t nN = (m8[jj] >> 4) & 0xFFFu;
+        ncx_run += (int32_t)m8[jj] >> 16;
         const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
         const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-        const uint32_t mask = ref_mask(m8[j], e16[j], e16[8 + j], cA, cC, cT, cG);
+        const uint32_t mask = ref_mask(m8[jj], eac[jj], etg[jj], cA, cC, cT, cG);
         // branch-free (0/1 integers): the common hom-ref locus writes nothing
         const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
         const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
@@ -314,6 +376,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         kinds |= kind << (2 * j);
         nrec += emit_hr + 2u * general;
         ncpx += to_complex;
+        }
       }
     }
     if (__ballot(kinds != 0) != 0) {  // rare: records / complex items to write
@@ -371,8 +434,11 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         }
       }
     }
-    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = make_uint4(0u, 0u, 0u, 0u);  // this lane's words, for the next tile
-    if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup, first loads, entries, counting, decision
+    {  // separate stores (a chained assignment re-reads each word from LDS)
+      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4;
+    }  // this lane's words, for the next tile
+    if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup + entries, counting, -, widen, decision
       const uint64_t t_f = __builtin_readcyclecounter();
       clk[0] += t_b - t_a;
       clk[1] += t_c - t_b;

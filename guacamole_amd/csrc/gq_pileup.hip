@@ -2193,6 +2193,8 @@ static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, co
                                  CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr) {
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
+  // germline_proj reads the Tile + TileX arrays through one buffer of 128 B per tile
+  if (tiles >= (int64_t)1 << 24) return set_err(GQ_E_ARG, "%lld tiles in one call (at most 2^24)", (long long)tiles);
   hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
                      (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.proj,
                      R.pev, R.n_samples,
@@ -2382,7 +2384,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
             (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
   if ((gq_dbg() & 16) && hc.prof[5])
     fprintf(stderr,
-            "gq prof (cycles/tile/wave): setup %.0f first-loads %.0f entries %.0f counting %.0f decision %.0f (%llu)\n",
+            "gq prof (cycles/tile/wave): setup+entries %.0f counting %.0f - %.0f widen %.0f decision %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
             (double)hc.prof[3] / hc.prof[5], (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
   for (int k = 0; k < kSpread; ++k) {

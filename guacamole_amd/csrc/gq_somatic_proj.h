@@ -182,7 +182,10 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
           *c4 = reinterpret_cast<uint4 *>(cv + 8 * lane);
-    e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+    {  // separate stores (a chained assignment re-reads each word from LDS)
+      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4; c4[0] = z4; c4[1] = z4;
+    }
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
@@ -369,7 +372,10 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       e16[14] = ed.z, e16[15] = ed.w;
       m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w, m8[4] = mb.x, m8[5] = mb.y, m8[6] = mb.z, m8[7] = mb.w;
       v8[0] = va.x, v8[1] = va.y, v8[2] = va.z, v8[3] = va.w, v8[4] = vb.x, v8[5] = vb.y, v8[6] = vb.z, v8[7] = vb.w;
-      e4[0] = e4[1] = f4[0] = f4[1] = m4[0] = m4[1] = c4[0] = c4[1] = make_uint4(0u, 0u, 0u, 0u);
+      {  // separate stores (a chained assignment re-reads each word from LDS)
+        const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+        e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4; c4[0] = z4; c4[1] = z4;
+      }
     }
     int32_t run_c = 0, run_n = 0;
 #pragma unroll
