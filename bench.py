@@ -223,7 +223,7 @@ def main() -> int:
     #      base, 16 B of metadata per read, 4 B per CIGAR op and per MD event, 32 B per record
     #      and 12 B per queued locus written.  Its share is the tiles it kept (walk_tiles go to
     #      the walker).  The bytes it actually reads are reported beside it (`read_bytes`: the
-    #      8-locus-aligned projection, 4-B piece records, 8-B sparse entries).
+    #      projection rows of 4-bit codes, 8-B sparse entries).
     st = ctx.proj_stats(reads)
     a = g.arrays
     n_reads = int(a["start"].shape[0])
@@ -465,7 +465,8 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
     b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
              + 8 * ng.n)
     st = ctx.proj_stats(t)
-    read_bytes = 3 * int(st["proj_bytes"]) + 8 * int(st["pev_count"]) + 8 * ng.n
+    # tumor rows: 4-bit codes (proj_bytes) + 16-bit margin terms (4 x proj_bytes)
+    read_bytes = 5 * int(st["proj_bytes"]) + 8 * int(st["pev_count"]) + 8 * ng.n
     k_ms = float(np.mean(stages["pileup_ms"]))
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)

@@ -5,12 +5,14 @@
 // One WAVE per 512-locus tile, no workgroup barriers: tiles are aligned to 512-locus blocks
 // (plan(..., aligned)), so lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8) of its tile's
 // block B0, and lanes 16g .. 16g + 15 own slice g's projection rows (ProjRec: 16 words each,
-// word c = column c of the slice, the reads packed into rows by interval partitioning), one
-// 128-byte row per group and load, no per-row address arithmetic beyond the slice's bound:
+// word c = column c of the slice as eight 4-bit codes, the reads packed into rows by interval
+// partitioning), one 64-byte row per group and load, no per-row address arithmetic beyond the
+// slice's bound:
 //
-//     w    = buffer_load_b64(row k of slice g, lane l16)          (rows past the slice's: 0)
-//     nac += perm(0, 0x10000100, w.x | w.y)               A -> 0x01, C -> 0x10 per byte
-//     ntg += perm(0x10000001, 0, w.x | w.y)               T -> 0x01, G -> 0x10 per byte
+//     w    = buffer_load_b32(row k of slice g, lane l16)          (rows past the slice's: 0)
+//     lo, hi = w & 0x0F0F0F0F, (w >> 4) & 0x0F0F0F0F      loci 0-3, 4-7 as byte codes
+//     nac += perm(0, 0x10000100, lo | hi)                 A -> 0x01, C -> 0x10 per byte
+//     ntg += perm(0x10000001, 0, lo | hi)                 T -> 0x01, G -> 0x10 per byte
 //
 // (the projection holds base codes A 1, C 3, T 4, G 7 and 0 where the read has no
 // Match/Mismatch element, so neither the read's ends nor its deletions need a mask).  Counts
@@ -126,9 +128,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     // (masks, not selects: nested selects on the lane's group compile to divergent branches)
     const int32_t gbase = (nr0 & -(int32_t)(g >= 1)) + (nr1 & -(int32_t)(g >= 2)) + (nr2 & -(int32_t)(g >= 3));
     RowCtx x;
-    x.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(proj + 128 * row0), (short)0,
-                                               (dbg & 1) ? 0 : 128 * (nr0 + nr1 + nr2 + nr3), 0x00020000);
-    x.vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
+    x.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(proj + kProjRowBytes * row0), (short)0,
+                                               (dbg & 1) ? 0 : kProjRowBytes * (nr0 + nr1 + nr2 + nr3), 0x00020000);
+    x.vl = 4u * (uint32_t)(lane & 15) + (uint32_t)kProjRowBytes * (uint32_t)gbase;
     x.gn = (nr0 & -(int32_t)(g == 0)) | (nr1 & -(int32_t)(g == 1)) | (nr2 & -(int32_t)(g == 2)) |
            (nr3 & -(int32_t)(g == 3));
     return x;
@@ -141,16 +143,15 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     return f64(rec, 4) > f64(rec, 2) && f32(rec, 22) == 0u && rec_rows(rec) <= C::kMaxRows;
   };
   // rows k0 .. k0 + U - 1 of each group's slice: the lane offset, or an out-of-range one past
-  // the slice's rows; + 128 u in the scalar offset (in range whenever the lane offset is)
-  auto issue = [&](const RowCtx &x, int32_t k0, uint32_t (&w0)[U], uint32_t (&w1)[U]) {
-    const uint32_t vb = x.vl + 128u * (uint32_t)k0;
+  // the slice's rows; + 64 u in the scalar offset (in range whenever the lane offset is).  One
+  // 32-bit word per lane and row: the column's eight 4-bit codes.
+  auto issue = [&](const RowCtx &x, int32_t k0, uint32_t (&w)[U]) {
+    const uint32_t vb = x.vl + (uint32_t)kProjRowBytes * (uint32_t)k0;
     const int32_t rem = x.gn - k0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t v = u < rem ? vb : 0x80000000u;
-      const auto w = __builtin_amdgcn_raw_buffer_load_b64(x.rsrc, (int)v, 128 * u, 0);
-      w0[u] = w[0];
-      w1[u] = w[1];
+      w[u] = __builtin_amdgcn_raw_buffer_load_b32(x.rsrc, (int)v, kProjRowBytes * u, 0);
     }
   };
   // Tiles are software-pipelined: the Tile + TileX records arrive two tiles ahead, and a tile's
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // flight while this tile's sparse entries and decision run (no loads past the rows are
   // issued, and nothing waits for them).  primed: rows 0 .. 3U - 1 of the tile starting now are
   // already in a, b, c.
-  uint32_t a0[U], a1[U], b0[U], b1[U], c0[U], c1[U], d0[U], d1[U];
+  uint32_t a0[U], b0[U], c0[U], d0[U];
   // the first kEnt sparse entries per lane of a tile's reads (the rest: a loop), applied before
   // its counting (the entry loads' latency overlaps the primed row batches')
   constexpr int NE = C::kEnt;
@@ -200,9 +201,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     }
     const RowCtx cur = row_ctx(rec);
     if (!was_primed) {
-      issue(cur, 0, a0, a1);
-      issue(cur, U, b0, b1);
-      issue(cur, 2 * U, c0, c1);
+      issue(cur, 0, a0);
+      issue(cur, U, b0);
+      issue(cur, 2 * U, c0);
     }
     const int64_t e0 = f64(rec, 24), e1 = f64(rec, 26);
     uint2 ent[NE];
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     if (next_ok) nxt = row_ctx(rec_c);
     // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]),
     //      widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 rows and at the end.
-    //      Row k of each group's slice: one 128-byte load per group.  Three batches of loads
+    //      Row k of each group's slice: one 64-byte load per group.  Three batches of loads
     //      stay in flight while a fourth is counted.
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
@@ -270,14 +271,17 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       w2(wT, ct);
       w2(wG, cg);
     };
-    auto count = [&](const uint32_t (&w0)[U], const uint32_t (&w1)[U]) {
+    // a row word holds loci 0-3 of the column in its low nibbles (byte j: locus j) and loci 4-7
+    // in its high nibbles; split, each half is four byte codes for the perm tables
+    auto count = [&](const uint32_t (&w)[U]) {
       if (nn + U > 15) fold();
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w0[u]);
-        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w0[u]);
-        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w1[u]);
-        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w1[u]);
+        const uint32_t lo = w[u] & 0x0F0F0F0Fu, hi = (w[u] >> 4) & 0x0F0F0F0Fu;
+        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, lo);
+        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, lo);
+        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, hi);
+        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, hi);
       }
       nn += U;
     };
@@ -285,14 +289,14 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     // 0 .. 3U - 1 instead of this tile's past its end
     for (int32_t k0 = 0, since = 0;; k0 += 4 * U) {
       const bool last = k0 + 4 * U >= nrows;
-      issue(cur, k0 + 3 * U, d0, d1);
-      count(a0, a1);
-      issue(last ? nxt : cur, last ? 0 : k0 + 4 * U, a0, a1);
-      count(b0, b1);
-      issue(last ? nxt : cur, last ? U : k0 + 5 * U, b0, b1);
-      count(c0, c1);
-      issue(last ? nxt : cur, last ? 2 * U : k0 + 6 * U, c0, c1);
-      count(d0, d1);
+      issue(cur, k0 + 3 * U, d0);
+      count(a0);
+      issue(last ? nxt : cur, last ? 0 : k0 + 4 * U, a0);
+      count(b0);
+      issue(last ? nxt : cur, last ? U : k0 + 5 * U, b0);
+      count(c0);
+      issue(last ? nxt : cur, last ? 2 * U : k0 + 6 * U, c0);
+      count(d0);
       if (last) break;
       since += 4 * U;
       if (since == 240) {  // uniform: bytes hold 240 rows at most

@@ -432,7 +432,7 @@ struct gq_dev_reads {
   int64_t seq_bytes = 0;
   int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // projection sizes (derive_shape)
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
-  int64_t n_rows = 0;                                      // projection rows (512 B each, ProjRec)
+  int64_t n_rows = 0;                                      // projection rows (kProjRowBytes each, ProjRec)
   float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
   mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
   mutable int mproj_mapq = -1;

@@ -54,7 +54,7 @@ struct DevReads {
   const int64_t *caux_off;      // n_reads + 1 offsets into cev
   // derived at upload for the projection kernels (germline_proj / somatic_proj, see ProjRec)
   const struct ProjRec *prec;   // n_reads + 1 (the last: a zero record)
-  const uint8_t *proj;          // base codes, 8 loci per word, in block rows (see ProjRec)
+  const uint8_t *proj;          // base codes, 8 loci (4 bits each) per word, in slice rows (see ProjRec)
   const int64_t *qoff;          // n_contigs + 1: each contig's first slice (slice = 128 loci)
   const int64_t *srow;          // qoff[n_contigs] + 1: each slice's first row in proj
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
@@ -69,12 +69,14 @@ struct DevReads {
 };
 
 // Per-read record of the projection kernels (8 bytes): the read spans the 8-locus columns
-// [col0, col1).  Its projection holds one byte per locus, the read's base there as a code
+// [col0, col1).  Its projection holds four bits per locus, the read's base there as a code
 // (A 1, C 3, T 4, G 7: ASCII & 7) where the element is a Match/Mismatch
 // (PileupElement.scala:68-135), 0 elsewhere (outside the read, deleted / skipped loci,
-// insertion and deletion anchors, N bases).  A PIECE is one read's run of columns inside one
-// 128-locus slice (16 columns).  The pool is in SLICE ROWS: slice q owns rows [srow[q],
-// srow[q + 1]) of 16 words (128 bytes), word c of a row = column c of the slice.  The slice's
+// insertion and deletion anchors, N bases).  A column's word is 32 bits: byte j holds locus j
+// in its low nibble and locus 4 + j in its high nibble.  A PIECE is one read's run of columns
+// inside one 128-locus slice (16 columns).  The pool is in SLICE ROWS: slice q owns rows
+// [srow[q], srow[q + 1]) of 16 words (kProjRowBytes = 64 bytes), word c of a row = column c of
+// the slice.  The slice's
 // pieces are packed into its rows by greedy interval partitioning in read order (a piece takes
 // the first row that is free from its first column: as few rows as the slice's deepest column
 // holds reads); the words no piece covers are zero.  So the 16 lanes that own a slice read row
@@ -87,6 +89,7 @@ struct ProjRec {
 };
 static_assert(sizeof(ProjRec) == 8, "ProjRec layout");
 constexpr int32_t kProjNone = (int32_t)0x80000000;
+constexpr int kProjRowBytes = 64;  // a slice row: 16 columns x 8 loci x 4 bits
 // Sparse entries of a read (uint2 {x = locus, y}), in any order:
 //   y bit 31 clear: MD event / N base at locus x: bits 0-3 the MD reference base's std_bit
 //     (0 for an N base without an MD event), bits 4-6 the read base's category there (0-3 A C

@@ -435,7 +435,10 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
     if (R.pbad[slot]) continue;  // uniform
     const int64_t base = 16 * R.srow[slot];  // words
     walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
-      if (act) *reinterpret_cast<uint2 *>(proj + 8 * (base + 16 * (int64_t)row + (col & 15))) = proj_word(R, r, col);
+      if (act) {
+        const uint2 w = proj_word(R, r, col);  // byte codes of loci 0-3, 4-7 -> nibbles
+        *reinterpret_cast<uint32_t *>(proj + 4 * (base + 16 * (int64_t)row + (col & 15))) = w.x | (w.y << 4);
+      }
     });
   }
 }
@@ -1725,7 +1728,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.pbad = (const uint8_t *)pbd;
     d->n_rows = tot[0];
     // the pool: rows of 16 words, zero where no piece lies
-    const size_t pool_bytes = (size_t)128 * (size_t)tot[0] + 16;
+    const size_t pool_bytes = (size_t)kProjRowBytes * (size_t)tot[0] + 16;
     HIP_TRY(hipMalloc(&pj, pool_bytes));
     d->owned.push_back(pj);
     HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
@@ -1744,7 +1747,7 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.proj = (const uint8_t *)pj;
     d->d.pev = (const uint2 *)pe;
     d->d.pev_off = (const int64_t *)eo;
-    d->proj_bytes = 128 * tot[0];
+    d->proj_bytes = kProjRowBytes * tot[0];
     d->n_slices = n_sl;
     d->pev_count = tot[1];
     if (n > 0) {  // reads the projection takes

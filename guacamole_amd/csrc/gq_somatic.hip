@@ -1149,9 +1149,9 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   if (t->mproj && t->mproj_mapq == key) return GQ_OK;
   if (!t->mproj) {
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, (size_t)(2 * t->proj_bytes + 32)));
+    HIP_TRY(hipMalloc(&p, (size_t)(256 * t->n_rows + 32)));  // 16 int16 terms per 4-byte word of codes
     t->mproj = p;
-    HIP_TRY(hipMemsetAsync(p, 0, (size_t)(2 * t->proj_bytes + 32), c->stream));  // the words no piece covers
+    HIP_TRY(hipMemsetAsync(p, 0, (size_t)(256 * t->n_rows + 32), c->stream));  // the words no piece covers
     void *q = nullptr;
     HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
     t->mnb = q;

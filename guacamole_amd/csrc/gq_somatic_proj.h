@@ -237,16 +237,16 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     // ---- tumor column counts (bytes, widened into 16-bit pairs every 240 rows and at the end)
     //      and margin sums (exact 16-bit pairs over one batch of four rows, loci 2k, 2k + 1 in
     //      msum[k], folded into 32 bits per locus after each batch): row k of each group's slice
-    //      is one 128-byte load of base codes and one 256-byte load of margin terms (past the
+    //      is one 64-byte load of base codes and one 256-byte load of margin terms (past the
     //      slice's rows: out-of-range offsets, 0)
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
     int32_t m32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(RT.proj + 128 * row0), (short)0, 128 * ntot, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(RT.proj + kProjRowBytes * row0), (short)0, kProjRowBytes * ntot, 0x00020000);
     const __amdgpu_buffer_rsrc_t msrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 128 * row0), (short)0, 256 * ntot, 0x00020000);
-    const uint32_t vl = 8u * (uint32_t)(lane & 15) + 128u * (uint32_t)gbase;
+    const uint32_t vl = 4u * (uint32_t)(lane & 15) + (uint32_t)kProjRowBytes * (uint32_t)gbase;
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
     auto fold = [&]() {
@@ -274,28 +274,28 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       w2(wT, ct);
       w2(wG, cg);
     };
-    auto issue = [&](int k0, uint2 (&w)[U], uint4 (&m)[U]) {  // rows k0 .. k0 + U - 1
-      const uint32_t va = vl + 128u * (uint32_t)k0;
+    auto issue = [&](int k0, uint32_t (&w)[U], uint4 (&m)[U]) {  // rows k0 .. k0 + U - 1
+      const uint32_t va = vl + (uint32_t)kProjRowBytes * (uint32_t)k0;
       const int32_t rem = gn - k0;  // this group's rows left
-      const uint32_t vm = 2u * va;
+      const uint32_t vm = 4u * va;  // 16 bytes of margin terms per 4-byte word of codes
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // past the slice's rows: out-of-range lane offsets
         const bool ok = u < rem;
-        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)(ok ? va : 0x80000000u), 128 * u, 0);
+        w[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(ok ? va : 0x80000000u), kProjRowBytes * u, 0);
         const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(ok ? vm : 0x80000000u), 256 * u, 0);
-        w[u] = make_uint2(a[0], a[1]);
         m[u] = make_uint4(b[0], b[1], b[2], b[3]);
       }
     };
-    auto count = [&](const uint2 (&w)[U], const uint4 (&m)[U]) {
+    auto count = [&](const uint32_t (&w)[U], const uint4 (&m)[U]) {
       if (nn + U > 15) fold();
       uint32_t msum[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].x);
-        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].x);
-        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, w[u].y);
-        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, w[u].y);
+        const uint32_t lo = w[u] & 0x0F0F0F0Fu, hi = (w[u] >> 4) & 0x0F0F0F0Fu;  // loci 0-3, 4-7
+        nac[0] += __builtin_amdgcn_perm(0u, 0x10000100u, lo);
+        ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, lo);
+        nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, hi);
+        ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, hi);
         msum[0] = add_sat2(msum[0], m[u].x);  // exact: four terms >= -8191
         msum[1] = add_sat2(msum[1], m[u].y);
         msum[2] = add_sat2(msum[2], m[u].z);
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       }
       nn += U;
     };
-    uint2 aw[U], bw[U];
+    uint32_t aw[U], bw[U];
     uint4 am[U], bm[U];
     issue(0, aw, am);
     // ---- tumor sparse entries, one lane per entry (germline_proj's encoding)

@@ -195,7 +195,7 @@ void gq_reads_free(gq_dev_reads *r);
 /* projection pool and its sparse entries): for measurement and capacity planning.             */
 typedef struct gq_reads_info {
   int64_t n_reads, seq_bytes, proj_bytes, pev_count, proj_reads;  /* proj_reads: reads the projection takes */
-  int64_t n_rows;    /* projection rows (512 bytes each: proj_bytes = 512 n_rows) */
+  int64_t n_rows;    /* projection rows (64 bytes each: proj_bytes = 64 n_rows) */
   float h2d_ms;      /* gq_reads_upload: host wall time of the copies (pinned staging, PCIe) */
   float derive_ms;   /* gq_reads_upload / wrap: the upload-time derivation on the device    */
 } gq_reads_info;
