@@ -53,6 +53,8 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_ord;        // germline loci whose Scala map order depends on element order
   unsigned long long n_deep;       // somatic candidates handed to the deep caller
   unsigned long long deep_max;     // deepest per-sample pileup among them and the listed loci
+  unsigned long long n_out;        // germline records in the result image (calls_image)
+  unsigned long long out_pool;     // their allele bytes (the image's pool length)
   // per-tile run counters, spread over kSpread addresses (summed on the host)
   unsigned long long spread[4][64];  // visited, ambiguous, ties, dead record slots
   unsigned long long prof[8];  // diagnostic phase clocks (GQ_DBG=16 only)

@@ -1333,10 +1333,10 @@ __global__ __launch_bounds__(kBlock) void vaf_tile(const Tile *__restrict__ tile
 // ------------------------------------------------------------------------------------------
 // Result image: the gq_calls arrays built on device in output order (one D2H copy)
 // ------------------------------------------------------------------------------------------
-struct CallsLayout {  // byte offsets inside the image; header = int64 pool_len
+struct CallsLayout {  // byte offsets inside the image; header = int64 pool_len, int64 n
   size_t contig, pos, ref_off, alt_off, ref_len, alt_len, sample, gt0, gt1, flags, pool, bytes;
 };
-static CallsLayout calls_layout(int64_t n, int64_t dev_pool_used) {
+__host__ __device__ inline CallsLayout calls_layout(int64_t n, int64_t dev_pool_used) {
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
   const size_t N = (size_t)n;
   CallsLayout L;
@@ -1413,42 +1413,55 @@ __global__ void gather_keys(const CallRec *__restrict__ recs, const Counters *__
 // bucket is the number of the bucket's records with a smaller key (keys of live records are
 // unique).  Buckets hold few records: 512 loci of a sparse call set (bshift 9), one locus when
 // every locus emits (bshift 0).  Unused candidate slots (dead_key) are dropped.
+//
+// The chain reads every size from the device (record slots: part_scan's n_rec; records: the
+// bucket scan's total), so it is launched right behind the pileup kernels with grid-stride
+// loops and no host round trip; the host reads the counters once, at the end.
+constexpr int kFinBlocks = 1024;  // grid of the record-slot kernels
+constexpr int kImgBlocks = 512;   // calls_image chunks (one workgroup each)
 __global__ __launch_bounds__(kBlock) void bucket_count(const CallRec *__restrict__ recs, const Counters *__restrict__ ctr,
-                                                        OutGeom og, int64_t n_all, uint64_t dead_key, int bshift,
+                                                        OutGeom og, uint64_t dead_key, int bshift,
                                                         uint64_t *__restrict__ keys, int32_t *__restrict__ slot,
                                                         int64_t *__restrict__ bkt, uint32_t *__restrict__ cnt) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_all) return;
-  const unsigned long long src = part_slot(ctr->part_off[0], (unsigned long long)k, og, 0);
-  const uint64_t key = recs[src].key;
-  keys[k] = key;
-  slot[k] = (int32_t)src;
-  const int64_t b = key == dead_key ? -1 : (int64_t)(key >> (12 + bshift));
-  bkt[k] = b;
-  if (b >= 0) atomicAdd(&cnt[b], 1u);
+  const int64_t n_all = (int64_t)ctr->n_rec;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_all; k += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long src = part_slot(ctr->part_off[0], (unsigned long long)k, og, 0);
+    const uint64_t key = recs[src].key;
+    keys[k] = key;
+    slot[k] = (int32_t)src;
+    const int64_t b = key == dead_key ? -1 : (int64_t)(key >> (12 + bshift));
+    bkt[k] = b;
+    if (b >= 0) atomicAdd(&cnt[b], 1u);
+  }
 }
 
-__global__ void bucket_scatter(int64_t n_all, const int64_t *__restrict__ bkt, const uint32_t *__restrict__ off,
-                               uint32_t *__restrict__ fill, int32_t *__restrict__ members) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_all) return;
-  const int64_t b = bkt[k];
-  if (b < 0) return;
-  members[off[b] + atomicAdd(&fill[b], 1u)] = (int32_t)k;
+__global__ void bucket_scatter(const Counters *__restrict__ ctr, const int64_t *__restrict__ bkt,
+                               const uint32_t *__restrict__ off, uint32_t *__restrict__ fill,
+                               int32_t *__restrict__ members) {
+  const int64_t n_all = (int64_t)ctr->n_rec;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_all; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = bkt[k];
+    if (b >= 0) members[off[b] + atomicAdd(&fill[b], 1u)] = (int32_t)k;
+  }
 }
 
-__global__ void bucket_rank(int64_t n, const uint32_t *__restrict__ off, const int32_t *__restrict__ members,
+__global__ void bucket_rank(int64_t nbk, const uint32_t *__restrict__ off, const int32_t *__restrict__ members,
                             const uint64_t *__restrict__ keys, const int32_t *__restrict__ slot,
                             const int64_t *__restrict__ bkt, int32_t *__restrict__ order) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const int32_t k = members[p];
-  const int64_t b = bkt[k];
-  const uint32_t lo = off[b], hi = off[b + 1];
-  const uint64_t key = keys[k];
-  uint32_t rank = 0;
-  for (uint32_t q = lo; q < hi; ++q) rank += keys[members[q]] < key ? 1u : 0u;
-  order[lo + rank] = slot[k];
+  const int64_t n = off[nbk];  // live records
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = members[p];
+    const int64_t b = bkt[k];
+    const uint32_t lo = off[b], hi = off[b + 1];
+    const uint64_t key = keys[k];
+    uint32_t rank = 0;
+    for (uint32_t q = lo; q < hi; ++q) rank += keys[members[q]] < key ? 1u : 0u;
+    order[lo + rank] = slot[k];
+  }
+}
+
+__global__ void zero_u32(uint32_t *__restrict__ v, int64_t n) {  // one launch for the bucket words (memsets split in four)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) v[i] = 0u;
 }
 
 __global__ void iota_i32(int32_t *__restrict__ v, int64_t n) {
@@ -1456,39 +1469,102 @@ __global__ void iota_i32(int32_t *__restrict__ v, int64_t n) {
   if (i < n) v[i] = (int32_t)i;
 }
 
-__global__ void calls_lengths(const CallRec *__restrict__ recs, const int32_t *__restrict__ order, int64_t n,
-                              int64_t *__restrict__ len) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const CallRec r = recs[order[k]];
-  len[k] = (int64_t)r.ref_len + (int64_t)r.alt_len;
+// calls_image works in kImgBlocks contiguous chunks of the n records (output order); the pool
+// offsets are a scan of the records' allele lengths: chunk sums (img_sums), their exclusive
+// scan (img_scan, one workgroup), then each chunk's own scan inside calls_image.
+__device__ __forceinline__ void img_chunk(int64_t n, int64_t &a, int64_t &b) {
+  const int64_t per = (n + kImgBlocks - 1) / kImgBlocks;
+  a = min(n, (int64_t)blockIdx.x * per);
+  b = min(n, a + per);
+}
+__device__ __forceinline__ uint32_t rec_len(const CallRec &r) { return (uint32_t)r.ref_len + (uint32_t)r.alt_len; }
+
+__global__ __launch_bounds__(kBlock) void img_sums(const CallRec *__restrict__ recs, const int32_t *__restrict__ order,
+                                                    const uint32_t *__restrict__ off, int64_t nbk,
+                                                    int64_t *__restrict__ bsum) {
+  __shared__ unsigned long long red;
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  int64_t a, b;
+  img_chunk((int64_t)off[nbk], a, b);
+  unsigned long long s = 0;
+  for (int64_t k = a + threadIdx.x; k < b; k += blockDim.x) s += rec_len(recs[order[k]]);
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(&red, s);
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (int64_t)red;
 }
 
-__global__ void calls_image(const CallRec *__restrict__ recs, const int32_t *__restrict__ order,
-                            const int64_t *__restrict__ off, const uint8_t *__restrict__ dpool, int64_t n,
-                            CallsLayout L, uint8_t *__restrict__ img) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const CallRec r = recs[order[k]];
-  const int64_t o = off[k];
-  const int tot = (int)r.ref_len + (int)r.alt_len;
-  reinterpret_cast<int32_t *>(img + L.contig)[k] = r.contig;
-  reinterpret_cast<int64_t *>(img + L.pos)[k] = r.pos;
-  reinterpret_cast<int64_t *>(img + L.ref_off)[k] = o;
-  reinterpret_cast<int64_t *>(img + L.alt_off)[k] = o + r.ref_len;
-  reinterpret_cast<int32_t *>(img + L.ref_len)[k] = r.ref_len;
-  reinterpret_cast<int32_t *>(img + L.alt_len)[k] = r.alt_len;
-  img[L.sample + k] = r.sample;
-  img[L.gt0 + k] = r.gt0;
-  img[L.gt1 + k] = r.gt1;
-  img[L.flags + k] = r.flags;
-  uint8_t *dst = img + L.pool + o;
-  if (tot <= 8) {
-    for (int i = 0; i < tot; ++i) dst[i] = (uint8_t)(r.allele >> (8 * i));
-  } else {
-    for (int i = 0; i < tot; ++i) dst[i] = dpool[r.allele + i];
+__global__ __launch_bounds__(kImgBlocks) void img_scan(int64_t *__restrict__ bsum) {  // in place, exclusive; total at [kImgBlocks]
+  __shared__ int64_t s[kImgBlocks];
+  const int t = threadIdx.x;
+  const int64_t v = bsum[t];
+  s[t] = v;
+  __syncthreads();
+  for (int d = 1; d < kImgBlocks; d <<= 1) {
+    const int64_t y = t >= d ? s[t - d] : 0;
+    __syncthreads();
+    s[t] += y;
+    __syncthreads();
   }
-  if (k == n - 1) *reinterpret_cast<int64_t *>(img) = o + tot;  // pool_len
+  bsum[t] = s[t] - v;
+  if (t == kImgBlocks - 1) bsum[kImgBlocks] = s[t];
+}
+
+__global__ __launch_bounds__(kBlock) void calls_image(const CallRec *__restrict__ recs, const int32_t *__restrict__ order,
+                                                       const uint32_t *__restrict__ off, int64_t nbk,
+                                                       const int64_t *__restrict__ bsum, const uint8_t *__restrict__ dpool,
+                                                       Counters *__restrict__ ctr, uint8_t *__restrict__ img) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int64_t n = (int64_t)off[nbk];
+  const CallsLayout L = calls_layout(n, 0);
+  int64_t a, b;
+  img_chunk(n, a, b);
+  int64_t prefix = bsum[blockIdx.x];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t base = a; base < b; base += blockDim.x) {  // uniform trip count per workgroup
+    const int64_t k = base + threadIdx.x;
+    CallRec r{};
+    if (k < b) r = recs[order[k]];
+    const uint32_t tot = k < b ? rec_len(r) : 0u;
+    const uint32_t inc = wave_incl_scan(tot);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      before += w < wv ? wsum[w] : 0u;
+      all += wsum[w];
+    }
+    __syncthreads();
+    if (k < b) {
+      const int64_t o = prefix + before + inc - tot;
+      reinterpret_cast<int32_t *>(img + L.contig)[k] = r.contig;
+      reinterpret_cast<int64_t *>(img + L.pos)[k] = r.pos;
+      reinterpret_cast<int64_t *>(img + L.ref_off)[k] = o;
+      reinterpret_cast<int64_t *>(img + L.alt_off)[k] = o + r.ref_len;
+      reinterpret_cast<int32_t *>(img + L.ref_len)[k] = r.ref_len;
+      reinterpret_cast<int32_t *>(img + L.alt_len)[k] = r.alt_len;
+      img[L.sample + k] = r.sample;
+      img[L.gt0 + k] = r.gt0;
+      img[L.gt1 + k] = r.gt1;
+      img[L.flags + k] = r.flags;
+      uint8_t *dst = img + L.pool + o;
+      if (tot <= 8) {
+        for (uint32_t i = 0; i < tot; ++i) dst[i] = (uint8_t)(r.allele >> (8 * i));
+      } else {
+        for (uint32_t i = 0; i < tot; ++i) dst[i] = dpool[r.allele + i];
+      }
+    }
+    prefix += all;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // header and the counters the host reads back
+    const int64_t pool_len = bsum[kImgBlocks];
+    reinterpret_cast<int64_t *>(img)[0] = pool_len;
+    reinterpret_cast<int64_t *>(img)[1] = n;
+    ctr->n_out = (unsigned long long)n;
+    ctr->out_pool = (unsigned long long)pool_len;
+  }
 }
 
 }  // namespace
@@ -2246,12 +2322,65 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   og.capB[1] = (unsigned long long)pl.n_loci / 16384 + 256;
   unsigned long long pool_cap = 1 << 22, amb_cap = 4096;
   Counters hc{};
+  // output order: buckets of 2^bshift ordinals (one locus when every locus emits)
+  const int bshift = dense ? 0 : 9;
+  const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
+  const int64_t nbk = (pl.n_loci >> bshift) + 1;
+  size_t scan_tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (int)(nbk + 1), c->stream));
+  // ---- the finalize chain (record order, result image), sized from the device: see bucket_count
+  auto finalize = [&](Counters *ctr, size_t cap_rec) -> gq_status {
+    uint32_t *cnt = (uint32_t *)c->bkt.p, *off = cnt + (nbk + 1), *fill = off + (nbk + 1);
+    hipLaunchKernelGGL(zero_u32, dim3((unsigned)std::min<int64_t>((3 * (nbk + 1) + kBlock - 1) / kBlock, 1024)),
+                       dim3(kBlock), 0, c->stream, cnt, 3 * (nbk + 1));  // counts, (offsets), fills
+    const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(((int64_t)cap_rec + kBlock - 1) / kBlock, kFinBlocks));
+    hipLaunchKernelGGL(bucket_count, dim3(gb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const Counters *)ctr, og, dead_key, bshift, (uint64_t *)c->keys.p, (int32_t *)c->idx_sorted.p,
+                       (int64_t *)c->idx.p, cnt);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, scan_tmp, cnt, off, (int)(nbk + 1), c->stream));
+    hipLaunchKernelGGL(bucket_scatter, dim3(gb), dim3(kBlock), 0, c->stream, (const Counters *)ctr,
+                       (const int64_t *)c->idx.p, (const uint32_t *)off, fill, (int32_t *)c->keys_sorted.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(bucket_rank, dim3(gb), dim3(kBlock), 0, c->stream, nbk, (const uint32_t *)off,
+                       (const int32_t *)c->keys_sorted.p, (const uint64_t *)c->keys.p, (const int32_t *)c->idx_sorted.p,
+                       (const int64_t *)c->idx.p, (int32_t *)c->recs_sorted.p);
+    HIP_TRY(hipGetLastError());
+    int64_t *bsum = (int64_t *)c->keys_sorted.p + (cap_rec + 1) / 2 + 1;  // past the members (int32)
+    hipLaunchKernelGGL(img_sums, dim3(kImgBlocks), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const int32_t *)c->recs_sorted.p, (const uint32_t *)off, nbk, bsum);
+    hipLaunchKernelGGL(img_scan, dim3(1), dim3(kImgBlocks), 0, c->stream, bsum);
+    hipLaunchKernelGGL(calls_image, dim3(kImgBlocks), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
+                       (const int32_t *)c->recs_sorted.p, (const uint32_t *)off, nbk, (const int64_t *)bsum,
+                       (const uint8_t *)c->pool.p, ctr, (uint8_t *)c->image.p);
+    HIP_TRY(hipGetLastError());
+    return GQ_OK;
+  };
+  // the counters' head back to the host (one copy, one sync)
+  auto read_counters = [&](Counters *ctr) -> gq_status {
+    HIP_TRY(c->pinned(kCountersHead));
+    HIP_TRY(hipMemcpyAsync(c->pin, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(&hc, c->pin, kCountersHead);
+    return GQ_OK;
+  };
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(2 * amb_cap * sizeof(AmbItem)));  // heap-order loci, then order-dependent loci
-    HIP_TRY(c->recs.ensure(og.total(0) * sizeof(CallRec)));
+    const size_t cap_rec = (size_t)og.total(0);
+    HIP_TRY(c->recs.ensure(cap_rec * sizeof(CallRec)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
     HIP_TRY(c->pool.ensure(pool_cap));
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    // finalize buffers, by the record capacity (the chain never learns the count on the host)
+    HIP_TRY(c->keys.ensure((cap_rec + 1) * 8));
+    HIP_TRY(c->keys_sorted.ensure((cap_rec + 1) * 4 + 8 * (kImgBlocks + 2) + 16));  // members | chunk sums
+    HIP_TRY(c->idx.ensure((cap_rec + 1) * 8));
+    HIP_TRY(c->idx_sorted.ensure((cap_rec + 1) * 4));
+    HIP_TRY(c->recs_sorted.ensure((cap_rec + 1) * 4));
+    HIP_TRY(c->bkt.ensure(sizeof(uint32_t) * (size_t)(3 * (nbk + 1))));
+    HIP_TRY(c->sort_tmp.ensure(std::max<size_t>(scan_tmp, 16)));
+    HIP_TRY(c->image.ensure(calls_layout((int64_t)cap_rec, (int64_t)pool_cap).bytes));
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     if (attempt == 0) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -2280,7 +2409,6 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
-      const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
 #ifndef GQ_EXPAND_BLOCKS
 #define GQ_EXPAND_BLOCKS 1024  // workgroups of germline_expand (each walks kParts / this many partitions)
 #endif
@@ -2289,10 +2417,18 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(c->pinned(kCountersHead));
-    HIP_TRY(hipMemcpyAsync(c->pin, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    memcpy(&hc, c->pin, kCountersHead);
+    // the common case needs no re-run: order the records and build the image right away
+    st = finalize(ctr, cap_rec);
+    if (st) {
+      free(res);
+      return st;
+    }
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    st = read_counters(ctr);
+    if (st) {
+      free(res);
+      return st;
+    }
     bool retry = false;
     // part_max = the largest overflow of a partition: grow both capacities by it
     for (int w = 0; w < 2; ++w)
@@ -2312,14 +2448,15 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     // the windows' element order (initial groups in heap order) for the re-runs below: the
     // first occurrences the Scala map orders of those loci depend on
     SomWin sw{};
-    if (!retry && (hc.n_amb > 0 || hc.n_ord > 0) && !hc.err) {
+    const bool rerun = !retry && (hc.n_amb > 0 || hc.n_ord > 0) && !hc.err;
+    if (rerun) {
       st = build_somwin(c, pl, rd, rd, sw);
       if (st) {
         free(res);
         return st;
       }
     }
-    if (!retry && hc.n_ord > 0 && !hc.err) {
+    if (rerun && hc.n_ord > 0) {
       // loci whose output order depends on first occurrences in element order
       const int oblocks = (int)std::min<int64_t>(((int64_t)hc.n_ord + 3) / 4, 4096);
       hipLaunchKernelGGL(germline_complex, dim3(oblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
@@ -2329,20 +2466,8 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
                          (int64_t)hc.n_ord, gq_dbg(), sw);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
-      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-      HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (hc.part_max[0]) {
-        og.capA[0] += hc.part_max[0] + 64;
-        og.capB[0] += hc.part_max[0] + 64;
-        retry = true;
-      }
-      if (hc.pool_used > pool_cap) {
-        pool_cap = hc.pool_used + 4096;
-        retry = true;
-      }
     }
-    if (!retry && hc.n_amb > 0 && !hc.err) {
+    if (rerun && hc.n_amb > 0) {
       // loci whose reference base depends on heap order: replay the window's queue, then the
       // complex kernel again over just those loci with the resolved base
       std::vector<AmbItem> amb((size_t)hc.n_amb);
@@ -2362,9 +2487,14 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
                          (int64_t)amb.size(), gq_dbg(), sw);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
+    }
+    if (rerun) {  // the re-runs added records: check their capacities, then the chain again
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-      HIP_TRY(hipMemcpyAsync(&hc, ctr, kCountersHead, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      st = read_counters(ctr);
+      if (st) {
+        free(res);
+        return st;
+      }
       if (hc.part_max[0]) {
         og.capA[0] += hc.part_max[0] + 64;
         og.capB[0] += hc.part_max[0] + 64;
@@ -2373,6 +2503,17 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       if (hc.pool_used > pool_cap) {
         pool_cap = hc.pool_used + 4096;
         retry = true;
+      }
+      if (!retry) {
+        st = finalize(ctr, cap_rec);
+        if (!st) {
+          HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+          st = read_counters(ctr);
+        }
+        if (st) {
+          free(res);
+          return st;
+        }
       }
     }
     if (!retry) break;
@@ -2401,81 +2542,24 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     free(res);
     return st;
   }
-  // ---- sort records by key (output order), then build the host result image on device:
-  //      one D2H copy of [header | SoA arrays | allele pool] instead of per-record marshalling
-  const int64_t n_all = (int64_t)hc.n_rec;         // record slots, including unused candidate slots
-  const int64_t n = n_all - (int64_t)hc.n_dead;    // records (the unused slots sort last)
-  const size_t nn = (size_t)std::max<int64_t>(n_all, 1);
-  HIP_TRY(c->keys.ensure(nn * 8));
-  HIP_TRY(c->keys_sorted.ensure(nn * 8));
-  HIP_TRY(c->idx.ensure(nn * 8));
-  HIP_TRY(c->idx_sorted.ensure(nn * 4));
-  const CallsLayout lay = calls_layout(n, (int64_t)std::min<unsigned long long>(hc.pool_used, pool_cap));
-  HIP_TRY(c->image.ensure(lay.bytes));
-  if (n > 0) {
-    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock), nb_all = (unsigned)((n_all + kBlock - 1) / kBlock);
-    // output order: bucket counts, their scan, the members of each bucket, ranks inside it
-    const bool dense = p->emit_ref || p->emit_no_call;
-    const int bshift = dense ? 0 : 9;
-    const uint64_t dead_key = ((uint64_t)pl.n_loci << 12) | 0xFFFu;
-    const int64_t nbk = (pl.n_loci >> bshift) + 1;
-    HIP_TRY(c->bkt.ensure(sizeof(uint32_t) * (size_t)(3 * (nbk + 1))));
-    uint32_t *cnt = (uint32_t *)c->bkt.p, *off = cnt + (nbk + 1), *fill = off + (nbk + 1);
-    HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (size_t)(nbk + 1), c->stream));
-    HIP_TRY(hipMemsetAsync(fill, 0, sizeof(uint32_t) * (size_t)(nbk + 1), c->stream));
-    hipLaunchKernelGGL(bucket_count, dim3(nb_all), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const Counters *)c->counters.p, og, n_all, dead_key, bshift, (uint64_t *)c->keys.p,
-                       (int32_t *)c->idx_sorted.p, (int64_t *)c->idx.p, cnt);
-    HIP_TRY(hipGetLastError());
-    size_t tmp = 0, tmp2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, off, (int)(nbk + 1), c->stream));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p, (int)n,
-                                             c->stream));
-    HIP_TRY(c->sort_tmp.ensure(std::max(tmp, tmp2)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, cnt, off, (int)(nbk + 1), c->stream));
-    hipLaunchKernelGGL(bucket_scatter, dim3(nb_all), dim3(kBlock), 0, c->stream, n_all, (const int64_t *)c->idx.p,
-                       (const uint32_t *)off, fill, (int32_t *)c->keys_sorted.p);
-    HIP_TRY(hipGetLastError());
-    // order -> the record slot of each output position (c->recs_sorted as int32)
-    HIP_TRY(c->recs_sorted.ensure(nn * 4));
-    hipLaunchKernelGGL(bucket_rank, dim3(nb), dim3(kBlock), 0, c->stream, n, (const uint32_t *)off,
-                       (const int32_t *)c->keys_sorted.p, (const uint64_t *)c->keys.p, (const int32_t *)c->idx_sorted.p,
-                       (const int64_t *)c->idx.p, (int32_t *)c->recs_sorted.p);
-    HIP_TRY(hipGetLastError());
-    // allele byte lengths in output order -> exclusive offsets into the pool
-    hipLaunchKernelGGL(calls_lengths, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const int32_t *)c->recs_sorted.p, n, (int64_t *)c->idx.p);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp2, (const int64_t *)c->idx.p, (int64_t *)c->keys.p,
-                                             (int)n, c->stream));
-    hipLaunchKernelGGL(calls_image, dim3(nb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const int32_t *)c->recs_sorted.p, (const int64_t *)c->keys.p, (const uint8_t *)c->pool.p, n,
-                       lay, (uint8_t *)c->image.p);
-    HIP_TRY(hipGetLastError());
-  } else {
-    HIP_TRY(hipMemsetAsync(c->image.p, 0, 64, c->stream));
-  }
+  // ---- the image is in HBM (header: pool_len, n); the host block is one D2H copy of it
+  const int64_t n = (int64_t)hc.n_out;
+  const CallsLayout lay = calls_layout(n, (int64_t)hc.out_pool);
+  const int64_t pool_len = (int64_t)hc.out_pool;
   uint8_t *blk = nullptr;
-  int64_t pool_len = 0;
-  if (dev) {  // the image stays in HBM: only its pool length comes back
-    HIP_TRY(c->pinned(sizeof(pool_len)));
-    HIP_TRY(hipMemcpyAsync(c->pin, c->image.p, sizeof(pool_len), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    memcpy(&pool_len, c->pin, sizeof(pool_len));
+  if (dev) {  // the image stays in HBM
     blk = (uint8_t *)c->image.p;
     dev->image = c->image.p;
     dev->image_bytes = (int64_t)lay.pool + pool_len;
   } else {
-    blk = (uint8_t *)malloc(lay.bytes);
+    const size_t nbytes = (size_t)lay.pool + (size_t)pool_len;
+    blk = (uint8_t *)malloc(std::max<size_t>(nbytes, 64));
     if (!blk) {
       free(res);
-      return set_err(GQ_E_NOMEM, "result block of %zu bytes", lay.bytes);
+      return set_err(GQ_E_NOMEM, "result block of %zu bytes", nbytes);
     }
-    HIP_TRY(hipMemcpyAsync(blk, c->image.p, lay.bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(hipMemcpyAsync(blk, c->image.p, nbytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    pool_len = *(const int64_t *)blk;
   }
   // ---- point the result struct into the block (output order)
   const auto h1 = std::chrono::steady_clock::now();
