@@ -184,73 +184,83 @@ __global__ void germline_expand(CallRec *__restrict__ recs, Counters *ctr, OutGe
     const unsigned long long slot = og.slot(0, p, k);
     const CallRec cand = recs[slot];
     if (cand.flags != kCandidate) continue;  // an ordinary record, or the second slot of a pair
-    const uint32_t c[5] = {(uint32_t)(cand.allele & 0xFFFFu), (uint32_t)((cand.allele >> 16) & 0xFFFFu),
-                           (uint32_t)((cand.allele >> 32) & 0xFFFFu), (uint32_t)(cand.allele >> 48), cand.ref_len};
-    const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4];
+    // categories: (ref, A) (ref, C) (ref, T) (ref, G) (ref, N), and 5 the MidDeletion allele
+    // (ref, "") (Alignment.scala:87-92; its count in alt_len)
+    constexpr int NC = 6;
+    const uint32_t c[NC] = {(uint32_t)(cand.allele & 0xFFFFu), (uint32_t)((cand.allele >> 16) & 0xFFFFu),
+                            (uint32_t)((cand.allele >> 32) & 0xFFFFu), (uint32_t)(cand.allele >> 48), cand.ref_len,
+                            cand.alt_len};
+    const uint32_t depth = c[0] + c[1] + c[2] + c[3] + c[4] + c[5];
     const uint8_t ref = cand.gt0;
-    // the counts map's Scala order over the alleles present (ref, b): up to four, the mutable
-    // map's (bucket descending; no two share a bucket here: the one pair that could, ref C with
-    // G and N, went to germline_complex), five: the HashTrieMap's (gq_scala_order.h)
+    // the counts map's Scala order over the alleles present: up to four, the mutable map's
+    // (bucket descending; no two share a bucket here: the pairs that could went to
+    // germline_complex), five or more: the HashTrieMap's (gq_scala_order.h)
     int npres = 0;
 #pragma unroll
-    for (int cat = 0; cat < 5; ++cat) npres += c[cat] > 0 ? 1 : 0;
-    uint64_t sk[5];
+    for (int cat = 0; cat < NC; ++cat) npres += c[cat] > 0 ? 1 : 0;
+    uint64_t sk[NC];
 #pragma unroll
-    for (int cat = 0; cat < 5; ++cat) {
+    for (int cat = 0; cat < NC; ++cat) {
       scala::SeqHasher hr, ha;
       hr.add_byte(ref);
-      ha.add_byte(cat_base(cat));
+      if (cat < 5) ha.add_byte(cat_base(cat));
       const uint32_t h = scala::allele_hash(hr.result(), ha.result());
       sk[cat] = npres <= 4 ? (uint64_t)(15u - scala::mutable_bucket(h, 4)) : scala::trie_key(h);
     }
     uint32_t k0 = 0, k1 = 0, k2 = 0;  // top three passing keys: count << 16 | (255 - map rank) << 8 | category
     int npass = 0;
 #pragma unroll
-    for (int cat = 0; cat < 5; ++cat) {
+    for (int cat = 0; cat < NC; ++cat) {
       const uint32_t cc = c[cat];
       if (cc == 0 || !passes(cc, depth)) continue;
       ++npass;
       int rank = 0;
 #pragma unroll
-      for (int o = 0; o < 5; ++o)
+      for (int o = 0; o < NC; ++o)
         if (o != cat && c[o] > 0 && (sk[o] < sk[cat] || (sk[o] == sk[cat] && o < cat))) ++rank;
       uint32_t key = (cc << 16) | ((uint32_t)(255 - rank) << 8) | (uint32_t)cat;
       if (key > k0) { const uint32_t t = k0; k0 = key; key = t; }
       if (key > k1) { const uint32_t t = k1; k1 = key; key = t; }
       if (key > k2) { k2 = key; }
     }
-    auto key_base = [](uint32_t key) -> uint8_t { return cat_base((int)(key & 0xFFu)); };
     const bool tie = npass >= 2 && ((k0 >> 16) == (k1 >> 16) || (npass >= 3 && (k1 >> 16) == (k2 >> 16)));
     if (tie) ++ties;
     const uint8_t fl = tie ? GQ_FLAG_TIE : 0;
-    // the case split -> up to two records (g0, g1, alt base or the symbolic <ALT>)
-    const uint8_t b0 = key_base(k0), b1 = key_base(k1);
-    int nout = 0;
-    uint8_t ga0 = 0, ga1 = 0, aa = 0, gb0 = 0, gb1 = 0, ab = 0;
+    // the case split (GermlineThresholdCaller.scala:118-176) -> up to two records (g0, g1, the
+    // allele's category or the symbolic <ALT>).  Allele.isVariant: ref != alt; the MidDeletion
+    // allele (ref, "") is a variant with an empty alt.
+    const int t0 = (int)(k0 & 0xFFu), t1 = (int)(k1 & 0xFFu);
+    auto is_var = [&](int cat) { return cat == 5 || cat_base(cat) != ref; };
+    int nout = 0, aa = 0, ab = 0;
+    uint8_t ga0 = 0, ga1 = 0, gb0 = 0, gb1 = 0;
     bool syma = false;
     if (npass == 0) {
       if (emit_no_call) nout = 1, ga0 = ga1 = GQ_GT_NOCALL, syma = true;
-    } else if (npass == 1 && b0 == ref) {
+    } else if (npass == 1 && !is_var(t0)) {
       if (emit_ref) nout = 1, ga0 = ga1 = GQ_GT_REF, syma = true;
     } else if (npass == 1) {
-      nout = 1, ga0 = ga1 = GQ_GT_ALT, aa = b0;
+      nout = 1, ga0 = ga1 = GQ_GT_ALT, aa = t0;
     } else {
-      const bool v1 = b0 != ref, v2 = b1 != ref;
-      if (v1 != v2) {
-        nout = 1, ga0 = GQ_GT_REF, ga1 = GQ_GT_ALT, aa = v1 ? b0 : b1;
+      const bool v1 = is_var(t0), v2 = is_var(t1);
+      if ((!v1 || !v2) && ((t0 == 5) != (t1 == 5))) {
+        // heterozygous deletion (an empty alt beside a non-variant allele): no record
+      } else if (v1 != v2) {
+        nout = 1, ga0 = GQ_GT_REF, ga1 = GQ_GT_ALT, aa = v1 ? t0 : t1;
       } else if (v1 && v2) {
-        nout = 2, ga0 = gb0 = GQ_GT_ALT, ga1 = gb1 = GQ_GT_OTHERALT, aa = b0, ab = b1;
+        nout = 2, ga0 = gb0 = GQ_GT_ALT, ga1 = gb1 = GQ_GT_OTHERALT, aa = t0, ab = t1;
       }
-      // two non-variant single-base alleles cannot occur (all Match alleles share ref)
+      // two non-variant alleles cannot occur (every Match allele is (ref, ref))
     }
     // the pair's two slots are consecutive in the partition (reserved together); an unused
     // slot gets the dead key.  Records are written as two 16-byte halves (CallRec layout).
-    auto put = [&](unsigned long long at, bool live, int sub, uint8_t g0, uint8_t g1, uint8_t alt, bool sym) {
+    auto put = [&](unsigned long long at, bool live, int sub, uint8_t g0, uint8_t g1, int cat, bool sym) {
       const uint64_t key = live ? (cand.key | (uint64_t)sub) : dead_key;
-      const uint64_t allele = sym ? ((uint64_t)ref | kAltSym) : ((uint64_t)ref | ((uint64_t)alt << 8));
+      const uint32_t alt_len = sym ? 5u : cat == 5 ? 0u : 1u;
+      const uint64_t allele = sym ? ((uint64_t)ref | kAltSym)
+                                  : ((uint64_t)ref | (cat == 5 ? 0ull : (uint64_t)cat_base(cat) << 8));
       const uint32_t w3 = (uint32_t)cand.sample | ((uint32_t)g0 << 8) | ((uint32_t)g1 << 16) |
                           ((uint32_t)(live ? fl : 0) << 24);
-      const uint32_t w4 = 1u | ((uint32_t)(sym ? 5 : 1) << 16);  // ref_len 1, alt_len
+      const uint32_t w4 = 1u | (alt_len << 16);  // ref_len 1, alt_len
       uint4 *d = reinterpret_cast<uint4 *>(recs + at);
       d[0] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)cand.contig, (uint32_t)cand.pos);
       d[1] = make_uint4(w3, w4, (uint32_t)allele, (uint32_t)(allele >> 32));

@@ -72,15 +72,18 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // N << 4 | complex diff << 16
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
+  __shared__ __attribute__((aligned(16))) uint32_t dlw[C::kWaves][T];  // MidDeletion range differences
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint32_t *ev = evw[wave], *mk = mkw[wave];
+  uint32_t *ev = evw[wave], *mk = mkw[wave], *dl = dlw[wave];
   {
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
     {  // separate stores (a chained assignment re-reads each word from LDS)
       const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
       e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4;
+      uint4 *d4 = reinterpret_cast<uint4 *>(dl + 8 * lane);
+      d4[0] = z4; d4[1] = z4;
     }
   }
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
@@ -212,12 +215,14 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     // ---- sparse entries of the tile's reads, one lane per entry, into the LDS words
     auto apply = [&](uint2 p) {
       const int32_t l = (int32_t)p.x;
-      if (p.y & kPevComplex) {
+      if (p.y & kPevComplex) {  // a range: +1 at its first locus, -1 past its last
         const int64_t a = max((int64_t)l, (int64_t)B0);
-        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+        const int64_t b = min((int64_t)l + (int64_t)(p.y & kPevLenMask), (int64_t)B0 + T);
+        const bool mid = (p.y & kPevMidDel) != 0;  // MidDeletion elements: their own count
+        uint32_t *dw = mid ? dl : mk;
         if (a < b) {
-          atomicAdd(&mk[a - B0], 1u << 16);
-          if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
+          atomicAdd(&dw[a - B0], mid ? 1u : 1u << 16);
+          if (b < (int64_t)B0 + T) atomicAdd(&dw[b - B0], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
         }
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
@@ -313,7 +318,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dl + 8 * lane);
     uint32_t kinds = 0, nrec = 0, ncpx = 0;
+    int32_t mid0 = 0;  // MidDeletion elements entering this lane's first locus
     // locus j's 16-bit count of base w (a dynamic j selects among four registers)
     auto cnt16 = [](const uint32_t (&w)[4], int j) {
       const int q = j >> 1;
@@ -335,39 +342,44 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
               ((int32_t)mb.x >> 16) + ((int32_t)mb.y >> 16) + ((int32_t)mb.z >> 16) + ((int32_t)mb.w >> 16);
       }
       int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
-      // ---- decision (GermlineThresholdCaller.scala:97-177 for single-base pileups), eight loci
-      //      in two halves (the LDS words of four loci at a time: the next tile's row batches
-      //      are in flight in registers meanwhile): kind 0 nothing, 1 a Ref/NoCall record, 2 a
-      //      variant candidate (record pair), 3 complex
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint32_t eac[4], etg[4], m8[4];
+      {  // the same for the MidDeletion ranges
+        const uint4 da = d4[0], db = d4[1];
+        const int32_t mrun = (int32_t)(da.x + da.y + da.z + da.w + db.x + db.y + db.z + db.w);
+        mid0 = (int32_t)wave_incl_scan((uint32_t)mrun) - mrun;
+      }
+      int32_t mid_run = mid0;
+      // ---- decision (GermlineThresholdCaller.scala:97-177 for pileups of single-base and
+      //      MidDeletion alleles), eight loci, four unrolled at a time with their LDS words read
+      //      in the loop (the next tile's row batches are in flight in registers meanwhile):
+      //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
+#pragma unroll 4
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t eacj = ev[8 * lane + j], etgj = ev[T + 8 * lane + j], m8j = mk[8 * lane + j];
+        const int32_t ddj = (int32_t)dl[8 * lane + j];
         {
-          const uint4 ea = e4[h], ec = f4[h], ma = m4[h];
-          eac[0] = ea.x, eac[1] = ea.y, eac[2] = ea.z, eac[3] = ea.w;
-          etg[0] = ec.x, etg[1] = ec.y, etg[2] = ec.z, etg[3] = ec.w;
-          m8[0] = ma.x, m8[1] = ma.y, m8[2] = ma.z, m8[3] = ma.w;
-        }
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * h + jj;
         const int32_t l = B0 + 8 * lane + j;
         const bool in = l >= L0 && l < L1;
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
-        const uint32_t nN = (m8[jj] >> 4) & 0xFFFu;
-        ncx_run += (int32_t)m8[jj] >> 16;
+        const uint32_t nN = (m8j >> 4) & 0xFFFu;
+        ncx_run += (int32_t)m8j >> 16;
         const uint32_t ncx = ncx_run > 0 ? (uint32_t)ncx_run : 0u;
-        const uint32_t depth = cA + cC + cT + cG + nN + ncx;
-        const uint32_t mask = ref_mask(m8[jj], eac[jj], etg[jj], cA, cC, cT, cG);
+        mid_run += ddj;
+        const uint32_t nmid = mid_run > 0 ? (uint32_t)mid_run : 0u;  // MidDeletion elements (allele (ref, ""))
+        const uint32_t depth = cA + cC + cT + cG + nN + ncx + nmid;
+        const uint32_t mask = ref_mask(m8j, eacj, etgj, cA, cC, cT, cG);
         // branch-free (0/1 integers): the common hom-ref locus writes nothing
         const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
         const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
         const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit (or 0: N)
         const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
                                nN * (low == 0u ? 1u : 0u);
-        // ref C with G and N present: Scala map order by first occurrence (germline_complex)
-        const uint32_t cgn = (low == 2u ? 1u : 0u) & (cG > 0 ? 1u : 0u) & (nN > 0 ? 1u : 0u);
-        const uint32_t to_complex = live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u) | cgn);
+        // two alleles in one mutable.HashMap bucket (Scala map order by first occurrence:
+        // germline_complex): ref C with two of G, N and (C, ""); ref G with T and (G, "")
+        const uint32_t cgn = (low == 2u ? 1u : 0u) &
+                             ((cG > 0 ? 1u : 0u) + (nN > 0 ? 1u : 0u) + (nmid > 0 ? 1u : 0u) >= 2u ? 1u : 0u);
+        const uint32_t gtm = (low == 8u ? 1u : 0u) & (cT > 0 ? 1u : 0u) & (nmid > 0 ? 1u : 0u);
+        const uint32_t to_complex =
+            live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u) | cgn | gtm);
         const uint32_t simple = live & (to_complex ^ 1u);
         const uint32_t alt_pass = passes(depth - c_ref, depth) ? 1u : 0u;  // some other allele may pass
         const uint32_t homref = simple & (alt_pass ^ 1u);
@@ -390,7 +402,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       unsigned kr = rbase, kc = cbase;
       constexpr uint64_t kAltSym = ((uint64_t)'<' << 8) | ((uint64_t)'A' << 16) | ((uint64_t)'L' << 24) |
                                    ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
+      int32_t mrun = mid0;
       for (int j = 0; j < 8; ++j) {
+        mrun += (int32_t)dl[8 * lane + j];
+        const uint32_t nmid = mrun > 0 ? (uint32_t)mrun : 0u;
         const uint32_t kind = (kinds >> (2 * j)) & 3u;
         if (__ballot(kind != 0) == 0) continue;  // no lane writes for locus j (uniform skip)
         if (kind == 0) continue;
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         rr.pos = pos;
         rr.sample = 0;
         if (kind == 1) {
-          const uint32_t depth = cA + cC + cT + cG + nN;
+          const uint32_t depth = cA + cC + cT + cG + nN + nmid;
           const uint32_t low = mask & (0u - mask);
           const uint32_t c_ref = low == 1u ? cA : low == 2u ? cC : low == 4u ? cT : low == 8u ? cG : nN;
           const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
@@ -429,7 +444,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
           rr.gt1 = 0;
           rr.flags = kCandidate;
           rr.ref_len = (uint16_t)nN;
-          rr.alt_len = 0;
+          rr.alt_len = (uint16_t)nmid;
           rr.allele = (uint64_t)cA | ((uint64_t)cC << 16) | ((uint64_t)cT << 32) | ((uint64_t)cG << 48);
           if (kr < out.cap[0]) prec_out[kr] = rr;
           rr.flags = kCandidateSlot;
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     }
     {  // separate stores (a chained assignment re-reads each word from LDS)
       const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4;
+      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4; d4[0] = z4; d4[1] = z4;
     }  // this lane's words, for the next tile
     if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup + entries, counting, -, widen, decision
       const uint64_t t_f = __builtin_readcyclecounter();

@@ -95,10 +95,15 @@ constexpr int kProjRowBytes = 64;  // a slice row: 16 columns x 8 loci x 4 bits
 //     (0 for an N base without an MD event), bits 4-6 the read base's category there (0-3 A C
 //     T G: a Match/Mismatch element carrying an MD event; 4: an N base; 7: none, e.g. an event
 //     on a deleted base);
-//   y bit 31 set: loci [x, x + (y & 0x7FFFFFFF)) hold complex elements (insertion / deletion
-//     anchors, mid-deletions, clipped N-skips): the exact kernel decides them.
+//   y bit 31 set: loci [x, x + (y & kPevLenMask)) hold complex elements (insertion / deletion
+//     anchors, mid-deletions, clipped N-skips): the exact kernel decides them;
+//   y bits 31 and 30 set: loci [x, x + (y & kPevLenMask)) hold MidDeletion elements of one D
+//     op whose MD deleted bases are all A/C/G/T (Alignment.scala:87-92: allele (MD base, "")).
+//     germline_proj counts them as one more allele; the other kernels treat them as complex.
 constexpr int32_t kSliceRowsMax = 2048;  // rows of one slice (its deepest column); deeper: pbad
 constexpr uint32_t kPevComplex = 0x80000000u;
+constexpr uint32_t kPevMidDel = 0x40000000u;
+constexpr uint32_t kPevLenMask = 0x3FFFFFFFu;
 constexpr uint32_t kPevNone = 7u << 4;  // a padding entry (no effect)
 
 // Packed per-read record of the germline column kernel (24 bytes, DMA'd into LDS per tile).

@@ -205,11 +205,13 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
 //   count   loci [ref_off, ref_off + len) are Match/Mismatch elements whose bases start at
 //           sequence offset seq_off;
 //   complex loci [ref_off, ref_off + len) hold an insertion / deletion anchor, mid-deletions
-//           or clipped (N) elements: the exact kernel decides them.
+//           or clipped (N) elements: the exact kernel decides them;
+//   middel  loci [ref_off, ref_off + len) of a D op whose MD deleted bases are all A/C/G/T:
+//           MidDeletion elements (counted by germline_proj, complex for the other kernels).
 // Returns false if the in-kernel path cannot take the read (P op, M bases past the sequence,
 // a deleted locus without its MD base, sizes beyond the packed fields): such reads keep the
 // exact walker, which raises the reference's error where it applies.
-constexpr uint32_t kSegCount = 0, kSegComplex = 1;
+constexpr uint32_t kSegCount = 0, kSegComplex = 1, kSegMidDel = 2;
 template <class Emit>
 __device__ bool general_segments(const DevReads &R, int64_t r, Emit emit) {
   const int32_t s = R.start[r], nmd = R.n_md[r], slen = R.seq_len[r], ncig = R.n_cigar[r];
@@ -236,12 +238,14 @@ __device__ bool general_segments(const DevReads &R, int64_t r, Emit emit) {
         if (first_ins) emit(kSegComplex, ra, 1, 0, nseg++);
         if (anchor && !(first_ins && rb - 1 == ra)) emit(kSegComplex, rb - 1, 1, 0, nseg++);
       } else {
+        bool std_bases = op == OP_D;
         if (op == OP_D)
           for (int32_t l = ra; l < rb; ++l) {
             while (k < nmd && (int32_t)(ev[k] >> 8) < l) ++k;
             if (k >= nmd || (int32_t)(ev[k] >> 8) != l) return false;
+            std_bases = std_bases && std_bit((uint8_t)(ev[k] & 0xFFu)) != 0u;
           }
-        emit(kSegComplex, ra, len, 0, nseg++);
+        emit(std_bases ? kSegMidDel : kSegComplex, ra, len, 0, nseg++);
       }
       ref += len;
     }
@@ -478,7 +482,8 @@ __global__ void pev_fill(DevReads R, const int64_t *__restrict__ eoff, uint2 *__
     for (int32_t q = 0; q < nseg; ++q) {
       const uint32_t a = sg[2 * q], b = sg[2 * q + 1];
       const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
-      if ((b >> 16) != kSegCount) pev[o++] = make_uint2((uint32_t)ra, kPevComplex | (uint32_t)rl);
+      if ((b >> 16) != kSegCount)
+        pev[o++] = make_uint2((uint32_t)ra, kPevComplex | ((b >> 16) == kSegMidDel ? kPevMidDel : 0u) | (uint32_t)rl);
       else if (o < o1) n_run(ra, rl, R.seq_off[r] + (int32_t)(b & 0xFFFFu));
     }
   } else if (o < o1) {

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       const int32_t l = (int32_t)p.x;
       if (p.y & kPevComplex) {
         const int64_t a = max((int64_t)l, (int64_t)B0);
-        const int64_t b = min((int64_t)l + (int64_t)(p.y & ~kPevComplex), (int64_t)B0 + T);
+        const int64_t b = min((int64_t)l + (int64_t)(p.y & kPevLenMask), (int64_t)B0 + T);  // mid-deletions too
         if (a < b) {
           atomicAdd(&mk[a - B0], 1u << 16);
           if (b < (int64_t)B0 + T) atomicAdd(&mk[b - B0], 0xFFFF0000u);
