@@ -56,6 +56,72 @@ __device__ __forceinline__ uint8_t allele_byte(const DevReads &R, const AlleleDe
   }
 }
 
+// An allele's bytes (ref then alt, little-endian in w) gathered with every load of the
+// allele issued together, instead of one dependent load chain per byte (allele_byte; a
+// deletion's bytes after the first each took an MD search).  ok = false when ref + alt is
+// longer than 13 bytes: callers then take allele_byte.
+struct AlleleBytes {
+  uint32_t w[4];
+  int rl, al;
+  bool ok;
+  // byte k of ref ++ alt (k a compile-time constant after unrolling: no indexed array)
+  __device__ __forceinline__ uint8_t byte(int k) const { return (uint8_t)(w[k >> 2] >> (8 * (k & 3))); }
+};
+__device__ __forceinline__ AlleleBytes allele_bytes(const DevReads &R, const AlleleDesc &d, int32_t pos) {
+  AlleleBytes a;
+  a.rl = allele_ref_len(d);
+  a.al = allele_alt_len(d);
+  a.w[0] = a.w[1] = a.w[2] = a.w[3] = 0;
+  const int n = a.rl + a.al;
+  a.ok = n <= 13;  // key_from's exact packing (longer alleles: allele_byte)
+  if (!a.ok) return a;
+  uint32_t b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = 0;
+  if (d.kind == K_SNV) {
+    b[0] = d.rb;
+    b[1] = d.base;
+  } else if (d.kind == K_MID) {
+    b[0] = d.base;
+  } else if (d.kind == K_INS) {
+    // ref: the anchor s[0] (when aux > 0), alt: s[0 .. aux); reads past the read's end stay
+    // inside the pool (its zeroed tail) and are masked off
+    const uint8_t *sq = R.seq + R.seq_off[d.read] + d.rp;
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = sq[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = i < n ? ((a.rl == 1 && i > 0) ? v[i - 1] : v[i]) : 0u;
+  } else if (d.kind == K_DEL) {
+    // ref: the pileup base, then the MD deleted bases at pos + 1 .. (consecutive events: one
+    // search, then one batch of loads); alt: the pileup base
+    const int64_t r = d.read;
+    const uint32_t *ev = R.md_ev + R.md_off[r];
+    const int32_t nmd = R.n_md[r], off = pos + 1 - R.start[r];
+    int lo = 0, hi = nmd;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((int32_t)(ev[mid] >> 8) < off) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t e[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) e[i] = nmd > 0 ? ev[min(lo + i, nmd - 1)] : 0u;
+    b[0] = d.rb;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) {
+      const bool hit = lo + i < nmd && (int32_t)(e[i] >> 8) == off + i;
+      if (1 + i < a.rl) b[1 + i] = hit ? (e[i] & 0xFFu) : (uint32_t)'?';
+    }
+#pragma unroll
+    for (int i = 1; i < 16; ++i)
+      if (i == a.rl) b[i] = d.rb;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a.w[i >> 2] |= (b[i] & 0xFFu) << (8 * (i & 3));
+  return a;
+}
+
 struct Key128 {
   uint64_t lo, hi;
 };
@@ -90,7 +156,23 @@ __device__ __forceinline__ Key128 key_from(int rl, int al, int sample, F byte) {
   }
   return k;
 }
+// kGather: the bytes through allele_bytes (one batch of loads; more registers)
+// key_from over gathered bytes, with every byte at a constant position (registers only)
+__device__ __forceinline__ Key128 key_from_bytes(const AlleleBytes &ab, int sample) {
+  Key128 k{0, 0};
+  const uint64_t lo = (uint64_t)ab.w[0] | ((uint64_t)ab.w[1] << 32), hi = (uint64_t)ab.w[2] | ((uint64_t)ab.w[3] << 32);
+  // key_from's exact packing (allele_bytes gathers n <= 13 only): lengths, sample, then the
+  // bytes from byte 3
+  k.lo = (uint64_t)(uint8_t)ab.rl | ((uint64_t)(uint8_t)ab.al << 8) | ((uint64_t)(uint8_t)sample << 16) | (lo << 24);
+  k.hi = (lo >> 40) | (hi << 24);
+  return k;
+}
+template <bool kGather = false>
 __device__ __forceinline__ Key128 allele_key(const DevReads &R, const AlleleDesc &d, int32_t pos, int sample) {
+  if constexpr (kGather) {
+    const AlleleBytes ab = allele_bytes(R, d, pos);
+    if (ab.ok) return key_from_bytes(ab, sample);
+  }
   return key_from(allele_ref_len(d), allele_alt_len(d), sample,
                   [&](int which, int i) { return allele_byte(R, d, pos, which, i); });
 }

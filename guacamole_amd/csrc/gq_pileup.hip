@@ -678,7 +678,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
   __shared__ int32_t cover_buf[kBlock / 64][kCover];
   int32_t *cover = cover_buf[threadIdx.x >> 6];
   // dbg & 32: phase clocks per item (cover, reference base, elements, decision + records, items)
-  uint64_t clk[5] = {0, 0, 0, 0, 0}, tk = 0;
+  uint64_t clk[6] = {0, 0, 0, 0, 0, 0}, tk = 0;
   auto tick = [&](int k) {
     if (dbg & 32) {
       const uint64_t t = __builtin_readcyclecounter();
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         act = false;
         smp = 0;
       }
-      if (act) key = allele_key(R, d, pos, smp);
+      if (act) key = allele_key<true>(R, d, pos, smp);
       add_batch(act, fr, d, smp, key);
     } else {
       for (int64_t k0 = 0; k0 < n_slots; k0 += 64) {
@@ -893,7 +893,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
             act = false;
             smp = 0;
           } else {
-            key = allele_key(R, d, pos, smp);
+            key = allele_key<true>(R, d, pos, smp);
           }
         }
         add_batch(act, r, d, smp, key);
@@ -1022,6 +1022,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       }
       continue;
     }
+    tick(5);
     // ---- pass 3: GermlineThreshold decision per sample (uniform serial code)
     const uint64_t ord = (uint64_t)(tl.ordinal0 + (pos - tl.L0));
     for (int sm = 0; sm < R.n_samples && sm < 8; ++sm) {
@@ -1089,25 +1090,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       const uint8_t fl = (tie ? GQ_FLAG_TIE : 0) | (ambiguous ? GQ_FLAG_AMBIGUOUS_REF : 0);
       if (lane == 0 && tie) atomicAdd(&ctr->ties, 1ull);
       // emit helper: alleles from descriptors, or symbolic "<ALT>" with an explicit ref
-      auto emit = [&](const AlleleDesc *a, uint8_t sym_ref_kind, const AlleleDesc *ref_src, uint8_t g0, uint8_t g1,
+      // (descriptors by value: a pointer into topd would put the array in scratch memory, one
+      //  global-latency load per field read)
+      auto emit = [&](const AlleleDesc a, uint8_t sym_ref_kind, const AlleleDesc ref_src, uint8_t g0, uint8_t g1,
                       int sub) {
         // sym_ref_kind: 0 => allele `a`; 1 => (refbase, <ALT>); 2 => (ref of ref_src, <ALT>)
         int rl, al;
         if (sym_ref_kind == 0) {
-          rl = allele_ref_len(*a);
-          al = allele_alt_len(*a);
+          rl = allele_ref_len(a);
+          al = allele_alt_len(a);
         } else if (sym_ref_kind == 1) {
           rl = 1;
           al = 5;
         } else {
-          rl = allele_ref_len(*ref_src);
+          rl = allele_ref_len(ref_src);
           al = 5;
         }
         auto byte_at = [&](int which, int i) -> uint8_t {
-          if (sym_ref_kind == 0) return allele_byte(R, *a, pos, which, i);
+          if (sym_ref_kind == 0) return allele_byte(R, a, pos, which, i);
           if (which == 1) return (uint8_t)"<ALT>"[i];
           if (sym_ref_kind == 1) return refbase;
-          return allele_byte(R, *ref_src, pos, 0, i);
+          return allele_byte(R, ref_src, pos, 0, i);
         };
         CallRec rr;
         rr.key = (ord << 12) | ((uint64_t)rank_sm << 4) | (uint64_t)sub;  // bySample order
@@ -1120,10 +1123,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         rr.ref_len = (uint16_t)rl;
         rr.alt_len = (uint16_t)al;
         if (rl + al <= 8) {
+          // lane i fetches byte i (one load chain for all of them, not one per byte: a
+          // deletion's bytes each take an MD search), then the bytes are packed by readlane
+          uint32_t bv = 0;
+          if (lane < rl + al) bv = byte_at(lane < rl ? 0 : 1, lane < rl ? lane : lane - rl);
           uint64_t v = 0;
-          int j = 0;
-          for (int i = 0; i < rl; ++i) v |= (uint64_t)byte_at(0, i) << (8 * j++);
-          for (int i = 0; i < al; ++i) v |= (uint64_t)byte_at(1, i) << (8 * j++);
+          for (int i = 0; i < rl + al; ++i) v |= (uint64_t)(uint8_t)__builtin_amdgcn_readlane((int)bv, i) << (8 * i);
           rr.allele = v;
         } else {
           unsigned long long off = 0;
@@ -1141,7 +1146,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         }
       };
       if (npass == 0) {
-        if (emit_no_call) emit(nullptr, 1, nullptr, GQ_GT_NOCALL, GQ_GT_NOCALL, 0);
+        if (emit_no_call) emit(AlleleDesc{}, 1, AlleleDesc{}, GQ_GT_NOCALL, GQ_GT_NOCALL, 0);
       } else {
         auto isvar = [&](const AlleleDesc &a) {  // Allele.isVariant: refBases != altBases
           const int rl = allele_ref_len(a), al = allele_alt_len(a);
@@ -1152,23 +1157,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         };
         const bool v1 = isvar(topd[0]);
         if (npass == 1 && !v1) {
-          if (emit_ref) emit(nullptr, 1, nullptr, GQ_GT_REF, GQ_GT_REF, 0);
+          if (emit_ref) emit(AlleleDesc{}, 1, AlleleDesc{}, GQ_GT_REF, GQ_GT_REF, 0);
         } else if (npass == 1) {
-          emit(&topd[0], 0, nullptr, GQ_GT_ALT, GQ_GT_ALT, 0);
+          emit(topd[0], 0, AlleleDesc{}, GQ_GT_ALT, GQ_GT_ALT, 0);
         } else {
           const bool v2 = isvar(topd[1]);
           const bool e1 = allele_alt_len(topd[0]) == 0, e2 = allele_alt_len(topd[1]) == 0;
           if ((!v1 || !v2) && (e1 != e2)) {
             // heterozygous deletion: no call (GermlineThresholdCaller.scala:146-149)
           } else if (v1 != v2) {
-            emit(v1 ? &topd[0] : &topd[1], 0, nullptr, GQ_GT_REF, GQ_GT_ALT, 0);
+            emit(v1 ? topd[0] : topd[1], 0, AlleleDesc{}, GQ_GT_REF, GQ_GT_ALT, 0);
           } else if (v1 && v2) {
-            emit(&topd[0], 0, nullptr, GQ_GT_ALT, GQ_GT_OTHERALT, 0);
-            emit(&topd[1], 0, nullptr, GQ_GT_ALT, GQ_GT_OTHERALT, 1);
+            emit(topd[0], 0, AlleleDesc{}, GQ_GT_ALT, GQ_GT_OTHERALT, 0);
+            emit(topd[1], 0, AlleleDesc{}, GQ_GT_ALT, GQ_GT_OTHERALT, 1);
           } else {
             const bool n1 = allele_ref_len(topd[0]) == 1 && allele_byte(R, topd[0], pos, 0, 0) == 'N';
             const bool n2 = allele_ref_len(topd[1]) == 1 && allele_byte(R, topd[1], pos, 0, 0) == 'N';
-            if (n1 || n2) emit(nullptr, 2, n1 ? &topd[1] : &topd[0], GQ_GT_REF, GQ_GT_REF, 0);
+            if (n1 || n2) emit(AlleleDesc{}, 2, n1 ? topd[1] : topd[0], GQ_GT_REF, GQ_GT_REF, 0);
             else raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_MULTI_REF, pos);
           }
         }
@@ -1177,7 +1182,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     tick(3);
   }
   if ((dbg & 32) && (threadIdx.x & 63) == 0 && clk[4])
-    for (int k = 0; k < 5; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2529,8 +2534,9 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   }
   if ((gq_dbg() & 32) && hc.prof[4])
     fprintf(stderr, "gq germline_complex prof (cycles/item/wave): cover %.0f reference-base %.0f elements %.0f "
-            "decision %.0f (%llu items)\n", (double)hc.prof[0] / hc.prof[4], (double)hc.prof[1] / hc.prof[4],
-            (double)hc.prof[2] / hc.prof[4], (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
+            "map-order %.0f decision %.0f (%llu items)\n", (double)hc.prof[0] / hc.prof[4],
+            (double)hc.prof[1] / hc.prof[4], (double)hc.prof[2] / hc.prof[4], (double)hc.prof[5] / hc.prof[4],
+            (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
   if ((gq_dbg() & 16) && hc.prof[5])
     fprintf(stderr,
             "gq prof (cycles/tile/wave): setup+entries %.0f counting %.0f - %.0f widen %.0f decision %.0f (%llu)\n",

@@ -354,9 +354,8 @@ def _region_counts(micro: LociMap, regions: Iterable[Tuple[str, np.ndarray, np.n
         last = np.searchsorted(rs, ends, side="left") - 1       # last entry with start < end
         hit = first <= last
         first, last = first[hit], last[hit]
-        diff = np.zeros(len(run_val) + 1, dtype=np.int64)
-        np.add.at(diff, run_id[first], 1)
-        np.add.at(diff, run_id[last] + 1, -1)
+        nr = len(run_val) + 1
+        diff = (np.bincount(run_id[first], minlength=nr) - np.bincount(run_id[last] + 1, minlength=nr)).astype(np.int64)
         counts_runs = np.cumsum(diff)[:-1]
         np.add.at(counts, run_val, counts_runs)
     return counts

@@ -101,8 +101,16 @@ class ReadSet:
     def regions(self):
         """(contig name, starts, ends) per contig, for partitionLociByApproximateDepth."""
         out = []
+        c = self.contig
+        if len(c) and bool(np.all(c[1:] >= c[:-1])):  # sorted by contig (the loaders' order): slices, no copies
+            bounds = np.searchsorted(c, np.arange(len(self.contig_names) + 1), side="left")
+            for ci, name in enumerate(self.contig_names):
+                a, b = int(bounds[ci]), int(bounds[ci + 1])
+                if b > a:
+                    out.append((name, self.start[a:b], self.end[a:b]))
+            return out
         for ci, name in enumerate(self.contig_names):
-            m = self.contig == ci
+            m = c == ci
             if m.any():
                 out.append((name, self.start[m], self.end[m]))
         return out
