@@ -1,0 +1,191 @@
+"""BAM reads decoded on the GPU (gqpileup.h: gq_bam_dev_*), for the callers' single pass.
+
+The host loader (``ingest.load_bam``: libgqingest, 16 host threads) inflates and decodes the
+BAM on the CPU, then ``soa.pack`` + ``Context.upload`` parse MD tags and copy the SoA to HBM.
+Here the compressed file is copied to HBM once, and the BGZF inflate, record parse, the
+loader's filters (Read.InputFilters, reads/Read.scala:95-122, :411-428), MD events and the SoA
+layout all run on the device.  The same rules give the same arrays, read for read
+(tests/test_gpu_bamdev.py compares every array with the host loader's).
+
+``load_reads_device`` returns a ``DeviceReadSet``: the host-side facts the commands use
+(contig dictionary, sample names, read count, read regions on demand) plus the resident
+read set, already in the ``commands.device_reads`` cache of its context.  It returns None
+where the host loader must run instead: a gzip stream without BGZF block sizes, or kept reads
+out of (contig, start) order (the host loader sorts them).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+import weakref
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import native, soa
+from .reads import InputFilters, ReadLoadError, _header_read_groups
+
+GQ_E_UNSORTED = 6
+GQ_E_BAM_IO = 11
+GQ_E_BAM_FORMAT = 12
+GQ_E_BAM_RECORD = 13
+GQ_E_MD_PARSE = 14
+GQ_E_NOT_BGZF = 15
+
+
+class gq_bam_dev_filters(C.Structure):
+    _fields_ = [("non_duplicate", C.c_int32), ("passed_vendor_quality_checks", C.c_int32),
+                ("is_paired", C.c_int32), ("has_md_tag", C.c_int32), ("use_loci", C.c_int32),
+                ("loci_begin", C.c_void_p), ("loci_start", C.c_void_p), ("loci_end", C.c_void_p),
+                ("n_rg", C.c_int32), ("rg_ids", C.c_char_p)]
+
+
+class gq_bam_dev_sizes(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("n_records", "n_reads", "seq_bytes", "cigar_len", "md_events", "comp_bytes",
+                                         "bam_bytes", "n_blocks")] + [
+        (k, C.c_float) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms")]
+
+
+class DeviceReadSet:
+    """A read set loaded straight into HBM: what the commands read on the host, and the
+    resident gq_dev_reads (``reads``)."""
+
+    def __init__(self, ctx: native.Context, reads: native.DeviceReads, contig_names: List[str],
+                 contig_lengths: List[int], sample_names: List[str], n: int, timings: Dict[str, float]):
+        self.contig_names = contig_names
+        self.contig_lengths = contig_lengths
+        self.sample_names = sample_names
+        self._n = n
+        self.reads = reads
+        self.timings = timings
+        self._pos = None
+        # commands.device_reads finds the resident set here (no host SoA to upload)
+        self._device = {id(ctx): (weakref.ref(ctx), reads)}
+
+    @property
+    def n(self) -> int:
+        return self._n
+
+    @property
+    def contig_lengths_map(self) -> Dict[str, int]:
+        return dict(zip(self.contig_names, self.contig_lengths))
+
+    def contig_index(self) -> Dict[str, int]:
+        return {c: i for i, c in enumerate(self.contig_names)}
+
+    def positions(self):
+        """(contig_read_begin, start, end) copied from HBM (once)."""
+        if self._pos is None:
+            L = native.lib()
+            begin = np.zeros(len(self.contig_names) + 1, np.int64)
+            start = np.empty(self._n, np.int32)
+            end = np.empty(self._n, np.int32)
+            native._check(L.gq_reads_contig_begin(self.reads.h, begin.ctypes.data))
+            if self._n:
+                native._check(L.gq_reads_positions(self.reads.h, start.ctypes.data, end.ctypes.data))
+            self._pos = (begin, start.astype(np.int64), end.astype(np.int64))
+        return self._pos
+
+    def regions(self):
+        """(contig name, starts, ends) per contig, for partitionLociByApproximateDepth."""
+        begin, start, end = self.positions()
+        return [(name, start[begin[i]:begin[i + 1]], end[begin[i]:begin[i + 1]])
+                for i, name in enumerate(self.contig_names) if begin[i + 1] > begin[i]]
+
+
+def download(reads: native.DeviceReads) -> Dict[str, np.ndarray]:
+    """Every SoA array of a resident read set, copied to the host (gq_reads_download)."""
+    L = native.lib()
+    info = native.gq_reads_info()
+    native._check(L.gq_reads_get_info(reads.h, C.byref(info)))
+    n, nc = int(info.n_reads), int(info.n_contigs)
+    arrs = dict(contig_read_begin=np.empty(nc + 1, np.int64), start=np.empty(n, np.int32),
+                end=np.empty(n, np.int32), pmax_end=np.empty(n, np.int32), mapq=np.empty(n, np.uint8),
+                flags=np.empty(n, np.uint8), sample=np.empty(n, np.uint8), seq_off=np.empty(n, np.int64),
+                seq_len=np.empty(n, np.int32), cigar_off=np.empty(n, np.int64), n_cigar=np.empty(n, np.int32),
+                md_off=np.empty(n, np.int64), n_md=np.empty(n, np.int32), n_mismatch=np.empty(n, np.uint16),
+                seq=np.empty(int(info.seq_bytes), np.uint8), qual=np.empty(int(info.seq_bytes), np.uint8),
+                cigar=np.empty(int(info.cigar_len), np.uint32), md_ev=np.empty(int(info.md_len), np.uint32),
+                sample_hash=np.zeros(int(info.n_samples), np.uint32),
+                n_contigs=np.int64(nc), n_samples=np.int64(info.n_samples))
+    s, _ = native.make_gq_reads(arrs)
+    native._check(L.gq_reads_download(reads.h, C.byref(s)))
+    return arrs
+
+
+def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = InputFilters()) -> Optional[DeviceReadSet]:
+    """BAM -> resident read set on ctx's GPU (None: the host loader must run, see the module
+    docstring).  Raises ReadLoadError / soa.MdParseError as the host loader does."""
+    L = native.lib()
+    t0 = time.perf_counter()
+    h = C.c_void_p()
+    rc = L.gq_bam_dev_open(ctx.h, path.encode(), C.byref(h))
+    if rc == GQ_E_NOT_BGZF:
+        return None
+    _raise(rc)
+    try:
+        t1 = time.perf_counter()
+        n_ref = L.gq_bam_dev_n_contigs(h)
+        names = [L.gq_bam_dev_contig_name(h, i).decode() for i in range(n_ref)]
+        lengths = [int(L.gq_bam_dev_contig_length(h, i)) for i in range(n_ref)]
+        text = L.gq_bam_dev_header_text(h).decode("utf-8", "replace")
+        rg_samples = _header_read_groups(text)  # ID -> SM (None: no SM), header order
+        rg_ids = list(rg_samples)
+        f = gq_bam_dev_filters(int(filters.non_duplicate), int(filters.passed_vendor_quality_checks),
+                               int(filters.is_paired), int(filters.has_md_tag), 0, None, None, None, len(rg_ids),
+                               b"".join(x.encode() + b"\0" for x in rg_ids) or None)
+        keep = []
+        if filters.overlaps_loci is not None:
+            loci = filters.overlaps_loci.result(dict(zip(names, lengths)))
+            begin, starts, ends = [0], [], []
+            for name in names:
+                for s, e in loci.on_contig(name).ranges:
+                    starts.append(s)
+                    ends.append(e)
+                begin.append(len(starts))
+            keep = [np.asarray(begin, np.int64), np.asarray(starts or [0], np.int64), np.asarray(ends or [0], np.int64)]
+            f.use_loci = 1
+            f.loci_begin, f.loci_start, f.loci_end = (a.ctypes.data for a in keep)
+        first = np.full(len(rg_ids) + 1, -1, np.int64)
+        z = gq_bam_dev_sizes()
+        _raise(L.gq_bam_dev_scan(h, C.byref(f), first.ctypes.data, C.byref(z)))
+        t2 = time.perf_counter()
+        # samples: RG -> SM (else "default"), numbered by first appearance in file order
+        samples: List[str] = []
+        class_sample = np.zeros(256, np.uint8)
+        for k in sorted(range(len(first)), key=lambda k: first[k]):
+            if first[k] < 0:
+                continue
+            name = (rg_samples[rg_ids[k]] if k < len(rg_ids) else None) or "default"
+            if name not in samples:
+                samples.append(name)
+            class_sample[k] = samples.index(name)
+        n_samples = max(1, len(samples))
+        sh = soa.sample_hashes(samples, n_samples)
+        out = C.c_void_p()
+        fill_ms = C.c_float()
+        rc = L.gq_bam_dev_reads(h, class_sample.ctypes.data, n_samples, sh.ctypes.data, C.byref(out), C.byref(fill_ms))
+        if rc == GQ_E_UNSORTED:
+            return None
+        _raise(rc)
+    finally:
+        L.gq_bam_dev_close(h)
+    dr = native.DeviceReads(ctx, out, None)
+    timings = {k: float(getattr(z, k)) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms")}
+    info = ctx.proj_stats(dr)
+    timings.update(fill_ms=float(fill_ms.value), derive_ms=float(info.get("derive_ms", 0.0)),
+                   open_s=t1 - t0, scan_s=t2 - t1, total_s=time.perf_counter() - t0,
+                   records=int(z.n_records), comp_bytes=int(z.comp_bytes), bam_bytes=int(z.bam_bytes),
+                   blocks=int(z.n_blocks))
+    return DeviceReadSet(ctx, dr, names, lengths, samples, int(z.n_reads), timings)
+
+
+def _raise(rc: int) -> None:
+    if rc == 0:
+        return
+    msg = native.lib().gq_last_error().decode()
+    if rc == GQ_E_MD_PARSE:
+        raise soa.MdParseError(msg)
+    if rc in (GQ_E_BAM_IO, GQ_E_BAM_FORMAT, GQ_E_BAM_RECORD):
+        raise ReadLoadError(msg)
+    raise native.GQError(rc, msg)

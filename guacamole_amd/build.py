@@ -10,7 +10,7 @@ PKG = os.path.join(ROOT, "guacamole_amd")
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "libgqpileup.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gq_pileup.hip", "gq_somatic.hip", "gq_heapref.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gq_pileup.hip", "gq_somatic.hip", "gq_heapref.hip", "gq_bamdev.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
     os.path.join(ROOT, "include", "gqpileup.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

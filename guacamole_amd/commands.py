@@ -32,7 +32,8 @@ from .distributed import (assign_tasks_to_ranks, gather_germline, gather_somatic
                           reads_overlapping)
 from .loci import (LociSet, LociSetBuilder, flatten_partitions, partition_loci_by_approximate_depth,
                    partition_loci_uniformly)
-from .reads import InputFilters, ReadSet, load_reads
+from .bamdev import DeviceReadSet, load_reads_device
+from .reads import InputFilters, ReadSet, is_bam, load_reads
 
 def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
     """Upload a ReadSet once per context and keep it resident for as long as the ReadSet lives
@@ -81,7 +82,9 @@ def task_count(parallelism: int, world: int = 1) -> int:
 def partition(loci: LociSet, parallelism: int, accuracy: int, *read_sets: ReadSet, world: int = 1):
     """DistributedUtil.partitionLociAccordingToArgs (DistributedUtil.scala:55-69)."""
     tasks = task_count(parallelism, world)
-    if accuracy == 0:
+    if accuracy == 0 or (tasks == 1 and loci.count > 0):
+        # one task takes every locus whatever the depths are (the map is the same; the
+        # read-region counts are only needed to cut loci between tasks)
         return partition_loci_uniformly(tasks, loci)
     return partition_loci_by_approximate_depth(tasks, loci, accuracy, *[r.regions() for r in read_sets])
 
@@ -199,6 +202,20 @@ def check_output_path(path: str) -> None:
                             "294-302), which this build does not produce; use a .vcf or .json path" % path)
 
 
+def device_ingest(args, *paths: str) -> bool:
+    """Decode these BAMs on the GPU (bamdev.load_reads_device) rather than with the host
+    loader: single-rank runs of BAM input without MD recomputation or contig lengths from
+    the reads (GQ_INGEST=host forces the host loader)."""
+    import os
+    if os.environ.get("GQ_INGEST", "device") == "host":
+        return False
+    if getattr(args, "recompute_md_tags", False) or getattr(args, "no_sequence_dictionary", False):
+        return False
+    if getattr(args, "reference_fasta", ""):
+        return False
+    return all(is_bam(p) for p in paths)
+
+
 def germline_threshold_main(argv: Sequence[str]) -> int:
     p = argparse.ArgumentParser(prog="germline-threshold",
                                 description="call variants by thresholding read counts (toy example)")
@@ -214,15 +231,22 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     builder = _loci_builder(args)
     # germline-threshold takes no reference (GermlineThresholdCaller.scala:64-70): with
     # --recompute-md-tags read loading fails (Read.scala:223-225)
-    rs = load_reads(args.reads, InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True),
-                    recompute_md=args.recompute_md_tags,
-                    contig_lengths_from_dictionary=not args.no_sequence_dictionary)
+    filters = InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True)
+    ctx = None
+    rs = None
+    if world == 1 and device_ingest(args, args.reads):
+        ctx = native.Context(args.device)
+        rs = load_reads_device(ctx, args.reads, filters)
+    if rs is None:
+        rs = load_reads(args.reads, filters, recompute_md=args.recompute_md_tags,
+                        contig_lengths_from_dictionary=not args.no_sequence_dictionary)
     clock.mark("load_reads")
     loci = builder.result(rs.contig_lengths_map)
     parts = partition(loci, args.parallelism, args.partition_accuracy, rs, world=world)
     flat = flatten_partitions(parts, rs.contig_index())
     clock.mark("partition")
-    ctx = native.Context(local if world > 1 else args.device)
+    if ctx is None:
+        ctx = native.Context(local if world > 1 else args.device)
     if world == 1:
         device_reads(ctx, rs)
         clock.mark("upload")
@@ -244,7 +268,9 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
     clock.mark("write")
     print("Called %d genotypes." % len(out), file=sys.stderr)
-    clock.report(reads=int(rs.n), genotypes=len(out), loci=int(loci.count))
+    clock.report(reads=int(rs.n), genotypes=len(out), loci=int(loci.count),
+                 ingest="device" if isinstance(rs, DeviceReadSet) else "host",
+                 device_ingest=getattr(rs, "timings", None))
     return _finish_rank(0)
 
 
@@ -281,15 +307,22 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     if args.reference_fasta:  # SomaticStandardCaller.scala:75
         from .reference import ReferenceGenome
         reference = ReferenceGenome.load_fasta(args.reference_fasta)
-    tumor, normal = [load_reads(path, f, reference=reference, recompute_md=args.recompute_md_tags,
+    ctx = None
+    sets = [None, None]
+    if world == 1 and device_ingest(args, args.tumor_reads, args.normal_reads):
+        ctx = native.Context(args.device)
+        sets = [load_reads_device(ctx, path, f) for path in (args.tumor_reads, args.normal_reads)]
+    tumor, normal = [s if s is not None else
+                     load_reads(path, f, reference=reference, recompute_md=args.recompute_md_tags,
                                 contig_lengths_from_dictionary=not args.no_sequence_dictionary)
-                     for path in (args.tumor_reads, args.normal_reads)]
+                     for s, path in zip(sets, (args.tumor_reads, args.normal_reads))]
     if tumor.contig_lengths_map != normal.contig_lengths_map:
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
     loci = builder.result(normal.contig_lengths_map)
     parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal, world=world)
     flat = flatten_partitions(parts, tumor.contig_index())
-    ctx = native.Context(local if world > 1 else args.device)
+    if ctx is None:
+        ctx = native.Context(local if world > 1 else args.device)
     if world > 1:
         rr = assign_tasks_to_ranks(flat, world, [tumor, normal], len(tumor.contig_names))
         tumor, flat = rank_share(tumor, flat, rr, rank)

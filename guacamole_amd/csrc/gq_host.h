@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstring>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -442,6 +444,83 @@ struct gq_dev_reads {
 };
 
 namespace gq {
+// H2D of large pageable host arrays at PCIe rate: a copy from pageable memory goes through the
+// runtime's own small bounce buffer (≈ 3 GB/s measured for the 4 GB bench shard); here the host
+// bytes are copied by several threads into one of two pinned 64 MiB chunks while the DMA engine
+// drains the other.
+struct H2DStager {
+  static constexpr size_t kChunk = size_t(64) << 20;
+  hipStream_t stream;
+  void *buf[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  bool used[2] = {false, false};
+  int slot = 0;
+  unsigned threads = 1;
+  explicit H2DStager(hipStream_t s) : stream(s) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    threads = std::min(16u, hw);  // the GPU box's CPU share is 16 threads
+  }
+  ~H2DStager() {
+    for (int i = 0; i < 2; ++i) {
+      if (done[i]) {
+        (void)hipEventSynchronize(done[i]);
+        (void)hipEventDestroy(done[i]);
+      }
+      if (buf[i]) (void)hipHostFree(buf[i]);
+    }
+  }
+  hipError_t init() {
+    for (int i = 0; i < 2; ++i) {
+      hipError_t e = hipHostMalloc(&buf[i], kChunk, hipHostMallocDefault);
+      if (e != hipSuccess) return e;
+      e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  // out[0, k) <- bytes [o, o + k) of the logical source, split over the threads
+  template <class F>
+  void fill(uint8_t *out, size_t o, size_t k, const F &src_range) const {
+    const unsigned t = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, k >> 22));  // >= 4 MiB / thread
+    if (t <= 1) {
+      src_range(out, o, k);
+      return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (k + t - 1) / t;
+    for (unsigned i = 0; i < t; ++i) {
+      const size_t a = (size_t)i * per;
+      if (a >= k) break;
+      th.emplace_back([&, a] { src_range(out + a, o + a, std::min(per, k - a)); });
+    }
+    for (auto &x : th) x.join();
+  }
+  template <class F>
+  hipError_t copy_from(void *dst, size_t bytes, const F &src_range) {
+    for (size_t o = 0; o < bytes; o += kChunk) {
+      const size_t k = std::min(kChunk, bytes - o);
+      if (used[slot]) {
+        hipError_t e = hipEventSynchronize(done[slot]);
+        if (e != hipSuccess) return e;
+      }
+      fill((uint8_t *)buf[slot], o, k, src_range);
+      hipError_t e = hipMemcpyAsync((char *)dst + o, buf[slot], k, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipEventRecord(done[slot], stream);
+      if (e != hipSuccess) return e;
+      used[slot] = true;
+      slot ^= 1;
+    }
+    return hipSuccess;
+  }
+  hipError_t copy(void *dst, const void *src, size_t bytes) {
+    return copy_from(dst, bytes, [src](uint8_t *out, size_t o, size_t k) { memcpy(out, (const uint8_t *)src + o, k); });
+  }
+};
+
+// Upload-time derivation of a resident read set whose SoA arrays (and host copy of
+// contig_read_begin) are in place: validation, read shape, projection pool, block index.
+gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
+
 // Loci ranges -> locus tiles of T loci with each tile's read window in `rd`, written to `tiles`.
 gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,
                int stage_cap = 0, int meta_cap = 0, int ev_cap = 0, bool aligned = false);

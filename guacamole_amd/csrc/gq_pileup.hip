@@ -1637,7 +1637,7 @@ static gq_status validate_reads(const gq_reads *h) {
   return GQ_OK;
 }
 
-static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
+static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   {  // contig_read_begin: 0, non-decreasing, n_reads (host copy)
     const auto &b = d->contig_read_begin;
     bool ok = !b.empty() && b.front() == 0 && b.back() == d->d.n_reads;
@@ -1855,82 +1855,6 @@ static gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   return GQ_OK;
 }
 
-extern "C++" {
-namespace {
-// H2D of large pageable host arrays at PCIe rate: a copy from pageable memory goes through the
-// runtime's own small bounce buffer (≈ 3 GB/s measured for the 4 GB bench shard); here the host
-// bytes are copied by several threads into one of two pinned 64 MiB chunks while the DMA engine
-// drains the other.
-struct H2DStager {
-  static constexpr size_t kChunk = size_t(64) << 20;
-  hipStream_t stream;
-  void *buf[2] = {nullptr, nullptr};
-  hipEvent_t done[2] = {nullptr, nullptr};
-  bool used[2] = {false, false};
-  int slot = 0;
-  unsigned threads = 1;
-  explicit H2DStager(hipStream_t s) : stream(s) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    threads = std::min(16u, hw);  // the GPU box's CPU share is 16 threads
-  }
-  ~H2DStager() {
-    for (int i = 0; i < 2; ++i) {
-      if (done[i]) {
-        (void)hipEventSynchronize(done[i]);
-        (void)hipEventDestroy(done[i]);
-      }
-      if (buf[i]) (void)hipHostFree(buf[i]);
-    }
-  }
-  hipError_t init() {
-    for (int i = 0; i < 2; ++i) {
-      hipError_t e = hipHostMalloc(&buf[i], kChunk, hipHostMallocDefault);
-      if (e != hipSuccess) return e;
-      e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
-  // out[0, k) <- bytes [o, o + k) of the logical source, split over the threads
-  template <class F>
-  void fill(uint8_t *out, size_t o, size_t k, const F &src_range) const {
-    const unsigned t = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, k >> 22));  // >= 4 MiB / thread
-    if (t <= 1) {
-      src_range(out, o, k);
-      return;
-    }
-    std::vector<std::thread> th;
-    const size_t per = (k + t - 1) / t;
-    for (unsigned i = 0; i < t; ++i) {
-      const size_t a = (size_t)i * per;
-      if (a >= k) break;
-      th.emplace_back([&, a] { src_range(out + a, o + a, std::min(per, k - a)); });
-    }
-    for (auto &x : th) x.join();
-  }
-  template <class F>
-  hipError_t copy_from(void *dst, size_t bytes, const F &src_range) {
-    for (size_t o = 0; o < bytes; o += kChunk) {
-      const size_t k = std::min(kChunk, bytes - o);
-      if (used[slot]) {
-        hipError_t e = hipEventSynchronize(done[slot]);
-        if (e != hipSuccess) return e;
-      }
-      fill((uint8_t *)buf[slot], o, k, src_range);
-      hipError_t e = hipMemcpyAsync((char *)dst + o, buf[slot], k, hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess) e = hipEventRecord(done[slot], stream);
-      if (e != hipSuccess) return e;
-      used[slot] = true;
-      slot ^= 1;
-    }
-    return hipSuccess;
-  }
-  hipError_t copy(void *dst, const void *src, size_t bytes) {
-    return copy_from(dst, bytes, [src](uint8_t *out, size_t o, size_t k) { memcpy(out, (const uint8_t *)src + o, k); });
-  }
-};
-}  // namespace
-}  // extern "C++"
 
 gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   if (!c || !out) return set_err(GQ_E_ARG, "gq_reads_upload: null argument");
@@ -2079,7 +2003,7 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   }
   const auto t1 = std::chrono::steady_clock::now();
   d->h2d_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-  gq_status st2 = derive_shape(c, d, h->md_len);
+  gq_status st2 = derive_shape_impl(c, d, h->md_len);
   d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
   if (st2) {
     gq_reads_free(d);
@@ -2130,7 +2054,7 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   }
   d->seq_bytes = h->seq_bytes;
   const auto t1 = std::chrono::steady_clock::now();
-  gq_status st2 = derive_shape(c, d, h->md_len);
+  gq_status st2 = derive_shape_impl(c, d, h->md_len);
   d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
   if (st2) {
     gq_reads_free(d);
@@ -2150,6 +2074,10 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->proj_reads = d->proj_reads;
   out->h2d_ms = d->h2d_ms;
   out->derive_ms = d->derive_ms;
+  out->cigar_len = d->d.cigar_len;
+  out->md_len = d->d.md_len;
+  out->n_contigs = d->d.n_contigs;
+  out->n_samples = d->d.n_samples;
   return GQ_OK;
 }
 
@@ -2817,3 +2745,5 @@ void gq_free_counts(gq_counts *r) {
 
 
 }  // extern "C"
+
+gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return derive_shape_impl(c, d, md_len); }

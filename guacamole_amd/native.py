@@ -100,7 +100,8 @@ class gq_timings(C.Structure):
 
 class gq_reads_info(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_rows")] + [
-        ("h2d_ms", C.c_float), ("derive_ms", C.c_float)]
+        ("h2d_ms", C.c_float), ("derive_ms", C.c_float), ("cigar_len", C.c_int64), ("md_len", C.c_int64),
+        ("n_contigs", C.c_int32), ("n_samples", C.c_int32)]
 
 
 class gq_somatic_params(C.Structure):
@@ -150,7 +151,9 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
             "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts",
-            "gq_vaf_histogram", "gq_germline_standard")
+            "gq_vaf_histogram", "gq_germline_standard", "gq_bam_dev_open", "gq_bam_dev_close", "gq_bam_dev_header_text",
+            "gq_bam_dev_n_contigs", "gq_bam_dev_contig_name", "gq_bam_dev_contig_length", "gq_bam_dev_scan",
+            "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin", "gq_reads_download")
 
 
 def lib():
@@ -193,6 +196,26 @@ def lib():
         L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
         L.gq_reads_free.argtypes = [C.c_void_p]
         L.gq_close.argtypes = [C.c_void_p]
+        vp = C.c_void_p
+        for f in ("gq_bam_dev_open", "gq_bam_dev_scan", "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin",
+                  "gq_reads_download"):
+            getattr(L, f).restype = C.c_int
+        L.gq_bam_dev_open.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
+        L.gq_bam_dev_close.argtypes = [vp]
+        L.gq_bam_dev_close.restype = None
+        L.gq_bam_dev_header_text.argtypes = [vp]
+        L.gq_bam_dev_header_text.restype = C.c_char_p
+        L.gq_bam_dev_n_contigs.argtypes = [vp]
+        L.gq_bam_dev_n_contigs.restype = C.c_int32
+        L.gq_bam_dev_contig_name.argtypes = [vp, C.c_int32]
+        L.gq_bam_dev_contig_name.restype = C.c_char_p
+        L.gq_bam_dev_contig_length.argtypes = [vp, C.c_int32]
+        L.gq_bam_dev_contig_length.restype = C.c_int64
+        L.gq_bam_dev_scan.argtypes = [vp, vp, vp, vp]
+        L.gq_bam_dev_reads.argtypes = [vp, vp, C.c_int32, vp, C.POINTER(vp), C.POINTER(C.c_float)]
+        L.gq_reads_positions.argtypes = [vp, vp, vp]
+        L.gq_reads_contig_begin.argtypes = [vp, vp]
+        L.gq_reads_download.argtypes = [vp, C.POINTER(gq_reads)]
         _lib = L
     return _lib
 

@@ -273,18 +273,24 @@ def load_reads(path: str, filters: InputFilters = InputFilters(), reference=None
         return rs
     if not contig_lengths_from_dictionary:
         return contig_lengths_from_reads(load_reads(path, filters))
+    if is_bam(path):
+        from .ingest import load_bam  # native (libgqingest); raises if not built
+        return load_bam(path, filters)
+    return _load_sam(path, filters)
+
+
+def is_bam(path: str) -> bool:
+    """A BGZF/gzip stream holding BAM (a damaged first block counts: the BAM decoder names
+    the fault); anything else is read as SAM text."""
     with open(path, "rb") as fh:
         head = fh.read(2)
-    if head == b"\x1f\x8b":  # BGZF (BAM) or a gzip-compressed SAM
-        try:
-            with gzip.open(path, "rb") as fh:
-                is_bam = fh.read(4) == b"BAM\x01"
-        except (OSError, EOFError, zlib.error):
-            is_bam = True  # a damaged first block: the BAM decoder names the fault
-        if is_bam:
-            from .ingest import load_bam  # native (libgqingest); raises if not built
-            return load_bam(path, filters)
-    return _load_sam(path, filters)
+    if head != b"\x1f\x8b":
+        return False
+    try:
+        with gzip.open(path, "rb") as fh:
+            return fh.read(4) == b"BAM\x01"
+    except (OSError, EOFError, zlib.error):
+        return True
 
 
 def contig_lengths_from_reads(rs: ReadSet) -> ReadSet:

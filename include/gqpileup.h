@@ -48,7 +48,13 @@ typedef enum {
   GQ_E_ARG = 7,             /* IllegalArgumentException (bad arguments / loci)             */
   GQ_E_HIP = 8,             /* device runtime error                                       */
   GQ_E_NOMEM = 9,
-  GQ_E_CAPACITY = 10        /* a per-locus table overflowed (distinct alleles > capacity)  */
+  GQ_E_CAPACITY = 10,       /* a per-locus table overflowed (distinct alleles > capacity)  */
+  /* gq_bam_dev_* (BAM decoded on the device), the host loader's gqi_status classes:          */
+  GQ_E_BAM_IO = 11,         /* open / stat / map failed                        (GQI_E_IO)     */
+  GQ_E_BAM_FORMAT = 12,     /* not BAM, corrupt BGZF block, truncated record   (GQI_E_FORMAT) */
+  GQ_E_BAM_RECORD = 13,     /* ReadLoadError: bad aux type, missing qualities  (GQI_E_RECORD) */
+  GQ_E_MD_PARSE = 14,       /* MdTag parse error (ADAM MdTag.apply)            (GQI_E_MD)     */
+  GQ_E_NOT_BGZF = 15        /* a gzip stream without BGZF block sizes: use the host loader    */
 } gq_status;
 
 /* CIGAR ops use BAM packing: len << 4 | op, op in M I D N S H P = X -> 0..8. */
@@ -198,8 +204,71 @@ typedef struct gq_reads_info {
   int64_t n_rows;    /* projection rows (64 bytes each: proj_bytes = 64 n_rows) */
   float h2d_ms;      /* gq_reads_upload: host wall time of the copies (pinned staging, PCIe) */
   float derive_ms;   /* gq_reads_upload / wrap: the upload-time derivation on the device    */
+  int64_t cigar_len, md_len;  /* pool sizes (CIGAR ops, MD events) */
+  int32_t n_contigs, n_samples;
 } gq_reads_info;
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
+
+/* ---- BAM decoded on the device ----------------------------------------------------------
+ * The host loader of gqingest.h (Read.loadReadRDDAndSequenceDictionaryFromBAM and its
+ * filters, reads/Read.scala:368-451 / :411-428; Read.fromSAMRecord :217-291;
+ * ReadSet.mappedReads ReadSet.scala:47-53; MappedRead.end :87; the MdTag of
+ * MappedRead.apply :114-131) with every step after the file read in HBM: the BGZF blocks are
+ * inflated on the device (CRC32 and ISIZE checked), record boundaries found there, each record
+ * parsed and filtered, MD tags turned into events, and the kept reads laid out as a resident
+ * gq_dev_reads.  The compressed file is the only host -> device copy.  Same rules, same
+ * arrays as gq_bam_open / gq_bam_scan / gq_bam_fill + gq_md_count / gq_md_fill + upload.
+ *   open  -> header (text, reference dictionary) on the host, inflated stream in HBM
+ *   scan  -> filters, sizes, the read-group classes' first kept records (the caller maps
+ *            read groups to samples, numbered by first appearance: Read.scala:233-237)
+ *   reads -> the resident read set (GQ_E_UNSORTED if the kept reads are not in (contig,
+ *            start) order: the host loader sorts such files)                               */
+typedef struct gq_bam_dev gq_bam_dev;
+
+gq_status gq_bam_dev_open(gq_ctx *ctx, const char *path, gq_bam_dev **out);
+void gq_bam_dev_close(gq_bam_dev *b);
+const char *gq_bam_dev_header_text(const gq_bam_dev *b); /* SAM text, trailing NULs stripped */
+int32_t gq_bam_dev_n_contigs(const gq_bam_dev *b);
+const char *gq_bam_dev_contig_name(const gq_bam_dev *b, int32_t i);
+int64_t gq_bam_dev_contig_length(const gq_bam_dev *b, int32_t i);
+
+typedef struct {
+  int32_t non_duplicate;   /* Read.InputFilters, as gqingest.h gq_bam_filters                   */
+  int32_t passed_vendor_quality_checks;
+  int32_t is_paired;
+  int32_t has_md_tag;
+  int32_t use_loci;
+  const int64_t *loci_begin; /* [n_contigs + 1] */
+  const int64_t *loci_start;
+  const int64_t *loci_end;
+  int32_t n_rg;            /* the header's @RG IDs: n_rg NUL-terminated strings back to back */
+  const char *rg_ids;
+} gq_bam_dev_filters;
+
+typedef struct {
+  int64_t n_records;       /* alignment records in the file */
+  int64_t n_reads;         /* kept                          */
+  int64_t seq_bytes, cigar_len, md_events;
+  int64_t comp_bytes, bam_bytes; /* compressed file / inflated stream */
+  int64_t n_blocks;        /* BGZF blocks                   */
+  float map_ms, h2d_ms, inflate_ms, records_ms, parse_ms;  /* open: map + block walk, copy, inflate; scan */
+} gq_bam_dev_sizes;
+
+/* rg_first[k] (k < n_rg): file-order index of the first kept record whose RG tag is header ID
+ * k; rg_first[n_rg]: of the first kept record without an RG tag or with an ID the header
+ * lacks (both are sample "default"); -1 where none.                                         */
+gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *f, int64_t *rg_first, gq_bam_dev_sizes *sizes);
+/* class_sample[k] (k <= n_rg): the sample slot of read-group class k; sample_hash as in
+ * gq_reads, may be NULL.  The handle is independent of b (b may be closed after).          */
+gq_status gq_bam_dev_reads(gq_bam_dev *b, const uint8_t *class_sample, int32_t n_samples,
+                           const uint32_t *sample_hash, gq_dev_reads **out, float *fill_ms);
+
+/* Copies out of a resident read set (host buffers of n_reads / n_contigs + 1 entries).      */
+gq_status gq_reads_positions(const gq_dev_reads *r, int32_t *start, int32_t *end);
+gq_status gq_reads_contig_begin(const gq_dev_reads *r, int64_t *out);
+/* The whole SoA of a resident read set copied into host buffers (dst's pointers, sized from
+ * gq_reads_info; a NULL pointer is skipped): the parity tests compare it with the host loader. */
+gq_status gq_reads_download(const gq_dev_reads *r, const gq_reads *dst);
 
 /* germline-threshold over the given loci partitions.                         */
 gq_status gq_germline_threshold(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,

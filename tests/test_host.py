@@ -43,6 +43,20 @@ def test_partition_by_depth():  # :77-94
     assert str(partition_loci_by_approximate_depth(2, loci, 100, reads.regions())) == "chr1:0-7=0,chr1:7-100=1"
 
 
+def test_partition_one_task_shortcut():
+    """commands.partition takes the uniform map for one task: the approximate-depth map of a
+    single task is the same map (every locus on task 0), so the region counts are skipped."""
+    from guacamole_amd.commands import partition
+    reads = make_read_set([make_read("A", "1M", "1", st) for st in (5, 6, 7, 8, 50)] +
+                          [make_read("AC", "2M", "2", st) for st in (3, 90)])
+    for spec in ("chr1:0-100,chr2:0-40,chr2:60-100", "chr1:5-6", "all"):
+        loci = LociSet.parse(spec).result({"chr1": 100, "chr2": 100})
+        for acc in (0, 1, 250):
+            want = partition_loci_by_approximate_depth(1, loci, max(acc, 1), reads.regions())
+            assert partition(loci, 1, acc, reads) == want
+            assert partition(loci, 0, acc, reads, world=1) == want
+
+
 # ---- LociSetSuite.scala:155-167 -----------------------------------------------------------
 def test_loci_set_strings():
     assert str(LociSet.parse("chr1:40-43").result().union(LociSet.parse("chr1:40-42").result())) == "chr1:40-43"
