@@ -262,13 +262,18 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     else:
         rows = germline_threshold_reads(ctx, rs, flat, args.threshold, args.emit_ref, args.emit_no_call)
     clock.mark("call")
-    from .output import germline_genotype
-    out = [germline_genotype(c, l, rs.sample_names[s] if s < len(rs.sample_names) else "default", gt, ref, alt)
-           for c, l, s, gt, ref, alt, fl in rows]
-    _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
+    from .output import germline_genotype, write_vcf_dir_germline
+    names = rs.sample_names
+    sample_name = lambda s: names[s] if s < len(names) else "default"  # noqa: E731
+    if args.out.lower().endswith(".vcf") and args.max_genotypes <= 1:
+        # the lines _write_genotypes writes for these records, without building the records
+        write_vcf_dir_germline(args.out, rows, sample_name, rs.contig_lengths_map)
+    else:
+        out = [germline_genotype(c, l, sample_name(s), gt, ref, alt) for c, l, s, gt, ref, alt, fl in rows]
+        _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
     clock.mark("write")
-    print("Called %d genotypes." % len(out), file=sys.stderr)
-    clock.report(reads=int(rs.n), genotypes=len(out), loci=int(loci.count),
+    print("Called %d genotypes." % len(rows), file=sys.stderr)
+    clock.report(reads=int(rs.n), genotypes=len(rows), loci=int(loci.count),
                  ingest="device" if isinstance(rs, DeviceReadSet) else "host",
                  device_ingest=getattr(rs, "timings", None))
     return _finish_rank(0)

@@ -57,6 +57,8 @@ enum : int { E_OK = 0, E_INFLATE = 1, E_SIZE = 2, E_CRC = 3 };
 __device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
+typedef uint32_t u32u __attribute__((aligned(1)));  // unaligned dword access (gfx950 global memory)
+
 __device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
 struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end
@@ -240,24 +242,44 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
       }
       if (dist > op || op + len > osz) return E_INFLATE;
       uint8_t *o = out + op;
-      const uint8_t *s = o - dist;
-      if (dist >= 8) {  // source bytes precede the chunk being written: 8 loads, then 8 stores
-        int i = 0;
-        for (; i + 8 <= len; i += 8) {
-          uint8_t t[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) t[k] = s[i + k];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[i + k] = t[k];
-        }
-        for (; i < len; ++i) o[i] = s[i];
-      } else {  // a period-`dist` pattern: read it once
+      const int64_t room = osz - op;  // bytes up to the block's end: chunks may over-store below it
+      int i = 0;
+      int d = dist;
+      if (d < 8) {  // a run of period d: its first bytes one by one, then chunks at a multiple of d >= 8
         uint64_t pat = 0;
-        for (int k = 0; k < dist; ++k) pat |= (uint64_t)s[k] << (8 * k);
-        int k = 0;
-        for (int i = 0; i < len; ++i) {
+        for (int k = 0; k < d; ++k) pat |= (uint64_t)o[k - d] << (8 * k);
+        const int first = min(len, d * ((8 + d - 1) / d));
+        for (int k = 0; i < first; ++i) {
           o[i] = (uint8_t)(pat >> (8 * k));
-          if (++k == dist) k = 0;
+          if (++k == d) k = 0;
+        }
+        d *= (8 + d - 1) / d;
+      }
+      if (d >= 32) {  // 32-byte chunks: every source byte precedes the chunk it lands in
+        for (; i < len; i += 32) {
+          if (i + 32 > room) {
+            for (; i < len; ++i) o[i] = o[i - d];
+            break;
+          }
+          const u32u *src = (const u32u *)(o + i - d);
+          uint32_t t[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[k] = src[k];
+          u32u *dst = (u32u *)(o + i);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dst[k] = t[k];
+        }
+      } else {  // 8 <= d < 32: 8-byte chunks
+        for (; i < len; i += 8) {
+          if (i + 8 > room) {
+            for (; i < len; ++i) o[i] = o[i - d];
+            break;
+          }
+          const u32u *src = (const u32u *)(o + i - d);
+          const uint32_t t0 = src[0], t1 = src[1];
+          u32u *dst = (u32u *)(o + i);
+          dst[0] = t0;
+          dst[1] = t1;
         }
       }
       op += len;

@@ -548,9 +548,11 @@ class GermlineCalls:
     def tuples(self, contig_names: Sequence[str]) -> List[tuple]:
         """(contig, locus, sample, (gt0, gt1), ref, alt, flags) — same shape as the oracle's rows."""
         a = self.a
-        return [(contig_names[a["contig"][i]], int(a["pos"][i]), int(a["sample"][i]),
-                 (GT_NAMES[int(a["gt0"][i])], GT_NAMES[int(a["gt1"][i])]), self.ref(i), self.alt(i),
-                 int(a["flags"][i])) for i in range(len(self))]
+        pool = self.pool
+        cols = [a[k].tolist() for k in ("contig", "pos", "sample", "gt0", "gt1", "ref_off", "ref_len", "alt_off",
+                                         "alt_len", "flags")]
+        return [(contig_names[c], p, s, (GT_NAMES[g0], GT_NAMES[g1]), pool[ro:ro + rl].decode("latin-1"),
+                 pool[ao:ao + al].decode("latin-1"), f) for c, p, s, g0, g1, ro, rl, ao, al, f in zip(*cols)]
 
 
 class SomaticCalls:

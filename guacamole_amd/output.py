@@ -193,30 +193,57 @@ def write_vcf_dir(path: str, genotypes: List[Dict], contig_lengths: Optional[Dic
 
 def write_vcf(path: str, genotypes: List[Dict], contig_lengths: Optional[Dict[str, int]] = None) -> None:
     """One VCF line per Genotype (VCF 4.1; POS is 1-based = start + 1) into the file `path`."""
-    samples: List[str] = []
-    for g in genotypes:
-        if g["sampleId"] not in samples:
-            samples.append(g["sampleId"])
+    def fields(g):
+        v = g["variant"]
+        fmt, vals = "GT", "/".join(GT_CODE.get(a, ".") for a in g["alleles"])
+        if "genotypeQuality" in g:
+            fmt += ":GQ:DP:AD"
+            vals += ":%d:%d:%d,%d" % (g["genotypeQuality"], g["readDepth"], g["referenceReadDepth"],
+                                       g["alternateReadDepth"])
+        return (v["contig"]["contigName"], v["start"], v["referenceAllele"], v["alternateAllele"], g["sampleId"],
+                fmt, vals)
+    _write_vcf_fields(path, [fields(g) for g in genotypes], contig_lengths)
+
+
+def write_vcf_dir_germline(path: str, rows, sample_name, contig_lengths: Optional[Dict[str, int]] = None) -> str:
+    """write_vcf_dir for germline-threshold rows (contig, locus, sample slot, (gt0, gt1), ref, alt, ...)
+    straight from the caller's columns: the lines write_vcf writes for their germline_genotype
+    records (GermlineThresholdCaller.scala:106-117 sets alleles, sample, variant only)."""
+    import os
+    os.makedirs(path, exist_ok=False)
+    part = os.path.join(path, VCF_PART)
+    gt = {(a, b): GT_CODE.get(a, ".") + "/" + GT_CODE.get(b, ".") for a in GT_CODE for b in GT_CODE}
+    _write_vcf_fields(part, [(c, l, ref, alt, sample_name(s), "GT", gt[g]) for c, l, s, g, ref, alt, *_ in rows],
+                      contig_lengths)
+    open(os.path.join(path, "_SUCCESS"), "w").close()
+    return part
+
+
+def _write_vcf_fields(path: str, recs, contig_lengths: Optional[Dict[str, int]]) -> None:
+    """recs: (contig, start, ref, alt, sampleId, FORMAT, values) per genotype, in output order."""
+    samples: Dict[str, int] = {}
+    for r in recs:
+        if r[4] not in samples:
+            samples[r[4]] = len(samples)
+    ns = len(samples)
+    out = ["##fileformat=VCFv4.1\n",
+           '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">\n',
+           '##FORMAT=<ID=GQ,Number=1,Type=Integer,Description="Genotype Quality">\n',
+           '##FORMAT=<ID=DP,Number=1,Type=Integer,Description="Read Depth">\n',
+           '##FORMAT=<ID=AD,Number=R,Type=Integer,Description="Allelic depths (ref, alt)">\n']
+    for c, ln in (contig_lengths or {}).items():
+        out.append("##contig=<ID=%s,length=%d>\n" % (c, ln))
+    out.append("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples) + "\n")
+    if ns == 1:
+        out.extend("%s\t%d\t.\t%s\t%s\t.\t.\t.\t%s\t%s\n" % (c, s + 1, ref, alt, fmt, vals)
+                   for c, s, ref, alt, _, fmt, vals in recs)
+    else:
+        for c, s, ref, alt, sid, fmt, vals in recs:
+            cols = ["."] * ns
+            cols[samples[sid]] = vals
+            out.append("%s\t%d\t.\t%s\t%s\t.\t.\t.\t%s\t%s\n" % (c, s + 1, ref, alt, fmt, "\t".join(cols)))
     with open(path, "w") as fh:
-        fh.write("##fileformat=VCFv4.1\n")
-        fh.write('##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">\n')
-        fh.write('##FORMAT=<ID=GQ,Number=1,Type=Integer,Description="Genotype Quality">\n')
-        fh.write('##FORMAT=<ID=DP,Number=1,Type=Integer,Description="Read Depth">\n')
-        fh.write('##FORMAT=<ID=AD,Number=R,Type=Integer,Description="Allelic depths (ref, alt)">\n')
-        for c, ln in (contig_lengths or {}).items():
-            fh.write("##contig=<ID=%s,length=%d>\n" % (c, ln))
-        fh.write("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples) + "\n")
-        for g in genotypes:
-            v = g["variant"]
-            fmt, vals = ["GT"], ["/".join(GT_CODE.get(a, ".") for a in g["alleles"])]
-            if "genotypeQuality" in g:
-                fmt += ["GQ", "DP", "AD"]
-                vals += [str(g["genotypeQuality"]), str(g["readDepth"]),
-                         "%d,%d" % (g["referenceReadDepth"], g["alternateReadDepth"])]
-            cols = ["."] * len(samples)
-            cols[samples.index(g["sampleId"])] = ":".join(vals)
-            fh.write("\t".join([v["contig"]["contigName"], str(v["start"] + 1), ".", v["referenceAllele"],
-                                v["alternateAllele"], ".", ".", ".", ":".join(fmt)] + cols) + "\n")
+        fh.write("".join(out))
 
 
 # ---- dbSNP annotation join ----------------------------------------------------------------

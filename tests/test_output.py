@@ -5,7 +5,7 @@ import pytest
 
 from guacamole_amd.output import (GENOTYPE_SCHEMA, VARIANT_SCHEMA, dbsnp_join, germline_genotype, java_float,
                                   read_avro_json, read_dbsnp_vcf, somatic_genotype, write_json, write_vcf,
-                                  write_vcf_dir)
+                                  write_vcf_dir, write_vcf_dir_germline)
 
 
 def test_vcf_lines(tmp_path):
@@ -20,6 +20,24 @@ def test_vcf_lines(tmp_path):
     assert body[1][-1] == "1/1"
     assert body[2][8] == "GT:GQ:DP:AD" and body[2][-1] == "0/1:42:50:40,10"
     assert g[2]["expectedAlleleDosage"] == 0.20000000298023224  # float32(10) / float32(50)
+
+
+def test_germline_vcf_writer_equals_record_writer(tmp_path):
+    """write_vcf_dir_germline (the CLI's germline path, rows straight from the call columns)
+    writes the bytes write_vcf_dir writes for the same germline_genotype records: one and
+    three samples, every allele pair, indels, an empty call list."""
+    names = ["s1", "s2", "default"]
+    gts = [("Ref", "Alt"), ("Alt", "Alt"), ("Alt", "OtherAlt"), ("Ref", "Ref"), ("NoCall", "NoCall")]
+    for samples in (1, 3):
+        rows = [("chrM" if i % 3 else "1", 10 * i, i % samples, gts[i % len(gts)], "ACGT"[i % 4],
+                 "ACGT"[(i + 1) % 4] + ("T" if i % 7 == 0 else ""), 0) for i in range(40)]
+        for rs in (rows, []):
+            a, b = tmp_path / ("a%d%d.vcf" % (samples, len(rs))), tmp_path / ("b%d%d.vcf" % (samples, len(rs)))
+            write_vcf_dir(str(a), [germline_genotype(c, l, names[s], gt, ref, alt) for c, l, s, gt, ref, alt, _ in rs],
+                          {"1": 5000, "chrM": 16571})
+            write_vcf_dir_germline(str(b), rs, lambda s: names[s], {"1": 5000, "chrM": 16571})
+            assert (a / "part-r-00000").read_bytes() == (b / "part-r-00000").read_bytes()
+            assert (b / "_SUCCESS").exists()
 
 
 def _records(text):
