@@ -492,7 +492,33 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
             "roofline": {"bound": "hbm", "kernel": "somatic_proj", "kernel_ms": k_ms, "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes},
+            "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), workload),
             "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s}
+
+
+CALLER_PMC = os.path.join(ROOT, "profiles", "r03_h2_somatic_call_pmc.csv")
+
+
+def caller_roofline(call_ms: float, workload: str):
+    """The exact somatic caller (somatic_call_k<false>) is FP64 VALU work behind dependent loads.
+    Its issue roofline: VALU wave-instructions per launch (PMC of the same chr1 configs[2] launch,
+    CALLER_PMC, by scripts/profile_somatic.sh) over this run's kernel time, against the chip's
+    VALU issue rate (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, the convention of
+    DESIGN.md's PMC readings); the wait share says what bounds it instead."""
+    if "chr1" not in workload or not os.path.exists(CALLER_PMC) or call_ms <= 0:
+        return None
+    import csv
+    pm = {r["counter"]: float(r["mean_per_launch"]) for r in csv.DictReader(open(CALLER_PMC))}
+    insts = pm.get("SQ_INSTS_VALU")
+    if not insts:
+        return None
+    peak = 1024 * 2.4e9 / 2
+    ach = insts / (call_ms * 1e-3)
+    return {"bound": "issue/latency", "kernel": "somatic_call_k<false>", "kernel_ms": call_ms,
+            "valu_wave_insts_per_launch": insts, "achieved": ach, "peak": peak, "unit": "wave-instr/s",
+            "frac": ach / peak,
+            "wait_frac": pm.get("SQ_WAIT_ANY", 0.0) / max(1.0, pm.get("SQ_WAVE_CYCLES", 1.0)),
+            "source": os.path.relpath(CALLER_PMC, ROOT)}
 
 
 if __name__ == "__main__":

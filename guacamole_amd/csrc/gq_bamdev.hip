@@ -3,7 +3,7 @@
 // The host loader (gq_ingest.cpp) spends its time inflating BGZF blocks and walking records;
 // here the compressed file is the only host -> device copy and everything after it runs on
 // the device:
-//   bgzf_inflate   thread / BGZF block: DEFLATE (RFC 1951) into the block's place in one
+//   bgzf_inflate   thread / BGZF block (Huffman tables in LDS): DEFLATE (RFC 1951) into the block's place in one
 //                  inflated stream (offsets from the blocks' ISIZE footers, known on the host)
 //   bgzf_crc       thread / block: CRC32 of the inflated bytes against the footer
 //   rec_sync       wave / block: the first offset in the block that chains into 8 more
@@ -45,11 +45,18 @@ struct BgzfBlock {
   uint32_t isize, crc, pad;
 };
 
-constexpr int kLitBits = 10, kDistBits = 8;
-// per-thread inflate scratch (global): primary tables, canonical counts / symbols, lengths
-constexpr int kLitTab = 0, kDistTab = kLitTab + (1 << kLitBits), kLCount = kDistTab + (1 << kDistBits),
-              kLSym = kLCount + 16, kDCount = kLSym + 288, kDSym = kDCount + 16, kTabEnd = kDSym + 32;
-constexpr int kScratchBytes = 4096;  // kTabEnd u16 + 320 + 19 length bytes
+// Huffman decoding: each lane's primary tables live in LDS, lane-minor (entry k of lane l at
+// [k][l]): 8-bit literal/length codes (u16 entries: symbol << 4 | length) and 7-bit distance /
+// code-length codes (u8 entries: symbol << 3 | length); 0 marks a longer code, which continues
+// canonically from its first table-width bits with the lane's counts in global scratch.  A
+// 64-lane workgroup takes 40 KiB, so four share a CU and every block of a 3.6 GB stream
+// (55 k blocks, 861 workgroups) is decoded at once.
+constexpr int kInfLanes = 64, kLitBits = 8, kDistBits = 7;
+// per-lane global scratch (u16 units): per code (literal/length, distance): counts, first
+// canonical code and first symbol index per length, symbols; then the code lengths (bytes)
+constexpr int kLCount = 0, kLFirst = 16, kLIndex = 32, kLSym = 48, kDCount = kLSym + 288, kDFirst = kDCount + 16,
+              kDIndex = kDFirst + 16, kDSym = kDIndex + 16, kTabEnd = kDSym + 32;
+constexpr int kScratchBytes = 1536;
 static_assert(kTabEnd * 2 + 352 <= kScratchBytes, "inflate scratch");
 
 enum : int { E_OK = 0, E_INFLATE = 1, E_SIZE = 2, E_CRC = 3 };
@@ -91,67 +98,82 @@ struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer
   }
 };
 
-// canonical Huffman code from lengths: counts, symbols by (length, value), primary table of
-// `tb` bits indexed by the next stream bits (entry = symbol << 4 | length; 0: longer code)
-__device__ bool huff_build(const uint8_t *len, int n, uint16_t *count, uint16_t *sym, uint16_t *tab, int tb) {
-  for (int l = 0; l < 16; ++l) count[l] = 0;
-  for (int s = 0; s < n; ++s) count[len[s]]++;
-  count[0] = 0;
+struct Code {  // one canonical code of a lane: global counts / first codes / indexes / symbols
+  uint16_t *count, *first, *index, *sym;
+};
+
+// canonical Huffman code from lengths: counts, first codes and indexes per length, symbols by
+// (length, value), and the primary table (stride kInfLanes) of `tb` bits indexed by the next
+// stream bits; entries T(symbol, length), 0 where the code is longer
+template <class E, int kShift>
+__device__ bool huff_build(const uint8_t *len, int n, Code c, E *tab, int tb) {
+  uint16_t cnt[16];
+  for (int l = 0; l < 16; ++l) cnt[l] = 0;
+  for (int s = 0; s < n; ++s) cnt[len[s]]++;
+  cnt[0] = 0;
   int left = 1;
   for (int l = 1; l < 16; ++l) {
-    left = (left << 1) - count[l];
+    left = (left << 1) - cnt[l];
     if (left < 0) return false;  // over-subscribed
   }
   uint16_t offs[16];
-  offs[1] = 0;
-  for (int l = 1; l < 15; ++l) offs[l + 1] = offs[l] + count[l];
-  for (int s = 0; s < n; ++s)
-    if (len[s]) sym[offs[len[s]]++] = (uint16_t)s;
-  for (int k = 0; k < (1 << tb); ++k) tab[k] = 0;
   int code = 0, idx = 0;
+  for (int l = 0; l < 16; ++l) {
+    c.count[l] = cnt[l];
+    c.first[l] = (uint16_t)code;
+    c.index[l] = (uint16_t)idx;
+    offs[l] = (uint16_t)idx;
+    idx += cnt[l];
+    code = (code + cnt[l]) << 1;
+  }
+  for (int s = 0; s < n; ++s)
+    if (len[s]) c.sym[offs[len[s]]++] = (uint16_t)s;
+  for (int k = 0; k < (1 << tb); ++k) tab[k * kInfLanes] = 0;
+  code = 0;
+  idx = 0;
   for (int l = 1; l <= tb; ++l) {
-    for (int j = 0; j < count[l]; ++j, ++code) {
-      const uint16_t s = sym[idx++];
+    for (int j = 0; j < cnt[l]; ++j, ++code) {
+      const int s = c.sym[idx++];
       const int rev = (int)(__builtin_bitreverse32((uint32_t)code) >> (32 - l));
-      for (int k = rev; k < (1 << tb); k += 1 << l) tab[k] = (uint16_t)((s << 4) | l);
+      for (int k = rev; k < (1 << tb); k += 1 << l) tab[k * kInfLanes] = (E)((s << kShift) | l);
     }
     code <<= 1;
   }
   return true;
 }
 
-// a code longer than the primary table: bit by bit from its first bit (RFC 1951 §3.2.2)
-__device__ int huff_slow(BitIn &in, const uint16_t *count, const uint16_t *sym) {
-  int code = 0, first = 0, index = 0;
-  for (int l = 1; l < 16; ++l) {
-    code |= (int)in.get(1);
-    const int c = count[l];
-    if (code - c < first) return sym[index + (code - first)];
-    index += c;
-    first += c;
-    first <<= 1;
-    code <<= 1;
+// a code longer than the primary table: its first tb bits (stream order) reversed into code
+// order, then one bit per length (RFC 1951 §3.2.2)
+__device__ __noinline__ int huff_long(BitIn &in, Code c, int tb) {
+  in.need(tb);
+  int code = (int)(__builtin_bitreverse32((uint32_t)(in.bb & ((1u << tb) - 1))) >> (32 - tb));
+  in.drop(tb);
+  for (int l = tb + 1; l < 16; ++l) {
+    code = (code << 1) | (int)in.get(1);
+    const int f = c.first[l], k = c.count[l];
+    if (code - f < k) return c.sym[c.index[l] + code - f];
   }
   return -1;
 }
 
-__device__ __forceinline__ int huff_decode(BitIn &in, const uint16_t *tab, int tb, const uint16_t *count,
-                                           const uint16_t *sym) {
+template <class E, int kShift>
+__device__ __forceinline__ int huff_decode(BitIn &in, const E *tab, int tb, Code c) {
   in.need(16);
-  const uint32_t e = tab[in.bb & ((1u << tb) - 1)];
+  const uint32_t e = tab[(in.bb & ((1u << tb) - 1)) * kInfLanes];
   if (e) {
-    in.drop((int)(e & 15));
-    return (int)(e >> 4);
+    in.drop((int)(e & ((1u << kShift) - 1)));
+    return (int)(e >> kShift);
   }
-  return huff_slow(in, count, sym);
+  return huff_long(in, c, tb);
 }
 
 // one BGZF block's raw DEFLATE stream -> out[0, isize); E_OK or an error
-__device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBlock &b, uint8_t *out, uint16_t *S) {
+__device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBlock &b, uint8_t *out, uint16_t *S,
+                           uint16_t *lt, uint8_t *dt) {
   uint8_t *lens = (uint8_t *)(S + kTabEnd);
   uint8_t *cl = lens + 320;
-  uint16_t *lt = S + kLitTab, *dt = S + kDistTab, *lc = S + kLCount, *ls = S + kLSym, *dc = S + kDCount,
-           *ds = S + kDSym;
+  const Code lc{S + kLCount, S + kLFirst, S + kLIndex, S + kLSym};
+  const Code dc{S + kDCount, S + kDFirst, S + kDIndex, S + kDSym};
   BitIn in;
   in.init(comp, b.in_off, comp_len);
   const int64_t osz = b.isize;
@@ -175,20 +197,20 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
     if (type == 3) return E_INFLATE;
     if (type == 1) {  // fixed codes
       for (int s = 0; s < 288; ++s) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-      huff_build(lens, 288, lc, ls, lt, kLitBits);
+      huff_build<uint16_t, 4>(lens, 288, lc, lt, kLitBits);
       for (int s = 0; s < 30; ++s) lens[s] = 5;
-      huff_build(lens, 30, dc, ds, dt, kDistBits);
+      huff_build<uint8_t, 3>(lens, 30, dc, dt, kDistBits);
     } else {  // dynamic codes
       const int hlit = (int)in.get(5) + 257, hdist = (int)in.get(5) + 1, hclen = (int)in.get(4) + 4;
       if (hlit > 286 || hdist > 30) return E_INFLATE;
       const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
       for (int k = 0; k < 19; ++k) cl[k] = 0;
       for (int k = 0; k < hclen; ++k) cl[order[k]] = (uint8_t)in.get(3);
-      // the code-length code goes in the distance table's place (7-bit primary table)
-      if (!huff_build(cl, 19, dc, ds, dt, 7)) return E_INFLATE;
+      // the code-length code (lengths <= 7) in the distance table's place
+      if (!huff_build<uint8_t, 3>(cl, 19, dc, dt, kDistBits)) return E_INFLATE;
       int i = 0;
       while (i < hlit + hdist) {
-        const int s = huff_decode(in, dt, 7, dc, ds);
+        const int s = huff_decode<uint8_t, 3>(in, dt, kDistBits, dc);
         if (s < 0) return E_INFLATE;
         if (s < 16) {
           lens[i++] = (uint8_t)s;
@@ -209,11 +231,11 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
         for (int k = 0; k < rep; ++k) lens[i++] = v;
       }
       if (lens[256] == 0) return E_INFLATE;
-      if (!huff_build(lens, hlit, lc, ls, lt, kLitBits)) return E_INFLATE;
-      if (!huff_build(lens + hlit, hdist, dc, ds, dt, kDistBits)) return E_INFLATE;
+      if (!huff_build<uint16_t, 4>(lens, hlit, lc, lt, kLitBits)) return E_INFLATE;
+      if (!huff_build<uint8_t, 3>(lens + hlit, hdist, dc, dt, kDistBits)) return E_INFLATE;
     }
     for (;;) {  // symbols
-      int sym = huff_decode(in, lt, kLitBits, lc, ls);
+      int sym = huff_decode<uint16_t, 4>(in, lt, kLitBits, lc);
       if (sym < 256) {
         if (sym < 0 || op >= osz) return E_INFLATE;
         out[op++] = (uint8_t)sym;
@@ -231,7 +253,7 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
         const int ex = (sym - 4) >> 2;
         len = ((4 + (sym & 3)) << ex) + 3 + (int)in.get(ex);
       }
-      const int dsym = huff_decode(in, dt, kDistBits, dc, ds);
+      const int dsym = huff_decode<uint8_t, 3>(in, dt, kDistBits, dc);
       if (dsym < 0 || dsym >= 30) return E_INFLATE;
       int dist;
       if (dsym < 4) {
@@ -289,15 +311,16 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
   return op == osz ? E_OK : E_SIZE;
 }
 
-__global__ void __launch_bounds__(128) bgzf_inflate(const uint8_t *comp, int64_t comp_len, const BgzfBlock *blk, int64_t n_blk,
-                                                    uint8_t *out, uint16_t *scratch, int64_t n_slots, int *status) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_slots) return;
-  uint16_t *S = scratch + t * (kScratchBytes / 2);
-  for (int64_t b = t; b < n_blk; b += n_slots) {
-    const BgzfBlock k = blk[b];
-    status[b] = inflate_one(comp, comp_len, k, out + k.out_off, S);
-  }
+__global__ void __launch_bounds__(kInfLanes) bgzf_inflate(const uint8_t *comp, int64_t comp_len,
+                                                          const BgzfBlock *blk, int64_t n_blk, uint8_t *out,
+                                                          uint16_t *scratch, int *status) {
+  __shared__ uint16_t lt[(1 << kLitBits) * kInfLanes];
+  __shared__ uint8_t dt[(1 << kDistBits) * kInfLanes];
+  const int64_t b = (int64_t)blockIdx.x * kInfLanes + threadIdx.x;
+  if (b >= n_blk) return;
+  const BgzfBlock k = blk[b];
+  status[b] = inflate_one(comp, comp_len, k, out + k.out_off, scratch + b * (kScratchBytes / 2), lt + threadIdx.x,
+                          dt + threadIdx.x);
 }
 
 __global__ void __launch_bounds__(256) bgzf_crc(const uint8_t *out, const BgzfBlock *blk, int64_t n_blk, int *status) {
@@ -887,14 +910,13 @@ gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
   HIP_TRY(b->out.ensure((size_t)outn + 64));
   HIP_TRY(hipMemsetAsync((uint8_t *)b->out.p + outn, 0, 64, c->stream));
   {
-    const int64_t slots = std::min<int64_t>(std::max<int64_t>(nb, 1), 1 << 17);
     DevBuf scratch, status;
-    HIP_TRY(scratch.ensure((size_t)slots * kScratchBytes));
+    HIP_TRY(scratch.ensure((size_t)std::max<int64_t>(nb, 1) * kScratchBytes));
     HIP_TRY(status.ensure(sizeof(int) * (size_t)std::max<int64_t>(nb, 1)));
     if (nb) {
-      hipLaunchKernelGGL(bgzf_inflate, dim3(grid(slots, 128)), dim3(128), 0, c->stream, (const uint8_t *)b->comp.p,
-                         n + 64, (const BgzfBlock *)b->blk.p, nb, (uint8_t *)b->out.p, (uint16_t *)scratch.p, slots,
-                         (int *)status.p);
+      hipLaunchKernelGGL(bgzf_inflate, dim3(grid(nb, kInfLanes)), dim3(kInfLanes), 0, c->stream,
+                         (const uint8_t *)b->comp.p, n + 64, (const BgzfBlock *)b->blk.p, nb, (uint8_t *)b->out.p,
+                         (uint16_t *)scratch.p, (int *)status.p);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(bgzf_crc, dim3(grid(nb, 256)), dim3(256), 0, c->stream, (const uint8_t *)b->out.p,
                          (const BgzfBlock *)b->blk.p, nb, (int *)status.p);
