@@ -102,49 +102,68 @@ struct Code {  // one canonical code of a lane: global counts / first codes / in
   uint16_t *count, *first, *index, *sym;
 };
 
+// 16 per-length 16-bit counters in four registers (no dynamically indexed arrays: those live in
+// scratch memory, and a lane's slow build would stall its whole wave)
+struct Pack16 {
+  uint64_t w[4] = {0, 0, 0, 0};
+  __device__ __forceinline__ uint32_t get(int l) const {
+    const uint64_t x = l < 4 ? w[0] : l < 8 ? w[1] : l < 12 ? w[2] : w[3];
+    return (uint32_t)(x >> (16 * (l & 3))) & 0xFFFF;
+  }
+  __device__ __forceinline__ void add(int l, uint32_t v) {
+    const uint64_t d = (uint64_t)v << (16 * (l & 3));
+    if (l < 4) w[0] += d;
+    else if (l < 8) w[1] += d;
+    else if (l < 12) w[2] += d;
+    else w[3] += d;
+  }
+};
+
 // canonical Huffman code from lengths: counts, first codes and indexes per length, symbols by
-// (length, value), and the primary table (stride kInfLanes) of `tb` bits indexed by the next
-// stream bits; entries T(symbol, length), 0 where the code is longer
+// (length, value) (for codes longer than the table), and the primary table (stride
+// kInfLanes) of `tb` bits indexed by the next stream bits; entries (symbol << kShift) |
+// length, 0 where the code is longer
 template <class E, int kShift>
 __device__ bool huff_build(const uint8_t *len, int n, Code c, E *tab, int tb) {
-  uint16_t cnt[16];
-  for (int l = 0; l < 16; ++l) cnt[l] = 0;
-  for (int s = 0; s < n; ++s) cnt[len[s]]++;
-  cnt[0] = 0;
+  Pack16 cnt;
+  for (int s = 0; s < n; ++s) cnt.add(len[s], 1);
   int left = 1;
   for (int l = 1; l < 16; ++l) {
-    left = (left << 1) - cnt[l];
+    left = (left << 1) - (int)cnt.get(l);
     if (left < 0) return false;  // over-subscribed
   }
-  uint16_t offs[16];
+  Pack16 next, offs;  // next canonical code / next symbol slot per length
   int code = 0, idx = 0;
-  for (int l = 0; l < 16; ++l) {
-    c.count[l] = cnt[l];
+  for (int l = 1; l < 16; ++l) {
+    const int k = (int)cnt.get(l);
+    c.count[l] = (uint16_t)k;
     c.first[l] = (uint16_t)code;
     c.index[l] = (uint16_t)idx;
-    offs[l] = (uint16_t)idx;
-    idx += cnt[l];
-    code = (code + cnt[l]) << 1;
+    next.add(l, (uint32_t)code);
+    offs.add(l, (uint32_t)idx);
+    idx += k;
+    code = (code + k) << 1;
   }
-  for (int s = 0; s < n; ++s)
-    if (len[s]) c.sym[offs[len[s]]++] = (uint16_t)s;
   for (int k = 0; k < (1 << tb); ++k) tab[k * kInfLanes] = 0;
-  code = 0;
-  idx = 0;
-  for (int l = 1; l <= tb; ++l) {
-    for (int j = 0; j < cnt[l]; ++j, ++code) {
-      const int s = c.sym[idx++];
-      const int rev = (int)(__builtin_bitreverse32((uint32_t)code) >> (32 - l));
+  for (int s = 0; s < n; ++s) {
+    const int l = len[s];
+    if (!l) continue;
+    const int o = (int)offs.get(l);
+    offs.add(l, 1);
+    c.sym[o] = (uint16_t)s;
+    if (l <= tb) {
+      const int cd = (int)next.get(l);
+      const int rev = (int)(__builtin_bitreverse32((uint32_t)cd) >> (32 - l));
       for (int k = rev; k < (1 << tb); k += 1 << l) tab[k * kInfLanes] = (E)((s << kShift) | l);
     }
-    code <<= 1;
+    next.add(l, 1);
   }
   return true;
 }
 
 // a code longer than the primary table: its first tb bits (stream order) reversed into code
 // order, then one bit per length (RFC 1951 §3.2.2)
-__device__ __noinline__ int huff_long(BitIn &in, Code c, int tb) {
+__device__ __forceinline__ int huff_long(BitIn &in, Code c, int tb) {
   in.need(tb);
   int code = (int)(__builtin_bitreverse32((uint32_t)(in.bb & ((1u << tb) - 1))) >> (32 - tb));
   in.drop(tb);
@@ -203,9 +222,11 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
     } else {  // dynamic codes
       const int hlit = (int)in.get(5) + 257, hdist = (int)in.get(5) + 1, hclen = (int)in.get(4) + 4;
       if (hlit > 286 || hdist > 30) return E_INFLATE;
-      const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+      // RFC 1951 code-length order {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15},
+      // 5 bits per entry (a constant array indexed by a lane value would go to scratch memory)
+      const uint64_t ordA = 0x22caa324e804a30ull, ordB = 0x3c2e1346cull;
       for (int k = 0; k < 19; ++k) cl[k] = 0;
-      for (int k = 0; k < hclen; ++k) cl[order[k]] = (uint8_t)in.get(3);
+      for (int k = 0; k < hclen; ++k) cl[(k < 12 ? ordA >> (5 * k) : ordB >> (5 * (k - 12))) & 31] = (uint8_t)in.get(3);
       // the code-length code (lengths <= 7) in the distance table's place
       if (!huff_build<uint8_t, 3>(cl, 19, dc, dt, kDistBits)) return E_INFLATE;
       int i = 0;
