@@ -113,17 +113,69 @@ def download(reads: native.DeviceReads) -> Dict[str, np.ndarray]:
     return arrs
 
 
-def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = InputFilters()) -> Optional[DeviceReadSet]:
+class MappedBam:
+    """A BAM file mapped on the host with its BGZF block table (gq_bam_dev_map): the part of
+    the device load that needs no GPU, so it can run while the context starts.  None-like
+    (``ok`` False) for a plain gzip stream."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.h = C.c_void_p()
+        self.t = time.perf_counter()
+        rc = native.lib().gq_bam_dev_map(path.encode(), C.byref(self.h))
+        self.ok = rc != GQ_E_NOT_BGZF
+        if self.ok:
+            _raise(rc)
+
+    def close(self) -> None:
+        if self.h:
+            native.lib().gq_bam_dev_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def map_bams(paths) -> Dict[str, object]:
+    """MappedBam per path, on a host thread (ctypes releases the GIL in the native calls):
+    start it, create the GPU context, then join().  join() returns {path: MappedBam} or raises
+    what the mapping raised."""
+    import threading
+    box: Dict[str, object] = {}
+
+    def run():
+        try:
+            box["maps"] = {p: MappedBam(p) for p in paths}
+        except BaseException as e:  # re-raised by join
+            box["err"] = e
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+
+    def join():
+        th.join()
+        if "err" in box:
+            raise box["err"]
+        return box["maps"]
+    return {"join": join}
+
+
+def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = InputFilters(),
+                      mapped: Optional[MappedBam] = None) -> Optional[DeviceReadSet]:
     """BAM -> resident read set on ctx's GPU (None: the host loader must run, see the module
-    docstring).  Raises ReadLoadError / soa.MdParseError as the host loader does."""
+    docstring).  Raises ReadLoadError / soa.MdParseError as the host loader does.  `mapped`:
+    the file already mapped (map_bams), else it is mapped here."""
     L = native.lib()
-    t0 = time.perf_counter()
-    h = C.c_void_p()
-    rc = L.gq_bam_dev_open(ctx.h, path.encode(), C.byref(h))
-    if rc == GQ_E_NOT_BGZF:
+    m = mapped if mapped is not None and (mapped.h or not mapped.ok) else MappedBam(path)  # (a used mapping: again)
+    if not m.ok:
         return None
-    _raise(rc)
+    t0 = m.t
+    h, m.h = m.h, C.c_void_p()  # the handle now belongs to this load
     try:
+        _raise(L.gq_bam_dev_load(ctx.h, h))
         t1 = time.perf_counter()
         n_ref = L.gq_bam_dev_n_contigs(h)
         names = [L.gq_bam_dev_contig_name(h, i).decode() for i in range(n_ref)]

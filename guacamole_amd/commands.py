@@ -32,7 +32,7 @@ from .distributed import (assign_tasks_to_ranks, gather_germline, gather_somatic
                           reads_overlapping)
 from .loci import (LociSet, LociSetBuilder, flatten_partitions, partition_loci_by_approximate_depth,
                    partition_loci_uniformly)
-from .bamdev import DeviceReadSet, load_reads_device
+from .bamdev import DeviceReadSet, load_reads_device, map_bams
 from .reads import InputFilters, ReadSet, is_bam, load_reads
 
 def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
@@ -235,8 +235,9 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     ctx = None
     rs = None
     if world == 1 and device_ingest(args, args.reads):
+        maps = map_bams([args.reads])  # the file mapped on a host thread while the context starts
         ctx = native.Context(args.device)
-        rs = load_reads_device(ctx, args.reads, filters)
+        rs = load_reads_device(ctx, args.reads, filters, maps["join"]()[args.reads])
     if rs is None:
         rs = load_reads(args.reads, filters, recompute_md=args.recompute_md_tags,
                         contig_lengths_from_dictionary=not args.no_sequence_dictionary)
@@ -315,8 +316,10 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     ctx = None
     sets = [None, None]
     if world == 1 and device_ingest(args, args.tumor_reads, args.normal_reads):
+        maps = map_bams([args.tumor_reads, args.normal_reads])
         ctx = native.Context(args.device)
-        sets = [load_reads_device(ctx, path, f) for path in (args.tumor_reads, args.normal_reads)]
+        mapped = maps["join"]()
+        sets = [load_reads_device(ctx, path, f, mapped[path]) for path in (args.tumor_reads, args.normal_reads)]
     tumor, normal = [s if s is not None else
                      load_reads(path, f, reference=reference, recompute_md=args.recompute_md_tags,
                                 contig_lengths_from_dictionary=not args.no_sequence_dictionary)

@@ -68,22 +68,30 @@ typedef uint32_t u32u __attribute__((aligned(1)));  // unaligned dword access (g
 
 __device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
-struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end
-  const uint32_t *w, *wend;
+struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end.  The next
+                // word is loaded one refill ahead, so its latency overlaps the symbols between
+  const uint32_t *w, *wend;  // w: the word after `nw`
   uint64_t bb;
+  uint32_t nw;
   int bc;
+  __device__ __forceinline__ uint32_t fetch() {
+    const uint32_t v = w < wend ? *w : 0u;
+    ++w;
+    return v;
+  }
   __device__ void init(const uint8_t *base, int64_t off, int64_t base_len) {
     wend = (const uint32_t *)(base + (base_len & ~int64_t(3)));
     w = (const uint32_t *)(base + (off & ~int64_t(3)));
     const int sk = (int)(off & 3);
-    bb = (uint64_t)(*w++ >> (8 * sk));
+    bb = (uint64_t)(fetch() >> (8 * sk));
     bc = 32 - 8 * sk;
+    nw = fetch();
   }
   __device__ __forceinline__ void need(int n) {  // n <= 32
     if (bc < n) {
-      bb |= (uint64_t)(w < wend ? *w : 0u) << bc;
-      ++w;
+      bb |= (uint64_t)nw << bc;
       bc += 32;
+      nw = fetch();
     }
   }
   __device__ __forceinline__ void drop(int n) {
@@ -98,8 +106,13 @@ struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer
   }
 };
 
-struct Code {  // one canonical code of a lane: global counts / first codes / indexes / symbols
-  uint16_t *count, *first, *index, *sym;
+// one canonical code of a lane: its symbols by (length, value) in global scratch, and for the
+// lengths past the primary table, (limit << 16 | (index - first) & 0xFFFF) in registers (a code
+// of length l is its symbol sym[code + index - first] when code < limit = first + count)
+template <int kTb>
+struct Code {
+  uint16_t *sym;
+  uint32_t lb[15 - kTb];
 };
 
 // 16 per-length 16-bit counters in four registers (no dynamically indexed arrays: those live in
@@ -123,8 +136,9 @@ struct Pack16 {
 // (length, value) (for codes longer than the table), and the primary table (stride
 // kInfLanes) of `tb` bits indexed by the next stream bits; entries (symbol << kShift) |
 // length, 0 where the code is longer
-template <class E, int kShift>
-__device__ bool huff_build(const uint8_t *len, int n, Code c, E *tab, int tb) {
+template <class E, int kShift, int kTb>
+__device__ bool huff_build(const uint8_t *len, int n, Code<kTb> &c, E *tab) {
+  constexpr int tb = kTb;
   Pack16 cnt;
   for (int s = 0; s < n; ++s) cnt.add(len[s], 1);
   int left = 1;
@@ -134,11 +148,10 @@ __device__ bool huff_build(const uint8_t *len, int n, Code c, E *tab, int tb) {
   }
   Pack16 next, offs;  // next canonical code / next symbol slot per length
   int code = 0, idx = 0;
+#pragma unroll
   for (int l = 1; l < 16; ++l) {
     const int k = (int)cnt.get(l);
-    c.count[l] = (uint16_t)k;
-    c.first[l] = (uint16_t)code;
-    c.index[l] = (uint16_t)idx;
+    if (l > tb) c.lb[l - tb - 1] = ((uint32_t)(code + k) << 16) | ((uint32_t)(idx - code) & 0xFFFFu);
     next.add(l, (uint32_t)code);
     offs.add(l, (uint32_t)idx);
     idx += k;
@@ -161,29 +174,31 @@ __device__ bool huff_build(const uint8_t *len, int n, Code c, E *tab, int tb) {
   return true;
 }
 
-// a code longer than the primary table: its first tb bits (stream order) reversed into code
-// order, then one bit per length (RFC 1951 §3.2.2)
-__device__ __forceinline__ int huff_long(BitIn &in, Code c, int tb) {
-  in.need(tb);
-  int code = (int)(__builtin_bitreverse32((uint32_t)(in.bb & ((1u << tb) - 1))) >> (32 - tb));
-  in.drop(tb);
-  for (int l = tb + 1; l < 16; ++l) {
-    code = (code << 1) | (int)in.get(1);
-    const int f = c.first[l], k = c.count[l];
-    if (code - f < k) return c.sym[c.index[l] + code - f];
+// a code longer than the primary table: its first kTb bits (stream order) reversed into code
+// order, then one bit per length (RFC 1951 §3.2.2) against the register limits
+template <int kTb>
+__device__ __forceinline__ int huff_long(BitIn &in, const Code<kTb> &c) {
+  in.need(16);
+  int code = (int)(__builtin_bitreverse32((uint32_t)(in.bb & ((1u << kTb) - 1))) >> (32 - kTb));
+  in.drop(kTb);
+#pragma unroll
+  for (int j = 0; j < 15 - kTb; ++j) {
+    code = (code << 1) | (int)(in.bb & 1);
+    in.drop(1);
+    if (code < (int)(c.lb[j] >> 16)) return c.sym[code + (int)(int16_t)(c.lb[j] & 0xFFFF)];
   }
   return -1;
 }
 
-template <class E, int kShift>
-__device__ __forceinline__ int huff_decode(BitIn &in, const E *tab, int tb, Code c) {
+template <class E, int kShift, int kTb>
+__device__ __forceinline__ int huff_decode(BitIn &in, const E *tab, const Code<kTb> &c) {
   in.need(16);
-  const uint32_t e = tab[(in.bb & ((1u << tb) - 1)) * kInfLanes];
+  const uint32_t e = tab[(in.bb & ((1u << kTb) - 1)) * kInfLanes];
   if (e) {
     in.drop((int)(e & ((1u << kShift) - 1)));
     return (int)(e >> kShift);
   }
-  return huff_long(in, c, tb);
+  return huff_long<kTb>(in, c);
 }
 
 // one BGZF block's raw DEFLATE stream -> out[0, isize); E_OK or an error
@@ -191,8 +206,10 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
                            uint16_t *lt, uint8_t *dt) {
   uint8_t *lens = (uint8_t *)(S + kTabEnd);
   uint8_t *cl = lens + 320;
-  const Code lc{S + kLCount, S + kLFirst, S + kLIndex, S + kLSym};
-  const Code dc{S + kDCount, S + kDFirst, S + kDIndex, S + kDSym};
+  Code<kLitBits> lc;
+  Code<kDistBits> dc;
+  lc.sym = S + kLSym;
+  dc.sym = S + kDSym;
   BitIn in;
   in.init(comp, b.in_off, comp_len);
   const int64_t osz = b.isize;
@@ -200,7 +217,7 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
   const int64_t in_bits = (int64_t)b.in_len * 8;
   const uint32_t *w0 = (const uint32_t *)(comp + (b.in_off & ~int64_t(3)));
   const int sk = (int)(b.in_off & 3);
-  auto used_bits = [&]() -> int64_t { return (int64_t)(in.w - w0) * 32 - in.bc - 8 * sk; };
+  auto used_bits = [&]() -> int64_t { return (int64_t)(in.w - w0 - 1) * 32 - in.bc - 8 * sk; };
   int final_blk = 0;
   do {
     if (used_bits() > in_bits) return E_INFLATE;
@@ -216,9 +233,9 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
     if (type == 3) return E_INFLATE;
     if (type == 1) {  // fixed codes
       for (int s = 0; s < 288; ++s) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-      huff_build<uint16_t, 4>(lens, 288, lc, lt, kLitBits);
+      huff_build<uint16_t, 4, kLitBits>(lens, 288, lc, lt);
       for (int s = 0; s < 30; ++s) lens[s] = 5;
-      huff_build<uint8_t, 3>(lens, 30, dc, dt, kDistBits);
+      huff_build<uint8_t, 3, kDistBits>(lens, 30, dc, dt);
     } else {  // dynamic codes
       const int hlit = (int)in.get(5) + 257, hdist = (int)in.get(5) + 1, hclen = (int)in.get(4) + 4;
       if (hlit > 286 || hdist > 30) return E_INFLATE;
@@ -228,10 +245,10 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
       for (int k = 0; k < 19; ++k) cl[k] = 0;
       for (int k = 0; k < hclen; ++k) cl[(k < 12 ? ordA >> (5 * k) : ordB >> (5 * (k - 12))) & 31] = (uint8_t)in.get(3);
       // the code-length code (lengths <= 7) in the distance table's place
-      if (!huff_build<uint8_t, 3>(cl, 19, dc, dt, kDistBits)) return E_INFLATE;
+      if (!huff_build<uint8_t, 3, kDistBits>(cl, 19, dc, dt)) return E_INFLATE;
       int i = 0;
       while (i < hlit + hdist) {
-        const int s = huff_decode<uint8_t, 3>(in, dt, kDistBits, dc);
+        const int s = huff_decode<uint8_t, 3, kDistBits>(in, dt, dc);
         if (s < 0) return E_INFLATE;
         if (s < 16) {
           lens[i++] = (uint8_t)s;
@@ -252,11 +269,11 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
         for (int k = 0; k < rep; ++k) lens[i++] = v;
       }
       if (lens[256] == 0) return E_INFLATE;
-      if (!huff_build<uint16_t, 4>(lens, hlit, lc, lt, kLitBits)) return E_INFLATE;
-      if (!huff_build<uint8_t, 3>(lens + hlit, hdist, dc, dt, kDistBits)) return E_INFLATE;
+      if (!huff_build<uint16_t, 4, kLitBits>(lens, hlit, lc, lt)) return E_INFLATE;
+      if (!huff_build<uint8_t, 3, kDistBits>(lens + hlit, hdist, dc, dt)) return E_INFLATE;
     }
     for (;;) {  // symbols
-      int sym = huff_decode<uint16_t, 4>(in, lt, kLitBits, lc);
+      int sym = huff_decode<uint16_t, 4, kLitBits>(in, lt, lc);
       if (sym < 256) {
         if (sym < 0 || op >= osz) return E_INFLATE;
         out[op++] = (uint8_t)sym;
@@ -274,7 +291,7 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
         const int ex = (sym - 4) >> 2;
         len = ((4 + (sym & 3)) << ex) + 3 + (int)in.get(ex);
       }
-      const int dsym = huff_decode<uint8_t, 3>(in, dt, kDistBits, dc);
+      const int dsym = huff_decode<uint8_t, 3, kDistBits>(in, dt, dc);
       if (dsym < 0 || dsym >= 30) return E_INFLATE;
       int dist;
       if (dsym < 4) {
@@ -869,13 +886,11 @@ gq_status d2h_i64(gq_ctx *c, const void *src, int64_t *dst) {
 
 extern "C" {
 
-gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
-  if (!c || !path || !out) return set_err(GQ_E_ARG, "gq_bam_dev_open: null argument");
+gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) {
+  if (!path || !out) return set_err(GQ_E_ARG, "gq_bam_dev_map: null argument");
   *out = nullptr;
-  HIP_TRY(hipSetDevice(c->device));
   auto t0 = std::chrono::steady_clock::now();
   std::unique_ptr<gq_bam_dev> b(new gq_bam_dev());
-  b->ctx = c;
   b->fd = open(path, O_RDONLY);
   if (b->fd < 0) return set_err(GQ_E_BAM_IO, "cannot open %s", path);
   struct stat st;
@@ -912,6 +927,36 @@ gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
   z.bam_bytes = outn;
   z.n_blocks = nb;
   z.map_ms = ms_since(t0);
+  *out = b.release();
+  return GQ_OK;
+}
+
+gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
+  if (!c || !path || !out) return set_err(GQ_E_ARG, "gq_bam_dev_open: null argument");
+  gq_bam_dev *m = nullptr;
+  gq_status st = gq_bam_dev_map(path, &m);
+  if (st) return st;
+  st = gq_bam_dev_load(c, m);
+  if (st) {
+    gq_bam_dev_close(m);
+    return st;
+  }
+  *out = m;
+  return GQ_OK;
+}
+
+gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
+  if (!c || !mapped) return set_err(GQ_E_ARG, "gq_bam_dev_load: null argument");
+  if (mapped->ctx) return set_err(GQ_E_ARG, "gq_bam_dev_load: already loaded");
+  HIP_TRY(hipSetDevice(c->device));
+  gq_bam_dev *b = mapped;
+  b->ctx = c;
+  const uint8_t *p = b->map;
+  const int64_t n = (int64_t)b->map_len;
+  const int64_t outn = b->n_out;
+  const int64_t nb = (int64_t)b->blocks.size();
+  gq_bam_dev_sizes &z = b->sizes;
+  auto t0 = std::chrono::steady_clock::now();
   // the file -> HBM (pinned chunks filled by host threads while the DMA drains the other)
   t0 = std::chrono::steady_clock::now();
   HIP_TRY(b->comp.ensure((size_t)n + 64));
@@ -998,7 +1043,6 @@ gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
     }
     b->rec0 = o;
   }
-  *out = b.release();
   return GQ_OK;
 }
 

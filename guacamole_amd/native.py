@@ -153,7 +153,8 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts",
             "gq_vaf_histogram", "gq_germline_standard", "gq_bam_dev_open", "gq_bam_dev_close", "gq_bam_dev_header_text",
             "gq_bam_dev_n_contigs", "gq_bam_dev_contig_name", "gq_bam_dev_contig_length", "gq_bam_dev_scan",
-            "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin", "gq_reads_download")
+            "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin", "gq_reads_download", "gq_bam_dev_map",
+            "gq_bam_dev_load")
 
 
 def lib():
@@ -201,6 +202,10 @@ def lib():
                   "gq_reads_download"):
             getattr(L, f).restype = C.c_int
         L.gq_bam_dev_open.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
+        L.gq_bam_dev_map.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.gq_bam_dev_map.restype = C.c_int
+        L.gq_bam_dev_load.argtypes = [vp, vp]
+        L.gq_bam_dev_load.restype = C.c_int
         L.gq_bam_dev_close.argtypes = [vp]
         L.gq_bam_dev_close.restype = None
         L.gq_bam_dev_header_text.argtypes = [vp]

@@ -226,6 +226,10 @@ gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 typedef struct gq_bam_dev gq_bam_dev;
 
 gq_status gq_bam_dev_open(gq_ctx *ctx, const char *path, gq_bam_dev **out);
+/* gq_bam_dev_open in two steps: map (host only: the file and its BGZF block table; may run
+ * while the device context starts) and load (copy, inflate, header) on a context.           */
+gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out);
+gq_status gq_bam_dev_load(gq_ctx *ctx, gq_bam_dev *mapped);
 void gq_bam_dev_close(gq_bam_dev *b);
 const char *gq_bam_dev_header_text(const gq_bam_dev *b); /* SAM text, trailing NULs stripped */
 int32_t gq_bam_dev_n_contigs(const gq_bam_dev *b);

@@ -26,3 +26,28 @@ def test_ingest_library_exports_every_declared_symbol():
     L = ingest.lib()
     missing = [s for s in declared if not hasattr(L, s)]
     assert not missing, missing
+
+
+def test_bam_map_on_the_host(tmp_path):
+    """gq_bam_dev_map (the host half of the device BAM load: file map + BGZF block table) needs
+    no GPU: BAM -> mapped, plain gzip -> not BGZF (the host loader's case), errors as ReadLoadError."""
+    import gzip
+    import pytest
+    from guacamole_amd import bamdev
+    from guacamole_amd.reads import ReadLoadError
+    from conftest import fixture
+    m = bamdev.MappedBam(fixture("chrM.sorted.bam"))
+    assert m.ok and m.h
+    m.close()
+    g = tmp_path / "plain.gz"
+    with gzip.open(g, "wb") as fh:
+        fh.write(b"BAM\1" + b"\0" * 100)
+    assert not bamdev.MappedBam(str(g)).ok
+    with pytest.raises(ReadLoadError):
+        bamdev.MappedBam(str(tmp_path / "missing.bam"))
+    bad = tmp_path / "bad.bam"
+    bad.write_bytes(b"not a bam at all" * 10)
+    with pytest.raises(ReadLoadError):
+        bamdev.MappedBam(str(bad))
+    joined = bamdev.map_bams([fixture("chrM.sorted.bam")])["join"]()
+    assert joined[fixture("chrM.sorted.bam")].ok
