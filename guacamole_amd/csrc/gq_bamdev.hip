@@ -48,10 +48,12 @@ struct BgzfBlock {
 // Huffman decoding: each lane's primary tables live in LDS, lane-minor (entry k of lane l at
 // [k][l]): 8-bit literal/length codes (u16 entries: symbol << 4 | length) and 7-bit distance /
 // code-length codes (u8 entries: symbol << 3 | length); 0 marks a longer code, which continues
-// canonically from its first table-width bits with the lane's counts in global scratch.  A
-// 64-lane workgroup takes 40 KiB, so four share a CU and every block of a 3.6 GB stream
-// (55 k blocks, 861 workgroups) is decoded at once.
-constexpr int kInfLanes = 64, kLitBits = 8, kDistBits = 7;
+// canonically from its first table-width bits against per-length limits in registers.  A
+// workgroup is one wave with 32 lanes (blocks) active: 20 KiB of tables, and the 55 k blocks of
+// a 3.6 GB stream make 1,720 waves, ~1.7 per SIMD, so two waves' dependent loads overlap and a
+// wave waits on the slowest of 32 lanes, not 64 (measured: 64 lanes 127 ms, 32 lanes 103 ms,
+// 16 lanes 120 ms for the chr20 30x BAM).
+constexpr int kInfLanes = 32, kLitBits = 8, kDistBits = 7;  // lanes (blocks) per wave: see above
 // per-lane global scratch (u16 units): per code (literal/length, distance): counts, first
 // canonical code and first symbol index per length, symbols; then the code lengths (bytes)
 constexpr int kLCount = 0, kLFirst = 16, kLIndex = 32, kLSym = 48, kDCount = kLSym + 288, kDFirst = kDCount + 16,
