@@ -30,6 +30,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gq_host.h"
@@ -856,13 +857,14 @@ struct gq_bam_dev {
   std::vector<std::string> names;
   std::vector<int64_t> lengths;
   DevBuf comp, blk, out;  // compressed file, block table, inflated stream
+  DevBuf scratch, status;  // inflate: per-block code tables and status
   // last scan
   DevBuf rec, info, kidx, seq_o, cig_o, md_o;
   int64_t n_rec = 0, n_keep = 0, seq_bytes = 0, cigar_len = 0, md_events = 0;
   bool scanned = false;
   gq_bam_dev_sizes sizes{};
   ~gq_bam_dev() {
-    for (DevBuf *b : {&comp, &blk, &out, &rec, &info, &kidx, &seq_o, &cig_o, &md_o}) b->release();
+    for (DevBuf *b : {&comp, &blk, &out, &scratch, &status, &rec, &info, &kidx, &seq_o, &cig_o, &md_o}) b->release();
     if (map) munmap(const_cast<uint8_t *>(map), map_len);
     if (fd >= 0) close(fd);
   }
@@ -959,8 +961,21 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
   const int64_t nb = (int64_t)b->blocks.size();
   gq_bam_dev_sizes &z = b->sizes;
   auto t0 = std::chrono::steady_clock::now();
+  // the inflate's buffers are allocated on another host thread while this one copies the file
+  hipError_t alloc_err = hipSuccess;
+  std::thread alloc([&] {
+    alloc_err = hipSetDevice(c->device);
+    if (alloc_err == hipSuccess) alloc_err = b->out.ensure((size_t)outn + 64);
+    if (alloc_err == hipSuccess) alloc_err = b->scratch.ensure((size_t)std::max<int64_t>(nb, 1) * kScratchBytes);
+    if (alloc_err == hipSuccess) alloc_err = b->status.ensure(sizeof(int) * (size_t)std::max<int64_t>(nb, 1));
+  });
+  struct Join {
+    std::thread &t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } join{alloc};
   // the file -> HBM (pinned chunks filled by host threads while the DMA drains the other)
-  t0 = std::chrono::steady_clock::now();
   HIP_TRY(b->comp.ensure((size_t)n + 64));
   HIP_TRY(hipMemsetAsync((uint8_t *)b->comp.p + n, 0, 64, c->stream));
   {
@@ -975,12 +990,11 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
   z.h2d_ms = ms_since(t0);
   // inflate + CRC32
   t0 = std::chrono::steady_clock::now();
-  HIP_TRY(b->out.ensure((size_t)outn + 64));
+  alloc.join();
+  HIP_TRY(alloc_err);
   HIP_TRY(hipMemsetAsync((uint8_t *)b->out.p + outn, 0, 64, c->stream));
   {
-    DevBuf scratch, status;
-    HIP_TRY(scratch.ensure((size_t)std::max<int64_t>(nb, 1) * kScratchBytes));
-    HIP_TRY(status.ensure(sizeof(int) * (size_t)std::max<int64_t>(nb, 1)));
+    DevBuf &scratch = b->scratch, &status = b->status;
     if (nb) {
       hipLaunchKernelGGL(bgzf_inflate, dim3(grid(nb, kInfLanes)), dim3(kInfLanes), 0, c->stream,
                          (const uint8_t *)b->comp.p, n + 64, (const BgzfBlock *)b->blk.p, nb, (uint8_t *)b->out.p,
@@ -993,8 +1007,6 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
     std::vector<int> sth((size_t)nb);
     if (nb) HIP_TRY(hipMemcpyAsync(sth.data(), status.p, sizeof(int) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    scratch.release();
-    status.release();
     for (int64_t i = 0; i < nb; ++i)
       if (sth[(size_t)i] != E_OK)
         return set_err(GQ_E_BAM_FORMAT, "corrupt BGZF block (inflate, ISIZE or CRC32) with payload at file offset %lld",
