@@ -77,3 +77,14 @@ def test_bench_two_ranks_equal_one(tmp_path):
     one, _ = _bench(1, str(tmp_path / "one.json"), ["--length", L, "--genome-ranks", "2"])
     assert one == two and one.count("], [") > 100
     assert '"n_gpus": 2' in out2
+
+
+def test_rccl_gather_branch_world_one():
+    """distributed.gather_germline's RCCL branch (device "cuda:0"): the device-to-device copy of
+    the library's result image into a torch tensor and the RCCL collectives, at world size 1 (the
+    one-GPU box cannot host two RCCL ranks); records equal the library's own host copy."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_gather_probe.py")], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert '"identical": true' in r.stdout
