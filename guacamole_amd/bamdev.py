@@ -26,6 +26,7 @@ from . import native, soa
 from .reads import InputFilters, ReadLoadError, _header_read_groups
 
 GQ_E_UNSORTED = 6
+GQ_E_HIP = 8
 GQ_E_BAM_IO = 11
 GQ_E_BAM_FORMAT = 12
 GQ_E_BAM_RECORD = 13
@@ -43,7 +44,21 @@ class gq_bam_dev_filters(C.Structure):
 class gq_bam_dev_sizes(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("n_records", "n_reads", "seq_bytes", "cigar_len", "md_events", "comp_bytes",
                                          "bam_bytes", "n_blocks")] + [
-        (k, C.c_float) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms")]
+        (k, C.c_float) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms")] + [
+        ("max_span", C.c_int64)]
+
+
+class gq_bam_dev_plan_info(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("n_segments", "n_blocks", "comp_bytes", "bam_bytes", "probes")] + [
+        ("used_index", C.c_int32), ("pad", C.c_int32)]
+
+
+GQ_E_PLAN = 16
+# Loci of margin before each planned range when the BAM has no index: a read that starts further
+# back and still overlaps the range is missed unless some rank sees one that long (the load then
+# re-plans with a wider halo, see load_reads_device).  1 Mb at 30x is ~0.2 M extra records
+# decoded per range boundary.
+DEFAULT_HALO = 1 << 20
 
 
 class DeviceReadSet:
@@ -65,19 +80,6 @@ class DeviceReadSet:
     @property
     def n(self) -> int:
         return self._n
-
-    def close_loader(self) -> None:
-        """Release the device loader's buffers (the resident reads stay)."""
-        h = getattr(self, "_bam", None)
-        if h:
-            native.lib().gq_bam_dev_close(h)
-            self._bam = None
-
-    def __del__(self):
-        try:
-            self.close_loader()
-        except Exception:
-            pass
 
     @property
     def contig_lengths_map(self) -> Dict[str, int]:
@@ -127,18 +129,50 @@ def download(reads: native.DeviceReads) -> Dict[str, np.ndarray]:
 
 
 class MappedBam:
-    """A BAM file mapped on the host with its BGZF block table (gq_bam_dev_map): the part of
-    the device load that needs no GPU, so it can run while the context starts.  None-like
-    (``ok`` False) for a plain gzip stream."""
+    """A BAM file mapped on the host with its BGZF block table and header (gq_bam_dev_map): the
+    part of the device load that needs no GPU, so it can run while the context starts.  None-like
+    (``ok`` False) for a plain gzip stream.  populate=False: the file's pages are not faulted in
+    up front (a region-restricted load reads only its segments)."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, populate: bool = True):
         self.path = path
         self.h = C.c_void_p()
         self.t = time.perf_counter()
-        rc = native.lib().gq_bam_dev_map(path.encode(), C.byref(self.h))
+        rc = native.lib().gq_bam_dev_map_ex(path.encode(), int(populate), C.byref(self.h))
         self.ok = rc != GQ_E_NOT_BGZF
         if self.ok:
             _raise(rc)
+
+    def contigs(self):
+        """(names, lengths) of the header's reference dictionary."""
+        L = native.lib()
+        n = L.gq_bam_dev_n_contigs(self.h)
+        return ([L.gq_bam_dev_contig_name(self.h, i).decode() for i in range(n)],
+                [int(L.gq_bam_dev_contig_length(self.h, i)) for i in range(n)])
+
+    def plan(self, region, halo: int = DEFAULT_HALO, bai: Optional[str] = None):
+        """gq_bam_dev_plan over a LociSet (the ranges of the header's contigs it names): the next
+        load reads only the records that can overlap it.  Returns the plan info as a dict with
+        its segments, or None when the file does not allow a plan (GQ_E_PLAN: not declared
+        coordinate-sorted) — the load then reads the whole file."""
+        names, _ = self.contigs()
+        begin, starts, ends = _loci_arrays(region, names)
+        info = gq_bam_dev_plan_info()
+        L = native.lib()
+        rc = L.gq_bam_dev_plan(self.h, begin.ctypes.data, starts.ctypes.data, ends.ctypes.data, int(halo),
+                               (bai or "").encode(), C.byref(info))
+        if rc == GQ_E_PLAN:
+            return None
+        _raise(rc)
+        n = int(info.n_segments)
+        b0, off, b1 = (np.zeros(max(n, 1), np.int64) for _ in range(3))
+        eof = np.zeros(max(n, 1), np.int32)
+        _raise(L.gq_bam_dev_plan_segments(self.h, b0.ctypes.data, off.ctypes.data, b1.ctypes.data, eof.ctypes.data))
+        out = {k: int(getattr(info, k)) for k in ("n_segments", "n_blocks", "comp_bytes", "bam_bytes", "probes",
+                                                  "used_index")}
+        out["segments"] = [(int(b0[i]), int(off[i]), int(b1[i]), bool(eof[i])) for i in range(n)]
+        out["halo"] = int(halo)
+        return out
 
     def close(self) -> None:
         if self.h:
@@ -176,19 +210,70 @@ def map_bams(paths) -> Dict[str, object]:
     return {"join": join}
 
 
+def _loci_arrays(loci, names):
+    """A LociSet as gq_bam_dev loci arrays over the header's contigs: (begin[n + 1], starts, ends)."""
+    begin, starts, ends = [0], [], []
+    for name in names:
+        for s, e in loci.on_contig(name).ranges:
+            starts.append(s)
+            ends.append(e)
+        begin.append(len(starts))
+    return np.asarray(begin, np.int64), np.asarray(starts or [0], np.int64), np.asarray(ends or [0], np.int64)
+
+
+def bai_path(path: str) -> Optional[str]:
+    """The BAM's index by samtools' names (X.bam.bai, then X.bai), if present."""
+    import os
+    for p in (path + ".bai", path[:-4] + ".bai" if path.endswith(".bam") else None):
+        if p and os.path.exists(p):
+            return p
+    return None
+
+
 def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = InputFilters(),
-                      mapped: Optional[MappedBam] = None) -> Optional[DeviceReadSet]:
+                      mapped: Optional[MappedBam] = None, region=None,
+                      halo: int = DEFAULT_HALO) -> Optional[DeviceReadSet]:
     """BAM -> resident read set on ctx's GPU (None: the host loader must run, see the module
     docstring).  Raises ReadLoadError / soa.MdParseError as the host loader does.  `mapped`:
-    the file already mapped (map_bams), else it is mapped here."""
+    the file already mapped (map_bams), else it is mapped here.
+
+    region (a LociSet, the multi-GPU ingest): keep only the reads overlapping it, reading only
+    the BGZF blocks whose records can overlap it (gq_bam_dev_plan: from the BAI's linear index
+    when the file has one, else by host probes with `halo` loci of margin).  The reads kept are
+    those of the filters within the region (the region lies inside the filters' loci).  Without
+    an index the load checks the longest reference span it saw against the halo and, if a read
+    could reach further back, plans again with twice that span (timings["replans"])."""
+    replans = 0
+    while True:
+        rs = _load_reads_device(ctx, path, filters, mapped, region, halo)
+        if rs is None or region is None or rs.timings.get("plan") is None:
+            break
+        plan = rs.timings["plan"]
+        if plan["used_index"] or rs.timings["max_span"] <= halo:
+            break
+        halo = 2 * rs.timings["max_span"]
+        mapped = None
+        replans += 1
+    if rs is not None:
+        rs.timings["replans"] = replans
+    return rs
+
+
+def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
     L = native.lib()
-    m = mapped if mapped is not None and (mapped.h or not mapped.ok) else MappedBam(path)  # (a used mapping: again)
+    planned = region is not None and use_plan
+    m = mapped if mapped is not None and (mapped.h or not mapped.ok) else MappedBam(path, populate=not planned)
     if not m.ok:
         return None
     t0 = m.t
+    plan = m.plan(region, halo, bai_path(path)) if planned else None
     h, m.h = m.h, C.c_void_p()  # the handle now belongs to this load
     try:
-        _raise(L.gq_bam_dev_load(ctx.h, h))
+        rc = L.gq_bam_dev_load(ctx.h, h)
+        if rc == GQ_E_HIP:  # out of device memory for the loader's buffers: the host loader's footprint is smaller
+            L.gq_bam_dev_close(h)
+            return None
+        _raise(rc)
         t1 = time.perf_counter()
         n_ref = L.gq_bam_dev_n_contigs(h)
         names = [L.gq_bam_dev_contig_name(h, i).decode() for i in range(n_ref)]
@@ -196,24 +281,30 @@ def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = In
         text = L.gq_bam_dev_header_text(h).decode("utf-8", "replace")
         rg_samples = _header_read_groups(text)  # ID -> SM (None: no SM), header order
         rg_ids = list(rg_samples)
+        if len(rg_ids) > 254:  # the device classes read groups in a byte: the host loader takes such headers
+            L.gq_bam_dev_close(h)
+            return None
         f = gq_bam_dev_filters(int(filters.non_duplicate), int(filters.passed_vendor_quality_checks),
                                int(filters.is_paired), int(filters.has_md_tag), 0, None, None, None, len(rg_ids),
                                b"".join(x.encode() + b"\0" for x in rg_ids) or None)
         keep = []
-        if filters.overlaps_loci is not None:
+        loci = region
+        if loci is None and filters.overlaps_loci is not None:
             loci = filters.overlaps_loci.result(dict(zip(names, lengths)))
-            begin, starts, ends = [0], [], []
-            for name in names:
-                for s, e in loci.on_contig(name).ranges:
-                    starts.append(s)
-                    ends.append(e)
-                begin.append(len(starts))
-            keep = [np.asarray(begin, np.int64), np.asarray(starts or [0], np.int64), np.asarray(ends or [0], np.int64)]
+        if loci is not None:
+            keep = list(_loci_arrays(loci, names))
             f.use_loci = 1
             f.loci_begin, f.loci_start, f.loci_end = (a.ctypes.data for a in keep)
         first = np.full(len(rg_ids) + 1, -1, np.int64)
         z = gq_bam_dev_sizes()
-        _raise(L.gq_bam_dev_scan(h, C.byref(f), first.ctypes.data, C.byref(z)))
+        rc = L.gq_bam_dev_scan(h, C.byref(f), first.ctypes.data, C.byref(z))
+        if rc == GQ_E_PLAN:  # a record runs past a planned segment: read the whole file
+            L.gq_bam_dev_close(h)
+            return _load_reads_device(ctx, path, filters, None, region, halo, use_plan=False)
+        if rc == GQ_E_HIP:
+            L.gq_bam_dev_close(h)
+            return None
+        _raise(rc)
         t2 = time.perf_counter()
         # samples: RG -> SM (else "default"), numbered by first appearance in file order
         samples: List[str] = []
@@ -230,7 +321,7 @@ def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = In
         out = C.c_void_p()
         fill_ms = C.c_float()
         rc = L.gq_bam_dev_reads(h, class_sample.ctypes.data, n_samples, sh.ctypes.data, C.byref(out), C.byref(fill_ms))
-        if rc == GQ_E_UNSORTED:
+        if rc in (GQ_E_UNSORTED, GQ_E_HIP):
             L.gq_bam_dev_close(h)
             return None
         _raise(rc)
@@ -243,11 +334,13 @@ def load_reads_device(ctx: native.Context, path: str, filters: InputFilters = In
     timings.update(fill_ms=float(fill_ms.value), derive_ms=float(info.get("derive_ms", 0.0)),
                    open_s=t1 - t0, scan_s=t2 - t1, total_s=time.perf_counter() - t0,
                    records=int(z.n_records), comp_bytes=int(z.comp_bytes), bam_bytes=int(z.bam_bytes),
-                   blocks=int(z.n_blocks))
+                   blocks=int(z.n_blocks), max_span=int(z.max_span), plan=plan)
     rs = DeviceReadSet(ctx, dr, names, lengths, samples, int(z.n_reads), timings)
-    # the loader's buffers (compressed file, inflated stream, record tables) are released with
-    # the read set, off the load's critical path (their hipFree calls take ~45 ms at chr20 30x)
-    rs._bam = h
+    # the loader's buffers (compressed file, inflated stream, record tables: ~2.5x the file's
+    # inflated size) are released now, so the callers have the HBM; on a host thread, off the
+    # load's critical path (their hipFree calls take ~45 ms at chr20 30x)
+    import threading
+    threading.Thread(target=L.gq_bam_dev_close, args=(h,), name="gq_bam_dev_close").start()
     return rs
 
 

@@ -39,7 +39,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
         for cmd, p in procs:
             if p.wait() != 0:
                 raise subprocess.CalledProcessError(p.returncode, cmd)
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)

@@ -28,8 +28,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import native, soa
-from .distributed import (assign_tasks_to_ranks, gather_germline, gather_somatic, init_from_env, rank_share,
-                          reads_overlapping)
+from .distributed import (all_gather_objects, assign_tasks_to_ranks, device_ingest_ranks, gather_germline,
+                          gather_somatic, init_from_env, rank_share, reads_overlapping)
 from .loci import (LociSet, LociSetBuilder, flatten_partitions, partition_loci_by_approximate_depth,
                    partition_loci_uniformly)
 from .bamdev import DeviceReadSet, load_reads_device, map_bams
@@ -204,8 +204,9 @@ def check_output_path(path: str) -> None:
 
 def device_ingest(args, *paths: str) -> bool:
     """Decode these BAMs on the GPU (bamdev.load_reads_device) rather than with the host
-    loader: single-rank runs of BAM input without MD recomputation or contig lengths from
-    the reads (GQ_INGEST=host forces the host loader)."""
+    loader: BAM input without MD recomputation or contig lengths from the reads (GQ_INGEST=host
+    forces the host loader).  Under torch.distributed.run each rank decodes only the part of the
+    file its tasks need (distributed.device_ingest_ranks)."""
     import os
     if os.environ.get("GQ_INGEST", "device") == "host":
         return False
@@ -228,44 +229,65 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     clock = StageClock()
     check_output_path(args.out)
     rank, world, local, gdev = init_from_env()
+    warn_default_parallelism(args, world)
     builder = _loci_builder(args)
     # germline-threshold takes no reference (GermlineThresholdCaller.scala:64-70): with
     # --recompute-md-tags read loading fails (Read.scala:223-225)
     filters = InputFilters.make(overlaps_loci=builder, non_duplicate=True, has_md_tag=True)
     ctx = None
     rs = None
-    if world == 1 and device_ingest(args, args.reads):
-        maps = map_bams([args.reads])  # the file mapped on a host thread while the context starts
-        ctx = native.Context(args.device)
-        rs = load_reads_device(ctx, args.reads, filters, maps["join"]()[args.reads])
+    mine = None  # this rank's loci ranges, when the device ingest planned them
+    if device_ingest(args, args.reads):
+        if world == 1:
+            maps = map_bams([args.reads])  # the file mapped on a host thread while the context starts
+            ctx = native.Context(args.device)
+            rs = load_reads_device(ctx, args.reads, filters, maps["join"]()[args.reads])
+        else:
+            ctx = native.Context(local)
+            got = device_ingest_ranks(ctx, [args.reads], filters, builder, args.parallelism, args.partition_accuracy,
+                                      rank, world, gdev)
+            if got is not None:
+                (rs,), mine, _ = got
     if rs is None:
         rs = load_reads(args.reads, filters, recompute_md=args.recompute_md_tags,
                         contig_lengths_from_dictionary=not args.no_sequence_dictionary)
     clock.mark("load_reads")
     loci = builder.result(rs.contig_lengths_map)
-    parts = partition(loci, args.parallelism, args.partition_accuracy, rs, world=world)
-    flat = flatten_partitions(parts, rs.contig_index())
+    if mine is None:
+        parts = partition(loci, args.parallelism, args.partition_accuracy, rs, world=world)
+        flat = flatten_partitions(parts, rs.contig_index())
     clock.mark("partition")
     if ctx is None:
         ctx = native.Context(local if world > 1 else args.device)
     if world == 1:
         device_reads(ctx, rs)
         clock.mark("upload")
+    names = rs.sample_names
+    sample_name = lambda s: names[s] if s < len(names) else "default"  # noqa: E731
     if world > 1:
-        rr = assign_tasks_to_ranks(flat, world, [rs], len(rs.contig_names))
-        mine_rs, mine = rank_share(rs, flat, rr, rank)
+        if mine is None:
+            rr = assign_tasks_to_ranks(flat, world, [rs], len(rs.contig_names))
+            mine_rs, mine = rank_share(rs, flat, rr, rank)
+        else:
+            mine_rs = rs
         calls = ctx.germline_threshold_device(device_reads(ctx, mine_rs), mine, args.threshold, args.emit_ref,
                                               args.emit_no_call)
         per_rank = gather_germline(calls, gdev)
+        # each rank numbers its own samples (by first appearance in what it read): names travel
+        rank_names = all_gather_objects(list(mine_rs.sample_names))
         if per_rank is None:
+            clock.mark("call")
+            clock.report(rank=rank, reads=int(mine_rs.n), loci=int(sum(np.asarray(mine[2]) - np.asarray(mine[1]))),
+                         ingest="device" if isinstance(rs, DeviceReadSet) else "host",
+                         device_ingest=getattr(rs, "timings", None))
             return _finish_rank(0)
-        rows = [t for c in per_rank for t in c.tuples(rs.contig_names)]
+        rows = [(c, l, nm[s] if s < len(nm) else "default", g, ref, alt, fl)
+                for calls_r, nm in zip(per_rank, rank_names) for c, l, s, g, ref, alt, fl in calls_r.tuples(rs.contig_names)]
+        sample_name = lambda s: s  # noqa: E731
     else:
         rows = germline_threshold_reads(ctx, rs, flat, args.threshold, args.emit_ref, args.emit_no_call)
     clock.mark("call")
     from .output import germline_genotype, write_vcf_dir_germline
-    names = rs.sample_names
-    sample_name = lambda s: names[s] if s < len(names) else "default"  # noqa: E731
     if args.out.lower().endswith(".vcf") and args.max_genotypes <= 1:
         # the lines _write_genotypes writes for these records, without building the records
         write_vcf_dir_germline(args.out, rows, sample_name, rs.contig_lengths_map)
@@ -274,7 +296,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
         _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
     clock.mark("write")
     print("Called %d genotypes." % len(rows), file=sys.stderr)
-    clock.report(reads=int(rs.n), genotypes=len(rows), loci=int(loci.count),
+    clock.report(rank=rank, reads=int(mine_rs.n if world > 1 else rs.n), genotypes=len(rows), loci=int(loci.count),
                  ingest="device" if isinstance(rs, DeviceReadSet) else "host",
                  device_ingest=getattr(rs, "timings", None))
     return _finish_rank(0)
@@ -304,8 +326,10 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     p.add_argument("--dbsnp-vcf", default="", help="VCF file to identify DBSNP variants")
     _common_args(p)
     args = p.parse_args(argv)
+    clock = StageClock()
     check_output_path(args.out)
     rank, world, local, gdev = init_from_env()
+    warn_default_parallelism(args, world)
     builder = _loci_builder(args)
     f = InputFilters.make(overlaps_loci=builder, non_duplicate=True, passed_vendor_quality_checks=True,
                           has_md_tag=True)
@@ -315,26 +339,42 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         reference = ReferenceGenome.load_fasta(args.reference_fasta)
     ctx = None
     sets = [None, None]
-    if world == 1 and device_ingest(args, args.tumor_reads, args.normal_reads):
-        maps = map_bams([args.tumor_reads, args.normal_reads])
-        ctx = native.Context(args.device)
-        mapped = maps["join"]()
-        sets = [load_reads_device(ctx, path, f, mapped[path]) for path in (args.tumor_reads, args.normal_reads)]
+    mine = None  # this rank's loci ranges, when the device ingest planned them
+    if device_ingest(args, args.tumor_reads, args.normal_reads):
+        if world == 1:
+            maps = map_bams([args.tumor_reads, args.normal_reads])
+            ctx = native.Context(args.device)
+            mapped = maps["join"]()
+            sets = [load_reads_device(ctx, path, f, mapped[path]) for path in (args.tumor_reads, args.normal_reads)]
+        else:
+            ctx = native.Context(local)
+            got = device_ingest_ranks(ctx, [args.tumor_reads, args.normal_reads], f, builder, args.parallelism,
+                                      args.partition_accuracy, rank, world, gdev)
+            if got is not None:
+                sets, mine, _ = got
     tumor, normal = [s if s is not None else
                      load_reads(path, f, reference=reference, recompute_md=args.recompute_md_tags,
                                 contig_lengths_from_dictionary=not args.no_sequence_dictionary)
                      for s, path in zip(sets, (args.tumor_reads, args.normal_reads))]
     if tumor.contig_lengths_map != normal.contig_lengths_map:
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
+    clock.mark("load_reads")
     loci = builder.result(normal.contig_lengths_map)
-    parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal, world=world)
-    flat = flatten_partitions(parts, tumor.contig_index())
+    if mine is None:
+        parts = partition(loci, args.parallelism, args.partition_accuracy, tumor, normal, world=world)
+        flat = flatten_partitions(parts, tumor.contig_index())
+    else:
+        flat = mine
     if ctx is None:
         ctx = native.Context(local if world > 1 else args.device)
+    sample = tumor.sample_names[0] if tumor.sample_names else "default"
     if world > 1:
-        rr = assign_tasks_to_ranks(flat, world, [tumor, normal], len(tumor.contig_names))
-        tumor, flat = rank_share(tumor, flat, rr, rank)
-        normal = normal.subset(reads_overlapping(normal, *flat[:3]))
+        if mine is None:
+            rr = assign_tasks_to_ranks(flat, world, [tumor, normal], len(tumor.contig_names))
+            tumor, flat = rank_share(tumor, flat, rr, rank)
+            normal = normal.subset(reads_overlapping(normal, *flat[:3]))
+        else:  # each rank read its own part: the first tumor sample of the lowest rank that has one
+            sample = next((n[0] for n in all_gather_objects(list(tumor.sample_names)) if n), "default")
     rows = somatic_standard_reads(
         ctx, tumor, normal, flat, odds=args.odds, min_mapq=args.min_mapq,
         filter_multi_allelic=int(args.filter_multi_allelic), max_read_depth=args.max_tumor_read_depth,
@@ -345,16 +385,21 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         min_average_mapping_quality=args.min_average_mapping_quality,
         min_average_base_quality=args.min_average_base_quality, max_median_mismatches=args.max_median_mismatches,
         apply_filters=1, _gather=gdev if world > 1 else None, reference=reference)
+    clock.mark("call")
+    report = dict(rank=rank, reads=[int(tumor.n), int(normal.n)], ingest="device" if isinstance(tumor, DeviceReadSet)
+                  else "host", device_ingest=[getattr(x, "timings", None) for x in (tumor, normal)])
     if rows is None:
+        clock.report(**report)
         return _finish_rank(0)
     if args.dbsnp_vcf:  # SomaticStandardCaller.scala:139-149
         from .output import dbsnp_join, read_dbsnp_vcf
         rows = dbsnp_join(rows, read_dbsnp_vcf(args.dbsnp_vcf))
     from .output import somatic_genotype
-    sample = tumor.sample_names[0] if tumor.sample_names else "default"
     out = [somatic_genotype(r["contig"], r, sample) for r in rows]
     _write_genotypes(args.out, out, tumor.contig_lengths_map, args.max_genotypes)
+    clock.mark("write")
     print("Called %d somatic genotypes." % len(out), file=sys.stderr)
+    clock.report(genotypes=len(out), **report)
     return _finish_rank(0)
 
 
@@ -544,6 +589,17 @@ def vaf_histogram_main(argv: Sequence[str]) -> int:
         for row in plain:
             print(row)
     return 0
+
+
+def warn_default_parallelism(args, world: int) -> None:
+    """--parallelism 0 means one task per rank (task_count): the records at heap-order loci then
+    depend on the rank count, so say so when a multi-rank run takes the default."""
+    if world > 1 and args.parallelism == 0:
+        import os
+        if int(os.environ.get("RANK", "0")) == 0:
+            print("warning: --parallelism 0 makes %d tasks (one per rank); the records at heap-order loci (the first "
+                  "pileup of each task) can then differ from a run with another rank count. Pass the same explicit "
+                  "--parallelism to compare runs." % world, file=sys.stderr)
 
 
 def single_process_only(command: str) -> None:

@@ -26,8 +26,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <zlib.h>
+
 #include <chrono>
+#include <climits>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
 #include <thread>
@@ -64,12 +68,12 @@ static_assert(kTabEnd * 2 + 352 <= kScratchBytes, "inflate scratch");
 
 enum : int { E_OK = 0, E_INFLATE = 1, E_SIZE = 2, E_CRC = 3 };
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
+__host__ __device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 typedef uint32_t u32u __attribute__((aligned(1)));  // unaligned dword access (gfx950 global memory)
 
-__device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+__host__ __device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
 struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end.  The next
                 // word is loaded one refill ahead, so its latency overlaps the symbols between
@@ -394,7 +398,7 @@ __global__ void __launch_bounds__(256) bgzf_crc(const uint8_t *out, const BgzfBl
 // ---- records ------------------------------------------------------------------------------
 // plausible alignment record at o: every length field consistent with block_size (as the host
 // loader's record_at)
-__device__ bool record_at(const uint8_t *d, int64_t n, int64_t o, int32_t n_ref) {
+__host__ __device__ bool record_at(const uint8_t *d, int64_t n, int64_t o, int32_t n_ref) {
   if (o + 40 > n) return false;
   const int32_t bs = (int32_t)ld32(d + o);
   if (bs < 32 || o + 4 + bs > n) return false;
@@ -580,16 +584,23 @@ __device__ bool loci_intersect(const DevFilters &f, int32_t contig, int64_t s, i
 
 __device__ __forceinline__ void parse_one(const uint8_t *d, const int64_t *rec, int64_t n_rec, const DevFilters &f,
                                           RecInfo *info, int64_t *keep, int64_t *seq_k, int64_t *cig_k, int64_t *md_k,
-                                          unsigned long long *err, int64_t r, int &cls);
+                                          unsigned long long *err, int64_t r, int &cls, int64_t &span);
 
 // thread / record: the host loader's scan_chunk + the MD event count of gq_md_count
 __global__ void __launch_bounds__(256) rec_parse(const uint8_t *d, const int64_t *rec, int64_t n_rec, DevFilters f,
                                                  RecInfo *info, int64_t *keep, int64_t *seq_k, int64_t *cig_k,
                                                  int64_t *md_k, unsigned long long *rg_first,
-                                                 unsigned long long *err) {
+                                                 unsigned long long *err, unsigned long long *span_max) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int cls = -1;  // the kept record's read-group class (for rg_first), -1: not kept
-  parse_one(d, rec, n_rec, f, info, keep, seq_k, cig_k, md_k, err, r, cls);
+  int64_t span = 0;  // reference span of a mapped record (the region plan's halo check)
+  parse_one(d, rec, n_rec, f, info, keep, seq_k, cig_k, md_k, err, r, cls, span);
+  unsigned long long sm = (unsigned long long)span;
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long x = __shfl_xor(sm, o, 64);
+    sm = x > sm ? x : sm;
+  }
+  if ((threadIdx.x & 63) == 0 && sm) atomicMax(span_max, sm);
   // first kept record per class: one atomic per (wave, class) — lanes hold increasing r
   for (;;) {
     const uint64_t m = __ballot(cls >= 0);
@@ -603,7 +614,7 @@ __global__ void __launch_bounds__(256) rec_parse(const uint8_t *d, const int64_t
 
 __device__ __forceinline__ void parse_one(const uint8_t *d, const int64_t *rec, int64_t n_rec, const DevFilters &f,
                                           RecInfo *info, int64_t *keep, int64_t *seq_k, int64_t *cig_k, int64_t *md_k,
-                                          unsigned long long *err, int64_t r, int &cls) {
+                                          unsigned long long *err, int64_t r, int &cls, int64_t &span) {
   if (r >= n_rec) return;
   RecInfo ri{-1, 0, 0, 0, 0, 0, 0};
   keep[r] = 0;
@@ -652,6 +663,7 @@ __device__ __forceinline__ void parse_one(const uint8_t *d, const int64_t *rec, 
           case 'i': case 'I': case 'f': w = 4; break;
           default: return fail(X_AUX_ARR_TYPE | ((uint64_t)0));
         }
+        if (cnt < 0 || q + 5 + cnt * w > end) return fail(X_AUX_ARR);  // (a negative count would walk backwards)
         q += 5 + cnt * w;
         break;
       }
@@ -660,13 +672,14 @@ __device__ __forceinline__ void parse_one(const uint8_t *d, const int64_t *rec, 
   }
   // Read.scala:411-418 record filters, then isMapped / hasMdTag (Read.scala:421-428)
   bool kept = !((flag & 0x4) || ref_id < 0) && pos >= 0 && ref_id < f.n_ref;
-  if (kept && f.use_loci) {
+  if (kept) {
     int64_t ref_len = 0;
     for (uint32_t k = 0; k < n_cig; ++k) {
       const uint32_t v = ld32(d + cig_at + 4 * k), op = v & 15;
       if (op < 9 && (kConsumesRef >> op) & 1) ref_len += v >> 4;
     }
-    kept = loci_intersect(f, ref_id, pos, pos + ref_len);
+    span = ref_len;
+    if (f.use_loci) kept = loci_intersect(f, ref_id, pos, pos + ref_len);
   }
   if (kept && f.non_duplicate && (flag & 0x400)) kept = false;
   if (kept && f.passed_vendor && (flag & 0x200)) kept = false;
@@ -846,13 +859,39 @@ bool gzip_member(const uint8_t *p, int64_t avail, int64_t *payload, int64_t *bsi
 
 }  // namespace
 
+namespace {
+// a planned segment (gq_bam_dev_plan): BGZF blocks [b0, b1) are inflated; its records run from
+// offset `first` of block b0 up to block b1 - 1 (which only completes the last record), or to
+// the end of the stream when `eof`
+struct Seg {
+  int64_t b0, first, b1;
+  bool eof;
+};
+// host probe of one BGZF block: the key (contig << 32 | pos + 1) of the last record starting
+// in it and the stream offset its chain lands on (the next record's start)
+struct Probe {
+  bool has = false;
+  int64_t last = 0, land = 0;
+};
+}  // namespace
+
 struct gq_bam_dev {
   gq_ctx *ctx = nullptr;
   int fd = -1;
   const uint8_t *map = nullptr;
   size_t map_len = 0;
   std::vector<BgzfBlock> blocks;
+  std::vector<int64_t> foff;  // file offset of each block's gzip member
   int64_t n_out = 0, rec0 = 0;
+  bool sorted = false;        // @HD SO:coordinate
+  // region plan: segments, the probe cache, the linear index of the BAI (per contig)
+  bool planned = false;
+  std::vector<Seg> segs;
+  std::vector<BgzfBlock> sel;  // the load's blocks (planned: segment by segment, stream offsets compacted)
+  std::vector<int64_t> sel_seg0;  // first entry of each segment in `sel`
+  std::map<int64_t, Probe> probes;
+  int64_t n_probes = 0;
+  std::vector<std::vector<uint64_t>> bai_ioff;
   std::string text;
   std::vector<std::string> names;
   std::vector<int64_t> lengths;
@@ -886,11 +925,266 @@ gq_status d2h_i64(gq_ctx *c, const void *src, int64_t *dst) {
   return GQ_OK;
 }
 
+// ---- host side of the file: header, block probes, BAI, region plan -----------------------
+
+// block k's raw DEFLATE payload inflated on the host (zlib), appended to `out`
+bool host_inflate(const gq_bam_dev *b, int64_t k, std::vector<uint8_t> &out) {
+  const BgzfBlock &blk = b->blocks[(size_t)k];
+  const size_t at = out.size();
+  out.resize(at + blk.isize);
+  z_stream z;
+  memset(&z, 0, sizeof(z));
+  if (inflateInit2(&z, -15) != Z_OK) return false;
+  z.next_in = const_cast<Bytef *>(b->map + blk.in_off);
+  z.avail_in = (uInt)blk.in_len;
+  z.next_out = out.data() + at;
+  z.avail_out = (uInt)blk.isize;
+  const int rc = inflate(&z, Z_FINISH);
+  const bool ok = rc == Z_STREAM_END && z.total_out == blk.isize;
+  inflateEnd(&z);
+  return ok;
+}
+
+gq_status corrupt_block(const gq_bam_dev *b, int64_t k) {
+  return set_err(GQ_E_BAM_FORMAT, "corrupt BGZF block (inflate, ISIZE or CRC32) with payload at file offset %lld",
+                 (long long)b->blocks[(size_t)k].in_off);
+}
+
+// the BAM header (magic, SAM text, reference dictionary) from the first blocks, on the host;
+// rec0 = the first alignment record's stream offset
+gq_status parse_header(gq_bam_dev *b) {
+  std::vector<uint8_t> h;
+  int64_t k = 0;
+  const int64_t nb = (int64_t)b->blocks.size();
+  bool bad = false;
+  auto need = [&](int64_t upto) -> bool {  // h holds >= upto bytes (false: the stream is shorter)
+    while ((int64_t)h.size() < upto && k < nb) {
+      if (!host_inflate(b, k, h)) {
+        bad = true;
+        return false;
+      }
+      ++k;
+    }
+    return (int64_t)h.size() >= upto;
+  };
+  auto fail = [&](const char *what) { return bad ? corrupt_block(b, k) : set_err(GQ_E_BAM_FORMAT, "%s", what); };
+  if (!need(12) || memcmp(h.data(), "BAM\1", 4) != 0) return fail("not a BAM file (magic)");
+  int64_t o = 4;
+  int32_t l_text;
+  memcpy(&l_text, h.data() + o, 4);
+  o += 4;
+  if (l_text < 0 || !need(o + l_text + 4)) return fail("truncated BAM header");
+  b->text.assign((const char *)h.data() + o, (size_t)l_text);
+  while (!b->text.empty() && b->text.back() == '\0') b->text.pop_back();
+  o += l_text;
+  int32_t n_ref;
+  memcpy(&n_ref, h.data() + o, 4);
+  o += 4;
+  for (int32_t i = 0; i < n_ref; ++i) {
+    int32_t l_name;
+    if (!need(o + 4)) return fail("truncated BAM reference dictionary");
+    memcpy(&l_name, h.data() + o, 4);
+    o += 4;
+    if (l_name < 1 || !need(o + l_name + 4)) return fail("truncated BAM reference dictionary");
+    b->names.emplace_back((const char *)h.data() + o, (size_t)(l_name - 1));
+    o += l_name;
+    int32_t ln;
+    memcpy(&ln, h.data() + o, 4);
+    b->lengths.push_back(ln);
+    o += 4;
+  }
+  b->rec0 = o;
+  // SAM spec @HD SO:coordinate (the plan's binary searches need the sort order)
+  const size_t hd = b->text.compare(0, 3, "@HD") == 0 ? 0 : b->text.find("\n@HD");
+  if (hd != std::string::npos) {
+    const size_t eol = b->text.find('\n', hd + 1);
+    const std::string line = b->text.substr(hd, eol == std::string::npos ? std::string::npos : eol - hd);
+    b->sorted = line.find("\tSO:coordinate") != std::string::npos;
+  }
+  return GQ_OK;
+}
+
+inline int64_t rec_key(int32_t ref, int32_t pos) {  // file order of a sorted BAM; unmapped last
+  return ref < 0 ? INT64_MAX : ((int64_t)ref << 32) + (int64_t)pos + 1;
+}
+
+// Probe block k: inflate it (and the next blocks a record needs), find the first offset whose
+// chain of plausible, key-sorted records runs through the block's end onto a plausible record
+// (or the stream's end), and report the key of the chain's last record in the block and where
+// it lands.  A false sync can only pass by merging into the true chain within the block, so the
+// last record and the landing are true records.  has = false: no record starts in the block
+// (header bytes only, an empty block, or one inside a longer record).
+gq_status probe(gq_bam_dev *b, int64_t k, Probe &out) {
+  auto hit = b->probes.find(k);
+  if (hit != b->probes.end()) {
+    out = hit->second;
+    return GQ_OK;
+  }
+  Probe P;
+  const BgzfBlock &blk = b->blocks[(size_t)k];
+  const int64_t o0 = blk.out_off, hi = blk.isize, nb = (int64_t)b->blocks.size();
+  const int32_t n_ref = (int32_t)b->names.size();
+  if (hi > 0 && o0 + hi > b->rec0) {
+    ++b->n_probes;
+    std::vector<uint8_t> buf;
+    if (!host_inflate(b, k, buf)) return corrupt_block(b, k);
+    int64_t next = k + 1;
+    auto extend = [&](int64_t upto) -> gq_status {  // buf holds >= upto bytes where the stream has them
+      while ((int64_t)buf.size() < upto && next < nb && next <= k + 8)
+        if (!host_inflate(b, next++, buf)) return corrupt_block(b, next - 1);
+      return GQ_OK;
+    };
+    auto rec_ok = [&](int64_t q, int64_t &key, int64_t &len, gq_status &st) -> bool {
+      if ((st = extend(q + 4))) return false;
+      if (q + 4 > (int64_t)buf.size()) return false;
+      const int32_t bs = (int32_t)ld32(buf.data() + q);
+      if (bs < 32) return false;
+      if ((st = extend(q + 4 + bs))) return false;
+      if (!record_at(buf.data(), (int64_t)buf.size(), q, n_ref)) return false;
+      key = rec_key((int32_t)ld32(buf.data() + q + 4), (int32_t)ld32(buf.data() + q + 8));
+      len = 4 + bs;
+      return true;
+    };
+    const int64_t lo = std::max<int64_t>(0, b->rec0 - o0);
+    const int64_t top = b->rec0 > o0 ? lo + 1 : hi;  // the block holding rec0: its first record is known
+    for (int64_t o = lo; o < top && !P.has; ++o) {
+      int64_t q = o, prev = INT64_MIN, key = 0, len = 0;
+      gq_status st = GQ_OK;
+      bool ok = true;
+      while (ok && q < hi) {
+        ok = rec_ok(q, key, len, st) && key >= prev;
+        if (st) return st;
+        prev = key;
+        q += len;
+      }
+      if (!ok) continue;
+      const int64_t last = prev;
+      if ((st = extend(q + 4))) return st;
+      if (q < (int64_t)buf.size() || next < nb) {  // not the stream's end: a record must start there
+        if (!rec_ok(q, key, len, st) || key < last) {
+          if (st) return st;
+          continue;
+        }
+      }
+      P.has = true;
+      P.last = last;
+      P.land = o0 + q;
+    }
+  }
+  b->probes[k] = P;
+  out = P;
+  return GQ_OK;
+}
+
+// the last record key at or before block k (INT64_MIN: none — only header bytes so far)
+gq_status key_upto(gq_bam_dev *b, int64_t k, int64_t &key, int64_t *land = nullptr, int64_t *blk = nullptr) {
+  for (int64_t j = k; j >= 0; --j) {
+    Probe P;
+    gq_status st = probe(b, j, P);
+    if (st) return st;
+    if (P.has) {
+      key = P.last;
+      if (land) *land = P.land;
+      if (blk) *blk = j;
+      return GQ_OK;
+    }
+  }
+  key = INT64_MIN;
+  if (land) *land = b->rec0;
+  if (blk) *blk = -1;
+  return GQ_OK;
+}
+
+// smallest block b in [lo, nb) whose key_upto >= K (nb if none)
+gq_status first_block_at(gq_bam_dev *b, int64_t lo, int64_t K, int64_t &out) {
+  int64_t hi = (int64_t)b->blocks.size();
+  while (lo < hi) {
+    const int64_t m = lo + (hi - lo) / 2;
+    int64_t key;
+    gq_status st = key_upto(b, m, key);
+    if (st) return st;
+    if (key >= K) hi = m;
+    else lo = m + 1;
+  }
+  out = lo;
+  return GQ_OK;
+}
+
+// stream offset -> (block, offset in it)
+void stream_pos(const gq_bam_dev *b, int64_t at, int64_t &blk, int64_t &off) {
+  int64_t lo = 0, hi = (int64_t)b->blocks.size() - 1;
+  while (lo < hi) {  // last block with out_off <= at
+    const int64_t m = (lo + hi + 1) / 2;
+    if (b->blocks[(size_t)m].out_off <= at) lo = m;
+    else hi = m - 1;
+  }
+  // an offset at a block's end is the start of the next non-empty block
+  while (lo + 1 < (int64_t)b->blocks.size() &&
+         at >= b->blocks[(size_t)lo].out_off + (int64_t)b->blocks[(size_t)lo].isize)
+    ++lo;
+  blk = lo;
+  off = at - b->blocks[(size_t)lo].out_off;
+}
+
+// the BAI's linear index (SAM spec §5.2): per reference, the virtual offset of the first
+// record overlapping each 16 kb window.  false: no usable index (absent, older than the BAM,
+// malformed, or for another dictionary).
+bool load_bai(gq_bam_dev *b, const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  std::vector<uint8_t> v;
+  {
+    uint8_t buf[1 << 16];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof(buf), f)) > 0) v.insert(v.end(), buf, buf + k);
+    fclose(f);
+  }
+  size_t o = 0;
+  auto rd = [&](void *dst, size_t n) -> bool {
+    if (o + n > v.size()) return false;
+    memcpy(dst, v.data() + o, n);
+    o += n;
+    return true;
+  };
+  char magic[4];
+  int32_t n_ref;
+  if (!rd(magic, 4) || memcmp(magic, "BAI\1", 4) != 0 || !rd(&n_ref, 4) || n_ref != (int32_t)b->names.size())
+    return false;
+  b->bai_ioff.assign((size_t)n_ref, {});
+  for (int32_t r = 0; r < n_ref; ++r) {
+    int32_t n_bin;
+    if (!rd(&n_bin, 4) || n_bin < 0) return false;
+    for (int32_t i = 0; i < n_bin; ++i) {
+      uint32_t bin;
+      int32_t n_chunk;
+      if (!rd(&bin, 4) || !rd(&n_chunk, 4) || n_chunk < 0 || o + 16 * (size_t)n_chunk > v.size()) return false;
+      o += 16 * (size_t)n_chunk;
+    }
+    int32_t n_intv;
+    if (!rd(&n_intv, 4) || n_intv < 0 || o + 8 * (size_t)n_intv > v.size()) return false;
+    b->bai_ioff[(size_t)r].resize((size_t)n_intv);
+    if (n_intv) memcpy(b->bai_ioff[(size_t)r].data(), v.data() + o, 8 * (size_t)n_intv);
+    o += 8 * (size_t)n_intv;
+  }
+  return true;
+}
+
+// BGZF virtual offset -> (block, offset in its inflated bytes); false if it names no block
+bool voff_pos(const gq_bam_dev *b, uint64_t v, int64_t &blk, int64_t &off) {
+  const int64_t fo = (int64_t)(v >> 16), uo = (int64_t)(v & 0xFFFF);
+  auto it = std::lower_bound(b->foff.begin(), b->foff.end(), fo);
+  if (it == b->foff.end() || *it != fo) return false;
+  blk = it - b->foff.begin();
+  if (uo > (int64_t)b->blocks[(size_t)blk].isize) return false;
+  stream_pos(b, b->blocks[(size_t)blk].out_off + uo, blk, off);
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
 
-gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) {
+gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out) {
   if (!path || !out) return set_err(GQ_E_ARG, "gq_bam_dev_map: null argument");
   *out = nullptr;
   auto t0 = std::chrono::steady_clock::now();
@@ -900,7 +1194,7 @@ gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) {
   struct stat st;
   if (fstat(b->fd, &st) != 0 || st.st_size == 0) return set_err(GQ_E_BAM_IO, "cannot stat (or empty) %s", path);
   b->map_len = (size_t)st.st_size;
-  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, b->fd, 0);
+  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), b->fd, 0);
   if (m == MAP_FAILED) return set_err(GQ_E_BAM_IO, "cannot map %s", path);
   b->map = (const uint8_t *)m;
   const uint8_t *p = b->map;
@@ -922,9 +1216,12 @@ gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) {
     k.out_off = outn;
     outn += k.isize;
     b->blocks.push_back(k);
+    b->foff.push_back(off);
     off += bsize;
   }
   b->n_out = outn;
+  gq_status hs = parse_header(b.get());
+  if (hs) return hs;
   const int64_t nb = (int64_t)b->blocks.size();
   gq_bam_dev_sizes &z = b->sizes;
   z.comp_bytes = n;
@@ -934,6 +1231,8 @@ gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) {
   *out = b.release();
   return GQ_OK;
 }
+
+gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out) { return gq_bam_dev_map_ex(path, 1, out); }
 
 gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
   if (!c || !path || !out) return set_err(GQ_E_ARG, "gq_bam_dev_open: null argument");
@@ -949,6 +1248,121 @@ gq_status gq_bam_dev_open(gq_ctx *c, const char *path, gq_bam_dev **out) {
   return GQ_OK;
 }
 
+gq_status gq_bam_dev_plan(gq_bam_dev *b, const int64_t *loci_begin, const int64_t *loci_start, const int64_t *loci_end,
+                          int64_t halo, const char *bai_path, gq_bam_dev_plan_info *info) {
+  if (!b || !loci_begin || !info) return set_err(GQ_E_ARG, "gq_bam_dev_plan: null argument");
+  if (b->ctx) return set_err(GQ_E_ARG, "gq_bam_dev_plan: after gq_bam_dev_load");
+  const int32_t n_ref = (int32_t)b->names.size();
+  if (loci_begin[n_ref] > 0 && (!loci_start || !loci_end)) return set_err(GQ_E_ARG, "gq_bam_dev_plan: loci arrays");
+  if (halo < 0) return set_err(GQ_E_ARG, "gq_bam_dev_plan: halo < 0");
+  if (!b->sorted) return set_err(GQ_E_PLAN, "the BAM header does not declare SO:coordinate");
+  const int64_t nb = (int64_t)b->blocks.size();
+  // the index, when it is at least as new as the BAM and describes its dictionary
+  bool bai = false;
+  if (bai_path && *bai_path) {
+    struct stat sb, si;
+    if (stat(bai_path, &si) == 0 && fstat(b->fd, &sb) == 0 && si.st_mtime >= sb.st_mtime) bai = load_bai(b, bai_path);
+  }
+  std::vector<Seg> segs;
+  int64_t from = 0;  // the searches move forward (ranges in file order)
+  for (int32_t c = 0; c < n_ref; ++c) {
+    for (int64_t i = loci_begin[c]; i < loci_begin[c + 1]; ++i) {
+      const int64_t S = loci_start[i], E = loci_end[i];
+      if (E <= S) continue;
+      if (i > loci_begin[c] && S < loci_end[i - 1]) return set_err(GQ_E_ARG, "gq_bam_dev_plan: unsorted loci");
+      Seg g{0, 0, 0, false};
+      bool have_start = false;
+      if (bai) {
+        const std::vector<uint64_t> &lx = b->bai_ioff[(size_t)c];
+        const int64_t w = S >> 14;
+        if (w >= (int64_t)lx.size()) continue;  // no record overlaps a window from here on
+        // the window's entry, or (an older writer's empty window) the first later one
+        int64_t j = w;
+        while (j < (int64_t)lx.size() && lx[(size_t)j] == 0) ++j;
+        if (j < (int64_t)lx.size()) {
+          if (!voff_pos(b, lx[(size_t)j], g.b0, g.first)) {
+            bai = false;
+            b->bai_ioff.clear();
+          } else {
+            have_start = true;
+          }
+        } else {
+          continue;
+        }
+      }
+      if (!have_start) {
+        int64_t bs;
+        gq_status st = first_block_at(b, from, rec_key(c, (int32_t)std::max<int64_t>(0, S - halo)), bs);
+        if (st) return st;
+        if (bs >= nb) continue;  // every record is before the range
+        // the first record starting at or after the end of the last block before it
+        int64_t kprev, land;
+        if (bs > 0) {
+          if ((st = key_upto(b, bs - 1, kprev, &land))) return st;
+        } else {
+          land = b->rec0;
+        }
+        stream_pos(b, land, g.b0, g.first);
+      }
+      // stop: the first block whose records all start at or past (c, E)
+      int64_t be;
+      gq_status st = first_block_at(b, std::max<int64_t>(g.b0, from), rec_key(c, (int32_t)std::min<int64_t>(E, INT32_MAX - 1)), be);
+      if (st) return st;
+      if (be + 1 >= nb) {
+        g.b1 = nb;
+        g.eof = true;
+      } else {
+        g.b1 = be + 2;  // records start up to block be; block be + 1 completes the last one
+      }
+      from = g.b0;
+      segs.push_back(g);
+    }
+  }
+  // file order, then merge segments whose blocks meet
+  std::sort(segs.begin(), segs.end(), [](const Seg &x, const Seg &y) {
+    return x.b0 != y.b0 ? x.b0 < y.b0 : x.first < y.first;
+  });
+  std::vector<Seg> merged;
+  for (const Seg &g : segs) {
+    if (!merged.empty() && g.b0 <= merged.back().b1) {
+      Seg &m = merged.back();
+      if (g.b1 > m.b1 || g.eof) {
+        m.b1 = std::max(m.b1, g.b1);
+        m.eof = m.eof || g.eof;
+      }
+    } else {
+      merged.push_back(g);
+    }
+  }
+  b->segs = merged;
+  b->planned = true;
+  info->n_segments = (int64_t)merged.size();
+  info->n_blocks = info->comp_bytes = info->bam_bytes = 0;
+  for (const Seg &g : merged) {
+    info->n_blocks += g.b1 - g.b0;
+    const int64_t f1 = g.b1 < nb ? b->foff[(size_t)g.b1] : (int64_t)b->map_len;
+    info->comp_bytes += f1 - b->foff[(size_t)g.b0];
+    for (int64_t k = g.b0; k < g.b1; ++k) info->bam_bytes += b->blocks[(size_t)k].isize;
+  }
+  info->probes = b->n_probes;
+  info->used_index = bai ? 1 : 0;
+  info->pad = 0;
+  return GQ_OK;
+}
+
+gq_status gq_bam_dev_plan_segments(const gq_bam_dev *b, int64_t *first_block, int64_t *first_offset,
+                                   int64_t *end_block, int32_t *to_eof) {
+  if (!b || !first_block || !first_offset || !end_block || !to_eof)
+    return set_err(GQ_E_ARG, "gq_bam_dev_plan_segments: null argument");
+  for (size_t i = 0; i < b->segs.size(); ++i) {
+    first_block[i] = b->segs[i].b0;
+    first_offset[i] = b->segs[i].first;
+    end_block[i] = b->segs[i].b1;
+    to_eof[i] = b->segs[i].eof ? 1 : 0;
+  }
+  return GQ_OK;
+}
+
 gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
   if (!c || !mapped) return set_err(GQ_E_ARG, "gq_bam_dev_load: null argument");
   if (mapped->ctx) return set_err(GQ_E_ARG, "gq_bam_dev_load: already loaded");
@@ -956,10 +1370,41 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
   gq_bam_dev *b = mapped;
   b->ctx = c;
   const uint8_t *p = b->map;
-  const int64_t n = (int64_t)b->map_len;
-  const int64_t outn = b->n_out;
-  const int64_t nb = (int64_t)b->blocks.size();
+  // the blocks to inflate and the file bytes to copy: the whole file, or the planned
+  // segments back to back (their blocks' payload and stream offsets compacted)
+  std::vector<std::pair<int64_t, int64_t>> pieces;  // (file offset, bytes) copied in order
+  b->sel_seg0.clear();
+  if (!b->planned) {
+    b->sel = b->blocks;
+    pieces.emplace_back(0, (int64_t)b->map_len);
+  } else {
+    b->sel.clear();
+    int64_t in_acc = 0, out_acc = 0;
+    const int64_t nb = (int64_t)b->blocks.size();
+    for (const Seg &g : b->segs) {
+      b->sel_seg0.push_back((int64_t)b->sel.size());
+      const int64_t f0 = b->foff[(size_t)g.b0], f1 = g.b1 < nb ? b->foff[(size_t)g.b1] : (int64_t)b->map_len;
+      for (int64_t k = g.b0; k < g.b1; ++k) {
+        BgzfBlock x = b->blocks[(size_t)k];
+        x.in_off = in_acc + (x.in_off - f0);
+        x.out_off = out_acc;
+        out_acc += x.isize;
+        b->sel.push_back(x);
+      }
+      pieces.emplace_back(f0, f1 - f0);
+      in_acc += f1 - f0;
+    }
+  }
+  b->sel_seg0.push_back((int64_t)b->sel.size());
+  int64_t n = 0, outn = 0;
+  for (auto &pc : pieces) n += pc.second;
+  for (const BgzfBlock &x : b->sel) outn += x.isize;
+  b->n_out = outn;
+  const int64_t nb = (int64_t)b->sel.size();
   gq_bam_dev_sizes &z = b->sizes;
+  z.comp_bytes = n;
+  z.bam_bytes = outn;
+  z.n_blocks = nb;
   auto t0 = std::chrono::steady_clock::now();
   // the inflate's buffers are allocated on another host thread while this one copies the file
   hipError_t alloc_err = hipSuccess;
@@ -975,16 +1420,29 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
       if (t.joinable()) t.join();
     }
   } join{alloc};
-  // the file -> HBM (pinned chunks filled by host threads while the DMA drains the other)
+  // the file (or its segments) -> HBM (pinned chunks filled by host threads while the DMA drains the other)
   HIP_TRY(b->comp.ensure((size_t)n + 64));
   HIP_TRY(hipMemsetAsync((uint8_t *)b->comp.p + n, 0, 64, c->stream));
   {
     H2DStager stager(c->stream);
     HIP_TRY(stager.init());
-    HIP_TRY(stager.copy(b->comp.p, p, (size_t)n));
+    std::vector<int64_t> at(pieces.size() + 1, 0);  // logical offset of each piece
+    for (size_t i = 0; i < pieces.size(); ++i) at[i + 1] = at[i] + pieces[i].second;
+    HIP_TRY(stager.copy_from(b->comp.p, (size_t)n, [&](uint8_t *dst, size_t o, size_t k) {
+      size_t i = (size_t)(std::upper_bound(at.begin(), at.end(), (int64_t)o) - at.begin()) - 1;
+      while (k > 0) {
+        const size_t in_piece = (size_t)(at[i + 1] - (int64_t)o);
+        const size_t take = std::min(k, in_piece);
+        memcpy(dst, p + pieces[i].first + ((int64_t)o - at[i]), take);
+        dst += take;
+        o += take;
+        k -= take;
+        ++i;
+      }
+    }));
     HIP_TRY(b->blk.ensure(sizeof(BgzfBlock) * (size_t)std::max<int64_t>(nb, 1)));
-    HIP_TRY(hipMemcpyAsync(b->blk.p, b->blocks.data(), sizeof(BgzfBlock) * (size_t)nb, hipMemcpyHostToDevice,
-                           c->stream));
+    if (nb)
+      HIP_TRY(hipMemcpyAsync(b->blk.p, b->sel.data(), sizeof(BgzfBlock) * (size_t)nb, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
   z.h2d_ms = ms_since(t0);
@@ -1008,55 +1466,20 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
     if (nb) HIP_TRY(hipMemcpyAsync(sth.data(), status.p, sizeof(int) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int64_t i = 0; i < nb; ++i)
-      if (sth[(size_t)i] != E_OK)
+      if (sth[(size_t)i] != E_OK) {  // report the block's payload offset in the file
+        const int64_t fo = b->sel[(size_t)i].in_off;
+        int64_t file_off = fo;
+        if (b->planned) {
+          size_t s = 0;
+          while (s + 1 < b->segs.size() && b->sel_seg0[s + 1] <= i) ++s;
+          const BgzfBlock &orig = b->blocks[(size_t)(b->segs[s].b0 + (i - b->sel_seg0[s]))];
+          file_off = orig.in_off;
+        }
         return set_err(GQ_E_BAM_FORMAT, "corrupt BGZF block (inflate, ISIZE or CRC32) with payload at file offset %lld",
-                       (long long)b->blocks[(size_t)i].in_off);
+                       (long long)file_off);
+      }
   }
   z.inflate_ms = ms_since(t0);
-  // header (host): magic, text, reference dictionary
-  {
-    std::vector<uint8_t> h;
-    auto fetch = [&](int64_t upto) -> gq_status {
-      upto = std::min(upto, outn);
-      if ((int64_t)h.size() >= upto) return GQ_OK;
-      const int64_t have = (int64_t)h.size();
-      h.resize((size_t)upto);
-      HIP_TRY(hipMemcpy(h.data() + have, (const uint8_t *)b->out.p + have, (size_t)(upto - have),
-                        hipMemcpyDeviceToHost));
-      return GQ_OK;
-    };
-    gq_status s = fetch(1 << 16);
-    if (s) return s;
-    if (h.size() < 12 || memcmp(h.data(), "BAM\1", 4) != 0) return set_err(GQ_E_BAM_FORMAT, "not a BAM file (magic)");
-    int64_t o = 4;
-    int32_t l_text;
-    memcpy(&l_text, h.data() + o, 4);
-    o += 4;
-    if (l_text < 0 || o + l_text + 4 > outn) return set_err(GQ_E_BAM_FORMAT, "truncated BAM header");
-    if ((s = fetch(o + l_text + 4 + (1 << 16)))) return s;
-    b->text.assign((const char *)h.data() + o, (size_t)l_text);
-    while (!b->text.empty() && b->text.back() == '\0') b->text.pop_back();
-    o += l_text;
-    int32_t n_ref;
-    memcpy(&n_ref, h.data() + o, 4);
-    o += 4;
-    for (int32_t i = 0; i < n_ref; ++i) {
-      if ((s = fetch(o + 4 + (1 << 16)))) return s;
-      if (o + 4 > outn) return set_err(GQ_E_BAM_FORMAT, "truncated BAM reference dictionary");
-      int32_t l_name;
-      memcpy(&l_name, h.data() + o, 4);
-      o += 4;
-      if (l_name < 1 || o + l_name + 4 > outn) return set_err(GQ_E_BAM_FORMAT, "truncated BAM reference dictionary");
-      if ((s = fetch(o + l_name + 4))) return s;
-      b->names.emplace_back((const char *)h.data() + o, (size_t)(l_name - 1));
-      o += l_name;
-      int32_t ln;
-      memcpy(&ln, h.data() + o, 4);
-      b->lengths.push_back(ln);
-      o += 4;
-    }
-    b->rec0 = o;
-  }
   return GQ_OK;
 }
 
@@ -1081,7 +1504,7 @@ gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *fl, int64_t *
   b->scanned = false;
   auto t0 = std::chrono::steady_clock::now();
   const uint8_t *d = (const uint8_t *)b->out.p;
-  const int64_t n = b->n_out, nb = (int64_t)b->blocks.size();
+  const int64_t n = b->n_out, nb = (int64_t)b->sel.size();
   const BgzfBlock *blk = (const BgzfBlock *)b->blk.p;
   // record boundaries: candidate starts per block, chains, the host walk of the true chain
   DevBuf first, cnt, land, base, tmp;
@@ -1091,7 +1514,7 @@ gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *fl, int64_t *
   HIP_TRY(land.ensure(nbb));
   HIP_TRY(base.ensure(nbb));
   if (nb) {
-    hipLaunchKernelGGL(rec_sync, dim3(grid(nb, 4)), dim3(256), 0, c->stream, d, n, blk, nb, b->rec0, n_ref,
+    hipLaunchKernelGGL(rec_sync, dim3(grid(nb, 4)), dim3(256), 0, c->stream, d, n, blk, nb, b->planned ? 0 : b->rec0, n_ref,
                        (int64_t *)first.p);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(rec_hop, dim3(grid(nb, 256)), dim3(256), 0, c->stream, d, n, blk, (int64_t)0, nb,
@@ -1105,32 +1528,46 @@ gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *fl, int64_t *
     HIP_TRY(hipMemcpyAsync(hl.data(), land.p, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
-  int64_t at = b->rec0, n_rec = 0;
+  // the true chain, segment by segment (an unplanned load: one segment from the first record
+  // to the stream's end)
+  const std::vector<BgzfBlock> &sel = b->sel;
+  int64_t n_rec = 0;
   int64_t rehops = 0;
-  for (int64_t k = 0; k < nb; ++k) {
-    const int64_t hi = b->blocks[(size_t)k].out_off + (int64_t)b->blocks[(size_t)k].isize;
-    if (at >= hi) {  // no record of the chain starts in this block
-      hf[(size_t)k] = -1;
-      hc[(size_t)k] = 0;
-      continue;
+  const size_t n_seg = b->planned ? b->segs.size() : 1;
+  for (size_t s = 0; s < n_seg; ++s) {
+    const int64_t k0 = b->planned ? b->sel_seg0[s] : 0, k1 = b->planned ? b->sel_seg0[s + 1] : nb;
+    const bool eof = b->planned ? b->segs[s].eof : true;
+    const int64_t kr = eof ? k1 : k1 - 1;  // blocks whose records are read (the last one only completes a record)
+    int64_t at = b->planned ? sel[(size_t)k0].out_off + b->segs[s].first : b->rec0;
+    for (int64_t k = k0; k < k1; ++k) {
+      const int64_t hi = sel[(size_t)k].out_off + (int64_t)sel[(size_t)k].isize;
+      if (k >= kr || at >= hi) {  // no record of the chain starts in this block
+        hf[(size_t)k] = -1;
+        hc[(size_t)k] = 0;
+        continue;
+      }
+      if (hf[(size_t)k] != at || hl[(size_t)k] < 0) {  // a false sync (or none): re-hop from the chain
+        ++rehops;
+        hf[(size_t)k] = at;
+        HIP_TRY(hipMemcpyAsync((int64_t *)first.p + k, &at, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(rec_hop, dim3(1), dim3(64), 0, c->stream, d, n, blk, k, k + 1, (const int64_t *)first.p,
+                           (int64_t *)cnt.p, (int64_t *)land.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&hc[(size_t)k], (int64_t *)cnt.p + k, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&hl[(size_t)k], (int64_t *)land.p + k, sizeof(int64_t), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (hl[(size_t)k] < 0)
+          return set_err(GQ_E_BAM_FORMAT, "truncated BAM record %lld", (long long)(n_rec + hc[(size_t)k]));
+      }
+      n_rec += hc[(size_t)k];
+      at = hl[(size_t)k];
     }
-    if (hf[(size_t)k] != at || hl[(size_t)k] < 0) {  // a false sync (or none): re-hop from the chain
-      ++rehops;
-      hf[(size_t)k] = at;
-      HIP_TRY(hipMemcpyAsync((int64_t *)first.p + k, &at, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-      hipLaunchKernelGGL(rec_hop, dim3(1), dim3(64), 0, c->stream, d, n, blk, k, k + 1, (const int64_t *)first.p,
-                         (int64_t *)cnt.p, (int64_t *)land.p);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(&hc[(size_t)k], (int64_t *)cnt.p + k, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipMemcpyAsync(&hl[(size_t)k], (int64_t *)land.p + k, sizeof(int64_t), hipMemcpyDeviceToHost,
-                             c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (hl[(size_t)k] < 0) return set_err(GQ_E_BAM_FORMAT, "truncated BAM record %lld", (long long)(n_rec + hc[(size_t)k]));
-    }
-    n_rec += hc[(size_t)k];
-    at = hl[(size_t)k];
+    const int64_t seg_end = sel[(size_t)k1 - 1].out_off + (int64_t)sel[(size_t)k1 - 1].isize;
+    if (eof && at != seg_end) return set_err(GQ_E_BAM_FORMAT, "truncated BAM record %lld", (long long)n_rec);
+    if (!eof && at > seg_end)
+      return set_err(GQ_E_PLAN, "a BAM record runs past the end of planned segment %lld", (long long)s);
   }
-  if (at != n) return set_err(GQ_E_BAM_FORMAT, "truncated BAM record %lld", (long long)n_rec);
   std::vector<int64_t> hb((size_t)nb + 1, 0);
   for (int64_t k = 0; k < nb; ++k) hb[(size_t)k + 1] = hb[(size_t)k] + hc[(size_t)k];
   if (nb) {
@@ -1197,15 +1634,17 @@ gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *fl, int64_t *
   }
   HIP_TRY(rgf.ensure(sizeof(uint64_t) * (size_t)(fl->n_rg + 1)));
   HIP_TRY(hipMemsetAsync(rgf.p, 0xFF, sizeof(uint64_t) * (size_t)(fl->n_rg + 1), c->stream));
-  HIP_TRY(errb.ensure(2 * sizeof(uint64_t)));
+  HIP_TRY(errb.ensure(3 * sizeof(uint64_t)));
   HIP_TRY(hipMemsetAsync(errb.p, 0xFF, 2 * sizeof(uint64_t), c->stream));
+  HIP_TRY(hipMemsetAsync((uint64_t *)errb.p + 2, 0, sizeof(uint64_t), c->stream));  // the largest span
   if (n_rec) {
     hipLaunchKernelGGL(rec_parse, dim3(grid(n_rec, 256)), dim3(256), 0, c->stream, d, (const int64_t *)b->rec.p, n_rec,
                        f, (RecInfo *)b->info.p, (int64_t *)keep.p, (int64_t *)seq_k.p, (int64_t *)cig_k.p,
-                       (int64_t *)md_k.p, (unsigned long long *)rgf.p, (unsigned long long *)errb.p);
+                       (int64_t *)md_k.p, (unsigned long long *)rgf.p, (unsigned long long *)errb.p,
+                       (unsigned long long *)errb.p + 2);
     HIP_TRY(hipGetLastError());
   }
-  uint64_t err[2];
+  uint64_t err[3];
   HIP_TRY(hipMemcpyAsync(err, errb.p, sizeof(err), hipMemcpyDeviceToHost, c->stream));
   std::vector<uint64_t> rgh((size_t)fl->n_rg + 1);
   HIP_TRY(hipMemcpyAsync(rgh.data(), rgf.p, sizeof(uint64_t) * rgh.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1287,6 +1726,7 @@ gq_status gq_bam_dev_scan(gq_bam_dev *b, const gq_bam_dev_filters *fl, int64_t *
   b->n_rec = n_rec;
   b->sizes.parse_ms = ms_since(t0);
   b->sizes.n_records = n_rec;
+  b->sizes.max_span = (int64_t)err[2];
   b->sizes.n_reads = b->n_keep;
   b->sizes.seq_bytes = b->seq_bytes;
   b->sizes.cigar_len = b->cigar_len;

@@ -527,6 +527,10 @@ void scan_chunk(const gq_bam *b, const std::vector<int64_t> &recs, int64_t r0, i
               error(GQI_E_RECORD, "bad aux array type '%c'", (char)sub);
               return;
           }
+          if (cnt < 0 || q + 5 + cnt * w > end) {  // (a negative count would walk backwards)
+            error(GQI_E_FORMAT, "truncated aux array in BAM record %lld", (long long)r);
+            return;
+          }
           q += 5 + cnt * w;
           break;
         }

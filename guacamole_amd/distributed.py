@@ -114,6 +114,160 @@ def rank_share(rs, flat_loci, rank_of_range: np.ndarray, rank: int):
     return rs.subset(reads_overlapping(rs, loci[0], loci[1], loci[2])), loci
 
 
+def _positions(flat_loci):
+    """Each flattened range's first locus as a position in loci order (flatten order: task,
+    contig, start — tasks take consecutive loci, so this is LociSet order) and each task's
+    (first position, loci)."""
+    contig, start, end, task = (np.asarray(a) for a in flat_loci)
+    n = np.asarray(end, np.int64) - np.asarray(start, np.int64)
+    pos = np.concatenate([[0], np.cumsum(n)])[:-1] if len(n) else np.zeros(0, np.int64)
+    return pos, n
+
+
+def ranks_by_position(flat_loci, bounds: Sequence[int]) -> np.ndarray:
+    """Rank of each flattened range: every task goes whole to the rank whose loci-position
+    interval [bounds[r], bounds[r + 1]) holds the task's middle locus (contiguous blocks of
+    tasks, rank order = task order)."""
+    contig, start, end, task = (np.asarray(a) for a in flat_loci)
+    if len(task) == 0:
+        return np.zeros(0, np.int64)
+    pos, n = _positions(flat_loci)
+    tasks, first = np.unique(task, return_index=True)
+    tot = np.zeros(len(tasks), np.int64)
+    np.add.at(tot, np.searchsorted(tasks, task), n)
+    mid = pos[first] + tot // 2
+    rot = np.clip(np.searchsorted(np.asarray(bounds[1:-1], np.int64), mid, "right"), 0, len(bounds) - 2)
+    rot = np.maximum.accumulate(rot)
+    return rot[np.searchsorted(tasks, task)]
+
+
+def loci_of(flat_loci, names: Sequence[str]) -> LociSet:
+    """The LociSet of some flattened ranges (contig ids index `names`)."""
+    from .loci import LociMapBuilder
+    b = LociMapBuilder()
+    for c, s, e in zip(*(np.asarray(a) for a in flat_loci[:3])):
+        b.put(names[int(c)], int(s), int(e), 0)
+    return LociSet(b.result())
+
+
+def covers(outer: LociSet, inner: LociSet) -> bool:
+    """Every locus of `inner` is in `outer`."""
+    for c in inner.contigs:
+        o = outer.on_contig(c).ranges
+        starts = [s for s, _ in o]
+        import bisect
+        for s, e in inner.on_contig(c).ranges:
+            i = bisect.bisect_right(starts, s) - 1
+            if i < 0 or o[i][1] < e:
+                return False
+    return True
+
+
+def _all_true(ok: bool, device) -> bool:
+    """Logical AND of a flag over the ranks (so every rank takes the same branch)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=torch.device(device))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def all_gather_objects(obj) -> list:
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def device_ingest_ranks(ctx, paths: Sequence[str], filters, builder, parallelism: int, accuracy: int, rank: int,
+                        world: int, device):
+    """The multi-GPU ingest: each rank decodes on its own GPU only the BGZF blocks whose records
+    can overlap its tasks' loci (bamdev.load_reads_device with a region; the reference ships a
+    read to exactly the tasks it overlaps, DistributedUtil.scala:584-597), with no host copy of
+    the whole input on any rank.  Returns ([DeviceReadSet per path], this rank's flattened loci
+    ranges with their task ids, the contig names) or None when some rank cannot take the device
+    path (plain gzip, an unsorted file, device memory): every rank then takes the host loader."""
+    from .bamdev import MappedBam, load_reads_device
+    maps = [MappedBam(p, populate=False) for p in paths]
+    if not _all_true(all(m.ok for m in maps), device):
+        return None
+    dicts = [m.contigs() for m in maps]
+    names, lengths = dicts[0]
+    if any(d != dicts[0] for d in dicts[1:]):
+        raise ValueError("Tumor and normal samples have different sequence dictionaries.")
+    first = {"maps": maps}
+
+    def load(region):
+        ms = first.pop("maps", [None] * len(paths))  # the host mappings serve the first load
+        return [load_reads_device(ctx, p, filters, m, region=region) for p, m in zip(paths, ms)]
+    got = rank_loci_and_reads(load, names, lengths, builder, parallelism, accuracy, rank, world, device)
+    return None if got is None else (got[0], got[1], names)
+
+
+def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accuracy: int, rank: int, world: int,
+                        device):
+    """This rank's share of the single-process task partition and its reads, with reads loaded
+    by region only: load(LociSet) -> [read set per input] (None entries: that input cannot be
+    loaded so; every rank then gives up, None).
+
+    partitionLociUniformly (DistributedUtil.scala:83-108) needs no reads.  For
+    partitionLociByApproximateDepth (:162-251) the micro partitions are split across the ranks;
+    each rank loads its share (+ 5 % slack each side), counts the reads overlapping its own micro
+    partitions (:181-189), and an all-reduce of the counts gives every rank the counts one
+    process computes — so the same tasks.  Tasks go whole to ranks in contiguous blocks
+    (ranks_by_position); a rank whose tasks reach past what it loaded loads its tasks' loci."""
+    from .loci import (LociMapBuilder, flatten_partitions, micro_partition_count, partition_loci_by_counts,
+                       partition_loci_uniformly, _region_counts)
+    loci = builder.result(dict(zip(names, lengths)))
+    tasks = parallelism if parallelism > 0 else max(1, world)
+    cidx = {c: i for i, c in enumerate(names)}
+    sets = None
+    decoded = None
+    if accuracy == 0 or (tasks == 1 and loci.count > 0):
+        parts = partition_loci_uniformly(tasks, loci)
+        flat = flatten_partitions(parts, cidx)
+        total = int(loci.count)
+        bounds = [total * r // world for r in range(world + 1)]
+    else:
+        n_micro = micro_partition_count(tasks, loci, accuracy)
+        micro = partition_loci_uniformly(n_micro, loci)
+        inv = micro.as_inverse_map()
+        m0, m1 = rank * n_micro // world, (rank + 1) * n_micro // world
+        slack = max(1, (m1 - m0) // 20)
+        b = LociMapBuilder()
+        for m in range(max(0, m0 - slack), min(n_micro, m1 + slack)):
+            b.put_set(inv[m], 0)
+        decoded = LociSet(b.result())
+        sets = load(decoded)
+        if not _all_true(all(x is not None for x in sets), device):
+            return None
+        counts = np.zeros(n_micro, np.int64)
+        for x in sets:
+            counts += _region_counts(micro, x.regions(), n_micro)
+        counts[:m0] = 0
+        counts[m1:] = 0
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(counts).to(torch.device(device))
+        dist.all_reduce(t)
+        counts = t.cpu().numpy()
+        parts = partition_loci_by_counts(tasks, loci, micro, counts)
+        flat = flatten_partitions(parts, cidx)
+        sizes = np.array([inv[m].count for m in range(n_micro)], np.int64)
+        edge = np.concatenate([[0], np.cumsum(sizes)])
+        bounds = [int(edge[r * n_micro // world]) for r in range(world + 1)]
+    rr = ranks_by_position(flat, bounds)
+    sel = rr == rank
+    mine = tuple(np.ascontiguousarray(np.asarray(a)[sel]) for a in flat)
+    region = loci_of(mine, names)
+    if sets is None or not covers(decoded, region):
+        sets = None  # (the first load's memory goes before the second)
+        sets = load(region)
+    if not _all_true(all(x is not None for x in sets), device):
+        return None
+    return sets, mine
+
+
 def _gatherv_to_rank0(mine, sizes: List[int], device):
     """Variable-size gather of one uint8 tensor per rank (``mine``: exactly ``sizes[rank]``
     bytes, on ``device``) to rank 0, rank order.  Every rank's bytes travel once, at their own

@@ -369,11 +369,24 @@ def partition_loci_by_approximate_depth(tasks: int, loci_used: LociSet, accuracy
     assert tasks >= 1
     assert loci_used.count > 0
     assert len(region_sets) > 0
-    n_micro = accuracy * tasks if accuracy * tasks < loci_used.count else loci_used.count
+    n_micro = micro_partition_count(tasks, loci_used, accuracy)
     micro = partition_loci_uniformly(n_micro, loci_used)
     counts = np.zeros(n_micro, dtype=np.int64)
     for rs in region_sets:
         counts += _region_counts(micro, rs, n_micro)
+    return partition_loci_by_counts(tasks, loci_used, micro, counts)
+
+
+def micro_partition_count(tasks: int, loci_used: LociSet, accuracy: int) -> int:
+    """numMicroPartitions (DistributedUtil.scala:172-173)."""
+    return accuracy * tasks if accuracy * tasks < loci_used.count else loci_used.count
+
+
+def partition_loci_by_counts(tasks: int, loci_used: LociSet, micro: LociMap, counts: np.ndarray) -> LociMap:
+    """The second half of partitionLociByApproximateDepth (DistributedUtil.scala:191-251): the
+    greedy proportional take over micro partitions, from their region counts (computed in one
+    process, or summed over ranks that each counted their own micro partitions)."""
+    n_micro = len(counts)
     total = int(counts.sum())
     regions_per_task = max(1.0, total / float(tasks))
     inverse = micro.as_inverse_map()

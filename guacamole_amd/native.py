@@ -154,7 +154,7 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_vaf_histogram", "gq_germline_standard", "gq_bam_dev_open", "gq_bam_dev_close", "gq_bam_dev_header_text",
             "gq_bam_dev_n_contigs", "gq_bam_dev_contig_name", "gq_bam_dev_contig_length", "gq_bam_dev_scan",
             "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin", "gq_reads_download", "gq_bam_dev_map",
-            "gq_bam_dev_load")
+            "gq_bam_dev_load", "gq_bam_dev_map_ex", "gq_bam_dev_plan", "gq_bam_dev_plan_segments")
 
 
 def lib():
@@ -204,6 +204,12 @@ def lib():
         L.gq_bam_dev_open.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
         L.gq_bam_dev_map.argtypes = [C.c_char_p, C.POINTER(vp)]
         L.gq_bam_dev_map.restype = C.c_int
+        L.gq_bam_dev_map_ex.argtypes = [C.c_char_p, C.c_int32, C.POINTER(vp)]
+        L.gq_bam_dev_map_ex.restype = C.c_int
+        L.gq_bam_dev_plan.argtypes = [vp, vp, vp, vp, C.c_int64, C.c_char_p, vp]
+        L.gq_bam_dev_plan.restype = C.c_int
+        L.gq_bam_dev_plan_segments.argtypes = [vp, vp, vp, vp, vp]
+        L.gq_bam_dev_plan_segments.restype = C.c_int
         L.gq_bam_dev_load.argtypes = [vp, vp]
         L.gq_bam_dev_load.restype = C.c_int
         L.gq_bam_dev_close.argtypes = [vp]

@@ -428,7 +428,10 @@ def _load_bam_py(path: str, filters: InputFilters) -> ReadSet:
             elif ty == "B":
                 sub = chr(data[p])
                 (cnt,) = struct.unpack_from("<i", data, p + 1)
-                p += 5 + cnt * {"c": 1, "C": 1, "s": 2, "S": 2, "i": 4, "I": 4, "f": 4}[sub]
+                q = p + 5 + cnt * {"c": 1, "C": 1, "s": 2, "S": 2, "i": 4, "I": 4, "f": 4}[sub]
+                if cnt < 0 or q > off:
+                    raise ReadLoadError("truncated aux array in BAM record")
+                p = q
             else:
                 raise ReadLoadError("bad aux type %r" % ty)
         unmapped = bool(flag & FLAG_UNMAPPED) or ref_id < 0

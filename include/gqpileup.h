@@ -54,7 +54,10 @@ typedef enum {
   GQ_E_BAM_FORMAT = 12,     /* not BAM, corrupt BGZF block, truncated record   (GQI_E_FORMAT) */
   GQ_E_BAM_RECORD = 13,     /* ReadLoadError: bad aux type, missing qualities  (GQI_E_RECORD) */
   GQ_E_MD_PARSE = 14,       /* MdTag parse error (ADAM MdTag.apply)            (GQI_E_MD)     */
-  GQ_E_NOT_BGZF = 15        /* a gzip stream without BGZF block sizes: use the host loader    */
+  GQ_E_NOT_BGZF = 15,       /* a gzip stream without BGZF block sizes: use the host loader    */
+  GQ_E_PLAN = 16            /* a region plan (gq_bam_dev_plan) does not hold for this file:   */
+                            /* not coordinate-sorted, or a record runs past a planned segment */
+                            /* (load the whole file instead)                                  */
 } gq_status;
 
 /* CIGAR ops use BAM packing: len << 4 | op, op in M I D N S H P = X -> 0..8. */
@@ -226,10 +229,46 @@ gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 typedef struct gq_bam_dev gq_bam_dev;
 
 gq_status gq_bam_dev_open(gq_ctx *ctx, const char *path, gq_bam_dev **out);
-/* gq_bam_dev_open in two steps: map (host only: the file and its BGZF block table; may run
- * while the device context starts) and load (copy, inflate, header) on a context.           */
+/* gq_bam_dev_open in two steps: map (host only: the file, its BGZF block table and the header,
+ * inflated on the host; may run while the device context starts) and load (copy, inflate) on
+ * a context.  gq_bam_dev_map_ex(populate = 0) maps without faulting the whole file in (for a
+ * region-restricted load, which reads only its segments' pages).                            */
 gq_status gq_bam_dev_map(const char *path, gq_bam_dev **out);
+gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out);
 gq_status gq_bam_dev_load(gq_ctx *ctx, gq_bam_dev *mapped);
+
+/* Region-restricted load (the multi-GPU ingest): one rank reads only the records that can
+ * overlap its loci — the reads the reference ships to that rank's tasks
+ * (DistributedUtil.scala:584-597; the whole-file read Read.scala:368-451 is what it replaces
+ * at world size > 1).  Host only, before gq_bam_dev_load.  Loci: per contig of the BAM's
+ * dictionary, sorted disjoint half-open ranges (loci_begin[n_contigs + 1] indexes
+ * loci_start / loci_end, as gq_bam_dev_filters).  Each range's records are found
+ *   * from the BAI linear index (`bai_path`; NULL or "" for none): the first record that can
+ *     overlap the range's first locus (exact for any read length); or, without an index,
+ *     by host probes of BGZF blocks (binary search over the blocks' last record keys), from
+ *     `halo` loci before the range;
+ *   * up to the first BGZF block whose records all start at or past the range's end (probes).
+ * Ranges whose blocks meet are merged into one segment.  The next gq_bam_dev_load copies and
+ * inflates only the segments' blocks; gq_bam_dev_scan walks each segment's records from its
+ * first record.  GQ_E_PLAN: the header does not declare SO:coordinate, or the index does not
+ * fit the file (then load the whole file).                                                  */
+typedef struct {
+  int64_t n_segments;
+  int64_t n_blocks;        /* BGZF blocks the load will inflate                                  */
+  int64_t comp_bytes;      /* their compressed bytes (the load's host -> device copy)          */
+  int64_t bam_bytes;       /* their inflated bytes                                             */
+  int64_t probes;          /* host probes (blocks inflated on the host to read record keys)    */
+  int32_t used_index;      /* 1: range starts from the BAI linear index                        */
+  int32_t pad;
+} gq_bam_dev_plan_info;
+gq_status gq_bam_dev_plan(gq_bam_dev *b, const int64_t *loci_begin, const int64_t *loci_start,
+                          const int64_t *loci_end, int64_t halo, const char *bai_path,
+                          gq_bam_dev_plan_info *info);
+/* The planned segments (n_segments entries each): first BGZF block, offset of the first record
+ * in that block's inflated bytes, end block (exclusive), and whether records run to the end of
+ * the file (else block end - 1 is read only to complete the last record before it).         */
+gq_status gq_bam_dev_plan_segments(const gq_bam_dev *b, int64_t *first_block, int64_t *first_offset,
+                                   int64_t *end_block, int32_t *to_eof);
 void gq_bam_dev_close(gq_bam_dev *b);
 const char *gq_bam_dev_header_text(const gq_bam_dev *b); /* SAM text, trailing NULs stripped */
 int32_t gq_bam_dev_n_contigs(const gq_bam_dev *b);
@@ -256,6 +295,7 @@ typedef struct {
   int64_t comp_bytes, bam_bytes; /* compressed file / inflated stream */
   int64_t n_blocks;        /* BGZF blocks                   */
   float map_ms, h2d_ms, inflate_ms, records_ms, parse_ms;  /* open: map + block walk, copy, inflate; scan */
+  int64_t max_span;        /* largest reference span (end - start) of a mapped record scanned  */
 } gq_bam_dev_sizes;
 
 /* rg_first[k] (k < n_rg): file-order index of the first kept record whose RG tag is header ID

@@ -148,3 +148,66 @@ def test_gatherv_gloo_world3_exact_sizes():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == [list(range(5)), [], [2 + i for i in range(17)]]
+
+
+def _plan_worker(rank, world, port, q, parallelism, accuracy):
+    """rank_loci_and_reads with the host loader standing in for the device one: each load
+    returns only the reads overlapping the region, as a region-restricted BAM load does."""
+    import torch.distributed as dist
+    from guacamole_amd.distributed import rank_loci_and_reads
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = _chrm()
+    loads = []
+
+    def load(region):
+        loads.append([(s, e) for _, s, e in region.ranges()])
+        idx = reads_overlapping(full, *[np.asarray(a) for a in zip(*[(0, s, e) for _, s, e in region.ranges()])])
+        return [full.subset(idx)]
+    sets, mine = rank_loci_and_reads(load, full.contig_names, full.contig_lengths, LociSet.parse("all"), parallelism,
+                                     accuracy, rank, world, "cpu")
+    q.put((rank, [a.tolist() for a in mine], int(sets[0].n), loads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_loci_world2_equal_one_process_partition():
+    """The ranks' task split is the one-process partition (uniform, and by approximate depth with
+    the micro-partition counts summed over ranks), every task on exactly one rank, and each rank
+    holds exactly the reads overlapping its tasks' loci."""
+    from guacamole_amd.commands import partition
+    full = _chrm()
+    loci = LociSet.parse("all").result(full.contig_lengths_map)
+    for parallelism, accuracy in ((5, 0), (2, 250), (7, 250)):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_plan_worker, args=(r, 2, port, q, parallelism, accuracy)) for r in range(2)]
+        for p in ps:
+            p.start()
+        got = sorted(q.get(timeout=120) for _ in range(2))
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        want = flatten_partitions(partition(loci, parallelism, accuracy, full), full.contig_index())
+        joined = [np.concatenate([np.asarray(g[1][k]) for g in got]) for k in range(4)]
+        for a, b in zip(joined, want):
+            assert np.array_equal(a, b), (parallelism, accuracy)
+        for rank, mine, n, loads in got:
+            assert len(mine[0]) > 0
+            # the rank holds the reads overlapping what it loaded: exactly its tasks' loci, or (by
+            # depth, when the micro-partition share + slack already covers its tasks) a superset
+            need = len(reads_overlapping(full, *[np.asarray(x) for x in mine[:3]]))
+            last = np.asarray(loads[-1])
+            assert n == len(reads_overlapping(full, np.zeros(len(last), np.int32), last[:, 0], last[:, 1]))
+            assert n >= need
+            if loads[-1] == [(int(s), int(e)) for s, e in zip(mine[1], mine[2])]:
+                assert n == need
+            # uniform: one load of the tasks' loci; by depth: the micro-partition share (+ slack),
+            # then the tasks' loci again where the depth-balanced cut lies outside it (chrM's depth
+            # varies 2x along the contig)
+            assert len(loads) <= (1 if accuracy == 0 else 2), loads
+            if accuracy == 0:
+                assert n == need

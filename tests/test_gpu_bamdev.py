@@ -161,3 +161,83 @@ def test_cli_device_ingest_equals_host(tmp_path):
                     "--out", str(out)])
         outs[mode] = out.read_text()
     assert outs["device"] == outs["host"]
+
+
+# ---- region-restricted loads (the multi-GPU ingest, gq_bam_dev_plan) ------------------------
+def compare_region(ctx, path, f, region, halo=bamdev.DEFAULT_HALO):
+    """A planned device load of `region` against the host loader's reads overlapping it."""
+    from guacamole_amd.distributed import reads_overlapping
+    host = load_reads(path, f)
+    idx = host.contig_index()
+    rng = [(idx[c], s, e) for c, s, e in region.ranges()]
+    sub = host.subset(reads_overlapping(host, *[np.asarray(a) for a in zip(*rng)])) if rng else host.subset([])
+    want = soa.pack(sub)
+    dev = bamdev.load_reads_device(ctx, path, f, region=region, halo=halo)
+    assert dev is not None and dev.n == sub.n
+    got = bamdev.download(dev.reads)
+    for k in KEYS:
+        assert np.array_equal(got[k], want[k]), k
+    return dev
+
+
+@pytest.mark.parametrize("index", [False, True])
+def test_region_load_equals_host_subset(gpu_ctx, tmp_path, index):
+    from tests.test_region_plan import CONTIGS as RC, HEADER as RH, _records as region_records
+    rng = random.Random(21 + index)
+    p = str(tmp_path / "r.bam")
+    bw.write_bam(p, RH, RC, region_records(rng, 4000, long_every=40), block=4000, index=index)
+    f = InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True)
+    lengths = dict(RC)
+    for expr in ("c2:100000-100500", "c1:0-50000,c10:150000-200000", "c1:200000-210000,c1:230000-240000", "c2"):
+        dev = compare_region(gpu_ctx, p, f, LociSet.parse(expr).result(lengths))
+        plan = dev.timings["plan"]
+        assert plan is not None and plan["used_index"] == int(index)
+        assert dev.timings["blocks"] < 0.8 * 440  # a part of the ~440-block file
+    # a halo shorter than the 3 kb reads: without an index the load plans again from the span it saw
+    dev = compare_region(gpu_ctx, p, f, LociSet.parse("c1:100000-100100").result(lengths), halo=500)
+    assert dev.timings["replans"] == (0 if index else 1)
+
+
+def test_region_load_gatk_bundle(gpu_ctx):
+    p = fixture("gatk_mini_bundle_extract.bam")
+    f = InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, passed_vendor_quality_checks=True,
+                          has_md_tag=True)
+    host = load_reads(p, f)
+    c = host.contig_names[int(host.contig[0])]
+    s0, s1 = int(host.start[0]), int(host.start[-1])
+    region = LociSet.parse("%s:%d-%d" % (c, (s0 + s1) // 2, (s0 + s1) // 2 + 200)).result(host.contig_lengths_map)
+    compare_region(gpu_ctx, p, f, region)
+
+
+def test_region_load_without_sort_order_reads_everything(gpu_ctx, tmp_path):
+    """No SO:coordinate: no plan, the whole file decoded and filtered to the region."""
+    from tests.test_region_plan import CONTIGS as RC, _records as region_records
+    p = str(tmp_path / "n.bam")
+    bw.write_bam(p, "@HD\tVN:1.6\n", RC, region_records(random.Random(3), 500))
+    dev = compare_region(gpu_ctx, p, InputFilters(), LociSet.parse("c2:1000-40000").result(dict(RC)))
+    assert dev.timings["plan"] is None
+
+
+@pytest.mark.parametrize("level,strategy", [(0, 0), (6, 4)])  # stored blocks; fixed Huffman codes (Z_FIXED)
+def test_stored_and_fixed_huffman_blocks(gpu_ctx, tmp_path, level, strategy):
+    rng = random.Random(31 + level)
+    p = str(tmp_path / "z.bam")
+    bw.write_bam(p, HEADER, CONTIGS, _sorted(_records(rng, 1500, CONTIGS)), level=level, strategy=strategy)
+    compare(gpu_ctx, p, InputFilters())
+
+
+def test_malformed_aux_array(gpu_ctx, tmp_path):
+    """A B array whose count is negative (or runs past the record) is a truncated aux array, on
+    the device as on the host loader (it must not walk the aux scan backwards)."""
+    bad = b"ZBB" + b"i" + (-2).to_bytes(4, "little", signed=True) + b"\0" * 8
+    p = str(tmp_path / "b.bam")
+    bw.write_bam(p, "", CONTIGS, [bw.record(0, 10, "a", "4M", "ACGT", [30] * 4, tags=bad)])
+    with pytest.raises(ReadLoadError, match="truncated aux array"):
+        load_reads(p)
+    with pytest.raises(ReadLoadError, match="truncated aux array"):
+        bamdev.load_reads_device(gpu_ctx, p, InputFilters())
+    long_arr = b"ZBB" + b"C" + (1000).to_bytes(4, "little") + b"\0" * 4
+    q = str(tmp_path / "c.bam")
+    bw.write_bam(q, "", CONTIGS, [bw.record(0, 10, "a", "4M", "ACGT", [30] * 4, tags=long_arr)])
+    with pytest.raises(ReadLoadError, match="truncated aux array"):
+        bamdev.load_reads_device(gpu_ctx, q, InputFilters())

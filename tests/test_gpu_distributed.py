@@ -7,6 +7,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import fixture
@@ -21,8 +22,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(args, world, out):
-    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+def _run(args, world, out, reports=None):
+    """The CLI at `world` ranks; reports: a list that receives each rank's GQ_TIMING report."""
+    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT, GQ_TIMING="1")
     if world == 1:
         cmd = [sys.executable, "-m", "guacamole_amd"] + args + ["--out", out]
     else:
@@ -30,6 +32,11 @@ def _run(args, world, out):
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "guacamole_amd"] + args + ["--out", out]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if reports is not None:
+        import json
+        for line in r.stderr.splitlines():
+            if "GQ_TIMING " in line:
+                reports.append(json.loads(line.split("GQ_TIMING ", 1)[1]))
     with open(out) as fh:
         return fh.read()
 
@@ -88,3 +95,60 @@ def test_rccl_gather_branch_world_one():
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert '"identical": true' in r.stdout
+
+
+def _synthetic_bam(tmp_path, name, length, depth, seed, index):
+    from guacamole_amd import synthetic
+    from tests import bam_writer as bw
+    p = str(tmp_path / name)
+    synthetic.generate(length, depth, seed=synthetic.SEED + seed).write_bam(p)
+    if index:
+        bw.index_bam(p)
+    return p
+
+
+@pytest.mark.parametrize("index", [False, True])
+@pytest.mark.parametrize("parallelism,accuracy", [("5", "0"), ("4", "250")])
+def test_germline_two_ranks_device_ingest_equal_one(tmp_path, index, parallelism, accuracy):
+    """configs[3]'s multi-GPU ingest on one GPU: each of two ranks decodes on the device only the
+    BGZF blocks its tasks need (from the BAI, or by host probes without one) — no rank loads the
+    whole file — and the gathered VCF equals one process's.  Each rank holds exactly the reads
+    overlapping its tasks' loci (uniform tasks), or those of its micro-partition share when that
+    already covers its tasks (by depth: a superset, the same calls)."""
+    from guacamole_amd.distributed import ranks_by_position, reads_overlapping
+    from guacamole_amd.loci import LociSet, flatten_partitions, partition_loci_uniformly
+    from guacamole_amd.reads import InputFilters, load_reads
+    bam = _synthetic_bam(tmp_path, "g.bam", 300_000, 30.0, 8, index)
+    args = ["germline-threshold", "--reads", bam, "--parallelism", parallelism, "--partition-accuracy", accuracy]
+    one = _run(args, 1, str(tmp_path / "one.json"))
+    reps = []
+    two = _run(args, 2, str(tmp_path / "two.json"), reps)
+    assert one == two and one.count("\n") > 100
+    assert len(reps) == 2
+    host = load_reads(bam, InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True))
+    comp = []
+    for rep in sorted(reps, key=lambda r: r["rank"]):
+        plan = rep["device_ingest"]["plan"]
+        assert rep["ingest"] == "device" and plan is not None and plan["used_index"] == int(index)
+        comp.append(plan["comp_bytes"])
+    total = os.path.getsize(bam)
+    assert sum(comp) < 1.3 * total and max(comp) < 0.75 * total, (comp, total)
+    if accuracy == "0":
+        loci = LociSet.parse("all").result(host.contig_lengths_map)
+        flat = flatten_partitions(partition_loci_uniformly(int(parallelism), loci), host.contig_index())
+        rr = ranks_by_position(flat, [0, loci.count // 2, loci.count])
+        for rep in reps:
+            mine = [np.asarray(a)[rr == rep["rank"]] for a in flat]
+            assert rep["reads"] == len(reads_overlapping(host, *mine[:3]))
+
+
+def test_somatic_two_ranks_device_ingest_equal_one(tmp_path):
+    tumor = _synthetic_bam(tmp_path, "t.bam", 200_000, 40.0, 9, True)
+    normal = _synthetic_bam(tmp_path, "n.bam", 200_000, 30.0, 10, False)
+    args = ["somatic-standard", "--tumor-reads", tumor, "--normal-reads", normal, "--loci", "20:10000-190000",
+            "--parallelism", "3", "--partition-accuracy", "0", "--odds", "2"]
+    one = _run(args, 1, str(tmp_path / "one.json"))
+    reps = []
+    two = _run(args, 2, str(tmp_path / "two.json"), reps)
+    assert one == two and one.count("\n") > 10
+    assert all(r.get("ingest") == "device" for r in reps) and len(reps) == 2
