@@ -216,16 +216,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// One wave over projection slice `slot` (the block-row pool, ProjRec in gq_kernels.h): its
-// reads are those of the slice's contig with pmax_end > the slice's first locus and start <
-// its end, in read order; each piece (a read's columns inside the slice) takes the first row
-// that is free from its first column (greedy interval partitioning over pieces sorted by first
-// column: as many rows as the slice's deepest column has reads).  Returns the slice's rows,
-// or -1 past kSliceRowsMax.  With kWords, put(active, read, column, row) then runs once per
-// word with every lane of the wave (uniform control flow), active for lanes that hold a word.
-template <bool kWords, class F>
-__device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t slot, F &&put) {
-  const int lane = threadIdx.x & 63;
+// Projection slice `slot` (the block-row pool, ProjRec in gq_kernels.h): its contig c, its
+// 16-column span [qc0, qc0 + 16) and its read window [ra, rz) — the reads of the contig with
+// pmax_end > the slice's first locus and start < its end, in read order (every read with a piece
+// in the slice, and the reads between them).
+struct SliceWin {
+  int32_t c, qc0;
+  int64_t ra, rz;
+};
+__device__ __forceinline__ SliceWin slice_window(const DevReads &R, int64_t slot) {
   int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
@@ -234,7 +233,7 @@ __device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t sl
   }
   const int c = lo;
   const int32_t q = (int32_t)(slot - R.qoff[c]);
-  const int32_t L = 128 * q, qc0 = 16 * q, qc1 = qc0 + 16;
+  const int32_t L = 128 * q;
   const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
   int64_t a0 = cb, a1 = ce;
   while (a0 < a1) {  // first read with pmax_end > L
@@ -249,7 +248,43 @@ __device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t sl
     if (R.start[m] >= L + 128) a1 = m;
     else a0 = m + 1;
   }
-  const int64_t rz = a0;
+  return SliceWin{c, 16 * q, ra, a0};
+}
+
+// Slice `slot` with its stored window (slice_windows + the scan of its sizes).
+__device__ __forceinline__ SliceWin slice_stored(const DevReads &R, int64_t slot) {
+  int lo = 0, hi = R.n_contigs - 1;  // contig: last c with qoff[c] <= slot
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (R.qoff[m] <= slot) lo = m;
+    else hi = m - 1;
+  }
+  const int64_t ra = R.sra[slot];
+  return SliceWin{lo, 16 * (int32_t)(slot - R.qoff[lo]), ra, ra + (R.soff[slot + 1] - R.soff[slot])};
+}
+
+// Read r's piece in a slice: first column (slice-relative s0 - qc0 = its offset) and length in
+// columns; sl = 0: no piece (the read ends before the slice, or the projection cannot take it).
+__device__ __forceinline__ void slice_piece(const DevReads &R, int64_t r, int32_t qc0, int32_t &s0, int32_t &sl) {
+  s0 = qc0;
+  sl = 0;
+  const ProjRec p = R.prec[r];
+  if (p.col1 != kProjNone) {
+    s0 = p.col0 > qc0 ? p.col0 : qc0;
+    const int32_t e = p.col1 < qc0 + 16 ? p.col1 : qc0 + 16;
+    sl = e > s0 ? e - s0 : 0;
+  }
+}
+
+// One wave over slice `slot` with window [ra, rz): each piece (a read's columns inside the slice)
+// takes the first row that is free from its first column — greedy interval partitioning over
+// pieces sorted by first column, which is read order (reads are sorted by start; pieces of reads
+// that began before the slice all start at its column 0): as many rows as the slice's deepest
+// column has reads.  Each read's row goes to rows[r - ra] (0xFFFF: no piece), so the fill kernels
+// place words without redoing this serial pass.  Returns the slice's rows, or -1 past
+// kSliceRowsMax.
+__device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const SliceWin &W, uint16_t *__restrict__ rows) {
+  const int lane = threadIdx.x & 63;
   // row k's first free column (0-16) is byte k & 3 of rend[k >> 8] on lane (k >> 2) & 63;
   // 0x7F: not opened.  A free row: byte <= s, tested four at a time without borrows.
   constexpr int kRD = kSliceRowsMax / 256;
@@ -258,23 +293,16 @@ __device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t sl
   for (int j = 0; j < kRD; ++j) rend[j] = 0x7F7F7F7Fu;
   int32_t nrows = 0;
   bool over = false;
-  for (int64_t r0 = ra; r0 < rz; r0 += 64) {
+  for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
-    int32_t s0 = 0, sl = 0;
-    if (r < rz) {
-      const ProjRec p = R.prec[r];
-      if (p.col1 != kProjNone) {
-        s0 = p.col0 > qc0 ? p.col0 : qc0;
-        const int32_t e = p.col1 < qc1 ? p.col1 : qc1;
-        sl = e > s0 ? e - s0 : 0;
-      }
-    }
+    int32_t s0 = W.qc0, sl = 0;
+    if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
     int32_t myrow = -1;
     unsigned long long pend = __ballot(sl > 0);
     while (pend) {  // the batch's pieces in read order (uniform)
       const int pl = __ffsll((long long)pend) - 1;
       pend &= pend - 1;
-      const uint32_t ps = (uint32_t)__builtin_amdgcn_readlane(s0 - qc0, pl);
+      const uint32_t ps = (uint32_t)__builtin_amdgcn_readlane(s0 - W.qc0, pl);
       const uint32_t pe = ps + (uint32_t)__builtin_amdgcn_readlane(sl, pl);
       const uint32_t lim = (ps + 1u) * 0x01010101u;
       int32_t k = -1;
@@ -302,22 +330,42 @@ __device__ __forceinline__ int32_t walk_slice_rows(const DevReads &R, int64_t sl
         if (j == (k >> 8) && lane == kl) rend[j] = (rend[j] & ~(0xFFu << sh)) | (pe << sh);
       if (lane == pl) myrow = k;
     }
-    if constexpr (kWords) {
-      const uint32_t len = myrow >= 0 ? (uint32_t)sl : 0u;
-      const uint32_t incl = wave_incl_scan(len), ex = incl - len;
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
-        const uint32_t w = w0 + (uint32_t)lane;
-        int k = 0;  // the last lane whose words start at or before w
-#pragma unroll
-        for (int b = 32; b >= 1; b >>= 1)
-          if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
-        const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
-        put(w < tot, r0 + k, col, __shfl(myrow, k, 64));
-      }
-    }
+    if (rows && r < W.rz) rows[r - W.ra] = myrow >= 0 ? (uint16_t)myrow : (uint16_t)0xFFFFu;
   }
   return over ? -1 : nrows;
+}
+
+// put(active, read, column, row) once per word of the slice's pieces, rows from
+// slice_assign_rows (rows[r - ra]), every lane of the wave in uniform control flow, active for
+// lanes that hold a word; a batch's words go out in piece order (consecutive words of a piece
+// to consecutive lanes).
+template <class F>
+__device__ __forceinline__ void slice_words(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
+                                            F &&put) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
+    const int64_t r = r0 + lane;
+    int32_t s0 = W.qc0, sl = 0, myrow = -1;
+    if (r < W.rz) {
+      const uint16_t k = rows[r - W.ra];
+      if (k != 0xFFFFu) {
+        slice_piece(R, r, W.qc0, s0, sl);
+        myrow = k;
+      }
+    }
+    const uint32_t len = myrow >= 0 ? (uint32_t)sl : 0u;
+    const uint32_t incl = wave_incl_scan(len), ex = incl - len;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
+      const uint32_t w = w0 + (uint32_t)lane;
+      int k = 0;  // the last lane whose words start at or before w
+#pragma unroll
+      for (int b = 32; b >= 1; b >>= 1)
+        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+      const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
+      put(w < tot, r0 + k, col, __shfl(myrow, k, 64));
+    }
+  }
 }
 
 // Wave-aggregated reservation of n <= 3 slots per lane on an LDS counter: lane prefixes
@@ -438,6 +486,9 @@ struct gq_dev_reads {
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
   int64_t n_rows = 0;                                      // projection rows (kProjRowBytes each, ProjRec)
   float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
+  bool projected = false;          // the projection is derived (ensure_projection)
+  void *nnb = nullptr;             // N bases per read (pool_clean), for the projection's sparse entries
+  float proj_ms = 0;               // ensure_projection's wall time
   mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
   mutable int mproj_mapq = -1;
   mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMarginNone (no bound)
@@ -520,6 +571,8 @@ struct H2DStager {
 // Upload-time derivation of a resident read set whose SoA arrays (and host copy of
 // contig_read_begin) are in place: validation, read shape, projection pool, block index.
 gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
+// The projection (ProjRec) of a resident read set, derived on first use.
+gq_status ensure_projection(gq_ctx *c, const gq_dev_reads *d);
 
 // Loci ranges -> locus tiles of T loci with each tile's read window in `rd`, written to `tiles`.
 gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,

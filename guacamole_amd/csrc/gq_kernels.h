@@ -60,6 +60,9 @@ struct DevReads {
   const uint2 *pev;             // per read: its sparse entries (MD events, N bases, complex ranges)
   const int64_t *pev_off;       // n_reads + 1 offsets into pev
   const uint8_t *pbad;          // per slice: 1 if a read the projection cannot take overlaps it
+  const int64_t *sra;           // per slice: the first read of its window (slice_window)
+  const int64_t *soff;          // per slice + 1: offsets of its window's reads' rows in prow
+  const uint16_t *prow;         // per (slice, window read): the read's row there, 0xFFFF: no piece
   // derived at upload for plan_tiles: per 512-locus block g (qoff[c] / 4 + block in contig c),
   // the first read with pmax_end > the block's first locus and the first read starting at or
   // after it (a block index of the reads, so aligned tiles need no search over the contig)

@@ -371,14 +371,30 @@ __global__ void slice_bad(DevReads R, const ProjRec *__restrict__ prec, uint8_t 
     for (int32_t q = s >> 7; q <= (e - 1) >> 7; ++q) pbad[q0 + q] = 1;
 }
 
-// Rows of each slice (walk_slice_rows, one wave per slice); past kSliceRowsMax the slice is
-// pbad (and gets no rows).
-__global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, int32_t *__restrict__ srows,
-                                                 uint8_t *__restrict__ pbad) {
+// Each slice's read window (slice_window), thread per slice: its first read and its number of
+// reads (scanned into the offsets of their rows); entry n_slices: 0.
+__global__ void slice_windows(DevReads R, int64_t n_slices, int64_t *__restrict__ sra, int64_t *__restrict__ scnt) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > n_slices) return;
+  if (q == n_slices) {
+    sra[q] = 0;
+    scnt[q] = 0;
+    return;
+  }
+  const SliceWin W = slice_window(R, q);
+  sra[q] = W.ra;
+  scnt[q] = W.rz - W.ra;
+}
+
+// Rows of each slice and each of its reads' row (slice_assign_rows, one wave per slice); past
+// kSliceRowsMax the slice is pbad (and gets no rows).
+__global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, uint16_t *__restrict__ prow,
+                                                 int32_t *__restrict__ srows, uint8_t *__restrict__ pbad) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
-    const int32_t n = walk_slice_rows<false>(R, slot, [](bool, int64_t, int32_t, int32_t) {});
+    const SliceWin W = slice_stored(R, slot);
+    const int32_t n = slice_assign_rows(R, W, prow + R.soff[slot]);
     if ((threadIdx.x & 63) == 0) {
       srows[slot] = n < 0 ? 0 : n;
       if (n < 0) pbad[slot] = 1;
@@ -438,7 +454,7 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     const int64_t base = 16 * R.srow[slot];  // words
-    walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
+    slice_words(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](bool act, int64_t r, int32_t col, int32_t row) {
       if (act) {
         const uint2 w = proj_word(R, r, col);  // byte codes of loci 0-3, 4-7 -> nibbles
         *reinterpret_cast<uint32_t *>(proj + 4 * (base + 16 * (int64_t)row + (col & 15))) = w.x | (w.y << 4);
@@ -1723,9 +1739,9 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       HIP_TRY(hipGetLastError());
     }
   }
-  {  // projections: records, the slice-major pool (slices of whole 512-locus blocks up to each
-     // contig's largest read end), sparse entries
-    const int64_t n = d->d.n_reads;
+  {  // the projections' slices (whole 512-locus blocks up to each contig's largest read end) and
+     // the block index of the reads (plan_tiles' windows of aligned tiles); the projection
+     // itself is derived on first use (ensure_projection)
     const int nc = d->d.n_contigs;
     std::vector<int64_t> qoff((size_t)nc + 1, 0);
     {
@@ -1741,116 +1757,30 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
         qoff[(size_t)k + 1] = qoff[(size_t)k] + 4 * ((col1 + 63) >> 6);
       }
     }
-    const int64_t n_sl = qoff[(size_t)nc];
-    void *qo = nullptr, *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr,
-         *ne = nullptr, *eo = nullptr, *pe = nullptr, *pbd = nullptr;
+    void *qo = nullptr;
     HIP_TRY(hipMalloc(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
     d->owned.push_back(qo);
     HIP_TRY(hipMemcpyAsync(qo, qoff.data(), sizeof(int64_t) * ((size_t)nc + 1), hipMemcpyHostToDevice, c->stream));
     d->d.qoff = (const int64_t *)qo;
-    {  // the block index of the reads (plan_tiles' windows of aligned tiles)
-      const int64_t n_blk = qoff[(size_t)nc] / 4;
-      void *bi = nullptr;
-      HIP_TRY(hipMalloc(&bi, sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_blk, 1)));
-      d->owned.push_back(bi);
-      int64_t *brb = (int64_t *)bi, *brs = brb + std::max<int64_t>(n_blk, 1);
-      if (n_blk > 0) {
-        hipLaunchKernelGGL(block_index, dim3((unsigned)((n_blk + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                           n_blk, brb, brs);
-        HIP_TRY(hipGetLastError());
-      }
-      d->d.blk_rb = brb;
-      d->d.blk_rs = brs;
-    }
-    HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
-    d->owned.push_back(pr);
-    const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
-    HIP_TRY(hipGetLastError());
-    d->d.prec = (const ProjRec *)pr;
-    // sparse-entry offsets; slices a read the projection cannot take touches (pbad); each
-    // slice's rows and first row (scan)
-    HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
-    d->owned.push_back(pbd);
-    HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
-    if (n > 0) {
-      hipLaunchKernelGGL(slice_bad, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const ProjRec *)pr, (uint8_t *)pbd);
+    d->n_slices = qoff[(size_t)nc];
+    const int64_t n_blk = qoff[(size_t)nc] / 4;
+    void *bi = nullptr;
+    HIP_TRY(hipMalloc(&bi, sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_blk, 1)));
+    d->owned.push_back(bi);
+    int64_t *brb = (int64_t *)bi, *brs = brb + std::max<int64_t>(n_blk, 1);
+    if (n_blk > 0) {
+      hipLaunchKernelGGL(block_index, dim3((unsigned)((n_blk + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         n_blk, brb, brs);
       HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipMalloc(&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
-    HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
-    d->owned.push_back(sb);
-    if (n_sl > 0) {
-      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-      hipLaunchKernelGGL(row_count, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (int32_t *)sc,
-                         (uint8_t *)pbd);
-      HIP_TRY(hipGetLastError());
-    }
-    hipLaunchKernelGGL(rows64, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_sl,
-                       (const int32_t *)sc, (int64_t *)br);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
-    HIP_TRY(hipMalloc(&eo, sizeof(int64_t) * (size_t)(n + 1)));
-    d->owned.push_back(eo);
-    hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)nnb, (int64_t *)ne);
-    HIP_TRY(hipGetLastError());
-    size_t tb = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
-    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
-    int64_t tot[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(tmp);
-    (void)hipFree(sc);
-    (void)hipFree(br);
-    (void)hipFree(ne);
-    d->d.srow = (const int64_t *)sb;
-    d->d.pbad = (const uint8_t *)pbd;
-    d->n_rows = tot[0];
-    // the pool: rows of 16 words, zero where no piece lies
-    const size_t pool_bytes = (size_t)kProjRowBytes * (size_t)tot[0] + 16;
-    HIP_TRY(hipMalloc(&pj, pool_bytes));
-    d->owned.push_back(pj);
-    HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
-    HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
-    d->owned.push_back(pe);
-    if (n_sl > 0) {
-      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-      hipLaunchKernelGGL(proj_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
-      HIP_TRY(hipGetLastError());
-    }
-    if (n > 0) {
-      hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const int64_t *)eo, (uint2 *)pe);
-      HIP_TRY(hipGetLastError());
-    }
-    d->d.proj = (const uint8_t *)pj;
-    d->d.pev = (const uint2 *)pe;
-    d->d.pev_off = (const int64_t *)eo;
-    d->proj_bytes = kProjRowBytes * tot[0];
-    d->n_slices = n_sl;
-    d->pev_count = tot[1];
-    if (n > 0) {  // reads the projection takes
-      unsigned long long *nok = nullptr, hk[kSpread];
-      HIP_TRY(hipMalloc(&nok, sizeof(hk)));
-      HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
-      hipLaunchKernelGGL(proj_count_ok, dim3(1024), dim3(kBlock), 0, c->stream, d->d, (const ProjRec *)pr, nok);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      (void)hipFree(nok);
-      d->proj_reads = 0;
-      for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
-    }
+    d->d.blk_rb = brb;
+    d->d.blk_rs = brs;
   }
+  d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
+  d->owned.push_back(nnb);
+  nnb = nullptr;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(nnb);
+  if (nnb) (void)hipFree(nnb);
   d->d.pool_ordered = unordered ? 0 : 1;
   return GQ_OK;
 }
@@ -2238,7 +2168,9 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true);
+  gq_status st = ensure_projection(c, rd);  // (derived on first use)
+  if (st) return st;
+  st = plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true);
   if (st) return st;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   gq_calls *res = (gq_calls *)calloc(1, sizeof(gq_calls));
@@ -2747,3 +2679,132 @@ void gq_free_counts(gq_counts *r) {
 }  // extern "C"
 
 gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return derive_shape_impl(c, d, md_len); }
+
+// The projection of a resident read set (ProjRec in gq_kernels.h), derived on first use by a
+// kernel that reads it (germline_proj, somatic_proj over the tumor, mproj_fill): records, pbad
+// slices, each slice's read window and its pieces' rows (one greedy pass, stored), the rows'
+// offsets, the 4-bit code pool, the sparse entries.  A set no such kernel reads (the somatic
+// normal) never pays for it.
+gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
+  gq_dev_reads *d = const_cast<gq_dev_reads *>(cd);
+  if (d->projected) return GQ_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t n = d->d.n_reads;
+  const int64_t n_sl = d->n_slices;
+  void *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
+       *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
+  HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
+  d->owned.push_back(pr);
+  const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
+  HIP_TRY(hipGetLastError());
+  d->d.prec = (const ProjRec *)pr;
+  // slices a read the projection cannot take touches (pbad)
+  HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
+  d->owned.push_back(pbd);
+  HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
+  if (n > 0) {
+    hipLaunchKernelGGL(slice_bad, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                       (const ProjRec *)pr, (uint8_t *)pbd);
+    HIP_TRY(hipGetLastError());
+  }
+  // each slice's read window and the offsets of its reads' rows
+  HIP_TRY(hipMalloc(&sra, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  d->owned.push_back(sra);
+  HIP_TRY(hipMalloc(&scn, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  HIP_TRY(hipMalloc(&so, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  d->owned.push_back(so);
+  hipLaunchKernelGGL(slice_windows, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                     d->d, n_sl, (int64_t *)sra, (int64_t *)scn);
+  HIP_TRY(hipGetLastError());
+  {
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)scn, (int64_t *)so, (int)(n_sl + 1), c->stream));
+    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)scn, (int64_t *)so, (int)(n_sl + 1), c->stream));
+    int64_t tot = 0;
+    HIP_TRY(hipMemcpyAsync(&tot, (int64_t *)so + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(tmp);
+    (void)hipFree(scn);
+    HIP_TRY(hipMalloc(&pw, sizeof(uint16_t) * (size_t)std::max<int64_t>(tot, 1)));
+    d->owned.push_back(pw);
+  }
+  d->d.sra = (const int64_t *)sra;
+  d->d.soff = (const int64_t *)so;
+  d->d.prow = (const uint16_t *)pw;
+  HIP_TRY(hipMalloc(&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
+  HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  d->owned.push_back(sb);
+  if (n_sl > 0) {
+    const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+    hipLaunchKernelGGL(row_count, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint16_t *)pw,
+                       (int32_t *)sc, (uint8_t *)pbd);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(rows64, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_sl,
+                     (const int32_t *)sc, (int64_t *)br);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
+  HIP_TRY(hipMalloc(&eo, sizeof(int64_t) * (size_t)(n + 1)));
+  d->owned.push_back(eo);
+  hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (int64_t *)ne);
+  HIP_TRY(hipGetLastError());
+  size_t tb = 0, tb2 = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+  HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+  int64_t tot[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(tmp);
+  (void)hipFree(sc);
+  (void)hipFree(br);
+  (void)hipFree(ne);
+  d->d.srow = (const int64_t *)sb;
+  d->d.pbad = (const uint8_t *)pbd;
+  d->n_rows = tot[0];
+  // the pool: rows of 16 words, zero where no piece lies
+  const size_t pool_bytes = (size_t)kProjRowBytes * (size_t)tot[0] + 16;
+  HIP_TRY(hipMalloc(&pj, pool_bytes));
+  d->owned.push_back(pj);
+  HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
+  HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
+  d->owned.push_back(pe);
+  if (n_sl > 0) {
+    const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+    hipLaunchKernelGGL(proj_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
+    HIP_TRY(hipGetLastError());
+  }
+  if (n > 0) {
+    hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                       (const int64_t *)eo, (uint2 *)pe);
+    HIP_TRY(hipGetLastError());
+  }
+  d->d.proj = (const uint8_t *)pj;
+  d->d.pev = (const uint2 *)pe;
+  d->d.pev_off = (const int64_t *)eo;
+  d->proj_bytes = kProjRowBytes * tot[0];
+  d->pev_count = tot[1];
+  if (n > 0) {  // reads the projection takes
+    unsigned long long *nok = nullptr, hk[kSpread];
+    HIP_TRY(hipMalloc(&nok, sizeof(hk)));
+    HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
+    hipLaunchKernelGGL(proj_count_ok, dim3(1024), dim3(kBlock), 0, c->stream, d->d, (const ProjRec *)pr, nok);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(nok);
+    d->proj_reads = 0;
+    for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  d->projected = true;
+  d->proj_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return GQ_OK;
+}
+

@@ -1442,7 +1442,9 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   // one loci plan per sample, 512-locus tiles aligned to 512-locus blocks (somatic_proj)
   Plan pt, pn;
-  gq_status st = plan(c, t, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
+  gq_status st = ensure_projection(c, t);  // (derived on first use)
+  if (st) return st;
+  st = plan(c, t, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;
   st = plan(c, n, loci, SomProjCfg::kT, pn, c->tiles2, 0, 0, 0, true);
   if (st) return st;
@@ -1831,7 +1833,9 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
   c->timings = gq_timings{};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pt;
-  gq_status st = plan(c, rd, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
+  gq_status st = ensure_projection(c, rd);  // (derived on first use)
+  if (st) return st;
+  st = plan(c, rd, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;
   gq_somatic_calls *res = (gq_somatic_calls *)calloc(1, sizeof(gq_somatic_calls));
   if (!res) return set_err(GQ_E_NOMEM, "calloc");

@@ -97,7 +97,7 @@ __device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_
 
 // The margin projection of the tumor reads, laid out as `proj` (an int16 per projection byte:
 // word w of the row pool at mproj + 8 w, 16 bytes), one wave per slice (the same rows:
-// walk_slice_rows packs a slice's pieces the same way every time).
+// the rows row_count assigned, stored).
 __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq, int incl_align,
                                                   int16_t *__restrict__ mproj, uint8_t *__restrict__ mnb) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     if (R.pbad[slot]) continue;  // uniform
     const int64_t base = 16 * R.srow[slot];  // words
     bool none = false;
-    walk_slice_rows<true>(R, slot, [&](bool act, int64_t r, int32_t col, int32_t row) {
+    slice_words(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](bool act, int64_t r, int32_t col, int32_t row) {
       if (act) {
         const uint4 w = margin_word(R, r, col, min_mapq, incl_align != 0);
         *reinterpret_cast<uint4 *>(mproj + 8 * (base + 16 * (int64_t)row + (col & 15))) = w;
