@@ -489,9 +489,9 @@ struct gq_dev_reads {
   bool projected = false;          // the projection is derived (ensure_projection)
   void *nnb = nullptr;             // N bases per read (pool_clean), for the projection's sparse entries
   float proj_ms = 0;               // ensure_projection's wall time
-  mutable void *mproj = nullptr;  // somatic margin projection (int16 per projection byte), for mproj_mapq
+  mutable void *mproj = nullptr;  // somatic margin projection (a biased byte per locus-read), for mproj_mapq
   mutable int mproj_mapq = -1;
-  mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMarginNone (no bound)
+  mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMargin8None (no bound)
 };
 
 namespace gq {

@@ -1149,19 +1149,26 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   if (t->mproj && t->mproj_mapq == key) return GQ_OK;
   if (!t->mproj) {
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, (size_t)(256 * t->n_rows + 32)));  // 16 int16 terms per 4-byte word of codes
+    HIP_TRY(hipMalloc(&p, (size_t)(128 * t->n_rows + 32)));  // a byte per locus: 8 per 4-byte word of codes
     t->mproj = p;
-    HIP_TRY(hipMemsetAsync(p, 0, (size_t)(256 * t->n_rows + 32), c->stream));  // the words no piece covers
     void *q = nullptr;
     HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
     t->mnb = q;
     HIP_TRY(hipMemsetAsync(q, 0, (size_t)t->n_slices + 16, c->stream));
   }
+  // the words no piece covers: biased zero terms (a rebuild for another filter rewrites only pieces)
+  HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
+  void *tab = nullptr;  // margin_term8 by (mapq, quality, match)
+  HIP_TRY(hipMalloc(&tab, 256 * 256));
+  hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, incl_align ? 1 : 0, (uint8_t *)tab);
+  HIP_TRY(hipGetLastError());
   if (t->n_slices > 0)
     hipLaunchKernelGGL(mproj_fill, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
-                       c->stream, t->d, t->n_slices, min_mapq, incl_align ? 1 : 0, (int16_t *)t->mproj,
+                       c->stream, t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,
                        (uint8_t *)t->mnb);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(tab);
   t->mproj_mapq = key;
   return GQ_OK;
 }
@@ -1511,12 +1518,12 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     if (rv.b)
       hipLaunchKernelGGL(somatic_proj<true>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
-                         (const int16_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (const uint8_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
                          (int32_t *)c->slow.p, rv);
     else
       hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
-                         (const int16_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
+                         (const uint8_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
                          (int32_t *)c->slow.p, rv);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((somatic_tile<SomProjCfg::kT>), dim3((unsigned)std::min<int64_t>(pt.n_tiles, 2048)), dim3(kBlock), 0,
@@ -1892,7 +1899,7 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     hipLaunchKernelGGL(somatic_proj<false>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
-                       (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, pt.n_tiles, rd->d, (const int16_t *)rd->mproj, (const uint8_t *)rd->mnb,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles.p, pt.n_tiles, rd->d, (const uint8_t *)rd->mproj, (const uint8_t *)rd->mnb,
                        rd->d.start, rd->d.end, (ComplexItem *)c->cplx.p, og, ctr, (int32_t *)c->slow.p,
                        RefView{nullptr, nullptr}, no_bound);
     HIP_TRY(hipGetLastError());

@@ -17,37 +17,50 @@
 
 #include "gq_kernels.h"
 
-// The margin term of one tumor element (hom_ref_margin_lane's t, in units of 1/256, rounded
-// down; kMarginNone when it is below -8191/256 or -inf), so that a sum of terms never exceeds
-// the margin it stands for: a sum that passes the bound proves what the FP32 sum proved.
-// Four terms >= -8191 sum exactly in 16 bits (somatic_proj folds every four rows into 32
-// bits); a slice holding kMarginNone gets no bound at all (mnb).
-constexpr int16_t kMarginNone = -8192;
-__device__ __forceinline__ int16_t margin_term(bool match, int q, float em, float lsm) {
+// The margin term of one tumor element (hom_ref_margin_lane's t) in units of 1/8, rounded down
+// with room for the FP32 rounding of t, so that a sum of terms never exceeds the margin it stands
+// for: a sum that passes the bound proves what the FP32 sum proved.  Stored biased in a byte:
+// 128 + term for terms in [-127, 127] (128: no element), kMargin8None (0) below -127/8 or for a
+// quality outside the table — a slice holding one gets no bound at all (mnb).  A byte per element
+// (half the int16 terms of round 3) halves somatic_proj's margin traffic; the coarser floor only
+// sends a few more loci to the exact caller, whose decisions are the reference's.
+constexpr uint8_t kMargin8None = 0, kMargin8Zero = 128;
+__device__ __forceinline__ uint8_t margin_term8(bool match, int q, float em, float lsm) {
   constexpr float kLn2 = 0.69314718f;
-  if (q < 0) return kMarginNone;  // outside the quality table: no bound
+  if (q < 0) return kMargin8None;  // outside the quality table: no bound
   const float eb = exp2f(-0.33219281f * (float)q);
   const float lsq = log1pf(-eb);
   const float f = eb + em - eb * em;  // 1 - pc
   const float t = match ? kLn2 + lsq + lsm - fmaxf(0.0f, kLn2 + __logf(f)) : __logf(f);
-  const float v = floorf(t * 256.0f) - 1.0f;  // -1: room for the FP32 rounding of t
-  if (!(v >= -8191.0f)) return kMarginNone;
-  return (int16_t)(v > 8191.0f ? 8191.0f : v);
+  const float v = floorf(t * 8.0f - 0.015625f);  // -1/64: room for the FP32 rounding of t
+  if (!(v >= -127.0f)) return kMargin8None;
+  return (uint8_t)(128 + (int)(v > 127.0f ? 127.0f : v));
 }
 
-// The margin word of tumor read r at column col (8 loci, int16 each; hom_ref_margin_lane's
+// margin_term8 for every (mapq, quality 0-127, match) of one probability model: byte
+// (mq << 8 | q << 1 | match), so the fill looks terms up instead of evaluating exp / log per
+// element (the same function, so the same bytes).
+__global__ void margin_table(int incl_align, uint8_t *__restrict__ tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 256 * 256) return;
+  const int mq = i >> 8, q = (i >> 1) & 127, match = i & 1;
+  // probabilityCorrectIncludingAlignment (somatic tumor) or IgnoringAlignment (germline-standard)
+  const float em = incl_align ? exp2f(-0.33219281f * (float)mq) : 0.0f;
+  const float lsm = log1pf(-em);
+  tab[i] = margin_term8(match != 0, q, em, lsm);
+}
+
+// The margin word of tumor read r at column col (8 loci, a byte each; hom_ref_margin_lane's
 // terms).  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
-// 25-36) and non-Match/Mismatch loci hold 0.
-__device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq, bool incl_align) {
+// 25-36) and non-Match/Mismatch loci hold kMargin8Zero.
+__device__ uint2 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq, const uint8_t *__restrict__ tab) {
   const ColDesc d = R.cdesc[r];
   const int32_t s = d.start;
   const int32_t lb = 8 * col;
-  int16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t v[2] = {0x80808080u, 0x80808080u};
   const int mq = (int)R.mapq[r];
   if (!(min_mapq > 0 && mq < min_mapq)) {
-    // probabilityCorrectIncludingAlignment (somatic tumor) or IgnoringAlignment (germline-standard)
-    const float em = incl_align ? exp2f(-0.33219281f * (float)mq) : 0.0f;
-    const float lsm = log1pf(-em);
+    const uint8_t *tm = tab + (mq << 8);
     const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
     const uint32_t *ev = R.md_ev + R.md_off[r];
     // MD events at offsets >= lb - s (sorted)
@@ -62,10 +75,12 @@ __device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_
       while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
       const bool event = k < nmd && (int32_t)(ev[k] >> 8) == off;
       const int q = (int)(int8_t)R.qual[p];
-      v[q8] = margin_term(!event, q, em, lsm);
+      const uint32_t t = q < 0 ? kMargin8None : tm[(q << 1) | (event ? 0 : 1)];
+      v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
     };
     if (d.info & kColEligible) {
       const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+#pragma unroll
       for (int q8 = 0; q8 < 8; ++q8) {
         const int32_t l = lb + q8;
         if (l >= s && l < d.end) term_at(q8, l, p0 + l);
@@ -87,19 +102,15 @@ __device__ uint4 margin_word(const DevReads &R, int64_t r, int32_t col, int min_
       }
     }
   }
-  uint4 o;
-  o.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
-  o.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
-  o.z = (uint32_t)(uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16);
-  o.w = (uint32_t)(uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16);
-  return o;
+  return make_uint2(v[0], v[1]);
 }
 
-// The margin projection of the tumor reads, laid out as `proj` (an int16 per projection byte:
-// word w of the row pool at mproj + 8 w, 16 bytes), one wave per slice (the same rows:
-// the rows row_count assigned, stored).
-__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq, int incl_align,
-                                                  int16_t *__restrict__ mproj, uint8_t *__restrict__ mnb) {
+// The margin projection of the tumor reads, laid out as `proj` (a byte per projection nibble:
+// word w of the row pool at mproj + 8 w), one wave per slice (the rows row_count assigned,
+// stored); mnb marks slices holding a kMargin8None term.
+__global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
+                                                  const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
+                                                  uint8_t *__restrict__ mnb) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
@@ -108,12 +119,12 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     bool none = false;
     slice_words(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](bool act, int64_t r, int32_t col, int32_t row) {
       if (act) {
-        const uint4 w = margin_word(R, r, col, min_mapq, incl_align != 0);
-        *reinterpret_cast<uint4 *>(mproj + 8 * (base + 16 * (int64_t)row + (col & 15))) = w;
-        auto has = [](uint32_t x) {
-          return (int16_t)(x & 0xFFFFu) == kMarginNone || (int16_t)(x >> 16) == kMarginNone;
+        const uint2 w = margin_word(R, r, col, min_mapq, tab);
+        *reinterpret_cast<uint2 *>(mproj + 8 * (base + 16 * (int64_t)row + (col & 15))) = w;
+        auto has = [](uint32_t x) {  // a zero byte
+          return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
         };
-        none = none || has(w.x) || has(w.y) || has(w.z) || has(w.w);
+        none = none || has(w.x) || has(w.y);
       }
     });
     const bool any = __ballot(none) != 0;
@@ -164,7 +175,7 @@ __device__ __forceinline__ bool ref_agrees(uint32_t md_mask, uint32_t base) {
 template <bool kRef>
 __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void somatic_proj(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, int64_t n_tiles, DevReads RT,
-    const int16_t *__restrict__ mproj, const uint8_t *__restrict__ mnb, const int32_t *__restrict__ n_start,
+    const uint8_t *__restrict__ mproj, const uint8_t *__restrict__ mnb, const int32_t *__restrict__ n_start,
     const int32_t *__restrict__ n_end,
     ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref,
     int no_bound = 0) {
@@ -235,17 +246,19 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       continue;
     }
     // ---- tumor column counts (bytes, widened into 16-bit pairs every 240 rows and at the end)
-    //      and margin sums (exact 16-bit pairs over one batch of four rows, loci 2k, 2k + 1 in
-    //      msum[k], folded into 32 bits per locus after each batch): row k of each group's slice
-    //      is one 64-byte load of base codes and one 256-byte load of margin terms (past the
-    //      slice's rows: out-of-range offsets, 0)
+    //      and margin sums (the biased byte terms zero-extended into 16-bit pairs, loci 2k,
+    //      2k + 1 in msum[k]: 240 rows of bytes fit, folded into 32 bits per locus with the
+    //      counts): row k of each group's slice is one 64-byte load of base codes and one
+    //      128-byte load of margin terms (past the slice's rows: out-of-range offsets, 0 — the
+    //      bias is taken off for the group's own rows only)
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0};
     int32_t m32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t msum[4] = {0, 0, 0, 0};
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(RT.proj + kProjRowBytes * row0), (short)0, kProjRowBytes * ntot, 0x00020000);
     const __amdgpu_buffer_rsrc_t msrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 128 * row0), (short)0, 256 * ntot, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(mproj + 128 * row0), (short)0, 128 * ntot, 0x00020000);
     const uint32_t vl = 4u * (uint32_t)(lane & 15) + (uint32_t)kProjRowBytes * (uint32_t)gbase;
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
     int nn = 0;
@@ -273,22 +286,27 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       w2(wC, cc);
       w2(wT, ct);
       w2(wG, cg);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // margin pairs into 32 bits per locus
+        m32[2 * q] += (int32_t)(msum[q] & 0xFFFFu);
+        m32[2 * q + 1] += (int32_t)(msum[q] >> 16);
+        msum[q] = 0;
+      }
     };
-    auto issue = [&](int k0, uint32_t (&w)[U], uint4 (&m)[U]) {  // rows k0 .. k0 + U - 1
+    auto issue = [&](int k0, uint32_t (&w)[U], uint2 (&m)[U]) {  // rows k0 .. k0 + U - 1
       const uint32_t va = vl + (uint32_t)kProjRowBytes * (uint32_t)k0;
       const int32_t rem = gn - k0;  // this group's rows left
-      const uint32_t vm = 4u * va;  // 16 bytes of margin terms per 4-byte word of codes
+      const uint32_t vm = 2u * va;  // 8 bytes of margin terms per 4-byte word of codes
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // past the slice's rows: out-of-range lane offsets
         const bool ok = u < rem;
         w[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(ok ? va : 0x80000000u), kProjRowBytes * u, 0);
-        const auto b = __builtin_amdgcn_raw_buffer_load_b128(msrc, (int)(ok ? vm : 0x80000000u), 256 * u, 0);
-        m[u] = make_uint4(b[0], b[1], b[2], b[3]);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b64(msrc, (int)(ok ? vm : 0x80000000u), 128 * u, 0);
+        m[u] = make_uint2(b[0], b[1]);
       }
     };
-    auto count = [&](const uint32_t (&w)[U], const uint4 (&m)[U]) {
+    auto count = [&](const uint32_t (&w)[U], const uint2 (&m)[U]) {
       if (nn + U > 15) fold();
-      uint32_t msum[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t lo = w[u] & 0x0F0F0F0Fu, hi = (w[u] >> 4) & 0x0F0F0F0Fu;  // loci 0-3, 4-7
@@ -296,20 +314,15 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
         ntg[0] += __builtin_amdgcn_perm(0x10000001u, 0u, lo);
         nac[1] += __builtin_amdgcn_perm(0u, 0x10000100u, hi);
         ntg[1] += __builtin_amdgcn_perm(0x10000001u, 0u, hi);
-        msum[0] = add_sat2(msum[0], m[u].x);  // exact: four terms >= -8191
-        msum[1] = add_sat2(msum[1], m[u].y);
-        msum[2] = add_sat2(msum[2], m[u].z);
-        msum[3] = add_sat2(msum[3], m[u].w);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        m32[2 * q] += (int32_t)(int16_t)(msum[q] & 0xFFFFu);
-        m32[2 * q + 1] += (int32_t)msum[q] >> 16;
+        msum[0] += __builtin_amdgcn_perm(0u, m[u].x, 0x0c010c00u);  // loci 0, 1 (biased bytes -> halves)
+        msum[1] += __builtin_amdgcn_perm(0u, m[u].x, 0x0c030c02u);  // loci 2, 3
+        msum[2] += __builtin_amdgcn_perm(0u, m[u].y, 0x0c010c00u);
+        msum[3] += __builtin_amdgcn_perm(0u, m[u].y, 0x0c030c02u);
       }
       nn += U;
     };
     uint32_t aw[U], bw[U];
-    uint4 am[U], bm[U];
+    uint2 am[U], bm[U];
     issue(0, aw, am);
     // ---- tumor sparse entries, one lane per entry (germline_proj's encoding)
     auto apply = [&](uint2 p) {
@@ -360,6 +373,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
     }
     fold();
     widen();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m32[j] -= 128 * gn;  // the bias of the group's own rows
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // ---- decision: candidate loci (somatic_tile's test)
     uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane),
@@ -411,7 +426,7 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
       const bool nonmatch = !agree || (mask & (mask - 1u)) != 0 || ncx > 0 || depth > c_ref;
       const bool bound = !no_bound && !nb && agree && single && ncx == 0 && nN == 0 &&
-                         (float)m32[j] * (1.0f / 256.0f) > 0.02f + 2e-4f * (float)depth;
+                         (float)m32[j] * 0.125f > 0.02f + 2e-4f * (float)depth;
       const bool tcand = depth > 0 && nonmatch && !bound;
       visited += (in && (depth > 0 || dn_run > 0)) ? 1u : 0u;
       const bool q = in && tcand && dn_run > 0;
