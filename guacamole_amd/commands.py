@@ -98,7 +98,7 @@ def germline_threshold_reads(ctx: native.Context, rs: ReadSet, loci, threshold: 
 
 
 def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet, loci, _gather=None,
-                           reference=None, **params) -> Optional[List[dict]]:
+                           reference=None, _stats=None, **params) -> Optional[List[dict]]:
     """pileupFlatMapTwoRDDs(tumor, normal, partitions, skipEmpty=true, findPotentialVariantAtLocus,
     referenceGenome) + the driver's filters on the GPU.  Rows as the oracle's somatic_standard
     (contig by name).  reference: a reference.ReferenceGenome (--reference-fasta) or None.
@@ -112,6 +112,8 @@ def somatic_standard_reads(ctx: native.Context, tumor: ReadSet, normal: ReadSet,
     finally:
         if dref is not None:
             dref.free()
+    if _stats is not None:
+        _stats["visited_loci"] = int(calls.visited_loci)
     per_rank = [calls] if _gather is None else gather_somatic(calls, _gather)
     if per_rank is None:
         return None
@@ -375,6 +377,7 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
             normal = normal.subset(reads_overlapping(normal, *flat[:3]))
         else:  # each rank read its own part: the first tumor sample of the lowest rank that has one
             sample = next((n[0] for n in all_gather_objects(list(tumor.sample_names)) if n), "default")
+    stats: Dict[str, int] = {}
     rows = somatic_standard_reads(
         ctx, tumor, normal, flat, odds=args.odds, min_mapq=args.min_mapq,
         filter_multi_allelic=int(args.filter_multi_allelic), max_read_depth=args.max_tumor_read_depth,
@@ -384,10 +387,10 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         min_likelihood=args.min_likelihood, min_vaf=args.min_vaf,
         min_average_mapping_quality=args.min_average_mapping_quality,
         min_average_base_quality=args.min_average_base_quality, max_median_mismatches=args.max_median_mismatches,
-        apply_filters=1, _gather=gdev if world > 1 else None, reference=reference)
+        apply_filters=1, _gather=gdev if world > 1 else None, reference=reference, _stats=stats)
     clock.mark("call")
     report = dict(rank=rank, reads=[int(tumor.n), int(normal.n)], ingest="device" if isinstance(tumor, DeviceReadSet)
-                  else "host", device_ingest=[getattr(x, "timings", None) for x in (tumor, normal)])
+                  else "host", device_ingest=[getattr(x, "timings", None) for x in (tumor, normal)], **stats)
     if rows is None:
         clock.report(**report)
         return _finish_rank(0)

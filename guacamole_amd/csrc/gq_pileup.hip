@@ -2008,6 +2008,8 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->md_len = d->d.md_len;
   out->n_contigs = d->d.n_contigs;
   out->n_samples = d->d.n_samples;
+  out->proj_ms = d->proj_ms;
+  out->projected = d->projected ? 1 : 0;
   return GQ_OK;
 }
 

@@ -209,6 +209,8 @@ typedef struct gq_reads_info {
   float derive_ms;   /* gq_reads_upload / wrap: the upload-time derivation on the device    */
   int64_t cigar_len, md_len;  /* pool sizes (CIGAR ops, MD events) */
   int32_t n_contigs, n_samples;
+  float proj_ms;     /* the projection, derived on the first call that reads it (0: not yet) */
+  int32_t projected; /* 1 once it is: the proj_* / n_rows / pev_count sizes above are then set */
 } gq_reads_info;
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
