@@ -54,7 +54,9 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
   unsigned long long n_ord;        // germline loci whose Scala map order depends on element order
   unsigned long long n_deep;       // somatic candidates handed to the deep caller
+  unsigned long long n_gdeep[3];   // germline_complex loci handed to the wide table (first pass, order, heap-order runs)
   unsigned long long deep_max;     // deepest per-sample pileup among them and the listed loci
+  unsigned long long deep_nt;      // germline-standard: largest allele table among the loci handed to the deep caller
   unsigned long long n_out;        // germline records in the result image (calls_image)
   unsigned long long out_pool;     // their allele bytes (the image's pool length)
   // per-tile run counters, spread over kSpread addresses (summed on the host)

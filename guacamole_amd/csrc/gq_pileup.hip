@@ -655,11 +655,25 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 // germline_complex: exact per-element classification for queued loci (one wave per locus)
 // ------------------------------------------------------------------------------------------
 
+// The hand-off of loci from the fast germline_complex (64 NS = 128 table keys) to the wide one:
+// the fast launch appends the positions (in its item list) of loci whose table overflows to
+// `out` (at most cap, counted in *n_out: more means a retry with a larger list); the wide
+// launch over the same item list takes those positions from `sel`, *n_sel of them (read on the
+// device, so the pair runs without a host round trip).
+struct DeepList {
+  int64_t *out;
+  unsigned long long *n_out;
+  const int64_t *sel;
+  const unsigned long long *n_sel;
+  unsigned long long cap;
+};
+
 // four waves per SIMD (128 VGPRs; a few spills) beat three without spills: the kernel is latency-bound
 #ifndef GQ_CPLX_WPE
 #define GQ_CPLX_WPE 3  // waves per SIMD the register budget must allow (4: 120 B/lane of spills)
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_WPE))) void germline_complex(const Tile *__restrict__ tiles,
+template <int NS>  // allele-table slots: 64 NS distinct (sample, allele) keys per locus
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NS > 2 ? 1 : GQ_CPLX_WPE))) void germline_complex(const Tile *__restrict__ tiles,
                                                            const ComplexItem *__restrict__ items, DevReads R,
                                                            int threshold, int emit_ref, int emit_no_call,
                                                            CallRec *__restrict__ recs, OutGeom og,
@@ -668,7 +682,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
                                                            unsigned long long amb_cap,
                                                            const AmbItem *__restrict__ amb_in,
                                                            const uint8_t *__restrict__ amb_ref, int64_t n_amb_in,
-                                                           int dbg, SomWin sw) {
+                                                           int dbg, SomWin sw, DeepList dl) {
   // amb_in == nullptr: every queued item; a locus whose reads' MD-derived bases disagree
   // (Pileup.referenceBaseAtLocus then depends on the queue's heap order) is only listed in
   // amb_out.  amb_in != nullptr: the listed loci again, with their reference base resolved
@@ -686,7 +700,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // items beyond a partition's capacity were never written (the host retries with larger ones)
-  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
+  //
+  // Table capacity: the fast instantiation (NS = 2) hands a locus with more than 128 distinct
+  // (sample, allele) keys to the wide one (deep_out, whole: nothing of it is counted or written
+  // here), which runs over that list (sel: positions in this launch's item list) with 1024
+  // keys in registers; Pileup.scala:37-146 has no such limit, and 1024 distinct keys at one
+  // locus is past any real pileup's depth-bounded allele count.
+  const unsigned long long n_list = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
+  const unsigned long long n_items = dl.sel ? min(*dl.n_sel, dl.cap) : n_list;
   const int rpart = kPartsCols + (int)(gwave & (kPartsWalk - 1));  // this wave's record partition
   // the reads covering the locus, compacted (tile-relative indices): the two per-read passes
   // then run over ~depth lanes instead of every read of the tile (one latency chain, not three)
@@ -702,9 +723,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       tk = t;
     }
   };
-  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+  for (int64_t si = gwave; si < (int64_t)n_items; si += nwaves_total) {
     tick(-1);
     if (dbg & 32) clk[4] += 1;
+    const int64_t li = dl.sel ? dl.sel[si] : si;
     const int64_t it = amb_in ? amb_in[li].item : li;
     const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tl = tiles[item.tile];
@@ -795,12 +817,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     }
     tick(1);
     // ---- pass 2: classify elements, group alleles per (sample, allele) in registers
-    uint64_t tlo[kSlots], thi[kSlots];
-    uint32_t tcnt[kSlots];
-    int64_t tfirst[kSlots];  // first occurrence (element-order key) of each entry
-    AlleleDesc tdesc[kSlots];
+    uint64_t tlo[NS], thi[NS];
+    uint32_t tcnt[NS];
+    int64_t tfirst[NS];  // first occurrence (element-order key) of each entry
+    AlleleDesc tdesc[NS];
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < NS; ++s) {
       tlo[s] = thi[s] = 0;
       tcnt[s] = 0;
       tfirst[s] = INT64_MAX;
@@ -838,13 +860,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         // find the key in the table
         int found = -1;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s) {
+        for (int s = 0; s < NS; ++s) {
           const bool hit = (s * 64 + lane) < nt && tlo[s] == klo && thi[s] == khi;
           const unsigned long long hb = __ballot(hit);
           if (found < 0 && hb) found = s * 64 + (__ffsll((long long)hb) - 1);
         }
         if (found < 0) {
-          if (nt >= 64 * kSlots) {
+          if (nt >= 64 * NS) {
             overflow = true;
           } else {
             found = nt++;
@@ -860,7 +882,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
             ld.pad = (uint8_t)smp;  // sample in pad
             ld.pad = (uint8_t)__shfl((int)smp, leader, 64);
 #pragma unroll
-            for (int s = 0; s < kSlots; ++s)
+            for (int s = 0; s < NS; ++s)
               if (s == sl && lane == owner) {
                 tlo[s] = klo;
                 thi[s] = khi;
@@ -873,7 +895,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
           const int owner = found & 63, sl = found >> 6;
           const int64_t f = by_lane ? lane_u64(okey, leader) : wave_min_i64(match ? okey : INT64_MAX);
 #pragma unroll
-          for (int s = 0; s < kSlots; ++s)
+          for (int s = 0; s < NS; ++s)
             if (s == sl && lane == owner) {
               tcnt[s] += n;
               tfirst[s] = f < tfirst[s] ? f : tfirst[s];
@@ -916,7 +938,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
       }
     }
     if (overflow) {
-      raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_CAPACITY, pos);
+      if (NS <= 2 && dl.out) {  // the wide instantiation's, whole
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(dl.n_out, 1ull);
+          if (k < dl.cap) dl.out[k] = li;
+        }
+      } else {
+        raise_error(&ctr->err, (int64_t *)&ctr->err_pos, GQ_E_CAPACITY, pos);
+      }
       continue;
     }
     if ((item.flags & 1) && !amb_in) {  // queued from a wide tile: count the visit here
@@ -932,12 +961,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     //      counts map, each present sample's within bySample, and whether either depends on
     //      first occurrences (two keys in one mutable.HashMap bucket, up to four keys)
     const int ns_all = R.n_samples < 8 ? R.n_samples : 8;
-    uint64_t tkey[kSlots];
+    uint64_t tkey[NS];
     bool dep = false;
-    int tsm[kSlots];
-    bool tpass[kSlots];
+    int tsm[NS];
+    bool tpass[NS];
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < NS; ++s) {
       const bool live = s * 64 + lane < nt;
       tsm[s] = live ? (int)tdesc[s].pad : -1;
       const uint32_t tot = (uint32_t)__shfl((int)st_lane, tsm[s] < 0 ? 0 : tsm[s], 64);
@@ -947,7 +976,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
     // the map order only decides between passing entries of one sample with equal counts
     bool tie_any = false;
 #pragma unroll
-    for (int s2 = 0; s2 < kSlots; ++s2) {
+    for (int s2 = 0; s2 < NS; ++s2) {
       unsigned long long pb = __ballot(tpass[s2]);
       while (pb && !tie_any) {
         const int ow = __ffsll((long long)pb) - 1;
@@ -956,22 +985,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         const int cj = __builtin_amdgcn_readlane((int)tcnt[s2], ow);
         bool hit = false;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NS; ++s)
           hit |= tpass[s] && tsm[s] == smj && (int)tcnt[s] == cj && !(s == s2 && lane == ow);
         tie_any = __ballot(hit) != 0;
       }
     }
     if (tie_any) {
-      uint32_t tb[kSlots];
+      uint32_t tb[NS];
 #pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
+      for (int s = 0; s < NS; ++s) {
         const uint32_t h = tsm[s] >= 0 ? allele_scala_hash(R, tdesc[s], pos) : 0u;
         tb[s] = scala::mutable_bucket(h, 4);
         tkey[s] = scala::trie_key(h);  // five or more alleles in the sample: HashTrieMap order
       }
       // entries of the same sample, and same-bucket ties among passing ones
 #pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
+      for (int s = 0; s < NS; ++s) {
         int n_same = 0;
         bool pair = false;
         for (int k = 0; k < nt; ++k) {
@@ -980,7 +1009,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
           uint32_t kb = 0, kc = 0;
           bool kp = false;
 #pragma unroll
-          for (int t = 0; t < kSlots; ++t)
+          for (int t = 0; t < NS; ++t)
             if (t == sl) {
               ksm = __shfl(tsm[t], ow, 64);
               kb = (uint32_t)__shfl((int)tb[t], ow, 64);
@@ -1057,7 +1086,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CPLX_
         uint64_t kj = 0;
         AlleleDesc dj;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NS; ++s)
           if (s == sl) {
             kj = lane_u64(tkey[s], owner);
             cj = (uint32_t)__shfl((int)tcnt[s], owner, 64);
@@ -2193,6 +2222,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   og.capB[0] = dense ? 2ull * ns * (unsigned long long)pl.n_loci / 8192 + 256 : (unsigned long long)pl.n_loci / 16384 + 256;
   og.capB[1] = (unsigned long long)pl.n_loci / 16384 + 256;
   unsigned long long pool_cap = 1 << 22, amb_cap = 4096;
+  unsigned long long gdeep_cap = 1024;  // loci per wide-table hand-off list (grown on overflow)
   Counters hc{};
   // output order: buckets of 2^bshift ordinals (one locus when every locus emits)
   const int bshift = dense ? 0 : 9;
@@ -2274,11 +2304,32 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       return st;
     }
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 1, og);
-    hipLaunchKernelGGL(germline_complex, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                       (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                       (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap,
-                       (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, gq_dbg(), wb);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(c->deep_list.ensure(3 * sizeof(int64_t) * (size_t)gdeep_cap));
+    auto complex_pair = [&](int blocks, int which, AmbItem *amb_out, unsigned long long acap, const AmbItem *amb_in,
+                            const uint8_t *amb_ref, int64_t n_amb_in, const SomWin &sw_) -> gq_status {
+      // the fast table, then the wide one over the loci it handed over (an empty list: the wide
+      // launch's waves read a zero count and leave)
+      int64_t *region = (int64_t *)c->deep_list.p + (size_t)which * gdeep_cap;
+      const DeepList fast{region, &ctr->n_gdeep[which], nullptr, nullptr, gdeep_cap};
+      const DeepList wide{nullptr, nullptr, region, &ctr->n_gdeep[which], gdeep_cap};
+      hipLaunchKernelGGL(germline_complex<2>, dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
+                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, amb_out, acap, amb_in, amb_ref,
+                         n_amb_in, gq_dbg(), sw_, fast);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(germline_complex<16>, dim3(64), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
+                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, amb_out, acap, amb_in, amb_ref,
+                         n_amb_in, gq_dbg(), sw_, wide);
+      HIP_TRY(hipGetLastError());
+      return GQ_OK;
+    };
+    st = complex_pair(cblocks, 0, (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr,
+                      (int64_t)0, wb);
+    if (st) {
+      free(res);
+      return st;
+    }
     hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     {  // variant candidates -> records; unused slots get a key behind every ordinal
 #ifndef GQ_EXPAND_BLOCKS
@@ -2317,6 +2368,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       amb_cap = std::max(hc.n_amb, hc.n_ord) + 1024;
       retry = true;
     }
+    if (hc.n_gdeep[0] > gdeep_cap) {
+      gdeep_cap = hc.n_gdeep[0] + 1024;
+      retry = true;
+    }
     // the windows' element order (initial groups in heap order) for the re-runs below: the
     // first occurrences the Scala map orders of those loci depend on
     SomWin sw{};
@@ -2331,12 +2386,12 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     if (rerun && hc.n_ord > 0) {
       // loci whose output order depends on first occurrences in element order
       const int oblocks = (int)std::min<int64_t>(((int64_t)hc.n_ord + 3) / 4, 4096);
-      hipLaunchKernelGGL(germline_complex, dim3(oblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
-                         (unsigned long long)0, (const AmbItem *)c->amb.p + amb_cap, (const uint8_t *)nullptr,
-                         (int64_t)hc.n_ord, gq_dbg(), sw);
-      HIP_TRY(hipGetLastError());
+      st = complex_pair(oblocks, 1, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p + amb_cap,
+                        (const uint8_t *)nullptr, (int64_t)hc.n_ord, sw);
+      if (st) {
+        free(res);
+        return st;
+      }
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     }
     if (rerun && hc.n_amb > 0) {
@@ -2352,12 +2407,12 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
         return st;
       }
       const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 4096);
-      hipLaunchKernelGGL(germline_complex, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         (const ComplexItem *)c->cplx.p, rd->d, p->threshold, p->emit_ref, p->emit_no_call,
-                         (CallRec *)c->recs.p, og, (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr,
-                         (unsigned long long)0, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p,
-                         (int64_t)amb.size(), gq_dbg(), sw);
-      HIP_TRY(hipGetLastError());
+      st = complex_pair(ablocks, 2, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
+                        (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), sw);
+      if (st) {
+        free(res);
+        return st;
+      }
       hipLaunchKernelGGL(part_scan, dim3(1), dim3(1024), 0, c->stream, ctr, 0, og);
     }
     if (rerun) {  // the re-runs added records: check their capacities, then the chain again
@@ -2374,6 +2429,10 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
       }
       if (hc.pool_used > pool_cap) {
         pool_cap = hc.pool_used + 4096;
+        retry = true;
+      }
+      if (std::max(hc.n_gdeep[1], hc.n_gdeep[2]) > gdeep_cap) {
+        gdeep_cap = std::max(hc.n_gdeep[1], hc.n_gdeep[2]) + 1024;
         retry = true;
       }
       if (!retry) {

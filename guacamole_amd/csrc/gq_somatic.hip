@@ -369,6 +369,7 @@ struct Cover {
   const int32_t *lst;
   int64_t rb, n;  // slots
   bool compact;
+  bool deep;  // the list cannot hold what the pileup order needs: the deep instantiation's locus
   int sel;  // sample filter (-1: every read)
   // read of slot k and whether it covers pos
   __device__ __forceinline__ int64_t read(const DevReads &R, int64_t k, int32_t pos, bool *act) const {
@@ -385,8 +386,9 @@ struct Cover {
     return r;
   }
 };
+// lst holds `cap` reads, tmp 2 th words (the initial group's reorder: at most th reads).
 __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64_t re, int32_t pos, int32_t *lst, uint32_t *tmp,
-                            const WinInit &w, const int64_t *__restrict__ init_reads,
+                            int cap, int th, const WinInit &w, const int64_t *__restrict__ init_reads,
                             const int32_t *__restrict__ init_rank, Counters *ctr, int sel = -1) {
   const int lane = threadIdx.x & 63;
   int64_t n = 0;
@@ -400,19 +402,20 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
     const bool c = r < rz && R.start[r] <= pos && pos < R.end[r] && (sel < 0 || (int)R.sample[r] == sel);
     const unsigned long long b = __ballot(c);
     const int64_t at = n + (int64_t)__popcll(b & ((1ull << lane) - 1ull));
-    if (c && at < kCover) lst[at] = (int32_t)(r - rb);
+    if (c && at < cap) lst[at] = (int32_t)(r - rb);
     n += (int64_t)__popcll(b);
   }
   __builtin_amdgcn_wave_barrier();
   Cover cv;
   cv.lst = lst;
   cv.rb = rb;
-  cv.compact = n <= kCover;
+  cv.compact = n <= cap;
   cv.n = cv.compact ? n : (re - rb);
   cv.sel = sel;
+  cv.deep = false;
   if (w.n > 0 && pos < w.E) {
-    if (!cv.compact) {
-      raise_at(ctr, GQ_E_CAPACITY, pos);
+    if (!cv.compact) {  // the initial group's heap order needs the list
+      cv.deep = true;
       return cv;
     }
     // the initial group's reads covering pos are a prefix of the list (they start at or
@@ -422,8 +425,8 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
       const int k = k0 + lane;
       p += (int)__popcll(__ballot(k < (int)n && R.start[rb + lst[k]] <= w.F));
     }
-    if (p > 512) {
-      raise_at(ctr, GQ_E_CAPACITY, pos);
+    if (p > th) {
+      cv.deep = true;
       return cv;
     }
     for (int k = lane; k < p; k += 64) {
@@ -441,11 +444,11 @@ __device__ __forceinline__ Cover make_cover(const DevReads &R, int64_t rb, int64
     for (int k = lane; k < p; k += 64) {
       int before = 0;
       for (int j = 0; j < p; ++j) before += tmp[j] < tmp[k] ? 1 : 0;
-      tmp[512 + before] = (uint32_t)lst[k];
+      tmp[th + before] = (uint32_t)lst[k];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k = lane; k < p; k += 64) lst[k] = (int32_t)tmp[512 + k];
+    for (int k = lane; k < p; k += 64) lst[k] = (int32_t)tmp[th + k];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
@@ -477,11 +480,12 @@ __device__ __forceinline__ void pileup_ref(const DevReads &R, const Cover &cv, i
 }
 
 // Per-sample pileup summary held by one wave: a distinct-allele table (slot s * 64 + lane
-// lives in lane `lane`, register slot s) with per-allele element counts.
+// lives in lane `lane`, register slot s) with per-allele element counts; 64 NS entries.
+template <int NS>
 struct SamplePile {
-  uint64_t klo[kSlots], khi[kSlots];
-  AlleleDesc desc[kSlots];
-  uint32_t n_all[kSlots], n_f[kSlots];
+  uint64_t klo[NS], khi[NS];
+  AlleleDesc desc[NS];
+  uint32_t n_all[NS], n_f[NS];
   int nt;             // used table entries (wave-uniform)
   uint32_t depth_all; // elements
   uint32_t depth_f;   // elements passing the mapping-quality filter
@@ -491,12 +495,13 @@ struct SamplePile {
 };
 
 // Build the allele table of one sample's pileup at pos (counts only: order-free).
+template <int NS>
 __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, int ref_override,
-                              Counters *ctr, SamplePile &P) {
+                              Counters *ctr, SamplePile<NS> &P) {
   const int lane = threadIdx.x & 63;
   pileup_ref(R, cv, pos, ctr, ref_override, P.refbase, P.ambiguous);
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < NS; ++s) {
     P.klo[s] = P.khi[s] = 0;
     P.n_all[s] = P.n_f[s] = 0;
   }
@@ -534,13 +539,13 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
       const uint32_t na = (uint32_t)__popcll(mb), nf = (uint32_t)__popcll(mb & passb);
       int found = -1;
 #pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
+      for (int s = 0; s < NS; ++s) {
         const bool hit = (s * 64 + lane) < P.nt && P.klo[s] == klo && P.khi[s] == khi;
         const unsigned long long hb = __ballot(hit);
         if (found < 0 && hb) found = s * 64 + (__ffsll((long long)hb) - 1);
       }
       if (found < 0) {
-        if (P.nt >= 64 * kSlots) {
+        if (P.nt >= 64 * NS) {
           P.overflow = true;
         } else {
           found = P.nt++;
@@ -554,7 +559,7 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
           ld.base = (uint8_t)__shfl((int)d.base, leader, 64);
           ld.pad = 0;
 #pragma unroll
-          for (int s = 0; s < kSlots; ++s)
+          for (int s = 0; s < NS; ++s)
             if (s == sl && lane == owner) {
               P.klo[s] = klo;
               P.khi[s] = khi;
@@ -565,7 +570,7 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
       if (found >= 0) {
         const int owner = found & 63, sl = found >> 6;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NS; ++s)
           if (s == sl && lane == owner) {
             P.n_all[s] += na;
             P.n_f[s] += nf;
@@ -576,10 +581,11 @@ __device__ __forceinline__ void gather_sample(const DevReads &R, const Cover &cv
   }
 }
 
-__device__ __forceinline__ AlleleDesc pile_desc(const SamplePile &P, int j) {
+template <int NS>
+__device__ __forceinline__ AlleleDesc pile_desc(const SamplePile<NS> &P, int j) {
   AlleleDesc d{};
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s)
+  for (int s = 0; s < NS; ++s)
     if (s == (j >> 6)) {
       const int o = j & 63;
       d.read = __shfl(P.desc[s].read, o, 64);
@@ -599,6 +605,7 @@ __device__ __forceinline__ AlleleDesc pile_desc(const SamplePile &P, int j) {
 struct GenoResult {
   int n;          // eligible alleles
   int G;          // genotypes
+  bool deep;      // more genotypes than ll holds: the deep instantiation's locus
   int best_g;     // maxBy (first maximum)
   double best_l;  // its normalised likelihood
   double var_sum; // sum of normalised likelihoods of genotypes with a variant allele
@@ -673,15 +680,16 @@ __device__ __forceinline__ double fold_genotypes(const DevReads &R, const Cover 
   return agg;
 }
 
-__device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SamplePile &P, const Cover &cv, int32_t pos,
+template <int NS>
+__device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SamplePile<NS> &P, const Cover &cv, int32_t pos,
                                 int min_mapq, bool include_alignment, int16_t *order, uint8_t *is_var,
-                                double *ll_lds, Counters *ctr, bool by_log = false) {
+                                double *ll_lds, int maxG, Counters *ctr, bool by_log = false) {
   const int lane = threadIdx.x & 63;
   GenoResult res{};
   // eligibility + variant flag per entry (entry j on lane j & 63, slot j >> 6)
-  bool elig[kSlots], var[kSlots];
+  bool elig[NS], var[NS];
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < NS; ++s) {
     const int j = s * 64 + lane;
     elig[s] = j < P.nt && P.n_f[s] > 0 && allele_std_alt(R, P.desc[s], pos);
     var[s] = j < P.nt && allele_is_variant(R, P.desc[s], pos);
@@ -689,27 +697,27 @@ __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SampleP
   // rank of each eligible entry among eligible entries by Allele order
   int n = 0;
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) n += __popcll(__ballot(elig[s]));
+  for (int s = 0; s < NS; ++s) n += __popcll(__ballot(elig[s]));
   res.n = n;
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
+  for (int s = 0; s < NS; ++s) {
     int rank = 0;
     for (int k = 0; k < P.nt; ++k) {
       const AlleleDesc dk = pile_desc(P, k);
       bool ek = false;
-      _Pragma("unroll") for (int t = 0; t < kSlots; ++t) if (t == (k >> 6)) ek = __shfl((int)elig[t], k & 63, 64);
+      _Pragma("unroll") for (int t = 0; t < NS; ++t) if (t == (k >> 6)) ek = __shfl((int)elig[t], k & 63, 64);
       if (elig[s] && ek && k != s * 64 + lane && allele_cmp(R, dk, P.desc[s], pos) < 0) ++rank;
     }
     if (elig[s]) order[rank] = (int16_t)(s * 64 + lane);
-    if (s * 64 + lane < 64 * kSlots) is_var[s * 64 + lane] = var[s] ? 1 : 0;
+    if (s * 64 + lane < 64 * NS) is_var[s * 64 + lane] = var[s] ? 1 : 0;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const int G = n * (n + 1) / 2;
   res.G = G;
   if (G == 0) return res;
-  if (G > kMaxG) {
-    raise_at(ctr, GQ_E_CAPACITY, pos);
+  if (G > maxG) {
+    res.deep = true;
     res.G = 0;
     return res;
   }
@@ -723,7 +731,7 @@ __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SampleP
     // the table keys live on their owner lanes (entry e: lane e & 63, slot e >> 6)
     Key128 k1{~0ull, ~0ull}, k2{~0ull, ~0ull};
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < NS; ++s) {
       const uint64_t lo1 = __shfl(P.klo[s], ei & 63, 64), hi1 = __shfl(P.khi[s], ei & 63, 64);
       const uint64_t lo2 = __shfl(P.klo[s], ej & 63, 64), hi2 = __shfl(P.khi[s], ej & 63, 64);
       if (g < G && s == (ei >> 6)) k1 = Key128{lo1, hi1};
@@ -783,8 +791,12 @@ __device__ __forceinline__ GenoResult genotypes(const DevReads &R, const SampleP
 // AlleleEvidence.apply (AlleleEvidence.scala:58-101) for the elements of one sample whose
 // allele key is `target`.  Supporting elements' (mapq, quality, mismatches) go to `ev_lds`
 // in element order for the running mean (Breeze, in element order) and the medians.
-__device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, const SamplePile &P,
-                                Key128 target, double likelihood, uint32_t *ev_lds, Counters *ctr, gq_evidence &ev) {
+// Returns false when more elements support the allele than ev_lds holds (evcap): the deep
+// instantiation's locus.
+template <int NS>
+__device__ __forceinline__ bool allele_evidence(const DevReads &R, const Cover &cv, int32_t pos, int min_mapq, const SamplePile<NS> &P,
+                                Key128 target, double likelihood, uint32_t *ev_lds, uint32_t evcap, Counters *ctr,
+                                gq_evidence &ev) {
   const int lane = threadIdx.x & 63;
   uint32_t n = 0, fwd = 0;
   for (int64_t k0 = 0; k0 < cv.n; k0 += 64) {
@@ -812,7 +824,7 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
     }
     const unsigned long long hb = __ballot(hit);
     const uint32_t before = (uint32_t)__popcll(hb & ((1ull << lane) - 1ull));
-    if (hit && n + before < (uint32_t)kEvCap) ev_lds[n + before] = packed;
+    if (hit && n + before < evcap) ev_lds[n + before] = packed;
     fwd += (uint32_t)__popcll(__ballot(hit && !(R.flags[r] & 1)));
     n += (uint32_t)__popcll(hb);
   }
@@ -824,13 +836,9 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
   ev.allele_forward_depth = (int32_t)fwd;
   if (n == 0) {
     ev.mean_mq = ev.median_mq = ev.mean_bq = ev.median_bq = ev.median_mismatches = __builtin_nan("");
-    return;
+    return true;
   }
-  if (n > (uint32_t)kEvCap) {
-    raise_at(ctr, GQ_E_CAPACITY, pos);
-    ev.mean_mq = ev.median_mq = ev.mean_bq = ev.median_bq = ev.median_mismatches = __builtin_nan("");
-    return;
-  }
+  if (n > evcap) return false;
   // breeze.stats.mean: running mean in element order
   double mq = 0.0, bq = 0.0;
   for (uint32_t k = 0; k < n; ++k) {
@@ -868,6 +876,7 @@ __device__ __forceinline__ void allele_evidence(const DevReads &R, const Cover &
     ev.median_bq = ((double)kth(1, n / 2 - 1) + (double)kth(1, n / 2)) / 2.0;
     ev.median_mismatches = (double)((kth(2, n / 2 - 1) + kth(2, n / 2)) / 2);  // Int median (parity unpinned)
   }
+  return true;
 }
 
 constexpr int kSomWaves = kBlock / 64;
@@ -886,29 +895,104 @@ constexpr int kSomWaves = kBlock / 64;
 // order) the QualityAlignedReadsFilter pileup's genotype likelihoods in log space, normalized,
 // the first maximum, and each non-reference allele of that genotype (twice for a hom-alt) with
 // its evidence over the sample's unfiltered pileup.  Records keep the sample in key bits 4-11.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_WPE))) void germline_standard_call(
+// Capacities of the LDS working set (fast instantiation): covering reads kCover, supporting
+// elements kEvCap, genotypes kMaxG, 128 distinct alleles per sample.  A locus past any of them is
+// handed whole (from the sample it reached on) to the deep instantiation: per-wave global scratch
+// sized from the deepest handed-over pileup and its largest allele table, 1024 alleles per
+// sample — the reference (Pileup.scala:37-146, Likelihood.scala:99-113, VariantSupport.scala:
+// 110-118) has no depth limit.
+struct DeepSel {
+  int64_t *out;              // fast: (list position << 3 | sample) of handed-over loci
+  unsigned long long cap;    // out's / sel's capacity
+  const int64_t *sel;        // deep: the handed-over entries
+  int64_t n_sel;
+  uint8_t *scratch;          // deep: one slice per wave (gs_wave_bytes)
+  int scap, maxG;            // deep: reads per slice list, genotypes
+};
+constexpr int kDeepNS = 16;  // deep allele tables: 64 x 16 = 1024 distinct alleles per sample
+__host__ __device__ __forceinline__ size_t gs_wave_bytes(int scap, int maxG) {
+  return (size_t)maxG * 8 + (size_t)scap * 4 * 4 + 64 * kDeepNS * 3 + 64;
+}
+struct GsMem {
+  int32_t *cov_a, *cov_s;
+  uint32_t *ev;  // 2 scap words: the heap-order reorder, then the evidence values
+  int16_t *order;
+  uint8_t *is_var;
+  double *ll;
+  int cap, th, maxG;
+};
+__device__ __forceinline__ GsMem gs_deep_mem(uint8_t *base, int scap, int maxG) {
+  GsMem m;
+  uint8_t *p = base;
+  m.ll = (double *)p;
+  p += (size_t)maxG * 8;
+  m.cov_a = (int32_t *)p;
+  p += (size_t)scap * 4;
+  m.cov_s = (int32_t *)p;
+  p += (size_t)scap * 4;
+  m.ev = (uint32_t *)p;
+  p += (size_t)scap * 8;
+  m.order = (int16_t *)p;
+  p += 64 * kDeepNS * 2;
+  m.is_var = p;
+  m.cap = scap;
+  m.th = scap;
+  m.maxG = maxG;
+  return m;
+}
+
+template <bool DEEP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 1 : GQ_CALL_WPE))) void germline_standard_call(
     const Tile *__restrict__ tiles, const ComplexItem *__restrict__ items, DevReads R, gq_germline_std_params prm,
     SomRec *__restrict__ recs, unsigned long long rec_cap, uint8_t *__restrict__ pool, unsigned long long pool_cap,
     OutGeom og, Counters *ctr, SomWin sw, AmbItem *__restrict__ amb_out, unsigned long long amb_cap,
-    const AmbItem *__restrict__ amb_in, const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
-  __shared__ int16_t order_lds[kSomWaves][64 * kSlots];
-  __shared__ uint8_t var_lds[kSomWaves][64 * kSlots];
-  __shared__ uint32_t ev_lds[kSomWaves][kEvCap];
-  __shared__ int32_t cover_a[kSomWaves][kCover], cover_s[kSomWaves][kCover];
-  __shared__ double ll_lds[kSomWaves][kMaxG];
+    const AmbItem *__restrict__ amb_in, const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, DeepSel dd) {
+  constexpr int NS = DEEP ? kDeepNS : kSlots;
+  constexpr int FW = DEEP ? 1 : kSomWaves;
+  __shared__ int16_t order_lds[FW][64 * kSlots];
+  __shared__ uint8_t var_lds[FW][64 * kSlots];
+  __shared__ uint32_t ev_lds[FW][kEvCap];
+  __shared__ int32_t cover_a[FW][kCover], cover_s[FW][kCover];
+  __shared__ double ll_lds[FW][kMaxG];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
-  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+  GsMem m;
+  if constexpr (DEEP) {
+    m = gs_deep_mem(dd.scratch + (size_t)gwave * gs_wave_bytes(dd.scap, dd.maxG), dd.scap, dd.maxG);
+  } else {
+    m = GsMem{cover_a[wv], cover_s[wv], ev_lds[wv], order_lds[wv], var_lds[wv], ll_lds[wv], kCover, 512, kMaxG};
+  }
+  const unsigned long long n_items =
+      DEEP ? (unsigned long long)dd.n_sel : amb_in ? (unsigned long long)n_amb_in : ctr->part_off[1][kParts];
+  for (int64_t si = gwave; si < (int64_t)n_items; si += nwaves_total) {
+    const int64_t li = DEEP ? (dd.sel[si] >> 3) : si;
+    const int smp0 = DEEP ? (int)(dd.sel[si] & 7) : 0;  // the first sample the fast pass did not finish
     const int64_t it = amb_in ? amb_in[li].item : li;
     const ComplexItem item = items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
     const Tile tt = tiles[item.tile];
     const int32_t pos = item.pos;
     const int32_t win = sw.range_win[tt.range];
+    // a locus (from sample smp on) the working set cannot hold: the deep instantiation's
+    auto hand_over = [&](int smp, uint32_t depth, int nt) {
+      if constexpr (!DEEP) {
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
+          if (k < dd.cap) dd.out[k] = (li << 3) | smp;
+          atomicMax(&ctr->deep_max, (unsigned long long)depth);
+          atomicMax(&ctr->deep_nt, (unsigned long long)nt);
+        }
+      } else {
+        raise_at(ctr, GQ_E_CAPACITY, pos);
+      }
+    };
     // the pileup's reference base (Pileup.referenceBaseAtLocus over every read)
-    const Cover ca = make_cover(R, tt.rb, tt.re, pos, cover_a[wv], ev_lds[wv], sw.wi[2 * win], sw.init_reads,
+    const Cover ca = make_cover(R, tt.rb, tt.re, pos, m.cov_a, m.ev, m.cap, m.th, sw.wi[2 * win], sw.init_reads,
                                 sw.init_rank, ctr);
+    if (ca.deep) {
+      hand_over(0, (uint32_t)(tt.re - tt.rb), 64 * NS);
+      continue;
+    }
     uint8_t refbase;
     bool ambiguous;
     pileup_ref(R, ca, pos, ctr, amb_in ? (int)amb_ref[li] : -1, refbase, ambiguous);
@@ -919,19 +1003,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_
       }
       continue;
     }
-    for (int smp = 0; smp < R.n_samples; ++smp) {
+    for (int smp = smp0; smp < R.n_samples; ++smp) {
       const Cover cs = R.n_samples == 1 ? ca
-                                        : make_cover(R, tt.rb, tt.re, pos, cover_s[wv], ev_lds[wv], sw.wi[2 * win],
+                                        : make_cover(R, tt.rb, tt.re, pos, m.cov_s, m.ev, m.cap, m.th, sw.wi[2 * win],
                                                      sw.init_reads, sw.init_rank, ctr, smp);
-      SamplePile PF;
+      if (cs.deep) {
+        hand_over(smp, (uint32_t)(tt.re - tt.rb), 64 * NS);
+        break;
+      }
+      SamplePile<NS> PF;
       gather_sample(R, cs, pos, prm.min_mapq, refbase, ctr, PF);
       if (PF.overflow) {
-        raise_at(ctr, GQ_E_CAPACITY, pos);
-        continue;
+        hand_over(smp, (uint32_t)cs.n, 64 * kDeepNS);
+        break;
       }
       if (PF.depth_f == 0) continue;  // no sample pileup, or nothing left after the mapq filter
       const GenoResult g =
-          genotypes(R, PF, cs, pos, prm.min_mapq, false, order_lds[wv], var_lds[wv], ll_lds[wv], ctr, true);
+          genotypes(R, PF, cs, pos, prm.min_mapq, false, m.order, m.is_var, m.ll, m.maxG, ctr, true);
+      if (g.deep) {
+        hand_over(smp, (uint32_t)cs.n, PF.nt);
+        break;
+      }
       if (g.G == 0) {
         raise_at(ctr, GQ_E_ASSERT, pos);  // empty.maxBy: no allele with standard bases
         continue;
@@ -939,14 +1031,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_CALL_
       const AlleleDesc a1 = pile_desc(PF, g.bi), a2 = pile_desc(PF, g.bj);
       const bool v1 = allele_is_variant(R, a1, pos), v2 = allele_is_variant(R, a2, pos);
       if (!v1 && !v2) continue;
-      SamplePile PA;  // the sample's unfiltered pileup: AlleleEvidence's
+      SamplePile<NS> PA;  // the sample's unfiltered pileup: AlleleEvidence's
       gather_sample(R, cs, pos, 0, refbase, ctr, PA);
+      // both alleles' evidence first: a sample is handed over whole or not at all
+      gq_evidence evs[2];
+      bool fits = true;
+      for (int sub = 0; sub < 2 && fits; ++sub)
+        if (sub == 0 ? v1 : v2)
+          fits = allele_evidence(R, cs, pos, 0, PA, allele_key(R, sub == 0 ? a1 : a2, pos, 0), g.best_l, m.ev,
+                                 (uint32_t)(DEEP ? 2 * m.cap : kEvCap), ctr, evs[sub]);
+      if (!fits || PA.overflow) {
+        hand_over(smp, (uint32_t)cs.n, PF.nt);
+        break;
+      }
       for (int sub = 0; sub < 2; ++sub) {
         if (!(sub == 0 ? v1 : v2)) continue;
         const AlleleDesc al = sub == 0 ? a1 : a2;
-        const Key128 key = allele_key(R, al, pos, 0);
-        gq_evidence ev;
-        allele_evidence(R, cs, pos, 0, PA, key, g.best_l, ev_lds[wv], ctr, ev);
+        const gq_evidence ev = evs[sub];
         const int gqv = success_to_phred(ev.likelihood - 1e-10);
         if (prm.apply_filters) {
           if (!(ev.read_depth >= prm.min_read_depth && ev.read_depth < prm.max_read_depth)) continue;
@@ -1044,20 +1145,23 @@ static_assert(sizeof(VsRec) == 40, "VsRec layout");
 // One wave per locus of the loci set: the covering reads' pileup (every element, no filter),
 // its distinct alleles and their element counts (gather_sample's table).  Loci whose reference
 // base depends on heap order are listed first (amb_out) and redone with the replayed base.
-__global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__restrict__ tiles, int64_t n_tiles,
-                                                               int64_t n_items, DevReads R, VsRec *__restrict__ recs,
-                                                               unsigned long long rec_cap, uint8_t *__restrict__ pool,
-                                                               unsigned long long pool_cap, Counters *ctr,
-                                                               AmbItem *__restrict__ amb_out, unsigned long long amb_cap,
-                                                               const AmbItem *__restrict__ amb_in,
-                                                               const uint8_t *__restrict__ amb_ref, int64_t n_amb_in) {
+// A locus with more distinct alleles than the fast table (128) goes whole to the deep
+// instantiation (1024 alleles; the cover list is only a shortcut: past it the reads are walked).
+template <bool DEEP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 1 : 2))) void variant_support_call(
+    const Tile *__restrict__ tiles, int64_t n_tiles, int64_t n_items, DevReads R, VsRec *__restrict__ recs,
+    unsigned long long rec_cap, uint8_t *__restrict__ pool, unsigned long long pool_cap, Counters *ctr,
+    AmbItem *__restrict__ amb_out, unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
+    const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, DeepSel dd) {
+  constexpr int NS = DEEP ? kDeepNS : kSlots;
   __shared__ int32_t cover[kSomWaves][kCover];
   __shared__ uint32_t tmp[kSomWaves][kEvCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t n = amb_in ? n_amb_in : n_items;
-  for (int64_t li = gwave; li < n; li += nwaves_total) {
+  const int64_t n = DEEP ? dd.n_sel : amb_in ? n_amb_in : n_items;
+  for (int64_t si = gwave; si < n; si += nwaves_total) {
+    const int64_t li = DEEP ? dd.sel[si] : si;
     const int64_t k = amb_in ? amb_in[li].item : li;
     int64_t t;
     if (amb_in) {
@@ -1076,12 +1180,19 @@ __global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__res
     if (k < tt.ordinal0 || pos64 >= tt.L1) continue;
     const int32_t pos = (int32_t)pos64;
     WinInit w0{};
-    const Cover cv = make_cover(R, tt.rb, tt.re, pos, cover[wv], tmp[wv], w0, nullptr, nullptr, ctr);
-    SamplePile P;
+    const Cover cv = make_cover(R, tt.rb, tt.re, pos, cover[wv], tmp[wv], kCover, 512, w0, nullptr, nullptr, ctr);
+    SamplePile<NS> P;
     gather_sample(R, cv, pos, 0, amb_in ? (int)amb_ref[li] : -1, ctr, P);
     if (P.depth_all == 0) continue;  // skipEmpty
     if (P.overflow) {
-      raise_at(ctr, GQ_E_CAPACITY, pos);
+      if constexpr (!DEEP) {
+        if (lane == 0) {
+          const unsigned long long q = atomicAdd(&ctr->n_deep, 1ull);
+          if (q < dd.cap) dd.out[q] = li;
+        }
+      } else {
+        raise_at(ctr, GQ_E_CAPACITY, pos);
+      }
       continue;
     }
     if (!amb_in && P.ambiguous) {
@@ -1109,7 +1220,7 @@ __global__ __launch_bounds__(kBlock) void variant_support_call(const Tile *__res
       const AlleleDesc d = pile_desc(P, j);
       uint32_t cnt = 0;
 #pragma unroll
-      for (int s2 = 0; s2 < kSlots; ++s2)
+      for (int s2 = 0; s2 < NS; ++s2)
         if (s2 == (j >> 6)) cnt = (uint32_t)__shfl((int)P.n_all[s2], j & 63, 64);
       const int rl = allele_ref_len(d), al = allele_alt_len(d);
       VsRec rr;
@@ -1701,7 +1812,7 @@ gq_status gq_variant_support(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *l
     return e;
   };
   unsigned long long rec_cap = (unsigned long long)std::max<int64_t>(pl.n_loci * 2, 1024), pool_cap = 1 << 16,
-                     amb_cap = 4096;
+                     amb_cap = 4096, deep_cap = 1024;
   Counters hc{};
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>((pl.n_loci + kSomWaves - 1) / kSomWaves, 1), 8192);
   for (int attempt = 0; pl.n_tiles > 0; ++attempt) {
@@ -1709,18 +1820,43 @@ gq_status gq_variant_support(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *l
     HIP_TRY(c->srecs.ensure(rec_cap * sizeof(VsRec)));
     HIP_TRY(c->pool.ensure(pool_cap));
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    HIP_TRY(c->deep_list.ensure(deep_cap * sizeof(int64_t)));
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(variant_support_call, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                       pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, ctr,
-                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0);
+    int64_t *dl = (int64_t *)c->deep_list.p;
+    const DeepSel fast{dl, deep_cap, nullptr, 0, nullptr, 0, 0};
+    // the loci the fast table handed over [from, hc.n_deep): the deep instantiation, same mode
+    auto run_deep = [&](int64_t from, const AmbItem *ain, const uint8_t *aref, int64_t n_ain) -> gq_status {
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      const int64_t nd = (int64_t)std::min<unsigned long long>(hc.n_deep, deep_cap) - from;
+      if (nd <= 0 || hc.err) return GQ_OK;
+      const DeepSel deep{nullptr, deep_cap, dl + from, nd, nullptr, 0, 0};
+      const int db = (int)std::min<int64_t>((nd + kSomWaves - 1) / kSomWaves, 64);
+      hipLaunchKernelGGL(variant_support_call<true>, dim3((unsigned)db), dim3(kBlock), 0, c->stream,
+                         (const Tile *)c->tiles.p, pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap,
+                         (uint8_t *)c->pool.p, pool_cap, ctr, ain ? (AmbItem *)nullptr : (AmbItem *)c->amb.p,
+                         ain ? (unsigned long long)0 : amb_cap, ain, aref, n_ain, deep);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      return GQ_OK;
+    };
+    hipLaunchKernelGGL(variant_support_call<false>, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap,
+                       (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr,
+                       (const uint8_t *)nullptr, (int64_t)0, fast);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    st = run_deep(0, nullptr, nullptr, 0);
+    if (st) return fail(st);
     bool retry = false;
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (hc.n_deep > deep_cap) {
+      deep_cap = hc.n_deep + 1024;
       retry = true;
     }
     if (!retry && hc.n_amb > 0 && !hc.err) {  // heap-order reference bases: replay, then redo those loci
@@ -1731,13 +1867,18 @@ gq_status gq_variant_support(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *l
       st = heap_ref_bases(c, pl, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
       if (st) return fail(st);
       const int ab = (int)std::min<int64_t>(((int64_t)amb.size() + kSomWaves - 1) / kSomWaves, 8192);
-      hipLaunchKernelGGL(variant_support_call, dim3((unsigned)ab), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap,
-                         ctr, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
-                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      const int64_t from = (int64_t)hc.n_deep;
+      hipLaunchKernelGGL(variant_support_call<false>, dim3((unsigned)ab), dim3(kBlock), 0, c->stream,
+                         (const Tile *)c->tiles.p, pl.n_tiles, pl.n_loci, rd->d, (VsRec *)c->srecs.p, rec_cap,
+                         (uint8_t *)c->pool.p, pool_cap, ctr, (AmbItem *)nullptr, (unsigned long long)0,
+                         (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p, (int64_t)amb.size(), fast);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      st = run_deep(from, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      if (st) return fail(st);
+      if (hc.n_deep > deep_cap) {
+        deep_cap = hc.n_deep + 1024;
+        retry = true;
+      }
     }
     if (hc.n_rec > rec_cap) {
       rec_cap = hc.n_rec + 1024;
@@ -1922,17 +2063,47 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
       }
     }
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), 8192);
-    hipLaunchKernelGGL(germline_standard_call, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+    HIP_TRY(c->deep_list.ensure(deep_cap * sizeof(int64_t)));
+    int64_t *dl = (int64_t *)c->deep_list.p;
+    const DeepSel fast{dl, deep_cap, nullptr, 0, nullptr, 0, 0};
+    // the loci the fast working set handed over [from, hc.n_deep): the deep instantiation, same
+    // mode, its per-wave scratch sized from the deepest of them and their largest allele table
+    auto run_deep = [&](int64_t from, AmbItem *aout, unsigned long long acap, const AmbItem *ain, const uint8_t *aref,
+                        int64_t n_ain) -> gq_status {
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      const int64_t nd = (int64_t)std::min<unsigned long long>(hc.n_deep, deep_cap) - from;
+      if (nd <= 0 || hc.err) return GQ_OK;
+      const int scap = (int)std::max<unsigned long long>(hc.deep_max, 64);
+      const int64_t nt = (int64_t)std::min<unsigned long long>(std::max<unsigned long long>(hc.deep_nt, 2), 64 * kDeepNS);
+      const int maxG = (int)std::max<int64_t>(nt * (nt + 1) / 2, 16);
+      const int64_t waves = std::min<int64_t>(nd, 256);
+      HIP_TRY(c->deep_scratch.ensure((size_t)waves * gs_wave_bytes(scap, maxG) + 256));
+      const DeepSel deep{nullptr, deep_cap, dl + from, nd, (uint8_t *)c->deep_scratch.p, scap, maxG};
+      hipLaunchKernelGGL(germline_standard_call<true>, dim3((unsigned)((waves + kSomWaves - 1) / kSomWaves)),
+                         dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p, (const ComplexItem *)c->cplx.p, rd->d, *p,
+                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, aout, acap, ain,
+                         aref, n_ain, deep);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      return GQ_OK;
+    };
+    hipLaunchKernelGGL(germline_standard_call<false>, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                        (const ComplexItem *)c->cplx.p, rd->d, *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p,
                        pool_cap, og, ctr, sw, (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr,
-                       (const uint8_t *)nullptr, (int64_t)0);
+                       (const uint8_t *)nullptr, (int64_t)0, fast);
     HIP_TRY(hipGetLastError());
+    st = run_deep(0, (AmbItem *)c->amb.p, amb_cap, nullptr, nullptr, 0);
+    if (st) return fail(st);
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     bool retry = false;
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;
+      retry = true;
+    }
+    if (hc.n_deep > deep_cap) {
+      deep_cap = hc.n_deep + 1024;
       retry = true;
     }
     if (!retry && hc.n_amb > 0 && !hc.err) {  // heap-order reference bases: replay, then those loci again
@@ -1943,14 +2114,21 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
       st = heap_ref_bases(c, pt, c->tiles, {rd}, amb, (uint8_t *)c->amb_ref.p);
       if (st) return fail(st);
       const int ablocks = (int)std::min<int64_t>(((int64_t)amb.size() + 3) / 4, 8192);
-      hipLaunchKernelGGL(germline_standard_call, dim3(ablocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         (const ComplexItem *)c->cplx.p, rd->d, *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p,
-                         pool_cap, og, ctr, sw, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
-                         (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      const int64_t from = (int64_t)hc.n_deep;
+      hipLaunchKernelGGL(germline_standard_call<false>, dim3(ablocks), dim3(kBlock), 0, c->stream,
+                         (const Tile *)c->tiles.p, (const ComplexItem *)c->cplx.p, rd->d, *p, (SomRec *)c->srecs.p,
+                         rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)nullptr,
+                         (unsigned long long)0, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p,
+                         (int64_t)amb.size(), fast);
       HIP_TRY(hipGetLastError());
+      st = run_deep(from, (AmbItem *)nullptr, (unsigned long long)0, (const AmbItem *)c->amb.p,
+                    (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+      if (st) return fail(st);
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (hc.n_deep > deep_cap) {
+        deep_cap = hc.n_deep + 1024;
+        retry = true;
+      }
     }
     if (hc.n_rec > rec_cap) {
       rec_cap = hc.n_rec + 1024;

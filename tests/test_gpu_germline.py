@@ -233,3 +233,31 @@ def test_device_results_equal_host_results(gpu_ctx, chrm):
                 assert np.array_equal(x.a[k], h.a[k]), k
             assert x.pool == h.pool
             assert x.tuples(rs.contig_names) == h.tuples(rs.contig_names)
+
+
+def _many_insertions(n_distinct, n_ref=100, n_alt=40, start=100, singleton_qual=31):
+    """A locus holding `n_distinct` distinct insertion alleles (one read each, base quality
+    singleton_qual), n_alt reads of one more insertion and n_ref reference reads: 10M kI 10M over
+    a 20-base reference."""
+    ref = "ACGTTGCAACGGTACCATGA"
+    reads = []
+    for i in range(n_distinct):
+        ins = "".join("ACGT"[(i >> (2 * k)) & 3] for k in range(6))
+        reads.append(mr(ref[:10] + ins + ref[10:], "10M6I10M", "20", start, quals=[singleton_qual] * 26))
+    reads += [mr(ref[:10] + "TTTTTTT" + ref[10:], "10M7I10M", "20", start)] * n_alt
+    reads += [mr(ref, "20M", "20", start)] * n_ref
+    reads.sort(key=lambda r: r["start"])
+    return make_read_set(reads)
+
+
+@pytest.mark.parametrize("n_distinct", [100, 200, 700])
+def test_more_distinct_alleles_than_the_fast_table(gpu_ctx, n_distinct):
+    """germline_complex keeps 128 (sample, allele) keys in registers; a locus with more goes to
+    the wide instantiation (1024 keys) instead of a capacity error (Pileup.scala:37-146 has no
+    limit): records equal the oracle's."""
+    rs = _many_insertions(n_distinct)
+    for threshold in (8, 0):
+        loci = _loci(rs, "chr1:90-130")
+        got = germline_threshold_reads(gpu_ctx, rs, loci, threshold, True, True)
+        want = O.germline_threshold(rs, loci, threshold, True, True)
+        assert got == want and len(want) > 0

@@ -94,3 +94,21 @@ def test_cli_germline_standard(tmp_path):
     assert len(want) > 5
     assert [(v["start"]["long"], v["alternateAllele"]["string"]) for v in recs] == [(w["locus"], w["alt"]) for w in want]
     assert all(v["end"]["long"] == v["start"]["long"] + 1 for v in recs)
+
+
+def test_deep_pileups_match_oracle(gpu_ctx):
+    """1500x with the window's initial group deeper than the LDS cover list (768 reads), and a
+    locus with 200 distinct insertion alleles (past the fast allele table and genotype array):
+    both handed to the deep instantiation, no capacity error (the reference has no depth limit)."""
+    from test_gpu_germline import _many_insertions
+    rs = generate(3_000, 1500, seed=19, indel_rate=1e-3).to_read_set()
+    loci = _loci(rs, "20:200-2800", 2)
+    got = germline_standard_reads(gpu_ctx, rs, loci)
+    want = O.germline_standard(rs, loci)
+    assert len(want) > 0
+    assert_rows_match(got, want)
+    rs = _many_insertions(200, n_ref=60, n_alt=120, singleton_qual=5)  # (low: no likelihood underflow)
+    loci = _loci(rs, "chr1:90-130")
+    want = O.germline_standard(rs, loci)
+    assert any(len(r["alt"]) > 1 for r in want)
+    assert_rows_match(germline_standard_reads(gpu_ctx, rs, loci), want)

@@ -71,3 +71,16 @@ def test_cli_variant_support(tmp_path):
     want = ["%s, %s, %d, %s, %s, %d" % r[:6] for r in _oracle(rs, flatten_partitions(
         partition_loci_uniformly(2, ls), rs.contig_index()))]
     assert lines == want + want
+
+
+def test_deep_pileups_match_oracle(gpu_ctx):
+    """1500x, and a locus with 200 distinct insertion alleles (past the fast table of 128):
+    the deep instantiation, no capacity error."""
+    from test_gpu_germline import _many_insertions
+    rs = generate(3_000, 1500, seed=23, indel_rate=1e-3).to_read_set()
+    loci = _loci(rs, "20:200-2800", 2)
+    assert variant_support_reads(gpu_ctx, rs, loci) == _oracle(rs, loci)
+    rs = _many_insertions(200, n_ref=60, n_alt=120, singleton_qual=5)  # (low: no likelihood underflow)
+    loci = _loci(rs, "chr1:90-130")
+    got = variant_support_reads(gpu_ctx, rs, loci)
+    assert got == _oracle(rs, loci) and len({r[4] for r in got if r[2] == 109}) > 200
