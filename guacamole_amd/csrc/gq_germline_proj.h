@@ -69,7 +69,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   using C = ProjCfg;
   constexpr int T = C::kT, U = C::kU;
   // per locus: event read bases (A | C << 16 at [i], T | G << 16 at [T + i]); MD bits 0-3 |
-  // N << 4 | complex diff << 16
+  // N << 4 | complex diff << 16.  Locus x of the block is word ix(x) = (x & 7) * 64 + (x >> 3):
+  // lane l's eight loci (8 l + j) sit at j * 64 + l, so the decision's reads (every lane, one j)
+  // are 64 consecutive words — no bank conflicts (8 l + j put every lane of a read on four banks).
   __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ __attribute__((aligned(16))) uint32_t dlw[C::kWaves][T];  // MidDeletion range differences
@@ -77,15 +79,15 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave], *dl = dlw[wave];
-  {
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-    {  // separate stores (a chained assignment re-reads each word from LDS)
-      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4;
-      uint4 *d4 = reinterpret_cast<uint4 *>(dl + 8 * lane);
-      d4[0] = z4; d4[1] = z4;
-    }
-  }
+  auto ix = [](int32_t x) { return ((x & 7) << 6) | (x >> 3); };
+  // the tile's LDS words back to 0: 16-byte stores, lane l at 16 l (consecutive: no conflicts)
+  auto zero_words = [&]() {  // separate stores (a chained assignment re-reads each word from LDS)
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    uint4 *e4 = reinterpret_cast<uint4 *>(ev), *m4 = reinterpret_cast<uint4 *>(mk), *d4 = reinterpret_cast<uint4 *>(dl);
+    e4[lane] = z4; e4[64 + lane] = z4; e4[128 + lane] = z4; e4[192 + lane] = z4;
+    m4[lane] = z4; m4[64 + lane] = z4; d4[lane] = z4; d4[64 + lane] = z4;
+  };
+  zero_words();
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
   __syncthreads();
   const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
@@ -221,14 +223,15 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const bool mid = (p.y & kPevMidDel) != 0;  // MidDeletion elements: their own count
         uint32_t *dw = mid ? dl : mk;
         if (a < b) {
-          atomicAdd(&dw[a - B0], mid ? 1u : 1u << 16);
-          if (b < (int64_t)B0 + T) atomicAdd(&dw[b - B0], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
+          atomicAdd(&dw[ix((int32_t)(a - B0))], mid ? 1u : 1u << 16);
+          if (b < (int64_t)B0 + T) atomicAdd(&dw[ix((int32_t)(b - B0))], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
         }
       } else if (l >= B0 && l < B0 + T) {
         const uint32_t m = p.y & 15u, c = (p.y >> 4) & 7u;
-        if (m) atomicOr(&mk[l - B0], m);
-        if (c < 4) atomicAdd(&ev[(c >> 1) * T + (l - B0)], 1u << (16 * (c & 1)));
-        else if (c == 4) atomicAdd(&mk[l - B0], 1u << 4);
+        const int32_t x = ix(l - B0);
+        if (m) atomicOr(&mk[x], m);
+        if (c < 4) atomicAdd(&ev[(c >> 1) * T + x], 1u << (16 * (c & 1)));
+        else if (c == 4) atomicAdd(&mk[x], 1u << 4);
       }
     };
 #pragma unroll
@@ -317,8 +320,6 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     widen();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint4 *e4 = reinterpret_cast<uint4 *>(ev + 8 * lane), *f4 = reinterpret_cast<uint4 *>(ev + T + 8 * lane), *m4 = reinterpret_cast<uint4 *>(mk + 8 * lane);
-    uint4 *d4 = reinterpret_cast<uint4 *>(dl + 8 * lane);
     uint32_t kinds = 0, nrec = 0, ncpx = 0;
     int32_t mid0 = 0;  // MidDeletion elements entering this lane's first locus
     // locus j's 16-bit count of base w (a dynamic j selects among four registers)
@@ -335,18 +336,21 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     };
     if (!(dbg & 4)) {
       // complex elements per locus: prefix of the range differences over the block
-      int32_t run = 0;
-      {
-        const uint4 ma = m4[0], mb = m4[1];
-        run = ((int32_t)ma.x >> 16) + ((int32_t)ma.y >> 16) + ((int32_t)ma.z >> 16) + ((int32_t)ma.w >> 16) +
-              ((int32_t)mb.x >> 16) + ((int32_t)mb.y >> 16) + ((int32_t)mb.z >> 16) + ((int32_t)mb.w >> 16);
+      // this lane's eight words of each array, read once (conflict-free rows of 64 words)
+      uint32_t m8[8], d8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        m8[j] = mk[64 * j + lane];
+        d8[j] = dl[64 * j + lane];
+      }
+      int32_t run = 0, mrun0 = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        run += (int32_t)m8[j] >> 16;
+        mrun0 += (int32_t)d8[j];
       }
       int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
-      {  // the same for the MidDeletion ranges
-        const uint4 da = d4[0], db = d4[1];
-        const int32_t mrun = (int32_t)(da.x + da.y + da.z + da.w + db.x + db.y + db.z + db.w);
-        mid0 = (int32_t)wave_incl_scan((uint32_t)mrun) - mrun;
-      }
+      mid0 = (int32_t)wave_incl_scan((uint32_t)mrun0) - mrun0;  // the same for the MidDeletion ranges
       int32_t mid_run = mid0;
       // ---- decision (GermlineThresholdCaller.scala:97-177 for pileups of single-base and
       //      MidDeletion alleles), eight loci, four unrolled at a time with their LDS words read
@@ -354,8 +358,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
 #pragma unroll 4
       for (int j = 0; j < 8; ++j) {
-        const uint32_t eacj = ev[8 * lane + j], etgj = ev[T + 8 * lane + j], m8j = mk[8 * lane + j];
-        const int32_t ddj = (int32_t)dl[8 * lane + j];
+        const uint32_t eacj = ev[64 * j + lane], etgj = ev[T + 64 * j + lane], m8j = m8[j];
+        const int32_t ddj = (int32_t)d8[j];
         {
         const int32_t l = B0 + 8 * lane + j;
         const bool in = l >= L0 && l < L1;
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
                                    ((uint64_t)'T' << 32) | ((uint64_t)'>' << 40);
       int32_t mrun = mid0;
       for (int j = 0; j < 8; ++j) {
-        mrun += (int32_t)dl[8 * lane + j];
+        mrun += (int32_t)dl[64 * j + lane];
         const uint32_t nmid = mrun > 0 ? (uint32_t)mrun : 0u;
         const uint32_t kind = (kinds >> (2 * j)) & 3u;
         if (__ballot(kind != 0) == 0) continue;  // no lane writes for locus j (uniform skip)
@@ -416,9 +420,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
           continue;
         }
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
-        const uint32_t mw = mk[8 * lane + j];
+        const uint32_t mw = mk[64 * j + lane];
         const uint32_t nN = (mw >> 4) & 0xFFFu;
-        const uint32_t mask = ref_mask(mw, ev[8 * lane + j], ev[T + 8 * lane + j], cA, cC, cT, cG);
+        const uint32_t mask = ref_mask(mw, ev[64 * j + lane], ev[T + 64 * j + lane], cA, cC, cT, cG);
         const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
         const uint64_t ord = (uint64_t)(f64(rec, 0) + (pos - L0));
         CallRec rr;
@@ -453,10 +457,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         }
       }
     }
-    {  // separate stores (a chained assignment re-reads each word from LDS)
-      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-      e4[0] = z4; e4[1] = z4; f4[0] = z4; f4[1] = z4; m4[0] = z4; m4[1] = z4; d4[0] = z4; d4[1] = z4;
-    }  // this lane's words, for the next tile
+    zero_words();  // for the next tile (the wave's own words: no barrier)
     if (dbg & 16) {  // phase clocks (cycles per tile and wave): setup + entries, counting, -, widen, decision
       const uint64_t t_f = __builtin_readcyclecounter();
       clk[0] += t_b - t_a;
