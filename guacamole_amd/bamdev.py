@@ -340,8 +340,19 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
     # inflated size) are released now, so the callers have the HBM; on a host thread, off the
     # load's critical path (their hipFree calls take ~45 ms at chr20 30x)
     import threading
-    threading.Thread(target=L.gq_bam_dev_close, args=(h,), name="gq_bam_dev_close").start()
+    th = threading.Thread(target=L.gq_bam_dev_close, args=(h,), name="gq_bam_dev_close")
+    th.start()
+    _release_threads.append(th)
     return rs
+
+
+_release_threads: List[object] = []
+
+
+def join_release_threads() -> None:
+    """Wait for the device loaders' buffer releases (before a hard process exit)."""
+    while _release_threads:
+        _release_threads.pop().join()
 
 
 def _raise(rc: int) -> None:

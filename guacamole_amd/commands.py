@@ -287,18 +287,25 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
                 for calls_r, nm in zip(per_rank, rank_names) for c, l, s, g, ref, alt, fl in calls_r.tuples(rs.contig_names)]
         sample_name = lambda s: s  # noqa: E731
     else:
-        rows = germline_threshold_reads(ctx, rs, flat, args.threshold, args.emit_ref, args.emit_no_call)
+        calls = ctx.germline_threshold(device_reads(ctx, rs), flat, args.threshold, args.emit_ref, args.emit_no_call)
+        rows = None
     clock.mark("call")
-    from .output import germline_genotype, write_vcf_dir_germline
+    from .output import germline_genotype, write_vcf_dir_germline, write_vcf_dir_germline_calls
     if args.out.lower().endswith(".vcf") and args.max_genotypes <= 1:
         # the lines _write_genotypes writes for these records, without building the records
-        write_vcf_dir_germline(args.out, rows, sample_name, rs.contig_lengths_map)
+        if rows is None:
+            write_vcf_dir_germline_calls(args.out, calls, rs.contig_names, sample_name, rs.contig_lengths_map)
+        else:
+            write_vcf_dir_germline(args.out, rows, sample_name, rs.contig_lengths_map)
     else:
+        if rows is None:
+            rows = calls.tuples(rs.contig_names)
         out = [germline_genotype(c, l, sample_name(s), gt, ref, alt) for c, l, s, gt, ref, alt, fl in rows]
         _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
     clock.mark("write")
-    print("Called %d genotypes." % len(rows), file=sys.stderr)
-    clock.report(rank=rank, reads=int(mine_rs.n if world > 1 else rs.n), genotypes=len(rows), loci=int(loci.count),
+    n_out = len(rows) if rows is not None else len(calls)
+    print("Called %d genotypes." % n_out, file=sys.stderr)
+    clock.report(rank=rank, reads=int(mine_rs.n if world > 1 else rs.n), genotypes=n_out, loci=int(loci.count),
                  ingest="device" if isinstance(rs, DeviceReadSet) else "host",
                  device_ingest=getattr(rs, "timings", None))
     return _finish_rank(0)

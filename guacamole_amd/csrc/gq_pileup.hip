@@ -2556,6 +2556,51 @@ gq_status gq_germline_threshold_device(gq_ctx *c, const gq_dev_reads *rd, const 
   return GQ_OK;
 }
 
+gq_status gq_write_vcf_germline(const char *path, const char *header, int64_t n, const int32_t *contig,
+                                const int64_t *pos, const uint8_t *gt0, const uint8_t *gt1, const int64_t *ref_off,
+                                const int32_t *ref_len, const int64_t *alt_off, const int32_t *alt_len,
+                                const uint8_t *pool, int32_t n_contigs, const char *const *contig_names) {
+  if (!path || !header || (n > 0 && (!contig || !pos || !gt0 || !gt1 || !ref_off || !ref_len || !alt_off || !alt_len ||
+                                      !contig_names)))
+    return set_err(GQ_E_ARG, "gq_write_vcf_germline: null argument");
+  FILE *f = fopen(path, "wb");
+  if (!f) return set_err(GQ_E_ARG, "cannot write %s", path);
+  std::string buf(header);
+  buf.reserve((size_t)n * 48 + buf.size() + 64);
+  static const char kGt[4] = {'0', '1', '.', '.'};  // GenotypeAllele Ref, Alt, OtherAlt, NoCall
+  std::vector<size_t> clen((size_t)std::max(n_contigs, 0));
+  for (int32_t k = 0; k < n_contigs; ++k) clen[(size_t)k] = contig_names[k] ? strlen(contig_names[k]) : 0;
+  char num[24];
+  bool ok = true;
+  for (int64_t i = 0; i < n && ok; ++i) {
+    const int32_t c = contig[i];
+    if (c < 0 || c >= n_contigs || !contig_names[c]) {
+      fclose(f);
+      return set_err(GQ_E_ARG, "gq_write_vcf_germline: record %lld has contig %d", (long long)i, c);
+    }
+    buf.append(contig_names[c], clen[(size_t)c]);
+    buf += '\t';
+    const int k = snprintf(num, sizeof num, "%lld", (long long)(pos[i] + 1));
+    buf.append(num, (size_t)k);
+    buf.append("\t.\t", 3);
+    buf.append((const char *)pool + ref_off[i], (size_t)ref_len[i]);
+    buf += '\t';
+    buf.append((const char *)pool + alt_off[i], (size_t)alt_len[i]);
+    buf.append("\t.\t.\t.\tGT\t", 10);
+    buf += kGt[gt0[i] & 3];
+    buf += '/';
+    buf += kGt[gt1[i] & 3];
+    buf += '\n';
+    if (buf.size() > (size_t)(64 << 20)) {  // write in 64 MiB pieces
+      ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+      buf.clear();
+    }
+  }
+  if (ok && !buf.empty()) ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+  if (fclose(f) != 0) ok = false;
+  return ok ? GQ_OK : set_err(GQ_E_ARG, "write to %s failed", path);
+}
+
 void gq_free_calls(gq_calls *r) {
   if (!r) return;
   free(r->block_);

@@ -154,7 +154,8 @@ EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timing
             "gq_vaf_histogram", "gq_germline_standard", "gq_bam_dev_open", "gq_bam_dev_close", "gq_bam_dev_header_text",
             "gq_bam_dev_n_contigs", "gq_bam_dev_contig_name", "gq_bam_dev_contig_length", "gq_bam_dev_scan",
             "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin", "gq_reads_download", "gq_bam_dev_map",
-            "gq_bam_dev_load", "gq_bam_dev_map_ex", "gq_bam_dev_plan", "gq_bam_dev_plan_segments")
+            "gq_bam_dev_load", "gq_bam_dev_map_ex", "gq_bam_dev_plan", "gq_bam_dev_plan_segments",
+            "gq_write_vcf_germline")
 
 
 def lib():
@@ -210,6 +211,9 @@ def lib():
         L.gq_bam_dev_plan.restype = C.c_int
         L.gq_bam_dev_plan_segments.argtypes = [vp, vp, vp, vp, vp]
         L.gq_bam_dev_plan_segments.restype = C.c_int
+        L.gq_write_vcf_germline.argtypes = [C.c_char_p, C.c_char_p, C.c_int64] + [vp] * 9 + [C.c_int32,
+                                                                                           C.POINTER(C.c_char_p)]
+        L.gq_write_vcf_germline.restype = C.c_int
         L.gq_bam_dev_load.argtypes = [vp, vp]
         L.gq_bam_dev_load.restype = C.c_int
         L.gq_bam_dev_close.argtypes = [vp]
@@ -229,6 +233,18 @@ def lib():
         L.gq_reads_download.argtypes = [vp, C.POINTER(gq_reads)]
         _lib = L
     return _lib
+
+
+def write_vcf_germline(path: str, header: str, calls: "GermlineCalls", contig_names: Sequence[str]) -> None:
+    """gq_write_vcf_germline: the header, then one line per record of `calls` (one sample)."""
+    a = calls.a
+    n = len(calls)
+    cols = {k: np.ascontiguousarray(a[k]) for k in ("contig", "pos", "gt0", "gt1", "ref_off", "ref_len", "alt_off",
+                                                   "alt_len")}
+    names = (C.c_char_p * max(1, len(contig_names)))(*[x.encode() for x in contig_names])
+    pool = np.frombuffer(calls.pool, np.uint8) if calls.pool else np.zeros(1, np.uint8)
+    _check(lib().gq_write_vcf_germline(path.encode(), header.encode(), n, *[_ptr(cols[k]) or None for k in cols],
+                                       pool.ctypes.data, len(contig_names), names))
 
 
 def _check(rc: int) -> None:

@@ -219,13 +219,26 @@ def write_vcf_dir_germline(path: str, rows, sample_name, contig_lengths: Optiona
     return part
 
 
-def _write_vcf_fields(path: str, recs, contig_lengths: Optional[Dict[str, int]]) -> None:
-    """recs: (contig, start, ref, alt, sampleId, FORMAT, values) per genotype, in output order."""
-    samples: Dict[str, int] = {}
-    for r in recs:
-        if r[4] not in samples:
-            samples[r[4]] = len(samples)
-    ns = len(samples)
+def write_vcf_dir_germline_calls(path: str, calls, contig_names, sample_name, contig_lengths=None) -> str:
+    """write_vcf_dir_germline straight from a GermlineCalls' columns: records of one sample (the
+    common case) go through the library's line writer (gq_write_vcf_germline) without a Python
+    object per record; several samples take write_vcf_dir_germline's layout."""
+    import os
+    import numpy as np
+    from . import native
+    slots = np.unique(calls.a["sample"]) if len(calls) else np.zeros(0, np.uint8)
+    names = sorted({sample_name(int(s)) for s in slots})
+    if len(names) > 1:
+        return write_vcf_dir_germline(path, calls.tuples(contig_names), sample_name, contig_lengths)
+    os.makedirs(path, exist_ok=False)
+    part = os.path.join(path, VCF_PART)
+    native.write_vcf_germline(part, vcf_header(names, contig_lengths), calls, contig_names)
+    open(os.path.join(path, "_SUCCESS"), "w").close()
+    return part
+
+
+def vcf_header(samples, contig_lengths: Optional[Dict[str, int]]) -> str:
+    """The ## lines and the #CHROM line over `samples` (sample columns in order)."""
     out = ["##fileformat=VCFv4.1\n",
            '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">\n',
            '##FORMAT=<ID=GQ,Number=1,Type=Integer,Description="Genotype Quality">\n',
@@ -234,6 +247,17 @@ def _write_vcf_fields(path: str, recs, contig_lengths: Optional[Dict[str, int]])
     for c, ln in (contig_lengths or {}).items():
         out.append("##contig=<ID=%s,length=%d>\n" % (c, ln))
     out.append("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples) + "\n")
+    return "".join(out)
+
+
+def _write_vcf_fields(path: str, recs, contig_lengths: Optional[Dict[str, int]]) -> None:
+    """recs: (contig, start, ref, alt, sampleId, FORMAT, values) per genotype, in output order."""
+    samples: Dict[str, int] = {}
+    for r in recs:
+        if r[4] not in samples:
+            samples[r[4]] = len(samples)
+    ns = len(samples)
+    out = [vcf_header(samples, contig_lengths)]
     if ns == 1:
         out.extend("%s\t%d\t.\t%s\t%s\t.\t.\t.\t%s\t%s\n" % (c, s + 1, ref, alt, fmt, vals)
                    for c, s, ref, alt, _, fmt, vals in recs)

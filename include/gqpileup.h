@@ -320,6 +320,15 @@ gq_status gq_reads_download(const gq_dev_reads *r, const gq_reads *dst);
 gq_status gq_germline_threshold(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,
                                 const gq_germline_params *params, gq_calls **out);
 void gq_free_calls(gq_calls *c);
+/* The body of the VCF a germline-threshold run writes (Common.scala:290-293 saveAsVcf of the
+ * records' single sample: "CHROM POS . REF ALT . . . GT <gt>" per record, POS 1-based) after
+ * `header` (the ## lines and the #CHROM line), to `path`; contig_names[k] names contig id k.
+ * GQ_E_ARG on an unwritable path.  The CLI's writer for one-sample output (Python builds the
+ * multi-sample layout).                                                                     */
+gq_status gq_write_vcf_germline(const char *path, const char *header, int64_t n, const int32_t *contig,
+                                const int64_t *pos, const uint8_t *gt0, const uint8_t *gt1, const int64_t *ref_off,
+                                const int32_t *ref_len, const int64_t *alt_off, const int32_t *alt_len,
+                                const uint8_t *pool, int32_t n_contigs, const char *const *contig_names);
 /* gq_germline_threshold with the records left in HBM (no PCIe copy; the multi-GPU driver
  * gathers the images over xGMI).  Same decisions, same record order.                      */
 gq_status gq_germline_threshold_device(gq_ctx *ctx, const gq_dev_reads *reads, const gq_loci *loci,

@@ -40,6 +40,43 @@ def test_germline_vcf_writer_equals_record_writer(tmp_path):
             assert (b / "_SUCCESS").exists()
 
 
+def test_germline_vcf_column_writer_equals_record_writer(tmp_path):
+    """write_vcf_dir_germline_calls (the CLI's single-process path: the library's line writer
+    over the result columns, gq_write_vcf_germline) writes the record writer's bytes; one and
+    three samples (the latter through the row layout), indels, an empty call list."""
+    import numpy as np
+    from guacamole_amd import native
+    from guacamole_amd.output import write_vcf_dir_germline_calls
+    names = ["s1", "s2", "default"]
+    contigs = ["1", "chrM"]
+    code = {"Ref": 0, "Alt": 1, "OtherAlt": 2, "NoCall": 3}
+    gts = [("Ref", "Alt"), ("Alt", "Alt"), ("Alt", "OtherAlt"), ("Ref", "Ref"), ("NoCall", "NoCall")]
+    for samples in (1, 3):
+        for n in (40, 0):
+            rows = [(contigs[1 if i % 3 else 0], 10 * i, i % samples, gts[i % len(gts)], "ACGT"[i % 4],
+                     "ACGT"[(i + 1) % 4] + ("T" if i % 7 == 0 else ""), 0) for i in range(n)]
+            pool, ro, ao = b"", [], []
+            for r in rows:
+                ro.append(len(pool))
+                pool += r[4].encode()
+                ao.append(len(pool))
+                pool += r[5].encode()
+            a = {"contig": np.array([contigs.index(r[0]) for r in rows], np.int32),
+                 "pos": np.array([r[1] for r in rows], np.int64), "sample": np.array([r[2] for r in rows], np.uint8),
+                 "gt0": np.array([code[r[3][0]] for r in rows], np.uint8),
+                 "gt1": np.array([code[r[3][1]] for r in rows], np.uint8),
+                 "flags": np.zeros(n, np.uint8), "ref_off": np.array(ro, np.int64),
+                 "ref_len": np.array([len(r[4]) for r in rows], np.int32), "alt_off": np.array(ao, np.int64),
+                 "alt_len": np.array([len(r[5]) for r in rows], np.int32)}
+            calls = native.GermlineCalls(a, pool, 0, 0, 0, 0)
+            x, y = tmp_path / ("x%d%d.vcf" % (samples, n)), tmp_path / ("y%d%d.vcf" % (samples, n))
+            write_vcf_dir(str(x), [germline_genotype(c, l, names[s], gt, ref, alt) for c, l, s, gt, ref, alt, _ in rows],
+                          {"1": 5000, "chrM": 16571})
+            write_vcf_dir_germline_calls(str(y), calls, contigs, lambda s: names[s], {"1": 5000, "chrM": 16571})
+            assert (x / "part-r-00000").read_bytes() == (y / "part-r-00000").read_bytes()
+            assert (y / "_SUCCESS").exists()
+
+
 def _records(text):
     return read_avro_json(text)
 
