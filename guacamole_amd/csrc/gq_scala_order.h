@@ -1,5 +1,7 @@
 // gq_scala_order.h — the iteration order of the Scala 2.10.3 collections the reference's
-// output order depends on (host and device; also compiled into the oracle).
+// output order depends on (host and device code of the library).  The oracle has its own,
+// separate restatement (oracle/oracle.cpp scala_order), and the tests a third in Python
+// (tests/scala_order_py.py): three independent statements checked against each other.
 //
 // Three sites of the reference iterate a hash-based collection and let that order reach the
 // output (paths relative to /root/reference/src/main/scala/org/hammerlab/guacamole/):
