@@ -109,7 +109,7 @@ def main() -> int:
     ap.add_argument("--calls-out", default=None, help="rank 0 writes the gathered records (rank order) as JSON")
     ap.add_argument("--no-single-pass", dest="single_pass", action="store_false",
                     help="skip the measured single pass (the shard as a BAM through the CLI)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
@@ -271,6 +271,8 @@ def main() -> int:
                    "read_len": 150, "threshold": args.threshold, "parallelism": "loci-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     # the bus rate: measured HBM bytes (PMC) / the kernel's time / peak
+                     "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
                      "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
@@ -535,6 +537,8 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
     k_ms = float(np.mean(stages["pileup_ms"]))
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)
+    pmc = somatic_pmc("panel" if tdepth >= 500 else "chr1", L, tdepth, ndepth)
+    traffic = None if pmc is None else pmc["kernels"].get("somatic_proj", {}).get("hbm_bytes_per_launch")
     return {"metric": "somatic-standard loci/sec, tumor %gx / normal %gx" % (tdepth, ndepth),
             "value": visited * steps / el, "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
             "warmup": warmup,
@@ -556,8 +560,12 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
                        "ns_per_candidate": 1e6 * float(np.mean(stages["call_ms"])) / max(1, int(calls.candidate_loci))},
             "roofline": {"bound": "hbm", "kernel": "somatic_proj", "kernel_ms": k_ms, "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes},
-            "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), workload),
+                         "traffic": traffic,
+                         "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes,
+                         "traffic_source": None if traffic is None else pmc["source"]},
+            "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), pmc, "somatic_call_k<false>"),
+            "deep_caller_roofline": caller_roofline(float(np.mean(stages["deep_ms"])), pmc, "somatic_call_k<true>"),
             "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s,
             # a cold call on resident reads: both sets' upload-time derivation + the first call
             # (the tumor's projection and margin projection; the normal needs neither)
@@ -567,29 +575,42 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
                          "loci_per_s": visited / ((derive_ms + cold_ms) * 1e-3)}}
 
 
-CALLER_PMC = os.path.join(ROOT, "profiles", "r03_h2_somatic_call_pmc.csv")
+SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r04.json")
 
 
-def caller_roofline(call_ms: float, workload: str):
-    """The exact somatic caller (somatic_call_k<false>) is FP64 VALU work behind dependent loads.
-    Its issue roofline: VALU wave-instructions per launch (PMC of the same chr1 configs[2] launch,
-    CALLER_PMC, by scripts/profile_somatic.sh) over this run's kernel time, against the chip's
-    VALU issue rate (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, the convention of
-    DESIGN.md's PMC readings); the wait share says what bounds it instead."""
-    if "chr1" not in workload or not os.path.exists(CALLER_PMC) or call_ms <= 0:
+def somatic_pmc(workload: str, L: int, tdepth: float, ndepth: float):
+    """The PMC summary of the same somatic workload (scripts/profile_somatic.sh +
+    scripts/pmc_somatic.py), or None when none was taken at this size."""
+    try:
+        with open(SOMATIC_PMC) as fh:
+            w = json.load(fh).get(workload)
+    except (OSError, ValueError):
         return None
-    import csv
-    pm = {r["counter"]: float(r["mean_per_launch"]) for r in csv.DictReader(open(CALLER_PMC))}
+    if not w or w.get("length") != L or w.get("tumor_depth") != tdepth or w.get("normal_depth") != ndepth:
+        return None
+    return w
+
+
+def caller_roofline(call_ms: float, pmc, kernel: str):
+    """An exact somatic caller (somatic_call_k<false>, or <true> over the deep list) is FP64 VALU
+    work behind dependent loads.  Its issue roofline: VALU wave-instructions per launch (PMC of the
+    same workload, SOMATIC_PMC) over this run's kernel time, against the chip's VALU issue rate
+    (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, the convention of DESIGN.md's PMC
+    readings); the wait share says what bounds it instead."""
+    if pmc is None or call_ms <= 0:
+        return None
+    pm = pmc["kernels"].get(kernel, {})
     insts = pm.get("SQ_INSTS_VALU")
     if not insts:
         return None
     peak = 1024 * 2.4e9 / 2
     ach = insts / (call_ms * 1e-3)
-    return {"bound": "issue/latency", "kernel": "somatic_call_k<false>", "kernel_ms": call_ms,
+    return {"bound": "issue/latency", "kernel": kernel, "kernel_ms": call_ms,
             "valu_wave_insts_per_launch": insts, "achieved": ach, "peak": peak, "unit": "wave-instr/s",
             "frac": ach / peak,
             "wait_frac": pm.get("SQ_WAIT_ANY", 0.0) / max(1.0, pm.get("SQ_WAVE_CYCLES", 1.0)),
-            "source": os.path.relpath(CALLER_PMC, ROOT)}
+            "hbm_bytes_per_launch": pm.get("hbm_bytes_per_launch"),
+            "source": pmc["source"]}
 
 
 if __name__ == "__main__":

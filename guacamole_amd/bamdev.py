@@ -16,6 +16,7 @@ out of (contig, start) order (the host loader sorts them).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import time
 import weakref
 from typing import Dict, List, Optional
@@ -57,8 +58,8 @@ GQ_E_PLAN = 16
 # Loci of margin before each planned range when the BAM has no index: a read that starts further
 # back and still overlaps the range is missed unless some rank sees one that long (the load then
 # re-plans with a wider halo, see load_reads_device).  1 Mb at 30x is ~0.2 M extra records
-# decoded per range boundary.
-DEFAULT_HALO = 1 << 20
+# decoded per range boundary.  GQ_INGEST_HALO overrides it (tests use a small one).
+DEFAULT_HALO = int(os.environ.get("GQ_INGEST_HALO", 1 << 20))
 
 
 class DeviceReadSet:

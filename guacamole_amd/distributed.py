@@ -172,6 +172,21 @@ def _all_true(ok: bool, device) -> bool:
     return bool(t.item())
 
 
+def _any_true(flag: bool, device) -> bool:
+    return not _all_true(not flag, device)
+
+
+def _all_max(vals: Sequence[int], device) -> List[int]:
+    """Element-wise maximum of an int list over the ranks."""
+    import torch
+    import torch.distributed as dist
+    if not vals:
+        return []
+    t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=torch.device(device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [int(v) for v in t.cpu().tolist()]
+
+
 def all_gather_objects(obj) -> list:
     import torch.distributed as dist
     out = [None] * dist.get_world_size()
@@ -197,9 +212,11 @@ def device_ingest_ranks(ctx, paths: Sequence[str], filters, builder, parallelism
         raise ValueError("Tumor and normal samples have different sequence dictionaries.")
     first = {"maps": maps}
 
-    def load(region):
+    def load(region, halos=None):
         ms = first.pop("maps", [None] * len(paths))  # the host mappings serve the first load
-        return [load_reads_device(ctx, p, filters, m, region=region) for p, m in zip(paths, ms)]
+        if halos is None:
+            return [load_reads_device(ctx, p, filters, m, region=region) for p, m in zip(paths, ms)]
+        return [load_reads_device(ctx, p, filters, m, region=region, halo=h) for p, m, h in zip(paths, ms, halos)]
     got = rank_loci_and_reads(load, names, lengths, builder, parallelism, accuracy, rank, world, device)
     return None if got is None else (got[0], got[1], names)
 
@@ -265,6 +282,18 @@ def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accurac
         sets = load(region)
     if not _all_true(all(x is not None for x in sets), device):
         return None
+    # Without an index a rank plans `halo` loci back from each of its ranges: a read reaching
+    # further back is found only by the rank whose segments hold its start.  The longest span any
+    # rank saw (per input) is shared, and a rank whose probe plan's halo is shorter loads again.
+    spans = _all_max([int(getattr(x, "timings", {}).get("max_span", 0)) for x in sets], device)
+    plans = [getattr(x, "timings", {}).get("plan") for x in sets]
+    short = [p is not None and not p["used_index"] and g > p["halo"] for p, g in zip(plans, spans)]
+    if _any_true(any(short), device):  # every rank takes this branch together (collectives inside)
+        if any(short):
+            sets = None
+            sets = load(region, [max(2 * g, p["halo"]) if p is not None else 0 for p, g in zip(plans, spans)])
+        if not _all_true(all(x is not None for x in sets), device):
+            return None
     return sets, mine
 
 

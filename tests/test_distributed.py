@@ -211,3 +211,45 @@ def test_rank_loci_world2_equal_one_process_partition():
             assert len(loads) <= (1 if accuracy == 0 else 2), loads
             if accuracy == 0:
                 assert n == need
+
+
+class _Loaded:
+    def __init__(self, n, span, halo):
+        self.n = n
+        self.timings = {"max_span": span, "plan": {"used_index": 0, "halo": halo}}
+
+
+def _span_worker(rank, world, port, q):
+    """Rank 0's segments hold a read spanning 5000 loci; rank 1 planned with a 1000-locus halo and
+    saw none that long: rank 1 must load again with a halo covering it, rank 0 must not."""
+    import torch.distributed as dist
+    from guacamole_amd.distributed import rank_loci_and_reads
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def load(region, halos=None):
+        calls.append(halos)
+        h = 1000 if halos is None else halos[0]
+        return [_Loaded(1, 5000 if rank == 0 else 150, h)]
+    sets, _ = rank_loci_and_reads(load, ["c"], [100_000], LociSet.parse("all"), 4, 0, rank, world, "cpu")
+    q.put((rank, calls, sets[0].timings["plan"]["halo"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_probe_halo_is_widened_by_another_ranks_span():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_span_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == (0, [None, [10000]], 10000)  # (this stand-in load does not re-plan itself)
+    assert got[1] == (1, [None, [10000]], 10000)

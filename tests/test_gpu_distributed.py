@@ -22,9 +22,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(args, world, out, reports=None):
+def _run(args, world, out, reports=None, extra_env=None):
     """The CLI at `world` ranks; reports: a list that receives each rank's GQ_TIMING report."""
-    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT, GQ_TIMING="1")
+    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT, GQ_TIMING="1", **(extra_env or {}))
     if world == 1:
         cmd = [sys.executable, "-m", "guacamole_amd"] + args + ["--out", out]
     else:
@@ -122,7 +122,9 @@ def test_germline_two_ranks_device_ingest_equal_one(tmp_path, index, parallelism
     args = ["germline-threshold", "--reads", bam, "--parallelism", parallelism, "--partition-accuracy", accuracy]
     one = _run(args, 1, str(tmp_path / "one.json"))
     reps = []
-    two = _run(args, 2, str(tmp_path / "two.json"), reps)
+    # without an index the probes plan 20 kb back from each range (the default 1 Mb halo would
+    # cover this whole 300 kb contig)
+    two = _run(args, 2, str(tmp_path / "two.json"), reps, {"GQ_INGEST_HALO": "20000"})
     assert one == two and one.count("\n") > 100
     assert len(reps) == 2
     host = load_reads(bam, InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True))
