@@ -283,89 +283,93 @@ __device__ __forceinline__ void slice_piece(const DevReads &R, int64_t r, int32_
 // pieces sorted by first column, which is read order (reads are sorted by start; pieces of reads
 // that began before the slice all start at its column 0): as many rows as the slice's deepest
 // column has reads.  Each read's row goes to rows[r - ra] (0xFFFF: no piece), so the fill kernels
-// place words without redoing this serial pass.  Returns the slice's rows, or -1 past
-// kSliceRowsMax.
-__device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const SliceWin &W, uint16_t *__restrict__ rows) {
+// place words without redoing this pass.  Returns the slice's rows, or -1 past kSliceRowsMax.
+//
+// The pieces that start at one column are placed together: the rows free at that column (row
+// k's end column rend[k] <= c) are listed in ascending order by one wave-wide compaction, and
+// the group's t-th piece takes the t-th of them (new rows past the list) — what placing the
+// group's pieces one by one, each on the first free row, gives, since a placed piece's row is
+// busy at c.  rend (kSliceRowsMax bytes) and fl (kSliceRowsMax u16) are this wave's LDS.
+__device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const SliceWin &W, uint16_t *__restrict__ rows,
+                                                     uint8_t *__restrict__ rend, uint16_t *__restrict__ fl) {
   const int lane = threadIdx.x & 63;
-  // row k's first free column (0-16) is byte k & 3 of rend[k >> 8] on lane (k >> 2) & 63;
-  // 0x7F: not opened.  A free row: byte <= s, tested four at a time without borrows.
-  constexpr int kRD = kSliceRowsMax / 256;
-  uint32_t rend[kRD];
-#pragma unroll
-  for (int j = 0; j < kRD; ++j) rend[j] = 0x7F7F7F7Fu;
+  const unsigned long long below = (1ull << lane) - 1ull;
   int32_t nrows = 0;
   bool over = false;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
     int32_t s0 = W.qc0, sl = 0;
     if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    const int32_t c = s0 - W.qc0, e = c + sl;
     int32_t myrow = -1;
     unsigned long long pend = __ballot(sl > 0);
-    while (pend) {  // the batch's pieces in read order (uniform)
+    while (pend) {  // the batch's groups of equal first column, in read order (uniform)
       const int pl = __ffsll((long long)pend) - 1;
-      pend &= pend - 1;
-      const uint32_t ps = (uint32_t)__builtin_amdgcn_readlane(s0 - W.qc0, pl);
-      const uint32_t pe = ps + (uint32_t)__builtin_amdgcn_readlane(sl, pl);
-      const uint32_t lim = (ps + 1u) * 0x01010101u;
-      int32_t k = -1;
-#pragma unroll
-      for (int j = 0; j < kRD; ++j) {
-        if (k >= 0 || 256 * j >= nrows) continue;  // uniform
-        const uint32_t fr = ~((rend[j] | 0x80808080u) - lim) & 0x80808080u;
-        const unsigned long long b = __ballot(fr != 0);
-        if (b) {
-          const int ln = __ffsll((long long)b) - 1;
-          const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fr, ln);
-          k = 256 * j + 4 * ln + (__builtin_ctz(f) >> 3);
+      const int32_t cg = __builtin_amdgcn_readlane(c, pl);
+      const unsigned long long mem = __ballot(sl > 0 && c == cg);
+      pend &= ~mem;
+      const uint32_t S = (uint32_t)__popcll(mem);
+      // the first S rows free at column cg, ascending (rows k0..k0+3 on lane (k0 / 4) % 64)
+      uint32_t nf = 0;
+      const uint32_t lim = (uint32_t)(cg + 1) * 0x01010101u;
+      for (int32_t j0 = 0; j0 < nrows && nf < S; j0 += 256) {  // uniform
+        const int32_t k0 = j0 + 4 * lane;
+        uint32_t x = 0x7F7F7F7Fu;  // 0x7F: no such row (never free)
+        if (k0 < nrows) {
+          x = *reinterpret_cast<const uint32_t *>(rend + k0);
+          const int32_t nb = nrows - k0;
+          if (nb < 4) {
+            const uint32_t keep = (1u << (8 * nb)) - 1u;
+            x = (x & keep) | (0x7F7F7F7Fu & ~keep);
+          }
         }
+        uint32_t fr = ~((x | 0x80808080u) - lim) & 0x80808080u;  // bytes <= cg (no borrows: each >= 0x80)
+        const uint32_t n = (uint32_t)__popc(fr);
+        const uint32_t incl = wave_incl_scan(n);
+        uint32_t at = nf + incl - n;
+        while (fr) {
+          fl[at++] = (uint16_t)(k0 + (__builtin_ctz(fr) >> 3));
+          fr &= fr - 1u;
+        }
+        nf += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       }
-      if (k < 0) {
-        if (nrows >= kSliceRowsMax) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if ((mem >> lane) & 1ull) {
+        const uint32_t t = (uint32_t)__popcll(mem & below);
+        const int32_t k = t < nf ? (int32_t)fl[t] : nrows + (int32_t)(t - nf);
+        if (k >= kSliceRowsMax) {
           over = true;
-          continue;
+        } else {
+          rend[k] = (uint8_t)e;
+          myrow = k;
         }
-        k = nrows++;
       }
-      const int kl = (k >> 2) & 63, sh = 8 * (k & 3);
-#pragma unroll
-      for (int j = 0; j < kRD; ++j)
-        if (j == (k >> 8) && lane == kl) rend[j] = (rend[j] & ~(0xFFu << sh)) | (pe << sh);
-      if (lane == pl) myrow = k;
+      nrows += S > nf ? (int32_t)(S - nf) : 0;
+      if (nrows > kSliceRowsMax) nrows = kSliceRowsMax;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     if (rows && r < W.rz) rows[r - W.ra] = myrow >= 0 ? (uint16_t)myrow : (uint16_t)0xFFFFu;
   }
-  return over ? -1 : nrows;
+  return __ballot(over) ? -1 : nrows;
 }
 
-// put(active, read, column, row) once per word of the slice's pieces, rows from
-// slice_assign_rows (rows[r - ra]), every lane of the wave in uniform control flow, active for
-// lanes that hold a word; a batch's words go out in piece order (consecutive words of a piece
-// to consecutive lanes).
+// put(read, first column, columns, row) once per piece of the slice (a lane per read of each
+// 64-read batch, read order; lanes without a piece idle), rows from slice_assign_rows.
 template <class F>
-__device__ __forceinline__ void slice_words(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
-                                            F &&put) {
+__device__ __forceinline__ void slice_pieces(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
+                                             F &&put) {
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
-    int32_t s0 = W.qc0, sl = 0, myrow = -1;
     if (r < W.rz) {
       const uint16_t k = rows[r - W.ra];
       if (k != 0xFFFFu) {
+        int32_t s0 = W.qc0, sl = 0;
         slice_piece(R, r, W.qc0, s0, sl);
-        myrow = k;
+        if (sl > 0) put(r, s0, sl, (int32_t)k);
       }
-    }
-    const uint32_t len = myrow >= 0 ? (uint32_t)sl : 0u;
-    const uint32_t incl = wave_incl_scan(len), ex = incl - len;
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
-      const uint32_t w = w0 + (uint32_t)lane;
-      int k = 0;  // the last lane whose words start at or before w
-#pragma unroll
-      for (int b = 32; b >= 1; b >>= 1)
-        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
-      const int32_t col = __shfl(s0, k, 64) + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
-      put(w < tot, r0 + k, col, __shfl(myrow, k, 64));
     }
   }
 }
@@ -450,7 +454,7 @@ struct DevBuf {
 struct gq_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[8] = {};
   gq_timings timings{};
   int germ_tile = gq::kGermT;
   int n_cu = 0;
@@ -462,6 +466,8 @@ struct gq_ctx {
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
   gq::DevBuf deep_list, deep_scratch;              // somatic: the deep caller's list and per-wave scratch
+  int front_wg_per_cu = 0;                         // somatic_front: resident workgroups per CU
+  gq::DevBuf el_store;                             // somatic: the split caller's element store (ElemStore)
   gq::DevBuf win_bound;                            // germline: window bounds (window_bounds)
   gq::DevBuf bkt;                                  // germline output order: bucket counts / offsets / fill
   void *pin = nullptr;                             // pinned host staging for the small per-call copies

@@ -390,11 +390,14 @@ __global__ void slice_windows(DevReads R, int64_t n_slices, int64_t *__restrict_
 // kSliceRowsMax the slice is pbad (and gets no rows).
 __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, uint16_t *__restrict__ prow,
                                                  int32_t *__restrict__ srows, uint8_t *__restrict__ pbad) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_rend[4][kSliceRowsMax];
+  __shared__ uint16_t s_fl[4][kSliceRowsMax];
+  const int wv = threadIdx.x >> 6;
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     const SliceWin W = slice_stored(R, slot);
-    const int32_t n = slice_assign_rows(R, W, prow + R.soff[slot]);
+    const int32_t n = slice_assign_rows(R, W, prow + R.soff[slot], s_rend[wv], s_fl[wv]);
     if ((threadIdx.x & 63) == 0) {
       srows[slot] = n < 0 ? 0 : n;
       if (n < 0) pbad[slot] = 1;
@@ -416,49 +419,73 @@ __global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, unsi
   if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
 }
 
-// The projection word of read r at column col (loci [8 col, 8 col + 8)).
-__device__ uint2 proj_word(const DevReads &R, int64_t r, int32_t col) {
+// Byte codes of four ASCII bases (proj_code, SWAR): A 1, C 3, G 7, T 4, anything else 0.
+__device__ __forceinline__ uint32_t proj_codes4(uint32_t x) {
+  auto eq = [x](uint32_t pat) {  // 0x80 in the bytes equal to pat's (exact: no carries between bytes)
+    const uint32_t z = x ^ pat;
+    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+  };
+  const uint32_t m = eq(0x41414141u) | eq(0x43434343u) | eq(0x47474747u) | eq(0x54545454u);
+  return x & ((m >> 7) * 7u);
+}
+
+typedef uint64_t gq_u64u __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
+
+// The projection words of read r's piece [s0, s0 + sl) of its slice, written at `out` (the
+// piece's row, word s0 & 15 first).  Word col: byte j = code of locus 8 col + j | code of locus
+// 8 col + j + 4 << 4 (4-bit codes, proj_code).  A lane per piece: the read's descriptor once,
+// then eight bases per 8-byte load for the words inside the read.
+__device__ void proj_piece(const DevReads &R, int64_t r, int32_t s0, int32_t sl, uint32_t *__restrict__ out) {
   const ColDesc d = R.cdesc[r];
   const int32_t s = d.start, e = d.end;
-  const int32_t lb = 8 * col;  // locus of byte 0
-  uint32_t v[2] = {0, 0};
   if (d.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base seq_lo + (l - s)
     const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int32_t l = lb + q;
-      if (l >= s && l < e) v[q >> 2] |= proj_code(R.seq[p0 + l]) << (8 * (q & 3));
+    for (int32_t w = 0; w < sl; ++w) {
+      const int32_t lb = 8 * (s0 + w);
+      uint64_t b;
+      if (lb >= s && lb + 8 <= e) {
+        b = *reinterpret_cast<const gq_u64u *>(R.seq + p0 + lb);
+      } else {
+        b = 0;
+        for (int q = 0; q < 8; ++q) {
+          const int32_t l = lb + q;
+          if (l >= s && l < e) b |= (uint64_t)R.seq[p0 + l] << (8 * q);
+        }
+      }
+      out[w] = proj_codes4((uint32_t)b) | (proj_codes4((uint32_t)(b >> 32)) << 4);
     }
   } else {  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
     const int32_t nmd = (int32_t)(d.info & 0xFFFFu), nseg = (int32_t)((d.info >> 18) & 0xFFu);
     const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
     const int64_t so = R.seq_off[r];
-    for (int32_t q2 = 0; q2 < nseg; ++q2) {
-      const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-      if ((b >> 16) != kSegCount) continue;
-      const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
-      for (int q = 0; q < 8; ++q) {
-        const int32_t l = lb + q;
-        if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
+    for (int32_t w = 0; w < sl; ++w) {
+      const int32_t lb = 8 * (s0 + w);
+      uint32_t v[2] = {0, 0};
+      for (int32_t q2 = 0; q2 < nseg; ++q2) {
+        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+        if ((b >> 16) != kSegCount) continue;
+        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
+        if (ra >= lb + 8 || ra + rl <= lb) continue;
+        for (int q = 0; q < 8; ++q) {
+          const int32_t l = lb + q;
+          if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
+        }
       }
+      out[w] = v[0] | (v[1] << 4);
     }
   }
-  return make_uint2(v[0], v[1]);
 }
 
-// The projection pool in block rows, one wave per slice (walk_slice_rows; pbad slices stay
-// zero: their blocks go to the walker).
+// The projection pool in block rows, one wave per slice, a lane per piece (the rows row_count
+// assigned, stored; pbad slices stay zero: their blocks go to the walker).
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     const int64_t base = 16 * R.srow[slot];  // words
-    slice_words(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](bool act, int64_t r, int32_t col, int32_t row) {
-      if (act) {
-        const uint2 w = proj_word(R, r, col);  // byte codes of loci 0-3, 4-7 -> nibbles
-        *reinterpret_cast<uint32_t *>(proj + 4 * (base + 16 * (int64_t)row + (col & 15))) = w.x | (w.y << 4);
-      }
+    slice_pieces(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](int64_t r, int32_t s0, int32_t sl, int32_t row) {
+      proj_piece(R, r, s0, sl, reinterpret_cast<uint32_t *>(proj) + base + 16 * (int64_t)row + (s0 & 15));
     });
   }
 }

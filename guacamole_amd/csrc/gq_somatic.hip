@@ -1615,7 +1615,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096, deep_cap = 4096;
   Counters hc{};
-  float call_ms = 0, deep_ms = 0;
+  float call_ms = 0, deep_ms = 0, front_ms = 0;
+  static const bool split = !getenv("GQ_CALL_SPLIT") || atoi(getenv("GQ_CALL_SPLIT")) != 0;  // A/B: 0 = one kernel
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
@@ -1644,9 +1645,11 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     hipLaunchKernelGGL(part_scan_som, dim3(1), dim3(1024), 0, c->stream, ctr, og);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    unsigned long long n_cand = 0;
     {  // candidate overflow: grow and re-run the tile kernels before the (costly) caller runs
       unsigned long long pm = 0;
       HIP_TRY(hipMemcpyAsync(&pm, &ctr->part_max[1], sizeof(pm), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(&n_cand, &ctr->part_off[1][kParts], sizeof(n_cand), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       if (pm) {
         og.capA[1] += pm + 64;
@@ -1666,23 +1669,75 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     // many generations leaves a tail of idle SIMDs behind the last ones)
     if (c->call_wg_per_cu <= 0) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_call_k<false>, kBlock, 0) != hipSuccess || nb <= 0)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_call_k<false, true>, kBlock, 0) != hipSuccess ||
+          nb <= 0)
         nb = 3;
       c->call_wg_per_cu = nb;
     }
     static const int grid_env = getenv("GQ_CALL_GRID") ? atoi(getenv("GQ_CALL_GRID")) : 0;  // A/B: 0 = resident
     const int64_t grid_cap = grid_env > 0 ? (int64_t)grid_env : (int64_t)c->call_wg_per_cu * c->n_cu;
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), grid_cap);
-    hipLaunchKernelGGL(somatic_call_k<false>, dim3(cblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                       (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
-                       (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
-                       (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
-                       rv, dbg, DeepIO{(int64_t *)c->deep_list.p, deep_cap, 0, nullptr, 0, 0});
-    HIP_TRY(hipGetLastError());
+    const DeepIO dio{(int64_t *)c->deep_list.p, deep_cap, 0, nullptr, 0, 0};
+    front_ms = 0;
+    if (!split) {
+      hipLaunchKernelGGL((somatic_call_k<false, false>), dim3(cblocks), dim3(kBlock), 0, c->stream,
+                         (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+                         (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)c->amb.p,
+                         amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, rv, dbg, dio,
+                         ElemStore{});
+      HIP_TRY(hipGetLastError());
+    } else {
+      // the split caller, in batches of at most kStoreBatch candidates (the store: 5 KiB each):
+      // somatic_front (covers + element records, latency-bound, many waves) then the back end
+      // (tables, FP64 genotypes, evidence) over the stored records
+      constexpr int64_t kStoreBatch = 1 << 20;
+      const int64_t nb = std::min<int64_t>((int64_t)n_cand, kStoreBatch);
+      const size_t hdr_b = ((size_t)std::max<int64_t>(nb, 1) * sizeof(uint4) + 255) & ~(size_t)255;
+      const size_t el_b = (size_t)std::max<int64_t>(nb, 1) * 2 * kFastCap * sizeof(uint4);
+      const size_t cov_b = (size_t)std::max<int64_t>(nb, 1) * 2 * kFastCap * sizeof(int32_t);
+      HIP_TRY(c->el_store.ensure(hdr_b + el_b + cov_b));
+      if (c->front_wg_per_cu <= 0) {
+        int fb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&fb, somatic_front, kBlock, 0) != hipSuccess || fb <= 0) fb = 6;
+        c->front_wg_per_cu = fb;
+      }
+      uint8_t *sb = (uint8_t *)c->el_store.p;
+      for (int64_t b0 = 0; b0 < (int64_t)n_cand; b0 += kStoreBatch) {
+        const int64_t b1 = std::min<int64_t>((int64_t)n_cand, b0 + kStoreBatch);
+        const ElemStore es{(uint4 *)sb, (uint4 *)(sb + hdr_b), (int32_t *)(sb + hdr_b + el_b), b0, b1};
+        const int64_t waves = b1 - b0;
+        const unsigned fblocks = (unsigned)std::min<int64_t>((waves + kSomWaves - 1) / kSomWaves,
+                                                            (int64_t)c->front_wg_per_cu * c->n_cu);
+        const unsigned bblocks = (unsigned)std::min<int64_t>((waves + kSomWaves - 1) / kSomWaves, grid_cap);
+        if (b0 > 0) {  // the previous batch's front time (its back end keeps the GPU busy meanwhile)
+          HIP_TRY(hipEventSynchronize(c->ev[7]));
+          float ms = 0;
+          (void)hipEventElapsedTime(&ms, c->ev[6], c->ev[7]);
+          front_ms += ms;
+        }
+        HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+        hipLaunchKernelGGL(somatic_front, dim3(fblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+                           (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p, og, ctr, sw, dbg, dio,
+                           es);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev[7], c->stream));
+        hipLaunchKernelGGL((somatic_call_k<false, true>), dim3(bblocks), dim3(kBlock), 0, c->stream,
+                           (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d,
+                           *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
+                           (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
+                           rv, dbg, dio, es);
+        HIP_TRY(hipGetLastError());
+      }
+    }
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     (void)hipEventElapsedTime(&call_ms, c->ev[2], c->ev[3]);
+    if (split && n_cand > 0) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, c->ev[6], c->ev[7]);
+      front_ms += ms;
+    }
     deep_ms = 0;
     bool retry = false;
     if (hc.n_deep > deep_cap) {
@@ -1698,13 +1753,14 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
       HIP_TRY(hipEventRecord(c->ev[5], c->stream));
       const unsigned blocks = (unsigned)((nw + kSomWaves - 1) / kSomWaves);
-      hipLaunchKernelGGL(somatic_call_k<true>, dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
+      hipLaunchKernelGGL((somatic_call_k<true, false>), dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
                          (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                          (AmbItem *)(ain ? nullptr : c->amb.p), ain ? (unsigned long long)0 : amb_cap, ain, aref,
                          ain ? n_items : (int64_t)0, ain ? RefView{nullptr, nullptr} : rv, dbg,
                          DeepIO{(int64_t *)c->deep_list.p, 0, ain ? 0 : n_items, (uint8_t *)c->deep_scratch.p, scap,
-                                kMaxG});
+                                kMaxG},
+                         ElemStore{});
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
       HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -1759,7 +1815,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
   if ((dbg & 16) && hc.prof[5])
-    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): covers %.0f elements %.0f tables %.0f "
+    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): front|records %.0f - %.0f tables %.0f "
             "tumor-genotypes %.0f normal-genotypes+evidence %.0f (%llu candidates reached)\n", (double)hc.prof[0] / hc.prof[5],
             (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5], (double)hc.prof[3] / hc.prof[5],
             (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
@@ -1791,6 +1847,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   c->timings.deep_max = (int64_t)hc.deep_max;
   c->timings.call_ms = call_ms;
   c->timings.deep_ms = deep_ms;
+  c->timings.front_ms = front_ms;
   c->timings.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
   *out = res;
   return GQ_OK;

@@ -504,16 +504,193 @@ struct DeepIO {
   int scap, maxG;            // deep kernel: elements per sample per wave, genotypes
 };
 
+// The caller's front: the covering reads of both samples (pileup element order) and one element
+// record per covering read (m.el, m.cov), and per lane the std-bit mask of the MD-derived
+// reference bases it saw (mask; OR over the wave = the pileup's reference-base set).  Latency-bound
+// (dependent searches and per-read loads).  Returns false when the candidate leaves this kernel:
+// deeper than m.cap (the fast kernels list it for the deep one).
+template <bool DEEP>
+__device__ __forceinline__ bool call_front(const Tile &tt_, const Tile &tn_, int32_t pos, int64_t it, const DevReads &RT,
+                                           const DevReads &RN, const gq_somatic_params &prm, Counters *ctr,
+                                           const SomWin &sw, CallMem &m, int dbg, const DeepIO &dio, uint32_t (&nc)[2],
+                                           uint32_t (&mask)[2]) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rb[2] = {tt_.rb, tn_.rb}, re[2] = {tt_.re, tn_.re};
+  const int32_t win = sw.range_win[tt_.range];
+  const WinInit wi[2] = {sw.wi[2 * win], sw.wi[2 * win + 1]};
+  // ---- covering reads of both samples: [first pmax_end > pos, first start > pos) of each
+  //      tile window, the four searches in lockstep
+  int64_t ra[2], rz[2];
+  {
+    const int64_t lo[4] = {rb[0], rb[0], rb[1], rb[1]}, hi[4] = {re[0], re[0], re[1], re[1]};
+    int64_t out[4];
+    wave_first_true_k<4>(lo, hi, [&](int k, int64_t r) {
+      const DevReads &R = k < 2 ? RT : RN;
+      return (k & 1) ? R.start[r] > pos : R.pmax_end[r] > pos;
+    }, out);
+    ra[0] = out[0], rz[0] = out[1], ra[1] = out[2], rz[1] = out[3];
+  }
+  nc[0] = nc[1] = 0;
+  {
+    const int64_t span = max(rz[0] - ra[0], rz[1] - ra[1]);
+    for (int64_t c0 = 0; c0 < span; c0 += 64) {
+      bool c[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const DevReads &R = s ? RN : RT;
+        const int64_t r = ra[s] + c0 + lane;
+        c[s] = r < rz[s] && R.start[r] <= pos && pos < R.end[r];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const unsigned long long b = __ballot(c[s]);
+        const uint32_t at = nc[s] + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+        if (c[s] && at < (uint32_t)m.cap) m.cov[s][at] = (int32_t)(ra[s] + c0 + lane - rb[s]);
+        nc[s] += (uint32_t)__popcll(b);
+      }
+    }
+  }
+  if (nc[0] > (uint32_t)m.cap || nc[1] > (uint32_t)m.cap || (!DEEP && (dbg & 64))) {
+    if constexpr (!DEEP) {  // deeper than the LDS records (or GQ_DBG & 64, tests): the deep kernel's, whole
+      if (lane == 0) {
+        const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
+        if (k < dio.cap) dio.list[k] = it;
+        atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
+      }
+    } else {
+      raise_at(ctr, GQ_E_CAPACITY, pos);  // the host sized the scratch from deep_max
+    }
+    return false;
+  }
+  // ---- pileup element order: where the window's initial (heap-ordered) group still covers
+  //      pos, its reads are a prefix of the list, reordered by heap rank (SlidingWindow
+  //      currentRegions(), DistributedUtil.scala:260-274; Pile.atGreaterLocus keeps them first)
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const WinInit &w = wi[s];
+    if (!(w.n > 0 && pos < w.E)) continue;  // uniform
+    const DevReads &R = s ? RN : RT;
+    int p = 0;
+    for (int k0 = 0; k0 < (int)nc[s]; k0 += 64) {
+      const int k = k0 + lane;
+      p += (int)__popcll(__ballot(k < (int)nc[s] && R.start[rb[s] + m.cov[s][k]] <= w.F));
+    }
+    for (int k = lane; k < p; k += 64) {
+      const int64_t r = rb[s] + m.cov[s][k];
+      int lo = 0, hi = w.n;
+      while (lo < hi) {
+        const int md = (lo + hi) >> 1;
+        if (sw.init_reads[w.off + md] < r) lo = md + 1;
+        else hi = md;
+      }
+      m.tmp[k] = (uint32_t)sw.init_rank[w.off + lo];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < p; k += 64) {
+      int before = 0;
+      for (int j = 0; j < p; ++j) before += m.tmp[j] < m.tmp[k] ? 1 : 0;
+      m.tmp[m.cap + before] = (uint32_t)m.cov[s][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < p; k += 64) m.cov[s][k] = (int32_t)m.tmp[m.cap + k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  // ---- elements, both samples' chunks together: each covering read's scalars in one round,
+  //      then (a single aligned block, the common read) its base, quality and MD event at
+  //      pos; other reads take the general CIGAR walk (classify) and md_ref_at
+  mask[0] = mask[1] = 0;
+  {
+    const uint32_t span = max(nc[0], nc[1]);
+    for (uint32_t c0 = 0; c0 < span; c0 += 64) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const DevReads &R = s ? RN : RT;
+        const uint32_t k = c0 + lane;
+        if (k >= nc[s]) continue;
+        const int64_t r = rb[s] + m.cov[s][k];
+        const int32_t st = R.start[r];
+        const int ld = (int)R.lead[r];
+        const int64_t so = R.seq_off[r];
+        const int mq = (int)R.mapq[r];
+        const uint8_t rfl = R.flags[r];
+        const int32_t nmd = R.n_md[r];
+        const int64_t mdo = R.md_off[r];
+        const uint32_t nmm = (uint32_t)R.n_mismatch[r];
+        uint32_t fl = 0;
+        int32_t rp = 0, aux = 0;
+        uint32_t base = 0, kind = K_SNV;
+        int q = 0;
+        if (ld >= 0) {
+          const int32_t off = pos - st;
+          rp = ld + off;
+          base = R.seq[so + rp];
+          q = (int)(int8_t)R.qual[so + rp];
+          if (nmd < 0) {
+            raise_at(ctr, GQ_E_NO_MD, pos);
+          } else {
+            const int v = nmd > 0 ? md_find(R.md_ev + mdo, nmd, off) : -1;
+            mask[s] |= std_bit((uint8_t)(v >= 0 ? v : (int)base));
+            fl = kElAct;
+          }
+        } else {
+          const int v = md_ref_at(R, r, pos);
+          if (v < 0) {
+            raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
+          } else {
+            mask[s] |= std_bit((uint8_t)v);
+            AlleleDesc d;
+            int errc = 0;
+            if (!classify(R, r, pos, 0, d, &errc)) {
+              raise_at(ctr, errc, pos);
+            } else {
+              fl = kElAct;
+              kind = d.kind;
+              base = d.base;
+              rp = d.rp;
+              aux = d.aux;
+              q = elem_quality(R, d, so, mq);
+            }
+          }
+        }
+        if (prm.min_mapq <= 0 || mq >= prm.min_mapq) fl |= kElPass;  // QualityAlignedReadsFilter
+        if (!(rfl & 1)) fl |= kElFwd;
+        m.el[s][k] = make_uint4((uint32_t)rp, (uint32_t)aux,
+                                base | (kind << 8) | ((uint32_t)(uint8_t)(int8_t)q << 16) | ((uint32_t)mq << 24),
+                                (nmm & 0xFFFFu) | (fl << 16));
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return true;
+}
+
+// The element store between the split caller's kernels (somatic_front -> somatic_call_k<false,
+// true>), for the candidates [b0, b1) of the list: per candidate a header {nc tumor, nc normal,
+// reference-base mask tumor, normal} (nc tumor = kElSkip: the front listed it for the deep
+// kernel) and kFastCap element records and covering-read offsets per sample.
+constexpr uint32_t kElSkip = 0xFFFFFFFFu;
+struct ElemStore {
+  uint4 *hdr;
+  uint4 *el;
+  int32_t *cov;
+  int64_t b0, b1;
+};
+
 #ifndef GQ_CALL_WPE2
 #define GQ_CALL_WPE2 3  // fast kernel: waves per SIMD the register budget must allow (4: 69 VGPRs spilled)
 #endif
-template <bool DEEP>
+template <bool DEEP, bool BACK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : GQ_CALL_WPE2))) void somatic_call_k(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
     DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs, unsigned long long rec_cap,
     uint8_t *__restrict__ pool, unsigned long long pool_cap, OutGeom og, Counters *ctr, SomWin sw,
     AmbItem *__restrict__ amb_out, unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
-    const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, RefView ref, int dbg, DeepIO dio) {
+    const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, RefView ref, int dbg, DeepIO dio, ElemStore es) {
+  // BACK: the candidates [es.b0, es.b1) whose covers and element records somatic_front stored.
   // amb_in == nullptr: the candidates (fast kernel) or the deep list (deep kernel); loci where a
   // sample's MD-derived reference bases disagree are listed (amb_out) for the heap-order replay.
   // amb_in != nullptr (deep kernel only): the listed loci with both samples' bases resolved
@@ -546,10 +723,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.cap = kFastCap;
     m.maxG = kMaxG;
   }
-  const unsigned long long n_items =
-      amb_in ? (unsigned long long)n_amb_in : DEEP ? (unsigned long long)dio.n_in : ctr->part_off[1][kParts];
-  // dbg & 16: phase clocks per candidate and wave (covers, elements, tables, tumor genotypes,
-  // normal genotypes + evidence + record, candidates), summed per workgroup in LDS (a global
+  static_assert(!(DEEP && BACK), "the deep kernel runs its own front");
+  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in
+                                     : DEEP ? (unsigned long long)dio.n_in
+                                     : BACK ? (unsigned long long)es.b1
+                                            : ctr->part_off[1][kParts];
+  const int64_t li0 = BACK ? es.b0 + gwave : gwave;
+  // dbg & 16: phase clocks per candidate and wave (front or the stored records' load, -, tables,
+  // tumor genotypes, normal genotypes + evidence + record, candidates), summed per workgroup in LDS (a global
   // atomic per phase would queue every wave on one address) and added to ctr->prof at the end
   __shared__ unsigned long long s_clk[6];
   if (threadIdx.x < 6) s_clk[threadIdx.x] = 0;
@@ -569,8 +750,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   };
   int64_t it_next = 0;
   ComplexItem item_next{0, 0, 0};
-  if (gwave < (int64_t)n_items) item_next = fetch_item(gwave, it_next);
-  for (int64_t li = gwave; li < (int64_t)n_items; li += nwaves_total) {
+  if (li0 < (int64_t)n_items) item_next = fetch_item(li0, it_next);
+  for (int64_t li = li0; li < (int64_t)n_items; li += nwaves_total) {
     tick(-1);
     if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[5], 1ull);
     const int64_t it = it_next;
@@ -580,158 +761,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     const int32_t pos = item.pos;
     const int32_t t_contig = tt_.contig, t_L0 = tt_.L0;
     const int64_t t_ord0 = tt_.ordinal0;
-    const int64_t rb[2] = {tt_.rb, tn_.rb}, re[2] = {tt_.re, tn_.re};
-    const int32_t win = sw.range_win[tt_.range];
-    const WinInit wi[2] = {sw.wi[2 * win], sw.wi[2 * win + 1]};
-    // ---- covering reads of both samples: [first pmax_end > pos, first start > pos) of each
-    //      tile window, the four searches in lockstep
-    int64_t ra[2], rz[2];
-    {
-      const int64_t lo[4] = {rb[0], rb[0], rb[1], rb[1]}, hi[4] = {re[0], re[0], re[1], re[1]};
-      int64_t out[4];
-      wave_first_true_k<4>(lo, hi, [&](int k, int64_t r) {
-        const DevReads &R = k < 2 ? RT : RN;
-        return (k & 1) ? R.start[r] > pos : R.pmax_end[r] > pos;
-      }, out);
-      ra[0] = out[0], rz[0] = out[1], ra[1] = out[2], rz[1] = out[3];
-    }
-    uint32_t nc[2] = {0, 0};
-    {
-      const int64_t span = max(rz[0] - ra[0], rz[1] - ra[1]);
-      for (int64_t c0 = 0; c0 < span; c0 += 64) {
-        bool c[2];
+    const int64_t rb[2] = {tt_.rb, tn_.rb};
+    uint32_t nc[2], mask[2];
+    if constexpr (BACK) {
+      // the front's records -> LDS (the tables, folds and evidence read them across lanes)
+      const uint4 h = es.hdr[li - es.b0];
+      if (h.x == kElSkip) continue;
+      nc[0] = h.x;
+      nc[1] = h.y;
+      mask[0] = h.z;
+      mask[1] = h.w;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const DevReads &R = s ? RN : RT;
-          const int64_t r = ra[s] + c0 + lane;
-          c[s] = r < rz[s] && R.start[r] <= pos && pos < R.end[r];
+      for (int s = 0; s < 2; ++s) {
+        const size_t o = ((size_t)(li - es.b0) * 2 + s) * kFastCap;
+        for (uint32_t k = lane; k < nc[s]; k += 64) {
+          m.el[s][k] = es.el[o + k];
+          m.cov[s][k] = es.cov[o + k];
         }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const unsigned long long b = __ballot(c[s]);
-          const uint32_t at = nc[s] + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-          if (c[s] && at < (uint32_t)m.cap) m.cov[s][at] = (int32_t)(ra[s] + c0 + lane - rb[s]);
-          nc[s] += (uint32_t)__popcll(b);
-        }
-      }
-    }
-    if (nc[0] > (uint32_t)m.cap || nc[1] > (uint32_t)m.cap || (!DEEP && (dbg & 64))) {
-      if constexpr (!DEEP) {  // deeper than the LDS records (or GQ_DBG & 64, tests): the deep kernel's, whole
-        if (lane == 0) {
-          const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
-          if (k < dio.cap) dio.list[k] = it;
-          atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
-        }
-      } else {
-        raise_at(ctr, GQ_E_CAPACITY, pos);  // the host sized the scratch from deep_max
-      }
-      continue;
-    }
-    // ---- pileup element order: where the window's initial (heap-ordered) group still covers
-    //      pos, its reads are a prefix of the list, reordered by heap rank (SlidingWindow
-    //      currentRegions(), DistributedUtil.scala:260-274; Pile.atGreaterLocus keeps them first)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const WinInit &w = wi[s];
-      if (!(w.n > 0 && pos < w.E)) continue;  // uniform
-      const DevReads &R = s ? RN : RT;
-      int p = 0;
-      for (int k0 = 0; k0 < (int)nc[s]; k0 += 64) {
-        const int k = k0 + lane;
-        p += (int)__popcll(__ballot(k < (int)nc[s] && R.start[rb[s] + m.cov[s][k]] <= w.F));
-      }
-      for (int k = lane; k < p; k += 64) {
-        const int64_t r = rb[s] + m.cov[s][k];
-        int lo = 0, hi = w.n;
-        while (lo < hi) {
-          const int md = (lo + hi) >> 1;
-          if (sw.init_reads[w.off + md] < r) lo = md + 1;
-          else hi = md;
-        }
-        m.tmp[k] = (uint32_t)sw.init_rank[w.off + lo];
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      for (int k = lane; k < p; k += 64) {
-        int before = 0;
-        for (int j = 0; j < p; ++j) before += m.tmp[j] < m.tmp[k] ? 1 : 0;
-        m.tmp[m.cap + before] = (uint32_t)m.cov[s][k];
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      for (int k = lane; k < p; k += 64) m.cov[s][k] = (int32_t)m.tmp[m.cap + k];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    } else {
+      if (!call_front<DEEP>(tt_, tn_, pos, it, RT, RN, prm, ctr, sw, m, dbg, dio, nc, mask)) continue;
     }
-    tick(0);
-    if (dbg & 1024) continue;  // ablation (diagnostics only): covers alone
-    // ---- elements, both samples' chunks together: each covering read's scalars in one round,
-    //      then (a single aligned block, the common read) its base, quality and MD event at
-    //      pos; other reads take the general CIGAR walk (classify) and md_ref_at
-    uint32_t mask[2] = {0, 0};
-    {
-      const uint32_t span = max(nc[0], nc[1]);
-      for (uint32_t c0 = 0; c0 < span; c0 += 64) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const DevReads &R = s ? RN : RT;
-          const uint32_t k = c0 + lane;
-          if (k >= nc[s]) continue;
-          const int64_t r = rb[s] + m.cov[s][k];
-          const int32_t st = R.start[r];
-          const int ld = (int)R.lead[r];
-          const int64_t so = R.seq_off[r];
-          const int mq = (int)R.mapq[r];
-          const uint8_t rfl = R.flags[r];
-          const int32_t nmd = R.n_md[r];
-          const int64_t mdo = R.md_off[r];
-          const uint32_t nmm = (uint32_t)R.n_mismatch[r];
-          uint32_t fl = 0;
-          int32_t rp = 0, aux = 0;
-          uint32_t base = 0, kind = K_SNV;
-          int q = 0;
-          if (ld >= 0) {
-            const int32_t off = pos - st;
-            rp = ld + off;
-            base = R.seq[so + rp];
-            q = (int)(int8_t)R.qual[so + rp];
-            if (nmd < 0) {
-              raise_at(ctr, GQ_E_NO_MD, pos);
-            } else {
-              const int v = nmd > 0 ? md_find(R.md_ev + mdo, nmd, off) : -1;
-              mask[s] |= std_bit((uint8_t)(v >= 0 ? v : (int)base));
-              fl = kElAct;
-            }
-          } else {
-            const int v = md_ref_at(R, r, pos);
-            if (v < 0) {
-              raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
-            } else {
-              mask[s] |= std_bit((uint8_t)v);
-              AlleleDesc d;
-              int errc = 0;
-              if (!classify(R, r, pos, 0, d, &errc)) {
-                raise_at(ctr, errc, pos);
-              } else {
-                fl = kElAct;
-                kind = d.kind;
-                base = d.base;
-                rp = d.rp;
-                aux = d.aux;
-                q = elem_quality(R, d, so, mq);
-              }
-            }
-          }
-          if (prm.min_mapq <= 0 || mq >= prm.min_mapq) fl |= kElPass;  // QualityAlignedReadsFilter
-          if (!(rfl & 1)) fl |= kElFwd;
-          m.el[s][k] = make_uint4((uint32_t)rp, (uint32_t)aux,
-                                  base | (kind << 8) | ((uint32_t)(uint8_t)(int8_t)q << 16) | ((uint32_t)mq << 24),
-                                  (nmm & 0xFFFFu) | (fl << 16));
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     Pile<NS> PS[2];
     const int fb = ref.b ? (int)ref.b[ref.off[t_contig] + pos] : -1;
 #pragma unroll
@@ -741,7 +793,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       PS[s].ambiguous = fb < 0 && __popc(mk) > 1;
       PS[s].refbase = amb_in ? amb_ref[2 * li + s] : fb >= 0 ? (uint8_t)fb : mk ? bit_base(mk) : (uint8_t)'N';
     }
-    tick(1);
+    tick(0);
     if (dbg & 2048) continue;  // ablation: covers + elements
     // ---- allele tables (the records now get their pileup reference base: SNV / DEL keys)
 #pragma unroll
@@ -968,5 +1020,55 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   if (dbg & 16) {
     __syncthreads();
     if (threadIdx.x < 6 && s_clk[threadIdx.x]) atomicAdd(&ctr->prof[threadIdx.x], s_clk[threadIdx.x]);
+  }
+}
+
+// The split caller's front (GQ_CALL_SPLIT, default on): covers and element records of the
+// candidates [es.b0, es.b1) into the element store, one wave per candidate.  It holds only the
+// front's registers, so more waves per SIMD hide its dependent loads than in the one-kernel
+// caller, whose FP64 back end sets the register budget.
+#ifndef GQ_FRONT_WPE
+#define GQ_FRONT_WPE 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_FRONT_WPE))) void somatic_front(
+    const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
+    DevReads RT, DevReads RN, gq_somatic_params prm, OutGeom og, Counters *ctr, SomWin sw, int dbg, DeepIO dio,
+    ElemStore es) {
+  constexpr int FW = kSomWaves;
+  __shared__ int32_t s_cov[FW][2][kFastCap];
+  __shared__ uint32_t s_tmp[FW][2 * kFastCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  CallMem m{};
+  m.cov[0] = s_cov[wv][0];
+  m.cov[1] = s_cov[wv][1];
+  m.tmp = s_tmp[wv];
+  m.cap = kFastCap;
+  m.maxG = kMaxG;
+  auto fetch = [&](int64_t li) { return items[part_slot_wave(ctr->part_off[1], (unsigned long long)li, og, 1)]; };
+  ComplexItem item_next{0, 0, 0};
+  if (es.b0 + gwave < es.b1) item_next = fetch(es.b0 + gwave);
+  for (int64_t li = es.b0 + gwave; li < es.b1; li += nwaves_total) {
+    const ComplexItem item = item_next;
+    if (li + nwaves_total < es.b1) item_next = fetch(li + nwaves_total);
+    const size_t o = (size_t)(li - es.b0) * 2 * kFastCap;
+    m.el[0] = es.el + o;  // the element records go straight to the store
+    m.el[1] = es.el + o + kFastCap;
+    uint32_t nc[2], mask[2];
+    const bool go = call_front<false>(tiles_t[item.tile], tiles_n[item.tile], item.pos, li, RT, RN, prm, ctr, sw, m, dbg,
+                                      dio, nc, mask);
+    uint4 h = make_uint4(kElSkip, 0, 0, 0);
+    if (go) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        for (int d = 1; d < 64; d <<= 1) mask[s] |= __shfl_xor(mask[s], d, 64);
+        for (uint32_t k = lane; k < nc[s]; k += 64) es.cov[o + (size_t)s * kFastCap + k] = m.cov[s][k];
+      }
+      h = make_uint4(nc[0], nc[1], mask[0], mask[1]);
+    }
+    if (lane == 0) es.hdr[li - es.b0] = h;
+    __builtin_amdgcn_wave_barrier();  // (the next candidate rewrites this wave's LDS)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
 }

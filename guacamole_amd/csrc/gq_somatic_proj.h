@@ -50,64 +50,95 @@ __global__ void margin_table(int incl_align, uint8_t *__restrict__ tab) {
   tab[i] = margin_term8(match != 0, q, em, lsm);
 }
 
-// The margin word of tumor read r at column col (8 loci, a byte each; hom_ref_margin_lane's
-// terms).  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
-// 25-36) and non-Match/Mismatch loci hold kMargin8Zero.
-__device__ uint2 margin_word(const DevReads &R, int64_t r, int32_t col, int min_mapq, const uint8_t *__restrict__ tab) {
-  const ColDesc d = R.cdesc[r];
-  const int32_t s = d.start;
-  const int32_t lb = 8 * col;
-  uint32_t v[2] = {0x80808080u, 0x80808080u};
+typedef uint64_t gq_u64m __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
+
+// The margin words of tumor read r's piece [s0, s0 + sl) of its slice (8 loci per word, a byte
+// each; hom_ref_margin_lane's terms) at `out` (the piece's row, word s0 & 15 first), a lane per
+// piece.  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
+// 25-36) and non-Match/Mismatch loci keep the pool's kMargin8Zero fill (nothing is written for a
+// dropped read).  The read's MD events are walked once across the piece (a cursor from one
+// search); qualities come eight per 8-byte load inside the read.  Returns whether a word holds a
+// kMargin8None term.
+__device__ bool margin_piece(const DevReads &R, int64_t r, int32_t s0, int32_t sl, int min_mapq,
+                             const uint8_t *__restrict__ tab, uint2 *__restrict__ out) {
   const int mq = (int)R.mapq[r];
-  if (!(min_mapq > 0 && mq < min_mapq)) {
-    const uint8_t *tm = tab + (mq << 8);
-    const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
-    const uint32_t *ev = R.md_ev + R.md_off[r];
-    // MD events at offsets >= lb - s (sorted)
-    int k = 0, hi2 = nmd;
-    while (k < hi2) {
-      const int m = (k + hi2) >> 1;
-      if ((int32_t)(ev[m] >> 8) < lb - s) k = m + 1;
-      else hi2 = m;
+  if (min_mapq > 0 && mq < min_mapq) return false;
+  const ColDesc d = R.cdesc[r];
+  const int32_t s = d.start, e = d.end;
+  const uint8_t *tm = tab + (mq << 8);
+  const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+  const uint32_t *ev = R.md_ev + R.md_off[r];
+  // the first MD event at or past the piece's first locus (sorted offsets)
+  int k = 0, hi2 = nmd;
+  const int32_t off0 = 8 * s0 - s;
+  while (k < hi2) {
+    const int m = (k + hi2) >> 1;
+    if ((int32_t)(ev[m] >> 8) < off0) k = m + 1;
+    else hi2 = m;
+  }
+  int32_t next = k < nmd ? (int32_t)(ev[k] >> 8) : INT32_MAX;  // offset of the cursor's event
+  auto term = [&](int32_t l, int qv) -> uint32_t {  // the element at locus l with quality qv
+    const int32_t off = l - s;
+    while (next < off) {
+      ++k;
+      next = k < nmd ? (int32_t)(ev[k] >> 8) : INT32_MAX;
     }
-    auto term_at = [&](int q8, int32_t l, int64_t p) {  // element at locus l, base / quality at pool offset p
-      const int32_t off = l - s;
-      while (k < nmd && (int32_t)(ev[k] >> 8) < off) ++k;
-      const bool event = k < nmd && (int32_t)(ev[k] >> 8) == off;
-      const int q = (int)(int8_t)R.qual[p];
-      const uint32_t t = q < 0 ? kMargin8None : tm[(q << 1) | (event ? 0 : 1)];
-      v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
-    };
-    if (d.info & kColEligible) {
-      const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+    return qv < 0 ? (uint32_t)kMargin8None : (uint32_t)tm[(qv << 1) | (next == off ? 0 : 1)];
+  };
+  auto has_zero = [](uint32_t x) { return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
+  bool none = false;
+  if (d.info & kColEligible) {
+    const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
+    for (int32_t w = 0; w < sl; ++w) {
+      const int32_t lb = 8 * (s0 + w);
+      uint32_t v[2] = {0x80808080u, 0x80808080u};
+      if (lb >= s && lb + 8 <= e) {
+        const uint64_t qb = *reinterpret_cast<const gq_u64m *>(R.qual + p0 + lb);
 #pragma unroll
-      for (int q8 = 0; q8 < 8; ++q8) {
-        const int32_t l = lb + q8;
-        if (l >= s && l < d.end) term_at(q8, l, p0 + l);
+        for (int q8 = 0; q8 < 8; ++q8) {
+          const uint32_t t = term(lb + q8, (int)(int8_t)(uint8_t)(qb >> (8 * q8)));
+          v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
+        }
+      } else {
+        for (int q8 = 0; q8 < 8; ++q8) {
+          const int32_t l = lb + q8;
+          if (l < s || l >= e) continue;
+          const uint32_t t = term(l, (int)(int8_t)R.qual[p0 + l]);
+          v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
+        }
       }
-    } else {  // general CIGAR: the count segments
-      const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
-      const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-      const int64_t so = R.seq_off[r];
+      out[w] = make_uint2(v[0], v[1]);
+      none = none || has_zero(v[0]) || has_zero(v[1]);
+    }
+  } else {  // general CIGAR: the count segments
+    const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+    const int64_t so = R.seq_off[r];
+    for (int32_t w = 0; w < sl; ++w) {
+      const int32_t lb = 8 * (s0 + w);
+      uint32_t v[2] = {0x80808080u, 0x80808080u};
       for (int q8 = 0; q8 < 8; ++q8) {
         const int32_t l = lb + q8;
         for (int32_t q2 = 0; q2 < nseg; ++q2) {
           const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
           const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
           if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
-            term_at(q8, l, so + (int32_t)(b & 0xFFFFu) + (l - ra));
+            const uint32_t t = term(l, (int)(int8_t)R.qual[so + (int32_t)(b & 0xFFFFu) + (l - ra)]);
+            v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
             break;
           }
         }
       }
+      out[w] = make_uint2(v[0], v[1]);
+      none = none || has_zero(v[0]) || has_zero(v[1]);
     }
   }
-  return make_uint2(v[0], v[1]);
+  return none;
 }
 
 // The margin projection of the tumor reads, laid out as `proj` (a byte per projection nibble:
-// word w of the row pool at mproj + 8 w), one wave per slice (the rows row_count assigned,
-// stored); mnb marks slices holding a kMargin8None term.
+// word w of the row pool at mproj + 8 w), one wave per slice, a lane per piece (the rows
+// row_count assigned, stored); mnb marks slices holding a kMargin8None term.
 __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
                                                   const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
                                                   uint8_t *__restrict__ mnb) {
@@ -117,15 +148,9 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     if (R.pbad[slot]) continue;  // uniform
     const int64_t base = 16 * R.srow[slot];  // words
     bool none = false;
-    slice_words(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](bool act, int64_t r, int32_t col, int32_t row) {
-      if (act) {
-        const uint2 w = margin_word(R, r, col, min_mapq, tab);
-        *reinterpret_cast<uint2 *>(mproj + 8 * (base + 16 * (int64_t)row + (col & 15))) = w;
-        auto has = [](uint32_t x) {  // a zero byte
-          return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
-        };
-        none = none || has(w.x) || has(w.y);
-      }
+    slice_pieces(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](int64_t r, int32_t s0, int32_t sl, int32_t row) {
+      none = margin_piece(R, r, s0, sl, min_mapq, tab,
+                          reinterpret_cast<uint2 *>(mproj) + base + 16 * (int64_t)row + (s0 & 15)) || none;
     });
     const bool any = __ballot(none) != 0;
     if ((threadIdx.x & 63) == 0) mnb[slot] = any ? 1 : 0;

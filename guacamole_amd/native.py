@@ -95,7 +95,8 @@ class gq_timings(C.Structure):
                 ("finalize_ms", C.c_float), ("total_ms", C.c_float), ("pileup_launches", C.c_int64),
                 ("tiles", C.c_int64), ("host_ms", C.c_float), ("marshal_ms", C.c_float),
                 ("walk_ms", C.c_float), ("walk_tiles", C.c_int64), ("order_loci", C.c_int64),
-                ("deep_loci", C.c_int64), ("deep_max", C.c_int64), ("call_ms", C.c_float), ("deep_ms", C.c_float)]
+                ("deep_loci", C.c_int64), ("deep_max", C.c_int64), ("call_ms", C.c_float), ("deep_ms", C.c_float),
+                ("front_ms", C.c_float)]
 
 
 class gq_reads_info(C.Structure):

@@ -183,6 +183,8 @@ typedef struct {
   int64_t deep_max;    /* somatic: deepest per-sample pileup among them                     */
   float call_ms;       /* somatic: the fast exact-caller kernel alone (inside complex_ms)    */
   float deep_ms;       /* somatic: the deep caller launches (inside complex_ms)              */
+  float front_ms;      /* somatic: the split caller's front kernel (covers + element records, */
+                       /* inside call_ms)                                                     */
 } gq_timings;
 
 const char *gq_version(void);
