@@ -357,8 +357,8 @@ def single_pass(g, visited: int):
         t = time.perf_counter()
         g.write_bam(bam)
         write_s = time.perf_counter() - t
-        env = dict(os.environ, GQ_TIMING="1", PYTHONPATH=ROOT)
         cmd = [sys.executable, "-m", "guacamole_amd", "germline-threshold", "--reads", bam, "--out", out]
+        env = dict(os.environ, GQ_TIMING="1", PYTHONPATH=ROOT, GQ_T_SPAWN=repr(time.time()))
         t = time.perf_counter()
         r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
         wall = time.perf_counter() - t
@@ -368,6 +368,8 @@ def single_pass(g, visited: int):
         for ln in r.stderr.splitlines():
             if ln.startswith("GQ_TIMING "):
                 stages = json.loads(ln[len("GQ_TIMING "):])
+        if "report_at_s" in stages:  # after the report: closing the output, releasing HBM, exit
+            stages["exit_s"] = wall - stages["report_at_s"]
         return {"wall_s": wall, "loci_per_s": visited / wall, "bam_bytes": os.path.getsize(bam),
                 "bam_write_s": write_s, "stages_s": stages,
                 "command": "python -m guacamole_amd germline-threshold --reads <shard>.bam --out <out>.vcf"}
@@ -395,9 +397,9 @@ def somatic_single_pass(args, L: int = CHR20):
         for path, depth, tumor, rseed in ((paths[0], 60.0, True, 11), (paths[1], 30.0, False, 12)):
             synthetic.generate(L, depth, seed=seed, somatic_rate=2e-4, tumor=tumor, read_seed=rseed).write_bam(path)
         write_s = time.perf_counter() - t
-        env = dict(os.environ, GQ_TIMING="1", PYTHONPATH=ROOT)
         cmd = [sys.executable, "-m", "guacamole_amd", "somatic-standard", "--tumor-reads", paths[0], "--normal-reads",
                paths[1], "--out", out]
+        env = dict(os.environ, GQ_TIMING="1", PYTHONPATH=ROOT, GQ_T_SPAWN=repr(time.time()))
         t = time.perf_counter()
         r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
         wall = time.perf_counter() - t
@@ -407,6 +409,8 @@ def somatic_single_pass(args, L: int = CHR20):
         for ln in r.stderr.splitlines():
             if ln.startswith("GQ_TIMING "):
                 stages = json.loads(ln[len("GQ_TIMING "):])
+        if "report_at_s" in stages:
+            stages["exit_s"] = wall - stages["report_at_s"]
         visited = int(stages.get("visited_loci", 0))
         return {"wall_s": wall, "loci_per_s": visited / wall if visited else None, "visited_loci": visited,
                 "bam_bytes": [os.path.getsize(p) for p in paths], "bam_write_s": write_s, "stages_s": stages,

@@ -57,6 +57,15 @@ class StageClock:
         self.t = time.perf_counter
         self.t0 = self.last = self.t()
         self.stages: Dict[str, float] = {}
+        # GQ_T_SPAWN (the launcher's time.time() at spawn): interpreter start + imports before the
+        # command, and when the report is written (the rest of the launcher's wall time is exit)
+        self.spawn = float(os.environ.get("GQ_T_SPAWN", "0") or 0)
+        if self.spawn:
+            self.stages["startup_s"] = time.time() - self.spawn
+
+    def note(self, name: str, seconds: float) -> None:
+        """A timed sub-step (inside some stage), reported beside the stages."""
+        self.stages[name] = self.stages.get(name, 0.0) + seconds
 
     def mark(self, name: str) -> None:
         now = self.t()
@@ -65,7 +74,9 @@ class StageClock:
 
     def report(self, **extra) -> None:
         if self.on:
-            print("GQ_TIMING " + json.dumps(dict(self.stages, total_s=self.t() - self.t0, **extra)), file=sys.stderr)
+            import time
+            at = {"report_at_s": time.time() - self.spawn} if self.spawn else {}
+            print("GQ_TIMING " + json.dumps(dict(self.stages, total_s=self.t() - self.t0, **at, **extra)), file=sys.stderr)
 
 
 def task_count(parallelism: int, world: int = 1) -> int:
@@ -242,7 +253,9 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     if device_ingest(args, args.reads):
         if world == 1:
             maps = map_bams([args.reads])  # the file mapped on a host thread while the context starts
+            t = clock.t()
             ctx = native.Context(args.device)
+            clock.note("ctx_open_s", clock.t() - t)
             rs = load_reads_device(ctx, args.reads, filters, maps["join"]()[args.reads])
         else:
             ctx = native.Context(local)
@@ -352,7 +365,9 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     if device_ingest(args, args.tumor_reads, args.normal_reads):
         if world == 1:
             maps = map_bams([args.tumor_reads, args.normal_reads])
+            t = clock.t()
             ctx = native.Context(args.device)
+            clock.note("ctx_open_s", clock.t() - t)
             mapped = maps["join"]()
             sets = [load_reads_device(ctx, path, f, mapped[path]) for path in (args.tumor_reads, args.normal_reads)]
         else:

@@ -355,22 +355,59 @@ __device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const Sl
   return __ballot(over) ? -1 : nrows;
 }
 
-// put(read, first column, columns, row) once per piece of the slice (a lane per read of each
-// 64-read batch, read order; lanes without a piece idle), rows from slice_assign_rows.
-template <class F>
-__device__ __forceinline__ void slice_pieces(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
-                                             F &&put) {
+// A piece of a 64-read batch, for the word-per-lane fills (slice_fill): set up once by the
+// piece's lane, read from LDS by the lanes of its words.
+struct PieceMeta {
+  int64_t p0;         // pool offset of locus 0: a column-eligible read's base / quality at locus l is p0 + l
+  int32_t s, e;       // the read's [start, end)
+  int32_t s0, row;    // the piece's first column and its row
+  uint32_t info, mq;  // ColDesc info, mapping quality
+  uint32_t ev[4];     // MD events at the piece's loci: bit i = locus 8 s0 + i (margin fill)
+};
+
+// word(read, meta, column, word index in the pool row) once per word of the slice's pieces, a
+// lane per word (a batch's words in piece order: consecutive words of a piece on consecutive
+// lanes, so the loads of a piece's bases and the stores of its row coalesce).  setup(read, meta)
+// runs once per piece on the piece's lane and returns false to drop it.  meta: this wave's 64
+// LDS entries.  Every lane of the wave calls word in uniform control flow (act: holds a word).
+template <class S, class F>
+__device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
+                                           PieceMeta *__restrict__ meta, S &&setup, F &&word) {
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
+    int32_t s0 = W.qc0, sl = 0;
     if (r < W.rz) {
       const uint16_t k = rows[r - W.ra];
       if (k != 0xFFFFu) {
-        int32_t s0 = W.qc0, sl = 0;
         slice_piece(R, r, W.qc0, s0, sl);
-        if (sl > 0) put(r, s0, sl, (int32_t)k);
+        if (sl > 0) {
+          PieceMeta m;
+          m.s0 = s0;
+          m.row = k;
+          if (setup(r, m)) meta[lane] = m;
+          else sl = 0;
+        }
       }
     }
+    const uint32_t len = (uint32_t)sl;
+    const uint32_t incl = wave_incl_scan(len), ex = incl - len;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
+      const uint32_t w = w0 + (uint32_t)lane;
+      int k = 0;  // the last lane whose words start at or before w
+#pragma unroll
+      for (int b = 32; b >= 1; b >>= 1)
+        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+      const uint32_t j = w - (uint32_t)__shfl((int)ex, k, 64);
+      const bool act = w < tot;
+      const PieceMeta &m = meta[act ? k : 0];  // (read in place: fields load from LDS as used)
+      word(act, r0 + k, m, m.s0 + (int32_t)j);
+    }
+    __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
 }
 

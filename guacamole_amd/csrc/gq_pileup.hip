@@ -431,62 +431,67 @@ __device__ __forceinline__ uint32_t proj_codes4(uint32_t x) {
 
 typedef uint64_t gq_u64u __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
 
-// The projection words of read r's piece [s0, s0 + sl) of its slice, written at `out` (the
-// piece's row, word s0 & 15 first).  Word col: byte j = code of locus 8 col + j | code of locus
-// 8 col + j + 4 << 4 (4-bit codes, proj_code).  A lane per piece: the read's descriptor once,
-// then eight bases per 8-byte load for the words inside the read.
-__device__ void proj_piece(const DevReads &R, int64_t r, int32_t s0, int32_t sl, uint32_t *__restrict__ out) {
-  const ColDesc d = R.cdesc[r];
-  const int32_t s = d.start, e = d.end;
-  if (d.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base seq_lo + (l - s)
-    const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
-    for (int32_t w = 0; w < sl; ++w) {
-      const int32_t lb = 8 * (s0 + w);
-      uint64_t b;
-      if (lb >= s && lb + 8 <= e) {
-        b = *reinterpret_cast<const gq_u64u *>(R.seq + p0 + lb);
-      } else {
-        b = 0;
-        for (int q = 0; q < 8; ++q) {
-          const int32_t l = lb + q;
-          if (l >= s && l < e) b |= (uint64_t)R.seq[p0 + l] << (8 * q);
-        }
+// The projection word of read r at column col (loci [8 col, 8 col + 8)): byte j = code of locus
+// 8 col + j | code of locus 8 col + j + 4 << 4 (4-bit codes, proj_code).  m: the read's piece
+// (slice_fill); inside a column-eligible read, eight bases in one 8-byte load.
+__device__ __forceinline__ uint32_t proj_word(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col) {
+  const int32_t s = m.s, e = m.e;
+  const int32_t lb = 8 * col;  // locus of byte 0
+  if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
+    uint64_t b;
+    if (lb >= s && lb + 8 <= e) {
+      b = *reinterpret_cast<const gq_u64u *>(R.seq + m.p0 + lb);
+    } else {
+      b = 0;
+      for (int q = 0; q < 8; ++q) {
+        const int32_t l = lb + q;
+        if (l >= s && l < e) b |= (uint64_t)R.seq[m.p0 + l] << (8 * q);
       }
-      out[w] = proj_codes4((uint32_t)b) | (proj_codes4((uint32_t)(b >> 32)) << 4);
     }
-  } else {  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
-    const int32_t nmd = (int32_t)(d.info & 0xFFFFu), nseg = (int32_t)((d.info >> 18) & 0xFFu);
-    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-    const int64_t so = R.seq_off[r];
-    for (int32_t w = 0; w < sl; ++w) {
-      const int32_t lb = 8 * (s0 + w);
-      uint32_t v[2] = {0, 0};
-      for (int32_t q2 = 0; q2 < nseg; ++q2) {
-        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-        if ((b >> 16) != kSegCount) continue;
-        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
-        if (ra >= lb + 8 || ra + rl <= lb) continue;
-        for (int q = 0; q < 8; ++q) {
-          const int32_t l = lb + q;
-          if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
-        }
-      }
-      out[w] = v[0] | (v[1] << 4);
+    return proj_codes4((uint32_t)b) | (proj_codes4((uint32_t)(b >> 32)) << 4);
+  }
+  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
+  const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
+  const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+  const int64_t so = R.seq_off[r];
+  uint32_t v[2] = {0, 0};
+  for (int32_t q2 = 0; q2 < nseg; ++q2) {
+    const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+    if ((b >> 16) != kSegCount) continue;
+    const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
+    if (ra >= lb + 8 || ra + rl <= lb) continue;
+    for (int q = 0; q < 8; ++q) {
+      const int32_t l = lb + q;
+      if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
     }
   }
+  return v[0] | (v[1] << 4);
 }
 
-// The projection pool in block rows, one wave per slice, a lane per piece (the rows row_count
+// The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
 // assigned, stored; pbad slices stay zero: their blocks go to the walker).
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
+  __shared__ PieceMeta s_meta[4][64];
+  PieceMeta *meta = s_meta[threadIdx.x >> 6];
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
-    const int64_t base = 16 * R.srow[slot];  // words
-    slice_pieces(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](int64_t r, int32_t s0, int32_t sl, int32_t row) {
-      proj_piece(R, r, s0, sl, reinterpret_cast<uint32_t *>(proj) + base + 16 * (int64_t)row + (s0 & 15));
-    });
+    uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * R.srow[slot];  // the slice's block rows
+    slice_fill(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta,
+        [&](int64_t r, PieceMeta &m) {
+          const ColDesc d = R.cdesc[r];
+          m.s = d.start;
+          m.e = d.end;
+          m.info = d.info;
+          m.mq = 0;
+          m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
+          return true;
+        },
+        [&](bool act, int64_t r, const PieceMeta &m, int32_t col) {
+          if (act) out[16 * (int64_t)m.row + (col & 15)] = proj_word(R, r, m, col);
+        });
   }
 }
 

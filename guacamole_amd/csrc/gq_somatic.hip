@@ -1616,7 +1616,10 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   unsigned long long rec_cap = 1 << 16, pool_cap = 1 << 20, amb_cap = 4096, deep_cap = 4096;
   Counters hc{};
   float call_ms = 0, deep_ms = 0, front_ms = 0;
-  static const bool split = !getenv("GQ_CALL_SPLIT") || atoi(getenv("GQ_CALL_SPLIT")) != 0;  // A/B: 0 = one kernel
+  // GQ_CALL_SPLIT=1: the split caller (somatic_front + the back end over stored records).  Measured
+  // slower at chr1 60x/30x (front 3.9 ms + back 5.5 ms against 8.6 ms for the one kernel,
+  // profiles/r04_a5_kernel_stats.csv), so the one kernel is the default.
+  static const bool split = getenv("GQ_CALL_SPLIT") && atoi(getenv("GQ_CALL_SPLIT")) != 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));

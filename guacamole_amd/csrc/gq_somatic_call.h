@@ -1023,10 +1023,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   }
 }
 
-// The split caller's front (GQ_CALL_SPLIT, default on): covers and element records of the
-// candidates [es.b0, es.b1) into the element store, one wave per candidate.  It holds only the
-// front's registers, so more waves per SIMD hide its dependent loads than in the one-kernel
-// caller, whose FP64 back end sets the register budget.
+// The split caller's front (GQ_CALL_SPLIT=1; off by default, see gq_somatic_standard): covers
+// and element records of the candidates [es.b0, es.b1) into the element store, one wave per
+// candidate.  It holds only the front's registers (4 waves per SIMD against the one kernel's 3);
+// measured, that did not pay for the store's traffic and the second pass over the candidates.
 #ifndef GQ_FRONT_WPE
 #define GQ_FRONT_WPE 4
 #endif

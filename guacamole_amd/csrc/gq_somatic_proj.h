@@ -52,106 +52,119 @@ __global__ void margin_table(int incl_align, uint8_t *__restrict__ tab) {
 
 typedef uint64_t gq_u64m __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
 
-// The margin words of tumor read r's piece [s0, s0 + sl) of its slice (8 loci per word, a byte
-// each; hom_ref_margin_lane's terms) at `out` (the piece's row, word s0 & 15 first), a lane per
-// piece.  Reads the mapq filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:
-// 25-36) and non-Match/Mismatch loci keep the pool's kMargin8Zero fill (nothing is written for a
-// dropped read).  The read's MD events are walked once across the piece (a cursor from one
-// search); qualities come eight per 8-byte load inside the read.  Returns whether a word holds a
-// kMargin8None term.
-__device__ bool margin_piece(const DevReads &R, int64_t r, int32_t s0, int32_t sl, int min_mapq,
-                             const uint8_t *__restrict__ tab, uint2 *__restrict__ out) {
+// Piece setup of the margin fill: the read's descriptor and its MD events at the piece's loci as
+// a bit mask (MD offsets are reference offsets from the read's start, sorted).  Reads the mapq
+// filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:25-36) are skipped: their
+// loci keep the pool's kMargin8Zero fill.
+__device__ __forceinline__ bool margin_setup(const DevReads &R, int64_t r, int min_mapq, PieceMeta &m) {
   const int mq = (int)R.mapq[r];
   if (min_mapq > 0 && mq < min_mapq) return false;
   const ColDesc d = R.cdesc[r];
-  const int32_t s = d.start, e = d.end;
-  const uint8_t *tm = tab + (mq << 8);
+  m.s = d.start;
+  m.e = d.end;
+  m.info = d.info;
+  m.mq = (uint32_t)mq;
+  m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
   const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
   const uint32_t *ev = R.md_ev + R.md_off[r];
-  // the first MD event at or past the piece's first locus (sorted offsets)
-  int k = 0, hi2 = nmd;
-  const int32_t off0 = 8 * s0 - s;
-  while (k < hi2) {
-    const int m = (k + hi2) >> 1;
-    if ((int32_t)(ev[m] >> 8) < off0) k = m + 1;
-    else hi2 = m;
+  const int32_t o0 = 8 * m.s0 - d.start;  // offset of the piece's first locus
+  int k = 0, hi = nmd;
+  while (k < hi) {
+    const int mid = (k + hi) >> 1;
+    if ((int32_t)(ev[mid] >> 8) < o0) k = mid + 1;
+    else hi = mid;
   }
-  int32_t next = k < nmd ? (int32_t)(ev[k] >> 8) : INT32_MAX;  // offset of the cursor's event
-  auto term = [&](int32_t l, int qv) -> uint32_t {  // the element at locus l with quality qv
-    const int32_t off = l - s;
-    while (next < off) {
-      ++k;
-      next = k < nmd ? (int32_t)(ev[k] >> 8) : INT32_MAX;
-    }
-    return qv < 0 ? (uint32_t)kMargin8None : (uint32_t)tm[(qv << 1) | (next == off ? 0 : 1)];
+  uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // (registers: a dynamic index would go to scratch)
+  for (; k < nmd; ++k) {
+    const int32_t i = (int32_t)(ev[k] >> 8) - o0;
+    if (i >= 128) break;
+    const uint32_t bit = 1u << (i & 31);
+    e0 |= (i >> 5) == 0 ? bit : 0u;
+    e1 |= (i >> 5) == 1 ? bit : 0u;
+    e2 |= (i >> 5) == 2 ? bit : 0u;
+    e3 |= (i >> 5) == 3 ? bit : 0u;
+  }
+  m.ev[0] = e0;
+  m.ev[1] = e1;
+  m.ev[2] = e2;
+  m.ev[3] = e3;
+  return true;
+}
+
+// The margin word (8 loci, a byte each; hom_ref_margin_lane's terms in 1/8 units, biased) of read
+// r at column col, from its piece m.  Loci outside the read's Match/Mismatch blocks hold
+// kMargin8Zero; inside a column-eligible read, eight qualities in one 8-byte load.
+__device__ __forceinline__ uint2 margin_word(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col,
+                                             const uint8_t *__restrict__ tab) {
+  const int32_t s = m.s, e = m.e;
+  const int32_t lb = 8 * col;
+  const uint8_t *tm = tab + (m.mq << 8);
+  const int32_t i0 = 8 * (col - m.s0);                        // bit of locus lb in m.ev
+  const uint32_t evb = (m.ev[i0 >> 5] >> (i0 & 31)) & 0xFFu;  // events at loci lb .. lb + 7 (m: in LDS)
+  uint32_t v[2] = {0x80808080u, 0x80808080u};
+  auto put = [&](int q8, int qv) {
+    const uint32_t t = qv < 0 ? (uint32_t)kMargin8None : (uint32_t)tm[(qv << 1) | ((evb >> q8) & 1u ? 0 : 1)];
+    v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
   };
-  auto has_zero = [](uint32_t x) { return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
-  bool none = false;
-  if (d.info & kColEligible) {
-    const int64_t p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - s;
-    for (int32_t w = 0; w < sl; ++w) {
-      const int32_t lb = 8 * (s0 + w);
-      uint32_t v[2] = {0x80808080u, 0x80808080u};
-      if (lb >= s && lb + 8 <= e) {
-        const uint64_t qb = *reinterpret_cast<const gq_u64m *>(R.qual + p0 + lb);
+  if (m.info & kColEligible) {
+    if (lb >= s && lb + 8 <= e) {
+      const uint64_t qb = *reinterpret_cast<const gq_u64m *>(R.qual + m.p0 + lb);
 #pragma unroll
-        for (int q8 = 0; q8 < 8; ++q8) {
-          const uint32_t t = term(lb + q8, (int)(int8_t)(uint8_t)(qb >> (8 * q8)));
-          v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
-        }
-      } else {
-        for (int q8 = 0; q8 < 8; ++q8) {
-          const int32_t l = lb + q8;
-          if (l < s || l >= e) continue;
-          const uint32_t t = term(l, (int)(int8_t)R.qual[p0 + l]);
-          v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
-        }
-      }
-      out[w] = make_uint2(v[0], v[1]);
-      none = none || has_zero(v[0]) || has_zero(v[1]);
-    }
-  } else {  // general CIGAR: the count segments
-    const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
-    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-    const int64_t so = R.seq_off[r];
-    for (int32_t w = 0; w < sl; ++w) {
-      const int32_t lb = 8 * (s0 + w);
-      uint32_t v[2] = {0x80808080u, 0x80808080u};
+      for (int q8 = 0; q8 < 8; ++q8) put(q8, (int)(int8_t)(uint8_t)(qb >> (8 * q8)));
+    } else {
+#pragma unroll
       for (int q8 = 0; q8 < 8; ++q8) {
         const int32_t l = lb + q8;
-        for (int32_t q2 = 0; q2 < nseg; ++q2) {
-          const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-          const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
-          if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
-            const uint32_t t = term(l, (int)(int8_t)R.qual[so + (int32_t)(b & 0xFFFFu) + (l - ra)]);
-            v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
-            break;
-          }
+        if (l >= s && l < e) put(q8, (int)(int8_t)R.qual[m.p0 + l]);
+      }
+    }
+  } else {  // general CIGAR: the count segments
+    const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
+    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+    const int64_t so = R.seq_off[r];
+#pragma unroll
+    for (int q8 = 0; q8 < 8; ++q8) {
+      const int32_t l = lb + q8;
+      for (int32_t q2 = 0; q2 < nseg; ++q2) {
+        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
+        if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
+          put(q8, (int)(int8_t)R.qual[so + (int32_t)(b & 0xFFFFu) + (l - ra)]);
+          break;
         }
       }
-      out[w] = make_uint2(v[0], v[1]);
-      none = none || has_zero(v[0]) || has_zero(v[1]);
     }
   }
-  return none;
+  return make_uint2(v[0], v[1]);
 }
 
 // The margin projection of the tumor reads, laid out as `proj` (a byte per projection nibble:
-// word w of the row pool at mproj + 8 w), one wave per slice, a lane per piece (the rows
-// row_count assigned, stored); mnb marks slices holding a kMargin8None term.
+// word w of the row pool at mproj + 8 w), one wave per slice, a lane per word (the rows row_count
+// assigned, stored); mnb marks slices holding a kMargin8None term.
 __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
                                                   const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
                                                   uint8_t *__restrict__ mnb) {
+  __shared__ PieceMeta s_meta[4][64];
+  PieceMeta *meta = s_meta[threadIdx.x >> 6];
   const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
-    const int64_t base = 16 * R.srow[slot];  // words
+    uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * R.srow[slot];  // the slice's block rows
     bool none = false;
-    slice_pieces(R, slice_stored(R, slot), R.prow + R.soff[slot], [&](int64_t r, int32_t s0, int32_t sl, int32_t row) {
-      none = margin_piece(R, r, s0, sl, min_mapq, tab,
-                          reinterpret_cast<uint2 *>(mproj) + base + 16 * (int64_t)row + (s0 & 15)) || none;
-    });
+    slice_fill(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta,
+        [&](int64_t r, PieceMeta &m) { return margin_setup(R, r, min_mapq, m); },
+        [&](bool act, int64_t r, const PieceMeta &m, int32_t col) {
+          if (act) {
+            const uint2 w = margin_word(R, r, m, col, tab);
+            out[16 * (int64_t)m.row + (col & 15)] = w;
+            auto has = [](uint32_t x) {  // a zero byte
+              return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
+            };
+            none = none || has(w.x) || has(w.y);
+          }
+        });
     const bool any = __ballot(none) != 0;
     if ((threadIdx.x & 63) == 0) mnb[slot] = any ? 1 : 0;
   }
