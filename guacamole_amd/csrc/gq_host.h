@@ -591,8 +591,10 @@ struct H2DStager {
     }
     for (auto &x : th) x.join();
   }
-  template <class F>
-  hipError_t copy_from(void *dst, size_t bytes, const F &src_range) {
+  // landed(end): called after each chunk's copy is enqueued on the stream (bytes [0, end) are
+  // then in order on it), e.g. to start work on another stream behind an event
+  template <class F, class G>
+  hipError_t copy_from(void *dst, size_t bytes, const F &src_range, const G &landed) {
     for (size_t o = 0; o < bytes; o += kChunk) {
       const size_t k = std::min(kChunk, bytes - o);
       if (used[slot]) {
@@ -605,8 +607,14 @@ struct H2DStager {
       if (e != hipSuccess) return e;
       used[slot] = true;
       slot ^= 1;
+      e = landed(o + k);
+      if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  }
+  template <class F>
+  hipError_t copy_from(void *dst, size_t bytes, const F &src_range) {
+    return copy_from(dst, bytes, src_range, [](size_t) { return hipSuccess; });
   }
   hipError_t copy(void *dst, const void *src, size_t bytes) {
     return copy_from(dst, bytes, [src](uint8_t *out, size_t o, size_t k) { memcpy(out, (const uint8_t *)src + o, k); });
