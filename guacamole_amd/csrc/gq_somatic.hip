@@ -1620,6 +1620,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   // slower at chr1 60x/30x (front 3.9 ms + back 5.5 ms against 8.6 ms for the one kernel,
   // profiles/r04_a5_kernel_stats.csv), so the one kernel is the default.
   static const bool split = getenv("GQ_CALL_SPLIT") && atoi(getenv("GQ_CALL_SPLIT")) != 0;
+  // GQ_CALL_WPE=2: the one-kernel caller built for 2 waves per SIMD (no spills) instead of 3
+  static const bool wpe2 = getenv("GQ_CALL_WPE") && atoi(getenv("GQ_CALL_WPE")) == 2;
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(c->amb.ensure(amb_cap * sizeof(AmbItem)));
     HIP_TRY(c->cplx.ensure(og.total(1) * sizeof(ComplexItem)));
@@ -1672,7 +1674,10 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     // many generations leaves a tail of idle SIMDs behind the last ones)
     if (c->call_wg_per_cu <= 0) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_call_k<false, true>, kBlock, 0) != hipSuccess ||
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, split ? (const void *)somatic_call_k<false, true>
+                                                             : wpe2 ? (const void *)somatic_call_k<false, false, 2>
+                                                                    : (const void *)somatic_call_k<false, false, 3>,
+                                                       kBlock, 0) != hipSuccess ||
           nb <= 0)
         nb = 3;
       c->call_wg_per_cu = nb;
@@ -1683,7 +1688,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     const DeepIO dio{(int64_t *)c->deep_list.p, deep_cap, 0, nullptr, 0, 0};
     front_ms = 0;
     if (!split) {
-      hipLaunchKernelGGL((somatic_call_k<false, false>), dim3(cblocks), dim3(kBlock), 0, c->stream,
+      auto k1 = wpe2 ? somatic_call_k<false, false, 2> : somatic_call_k<false, false, 3>;
+      hipLaunchKernelGGL(k1, dim3(cblocks), dim3(kBlock), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)c->amb.p,
                          amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, rv, dbg, dio,

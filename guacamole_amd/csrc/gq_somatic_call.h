@@ -39,13 +39,12 @@ struct CallMem {
   int16_t *order;   // [64 kSlots]
   uint8_t *is_var;  // [64 kSlots]
   double *ll;       // [maxG]
-  double *terms;    // [3 cap] per element: log(2(1 - pc)), log(pc + (1 - pc)), log(2 pc) (0 when filtered out)
   int cap, maxG;
 };
 
 // Deep-kernel scratch geometry: bytes per wave for `cap` elements per sample.
 __host__ __device__ __forceinline__ size_t deep_wave_bytes(int cap, int maxG) {
-  return (size_t)cap * (2 * 4 + 2 * 16 + 2 * 4 + 3 * 8) + 64 * kSlots * 3 + (size_t)maxG * 8 + 64;
+  return (size_t)cap * (2 * 4 + 2 * 16 + 2 * 4) + 64 * kSlots * 3 + (size_t)maxG * 8 + 64;
 }
 __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   CallMem m;
@@ -56,8 +55,6 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   p += (size_t)cap * 16;
   m.ll = (double *)p;
   p += (size_t)maxG * 8;
-  m.terms = (double *)p;
-  p += (size_t)cap * 24;
   m.cov[0] = (int32_t *)p;
   p += (size_t)cap * 4;
   m.cov[1] = (int32_t *)p;
@@ -228,43 +225,43 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
     return res;
   }
   const double ln2d = sm::log(2.0) * (double)P.depth_f;
-  // the three possible log terms of each element (lanes = elements), 0 for an element the
-  // mapq filter drops: starting the fold at +0.0 and adding 0.0 for those is bit-identical
-  // to Colt's fold over the filtered elements (no term is -0.0)
-  for (int c0 = 0; c0 < n_el; c0 += 64) {
-    const int k = c0 + lane;
-    if (k >= n_el) continue;
-    const uint4 e = el[k];
-    const uint32_t fl = el_flags(e);
-    double t2 = 0.0, th = 0.0, t0 = 0.0;
-    if ((fl & kElAct) && (fl & kElPass)) {
-      const int q = el_q(e);
-      if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
-      double pc = phred_success(q);
-      if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
-      const double pw = 1.0 - pc;
-      t2 = sm::log(pc + pc);
-      th = sm::log(pc + pw);
-      t0 = sm::log(pw + pw);
-    }
-    m.terms[3 * k] = t0;
-    m.terms[3 * k + 1] = th;
-    m.terms[3 * k + 2] = t2;
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element
+  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element.  The elements
+  // go by 64-element chunks, last chunk first: lane k of a chunk computes its element's three
+  // possible log terms (0 for an element the mapq filter drops: starting the fold at +0.0 and
+  // adding 0.0 for those is bit-identical to Colt's fold over the filtered elements, no term is
+  // -0.0), and the genotype lanes take them by readlane, element by element in descending order
+  // (no LDS round trip on the fold's dependence chain).
   for (int g0 = 0; g0 < G; g0 += 64) {
     const int g = g0 + lane;
     int i = 0, j = 0;
     if (g < G) genotype_index(g, n, i, j);
     const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
     double agg = 0.0;
-#pragma unroll 4
-    for (int k = n_el - 1; k >= 0; --k) {
-      const int tj = el_tidx(el[k]);
-      const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
-      agg = agg + m.terms[3 * k + sel];
+    for (int c0 = ((n_el - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {
+      const int k = c0 + lane;
+      int tjl = -1;
+      double t2 = 0.0, th = 0.0, t0 = 0.0;
+      if (k < n_el) {
+        const uint4 e = el[k];
+        const uint32_t fl = el_flags(e);
+        tjl = el_tidx(e);
+        if ((fl & kElAct) && (fl & kElPass)) {
+          const int q = el_q(e);
+          if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
+          double pc = phred_success(q);
+          if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
+          const double pw = 1.0 - pc;
+          t2 = sm::log(pc + pc);
+          th = sm::log(pc + pw);
+          t0 = sm::log(pw + pw);
+        }
+      }
+      for (int kk = min(63, n_el - 1 - c0); kk >= 0; --kk) {
+        const int tj = __builtin_amdgcn_readlane(tjl, kk);
+        const double a0 = lane_f64(t0, kk), ah = lane_f64(th, kk), a2 = lane_f64(t2, kk);
+        const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
+        agg = agg + (sel == 0 ? a0 : sel == 1 ? ah : a2);
+      }
     }
     if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
   }
@@ -680,11 +677,10 @@ struct ElemStore {
   int64_t b0, b1;
 };
 
-#ifndef GQ_CALL_WPE2
-#define GQ_CALL_WPE2 3  // fast kernel: waves per SIMD the register budget must allow (4: 69 VGPRs spilled)
-#endif
-template <bool DEEP, bool BACK = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : GQ_CALL_WPE2))) void somatic_call_k(
+// WPE: waves per SIMD the fast kernel's register budget must allow (3: 168 VGPRs and some
+// spills; 2: no spills; GQ_CALL_WPE picks, see gq_somatic_standard).  The deep kernel: 2.
+template <bool DEEP, bool BACK = false, int WPE = 3>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : WPE))) void somatic_call_k(
     const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
     DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs, unsigned long long rec_cap,
     uint8_t *__restrict__ pool, unsigned long long pool_cap, OutGeom og, Counters *ctr, SomWin sw,
@@ -703,7 +699,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   __shared__ int16_t s_order[DEEP ? 1 : FW][64 * NS];
   __shared__ uint8_t s_var[DEEP ? 1 : FW][64 * NS];
   __shared__ double s_ll[DEEP ? 1 : FW][kMaxG];
-  __shared__ double s_terms[DEEP ? 1 : FW][3 * kFastCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -719,7 +714,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.order = s_order[wv];
     m.is_var = s_var[wv];
     m.ll = s_ll[wv];
-    m.terms = s_terms[wv];
     m.cap = kFastCap;
     m.maxG = kMaxG;
   }
