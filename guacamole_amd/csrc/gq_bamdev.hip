@@ -1421,99 +1421,45 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
     }
   } join{alloc};
   // the file (or its segments) -> HBM (pinned chunks filled by host threads while the DMA drains
-  // the other), and the inflate started behind it: the blocks whose bytes have landed go to
-  // bgzf_inflate + bgzf_crc on one of kParts streams as each quarter of the blocks lands (one
-  // lane decodes a whole block, so a launch lasts about one block's decode whatever its size, and
-  // launches on separate streams run side by side)
+  // the other), then the inflate of every block at once.  (Launching each quarter of the blocks
+  // on its own stream as its bytes landed measured slower: a launch lasts about one block's
+  // decode whatever its size, and the extra streams cost their creation.)
   HIP_TRY(b->comp.ensure((size_t)n + 64));
   HIP_TRY(hipMemsetAsync((uint8_t *)b->comp.p + n, 0, 64, c->stream));
   HIP_TRY(b->blk.ensure(sizeof(BgzfBlock) * (size_t)std::max<int64_t>(nb, 1)));
   if (nb)
     HIP_TRY(hipMemcpyAsync(b->blk.p, b->sel.data(), sizeof(BgzfBlock) * (size_t)nb, hipMemcpyHostToDevice, c->stream));
-  constexpr int kParts = 4;
-  struct PartStreams {
-    hipStream_t s[kParts] = {};
-    hipEvent_t e[kParts] = {};
-    ~PartStreams() {
-      for (int i = 0; i < kParts; ++i) {
-        if (s[i]) {
-          (void)hipStreamSynchronize(s[i]);
-          (void)hipStreamDestroy(s[i]);
-        }
-        if (e[i]) (void)hipEventDestroy(e[i]);
-      }
-    }
-  } ps;
-  for (int i = 0; i < kParts; ++i) {
-    HIP_TRY(hipStreamCreateWithFlags(&ps.s[i], hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&ps.e[i], hipEventDisableTiming));
-  }
-  int64_t bnext = 0;  // blocks before it are launched
-  int part = 0;
-  bool allocated = false;
-  auto launch_upto = [&](int64_t bend) -> hipError_t {
-    if (bend <= bnext) return hipSuccess;
-    if (!allocated) {
-      alloc.join();
-      if (alloc_err != hipSuccess) return alloc_err;
-      allocated = true;
-    }
-    hipStream_t s = ps.s[part % kParts];
-    hipError_t e = hipEventRecord(ps.e[part % kParts], c->stream);  // the bytes so far are on the device
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, ps.e[part % kParts], 0);
-    if (e != hipSuccess) return e;
-    const int64_t k = bend - bnext;
-    hipLaunchKernelGGL(bgzf_inflate, dim3(grid(k, kInfLanes)), dim3(kInfLanes), 0, s, (const uint8_t *)b->comp.p,
-                       n + 64, (const BgzfBlock *)b->blk.p + bnext, k, (uint8_t *)b->out.p,
-                       (uint16_t *)b->scratch.p + bnext * (kScratchBytes / 2), (int *)b->status.p + bnext);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bgzf_crc, dim3(grid(k, 256)), dim3(256), 0, s, (const uint8_t *)b->out.p,
-                       (const BgzfBlock *)b->blk.p + bnext, k, (int *)b->status.p + bnext);
-    e = hipGetLastError();
-    bnext = bend;
-    ++part;
-    return e;
-  };
   {
-    H2DStager stager(c->stream);
+    H2DStager stager(c);
     HIP_TRY(stager.init());
     std::vector<int64_t> at(pieces.size() + 1, 0);  // logical offset of each piece
     for (size_t i = 0; i < pieces.size(); ++i) at[i + 1] = at[i] + pieces[i].second;
-    int64_t bland = 0;  // blocks before it have landed (their payload + the decoder's 64-byte lookahead)
-    HIP_TRY(stager.copy_from(
-        b->comp.p, (size_t)n,
-        [&](uint8_t *dst, size_t o, size_t k) {
-          size_t i = (size_t)(std::upper_bound(at.begin(), at.end(), (int64_t)o) - at.begin()) - 1;
-          while (k > 0) {
-            const size_t in_piece = (size_t)(at[i + 1] - (int64_t)o);
-            const size_t take = std::min(k, in_piece);
-            memcpy(dst, p + pieces[i].first + ((int64_t)o - at[i]), take);
-            dst += take;
-            o += take;
-            k -= take;
-            ++i;
-          }
-        },
-        [&](size_t end) -> hipError_t {
-          if ((int64_t)end >= n) return hipSuccess;  // the last part goes after the loop
-          while (bland < nb && b->sel[(size_t)bland].in_off + b->sel[(size_t)bland].in_len + 64 <= (int64_t)end) ++bland;
-          if (part < kParts - 1 && bland - bnext >= (nb + kParts - 1) / kParts) return launch_upto(bland);
-          return hipSuccess;
-        }));
+    HIP_TRY(stager.copy_from(b->comp.p, (size_t)n, [&](uint8_t *dst, size_t o, size_t k) {
+      size_t i = (size_t)(std::upper_bound(at.begin(), at.end(), (int64_t)o) - at.begin()) - 1;
+      while (k > 0) {
+        const size_t in_piece = (size_t)(at[i + 1] - (int64_t)o);
+        const size_t take = std::min(k, in_piece);
+        memcpy(dst, p + pieces[i].first + ((int64_t)o - at[i]), take);
+        dst += take;
+        o += take;
+        k -= take;
+        ++i;
+      }
+    }));
     z.h2d_ms = ms_since(t0);
     t0 = std::chrono::steady_clock::now();
-    HIP_TRY(launch_upto(nb));
-    if (!allocated) {
-      alloc.join();
-      HIP_TRY(alloc_err);
-    }
-    for (int i = 0; i < std::min(part, kParts); ++i) {  // the copy stream waits for every part
-      HIP_TRY(hipEventRecord(ps.e[i], ps.s[i]));
-      HIP_TRY(hipStreamWaitEvent(c->stream, ps.e[i], 0));
-    }
+    alloc.join();
+    HIP_TRY(alloc_err);
     HIP_TRY(hipMemsetAsync((uint8_t *)b->out.p + outn, 0, 64, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));  // (before the stager's pinned chunks go)
+    if (nb) {
+      hipLaunchKernelGGL(bgzf_inflate, dim3(grid(nb, kInfLanes)), dim3(kInfLanes), 0, c->stream,
+                         (const uint8_t *)b->comp.p, n + 64, (const BgzfBlock *)b->blk.p, nb, (uint8_t *)b->out.p,
+                         (uint16_t *)b->scratch.p, (int *)b->status.p);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(bgzf_crc, dim3(grid(nb, 256)), dim3(256), 0, c->stream, (const uint8_t *)b->out.p,
+                         (const BgzfBlock *)b->blk.p, nb, (int *)b->status.p);
+      HIP_TRY(hipGetLastError());
+    }
   }
   {
     DevBuf &status = b->status;
@@ -1978,3 +1924,11 @@ gq_status gq_reads_download(const gq_dev_reads *r, const gq_reads *dst) {
 }
 
 }  // extern "C"
+
+namespace {
+__global__ void warm_k() {}
+}  // namespace
+hipError_t gq::warm_bamdev(hipStream_t s) {
+  hipLaunchKernelGGL(warm_k, dim3(1), dim3(64), 0, s);
+  return hipGetLastError();
+}

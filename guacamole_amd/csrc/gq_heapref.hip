@@ -240,3 +240,11 @@ gq_status gq::reads_overlap(gq_ctx *c, const gq_dev_reads *set, int32_t contig,
     out[i] = (first[i] < ce && (int64_t)st[i] < ranges[i].second && ranges[i].first < ranges[i].second) ? 1 : 0;
   return GQ_OK;
 }
+
+namespace {
+__global__ void warm_k() {}
+}  // namespace
+hipError_t gq::warm_heapref(hipStream_t s) {
+  hipLaunchKernelGGL(warm_k, dim3(1), dim3(64), 0, s);
+  return hipGetLastError();
+}

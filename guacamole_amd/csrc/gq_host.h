@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <cstdarg>
 #include <cstdio>
@@ -504,9 +506,28 @@ struct gq_ctx {
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
   gq::DevBuf deep_list, deep_scratch;              // somatic: the deep caller's list and per-wave scratch
   int front_wg_per_cu = 0;                         // somatic_front: resident workgroups per CU
+  gq::DevBuf cands;                                // somatic: the candidates' records (CandRec)
   gq::DevBuf el_store;                             // somatic: the split caller's element store (ElemStore)
   gq::DevBuf win_bound;                            // germline: window bounds (window_bounds)
   gq::DevBuf bkt;                                  // germline output order: bucket counts / offsets / fill
+  // The bulk host -> device staging (H2DStager): two pinned chunks kept for the context's life
+  // and allocated by `prep`, a helper thread gq_open starts (pinning 128 MB takes ~20 ms, and
+  // freeing it as long: neither belongs on a load's path).  prep also loads the library's code
+  // objects onto the device (a no-op launch per translation unit), which HIP otherwise does at a
+  // module's first launch (~30 ms).
+  void *stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_done[2] = {};
+  bool stage_used[2] = {false, false};
+  std::mutex stage_m;
+  std::condition_variable stage_cv;
+  bool stage_ready = false;
+  hipError_t stage_err = hipSuccess;
+  std::thread prep;
+  hipError_t wait_stage() {
+    std::unique_lock<std::mutex> lk(stage_m);
+    stage_cv.wait(lk, [this] { return stage_ready; });
+    return stage_err;
+  }
   void *pin = nullptr;                             // pinned host staging for the small per-call copies
   size_t pin_n = 0;
   hipError_t pinned(size_t bytes) {                // pin has >= bytes (contents not kept)
@@ -546,32 +567,27 @@ namespace gq {
 // drains the other.
 struct H2DStager {
   static constexpr size_t kChunk = size_t(64) << 20;
+  gq_ctx *c;
   hipStream_t stream;
-  void *buf[2] = {nullptr, nullptr};
-  hipEvent_t done[2] = {nullptr, nullptr};
-  bool used[2] = {false, false};
+  void **buf = nullptr;
+  hipEvent_t *done = nullptr;
+  bool *used = nullptr;
   int slot = 0;
   unsigned threads = 1;
-  explicit H2DStager(hipStream_t s) : stream(s) {
+  explicit H2DStager(gq_ctx *ctx) : c(ctx), stream(ctx->stream) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     threads = std::min(16u, hw);  // the GPU box's CPU share is 16 threads
   }
-  ~H2DStager() {
-    for (int i = 0; i < 2; ++i) {
-      if (done[i]) {
-        (void)hipEventSynchronize(done[i]);
-        (void)hipEventDestroy(done[i]);
-      }
-      if (buf[i]) (void)hipHostFree(buf[i]);
-    }
+  ~H2DStager() {  // the chunks stay with the context; its copies must have drained
+    for (int i = 0; done && i < 2; ++i)
+      if (used[i]) (void)hipEventSynchronize(done[i]);
   }
   hipError_t init() {
-    for (int i = 0; i < 2; ++i) {
-      hipError_t e = hipHostMalloc(&buf[i], kChunk, hipHostMallocDefault);
-      if (e != hipSuccess) return e;
-      e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
+    const hipError_t e = c->wait_stage();
+    if (e != hipSuccess) return e;
+    buf = c->stage;
+    done = c->stage_done;
+    used = c->stage_used;
     return hipSuccess;
   }
   // out[0, k) <- bytes [o, o + k) of the logical source, split over the threads
@@ -626,6 +642,11 @@ struct H2DStager {
 gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
 // The projection (ProjRec) of a resident read set, derived on first use.
 gq_status ensure_projection(gq_ctx *c, const gq_dev_reads *d);
+// No-op launches that load each translation unit's code object onto the device (gq_open's prep).
+hipError_t warm_pileup(hipStream_t s);
+hipError_t warm_somatic(hipStream_t s);
+hipError_t warm_heapref(hipStream_t s);
+hipError_t warm_bamdev(hipStream_t s);
 
 // Loci ranges -> locus tiles of T loci with each tile's read window in `rd`, written to `tiles`.
 gq_status plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T, Plan &pl, DevBuf &tiles,

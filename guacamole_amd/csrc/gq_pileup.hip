@@ -1659,6 +1659,14 @@ __global__ __launch_bounds__(kBlock) void calls_image(const CallRec *__restrict_
 // ==========================================================================================
 // Host side: context, resident read sets, entry points
 // ==========================================================================================
+namespace {
+__global__ void warm_k() {}
+}  // namespace
+hipError_t gq::warm_pileup(hipStream_t s) {
+  hipLaunchKernelGGL(warm_k, dim3(1), dim3(64), 0, s);
+  return hipGetLastError();
+}
+
 extern "C" {
 
 const char *gq_version(void) { return "guacamole-amd gqpileup 0.1 (gfx950)"; }
@@ -1674,14 +1682,39 @@ gq_status gq_open(int device, gq_ctx **out) {
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  // the staging chunks first (a load may wait on them), then the code objects
+  c->prep = std::thread([c] {
+    hipError_t e = hipSetDevice(c->device);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipHostMalloc(&c->stage[i], H2DStager::kChunk, hipHostMallocDefault);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->stage_done[i], hipEventDisableTiming);
+    }
+    {
+      std::lock_guard<std::mutex> lk(c->stage_m);
+      c->stage_err = e;
+      c->stage_ready = true;
+    }
+    c->stage_cv.notify_all();
+    if (e == hipSuccess) e = gq::warm_pileup(c->stream);
+    if (e == hipSuccess) e = gq::warm_somatic(c->stream);
+    if (e == hipSuccess) e = gq::warm_heapref(c->stream);
+    if (e == hipSuccess) e = gq::warm_bamdev(c->stream);
+    (void)e;  // (a failed warm-up only leaves the loading to the first launch)
+  });
   *out = c;
   return GQ_OK;
 }
 
+
 void gq_close(gq_ctx *c) {
   if (!c) return;
+  if (c->prep.joinable()) c->prep.join();
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  for (int i = 0; i < 2; ++i) {
+    if (c->stage_done[i]) (void)hipEventDestroy(c->stage_done[i]);
+    if (c->stage[i]) (void)hipHostFree(c->stage[i]);
+  }
   for (DevBuf *b : {&c->ranges, &c->tiles, &c->recs, &c->recs_sorted, &c->keys, &c->keys_sorted, &c->idx,
                     &c->idx_sorted, &c->cplx, &c->pool, &c->counters, &c->sort_tmp, &c->image, &c->tiles2, &c->srecs, &c->c_depth, &c->c_pos,
                     &c->c_base, &c->c_indel, &c->c_ref, &c->c_rb, &c->c_amb, &c->slow, &c->amb, &c->amb_ref,
@@ -1856,7 +1889,7 @@ gq_status gq_reads_upload(gq_ctx *c, const gq_reads *h, gq_dev_reads **out) {
   d->ctx = c;
   const int64_t n = h->n_reads;
   const auto t0 = std::chrono::steady_clock::now();
-  H2DStager stager(c->stream);
+  H2DStager stager(c);
   {
     hipError_t e = stager.init();
     if (e != hipSuccess) {

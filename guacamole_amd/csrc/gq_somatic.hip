@@ -1686,11 +1686,16 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     const int64_t grid_cap = grid_env > 0 ? (int64_t)grid_env : (int64_t)c->call_wg_per_cu * c->n_cu;
     const int cblocks = (int)std::min<int64_t>(std::max<int64_t>(pt.n_tiles, 1), grid_cap);
     const DeepIO dio{(int64_t *)c->deep_list.p, deep_cap, 0, nullptr, 0, 0};
+    // the candidates' records in list order (every caller kernel below reads them)
+    HIP_TRY(c->cands.ensure(sizeof(CandRec) * (size_t)std::max<unsigned long long>(n_cand, 1)));
+    hipLaunchKernelGGL(cand_prep, dim3((unsigned)((kParts + kSomWaves - 1) / kSomWaves)), dim3(kBlock), 0, c->stream,
+                       (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, og,
+                       (const Counters *)ctr, sw, (CandRec *)c->cands.p);
+    HIP_TRY(hipGetLastError());
     front_ms = 0;
     if (!split) {
       auto k1 = wpe2 ? somatic_call_k<false, false, 2> : somatic_call_k<false, false, 3>;
-      hipLaunchKernelGGL(k1, dim3(cblocks), dim3(kBlock), 0, c->stream,
-                         (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+      hipLaunchKernelGGL(k1, dim3(cblocks), dim3(kBlock), 0, c->stream, (const CandRec *)c->cands.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)c->amb.p,
                          amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, rv, dbg, dio,
                          ElemStore{});
@@ -1725,14 +1730,12 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
           front_ms += ms;
         }
         HIP_TRY(hipEventRecord(c->ev[6], c->stream));
-        hipLaunchKernelGGL(somatic_front, dim3(fblocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                           (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p, og, ctr, sw, dbg, dio,
-                           es);
+        hipLaunchKernelGGL(somatic_front, dim3(fblocks), dim3(kBlock), 0, c->stream, (const CandRec *)c->cands.p, t->d,
+                           n->d, *p, ctr, sw, dbg, dio, es);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[7], c->stream));
         hipLaunchKernelGGL((somatic_call_k<false, true>), dim3(bblocks), dim3(kBlock), 0, c->stream,
-                           (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d,
-                           *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
+                           (const CandRec *)c->cands.p, t->d, n->d, *p, (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                            (AmbItem *)c->amb.p, amb_cap, (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0,
                            rv, dbg, dio, es);
         HIP_TRY(hipGetLastError());
@@ -1762,8 +1765,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
       HIP_TRY(hipEventRecord(c->ev[5], c->stream));
       const unsigned blocks = (unsigned)((nw + kSomWaves - 1) / kSomWaves);
-      hipLaunchKernelGGL((somatic_call_k<true, false>), dim3(blocks), dim3(kBlock), 0, c->stream, (const Tile *)c->tiles.p,
-                         (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, t->d, n->d, *p,
+      hipLaunchKernelGGL((somatic_call_k<true, false>), dim3(blocks), dim3(kBlock), 0, c->stream,
+                         (const CandRec *)c->cands.p, t->d, n->d, *p,
                          (SomRec *)c->srecs.p, rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw,
                          (AmbItem *)(ain ? nullptr : c->amb.p), ain ? (unsigned long long)0 : amb_cap, ain, aref,
                          ain ? n_items : (int64_t)0, ain ? RefView{nullptr, nullptr} : rv, dbg,
@@ -2253,3 +2256,11 @@ void gq_free_somatic(gq_somatic_calls *r) {
 }
 
 }  // extern "C"
+
+namespace {
+__global__ void warm_k() {}
+}  // namespace
+hipError_t gq::warm_somatic(hipStream_t s) {
+  hipLaunchKernelGGL(warm_k, dim3(1), dim3(64), 0, s);
+  return hipGetLastError();
+}

@@ -31,6 +31,13 @@ __device__ __forceinline__ int el_mq(const uint4 &e) { return (int)(e.z >> 24); 
 __device__ __forceinline__ uint32_t el_flags(const uint4 &e) { return (e.w >> 16) & 0xFFu; }
 __device__ __forceinline__ int el_tidx(const uint4 &e) { return (int)(e.w >> 24); }
 
+// One element's three possible log terms (log(2(1 - pc)), log(pc + (1 - pc)), log(2 pc); 0 when
+// the mapq filter drops it) and its allele-table index: one 32-byte LDS record per element.
+struct TermRec {
+  double t0, th, t2;
+  int32_t tj, pad;
+};
+
 // Per-wave working memory (LDS for the fast kernel, a global scratch slice for the deep one).
 struct CallMem {
   int32_t *cov[2];  // [cap] covering reads (offset from the tile's rb), pileup element order
@@ -39,6 +46,7 @@ struct CallMem {
   int16_t *order;   // [64 kSlots]
   uint8_t *is_var;  // [64 kSlots]
   double *ll;       // [maxG]
+  struct TermRec *terms;  // [cap] fast kernel (LDS): each element's log terms + table index; deep: nullptr
   int cap, maxG;
 };
 
@@ -64,6 +72,7 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   m.order = (int16_t *)p;
   p += 64 * kSlots * 2;
   m.is_var = p;
+  m.terms = nullptr;
   m.cap = cap;
   m.maxG = maxG;
   return m;
@@ -183,7 +192,7 @@ struct GenoOut {
 // the variant genotypes' likelihoods in the iteration order of the immutable Map `toMap`
 // builds (SomaticStandardCaller.scala:206-217): generation order up to four genotypes, the
 // HashTrieMap's beyond (gq_scala_order.h).
-template <int NS>
+template <int NS, bool LDS_TERMS>
 __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS> &P, const uint4 *el, int n_el, int32_t pos,
                                                 bool include_alignment, bool with_var_sum, CallMem &m, Counters *ctr) {
   const int lane = threadIdx.x & 63;
@@ -225,45 +234,85 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
     return res;
   }
   const double ln2d = sm::log(2.0) * (double)P.depth_f;
-  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element.  The elements
-  // go by 64-element chunks, last chunk first: lane k of a chunk computes its element's three
-  // possible log terms (0 for an element the mapq filter drops: starting the fold at +0.0 and
-  // adding 0.0 for those is bit-identical to Colt's fold over the filtered elements, no term is
-  // -0.0), and the genotype lanes take them by readlane, element by element in descending order
-  // (no LDS round trip on the fold's dependence chain).
-  for (int g0 = 0; g0 < G; g0 += 64) {
-    const int g = g0 + lane;
-    int i = 0, j = 0;
-    if (g < G) genotype_index(g, n, i, j);
-    const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
-    double agg = 0.0;
-    for (int c0 = ((n_el - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {
+  // the three possible log terms of an element (0 for an element the mapq filter drops: starting
+  // the fold at +0.0 and adding 0.0 for those is bit-identical to Colt's fold over the filtered
+  // elements; no term is -0.0)
+  auto elem_terms = [&](int k, int &tj, double &t0, double &th, double &t2) {
+    const uint4 e = el[k];
+    const uint32_t fl = el_flags(e);
+    tj = el_tidx(e);
+    t0 = th = t2 = 0.0;
+    if ((fl & kElAct) && (fl & kElPass)) {
+      const int q = el_q(e);
+      if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
+      double pc = phred_success(q);
+      if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
+      const double pw = 1.0 - pc;
+      t2 = sm::log(pc + pc);
+      th = sm::log(pc + pw);
+      t0 = sm::log(pw + pw);
+    }
+  };
+  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element
+  if constexpr (LDS_TERMS) {
+    // fast kernel: the terms go to LDS records (lanes = elements), then each genotype lane folds
+    // them four records per batch, the batch's loads issued before its adds
+    for (int c0 = 0; c0 < n_el; c0 += 64) {
       const int k = c0 + lane;
-      int tjl = -1;
-      double t2 = 0.0, th = 0.0, t0 = 0.0;
-      if (k < n_el) {
-        const uint4 e = el[k];
-        const uint32_t fl = el_flags(e);
-        tjl = el_tidx(e);
-        if ((fl & kElAct) && (fl & kElPass)) {
-          const int q = el_q(e);
-          if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
-          double pc = phred_success(q);
-          if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
-          const double pw = 1.0 - pc;
-          t2 = sm::log(pc + pc);
-          th = sm::log(pc + pw);
-          t0 = sm::log(pw + pw);
+      if (k >= n_el) continue;
+      TermRec t;
+      elem_terms(k, t.tj, t.t0, t.th, t.t2);
+      t.pad = 0;
+      m.terms[k] = t;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      int i = 0, j = 0;
+      if (g < G) genotype_index(g, n, i, j);
+      const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
+      auto pick = [&](const TermRec &t) {
+        const int sel = (ei == t.tj ? 1 : 0) + (ej == t.tj ? 1 : 0);
+        return sel == 0 ? t.t0 : sel == 1 ? t.th : t.t2;
+      };
+      double agg = 0.0;
+      int k = n_el - 1;
+      for (; k >= 3; k -= 4) {
+        const TermRec a = m.terms[k], b = m.terms[k - 1], c = m.terms[k - 2], d = m.terms[k - 3];
+        const double pa = pick(a), pb = pick(b), pc = pick(c), pd = pick(d);
+        agg = agg + pa;
+        agg = agg + pb;
+        agg = agg + pc;
+        agg = agg + pd;
+      }
+      for (; k >= 0; --k) agg = agg + pick(m.terms[k]);
+      if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
+    }
+  } else {
+    // deep kernel (records in global scratch): lane k of each 64-element chunk, last chunk first,
+    // computes its element's terms and the genotype lanes take them by readlane, element by
+    // element in descending order (no memory round trip on the fold's dependence chain)
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      int i = 0, j = 0;
+      if (g < G) genotype_index(g, n, i, j);
+      const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
+      double agg = 0.0;
+      for (int c0 = ((n_el - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {
+        const int k = c0 + lane;
+        int tjl = -1;
+        double t2 = 0.0, th = 0.0, t0 = 0.0;
+        if (k < n_el) elem_terms(k, tjl, t0, th, t2);
+        for (int kk = min(63, n_el - 1 - c0); kk >= 0; --kk) {
+          const int tj = __builtin_amdgcn_readlane(tjl, kk);
+          const double a0 = lane_f64(t0, kk), ah = lane_f64(th, kk), a2 = lane_f64(t2, kk);
+          const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
+          agg = agg + (sel == 0 ? a0 : sel == 1 ? ah : a2);
         }
       }
-      for (int kk = min(63, n_el - 1 - c0); kk >= 0; --kk) {
-        const int tj = __builtin_amdgcn_readlane(tjl, kk);
-        const double a0 = lane_f64(t0, kk), ah = lane_f64(th, kk), a2 = lane_f64(t2, kk);
-        const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
-        agg = agg + (sel == 0 ? a0 : sel == 1 ? ah : a2);
-      }
+      if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
     }
-    if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -501,20 +550,64 @@ struct DeepIO {
   int scap, maxG;            // deep kernel: elements per sample per wave, genotypes
 };
 
+// One candidate with what its wave needs before the first search, gathered by cand_prep in list
+// order, so the caller loads one record (one candidate ahead) instead of walking the item ->
+// tile -> window -> initial group chain of dependent loads on its critical path.
+struct CandRec {
+  int64_t rb[2], re[2];  // the tile's read windows (tumor, normal)
+  int64_t ord0;          // output ordinal of the tile's first locus
+  int32_t pos, contig, L0, flags;
+  int32_t win, tile;
+  int32_t E[2];  // per sample: end of its window's initial group (reorder where pos < E); INT32_MIN: none
+};
+
+// The candidates' records, a wave per output partition (lanes over its items: no search for
+// the partition of a flat index).
+__global__ void cand_prep(const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n,
+                          const ComplexItem *__restrict__ items, OutGeom og, const Counters *__restrict__ ctr, SomWin sw,
+                          CandRec *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t q = w0; q < kParts; q += nw) {
+    const unsigned long long o0 = ctr->part_off[1][q], o1 = ctr->part_off[1][q + 1];
+    for (unsigned long long k = lane; k < o1 - o0; k += 64) {
+      const ComplexItem item = items[og.slot(1, (int)q, k)];
+      const Tile &tt = tiles_t[item.tile], &tn = tiles_n[item.tile];
+      CandRec c;
+      c.rb[0] = tt.rb;
+      c.rb[1] = tn.rb;
+      c.re[0] = tt.re;
+      c.re[1] = tn.re;
+      c.ord0 = tt.ordinal0;
+      c.pos = item.pos;
+      c.contig = tt.contig;
+      c.L0 = tt.L0;
+      c.flags = item.flags;
+      c.win = sw.range_win[tt.range];
+      c.tile = item.tile;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const WinInit wi = sw.wi[2 * c.win + s];
+        c.E[s] = wi.n > 0 ? wi.E : INT32_MIN;
+      }
+      out[o0 + k] = c;
+    }
+  }
+}
+
 // The caller's front: the covering reads of both samples (pileup element order) and one element
 // record per covering read (m.el, m.cov), and per lane the std-bit mask of the MD-derived
 // reference bases it saw (mask; OR over the wave = the pileup's reference-base set).  Latency-bound
 // (dependent searches and per-read loads).  Returns false when the candidate leaves this kernel:
 // deeper than m.cap (the fast kernels list it for the deep one).
 template <bool DEEP>
-__device__ __forceinline__ bool call_front(const Tile &tt_, const Tile &tn_, int32_t pos, int64_t it, const DevReads &RT,
-                                           const DevReads &RN, const gq_somatic_params &prm, Counters *ctr,
-                                           const SomWin &sw, CallMem &m, int dbg, const DeepIO &dio, uint32_t (&nc)[2],
-                                           uint32_t (&mask)[2]) {
+__device__ __forceinline__ bool call_front(const CandRec &cr, int64_t it, const DevReads &RT, const DevReads &RN,
+                                           const gq_somatic_params &prm, Counters *ctr, const SomWin &sw, CallMem &m,
+                                           int dbg, const DeepIO &dio, uint32_t (&nc)[2], uint32_t (&mask)[2]) {
   const int lane = threadIdx.x & 63;
-  const int64_t rb[2] = {tt_.rb, tn_.rb}, re[2] = {tt_.re, tn_.re};
-  const int32_t win = sw.range_win[tt_.range];
-  const WinInit wi[2] = {sw.wi[2 * win], sw.wi[2 * win + 1]};
+  const int32_t pos = cr.pos;
+  const int64_t rb[2] = {cr.rb[0], cr.rb[1]}, re[2] = {cr.re[0], cr.re[1]};
   // ---- covering reads of both samples: [first pmax_end > pos, first start > pos) of each
   //      tile window, the four searches in lockstep
   int64_t ra[2], rz[2];
@@ -564,8 +657,8 @@ __device__ __forceinline__ bool call_front(const Tile &tt_, const Tile &tn_, int
   //      currentRegions(), DistributedUtil.scala:260-274; Pile.atGreaterLocus keeps them first)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const WinInit &w = wi[s];
-    if (!(w.n > 0 && pos < w.E)) continue;  // uniform
+    if (!(pos < cr.E[s])) continue;  // uniform
+    const WinInit w = sw.wi[2 * cr.win + s];
     const DevReads &R = s ? RN : RT;
     int p = 0;
     for (int k0 = 0; k0 < (int)nc[s]; k0 += 64) {
@@ -681,8 +774,8 @@ struct ElemStore {
 // spills; 2: no spills; GQ_CALL_WPE picks, see gq_somatic_standard).  The deep kernel: 2.
 template <bool DEEP, bool BACK = false, int WPE = 3>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : WPE))) void somatic_call_k(
-    const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
-    DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs, unsigned long long rec_cap,
+    const CandRec *__restrict__ cands, DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
+    unsigned long long rec_cap,
     uint8_t *__restrict__ pool, unsigned long long pool_cap, OutGeom og, Counters *ctr, SomWin sw,
     AmbItem *__restrict__ amb_out, unsigned long long amb_cap, const AmbItem *__restrict__ amb_in,
     const uint8_t *__restrict__ amb_ref, int64_t n_amb_in, RefView ref, int dbg, DeepIO dio, ElemStore es) {
@@ -699,8 +792,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   __shared__ int16_t s_order[DEEP ? 1 : FW][64 * NS];
   __shared__ uint8_t s_var[DEEP ? 1 : FW][64 * NS];
   __shared__ double s_ll[DEEP ? 1 : FW][kMaxG];
+  __shared__ TermRec s_terms[DEEP ? 1 : FW][kFastCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // (wave-uniform, and known to be: the candidate records then load into scalar registers)
+  const int64_t gwave = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   CallMem m;
   if constexpr (DEEP) {
@@ -714,6 +809,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.order = s_order[wv];
     m.is_var = s_var[wv];
     m.ll = s_ll[wv];
+    m.terms = s_terms[wv];
     m.cap = kFastCap;
     m.maxG = kMaxG;
   }
@@ -738,24 +834,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     }
   };
   // the next candidate's record is loaded one candidate ahead (it lands while this one runs)
-  auto fetch_item = [&](int64_t li, int64_t &it) -> ComplexItem {
+  auto fetch_item = [&](int64_t li, int64_t &it) -> CandRec {
     it = amb_in ? amb_in[li].item : DEEP ? dio.list[li] : li;
-    return items[part_slot_wave(ctr->part_off[1], (unsigned long long)it, og, 1)];
+    return cands[it];
   };
   int64_t it_next = 0;
-  ComplexItem item_next{0, 0, 0};
+  CandRec item_next{};
   if (li0 < (int64_t)n_items) item_next = fetch_item(li0, it_next);
   for (int64_t li = li0; li < (int64_t)n_items; li += nwaves_total) {
     tick(-1);
     if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[5], 1ull);
     const int64_t it = it_next;
-    const ComplexItem item = item_next;
+    const CandRec item = item_next;
     if (li + nwaves_total < (int64_t)n_items) item_next = fetch_item(li + nwaves_total, it_next);
-    const Tile &tt_ = tiles_t[item.tile], &tn_ = tiles_n[item.tile];
     const int32_t pos = item.pos;
-    const int32_t t_contig = tt_.contig, t_L0 = tt_.L0;
-    const int64_t t_ord0 = tt_.ordinal0;
-    const int64_t rb[2] = {tt_.rb, tn_.rb};
+    const int32_t t_contig = item.contig, t_L0 = item.L0;
+    const int64_t t_ord0 = item.ord0;
+    const int64_t rb[2] = {item.rb[0], item.rb[1]};
     uint32_t nc[2], mask[2];
     if constexpr (BACK) {
       // the front's records -> LDS (the tables, folds and evidence read them across lanes)
@@ -776,7 +871,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     } else {
-      if (!call_front<DEEP>(tt_, tn_, pos, it, RT, RN, prm, ctr, sw, m, dbg, dio, nc, mask)) continue;
+      if (!call_front<DEEP>(item, it, RT, RN, prm, ctr, sw, m, dbg, dio, nc, mask)) continue;
     }
     Pile<NS> PS[2];
     const int fb = ref.b ? (int)ref.b[ref.off[t_contig] + pos] : -1;
@@ -921,14 +1016,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     }
     // the multi-allelic filter empties a pileup: no element passes then
     const int nT = PT.depth_f ? (int)nc[0] : 0, nN = PN.depth_f ? (int)nc[1] : 0;
-    const GenoOut tg = genotypes_el(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
+    const GenoOut tg = genotypes_el<NS, !DEEP>(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
     tick(3);
     if (dbg & 8192) continue;  // ablation: up to the tumor genotypes
     if (tg.G == 0) continue;
     const bool t_var = m.is_var[tg.bi] || m.is_var[tg.bj];
     if (!t_var) continue;
     const AlleleDesc a1 = pile_entry(PT, tg.bi), a2 = pile_entry(PT, tg.bj);
-    const GenoOut ng = genotypes_el(RN, PN, m.el[1], nN, pos, false, true, m, ctr);
+    const GenoOut ng = genotypes_el<NS, !DEEP>(RN, PN, m.el[1], nN, pos, false, true, m, ctr);
     const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
     const double odds = tg.best_l / nvs;
     if (!(odds * 100.0 >= (double)prm.odds)) continue;
@@ -1025,14 +1120,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
 #define GQ_FRONT_WPE 4
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_FRONT_WPE))) void somatic_front(
-    const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n, const ComplexItem *__restrict__ items,
-    DevReads RT, DevReads RN, gq_somatic_params prm, OutGeom og, Counters *ctr, SomWin sw, int dbg, DeepIO dio,
-    ElemStore es) {
+    const CandRec *__restrict__ cands, DevReads RT, DevReads RN, gq_somatic_params prm, Counters *ctr, SomWin sw,
+    int dbg, DeepIO dio, ElemStore es) {
   constexpr int FW = kSomWaves;
   __shared__ int32_t s_cov[FW][2][kFastCap];
   __shared__ uint32_t s_tmp[FW][2 * kFastCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // (wave-uniform, and known to be: the candidate records then load into scalar registers)
+  const int64_t gwave = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   CallMem m{};
   m.cov[0] = s_cov[wv][0];
@@ -1040,18 +1135,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GQ_FRONT
   m.tmp = s_tmp[wv];
   m.cap = kFastCap;
   m.maxG = kMaxG;
-  auto fetch = [&](int64_t li) { return items[part_slot_wave(ctr->part_off[1], (unsigned long long)li, og, 1)]; };
-  ComplexItem item_next{0, 0, 0};
-  if (es.b0 + gwave < es.b1) item_next = fetch(es.b0 + gwave);
+  CandRec item_next{};
+  if (es.b0 + gwave < es.b1) item_next = cands[es.b0 + gwave];
   for (int64_t li = es.b0 + gwave; li < es.b1; li += nwaves_total) {
-    const ComplexItem item = item_next;
-    if (li + nwaves_total < es.b1) item_next = fetch(li + nwaves_total);
+    const CandRec item = item_next;
+    if (li + nwaves_total < es.b1) item_next = cands[li + nwaves_total];
     const size_t o = (size_t)(li - es.b0) * 2 * kFastCap;
     m.el[0] = es.el + o;  // the element records go straight to the store
     m.el[1] = es.el + o + kFastCap;
     uint32_t nc[2], mask[2];
-    const bool go = call_front<false>(tiles_t[item.tile], tiles_n[item.tile], item.pos, li, RT, RN, prm, ctr, sw, m, dbg,
-                                      dio, nc, mask);
+    const bool go = call_front<false>(item, li, RT, RN, prm, ctr, sw, m, dbg, dio, nc, mask);
     uint4 h = make_uint4(kElSkip, 0, 0, 0);
     if (go) {
 #pragma unroll
