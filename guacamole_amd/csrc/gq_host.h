@@ -367,14 +367,17 @@ struct PieceMeta {
   uint32_t ev[4];     // MD events at the piece's loci: bit i = locus 8 s0 + i (margin fill)
 };
 
-// word(read, meta, column, word index in the pool row) once per word of the slice's pieces, a
-// lane per word (a batch's words in piece order: consecutive words of a piece on consecutive
-// lanes, so the loads of a piece's bases and the stores of its row coalesce).  setup(read, meta)
-// runs once per piece on the piece's lane and returns false to drop it.  meta: this wave's 64
-// LDS entries.  Every lane of the wave calls word in uniform control flow (act: holds a word).
-template <class S, class F>
+// Once per word of the slice's pieces, a lane per word (a batch's words in piece order:
+// consecutive words of a piece on consecutive lanes, so the loads of a piece's bases and the
+// stores of its row coalesce): raw = fetch(read, meta, column) (the word's loads), then
+// emit(raw, read, meta, column).  Each lane takes kU words per round and issues all their loads
+// before the first emit (one load latency per kU words).  setup(read, meta) runs once per piece
+// on the piece's lane and returns false to drop it.  meta: this wave's 64 LDS entries.  emit
+// runs in uniform control flow (act: the lane holds a word).
+template <class S, class F, class E>
 __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
-                                           PieceMeta *__restrict__ meta, S &&setup, F &&word) {
+                                           PieceMeta *__restrict__ meta, S &&setup, F &&fetch, E &&emit) {
+  constexpr int kU = 4;
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
@@ -397,16 +400,27 @@ __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W,
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t w0 = 0; w0 < tot; w0 += 64) {
-      const uint32_t w = w0 + (uint32_t)lane;
-      int k = 0;  // the last lane whose words start at or before w
+    for (uint32_t w0 = 0; w0 < tot; w0 += 64 * kU) {
+      int kk[kU];
+      int32_t col[kU];
+      bool act[kU];
+      decltype(fetch((int64_t)0, meta[0], (int32_t)0)) raw[kU];
 #pragma unroll
-      for (int b = 32; b >= 1; b >>= 1)
-        if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
-      const uint32_t j = w - (uint32_t)__shfl((int)ex, k, 64);
-      const bool act = w < tot;
-      const PieceMeta &m = meta[act ? k : 0];  // (read in place: fields load from LDS as used)
-      word(act, r0 + k, m, m.s0 + (int32_t)j);
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t w = w0 + 64 * u + (uint32_t)lane;
+        int k = 0;  // the last lane whose words start at or before w
+#pragma unroll
+        for (int b = 32; b >= 1; b >>= 1)
+          if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+        act[u] = w < tot;
+        kk[u] = act[u] ? k : 0;
+        col[u] = meta[kk[u]].s0 + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (act[u]) raw[u] = fetch(r0 + kk[u], meta[kk[u]], col[u]);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) emit(act[u], raw[u], r0 + kk[u], meta[kk[u]], col[u]);
     }
     __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

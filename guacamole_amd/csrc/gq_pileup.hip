@@ -433,22 +433,27 @@ typedef uint64_t gq_u64u __attribute__((aligned(1)));  // unaligned 8-byte loads
 
 // The projection word of read r at column col (loci [8 col, 8 col + 8)): byte j = code of locus
 // 8 col + j | code of locus 8 col + j + 4 << 4 (4-bit codes, proj_code).  m: the read's piece
-// (slice_fill); inside a column-eligible read, eight bases in one 8-byte load.
-__device__ __forceinline__ uint32_t proj_word(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col) {
+// (slice_fill).  proj_fetch loads the word's eight bases (one 8-byte load inside a column-eligible
+// read; a general CIGAR's word is complete here); proj_code8 turns them into the word.
+struct ProjRaw {
+  uint64_t b;     // the bases, byte q = locus 8 col + q (0 outside the read)
+  uint32_t word;  // general CIGAR: the word itself
+  uint32_t gen;
+};
+__device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col) {
   const int32_t s = m.s, e = m.e;
   const int32_t lb = 8 * col;  // locus of byte 0
+  ProjRaw x{0, 0, 0};
   if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
-    uint64_t b;
     if (lb >= s && lb + 8 <= e) {
-      b = *reinterpret_cast<const gq_u64u *>(R.seq + m.p0 + lb);
+      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + m.p0 + lb);
     } else {
-      b = 0;
       for (int q = 0; q < 8; ++q) {
         const int32_t l = lb + q;
-        if (l >= s && l < e) b |= (uint64_t)R.seq[m.p0 + l] << (8 * q);
+        if (l >= s && l < e) x.b |= (uint64_t)R.seq[m.p0 + l] << (8 * q);
       }
     }
-    return proj_codes4((uint32_t)b) | (proj_codes4((uint32_t)(b >> 32)) << 4);
+    return x;
   }
   // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
   const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
@@ -465,7 +470,9 @@ __device__ __forceinline__ uint32_t proj_word(const DevReads &R, int64_t r, cons
       if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
     }
   }
-  return v[0] | (v[1] << 4);
+  x.word = v[0] | (v[1] << 4);
+  x.gen = 1;
+  return x;
 }
 
 // The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
@@ -489,8 +496,11 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
           m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
           return true;
         },
-        [&](bool act, int64_t r, const PieceMeta &m, int32_t col) {
-          if (act) out[16 * (int64_t)m.row + (col & 15)] = proj_word(R, r, m, col);
+        [&](int64_t r, const PieceMeta &m, int32_t col) { return proj_fetch(R, r, m, col); },
+        [&](bool act, const ProjRaw &x, int64_t, const PieceMeta &m, int32_t col) {
+          if (act)
+            out[16 * (int64_t)m.row + (col & 15)] =
+                x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
         });
   }
 }

@@ -93,49 +93,71 @@ __device__ __forceinline__ bool margin_setup(const DevReads &R, int64_t r, int m
 
 // The margin word (8 loci, a byte each; hom_ref_margin_lane's terms in 1/8 units, biased) of read
 // r at column col, from its piece m.  Loci outside the read's Match/Mismatch blocks hold
-// kMargin8Zero; inside a column-eligible read, eight qualities in one 8-byte load.
-__device__ __forceinline__ uint2 margin_word(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col,
-                                             const uint8_t *__restrict__ tab) {
-  const int32_t s = m.s, e = m.e;
-  const int32_t lb = 8 * col;
+// kMargin8Zero.  margin_fetch loads the word's eight qualities (one 8-byte load inside a
+// column-eligible read; a general CIGAR's word is complete here); margin_terms8 looks the terms up.
+struct MarginRaw {
+  uint64_t q;   // qualities, byte k = locus 8 col + k (eligible reads)
+  uint2 word;   // general CIGAR: the word itself
+  uint32_t valid, gen;  // valid: byte mask of loci inside the read
+};
+__device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, int32_t col, uint64_t q, uint32_t valid,
+                                               const uint8_t *__restrict__ tab) {
   const uint8_t *tm = tab + (m.mq << 8);
-  const int32_t i0 = 8 * (col - m.s0);                        // bit of locus lb in m.ev
-  const uint32_t evb = (m.ev[i0 >> 5] >> (i0 & 31)) & 0xFFu;  // events at loci lb .. lb + 7 (m: in LDS)
+  const int32_t i0 = 8 * (col - m.s0);                        // bit of locus 8 col in m.ev
+  const uint32_t evb = (m.ev[i0 >> 5] >> (i0 & 31)) & 0xFFu;  // events at the word's loci (m: in LDS)
   uint32_t v[2] = {0x80808080u, 0x80808080u};
-  auto put = [&](int q8, int qv) {
+#pragma unroll
+  for (int q8 = 0; q8 < 8; ++q8) {
+    if (!((valid >> q8) & 1u)) continue;
+    const int qv = (int)(int8_t)(uint8_t)(q >> (8 * q8));
     const uint32_t t = qv < 0 ? (uint32_t)kMargin8None : (uint32_t)tm[(qv << 1) | ((evb >> q8) & 1u ? 0 : 1)];
     v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
-  };
+  }
+  return make_uint2(v[0], v[1]);
+}
+__device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col,
+                                                  const uint8_t *__restrict__ tab) {
+  const int32_t s = m.s, e = m.e;
+  const int32_t lb = 8 * col;
+  MarginRaw x{0, make_uint2(0x80808080u, 0x80808080u), 0, 0};
   if (m.info & kColEligible) {
     if (lb >= s && lb + 8 <= e) {
-      const uint64_t qb = *reinterpret_cast<const gq_u64m *>(R.qual + m.p0 + lb);
-#pragma unroll
-      for (int q8 = 0; q8 < 8; ++q8) put(q8, (int)(int8_t)(uint8_t)(qb >> (8 * q8)));
+      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + m.p0 + lb);
+      x.valid = 0xFFu;
     } else {
 #pragma unroll
       for (int q8 = 0; q8 < 8; ++q8) {
         const int32_t l = lb + q8;
-        if (l >= s && l < e) put(q8, (int)(int8_t)R.qual[m.p0 + l]);
-      }
-    }
-  } else {  // general CIGAR: the count segments
-    const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
-    const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-    const int64_t so = R.seq_off[r];
-#pragma unroll
-    for (int q8 = 0; q8 < 8; ++q8) {
-      const int32_t l = lb + q8;
-      for (int32_t q2 = 0; q2 < nseg; ++q2) {
-        const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-        const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
-        if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
-          put(q8, (int)(int8_t)R.qual[so + (int32_t)(b & 0xFFFFu) + (l - ra)]);
-          break;
+        if (l >= s && l < e) {
+          x.q |= (uint64_t)R.qual[m.p0 + l] << (8 * q8);
+          x.valid |= 1u << q8;
         }
       }
     }
+    return x;
   }
-  return make_uint2(v[0], v[1]);
+  // general CIGAR: the count segments
+  const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
+  const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+  const int64_t so = R.seq_off[r];
+  uint64_t q = 0;
+  uint32_t valid = 0;
+#pragma unroll
+  for (int q8 = 0; q8 < 8; ++q8) {
+    const int32_t l = lb + q8;
+    for (int32_t q2 = 0; q2 < nseg; ++q2) {
+      const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+      const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16);
+      if ((b >> 16) == 0 /* kSegCount */ && l >= ra && l < ra + rl) {
+        q |= (uint64_t)R.qual[so + (int32_t)(b & 0xFFFFu) + (l - ra)] << (8 * q8);
+        valid |= 1u << q8;
+        break;
+      }
+    }
+  }
+  x.word = margin_terms8(m, col, q, valid, tab);
+  x.gen = 1;
+  return x;
 }
 
 // The margin projection of the tumor reads, laid out as `proj` (a byte per projection nibble:
@@ -155,12 +177,13 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     slice_fill(
         R, slice_stored(R, slot), R.prow + R.soff[slot], meta,
         [&](int64_t r, PieceMeta &m) { return margin_setup(R, r, min_mapq, m); },
-        [&](bool act, int64_t r, const PieceMeta &m, int32_t col) {
+        [&](int64_t r, const PieceMeta &m, int32_t col) { return margin_fetch(R, r, m, col, tab); },
+        [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col) {
           if (act) {
-            const uint2 w = margin_word(R, r, m, col, tab);
+            const uint2 w = x.gen ? x.word : margin_terms8(m, col, x.q, x.valid, tab);
             out[16 * (int64_t)m.row + (col & 15)] = w;
-            auto has = [](uint32_t x) {  // a zero byte
-              return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
+            auto has = [](uint32_t v) {  // a zero byte
+              return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
             };
             none = none || has(w.x) || has(w.y);
           }
