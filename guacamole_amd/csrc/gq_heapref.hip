@@ -25,7 +25,7 @@ __global__ void heap_refbase(const int64_t *__restrict__ off, const int64_t *__r
                              const int32_t *__restrict__ pos, int64_t n, int nsets, int set, DevReads R,
                              uint8_t *__restrict__ out, Counters *ctr) {
   const int lane = threadIdx.x & 63;
-  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w = wave_id();
   if (w >= n) return;
   const int32_t p = pos[w];
   const int64_t a = off[w], b = off[w + 1];

@@ -208,6 +208,12 @@ __device__ __forceinline__ unsigned long long part_slot_wave(const unsigned long
   return g.slot(which, q, k - off[q]);
 }
 
+// This wave's index in the grid (blockDim a multiple of 64), known wave-uniform to the compiler:
+// loads indexed by it go to scalar registers.
+__device__ __forceinline__ int64_t wave_id() {
+  return (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
 // Inclusive prefix sum over the 64 lanes of a wave with DPP row shifts and row broadcasts
 // (no LDS round trips).  Every lane must be active.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {

@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, u
   __shared__ __attribute__((aligned(16))) uint8_t s_rend[4][kSliceRowsMax];
   __shared__ uint16_t s_fl[4][kSliceRowsMax];
   const int wv = threadIdx.x >> 6;
-  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     const SliceWin W = slice_stored(R, slot);
@@ -480,7 +480,7 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   __shared__ PieceMeta s_meta[4][64];
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
-  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NS > 2 ?
   // bucket (up to four keys); such loci are listed with the heap-order ones (amb_out) and
   // redone with the windows' element order.
   const int lane = threadIdx.x & 63;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t gwave = wave_id();
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   // items beyond a partition's capacity were never written (the host retries with larger ones)
   //

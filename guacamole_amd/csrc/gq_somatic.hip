@@ -955,7 +955,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 1
   __shared__ int32_t cover_a[FW][kCover], cover_s[FW][kCover];
   __shared__ double ll_lds[FW][kMaxG];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t gwave = wave_id();
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   GsMem m;
   if constexpr (DEEP) {
@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 1
   __shared__ int32_t cover[kSomWaves][kCover];
   __shared__ uint32_t tmp[kSomWaves][kEvCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t gwave = wave_id();
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t n = DEEP ? dd.n_sel : amb_in ? n_amb_in : n_items;
   for (int64_t si = gwave; si < n; si += nwaves_total) {

@@ -567,7 +567,7 @@ __global__ void cand_prep(const Tile *__restrict__ tiles_t, const Tile *__restri
                           const ComplexItem *__restrict__ items, OutGeom og, const Counters *__restrict__ ctr, SomWin sw,
                           CandRec *__restrict__ out) {
   const int lane = threadIdx.x & 63;
-  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t q = w0; q < kParts; q += nw) {
     const unsigned long long o0 = ctr->part_off[1][q], o1 = ctr->part_off[1][q + 1];

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
                                                   uint8_t *__restrict__ mnb) {
   __shared__ PieceMeta s_meta[4][64];
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
-  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform

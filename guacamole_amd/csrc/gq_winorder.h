@@ -26,7 +26,7 @@ struct WinInit {
 __global__ void window_first(const int32_t *__restrict__ w_contig, const int64_t *__restrict__ w_roff,
                              const int64_t *__restrict__ r_s, const int64_t *__restrict__ r_e, int64_t n_win,
                              DevReads RT, DevReads RN, WinInit *__restrict__ wi, int64_t *__restrict__ wi_lo) {
-  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t w = wave_id();
   if (w >= n_win) return;  // wave-uniform
   const int lane = threadIdx.x & 63;
   const int32_t c = w_contig[w];
