@@ -1827,7 +1827,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   }
   for (int k = 0; k < kSpread; ++k) hc.visited += hc.spread[0][k];
   if ((dbg & 16) && hc.prof[5])
-    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): front|records %.0f - %.0f tables %.0f "
+    fprintf(stderr, "gq somatic_call prof (cycles/candidate/wave): front|records %.0f (tumor fold %.0f) tables %.0f "
             "tumor-genotypes %.0f normal-genotypes+evidence %.0f (%llu candidates reached)\n", (double)hc.prof[0] / hc.prof[5],
             (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5], (double)hc.prof[3] / hc.prof[5],
             (double)hc.prof[4] / hc.prof[5], hc.prof[5]);

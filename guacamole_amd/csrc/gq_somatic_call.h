@@ -47,6 +47,7 @@ struct CallMem {
   uint8_t *is_var;  // [64 kSlots]
   double *ll;       // [maxG]
   struct TermRec *terms;  // [cap] fast kernel (LDS): each element's log terms + table index; deep: nullptr
+  const double *succ;     // PhredUtils.phredToSuccessProbability table (g_succ) copied to LDS
   int cap, maxG;
 };
 
@@ -180,7 +181,8 @@ __device__ __forceinline__ int pile_find(const Pile<NS> &P, Key128 key) {
 struct GenoOut {
   int n, G, best_g, bi, bj;
   double best_l, var_sum;
-  bool order_tie;  // two variant genotypes with equal immutable-map keys (insertion order used)
+  bool order_tie;    // two variant genotypes with equal immutable-map keys (insertion order used)
+  uint64_t cyc_fold; // (diagnostics) cycles from entry to the end of the row fold
 };
 
 // Likelihood.likelihoodsOfAllPossibleGenotypesFromPileup (normalised, not log space) over the
@@ -197,6 +199,7 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
                                                 bool include_alignment, bool with_var_sum, CallMem &m, Counters *ctr) {
   const int lane = threadIdx.x & 63;
   GenoOut res{};
+  const uint64_t cyc0 = __builtin_readcyclecounter();
   bool elig[NS], var[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -245,8 +248,9 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
     if ((fl & kElAct) && (fl & kElPass)) {
       const int q = el_q(e);
       if (q < 0) raise_at(ctr, GQ_E_ASSERT, pos);  // PhredUtils: negative phred
-      double pc = phred_success(q);
-      if (include_alignment) pc = pc * phred_success(el_mq(e));  // probabilityCorrectIncludingAlignment
+      auto succ = [&](int x) { return m.succ[x > 255 ? 255 : (x < 0 ? 0 : x)]; };  // phred_success from LDS
+      double pc = succ(q);
+      if (include_alignment) pc = pc * succ(el_mq(e));  // probabilityCorrectIncludingAlignment
       const double pw = 1.0 - pc;
       t2 = sm::log(pc + pc);
       th = sm::log(pc + pw);
@@ -316,6 +320,7 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  res.cyc_fold = __builtin_readcyclecounter() - cyc0;
   double tot = 0.0;
   for (int g0 = 0; g0 < G; g0 += 64) {
     const double e = (g0 + lane < G) ? sm::exp(m.ll[g0 + lane]) : 0.0;
@@ -823,8 +828,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   // tumor genotypes, normal genotypes + evidence + record, candidates), summed per workgroup in LDS (a global
   // atomic per phase would queue every wave on one address) and added to ctr->prof at the end
   __shared__ unsigned long long s_clk[6];
+  __shared__ double s_succ[256];
   if (threadIdx.x < 6) s_clk[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_succ[i] = g_succ[i];
   __syncthreads();
+  m.succ = s_succ;
   uint64_t tk = 0;
   auto tick = [&](int k) {
     if (dbg & 16) {
@@ -1018,6 +1026,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     const int nT = PT.depth_f ? (int)nc[0] : 0, nN = PN.depth_f ? (int)nc[1] : 0;
     const GenoOut tg = genotypes_el<NS, !DEEP>(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
     tick(3);
+    if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[1], (unsigned long long)tg.cyc_fold);  // (inside phase 3)
     if (dbg & 8192) continue;  // ablation: up to the tumor genotypes
     if (tg.G == 0) continue;
     const bool t_var = m.is_var[tg.bi] || m.is_var[tg.bj];
