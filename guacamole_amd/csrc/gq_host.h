@@ -365,24 +365,40 @@ __device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const Sl
 
 // A piece of a 64-read batch, for the word-per-lane fills (slice_fill): set up once by the
 // piece's lane, read from LDS by the lanes of its words.
-struct PieceMeta {
+struct __attribute__((aligned(16))) PieceMeta {
   int64_t p0;         // pool offset of locus 0: a column-eligible read's base / quality at locus l is p0 + l
   int32_t s, e;       // the read's [start, end)
   int32_t s0, row;    // the piece's first column and its row
   uint32_t info, mq;  // ColDesc info, mapping quality
   uint32_t ev[4];     // MD events at the piece's loci: bit i = locus 8 s0 + i (margin fill)
 };
+static_assert(sizeof(PieceMeta) == 48, "PieceMeta: three 16-byte LDS reads");
+
+// Inclusive prefix maximum over the 64 lanes of a wave (values >= 0), DPP as wave_incl_scan.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
 
 // Once per word of the slice's pieces, a lane per word (a batch's words in piece order:
 // consecutive words of a piece on consecutive lanes, so the loads of a piece's bases and the
-// stores of its row coalesce): raw = fetch(read, meta, column) (the word's loads), then
-// emit(raw, read, meta, column).  Each lane takes kU words per round and issues all their loads
-// before the first emit (one load latency per kU words).  setup(read, meta) runs once per piece
-// on the piece's lane and returns false to drop it.  meta: this wave's 64 LDS entries.  emit
-// runs in uniform control flow (act: the lane holds a word).
-template <class S, class F, class E>
+// stores of its row coalesce): raw = fetch(read, meta, column, events) (the word's loads), then
+// emit(act, raw, read, meta, column, events).  events: the word's eight MD-event bits (EV only).
+// Each lane takes kU words per round and issues all their loads before the first emit.  A word
+// finds its piece without a search: the pieces starting inside the round's words mark their first
+// word in LDS (owner), a prefix maximum carries each mark over the piece's words, and one ballot
+// gives the piece already running at each 64-word window's start.  setup(read, meta) runs once
+// per piece on the piece's lane and returns false to drop it.  meta: this wave's 64 LDS entries;
+// owner: its kU * 64 LDS words.
+template <bool EV, class S, class F, class E>
 __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
-                                           PieceMeta *__restrict__ meta, S &&setup, F &&fetch, E &&emit) {
+                                           PieceMeta *__restrict__ meta, uint32_t *__restrict__ owner, S &&setup,
+                                           F &&fetch, E &&emit) {
   constexpr int kU = 4;
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
@@ -404,29 +420,55 @@ __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W,
     const uint32_t len = (uint32_t)sl;
     const uint32_t incl = wave_incl_scan(len), ex = incl - len;
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t w0 = 0; w0 < tot; w0 += 64 * kU) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) owner[64 * u + lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (len > 0 && ex > w0 && ex < w0 + 64 * kU) owner[ex - w0] = (uint32_t)lane + 1;  // the piece's first word
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       int kk[kU];
       int32_t col[kU];
       bool act[kU];
-      decltype(fetch((int64_t)0, meta[0], (int32_t)0)) raw[kU];
+      PieceMeta pm[kU];
+      uint32_t evb[kU];
+      decltype(fetch((int64_t)0, pm[0], (int32_t)0, 0u)) raw[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const uint32_t w = w0 + 64 * u + (uint32_t)lane;
-        int k = 0;  // the last lane whose words start at or before w
-#pragma unroll
-        for (int b = 32; b >= 1; b >>= 1)
-          if ((uint32_t)__shfl((int)ex, k + b, 64) <= w) k += b;
+        const uint32_t wb = w0 + 64 * u, w = wb + (uint32_t)lane;
+        const unsigned long long run = __ballot(len > 0 && ex <= wb);  // the last of them runs at wb
+        const uint32_t k_at = run ? 64u - (uint32_t)__clzll((long long)run) : 0u;  // its lane + 1
+        const uint32_t k1 = max(wave_incl_max(owner[64 * u + lane]), k_at);
         act[u] = w < tot;
-        kk[u] = act[u] ? k : 0;
-        col[u] = meta[kk[u]].s0 + (int32_t)(w - (uint32_t)__shfl((int)ex, k, 64));
+        const int k = act[u] ? (int)k1 - 1 : 0;
+        kk[u] = k;
+        const uint4 *src = reinterpret_cast<const uint4 *>(meta + k);
+        const uint4 a = src[0], b = src[1];
+        PieceMeta &m = pm[u];
+        m.p0 = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
+        m.s = (int32_t)a.z;
+        m.e = (int32_t)a.w;
+        m.s0 = (int32_t)b.x;
+        m.row = (int32_t)b.y;
+        m.info = b.z;
+        m.mq = b.w;
+        const uint32_t kex = (uint32_t)__shfl((int)ex, k, 64);
+        col[u] = m.s0 + (int32_t)(w - kex);
+        evb[u] = 0;
+        if constexpr (EV) {
+          const uint4 c = src[2];
+          const int32_t i0 = 8 * (col[u] - m.s0);  // bit of the word's first locus
+          const int iw = i0 >> 5;
+          const uint32_t ew = (iw & 2) ? ((iw & 1) ? c.w : c.z) : ((iw & 1) ? c.y : c.x);
+          evb[u] = (ew >> (i0 & 31)) & 0xFFu;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)
-        if (act[u]) raw[u] = fetch(r0 + kk[u], meta[kk[u]], col[u]);
+        if (act[u]) raw[u] = fetch(r0 + kk[u], pm[u], col[u], evb[u]);
 #pragma unroll
-      for (int u = 0; u < kU; ++u) emit(act[u], raw[u], r0 + kk[u], meta[kk[u]], col[u]);
+      for (int u = 0; u < kU; ++u) emit(act[u], raw[u], r0 + kk[u], pm[u], col[u], evb[u]);
     }
     __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

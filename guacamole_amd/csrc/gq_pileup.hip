@@ -479,14 +479,16 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
 // assigned, stored; pbad slices stay zero: their blocks go to the walker).
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   __shared__ PieceMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][4 * 64];
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
+  uint32_t *owner = s_owner[threadIdx.x >> 6];
   const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * R.srow[slot];  // the slice's block rows
-    slice_fill(
-        R, slice_stored(R, slot), R.prow + R.soff[slot], meta,
+    slice_fill<false>(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
         [&](int64_t r, PieceMeta &m) {
           const ColDesc d = R.cdesc[r];
           m.s = d.start;
@@ -496,8 +498,8 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
           m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
           return true;
         },
-        [&](int64_t r, const PieceMeta &m, int32_t col) { return proj_fetch(R, r, m, col); },
-        [&](bool act, const ProjRaw &x, int64_t, const PieceMeta &m, int32_t col) {
+        [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t) { return proj_fetch(R, r, m, col); },
+        [&](bool act, const ProjRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t) {
           if (act)
             out[16 * (int64_t)m.row + (col & 15)] =
                 x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);

@@ -1690,7 +1690,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     HIP_TRY(c->cands.ensure(sizeof(CandRec) * (size_t)std::max<unsigned long long>(n_cand, 1)));
     hipLaunchKernelGGL(cand_prep, dim3((unsigned)((kParts + kSomWaves - 1) / kSomWaves)), dim3(kBlock), 0, c->stream,
                        (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, (const ComplexItem *)c->cplx.p, og,
-                       (const Counters *)ctr, sw, (CandRec *)c->cands.p);
+                       (const Counters *)ctr, sw, t->d, n->d, (CandRec *)c->cands.p);
     HIP_TRY(hipGetLastError());
     front_ms = 0;
     if (!split) {

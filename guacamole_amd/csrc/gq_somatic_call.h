@@ -79,60 +79,6 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   return m;
 }
 
-// K lockstep wave_first_true searches (each over its own [lo, hi)): every round issues all
-// unfinished searches' probes before any ballot is read.  pred(k, index) is monotone.
-template <int K, class P>
-__device__ __forceinline__ void wave_first_true_k(const int64_t (&lo0)[K], const int64_t (&hi0)[K], P &&pred,
-                                                  int64_t (&out)[K]) {
-  const int lane = threadIdx.x & 63;
-  int64_t lo[K], hi[K];
-  bool done[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    lo[k] = lo0[k];
-    hi[k] = hi0[k];
-    done[k] = false;
-    out[k] = hi0[k];
-  }
-  for (;;) {
-    bool all = true;
-#pragma unroll
-    for (int k = 0; k < K; ++k) all = all && done[k];
-    if (all) break;
-    bool hit[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int64_t s = hi[k] - lo[k] > 64 ? (hi[k] - lo[k] + 63) / 64 : 1;
-      const int64_t p = lo[k] + (int64_t)lane * s;
-      hit[k] = !done[k] && (p >= hi[k] || pred(k, p));
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (done[k]) continue;
-      const unsigned long long b = __ballot(hit[k]);
-      if (hi[k] - lo[k] > 64) {
-        const int64_t step = (hi[k] - lo[k] + 63) / 64;
-        if (!b) {
-          lo[k] = lo[k] + 63 * step + 1;
-          continue;
-        }
-        const int f = __ffsll((long long)b) - 1;
-        if (f == 0) {
-          out[k] = lo[k];
-          done[k] = true;
-          continue;
-        }
-        const int64_t nh = lo[k] + (int64_t)f * step;
-        lo[k] = lo[k] + (int64_t)(f - 1) * step + 1;
-        hi[k] = nh < hi[k] ? nh : hi[k];
-      } else {
-        out[k] = b ? lo[k] + (__ffsll((long long)b) - 1) : hi[k];
-        done[k] = true;
-      }
-    }
-  }
-}
-
 // The pileup's allele table (a sample's distinct alleles; entry j on lane j & 63, register
 // slot j >> 6) and its totals.
 template <int NS>
@@ -559,7 +505,8 @@ struct DeepIO {
 // order, so the caller loads one record (one candidate ahead) instead of walking the item ->
 // tile -> window -> initial group chain of dependent loads on its critical path.
 struct CandRec {
-  int64_t rb[2], re[2];  // the tile's read windows (tumor, normal)
+  int64_t rb[2];         // the tile's first read (tumor, normal): element read offsets are relative to it
+  int64_t ra[2], rz[2];  // the reads that can cover pos: [first pmax_end > pos, first start > pos) of the tile window
   int64_t ord0;          // output ordinal of the tile's first locus
   int32_t pos, contig, L0, flags;
   int32_t win, tile;
@@ -567,10 +514,11 @@ struct CandRec {
 };
 
 // The candidates' records, a wave per output partition (lanes over its items: no search for
-// the partition of a flat index).
+// the partition of a flat index), each with the binary searches for its covering-read range
+// done here, a thread per candidate, where half a million of them overlap.
 __global__ void cand_prep(const Tile *__restrict__ tiles_t, const Tile *__restrict__ tiles_n,
                           const ComplexItem *__restrict__ items, OutGeom og, const Counters *__restrict__ ctr, SomWin sw,
-                          CandRec *__restrict__ out) {
+                          DevReads RT, DevReads RN, CandRec *__restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -582,8 +530,28 @@ __global__ void cand_prep(const Tile *__restrict__ tiles_t, const Tile *__restri
       CandRec c;
       c.rb[0] = tt.rb;
       c.rb[1] = tn.rb;
-      c.re[0] = tt.re;
-      c.re[1] = tn.re;
+      {  // the four binary searches in one loop (independent dependence chains)
+        const int32_t pos = item.pos;
+        int64_t lo[4] = {tt.rb, tt.rb, tn.rb, tn.rb}, hi[4] = {tt.re, tt.re, tn.re, tn.re};
+        for (;;) {
+          bool any = false;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (lo[q] >= hi[q]) continue;
+            any = true;
+            const int64_t mid = (lo[q] + hi[q]) >> 1;
+            const DevReads &R = q < 2 ? RT : RN;
+            const bool past = (q & 1) ? R.start[mid] > pos : R.pmax_end[mid] > pos;
+            if (past) hi[q] = mid;
+            else lo[q] = mid + 1;
+          }
+          if (!any) break;
+        }
+        c.ra[0] = lo[0];
+        c.rz[0] = lo[1];
+        c.ra[1] = lo[2];
+        c.rz[1] = lo[3];
+      }
       c.ord0 = tt.ordinal0;
       c.pos = item.pos;
       c.contig = tt.contig;
@@ -612,19 +580,10 @@ __device__ __forceinline__ bool call_front(const CandRec &cr, int64_t it, const 
                                            int dbg, const DeepIO &dio, uint32_t (&nc)[2], uint32_t (&mask)[2]) {
   const int lane = threadIdx.x & 63;
   const int32_t pos = cr.pos;
-  const int64_t rb[2] = {cr.rb[0], cr.rb[1]}, re[2] = {cr.re[0], cr.re[1]};
-  // ---- covering reads of both samples: [first pmax_end > pos, first start > pos) of each
-  //      tile window, the four searches in lockstep
-  int64_t ra[2], rz[2];
-  {
-    const int64_t lo[4] = {rb[0], rb[0], rb[1], rb[1]}, hi[4] = {re[0], re[0], re[1], re[1]};
-    int64_t out[4];
-    wave_first_true_k<4>(lo, hi, [&](int k, int64_t r) {
-      const DevReads &R = k < 2 ? RT : RN;
-      return (k & 1) ? R.start[r] > pos : R.pmax_end[r] > pos;
-    }, out);
-    ra[0] = out[0], rz[0] = out[1], ra[1] = out[2], rz[1] = out[3];
-  }
+  const int64_t rb[2] = {cr.rb[0], cr.rb[1]};
+  // ---- covering reads of both samples: in [first pmax_end > pos, first start > pos) of each
+  //      tile window (cand_prep's searches)
+  const int64_t ra[2] = {cr.ra[0], cr.ra[1]}, rz[2] = {cr.rz[0], cr.rz[1]};
   nc[0] = nc[1] = 0;
   {
     const int64_t span = max(rz[0] - ra[0], rz[1] - ra[1]);

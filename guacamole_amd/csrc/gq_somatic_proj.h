@@ -100,11 +100,9 @@ struct MarginRaw {
   uint2 word;   // general CIGAR: the word itself
   uint32_t valid, gen;  // valid: byte mask of loci inside the read
 };
-__device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, int32_t col, uint64_t q, uint32_t valid,
+__device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, uint64_t q, uint32_t valid, uint32_t evb,
                                                const uint8_t *__restrict__ tab) {
-  const uint8_t *tm = tab + (m.mq << 8);
-  const int32_t i0 = 8 * (col - m.s0);                        // bit of locus 8 col in m.ev
-  const uint32_t evb = (m.ev[i0 >> 5] >> (i0 & 31)) & 0xFFu;  // events at the word's loci (m: in LDS)
+  const uint8_t *tm = tab + (m.mq << 8);  // evb: the MD events at the word's loci
   uint32_t v[2] = {0x80808080u, 0x80808080u};
 #pragma unroll
   for (int q8 = 0; q8 < 8; ++q8) {
@@ -116,7 +114,7 @@ __device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, int32_t col, 
   return make_uint2(v[0], v[1]);
 }
 __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col,
-                                                  const uint8_t *__restrict__ tab) {
+                                                  uint32_t evb, const uint8_t *__restrict__ tab) {
   const int32_t s = m.s, e = m.e;
   const int32_t lb = 8 * col;
   MarginRaw x{0, make_uint2(0x80808080u, 0x80808080u), 0, 0};
@@ -155,7 +153,7 @@ __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, 
       }
     }
   }
-  x.word = margin_terms8(m, col, q, valid, tab);
+  x.word = margin_terms8(m, q, valid, evb, tab);
   x.gen = 1;
   return x;
 }
@@ -167,20 +165,22 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
                                                   const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
                                                   uint8_t *__restrict__ mnb) {
   __shared__ PieceMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][4 * 64];
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
+  uint32_t *owner = s_owner[threadIdx.x >> 6];
   const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * R.srow[slot];  // the slice's block rows
     bool none = false;
-    slice_fill(
-        R, slice_stored(R, slot), R.prow + R.soff[slot], meta,
+    slice_fill<true>(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
         [&](int64_t r, PieceMeta &m) { return margin_setup(R, r, min_mapq, m); },
-        [&](int64_t r, const PieceMeta &m, int32_t col) { return margin_fetch(R, r, m, col, tab); },
-        [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col) {
+        [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t evb) { return margin_fetch(R, r, m, col, evb, tab); },
+        [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t evb) {
           if (act) {
-            const uint2 w = x.gen ? x.word : margin_terms8(m, col, x.q, x.valid, tab);
+            const uint2 w = x.gen ? x.word : margin_terms8(m, x.q, x.valid, evb, tab);
             out[16 * (int64_t)m.row + (col & 15)] = w;
             auto has = [](uint32_t v) {  // a zero byte
               return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
