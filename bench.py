@@ -568,8 +568,8 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
                          "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": b_alg, "read_bytes_per_launch": read_bytes,
                          "traffic_source": None if traffic is None else pmc["source"]},
-            "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), pmc, "somatic_call_k<false>"),
-            "deep_caller_roofline": caller_roofline(float(np.mean(stages["deep_ms"])), pmc, "somatic_call_k<true>"),
+            "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), pmc, "somatic_call_k<false,false"),
+            "deep_caller_roofline": caller_roofline(float(np.mean(stages["deep_ms"])), pmc, "somatic_call_k<true,"),
             "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s,
             # a cold call on resident reads: both sets' upload-time derivation + the first call
             # (the tumor's projection and margin projection; the normal needs neither)
@@ -603,7 +603,9 @@ def caller_roofline(call_ms: float, pmc, kernel: str):
     readings); the wait share says what bounds it instead."""
     if pmc is None or call_ms <= 0:
         return None
-    pm = pmc["kernels"].get(kernel, {})
+    # the PMC file names kernels with their template arguments: "somatic_call_k<false, false, 3>"
+    kernel, pm = next(((k, v) for k, v in sorted(pmc["kernels"].items())
+                       if k.replace(" ", "").startswith(kernel.rstrip(">"))), (kernel, {}))
     insts = pm.get("SQ_INSTS_VALU")
     if not insts:
         return None
