@@ -542,7 +542,8 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)
     pmc = somatic_pmc("panel" if tdepth >= 500 else "chr1", L, tdepth, ndepth)
-    traffic = None if pmc is None else pmc["kernels"].get("somatic_proj", {}).get("hbm_bytes_per_launch")
+    traffic = None if pmc is None else next(
+        (v.get("hbm_bytes_per_launch") for k, v in sorted(pmc["kernels"].items()) if k.startswith("somatic_proj")), None)
     return {"metric": "somatic-standard loci/sec, tumor %gx / normal %gx" % (tdepth, ndepth),
             "value": visited * steps / el, "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
             "warmup": warmup,

@@ -275,6 +275,15 @@ __device__ __forceinline__ SliceWin slice_stored(const DevReads &R, int64_t slot
 
 // Read r's piece in a slice: first column (slice-relative s0 - qc0 = its offset) and length in
 // columns; sl = 0: no piece (the read ends before the slice, or the projection cannot take it).
+__device__ __forceinline__ void piece_of(const ProjRec &p, int32_t qc0, int32_t &s0, int32_t &sl) {
+  s0 = qc0;
+  sl = 0;
+  if (p.col1 != kProjNone) {
+    s0 = p.col0 > qc0 ? p.col0 : qc0;
+    const int32_t e = p.col1 < qc0 + 16 ? p.col1 : qc0 + 16;
+    sl = e > s0 ? e - s0 : 0;
+  }
+}
 __device__ __forceinline__ void slice_piece(const DevReads &R, int64_t r, int32_t qc0, int32_t &s0, int32_t &sl) {
   s0 = qc0;
   sl = 0;
@@ -392,29 +401,45 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 // Each lane takes kU words per round and issues all their loads before the first emit.  A word
 // finds its piece without a search: the pieces starting inside the round's words mark their first
 // word in LDS (owner), a prefix maximum carries each mark over the piece's words, and one ballot
-// gives the piece already running at each 64-word window's start.  setup(read, meta) runs once
-// per piece on the piece's lane and returns false to drop it.  meta: this wave's 64 LDS entries;
+// gives the piece already running at each 64-word window's start.  setup(read, meta, md_off)
+// runs once per piece on the piece's lane (meta's read fields filled) and returns false to drop it.  meta: this wave's 64 LDS entries;
 // owner: its kU * 64 LDS words.
-template <bool EV, class S, class F, class E>
+template <bool EV, int kU, class S, class F, class E>
 __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W, const uint16_t *__restrict__ rows,
                                            PieceMeta *__restrict__ meta, uint32_t *__restrict__ owner, S &&setup,
                                            F &&fetch, E &&emit) {
-  constexpr int kU = 4;
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
     int32_t s0 = W.qc0, sl = 0;
-    if (r < W.rz) {
-      const uint16_t k = rows[r - W.ra];
-      if (k != 0xFFFFu) {
-        slice_piece(R, r, W.qc0, s0, sl);
-        if (sl > 0) {
-          PieceMeta m;
-          m.s0 = s0;
-          m.row = k;
-          if (setup(r, m)) meta[lane] = m;
-          else sl = 0;
-        }
+    // the read's records in one round, loaded whether or not it has a piece here (a valid read
+    // index either way): no load waits on another
+    const bool in = r < W.rz;
+    const int64_t rr = in ? r : W.ra;
+    const uint16_t k = rows[rr - W.ra];
+    const ProjRec pr = R.prec[rr];
+    const ColDesc d = R.cdesc[rr];
+    const int64_t so = R.seq_off[rr];
+    const int32_t ld = R.lead[rr];
+    uint32_t mq = 0;
+    int64_t mdo = 0;
+    if constexpr (EV) {
+      mq = R.mapq[rr];
+      mdo = R.md_off[rr];
+    }
+    if (in && k != 0xFFFFu) {
+      piece_of(pr, W.qc0, s0, sl);
+      if (sl > 0) {
+        PieceMeta m;
+        m.s0 = s0;
+        m.row = k;
+        m.s = d.start;
+        m.e = d.end;
+        m.info = d.info;
+        m.mq = mq;
+        m.p0 = so + (ld > 0 ? ld : 0) - d.start;
+        if (setup(r, m, mdo)) meta[lane] = m;
+        else sl = 0;
       }
     }
     const uint32_t len = (uint32_t)sl;

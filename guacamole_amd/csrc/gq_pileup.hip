@@ -477,6 +477,9 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
 
 // The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
 // assigned, stored; pbad slices stay zero: their blocks go to the walker).
+// KU: words per lane per round (GQ_FILL_U picks 1 or 4: fewer registers and more waves, or more
+// loads in flight per wave)
+template <int KU>
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   __shared__ PieceMeta s_meta[4][64];
   __shared__ uint32_t s_owner[4][4 * 64];
@@ -487,17 +490,9 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * R.srow[slot];  // the slice's block rows
-    slice_fill<false>(
+    slice_fill<false, KU>(
         R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
-        [&](int64_t r, PieceMeta &m) {
-          const ColDesc d = R.cdesc[r];
-          m.s = d.start;
-          m.e = d.end;
-          m.info = d.info;
-          m.mq = 0;
-          m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
-          return true;
-        },
+        [&](int64_t, PieceMeta &, int64_t) { return true; },
         [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t) { return proj_fetch(R, r, m, col); },
         [&](bool act, const ProjRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t) {
           if (act)
@@ -2960,7 +2955,9 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
   d->owned.push_back(pe);
   if (n_sl > 0) {
     const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-    hipLaunchKernelGGL(proj_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
+    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 4;
+    auto kf = fill_u == 1 ? proj_fill<1> : proj_fill<4>;
+    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
     HIP_TRY(hipGetLastError());
   }
   if (n > 0) {

@@ -56,33 +56,40 @@ typedef uint64_t gq_u64m __attribute__((aligned(1)));  // unaligned 8-byte loads
 // a bit mask (MD offsets are reference offsets from the read's start, sorted).  Reads the mapq
 // filter drops (QualityAlignedReadsFilter, PileupElementsFilter.scala:25-36) are skipped: their
 // loci keep the pool's kMargin8Zero fill.
-__device__ __forceinline__ bool margin_setup(const DevReads &R, int64_t r, int min_mapq, PieceMeta &m) {
-  const int mq = (int)R.mapq[r];
-  if (min_mapq > 0 && mq < min_mapq) return false;
-  const ColDesc d = R.cdesc[r];
-  m.s = d.start;
-  m.e = d.end;
-  m.info = d.info;
-  m.mq = (uint32_t)mq;
-  m.p0 = R.seq_off[r] + (R.lead[r] > 0 ? R.lead[r] : 0) - d.start;
-  const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
-  const uint32_t *ev = R.md_ev + R.md_off[r];
-  const int32_t o0 = 8 * m.s0 - d.start;  // offset of the piece's first locus
-  int k = 0, hi = nmd;
-  while (k < hi) {
-    const int mid = (k + hi) >> 1;
-    if ((int32_t)(ev[mid] >> 8) < o0) k = mid + 1;
-    else hi = mid;
-  }
+__device__ __forceinline__ bool margin_setup(const DevReads &R, int min_mapq, int64_t md_off, PieceMeta &m) {
+  if (min_mapq > 0 && (int)m.mq < min_mapq) return false;
+  const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
+  const uint32_t *ev = R.md_ev + md_off;
+  const int32_t o0 = 8 * m.s0 - m.s;  // offset of the piece's first locus
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // (registers: a dynamic index would go to scratch)
-  for (; k < nmd; ++k) {
-    const int32_t i = (int32_t)(ev[k] >> 8) - o0;
-    if (i >= 128) break;
+  auto mark = [&](uint32_t v) {
+    const int32_t i = (int32_t)(v >> 8) - o0;
+    if (i < 0 || i >= 128) return;
     const uint32_t bit = 1u << (i & 31);
     e0 |= (i >> 5) == 0 ? bit : 0u;
     e1 |= (i >> 5) == 1 ? bit : 0u;
     e2 |= (i >> 5) == 2 ? bit : 0u;
     e3 |= (i >> 5) == 3 ? bit : 0u;
+  };
+  if (nmd <= 4) {  // the common read: its (few) events in one round of loads
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nmd) mark(v[k]);
+  } else {  // the first event at or past the piece's first locus, then the piece's events
+    int k = 0, hi = nmd;
+    while (k < hi) {
+      const int mid = (k + hi) >> 1;
+      if ((int32_t)(ev[mid] >> 8) < o0) k = mid + 1;
+      else hi = mid;
+    }
+    for (; k < nmd; ++k) {
+      const uint32_t v = ev[k];
+      if ((int32_t)(v >> 8) - o0 >= 128) break;
+      mark(v);
+    }
   }
   m.ev[0] = e0;
   m.ev[1] = e1;
@@ -161,6 +168,7 @@ __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, 
 // The margin projection of the tumor reads, laid out as `proj` (a byte per projection nibble:
 // word w of the row pool at mproj + 8 w), one wave per slice, a lane per word (the rows row_count
 // assigned, stored); mnb marks slices holding a kMargin8None term.
+template <int KU>
 __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, int min_mapq,
                                                   const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
                                                   uint8_t *__restrict__ mnb) {
@@ -174,9 +182,9 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     if (R.pbad[slot]) continue;  // uniform
     uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * R.srow[slot];  // the slice's block rows
     bool none = false;
-    slice_fill<true>(
+    slice_fill<true, KU>(
         R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
-        [&](int64_t r, PieceMeta &m) { return margin_setup(R, r, min_mapq, m); },
+        [&](int64_t, PieceMeta &m, int64_t mdo) { return margin_setup(R, min_mapq, mdo, m); },
         [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t evb) { return margin_fetch(R, r, m, col, evb, tab); },
         [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t evb) {
           if (act) {
