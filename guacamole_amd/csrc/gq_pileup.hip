@@ -478,7 +478,7 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
 // The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
 // assigned, stored; pbad slices stay zero: their blocks go to the walker).
 // KU: words per lane per round (GQ_FILL_U picks 1 or 4: fewer registers and more waves, or more
-// loads in flight per wave)
+// loads in flight per wave; measured at chr20 60x: 1 word 4.8 ms, 4 words 5.8 ms, so 1 is the default)
 template <int KU>
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   __shared__ PieceMeta s_meta[4][64];
@@ -2955,7 +2955,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
   d->owned.push_back(pe);
   if (n_sl > 0) {
     const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 4;
+    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;
     auto kf = fill_u == 1 ? proj_fill<1> : proj_fill<4>;
     hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
     HIP_TRY(hipGetLastError());

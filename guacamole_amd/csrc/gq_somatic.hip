@@ -1274,7 +1274,7 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, incl_align ? 1 : 0, (uint8_t *)tab);
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
-    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 4;  // A/B: 1 or 4 words per lane
+    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;  // A/B: 1 or 4 words per lane
     auto kf = fill_u == 1 ? mproj_fill<1> : mproj_fill<4>;
     hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0, c->stream,
                        t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);

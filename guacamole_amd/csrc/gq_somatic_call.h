@@ -18,7 +18,8 @@
 //                 listed pileup: no depth limit.  Also runs the heap-order loci (amb_in).
 #pragma once
 
-constexpr int kFastCap = 128;  // elements per sample held in LDS by the fast kernel
+constexpr int kFastCap = 128;      // elements per sample held in LDS by the fast kernel
+constexpr int kDeepTermCap = 256;  // deep kernel: elements per LDS chunk of the likelihood fold
 
 // Element record (16 bytes), one per covering read in pileup element order:
 //   x  rp    read position of the element (SNV / DEL: its base; INS: its first alt byte)
@@ -46,7 +47,8 @@ struct CallMem {
   int16_t *order;   // [64 kSlots]
   uint8_t *is_var;  // [64 kSlots]
   double *ll;       // [maxG]
-  struct TermRec *terms;  // [cap] fast kernel (LDS): each element's log terms + table index; deep: nullptr
+  struct TermRec *terms;  // [tcap] LDS: a chunk of elements' log terms + table indexes (the fold)
+  int tcap;
   const double *succ;     // PhredUtils.phredToSuccessProbability table (g_succ) copied to LDS
   int cap, maxG;
 };
@@ -73,7 +75,8 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   m.order = (int16_t *)p;
   p += 64 * kSlots * 2;
   m.is_var = p;
-  m.terms = nullptr;
+  m.terms = nullptr;  // (the kernel points it at its LDS)
+  m.tcap = 0;
   m.cap = cap;
   m.maxG = maxG;
   return m;
@@ -140,7 +143,7 @@ struct GenoOut {
 // the variant genotypes' likelihoods in the iteration order of the immutable Map `toMap`
 // builds (SomaticStandardCaller.scala:206-217): generation order up to four genotypes, the
 // HashTrieMap's beyond (gq_scala_order.h).
-template <int NS, bool LDS_TERMS>
+template <int NS>
 __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS> &P, const uint4 *el, int n_el, int32_t pos,
                                                 bool include_alignment, bool with_var_sum, CallMem &m, Counters *ctr) {
   const int lane = threadIdx.x & 63;
@@ -203,69 +206,47 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
       t0 = sm::log(pw + pw);
     }
   };
-  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element
-  if constexpr (LDS_TERMS) {
-    // fast kernel: the terms go to LDS records (lanes = elements), then each genotype lane folds
-    // them four records per batch, the batch's loads issued before its adds
-    for (int c0 = 0; c0 < n_el; c0 += 64) {
-      const int k = c0 + lane;
-      if (k >= n_el) continue;
-      TermRec t;
-      elem_terms(k, t.tj, t.t0, t.th, t.t2);
-      t.pad = 0;
-      m.terms[k] = t;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int g0 = 0; g0 < G; g0 += 64) {
-      const int g = g0 + lane;
-      int i = 0, j = 0;
-      if (g < G) genotype_index(g, n, i, j);
-      const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
-      auto pick = [&](const TermRec &t) {
-        const int sel = (ei == t.tj ? 1 : 0) + (ej == t.tj ? 1 : 0);
-        return sel == 0 ? t.t0 : sel == 1 ? t.th : t.t2;
-      };
-      double agg = 0.0;
-      int k = n_el - 1;
-      for (; k >= 3; k -= 4) {
-        const TermRec a = m.terms[k], b = m.terms[k - 1], c = m.terms[k - 2], d = m.terms[k - 3];
+  // the row fold, lanes = genotypes: Colt's aggregate starts from the LAST element.  The terms
+  // go to LDS records (lanes = elements) m.tcap elements at a time, last chunk first, and each
+  // genotype lane folds a chunk four records per batch, the batch's loads issued before its adds.
+  for (int g0 = 0; g0 < G; g0 += 64) {
+    const int g = g0 + lane;
+    int i = 0, j = 0;
+    if (g < G) genotype_index(g, n, i, j);
+    const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
+    auto pick = [&](const TermRec &t) {
+      const int sel = (ei == t.tj ? 1 : 0) + (ej == t.tj ? 1 : 0);
+      return sel == 0 ? t.t0 : sel == 1 ? t.th : t.t2;
+    };
+    double agg = 0.0;
+    for (int cend = n_el; cend > 0; cend -= m.tcap) {
+      const int cbeg = cend > m.tcap ? cend - m.tcap : 0;
+      for (int c0 = cbeg; c0 < cend; c0 += 64) {
+        const int k = c0 + lane;
+        if (k >= cend) continue;
+        TermRec t;
+        elem_terms(k, t.tj, t.t0, t.th, t.t2);
+        t.pad = 0;
+        m.terms[k - cbeg] = t;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const TermRec *tr = m.terms - cbeg;  // tr[k] = element k's record
+      int k = cend - 1;
+      for (; k >= cbeg + 3; k -= 4) {
+        const TermRec a = tr[k], b = tr[k - 1], c = tr[k - 2], d = tr[k - 3];
         const double pa = pick(a), pb = pick(b), pc = pick(c), pd = pick(d);
         agg = agg + pa;
         agg = agg + pb;
         agg = agg + pc;
         agg = agg + pd;
       }
-      for (; k >= 0; --k) agg = agg + pick(m.terms[k]);
-      if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
+      for (; k >= cbeg; --k) agg = agg + pick(tr[k]);
+      __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the records)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-  } else {
-    // deep kernel (records in global scratch): lane k of each 64-element chunk, last chunk first,
-    // computes its element's terms and the genotype lanes take them by readlane, element by
-    // element in descending order (no memory round trip on the fold's dependence chain)
-    for (int g0 = 0; g0 < G; g0 += 64) {
-      const int g = g0 + lane;
-      int i = 0, j = 0;
-      if (g < G) genotype_index(g, n, i, j);
-      const int ei = g < G ? m.order[i] : -1, ej = g < G ? m.order[j] : -1;
-      double agg = 0.0;
-      for (int c0 = ((n_el - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {
-        const int k = c0 + lane;
-        int tjl = -1;
-        double t2 = 0.0, th = 0.0, t0 = 0.0;
-        if (k < n_el) elem_terms(k, tjl, t0, th, t2);
-        for (int kk = min(63, n_el - 1 - c0); kk >= 0; --kk) {
-          const int tj = __builtin_amdgcn_readlane(tjl, kk);
-          const double a0 = lane_f64(t0, kk), ah = lane_f64(th, kk), a2 = lane_f64(t2, kk);
-          const int sel = (ei == tj ? 1 : 0) + (ej == tj ? 1 : 0);
-          agg = agg + (sel == 0 ? a0 : sel == 1 ? ah : a2);
-        }
-      }
-      if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
-    }
+    if (g < G) m.ll[g] = agg + sm::log(1.0) - ln2d;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   res.cyc_fold = __builtin_readcyclecounter() - cyc0;
   double tot = 0.0;
   for (int g0 = 0; g0 < G; g0 += 64) {
@@ -423,11 +404,21 @@ __device__ __forceinline__ void evidence_pair(const Pile<NS> &PT, const Pile<NS>
     const int s = (lane >> 1) & 1, f = lane & 1;
     const uint32_t ns = s ? n[1] : n[0];
     const uint32_t nmax = n[0] > n[1] ? n[0] : n[1];
-    for (uint32_t k = 0; k < nmax; ++k) {
-      if (lane < 4 && k < ns) {
-        const uint32_t v = m.tmp[s * m.cap + k];
-        const double x = f ? (double)(int8_t)((v >> 8) & 0xFFu) : (double)(v & 0xFFu);
-        mu += (x - mu) / (double)(k + 1);
+    for (uint32_t k0 = 0; k0 < nmax; k0 += 64) {
+      // 64 values of each sample in one round of loads (lane j: value k0 + j), then the running
+      // means by readlane (no memory on the loop's dependence chain)
+      const uint32_t v0 = k0 + lane < n[0] ? m.tmp[k0 + lane] : 0u;
+      const uint32_t v1 = k0 + lane < n[1] ? m.tmp[m.cap + k0 + lane] : 0u;
+      const uint32_t top = nmax - k0 < 64u ? nmax - k0 : 64u;
+      for (uint32_t kk = 0; kk < top; ++kk) {
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)v0, (int)kk);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)v1, (int)kk);
+        const uint32_t k = k0 + kk;
+        if (lane < 4 && k < ns) {
+          const uint32_t v = s ? a1 : a0;
+          const double x = f ? (double)(int8_t)((v >> 8) & 0xFFu) : (double)(v & 0xFFu);
+          mu += (x - mu) / (double)(k + 1);
+        }
       }
     }
   }
@@ -756,7 +747,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   __shared__ int16_t s_order[DEEP ? 1 : FW][64 * NS];
   __shared__ uint8_t s_var[DEEP ? 1 : FW][64 * NS];
   __shared__ double s_ll[DEEP ? 1 : FW][kMaxG];
-  __shared__ TermRec s_terms[DEEP ? 1 : FW][kFastCap];
+  __shared__ TermRec s_terms[FW][DEEP ? kDeepTermCap : kFastCap];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // (wave-uniform, and known to be: the candidate records then load into scalar registers)
   const int64_t gwave = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -764,6 +755,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   CallMem m;
   if constexpr (DEEP) {
     m = deep_mem(dio.scratch + (size_t)gwave * deep_wave_bytes(dio.scap, dio.maxG), dio.scap, dio.maxG);
+    m.terms = s_terms[wv];
+    m.tcap = kDeepTermCap;
   } else {
     m.cov[0] = s_cov[wv][0];
     m.cov[1] = s_cov[wv][1];
@@ -774,6 +767,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.is_var = s_var[wv];
     m.ll = s_ll[wv];
     m.terms = s_terms[wv];
+    m.tcap = kFastCap;
     m.cap = kFastCap;
     m.maxG = kMaxG;
   }
@@ -983,7 +977,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     }
     // the multi-allelic filter empties a pileup: no element passes then
     const int nT = PT.depth_f ? (int)nc[0] : 0, nN = PN.depth_f ? (int)nc[1] : 0;
-    const GenoOut tg = genotypes_el<NS, !DEEP>(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
+    const GenoOut tg = genotypes_el(RT, PT, m.el[0], nT, pos, true, false, m, ctr);
     tick(3);
     if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[1], (unsigned long long)tg.cyc_fold);  // (inside phase 3)
     if (dbg & 8192) continue;  // ablation: up to the tumor genotypes
@@ -991,7 +985,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     const bool t_var = m.is_var[tg.bi] || m.is_var[tg.bj];
     if (!t_var) continue;
     const AlleleDesc a1 = pile_entry(PT, tg.bi), a2 = pile_entry(PT, tg.bj);
-    const GenoOut ng = genotypes_el<NS, !DEEP>(RN, PN, m.el[1], nN, pos, false, true, m, ctr);
+    const GenoOut ng = genotypes_el(RN, PN, m.el[1], nN, pos, false, true, m, ctr);
     const double nvs = ng.G == 0 ? 0.0 : ng.var_sum;
     const double odds = tg.best_l / nvs;
     if (!(odds * 100.0 >= (double)prm.odds)) continue;
