@@ -199,6 +199,16 @@ __device__ __forceinline__ uint8_t bit_base(uint32_t m) {  // lowest set bit of 
 
 // MD event lookup for reference offset `off` (events sorted by offset).
 __device__ __forceinline__ int md_find(const uint32_t *ev, int32_t n, int32_t off) {
+  if (n <= 4) {  // the common read: its few events in one round of loads (no dependent search)
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = k < n ? ev[k] : 0xFFFFFFFFu;
+    int r = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r < 0 && k < n && (int32_t)(v[k] >> 8) == off) r = (int)(v[k] & 0xFFu);  // (the first, as the search)
+    return r;
+  }
   int lo = 0, hi = n;
   while (lo < hi) {
     int mid = (lo + hi) >> 1;

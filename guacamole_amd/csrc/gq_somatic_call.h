@@ -575,6 +575,92 @@ __device__ __forceinline__ bool call_front(const CandRec &cr, int64_t it, const 
   // ---- covering reads of both samples: in [first pmax_end > pos, first start > pos) of each
   //      tile window (cand_prep's searches)
   const int64_t ra[2] = {cr.ra[0], cr.ra[1]}, rz[2] = {cr.rz[0], cr.rz[1]};
+  // the element record of covering read r (its scalars given), and its MD-derived reference
+  // base's std bit into mk
+  auto elem = [&](const DevReads &R, int64_t r, int32_t st, int ld, int64_t so, int mq, uint8_t rfl, int32_t nmd,
+                  int64_t mdo, uint32_t nmm, uint32_t &mk) -> uint4 {
+    uint32_t fl = 0;
+    int32_t rp = 0, aux = 0;
+    uint32_t base = 0, kind = K_SNV;
+    int q = 0;
+    if (ld >= 0) {
+      const int32_t off = pos - st;
+      rp = ld + off;
+      base = R.seq[so + rp];
+      q = (int)(int8_t)R.qual[so + rp];
+      if (nmd < 0) {
+        raise_at(ctr, GQ_E_NO_MD, pos);
+      } else {
+        const int v = nmd > 0 ? md_find(R.md_ev + mdo, nmd, off) : -1;
+        mk |= std_bit((uint8_t)(v >= 0 ? v : (int)base));
+        fl = kElAct;
+      }
+    } else {
+      const int v = md_ref_at(R, r, pos);
+      if (v < 0) {
+        raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
+      } else {
+        mk |= std_bit((uint8_t)v);
+        AlleleDesc d;
+        int errc = 0;
+        if (!classify(R, r, pos, 0, d, &errc)) {
+          raise_at(ctr, errc, pos);
+        } else {
+          fl = kElAct;
+          kind = d.kind;
+          base = d.base;
+          rp = d.rp;
+          aux = d.aux;
+          q = elem_quality(R, d, so, mq);
+        }
+      }
+    }
+    if (prm.min_mapq <= 0 || mq >= prm.min_mapq) fl |= kElPass;  // QualityAlignedReadsFilter
+    if (!(rfl & 1)) fl |= kElFwd;
+    return make_uint4((uint32_t)rp, (uint32_t)aux,
+                      base | (kind << 8) | ((uint32_t)(uint8_t)(int8_t)q << 16) | ((uint32_t)mq << 24),
+                      (nmm & 0xFFFFu) | (fl << 16));
+  };
+  if (!DEEP && !(dbg & 64) && rz[0] - ra[0] <= 64 && rz[1] - ra[1] <= 64 && !(pos < cr.E[0]) && !(pos < cr.E[1])) {
+    // the common candidate: each window fits one chunk and no initial group reorders it, so the
+    // covers and the element records come in one pass, a lane per window read: its interval
+    // and scalars in one round of loads, then its base / quality / MD event
+    mask[0] = mask[1] = 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const DevReads &R = s ? RN : RT;
+      const int64_t r = ra[s] + lane;
+      const bool in = r < rz[s];
+      const int64_t rr = in ? r : ra[s];
+      int32_t st = 0, en = 0, nmd = 0;
+      int ld = 0, mq = 0;
+      int64_t so = 0, mdo = 0;
+      uint8_t rfl = 0;
+      uint32_t nmm = 0;
+      if (rz[s] > ra[s]) {
+        st = R.start[rr];
+        en = R.end[rr];
+        ld = (int)R.lead[rr];
+        so = R.seq_off[rr];
+        mq = (int)R.mapq[rr];
+        rfl = R.flags[rr];
+        nmd = R.n_md[rr];
+        mdo = R.md_off[rr];
+        nmm = (uint32_t)R.n_mismatch[rr];
+      }
+      const bool c = in && st <= pos && pos < en;
+      const unsigned long long b = __ballot(c);
+      const uint32_t at = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+      nc[s] = (uint32_t)__popcll(b);
+      if (c) {
+        m.cov[s][at] = (int32_t)(r - rb[s]);
+        m.el[s][at] = elem(R, r, st, ld, so, mq, rfl, nmd, mdo, nmm, mask[s]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return true;
+  }
   nc[0] = nc[1] = 0;
   {
     const int64_t span = max(rz[0] - ra[0], rz[1] - ra[1]);
@@ -656,55 +742,8 @@ __device__ __forceinline__ bool call_front(const CandRec &cr, int64_t it, const 
         const uint32_t k = c0 + lane;
         if (k >= nc[s]) continue;
         const int64_t r = rb[s] + m.cov[s][k];
-        const int32_t st = R.start[r];
-        const int ld = (int)R.lead[r];
-        const int64_t so = R.seq_off[r];
-        const int mq = (int)R.mapq[r];
-        const uint8_t rfl = R.flags[r];
-        const int32_t nmd = R.n_md[r];
-        const int64_t mdo = R.md_off[r];
-        const uint32_t nmm = (uint32_t)R.n_mismatch[r];
-        uint32_t fl = 0;
-        int32_t rp = 0, aux = 0;
-        uint32_t base = 0, kind = K_SNV;
-        int q = 0;
-        if (ld >= 0) {
-          const int32_t off = pos - st;
-          rp = ld + off;
-          base = R.seq[so + rp];
-          q = (int)(int8_t)R.qual[so + rp];
-          if (nmd < 0) {
-            raise_at(ctr, GQ_E_NO_MD, pos);
-          } else {
-            const int v = nmd > 0 ? md_find(R.md_ev + mdo, nmd, off) : -1;
-            mask[s] |= std_bit((uint8_t)(v >= 0 ? v : (int)base));
-            fl = kElAct;
-          }
-        } else {
-          const int v = md_ref_at(R, r, pos);
-          if (v < 0) {
-            raise_at(ctr, v == -4 ? GQ_E_NO_MD : v == -3 ? GQ_E_MD : GQ_E_ASSERT, pos);
-          } else {
-            mask[s] |= std_bit((uint8_t)v);
-            AlleleDesc d;
-            int errc = 0;
-            if (!classify(R, r, pos, 0, d, &errc)) {
-              raise_at(ctr, errc, pos);
-            } else {
-              fl = kElAct;
-              kind = d.kind;
-              base = d.base;
-              rp = d.rp;
-              aux = d.aux;
-              q = elem_quality(R, d, so, mq);
-            }
-          }
-        }
-        if (prm.min_mapq <= 0 || mq >= prm.min_mapq) fl |= kElPass;  // QualityAlignedReadsFilter
-        if (!(rfl & 1)) fl |= kElFwd;
-        m.el[s][k] = make_uint4((uint32_t)rp, (uint32_t)aux,
-                                base | (kind << 8) | ((uint32_t)(uint8_t)(int8_t)q << 16) | ((uint32_t)mq << 24),
-                                (nmm & 0xFFFFu) | (fl << 16));
+        m.el[s][k] = elem(R, r, R.start[r], (int)R.lead[r], R.seq_off[r], (int)R.mapq[r], R.flags[r], R.n_md[r],
+                          R.md_off[r], (uint32_t)R.n_mismatch[r], mask[s]);
       }
     }
   }
