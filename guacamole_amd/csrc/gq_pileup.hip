@@ -482,7 +482,7 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
 template <int KU>
 __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj) {
   __shared__ PieceMeta s_meta[4][64];
-  __shared__ uint32_t s_owner[4][4 * 64];
+  __shared__ uint32_t s_owner[4][KU * 64];
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
   uint32_t *owner = s_owner[threadIdx.x >> 6];
   const int64_t w0 = wave_id();

@@ -107,15 +107,20 @@ struct MarginRaw {
   uint2 word;   // general CIGAR: the word itself
   uint32_t valid, gen;  // valid: byte mask of loci inside the read
 };
+// lrow: the table row of mapping quality lmq staged in this wave's LDS (nullptr: none); a word of
+// a read with that mapq looks its terms up there, others in the global table.
 __device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, uint64_t q, uint32_t valid, uint32_t evb,
-                                               const uint8_t *__restrict__ tab) {
+                                               const uint8_t *__restrict__ tab, const uint8_t *lrow = nullptr,
+                                               uint32_t lmq = 0xFFFFFFFFu) {
   const uint8_t *tm = tab + (m.mq << 8);  // evb: the MD events at the word's loci
+  const bool local = lrow && m.mq == lmq;
   uint32_t v[2] = {0x80808080u, 0x80808080u};
 #pragma unroll
   for (int q8 = 0; q8 < 8; ++q8) {
     if (!((valid >> q8) & 1u)) continue;
     const int qv = (int)(int8_t)(uint8_t)(q >> (8 * q8));
-    const uint32_t t = qv < 0 ? (uint32_t)kMargin8None : (uint32_t)tm[(qv << 1) | ((evb >> q8) & 1u ? 0 : 1)];
+    const int ti = (qv << 1) | ((evb >> q8) & 1u ? 0 : 1);
+    const uint32_t t = qv < 0 ? (uint32_t)kMargin8None : local ? (uint32_t)lrow[ti] : (uint32_t)tm[ti];
     v[q8 >> 2] = (v[q8 >> 2] & ~(0xFFu << (8 * (q8 & 3)))) | (t << (8 * (q8 & 3)));
   }
   return make_uint2(v[0], v[1]);
@@ -173,22 +178,33 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
                                                   const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
                                                   uint8_t *__restrict__ mnb) {
   __shared__ PieceMeta s_meta[4][64];
-  __shared__ uint32_t s_owner[4][4 * 64];
+  __shared__ uint32_t s_owner[4][KU * 64];
+  __shared__ uint32_t s_row[4][64];  // the table row of the slice's first read's mapq (256 bytes)
   PieceMeta *meta = s_meta[threadIdx.x >> 6];
   uint32_t *owner = s_owner[threadIdx.x >> 6];
+  uint32_t *row = s_row[threadIdx.x >> 6];
+  const uint8_t *lrow = reinterpret_cast<const uint8_t *>(row);
+  const int lane = threadIdx.x & 63;
   const int64_t w0 = wave_id();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     if (R.pbad[slot]) continue;  // uniform
     uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * R.srow[slot];  // the slice's block rows
+    const SliceWin W = slice_stored(R, slot);
+    // most reads share one mapping quality: its table row in LDS saves the words' lookups a
+    // round trip to the cache hierarchy
+    const uint32_t lmq = W.rz > W.ra ? (uint32_t)R.mapq[W.ra] : 0u;
+    row[lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     bool none = false;
     slice_fill<true, KU>(
-        R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
+        R, W, R.prow + R.soff[slot], meta, owner,
         [&](int64_t, PieceMeta &m, int64_t mdo) { return margin_setup(R, min_mapq, mdo, m); },
         [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t evb) { return margin_fetch(R, r, m, col, evb, tab); },
         [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t evb) {
           if (act) {
-            const uint2 w = x.gen ? x.word : margin_terms8(m, x.q, x.valid, evb, tab);
+            const uint2 w = x.gen ? x.word : margin_terms8(m, x.q, x.valid, evb, tab, lrow, lmq);
             out[16 * (int64_t)m.row + (col & 15)] = w;
             auto has = [](uint32_t v) {  // a zero byte
               return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
