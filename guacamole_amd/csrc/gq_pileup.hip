@@ -2956,7 +2956,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
   if (n_sl > 0) {
     const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;
-    auto kf = fill_u == 1 ? proj_fill<1> : proj_fill<4>;
+    auto kf = fill_u == 4 ? proj_fill<4> : fill_u == 2 ? proj_fill<2> : proj_fill<1>;
     hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
     HIP_TRY(hipGetLastError());
   }

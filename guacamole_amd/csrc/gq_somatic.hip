@@ -1275,7 +1275,7 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;  // A/B: 1 or 4 words per lane
-    auto kf = fill_u == 1 ? mproj_fill<1> : mproj_fill<4>;
+    auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
     hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0, c->stream,
                        t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);
   }
