@@ -1,0 +1,31 @@
+"""The library's alternative kernel builds, picked per process from the environment, give the
+default build's records bit for bit (the default is checked against the oracle elsewhere):
+GQ_CALL_SPLIT=1 (somatic caller as a front kernel + back end over stored element records),
+GQ_CALL_WPE=2 (the one-kernel caller at 2 waves per SIMD), GQ_FILL_U=2 / 4 (projection and
+margin fills at 2 or 4 words per lane).  A synthetic 300 kb 60x / 30x pair with a raised somatic
+rate, so hundreds of candidates and calls reach every path."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, **extra)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_variant_runner.py"), "300000"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_kernel_variants_give_the_default_records():
+    base = _run({})
+    assert base["somatic"] > 20 and base["germline"] > 100
+    for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, {"GQ_FILL_U": "2"}, {"GQ_FILL_U": "4"}):
+        got = _run(extra)
+        assert got == base, (extra, got, base)
