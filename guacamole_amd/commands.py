@@ -230,6 +230,35 @@ def device_ingest(args, *paths: str) -> bool:
     return all(is_bam(p) for p in paths)
 
 
+def load_pair_device(ctx, ctx2, paths, filters, mapped):
+    """Two BAMs decoded on the device at once: the second on ctx2 (its own stream) on a host
+    thread while the first loads on ctx, so one's copy overlaps the other's inflate (ctypes
+    releases the GIL).  The second read set is then registered with ctx (device pointers are
+    valid across contexts of one device) and keeps ctx2 alive."""
+    import threading
+    import weakref
+    box = {}
+
+    def second():
+        try:
+            box["rs"] = load_reads_device(ctx2, paths[1], filters, mapped[paths[1]])
+        except BaseException as e:  # re-raised below
+            box["err"] = e
+    th = threading.Thread(target=second)
+    th.start()
+    try:
+        first = load_reads_device(ctx, paths[0], filters, mapped[paths[0]])
+    finally:
+        th.join()
+    if "err" in box:
+        raise box["err"]
+    rs = box["rs"]
+    if rs is not None:
+        rs._device[id(ctx)] = (weakref.ref(ctx), rs.reads)
+        rs._ctx2 = ctx2
+    return [first, rs]
+
+
 def germline_threshold_main(argv: Sequence[str]) -> int:
     p = argparse.ArgumentParser(prog="germline-threshold",
                                 description="call variants by thresholding read counts (toy example)")
@@ -367,9 +396,10 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
             maps = map_bams([args.tumor_reads, args.normal_reads])
             t = clock.t()
             ctx = native.Context(args.device)
+            ctx2 = native.Context(args.device)  # the normal's load: its own stream, alongside the tumor's
             clock.note("ctx_open_s", clock.t() - t)
             mapped = maps["join"]()
-            sets = [load_reads_device(ctx, path, f, mapped[path]) for path in (args.tumor_reads, args.normal_reads)]
+            sets = load_pair_device(ctx, ctx2, [args.tumor_reads, args.normal_reads], f, mapped)
         else:
             ctx = native.Context(local)
             got = device_ingest_ranks(ctx, [args.tumor_reads, args.normal_reads], f, builder, args.parallelism,
