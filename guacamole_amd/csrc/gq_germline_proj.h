@@ -102,7 +102,10 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // with count <= depth < 2^16 the factor clamps to [0, 101] (101: never; 0: always) in 32 bits
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
-  auto passes = [=](uint32_t count, uint32_t depth) { return count * 100u >= thr1u * depth; };
+  // (16-bit operands, so the products take full-rate 24-bit multiplies: a locus has at most
+  // kSliceRowsMax elements, one per row of its slice)
+  const uint32_t thr1b = thr1u & 0xFFu;
+  auto passes = [=](uint32_t count, uint32_t depth) { return (count & 0xFFFFu) * 100u >= thr1b * (depth & 0xFFFFu); };
   // the tile record (Tile + TileX: dword d on lane d < 32) of the wave's next tile, loaded one
   // tile ahead: its fields are in a register when the tile starts (no dependent setup rounds)
   // (TileX array follows the Tiles: one buffer over both, lane d < 16 reads Tile dword d,
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     widen();
     const uint64_t t_e = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint32_t kinds = 0, nrec = 0, ncpx = 0;
+    uint32_t kinds = 0, nrec = 0, ncpx = 0, livem = 0, ambm = 0;
     int32_t mid0 = 0;  // MidDeletion elements entering this lane's first locus
     // locus j's 16-bit count of base w (a dynamic j selects among four registers)
     auto cnt16 = [](const uint32_t (&w)[4], int j) {
@@ -352,17 +355,20 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
       mid0 = (int32_t)wave_incl_scan((uint32_t)mrun0) - mrun0;  // the same for the MidDeletion ranges
       int32_t mid_run = mid0;
+      // the lane's loci inside [L0, L1) as bits (most lanes: all eight)
+      const int32_t lb0 = B0 + 8 * lane;
+      const int32_t ilo = min(max(L0 - lb0, 0), 8), ihi = min(max(L1 - lb0, 0), 8);
+      const uint32_t inm = ((1u << ihi) - 1u) & ~((1u << ilo) - 1u);
       // ---- decision (GermlineThresholdCaller.scala:97-177 for pileups of single-base and
       //      MidDeletion alleles), eight loci, four unrolled at a time with their LDS words read
       //      in the loop (the next tile's row batches are in flight in registers meanwhile):
       //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
-#pragma unroll 4
+#pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t eacj = ev[64 * j + lane], etgj = ev[T + 64 * j + lane], m8j = m8[j];
         const int32_t ddj = (int32_t)d8[j];
         {
-        const int32_t l = B0 + 8 * lane + j;
-        const bool in = l >= L0 && l < L1;
+        const bool in = (inm >> j) & 1u;
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);
         const uint32_t nN = (m8j >> 4) & 0xFFFu;
         ncx_run += (int32_t)m8j >> 16;
@@ -371,33 +377,35 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
         const uint32_t nmid = mid_run > 0 ? (uint32_t)mid_run : 0u;  // MidDeletion elements (allele (ref, ""))
         const uint32_t depth = cA + cC + cT + cG + nN + ncx + nmid;
         const uint32_t mask = ref_mask(m8j, eacj, etgj, cA, cC, cT, cG);
-        // branch-free (0/1 integers): the common hom-ref locus writes nothing
-        const uint32_t live = (in ? 1u : 0u) & (depth > 0 ? 1u : 0u);
-        const uint32_t ambiguous = (mask & (mask - 1u)) != 0 ? 1u : 0u;
+        // lane predicates (the common hom-ref locus writes nothing); kinds carries the result
+        const bool live = ((inm >> j) & 1u) != 0 && depth > 0;
+        const bool ambiguous = (mask & (mask - 1u)) != 0;
         const uint32_t low = mask & (0u - mask);  // the first standard reference base, as a bit (or 0: N)
-        const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
-                               nN * (low == 0u ? 1u : 0u);
+        const uint32_t c_ref = (cA & (0u - (low & 1u))) + (cC & (0u - ((low >> 1) & 1u))) +
+                               (cT & (0u - ((low >> 2) & 1u))) + (cG & (0u - ((low >> 3) & 1u))) +
+                               (low == 0u ? nN : 0u);
         // two alleles in one mutable.HashMap bucket (Scala map order by first occurrence:
         // germline_complex): ref C with two of G, N and (C, ""); ref G with T and (G, "")
-        const uint32_t cgn = (low == 2u ? 1u : 0u) &
-                             ((cG > 0 ? 1u : 0u) + (nN > 0 ? 1u : 0u) + (nmid > 0 ? 1u : 0u) >= 2u ? 1u : 0u);
-        const uint32_t gtm = (low == 8u ? 1u : 0u) & (cT > 0 ? 1u : 0u) & (nmid > 0 ? 1u : 0u);
-        const uint32_t to_complex =
-            live & (ambiguous | (ncx > 0 ? 1u : 0u) | (multi_sample ? 1u : 0u) | cgn | gtm);
-        const uint32_t simple = live & (to_complex ^ 1u);
-        const uint32_t alt_pass = passes(depth - c_ref, depth) ? 1u : 0u;  // some other allele may pass
-        const uint32_t homref = simple & (alt_pass ^ 1u);
-        const uint32_t ref_pass = (c_ref > 0 && passes(c_ref, depth)) ? 1u : 0u;
-        const uint32_t emit_hr = homref & (ref_pass ? (uint32_t)(emit_ref != 0) : (uint32_t)(emit_no_call != 0));
-        const uint32_t general = simple & alt_pass;
-        visited += live;
-        amb += live & ambiguous;
-        const uint32_t kind = to_complex * 3u + general * 2u + emit_hr;  // at most one is set
-        kinds |= kind << (2 * j);
-        nrec += emit_hr + 2u * general;
-        ncpx += to_complex;
+        const bool g0 = cG > 0, n0 = nN > 0, d0 = nmid > 0;
+        const bool cgn = low == 2u && ((g0 && n0) || (g0 && d0) || (n0 && d0));
+        const bool gtm = low == 8u && cT > 0 && d0;
+        const bool to_complex = live && (ambiguous || ncx > 0 || multi_sample || cgn || gtm);
+        const bool alt_pass = passes(depth - c_ref, depth);  // some other allele may pass
+        const bool general = live && !to_complex && alt_pass;
+        const bool ref_pass = c_ref > 0 && passes(c_ref, depth);
+        const bool emit_hr = live && !to_complex && !alt_pass && (ref_pass ? emit_ref != 0 : emit_no_call != 0);
+        livem |= (live ? 1u : 0u) << j;
+        ambm |= (live && ambiguous ? 1u : 0u) << j;
+        kinds |= (to_complex ? 3u : general ? 2u : emit_hr ? 1u : 0u) << (2 * j);
         }
       }
+    }
+    {  // counts from the per-locus fields: kind 1 one record, 2 a record pair, 3 a complex item
+      const uint32_t hi = (kinds >> 1) & 0x5555u, lo = kinds & 0x5555u;
+      nrec = (uint32_t)__popc(lo & ~hi) + 2u * (uint32_t)__popc(hi & ~lo);
+      ncpx = (uint32_t)__popc(lo & hi);
+      visited += (uint32_t)__popc(livem);
+      amb += (uint32_t)__popc(ambm);
     }
     if (__ballot(kinds != 0) != 0) {  // rare: records / complex items to write
       const unsigned rbase = wave_reserve_lds_n(out.lds + 0, nrec);

@@ -374,6 +374,15 @@ __device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const Sl
 
 // A piece of a 64-read batch, for the word-per-lane fills (slice_fill): set up once by the
 // piece's lane, read from LDS by the lanes of its words.
+// Bytes [lo, hi) of an 8-byte word (clamped to [0, 8)) as a mask: an edge word's loci inside its read.
+__device__ __forceinline__ uint64_t edge_mask(int32_t lo, int32_t hi) {
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > 8 ? 8 : hi;
+  if (hi <= lo) return 0;
+  const uint64_t top = hi == 8 ? ~0ull : (1ull << (8 * hi)) - 1ull;
+  return top & ~((1ull << (8 * lo)) - 1ull);
+}
+
 struct __attribute__((aligned(16))) PieceMeta {
   int64_t p0;         // pool offset of locus 0: a column-eligible read's base / quality at locus l is p0 + l
   int32_t s, e;       // the read's [start, end)
@@ -494,6 +503,172 @@ __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W,
         if (act[u]) raw[u] = fetch(r0 + kk[u], pm[u], col[u], evb[u]);
 #pragma unroll
       for (int u = 0; u < kU; ++u) emit(act[u], raw[u], r0 + kk[u], pm[u], col[u], evb[u]);
+    }
+    __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
+// ---- Read-major fills (the default; slice_fill above is the A/B alternative, GQ_FILL=slice) ----
+inline int fill_dbg() {  // GQ_FILL_DBG (read_fill): diagnostics and the XCD-contiguous order
+  static const int v = getenv("GQ_FILL_DBG") ? atoi(getenv("GQ_FILL_DBG")) : 0;
+  return v;
+}
+inline bool fill_slice_major() {
+  static const bool v = getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "slice") == 0;
+  return v;
+}
+// One wave per batch of 64 consecutive reads, a lane per word of the batch's projections: a
+// read's words (its columns [col0, col1)) sit on consecutive lanes in column order, so its bases /
+// qualities load as one contiguous run and each of its pieces' words lands in one row segment.
+// No slice window is walked: each read looks up its pieces' rows once (the rows row_count stored
+// per (slice, window read)) and keeps their global row numbers in its LDS record, so a round of
+// words has no dependent record loads.  kU rounds' loads are issued before the first store.
+struct __attribute__((aligned(16))) ReadMeta {
+  int64_t p0;         // pool offset of locus 0 (column-eligible reads: base / quality of locus l at p0 + l)
+  int32_t s, e;       // the read's [start, end)
+  uint32_t info, mq;  // ColDesc info, mapping quality
+  int32_t col0, pad;  // first column
+  int64_t md_off;     // its MD events
+  int64_t qoff;       // its contig's first slice
+  int64_t grow[3];    // global row of its first three pieces (-1: no row / pbad slice)
+};
+static_assert(sizeof(ReadMeta) == 80, "ReadMeta: five 16-byte LDS reads");
+constexpr int kReadPieces = 3;  // pieces per read held in ReadMeta (a 150 bp read spans <= 3 slices)
+
+__device__ __forceinline__ PieceMeta piece_meta(const ReadMeta &m) {  // the fields the word fetches read
+  PieceMeta p;
+  p.p0 = m.p0;
+  p.s = m.s;
+  p.e = m.e;
+  p.s0 = 0;
+  p.row = 0;
+  p.info = m.info;
+  p.mq = m.mq;
+  return p;
+}
+
+// Global row of read r's piece in slice `slot` (-1: the slice is pbad or the read has no row there).
+__device__ __forceinline__ int64_t piece_grow(const DevReads &R, int64_t r, int64_t slot) {
+  if (R.pbad[slot]) return -1;
+  const uint16_t k = R.prow[R.soff[slot] + (r - R.sra[slot])];
+  return k == 0xFFFFu ? -1 : R.srow[slot] + (int64_t)k;
+}
+
+// Batches of 64 reads from batch b0 on, stride nb (grid-stride over waves).  For each word of
+// each kept read: raw = fetch(read, meta, column) (its loads), then emit(act, raw, read, meta,
+// column, grow, slot).  keep(meta) decides per read (false: no words); batch(first read) runs
+// at each batch's start (every lane).  meta: this wave's 64 LDS records; owner: its kU * 64 LDS
+// words.
+// dbg (diagnostics, GQ_FILL_DBG; the pool is wrong when set): 1 no word loads, 2 no word stores;
+// 4: XCD-contiguous batches (workgroup i runs on XCD i % 8: each XCD takes one contiguous
+// eighth of the batches, so rows that pieces of neighbouring batches share meet in one L2).
+template <int kU, class B, class K, class F, class E>
+__device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restrict__ meta, uint32_t *__restrict__ owner,
+                                          int dbg, B &&batch, K &&keep, F &&fetch, E &&emit) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nbat = (R.n_reads + 63) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t wid = wave_id();
+  if (dbg & 4) {
+    const int64_t per = (int64_t)gridDim.x >> 3;  // (the grid is a multiple of 8)
+    wid = ((int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3)) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    wid = __builtin_amdgcn_readfirstlane((int)wid);
+  }
+  for (int64_t b = wid; b < nbat; b += nw) {
+    batch(64 * b);
+    const int64_t r = 64 * b + lane;
+    const bool in = r < R.n_reads;
+    const int64_t rr = in ? r : 64 * b;
+    // the read's records in one round of loads
+    const ProjRec pr = R.prec[rr];
+    const ColDesc d = R.cdesc[rr];
+    const int64_t so = R.seq_off[rr];
+    const int32_t ld = R.lead[rr];
+    const uint32_t mq = R.mapq[rr];
+    const int64_t mdo = R.md_off[rr];
+    int lo = 0, hi = R.n_contigs - 1;  // contig: last c with contig_read_begin[c] <= r
+    while (lo < hi) {
+      const int m = (lo + hi + 1) >> 1;
+      if (R.contig_read_begin[m] <= rr) lo = m;
+      else hi = m - 1;
+    }
+    ReadMeta m;
+    m.p0 = so + (ld > 0 ? ld : 0) - d.start;
+    m.s = d.start;
+    m.e = d.end;
+    m.info = d.info;
+    m.mq = mq;
+    m.col0 = pr.col0;
+    m.pad = 0;
+    m.md_off = mdo;
+    m.qoff = R.qoff[lo];
+    uint32_t len = in && pr.col1 != kProjNone && pr.col1 > pr.col0 ? (uint32_t)(pr.col1 - pr.col0) : 0u;
+    if (len && !keep(m)) len = 0;
+    {
+      const int64_t q0 = m.qoff + (pr.col0 >> 4);
+      const int32_t npc = len ? ((pr.col1 - 1) >> 4) - (pr.col0 >> 4) + 1 : 0;
+      int64_t g[kReadPieces];
+#pragma unroll
+      for (int j = 0; j < kReadPieces; ++j) g[j] = j < npc ? piece_grow(R, rr, q0 + j) : -1;
+#pragma unroll
+      for (int j = 0; j < kReadPieces; ++j) m.grow[j] = g[j];
+    }
+    if (len) meta[lane] = m;
+    const uint32_t incl = wave_incl_scan(len), ex = incl - len;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    for (uint32_t w0 = 0; w0 < tot; w0 += 64 * kU) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) owner[64 * u + lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (len > 0 && ex > w0 && ex < w0 + 64 * kU) owner[ex - w0] = (uint32_t)lane + 1;  // the read's first word
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      int kk[kU];
+      int32_t col[kU];
+      bool act[kU];
+      int64_t grow[kU], slot[kU];
+      ReadMeta pm[kU];
+      decltype(fetch((int64_t)0, pm[0], (int32_t)0)) raw[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t wb = w0 + 64 * u, w = wb + (uint32_t)lane;
+        const unsigned long long run = __ballot(len > 0 && ex <= wb);  // the last of them runs at wb
+        const uint32_t k_at = run ? 64u - (uint32_t)__clzll((long long)run) : 0u;  // its lane + 1
+        const uint32_t k1 = max(wave_incl_max(owner[64 * u + lane]), k_at);
+        act[u] = w < tot;
+        const int k = act[u] ? (int)k1 - 1 : 0;
+        kk[u] = k;
+        const uint4 *src = reinterpret_cast<const uint4 *>(meta + k);
+        const uint4 a = src[0], bq = src[1], c = src[2], dq = src[3], eq = src[4];
+        ReadMeta &mm = pm[u];
+        mm.p0 = (int64_t)((uint64_t)a.x | ((uint64_t)a.y << 32));
+        mm.s = (int32_t)a.z;
+        mm.e = (int32_t)a.w;
+        mm.info = bq.x;
+        mm.mq = bq.y;
+        mm.col0 = (int32_t)bq.z;
+        mm.md_off = (int64_t)((uint64_t)c.x | ((uint64_t)c.y << 32));
+        mm.qoff = (int64_t)((uint64_t)c.z | ((uint64_t)c.w << 32));
+        const int64_t g0 = (int64_t)((uint64_t)dq.x | ((uint64_t)dq.y << 32));
+        const int64_t g1 = (int64_t)((uint64_t)dq.z | ((uint64_t)dq.w << 32));
+        const int64_t g2 = (int64_t)((uint64_t)eq.x | ((uint64_t)eq.y << 32));
+        const uint32_t kex = (uint32_t)__shfl((int)ex, k, 64);
+        col[u] = mm.col0 + (int32_t)(w - kex);
+        const int32_t pj = (col[u] >> 4) - (mm.col0 >> 4);
+        slot[u] = mm.qoff + (col[u] >> 4);
+        grow[u] = pj == 0 ? g0 : pj == 1 ? g1 : pj == 2 ? g2 : -2;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (act[u] && grow[u] == -2) grow[u] = piece_grow(R, 64 * b + kk[u], slot[u]);  // a long read's later piece
+        act[u] = act[u] && grow[u] >= 0;
+        if (act[u] && !(dbg & 1)) raw[u] = fetch(64 * b + kk[u], pm[u], col[u]);
+        else raw[u] = {};
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) emit(act[u] && !(dbg & 2), raw[u], 64 * b + kk[u], pm[u], col[u], grow[u], slot[u]);
     }
     __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -445,8 +445,11 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
   const int32_t lb = 8 * col;  // locus of byte 0
   ProjRaw x{0, 0, 0};
   if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
+    const int64_t a = m.p0 + lb;
     if (lb >= s && lb + 8 <= e) {
-      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + m.p0 + lb);
+      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a);
+    } else if (a >= 0 && a + 8 <= R.seq_cap) {  // an edge word: one load, the loci outside the read masked
+      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a) & edge_mask(s - lb, e - lb);
     } else {
       for (int q = 0; q < 8; ++q) {
         const int32_t l = lb + q;
@@ -500,6 +503,22 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
                 x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
         });
   }
+}
+
+// The projection pool, read-major (read_fill): a wave per 64 consecutive reads, a lane per word.
+template <int KU>
+__global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restrict__ proj, int dbg) {
+  __shared__ ReadMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][KU * 64];
+  uint32_t *out = reinterpret_cast<uint32_t *>(proj);
+  read_fill<KU>(
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, [](int64_t) {}, [](const ReadMeta &) { return true; },
+      [&](int64_t r, const ReadMeta &m, int32_t col) { return proj_fetch(R, r, piece_meta(m), col); },
+      [&](bool act, const ProjRaw &x, int64_t, const ReadMeta &, int32_t col, int64_t grow, int64_t) {
+        if (act)
+          out[16 * grow + (col & 15)] =
+              x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
+      });
 }
 
 // The sparse entries of each read (thread per read): MD events, N bases (without an event),
@@ -2954,10 +2973,16 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
   HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
   d->owned.push_back(pe);
   if (n_sl > 0) {
-    const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;
-    auto kf = fill_u == 4 ? proj_fill<4> : fill_u == 2 ? proj_fill<2> : proj_fill<1>;
-    hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
+    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
+    if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      auto kf = fill_u == 4 ? proj_fill<4> : fill_u == 2 ? proj_fill<2> : proj_fill<1>;
+      hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
+    } else if (n > 0) {
+      const int64_t blocks = (std::min<int64_t>((n + 255) / 256, 1 << 20) + 7) & ~(int64_t)7;  // a wave per 64 reads
+      auto kf = fill_u == 2 ? proj_fill_rw<2> : fill_u == 4 ? proj_fill_rw<4> : proj_fill_rw<1>;
+      hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, (uint8_t *)pj, fill_dbg());
+    }
     HIP_TRY(hipGetLastError());
   }
   if (n > 0) {

@@ -1274,10 +1274,20 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, incl_align ? 1 : 0, (uint8_t *)tab);
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
-    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 1;  // A/B: 1 or 4 words per lane
-    auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
-    hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0, c->stream,
-                       t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);
+    static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;  // A/B: words per lane and round
+    if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
+      auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
+      hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
+                         c->stream, t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,
+                         (uint8_t *)t->mnb);
+    } else if (t->d.n_reads > 0) {
+      // mnb: set per slice by the words (a rebuild for another filter starts from zero)
+      HIP_TRY(hipMemsetAsync(t->mnb, 0, (size_t)t->n_slices + 16, c->stream));
+      auto kf = fill_u == 2 ? mproj_fill_rw<2> : fill_u == 4 ? mproj_fill_rw<4> : mproj_fill_rw<1>;
+      hipLaunchKernelGGL(kf, dim3((unsigned)((std::min<int64_t>((t->d.n_reads + 255) / 256, 1 << 20) + 7) & ~(int64_t)7)),
+                         dim3(256), 0, c->stream, t->d, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,
+                         (uint8_t *)t->mnb, fill_dbg());
+    }
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));

@@ -131,9 +131,17 @@ __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, 
   const int32_t lb = 8 * col;
   MarginRaw x{0, make_uint2(0x80808080u, 0x80808080u), 0, 0};
   if (m.info & kColEligible) {
+    const int64_t a = m.p0 + lb;
     if (lb >= s && lb + 8 <= e) {
-      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + m.p0 + lb);
+      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a);
       x.valid = 0xFFu;
+    } else if (a >= 0 && a + 8 <= R.seq_cap) {  // an edge word: one load, the loci outside the read masked
+      const uint64_t k = edge_mask(s - lb, e - lb);
+      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a) & k;
+      uint32_t v = 0;
+#pragma unroll
+      for (int q8 = 0; q8 < 8; ++q8) v |= ((k >> (8 * q8)) & 1u) << q8;
+      x.valid = v;
     } else {
 #pragma unroll
       for (int q8 = 0; q8 < 8; ++q8) {
@@ -215,6 +223,92 @@ __global__ __launch_bounds__(256) void mproj_fill(DevReads R, int64_t n_slices, 
     const bool any = __ballot(none) != 0;
     if ((threadIdx.x & 63) == 0) mnb[slot] = any ? 1 : 0;
   }
+}
+
+// The MD-event bits of read m's word at column col (bit k: locus 8 col + k): v holds up to four
+// events loaded by the fetch (0xFFFFFFFF: none); a read with more has them in evb already.
+__device__ __forceinline__ uint32_t word_event_bits(const ReadMeta &m, int32_t col, const uint32_t (&v)[4], uint32_t evb) {
+  const int32_t i0 = 8 * col - m.s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = (uint32_t)((int32_t)(v[k] >> 8) - i0);
+    evb |= i < 8u ? 1u << i : 0u;
+  }
+  return evb;
+}
+struct MarginRW {
+  MarginRaw x;
+  uint32_t v[4];  // the read's events (up to four), for word_event_bits
+  uint32_t evb;
+};
+__device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r, const ReadMeta &m, int32_t col,
+                                                    const uint8_t *__restrict__ tab) {
+  MarginRW o;
+  const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
+  const uint32_t *ev = R.md_ev + m.md_off;
+  o.evb = 0;
+  if (nmd <= 4) {  // the common read: its events in the same round of loads as the qualities
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.v[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
+  } else {  // the first event at or past the word's first locus, then the word's events
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.v[k] = 0xFFFFFFFFu;
+    const int32_t i0 = 8 * col - m.s;
+    int k = 0, hi = nmd;
+    while (k < hi) {
+      const int mid = (k + hi) >> 1;
+      if ((int32_t)(ev[mid] >> 8) < i0) k = mid + 1;
+      else hi = mid;
+    }
+    for (; k < nmd; ++k) {
+      const int32_t i = (int32_t)(ev[k] >> 8) - i0;
+      if (i >= 8) break;
+      o.evb |= 1u << i;
+    }
+  }
+  const PieceMeta pm = piece_meta(m);
+  if (m.info & kColEligible) o.x = margin_fetch(R, r, pm, col, 0u, tab);  // (the terms come in the emit)
+  else o.x = margin_fetch(R, r, pm, col, word_event_bits(m, col, o.v, o.evb), tab);
+  return o;
+}
+
+// The margin projection, read-major (read_fill): a wave per 64 consecutive reads, a lane per
+// word; mnb (zeroed by the caller) gets 1 on each slice holding a kMargin8None term.
+template <int KU>
+__global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, const uint8_t *__restrict__ tab,
+                                                     uint8_t *__restrict__ mproj, uint8_t *__restrict__ mnb, int dbg) {
+  __shared__ ReadMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][KU * 64];
+  __shared__ uint32_t s_row[4][64];  // the table row of the batch's first read's mapq (256 bytes)
+  uint32_t *row = s_row[threadIdx.x >> 6];
+  const uint8_t *lrow = reinterpret_cast<const uint8_t *>(row);
+  const int lane = threadIdx.x & 63;
+  uint32_t lmq = 0;
+  uint2 *out = reinterpret_cast<uint2 *>(mproj);
+  read_fill<KU>(
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
+      [&](int64_t r0) {  // most reads share one mapping quality: its table row in LDS
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        lmq = (uint32_t)R.mapq[r0];
+        row[lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      },
+      [&](const ReadMeta &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); },
+      [&](int64_t r, const ReadMeta &m, int32_t col) { return margin_fetch_rw(R, r, m, col, tab); },
+      [&](bool act, const MarginRW &o, int64_t, const ReadMeta &m, int32_t col, int64_t grow, int64_t slot) {
+        if (act) {
+          const uint2 w = o.x.gen ? o.x.word
+                                  : margin_terms8(piece_meta(m), o.x.q, o.x.valid, word_event_bits(m, col, o.v, o.evb),
+                                                  tab, lrow, lmq);
+          out[16 * grow + (col & 15)] = w;
+          auto has = [](uint32_t v) {  // a zero byte
+            return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
+          };
+          if (has(w.x) || has(w.y)) mnb[slot] = 1;
+        }
+      });
 }
 
 struct SomProjCfg {
