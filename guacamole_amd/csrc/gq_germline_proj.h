@@ -40,6 +40,15 @@
 #ifndef GQ_PROJ_ENT
 #define GQ_PROJ_ENT 6
 #endif
+#ifndef GQ_PROJ_NB
+#define GQ_PROJ_NB 4  // row batches per round (NB - 1 in flight while one is counted)
+#endif
+#ifndef GQ_PROJ_LAZY
+#define GQ_PROJ_LAZY 0  // A/B: 1 reads each locus's complex / MidDeletion words twice instead of holding them
+#endif
+#ifndef GQ_PROJ_GMIN
+#define GQ_PROJ_GMIN 0  // A/B: 1 skips the per-group row bound below the block's fewest rows (measured slower)
+#endif
 struct ProjCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = GQ_PROJ_WAVES;  // waves per workgroup, each on its own tiles
@@ -128,6 +137,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t vl;
     int32_t gn;
+    int32_t gmin;  // the fewest rows of the block's four slices (wave-uniform): batches below it need no bound
   };
   auto row_ctx = [&](uint32_t rec) -> RowCtx {
     const int64_t row0 = f64(rec, 16);
@@ -141,6 +151,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     x.vl = 4u * (uint32_t)(lane & 15) + (uint32_t)kProjRowBytes * (uint32_t)gbase;
     x.gn = (nr0 & -(int32_t)(g == 0)) | (nr1 & -(int32_t)(g == 1)) | (nr2 & -(int32_t)(g == 2)) |
            (nr3 & -(int32_t)(g == 3));
+    x.gmin = (dbg & 1) ? 0 : min(min(nr0, nr1), min(nr2, nr3));
     return x;
   };
   // the block's fullest slice, and whether the tile runs here (reads, no pbad slice, rows in range)
@@ -155,6 +166,11 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // 32-bit word per lane and row: the column's eight 4-bit codes.
   auto issue = [&](const RowCtx &x, int32_t k0, uint32_t (&w)[U]) {
     const uint32_t vb = x.vl + (uint32_t)kProjRowBytes * (uint32_t)k0;
+    if (GQ_PROJ_GMIN && k0 + U <= x.gmin) {  // uniform: every group's slice has these rows (most batches)
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(x.rsrc, (int)vb, kProjRowBytes * u, 0);
+      return;
+    }
     const int32_t rem = x.gn - k0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -167,7 +183,9 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
   // flight while this tile's sparse entries and decision run (no loads past the rows are
   // issued, and nothing waits for them).  primed: rows 0 .. 3U - 1 of the tile starting now are
   // already in a, b, c.
-  uint32_t a0[U], b0[U], c0[U], d0[U];
+  constexpr int NB = GQ_PROJ_NB;
+  static_assert(240 % (NB * U) == 0, "the 16-bit widening runs on a round boundary");
+  uint32_t bf[NB][U];
   // the first kEnt sparse entries per lane of a tile's reads (the rest: a loop), applied before
   // its counting (the entry loads' latency overlaps the primed row batches')
   constexpr int NE = C::kEnt;
@@ -209,9 +227,8 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     }
     const RowCtx cur = row_ctx(rec);
     if (!was_primed) {
-      issue(cur, 0, a0);
-      issue(cur, U, b0);
-      issue(cur, 2 * U, c0);
+#pragma unroll
+      for (int q = 0; q + 1 < NB; ++q) issue(cur, q * U, bf[q]);
     }
     const int64_t e0 = f64(rec, 24), e1 = f64(rec, 26);
     uint2 ent[NE];
@@ -248,6 +265,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     const bool next_ok = i + C::kWaves < i1 && rec_runs(rec_c);
     RowCtx nxt = cur;
     nxt.gn = 0;
+    nxt.gmin = 0;
     if (next_ok) nxt = row_ctx(rec_c);
     // ---- column counts: byte counters per base (loci 0-3 of the column in [0], 4-7 in [1]),
     //      widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 rows and at the end.
@@ -296,20 +314,19 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       }
       nn += U;
     };
-    // rows k0 .. k0 + 4U - 1 per round; the last round (uniform) issues the next tile's rows
-    // 0 .. 3U - 1 instead of this tile's past its end
-    for (int32_t k0 = 0, since = 0;; k0 += 4 * U) {
-      const bool last = k0 + 4 * U >= nrows;
-      issue(cur, k0 + 3 * U, d0);
-      count(a0);
-      issue(last ? nxt : cur, last ? 0 : k0 + 4 * U, a0);
-      count(b0);
-      issue(last ? nxt : cur, last ? U : k0 + 5 * U, b0);
-      count(c0);
-      issue(last ? nxt : cur, last ? 2 * U : k0 + 6 * U, c0);
-      count(d0);
+    // rows k0 .. k0 + NB U - 1 per round; the last round (uniform) issues the next tile's rows
+    // 0 .. (NB - 1) U - 1 instead of this tile's past its end
+    for (int32_t k0 = 0, since = 0;; k0 += NB * U) {
+      const bool last = k0 + NB * U >= nrows;
+      issue(cur, k0 + (NB - 1) * U, bf[NB - 1]);
+#pragma unroll
+      for (int q = 0; q + 1 < NB; ++q) {
+        count(bf[q]);
+        issue(last ? nxt : cur, last ? q * U : k0 + (NB + q) * U, bf[q]);
+      }
+      count(bf[NB - 1]);
       if (last) break;
-      since += 4 * U;
+      since += NB * U;
       if (since == 240) {  // uniform: bytes hold 240 rows at most
         fold();
         widen();
@@ -340,18 +357,27 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     if (!(dbg & 4)) {
       // complex elements per locus: prefix of the range differences over the block
       // this lane's eight words of each array, read once (conflict-free rows of 64 words)
+      // (GQ_PROJ_LAZY: summed here, read again per locus below — fewer live registers)
+      int32_t run = 0, mrun0 = 0;
+#if GQ_PROJ_LAZY
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        run += (int32_t)mk[64 * j + lane] >> 16;
+        mrun0 += (int32_t)dl[64 * j + lane];
+      }
+#else
       uint32_t m8[8], d8[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         m8[j] = mk[64 * j + lane];
         d8[j] = dl[64 * j + lane];
       }
-      int32_t run = 0, mrun0 = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         run += (int32_t)m8[j] >> 16;
         mrun0 += (int32_t)d8[j];
       }
+#endif
       int32_t ncx_run = (int32_t)wave_incl_scan((uint32_t)run) - run;  // before this lane's loci
       mid0 = (int32_t)wave_incl_scan((uint32_t)mrun0) - mrun0;  // the same for the MidDeletion ranges
       int32_t mid_run = mid0;
@@ -365,8 +391,13 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       //      kind 0 nothing, 1 a Ref/NoCall record, 2 a variant candidate (record pair), 3 complex
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+#if GQ_PROJ_LAZY
+        const uint32_t eacj = ev[64 * j + lane], etgj = ev[T + 64 * j + lane], m8j = mk[64 * j + lane];
+        const int32_t ddj = (int32_t)dl[64 * j + lane];
+#else
         const uint32_t eacj = ev[64 * j + lane], etgj = ev[T + 64 * j + lane], m8j = m8[j];
         const int32_t ddj = (int32_t)d8[j];
+#endif
         {
         const bool in = (inm >> j) & 1u;
         const uint32_t cA = cnt16(wA, j), cC = cnt16(wC, j), cT = cnt16(wT, j), cG = cnt16(wG, j);

@@ -528,10 +528,12 @@ struct __attribute__((aligned(16))) ReadMeta {
   int64_t p0;         // pool offset of locus 0 (column-eligible reads: base / quality of locus l at p0 + l)
   int32_t s, e;       // the read's [start, end)
   uint32_t info, mq;  // ColDesc info, mapping quality
-  int32_t col0, pad;  // first column
+  int32_t col0;       // first column
+  uint32_t evin;      // 1: its MD events are all in ev01 / ev23 (read_fill<true>), else at md_off
   int64_t md_off;     // its MD events
   int64_t qoff;       // its contig's first slice
   int64_t grow[3];    // global row of its first three pieces (-1: no row / pbad slice)
+  uint32_t ev01, ev23;  // up to four MD-event offsets from the read's start, 16 bits each (0xFFFF: none)
 };
 static_assert(sizeof(ReadMeta) == 80, "ReadMeta: five 16-byte LDS reads");
 constexpr int kReadPieces = 3;  // pieces per read held in ReadMeta (a 150 bp read spans <= 3 slices)
@@ -563,7 +565,8 @@ __device__ __forceinline__ int64_t piece_grow(const DevReads &R, int64_t r, int6
 // dbg (diagnostics, GQ_FILL_DBG; the pool is wrong when set): 1 no word loads, 2 no word stores;
 // 4: XCD-contiguous batches (workgroup i runs on XCD i % 8: each XCD takes one contiguous
 // eighth of the batches, so rows that pieces of neighbouring batches share meet in one L2).
-template <int kU, class B, class K, class F, class E>
+// EV: each read's MD events (up to four) are loaded with its records into ev01 / ev23.
+template <int kU, bool EV, class B, class K, class F, class E>
 __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restrict__ meta, uint32_t *__restrict__ owner,
                                           int dbg, B &&batch, K &&keep, F &&fetch, E &&emit) {
   const int lane = threadIdx.x & 63;
@@ -600,8 +603,28 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
     m.info = d.info;
     m.mq = mq;
     m.col0 = pr.col0;
-    m.pad = 0;
+    m.evin = 0;
+    m.ev01 = m.ev23 = 0xFFFFFFFFu;
     m.md_off = mdo;
+    if constexpr (EV) {
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+      if (in && nmd <= 4 && d.end - d.start < 0xFFF0) {  // (no word of the read reaches the 0xFFFF marker)
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = k < nmd ? R.md_ev[mdo + k] : 0xFFFFFFFFu;
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = v[k] >> 8;  // offsets (none: 0xFFFFFF)
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ok = ok && (k >= nmd || o[k] < 0xFFFFu);
+        if (ok) {
+          m.evin = 1;
+          m.ev01 = (o[0] & 0xFFFFu) | ((o[1] & 0xFFFFu) << 16);
+          m.ev23 = (o[2] & 0xFFFFu) | ((o[3] & 0xFFFFu) << 16);
+        }
+      }
+    }
     m.qoff = R.qoff[lo];
     uint32_t len = in && pr.col1 != kProjNone && pr.col1 > pr.col0 ? (uint32_t)(pr.col1 - pr.col0) : 0u;
     if (len && !keep(m)) len = 0;
@@ -649,6 +672,9 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
         mm.info = bq.x;
         mm.mq = bq.y;
         mm.col0 = (int32_t)bq.z;
+        mm.evin = bq.w;
+        mm.ev01 = eq.z;
+        mm.ev23 = eq.w;
         mm.md_off = (int64_t)((uint64_t)c.x | ((uint64_t)c.y << 32));
         mm.qoff = (int64_t)((uint64_t)c.z | ((uint64_t)c.w << 32));
         const int64_t g0 = (int64_t)((uint64_t)dq.x | ((uint64_t)dq.y << 32));

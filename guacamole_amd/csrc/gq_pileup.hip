@@ -511,7 +511,7 @@ __global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restr
   __shared__ ReadMeta s_meta[4][64];
   __shared__ uint32_t s_owner[4][KU * 64];
   uint32_t *out = reinterpret_cast<uint32_t *>(proj);
-  read_fill<KU>(
+  read_fill<KU, false>(
       R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, [](int64_t) {}, [](const ReadMeta &) { return true; },
       [&](int64_t r, const ReadMeta &m, int32_t col) { return proj_fetch(R, r, piece_meta(m), col); },
       [&](bool act, const ProjRaw &x, int64_t, const ReadMeta &, int32_t col, int64_t grow, int64_t) {

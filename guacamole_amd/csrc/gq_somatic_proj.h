@@ -247,7 +247,12 @@ __device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r
   const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
   const uint32_t *ev = R.md_ev + m.md_off;
   o.evb = 0;
-  if (nmd <= 4) {  // the common read: its events in the same round of loads as the qualities
+  if (m.evin) {  // the common read: its events came with its records (16-bit offsets; none: 0xFFFF)
+    o.v[0] = (m.ev01 & 0xFFFFu) << 8;
+    o.v[1] = (m.ev01 >> 16) << 8;
+    o.v[2] = (m.ev23 & 0xFFFFu) << 8;
+    o.v[3] = (m.ev23 >> 16) << 8;
+  } else if (nmd <= 4) {  // its events in the same round of loads as the qualities
 #pragma unroll
     for (int k = 0; k < 4; ++k) o.v[k] = k < nmd ? ev[k] : 0xFFFFFFFFu;
   } else {  // the first event at or past the word's first locus, then the word's events
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
   const int lane = threadIdx.x & 63;
   uint32_t lmq = 0;
   uint2 *out = reinterpret_cast<uint2 *>(mproj);
-  read_fill<KU>(
+  read_fill<KU, true>(
       R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
       [&](int64_t r0) {  // most reads share one mapping quality: its table row in LDS
         __builtin_amdgcn_wave_barrier();
