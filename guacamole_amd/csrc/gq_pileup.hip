@@ -446,9 +446,7 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
   ProjRaw x{0, 0, 0};
   if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
     const int64_t a = m.p0 + lb;
-    if (lb >= s && lb + 8 <= e) {
-      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a);
-    } else if (a >= 0 && a + 8 <= R.seq_cap) {  // an edge word: one load, the loci outside the read masked
+    if (a >= 0 && a + 8 <= R.seq_cap) {  // one load; an edge word's loci outside the read masked
       x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a) & edge_mask(s - lb, e - lb);
     } else {
       for (int q = 0; q < 8; ++q) {

@@ -125,6 +125,19 @@ __device__ __forceinline__ uint2 margin_terms8(const PieceMeta &m, uint64_t q, u
   }
   return make_uint2(v[0], v[1]);
 }
+// margin_terms8 for a wave whose words all look their terms up in the LDS row (no branches).
+__device__ __forceinline__ uint2 margin_terms8_lds(uint64_t q, uint32_t valid, uint32_t evb, const uint8_t *lrow) {
+  uint32_t v[2] = {0u, 0u};
+#pragma unroll
+  for (int q8 = 0; q8 < 8; ++q8) {
+    const uint32_t b = (uint32_t)(q >> (8 * q8)) & 0xFFu;
+    const uint32_t t0 = lrow[((b & 0x7Fu) << 1) | (((evb >> q8) & 1u) ^ 1u)];
+    const uint32_t t1 = (b & 0x80u) ? (uint32_t)kMargin8None : t0;  // a quality outside the table
+    const uint32_t t = ((valid >> q8) & 1u) ? t1 : (uint32_t)kMargin8Zero;
+    v[q8 >> 2] |= t << (8 * (q8 & 3));
+  }
+  return make_uint2(v[0], v[1]);
+}
 __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col,
                                                   uint32_t evb, const uint8_t *__restrict__ tab) {
   const int32_t s = m.s, e = m.e;
@@ -132,16 +145,10 @@ __device__ __forceinline__ MarginRaw margin_fetch(const DevReads &R, int64_t r, 
   MarginRaw x{0, make_uint2(0x80808080u, 0x80808080u), 0, 0};
   if (m.info & kColEligible) {
     const int64_t a = m.p0 + lb;
-    if (lb >= s && lb + 8 <= e) {
-      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a);
-      x.valid = 0xFFu;
-    } else if (a >= 0 && a + 8 <= R.seq_cap) {  // an edge word: one load, the loci outside the read masked
-      const uint64_t k = edge_mask(s - lb, e - lb);
-      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a) & k;
-      uint32_t v = 0;
-#pragma unroll
-      for (int q8 = 0; q8 < 8; ++q8) v |= ((k >> (8 * q8)) & 1u) << q8;
-      x.valid = v;
+    if (a >= 0 && a + 8 <= R.seq_cap) {  // one load; an edge word's loci outside the read masked
+      const int32_t lo = min(max(s - lb, 0), 8), hi = min(max(e - lb, 0), 8);
+      x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a) & edge_mask(lo, hi);
+      x.valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
     } else {
 #pragma unroll
       for (int q8 = 0; q8 < 8; ++q8) {
@@ -303,10 +310,13 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
       [&](const ReadMeta &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); },
       [&](int64_t r, const ReadMeta &m, int32_t col) { return margin_fetch_rw(R, r, m, col, tab); },
       [&](bool act, const MarginRW &o, int64_t, const ReadMeta &m, int32_t col, int64_t grow, int64_t slot) {
+        // (uniform: the wave's table lookups all in the LDS row, or per lane)
+        const bool all_lds = __ballot(act && !o.x.gen && m.mq != lmq) == 0;
         if (act) {
+          const uint32_t evb = word_event_bits(m, col, o.v, o.evb);
           const uint2 w = o.x.gen ? o.x.word
-                                  : margin_terms8(piece_meta(m), o.x.q, o.x.valid, word_event_bits(m, col, o.v, o.evb),
-                                                  tab, lrow, lmq);
+                          : all_lds ? margin_terms8_lds(o.x.q, o.x.valid, evb, lrow)
+                                    : margin_terms8(piece_meta(m), o.x.q, o.x.valid, evb, tab, lrow, lmq);
           out[16 * grow + (col & 15)] = w;
           auto has = [](uint32_t v) {  // a zero byte
             return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;

@@ -9,5 +9,5 @@ timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 rc=$?; echo "tests rc=$rc"; stop $rc
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "bench rc=$rc"; stop $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py > gpurun_out/${TAG}_prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --no-single-pass > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; exit $rc

@@ -39,7 +39,7 @@ def main():
     t = ctx.upload(tg.arrays)
     n = ctx.upload(ng.arrays)
     loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([L - 1], np.int64), np.array([0], np.int64))
-    som = ctx.somatic_standard(t, n, loci).rows()
+    som = ctx.somatic_standard(t, n, loci).rows
     germ = ctx.germline_threshold(t, loci, 8, False, False).tuples(["20"])
     print(json.dumps({"somatic": len(som), "somatic_digest": digest(som), "germline": len(germ),
                       "germline_digest": digest([list(map(str, r)) for r in germ])}))
