@@ -613,8 +613,8 @@ __global__ __launch_bounds__(SomProjCfg::kThreads) __attribute__((amdgpu_waves_p
       const uint32_t mask = (m8[j] & 15u) | (cA > (eac & 0xFFFFu) ? 1u : 0u) | (cC > (eac >> 16) ? 2u : 0u) |
                             (cT > (etg & 0xFFFFu) ? 4u : 0u) | (cG > (etg >> 16) ? 8u : 0u);
       const uint32_t low = mask & (0u - mask);
-      const uint32_t c_ref = cA * (low & 1u) + cC * ((low >> 1) & 1u) + cT * ((low >> 2) & 1u) + cG * (low >> 3) +
-                             nN * (low == 0u ? 1u : 0u);
+      const uint32_t c_ref = (cA & (0u - (low & 1u))) + (cC & (0u - ((low >> 1) & 1u))) +
+                             (cT & (0u - ((low >> 2) & 1u))) + (cG & (0u - ((low >> 3) & 1u))) + (low == 0u ? nN : 0u);
       bool agree = true;
       if constexpr (kRef) agree = ref_agrees(mask, ((j < 4 ? fb8.x : fb8.y) >> (8 * (j & 3))) & 0xFFu);
       const bool single = mask != 0 && (mask & (mask - 1u)) == 0;
