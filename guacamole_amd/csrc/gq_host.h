@@ -566,7 +566,8 @@ __device__ __forceinline__ int64_t piece_grow(const DevReads &R, int64_t r, int6
 // 4: XCD-contiguous batches (workgroup i runs on XCD i % 8: each XCD takes one contiguous
 // eighth of the batches, so rows that pieces of neighbouring batches share meet in one L2).
 // EV: each read's MD events (up to four) are loaded with its records into ev01 / ev23.
-template <int kU, bool EV, class B, class K, class F, class E>
+// kW: consecutive words of a read per lane (the lane-to-word mapping is done once per kW words).
+template <int kU, bool EV, int kW, class B, class K, class F, class E>
 __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restrict__ meta, uint32_t *__restrict__ owner,
                                           int dbg, B &&batch, K &&keep, F &&fetch, E &&emit) {
   const int lane = threadIdx.x & 63;
@@ -628,6 +629,7 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
     m.qoff = R.qoff[lo];
     uint32_t len = in && pr.col1 != kProjNone && pr.col1 > pr.col0 ? (uint32_t)(pr.col1 - pr.col0) : 0u;
     if (len && !keep(m)) len = 0;
+    const uint32_t nun = (len + (uint32_t)kW - 1u) / (uint32_t)kW;  // the read's lane units
     {
       const int64_t q0 = m.qoff + (pr.col0 >> 4);
       const int32_t npc = len ? ((pr.col1 - 1) >> 4) - (pr.col0 >> 4) + 1 : 0;
@@ -638,31 +640,31 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
       for (int j = 0; j < kReadPieces; ++j) m.grow[j] = g[j];
     }
     if (len) meta[lane] = m;
-    const uint32_t incl = wave_incl_scan(len), ex = incl - len;
+    const uint32_t incl = wave_incl_scan(nun), ex = incl - nun;
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     for (uint32_t w0 = 0; w0 < tot; w0 += 64 * kU) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) owner[64 * u + lane] = 0;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (len > 0 && ex > w0 && ex < w0 + 64 * kU) owner[ex - w0] = (uint32_t)lane + 1;  // the read's first word
+      if (nun > 0 && ex > w0 && ex < w0 + 64 * kU) owner[ex - w0] = (uint32_t)lane + 1;  // the read's first unit
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      int kk[kU];
-      int32_t col[kU];
-      bool act[kU];
-      int64_t grow[kU], slot[kU];
+      constexpr int N = kU * kW;
+      int kk[N];
+      int32_t col[N];
+      bool act[N];
+      int64_t grow[N], slot[N];
       ReadMeta pm[kU];
-      decltype(fetch((int64_t)0, pm[0], (int32_t)0)) raw[kU];
+      decltype(fetch((int64_t)0, pm[0], (int32_t)0)) raw[N];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const uint32_t wb = w0 + 64 * u, w = wb + (uint32_t)lane;
-        const unsigned long long run = __ballot(len > 0 && ex <= wb);  // the last of them runs at wb
+        const unsigned long long run = __ballot(nun > 0 && ex <= wb);  // the last of them runs at wb
         const uint32_t k_at = run ? 64u - (uint32_t)__clzll((long long)run) : 0u;  // its lane + 1
         const uint32_t k1 = max(wave_incl_max(owner[64 * u + lane]), k_at);
-        act[u] = w < tot;
-        const int k = act[u] ? (int)k1 - 1 : 0;
-        kk[u] = k;
+        const bool au = w < tot;
+        const int k = au ? (int)k1 - 1 : 0;
         const uint4 *src = reinterpret_cast<const uint4 *>(meta + k);
         const uint4 a = src[0], bq = src[1], c = src[2], dq = src[3], eq = src[4];
         ReadMeta &mm = pm[u];
@@ -681,20 +683,29 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
         const int64_t g1 = (int64_t)((uint64_t)dq.z | ((uint64_t)dq.w << 32));
         const int64_t g2 = (int64_t)((uint64_t)eq.x | ((uint64_t)eq.y << 32));
         const uint32_t kex = (uint32_t)__shfl((int)ex, k, 64);
-        col[u] = mm.col0 + (int32_t)(w - kex);
-        const int32_t pj = (col[u] >> 4) - (mm.col0 >> 4);
-        slot[u] = mm.qoff + (col[u] >> 4);
-        grow[u] = pj == 0 ? g0 : pj == 1 ? g1 : pj == 2 ? g2 : -2;
+        const int32_t cbase = mm.col0 + kW * (int32_t)(w - kex);
+        const int32_t col1 = (mm.e + 7) >> 3;  // the read's column end (prec_fill)
+#pragma unroll
+        for (int q = 0; q < kW; ++q) {
+          const int i = kW * u + q;
+          kk[i] = k;
+          col[i] = cbase + q;
+          act[i] = au && col[i] < col1;
+          const int32_t pj = (col[i] >> 4) - (mm.col0 >> 4);
+          slot[i] = mm.qoff + (col[i] >> 4);
+          grow[i] = pj == 0 ? g0 : pj == 1 ? g1 : pj == 2 ? g2 : -2;
+        }
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (act[u] && grow[u] == -2) grow[u] = piece_grow(R, 64 * b + kk[u], slot[u]);  // a long read's later piece
-        act[u] = act[u] && grow[u] >= 0;
-        if (act[u] && !(dbg & 1)) raw[u] = fetch(64 * b + kk[u], pm[u], col[u]);
-        else raw[u] = {};
+      for (int i = 0; i < N; ++i) {
+        if (act[i] && grow[i] == -2) grow[i] = piece_grow(R, 64 * b + kk[i], slot[i]);  // a long read's later piece
+        act[i] = act[i] && grow[i] >= 0;
+        if (act[i] && !(dbg & 1)) raw[i] = fetch(64 * b + kk[i], pm[i / kW], col[i]);
+        else raw[i] = {};
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) emit(act[u] && !(dbg & 2), raw[u], 64 * b + kk[u], pm[u], col[u], grow[u], slot[u]);
+      for (int i = 0; i < N; ++i)
+        emit(act[i] && !(dbg & 2), raw[i], 64 * b + kk[i], pm[i / kW], col[i], grow[i], slot[i]);
     }
     __builtin_amdgcn_wave_barrier();  // (the next batch rewrites meta)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -504,12 +504,12 @@ __global__ __launch_bounds__(256) void proj_fill(DevReads R, int64_t n_slices, u
 }
 
 // The projection pool, read-major (read_fill): a wave per 64 consecutive reads, a lane per word.
-template <int KU>
+template <int KU, int KW>
 __global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restrict__ proj, int dbg) {
   __shared__ ReadMeta s_meta[4][64];
   __shared__ uint32_t s_owner[4][KU * 64];
   uint32_t *out = reinterpret_cast<uint32_t *>(proj);
-  read_fill<KU, false>(
+  read_fill<KU, false, KW>(
       R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, [](int64_t) {}, [](const ReadMeta &) { return true; },
       [&](int64_t r, const ReadMeta &m, int32_t col) { return proj_fetch(R, r, piece_meta(m), col); },
       [&](bool act, const ProjRaw &x, int64_t, const ReadMeta &, int32_t col, int64_t grow, int64_t) {
@@ -2978,7 +2978,12 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
       hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
     } else if (n > 0) {
       const int64_t blocks = (std::min<int64_t>((n + 255) / 256, 1 << 20) + 7) & ~(int64_t)7;  // a wave per 64 reads
-      auto kf = fill_u == 2 ? proj_fill_rw<2> : fill_u == 4 ? proj_fill_rw<4> : proj_fill_rw<1>;
+      static const int fill_w = getenv("GQ_FILL_W") ? atoi(getenv("GQ_FILL_W")) : 1;  // words per lane unit
+      auto kf = fill_u == 2 ? proj_fill_rw<2, 1>
+                : fill_u == 4 ? proj_fill_rw<4, 1>
+                : fill_w == 2 ? proj_fill_rw<1, 2>
+                : fill_w == 4 ? proj_fill_rw<1, 4>
+                              : proj_fill_rw<1, 1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, (uint8_t *)pj, fill_dbg());
     }
     HIP_TRY(hipGetLastError());

@@ -1283,7 +1283,12 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
     } else if (t->d.n_reads > 0) {
       // mnb: set per slice by the words (a rebuild for another filter starts from zero)
       HIP_TRY(hipMemsetAsync(t->mnb, 0, (size_t)t->n_slices + 16, c->stream));
-      auto kf = fill_u == 2 ? mproj_fill_rw<2> : fill_u == 4 ? mproj_fill_rw<4> : mproj_fill_rw<1>;
+      static const int fill_w = getenv("GQ_FILL_W") ? atoi(getenv("GQ_FILL_W")) : 1;  // words per lane unit
+      auto kf = fill_u == 2 ? mproj_fill_rw<2, 1>
+                : fill_u == 4 ? mproj_fill_rw<4, 1>
+                : fill_w == 2 ? mproj_fill_rw<1, 2>
+                : fill_w == 4 ? mproj_fill_rw<1, 4>
+                              : mproj_fill_rw<1, 1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)((std::min<int64_t>((t->d.n_reads + 255) / 256, 1 << 20) + 7) & ~(int64_t)7)),
                          dim3(256), 0, c->stream, t->d, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,
                          (uint8_t *)t->mnb, fill_dbg());

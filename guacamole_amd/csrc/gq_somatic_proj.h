@@ -286,7 +286,7 @@ __device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r
 
 // The margin projection, read-major (read_fill): a wave per 64 consecutive reads, a lane per
 // word; mnb (zeroed by the caller) gets 1 on each slice holding a kMargin8None term.
-template <int KU>
+template <int KU, int KW>
 __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, const uint8_t *__restrict__ tab,
                                                      uint8_t *__restrict__ mproj, uint8_t *__restrict__ mnb, int dbg) {
   __shared__ ReadMeta s_meta[4][64];
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
   const int lane = threadIdx.x & 63;
   uint32_t lmq = 0;
   uint2 *out = reinterpret_cast<uint2 *>(mproj);
-  read_fill<KU, true>(
+  read_fill<KU, true, KW>(
       R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
       [&](int64_t r0) {  // most reads share one mapping quality: its table row in LDS
         __builtin_amdgcn_wave_barrier();
