@@ -509,6 +509,70 @@ __device__ __forceinline__ void slice_fill(const DevReads &R, const SliceWin &W,
   }
 }
 
+// ---- Projection words (proj_fill / proj_fill_rw and the somatic fused fill) ----
+// A general CIGAR's count segments (col_derive): Match/Mismatch runs, complex runs, MidDeletion runs.
+constexpr uint32_t kSegCount = 0, kSegComplex = 1, kSegMidDel = 2;
+__device__ __forceinline__ uint32_t proj_code(uint8_t b) {  // A 1, C 3, T 4, G 7; N and the rest 0
+  return (b == 'A' || b == 'C' || b == 'G' || b == 'T') ? (uint32_t)(b & 7u) : 0u;
+}
+
+// Byte codes of four ASCII bases (proj_code, SWAR): A 1, C 3, G 7, T 4, anything else 0.
+__device__ __forceinline__ uint32_t proj_codes4(uint32_t x) {
+  auto eq = [x](uint32_t pat) {  // 0x80 in the bytes equal to pat's (exact: no carries between bytes)
+    const uint32_t z = x ^ pat;
+    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+  };
+  const uint32_t m = eq(0x41414141u) | eq(0x43434343u) | eq(0x47474747u) | eq(0x54545454u);
+  return x & ((m >> 7) * 7u);
+}
+
+typedef uint64_t gq_u64u __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
+
+// The projection word of read r at column col (loci [8 col, 8 col + 8)): byte j = code of locus
+// 8 col + j | code of locus 8 col + j + 4 << 4 (4-bit codes, proj_code).  m: the read's piece
+// (slice_fill).  proj_fetch loads the word's eight bases (one 8-byte load inside a column-eligible
+// read; a general CIGAR's word is complete here); proj_code8 turns them into the word.
+struct ProjRaw {
+  uint64_t b;     // the bases, byte q = locus 8 col + q (0 outside the read)
+  uint32_t word;  // general CIGAR: the word itself
+  uint32_t gen;
+};
+__device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col) {
+  const int32_t s = m.s, e = m.e;
+  const int32_t lb = 8 * col;  // locus of byte 0
+  ProjRaw x{0, 0, 0};
+  if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
+    const int64_t a = m.p0 + lb;
+    if (a >= 0 && a + 8 <= R.seq_cap) {  // one load; an edge word's loci outside the read masked
+      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a) & edge_mask(s - lb, e - lb);
+    } else {
+      for (int q = 0; q < 8; ++q) {
+        const int32_t l = lb + q;
+        if (l >= s && l < e) x.b |= (uint64_t)R.seq[m.p0 + l] << (8 * q);
+      }
+    }
+    return x;
+  }
+  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
+  const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
+  const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+  const int64_t so = R.seq_off[r];
+  uint32_t v[2] = {0, 0};
+  for (int32_t q2 = 0; q2 < nseg; ++q2) {
+    const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
+    if ((b >> 16) != kSegCount) continue;
+    const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
+    if (ra >= lb + 8 || ra + rl <= lb) continue;
+    for (int q = 0; q < 8; ++q) {
+      const int32_t l = lb + q;
+      if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
+    }
+  }
+  x.word = v[0] | (v[1] << 4);
+  x.gen = 1;
+  return x;
+}
+
 // ---- Read-major fills (the default; slice_fill above is the A/B alternative, GQ_FILL=slice) ----
 inline int fill_dbg() {  // GQ_FILL_DBG (read_fill): diagnostics and the XCD-contiguous order
   static const int v = getenv("GQ_FILL_DBG") ? atoi(getenv("GQ_FILL_DBG")) : 0;
@@ -940,7 +1004,16 @@ struct H2DStager {
 // contig_read_begin) are in place: validation, read shape, projection pool, block index.
 gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
 // The projection (ProjRec) of a resident read set, derived on first use.
-gq_status ensure_projection(gq_ctx *c, const gq_dev_reads *d);
+// A margin projection wanted with the projection (the somatic tumor, germline-standard): with
+// GQ_FILL_ONE both are filled in one read-major pass (fused_projection_fill) when the projection
+// is derived — an A/B alternative: at chr20 60x it took 9.0 ms against 2.8 + 5.6 ms for the two
+// passes, so the default keeps them separate.
+struct MarginReq {
+  int min_mapq;
+  bool incl_align;
+};
+gq_status ensure_projection(gq_ctx *c, const gq_dev_reads *d, const MarginReq *mr = nullptr);
+gq_status fused_projection_fill(gq_ctx *c, const gq_dev_reads *d, uint8_t *proj_pool, const MarginReq &mr);
 // No-op launches that load each translation unit's code object onto the device (gq_open's prep).
 hipError_t warm_pileup(hipStream_t s);
 hipError_t warm_somatic(hipStream_t s);

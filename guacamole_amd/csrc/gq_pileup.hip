@@ -211,7 +211,7 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
 // Returns false if the in-kernel path cannot take the read (P op, M bases past the sequence,
 // a deleted locus without its MD base, sizes beyond the packed fields): such reads keep the
 // exact walker, which raises the reference's error where it applies.
-constexpr uint32_t kSegCount = 0, kSegComplex = 1, kSegMidDel = 2;
+// (segment kinds kSegCount / kSegComplex / kSegMidDel: gq_host.h)
 template <class Emit>
 __device__ bool general_segments(const DevReads &R, int64_t r, Emit emit) {
   const int32_t s = R.start[r], nmd = R.n_md[r], slen = R.seq_len[r], ncig = R.n_cigar[r];
@@ -315,9 +315,6 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
 }
 
 // ---- Projections (germline_proj, ProjRec in gq_kernels.h), derived after col_derive -------
-__device__ __forceinline__ uint32_t proj_code(uint8_t b) {  // A 1, C 3, T 4, G 7; N and the rest 0
-  return (b == 'A' || b == 'C' || b == 'G' || b == 'T') ? (uint32_t)(b & 7u) : 0u;
-}
 __device__ __forceinline__ bool proj_ok(uint32_t info) { return (info & (kColEligible | kColGeneral)) != 0; }
 
 // Sparse entries of each read's projection; entry n is 0.
@@ -417,63 +414,6 @@ __global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, unsi
     k += prec[r].col1 != kProjNone ? 1u : 0u;
   for (int d = 32; d >= 1; d >>= 1) k += __shfl_xor(k, d, 64);
   if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
-}
-
-// Byte codes of four ASCII bases (proj_code, SWAR): A 1, C 3, G 7, T 4, anything else 0.
-__device__ __forceinline__ uint32_t proj_codes4(uint32_t x) {
-  auto eq = [x](uint32_t pat) {  // 0x80 in the bytes equal to pat's (exact: no carries between bytes)
-    const uint32_t z = x ^ pat;
-    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
-  };
-  const uint32_t m = eq(0x41414141u) | eq(0x43434343u) | eq(0x47474747u) | eq(0x54545454u);
-  return x & ((m >> 7) * 7u);
-}
-
-typedef uint64_t gq_u64u __attribute__((aligned(1)));  // unaligned 8-byte loads (gfx950 global memory)
-
-// The projection word of read r at column col (loci [8 col, 8 col + 8)): byte j = code of locus
-// 8 col + j | code of locus 8 col + j + 4 << 4 (4-bit codes, proj_code).  m: the read's piece
-// (slice_fill).  proj_fetch loads the word's eight bases (one 8-byte load inside a column-eligible
-// read; a general CIGAR's word is complete here); proj_code8 turns them into the word.
-struct ProjRaw {
-  uint64_t b;     // the bases, byte q = locus 8 col + q (0 outside the read)
-  uint32_t word;  // general CIGAR: the word itself
-  uint32_t gen;
-};
-__device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, const PieceMeta &m, int32_t col) {
-  const int32_t s = m.s, e = m.e;
-  const int32_t lb = 8 * col;  // locus of byte 0
-  ProjRaw x{0, 0, 0};
-  if (m.info & kColEligible) {  // [S|H]* (M|=|X) [S|H]*: locus l holds base p0 + l
-    const int64_t a = m.p0 + lb;
-    if (a >= 0 && a + 8 <= R.seq_cap) {  // one load; an edge word's loci outside the read masked
-      x.b = *reinterpret_cast<const gq_u64u *>(R.seq + a) & edge_mask(s - lb, e - lb);
-    } else {
-      for (int q = 0; q < 8; ++q) {
-        const int32_t l = lb + q;
-        if (l >= s && l < e) x.b |= (uint64_t)R.seq[m.p0 + l] << (8 * q);
-      }
-    }
-    return x;
-  }
-  // general CIGAR: the count segments (ref_off | len << 16, seq_off | kind << 16)
-  const int32_t nmd = (int32_t)(m.info & 0xFFFFu), nseg = (int32_t)((m.info >> 18) & 0xFFu);
-  const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-  const int64_t so = R.seq_off[r];
-  uint32_t v[2] = {0, 0};
-  for (int32_t q2 = 0; q2 < nseg; ++q2) {
-    const uint32_t a = sg[2 * q2], b = sg[2 * q2 + 1];
-    if ((b >> 16) != kSegCount) continue;
-    const int32_t ra = s + (int32_t)(a & 0xFFFFu), rl = (int32_t)(a >> 16), sp = (int32_t)(b & 0xFFFFu);
-    if (ra >= lb + 8 || ra + rl <= lb) continue;
-    for (int q = 0; q < 8; ++q) {
-      const int32_t l = lb + q;
-      if (l >= ra && l < ra + rl) v[q >> 2] |= proj_code(R.seq[so + sp + (l - ra)]) << (8 * (q & 3));
-    }
-  }
-  x.word = v[0] | (v[1] << 4);
-  x.gen = 1;
-  return x;
 }
 
 // The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
@@ -2880,7 +2820,7 @@ gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return 
 // slices, each slice's read window and its pieces' rows (one greedy pass, stored), the rows'
 // offsets, the 4-bit code pool, the sparse entries.  A set no such kernel reads (the somatic
 // normal) never pays for it.
-gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
+gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginReq *mr) {
   gq_dev_reads *d = const_cast<gq_dev_reads *>(cd);
   if (d->projected) return GQ_OK;
   const auto t0 = std::chrono::steady_clock::now();
@@ -2976,6 +2916,9 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd) {
       const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
       auto kf = fill_u == 4 ? proj_fill<4> : fill_u == 2 ? proj_fill<2> : proj_fill<1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
+    } else if (n > 0 && mr && getenv("GQ_FILL_ONE")) {  // A/B: with the margin projection in one pass (measured slower)
+      const gq_status st = fused_projection_fill(c, d, (uint8_t *)pj, *mr);
+      if (st) return st;
     } else if (n > 0) {
       const int64_t blocks = (std::min<int64_t>((n + 255) / 256, 1 << 20) + 7) & ~(int64_t)7;  // a wave per 64 reads
       static const int fill_w = getenv("GQ_FILL_W") ? atoi(getenv("GQ_FILL_W")) : 1;  // words per lane unit

@@ -1255,6 +1255,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 1
   }
 }
 
+}  // namespace (reopened below)
+
+// The projection's pool and the margin projection filled together (ensure_projection with a
+// MarginReq): the margin pool and its slice flags allocated and preset, the term table built, then
+// one pm_fill_rw pass.
+gq_status gq::fused_projection_fill(gq_ctx *c, const gq_dev_reads *t, uint8_t *proj_pool, const MarginReq &mr) {
+  const int key = 2 * mr.min_mapq + (mr.incl_align ? 1 : 0);
+  if (!t->mproj) {
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)(128 * t->n_rows + 32)));
+    t->mproj = p;
+    void *q = nullptr;
+    HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
+    t->mnb = q;
+  }
+  HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
+  HIP_TRY(hipMemsetAsync(t->mnb, 0, (size_t)t->n_slices + 16, c->stream));
+  void *tab = nullptr;
+  HIP_TRY(hipMalloc(&tab, 256 * 256));
+  hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, mr.incl_align ? 1 : 0, (uint8_t *)tab);
+  HIP_TRY(hipGetLastError());
+  if (t->d.n_reads > 0) {
+    hipLaunchKernelGGL(pm_fill_rw, dim3((unsigned)((std::min<int64_t>((t->d.n_reads + 255) / 256, 1 << 20) + 7) & ~(int64_t)7)),
+                       dim3(256), 0, c->stream, t->d, proj_pool, mr.min_mapq, (const uint8_t *)tab,
+                       (uint8_t *)t->mproj, (uint8_t *)t->mnb, fill_dbg());
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(tab);
+  t->mproj_mapq = key;
+  return GQ_OK;
+}
+
+namespace {
+
 gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_mapq, bool incl_align = true) {
   const int key = 2 * min_mapq + (incl_align ? 1 : 0);  // the projection's filter and probability model
   if (t->mproj && t->mproj_mapq == key) return GQ_OK;
@@ -1577,7 +1612,8 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   // one loci plan per sample, 512-locus tiles aligned to 512-locus blocks (somatic_proj)
   Plan pt, pn;
-  gq_status st = ensure_projection(c, t);  // (derived on first use)
+  const MarginReq mreq{(int)p->min_mapq, true};  // (with the projection, the margin projection in the same pass)
+  gq_status st = ensure_projection(c, t, &mreq);  // (derived on first use)
   if (st) return st;
   st = plan(c, t, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;
@@ -2067,7 +2103,8 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
   c->timings = gq_timings{};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pt;
-  gq_status st = ensure_projection(c, rd);  // (derived on first use)
+  const MarginReq mreq{(int)p->min_mapq, false};  // (with the projection, the margin projection in the same pass)
+  gq_status st = ensure_projection(c, rd, &mreq);  // (derived on first use)
   if (st) return st;
   st = plan(c, rd, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;

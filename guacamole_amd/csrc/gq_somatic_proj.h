@@ -326,6 +326,61 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
       });
 }
 
+// The projection and the margin projection of one read set in one read-major pass (the
+// projection derived for a caller that also reads the margin projection): one batch setup per 64
+// reads, each word's bases and qualities loaded together; margin words only for reads the mapq
+// filter keeps (the others keep the pool's kMargin8Zero fill).
+struct PmRaw {
+  ProjRaw p;
+  MarginRW m;
+};
+__global__ __launch_bounds__(256) void pm_fill_rw(DevReads R, uint8_t *__restrict__ proj, int min_mapq,
+                                                  const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
+                                                  uint8_t *__restrict__ mnb, int dbg) {
+  __shared__ ReadMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][64];
+  __shared__ uint32_t s_row[4][64];  // the table row of the batch's first read's mapq (256 bytes)
+  uint32_t *row = s_row[threadIdx.x >> 6];
+  const uint8_t *lrow = reinterpret_cast<const uint8_t *>(row);
+  const int lane = threadIdx.x & 63;
+  uint32_t lmq = 0;
+  uint32_t *pout = reinterpret_cast<uint32_t *>(proj);
+  uint2 *mout = reinterpret_cast<uint2 *>(mproj);
+  auto kept = [=](const ReadMeta &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); };
+  read_fill<1, true, 1>(
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
+      [&](int64_t r0) {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        lmq = (uint32_t)R.mapq[r0];
+        row[lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      },
+      [](const ReadMeta &) { return true; },
+      [&](int64_t r, const ReadMeta &m, int32_t col) {
+        return PmRaw{proj_fetch(R, r, piece_meta(m), col), margin_fetch_rw(R, r, m, col, tab)};
+      },
+      [&](bool act, const PmRaw &o, int64_t, const ReadMeta &m, int32_t col, int64_t grow, int64_t slot) {
+        if (act)
+          pout[16 * grow + (col & 15)] =
+              o.p.gen ? o.p.word : proj_codes4((uint32_t)o.p.b) | (proj_codes4((uint32_t)(o.p.b >> 32)) << 4);
+        const bool mact = act && kept(m);
+        const bool all_lds = __ballot(mact && !o.m.x.gen && m.mq != lmq) == 0;  // uniform
+        if (mact) {
+          const uint32_t evb = word_event_bits(m, col, o.m.v, o.m.evb);
+          const uint2 w = o.m.x.gen ? o.m.x.word
+                          : all_lds ? margin_terms8_lds(o.m.x.q, o.m.x.valid, evb, lrow)
+                                    : margin_terms8(piece_meta(m), o.m.x.q, o.m.x.valid, evb, tab, lrow, lmq);
+          mout[16 * grow + (col & 15)] = w;
+          auto has = [](uint32_t v) {  // a zero byte
+            return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
+          };
+          if (has(w.x) || has(w.y)) mnb[slot] = 1;
+        }
+      });
+}
+
 struct SomProjCfg {
   static constexpr int kT = 512;
   static constexpr int kWaves = 4;

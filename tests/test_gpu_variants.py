@@ -3,7 +3,8 @@ default build's records bit for bit (the default is checked against the oracle e
 GQ_CALL_SPLIT=1 (somatic caller as a front kernel + back end over stored element records),
 GQ_CALL_WPE=2 (the one-kernel caller at 2 waves per SIMD), GQ_FILL_U=2 / 4 (the read-major
 projection and margin fills at 2 or 4 words per lane and round; GQ_FILL_W: 2 or 4 consecutive
-words of a read per lane), GQ_FILL=slice (the slice-major
+words of a read per lane), GQ_FILL_ONE=1 (the projection and the margin projection in one pass
+instead of two), GQ_FILL=slice (the slice-major
 fills).  A synthetic 300 kb 60x / 30x pair with a raised somatic
 rate, so hundreds of candidates and calls reach every path."""
 import json
@@ -29,7 +30,7 @@ def test_kernel_variants_give_the_default_records():
     base = _run({})
     assert base["somatic"] > 20 and base["germline"] > 100
     for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, {"GQ_FILL_U": "2"}, {"GQ_FILL_U": "4"}, {"GQ_FILL_W": "2"},
-                  {"GQ_FILL_W": "4"},
+                  {"GQ_FILL_W": "4"}, {"GQ_FILL_ONE": "1"},
                   {"GQ_FILL": "slice"}):
         got = _run(extra)
         assert got == base, (extra, got, base)
