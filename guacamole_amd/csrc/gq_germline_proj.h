@@ -171,13 +171,13 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       for (int u = 0; u < U; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(x.rsrc, (int)vb, kProjRowBytes * u, 0);
       return;
     }
-    const int32_t rem = x.gn - k0;
+    // (slices hold a multiple of kRowPad = U rows: a batch lies wholly inside its group's slice or
+    // wholly past it, one bound per batch)
+    const uint32_t v = k0 < x.gn ? vb : 0x80000000u;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t v = u < rem ? vb : 0x80000000u;
-      w[u] = __builtin_amdgcn_raw_buffer_load_b32(x.rsrc, (int)v, kProjRowBytes * u, 0);
-    }
+    for (int u = 0; u < U; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(x.rsrc, (int)v, kProjRowBytes * u, 0);
   };
+  static_assert(U == kRowPad, "row batches are the slices' row padding");
   // Tiles are software-pipelined: the Tile + TileX records arrive two tiles ahead, and a tile's
   // last counting round issues the NEXT tile's first three row batches, so those loads are in
   // flight while this tile's sparse entries and decision run (no loads past the rows are

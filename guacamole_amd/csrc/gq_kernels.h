@@ -93,6 +93,9 @@ struct ProjRec {
 static_assert(sizeof(ProjRec) == 8, "ProjRec layout");
 constexpr int32_t kProjNone = (int32_t)0x80000000;
 constexpr int kProjRowBytes = 64;  // a slice row: 16 columns x 8 loci x 4 bits
+// A slice's rows are padded with zero rows to a multiple of kRowPad (row_count), so
+// germline_proj bounds its row batches (kRowPad rows) once per batch, not once per row.
+constexpr int kRowPad = 4;
 // Sparse entries of a read (uint2 {x = locus, y}), in any order:
 //   y bit 31 clear: MD event / N base at locus x: bits 0-3 the MD reference base's std_bit
 //     (0 for an N base without an MD event), bits 4-6 the read base's category there (0-3 A C

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, u
     const SliceWin W = slice_stored(R, slot);
     const int32_t n = slice_assign_rows(R, W, prow + R.soff[slot], s_rend[wv], s_fl[wv]);
     if ((threadIdx.x & 63) == 0) {
-      srows[slot] = n < 0 ? 0 : n;
+      srows[slot] = n < 0 ? 0 : (n + kRowPad - 1) & ~(kRowPad - 1);  // zero rows up to a multiple of kRowPad
       if (n < 0) pbad[slot] = 1;
     }
   }
