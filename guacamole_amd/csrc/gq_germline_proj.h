@@ -74,7 +74,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr,
     int32_t *__restrict__ slow, int dbg) {
   // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the projection loads,
-  // 2 skip the sparse entries, 4 skip the decision
+  // 2 skip the sparse entries, 4 skip the decision, 8 skip writing its records
   using C = ProjCfg;
   constexpr int T = C::kT, U = C::kU;
   // per locus: event read bases (A | C << 16 at [i], T | G << 16 at [T + i]); MD bits 0-3 |
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(ProjCfg::kThreads) __attribute__((amdgpu_waves_per_
       visited += (uint32_t)__popc(livem);
       amb += (uint32_t)__popc(ambm);
     }
-    if (__ballot(kinds != 0) != 0) {  // rare: records / complex items to write
+    if (!(dbg & 8) && __ballot(kinds != 0) != 0) {  // rare: records / complex items to write
       const unsigned rbase = wave_reserve_lds_n(out.lds + 0, nrec);
       const unsigned cbase = wave_reserve_lds_n(out.lds + 1, ncpx);
       CallRec *prec_out = recs + out.base[0];
