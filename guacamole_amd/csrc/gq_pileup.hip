@@ -610,6 +610,15 @@ __global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__re
   if (nmd <= 0) return;
   const uint32_t *ev = R.md_ev + R.md_off[r];
   uint8_t *rb = ev_rb + R.md_off[r];
+  if (simple) {  // [S|H]* (M|=|X) [S|H]*: the event at reference offset o reads base lead + o
+    const int64_t so = R.seq_off[r];
+    const int32_t sl = R.seq_len[r];
+    for (int k = 0; k < nmd; ++k) {
+      const int32_t o = (int32_t)(ev[k] >> 8);
+      rb[k] = (o < mlen && ld + o < sl) ? R.seq[so + ld + o] : (uint8_t)0;
+    }
+    return;
+  }
   int32_t ref = 0, rp = 0;
   int k = 0;
   for (int c = 0; c < n && k < nmd; ++c) {
