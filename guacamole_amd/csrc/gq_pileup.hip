@@ -535,33 +535,52 @@ __global__ void validate_reads(DevReads R, int *__restrict__ bad) {
 // precondition).  Pool in read order: 16 bytes per thread, coalesced; the rare other bytes
 // find their read by binary search of seq_off and clear its flag (clean preset to 1).
 __global__ void pool_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__restrict__ n_nbase) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte chunk
-  const int64_t b0 = c * 16;
-  if (b0 >= R.seq_bytes) return;
-  uint32_t ws[4] = {0, 0, 0, 0};
-  if (b0 + 16 <= R.seq_cap) {  // uploaded pools have a zeroed tail; a wrapped one may end anywhere
-    const uint4 w = *reinterpret_cast<const uint4 *>(R.seq + b0);
-    ws[0] = w.x, ws[1] = w.y, ws[2] = w.z, ws[3] = w.w;
-  } else {
-    for (int k = 0; k < 16 && b0 + k < R.seq_bytes; ++k) ws[k >> 2] |= (uint32_t)R.seq[b0 + k] << (8 * (k & 3));
-  }
+  // two 16-byte chunks per thread (both loads in flight before either is checked), kBlock apart
+  const int64_t c0 = (int64_t)blockIdx.x * (2 * kBlock) + threadIdx.x;
+  uint32_t ws[2][4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint8_t x = (uint8_t)(ws[k >> 2] >> (8 * (k & 3)));
-    if (b0 + k >= R.seq_bytes || x == 'A' || x == 'C' || x == 'G' || x == 'T') continue;
-    int64_t lo = 0, hi = R.n_reads - 1;  // last read with seq_off <= b0 + k
-    while (lo < hi) {
-      const int64_t m = (lo + hi + 1) >> 1;
-      if (R.seq_off[m] <= b0 + k) lo = m;
-      else hi = m - 1;
+  for (int h = 0; h < 2; ++h) {
+    const int64_t b0 = (c0 + (int64_t)h * kBlock) * 16;
+    ws[h][0] = ws[h][1] = ws[h][2] = ws[h][3] = 0x41414141u;  // past the pool: nothing to check
+    if (b0 >= R.seq_bytes) continue;
+    if (b0 + 16 <= R.seq_cap) {  // uploaded pools have a zeroed tail; a wrapped one may end anywhere
+      const uint4 w = *reinterpret_cast<const uint4 *>(R.seq + b0);
+      ws[h][0] = w.x, ws[h][1] = w.y, ws[h][2] = w.z, ws[h][3] = w.w;
+    } else {
+      ws[h][0] = ws[h][1] = ws[h][2] = ws[h][3] = 0;
+      for (int k = 0; k < 16 && b0 + k < R.seq_bytes; ++k) ws[h][k >> 2] |= (uint32_t)R.seq[b0 + k] << (8 * (k & 3));
     }
-    // zero-length reads share an offset with their neighbour: every read holding the byte.
-    // An N keeps the read clean and is counted (the projection's N-base entries).
-    for (int64_t r = lo; r >= 0 && R.seq_off[r] + R.seq_len[r] > b0 + k; --r)
-      if (R.seq_off[r] <= b0 + k) {
-        if (x == 'N') atomicAdd(&n_nbase[r], 1u);
-        else clean[r] = 0;
+  }
+  // bytes equal to A, C, G or T: 0x80 in their byte (exact SWAR compare, no carries between bytes)
+  auto acgt = [](uint32_t x) {
+    auto eq = [x](uint32_t pat) {
+      const uint32_t z = x ^ pat;
+      return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+    };
+    return eq(0x41414141u) | eq(0x43434343u) | eq(0x47474747u) | eq(0x54545454u);
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t b0 = (c0 + (int64_t)h * kBlock) * 16;
+    if (b0 >= R.seq_bytes) continue;
+    if ((acgt(ws[h][0]) & acgt(ws[h][1]) & acgt(ws[h][2]) & acgt(ws[h][3])) == 0x80808080u) continue;  // the common chunk
+    for (int k = 0; k < 16; ++k) {
+      const uint8_t x = (uint8_t)(ws[h][k >> 2] >> (8 * (k & 3)));
+      if (b0 + k >= R.seq_bytes || x == 'A' || x == 'C' || x == 'G' || x == 'T') continue;
+      int64_t lo = 0, hi = R.n_reads - 1;  // last read with seq_off <= b0 + k
+      while (lo < hi) {
+        const int64_t m = (lo + hi + 1) >> 1;
+        if (R.seq_off[m] <= b0 + k) lo = m;
+        else hi = m - 1;
       }
+      // zero-length reads share an offset with their neighbour: every read holding the byte.
+      // An N keeps the read clean and is counted (the projection's N-base entries).
+      for (int64_t r = lo; r >= 0 && R.seq_off[r] + R.seq_len[r] > b0 + k; --r)
+        if (R.seq_off[r] <= b0 + k) {
+          if (x == 'N') atomicAdd(&n_nbase[r], 1u);
+          else clean[r] = 0;
+        }
+    }
   }
 }
 // The same per read (a wrapped pool in another order), one thread per read.
@@ -1764,7 +1783,7 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->stream));
       const int64_t chunks = (d->d.seq_bytes + 15) / 16;
       if (chunks > 0)
-        hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+        hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, c->stream,
                            d->d, (uint8_t *)cl, (uint32_t *)nnb);
     } else {
       hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl, (uint32_t *)nnb);
