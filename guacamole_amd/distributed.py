@@ -194,6 +194,31 @@ def all_gather_objects(obj) -> list:
     return out
 
 
+class PeerLoadError(RuntimeError):
+    """Raised on every rank whose own load succeeded when another rank's load failed: the ranks
+    load different parts of the input, so an error in one rank's segments must end all of them
+    together instead of leaving the others blocked in the next collective."""
+
+
+def _together(fn, device):
+    """Run fn() on every rank; if it raised on any rank, raise on every rank.  The failing rank
+    re-raises its own exception (type and message unchanged: the CLI reports it as the
+    one-process run does); the others raise PeerLoadError naming the first failing rank and its
+    message."""
+    err, out = None, None
+    try:
+        out = fn()
+    except Exception as e:  # re-raised below, on every rank
+        err = e
+    if _all_true(err is None, device):
+        return out
+    msgs = all_gather_objects(None if err is None else "%s: %s" % (type(err).__name__, err))
+    if err is not None:
+        raise err
+    r = next(i for i, m in enumerate(msgs) if m is not None)
+    raise PeerLoadError("rank %d failed to load its reads (%s)" % (r, msgs[r]))
+
+
 def device_ingest_ranks(ctx, paths: Sequence[str], filters, builder, parallelism: int, accuracy: int, rank: int,
                         world: int, device):
     """The multi-GPU ingest: each rank decodes on its own GPU only the BGZF blocks whose records
@@ -203,7 +228,7 @@ def device_ingest_ranks(ctx, paths: Sequence[str], filters, builder, parallelism
     ranges with their task ids, the contig names) or None when some rank cannot take the device
     path (plain gzip, an unsorted file, device memory): every rank then takes the host loader."""
     from .bamdev import MappedBam, load_reads_device
-    maps = [MappedBam(p, populate=False) for p in paths]
+    maps = _together(lambda: [MappedBam(p, populate=False) for p in paths], device)
     if not _all_true(all(m.ok for m in maps), device):
         return None
     dicts = [m.contigs() for m in maps]
@@ -255,8 +280,12 @@ def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accurac
         for m in range(max(0, m0 - slack), min(n_micro, m1 + slack)):
             b.put_set(inv[m], 0)
         decoded = LociSet(b.result())
-        sets = load(decoded)
+        sets = _together(lambda: load(decoded), device)
         if not _all_true(all(x is not None for x in sets), device):
+            return None
+        # the counts must see every read overlapping the micro partitions: widen the halo first
+        sets = _widen_halos(sets, lambda halos: load(decoded, halos), device)
+        if sets is None:
             return None
         counts = np.zeros(n_micro, np.int64)
         for x in sets:
@@ -271,30 +300,58 @@ def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accurac
         parts = partition_loci_by_counts(tasks, loci, micro, counts)
         flat = flatten_partitions(parts, cidx)
         sizes = np.array([inv[m].count for m in range(n_micro)], np.int64)
-        edge = np.concatenate([[0], np.cumsum(sizes)])
-        bounds = [int(edge[r * n_micro // world]) for r in range(world + 1)]
+        bounds = depth_bounds(sizes, counts, world)
     rr = ranks_by_position(flat, bounds)
     sel = rr == rank
     mine = tuple(np.ascontiguousarray(np.asarray(a)[sel]) for a in flat)
     region = loci_of(mine, names)
-    if sets is None or not covers(decoded, region):
-        sets = None  # (the first load's memory goes before the second)
-        sets = load(region)
+    if _any_true(sets is None or not covers(decoded, region), device):
+        if sets is None or not covers(decoded, region):
+            sets = None  # (the first load's memory goes before the second)
+        sets = _together(lambda: load(region) if sets is None else sets, device)
     if not _all_true(all(x is not None for x in sets), device):
         return None
-    # Without an index a rank plans `halo` loci back from each of its ranges: a read reaching
-    # further back is found only by the rank whose segments hold its start.  The longest span any
-    # rank saw (per input) is shared, and a rank whose probe plan's halo is shorter loads again.
+    sets = _widen_halos(sets, lambda halos: load(region, halos), device)
+    return None if sets is None else (sets, mine)
+
+
+def depth_bounds(sizes: np.ndarray, counts: np.ndarray, world: int) -> List[int]:
+    """Rank bounds in loci positions from the all-reduced micro-partition read counts: rank r's
+    block starts at the micro-partition edge nearest to where the cumulative count (+ 1e-3 per
+    locus, so empty stretches still spread) crosses r / world of the total — balanced by read weight as
+    assign_tasks_to_ranks balances the host path, not by loci."""
+    sizes = np.asarray(sizes, np.int64)
+    w = np.asarray(counts, np.float64) + 1e-3 * sizes
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    edge = np.concatenate([[0], np.cumsum(sizes)])
+    total = cum[-1] if cum[-1] > 0 else 1.0
+    out = [0]
+    for r in range(1, world):
+        want = total * r / world
+        m = int(np.searchsorted(cum, want, "left"))  # the nearer of the two micro-partition edges
+        if m > 0 and (m >= len(cum) or want - cum[m - 1] < cum[m] - want):
+            m -= 1
+        out.append(max(out[-1], int(edge[min(m, len(sizes))])))
+    out.append(int(edge[-1]))
+    return out
+
+
+def _widen_halos(sets, reload, device):
+    """Without an index a rank plans `halo` loci back from each of its ranges: a read reaching
+    further back is found only by the rank whose segments hold its start.  The longest span any
+    rank saw (per input) is shared, and a rank whose probe plan's halo is shorter loads again
+    with twice that span (reload(halos) -> sets).  Every rank takes the branch together."""
     spans = _all_max([int(getattr(x, "timings", {}).get("max_span", 0)) for x in sets], device)
     plans = [getattr(x, "timings", {}).get("plan") for x in sets]
     short = [p is not None and not p["used_index"] and g > p["halo"] for p, g in zip(plans, spans)]
-    if _any_true(any(short), device):  # every rank takes this branch together (collectives inside)
+    if _any_true(any(short), device):  # (collectives inside)
+        halos = [max(2 * g, p["halo"]) if p is not None else 0 for p, g in zip(plans, spans)]
         if any(short):
             sets = None
-            sets = load(region, [max(2 * g, p["halo"]) if p is not None else 0 for p, g in zip(plans, spans)])
+        sets = _together(lambda: reload(halos) if sets is None else sets, device)
         if not _all_true(all(x is not None for x in sets), device):
             return None
-    return sets, mine
+    return sets
 
 
 def _gatherv_to_rank0(mine, sizes: List[int], device):

@@ -253,3 +253,53 @@ def test_probe_halo_is_widened_by_another_ranks_span():
         assert p.exitcode == 0
     assert got[0] == (0, [None, [10000]], 10000)  # (this stand-in load does not re-plan itself)
     assert got[1] == (1, [None, [10000]], 10000)
+
+
+def _fail_worker(rank, world, port, q):
+    """Rank 1's load raises (a malformed record in its segments only): both ranks must raise, rank
+    1 its own error and rank 0 a PeerLoadError naming it, instead of rank 0 blocking."""
+    import torch.distributed as dist
+    from guacamole_amd.distributed import PeerLoadError, rank_loci_and_reads
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def load(region, halos=None):
+        if rank == 1:
+            raise ValueError("bad record 7 in rank 1's segments")
+        return [_Loaded(1, 150, 1000)]
+    try:
+        rank_loci_and_reads(load, ["c"], [100_000], LociSet.parse("all"), 4, 0, rank, world, "cpu")
+        q.put((rank, "returned"))
+    except PeerLoadError as e:
+        q.put((rank, "peer: " + str(e)))
+    except ValueError as e:
+        q.put((rank, "own: " + str(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_load_error_on_one_rank_raises_on_every_rank():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == (0, "peer: rank 1 failed to load its reads (ValueError: bad record 7 in rank 1's segments)")
+    assert got[1] == (1, "own: bad record 7 in rank 1's segments")
+
+
+def test_depth_bounds_balance_reads_not_loci():
+    """Rank bounds by cumulative read counts: a deep first half puts the cut inside it."""
+    from guacamole_amd.distributed import depth_bounds
+    sizes = np.full(8, 1000, np.int64)
+    counts = np.array([300, 300, 300, 300, 50, 50, 50, 50], np.int64)
+    assert depth_bounds(sizes, counts, 2) == [0, 2000, 8000]
+    assert depth_bounds(sizes, np.zeros(8, np.int64), 4) == [0, 2000, 4000, 6000, 8000]
+    assert depth_bounds(sizes, counts, 1) == [0, 8000]
