@@ -154,11 +154,18 @@ def _common_args(p: argparse.ArgumentParser) -> None:
                    help="Maximum number of genotypes to output. 0 (default) means output all genotypes.")
     p.add_argument("--loci", default="", help="Loci at which to call variants (e.g. 'all', 'chr1:0-1000,chr2')")
     p.add_argument("--loci-from-file", default="", help="Path to file giving loci")
-    p.add_argument("--out", default="", help="Output path (.vcf or .json; empty = JSON to stdout)")
+    p.add_argument("--out", default="",
+                   help="Output path: .json (or empty: stdout) Avro-JSON, .vcf a VCF directory, else ADAM Parquet")
     p.add_argument("--parallelism", type=int, default=0, help="Num variant calling tasks (loci partitions)")
     p.add_argument("--partition-accuracy", type=int, default=250,
                    help="Num micro partitions per task in loci partitioning; 0 = uniform")
     p.add_argument("--device", type=int, default=0, help="GPU index")
+    # ParquetArgs (bdg-utils cli; Common.scala:50): the options of the ADAM Parquet output
+    p.add_argument("-parquet_block_size", type=int, default=128 * 1024 * 1024, help="Parquet block size (default = 128mb)")
+    p.add_argument("-parquet_page_size", type=int, default=1 * 1024 * 1024, help="Parquet page size (default = 1mb)")
+    p.add_argument("-parquet_compression_codec", default="GZIP", type=str.upper, help="Parquet compression codec")
+    p.add_argument("-parquet_disable_dictionary", action="store_true", help="Disable dictionary encoding")
+    p.add_argument("-parquet_logging_level", default="SEVERE", help="Parquet logging level (default = severe)")
 
 
 def _loci_builder(args) -> LociSetBuilder:
@@ -177,42 +184,82 @@ class OutputFormatError(ValueError):
     """An --out path the reference would write in a format this build does not produce."""
 
 
-def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None, max_genotypes: int = 0) -> None:
+def _write_genotypes(path: str, genotypes: List[dict], contig_lengths=None, max_genotypes: int = 0,
+                     parquet: Optional[dict] = None) -> None:
     """Common.writeVariantsFromArguments (Common.scala:246-304), by the path's extension
     (lower-cased, after stripMargin):
       * "" or .json: Avro-JSON, serially, to stdout or to the file (overwritten, :254-289);
       * .vcf: toVariantContext.coalesce(1).saveAsVcf (:290-293), a Hadoop output DIRECTORY
         holding one part-r-00000 and the committer's _SUCCESS marker (README.md:49-51); an
         existing path is refused, as Hadoop's checkOutputSpecs refuses it;
-      * anything else: adamParquetSave (:294-302).  ADAM Parquet is not produced here, so such
-        a path is refused up front rather than silently written in another format.
+      * anything else: adamParquetSave (:294-302): a Hadoop output directory of Parquet part
+        files, one per loci task (output.write_parquet_dir).  parquet: ParquetArgs (codec,
+        page_size, block_size, dictionary) and the records' task ids (part_of, n_parts).
     --max-genotypes reaches RDD.sample(false, maxGenotypes, 0) as the sampling FRACTION
     (Common.scala:247-249): 1 keeps every genotype, larger values are refused by Spark's
     Bernoulli sampler ("must be on interval [0, 1]"), as here.  --out-chunks only coalesces
     partitions (order-preserving), so it does not change what is written."""
-    from .output import write_json, write_vcf_dir
+    from .output import write_json, write_parquet_dir, write_vcf_dir
     check_output_path(path)
     if max_genotypes > 1:
         raise ValueError("Sampling fraction (%s) must be on interval [0, 1]" % float(max_genotypes))
-    if path.lower().endswith(".vcf"):
+    kind = output_kind(path)
+    if kind == "vcf":
         write_vcf_dir(path, genotypes, contig_lengths)
+    elif kind == "parquet":
+        write_parquet_dir(path, genotypes, **(parquet or {}))
     else:
         write_json(path, genotypes)
 
 
-def check_output_path(path: str) -> None:
-    """Refuse, before any work, an --out the reference would write as ADAM Parquet or a VCF
-    directory that already exists (Common.scala:254, 290, 294)."""
-    import os
+def output_kind(path: str) -> str:
+    """"json", "vcf" or "parquet" (Common.scala:253-302)."""
     low = path.lower()
     if path == "" or low.endswith(".json"):
+        return "json"
+    return "vcf" if low.endswith(".vcf") else "parquet"
+
+
+def check_output_path(path: str, codec: str = "GZIP") -> None:
+    """Refuse, before any work, an output directory (VCF or Parquet) that already exists, as
+    Hadoop's FileOutputFormat.checkOutputSpecs does (Common.scala:290, 294), and a Parquet codec
+    this build cannot write."""
+    import os
+    from .output import PARQUET_CODECS
+    kind = output_kind(path)
+    if kind == "json":
         return
-    if low.endswith(".vcf"):
-        if os.path.exists(path):
-            raise OutputFormatError("Output directory %s already exists" % path)
-        return
-    raise OutputFormatError("--out %s: the reference writes this as ADAM Parquet (adamParquetSave, Common.scala:"
-                            "294-302), which this build does not produce; use a .vcf or .json path" % path)
+    if os.path.exists(path):
+        raise OutputFormatError("Output directory %s already exists" % path)
+    if kind == "parquet" and codec not in PARQUET_CODECS:
+        raise OutputFormatError("-parquet_compression_codec %s: this build writes %s" % (codec, ", ".join(
+            sorted(PARQUET_CODECS))))
+
+
+def _all_flat(mine):
+    """Every rank's flattened loci ranges (rank order = task order), on every rank."""
+    got = all_gather_objects([np.asarray(a) for a in mine])
+    return tuple(np.concatenate([g[k] for g in got]) for k in range(4))
+
+
+def parquet_options(args, flat=None, contig_index=None, rows_contig=None, rows_pos=None) -> dict:
+    """ParquetArgs (bdg-utils cli, mixed into Common.Arguments.Base, Common.scala:50) and the part
+    file of each record: the loci task whose range holds it (flat = flatten_partitions arrays),
+    since the callers' genotypes RDD has one partition per task."""
+    opts = dict(codec=args.parquet_compression_codec, page_size=args.parquet_page_size,
+                block_size=args.parquet_block_size, dictionary=not args.parquet_disable_dictionary)
+    if flat is not None and rows_pos is not None:
+        contig, start, end, task = (np.asarray(a, np.int64) for a in flat)
+        part = np.zeros(len(rows_pos), np.int64)
+        if len(rows_pos) and len(task):
+            key = contig * (1 << 40) + start  # ranges sorted by (contig, start) within the key space
+            o = np.argsort(key, kind="stable")
+            rk = np.asarray([contig_index[c] for c in rows_contig], np.int64) * (1 << 40) + np.asarray(rows_pos,
+                                                                                                       np.int64)
+            i = np.clip(np.searchsorted(key[o], rk, "right") - 1, 0, len(o) - 1)
+            part = task[o][i]
+        opts.update(part_of=part, n_parts=int(task.max()) + 1 if len(task) else 1)
+    return opts
 
 
 def device_ingest(args, *paths: str) -> bool:
@@ -269,7 +316,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
     _common_args(p)
     args = p.parse_args(argv)
     clock = StageClock()
-    check_output_path(args.out)
+    check_output_path(args.out, args.parquet_compression_codec)
     rank, world, local, gdev = init_from_env()
     warn_default_parallelism(args, world)
     builder = _loci_builder(args)
@@ -319,6 +366,7 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
         per_rank = gather_germline(calls, gdev)
         # each rank numbers its own samples (by first appearance in what it read): names travel
         rank_names = all_gather_objects(list(mine_rs.sample_names))
+        flat = _all_flat(mine) if output_kind(args.out) == "parquet" else None
         if per_rank is None:
             clock.mark("call")
             clock.report(rank=rank, reads=int(mine_rs.n), loci=int(sum(np.asarray(mine[2]) - np.asarray(mine[1]))),
@@ -343,7 +391,10 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
         if rows is None:
             rows = calls.tuples(rs.contig_names)
         out = [germline_genotype(c, l, sample_name(s), gt, ref, alt) for c, l, s, gt, ref, alt, fl in rows]
-        _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
+        pq = None
+        if output_kind(args.out) == "parquet":
+            pq = parquet_options(args, flat, rs.contig_index(), [r[0] for r in rows], [r[1] for r in rows])
+        _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes, pq)
     clock.mark("write")
     n_out = len(rows) if rows is not None else len(calls)
     print("Called %d genotypes." % n_out, file=sys.stderr)
@@ -378,7 +429,7 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
     _common_args(p)
     args = p.parse_args(argv)
     clock = StageClock()
-    check_output_path(args.out)
+    check_output_path(args.out, args.parquet_compression_codec)
     rank, world, local, gdev = init_from_env()
     warn_default_parallelism(args, world)
     builder = _loci_builder(args)
@@ -430,6 +481,9 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         else:  # each rank read its own part: the first tumor sample of the lowest rank that has one
             sample = next((n[0] for n in all_gather_objects(list(tumor.sample_names)) if n), "default")
     stats: Dict[str, int] = {}
+    all_flat = None
+    if output_kind(args.out) == "parquet":  # every rank's tasks: the part file of each record
+        all_flat = _all_flat(flat) if world > 1 else flat
     rows = somatic_standard_reads(
         ctx, tumor, normal, flat, odds=args.odds, min_mapq=args.min_mapq,
         filter_multi_allelic=int(args.filter_multi_allelic), max_read_depth=args.max_tumor_read_depth,
@@ -451,7 +505,11 @@ def somatic_standard_main(argv: Sequence[str]) -> int:
         rows = dbsnp_join(rows, read_dbsnp_vcf(args.dbsnp_vcf))
     from .output import somatic_genotype
     out = [somatic_genotype(r["contig"], r, sample) for r in rows]
-    _write_genotypes(args.out, out, tumor.contig_lengths_map, args.max_genotypes)
+    pq = None
+    if all_flat is not None:
+        pq = parquet_options(args, all_flat, tumor.contig_index(), [r["contig"] for r in rows],
+                             [r["locus"] for r in rows])
+    _write_genotypes(args.out, out, tumor.contig_lengths_map, args.max_genotypes, pq)
     clock.mark("write")
     print("Called %d somatic genotypes." % len(out), file=sys.stderr)
     clock.report(genotypes=len(out), **report)
@@ -554,7 +612,7 @@ def germline_standard_main(argv: Sequence[str]) -> int:
     _common_args(p)
     args = p.parse_args(argv)
     single_process_only("germline-standard")
-    check_output_path(args.out)
+    check_output_path(args.out, args.parquet_compression_codec)
     if args.truth_genotypes:
         raise ValueError("--truth-genotypes (concordance report) is not supported")
     builder = _loci_builder(args)
@@ -572,7 +630,10 @@ def germline_standard_main(argv: Sequence[str]) -> int:
     from .output import called_allele_genotype
     out = [called_allele_genotype(r["contig"], r, rs.sample_names[r["sample"]] if r["sample"] < len(rs.sample_names)
                                   else "default") for r in rows]
-    _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes)
+    pq = None
+    if output_kind(args.out) == "parquet":
+        pq = parquet_options(args, flat, rs.contig_index(), [r["contig"] for r in rows], [r["locus"] for r in rows])
+    _write_genotypes(args.out, out, rs.contig_lengths_map, args.max_genotypes, pq)
     print("Called %d genotypes." % len(out), file=sys.stderr)
     return 0
 

@@ -22,7 +22,7 @@ from __future__ import annotations
 import json
 import math
 import sys
-from typing import Dict, Iterable, List, Optional, TextIO, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, TextIO, Tuple
 
 import numpy as np
 
@@ -50,6 +50,22 @@ GENOTYPE_SCHEMA: List[Tuple[str, str, object]] = [
     ("splitFromMultiAllelic", "boolean?", False), ("isPhased", "?boolean", None), ("phaseSetId", "?int", None),
     ("phaseQuality", "?int", None)]
 _RECORDS = {"Contig": CONTIG_SCHEMA, "Variant": VARIANT_SCHEMA, "Genotype": GENOTYPE_SCHEMA}
+# Records the callers never set (always null in their output) but which the Parquet schema still
+# carries as groups: restated from bdg-formats 0.6.1, parity unpinned like the rest
+STRUCTURAL_VARIANT_SCHEMA: List[Tuple[str, str, object]] = [
+    ("type", "?StructuralVariantType", None), ("assembly", "?string", None), ("precise", "boolean?", True),
+    ("startWindow", "?int", None), ("endWindow", "?int", None)]
+ANNOTATIONS_SCHEMA: List[Tuple[str, str, object]] = [
+    ("variantIsPassing", "?boolean", None), ("variantFilters", "[string]", []), ("downsampled", "?boolean", None),
+    ("baseQRankSum", "?float", None), ("fisherStrandBiasPValue", "?float", None), ("rmsMapQ", "?float", None),
+    ("mapq0Reads", "?int", None), ("mqRankSum", "?float", None), ("readPositionRankSum", "?float", None),
+    ("genotypePriors", "[float]", []), ("genotypePosteriors", "[float]", []), ("vqslod", "?float", None),
+    ("culprit", "?string", None), ("attributes", "{string}", {})]
+_ENUMS = {"GenotypeAllele": ["Ref", "Alt", "OtherAlt", "NoCall"],
+          "StructuralVariantType": ["DELETION", "INSERTION", "INVERSION", "MOBILE_INSERTION", "MOBILE_DELETION",
+                                    "DUPLICATION", "TANDEM_DUPLICATION"]}
+_ALL_RECORDS = dict(_RECORDS, StructuralVariant=STRUCTURAL_VARIANT_SCHEMA,
+                    VariantCallingAnnotations=ANNOTATIONS_SCHEMA)
 
 
 def germline_genotype(contig: str, start: int, sample: str, alleles, ref: str, alt: str) -> Dict:
@@ -189,6 +205,160 @@ def write_vcf_dir(path: str, genotypes: List[Dict], contig_lengths: Optional[Dic
     write_vcf(part, genotypes, contig_lengths)
     open(os.path.join(path, "_SUCCESS"), "w").close()
     return part
+
+
+# ---- ADAM Parquet (adamParquetSave) -------------------------------------------------------
+# parquet-mr names a part file getDefaultWorkFile(codec extension + ".parquet")
+PARQUET_CODECS = {"UNCOMPRESSED": ("none", ""), "SNAPPY": ("snappy", ".snappy"), "GZIP": ("gzip", ".gz")}
+
+
+def avro_schema(record: str = "Genotype", _seen=None) -> Dict:
+    """The Avro schema of a restated bdg-formats record, as parquet-avro stores it in the
+    footer (key "parquet.avro.schema"): named types spelled out at first use, then by name."""
+    seen = set() if _seen is None else _seen
+    seen.add(record)
+
+    def typ(t: str):
+        if t.startswith("["):
+            return {"type": "array", "items": typ(t[1:-1])}
+        if t.startswith("{"):
+            return {"type": "map", "values": typ(t[1:-1])}
+        base = t.strip("?")
+        if base in _ALL_RECORDS:
+            inner = _NS + base if base in seen else avro_schema(base, seen)
+        elif base in _ENUMS:
+            inner = _NS + base if base in seen else {"type": "enum", "name": base, "namespace": _NS[:-1],
+                                                     "symbols": _ENUMS[base]}
+            seen.add(base)
+        else:
+            inner = base
+        if t.startswith("?"):
+            return ["null", inner]
+        if t.endswith("?"):
+            return [inner, "null"]
+        return inner
+    fields = [{"name": n, "type": typ(t), "default": d} for n, t, d in _ALL_RECORDS[record]]
+    return {"type": "record", "name": record, "namespace": _NS[:-1], "fields": fields}
+
+
+def _arrow_type(t: str):
+    """parquet-avro's mapping of an Avro type (AvroSchemaConverter): a union with null is an
+    optional column, records groups, enums and strings UTF8 binaries, arrays and maps required."""
+    import pyarrow as pa
+    if t.startswith("["):
+        return pa.list_(pa.field("array", _arrow_type(t[1:-1]), nullable=False))
+    if t.startswith("{"):
+        return pa.map_(pa.string(), pa.field("value", _arrow_type(t[1:-1]), nullable=False))
+    base = t.strip("?")
+    if base in _ALL_RECORDS:
+        return pa.struct(_arrow_fields(base))
+    if base in _ENUMS or base == "string":
+        return pa.string()
+    return {"long": pa.int64(), "int": pa.int32(), "float": pa.float32(), "boolean": pa.bool_()}[base]
+
+
+def _arrow_fields(record: str):
+    import pyarrow as pa
+    return [pa.field(n, _arrow_type(t), nullable="?" in t) for n, t, _ in _ALL_RECORDS[record]]
+
+
+def plain_record(record: str, value: Optional[Dict]) -> Dict:
+    """Every schema field of a record in schema order with its default filled in (no union
+    wrappers): the row parquet-avro writes for a builder that set only some fields."""
+    out: Dict = {}
+    value = value or {}
+    for name, typ, default in _ALL_RECORDS[record]:
+        v = value.get(name, default)
+        base = typ.strip("?")
+        if typ.startswith("["):
+            v = list(v)
+        elif typ.startswith("{"):
+            v = dict(v)
+        elif v is not None and base in _ALL_RECORDS:
+            v = plain_record(base, v)
+        out[name] = v
+    return out
+
+
+def unwrap_avro_json(record: str, datum: Optional[Dict]) -> Optional[Dict]:
+    """A record read back from avro_json (unions wrapped as {"<type>": value}) as plain_record
+    shapes it, so the two writers' outputs compare field for field."""
+    if datum is None:
+        return None
+    out: Dict = {}
+    for name, typ, _ in _ALL_RECORDS[record]:
+        v = datum[name]
+        base = typ.strip("?")
+        if isinstance(v, dict) and not typ.startswith("{") and len(v) == 1:
+            (k, v), = v.items()
+        if v is not None and base in _ALL_RECORDS:
+            v = unwrap_avro_json(base, v)
+        out[name] = v
+    return out
+
+
+def write_parquet_dir(path: str, genotypes: List[Dict], part_of: Optional[Sequence[int]] = None, n_parts: int = 1,
+                      codec: str = "GZIP", page_size: int = 1 << 20, block_size: int = 128 << 20,
+                      dictionary: bool = True) -> List[str]:
+    """adamParquetSave (Common.scala:294-302; ADAM 0.18 rdd.map((null, _)).saveAsNewAPIHadoopFile
+    through AvroParquetOutputFormat) for Genotype records: the Hadoop output directory `path`
+    with one part-r-NNNNN<codec>.parquet per RDD partition (record i goes to part part_of[i]; the
+    callers' genotypes RDD has one partition per loci task, empty ones still written), the
+    summary files _metadata / _common_metadata, and _SUCCESS.  Options are ParquetArgs'
+    (-parquet_compression_codec GZIP, -parquet_page_size 1 MiB, -parquet_block_size 128 MiB,
+    dictionary encoding on).  The schema is the restated bdg-formats Genotype, with the Avro
+    schema in the footer; byte parity with parquet-mr's files is unpinned."""
+    import os
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    if codec not in PARQUET_CODECS:
+        raise ValueError("-parquet_compression_codec %s is not available (one of %s)"
+                         % (codec, ", ".join(sorted(PARQUET_CODECS))))
+    comp, ext = PARQUET_CODECS[codec]
+    schema = pa.schema(_arrow_fields("Genotype"),
+                       metadata={"parquet.avro.schema": json.dumps(avro_schema()), "writer.model.name": "avro"})
+    os.makedirs(path, exist_ok=False)
+    part_of = np.zeros(len(genotypes), np.int64) if part_of is None else np.asarray(part_of, np.int64)
+    n_parts = max(1, int(n_parts), int(part_of.max()) + 1 if len(part_of) else 1)
+    order = np.argsort(part_of, kind="stable")
+    bounds = np.searchsorted(part_of[order], np.arange(n_parts + 1))
+    collector, files = [], []
+    for p in range(n_parts):
+        rows = [plain_record("Genotype", genotypes[i]) for i in order[bounds[p]:bounds[p + 1]]]
+        table = pa.Table.from_pylist(rows, schema=schema)
+        per_row = table.nbytes / max(1, table.num_rows)
+        name = "part-r-%05d%s.parquet" % (p, ext)
+        pq.write_table(table, os.path.join(path, name), compression=comp, data_page_size=int(page_size),
+                       use_dictionary=bool(dictionary), row_group_size=max(1, int(block_size / max(1.0, per_row))),
+                       use_compliant_nested_type=False, metadata_collector=collector)
+        collector[-1].set_file_path(name)
+        files.append(os.path.join(path, name))
+    pq.write_metadata(schema, os.path.join(path, "_common_metadata"), use_compliant_nested_type=False)
+    pq.write_metadata(schema, os.path.join(path, "_metadata"), metadata_collector=collector,
+                      use_compliant_nested_type=False)
+    open(os.path.join(path, "_SUCCESS"), "w").close()
+    return files
+
+
+def read_parquet_dir(path: str) -> List[Dict]:
+    """The Genotype rows of a write_parquet_dir directory, part files in name order (maps as
+    dicts)."""
+    import glob
+    import os
+    import pyarrow.parquet as pq
+    out: List[Dict] = []
+
+    def fix(record: str, v):
+        for name, typ, _ in _ALL_RECORDS[record]:
+            base = typ.strip("?")
+            if typ.startswith("{"):
+                v[name] = dict(v[name])
+            elif v[name] is not None and base in _ALL_RECORDS:
+                fix(base, v[name])
+        return v
+    for f in sorted(glob.glob(os.path.join(path, "part-r-*.parquet"))):
+        out.extend(fix("Genotype", r) for r in pq.read_table(f).to_pylist())
+    return out
 
 
 def write_vcf(path: str, genotypes: List[Dict], contig_lengths: Optional[Dict[str, int]] = None) -> None:

@@ -123,6 +123,29 @@ def test_cli_germline_vcf_and_somatic_json(tmp_path):
     assert rows and all(r["alleles"] == ["Ref", "Alt"] and r["readDepth"]["int"] >= 8 for r in rows)
 
 
+def test_cli_parquet_equals_json(tmp_path):
+    """--out X.adam (adamParquetSave, Common.scala:294-302): the CLI's Parquet directory holds one
+    part per loci task and its rows equal the Avro-JSON output's records, for both callers."""
+    import os
+    from guacamole_amd.commands import main
+    from guacamole_amd.output import read_avro_json, read_parquet_dir, unwrap_avro_json
+    for cmd in (["germline-threshold", "--reads", fixture("chrM.sorted.bam"), "--parallelism", "3"],
+                ["somatic-standard", "--tumor-reads", fixture("tumor.chr20.tough.sam"), "--normal-reads",
+                 fixture("normal.chr20.tough.sam"), "--parallelism", "2"]):
+        js, pq = str(tmp_path / (cmd[0] + ".json")), str(tmp_path / (cmd[0] + ".adam"))
+        assert main(cmd + ["--out", js]) == 0
+        assert main(cmd + ["--out", pq]) == 0
+        parts = sorted(f for f in os.listdir(pq) if f.startswith("part-r-"))
+        assert len(parts) == int(cmd[-1])
+        want = [unwrap_avro_json("Genotype", r) for r in read_avro_json(open(js).read())]
+        got = read_parquet_dir(pq)
+        assert len(got) == len(want) > 0
+        for x, y in zip(got, want):
+            if y["expectedAlleleDosage"] is not None:
+                assert np.float32(x.pop("expectedAlleleDosage")) == np.float32(y.pop("expectedAlleleDosage"))
+            assert x == y
+
+
 def test_synthetic_column_path_dense_outputs(gpu_ctx):
     """emit_ref / emit_no_call through the column kernel (HomRef / NoCall rows inline,
     variant candidates through germline_expand); the column kernel keeps nearly every tile."""
