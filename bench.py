@@ -113,6 +113,15 @@ def main() -> int:
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
+    # --gpus N: one rank per GPU.  Without a launcher (WORLD_SIZE unset) N > 1 starts the N ranks
+    # itself as a child torch.distributed.run job, before anything here touches the GPU.
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%s: launch one rank per GPU (torch.distributed.run "
+              "--nproc-per-node %d)" % (args.gpus, os.environ.get("WORLD_SIZE"), args.gpus), file=sys.stderr)
+        return 2
+
     from guacamole_amd import native, synthetic
     from guacamole_amd.distributed import gather_images_to_rank0, rank_info
 
@@ -173,7 +182,18 @@ def main() -> int:
             torch.cuda.synchronize()
             dist.barrier()
 
-    def step():
+    def sync():  # the library's calls return with their stream drained; torch's too at N > 1
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+
+    def step(resident: bool = False):
+        """One pass over the shard from the resident SoA: every structure derived from the reads
+        (upload-time derivation, projection) built again, then the call (inputs
+        resident, pileups rebuilt per run as GermlineThresholdCaller.run does, :58-88).
+        resident=True: the call alone on the already-derived read set (resident_step_ms)."""
+        if not resident:
+            ctx.rederive(reads)
         calls = ctx.germline_threshold_device(reads, loci, args.threshold)
         if dist is not None:
             gather_images_to_rank0(calls, gather_dev)
@@ -181,26 +201,42 @@ def main() -> int:
 
     # one shot (cold): the first call on the fresh read set derives the projection it reads
     t = time.perf_counter()
-    step()
+    first = step(resident=True)
     cold_ms = (time.perf_counter() - t) * 1e3
     cold_tm = ctx.timings()
+    first_rows = first.to_host().tuples(g.contig_names) if rank == 0 and world == 1 else None
     for _ in range(args.warmup):
         step()
     barrier()
-    pileup_ms, walk_ms = [], []
+    pileup_ms, walk_ms, step_ms, derive_ms, proj_ms = [], [], [], [], []
     stage_ms = {"plan_ms": [], "complex_ms": [], "finalize_ms": []}
     walk_frac = []
     t = time.perf_counter()
     for _ in range(args.steps):
+        t1 = time.perf_counter()
         calls = step()
+        sync()
+        step_ms.append((time.perf_counter() - t1) * 1e3)
         tm = ctx.timings()
         pileup_ms.append(tm["pileup_ms"])
         walk_ms.append(tm["walk_ms"])
         for k in stage_ms:
             stage_ms[k].append(tm[k])
         walk_frac.append(tm["walk_tiles"] / max(1, tm["tiles"]))
+        sti = ctx.proj_stats(reads)
+        derive_ms.append(sti["derive_ms"])
+        proj_ms.append(sti["proj_ms"])
     barrier()
     elapsed = time.perf_counter() - t
+    # the re-derived pass gives the records of the first call on the freshly uploaded set
+    rederive_identical = None if first_rows is None else calls.to_host().tuples(g.contig_names) == first_rows
+    res_ms = []
+    for _ in range(max(5, min(args.steps, 20))):
+        t1 = time.perf_counter()
+        calls = step(resident=True)
+        sync()
+        res_ms.append((time.perf_counter() - t1) * 1e3)
+    barrier()
     if dist is not None:
         import torch
         dev = "cuda:%d" % local if backend == "nccl" else "cpu"
@@ -275,6 +311,11 @@ def main() -> int:
                      "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
                      "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
+        "step_ms_median": float(np.median(step_ms)),
+        "step_stages_ms": {"upload_derive_ms": float(np.median(derive_ms)), "projection_ms": float(np.median(proj_ms))},
+        "rederive_identical": rederive_identical,
+        "resident_step_ms": float(np.median(res_ms)),
+        "resident_step_loci_per_s": visited / (float(np.median(res_ms)) * 1e-3),
         "kernel_only_loci_per_s": visited / ((k_ms + float(np.mean(walk_ms))) * 1e-3),
         "device_stages_ms": {k: float(np.mean(v)) for k, v in stage_ms.items()},
         "host_results_loci_per_s": visited / (host_ms_step * 1e-3),
@@ -323,6 +364,19 @@ def main() -> int:
     if rank == 0:
         print(json.dumps(line))
     return 0
+
+
+def launch_ranks(n: int) -> int:
+    """python bench.py --gpus N without a launcher: the same command as N ranks under
+    torch.distributed.run (127.0.0.1, a free port), as a child process; its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def write_calls(args, calls, g, gather_dev, world: int, rank: int):

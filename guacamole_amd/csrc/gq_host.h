@@ -905,11 +905,57 @@ struct gq_ctx {
   }
 };
 
+// Device buffers of the structures derived from a resident read set's SoA (the upload-time
+// derivation, the projection, the margin projection) and of their temporaries.  A temporary goes
+// back to `spare` when done; gq_reads_rederive hands every live buffer back, and a derivation of
+// the same read set then takes its sizes from the spares: no hipMalloc / hipFree (each an
+// implicit device synchronisation) on a re-derivation.
+struct DerivedPool {
+  std::vector<std::pair<void *, size_t>> live, spare;
+  hipError_t get(void **p, size_t bytes) {
+    bytes = std::max(bytes, (size_t)16);
+    size_t best = spare.size();
+    for (size_t i = 0; i < spare.size(); ++i)  // the smallest spare that fits without much waste
+      if (spare[i].second >= bytes && spare[i].second <= bytes + bytes / 4 + 65536 &&
+          (best == spare.size() || spare[i].second < spare[best].second))
+        best = i;
+    if (best < spare.size()) {
+      *p = spare[best].first;
+      live.push_back(spare[best]);
+      spare.erase(spare.begin() + (long)best);
+      return hipSuccess;
+    }
+    *p = nullptr;
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) live.emplace_back(*p, bytes);
+    return e;
+  }
+  void put(void *p) {  // (stream-ordered: later work on the same stream may reuse it)
+    for (size_t i = 0; i < live.size(); ++i)
+      if (live[i].first == p) {
+        spare.push_back(live[i]);
+        live.erase(live.begin() + (long)i);
+        return;
+      }
+  }
+  void release_all() {
+    spare.insert(spare.end(), live.begin(), live.end());
+    live.clear();
+  }
+  void free_all() {
+    for (auto &x : live) (void)hipFree(x.first);
+    for (auto &x : spare) (void)hipFree(x.first);
+    live.clear();
+    spare.clear();
+  }
+};
+
 struct gq_dev_reads {
   gq_ctx *ctx = nullptr;
   gq::DevReads d{};
   std::vector<int64_t> contig_read_begin;  // host copy
-  std::vector<void *> owned;               // device allocations owned by this handle
+  std::vector<void *> owned;               // device allocations of the SoA owned by this handle
+  mutable DerivedPool dp;                  // the derived structures' buffers
   int64_t seq_bytes = 0;
   int64_t proj_bytes = 0, pev_count = 0, proj_reads = 0;  // projection sizes (derive_shape)
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs

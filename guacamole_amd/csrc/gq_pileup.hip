@@ -1747,23 +1747,19 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     if (!ok) return set_err(GQ_E_UNSORTED, "contig_read_begin must run from 0 to n_reads, non-decreasing");
   }
   void *p = nullptr, *q = nullptr, *cl = nullptr;
-  HIP_TRY(hipMalloc(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  d->owned.push_back(p);
-  HIP_TRY(hipMalloc(&cl, (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  d->owned.push_back(cl);
+  HIP_TRY(d->dp.get(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
+  HIP_TRY(d->dp.get(&cl, (size_t)std::max<int64_t>(d->d.n_reads, 1)));
   d->d.clean = (const uint8_t *)cl;
-  HIP_TRY(hipMalloc(&q, (size_t)std::max<int64_t>(md_len, 16)));
-  d->owned.push_back(q);
+  HIP_TRY(d->dp.get(&q, (size_t)std::max<int64_t>(md_len, 16)));
   d->d.lead = (const int16_t *)p;
   d->d.ev_rb = (const uint8_t *)q;
   int unordered = 0;
   void *nnb = nullptr;  // N bytes per read (pool_clean / read_clean), for the projection entries
-  HIP_TRY(hipMalloc(&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
+  HIP_TRY(d->dp.get((void **)&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
   HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1), c->stream));
   if (d->d.n_reads > 0) {
     void *flag = nullptr;
-    HIP_TRY(hipMalloc(&flag, sizeof(int)));
-    d->owned.push_back(flag);
+    HIP_TRY(d->dp.get(&flag, sizeof(int)));
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(validate_reads, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag);
@@ -1794,27 +1790,24 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     const int64_t n = d->d.n_reads;
     void *cd = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr, *tmp = nullptr;
     const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
-    HIP_TRY(hipMalloc(&cd, ncd));
-    d->owned.push_back(cd);
+    HIP_TRY(d->dp.get(&cd, ncd));
     HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
-    HIP_TRY(hipMalloc(&ao, sizeof(int64_t) * (size_t)(n + 1)));
-    d->owned.push_back(ao);
-    HIP_TRY(hipMalloc(&na, sizeof(int64_t) * (size_t)(n + 1)));
+    HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
+    HIP_TRY(d->dp.get((void **)&na, sizeof(int64_t) * (size_t)(n + 1)));
     const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int64_t *)na);
     HIP_TRY(hipGetLastError());
     size_t tb = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
-    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
     int64_t aux_len = 0;
     HIP_TRY(hipMemcpyAsync(&aux_len, (int64_t *)ao + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(tmp);
-    (void)hipFree(na);
+    d->dp.put(tmp);
+    d->dp.put(na);
     const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_len, 1) + 1024;
-    HIP_TRY(hipMalloc(&ce, nce));
-    d->owned.push_back(ce);
+    HIP_TRY(d->dp.get(&ce, nce));
     HIP_TRY(hipMemsetAsync(ce, 0, nce, c->stream));
     d->d.cdesc = (const ColDesc *)cd;
     d->d.cev = (const uint32_t *)ce;
@@ -1844,15 +1837,13 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
       }
     }
     void *qo = nullptr;
-    HIP_TRY(hipMalloc(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
-    d->owned.push_back(qo);
+    HIP_TRY(d->dp.get(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
     HIP_TRY(hipMemcpyAsync(qo, qoff.data(), sizeof(int64_t) * ((size_t)nc + 1), hipMemcpyHostToDevice, c->stream));
     d->d.qoff = (const int64_t *)qo;
     d->n_slices = qoff[(size_t)nc];
     const int64_t n_blk = qoff[(size_t)nc] / 4;
     void *bi = nullptr;
-    HIP_TRY(hipMalloc(&bi, sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_blk, 1)));
-    d->owned.push_back(bi);
+    HIP_TRY(d->dp.get(&bi, sizeof(int64_t) * 2 * (size_t)std::max<int64_t>(n_blk, 1)));
     int64_t *brb = (int64_t *)bi, *brs = brb + std::max<int64_t>(n_blk, 1);
     if (n_blk > 0) {
       hipLaunchKernelGGL(block_index, dim3((unsigned)((n_blk + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
@@ -1863,10 +1854,8 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     d->d.blk_rs = brs;
   }
   d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
-  d->owned.push_back(nnb);
   nnb = nullptr;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (nnb) (void)hipFree(nnb);
   d->d.pool_ordered = unordered ? 0 : 1;
   return GQ_OK;
 }
@@ -2080,6 +2069,34 @@ gq_status gq_reads_wrap_device(gq_ctx *c, const gq_reads *h, gq_dev_reads **out)
   return GQ_OK;
 }
 
+gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
+  if (!c || !d) return set_err(GQ_E_ARG, "gq_reads_rederive: null argument");
+  if (d->ctx != c) return set_err(GQ_E_ARG, "gq_reads_rederive: the read set belongs to another context");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));  // nothing queued may still read the derived buffers
+  d->dp.release_all();
+  DevReads &R = d->d;
+  R.lead = nullptr;
+  R.ev_rb = R.clean = nullptr;
+  R.pool_ordered = 0;
+  R.cdesc = nullptr;
+  R.cev = nullptr;
+  R.caux_off = R.qoff = R.srow = R.pev_off = R.sra = R.soff = R.blk_rb = R.blk_rs = nullptr;
+  R.prec = nullptr;
+  R.proj = R.pbad = nullptr;
+  R.pev = nullptr;
+  R.prow = nullptr;
+  d->projected = false;
+  d->nnb = d->mproj = d->mnb = nullptr;
+  d->mproj_mapq = -1;
+  d->proj_bytes = d->pev_count = d->proj_reads = d->n_rows = d->n_slices = 0;
+  d->proj_ms = 0;
+  const auto t1 = std::chrono::steady_clock::now();
+  const gq_status st = derive_shape_impl(c, d, R.md_len);
+  d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
+  return st;
+}
+
 gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   if (!d || !out) return set_err(GQ_E_ARG, "gq_reads_get_info: null argument");
   out->n_reads = d->d.n_reads;
@@ -2102,8 +2119,7 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
 void gq_reads_free(gq_dev_reads *d) {
   if (!d) return;
   for (void *p : d->owned) (void)hipFree(p);
-  if (d->mproj) (void)hipFree(d->mproj);
-  if (d->mnb) (void)hipFree(d->mnb);
+  d->dp.free_all();  // every derived structure, margin projection included
   delete d;
 }
 
@@ -2856,15 +2872,13 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   const int64_t n_sl = d->n_slices;
   void *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
        *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
-  HIP_TRY(hipMalloc(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
-  d->owned.push_back(pr);
+  HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
   const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
   HIP_TRY(hipGetLastError());
   d->d.prec = (const ProjRec *)pr;
   // slices a read the projection cannot take touches (pbad)
-  HIP_TRY(hipMalloc(&pbd, (size_t)n_sl + 16));
-  d->owned.push_back(pbd);
+  HIP_TRY(d->dp.get(&pbd, (size_t)n_sl + 16));
   HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
   if (n > 0) {
     hipLaunchKernelGGL(slice_bad, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
@@ -2872,34 +2886,30 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     HIP_TRY(hipGetLastError());
   }
   // each slice's read window and the offsets of its reads' rows
-  HIP_TRY(hipMalloc(&sra, sizeof(int64_t) * (size_t)(n_sl + 1)));
-  d->owned.push_back(sra);
-  HIP_TRY(hipMalloc(&scn, sizeof(int64_t) * (size_t)(n_sl + 1)));
-  HIP_TRY(hipMalloc(&so, sizeof(int64_t) * (size_t)(n_sl + 1)));
-  d->owned.push_back(so);
+  HIP_TRY(d->dp.get(&sra, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  HIP_TRY(d->dp.get((void **)&scn, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  HIP_TRY(d->dp.get(&so, sizeof(int64_t) * (size_t)(n_sl + 1)));
   hipLaunchKernelGGL(slice_windows, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
                      d->d, n_sl, (int64_t *)sra, (int64_t *)scn);
   HIP_TRY(hipGetLastError());
   {
     size_t tb = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)scn, (int64_t *)so, (int)(n_sl + 1), c->stream));
-    HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)scn, (int64_t *)so, (int)(n_sl + 1), c->stream));
     int64_t tot = 0;
     HIP_TRY(hipMemcpyAsync(&tot, (int64_t *)so + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(tmp);
-    (void)hipFree(scn);
-    HIP_TRY(hipMalloc(&pw, sizeof(uint16_t) * (size_t)std::max<int64_t>(tot, 1)));
-    d->owned.push_back(pw);
+    d->dp.put(tmp);
+    d->dp.put(scn);
+    HIP_TRY(d->dp.get(&pw, sizeof(uint16_t) * (size_t)std::max<int64_t>(tot, 1)));
   }
   d->d.sra = (const int64_t *)sra;
   d->d.soff = (const int64_t *)so;
   d->d.prow = (const uint16_t *)pw;
-  HIP_TRY(hipMalloc(&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
-  HIP_TRY(hipMalloc(&br, sizeof(int64_t) * (size_t)(n_sl + 1)));
-  HIP_TRY(hipMalloc(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
-  d->owned.push_back(sb);
+  HIP_TRY(d->dp.get((void **)&sc, sizeof(int32_t) * (size_t)std::max<int64_t>(n_sl, 1)));
+  HIP_TRY(d->dp.get((void **)&br, sizeof(int64_t) * (size_t)(n_sl + 1)));
+  HIP_TRY(d->dp.get(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
   if (n_sl > 0) {
     const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
     hipLaunchKernelGGL(row_count, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint16_t *)pw,
@@ -2909,35 +2919,32 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   hipLaunchKernelGGL(rows64, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_sl,
                      (const int32_t *)sc, (int64_t *)br);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMalloc(&ne, sizeof(int64_t) * (size_t)(n + 1)));
-  HIP_TRY(hipMalloc(&eo, sizeof(int64_t) * (size_t)(n + 1)));
-  d->owned.push_back(eo);
+  HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
+  HIP_TRY(d->dp.get(&eo, sizeof(int64_t) * (size_t)(n + 1)));
   hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (int64_t *)ne);
   HIP_TRY(hipGetLastError());
   size_t tb = 0, tb2 = 0;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
-  HIP_TRY(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
+  HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
   int64_t tot[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(tmp);
-  (void)hipFree(sc);
-  (void)hipFree(br);
-  (void)hipFree(ne);
+  d->dp.put(tmp);
+  d->dp.put(sc);
+  d->dp.put(br);
+  d->dp.put(ne);
   d->d.srow = (const int64_t *)sb;
   d->d.pbad = (const uint8_t *)pbd;
   d->n_rows = tot[0];
   // the pool: rows of 16 words, zero where no piece lies
   const size_t pool_bytes = (size_t)kProjRowBytes * (size_t)tot[0] + 16;
-  HIP_TRY(hipMalloc(&pj, pool_bytes));
-  d->owned.push_back(pj);
+  HIP_TRY(d->dp.get(&pj, pool_bytes));
   HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
-  HIP_TRY(hipMalloc(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
-  d->owned.push_back(pe);
+  HIP_TRY(d->dp.get(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
     if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
@@ -2971,13 +2978,13 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   d->pev_count = tot[1];
   if (n > 0) {  // reads the projection takes
     unsigned long long *nok = nullptr, hk[kSpread];
-    HIP_TRY(hipMalloc(&nok, sizeof(hk)));
+    HIP_TRY(d->dp.get((void **)&nok, sizeof(hk)));
     HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
     hipLaunchKernelGGL(proj_count_ok, dim3(1024), dim3(kBlock), 0, c->stream, d->d, (const ProjRec *)pr, nok);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(nok);
+    d->dp.put(nok);
     d->proj_reads = 0;
     for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
   }

@@ -1264,16 +1264,16 @@ gq_status gq::fused_projection_fill(gq_ctx *c, const gq_dev_reads *t, uint8_t *p
   const int key = 2 * mr.min_mapq + (mr.incl_align ? 1 : 0);
   if (!t->mproj) {
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, (size_t)(128 * t->n_rows + 32)));
+    HIP_TRY(t->dp.get(&p, (size_t)(128 * t->n_rows + 32)));
     t->mproj = p;
     void *q = nullptr;
-    HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
+    HIP_TRY(t->dp.get(&q, (size_t)t->n_slices + 16));
     t->mnb = q;
   }
   HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
   HIP_TRY(hipMemsetAsync(t->mnb, 0, (size_t)t->n_slices + 16, c->stream));
   void *tab = nullptr;
-  HIP_TRY(hipMalloc(&tab, 256 * 256));
+  HIP_TRY(t->dp.get(&tab, 256 * 256));
   hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, mr.incl_align ? 1 : 0, (uint8_t *)tab);
   HIP_TRY(hipGetLastError());
   if (t->d.n_reads > 0) {
@@ -1283,7 +1283,7 @@ gq_status gq::fused_projection_fill(gq_ctx *c, const gq_dev_reads *t, uint8_t *p
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(tab);
+  t->dp.put(tab);
   t->mproj_mapq = key;
   return GQ_OK;
 }
@@ -1295,17 +1295,17 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   if (t->mproj && t->mproj_mapq == key) return GQ_OK;
   if (!t->mproj) {
     void *p = nullptr;
-    HIP_TRY(hipMalloc(&p, (size_t)(128 * t->n_rows + 32)));  // a byte per locus: 8 per 4-byte word of codes
+    HIP_TRY(t->dp.get(&p, (size_t)(128 * t->n_rows + 32)));  // a byte per locus: 8 per 4-byte word of codes
     t->mproj = p;
     void *q = nullptr;
-    HIP_TRY(hipMalloc(&q, (size_t)t->n_slices + 16));
+    HIP_TRY(t->dp.get(&q, (size_t)t->n_slices + 16));
     t->mnb = q;
     HIP_TRY(hipMemsetAsync(q, 0, (size_t)t->n_slices + 16, c->stream));
   }
   // the words no piece covers: biased zero terms (a rebuild for another filter rewrites only pieces)
   HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
   void *tab = nullptr;  // margin_term8 by (mapq, quality, match)
-  HIP_TRY(hipMalloc(&tab, 256 * 256));
+  HIP_TRY(t->dp.get(&tab, 256 * 256));
   hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, incl_align ? 1 : 0, (uint8_t *)tab);
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
@@ -1331,7 +1331,7 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(tab);
+  t->dp.put(tab);
   t->mproj_mapq = key;
   return GQ_OK;
 }

@@ -420,145 +420,187 @@ int gq_synth_generate(const gq_synth_params *P, gq_synth_out *o) {
   return 0;
 }
 
-// Write the read set as a coordinate-sorted BAM (one contig, no read groups, read names
-// "r<index>"), BGZF level `level`: the input of the native ingest measurement
-// (scripts/bench_ingest.py).  MD strings are rebuilt from the MD events the way
+// One BAM record per read of [a, e) appended to `b` (ref_id from the read's local contig, read
+// name "r<name_base + index>"); MD strings are rebuilt from the MD events the way
 // synthetic.md_string does (a deleted base without an event is written as N).
-int gq_synth_write_bam(const gq_synth_out *o, const char *path, const char *contig, int64_t contig_len,
-                       int32_t level) {
+static void bam_records(const gq_synth_out *o, int64_t a, int64_t e, const int64_t *crb, int32_t n_local,
+                        const int32_t *ref_id, int64_t name_base, std::string &b) {
+  auto put32 = [](std::string &s, uint32_t v) { s.append((const char *)&v, 4); };
+  std::string md;
+  static const char kNib[] = "=ACMGRSVTWYHKDBN";
+  uint8_t code[256];
+  memset(code, 15, sizeof(code));
+  for (int k = 0; k < 16; ++k) code[(uint8_t)kNib[k]] = (uint8_t)k;
+  int32_t lc = 0;
+  while (lc + 1 < n_local && crb[lc + 1] <= a) ++lc;
+  for (int64_t r = a; r < e; ++r) {
+    while (lc + 1 < n_local && crb[lc + 1] <= r) ++lc;
+    const uint32_t *cg = o->cigar + o->cigar_off[r];
+    const int32_t nc = o->n_cigar[r], ls = o->seq_len[r];
+    const uint32_t *ev = o->md_ev + o->md_off[r];
+    const int32_t ne = std::max(o->n_md[r], 0);
+    md.clear();
+    int64_t run = 0, ref = 0;
+    int32_t k = 0;
+    for (int32_t c = 0; c < nc; ++c) {
+      const uint32_t op = cg[c] & 15, ln = cg[c] >> 4;
+      if (op == 0 || op == 7 || op == 8) {
+        const int64_t end = ref + ln;
+        while (k < ne && (int64_t)(ev[k] >> 8) < end) {
+          const int64_t off = ev[k] >> 8;
+          run += off - ref;
+          md += std::to_string(run);
+          md += (char)(ev[k] & 0xFF);
+          run = 0;
+          ref = off + 1;
+          ++k;
+        }
+        run += end - ref;
+        ref = end;
+      } else if (op == 2) {
+        md += std::to_string(run);
+        md += '^';
+        for (uint32_t j = 0; j < ln; ++j) {
+          if (k < ne && (int64_t)(ev[k] >> 8) == ref + j) md += (char)(ev[k++] & 0xFF);
+          else md += 'N';
+        }
+        run = 0;
+        ref += ln;
+      } else if (op == 3) {
+        ref += ln;
+      }
+    }
+    md += std::to_string(run);
+    const std::string name = "r" + std::to_string(name_base + r);
+    const uint32_t l_name = (uint32_t)name.size() + 1;
+    const uint32_t block = 32 + l_name + 4 * (uint32_t)nc + (uint32_t)(ls + 1) / 2 + (uint32_t)ls + 3 +
+                           (uint32_t)md.size() + 1;
+    put32(b, block);
+    put32(b, (uint32_t)ref_id[lc]);
+    put32(b, (uint32_t)o->start[r]);
+    b += (char)l_name;
+    b += (char)o->mapq[r];
+    b.append("\0\0", 2);  // bin (unused by readers here)
+    const uint16_t ncig = (uint16_t)nc, flag = (o->flags[r] & 1) ? 16 : 0;
+    b.append((const char *)&ncig, 2);
+    b.append((const char *)&flag, 2);
+    put32(b, (uint32_t)ls);
+    put32(b, 0xFFFFFFFFu);
+    put32(b, 0xFFFFFFFFu);
+    put32(b, 0);
+    b.append(name.c_str(), l_name);
+    b.append((const char *)cg, 4 * (size_t)nc);
+    const uint8_t *sq = o->seq + o->seq_off[r];
+    for (int32_t j = 0; j < ls; j += 2) {
+      const uint8_t hi = code[sq[j]], lo = j + 1 < ls ? code[sq[j + 1]] : 0;
+      b += (char)((hi << 4) | lo);
+    }
+    b.append((const char *)(o->qual + o->seq_off[r]), (size_t)ls);
+    b.append("MDZ", 3);
+    b.append(md.c_str(), md.size() + 1);
+  }
+}
+
+// One BGZF block of src[0, len) (len <= 65280; len 0: the EOF marker).
+static void bgzf_block(const uint8_t *src, int64_t len, int level, std::string &out) {
+  z_stream z;
+  memset(&z, 0, sizeof(z));
+  deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+  std::string buf(deflateBound(&z, (uLong)len) + 64, '\0');
+  z.next_in = const_cast<uint8_t *>(src);
+  z.avail_in = (uInt)len;
+  z.next_out = (Bytef *)&buf[18];
+  z.avail_out = (uInt)(buf.size() - 26);
+  deflate(&z, Z_FINISH);
+  const size_t clen = z.total_out;
+  deflateEnd(&z);
+  const uint32_t bsize = (uint32_t)(18 + clen + 8);
+  const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                           (uint8_t)((bsize - 1) & 0xFF), (uint8_t)((bsize - 1) >> 8)};
+  memcpy(&buf[0], hdr, 18);
+  const uint32_t crc = (uint32_t)crc32(0L, src, (uInt)len), isz = (uint32_t)len;
+  memcpy(&buf[18 + clen], &crc, 4);
+  memcpy(&buf[18 + clen + 4], &isz, 4);
+  buf.resize(bsize);
+  out.swap(buf);
+}
+
+// A coordinate-sorted BAM (or a piece of one) of the read set, streamed in chunks of reads:
+// each chunk's records are serialised and BGZF-compressed (level `level`) on every thread and
+// appended, so memory stays bounded by the chunk whatever the read count.
+//   n_ref / ref_names / ref_lens: the header's dictionary (written when flags & 1);
+//   crb[n_local + 1], ref_id[n_local]: the reads' local contigs and their header ids;
+//   flags: 1 = header first, 2 = the EOF block last, 4 = append to the file;
+//   name_base: read names are "r<name_base + index>" (unique across the pieces of one file).
+// A piece written without header / EOF is a run of whole BGZF blocks: pieces concatenate.
+int gq_synth_write_bam_ex(const gq_synth_out *o, const char *path, int32_t n_ref, const char **ref_names,
+                          const int64_t *ref_lens, int32_t n_local, const int64_t *crb, const int32_t *ref_id,
+                          int32_t level, int32_t flags, int64_t name_base) {
   const int64_t N = o->n_reads;
   const int T = nthreads();
-  const int64_t per = std::max<int64_t>(1, (N + T - 1) / T);
-  std::vector<std::string> parts((size_t)T);
-  auto put32 = [](std::string &b, uint32_t v) { b.append((const char *)&v, 4); };
-  parallel_for(N, [&](int t, int64_t a, int64_t e) {
-    (void)per;
-    std::string &b = parts[(size_t)t];
-    std::string md;
-    static const char kNib[] = "=ACMGRSVTWYHKDBN";
-    uint8_t code[256];
-    memset(code, 15, sizeof(code));
-    for (int k = 0; k < 16; ++k) code[(uint8_t)kNib[k]] = (uint8_t)k;
-    for (int64_t r = a; r < e; ++r) {
-      const uint32_t *cg = o->cigar + o->cigar_off[r];
-      const int32_t nc = o->n_cigar[r], ls = o->seq_len[r];
-      const uint32_t *ev = o->md_ev + o->md_off[r];
-      const int32_t ne = std::max(o->n_md[r], 0);
-      // MD string
-      md.clear();
-      int64_t run = 0, ref = 0;
-      int32_t k = 0;
-      for (int32_t c = 0; c < nc; ++c) {
-        const uint32_t op = cg[c] & 15, ln = cg[c] >> 4;
-        if (op == 0 || op == 7 || op == 8) {
-          const int64_t end = ref + ln;
-          while (k < ne && (int64_t)(ev[k] >> 8) < end) {
-            const int64_t off = ev[k] >> 8;
-            run += off - ref;
-            md += std::to_string(run);
-            md += (char)(ev[k] & 0xFF);
-            run = 0;
-            ref = off + 1;
-            ++k;
-          }
-          run += end - ref;
-          ref = end;
-        } else if (op == 2) {
-          md += std::to_string(run);
-          md += '^';
-          for (uint32_t j = 0; j < ln; ++j) {
-            if (k < ne && (int64_t)(ev[k] >> 8) == ref + j) md += (char)(ev[k++] & 0xFF);
-            else md += 'N';
-          }
-          run = 0;
-          ref += ln;
-        } else if (op == 3) {
-          ref += ln;
-        }
-      }
-      md += std::to_string(run);
-      const std::string name = "r" + std::to_string(r);
-      const uint32_t l_name = (uint32_t)name.size() + 1;
-      const uint32_t block = 32 + l_name + 4 * (uint32_t)nc + (uint32_t)(ls + 1) / 2 + (uint32_t)ls +
-                             3 + (uint32_t)md.size() + 1;
-      put32(b, block);
-      put32(b, 0);  // ref_id
-      put32(b, (uint32_t)o->start[r]);
-      b += (char)l_name;
-      b += (char)o->mapq[r];
-      b.append("\0\0", 2);  // bin (unused by readers here)
-      const uint16_t ncig = (uint16_t)nc, flag = (o->flags[r] & 1) ? 16 : 0;
-      b.append((const char *)&ncig, 2);
-      b.append((const char *)&flag, 2);
-      put32(b, (uint32_t)ls);
-      put32(b, 0xFFFFFFFFu);
-      put32(b, 0xFFFFFFFFu);
-      put32(b, 0);
-      b.append(name.c_str(), l_name);
-      b.append((const char *)cg, 4 * (size_t)nc);
-      const uint8_t *sq = o->seq + o->seq_off[r];
-      for (int32_t j = 0; j < ls; j += 2) {
-        const uint8_t hi = code[sq[j]], lo = j + 1 < ls ? code[sq[j + 1]] : 0;
-        b += (char)((hi << 4) | lo);
-      }
-      b.append((const char *)(o->qual + o->seq_off[r]), (size_t)ls);
-      b.append("MDZ", 3);
-      b.append(md.c_str(), md.size() + 1);
-    }
-  });
-  std::string data("BAM\1", 4);
-  const std::string text = std::string("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:") + contig + "\tLN:" +
-                           std::to_string(contig_len) + "\n";
-  put32(data, (uint32_t)text.size());
-  data += text;
-  put32(data, 1);
-  put32(data, (uint32_t)strlen(contig) + 1);
-  data.append(contig, strlen(contig) + 1);
-  put32(data, (uint32_t)contig_len);
-  for (auto &x : parts) {
-    data += x;
-    std::string().swap(x);
-  }
-  // BGZF blocks of 65280 input bytes, compressed in parallel
   const int64_t kBlk = 65280;
-  const int64_t nb = ((int64_t)data.size() + kBlk - 1) / kBlk;
-  std::vector<std::string> comp((size_t)nb + 1);
-  auto block = [&](const uint8_t *src, int64_t len, std::string &out) {
-    z_stream z;
-    memset(&z, 0, sizeof(z));
-    deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
-    std::string buf(deflateBound(&z, (uLong)len) + 64, '\0');
-    z.next_in = const_cast<uint8_t *>(src);
-    z.avail_in = (uInt)len;
-    z.next_out = (Bytef *)&buf[18];
-    z.avail_out = (uInt)(buf.size() - 26);
-    deflate(&z, Z_FINISH);
-    const size_t clen = z.total_out;
-    deflateEnd(&z);
-    const uint32_t bsize = (uint32_t)(18 + clen + 8);
-    const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
-                             (uint8_t)((bsize - 1) & 0xFF), (uint8_t)((bsize - 1) >> 8)};
-    memcpy(&buf[0], hdr, 18);
-    const uint32_t crc = (uint32_t)crc32(0L, src, (uInt)len), isz = (uint32_t)len;
-    memcpy(&buf[18 + clen], &crc, 4);
-    memcpy(&buf[18 + clen + 4], &isz, 4);
-    buf.resize(bsize);
-    out.swap(buf);
-  };
-  parallel_for(nb, [&](int, int64_t a, int64_t e) {
-    for (int64_t i = a; i < e; ++i)
-      block((const uint8_t *)data.data() + i * kBlk, std::min<int64_t>(kBlk, (int64_t)data.size() - i * kBlk),
-            comp[(size_t)i]);
-  });
-  block(nullptr, 0, comp[(size_t)nb]);  // EOF marker block
-  FILE *f = fopen(path, "wb");
+  FILE *f = fopen(path, (flags & 4) ? "ab" : "wb");
   if (!f) return 1;
-  for (auto &c : comp)
-    if (fwrite(c.data(), 1, c.size(), f) != c.size()) {
-      fclose(f);
-      return 2;
+  std::string data;  // uncompressed bytes not yet in a full block
+  auto put32 = [](std::string &s, uint32_t v) { s.append((const char *)&v, 4); };
+  if (flags & 1) {
+    std::string text = "@HD\tVN:1.6\tSO:coordinate\n";
+    for (int32_t k = 0; k < n_ref; ++k)
+      text += std::string("@SQ\tSN:") + ref_names[k] + "\tLN:" + std::to_string(ref_lens[k]) + "\n";
+    data.append("BAM\1", 4);
+    put32(data, (uint32_t)text.size());
+    data += text;
+    put32(data, (uint32_t)n_ref);
+    for (int32_t k = 0; k < n_ref; ++k) {
+      put32(data, (uint32_t)strlen(ref_names[k]) + 1);
+      data.append(ref_names[k], strlen(ref_names[k]) + 1);
+      put32(data, (uint32_t)ref_lens[k]);
     }
-  return fclose(f) == 0 ? 0 : 2;
+  }
+  int rc = 0;
+  auto flush = [&](bool all) {  // compress the whole blocks of `data` (all: the tail too)
+    const int64_t nb = all ? ((int64_t)data.size() + kBlk - 1) / kBlk : (int64_t)data.size() / kBlk;
+    if (nb <= 0) return;
+    std::vector<std::string> comp((size_t)nb);
+    parallel_for(nb, [&](int, int64_t a, int64_t e) {
+      for (int64_t i = a; i < e; ++i)
+        bgzf_block((const uint8_t *)data.data() + i * kBlk, std::min<int64_t>(kBlk, (int64_t)data.size() - i * kBlk),
+                   level, comp[(size_t)i]);
+    });
+    for (auto &c : comp)
+      if (!rc && fwrite(c.data(), 1, c.size(), f) != c.size()) rc = 2;
+    data.erase(0, (size_t)std::min<int64_t>((int64_t)data.size(), nb * kBlk));
+  };
+  const int64_t chunk = std::max<int64_t>(1 << 16, (int64_t)T * 8192);
+  std::vector<std::string> parts((size_t)T);
+  for (int64_t c0 = 0; c0 < N && !rc; c0 += chunk) {
+    const int64_t c1 = std::min(N, c0 + chunk);
+    parallel_for(c1 - c0, [&](int t, int64_t a, int64_t e) {
+      parts[(size_t)t].clear();
+      bam_records(o, c0 + a, c0 + e, crb, n_local, ref_id, name_base, parts[(size_t)t]);
+    });
+    for (auto &x : parts) {
+      data += x;
+      x.clear();
+    }
+    flush(false);
+  }
+  flush(true);
+  if (!rc && (flags & 2)) {
+    std::string eof;
+    bgzf_block(nullptr, 0, level, eof);
+    if (fwrite(eof.data(), 1, eof.size(), f) != eof.size()) rc = 2;
+  }
+  if (fclose(f) != 0 && !rc) rc = 2;
+  return rc;
+}
+
+// The one-contig form (contig id 0, the whole file): the input of the ingest measurements.
+int gq_synth_write_bam(const gq_synth_out *o, const char *path, const char *contig, int64_t contig_len,
+                       int32_t level) {
+  const int64_t crb[2] = {0, o->n_reads};
+  const int32_t id = 0;
+  return gq_synth_write_bam_ex(o, path, 1, &contig, &contig_len, 1, crb, &id, level, 3, 0);
 }
 
 }  // extern "C"

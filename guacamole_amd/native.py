@@ -148,7 +148,7 @@ class gq_somatic_calls(C.Structure):
 
 
 EXPORTED = ("gq_version", "gq_last_error", "gq_open", "gq_close", "gq_get_timings", "gq_set_tile", "gq_reads_upload",
-            "gq_reads_wrap_device", "gq_reads_free", "gq_germline_threshold", "gq_germline_threshold_device",
+            "gq_reads_wrap_device", "gq_reads_free", "gq_reads_rederive", "gq_germline_threshold", "gq_germline_threshold_device",
             "gq_free_calls", "gq_pileup_counts",
             "gq_free_counts", "gq_somatic_standard", "gq_free_somatic", "gq_reads_get_info", "gq_reference_upload",
             "gq_reference_free", "gq_somatic_standard_ref", "gq_variant_support", "gq_free_allele_counts",
@@ -171,6 +171,7 @@ def lib():
         L.gq_version.restype = C.c_char_p
         L.gq_last_error.restype = C.c_char_p
         for f in ("gq_open", "gq_get_timings", "gq_set_tile", "gq_reads_upload", "gq_reads_wrap_device", "gq_reads_get_info",
+                  "gq_reads_rederive",
                   "gq_germline_threshold", "gq_germline_threshold_device", "gq_pileup_counts", "gq_somatic_standard",
                   "gq_reference_upload", "gq_somatic_standard_ref", "gq_variant_support", "gq_vaf_histogram",
                   "gq_germline_standard"):
@@ -198,6 +199,7 @@ def lib():
         L.gq_free_counts.argtypes = [C.POINTER(gq_counts)]
         L.gq_free_somatic.argtypes = [C.POINTER(gq_somatic_calls)]
         L.gq_reads_free.argtypes = [C.c_void_p]
+        L.gq_reads_rederive.argtypes = [C.c_void_p, C.c_void_p]
         L.gq_close.argtypes = [C.c_void_p]
         vp = C.c_void_p
         for f in ("gq_bam_dev_open", "gq_bam_dev_scan", "gq_bam_dev_reads", "gq_reads_positions", "gq_reads_contig_begin",
@@ -320,6 +322,11 @@ class Context:
         h = C.c_void_p()
         _check(lib().gq_reads_upload(self.h, C.byref(s), C.byref(h)))
         return DeviceReads(self, h, None)
+
+    def rederive(self, reads: "DeviceReads") -> None:
+        """gq_reads_rederive: every derived structure of the resident read set dropped and the
+        upload-time part derived again (the projection on the next call that reads it)."""
+        _check(lib().gq_reads_rederive(self.h, reads.h))
 
     def wrap_device(self, arrs: Dict[str, object]) -> "DeviceReads":
         s, keep = make_gq_reads(arrs)

@@ -87,14 +87,46 @@ class SyntheticReads:
         idx = np.arange(lo, hi)
         return idx[a["end"][idx] > start]
 
-    def write_bam(self, path: str, level: int = 6) -> None:
-        """Coordinate-sorted BAM of every read (native writer; read names r<index>, no RG)."""
+    def write_bam(self, path: str, level: int = 6, dictionary=None, flags: int = 3, name_base: int = 0) -> None:
+        """Coordinate-sorted BAM of every read (native streaming writer; read names
+        r<name_base + index>, no RG).  dictionary: the header's [(contig, length)] (default: this
+        set's contigs), every local contig named in it.  flags: 1 header, 2 EOF block, 4 append
+        (a piece without header or EOF is whole BGZF blocks: pieces of one genome written by
+        several processes concatenate into one BAM)."""
         L = _load()
-        L.gq_synth_write_bam.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int64, C.c_int32]
-        rc = L.gq_synth_write_bam(C.byref(self._owner.out), os.fsencode(path), self.contig_names[0].encode(),
-                                  int(self.contig_lengths[0]), int(level))
+        vp = C.c_void_p
+        L.gq_synth_write_bam_ex.argtypes = [vp, C.c_char_p, C.c_int32, vp, vp, C.c_int32, vp, vp, C.c_int32,
+                                            C.c_int32, C.c_int64]
+        L.gq_synth_write_bam_ex.restype = C.c_int
+        dictionary = list(dictionary) if dictionary is not None else list(zip(self.contig_names, self.contig_lengths))
+        index = {c: i for i, (c, _) in enumerate(dictionary)}
+        names = (C.c_char_p * max(1, len(dictionary)))(*[c.encode() for c, _ in dictionary])
+        lens = np.array([int(n) for _, n in dictionary] or [0], np.int64)
+        ids = np.array([index[c] for c in self.contig_names] or [0], np.int32)
+        crb = np.ascontiguousarray(self.arrays["contig_read_begin"], np.int64)
+        out, keep = self._out()
+        rc = L.gq_synth_write_bam_ex(C.byref(out), os.fsencode(path), len(dictionary), C.cast(names, vp),
+                                     lens.ctypes.data, len(self.contig_names), crb.ctypes.data, ids.ctypes.data,
+                                     int(level), int(flags), int(name_base))
+        del keep
         if rc != 0:
-            raise OSError("gq_synth_write_bam failed (%d) for %s" % (rc, path))
+            raise OSError("gq_synth_write_bam_ex failed (%d) for %s" % (rc, path))
+
+    def _out(self):
+        """The native generator's output struct over this set's arrays (and what keeps them)."""
+        if self._owner is not None:
+            return self._owner.out, None
+        a = self.arrays
+        dt = dict(start=np.int32, end=np.int32, pmax_end=np.int32, mapq=np.uint8, flags=np.uint8, sample=np.uint8,
+                  seq_off=np.int64, seq_len=np.int32, cigar_off=np.int64, n_cigar=np.int32, md_off=np.int64,
+                  n_md=np.int32, n_mismatch=np.uint16, seq=np.uint8, qual=np.uint8, cigar=np.uint32, md_ev=np.uint32)
+        keep = {k: np.ascontiguousarray(a[k], t) for k, t in dt.items()}
+        ptr = {k: (v.ctypes.data if v.size else None) for k, v in keep.items()}
+        out = _Out(self.n, *[ptr[k] for k in ("start", "end", "pmax_end", "mapq", "flags", "sample", "seq_off",
+                                              "seq_len", "cigar_off", "n_cigar", "md_off", "n_md", "n_mismatch")],
+                   int(keep["seq"].size), int(keep["cigar"].size), int(keep["md_ev"].size),
+                   *[ptr[k] for k in ("seq", "qual", "cigar", "md_ev")], None, 0, 0, 0)
+        return out, keep
 
     def to_read_set(self, sel: Optional[np.ndarray] = None) -> ReadSet:
         """Raw ReadSet (MD strings) for the reads `sel` (default: all) — oracle input."""

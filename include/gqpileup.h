@@ -202,6 +202,13 @@ gq_status gq_reads_upload(gq_ctx *ctx, const gq_reads *host, gq_dev_reads **out)
 /* the caller keeps them alive.                                              */
 gq_status gq_reads_wrap_device(gq_ctx *ctx, const gq_reads *device_ptrs, gq_dev_reads **out);
 void gq_reads_free(gq_dev_reads *r);
+/* Drop every structure derived from a resident read set (the upload-time derivation, the     */
+/* projection, the margin projection) and derive the upload-time part again; the projection  */
+/* is derived again by the next call that reads it.  The SoA arrays stay resident and are not */
+/* read from the host again; the derived buffers are reused.  A cold pass over reads already  */
+/* in HBM: what one MappedRead RDD costs the reference per job, whose pileups are rebuilt by  */
+/* every pileupFlatMap (DistributedUtil.scala:288-306; GermlineThresholdCaller.scala:58-88).  */
+gq_status gq_reads_rederive(gq_ctx *ctx, gq_dev_reads *r);
 /* Sizes of a resident read set and of what the upload derived from it (the germline         */
 /* projection pool and its sparse entries): for measurement and capacity planning.             */
 typedef struct gq_reads_info {

@@ -284,3 +284,31 @@ def test_more_distinct_alleles_than_the_fast_table(gpu_ctx, n_distinct):
         got = germline_threshold_reads(gpu_ctx, rs, loci, threshold, True, True)
         want = O.germline_threshold(rs, loci, threshold, True, True)
         assert got == want and len(want) > 0
+
+
+def test_rederive_gives_the_same_records(gpu_ctx):
+    """gq_reads_rederive drops every derived structure and derives it again from the resident SoA
+    (the bench's cold step): the germline and somatic records are those of the first derivation,
+    and a second re-derivation reuses the same buffers."""
+    from guacamole_amd.commands import somatic_standard_reads
+    g = generate(120_000, 30, seed=11, indel_rate=3e-4)
+    reads = gpu_ctx.upload(g.arrays)
+    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([119_999], np.int64), np.array([0], np.int64))
+    want = gpu_ctx.germline_threshold(reads, loci, 8).tuples(g.contig_names)
+    st0 = gpu_ctx.proj_stats(reads)
+    for _ in range(2):
+        gpu_ctx.rederive(reads)
+        st = gpu_ctx.proj_stats(reads)
+        assert st["projected"] == 0
+        assert gpu_ctx.germline_threshold(reads, loci, 8).tuples(g.contig_names) == want
+        st = gpu_ctx.proj_stats(reads)
+        assert (st["proj_bytes"], st["pev_count"], st["n_rows"]) == (st0["proj_bytes"], st0["pev_count"], st0["n_rows"])
+    t = generate(100_000, 60, seed=3, somatic_rate=2e-4, tumor=True, read_seed=11)
+    n = generate(100_000, 30, seed=3, somatic_rate=2e-4, tumor=False, read_seed=12)
+    td, nd = gpu_ctx.upload(t.arrays), gpu_ctx.upload(n.arrays)
+    loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([99_999], np.int64), np.array([0], np.int64))
+    first = gpu_ctx.somatic_standard(td, nd, loci).rows
+    assert first
+    gpu_ctx.rederive(td)
+    gpu_ctx.rederive(nd)
+    assert gpu_ctx.somatic_standard(td, nd, loci).rows == first
