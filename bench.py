@@ -109,6 +109,9 @@ def main() -> int:
     ap.add_argument("--calls-out", default=None, help="rank 0 writes the gathered records (rank order) as JSON")
     ap.add_argument("--no-single-pass", dest="single_pass", action="store_false",
                     help="skip the measured single pass (the shard as a BAM through the CLI)")
+    ap.add_argument("--no-configs3", dest="configs3", action="store_false",
+                    help="skip the configs[3] rank share (one rank's share of the 30x b37 genome through the "
+                         "multi-GPU ingest path, on this GPU)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
@@ -350,6 +353,11 @@ def main() -> int:
         line["end_to_end"]["single_pass"] = single_pass(g, visited)
     if rank == 0 and world == 1 and n_parts == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], line["parity_window"] = cpu_baseline(g, ctx, reads, args)
+    if dist is not None and args.single_pass and n_parts == world:
+        sp = multi_rank_single_pass(args, g, pieces, rank, world, dist, barrier)
+        if rank == 0:
+            sp["loci_per_s"] = loci_total / sp["wall_s"]
+            line.setdefault("end_to_end", {})["single_pass"] = sp
     if dist is not None:
         dist.destroy_process_group()
     del reads, g
@@ -361,6 +369,8 @@ def main() -> int:
         line["configs4"] = somatic_run(ctx, args, steps=5, warmup=2, L=args.panel_length, tdepth=500.0, ndepth=500.0,
                                        rate=1e-3, workload="%d-locus targeted panel (configs[4], 1 GPU)"
                                        % args.panel_length)
+    if rank == 0 and world == 1 and args.configs3:
+        line["configs3_rank_share"] = configs3_rank_share(ctx, args)
     if rank == 0:
         print(json.dumps(line))
     return 0
@@ -586,6 +596,7 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
             stages[k].append(tm[k])
     el = time.perf_counter() - t1
     tm = ctx.timings()
+    parity = somatic_parity_window(ctx, t, n, tg, ng, L, 1_000_000 if tdepth < 500 else 100_000)
     ta = tg.arrays
     b_alg = (2 * int(ta["seq"].shape[0]) + 16 * tg.n + 4 * int(ta["cigar"].shape[0]) + 4 * int(ta["md_ev"].shape[0])
              + 8 * ng.n)
@@ -626,12 +637,227 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
             "caller_roofline": caller_roofline(float(np.mean(stages["call_ms"])), pmc, "somatic_call_k<false,false"),
             "deep_caller_roofline": caller_roofline(float(np.mean(stages["deep_ms"])), pmc, "somatic_call_k<true,"),
             "candidate_loci": int(calls.candidate_loci), "calls": len(calls), "gen_s": gen_s,
+            "parity_window": parity,
             # a cold call on resident reads: both sets' upload-time derivation + the first call
             # (the tumor's projection and margin projection; the normal needs neither)
             "one_shot": {"upload_derive_ms": derive_ms, "first_call_ms": cold_ms,
                          "first_call_device_ms": float(cold_tm["total_ms"]),
                          "tumor_projection_ms": float(st["proj_ms"]), "total_ms": derive_ms + cold_ms,
                          "loci_per_s": visited / ((derive_ms + cold_ms) * 1e-3)}}
+
+
+class HbmPeak:
+    """Device memory in use (hipMemGetInfo: total - free, every process's allocations on the
+    GPU), sampled every 2 ms on a host thread between start() and stop(): the peak and the
+    level at start."""
+
+    def __init__(self, device: int = 0):
+        import ctypes as C
+        self.C = C
+        self.hip = C.CDLL("libamdhip64.so.7")  # the HIP runtime the library already loaded
+        self.hip.hipMemGetInfo.argtypes = [C.c_void_p, C.c_void_p]
+        self.device = device
+        self.peak = self.base = 0
+        self._run = False
+        self._th = None
+
+    def used(self) -> int:
+        C = self.C
+        free, total = C.c_size_t(), C.c_size_t()
+        if self.hip.hipMemGetInfo(C.byref(free), C.byref(total)) != 0:
+            return 0
+        return int(total.value - free.value)
+
+    def start(self) -> "HbmPeak":
+        import threading
+        self.base = self.peak = self.used()
+        self._run = True
+
+        def poll():
+            self.hip.hipSetDevice(self.device)
+            while self._run:
+                self.peak = max(self.peak, self.used())
+                time.sleep(0.002)
+        self._th = threading.Thread(target=poll, daemon=True)
+        self._th.start()
+        return self
+
+    def stop(self) -> dict:
+        self._run = False
+        self._th.join()
+        self.peak = max(self.peak, self.used())
+        return {"peak_gb": self.peak / 1e9, "at_start_gb": self.base / 1e9, "peak_above_start_gb": (self.peak - self.base) / 1e9}
+
+
+def configs3_rank_share(ctx, args, share_rank: int = 7, world: int = 8, margin: int = 5_000_000):
+    """configs[3]'s per-GPU workload on this GPU, through the multi-GPU product path: rank
+    `share_rank` of 8 in the 30x b37 genome split (genome_parts(8, wgs): ~392 M loci, ~78 M reads;
+    rank 7 holds 65 contigs: 9's tail, the GL contigs, MT, X, Y, hs37d5).  Its reads, with `margin`
+    loci of rank 6's share before them (so the plan must skip blocks), are written as one BGZF
+    BAM (level 1) with the whole b37 dictionary; the rank's loci are planned through
+    gq_bam_dev_plan (host probes: the file has no BAI) and decoded on the device with
+    load_reads_device(region=...) as device_ingest_ranks does at world 8 (DistributedUtil.scala:
+    584-597), then called over the rank's task of the 8-task partition; the result image is
+    copied out as the gather would send it.  Peak device memory is sampled across ingest + call.
+    A 2 Mb oracle window on contig X checks the records."""
+    import shutil
+    from guacamole_amd import synthetic
+    from guacamole_amd.bamdev import load_reads_device
+    from guacamole_amd.genomes import B37
+    from guacamole_amd.loci import LociMapBuilder, LociSet
+    from guacamole_amd.reads import InputFilters
+    from oracle import oracle as O
+    parts, genome_loci = genome_parts(world, True)
+    mine = [p for p in parts if p[4] == share_rank]
+    first = mine[0]
+    pieces = merged_pieces(mine)
+    gen_pieces = [(c, ln, max(0, s - margin) if c == first[0] else s, e) for c, ln, s, e in pieces]
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    path = os.path.join(tmp, "gq_c3_%d.bam" % os.getpid())
+    out = {"workload": "germline-threshold, rank %d of %d in the 30x b37 genome split (configs[3] per-GPU share)"
+                       % (share_rank, world)}
+    try:
+        t = time.perf_counter()
+        g = synthetic.generate_pieces(gen_pieces, args.depth, seed=synthetic.SEED + 4 + 1000 * share_rank)
+        out["gen_s"] = time.perf_counter() - t
+        x = next(p for p in pieces if p[0] == "X")
+        w0 = x[2] + 50_000_000
+        w1 = w0 + args.cpu_window
+        win = synthetic.subset_pieces(g, gen_pieces, [("X", x[1], w0, w1)]).to_read_set()
+        t = time.perf_counter()
+        g.write_bam(path, level=1, dictionary=list(B37))
+        out["bam_write_s"] = time.perf_counter() - t
+        out["file_reads"] = g.n
+        del g
+        out["bam_bytes"] = os.path.getsize(path)
+        b = LociMapBuilder()
+        for c, _, s, e in pieces:
+            b.put(c, int(s), int(e), 0)
+        region = LociSet(b.result())
+        filters = InputFilters.make(overlaps_loci=LociSet.parse("all"), non_duplicate=True, has_md_tag=True)
+        hbm = HbmPeak(ctx.device).start()
+        t = time.perf_counter()
+        rs = load_reads_device(ctx, path, filters, region=region)
+        ingest_s = time.perf_counter() - t
+        cidx = rs.contig_index()
+        loci = (np.array([cidx[p[0]] for p in mine], np.int32), np.array([p[2] for p in mine], np.int64),
+                np.array([p[3] for p in mine], np.int64), np.array([p[4] for p in mine], np.int64))
+        t = time.perf_counter()
+        calls = ctx.germline_threshold_device(rs.reads, loci, args.threshold)
+        call_ms = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        img = calls.to_host()
+        image_ms = (time.perf_counter() - t) * 1e3
+        mem = hbm.stop()
+        st = ctx.proj_stats(rs.reads)
+        tm = rs.timings
+        wl = (np.array([cidx["X"]], np.int32), np.array([w0], np.int64), np.array([w1], np.int64),
+              np.array([0], np.int64))
+        gpu_win = ctx.germline_threshold(rs.reads, wl, args.threshold).tuples(rs.contig_names)
+        want = O.germline_threshold(win, (np.array([0], np.int32),) + wl[1:], args.threshold)
+        visited = int(calls.visited_loci)
+        out.update({
+            "loci": int(sum(p[3] - p[2] for p in mine)), "visited_loci": visited, "contigs": len(pieces),
+            "reads": int(rs.n), "genome_loci": genome_loci,
+            "stages_s": {"ingest": ingest_s, "call": call_ms / 1e3, "result_image_d2h": image_ms / 1e3},
+            "ingest": {k: tm.get(k) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms", "fill_ms",
+                                              "derive_ms", "comp_bytes", "bam_bytes", "blocks", "max_span", "replans")},
+            "plan": {k: v for k, v in (tm.get("plan") or {}).items() if k != "segments"},
+            "call_loci_per_s": visited / (call_ms * 1e-3),
+            "projection_ms": float(st["proj_ms"]), "calls": len(img),
+            "hbm": dict(mem, design_budget_gb={"load": 68, "calls": 47}),
+            "parity_window": {"contig": "X", "loci": [w0, w1], "calls": len(want), "identical": gpu_win == want},
+        })
+        del rs, calls
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+    return out
+
+
+def multi_rank_single_pass(args, g, pieces, rank: int, world: int, dist, barrier):
+    """The N-rank CLI single pass over one BAM of the whole split genome: every rank writes the
+    reads starting in its pieces as whole BGZF blocks, rank 0 joins the header, the pieces and
+    the EOF block into one file, then every rank runs `germline-threshold --reads X.bam --out
+    Y.vcf --parallelism N` in-process (commands.main over this job's process group):
+    region-restricted device ingest of its share, the call, the gather of the result images to
+    rank 0 over RCCL, rank 0's VCF.  Timed between barriers, the max over ranks; per-rank stage
+    times from the command's stage clock."""
+    import shutil
+    from guacamole_amd import commands, synthetic
+    from guacamole_amd.distributed import all_gather_objects
+    from guacamole_amd.genomes import B37
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    job = os.environ.get("TORCHELASTIC_RUN_ID", "job") + "_" + os.environ.get("MASTER_PORT", "0")
+    seg = os.path.join(tmp, "gq_mp_%s_%d.bgzf" % (job, rank))
+    bam = os.path.join(tmp, "gq_mp_%s.bam" % job)
+    out = os.path.join(tmp, "gq_mp_%s.vcf" % job)
+    try:
+        t = time.perf_counter()
+        synthetic.subset_pieces(g, pieces, pieces, starts_in=True).write_bam(seg, level=1, dictionary=list(B37),
+                                                                                flags=0, name_base=rank * 10 ** 10)
+        barrier()
+        if rank == 0:
+            synthetic.write_bam_header(bam, list(B37))
+            with open(bam, "ab") as fo:
+                for r in range(world):
+                    with open(os.path.join(tmp, "gq_mp_%s_%d.bgzf" % (job, r)), "rb") as fi:
+                        shutil.copyfileobj(fi, fo, 64 << 20)
+                fo.write(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+        barrier()
+        write_s = time.perf_counter() - t
+        os.remove(seg)
+        t = time.perf_counter()
+        rc = commands.main(["germline-threshold", "--reads", bam, "--out", out, "--parallelism", str(world)])
+        barrier()
+        wall = time.perf_counter() - t
+        import torch
+        x = torch.tensor([wall], dtype=torch.float64, device="cuda" if os.environ.get("GQ_DIST_BACKEND", "nccl") ==
+                         "nccl" else "cpu")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        stages = all_gather_objects(commands.LAST_TIMING)
+        if rank != 0:
+            return None
+        genotypes = stages[0].get("genotypes") if stages[0] else None
+        return {"wall_s": float(x.item()), "rc": rc, "bam_bytes": os.path.getsize(bam), "bam_write_s": write_s,
+                "genotypes": genotypes, "per_rank_stages_s": stages,
+                "command": "torch.distributed.run --nproc-per-node %d: germline-threshold --reads <genome>.bam "
+                           "--out <out>.vcf --parallelism %d (in the bench's ranks)" % (world, world)}
+    finally:
+        if os.path.exists(seg):
+            os.remove(seg)
+        if rank == 0:
+            if os.path.exists(bam):
+                os.remove(bam)
+            shutil.rmtree(out, ignore_errors=True)
+
+
+
+def somatic_parity_window(ctx, t, n, tg, ng, L: int, width: int):
+    """The CPU oracle's somatic-standard records (CLI defaults) on loci [L / 3, L / 3 + width) of
+    the same shard against the GPU's over the same loci: every field, FP64 likelihoods, log-odds
+    and evidence included, bit for bit (NaN = NaN)."""
+    import math
+    from oracle import oracle as O
+    w0 = L // 3
+    w1 = min(L - 1, w0 + width)
+    loci = (np.array([0], np.int32), np.array([w0], np.int64), np.array([w1], np.int64), np.array([0], np.int64))
+    got = ctx.somatic_standard(t, n, loci).rows
+    ts, ns = tg.to_read_set(tg.window(w0, w1)), ng.to_read_set(ng.window(w0, w1))
+    c0 = time.perf_counter()
+    want = O.somatic_standard(ts, ns, loci)
+    cpu_s = time.perf_counter() - c0
+
+    def same(a, b):
+        if isinstance(a, float) and isinstance(b, float) and math.isnan(a) and math.isnan(b):
+            return True
+        if isinstance(a, tuple):
+            return len(a) == len(b) and all(same(x, y) for x, y in zip(a, b))
+        return a == b
+    names = tg.contig_names
+    ok = len(got) == len(want) and all(
+        all(same(g[k] if k != "contig" else names[g[k]], w[k]) for k in w) for g, w in zip(got, want))
+    return {"loci": [w0, w1], "calls": len(want), "identical": bool(ok), "oracle_s": cpu_s}
 
 
 SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r04.json")

@@ -47,6 +47,9 @@ def device_reads(ctx: native.Context, rs: ReadSet) -> native.DeviceReads:
     return d
 
 
+LAST_TIMING: Optional[Dict[str, object]] = None  # the last command's stage report in this process
+
+
 class StageClock:
     """Wall time per stage of a command (GQ_TIMING=1: one JSON line on stderr at the end)."""
 
@@ -73,6 +76,8 @@ class StageClock:
         self.last = now
 
     def report(self, **extra) -> None:
+        global LAST_TIMING
+        LAST_TIMING = dict(self.stages, total_s=self.t() - self.t0, **extra)
         if self.on:
             import time
             at = {"report_at_s": time.time() - self.spawn} if self.spawn else {}
@@ -363,7 +368,9 @@ def germline_threshold_main(argv: Sequence[str]) -> int:
             mine_rs = rs
         calls = ctx.germline_threshold_device(device_reads(ctx, mine_rs), mine, args.threshold, args.emit_ref,
                                               args.emit_no_call)
+        t = clock.t()
         per_rank = gather_germline(calls, gdev)
+        clock.note("gather_s", clock.t() - t)
         # each rank numbers its own samples (by first appearance in what it read): names travel
         rank_names = all_gather_objects(list(mine_rs.sample_names))
         flat = _all_flat(mine) if output_kind(args.out) == "parquet" else None
@@ -733,9 +740,12 @@ def _finish_rank(rc: int) -> int:
     import os
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as dist
+        from . import distributed
         if dist.is_initialized():
             dist.barrier()
-            dist.destroy_process_group()
+            if distributed.OWN_GROUP:
+                dist.destroy_process_group()
+                distributed.OWN_GROUP = False
     return rc
 
 

@@ -22,6 +22,9 @@ import numpy as np
 from .loci import LociSet, partition_loci_uniformly
 
 
+OWN_GROUP = False  # init_from_env created the process group (and _finish_rank ends it)
+
+
 def rank_info() -> Tuple[int, int, int]:
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))
@@ -37,6 +40,12 @@ def init_from_env():
     import torch
     import torch.distributed as dist
     backend = os.environ.get("GQ_DIST_BACKEND", "nccl")
+    if dist.is_initialized():  # a caller's group (bench.py runs the commands in its ranks): joined, not owned
+        if backend == "nccl":
+            return rank, world, local, "cuda:%d" % local
+        return rank, world, local % max(1, torch.cuda.device_count()), "cpu"
+    global OWN_GROUP
+    OWN_GROUP = True
     if backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -263,11 +263,31 @@ def _gather_pool(pool: np.ndarray, off: np.ndarray, ln: np.ndarray):
     return pool[src], new_off
 
 
-def subset_pieces(g: "SyntheticReads", pieces, mine) -> "SyntheticReads":
+def write_bam_header(path: str, dictionary) -> None:
+    """A BAM holding only the header (no BGZF EOF block): the first piece of a file whose reads
+    other processes append (SyntheticReads.write_bam with flags 4)."""
+    L = _load()
+    out = _Out(0, *([None] * 13), 0, 0, 0, *([None] * 5), 0, 0, 0)
+    vp = C.c_void_p
+    L.gq_synth_write_bam_ex.argtypes = [vp, C.c_char_p, C.c_int32, vp, vp, C.c_int32, vp, vp, C.c_int32, C.c_int32,
+                                        C.c_int64]
+    L.gq_synth_write_bam_ex.restype = C.c_int
+    names = (C.c_char_p * max(1, len(dictionary)))(*[c.encode() for c, _ in dictionary])
+    lens = np.array([int(n) for _, n in dictionary] or [0], np.int64)
+    crb = np.zeros(2, np.int64)
+    ids = np.zeros(1, np.int32)
+    rc = L.gq_synth_write_bam_ex(C.byref(out), os.fsencode(path), len(dictionary), C.cast(names, vp), lens.ctypes.data,
+                                 1, crb.ctypes.data, ids.ctypes.data, 6, 1, 0)
+    if rc != 0:
+        raise OSError("gq_synth_write_bam_ex failed (%d) for %s" % (rc, path))
+
+
+def subset_pieces(g: "SyntheticReads", pieces, mine, starts_in: bool = False) -> "SyntheticReads":
     """The reads of `g` (generate_pieces over `pieces`) overlapping the ranges `mine` (a sub-list
     of (contig, contig_length, start, end), one per contig, in `pieces`' contig order): what a
     task over those loci receives (DistributedUtil.scala:584-597), with local contig ids in
-    `mine`'s order.  Reads straddling a cut are in both sides' subsets."""
+    `mine`'s order.  Reads straddling a cut are in both sides' subsets; with starts_in, only the
+    reads starting inside the ranges are kept (each read in exactly one side's subset)."""
     a = g.arrays
     crb = np.asarray(a["contig_read_begin"], np.int64)
     names = [p[0] for p in pieces]
@@ -275,7 +295,7 @@ def subset_pieces(g: "SyntheticReads", pieces, mine) -> "SyntheticReads":
     for contig, clen, s0, e0 in mine:
         k = names.index(contig)
         idx = np.arange(crb[k], crb[k + 1])
-        keep = idx[(a["start"][idx] < e0) & (a["end"][idx] > s0)]
+        keep = idx[(a["start"][idx] < e0) & ((a["start"][idx] >= s0) if starts_in else (a["end"][idx] > s0))]
         sel.append(keep)
         begin.append(begin[-1] + len(keep))
     idx = np.concatenate(sel) if sel else np.zeros(0, np.int64)

@@ -303,3 +303,14 @@ def test_depth_bounds_balance_reads_not_loci():
     assert depth_bounds(sizes, counts, 2) == [0, 2000, 8000]
     assert depth_bounds(sizes, np.zeros(8, np.int64), 4) == [0, 2000, 4000, 6000, 8000]
     assert depth_bounds(sizes, counts, 1) == [0, 8000]
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """bench.py --gpus N under a launcher with WORLD_SIZE != N exits non-zero before any GPU work."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr

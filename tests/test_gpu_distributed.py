@@ -61,7 +61,7 @@ def test_somatic_two_ranks_equal_one(tmp_path):
 def _bench(world, out, extra):
     env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
     args = ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "0", "--somatic-length", "0", "--panel-length", "0",
-            "--no-single-pass",
+            "--no-single-pass", "--no-configs3",
             "--no-cpu-baseline", "--shared-reads", "--calls-out", out] + extra
     if world == 1:
         cmd = [sys.executable] + args
@@ -84,6 +84,28 @@ def test_bench_two_ranks_equal_one(tmp_path):
     one, _ = _bench(1, str(tmp_path / "one.json"), ["--length", L, "--genome-ranks", "2"])
     assert one == two and one.count("], [") > 100
     assert '"n_gpus": 2' in out2
+
+
+def test_plain_bench_gpus_two_launches_its_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two ranks itself (torch.distributed.run,
+    before any GPU call) and reports n_gpus 2, with the 2-rank CLI single pass over one BAM of
+    the split genome: each rank's region-restricted device ingest, call and gather stages."""
+    import json
+    env = dict(os.environ, GQ_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--length", "2000000", "--steps", "2", "--warmup", "1",
+           "--somatic-length", "0", "--panel-length", "0", "--no-cpu-baseline", "--no-configs3"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    sp = line["end_to_end"]["single_pass"]
+    assert sp["rc"] == 0 and sp["genotypes"] > 100 and len(sp["per_rank_stages_s"]) == 2
+    for rk, st in enumerate(sp["per_rank_stages_s"]):
+        assert st["rank"] == rk and st["ingest"] == "device"
+        assert st["load_reads"] > 0 and st["call"] > 0 and "gather_s" in st
+        assert st["device_ingest"]["plan"] is not None  # region-restricted: planned segments only
 
 
 def test_rccl_gather_branch_world_one():
