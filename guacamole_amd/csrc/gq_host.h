@@ -372,6 +372,111 @@ __device__ __forceinline__ int32_t slice_assign_rows(const DevReads &R, const Sl
   return __ballot(over) ? -1 : nrows;
 }
 
+// Inclusive prefix minimum over the 64 lanes of a wave (signed), DPP as wave_incl_scan; lanes
+// shifted in from outside the row / wave contribute INT32_MAX.
+__device__ __forceinline__ int32_t wave_incl_min(int32_t v) {
+  constexpr int kMax = 0x7FFFFFFF;
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+
+// Rows of slice W's pieces without a sequential pass (one wave): greedy interval partitioning
+// in read order (= first column order) that reuses the row freed EARLIEST — as optimal as
+// first-fit (any greedy in start order that opens a row only when none is free uses as many rows
+// as the deepest column holds pieces), and computable in parallel.  With pieces k = 0, 1, ... in
+// read order, A_k = pieces ending at or before piece k's first column (a column histogram of the
+// ends), and U_k = reuses among pieces 0..k-1: U_{k+1} = min(U_k + 1, A_k), so
+// U_k = k + min(0, min_{j<k}(A_j - j) - 1) (a prefix minimum).  Piece k reuses a row iff
+// A_k > U_k: the row of E[U_k], the U_k-th piece in end order (which ended before k began, so it
+// precedes k); otherwise it opens row k - U_k.  Rows resolve by following E (chains inside a
+// 64-piece batch, a few steps).  Each window read's row goes to rows[r - ra] (0xFFFF: no piece).
+// lds: 2 * kRowsLdsPieces u16 (E and the pieces' rows) + 32 u32.  Returns the slice's rows, -1
+// past kSliceRowsMax, or -2 when the slice has more than kRowsLdsPieces pieces (the caller
+// takes slice_assign_rows there).
+constexpr int kRowsLdsPieces = 1024;
+__device__ __forceinline__ int32_t slice_rows_fifo(const DevReads &R, const SliceWin &W, uint16_t *__restrict__ rows,
+                                                   uint16_t *__restrict__ eord, uint16_t *__restrict__ prow_k,
+                                                   uint32_t *__restrict__ hist) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  constexpr int32_t kInf = 0x7FFFFFFF;
+  if (lane < 32) hist[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // pass 1: a histogram of the pieces' end columns (1..16) and the piece count
+  int32_t n = 0;
+  for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
+    const int64_t r = r0 + lane;
+    int32_t s0 = W.qc0, sl = 0;
+    if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    if (sl > 0) atomicAdd(&hist[s0 - W.qc0 + sl], 1u);
+    n += (int32_t)__popcll(__ballot(sl > 0));
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (n > kRowsLdsPieces) return -2;
+  // lane v (0..16): cum = pieces ending at or before column v
+  const uint32_t cum = wave_incl_scan(lane <= 16 ? hist[lane] : 0u);
+  uint32_t seen = 0;  // lane v: pieces ending at column v already ranked
+  int32_t runmin = kInf, base = 0;
+  for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
+    const int64_t r = r0 + lane;
+    int32_t s0 = W.qc0, sl = 0;
+    if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    const bool has = sl > 0;
+    const int32_t c0 = has ? s0 - W.qc0 : 0, c1 = c0 + sl;
+    const unsigned long long hm = __ballot(has);
+    const int32_t k = base + (int32_t)__popcll(hm & below);
+    // E[rank] = k, rank = pieces ending before piece k's end + those with its end ranked before it
+    int32_t rank = 0;
+    unsigned long long pend = hm;
+    while (pend) {  // the batch's distinct end columns (uniform)
+      const int pl = __ffsll((long long)pend) - 1;
+      const int32_t v = __builtin_amdgcn_readlane(c1, pl);
+      const unsigned long long m = __ballot(has && c1 == v);
+      pend &= ~m;
+      const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)cum, v - 1);
+      const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)seen, v);
+      if (has && c1 == v) rank = (int32_t)(before + sv + (uint32_t)__popcll(m & below));
+      seen += lane == v ? (uint32_t)__popcll(m) : 0u;
+    }
+    if (has) eord[rank] = (uint16_t)k;
+    // U_k = k + min(0, min_{j<k}(A_j - j) - 1), A_k = cum[c0]
+    const int32_t A = __builtin_amdgcn_ds_bpermute(4 * c0, (int)cum);
+    const int32_t incl = wave_incl_min(has ? A - k : kInf);
+    const int32_t excl = min(runmin, __builtin_amdgcn_update_dpp(kInf, incl, 0x138, 0xF, 0xF, false));  // wave_shr:1
+    const int32_t U = k + min(0, excl == kInf ? 0 : excl - 1);
+    const bool reuse = has && A > U;
+    if (has) prow_k[k] = reuse ? (uint16_t)0xFFFFu : (uint16_t)(k - U);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int32_t parent = reuse ? (int32_t)eord[U] : 0;
+    int32_t row = has && !reuse ? k - U : -1;
+    // a reused row is its parent's (the parent precedes it; chains inside the batch take a few rounds)
+    while (__ballot(reuse && row < 0)) {
+      if (reuse && row < 0) {
+        const uint32_t pr = prow_k[parent];
+        if (pr != 0xFFFFu) {
+          row = (int32_t)pr;
+          prow_k[k] = (uint16_t)pr;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (rows && r < W.rz) rows[r - W.ra] = has && row < kSliceRowsMax ? (uint16_t)row : (uint16_t)0xFFFFu;
+    runmin = min(runmin, __builtin_amdgcn_readlane(incl, 63));
+    base += (int32_t)__popcll(hm);
+  }
+  const int32_t nrows = n - (n + min(0, runmin == kInf ? 0 : runmin - 1));
+  return nrows > kSliceRowsMax ? -1 : nrows;
+}
+
 // A piece of a 64-read batch, for the word-per-lane fills (slice_fill): set up once by the
 // piece's lane, read from LDS by the lanes of its words.
 // Bytes [lo, hi) of an 8-byte word (clamped to [0, 8)) as a mask: an edge word's loci inside its read.
@@ -573,6 +678,133 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
   return x;
 }
 
+// ---- Piece fills: a wave per slice, a lane per piece, rows built in LDS (the default) ----
+// A wave takes a slice: each lane takes one of its window reads and, if the read has a piece in
+// the slice, issues the loads of all the piece's words at once (up to 16 columns), turns them into
+// words and writes them into the slice's rows in LDS (kPieceRows rows at a time, padded to 17
+// words per row against bank conflicts); the rows then leave LDS as whole rows, 64 consecutive
+// words per store (every word written, so the pool needs no preset).  A window over 64 reads
+// takes several batches, a slice over kPieceRows rows several row chunks.
+constexpr int kPieceRows = 64;
+constexpr int kPieceStride = 17;  // LDS words per row
+struct PieceRec {                 // a window read as one lane holds it
+  int64_t p0;                     // pool offset of locus 0 (column-eligible reads)
+  int32_t s, e;                   // [start, end)
+  uint32_t info, mq;              // ColDesc info, mapping quality
+  int64_t md_off;                 // its MD events
+  uint32_t ev[4];                 // (EV fills) its first four MD events (0xFFFFFFFF: none)
+};
+// proj_codes4 for the bytes of a column-eligible read (A C G T N only, zero outside the read):
+// A 1, C 3, G 7, T 4 are the low three bits, N (6) and zero bytes give 0.
+__device__ __forceinline__ uint32_t proj_codes4_clean(uint32_t x) {
+  const uint32_t y = x & 0x07070707u;
+  const uint32_t n = y ^ 0x06060606u;                                   // zero bytes: N
+  const uint32_t keep = (((n & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | n) & 0x80808080u;  // 0x80: not N
+  return y & ((keep >> 7) * 0xFFu);
+}
+__device__ __forceinline__ PieceMeta piece_rec_meta(const PieceRec &m) {
+  PieceMeta p;
+  p.p0 = m.p0;
+  p.s = m.s;
+  p.e = m.e;
+  p.s0 = 0;
+  p.row = 0;
+  p.info = m.info;
+  p.mq = m.mq;
+  return p;
+}
+
+// For every slice (grid-stride over waves): for each row chunk, rows zeroed in `lds` (words of
+// type T, `zero`), then each window read r with a piece whose row lies in the chunk:
+//   keep(rec)                      false: the piece writes nothing (its cells keep `zero`);
+//   fast(rec, col, raw) for each of its columns, all issued before any is used (false: that
+//                                  word takes slow(rec, r, col) instead, out of the unrolled path);
+//   word(rec, col, raw) -> T       the word;
+// then the chunk's rows go to pool (T words, 16 per row) at the slice's rows.  done(slot, flag)
+// closes the slice with the OR over its lanes of flag(word) (e.g. a kMargin8None term).  pbad
+// slices get `zero` rows.
+template <class T, class Raw, bool EV, class K, class F, class Wd, class S, class G, class D>
+__device__ __forceinline__ void piece_fill(const DevReads &R, int64_t n_slices, T *__restrict__ lds, T *__restrict__ pool,
+                                           T zero, K &&keep, F &&fast, Wd &&word, S &&slow, G &&flag, D &&done) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = wave_id(); slot < n_slices; slot += nw) {
+    const int64_t g0 = R.srow[slot];
+    const int32_t nr = (int32_t)(R.srow[slot + 1] - g0);
+    if (nr <= 0) continue;
+    T *out = pool + 16 * g0;
+    if (R.pbad[slot]) {
+      for (int32_t c = lane; c < 16 * nr; c += 64) out[c] = zero;
+      continue;
+    }
+    const SliceWin W = slice_stored(R, slot);
+    const uint16_t *prw = R.prow + R.soff[slot];
+    bool any = false;
+    for (int32_t k0 = 0; k0 < nr; k0 += kPieceRows) {
+      const int32_t nk = nr - k0 < kPieceRows ? nr - k0 : kPieceRows;
+      for (int32_t c = lane; c < kPieceStride * nk; c += 64) lds[c] = zero;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
+        const int64_t r = r0 + lane;
+        const bool in = r < W.rz;
+        const int64_t rr = in ? r : W.ra;
+        const int32_t row = in ? (int32_t)prw[rr - W.ra] : 0xFFFF;
+        const ProjRec pr = R.prec[rr];
+        const ColDesc d = R.cdesc[rr];
+        const int32_t ld = R.lead[rr];
+        const int64_t so = R.seq_off[rr];
+        PieceRec m;
+        m.mq = R.mapq[rr];
+        m.md_off = R.md_off[rr];
+        m.p0 = so + (ld > 0 ? ld : 0) - d.start;
+        m.s = d.start;
+        m.e = d.end;
+        m.info = d.info;
+        int32_t s0 = W.qc0, sl = 0;
+        piece_of(pr, W.qc0, s0, sl);
+        const bool mine = in && row != 0xFFFF && row >= k0 && row < k0 + nk && sl > 0 && keep(m);
+        if (!__ballot(mine)) continue;
+        if constexpr (EV) {
+          const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
+          const uint32_t *ev = R.md_ev + m.md_off;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) m.ev[q] = mine && q < nmd ? ev[q] : 0xFFFFFFFFu;
+        }
+        const int32_t c0 = s0 - W.qc0;
+        T *lrow = lds + kPieceStride * (mine ? row - k0 : 0);
+        uint32_t sm = 0;
+        const int32_t nj = mine ? sl : 0;
+        for (int32_t j0 = 0; __ballot(j0 < nj); j0 += 4) {  // four words at a time, their loads together
+          Raw raw[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            raw[j] = Raw{};
+            if (j0 + j < nj && !fast(m, s0 + j0 + j, raw[j])) sm |= 1u << (j0 + j);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j0 + j < nj && !((sm >> (j0 + j)) & 1u)) lrow[c0 + j0 + j] = word(m, s0 + j0 + j, raw[j]);
+        }
+#pragma unroll 1
+        for (int j = 0; j < 16; ++j)  // the rare words off the fast path, one copy of their code
+          if (mine && ((sm >> j) & 1u)) lrow[c0 + j] = slow(m, r, s0 + j);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      T *o = out + 16 * k0;
+      for (int32_t c = lane; c < 16 * nk; c += 64) {
+        const T w = lds[kPieceStride * (c >> 4) + (c & 15)];
+        o[c] = w;
+        any = any || flag(w);
+      }
+      __builtin_amdgcn_wave_barrier();  // (the next chunk rezeroes the rows)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    done(slot, __ballot(any) != 0);
+  }
+}
+
 // ---- Read-major fills (the default; slice_fill above is the A/B alternative, GQ_FILL=slice) ----
 inline int fill_dbg() {  // GQ_FILL_DBG (read_fill): diagnostics and the XCD-contiguous order
   static const int v = getenv("GQ_FILL_DBG") ? atoi(getenv("GQ_FILL_DBG")) : 0;
@@ -580,6 +812,17 @@ inline int fill_dbg() {  // GQ_FILL_DBG (read_fill): diagnostics and the XCD-con
 }
 inline bool fill_slice_major() {
   static const bool v = getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "slice") == 0;
+  return v;
+}
+// The cell / piece fills (a wave per slice, a lane per cell / piece) are the default; GQ_FILL=rw / slice: the
+// read-major / slice-major fills of round 4 (A/B alternatives).
+inline bool fill_pieces() {  // the cell or piece fills (no preset of the pool)
+  static const bool v = !getenv("GQ_FILL") || strcmp(getenv("GQ_FILL"), "pieces") == 0 ||
+                        strcmp(getenv("GQ_FILL"), "cells") == 0;
+  return v;
+}
+inline int fill_mode() {  // 0: cells (the projection's default), 1: pieces (GQ_FILL=pieces)
+  static const int v = getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "pieces") == 0 ? 1 : 0;
   return v;
 }
 // One wave per batch of 64 consecutive reads, a lane per word of the batch's projections: a

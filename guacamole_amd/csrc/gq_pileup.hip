@@ -199,7 +199,7 @@ __global__ void plan_tiles(const int32_t *__restrict__ r_contig, const int64_t *
   }
 }
 
-// Column-kernel records (derived once at upload, after read_shape).  A general-CIGAR read
+// Column-kernel records (derived once at upload, after the read shapes).  A general-CIGAR read
 // (not a single (M|=|X) block) becomes segments for the in-kernel path, PileupElement's rules
 // (PileupElement.scala:68-248, as walk_read_lane) over the whole read:
 //   count   loci [ref_off, ref_off + len) are Match/Mismatch elements whose bases start at
@@ -316,56 +316,10 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
 
 // ---- Projections (germline_proj, ProjRec in gq_kernels.h), derived after col_derive -------
 __device__ __forceinline__ bool proj_ok(uint32_t info) { return (info & (kColEligible | kColGeneral)) != 0; }
-
-// Sparse entries of each read's projection; entry n is 0.
-__global__ void proj_count(DevReads R, const uint32_t *__restrict__ n_nbase, int64_t *__restrict__ nents) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > R.n_reads) return;
-  int64_t e = 0;
-  if (r < R.n_reads) {
-    const ColDesc d = R.cdesc[r];
-    if (proj_ok(d.info)) {
-      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
-      e = nmd + (int64_t)n_nbase[r];
-      if (d.info & kColGeneral) {
-        const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
-        const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
-        for (int32_t q = 0; q < nseg; ++q) e += (sg[2 * q + 1] >> 16) != kSegCount ? 1 : 0;
-      }
-    }
-  }
-  nents[r] = e;
-}
-
-// ProjRec of each read (record n: zero).
-__global__ void prec_fill(DevReads R, ProjRec *__restrict__ prec) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > R.n_reads) return;
-  ProjRec p{0, 0};
-  if (r < R.n_reads) {
-    const ColDesc d = R.cdesc[r];
-    p.col0 = d.start >> 3;
-    p.col1 = proj_ok(d.info) ? (d.end + 7) >> 3 : kProjNone;
-  }
-  prec[r] = p;
-}
-
-// pbad = 1 on every slice a read the projection cannot take overlaps (the projection
-// kernels hand such blocks to the walkers), thread per read.
-__global__ void slice_bad(DevReads R, const ProjRec *__restrict__ prec, uint8_t *__restrict__ pbad) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R.n_reads) return;
-  if (prec[r].col1 != kProjNone) return;
-  int lo = 0, hi = R.n_contigs - 1;  // contig of r: last c with contig_read_begin[c] <= r
-  while (lo < hi) {
-    const int m = (lo + hi + 1) >> 1;
-    if (R.contig_read_begin[m] <= r) lo = m;
-    else hi = m - 1;
-  }
-  const int64_t q0 = R.qoff[lo];
-  const int32_t s = R.start[r], e = R.end[r];
-  if (e > s && s >= 0)
-    for (int32_t q = s >> 7; q <= (e - 1) >> 7; ++q) pbad[q0 + q] = 1;
+// Codes of four bases of a column-eligible read (A C G T N, 0 outside the read): the low three
+// bits index a v_perm table (A 1, C 3, T 4, N 0, G 7, 0 -> 0) — proj_codes4 for such bytes.
+__device__ __forceinline__ uint32_t perm_codes4(uint32_t x) {
+  return __builtin_amdgcn_perm(0x07000004u, 0x03000100u, x & 0x07070707u);
 }
 
 // Each slice's read window (slice_window), thread per slice: its first read and its number of
@@ -383,10 +337,54 @@ __global__ void slice_windows(DevReads R, int64_t n_slices, int64_t *__restrict_
   scnt[q] = W.rz - W.ra;
 }
 
+// The projection's per-read records in one pass (thread per read, record n: zeros): ProjRec
+// (prec_fill), the pbad slices of the reads the projection cannot take (slice_bad), the sparse
+// entries per read (proj_count) and the reads it takes, counted into kSpread words (proj_count_ok).
+__global__ void proj_prep(DevReads R, const uint32_t *__restrict__ n_nbase, ProjRec *__restrict__ prec,
+                          uint8_t *__restrict__ pbad, int64_t *__restrict__ nents, unsigned long long *__restrict__ n_ok) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  ProjRec p{0, 0};
+  int64_t e = 0;
+  bool ok = false;
+  if (r < R.n_reads) {
+    const ColDesc d = R.cdesc[r];
+    ok = proj_ok(d.info);
+    p.col0 = d.start >> 3;
+    p.col1 = ok ? (d.end + 7) >> 3 : kProjNone;
+    if (ok) {
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+      e = nmd + (int64_t)n_nbase[r];
+      if (d.info & kColGeneral) {
+        const int32_t nseg = (int32_t)((d.info >> 18) & 0xFFu);
+        const uint32_t *sg = R.cev + R.caux_off[r] + nmd;
+        for (int32_t q = 0; q < nseg; ++q) e += (sg[2 * q + 1] >> 16) != kSegCount ? 1 : 0;
+      }
+    } else {  // its slices go to the walkers
+      int lo = 0, hi = R.n_contigs - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (R.contig_read_begin[m] <= r) lo = m;
+        else hi = m - 1;
+      }
+      const int64_t q0 = R.qoff[lo];
+      const int32_t s = R.start[r], en = R.end[r];
+      if (en > s && s >= 0)
+        for (int32_t q = s >> 7; q <= (en - 1) >> 7; ++q) pbad[q0 + q] = 1;
+    }
+  }
+  if (r <= R.n_reads) {
+    prec[r] = p;
+    nents[r] = e;
+  }
+  const unsigned long long k = (unsigned long long)__popcll(__ballot(ok));
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
+}
+
 // Rows of each slice and each of its reads' row (slice_assign_rows, one wave per slice); past
 // kSliceRowsMax the slice is pbad (and gets no rows).
 __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, uint16_t *__restrict__ prow,
-                                                 int32_t *__restrict__ srows, uint8_t *__restrict__ pbad) {
+                                                 int32_t *__restrict__ srows, uint8_t *__restrict__ pbad,
+                                                 int first_fit) {
   __shared__ __attribute__((aligned(16))) uint8_t s_rend[4][kSliceRowsMax];
   __shared__ uint16_t s_fl[4][kSliceRowsMax];
   const int wv = threadIdx.x >> 6;
@@ -394,7 +392,11 @@ __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, u
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t slot = w0; slot < n_slices; slot += nw) {
     const SliceWin W = slice_stored(R, slot);
-    const int32_t n = slice_assign_rows(R, W, prow + R.soff[slot], s_rend[wv], s_fl[wv]);
+    // the parallel assignment (its E / row lists in the first-fit pass's LDS), first-fit past it
+    int32_t n = first_fit ? -2
+                                 : slice_rows_fifo(R, W, prow + R.soff[slot], reinterpret_cast<uint16_t *>(s_rend[wv]),
+                                                   s_fl[wv], reinterpret_cast<uint32_t *>(s_fl[wv] + kRowsLdsPieces));
+    if (n == -2) n = slice_assign_rows(R, W, prow + R.soff[slot], s_rend[wv], s_fl[wv]);
     if ((threadIdx.x & 63) == 0) {
       srows[slot] = n < 0 ? 0 : (n + kRowPad - 1) & ~(kRowPad - 1);  // zero rows up to a multiple of kRowPad
       if (n < 0) pbad[slot] = 1;
@@ -404,16 +406,6 @@ __global__ __launch_bounds__(256) void row_count(DevReads R, int64_t n_slices, u
 __global__ void rows64(int64_t n, const int32_t *__restrict__ srows, int64_t *__restrict__ out) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q <= n) out[q] = q < n ? srows[q] : 0;
-}
-
-// Reads the projection takes, into kSpread words (summed on the host): a grid-stride count per
-// thread, one add per wave.
-__global__ void proj_count_ok(DevReads R, const ProjRec *__restrict__ prec, unsigned long long *__restrict__ n_ok) {
-  unsigned long long k = 0;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R.n_reads; r += (int64_t)gridDim.x * blockDim.x)
-    k += prec[r].col1 != kProjNone ? 1u : 0u;
-  for (int d = 32; d >= 1; d >>= 1) k += __shfl_xor(k, d, 64);
-  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
 }
 
 // The projection pool in block rows, one wave per slice, a lane per word (the rows row_count
@@ -453,10 +445,204 @@ __global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restr
       R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, [](int64_t) {}, [](const ReadMeta &) { return true; },
       [&](int64_t r, const ReadMeta &m, int32_t col) { return proj_fetch(R, r, piece_meta(m), col); },
       [&](bool act, const ProjRaw &x, int64_t, const ReadMeta &, int32_t col, int64_t grow, int64_t) {
-        if (act)
+        if (act)  // (an eligible read's bytes are A C G T N: the v_perm lookup)
           out[16 * grow + (col & 15)] =
-              x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
+              x.gen ? x.word : perm_codes4((uint32_t)x.b) | (perm_codes4((uint32_t)(x.b >> 32)) << 4);
       });
+}
+
+// ---- The projection pool by cells (the default) ----
+// A wave per slice, a lane per cell (row k, column c) of its rows, every word written (zeros where
+// no piece lies: the pool needs no preset), 64 consecutive words per store.  The window's reads
+// are staged in LDS as 16-byte records (pool offset of locus 0 relative to the window's first
+// read, start, end, ColDesc info) and a map cell -> window read (u8) is marked from each piece's
+// stored row; a cell then costs one map read, one record read, one 8-byte load of its bases from
+// the pool (a 32-bit offset on the window's base), a v_perm code lookup and its store.  Slices
+// with more than kCell3Win window reads are listed in deep (their rows zeroed) for the
+// slice-major fill.
+constexpr int kCell3Win = 255;    // window reads a u8 map can name
+constexpr int kCell3Rows = 64;    // rows per map chunk
+struct __attribute__((aligned(16))) Cell3Rec {
+  uint32_t a;         // seq_off + leading clip - seq_off[window's first read]
+  int32_t s, e;       // [start, end)
+  uint32_t info;      // ColDesc info (bit kColEligible: the fast path)
+};
+__global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj,
+                                                       int64_t *__restrict__ deep, unsigned long long *__restrict__ n_deep,
+                                                       int dbg) {
+  __shared__ Cell3Rec s_rec[4][kCell3Win];
+  __shared__ uint8_t s_map[4][kCell3Rows * 16];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Cell3Rec *rec = s_rec[wv];
+  uint8_t *map = s_map[wv];
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = wave_id(); slot < n_slices; slot += nw) {
+    const int64_t g0 = R.srow[slot];
+    const int32_t nr = (int32_t)(R.srow[slot + 1] - g0);
+    if (nr <= 0) continue;
+    uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * g0;
+    const SliceWin W = slice_stored(R, slot);
+    const int32_t nwin = (int32_t)(W.rz - W.ra);
+    if (R.pbad[slot] || nwin > kCell3Win) {
+      for (int32_t c = lane; c < 16 * nr; c += 64) out[c] = 0u;
+      if (!R.pbad[slot] && lane == 0) deep[atomicAdd(n_deep, 1ull)] = slot;
+      continue;
+    }
+    const int64_t base = R.seq_off[W.ra];  // the window's bytes: [base, ...) in read order
+    const uint8_t *pool = R.seq + base;
+    const int64_t span = R.seq_cap - base;  // readable bytes from pool
+    const uint16_t *prw = R.prow + R.soff[slot];
+    int32_t prow_i = 0xFFFF, pc0 = 0, psl = 0;  // this lane's window read (first batch) and its piece
+    for (int32_t i = lane; i < nwin; i += 64) {
+      const int64_t r = W.ra + i;
+      const ColDesc d = R.cdesc[r];
+      const int32_t ld = R.lead[r];
+      const int64_t so = R.seq_off[r];
+      const ProjRec pr = R.prec[r];
+      const int32_t row = prw[i];
+      Cell3Rec m;
+      m.a = (uint32_t)(so + (ld > 0 ? ld : 0) - base);
+      m.s = d.start;
+      m.e = d.end;
+      m.info = d.info;
+      rec[i] = m;
+      int32_t s0, sl;
+      piece_of(pr, W.qc0, s0, sl);
+      if (i < 64) {
+        prow_i = row;
+        pc0 = s0 - W.qc0;
+        psl = row == 0xFFFF ? 0 : sl;
+      }
+    }
+    for (int32_t k0 = 0; k0 < nr; k0 += kCell3Rows) {
+      const int32_t nk = nr - k0 < kCell3Rows ? nr - k0 : kCell3Rows;
+      for (int32_t c = lane; c < 16 * nk; c += 64) map[c] = 0xFFu;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int32_t i = lane; i < nwin; i += 64) {  // each piece marks its cells in the chunk
+        int32_t row = prow_i, c0 = pc0, sl = psl;
+        if (i >= 64) {  // (windows over 64 reads: the later batches' pieces reloaded)
+          row = prw[i];
+          int32_t s0;
+          piece_of(R.prec[W.ra + i], W.qc0, s0, sl);
+          c0 = s0 - W.qc0;
+          sl = row == 0xFFFF ? 0 : sl;
+        }
+        if (sl <= 0 || row < k0 || row >= k0 + nk) continue;
+        uint8_t *mp = map + 16 * (row - k0) + c0;
+        for (int32_t j = 0; j < sl; ++j) mp[j] = (uint8_t)i;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      uint32_t *o = out + 16 * k0;
+      for (int32_t c00 = 0; c00 < 16 * nk; c00 += 256) {  // four cells per lane, their loads together
+        uint64_t b[4];
+        uint32_t pp[4];
+        uint32_t slow = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t c = c00 + 64 * u + lane;
+          pp[u] = c < 16 * nk ? map[c] : 0xFFu;
+          b[u] = 0;
+          if (pp[u] != 0xFFu) {
+            const Cell3Rec m = rec[pp[u]];
+            const int32_t lb = 8 * (W.qc0 + (c & 15));
+            const int64_t v = (int64_t)m.a + lb - m.s;
+            if (!(m.info & kColEligible) || v < 0 || v + 8 > span) {
+              slow |= 1u << u;
+            } else if (dbg & 1) {  // ablation: no loads
+              b[u] = (uint64_t)v;
+            } else {
+              b[u] = *reinterpret_cast<const gq_u64u *>(pool + (uint32_t)v);
+              if (m.s > lb || m.e < lb + 8) b[u] &= edge_mask(m.s - lb, m.e - lb);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t c = c00 + 64 * u + lane;
+          if (c < 16 * nk && !((slow >> u) & 1u))
+            o[c] = perm_codes4((uint32_t)b[u]) | (perm_codes4((uint32_t)(b[u] >> 32)) << 4);
+        }
+        if (slow) {  // rare: a general CIGAR, a word at the pool's end
+#pragma unroll 1
+          for (int u = 0; u < 4; ++u) {
+            if (!((slow >> u) & 1u)) continue;
+            const int32_t c = c00 + 64 * u + lane;
+            const uint32_t p = map[c];
+            const Cell3Rec m = rec[p];
+            PieceMeta pm;
+            pm.p0 = base + m.a - m.s;
+            pm.s = m.s;
+            pm.e = m.e;
+            pm.s0 = 0;
+            pm.row = 0;
+            pm.info = m.info;
+            pm.mq = 0;
+            const ProjRaw x = proj_fetch(R, W.ra + p, pm, W.qc0 + (c & 15));
+            o[c] = x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the map)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  }
+}
+
+// The listed (deep) slices, slice-major (their rows zeroed by proj_fill_cells).
+__global__ __launch_bounds__(256) void proj_fill_deep(DevReads R, const int64_t *__restrict__ deep,
+                                                      const unsigned long long *__restrict__ n_deep,
+                                                      uint8_t *__restrict__ proj) {
+  __shared__ PieceMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][64];
+  PieceMeta *meta = s_meta[threadIdx.x >> 6];
+  uint32_t *owner = s_owner[threadIdx.x >> 6];
+  const int64_t nd = (int64_t)*n_deep;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave_id(); i < nd; i += nw) {
+    const int64_t slot = deep[i];
+    uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * R.srow[slot];
+    slice_fill<false, 1>(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
+        [&](int64_t, PieceMeta &, int64_t) { return true; },
+        [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t) { return proj_fetch(R, r, m, col); },
+        [&](bool act, const ProjRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t) {
+          if (act)
+            out[16 * (int64_t)m.row + (col & 15)] =
+                x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
+        });
+  }
+}
+
+// The projection pool slice by slice (piece_fill in gq_host.h): a wave per slice, a lane per
+// piece, the rows built in LDS and written whole (zeros where no piece lies: no preset).
+__global__ __launch_bounds__(256) void proj_fill_pieces(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj,
+                                                        int dbg) {
+  __shared__ uint32_t s_rows[4][kPieceRows * kPieceStride];
+  piece_fill<uint32_t, uint64_t, false>(
+      R, n_slices, s_rows[threadIdx.x >> 6], reinterpret_cast<uint32_t *>(proj), 0u,
+      [](const PieceRec &) { return true; },
+      [&](const PieceRec &m, int32_t col, uint64_t &b) {  // a column-eligible read's eight bases, one load
+        const int32_t lb = 8 * col;
+        const int64_t a = m.p0 + lb;
+        if (!(m.info & kColEligible) || a < 0 || a + 8 > R.seq_cap) return false;
+        if (dbg & 1) {  // ablation: no loads
+          b = (uint64_t)a;
+          return true;
+        }
+        b = *reinterpret_cast<const gq_u64u *>(R.seq + a);
+        if (m.s > lb || m.e < lb + 8) b &= edge_mask(m.s - lb, m.e - lb);  // (the read's first / last word)
+        return true;
+      },
+      [](const PieceRec &, int32_t, uint64_t b) {
+        return proj_codes4_clean((uint32_t)b) | (proj_codes4_clean((uint32_t)(b >> 32)) << 4);
+      },
+      [&](const PieceRec &m, int64_t r, int32_t col) {
+        const ProjRaw x = proj_fetch(R, r, piece_rec_meta(m), col);
+        return x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
+      },
+      [](uint32_t) { return false; }, [](int64_t, bool) {});
 }
 
 // The sparse entries of each read (thread per read): MD events, N bases (without an event),
@@ -509,9 +695,7 @@ __global__ void pev_fill(DevReads R, const int64_t *__restrict__ eoff, uint2 *__
 // must be sorted"; plan_tiles binary-searches both); 2 = an offset / length outside its pool or
 // a sample slot >= n_samples (would read out of bounds); 4 = the sequence pool is not in read
 // order (flags only: such tiles take the walker).
-__global__ void validate_reads(DevReads R, int *__restrict__ bad) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R.n_reads) return;
+__device__ __forceinline__ int validate_one(const DevReads &R, int64_t r) {
   int lo = 0, hi = R.n_contigs;  // contig of r: last c with contig_read_begin[c] <= r
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
@@ -528,7 +712,7 @@ __global__ void validate_reads(DevReads R, int *__restrict__ bad) {
   if (R.n_md[r] > 0 && (R.md_off[r] < 0 || R.md_off[r] + R.n_md[r] > R.md_len)) b |= 2;
   if ((int)R.sample[r] >= R.n_samples) b |= 2;
   if (r > 0 && R.seq_off[r] < R.seq_off[r - 1] + R.seq_len[r - 1]) b |= 4;
-  if (b) atomicOr(bad, b);
+  return b;
 }
 
 // clean[r] = every sequenced byte of read r is one of A C G T N (the germline column path's
@@ -601,9 +785,8 @@ __global__ void read_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__
 
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
 // [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
-__global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R.n_reads) return;
+__device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t *__restrict__ lead,
+                                          uint8_t *__restrict__ ev_rb) {
   const int64_t off = R.cigar_off[r];
   const int32_t n = R.n_cigar[r];
   int32_t ld = 0, mlen = 0;
@@ -659,6 +842,17 @@ __global__ void read_shape(DevReads R, int16_t *__restrict__ lead, uint8_t *__re
     if (consumes_read(op)) rp += len;
   }
   for (; k < nmd; ++k) rb[k] = 0;
+}
+// The upload-time checks (validate_one) and the read shapes (shape_one) in one pass over the
+// reads: a read whose own offsets lie outside their pools (bit 2) gets no shape (the upload fails
+// on the flag anyway).
+__global__ void read_prep(DevReads R, int *__restrict__ bad, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const int b = validate_one(R, r);
+  if (b) atomicOr(bad, b);
+  if (b & 2) lead[r] = -1;
+  else shape_one(R, r, lead, ev_rb);
 }
 
 __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, int alt_len) {
@@ -1762,7 +1956,8 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     HIP_TRY(d->dp.get(&flag, sizeof(int)));
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(validate_reads, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag);
+    // validation and the read shapes in one pass (a read out of its pools gets no shape)
+    hipLaunchKernelGGL(read_prep, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag, (int16_t *)p, (uint8_t *)q);
     HIP_TRY(hipGetLastError());
     int bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1773,8 +1968,6 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     if (bad & 2)
       return set_err(GQ_E_ARG, "read set: an offset or length lies outside its pool, or a sample slot >= n_samples");
     unordered = (bad & 4) ? 1 : 0;
-    hipLaunchKernelGGL(read_shape, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int16_t *)p, (uint8_t *)q);
-    HIP_TRY(hipGetLastError());
     if (!unordered) {
       HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->stream));
       const int64_t chunks = (d->d.seq_bytes + 15) / 16;
@@ -2874,17 +3067,18 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
        *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
   HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
   const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(prec_fill, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (ProjRec *)pr);
-  HIP_TRY(hipGetLastError());
-  d->d.prec = (const ProjRec *)pr;
-  // slices a read the projection cannot take touches (pbad)
+  // the records, the slices a read the projection cannot take touches (pbad), the sparse entries
+  // per read and the reads taken, in one pass
   HIP_TRY(d->dp.get(&pbd, (size_t)n_sl + 16));
   HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
-  if (n > 0) {
-    hipLaunchKernelGGL(slice_bad, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                       (const ProjRec *)pr, (uint8_t *)pbd);
-    HIP_TRY(hipGetLastError());
-  }
+  HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
+  unsigned long long *nok = nullptr, hk[kSpread];
+  HIP_TRY(d->dp.get((void **)&nok, sizeof(hk)));
+  HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
+  hipLaunchKernelGGL(proj_prep, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (ProjRec *)pr,
+                     (uint8_t *)pbd, (int64_t *)ne, nok);
+  HIP_TRY(hipGetLastError());
+  d->d.prec = (const ProjRec *)pr;
   // each slice's read window and the offsets of its reads' rows
   HIP_TRY(d->dp.get(&sra, sizeof(int64_t) * (size_t)(n_sl + 1)));
   HIP_TRY(d->dp.get((void **)&scn, sizeof(int64_t) * (size_t)(n_sl + 1)));
@@ -2912,17 +3106,15 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   HIP_TRY(d->dp.get(&sb, sizeof(int64_t) * (size_t)(n_sl + 1)));
   if (n_sl > 0) {
     const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+    static const int first_fit = getenv("GQ_ROWS") && strcmp(getenv("GQ_ROWS"), "firstfit") == 0;  // A/B
     hipLaunchKernelGGL(row_count, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint16_t *)pw,
-                       (int32_t *)sc, (uint8_t *)pbd);
+                       (int32_t *)sc, (uint8_t *)pbd, first_fit);
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(rows64, dim3((unsigned)((n_sl + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, n_sl,
                      (const int32_t *)sc, (int64_t *)br);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
   HIP_TRY(d->dp.get(&eo, sizeof(int64_t) * (size_t)(n + 1)));
-  hipLaunchKernelGGL(proj_count, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (int64_t *)ne);
-  HIP_TRY(hipGetLastError());
   size_t tb = 0, tb2 = 0;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
@@ -2943,11 +3135,33 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   // the pool: rows of 16 words, zero where no piece lies
   const size_t pool_bytes = (size_t)kProjRowBytes * (size_t)tot[0] + 16;
   HIP_TRY(d->dp.get(&pj, pool_bytes));
-  HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
+  const bool cells = fill_pieces();  // the default: every word written, no preset of the pool
+  if (cells) HIP_TRY(hipMemsetAsync((uint8_t *)pj + pool_bytes - 16, 0, 16, c->stream));
+  else HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
   HIP_TRY(d->dp.get(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
-    if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
+    if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(proj_fill_pieces, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj,
+                         fill_dbg());
+      HIP_TRY(hipGetLastError());
+    } else if (cells) {
+      unsigned long long *nd = nullptr;
+      int64_t *dl = nullptr;
+      HIP_TRY(d->dp.get((void **)&nd, sizeof(unsigned long long)));
+      HIP_TRY(d->dp.get((void **)&dl, sizeof(int64_t) * (size_t)n_sl));
+      HIP_TRY(hipMemsetAsync(nd, 0, sizeof(unsigned long long), c->stream));
+      const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(proj_fill_cells, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj,
+                         dl, nd, fill_dbg());
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(proj_fill_deep, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0, c->stream, d->d,
+                         (const int64_t *)dl, (const unsigned long long *)nd, (uint8_t *)pj);
+      HIP_TRY(hipGetLastError());
+      d->dp.put(nd);
+      d->dp.put(dl);
+    } else if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
       const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
       auto kf = fill_u == 4 ? proj_fill<4> : fill_u == 2 ? proj_fill<2> : proj_fill<1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj);
@@ -2976,12 +3190,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   d->d.pev_off = (const int64_t *)eo;
   d->proj_bytes = kProjRowBytes * tot[0];
   d->pev_count = tot[1];
-  if (n > 0) {  // reads the projection takes
-    unsigned long long *nok = nullptr, hk[kSpread];
-    HIP_TRY(d->dp.get((void **)&nok, sizeof(hk)));
-    HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
-    hipLaunchKernelGGL(proj_count_ok, dim3(1024), dim3(kBlock), 0, c->stream, d->d, (const ProjRec *)pr, nok);
-    HIP_TRY(hipGetLastError());
+  {  // reads the projection takes (counted by proj_prep)
     HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->dp.put(nok);

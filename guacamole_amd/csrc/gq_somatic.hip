@@ -1302,15 +1302,22 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
     t->mnb = q;
     HIP_TRY(hipMemsetAsync(q, 0, (size_t)t->n_slices + 16, c->stream));
   }
-  // the words no piece covers: biased zero terms (a rebuild for another filter rewrites only pieces)
-  HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
+  // the words no piece covers: biased zero terms (a rebuild for another filter rewrites only
+  // pieces); the cell fill writes every word itself
+  const bool cells = fill_pieces();
+  if (cells) HIP_TRY(hipMemsetAsync((uint8_t *)t->mproj + 128 * t->n_rows, kMargin8Zero, 32, c->stream));
+  else HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
   void *tab = nullptr;  // margin_term8 by (mapq, quality, match)
   HIP_TRY(t->dp.get(&tab, 256 * 256));
   hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, incl_align ? 1 : 0, (uint8_t *)tab);
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;  // A/B: words per lane and round
-    if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
+    if (cells) {
+      const int64_t blocks = std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(mproj_fill_pieces, dim3((unsigned)blocks), dim3(256), 0, c->stream, t->d, t->n_slices, min_mapq,
+                         (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);
+    } else if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
       auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
                          c->stream, t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,

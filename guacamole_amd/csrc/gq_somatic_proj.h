@@ -326,6 +326,100 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
       });
 }
 
+// ---- The margin projection by pieces (piece_fill in gq_host.h; the default) ----
+struct MarginCell {
+  uint64_t q;       // the word's qualities (loci outside the read zero)
+  uint32_t valid;   // byte mask of its loci inside the read (0: a read the mapq filter drops)
+  uint16_t evb;     // its loci holding an MD event
+  uint16_t mq;      // the read's mapping quality (its table row)
+};
+// The MD-event bits of read r's word at column col (bit k: locus 8 col + k), from its events.
+__device__ __forceinline__ uint32_t word_events(const DevReads &R, int64_t md_off, uint32_t info, int32_t s,
+                                                int32_t col) {
+  const int32_t nmd = (int32_t)(info & 0xFFFFu);
+  const uint32_t *ev = R.md_ev + md_off;
+  const int32_t i0 = 8 * col - s;
+  int k = 0, hi = nmd;
+  while (k < hi) {
+    const int mid = (k + hi) >> 1;
+    if ((int32_t)(ev[mid] >> 8) < i0) k = mid + 1;
+    else hi = mid;
+  }
+  uint32_t evb = 0;
+  for (; k < nmd; ++k) {
+    const int32_t i = (int32_t)(ev[k] >> 8) - i0;
+    if (i >= 8) break;
+    evb |= 1u << i;
+  }
+  return evb;
+}
+
+// The tumor's margin projection (a biased byte per locus-read, 128 B per row) slice by slice
+// (piece_fill in gq_host.h): a wave per slice, a lane per piece, the rows built in LDS and written
+// whole (kMargin8Zero where no element of a kept read lies: no preset).  mnb[slot] = 1 where a
+// word holds a kMargin8None term.
+__global__ __launch_bounds__(256) void mproj_fill_pieces(DevReads R, int64_t n_slices, int min_mapq,
+                                                         const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
+                                                         uint8_t *__restrict__ mnb) {
+  __shared__ uint2 s_rows[4][kPieceRows * kPieceStride];
+  __shared__ uint32_t s_row[4][64];  // the table row of one mapping quality (256 bytes)
+  const int wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const uint8_t *lrow = reinterpret_cast<const uint8_t *>(s_row[wv]);
+  uint32_t lmq = 0;  // most reads share one mapping quality: its row (the wave's first slice's first read)
+  {
+    const int64_t slot = wave_id();
+    if (slot < n_slices) {
+      const int64_t ra = R.sra[slot];
+      lmq = ra < R.n_reads ? (uint32_t)R.mapq[ra] : 0u;
+    }
+    s_row[wv][lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  const uint2 zero = make_uint2(0x80808080u, 0x80808080u);
+  piece_fill<uint2, MarginCell, true>(
+      R, n_slices, s_rows[wv], reinterpret_cast<uint2 *>(mproj), zero,
+      [&](const PieceRec &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); },
+      [&](const PieceRec &m, int32_t col, MarginCell &x) {
+        const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
+        if (!(m.info & kColEligible) || nmd > 4) return false;
+        const int32_t lb = 8 * col;
+        const int64_t a = m.p0 + lb;
+        if (a < 0 || a + 8 > R.seq_cap) return false;
+        const int32_t lo = min(max(m.s - lb, 0), 8), hi = min(max(m.e - lb, 0), 8);
+        x.q = *reinterpret_cast<const gq_u64m *>(R.qual + a) & edge_mask(lo, hi);
+        x.valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+        const int32_t i0 = lb - m.s;
+        uint32_t evb = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // (the piece's events came with its record)
+          const uint32_t i = (uint32_t)((int32_t)(m.ev[k] >> 8) - i0);
+          evb |= (m.ev[k] != 0xFFFFFFFFu && i < 8u) ? 1u << i : 0u;
+        }
+        x.evb = (uint16_t)evb;
+        x.mq = (uint16_t)m.mq;
+        return true;
+      },
+      [&](const PieceRec &, int32_t, const MarginCell &x) {  // terms from the LDS row or the mapq's global row
+        return x.mq == lmq ? margin_terms8_lds(x.q, x.valid, x.evb, lrow)
+                           : margin_terms8_lds(x.q, x.valid, x.evb, tab + ((uint32_t)x.mq << 8));
+      },
+      [&](const PieceRec &m, int64_t r, int32_t col) {
+        const PieceMeta pm = piece_rec_meta(m);
+        const uint32_t evb = word_events(R, m.md_off, m.info, m.s, col);
+        const MarginRaw x = margin_fetch(R, r, pm, col, evb, tab);
+        return x.gen ? x.word : margin_terms8(pm, x.q, x.valid, evb, tab);
+      },
+      [](uint2 w) {  // a kMargin8None (zero) byte
+        auto z = [](uint32_t v) { return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u; };
+        return z(w.x) || z(w.y);
+      },
+      [&](int64_t slot, bool none) {
+        if (lane == 0) mnb[slot] = none ? 1 : 0;
+      });
+}
+
 // The projection and the margin projection of one read set in one read-major pass (the
 // projection derived for a caller that also reads the margin projection): one batch setup per 64
 // reads, each word's bases and qualities loaded together; margin words only for reads the mapq

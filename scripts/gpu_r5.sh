@@ -9,15 +9,11 @@ if [ $# -gt 0 ]; then
   timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu "$@" > gpurun_out/${TAG}_tests.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${TAG}_tests.log; stop $rc
 fi
-B="--steps 10 --warmup 3 --somatic-length 0 --panel-length 0 --no-single-pass --no-cpu-baseline"
+B="--steps 10 --warmup 3 --somatic-length 0 --panel-length 0 --no-single-pass --no-cpu-baseline --no-configs3 ${BENCH_ARGS}"
 timeout -k 10 300 python -u bench.py $B > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "bench rc=$rc"; stop $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py $B > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; stop $rc
 f=$(find gpurun_out/${TAG}_prof -name run_kernel_stats.csv | head -1)
 cp $f gpurun_out/${TAG}_kernel_stats.csv
-python3 - gpurun_out/${TAG}_kernel_stats.csv <<'PY'
-import csv, sys
-for row in csv.DictReader(open(sys.argv[1])):
-    print("%-50s calls %4s avg_us %9.1f tot_ms %8.2f" % (row["Name"][:50], row["Calls"], float(row["AverageNs"]) / 1e3, float(row["TotalDurationNs"]) / 1e6))
-PY
+python3 scripts/ktrace_median.py gpurun_out/${TAG}_prof | head -${KTOP:-30}

@@ -4,8 +4,8 @@ GQ_CALL_SPLIT=1 (somatic caller as a front kernel + back end over stored element
 GQ_CALL_WPE=2 (the one-kernel caller at 2 waves per SIMD), GQ_FILL_U=2 / 4 (the read-major
 projection and margin fills at 2 or 4 words per lane and round; GQ_FILL_W: 2 or 4 consecutive
 words of a read per lane), GQ_FILL_ONE=1 (the projection and the margin projection in one pass
-instead of two), GQ_FILL=slice (the slice-major
-fills).  A synthetic 300 kb 60x / 30x pair with a raised somatic
+instead of two) — each with GQ_FILL=rw (the read-major fills), GQ_FILL=slice (the slice-major
+fills), GQ_ROWS=firstfit (first-fit row assignment instead of the parallel earliest-freed one).  A synthetic 300 kb 60x / 30x pair with a raised somatic
 rate, so hundreds of candidates and calls reach every path."""
 import json
 import os
@@ -29,8 +29,9 @@ def _run(extra):
 def test_kernel_variants_give_the_default_records():
     base = _run({})
     assert base["somatic"] > 20 and base["germline"] > 100
-    for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, {"GQ_FILL_U": "2"}, {"GQ_FILL_U": "4"}, {"GQ_FILL_W": "2"},
-                  {"GQ_FILL_W": "4"}, {"GQ_FILL_ONE": "1"},
-                  {"GQ_FILL": "slice"}):
+    rw = {"GQ_FILL": "rw"}
+    for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, rw, dict(rw, GQ_FILL_U="2"), dict(rw, GQ_FILL_U="4"),
+                  dict(rw, GQ_FILL_W="2"), dict(rw, GQ_FILL_W="4"), dict(rw, GQ_FILL_ONE="1"), {"GQ_FILL": "slice"},
+                  {"GQ_ROWS": "firstfit"}):
         got = _run(extra)
         assert got == base, (extra, got, base)
