@@ -112,7 +112,7 @@ def main() -> int:
     ap.add_argument("--no-configs3", dest="configs3", action="store_false",
                     help="skip the configs[3] rank share (one rank's share of the 30x b37 genome through the "
                          "multi-GPU ingest path, on this GPU)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r04.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
@@ -211,7 +211,7 @@ def main() -> int:
     for _ in range(args.warmup):
         step()
     barrier()
-    pileup_ms, walk_ms, step_ms, derive_ms, proj_ms = [], [], [], [], []
+    pileup_ms, walk_ms, step_ms, derive_ms, proj_ms, fill_ms, dev_ms, dev_parts = [], [], [], [], [], [], [], []
     stage_ms = {"plan_ms": [], "complex_ms": [], "finalize_ms": []}
     walk_frac = []
     t = time.perf_counter()
@@ -229,6 +229,9 @@ def main() -> int:
         sti = ctx.proj_stats(reads)
         derive_ms.append(sti["derive_ms"])
         proj_ms.append(sti["proj_ms"])
+        fill_ms.append(sti["fill_ms"])
+        dev_parts.append((sti["derive_dev_ms"], sti["proj_dev_ms"], tm["total_ms"]))
+        dev_ms.append(sum(dev_parts[-1]))
     barrier()
     elapsed = time.perf_counter() - t
     # the re-derived pass gives the records of the first call on the freshly uploaded set
@@ -283,14 +286,24 @@ def main() -> int:
     b_alg = int(b_all * kept)
     k_ms = float(np.mean(pileup_ms))
     achieved = b_alg / (k_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        with open(args.traffic) as fh:
-            tr = json.load(fh)
-        if tr.get("length") == args.length and tr.get("depth") == args.depth and world == 1:
-            traffic = tr.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    def pmc_traffic(kernel: str):
+        """HBM bytes per launch of `kernel` from the PMC file (its own --pmc passes), or None."""
+        try:
+            with open(args.traffic) as fh:
+                tr = json.load(fh)
+        except (OSError, ValueError):
+            return None
+        if tr.get("length") != args.length or tr.get("depth") != args.depth or world != 1:
+            return None
+        return tr.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    traffic = pmc_traffic("germline_proj")
+    # the step's dominant kernel: the projection fill (read-major fill under GQ_FILL=rw).  Its
+    # algorithmic bytes: each projected read's bases over its span read once (sum of end - start)
+    # + the pool it writes (every word of every row: the layout the call reads).
+    elements = int((a["end"].astype(np.int64) - a["start"].astype(np.int64)).sum())
+    f_ms = float(np.median(fill_ms))
+    b_fill = elements + int(st["proj_bytes"])
+    f_traffic = pmc_traffic("proj_fill_cells")
 
     line = {
         "metric": "pileup loci/sec at 30x WGS; achieved HBM GB/s vs roofline",
@@ -308,14 +321,34 @@ def main() -> int:
         "config": {"workload": workload, "genome_loci": genome_loci, "visited_loci_per_gpu": visited,
                    "reads_per_gpu": n_reads, "contigs_per_gpu": len(g.contig_names), "depth": args.depth,
                    "read_len": 150, "threshold": args.threshold, "parallelism": "loci-sharded x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     # the bus rate: measured HBM bytes (PMC) / the kernel's time / peak
-                     "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
-                     "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
+        "roofline": {"bound": "hbm", "achieved": b_fill / (f_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": b_fill / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": f_traffic,
+                     "dram_frac": None if f_traffic is None else f_traffic / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel": os.environ.get("GQ_FILL", "cells") == "cells" and "proj_fill_cells" or
+                               "projection fill (GQ_FILL=%s)" % os.environ.get("GQ_FILL"),
+                     "kernel_ms": f_ms, "algorithmic_bytes_per_launch": b_fill,
+                     "basis": "bases over the projected reads' spans (sum end - start: %d) + the projection pool "
+                              "written (%d B); kernel_ms: median of the steps' HIP-event times on the context's "
+                              "stream" % (elements, int(st["proj_bytes"]))},
+        # the resident call's pileup kernel (the round-4 headline kernel)
+        "call_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                          # the bus rate: measured HBM bytes (PMC) / the kernel's time / peak
+                          "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
+                          "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
+        # the whole step on SURVEY §8(d)'s basis (bases, 16 B per read, CIGAR ops, MD events, output)
+        "step_roofline": {"algorithmic_bytes": b_all, "step_ms": float(np.median(step_ms)),
+                          "device_ms": float(np.median(dev_ms)),
+                          "achieved": b_all / (float(np.median(step_ms)) * 1e-3) / 1e9, "unit": "GB/s",
+                          "frac": b_all / (float(np.median(step_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "step_ms_median": float(np.median(step_ms)),
-        "step_stages_ms": {"upload_derive_ms": float(np.median(derive_ms)), "projection_ms": float(np.median(proj_ms))},
+        # wall times of the step's parts (host-side, each ending in a synchronisation) and their
+        # device spans (HIP events on the context's stream: first kernel to last)
+        "step_stages_ms": {"upload_derive_ms": float(np.median(derive_ms)), "projection_ms": float(np.median(proj_ms)),
+                           "upload_derive_device_ms": float(np.median([x[0] for x in dev_parts])),
+                           "projection_device_ms": float(np.median([x[1] for x in dev_parts])),
+                           "call_device_ms": float(np.median([x[2] for x in dev_parts])), "fill_ms": f_ms},
         "rederive_identical": rederive_identical,
         "resident_step_ms": float(np.median(res_ms)),
         "resident_step_loci_per_s": visited / (float(np.median(res_ms)) * 1e-3),

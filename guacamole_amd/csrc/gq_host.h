@@ -678,7 +678,11 @@ __device__ __forceinline__ ProjRaw proj_fetch(const DevReads &R, int64_t r, cons
   return x;
 }
 
-// ---- Piece fills: a wave per slice, a lane per piece, rows built in LDS (the default) ----
+// The cell fills' record offset of a read whose bytes are not in the window's byte run (a
+// wrapped pool in another order, or past 2 GiB of it): its cells take the slow path.
+constexpr uint32_t kCell3Far = 0x80000000u;
+
+// ---- Piece fills: a wave per slice, a lane per piece, rows built in LDS (A/B: GQ_FILL=pieces) ----
 // A wave takes a slice: each lane takes one of its window reads and, if the read has a piece in
 // the slice, issues the loads of all the piece's words at once (up to 16 columns), turns them into
 // words and writes them into the slice's rows in LDS (kPieceRows rows at a time, padded to 17
@@ -1100,6 +1104,7 @@ struct gq_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
+  hipEvent_t dev_ev[4] = {};  // the derivation's device spans (gq_reads_info: derive / projection / fill)
   gq_timings timings{};
   int germ_tile = gq::kGermT;
   int n_cu = 0;
@@ -1207,6 +1212,9 @@ struct gq_dev_reads {
   bool projected = false;          // the projection is derived (ensure_projection)
   void *nnb = nullptr;             // N bases per read (pool_clean), for the projection's sparse entries
   float proj_ms = 0;               // ensure_projection's wall time
+  float fill_ms = 0;               // its pool fill kernel(s), HIP events on the context's stream
+  float proj_dev_ms = 0;           // its device span (first kernel to last), HIP events
+  float derive_dev_ms = 0;         // the upload-time derivation's device span, HIP events
   mutable void *mproj = nullptr;  // somatic margin projection (a biased byte per locus-read), for mproj_mapq
   mutable int mproj_mapq = -1;
   mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMargin8None (no bound)

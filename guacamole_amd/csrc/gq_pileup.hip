@@ -483,9 +483,9 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
     uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * g0;
     const SliceWin W = slice_stored(R, slot);
     const int32_t nwin = (int32_t)(W.rz - W.ra);
-    if (R.pbad[slot] || nwin > kCell3Win) {
+    if (R.pbad[slot] || nwin > kCell3Win || nwin <= 0) {
       for (int32_t c = lane; c < 16 * nr; c += 64) out[c] = 0u;
-      if (!R.pbad[slot] && lane == 0) deep[atomicAdd(n_deep, 1ull)] = slot;
+      if (!R.pbad[slot] && nwin > kCell3Win && lane == 0) deep[atomicAdd(n_deep, 1ull)] = slot;
       continue;
     }
     const int64_t base = R.seq_off[W.ra];  // the window's bytes: [base, ...) in read order
@@ -500,8 +500,11 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
       const int64_t so = R.seq_off[r];
       const ProjRec pr = R.prec[r];
       const int32_t row = prw[i];
+      // a read whose bytes do not follow the window's first read's (a wrapped pool in another
+      // order) takes the slow path: a = kCell3Far
+      const int64_t av = so + (ld > 0 ? ld : 0) - base;
       Cell3Rec m;
-      m.a = (uint32_t)(so + (ld > 0 ? ld : 0) - base);
+      m.a = R.pool_ordered && av >= 0 && av < (int64_t)kCell3Far ? (uint32_t)av : kCell3Far;
       m.s = d.start;
       m.e = d.end;
       m.info = d.info;
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
             const Cell3Rec m = rec[pp[u]];
             const int32_t lb = 8 * (W.qc0 + (c & 15));
             const int64_t v = (int64_t)m.a + lb - m.s;
-            if (!(m.info & kColEligible) || v < 0 || v + 8 > span) {
+            if (!(m.info & kColEligible) || m.a == kCell3Far || v < 0 || v + 8 > span) {
               slow |= 1u << u;
             } else if (dbg & 1) {  // ablation: no loads
               b[u] = (uint64_t)v;
@@ -571,15 +574,17 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
             const int32_t c = c00 + 64 * u + lane;
             const uint32_t p = map[c];
             const Cell3Rec m = rec[p];
+            const int64_t r = W.ra + p;
+            const int32_t ld = R.lead[r];
             PieceMeta pm;
-            pm.p0 = base + m.a - m.s;
+            pm.p0 = R.seq_off[r] + (ld > 0 ? ld : 0) - m.s;  // (from the read itself: any pool order)
             pm.s = m.s;
             pm.e = m.e;
             pm.s0 = 0;
             pm.row = 0;
             pm.info = m.info;
             pm.mq = 0;
-            const ProjRaw x = proj_fetch(R, W.ra + p, pm, W.qc0 + (c & 15));
+            const ProjRaw x = proj_fetch(R, r, pm, W.qc0 + (c & 15));
             o[c] = x.gen ? x.word : proj_codes4((uint32_t)x.b) | (proj_codes4((uint32_t)(x.b >> 32)) << 4);
           }
         }
@@ -1868,6 +1873,7 @@ gq_status gq_open(int device, gq_ctx **out) {
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  for (auto &e : c->dev_ev) HIP_TRY(hipEventCreate(&e));
   // the staging chunks first (a load may wait on them), then the code objects
   c->prep = std::thread([c] {
     hipError_t e = hipSetDevice(c->device);
@@ -1907,6 +1913,7 @@ void gq_close(gq_ctx *c) {
                     &c->heap_off, &c->heap_reads, &c->win_meta, &c->win_grp, &c->bkt})
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
+  for (auto &e : c->dev_ev) (void)hipEventDestroy(e);
   if (c->pin) (void)hipHostFree(c->pin);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1934,6 +1941,7 @@ static gq_status validate_reads(const gq_reads *h) {
 }
 
 static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
+  HIP_TRY(hipEventRecord(c->dev_ev[2], c->stream));
   {  // contig_read_begin: 0, non-decreasing, n_reads (host copy)
     const auto &b = d->contig_read_begin;
     bool ok = !b.empty() && b.front() == 0 && b.back() == d->d.n_reads;
@@ -2048,7 +2056,9 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   }
   d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
   nnb = nullptr;
+  HIP_TRY(hipEventRecord(c->dev_ev[3], c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&d->derive_dev_ms, c->dev_ev[2], c->dev_ev[3]);
   d->d.pool_ordered = unordered ? 0 : 1;
   return GQ_OK;
 }
@@ -2306,6 +2316,9 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
   out->n_samples = d->d.n_samples;
   out->proj_ms = d->proj_ms;
   out->projected = d->projected ? 1 : 0;
+  out->fill_ms = d->fill_ms;
+  out->proj_dev_ms = d->proj_dev_ms;
+  out->derive_dev_ms = d->derive_dev_ms;
   return GQ_OK;
 }
 
@@ -3066,6 +3079,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   void *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
        *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
   HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
+  HIP_TRY(hipEventRecord(c->dev_ev[2], c->stream));
   const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
   // the records, the slices a read the projection cannot take touches (pbad), the sparse entries
   // per read and the reads taken, in one pass
@@ -3139,6 +3153,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   if (cells) HIP_TRY(hipMemsetAsync((uint8_t *)pj + pool_bytes - 16, 0, 16, c->stream));
   else HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
   HIP_TRY(d->dp.get(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
+  HIP_TRY(hipEventRecord(c->dev_ev[0], c->stream));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
     if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
@@ -3180,11 +3195,13 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     }
     HIP_TRY(hipGetLastError());
   }
+  HIP_TRY(hipEventRecord(c->dev_ev[1], c->stream));
   if (n > 0) {
     hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
                        (const int64_t *)eo, (uint2 *)pe);
     HIP_TRY(hipGetLastError());
   }
+  HIP_TRY(hipEventRecord(c->dev_ev[3], c->stream));
   d->d.proj = (const uint8_t *)pj;
   d->d.pev = (const uint2 *)pe;
   d->d.pev_off = (const int64_t *)eo;
@@ -3198,6 +3215,8 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&d->fill_ms, c->dev_ev[0], c->dev_ev[1]);
+  (void)hipEventElapsedTime(&d->proj_dev_ms, c->dev_ev[2], c->dev_ev[3]);
   d->projected = true;
   d->proj_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GQ_OK;

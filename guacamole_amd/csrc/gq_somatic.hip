@@ -1313,10 +1313,25 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;  // A/B: words per lane and round
-    if (cells) {
+    if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
       const int64_t blocks = std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20);
       hipLaunchKernelGGL(mproj_fill_pieces, dim3((unsigned)blocks), dim3(256), 0, c->stream, t->d, t->n_slices, min_mapq,
                          (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);
+    } else if (cells) {
+      unsigned long long *nd = nullptr;
+      int64_t *dl = nullptr;
+      HIP_TRY(t->dp.get((void **)&nd, sizeof(unsigned long long)));
+      HIP_TRY(t->dp.get((void **)&dl, sizeof(int64_t) * (size_t)t->n_slices));
+      HIP_TRY(hipMemsetAsync(nd, 0, sizeof(unsigned long long), c->stream));
+      const int64_t blocks = std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20);
+      hipLaunchKernelGGL(mproj_fill_cells, dim3((unsigned)blocks), dim3(256), 0, c->stream, t->d, t->n_slices, min_mapq,
+                         (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb, dl, nd);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(mproj_fill_deep, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0, c->stream, t->d,
+                         (const int64_t *)dl, (const unsigned long long *)nd, min_mapq, (const uint8_t *)tab,
+                         (uint8_t *)t->mproj, (uint8_t *)t->mnb);
+      t->dp.put(nd);
+      t->dp.put(dl);
     } else if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
       auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,

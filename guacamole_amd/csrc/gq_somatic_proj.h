@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, c
       });
 }
 
-// ---- The margin projection by pieces (piece_fill in gq_host.h; the default) ----
+// ---- The margin projection by pieces (piece_fill in gq_host.h; A/B: GQ_FILL=pieces) ----
 struct MarginCell {
   uint64_t q;       // the word's qualities (loci outside the read zero)
   uint32_t valid;   // byte mask of its loci inside the read (0: a read the mapq filter drops)
@@ -352,6 +352,224 @@ __device__ __forceinline__ uint32_t word_events(const DevReads &R, int64_t md_of
     evb |= 1u << i;
   }
   return evb;
+}
+
+// ---- The margin projection by cells (the default; the projection's proj_fill_cells design) ----
+// A wave per slice, a lane per cell: 32-byte window records in LDS (pool offset,
+// [start, end), ColDesc info, mapping quality, up to four MD-event offsets), a u8 map cell ->
+// window read, then per cell one 8-byte load of its qualities and eight table lookups in the
+// LDS row of the wave's common mapping quality.  Every word written (kMargin8Zero where no kept
+// element lies), 64 consecutive words per store; mnb[slot] = 1 where a word holds kMargin8None.
+struct __attribute__((aligned(16))) MCellRec {
+  uint32_t a;         // seq_off + leading clip - seq_off[window's first read]
+  int32_t s, e;       // [start, end)
+  uint32_t info;      // ColDesc info
+  uint32_t mq;        // mapping quality; bit 8: dropped by the mapq filter; bit 9: events not below
+  uint32_t ev01, ev23;  // up to four MD-event offsets from s, 16 bits each (0xFFFF: none)
+  uint32_t pad;
+};
+__global__ __launch_bounds__(256) void mproj_fill_cells(DevReads R, int64_t n_slices, int min_mapq,
+                                                        const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
+                                                        uint8_t *__restrict__ mnb, int64_t *__restrict__ deep,
+                                                        unsigned long long *__restrict__ n_deep) {
+  constexpr int kWin = 255, kRows = 64;
+  __shared__ MCellRec s_rec[4][kWin];
+  __shared__ uint8_t s_map[4][kRows * 16];
+  __shared__ uint32_t s_row[4][64];  // the table row of one mapping quality (256 bytes)
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  MCellRec *rec = s_rec[wv];
+  uint8_t *map = s_map[wv];
+  const uint8_t *lrow = reinterpret_cast<const uint8_t *>(s_row[wv]);
+  uint32_t lmq = 0;  // most reads share one mapping quality: its row (the wave's first slice's first read)
+  {
+    const int64_t slot = wave_id();
+    if (slot < n_slices) {
+      const int64_t ra = R.sra[slot];
+      lmq = ra < R.n_reads ? (uint32_t)R.mapq[ra] : 0u;
+    }
+    s_row[wv][lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  const uint2 zero = make_uint2(0x80808080u, 0x80808080u);
+  auto has_none = [](uint2 w) {  // a kMargin8None (zero) byte
+    auto z = [](uint32_t v) { return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u; };
+    return z(w.x) || z(w.y);
+  };
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t slot = wave_id(); slot < n_slices; slot += nw) {
+    const int64_t g0 = R.srow[slot];
+    const int32_t nr = (int32_t)(R.srow[slot + 1] - g0);
+    if (nr <= 0) continue;
+    uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * g0;
+    const SliceWin W = slice_stored(R, slot);
+    const int32_t nwin = (int32_t)(W.rz - W.ra);
+    if (R.pbad[slot] || nwin > kWin || nwin <= 0) {
+      for (int32_t c = lane; c < 16 * nr; c += 64) out[c] = zero;
+      if (!R.pbad[slot] && nwin > kWin && lane == 0) deep[atomicAdd(n_deep, 1ull)] = slot;
+      continue;
+    }
+    const int64_t base = R.seq_off[W.ra];
+    const uint8_t *pool = R.qual + base;
+    const int64_t span = R.seq_cap - base;
+    const uint16_t *prw = R.prow + R.soff[slot];
+    for (int32_t i = lane; i < nwin; i += 64) {
+      const int64_t r = W.ra + i;
+      const ColDesc d = R.cdesc[r];
+      const int32_t ld = R.lead[r];
+      const int64_t so = R.seq_off[r];
+      const uint32_t mq = R.mapq[r];
+      const int64_t mo = R.md_off[r];
+      const int64_t av = so + (ld > 0 ? ld : 0) - base;  // (off the window's byte run: the slow path)
+      MCellRec m;
+      m.a = R.pool_ordered && av >= 0 && av < (int64_t)kCell3Far ? (uint32_t)av : kCell3Far;
+      m.s = d.start;
+      m.e = d.end;
+      m.info = d.info;
+      m.mq = mq | (min_mapq > 0 && (int)mq < min_mapq ? 0x100u : 0u);
+      const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
+      uint32_t v[4];
+      bool in = nmd <= 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = q < nmd && in ? R.md_ev[mo + q] >> 8 : 0xFFFFu;
+        in = in && v[q] <= 0xFFFFu && (q >= nmd || v[q] < 0xFFFFu);
+      }
+      m.ev01 = (v[0] & 0xFFFFu) | (v[1] << 16);
+      m.ev23 = (v[2] & 0xFFFFu) | (v[3] << 16);
+      if (!in) m.mq |= 0x200u;
+      m.pad = 0;
+      rec[i] = m;
+    }
+    bool none = false;
+    for (int32_t k0 = 0; k0 < nr; k0 += kRows) {
+      const int32_t nk = nr - k0 < kRows ? nr - k0 : kRows;
+      for (int32_t c = lane; c < 16 * nk; c += 64) map[c] = 0xFFu;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (int32_t i = lane; i < nwin; i += 64) {
+        const int32_t row = prw[i];
+        int32_t s0, sl;
+        piece_of(R.prec[W.ra + i], W.qc0, s0, sl);
+        if (row == 0xFFFF || sl <= 0 || row < k0 || row >= k0 + nk) continue;
+        uint8_t *mp = map + 16 * (row - k0) + (s0 - W.qc0);
+        for (int32_t j = 0; j < sl; ++j) mp[j] = (uint8_t)i;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      uint2 *o = out + 16 * k0;
+      for (int32_t c00 = 0; c00 < 16 * nk; c00 += 256) {  // four cells per lane, their loads together
+        uint64_t q[4];
+        uint32_t valid[4], evb[4], mqs[4];
+        uint32_t slow = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t c = c00 + 64 * u + lane;
+          const uint32_t p = c < 16 * nk ? map[c] : 0xFFu;
+          q[u] = 0;
+          valid[u] = 0;
+          evb[u] = 0;
+          mqs[u] = lmq;
+          if (p == 0xFFu) continue;
+          const MCellRec m = rec[p];
+          if (m.mq & 0x100u) continue;  // dropped by the mapq filter: no element
+          const int32_t lb = 8 * (W.qc0 + (c & 15));
+          const int64_t v = (int64_t)m.a + lb - m.s;
+          if (!(m.info & kColEligible) || (m.mq & 0x200u) || m.a == kCell3Far || v < 0 || v + 8 > span) {
+            slow |= 1u << u;
+            continue;
+          }
+          const int32_t lo = min(max(m.s - lb, 0), 8), hi = min(max(m.e - lb, 0), 8);
+          q[u] = *reinterpret_cast<const gq_u64m *>(pool + (uint32_t)v);
+          if (lo > 0 || hi < 8) q[u] &= edge_mask(lo, hi);
+          valid[u] = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+          const int32_t i0 = lb - m.s;
+          uint32_t eb = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t off = ((k < 2 ? m.ev01 : m.ev23) >> (16 * (k & 1))) & 0xFFFFu;
+            const uint32_t ii = (uint32_t)((int32_t)off - i0);
+            eb |= (off != 0xFFFFu && ii < 8u) ? 1u << ii : 0u;
+          }
+          evb[u] = eb;
+          mqs[u] = m.mq & 0xFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t c = c00 + 64 * u + lane;
+          if (c >= 16 * nk || ((slow >> u) & 1u)) continue;
+          uint2 w = zero;
+          if (valid[u])
+            w = mqs[u] == lmq ? margin_terms8_lds(q[u], valid[u], evb[u], lrow)
+                              : margin_terms8_lds(q[u], valid[u], evb[u], tab + (mqs[u] << 8));
+          o[c] = w;
+          none = none || has_none(w);
+        }
+        if (slow) {  // rare: a general CIGAR, more than four MD events, a word at the pool's end
+#pragma unroll 1
+          for (int u = 0; u < 4; ++u) {
+            if (!((slow >> u) & 1u)) continue;
+            const int32_t c = c00 + 64 * u + lane;
+            const uint32_t p = map[c];
+            const MCellRec m = rec[p];
+            const int64_t r = W.ra + p;
+            const int32_t ld = R.lead[r];
+            PieceMeta pm;
+            pm.p0 = R.seq_off[r] + (ld > 0 ? ld : 0) - m.s;  // (from the read itself: any pool order)
+            pm.s = m.s;
+            pm.e = m.e;
+            pm.s0 = 0;
+            pm.row = 0;
+            pm.info = m.info;
+            pm.mq = m.mq & 0xFFu;
+            const int32_t col = W.qc0 + (c & 15);
+            const uint32_t eb = word_events(R, R.md_off[r], m.info, m.s, col);
+            const MarginRaw x = margin_fetch(R, r, pm, col, eb, tab);
+            const uint2 w = x.gen ? x.word : margin_terms8(pm, x.q, x.valid, eb, tab);
+            o[c] = w;
+            none = none || has_none(w);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the map)
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    const bool any = __ballot(none) != 0;
+    if (lane == 0) mnb[slot] = any ? 1 : 0;
+  }
+}
+
+// The listed (deep) slices' margin words, slice-major (their rows preset to kMargin8Zero by
+// mproj_fill_cells).
+__global__ __launch_bounds__(256) void mproj_fill_deep(DevReads R, const int64_t *__restrict__ deep,
+                                                       const unsigned long long *__restrict__ n_deep, int min_mapq,
+                                                       const uint8_t *__restrict__ tab, uint8_t *__restrict__ mproj,
+                                                       uint8_t *__restrict__ mnb) {
+  __shared__ PieceMeta s_meta[4][64];
+  __shared__ uint32_t s_owner[4][64];
+  PieceMeta *meta = s_meta[threadIdx.x >> 6];
+  uint32_t *owner = s_owner[threadIdx.x >> 6];
+  const int64_t nd = (int64_t)*n_deep;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave_id(); i < nd; i += nw) {
+    const int64_t slot = deep[i];
+    uint2 *out = reinterpret_cast<uint2 *>(mproj) + 16 * R.srow[slot];
+    bool none = false;
+    slice_fill<true, 1>(
+        R, slice_stored(R, slot), R.prow + R.soff[slot], meta, owner,
+        [&](int64_t, PieceMeta &m, int64_t mdo) { return margin_setup(R, min_mapq, mdo, m); },
+        [&](int64_t r, const PieceMeta &m, int32_t col, uint32_t evb) { return margin_fetch(R, r, m, col, evb, tab); },
+        [&](bool act, const MarginRaw &x, int64_t, const PieceMeta &m, int32_t col, uint32_t evb) {
+          if (act) {
+            const uint2 w = x.gen ? x.word : margin_terms8(m, x.q, x.valid, evb, tab);
+            out[16 * (int64_t)m.row + (col & 15)] = w;
+            auto has = [](uint32_t v) { return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u; };
+            none = none || has(w.x) || has(w.y);
+          }
+        });
+    const bool any = __ballot(none) != 0;
+    if ((threadIdx.x & 63) == 0) mnb[slot] = any ? 1 : 0;
+  }
 }
 
 // The tumor's margin projection (a biased byte per locus-read, 128 B per row) slice by slice

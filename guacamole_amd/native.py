@@ -102,7 +102,8 @@ class gq_timings(C.Structure):
 class gq_reads_info(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("n_reads", "seq_bytes", "proj_bytes", "pev_count", "proj_reads", "n_rows")] + [
         ("h2d_ms", C.c_float), ("derive_ms", C.c_float), ("cigar_len", C.c_int64), ("md_len", C.c_int64),
-        ("n_contigs", C.c_int32), ("n_samples", C.c_int32), ("proj_ms", C.c_float), ("projected", C.c_int32)]
+        ("n_contigs", C.c_int32), ("n_samples", C.c_int32), ("proj_ms", C.c_float), ("projected", C.c_int32),
+        ("fill_ms", C.c_float), ("proj_dev_ms", C.c_float), ("derive_dev_ms", C.c_float)]
 
 
 class gq_somatic_params(C.Structure):

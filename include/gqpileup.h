@@ -220,6 +220,9 @@ typedef struct gq_reads_info {
   int32_t n_contigs, n_samples;
   float proj_ms;     /* the projection, derived on the first call that reads it (0: not yet) */
   int32_t projected; /* 1 once it is: the proj_* / n_rows / pev_count sizes above are then set */
+  float fill_ms;       /* its pool fill kernel(s) (HIP events on the context's stream) */
+  float proj_dev_ms;   /* its device span, first kernel to last (HIP events) */
+  float derive_dev_ms; /* the upload-time derivation's device span (HIP events) */
 } gq_reads_info;
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
