@@ -1105,6 +1105,10 @@ struct gq_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
   hipEvent_t dev_ev[4] = {};  // the derivation's device spans (gq_reads_info: derive / projection / fill)
+  // a second stream for derivation kernels independent of the main stream's (the pool scan beside
+  // the read checks, the sparse entries beside the projection fill), joined by side_ev
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[4] = {};
   gq_timings timings{};
   int germ_tile = gq::kGermT;
   int n_cu = 0;

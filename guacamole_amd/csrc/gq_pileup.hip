@@ -340,6 +340,7 @@ __global__ void slice_windows(DevReads R, int64_t n_slices, int64_t *__restrict_
 // The projection's per-read records in one pass (thread per read, record n: zeros): ProjRec
 // (prec_fill), the pbad slices of the reads the projection cannot take (slice_bad), the sparse
 // entries per read (proj_count) and the reads it takes, counted into kSpread words (proj_count_ok).
+constexpr int kOkSpread = 1024;  // proj_prep's count words (summed on the host)
 __global__ void proj_prep(DevReads R, const uint32_t *__restrict__ n_nbase, ProjRec *__restrict__ prec,
                           uint8_t *__restrict__ pbad, int64_t *__restrict__ nents, unsigned long long *__restrict__ n_ok) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -376,8 +377,14 @@ __global__ void proj_prep(DevReads R, const uint32_t *__restrict__ n_nbase, Proj
     prec[r] = p;
     nents[r] = e;
   }
+  // the block's count: one LDS add per wave, one global add per block, spread over kOkSpread words
+  __shared__ unsigned long long s_ok;
+  if (threadIdx.x == 0) s_ok = 0;
+  __syncthreads();
   const unsigned long long k = (unsigned long long)__popcll(__ballot(ok));
-  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&n_ok[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kSpread - 1)], k);
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&s_ok, k);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_ok) atomicAdd(&n_ok[blockIdx.x & (kOkSpread - 1)], s_ok);
 }
 
 // Rows of each slice and each of its reads' row (slice_assign_rows, one wave per slice); past
@@ -1872,8 +1879,10 @@ gq_status gq_open(int device, gq_ctx **out) {
   gq_ctx *c = new gq_ctx();
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
   for (auto &e : c->dev_ev) HIP_TRY(hipEventCreate(&e));
+  for (auto &e : c->side_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // the staging chunks first (a load may wait on them), then the code objects
   c->prep = std::thread([c] {
     hipError_t e = hipSetDevice(c->device);
@@ -1914,6 +1923,11 @@ void gq_close(gq_ctx *c) {
     b->release();
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   for (auto &e : c->dev_ev) (void)hipEventDestroy(e);
+  for (auto &e : c->side_ev) (void)hipEventDestroy(e);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
   if (c->pin) (void)hipHostFree(c->pin);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1959,83 +1973,56 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   void *nnb = nullptr;  // N bytes per read (pool_clean / read_clean), for the projection entries
   HIP_TRY(d->dp.get((void **)&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
   HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1), c->stream));
+  const int nc = d->d.n_contigs;
+  std::vector<int32_t> last((size_t)nc, 0);  // each contig's largest read end (pmax_end of its last read)
   if (d->d.n_reads > 0) {
     void *flag = nullptr;
     HIP_TRY(d->dp.get(&flag, sizeof(int)));
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
+    // the pool's A/C/G/T/N scan on the side stream while the reads are checked and shaped: it
+    // touches only the pool and seq_off, and a pool in another order (flag bit 4) redoes it per read
+    HIP_TRY(hipEventRecord(c->side_ev[0], c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+    HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->side));
+    const int64_t chunks = (d->d.seq_bytes + 15) / 16;
+    if (chunks > 0)
+      hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, c->side,
+                         d->d, (uint8_t *)cl, (uint32_t *)nnb);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->side_ev[1], c->side));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
     // validation and the read shapes in one pass (a read out of its pools gets no shape)
     hipLaunchKernelGGL(read_prep, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag, (int16_t *)p, (uint8_t *)q);
     HIP_TRY(hipGetLastError());
     int bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    const auto &crb = d->contig_read_begin;
+    for (int k = 0; k < nc; ++k)
+      if (crb[(size_t)k + 1] > crb[(size_t)k])
+        HIP_TRY(hipMemcpyAsync(&last[(size_t)k], d->d.pmax_end + (crb[(size_t)k + 1] - 1), sizeof(int32_t),
+                               hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad & 3) HIP_TRY(hipStreamSynchronize(c->side));  // (nothing of the side stream outlives a failure)
     if (bad & 1)
       return set_err(GQ_E_UNSORTED, "Regions must be sorted by start locus: reads are not sorted by (contig, start), "
                                     "or pmax_end is not the running maximum of end within each contig");
     if (bad & 2)
       return set_err(GQ_E_ARG, "read set: an offset or length lies outside its pool, or a sample slot >= n_samples");
     unordered = (bad & 4) ? 1 : 0;
-    if (!unordered) {
-      HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->stream));
-      const int64_t chunks = (d->d.seq_bytes + 15) / 16;
-      if (chunks > 0)
-        hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, c->stream,
-                           d->d, (uint8_t *)cl, (uint32_t *)nnb);
-    } else {
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+    if (unordered) {  // the pool scan assumed read order: per read instead
+      HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)d->d.n_reads, c->stream));
       hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl, (uint32_t *)nnb);
-    }
-    HIP_TRY(hipGetLastError());
-  }
-  {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds
-    const int64_t n = d->d.n_reads;
-    void *cd = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr, *tmp = nullptr;
-    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
-    HIP_TRY(d->dp.get(&cd, ncd));
-    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
-    HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
-    HIP_TRY(d->dp.get((void **)&na, sizeof(int64_t) * (size_t)(n + 1)));
-    const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int64_t *)na);
-    HIP_TRY(hipGetLastError());
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
-    HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
-    int64_t aux_len = 0;
-    HIP_TRY(hipMemcpyAsync(&aux_len, (int64_t *)ao + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    d->dp.put(tmp);
-    d->dp.put(na);
-    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_len, 1) + 1024;
-    HIP_TRY(d->dp.get(&ce, nce));
-    HIP_TRY(hipMemsetAsync(ce, 0, nce, c->stream));
-    d->d.cdesc = (const ColDesc *)cd;
-    d->d.cev = (const uint32_t *)ce;
-    d->d.caux_off = (const int64_t *)ao;
-    if (n > 0) {
-      hipLaunchKernelGGL(col_derive, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const int64_t *)ao, (ColDesc *)cd, (uint32_t *)ce);
       HIP_TRY(hipGetLastError());
     }
   }
   {  // the projections' slices (whole 512-locus blocks up to each contig's largest read end) and
      // the block index of the reads (plan_tiles' windows of aligned tiles); the projection
      // itself is derived on first use (ensure_projection)
-    const int nc = d->d.n_contigs;
     std::vector<int64_t> qoff((size_t)nc + 1, 0);
-    {
-      std::vector<int32_t> last((size_t)nc, 0);
-      const auto &crb = d->contig_read_begin;
-      for (int k = 0; k < nc; ++k)
-        if (crb[(size_t)k + 1] > crb[(size_t)k])
-          HIP_TRY(hipMemcpyAsync(&last[(size_t)k], d->d.pmax_end + (crb[(size_t)k + 1] - 1), sizeof(int32_t),
-                                 hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      for (int k = 0; k < nc; ++k) {
-        const int64_t col1 = ((int64_t)std::max(last[(size_t)k], 0) + 7) >> 3;
-        qoff[(size_t)k + 1] = qoff[(size_t)k] + 4 * ((col1 + 63) >> 6);
-      }
+    for (int k = 0; k < nc; ++k) {
+      const int64_t col1 = ((int64_t)std::max(last[(size_t)k], 0) + 7) >> 3;
+      qoff[(size_t)k + 1] = qoff[(size_t)k] + 4 * ((col1 + 63) >> 6);
     }
     void *qo = nullptr;
     HIP_TRY(d->dp.get(&qo, sizeof(int64_t) * ((size_t)nc + 1)));
@@ -2053,6 +2040,37 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
     }
     d->d.blk_rb = brb;
     d->d.blk_rs = brs;
+  }
+  {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds.  The
+     // auxiliary list is sized by its bound (MD events + 6 words per CIGAR op: at most three
+     // segments of two words per op), so no count comes back to the host first.
+    const int64_t n = d->d.n_reads;
+    void *cd = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr, *tmp = nullptr;
+    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
+    HIP_TRY(d->dp.get(&cd, ncd));
+    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
+    HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
+    HIP_TRY(d->dp.get((void **)&na, sizeof(int64_t) * (size_t)(n + 1)));
+    const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int64_t *)na);
+    HIP_TRY(hipGetLastError());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    d->dp.put(tmp);
+    d->dp.put(na);
+    const int64_t aux_bound = std::max<int64_t>(md_len, 0) + 6 * std::max<int64_t>(d->d.cigar_len, 0);
+    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_bound, 1) + 1024;
+    HIP_TRY(d->dp.get(&ce, nce));
+    d->d.cdesc = (const ColDesc *)cd;
+    d->d.cev = (const uint32_t *)ce;
+    d->d.caux_off = (const int64_t *)ao;
+    if (n > 0) {
+      hipLaunchKernelGGL(col_derive, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (const int64_t *)ao, (ColDesc *)cd, (uint32_t *)ce);
+      HIP_TRY(hipGetLastError());
+    }
   }
   d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
   nnb = nullptr;
@@ -2277,6 +2295,7 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   if (d->ctx != c) return set_err(GQ_E_ARG, "gq_reads_rederive: the read set belongs to another context");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));  // nothing queued may still read the derived buffers
+  HIP_TRY(hipStreamSynchronize(c->side));
   d->dp.release_all();
   DevReads &R = d->d;
   R.lead = nullptr;
@@ -3086,9 +3105,10 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   HIP_TRY(d->dp.get(&pbd, (size_t)n_sl + 16));
   HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
   HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
-  unsigned long long *nok = nullptr, hk[kSpread];
-  HIP_TRY(d->dp.get((void **)&nok, sizeof(hk)));
-  HIP_TRY(hipMemsetAsync(nok, 0, sizeof(hk), c->stream));
+  unsigned long long *nok = nullptr;
+  std::vector<unsigned long long> hk(kOkSpread);
+  HIP_TRY(d->dp.get((void **)&nok, sizeof(unsigned long long) * kOkSpread));
+  HIP_TRY(hipMemsetAsync(nok, 0, sizeof(unsigned long long) * kOkSpread, c->stream));
   hipLaunchKernelGGL(proj_prep, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (ProjRec *)pr,
                      (uint8_t *)pbd, (int64_t *)ne, nok);
   HIP_TRY(hipGetLastError());
@@ -3153,6 +3173,18 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   if (cells) HIP_TRY(hipMemsetAsync((uint8_t *)pj + pool_bytes - 16, 0, 16, c->stream));
   else HIP_TRY(hipMemsetAsync(pj, 0, pool_bytes, c->stream));
   HIP_TRY(d->dp.get(&pe, sizeof(uint2) * (size_t)(tot[1] + 1)));
+  d->d.proj = (const uint8_t *)pj;
+  d->d.pev = (const uint2 *)pe;
+  d->d.pev_off = (const int64_t *)eo;
+  // the sparse entries on the side stream, beside the pool fill (they read neither the pool nor rows)
+  HIP_TRY(hipEventRecord(c->side_ev[2], c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->side, c->side_ev[2], 0));
+  if (n > 0) {
+    hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->side, d->d,
+                       (const int64_t *)eo, (uint2 *)pe);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(c->side_ev[3], c->side));
   HIP_TRY(hipEventRecord(c->dev_ev[0], c->stream));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
@@ -3196,19 +3228,12 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->dev_ev[1], c->stream));
-  if (n > 0) {
-    hipLaunchKernelGGL(pev_fill, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                       (const int64_t *)eo, (uint2 *)pe);
-    HIP_TRY(hipGetLastError());
-  }
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->side_ev[3], 0));  // (the sparse entries done)
   HIP_TRY(hipEventRecord(c->dev_ev[3], c->stream));
-  d->d.proj = (const uint8_t *)pj;
-  d->d.pev = (const uint2 *)pe;
-  d->d.pev_off = (const int64_t *)eo;
   d->proj_bytes = kProjRowBytes * tot[0];
   d->pev_count = tot[1];
   {  // reads the projection takes (counted by proj_prep)
-    HIP_TRY(hipMemcpyAsync(hk, nok, sizeof(hk), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(hk.data(), nok, sizeof(unsigned long long) * kOkSpread, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     d->dp.put(nok);
     d->proj_reads = 0;
