@@ -469,11 +469,13 @@ __global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restr
 // slice-major fill.
 constexpr int kCell3Win = 255;    // window reads a u8 map can name
 constexpr int kCell3Rows = 64;    // rows per map chunk
+static_assert(kCell3Rows % kRowPad == 0, "chunks hold whole kRowPad row groups");
 struct __attribute__((aligned(16))) Cell3Rec {
   uint32_t a;         // seq_off + leading clip - seq_off[window's first read]
   int32_t s, e;       // [start, end)
   uint32_t info;      // ColDesc info (bit kColEligible: the fast path)
 };
+template <int CU>  // cells per lane whose loads issue together (4; A/B GQ_FILL_U=8)
 __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj,
                                                        int64_t *__restrict__ deep, unsigned long long *__restrict__ n_deep,
                                                        int dbg) {
@@ -524,6 +526,7 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
         psl = row == 0xFFFF ? 0 : sl;
       }
     }
+    if (dbg & 16) continue;  // ablation: the window's records only
     for (int32_t k0 = 0; k0 < nr; k0 += kCell3Rows) {
       const int32_t nk = nr - k0 < kCell3Rows ? nr - k0 : kCell3Rows;
       for (int32_t c = lane; c < 16 * nk; c += 64) map[c] = 0xFFu;
@@ -545,38 +548,41 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       uint32_t *o = out + 16 * k0;
-      for (int32_t c00 = 0; c00 < 16 * nk; c00 += 256) {  // four cells per lane, their loads together
-        uint64_t b[4];
-        uint32_t pp[4];
+      for (int32_t c00 = (dbg & 8) ? 16 * nk : 0; c00 < 16 * nk; c00 += 64 * CU) {  // CU cells per lane, loads together
+        uint64_t b[CU], mk[CU];
         uint32_t slow = 0;
+        // Every lane loads (an empty or slow cell the window's first word, masked off): a load
+        // under a divergent branch, or a mask applied right after it, makes the wave wait for it
+        // before the next cell's — one load in flight instead of CU.
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < CU; ++u) {
           const int32_t c = c00 + 64 * u + lane;
-          pp[u] = c < 16 * nk ? map[c] : 0xFFu;
-          b[u] = 0;
-          if (pp[u] != 0xFFu) {
-            const Cell3Rec m = rec[pp[u]];
-            const int32_t lb = 8 * (W.qc0 + (c & 15));
-            const int64_t v = (int64_t)m.a + lb - m.s;
-            if (!(m.info & kColEligible) || m.a == kCell3Far || v < 0 || v + 8 > span) {
-              slow |= 1u << u;
-            } else if (dbg & 1) {  // ablation: no loads
-              b[u] = (uint64_t)v;
-            } else {
-              b[u] = *reinterpret_cast<const gq_u64u *>(pool + (uint32_t)v);
-              if (m.s > lb || m.e < lb + 8) b[u] &= edge_mask(m.s - lb, m.e - lb);
-            }
-          }
+          const uint32_t pp = c < 16 * nk ? map[c] : 0xFFu;
+          const Cell3Rec m = rec[pp != 0xFFu ? pp : 0];
+          const int32_t lb = 8 * (W.qc0 + (c & 15));
+          const int64_t v = (int64_t)m.a + lb - m.s;
+          const bool ok = (m.info & kColEligible) && m.a != kCell3Far && v >= 0 && v + 8 <= span;
+          if (pp != 0xFFu && !ok) slow |= 1u << u;
+          mk[u] = pp != 0xFFu && ok ? edge_mask(m.s - lb, m.e - lb) : 0ull;
+          const uint32_t off = pp != 0xFFu && ok ? (uint32_t)v : 0u;
+          b[u] = (dbg & 1) || span < 8 ? (uint64_t)off  // (ablation bit 0: no loads)
+                                       : *reinterpret_cast<const gq_u64u *>(pool + off);
         }
+        uint32_t x[CU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int32_t c = c00 + 64 * u + lane;
-          if (c < 16 * nk && !((slow >> u) & 1u))
-            o[c] = perm_codes4((uint32_t)b[u]) | (perm_codes4((uint32_t)(b[u] >> 32)) << 4);
+        for (int u = 0; u < CU; ++u) {
+          const uint64_t y = b[u] & mk[u];
+          x[u] = perm_codes4((uint32_t)y) | (perm_codes4((uint32_t)(y >> 32)) << 4);
         }
+        // Stores under a wave-uniform bound only (16 nk is a multiple of 64: rows are padded to
+        // kRowPad), slow cells included — their slow path below rewrites them: stores under
+        // divergent branches are each made to wait for the last one.
+#pragma unroll
+        for (int u = 0; u < CU; ++u)
+          if (c00 + 64 * u < 16 * nk) o[c00 + 64 * u + lane] = x[u];
         if (slow) {  // rare: a general CIGAR, a word at the pool's end
 #pragma unroll 1
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < CU; ++u) {
             if (!((slow >> u) & 1u)) continue;
             const int32_t c = c00 + 64 * u + lane;
             const uint32_t p = map[c];
@@ -3200,8 +3206,8 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
       HIP_TRY(d->dp.get((void **)&dl, sizeof(int64_t) * (size_t)n_sl));
       HIP_TRY(hipMemsetAsync(nd, 0, sizeof(unsigned long long), c->stream));
       const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
-      hipLaunchKernelGGL(proj_fill_cells, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj,
-                         dl, nd, fill_dbg());
+      hipLaunchKernelGGL(fill_u == 8 ? proj_fill_cells<8> : proj_fill_cells<4>, dim3((unsigned)blocks), dim3(256), 0,
+                         c->stream, d->d, n_sl, (uint8_t *)pj, dl, nd, fill_dbg());
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(proj_fill_deep, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0, c->stream, d->d,
                          (const int64_t *)dl, (const unsigned long long *)nd, (uint8_t *)pj);

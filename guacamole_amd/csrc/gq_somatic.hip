@@ -1304,7 +1304,8 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   }
   // the words no piece covers: biased zero terms (a rebuild for another filter rewrites only
   // pieces); the cell fill writes every word itself
-  const bool cells = fill_pieces();
+  const int mode = margin_fill_mode();
+  const bool cells = mode == 1 || mode == 2;  // these write every word: no preset
   if (cells) HIP_TRY(hipMemsetAsync((uint8_t *)t->mproj + 128 * t->n_rows, kMargin8Zero, 32, c->stream));
   else HIP_TRY(hipMemsetAsync(t->mproj, kMargin8Zero, (size_t)(128 * t->n_rows + 32), c->stream));
   void *tab = nullptr;  // margin_term8 by (mapq, quality, match)
@@ -1313,11 +1314,11 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
   HIP_TRY(hipGetLastError());
   if (t->n_slices > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;  // A/B: words per lane and round
-    if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
+    if (mode == 2) {  // A/B: GQ_MFILL=pieces
       const int64_t blocks = std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20);
       hipLaunchKernelGGL(mproj_fill_pieces, dim3((unsigned)blocks), dim3(256), 0, c->stream, t->d, t->n_slices, min_mapq,
                          (const uint8_t *)tab, (uint8_t *)t->mproj, (uint8_t *)t->mnb);
-    } else if (cells) {
+    } else if (mode == 1) {  // A/B: GQ_MFILL=cells
       unsigned long long *nd = nullptr;
       int64_t *dl = nullptr;
       HIP_TRY(t->dp.get((void **)&nd, sizeof(unsigned long long)));
@@ -1332,7 +1333,7 @@ gq_status ensure_margin_projection(gq_ctx *c, const gq_dev_reads *t, int min_map
                          (uint8_t *)t->mproj, (uint8_t *)t->mnb);
       t->dp.put(nd);
       t->dp.put(dl);
-    } else if (fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_FILL=slice)
+    } else if (mode == 3 || fill_slice_major()) {  // A/B: the slice-major fill of round 4 (GQ_MFILL / GQ_FILL=slice)
       auto kf = fill_u == 4 ? mproj_fill<4> : fill_u == 2 ? mproj_fill<2> : mproj_fill<1>;
       hipLaunchKernelGGL(kf, dim3((unsigned)std::min<int64_t>((t->n_slices + 3) / 4, 1 << 20)), dim3(256), 0,
                          c->stream, t->d, t->n_slices, min_mapq, (const uint8_t *)tab, (uint8_t *)t->mproj,

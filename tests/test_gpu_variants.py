@@ -5,7 +5,9 @@ GQ_CALL_WPE=2 (the one-kernel caller at 2 waves per SIMD), GQ_FILL_U=2 / 4 (the 
 projection and margin fills at 2 or 4 words per lane and round; GQ_FILL_W: 2 or 4 consecutive
 words of a read per lane), GQ_FILL_ONE=1 (the projection and the margin projection in one pass
 instead of two) — each with GQ_FILL=rw (the read-major fills), GQ_FILL=slice (the slice-major
-fills), GQ_ROWS=firstfit (first-fit row assignment instead of the parallel earliest-freed one).  A synthetic 300 kb 60x / 30x pair with a raised somatic
+fills), GQ_ROWS=firstfit (first-fit row assignment instead of the parallel earliest-freed one),
+GQ_FILL=pieces (the projection by pieces instead of cells), GQ_MFILL=cells / pieces (the margin
+projection by cells / pieces instead of read-major).  A synthetic 300 kb 60x / 30x pair with a raised somatic
 rate, so hundreds of candidates and calls reach every path."""
 import json
 import os
@@ -32,6 +34,6 @@ def test_kernel_variants_give_the_default_records():
     rw = {"GQ_FILL": "rw"}
     for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, rw, dict(rw, GQ_FILL_U="2"), dict(rw, GQ_FILL_U="4"),
                   dict(rw, GQ_FILL_W="2"), dict(rw, GQ_FILL_W="4"), dict(rw, GQ_FILL_ONE="1"), {"GQ_FILL": "slice"},
-                  {"GQ_ROWS": "firstfit"}):
+                  {"GQ_ROWS": "firstfit"}, {"GQ_FILL": "pieces"}, {"GQ_MFILL": "cells"}, {"GQ_MFILL": "pieces"}):
         got = _run(extra)
         assert got == base, (extra, got, base)
