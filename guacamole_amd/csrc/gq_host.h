@@ -877,6 +877,33 @@ __device__ __forceinline__ int64_t piece_grow(const DevReads &R, int64_t r, int6
   return k == 0xFFFFu ? -1 : R.srow[slot] + (int64_t)k;
 }
 
+// Global rows of read r's pieces in slices q0 .. q0 + npc - 1 (npc <= kReadPieces; -1: none).
+// Every load is issued together — the slices past the read's last piece load that piece's slice
+// again — so the pieces cost two dependent rounds of loads, not four each (a load under a
+// per-piece branch waits for the one before).  r lies in each of its pieces' slice windows.
+__device__ __forceinline__ void piece_grows(const DevReads &R, int64_t r, int64_t q0, int32_t npc,
+                                            int64_t (&g)[kReadPieces]) {
+  if (npc <= 0) {
+#pragma unroll
+    for (int j = 0; j < kReadPieces; ++j) g[j] = -1;
+    return;
+  }
+  int64_t so[kReadPieces], sa[kReadPieces], sr[kReadPieces];
+  uint32_t pb[kReadPieces], k[kReadPieces];
+#pragma unroll
+  for (int j = 0; j < kReadPieces; ++j) {
+    const int64_t sl = q0 + (j < npc ? j : npc - 1);
+    pb[j] = R.pbad[sl];
+    so[j] = R.soff[sl];
+    sa[j] = R.sra[sl];
+    sr[j] = R.srow[sl];
+  }
+#pragma unroll
+  for (int j = 0; j < kReadPieces; ++j) k[j] = R.prow[so[j] + (r - sa[j])];
+#pragma unroll
+  for (int j = 0; j < kReadPieces; ++j) g[j] = j < npc && !pb[j] && k[j] != 0xFFFFu ? sr[j] + (int64_t)k[j] : -1;
+}
+
 // Batches of 64 reads from batch b0 on, stride nb (grid-stride over waves).  For each word of
 // each kept read: raw = fetch(read, meta, column) (its loads), then emit(act, raw, read, meta,
 // column, grow, slot).  keep(meta) decides per read (false: no words); batch(first read) runs
@@ -887,9 +914,12 @@ __device__ __forceinline__ int64_t piece_grow(const DevReads &R, int64_t r, int6
 // eighth of the batches, so rows that pieces of neighbouring batches share meet in one L2).
 // EV: each read's MD events (up to four) are loaded with its records into ev01 / ev23.
 // kW: consecutive words of a read per lane (the lane-to-word mapping is done once per kW words).
+// src (R.seq or R.qual; nullptr: none): fetch(read, meta, column, pre, fast) gets the word's
+// eight bytes at src + p0 + 8 column already loaded when fast (a column-eligible read's word
+// inside the pool).
 template <int kU, bool EV, int kW, class B, class K, class F, class E>
 __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restrict__ meta, uint32_t *__restrict__ owner,
-                                          int dbg, B &&batch, K &&keep, F &&fetch, E &&emit) {
+                                          int dbg, const uint8_t *src, B &&batch, K &&keep, F &&fetch, E &&emit) {
   const int lane = threadIdx.x & 63;
   const int64_t nbat = (R.n_reads + 63) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -930,9 +960,14 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
     if constexpr (EV) {
       const int32_t nmd = (int32_t)(d.info & 0xFFFFu);
       if (in && nmd <= 4 && d.end - d.start < 0xFFF0) {  // (no word of the read reaches the 0xFFFF marker)
+        // (the four loads issued together: past the read's last event its last one again)
         uint32_t v[4];
+        if (nmd > 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = k < nmd ? R.md_ev[mdo + k] : 0xFFFFFFFFu;
+          for (int k = 0; k < 4; ++k) v[k] = R.md_ev[mdo + (k < nmd ? k : nmd - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = k < nmd ? v[k] : 0xFFFFFFFFu;
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = v[k] >> 8;  // offsets (none: 0xFFFFFF)
@@ -954,8 +989,7 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
       const int64_t q0 = m.qoff + (pr.col0 >> 4);
       const int32_t npc = len ? ((pr.col1 - 1) >> 4) - (pr.col0 >> 4) + 1 : 0;
       int64_t g[kReadPieces];
-#pragma unroll
-      for (int j = 0; j < kReadPieces; ++j) g[j] = j < npc ? piece_grow(R, rr, q0 + j) : -1;
+      piece_grows(R, rr, q0, npc < kReadPieces ? npc : kReadPieces, g);
 #pragma unroll
       for (int j = 0; j < kReadPieces; ++j) m.grow[j] = g[j];
     }
@@ -976,7 +1010,7 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
       bool act[N];
       int64_t grow[N], slot[N];
       ReadMeta pm[kU];
-      decltype(fetch((int64_t)0, pm[0], (int32_t)0)) raw[N];
+      decltype(fetch((int64_t)0, pm[0], (int32_t)0, 0ull, false)) raw[N];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const uint32_t wb = w0 + 64 * u, w = wb + (uint32_t)lane;
@@ -1020,7 +1054,24 @@ __device__ __forceinline__ void read_fill(const DevReads &R, ReadMeta *__restric
       for (int i = 0; i < N; ++i) {
         if (act[i] && grow[i] == -2) grow[i] = piece_grow(R, 64 * b + kk[i], slot[i]);  // a long read's later piece
         act[i] = act[i] && grow[i] >= 0;
-        if (act[i] && !(dbg & 1)) raw[i] = fetch(64 * b + kk[i], pm[i / kW], col[i]);
+      }
+      // The N words' 8-byte loads first, every lane's (a word off the fast path loads src[0],
+      // unused): a load under a per-word branch, or its mask applied right after it, would make
+      // the wave wait for each before issuing the next.
+      uint64_t pre[N];
+      bool fast[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const ReadMeta &mi = pm[i / kW];
+        const int64_t a = mi.p0 + 8 * (int64_t)col[i];
+        fast[i] = src != nullptr && act[i] && (mi.info & kColEligible) && a >= 0 && a + 8 <= R.seq_cap;
+        pre[i] = src != nullptr && R.seq_cap >= 8 && !(dbg & 1)
+                     ? *reinterpret_cast<const gq_u64u *>(src + (fast[i] ? a : 0))
+                     : 0ull;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        if (act[i] && !(dbg & 1)) raw[i] = fetch(64 * b + kk[i], pm[i / kW], col[i], pre[i], fast[i]);
         else raw[i] = {};
       }
 #pragma unroll

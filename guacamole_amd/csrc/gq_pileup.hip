@@ -449,8 +449,12 @@ __global__ __launch_bounds__(256) void proj_fill_rw(DevReads R, uint8_t *__restr
   __shared__ uint32_t s_owner[4][KU * 64];
   uint32_t *out = reinterpret_cast<uint32_t *>(proj);
   read_fill<KU, false, KW>(
-      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, [](int64_t) {}, [](const ReadMeta &) { return true; },
-      [&](int64_t r, const ReadMeta &m, int32_t col) { return proj_fetch(R, r, piece_meta(m), col); },
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, R.seq, [](int64_t) {},
+      [](const ReadMeta &) { return true; },
+      [&](int64_t r, const ReadMeta &m, int32_t col, uint64_t pre, bool fast) {
+        if (fast) return ProjRaw{pre & edge_mask(m.s - 8 * col, m.e - 8 * col), 0u, 0u};
+        return proj_fetch(R, r, piece_meta(m), col);
+      },
       [&](bool act, const ProjRaw &x, int64_t, const ReadMeta &, int32_t col, int64_t grow, int64_t) {
         if (act)  // (an eligible read's bytes are A C G T N: the v_perm lookup)
           out[16 * grow + (col & 15)] =

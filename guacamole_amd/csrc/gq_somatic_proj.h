@@ -249,7 +249,8 @@ struct MarginRW {
   uint32_t evb;
 };
 __device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r, const ReadMeta &m, int32_t col,
-                                                    const uint8_t *__restrict__ tab) {
+                                                    const uint8_t *__restrict__ tab, uint64_t pre = 0,
+                                                    bool fast = false) {
   MarginRW o;
   const int32_t nmd = (int32_t)(m.info & 0xFFFFu);
   const uint32_t *ev = R.md_ev + m.md_off;
@@ -279,7 +280,13 @@ __device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r
     }
   }
   const PieceMeta pm = piece_meta(m);
-  if (m.info & kColEligible) o.x = margin_fetch(R, r, pm, col, 0u, tab);  // (the terms come in the emit)
+  if (fast) {  // (read_fill loaded the word's qualities: margin_fetch's one-load case)
+    const int32_t lb = 8 * col;
+    const int32_t lo = min(max(m.s - lb, 0), 8), hi = min(max(m.e - lb, 0), 8);
+    o.x = MarginRaw{0, make_uint2(0x80808080u, 0x80808080u), 0, 0};
+    o.x.q = pre & edge_mask(lo, hi);
+    o.x.valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+  } else if (m.info & kColEligible) o.x = margin_fetch(R, r, pm, col, 0u, tab);  // (the terms come in the emit)
   else o.x = margin_fetch(R, r, pm, col, word_event_bits(m, col, o.v, o.evb), tab);
   return o;
 }
@@ -289,34 +296,55 @@ __device__ __forceinline__ MarginRW margin_fetch_rw(const DevReads &R, int64_t r
 template <int KU, int KW>
 __global__ __launch_bounds__(256) void mproj_fill_rw(DevReads R, int min_mapq, const uint8_t *__restrict__ tab,
                                                      uint8_t *__restrict__ mproj, uint8_t *__restrict__ mnb, int dbg) {
+  constexpr int kRows = 4;  // table rows staged per batch: its first kRows distinct mapping qualities
   __shared__ ReadMeta s_meta[4][64];
   __shared__ uint32_t s_owner[4][KU * 64];
-  __shared__ uint32_t s_row[4][64];  // the table row of the batch's first read's mapq (256 bytes)
+  __shared__ uint32_t s_row[4][kRows * 64];
   uint32_t *row = s_row[threadIdx.x >> 6];
   const uint8_t *lrow = reinterpret_cast<const uint8_t *>(row);
   const int lane = threadIdx.x & 63;
-  uint32_t lmq = 0;
+  uint32_t lmq[kRows];  // (wave-uniform) the staged rows' mapping qualities; 0xFFFFFFFF: none
   uint2 *out = reinterpret_cast<uint2 *>(mproj);
   read_fill<KU, true, KW>(
-      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
-      [&](int64_t r0) {  // most reads share one mapping quality: its table row in LDS
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, R.qual,
+      [&](int64_t r0) {
+        // a few mapping qualities cover a batch's reads (most share one): their table rows in LDS,
+        // so a wave's words look their terms up there without a round trip to the cache hierarchy
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        lmq = (uint32_t)R.mapq[r0];
-        row[lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
+        const int64_t rl = r0 + lane;
+        const uint32_t mq = (uint32_t)R.mapq[rl < R.n_reads ? rl : r0];
+        unsigned long long rem = __ballot(true);
+#pragma unroll
+        for (int k = 0; k < kRows; ++k) {
+          lmq[k] = 0xFFFFFFFFu;
+          if (rem) {  // (uniform)
+            const uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mq, __ffsll((long long)rem) - 1);
+            lmq[k] = mk;
+            rem &= ~__ballot(mq == mk);
+            row[64 * k + lane] = reinterpret_cast<const uint32_t *>(tab + (mk << 8))[lane];
+          }
+        }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       },
       [&](const ReadMeta &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); },
-      [&](int64_t r, const ReadMeta &m, int32_t col) { return margin_fetch_rw(R, r, m, col, tab); },
+      [&](int64_t r, const ReadMeta &m, int32_t col, uint64_t pre, bool fast) {
+        return margin_fetch_rw(R, r, m, col, tab, pre, fast);
+      },
       [&](bool act, const MarginRW &o, int64_t, const ReadMeta &m, int32_t col, int64_t grow, int64_t slot) {
-        // (uniform: the wave's table lookups all in the LDS row, or per lane)
-        const bool all_lds = __ballot(act && !o.x.gen && m.mq != lmq) == 0;
+        int k = -1;
+#pragma unroll
+        for (int j = kRows - 1; j >= 0; --j) k = m.mq == lmq[j] ? j : k;
+        // (uniform: the wave's table lookups all in its LDS rows, or per lane)
+        const bool all_lds = __ballot(act && !o.x.gen && k < 0) == 0;
         if (act) {
           const uint32_t evb = word_event_bits(m, col, o.v, o.evb);
+          const uint8_t *lr = lrow + 256 * (k < 0 ? 0 : k);
           const uint2 w = o.x.gen ? o.x.word
-                          : all_lds ? margin_terms8_lds(o.x.q, o.x.valid, evb, lrow)
-                                    : margin_terms8(piece_meta(m), o.x.q, o.x.valid, evb, tab, lrow, lmq);
+                          : all_lds ? margin_terms8_lds(o.x.q, o.x.valid, evb, lr)
+                                    : margin_terms8(piece_meta(m), o.x.q, o.x.valid, evb, tab, k < 0 ? nullptr : lr,
+                                                    m.mq);
           out[16 * grow + (col & 15)] = w;
           auto has = [](uint32_t v) {  // a zero byte
             return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u;
@@ -660,7 +688,7 @@ __global__ __launch_bounds__(256) void pm_fill_rw(DevReads R, uint8_t *__restric
   uint2 *mout = reinterpret_cast<uint2 *>(mproj);
   auto kept = [=](const ReadMeta &m) { return !(min_mapq > 0 && (int)m.mq < min_mapq); };
   read_fill<1, true, 1>(
-      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg,
+      R, s_meta[threadIdx.x >> 6], s_owner[threadIdx.x >> 6], dbg, nullptr,
       [&](int64_t r0) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -670,7 +698,7 @@ __global__ __launch_bounds__(256) void pm_fill_rw(DevReads R, uint8_t *__restric
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       },
       [](const ReadMeta &) { return true; },
-      [&](int64_t r, const ReadMeta &m, int32_t col) {
+      [&](int64_t r, const ReadMeta &m, int32_t col, uint64_t, bool) {
         return PmRaw{proj_fetch(R, r, piece_meta(m), col), margin_fetch_rw(R, r, m, col, tab)};
       },
       [&](bool act, const PmRaw &o, int64_t, const ReadMeta &m, int32_t col, int64_t grow, int64_t slot) {
