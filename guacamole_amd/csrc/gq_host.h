@@ -56,6 +56,7 @@ struct Counters {  // device-side run counters (one allocation, zeroed per call)
   unsigned long long n_amb;        // loci listed for the heap-order reference base (AmbItem list)
   unsigned long long n_ord;        // germline loci whose Scala map order depends on element order
   unsigned long long n_deep;       // somatic candidates handed to the deep caller
+  unsigned long long n_wide;       // somatic candidates the deep caller handed to the wide one (> 128 alleles)
   unsigned long long n_gdeep[3];   // germline_complex loci handed to the wide table (first pass, order, heap-order runs)
   unsigned long long deep_max;     // deepest per-sample pileup among them and the listed loci
   unsigned long long deep_nt;      // germline-standard: largest allele table among the loci handed to the deep caller

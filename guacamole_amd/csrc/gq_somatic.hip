@@ -1745,7 +1745,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     // the exact caller: the fast kernel (pileups up to kFastCap reads per sample, element
     // records in LDS), then the deep kernel over the deeper candidates it listed, then the
     // deep kernel again over the loci whose reference base heap order decides
-    HIP_TRY(c->deep_list.ensure(deep_cap * sizeof(int64_t)));
+    HIP_TRY(c->deep_list.ensure(2 * deep_cap * sizeof(int64_t)));  // the deep list, then the wide list
     // persistent: the resident workgroups, each wave over every (grid)-th candidate (a grid of
     // many generations leaves a tail of idle SIMDs behind the last ones)
     if (c->call_wg_per_cu <= 0) {
@@ -1847,7 +1847,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
                          (AmbItem *)(ain ? nullptr : c->amb.p), ain ? (unsigned long long)0 : amb_cap, ain, aref,
                          ain ? n_items : (int64_t)0, ain ? RefView{nullptr, nullptr} : rv, dbg,
                          DeepIO{(int64_t *)c->deep_list.p, 0, ain ? 0 : n_items, (uint8_t *)c->deep_scratch.p, scap,
-                                kMaxG},
+                                kMaxG, (int64_t *)c->deep_list.p + deep_cap, deep_cap},
                          ElemStore{});
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(c->ev[3], c->stream));
@@ -1864,6 +1864,35 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
         free(res);
         return st;
       }
+    }
+    if (hc.n_wide > deep_cap) {
+      deep_cap = hc.n_wide + 1024;
+      retry = true;
+    }
+    if (!retry && hc.n_wide > 0 && !hc.err) {
+      // the wide kernel: the candidates past the deep kernel's allele table or genotype scratch
+      // (64 kWideNS distinct alleles per sample, every genotype of them in its scratch); a few
+      // waves, each with a large scratch slice
+      const int scap = (int)std::max<unsigned long long>(hc.deep_max, (unsigned long long)kFastCap);
+      const int maxg = 64 * kWideNS * (64 * kWideNS + 1) / 2;
+      const int64_t nw = std::min<int64_t>((int64_t)hc.n_wide, 64);
+      const size_t wb = deep_wave_bytes(scap, maxg, kWideNS);
+      HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
+      HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+      hipLaunchKernelGGL((somatic_call_k<true, false, 3, kWideNS>), dim3((unsigned)((nw + kSomWaves - 1) / kSomWaves)),
+                         dim3(kBlock), 0, c->stream, (const CandRec *)c->cands.p, t->d, n->d, *p, (SomRec *)c->srecs.p,
+                         rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)c->amb.p, amb_cap,
+                         (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, rv, dbg,
+                         DeepIO{(int64_t *)c->deep_list.p + deep_cap, 0, (int64_t)hc.n_wide, (uint8_t *)c->deep_scratch.p,
+                                scap, maxg, nullptr, 0},
+                         ElemStore{});
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+      HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[3]);
+      deep_ms += ms;
     }
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;

@@ -19,6 +19,7 @@
 #pragma once
 
 constexpr int kFastCap = 128;      // elements per sample held in LDS by the fast kernel
+constexpr int kWideNS = 4;         // the wide kernel's allele-table slots: 256 distinct alleles per sample
 constexpr int kDeepTermCap = 256;  // deep kernel: elements per LDS chunk of the likelihood fold
 
 // Element record (16 bytes), one per covering read in pileup element order:
@@ -47,17 +48,20 @@ struct CallMem {
   int16_t *order;   // [64 kSlots]
   uint8_t *is_var;  // [64 kSlots]
   double *ll;       // [maxG]
+  uint32_t *gkey;   // deep kernels: [2 maxG] the genotypes' map keys (the variant mass past 128 genotypes)
+  double *gsum;     // deep kernels: [maxG] the variant likelihoods in map order
   struct TermRec *terms;  // [tcap] LDS: a chunk of elements' log terms + table indexes (the fold)
   int tcap;
   const double *succ;     // PhredUtils.phredToSuccessProbability table (g_succ) copied to LDS
   int cap, maxG;
 };
 
-// Deep-kernel scratch geometry: bytes per wave for `cap` elements per sample.
-__host__ __device__ __forceinline__ size_t deep_wave_bytes(int cap, int maxG) {
-  return (size_t)cap * (2 * 4 + 2 * 16 + 2 * 4) + 64 * kSlots * 3 + (size_t)maxG * 8 + 64;
+// Deep-kernel scratch geometry: bytes per wave for `cap` elements per sample, maxG genotypes and
+// ns allele-table slots.
+__host__ __device__ __forceinline__ size_t deep_wave_bytes(int cap, int maxG, int ns = kSlots) {
+  return (size_t)cap * (2 * 4 + 2 * 16 + 2 * 4) + 64 * (size_t)ns * 3 + (size_t)maxG * 24 + 64;
 }
-__device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
+__device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG, int ns = kSlots) {
   CallMem m;
   uint8_t *p = base;
   m.el[0] = (uint4 *)p;
@@ -66,6 +70,10 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   p += (size_t)cap * 16;
   m.ll = (double *)p;
   p += (size_t)maxG * 8;
+  m.gsum = (double *)p;
+  p += (size_t)maxG * 8;
+  m.gkey = (uint32_t *)p;
+  p += (size_t)maxG * 8;
   m.cov[0] = (int32_t *)p;
   p += (size_t)cap * 4;
   m.cov[1] = (int32_t *)p;
@@ -73,7 +81,7 @@ __device__ __forceinline__ CallMem deep_mem(uint8_t *base, int cap, int maxG) {
   m.tmp = (uint32_t *)p;
   p += (size_t)cap * 8;
   m.order = (int16_t *)p;
-  p += 64 * kSlots * 2;
+  p += 64 * (size_t)ns * 2;
   m.is_var = p;
   m.terms = nullptr;  // (the kernel points it at its LDS)
   m.tcap = 0;
@@ -288,6 +296,52 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
       genotype_index(g, n, a, b);
       if (m.is_var[m.order[a]] || m.is_var[m.order[b]]) vsum = vsum + m.ll[g];
     }
+  } else if (G > 128) {
+    // (the deep kernels' scratch, past 128 genotypes) the same map order: every genotype's key
+    // in m.gkey, each variant genotype's rank by a scan over them, its likelihood to m.gsum[rank]
+    for (int a0 = 0; a0 < n; a0 += 64) {
+      const int a = a0 + lane;
+      const uint32_t h = allele_scala_hash(R, pile_entry(P, m.order[a < n ? a : 0]), pos);  // (every lane: shuffles)
+      if (a < n) m.tmp[a] = h;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      if (g < G) {
+        int a = 0, b = 0;
+        genotype_index(g, n, a, b);
+        const bool v = m.is_var[m.order[a]] || m.is_var[m.order[b]];
+        const uint64_t key = scala::trie_key(scala::genotype_hash(m.tmp[a], m.tmp[b]));
+        m.gkey[2 * g] = (uint32_t)key;
+        m.gkey[2 * g + 1] = (uint32_t)(key >> 32) | (v ? 0x80000000u : 0u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    bool tie = false;
+    int nvar = 0;
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      const bool vg = g < G && (m.gkey[2 * g + 1] & 0x80000000u);
+      if (vg) {
+        const uint64_t kg = (uint64_t)m.gkey[2 * g] | ((uint64_t)(m.gkey[2 * g + 1] & 0x7FFFFFFFu) << 32);
+        int r = 0;
+        for (int h = 0; h < G; ++h) {
+          const uint32_t hi = m.gkey[2 * h + 1];
+          if (!(hi & 0x80000000u)) continue;
+          const uint64_t kh = (uint64_t)m.gkey[2 * h] | ((uint64_t)(hi & 0x7FFFFFFFu) << 32);
+          if (kh < kg || (kh == kg && h < g)) ++r;
+          if (kh == kg && h != g) tie = true;
+        }
+        m.gsum[r] = m.ll[g];
+      }
+      nvar += __popcll(__ballot(vg));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int r = 0; r < nvar; ++r) vsum = vsum + m.gsum[r];
+    res.order_tie = __ballot(tie) != 0;
   } else {
     // HashTrieMap: ascending trie key of each genotype's Scala hash; equal keys (a full 32-bit
     // hash collision, a ListMap there) keep insertion order and are flagged.  G <= kMaxG = 128:
@@ -490,6 +544,8 @@ struct DeepIO {
   int64_t n_in;              // deep kernel: list length
   uint8_t *scratch;          // deep kernel: per-wave slices
   int scap, maxG;            // deep kernel: elements per sample per wave, genotypes
+  int64_t *wide;             // deep kernel: out, the candidates past its allele table (the wide kernel's)
+  unsigned long long wcap;   // its capacity
 };
 
 // One candidate with what its wave needs before the first search, gathered by cand_prep in list
@@ -766,7 +822,7 @@ struct ElemStore {
 
 // WPE: waves per SIMD the fast kernel's register budget must allow (3: 168 VGPRs and some
 // spills; 2: no spills; GQ_CALL_WPE picks, see gq_somatic_standard).  The deep kernel: 2.
-template <bool DEEP, bool BACK = false, int WPE = 3>
+template <bool DEEP, bool BACK = false, int WPE = 3, int NSD = kSlots>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : WPE))) void somatic_call_k(
     const CandRec *__restrict__ cands, DevReads RT, DevReads RN, gq_somatic_params prm, SomRec *__restrict__ recs,
     unsigned long long rec_cap,
@@ -779,7 +835,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   // amb_in != nullptr (deep kernel only): the listed loci with both samples' bases resolved
   // (amb_ref[2 i + set]).  ref.b != nullptr: every pileup's base is the reference genome's.
   constexpr int FW = kSomWaves;
-  constexpr int NS = DEEP ? kSlots : 1;  // allele-table slots: 64 NS distinct alleles per sample
+  constexpr int NS = DEEP ? NSD : 1;  // allele-table slots: 64 NS distinct alleles per sample
   __shared__ int32_t s_cov[DEEP ? 1 : FW][2][kFastCap];
   __shared__ uint4 s_el[DEEP ? 1 : FW][2][kFastCap];
   __shared__ uint32_t s_tmp[DEEP ? 1 : FW][2 * kFastCap];
@@ -793,7 +849,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
   const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
   CallMem m;
   if constexpr (DEEP) {
-    m = deep_mem(dio.scratch + (size_t)gwave * deep_wave_bytes(dio.scap, dio.maxG), dio.scap, dio.maxG);
+    m = deep_mem(dio.scratch + (size_t)gwave * deep_wave_bytes(dio.scap, dio.maxG, NS), dio.scap, dio.maxG, NS);
     m.terms = s_terms[wv];
     m.tcap = kDeepTermCap;
   } else {
@@ -805,6 +861,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.order = s_order[wv];
     m.is_var = s_var[wv];
     m.ll = s_ll[wv];
+    m.gkey = nullptr;
+    m.gsum = nullptr;
     m.terms = s_terms[wv];
     m.tcap = kFastCap;
     m.cap = kFastCap;
@@ -973,12 +1031,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     Pile<NS> &PT = PS[0], &PN = PS[1];
-    if (PT.overflow || PN.overflow) {
+    // more genotypes than this kernel's likelihood scratch holds (n eligible alleles: n (n + 1) / 2)
+    // also leave for the next kernel up
+    auto too_many_g = [&](const DevReads &R, const Pile<NS> &P) {
+      int n = 0;
+#pragma unroll
+      for (int t = 0; t < NS; ++t)
+        n += __popcll(__ballot((t * 64 + lane) < P.nt && P.n_f[t] > 0 && allele_std_alt(R, P.desc[t], pos)));
+      return n * (n + 1) / 2 > m.maxG;
+    };
+    if (PT.overflow || PN.overflow || too_many_g(RT, PT) || too_many_g(RN, PN)) {
       if constexpr (!DEEP) {  // more distinct alleles than the fast table: the deep kernel's
         if (lane == 0) {
           const unsigned long long k = atomicAdd(&ctr->n_deep, 1ull);
           if (k < dio.cap) dio.list[k] = it;
           atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
+        }
+      } else if (NS < kWideNS && !amb_in) {  // more than the deep table: the wide kernel's
+        if (lane == 0) {
+          const unsigned long long k = atomicAdd(&ctr->n_wide, 1ull);
+          if (k < dio.wcap) dio.wide[k] = it;
         }
       } else {
         raise_at(ctr, GQ_E_CAPACITY, pos);

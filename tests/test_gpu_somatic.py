@@ -176,3 +176,35 @@ def test_1000x_panel_over_several_tasks(gpu_ctx):
         got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
         want = O.somatic_standard(t, n, loci, **params)
         assert_rows_match(got, want)
+
+
+def _insertion_sample(n_distinct, n_alt, n_ref, start=100):
+    """n_distinct reads of distinct 6-base insertions (base quality 2, so the pileup's genotype
+    likelihoods stay above FP64 underflow), n_alt reads of one 7-base insertion and n_ref
+    reference reads: 10M kI 10M over a 20-base reference."""
+    ref = "ACGTTGCAACGGTACCATGA"
+    reads = []
+    for i in range(n_distinct):
+        ins = "".join("ACGT"[(i >> (2 * k)) & 3] for k in range(6))
+        reads.append(mr(ref[:10] + ins + ref[10:], "10M6I10M", "20", start, quals=[2] * 26, mapq=60))
+    reads += [mr(ref[:10] + "TTTTTTT" + ref[10:], "10M7I10M", "20", start, mapq=60)] * n_alt
+    reads += [mr(ref, "20M", "20", start, mapq=60)] * n_ref
+    reads.sort(key=lambda r: r["start"])
+    return make_read_set(reads)
+
+
+@pytest.mark.parametrize("n_tumor,n_normal", [(200, 0), (20, 20), (100, 40)])
+def test_more_alleles_than_the_deep_table(gpu_ctx, n_tumor, n_normal):
+    """A tumor pileup with 200 distinct insertion alleles (more than the deep kernel's 128-allele
+    table), and normals with 21-41 eligible alleles (more genotypes than its 128-genotype scratch:
+    the variant mass in HashTrieMap order over the wide kernel's scratch): the wide kernel
+    (somatic_call_k, 256 alleles per sample) calls them; rows equal the oracle's."""
+    t = _insertion_sample(n_tumor, 40, 100)
+    n = _insertion_sample(n_normal, 0, 60)
+    loci = _loci(t, "chr1:90-130")
+    for mode in (0, 1):
+        params = dict(apply_filters=mode)
+        got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
+        want = O.somatic_standard(t, n, loci, **params)
+        assert len(want) > 0
+        assert_rows_match(got, want)
