@@ -894,7 +894,7 @@ def somatic_parity_window(ctx, t, n, tg, ng, L: int, width: int):
     return {"loci": [w0, w1], "calls": len(want), "identical": bool(ok), "oracle_s": cpu_s}
 
 
-SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r04.json")
+SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r05.json")
 
 
 def somatic_pmc(workload: str, L: int, tdepth: float, ndepth: float):
