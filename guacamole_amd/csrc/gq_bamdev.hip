@@ -1481,6 +1481,10 @@ gq_status gq_bam_dev_load(gq_ctx *c, gq_bam_dev *mapped) {
       }
   }
   z.inflate_ms = ms_since(t0);
+  // the compressed bytes and the inflate tables are not read again (a later load re-uploads):
+  // their HBM goes back before the scan and the SoA fill allocate (the load's peak)
+  b->comp.release();
+  b->scratch.release();
   return GQ_OK;
 }
 
