@@ -296,7 +296,9 @@ def main() -> int:
             return None
         if tr.get("length") != args.length or tr.get("depth") != args.depth or world != 1:
             return None
-        return tr.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        ks = tr.get("kernels", {})  # (named with template arguments: "proj_fill_cells<4>")
+        k = next((k for k in sorted(ks) if k == kernel or k.startswith(kernel + "<")), None)
+        return ks[k].get("hbm_bytes_per_launch") if k else None
     traffic = pmc_traffic("germline_proj")
     # the step's dominant kernel: the projection fill (read-major fill under GQ_FILL=rw).  Its
     # algorithmic bytes: each projected read's bases over its span read once (sum of end - start)
