@@ -1875,7 +1875,7 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       // waves, each with a large scratch slice
       const int scap = (int)std::max<unsigned long long>(hc.deep_max, (unsigned long long)kFastCap);
       const int maxg = 64 * kWideNS * (64 * kWideNS + 1) / 2;
-      const int64_t nw = std::min<int64_t>((int64_t)hc.n_wide, 64);
+      const int64_t nw = std::min<int64_t>((int64_t)hc.n_wide, 16);  // (12.6 MB of genotype scratch per wave)
       const size_t wb = deep_wave_bytes(scap, maxg, kWideNS);
       HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
       HIP_TRY(hipEventRecord(c->ev[5], c->stream));

@@ -19,19 +19,20 @@
 #pragma once
 
 constexpr int kFastCap = 128;      // elements per sample held in LDS by the fast kernel
-constexpr int kWideNS = 4;         // the wide kernel's allele-table slots: 256 distinct alleles per sample
+constexpr int kRankScanMaxG = 256 * 257 / 2;  // normal genotypes ranked in HashTrieMap order (256 eligible alleles)
+constexpr int kWideNS = 16;        // the wide kernel's allele-table slots: 1024 distinct alleles per sample
 constexpr int kDeepTermCap = 256;  // deep kernel: elements per LDS chunk of the likelihood fold
 
 // Element record (16 bytes), one per covering read in pileup element order:
 //   x  rp    read position of the element (SNV / DEL: its base; INS: its first alt byte)
 //   y  aux   INS: alt bytes; DEL: deleted length
 //   z  base | kind << 8 | quality (as a signed byte) << 16 | mapq << 24
-//   w  n_mismatch | flags << 16 | table index << 24
+//   w  n_mismatch | flags (3 bits) << 16 | allele-table index (13 bits) << 19
 constexpr uint32_t kElAct = 1u, kElPass = 2u, kElFwd = 4u;
 __device__ __forceinline__ int el_q(const uint4 &e) { return (int)(int8_t)(uint8_t)(e.z >> 16); }
 __device__ __forceinline__ int el_mq(const uint4 &e) { return (int)(e.z >> 24); }
-__device__ __forceinline__ uint32_t el_flags(const uint4 &e) { return (e.w >> 16) & 0xFFu; }
-__device__ __forceinline__ int el_tidx(const uint4 &e) { return (int)(e.w >> 24); }
+__device__ __forceinline__ uint32_t el_flags(const uint4 &e) { return (e.w >> 16) & 0x7u; }
+__device__ __forceinline__ int el_tidx(const uint4 &e) { return (int)(e.w >> 19); }
 
 // One element's three possible log terms (log(2(1 - pc)), log(pc + (1 - pc)), log(2 pc); 0 when
 // the mapq filter drops it) and its allele-table index: one 32-byte LDS record per element.
@@ -296,6 +297,8 @@ __device__ __forceinline__ GenoOut genotypes_el(const DevReads &R, const Pile<NS
       genotype_index(g, n, a, b);
       if (m.is_var[m.order[a]] || m.is_var[m.order[b]]) vsum = vsum + m.ll[g];
     }
+  } else if (G > kRankScanMaxG) {  // (the rank scan below is quadratic in G)
+    raise_at(ctr, GQ_E_CAPACITY, pos);
   } else if (G > 128) {
     // (the deep kernels' scratch, past 128 genotypes) the same map order: every genotype's key
     // in m.gkey, each variant genotype's rank by a scan over them, its likelihood to m.gsum[rank]
@@ -1025,7 +1028,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
           }
           pending &= ~mb;
         }
-        if (act && mine >= 0) m.el[s][k].w = (e.w & 0x00FFFFFFu) | ((uint32_t)mine << 24);
+        if (act && mine >= 0) m.el[s][k].w = (e.w & 0x0007FFFFu) | ((uint32_t)mine << 19);
       }
     }
     __builtin_amdgcn_wave_barrier();

@@ -193,12 +193,12 @@ def _insertion_sample(n_distinct, n_alt, n_ref, start=100):
     return make_read_set(reads)
 
 
-@pytest.mark.parametrize("n_tumor,n_normal", [(200, 0), (20, 20), (100, 40)])
+@pytest.mark.parametrize("n_tumor,n_normal", [(200, 0), (20, 20), (100, 40), (700, 0)])
 def test_more_alleles_than_the_deep_table(gpu_ctx, n_tumor, n_normal):
-    """A tumor pileup with 200 distinct insertion alleles (more than the deep kernel's 128-allele
-    table), and normals with 21-41 eligible alleles (more genotypes than its 128-genotype scratch:
-    the variant mass in HashTrieMap order over the wide kernel's scratch): the wide kernel
-    (somatic_call_k, 256 alleles per sample) calls them; rows equal the oracle's."""
+    """Tumor pileups with 200 and 700 distinct insertion alleles (more than the deep kernel's
+    128-allele table), and normals with 21-41 eligible alleles (more genotypes than its
+    128-genotype scratch: the variant mass in HashTrieMap order over the wide kernel's scratch):
+    the wide kernel (somatic_call_k, 1024 alleles per sample) calls them; rows equal the oracle's."""
     t = _insertion_sample(n_tumor, 40, 100)
     n = _insertion_sample(n_normal, 0, 60)
     loci = _loci(t, "chr1:90-130")
