@@ -1280,6 +1280,12 @@ struct gq_dev_reads {
   float fill_ms = 0;               // its pool fill kernel(s), HIP events on the context's stream
   float proj_dev_ms = 0;           // its device span (first kernel to last), HIP events
   float derive_dev_ms = 0;         // the upload-time derivation's device span, HIP events
+  // A re-derivation does not wait for its spans: their events (derive start / end, projection
+  // start, fill start / end, projection end) and the taken-read counters are read when the
+  // figures are asked for (gq_reads_get_info) or before the next re-derivation (settle_stats).
+  hipEvent_t tev[6] = {};
+  unsigned pending = 0;            // 1: derivation span, 2: projection span, fill and proj_reads
+  unsigned long long *nok = nullptr;  // proj_prep's spread counters (kOkSpread words) while pending & 2
   mutable void *mproj = nullptr;  // somatic margin projection (a biased byte per locus-read), for mproj_mapq
   mutable int mproj_mapq = -1;
   mutable void *mnb = nullptr;    // per slice: 1 if a margin term there is kMargin8None (no bound)

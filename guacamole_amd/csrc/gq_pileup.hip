@@ -1964,8 +1964,31 @@ static gq_status validate_reads(const gq_reads *h) {
   return GQ_OK;
 }
 
-static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
-  HIP_TRY(hipEventRecord(c->dev_ev[2], c->stream));
+// The spans a re-derivation recorded without waiting (gq_dev_reads::pending): wait for them now.
+static gq_status settle_stats(gq_dev_reads *d) {
+  if (d->pending & 1) {
+    HIP_TRY(hipEventSynchronize(d->tev[1]));
+    (void)hipEventElapsedTime(&d->derive_dev_ms, d->tev[0], d->tev[1]);
+  }
+  if (d->pending & 2) {
+    HIP_TRY(hipEventSynchronize(d->tev[5]));
+    (void)hipEventElapsedTime(&d->fill_ms, d->tev[3], d->tev[4]);
+    (void)hipEventElapsedTime(&d->proj_dev_ms, d->tev[2], d->tev[5]);
+    std::vector<unsigned long long> hk(kOkSpread);
+    HIP_TRY(hipMemcpy(hk.data(), d->nok, sizeof(unsigned long long) * kOkSpread, hipMemcpyDeviceToHost));
+    d->proj_reads = 0;
+    for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
+    d->dp.put(d->nok);
+    d->nok = nullptr;
+  }
+  d->pending = 0;
+  return GQ_OK;
+}
+
+static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, bool lazy = false) {
+  for (hipEvent_t &e : d->tev)
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventRecord(d->tev[0], c->stream));
   {  // contig_read_begin: 0, non-decreasing, n_reads (host copy)
     const auto &b = d->contig_read_begin;
     bool ok = !b.empty() && b.front() == 0 && b.back() == d->d.n_reads;
@@ -2084,10 +2107,14 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len) {
   }
   d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
   nnb = nullptr;
-  HIP_TRY(hipEventRecord(c->dev_ev[3], c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipEventElapsedTime(&d->derive_dev_ms, c->dev_ev[2], c->dev_ev[3]);
+  HIP_TRY(hipEventRecord(d->tev[1], c->stream));
   d->d.pool_ordered = unordered ? 0 : 1;
+  if (lazy) {  // (a re-derivation: the caller's next call goes on behind it on the stream)
+    d->pending |= 1;
+    return GQ_OK;
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&d->derive_dev_ms, d->tev[0], d->tev[1]);
   return GQ_OK;
 }
 
@@ -2306,6 +2333,10 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));  // nothing queued may still read the derived buffers
   HIP_TRY(hipStreamSynchronize(c->side));
+  {
+    const gq_status s0 = settle_stats(d);
+    if (s0) return s0;
+  }
   d->dp.release_all();
   DevReads &R = d->d;
   R.lead = nullptr;
@@ -2324,13 +2355,19 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   d->proj_bytes = d->pev_count = d->proj_reads = d->n_rows = d->n_slices = 0;
   d->proj_ms = 0;
   const auto t1 = std::chrono::steady_clock::now();
-  const gq_status st = derive_shape_impl(c, d, R.md_len);
+  const gq_status st = derive_shape_impl(c, d, R.md_len, true);
   d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
   return st;
 }
 
-gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
-  if (!d || !out) return set_err(GQ_E_ARG, "gq_reads_get_info: null argument");
+gq_status gq_reads_get_info(const gq_dev_reads *dc, gq_reads_info *out) {
+  if (!dc || !out) return set_err(GQ_E_ARG, "gq_reads_get_info: null argument");
+  gq_dev_reads *d = const_cast<gq_dev_reads *>(dc);  // (settling the pending spans fills cached figures)
+  if (d->pending) {
+    HIP_TRY(hipSetDevice(d->ctx->device));
+    const gq_status s0 = settle_stats(d);
+    if (s0) return s0;
+  }
   out->n_reads = d->d.n_reads;
   out->seq_bytes = d->seq_bytes;
   out->proj_bytes = d->proj_bytes;
@@ -2353,6 +2390,12 @@ gq_status gq_reads_get_info(const gq_dev_reads *d, gq_reads_info *out) {
 
 void gq_reads_free(gq_dev_reads *d) {
   if (!d) return;
+  if (d->ctx) (void)hipSetDevice(d->ctx->device);
+  for (hipEvent_t e : d->tev)
+    if (e) {
+      (void)hipEventSynchronize(e);
+      (void)hipEventDestroy(e);
+    }
   for (void *p : d->owned) (void)hipFree(p);
   d->dp.free_all();  // every derived structure, margin projection included
   delete d;
@@ -3108,7 +3151,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   void *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
        *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
   HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
-  HIP_TRY(hipEventRecord(c->dev_ev[2], c->stream));
+  HIP_TRY(hipEventRecord(d->tev[2], c->stream));
   const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
   // the records, the slices a read the projection cannot take touches (pbad), the sparse entries
   // per read and the reads taken, in one pass
@@ -3116,7 +3159,6 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
   HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
   unsigned long long *nok = nullptr;
-  std::vector<unsigned long long> hk(kOkSpread);
   HIP_TRY(d->dp.get((void **)&nok, sizeof(unsigned long long) * kOkSpread));
   HIP_TRY(hipMemsetAsync(nok, 0, sizeof(unsigned long long) * kOkSpread, c->stream));
   hipLaunchKernelGGL(proj_prep, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (ProjRec *)pr,
@@ -3195,7 +3237,7 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->side_ev[3], c->side));
-  HIP_TRY(hipEventRecord(c->dev_ev[0], c->stream));
+  HIP_TRY(hipEventRecord(d->tev[3], c->stream));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
     if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
@@ -3237,21 +3279,15 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
     }
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(c->dev_ev[1], c->stream));
+  HIP_TRY(hipEventRecord(d->tev[4], c->stream));
   HIP_TRY(hipStreamWaitEvent(c->stream, c->side_ev[3], 0));  // (the sparse entries done)
-  HIP_TRY(hipEventRecord(c->dev_ev[3], c->stream));
+  HIP_TRY(hipEventRecord(d->tev[5], c->stream));
   d->proj_bytes = kProjRowBytes * tot[0];
   d->pev_count = tot[1];
-  {  // reads the projection takes (counted by proj_prep)
-    HIP_TRY(hipMemcpyAsync(hk.data(), nok, sizeof(unsigned long long) * kOkSpread, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    d->dp.put(nok);
-    d->proj_reads = 0;
-    for (unsigned long long x : hk) d->proj_reads += (int64_t)x;
-  }
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipEventElapsedTime(&d->fill_ms, c->dev_ev[0], c->dev_ev[1]);
-  (void)hipEventElapsedTime(&d->proj_dev_ms, c->dev_ev[2], c->dev_ev[3]);
+  // the reads the projection takes (proj_prep's counters) and the spans: read when asked for
+  // (settle_stats), so the call behind the projection is queued without a host round trip
+  d->nok = nok;
+  d->pending |= 2;
   d->projected = true;
   d->proj_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return GQ_OK;
