@@ -409,12 +409,18 @@ __device__ __forceinline__ int32_t slice_rows_fifo(const DevReads &R, const Slic
   if (lane < 32) hist[lane] = 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // pass 1: a histogram of the pieces' end columns (1..16) and the piece count
+  // pass 1: a histogram of the pieces' end columns (1..16) and the piece count (the first
+  // batch's pieces kept for pass 2: most windows are one batch)
   int32_t n = 0;
+  int32_t s0_first = W.qc0, sl_first = 0;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
     int32_t s0 = W.qc0, sl = 0;
     if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    if (r0 == W.ra) {
+      s0_first = s0;
+      sl_first = sl;
+    }
     if (sl > 0) atomicAdd(&hist[s0 - W.qc0 + sl], 1u);
     n += (int32_t)__popcll(__ballot(sl > 0));
   }
@@ -427,8 +433,12 @@ __device__ __forceinline__ int32_t slice_rows_fifo(const DevReads &R, const Slic
   int32_t runmin = kInf, base = 0;
   for (int64_t r0 = W.ra; r0 < W.rz; r0 += 64) {
     const int64_t r = r0 + lane;
-    int32_t s0 = W.qc0, sl = 0;
-    if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    int32_t s0 = s0_first, sl = sl_first;
+    if (r0 != W.ra) {  // (uniform: later batches load their pieces again)
+      s0 = W.qc0;
+      sl = 0;
+      if (r < W.rz) slice_piece(R, r, W.qc0, s0, sl);
+    }
     const bool has = sl > 0;
     const int32_t c0 = has ? s0 - W.qc0 : 0, c1 = c0 + sl;
     const unsigned long long hm = __ballot(has);
