@@ -246,14 +246,24 @@ __device__ __forceinline__ SliceWin slice_window(const DevReads &R, int64_t slot
   const int32_t q = (int32_t)(slot - R.qoff[c]);
   const int32_t L = 128 * q;
   const int64_t cb = R.contig_read_begin[c], ce = R.contig_read_begin[c + 1];
+  // the block index (block_index: per 512-locus block g, the first read with pmax_end past its
+  // start and the first read starting in or after it) bounds both searches to the block's reads:
+  // ra >= blk_rb[g] (L is past the block's start) and every window read starts before the next
+  // block's first read, blk_rs[g + 1] (the contig's end for its last block)
   int64_t a0 = cb, a1 = ce;
+  if (R.blk_rb) {
+    const int64_t g = slot >> 2;  // (qoff[c] is a multiple of 4: slot / 4 is the global block)
+    a0 = R.blk_rb[g];
+    if (((slot >> 2) + 1) < (R.qoff[c + 1] >> 2)) a1 = R.blk_rs[g + 1];
+  }
+  const int64_t hi0 = a1;
   while (a0 < a1) {  // first read with pmax_end > L
     const int64_t m = (a0 + a1) >> 1;
     if (R.pmax_end[m] > L) a1 = m;
     else a0 = m + 1;
   }
   const int64_t ra = a0;
-  a1 = ce;
+  a1 = hi0;
   while (a0 < a1) {  // first read with start >= L + 128
     const int64_t m = (a0 + a1) >> 1;
     if (R.start[m] >= L + 128) a1 = m;

@@ -38,6 +38,13 @@
 
 using namespace gq;
 
+// Per-read counts are 32-bit; their scans widen them to 64-bit offsets on the fly (half the
+// bytes the scan reads).
+struct WidenU32 {
+  __host__ __device__ __forceinline__ int64_t operator()(uint32_t x) const { return (int64_t)x; }
+};
+typedef hipcub::TransformInputIterator<int64_t, WidenU32, const uint32_t *> U32Widen;
+
 namespace gq {
 thread_local std::string g_err;
 
@@ -260,7 +267,7 @@ __device__ __forceinline__ bool col_base_ok(const DevReads &R, int64_t r) {
 }
 
 // Words of each read's auxiliary list (MD events, then two per segment of a general read).
-__global__ void col_count(DevReads R, int64_t *__restrict__ n_aux) {
+__global__ void col_count(DevReads R, uint32_t *__restrict__ n_aux) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R.n_reads) return;
   if (r == R.n_reads) {
@@ -271,7 +278,7 @@ __global__ void col_count(DevReads R, int64_t *__restrict__ n_aux) {
   if (R.lead[r] < 0 && col_base_ok(R, r) &&
       !general_segments(R, r, [&](uint32_t, int32_t, int32_t, int32_t, int32_t) { ++nseg; }))
     nseg = 0;
-  n_aux[r] = (int64_t)(R.n_md[r] > 0 ? R.n_md[r] : 0) + 2 * nseg;
+  n_aux[r] = (uint32_t)(R.n_md[r] > 0 ? R.n_md[r] : 0) + 2u * (uint32_t)nseg;
 }
 
 // The packed ColDesc of each read and its auxiliary list at aux_off[r]: one u32 per MD event
@@ -342,7 +349,7 @@ __global__ void slice_windows(DevReads R, int64_t n_slices, int64_t *__restrict_
 // entries per read (proj_count) and the reads it takes, counted into kSpread words (proj_count_ok).
 constexpr int kOkSpread = 1024;  // proj_prep's count words (summed on the host)
 __global__ void proj_prep(DevReads R, const uint32_t *__restrict__ n_nbase, ProjRec *__restrict__ prec,
-                          uint8_t *__restrict__ pbad, int64_t *__restrict__ nents, unsigned long long *__restrict__ n_ok) {
+                          uint8_t *__restrict__ pbad, uint32_t *__restrict__ nents, unsigned long long *__restrict__ n_ok) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   ProjRec p{0, 0};
   int64_t e = 0;
@@ -375,7 +382,7 @@ __global__ void proj_prep(DevReads R, const uint32_t *__restrict__ n_nbase, Proj
   }
   if (r <= R.n_reads) {
     prec[r] = p;
-    nents[r] = e;
+    nents[r] = (uint32_t)e;
   }
   // the block's count: one LDS add per wave, one global add per block, spread over kOkSpread words
   __shared__ unsigned long long s_ok;
@@ -2083,14 +2090,15 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     HIP_TRY(d->dp.get(&cd, ncd));
     HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
     HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
-    HIP_TRY(d->dp.get((void **)&na, sizeof(int64_t) * (size_t)(n + 1)));
+    HIP_TRY(d->dp.get((void **)&na, sizeof(uint32_t) * (size_t)(n + 1)));
     const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int64_t *)na);
+    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint32_t *)na);
     HIP_TRY(hipGetLastError());
     size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    const U32Widen na64((const uint32_t *)na, WidenU32());  // (32-bit counts, 64-bit offsets)
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, na64, (int64_t *)ao, (int)(n + 1), c->stream));
     HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)na, (int64_t *)ao, (int)(n + 1), c->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, na64, (int64_t *)ao, (int)(n + 1), c->stream));
     d->dp.put(tmp);
     d->dp.put(na);
     const int64_t aux_bound = std::max<int64_t>(md_len, 0) + 6 * std::max<int64_t>(d->d.cigar_len, 0);
@@ -3157,12 +3165,12 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   // per read and the reads taken, in one pass
   HIP_TRY(d->dp.get(&pbd, (size_t)n_sl + 16));
   HIP_TRY(hipMemsetAsync(pbd, 0, (size_t)n_sl + 16, c->stream));
-  HIP_TRY(d->dp.get((void **)&ne, sizeof(int64_t) * (size_t)(n + 1)));
+  HIP_TRY(d->dp.get((void **)&ne, sizeof(uint32_t) * (size_t)(n + 1)));
   unsigned long long *nok = nullptr;
   HIP_TRY(d->dp.get((void **)&nok, sizeof(unsigned long long) * kOkSpread));
   HIP_TRY(hipMemsetAsync(nok, 0, sizeof(unsigned long long) * kOkSpread, c->stream));
   hipLaunchKernelGGL(proj_prep, dim3(nb1), dim3(kBlock), 0, c->stream, d->d, (const uint32_t *)d->nnb, (ProjRec *)pr,
-                     (uint8_t *)pbd, (int64_t *)ne, nok);
+                     (uint8_t *)pbd, (uint32_t *)ne, nok);
   HIP_TRY(hipGetLastError());
   d->d.prec = (const ProjRec *)pr;
   // each slice's read window and the offsets of its reads' rows
@@ -3203,10 +3211,11 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   HIP_TRY(d->dp.get(&eo, sizeof(int64_t) * (size_t)(n + 1)));
   size_t tb = 0, tb2 = 0;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+  const U32Widen ne64((const uint32_t *)ne, WidenU32());  // (32-bit counts, 64-bit offsets)
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, ne64, (int64_t *)eo, (int)(n + 1), c->stream));
   HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, (const int64_t *)ne, (int64_t *)eo, (int)(n + 1), c->stream));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ne64, (int64_t *)eo, (int)(n + 1), c->stream));
   int64_t tot[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
