@@ -38,12 +38,112 @@
 
 using namespace gq;
 
-// Per-read counts are 32-bit; their scans widen them to 64-bit offsets on the fly (half the
-// bytes the scan reads).
-struct WidenU32 {
-  __host__ __device__ __forceinline__ int64_t operator()(uint32_t x) const { return (int64_t)x; }
-};
-typedef hipcub::TransformInputIterator<int64_t, WidenU32, const uint32_t *> U32Widen;
+// ---- Exclusive scan of 32-bit per-read counts into 64-bit offsets (reduce, then scan) ------
+// Tiles of 4096 counts (256 threads x 16 consecutive counts): tile sums, one workgroup scanning
+// the tile sums, then each tile scanned again from its offset.  Reads the counts twice and
+// writes the offsets once.
+namespace {
+constexpr int kScanT = 256, kScanV = 16, kScanTile = kScanT * kScanV;
+
+__device__ __forceinline__ void scan_load16(const uint32_t *__restrict__ in, int64_t n, int64_t i0, uint32_t (&v)[kScanV]) {
+  if (i0 + kScanV <= n) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(in + i0);
+#pragma unroll
+    for (int k = 0; k < kScanV / 4; ++k) {
+      const uint4 w = p[k];
+      v[4 * k] = w.x, v[4 * k + 1] = w.y, v[4 * k + 2] = w.z, v[4 * k + 3] = w.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k) v[k] = i0 + k < n ? in[i0 + k] : 0u;
+  }
+}
+// Exclusive prefix of x over the workgroup's kScanT threads (LDS, Hillis-Steele); *total: the sum.
+__device__ __forceinline__ int64_t block_excl_i64(int64_t x, int64_t *lds, int64_t *total) {
+  const int t = threadIdx.x;
+  lds[t] = x;
+  __syncthreads();
+  for (int d = 1; d < kScanT; d <<= 1) {
+    const int64_t y = t >= d ? lds[t - d] : 0;
+    __syncthreads();
+    lds[t] += y;
+    __syncthreads();
+  }
+  const int64_t incl = lds[t];
+  if (total) *total = lds[kScanT - 1];
+  __syncthreads();
+  return incl - x;
+}
+__global__ __launch_bounds__(kScanT) void scan_tile_sums(const uint32_t *__restrict__ in, int64_t n,
+                                                         int64_t *__restrict__ sums) {
+  __shared__ int64_t lds[kScanT];
+  uint32_t v[kScanV];
+  scan_load16(in, n, (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanV, v);
+  int64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanV; ++k) x += v[k];
+  int64_t tot = 0;
+  (void)block_excl_i64(x, lds, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+// One workgroup: sums[0 .. nt) -> their exclusive prefix, in place.
+__global__ __launch_bounds__(kScanT) void scan_sums_excl(int64_t *__restrict__ sums, int64_t nt) {
+  __shared__ int64_t lds[kScanT];
+  const int64_t per = (nt + kScanT - 1) / kScanT;
+  const int64_t a = (int64_t)threadIdx.x * per, b = a + per < nt ? a + per : nt;
+  int64_t x = 0;
+  for (int64_t i = a; i < b; ++i) x += sums[i];
+  int64_t run = block_excl_i64(x, lds, nullptr);
+  for (int64_t i = a; i < b; ++i) {
+    const int64_t y = sums[i];
+    sums[i] = run;
+    run += y;
+  }
+}
+__global__ __launch_bounds__(kScanT) void scan_tiles(const uint32_t *__restrict__ in, int64_t n,
+                                                     const int64_t *__restrict__ base, int64_t *__restrict__ out) {
+  __shared__ int64_t lds[kScanT];
+  const int64_t i0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanV;
+  uint32_t v[kScanV];
+  scan_load16(in, n, i0, v);
+  int64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanV; ++k) x += v[k];
+  int64_t run = base[blockIdx.x] + block_excl_i64(x, lds, nullptr);
+  int64_t o[kScanV];
+#pragma unroll
+  for (int k = 0; k < kScanV; ++k) {
+    o[k] = run;
+    run += v[k];
+  }
+  if (i0 + kScanV <= n) {
+    int4 *q = reinterpret_cast<int4 *>(out + i0);
+#pragma unroll
+    for (int k = 0; k < kScanV / 2; ++k)
+      q[k] = make_int4((int)(uint32_t)o[2 * k], (int)(uint32_t)((uint64_t)o[2 * k] >> 32), (int)(uint32_t)o[2 * k + 1],
+                       (int)(uint32_t)((uint64_t)o[2 * k + 1] >> 32));
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k)
+      if (i0 + k < n) out[i0 + k] = o[k];
+  }
+}
+}  // namespace
+
+// out[i] = in[0] + ... + in[i - 1] for i < n (in and out 16-byte aligned).
+static hipError_t scan_u32_to_i64(DerivedPool &dp, const uint32_t *in, int64_t *out, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nt = (n + kScanTile - 1) / kScanTile;
+  void *sums = nullptr;
+  hipError_t e = dp.get(&sums, sizeof(int64_t) * (size_t)nt);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(scan_tile_sums, dim3((unsigned)nt), dim3(kScanT), 0, st, in, n, (int64_t *)sums);
+  hipLaunchKernelGGL(scan_sums_excl, dim3(1), dim3(kScanT), 0, st, (int64_t *)sums, nt);
+  hipLaunchKernelGGL(scan_tiles, dim3((unsigned)nt), dim3(kScanT), 0, st, in, n, (const int64_t *)sums, out);
+  e = hipGetLastError();
+  dp.put(sums);
+  return e;
+}
 
 namespace gq {
 thread_local std::string g_err;
@@ -2094,12 +2194,7 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint32_t *)na);
     HIP_TRY(hipGetLastError());
-    size_t tb = 0;
-    const U32Widen na64((const uint32_t *)na, WidenU32());  // (32-bit counts, 64-bit offsets)
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, na64, (int64_t *)ao, (int)(n + 1), c->stream));
-    HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, na64, (int64_t *)ao, (int)(n + 1), c->stream));
-    d->dp.put(tmp);
+    HIP_TRY(scan_u32_to_i64(d->dp, (const uint32_t *)na, (int64_t *)ao, n + 1, c->stream));
     d->dp.put(na);
     const int64_t aux_bound = std::max<int64_t>(md_len, 0) + 6 * std::max<int64_t>(d->d.cigar_len, 0);
     const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_bound, 1) + 1024;
@@ -3209,13 +3304,11 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
                      (const int32_t *)sc, (int64_t *)br);
   HIP_TRY(hipGetLastError());
   HIP_TRY(d->dp.get(&eo, sizeof(int64_t) * (size_t)(n + 1)));
-  size_t tb = 0, tb2 = 0;
+  size_t tb = 0;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-  const U32Widen ne64((const uint32_t *)ne, WidenU32());  // (32-bit counts, 64-bit offsets)
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, ne64, (int64_t *)eo, (int)(n + 1), c->stream));
-  HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(std::max(tb, tb2), 16)));
+  HIP_TRY(d->dp.get((void **)&tmp, std::max<size_t>(tb, 16)));
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, (const int64_t *)br, (int64_t *)sb, (int)(n_sl + 1), c->stream));
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, ne64, (int64_t *)eo, (int)(n + 1), c->stream));
+  HIP_TRY(scan_u32_to_i64(d->dp, (const uint32_t *)ne, (int64_t *)eo, n + 1, c->stream));
   int64_t tot[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(&tot[0], (int64_t *)sb + n_sl, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(&tot[1], (int64_t *)eo + n, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
