@@ -411,12 +411,22 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
   d.seq_lo = (uint32_t)(uint64_t)(R.seq_off[r] + (lead > 0 ? lead : 0));
   d.md_lo = (uint32_t)(uint64_t)aux_off[r];
   cd[r] = d;
-  if (nmd > 0) {
+  if (nmd > 0) {  // four events per round of loads (past the last: the last again)
     const uint32_t *ev = R.md_ev + R.md_off[r];
     const uint8_t *rb = R.ev_rb + R.md_off[r];
-    for (int32_t k = 0; k < nmd; ++k) {
-      const uint32_t off = ev[k] >> 8;
-      o[k] = off < 32768u ? (off << 16) | ((ev[k] & 0xFFu) << 8) | rb[k] : 0xFFFFFFFFu;
+    for (int32_t k0 = 0; k0 < nmd; k0 += 4) {
+      uint32_t e4[4], b4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t k = k0 + j < nmd ? k0 + j : nmd - 1;
+        e4[j] = ev[k];
+        b4[j] = rb[k];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = e4[j] >> 8;
+        if (k0 + j < nmd) o[k0 + j] = off < 32768u ? (off << 16) | ((e4[j] & 0xFFu) << 8) | b4[j] : 0xFFFFFFFFu;
+      }
     }
   }
 }
