@@ -931,8 +931,14 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
   int32_t ld = 0, mlen = 0;
   int mi = -1;
   bool simple = n > 0;
+  // the first four operations in one round of loads (past the last: the last again)
+  uint32_t c4[4] = {0u, 0u, 0u, 0u};
+  if (n > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c4[j] = R.cigar[off + (j < n ? j : n - 1)];
+  }
   for (int k = 0; k < n && simple; ++k) {
-    const uint32_t c = R.cigar[off + k];
+    const uint32_t c = k < 4 ? (k == 0 ? c4[0] : k == 1 ? c4[1] : k == 2 ? c4[2] : c4[3]) : R.cigar[off + k];
     const int op = (int)(c & 15u);
     if (op == OP_M || op == OP_EQ || op == OP_X) {
       if (mi >= 0) simple = false;
@@ -953,10 +959,21 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
   uint8_t *rb = ev_rb + R.md_off[r];
   if (simple) {  // [S|H]* (M|=|X) [S|H]*: the event at reference offset o reads base lead + o
     const int64_t so = R.seq_off[r];
-    const int32_t sl = R.seq_len[r];
-    for (int k = 0; k < nmd; ++k) {
-      const int32_t o = (int32_t)(ev[k] >> 8);
-      rb[k] = (o < mlen && ld + o < sl) ? R.seq[so + ld + o] : (uint8_t)0;
+    const int32_t sl = R.seq_len[r];  // (>= ld + mlen >= 1: a simple read has bases)
+    for (int k0 = 0; k0 < nmd; k0 += 4) {  // four events, then their bases, per round of loads
+      uint32_t o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = ev[k0 + j < nmd ? k0 + j : nmd - 1] >> 8;
+      uint8_t b4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool in = (int32_t)o4[j] < mlen && ld + (int32_t)o4[j] < sl;
+        b4[j] = R.seq[in ? so + ld + (int32_t)o4[j] : so];
+        b4[j] = in ? b4[j] : (uint8_t)0;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k0 + j < nmd) rb[k0 + j] = b4[j];
     }
     return;
   }
@@ -2133,10 +2150,12 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     // touches only the pool and seq_off, and a pool in another order (flag bit 4) redoes it per read
     HIP_TRY(hipEventRecord(c->side_ev[0], c->stream));
     HIP_TRY(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
-    HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, c->side));
+    static const bool clean_serial = getenv("GQ_CLEAN_SERIAL") != nullptr;  // A/B: on the main stream, first
+    hipStream_t cs = clean_serial ? c->stream : c->side;
+    HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, cs));
     const int64_t chunks = (d->d.seq_bytes + 15) / 16;
     if (chunks > 0)
-      hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, c->side,
+      hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, cs,
                          d->d, (uint8_t *)cl, (uint32_t *)nnb);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->side_ev[1], c->side));
