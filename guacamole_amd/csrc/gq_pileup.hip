@@ -841,16 +841,22 @@ __device__ __forceinline__ int validate_one(const DevReads &R, int64_t r) {
     if (R.contig_read_begin[m] <= r) lo = m;
     else hi = m - 1;
   }
+  // every field in one round of loads (read r - 1's as read 0's own for r = 0), then the tests
+  // without short-circuits (a load behind a || would wait for the one before)
+  const int64_t rp = r > 0 ? r - 1 : r;
   const bool first = R.contig_read_begin[lo] == r;
-  const int32_t s = R.start[r], e = R.end[r], pm = R.pmax_end[r];
+  const int32_t s = R.start[r], e = R.end[r], pm = R.pmax_end[r], s1 = R.start[rp], pm1 = R.pmax_end[rp];
+  const int64_t so = R.seq_off[r], so1 = R.seq_off[rp], co = R.cigar_off[r], mo = R.md_off[r];
+  const int32_t sl = R.seq_len[r], sl1 = R.seq_len[rp], nc = R.n_cigar[r], nm = R.n_md[r];
+  const int smp = (int)R.sample[r];
   int b = 0;
-  if (e < s || s < 0) b |= 1;
-  if (first ? pm != e : (s < R.start[r - 1] || pm != max(R.pmax_end[r - 1], e))) b |= 1;
-  if (R.seq_off[r] < 0 || R.seq_len[r] < 0 || R.seq_off[r] + R.seq_len[r] > R.seq_bytes) b |= 2;
-  if (R.cigar_off[r] < 0 || R.n_cigar[r] < 0 || R.cigar_off[r] + R.n_cigar[r] > R.cigar_len) b |= 2;
-  if (R.n_md[r] > 0 && (R.md_off[r] < 0 || R.md_off[r] + R.n_md[r] > R.md_len)) b |= 2;
-  if ((int)R.sample[r] >= R.n_samples) b |= 2;
-  if (r > 0 && R.seq_off[r] < R.seq_off[r - 1] + R.seq_len[r - 1]) b |= 4;
+  b |= (e < s) | (s < 0) ? 1 : 0;
+  b |= (first ? pm != e : ((s < s1) | (pm != max(pm1, e)))) ? 1 : 0;
+  b |= (so < 0) | (sl < 0) | (so + sl > R.seq_bytes) ? 2 : 0;
+  b |= (co < 0) | (nc < 0) | (co + nc > R.cigar_len) ? 2 : 0;
+  b |= (nm > 0) & ((mo < 0) | (mo + nm > R.md_len)) ? 2 : 0;
+  b |= smp >= R.n_samples ? 2 : 0;
+  b |= (r > 0) & (so < so1 + sl1) ? 4 : 0;
   return b;
 }
 
@@ -925,18 +931,29 @@ __global__ void read_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
 // [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
 __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t *__restrict__ lead,
-                                          uint8_t *__restrict__ ev_rb) {
+                                          uint8_t *__restrict__ ev_rb, bool bad) {
+  // a read whose offsets lie outside their pools (bad) reads nothing: n = nmd = 0
   const int64_t off = R.cigar_off[r];
-  const int32_t n = R.n_cigar[r];
+  const int32_t n = bad ? 0 : R.n_cigar[r];
+  const int32_t nmd = bad ? 0 : R.n_md[r];
+  const int64_t mdo = R.md_off[r];
+  // the first four CIGAR operations and MD events in one round of loads (past the last: the
+  // last again), ahead of the shape test that decides what they mean
+  // (indexes clamped into the pools: the loads do not wait for validate_one's verdict)
+  uint32_t c4[4] = {0u, 0u, 0u, 0u}, e4[4] = {0u, 0u, 0u, 0u};
+  const int32_t n_raw = R.n_cigar[r], nmd_raw = R.n_md[r];
+  auto clampi = [](int64_t x, int64_t len) { return x < 0 ? (int64_t)0 : x >= len ? len - 1 : x; };
+  if (R.cigar_len > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c4[j] = R.cigar[clampi(off + (j < n_raw ? j : n_raw - 1), R.cigar_len)];
+  }
+  if (R.md_len > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e4[j] = R.md_ev[clampi(mdo + (j < nmd_raw ? j : nmd_raw - 1), R.md_len)];
+  }
   int32_t ld = 0, mlen = 0;
   int mi = -1;
   bool simple = n > 0;
-  // the first four operations in one round of loads (past the last: the last again)
-  uint32_t c4[4] = {0u, 0u, 0u, 0u};
-  if (n > 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) c4[j] = R.cigar[off + (j < n ? j : n - 1)];
-  }
   for (int k = 0; k < n && simple; ++k) {
     const uint32_t c = k < 4 ? (k == 0 ? c4[0] : k == 1 ? c4[1] : k == 2 ? c4[2] : c4[3]) : R.cigar[off + k];
     const int op = (int)(c & 15u);
@@ -951,19 +968,18 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
     }
   }
   if (mi < 0 || ld > 32767 || ld + mlen > R.seq_len[r]) simple = false;
-  lead[r] = simple ? (int16_t)ld : (int16_t)-1;
+  lead[r] = bad ? (int16_t)-1 : simple ? (int16_t)ld : (int16_t)-1;
   // sequenced base under each MD event (0 where the event sits on a deletion / outside M)
-  const int32_t nmd = R.n_md[r];
   if (nmd <= 0) return;
-  const uint32_t *ev = R.md_ev + R.md_off[r];
-  uint8_t *rb = ev_rb + R.md_off[r];
+  const uint32_t *ev = R.md_ev + mdo;
+  uint8_t *rb = ev_rb + mdo;
   if (simple) {  // [S|H]* (M|=|X) [S|H]*: the event at reference offset o reads base lead + o
     const int64_t so = R.seq_off[r];
     const int32_t sl = R.seq_len[r];  // (>= ld + mlen >= 1: a simple read has bases)
     for (int k0 = 0; k0 < nmd; k0 += 4) {  // four events, then their bases, per round of loads
       uint32_t o4[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o4[j] = ev[k0 + j < nmd ? k0 + j : nmd - 1] >> 8;
+      for (int j = 0; j < 4; ++j) o4[j] = (k0 == 0 ? e4[j] : ev[k0 + j < nmd ? k0 + j : nmd - 1]) >> 8;
       uint8_t b4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1007,8 +1023,7 @@ __global__ void read_prep(DevReads R, int *__restrict__ bad, int16_t *__restrict
   if (r >= R.n_reads) return;
   const int b = validate_one(R, r);
   if (b) atomicOr(bad, b);
-  if (b & 2) lead[r] = -1;
-  else shape_one(R, r, lead, ev_rb);
+  shape_one(R, r, lead, ev_rb, (b & 2) != 0);  // (its loads go out beside validate_one's)
 }
 
 __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, int alt_len) {
