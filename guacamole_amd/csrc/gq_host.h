@@ -843,11 +843,13 @@ inline bool fill_slice_major() {
 // read-major / slice-major fills of round 4 (A/B alternatives).
 inline bool fill_pieces() {  // the cell or piece fills (no preset of the pool)
   static const bool v = !getenv("GQ_FILL") || strcmp(getenv("GQ_FILL"), "pieces") == 0 ||
-                        strcmp(getenv("GQ_FILL"), "cells") == 0;
+                        strcmp(getenv("GQ_FILL"), "cells") == 0 || strcmp(getenv("GQ_FILL"), "cellsb") == 0;
   return v;
 }
-inline int fill_mode() {  // 0: cells (the projection's default), 1: pieces (GQ_FILL=pieces)
-  static const int v = getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "pieces") == 0 ? 1 : 0;
+inline int fill_mode() {  // 0: cells (the projection's default), 1: pieces (GQ_FILL=pieces), 2: a workgroup per slice (cellsb)
+  static const int v = getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "pieces") == 0   ? 1
+                       : getenv("GQ_FILL") && strcmp(getenv("GQ_FILL"), "cellsb") == 0 ? 2
+                                                                                        : 0;
   return v;
 }
 // The margin projection's fill: read-major by default (chr20 60x: 5.5 ms against 8.6 ms by cells

@@ -729,6 +729,110 @@ __global__ __launch_bounds__(256) void proj_fill_cells(DevReads R, int64_t n_sli
   }
 }
 
+// The cell fill with a workgroup per slice (GQ_FILL=cellsb, A/B): the window's records in one
+// round (a thread per window read), the map marked by all four waves, each thread four cells.
+__global__ __launch_bounds__(256) void proj_fill_cellsb(DevReads R, int64_t n_slices, uint8_t *__restrict__ proj,
+                                                        int64_t *__restrict__ deep, unsigned long long *__restrict__ n_deep,
+                                                        int dbg) {
+  __shared__ Cell3Rec rec[kCell3Win + 1];
+  __shared__ uint8_t map[kCell3Rows * 16];
+  const int tid = threadIdx.x;
+  for (int64_t slot = blockIdx.x; slot < n_slices; slot += gridDim.x) {
+    const int64_t g0 = R.srow[slot];
+    const int32_t nr = (int32_t)(R.srow[slot + 1] - g0);
+    if (nr <= 0) continue;
+    uint32_t *out = reinterpret_cast<uint32_t *>(proj) + 16 * g0;
+    const SliceWin W = slice_stored(R, slot);
+    const int32_t nwin = (int32_t)(W.rz - W.ra);
+    if (R.pbad[slot] || nwin > kCell3Win || nwin <= 0) {
+      for (int32_t c = tid; c < 16 * nr; c += 256) out[c] = 0u;
+      if (!R.pbad[slot] && nwin > kCell3Win && tid == 0) deep[atomicAdd(n_deep, 1ull)] = slot;
+      continue;
+    }
+    const int64_t base = R.seq_off[W.ra];
+    const uint8_t *pool = R.seq + base;
+    const int64_t span = R.seq_cap - base;
+    int32_t prow_i = 0xFFFF, pc0 = 0, psl = 0;
+    if (tid < nwin) {
+      const int64_t r = W.ra + tid;
+      const ColDesc d = R.cdesc[r];
+      const int32_t ld = R.lead[r];
+      const int64_t so = R.seq_off[r];
+      const ProjRec pr = R.prec[r];
+      const int32_t row = R.prow[R.soff[slot] + tid];
+      const int64_t av = so + (ld > 0 ? ld : 0) - base;
+      Cell3Rec m;
+      m.a = R.pool_ordered && av >= 0 && av < (int64_t)kCell3Far ? (uint32_t)av : kCell3Far;
+      m.s = d.start;
+      m.e = d.end;
+      m.info = d.info;
+      rec[tid] = m;
+      int32_t s0, sl;
+      piece_of(pr, W.qc0, s0, sl);
+      prow_i = row;
+      pc0 = s0 - W.qc0;
+      psl = row == 0xFFFF ? 0 : sl;
+    }
+    for (int32_t k0 = 0; k0 < nr; k0 += kCell3Rows) {
+      const int32_t nk = nr - k0 < kCell3Rows ? nr - k0 : kCell3Rows;
+      for (int32_t c = tid; c < 16 * nk; c += 256) map[c] = 0xFFu;
+      __syncthreads();
+      if (psl > 0 && prow_i >= k0 && prow_i < k0 + nk) {
+        uint8_t *mp = map + 16 * (prow_i - k0) + pc0;
+        for (int32_t j = 0; j < psl; ++j) mp[j] = (uint8_t)tid;
+      }
+      __syncthreads();
+      uint32_t *o = out + 16 * k0;
+      uint64_t b[4], mk[4];
+      uint32_t slow = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int32_t c = 256 * u + tid;
+        const uint32_t pp = c < 16 * nk ? map[c] : 0xFFu;
+        const Cell3Rec m = rec[pp != 0xFFu ? pp : 0];
+        const int32_t lb = 8 * (W.qc0 + (c & 15));
+        const int64_t v = (int64_t)m.a + lb - m.s;
+        const bool ok = (m.info & kColEligible) && m.a != kCell3Far && v >= 0 && v + 8 <= span;
+        if (pp != 0xFFu && !ok) slow |= 1u << u;
+        mk[u] = pp != 0xFFu && ok ? edge_mask(m.s - lb, m.e - lb) : 0ull;
+        const uint32_t off = pp != 0xFFu && ok ? (uint32_t)v : 0u;
+        b[u] = span < 8 ? (uint64_t)off : *reinterpret_cast<const gq_u64u *>(pool + off);
+      }
+      uint32_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t y = b[u] & mk[u];
+        x[u] = perm_codes4((uint32_t)y) | (perm_codes4((uint32_t)(y >> 32)) << 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)  // (a wave's 64 cells lie all inside or all past 16 nk: rows padded to kRowPad)
+        if (256 * u + (tid & ~63) < 16 * nk) o[256 * u + tid] = x[u];
+      if (slow) {
+#pragma unroll 1
+        for (int u = 0; u < 4; ++u) {
+          if (!((slow >> u) & 1u)) continue;
+          const int32_t c = 256 * u + tid;
+          const uint32_t p = map[c];
+          const Cell3Rec m = rec[p];
+          const int64_t r = W.ra + p;
+          const int32_t ld = R.lead[r];
+          PieceMeta pm;
+          pm.p0 = R.seq_off[r] + (ld > 0 ? ld : 0) - m.s;
+          pm.s = m.s;
+          pm.e = m.e;
+          pm.s0 = 0;
+          pm.row = 0;
+          pm.info = m.info;
+          pm.mq = 0;
+          const ProjRaw xx = proj_fetch(R, r, pm, W.qc0 + (c & 15));
+          o[c] = xx.gen ? xx.word : proj_codes4((uint32_t)xx.b) | (proj_codes4((uint32_t)(xx.b >> 32)) << 4);
+        }
+      }
+      __syncthreads();  // (the next chunk rewrites the map, the next slice the records)
+    }
+  }
+}
+
 // The listed (deep) slices, slice-major (their rows zeroed by proj_fill_cells).
 __global__ __launch_bounds__(256) void proj_fill_deep(DevReads R, const int64_t *__restrict__ deep,
                                                       const unsigned long long *__restrict__ n_deep,
@@ -3386,7 +3490,22 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   HIP_TRY(hipEventRecord(d->tev[3], c->stream));
   if (n_sl > 0) {
     static const int fill_u = getenv("GQ_FILL_U") ? atoi(getenv("GQ_FILL_U")) : 0;
-    if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
+    if (cells && fill_mode() == 2) {  // A/B: GQ_FILL=cellsb (a workgroup per slice)
+      unsigned long long *nd = nullptr;
+      int64_t *dl = nullptr;
+      HIP_TRY(d->dp.get((void **)&nd, sizeof(unsigned long long)));
+      HIP_TRY(d->dp.get((void **)&dl, sizeof(int64_t) * (size_t)n_sl));
+      HIP_TRY(hipMemsetAsync(nd, 0, sizeof(unsigned long long), c->stream));
+      const int64_t blocks = std::min<int64_t>(n_sl, 1 << 20);
+      hipLaunchKernelGGL(proj_fill_cellsb, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj,
+                         dl, nd, fill_dbg());
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(proj_fill_deep, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0, c->stream, d->d,
+                         (const int64_t *)dl, (const unsigned long long *)nd, (uint8_t *)pj);
+      HIP_TRY(hipGetLastError());
+      d->dp.put(nd);
+      d->dp.put(dl);
+    } else if (cells && fill_mode() == 1) {  // A/B: GQ_FILL=pieces
       const int64_t blocks = std::min<int64_t>((n_sl + 3) / 4, 1 << 20);
       hipLaunchKernelGGL(proj_fill_pieces, dim3((unsigned)blocks), dim3(256), 0, c->stream, d->d, n_sl, (uint8_t *)pj,
                          fill_dbg());

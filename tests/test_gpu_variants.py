@@ -34,6 +34,6 @@ def test_kernel_variants_give_the_default_records():
     rw = {"GQ_FILL": "rw"}
     for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, rw, dict(rw, GQ_FILL_U="2"), dict(rw, GQ_FILL_U="4"),
                   dict(rw, GQ_FILL_W="2"), dict(rw, GQ_FILL_W="4"), dict(rw, GQ_FILL_ONE="1"), {"GQ_FILL": "slice"},
-                  {"GQ_ROWS": "firstfit"}, {"GQ_FILL": "pieces"}, {"GQ_MFILL": "cells"}, {"GQ_MFILL": "pieces"}):
+                  {"GQ_ROWS": "firstfit"}, {"GQ_FILL": "pieces"}, {"GQ_FILL": "cellsb"}, {"GQ_MFILL": "cells"}, {"GQ_MFILL": "pieces"}):
         got = _run(extra)
         assert got == base, (extra, got, base)
