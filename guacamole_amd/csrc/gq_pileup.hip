@@ -2584,10 +2584,10 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));  // nothing queued may still read the derived buffers
   HIP_TRY(hipStreamSynchronize(c->side));
-  {
-    const gq_status s0 = settle_stats(d);
-    if (s0) return s0;
-  }
+  // the previous derivation's figures nobody asked for are dropped (settling them would cost
+  // a host round trip per re-derivation)
+  d->nok = nullptr;
+  d->pending = 0;
   d->dp.release_all();
   DevReads &R = d->d;
   R.lead = nullptr;

@@ -225,7 +225,8 @@ typedef struct gq_reads_info {
   float derive_dev_ms; /* the upload-time derivation's device span (HIP events) */
 } gq_reads_info;
 /* A re-derivation and a projection do not wait for their device spans: this call waits for   */
-/* them (and reads the projection's taken-read count) the first time it is asked after them.  */
+/* them (and reads the projection's taken-read count) the first time it is asked after them;  */
+/* the next re-derivation drops figures nobody asked for.                                      */
 gq_status gq_reads_get_info(const gq_dev_reads *r, gq_reads_info *out);
 
 /* ---- BAM decoded on the device ----------------------------------------------------------
