@@ -302,14 +302,35 @@ def main() -> int:
         ks = tr.get("kernels", {})  # (named with template arguments: "proj_fill_cells<4>")
         k = next((k for k in sorted(ks) if k == kernel or k.startswith(kernel + "<")), None)
         return ks[k].get("hbm_bytes_per_launch") if k else None
-    traffic = pmc_traffic("germline_proj")
-    # the step's dominant kernel: the projection fill (read-major fill under GQ_FILL=rw).  Its
+    direct = os.environ.get("GQ_GERM", "direct") != "proj"
+    call_kernel = "germline_direct" if direct else "germline_proj"
+    traffic = pmc_traffic(call_kernel)
+    # the projection fill (GQ_GERM=proj only: the direct call derives no projection).  Its
     # algorithmic bytes: each projected read's bases over its span read once (sum of end - start)
     # + the pool it writes (every word of every row: the layout the call reads).
     elements = int((a["end"].astype(np.int64) - a["start"].astype(np.int64)).sum())
     f_ms = float(np.median(fill_ms))
     b_fill = elements + int(st["proj_bytes"])
     f_traffic = pmc_traffic("proj_fill_cells")
+    if direct:  # the step's dominant kernel is the call's own pileup kernel
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "kernel": call_kernel, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
+                "basis": "SURVEY 8(d) without qualities (germline-threshold never reads them): the sequence pool "
+                         "(%d B), 16 B per read, 4 B per CIGAR op and per MD event, 32 B per record and 12 B per "
+                         "queued locus written, times the share of tiles the kernel kept (%.4f); kernel_ms: mean "
+                         "of the steps' HIP-event times on the context's stream" % (bytes_seq, kept)}
+    else:
+        roof = {"bound": "hbm", "achieved": b_fill / (f_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": b_fill / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": f_traffic,
+                "dram_frac": None if f_traffic is None else f_traffic / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "kernel": os.environ.get("GQ_FILL", "cells") == "cells" and "proj_fill_cells" or
+                          "projection fill (GQ_FILL=%s)" % os.environ.get("GQ_FILL"),
+                "kernel_ms": f_ms, "algorithmic_bytes_per_launch": b_fill,
+                "basis": "bases over the projected reads' spans (sum end - start: %d) + the projection pool "
+                         "written (%d B); kernel_ms: median of the steps' HIP-event times on the context's "
+                         "stream" % (elements, int(st["proj_bytes"]))}
 
     line = {
         "metric": "pileup loci/sec at 30x WGS; achieved HBM GB/s vs roofline",
@@ -327,21 +348,13 @@ def main() -> int:
         "config": {"workload": workload, "genome_loci": genome_loci, "visited_loci_per_gpu": visited,
                    "reads_per_gpu": n_reads, "contigs_per_gpu": len(g.contig_names), "depth": args.depth,
                    "read_len": 150, "threshold": args.threshold, "parallelism": "loci-sharded x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": b_fill / (f_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": b_fill / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": f_traffic,
-                     "dram_frac": None if f_traffic is None else f_traffic / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "kernel": os.environ.get("GQ_FILL", "cells") == "cells" and "proj_fill_cells" or
-                               "projection fill (GQ_FILL=%s)" % os.environ.get("GQ_FILL"),
-                     "kernel_ms": f_ms, "algorithmic_bytes_per_launch": b_fill,
-                     "basis": "bases over the projected reads' spans (sum end - start: %d) + the projection pool "
-                              "written (%d B); kernel_ms: median of the steps' HIP-event times on the context's "
-                              "stream" % (elements, int(st["proj_bytes"]))},
+        "roofline": roof,
         # the resident call's pileup kernel (the round-4 headline kernel)
         "call_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                           # the bus rate: measured HBM bytes (PMC) / the kernel's time / peak
                           "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "kernel": "germline_proj", "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
+                          "kernel": call_kernel, "kernel_ms": k_ms, "algorithmic_bytes_per_launch": b_alg,
                           "read_bytes_per_launch": read_bytes, "tiles_kept": kept, "walker_ms": float(np.mean(walk_ms))},
         # the whole step on SURVEY §8(d)'s basis (bases, 16 B per read, CIGAR ops, MD events, output)
         "step_roofline": {"algorithmic_bytes": b_all, "step_ms": float(np.median(step_ms)),

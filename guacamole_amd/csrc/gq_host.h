@@ -1196,10 +1196,11 @@ struct gq_ctx {
   int germ_tile = gq::kGermT;
   int n_cu = 0;
   int proj_wg_per_cu = 0;  // resident germline_proj workgroups per CU (occupancy query, once)
+  int dir_wg_per_cu = 0;   // resident germline_direct workgroups per CU (occupancy query, once)
   int som_wg_per_cu = 0;   // resident somatic_proj workgroups per CU
   int call_wg_per_cu = 0;  // resident somatic_call_k<false> workgroups per CU
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
-  gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow;
+  gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow, deep_tiles;
   gq::DevBuf amb, amb_ref, heap_off, heap_reads;  // heap-order reference bases (heap_ref_bases)
   gq::DevBuf win_meta, win_grp;                    // somatic pileup element order (window_first / _group)
   gq::DevBuf deep_list, deep_scratch;              // somatic: the deep caller's list and per-wave scratch
@@ -1296,6 +1297,7 @@ struct gq_dev_reads {
   int64_t n_slices = 0;                                    // projection slices (128 loci) over all contigs
   int64_t n_rows = 0;                                      // projection rows (kProjRowBytes each, ProjRec)
   float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
+  bool columns = false;            // the column records and base classes are derived (ensure_columns)
   bool projected = false;          // the projection is derived (ensure_projection)
   void *nnb = nullptr;             // N bases per read (pool_clean), for the projection's sparse entries
   float proj_ms = 0;               // ensure_projection's wall time
@@ -1393,6 +1395,8 @@ struct H2DStager {
 // Upload-time derivation of a resident read set whose SoA arrays (and host copy of
 // contig_read_begin) are in place: validation, read shape, projection pool, block index.
 gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
+// The column records (ColDesc, the auxiliary list, clean / N-base counts), derived on first use.
+gq_status ensure_columns(gq_ctx *c, const gq_dev_reads *d);
 // The projection (ProjRec) of a resident read set, derived on first use.
 // A margin projection wanted with the projection (the somatic tumor, germline-standard): with
 // GQ_FILL_ONE both are filled in one read-major pass (fused_projection_fill) when the projection

@@ -346,7 +346,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   const int64_t seq_off = R.seq_off[r];
   const uint8_t fl = R.flags[r];
   const int32_t lead = R.lead[r];
-  const bool clean = R.clean[r] != 0;
+  const bool clean = R.clean && R.clean[r] != 0;  // (no column records: the checked path)
   const uint32_t *ev = R.md_ev + md_off;
   const uint8_t *evb = R.ev_rb + md_off;
   uint4 e4, b4;  // first four MD events and the read bases under them, loaded with the metadata

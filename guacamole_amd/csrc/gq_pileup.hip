@@ -384,12 +384,17 @@ __global__ void col_count(DevReads R, uint32_t *__restrict__ n_aux) {
 // The packed ColDesc of each read and its auxiliary list at aux_off[r]: one u32 per MD event
 // (offset << 16 | MD base << 8 | read base), then per segment (ref_off | len << 16,
 // seq_off | kind << 16).
+// aux_bound: the list's allocated words.  The list is sized from the pools (MD events + 6 words
+// per CIGAR op), which bounds it only when no two reads share MD or CIGAR pool words; a read whose
+// list would end past the allocation gets none (not column-eligible: the walkers take it).
 __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColDesc *__restrict__ cd,
-                           uint32_t *__restrict__ aux) {
+                           uint32_t *__restrict__ aux, int64_t aux_bound) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
-  const int32_t s = R.start[r], e = R.end[r], nmd = R.n_md[r], lead = R.lead[r];
-  const bool base_ok = col_base_ok(R, r);
+  const int32_t s = R.start[r], e = R.end[r], lead = R.lead[r];
+  const bool fits = aux_off[r + 1] <= aux_bound;
+  const int32_t nmd = R.n_md[r];
+  const bool base_ok = fits && col_base_ok(R, r);
   const bool ok = lead >= 0 && base_ok;
   uint32_t *o = aux + aux_off[r];
   const int32_t nev = nmd > 0 ? nmd : 0;
@@ -411,7 +416,7 @@ __global__ void col_derive(DevReads R, const int64_t *__restrict__ aux_off, ColD
   d.seq_lo = (uint32_t)(uint64_t)(R.seq_off[r] + (lead > 0 ? lead : 0));
   d.md_lo = (uint32_t)(uint64_t)aux_off[r];
   cd[r] = d;
-  if (nmd > 0) {  // four events per round of loads (past the last: the last again)
+  if (fits && nmd > 0) {  // four events per round of loads (past the last: the last again)
     const uint32_t *ev = R.md_ev + R.md_off[r];
     const uint8_t *rb = R.ev_rb + R.md_off[r];
     for (int32_t k0 = 0; k0 < nmd; k0 += 4) {
@@ -954,13 +959,13 @@ __device__ __forceinline__ int validate_one(const DevReads &R, int64_t r) {
   const int32_t sl = R.seq_len[r], sl1 = R.seq_len[rp], nc = R.n_cigar[r], nm = R.n_md[r];
   const int smp = (int)R.sample[r];
   int b = 0;
-  b |= (e < s) | (s < 0) ? 1 : 0;
+  b |= ((e < s) | (s < 0)) ? 1 : 0;
   b |= (first ? pm != e : ((s < s1) | (pm != max(pm1, e)))) ? 1 : 0;
-  b |= (so < 0) | (sl < 0) | (so + sl > R.seq_bytes) ? 2 : 0;
-  b |= (co < 0) | (nc < 0) | (co + nc > R.cigar_len) ? 2 : 0;
-  b |= (nm > 0) & ((mo < 0) | (mo + nm > R.md_len)) ? 2 : 0;
+  b |= ((so < 0) | (sl < 0) | (so + sl > R.seq_bytes)) ? 2 : 0;
+  b |= ((co < 0) | (nc < 0) | (co + nc > R.cigar_len)) ? 2 : 0;
+  b |= ((nm > 0) & ((mo < 0) | (mo + nm > R.md_len))) ? 2 : 0;
   b |= smp >= R.n_samples ? 2 : 0;
-  b |= (r > 0) & (so < so1 + sl1) ? 4 : 0;
+  b |= ((r > 0) & (so < so1 + sl1)) ? 4 : 0;
   return b;
 }
 
@@ -1142,6 +1147,7 @@ __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, 
 
 #include "gq_germline_common.h"
 #include "gq_germline_proj.h"
+#include "gq_germline_direct.h"
 #include "gq_winorder.h"
 
 // ------------------------------------------------------------------------------------------
@@ -2248,36 +2254,18 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     for (size_t i = 1; i < b.size() && ok; ++i) ok = b[i] >= b[i - 1];
     if (!ok) return set_err(GQ_E_UNSORTED, "contig_read_begin must run from 0 to n_reads, non-decreasing");
   }
-  void *p = nullptr, *q = nullptr, *cl = nullptr;
+  void *p = nullptr, *q = nullptr;
   HIP_TRY(d->dp.get(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  HIP_TRY(d->dp.get(&cl, (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  d->d.clean = (const uint8_t *)cl;
   HIP_TRY(d->dp.get(&q, (size_t)std::max<int64_t>(md_len, 16)));
   d->d.lead = (const int16_t *)p;
   d->d.ev_rb = (const uint8_t *)q;
   int unordered = 0;
-  void *nnb = nullptr;  // N bytes per read (pool_clean / read_clean), for the projection entries
-  HIP_TRY(d->dp.get((void **)&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1), c->stream));
   const int nc = d->d.n_contigs;
   std::vector<int32_t> last((size_t)nc, 0);  // each contig's largest read end (pmax_end of its last read)
   if (d->d.n_reads > 0) {
     void *flag = nullptr;
     HIP_TRY(d->dp.get(&flag, sizeof(int)));
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
-    // the pool's A/C/G/T/N scan on the side stream while the reads are checked and shaped: it
-    // touches only the pool and seq_off, and a pool in another order (flag bit 4) redoes it per read
-    HIP_TRY(hipEventRecord(c->side_ev[0], c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
-    static const bool clean_serial = getenv("GQ_CLEAN_SERIAL") != nullptr;  // A/B: on the main stream, first
-    hipStream_t cs = clean_serial ? c->stream : c->side;
-    HIP_TRY(hipMemsetAsync(cl, 1, (size_t)d->d.n_reads, cs));
-    const int64_t chunks = (d->d.seq_bytes + 15) / 16;
-    if (chunks > 0)
-      hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0, cs,
-                         d->d, (uint8_t *)cl, (uint32_t *)nnb);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->side_ev[1], c->side));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
     // validation and the read shapes in one pass (a read out of its pools gets no shape)
     hipLaunchKernelGGL(read_prep, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag, (int16_t *)p, (uint8_t *)q);
@@ -2290,19 +2278,12 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
         HIP_TRY(hipMemcpyAsync(&last[(size_t)k], d->d.pmax_end + (crb[(size_t)k + 1] - 1), sizeof(int32_t),
                                hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (bad & 3) HIP_TRY(hipStreamSynchronize(c->side));  // (nothing of the side stream outlives a failure)
     if (bad & 1)
       return set_err(GQ_E_UNSORTED, "Regions must be sorted by start locus: reads are not sorted by (contig, start), "
                                     "or pmax_end is not the running maximum of end within each contig");
     if (bad & 2)
       return set_err(GQ_E_ARG, "read set: an offset or length lies outside its pool, or a sample slot >= n_samples");
     unordered = (bad & 4) ? 1 : 0;
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
-    if (unordered) {  // the pool scan assumed read order: per read instead
-      HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)d->d.n_reads, c->stream));
-      hipLaunchKernelGGL(read_clean, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint8_t *)cl, (uint32_t *)nnb);
-      HIP_TRY(hipGetLastError());
-    }
   }
   {  // the projections' slices (whole 512-locus blocks up to each contig's largest read end) and
      // the block index of the reads (plan_tiles' windows of aligned tiles); the projection
@@ -2329,35 +2310,8 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     d->d.blk_rb = brb;
     d->d.blk_rs = brs;
   }
-  {  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds.  The
-     // auxiliary list is sized by its bound (MD events + 6 words per CIGAR op: at most three
-     // segments of two words per op), so no count comes back to the host first.
-    const int64_t n = d->d.n_reads;
-    void *cd = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr, *tmp = nullptr;
-    const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
-    HIP_TRY(d->dp.get(&cd, ncd));
-    HIP_TRY(hipMemsetAsync(cd, 0, ncd, c->stream));
-    HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
-    HIP_TRY(d->dp.get((void **)&na, sizeof(uint32_t) * (size_t)(n + 1)));
-    const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint32_t *)na);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(scan_u32_to_i64(d->dp, (const uint32_t *)na, (int64_t *)ao, n + 1, c->stream));
-    d->dp.put(na);
-    const int64_t aux_bound = std::max<int64_t>(md_len, 0) + 6 * std::max<int64_t>(d->d.cigar_len, 0);
-    const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_bound, 1) + 1024;
-    HIP_TRY(d->dp.get(&ce, nce));
-    d->d.cdesc = (const ColDesc *)cd;
-    d->d.cev = (const uint32_t *)ce;
-    d->d.caux_off = (const int64_t *)ao;
-    if (n > 0) {
-      hipLaunchKernelGGL(col_derive, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
-                         (const int64_t *)ao, (ColDesc *)cd, (uint32_t *)ce);
-      HIP_TRY(hipGetLastError());
-    }
-  }
-  d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
-  nnb = nullptr;
+  // (the column records, the pool's base classes and the projection are derived on first use:
+  // ensure_columns / ensure_projection; germline_direct needs none of them)
   HIP_TRY(hipEventRecord(d->tev[1], c->stream));
   d->d.pool_ordered = unordered ? 0 : 1;
   if (lazy) {  // (a re-derivation: the caller's next call goes on behind it on the stream)
@@ -2601,10 +2555,11 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   R.pev = nullptr;
   R.prow = nullptr;
   d->projected = false;
+  d->columns = false;
   d->nnb = d->mproj = d->mnb = nullptr;
   d->mproj_mapq = -1;
   d->proj_bytes = d->pev_count = d->proj_reads = d->n_rows = d->n_slices = 0;
-  d->proj_ms = 0;
+  d->proj_ms = d->fill_ms = d->proj_dev_ms = 0;
   const auto t1 = std::chrono::steady_clock::now();
   const gq_status st = derive_shape_impl(c, d, R.md_len, true);
   d->derive_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
@@ -2754,31 +2709,54 @@ gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
 
 extern "C" {
 
-static unsigned germline_grid(gq_ctx *c, int64_t tiles) {
+// The germline pileup kernel of a call: germline_direct (straight from the reads) unless
+// GQ_GERM=proj asks for germline_proj over the projection (A/B; the same records).
+static bool germline_direct_mode(const DevReads &R) {
+  static const char *m = getenv("GQ_GERM");
+  static const bool proj = m && strcmp(m, "proj") == 0;
+  return !proj && R.seq_cap >= 8;
+}
+
+static unsigned germline_grid(gq_ctx *c, int64_t tiles, bool direct) {
   if (c->n_cu <= 0 && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
     c->n_cu = 256;
-  // persistent: every resident workgroup (8 waves, a tile per wave at a time) over a contiguous run
-  if (c->proj_wg_per_cu <= 0) {
+  // persistent: every resident workgroup (4 waves, a tile per wave at a time) over a contiguous run
+  int &per_cu = direct ? c->dir_wg_per_cu : c->proj_wg_per_cu;
+  if (per_cu <= 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, germline_proj, ProjCfg::kThreads, 0) != hipSuccess || nb <= 0)
-      nb = 2;
-    c->proj_wg_per_cu = nb;
+    const hipError_t e = direct ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, germline_direct<false>, DirCfg::kThreads, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, germline_proj, ProjCfg::kThreads, 0);
+    if (e != hipSuccess || nb <= 0) nb = 2;
+    per_cu = nb;
   }
   const int64_t want = (tiles + ProjCfg::kWaves - 1) / ProjCfg::kWaves;
-  return (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>({want, (int64_t)c->proj_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>({want, (int64_t)per_cu * c->n_cu, (int64_t)kPartsCols}));
 }
 
 static gq_status launch_germline(gq_ctx *c, int64_t tiles, const DevReads &R, const gq_germline_params *p,
-                                 CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr) {
+                                 CallRec *recs, ComplexItem *cplx, const OutGeom &og, Counters *ctr, bool direct) {
   static const int dbg = getenv("GQ_DBG") ? atoi(getenv("GQ_DBG")) : 0;  // diagnostics only
   HIP_TRY(c->slow.ensure((size_t)tiles * sizeof(int32_t)));
   // germline_proj reads the Tile + TileX arrays through one buffer of 128 B per tile
   if (tiles >= (int64_t)1 << 24) return set_err(GQ_E_ARG, "%lld tiles in one call (at most 2^24)", (long long)tiles);
-  hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
-                     (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.proj,
-                     R.pev, R.n_samples,
-                     p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
+  if (direct) {
+    // the shallow instantiation over every tile, then the deep one over the tiles it listed
+    // (read on the device: no host round trip; an empty list sends its waves home at once)
+    HIP_TRY(c->deep_tiles.ensure((size_t)tiles * sizeof(int32_t)));
+    hipLaunchKernelGGL(germline_direct<false>, dim3((unsigned)og.ncols), dim3(DirCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, tiles, R, p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr,
+                       (int32_t *)c->slow.p, (int32_t *)c->deep_tiles.p, dbg);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(germline_direct<true>, dim3((unsigned)std::min<int64_t>((tiles + DirCfg::kWaves - 1) / DirCfg::kWaves, 512)),
+                       dim3(DirCfg::kThreads), 0, c->stream, (const Tile *)c->tiles.p, tiles, R, p->threshold,
+                       p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p,
+                       (int32_t *)c->deep_tiles.p, dbg);
+  } else {
+    hipLaunchKernelGGL(germline_proj, dim3((unsigned)og.ncols), dim3(ProjCfg::kThreads), 0, c->stream,
+                       (const Tile *)c->tiles.p, (const TileX *)((const Tile *)c->tiles.p + tiles), tiles, R.proj,
+                       R.pev, R.n_samples,
+                       p->threshold, p->emit_ref, p->emit_no_call, recs, cplx, og, ctr, (int32_t *)c->slow.p, dbg);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[5], c->stream));  // column kernel | walker kernel
   const unsigned wblocks = (unsigned)std::min<int64_t>(tiles, 2048);
@@ -2801,7 +2779,8 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   const auto h0 = std::chrono::steady_clock::now();
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = ensure_projection(c, rd);  // (derived on first use)
+  const bool direct = germline_direct_mode(rd->d);
+  gq_status st = direct ? GQ_OK : ensure_projection(c, rd);  // (derived on first use)
   if (st) return st;
   st = plan(c, rd, loci, T, pl, c->tiles, 0, 0, 0, true);
   if (st) return st;
@@ -2816,7 +2795,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
   // output partitions: per germline_proj workgroup (capA, its share of the loci) and per
   // walker / complex-kernel wave (capB); grown on overflow
   OutGeom og{};
-  og.ncols = (int)germline_grid(c, pl.n_tiles);
+  og.ncols = (int)germline_grid(c, pl.n_tiles, direct);
   const bool dense = p->emit_ref || p->emit_no_call;
   const unsigned long long wg_loci = (unsigned long long)((pl.n_tiles + og.ncols - 1) / og.ncols) * T;
   og.capA[0] = dense ? 2ull * ns * wg_loci + 64 : wg_loci / 32 + 256;
@@ -2888,7 +2867,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     if (attempt == 0) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    st = launch_germline(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, (ComplexItem *)c->cplx.p, og, ctr);
+    st = launch_germline(c, pl.n_tiles, rd->d, p, (CallRec *)c->recs.p, (ComplexItem *)c->cplx.p, og, ctr, direct);
     if (st) {
       free(res);
       return st;
@@ -3213,7 +3192,9 @@ gq_status gq_pileup_counts(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loc
   if (!c || !rd || !loci || !out) return set_err(GQ_E_ARG, "gq_pileup_counts: null argument");
   HIP_TRY(hipSetDevice(c->device));
   Plan pl;
-  gq_status st = plan(c, rd, loci, kCountT, pl, c->tiles);
+  gq_status st = ensure_columns(c, rd);  // (the walker's clean fast path)
+  if (st) return st;
+  st = plan(c, rd, loci, kCountT, pl, c->tiles);
   if (st) return st;
   gq_counts *res = (gq_counts *)calloc(1, sizeof(gq_counts));
   const int64_t n = pl.n_loci;
@@ -3308,7 +3289,9 @@ gq_status gq_vaf_histogram(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loc
   HIP_TRY(hipSetDevice(c->device));
   memset(out, 0, sizeof(*out));
   Plan pl;
-  gq_status st = plan(c, rd, loci, kCountT, pl, c->tiles);
+  gq_status st = ensure_columns(c, rd);  // (the walker's clean fast path)
+  if (st) return st;
+  st = plan(c, rd, loci, kCountT, pl, c->tiles);
   if (st) return st;
   if (pl.n_tiles == 0) return GQ_OK;
   unsigned long long amb_cap = 4096;
@@ -3388,6 +3371,64 @@ void gq_free_counts(gq_counts *r) {
 
 gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return derive_shape_impl(c, d, md_len); }
 
+// The column records of a resident read set, derived on first use by a kernel that reads them
+// (the projection's fills and sparse entries, somatic_proj, the walkers' clean fast path):
+// clean[r] (every sequenced byte of read r is A C G T N) and its N bytes (pool_clean, or
+// read_clean for a pool out of read order), then each read's ColDesc and auxiliary list (MD
+// events, a general read's segments).  germline_direct reads none of it.
+gq_status gq::ensure_columns(gq_ctx *c, const gq_dev_reads *cd) {
+  gq_dev_reads *d = const_cast<gq_dev_reads *>(cd);
+  if (d->columns) return GQ_OK;
+  const int64_t n = d->d.n_reads;
+  void *cl = nullptr, *nnb = nullptr;
+  HIP_TRY(d->dp.get(&cl, (size_t)std::max<int64_t>(n, 1)));
+  HIP_TRY(d->dp.get(&nnb, sizeof(uint32_t) * (size_t)std::max<int64_t>(n, 1)));
+  HIP_TRY(hipMemsetAsync(nnb, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(n, 1), c->stream));
+  if (n > 0) {
+    if (d->d.pool_ordered) {  // the pool in read order: 16-byte chunks, the rare other bytes searched
+      HIP_TRY(hipMemsetAsync(cl, 1, (size_t)n, c->stream));
+      const int64_t chunks = (d->d.seq_bytes + 15) / 16;
+      if (chunks > 0)
+        hipLaunchKernelGGL(pool_clean, dim3((unsigned)((chunks + 2 * kBlock - 1) / (2 * kBlock))), dim3(kBlock), 0,
+                           c->stream, d->d, (uint8_t *)cl, (uint32_t *)nnb);
+    } else {
+      hipLaunchKernelGGL(read_clean, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                         (uint8_t *)cl, (uint32_t *)nnb);
+    }
+    HIP_TRY(hipGetLastError());
+  }
+  d->d.clean = (const uint8_t *)cl;
+  d->nnb = nnb;  // N bases per read: the projection's sparse entries (ensure_projection)
+  // column-kernel records; 1 KiB zeroed tails keep the per-tile LDS-DMA pieces in bounds.  The
+  // auxiliary list is sized by its bound (MD events + 6 words per CIGAR op: at most three
+  // segments of two words per op, when no two reads share pool words), so no count comes back to
+  // the host first; col_derive refuses a read whose list would end past it.
+  void *cdp = nullptr, *ce = nullptr, *ao = nullptr, *na = nullptr;
+  const size_t ncd = sizeof(ColDesc) * (size_t)std::max<int64_t>(n, 1) + 1024;
+  HIP_TRY(d->dp.get(&cdp, ncd));
+  HIP_TRY(hipMemsetAsync(cdp, 0, ncd, c->stream));
+  HIP_TRY(d->dp.get(&ao, sizeof(int64_t) * (size_t)(n + 1)));
+  HIP_TRY(d->dp.get((void **)&na, sizeof(uint32_t) * (size_t)(n + 1)));
+  const unsigned nb = (unsigned)((n + 1 + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(col_count, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (uint32_t *)na);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(scan_u32_to_i64(d->dp, (const uint32_t *)na, (int64_t *)ao, n + 1, c->stream));
+  d->dp.put(na);
+  const int64_t aux_bound = std::max<int64_t>(d->d.md_len, 0) + 6 * std::max<int64_t>(d->d.cigar_len, 0);
+  const size_t nce = sizeof(uint32_t) * (size_t)std::max<int64_t>(aux_bound, 1) + 1024;
+  HIP_TRY(d->dp.get(&ce, nce));
+  d->d.cdesc = (const ColDesc *)cdp;
+  d->d.cev = (const uint32_t *)ce;
+  d->d.caux_off = (const int64_t *)ao;
+  if (n > 0) {
+    hipLaunchKernelGGL(col_derive, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream, d->d,
+                       (const int64_t *)ao, (ColDesc *)cdp, (uint32_t *)ce, aux_bound);
+    HIP_TRY(hipGetLastError());
+  }
+  d->columns = true;
+  return GQ_OK;
+}
+
 // The projection of a resident read set (ProjRec in gq_kernels.h), derived on first use by a
 // kernel that reads it (germline_proj, somatic_proj over the tumor, mproj_fill): records, pbad
 // slices, each slice's read window and its pieces' rows (one greedy pass, stored), the rows'
@@ -3401,8 +3442,12 @@ gq_status gq::ensure_projection(gq_ctx *c, const gq_dev_reads *cd, const MarginR
   const int64_t n_sl = d->n_slices;
   void *pr = nullptr, *sc = nullptr, *sb = nullptr, *br = nullptr, *tmp = nullptr, *pj = nullptr, *ne = nullptr,
        *eo = nullptr, *pe = nullptr, *pbd = nullptr, *sra = nullptr, *scn = nullptr, *so = nullptr, *pw = nullptr;
-  HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
   HIP_TRY(hipEventRecord(d->tev[2], c->stream));
+  {
+    const gq_status sc0 = ensure_columns(c, d);
+    if (sc0) return sc0;
+  }
+  HIP_TRY(d->dp.get(&pr, sizeof(ProjRec) * (size_t)(n + 1)));
   const unsigned nb1 = (unsigned)((n + 1 + kBlock - 1) / kBlock);
   // the records, the slices a read the projection cannot take touches (pbad), the sparse entries
   // per read and the reads taken, in one pass

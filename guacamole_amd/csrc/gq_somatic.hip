@@ -1869,21 +1869,23 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       deep_cap = hc.n_wide + 1024;
       retry = true;
     }
-    if (!retry && hc.n_wide > 0 && !hc.err) {
-      // the wide kernel: the candidates past the deep kernel's allele table or genotype scratch
-      // (64 kWideNS distinct alleles per sample, every genotype of them in its scratch); a few
-      // waves, each with a large scratch slice
+    // the wide kernel: the candidates past the deep kernel's allele table or genotype scratch
+    // (64 kWideNS distinct alleles per sample, every genotype of them in its scratch); a few
+    // waves, each with a large scratch slice.  ain: a heap-order replay's hand-over (the list
+    // holds positions in ain, whose resolved reference bases the kernel reads from aref).
+    auto run_wide = [&](int64_t n_items, const AmbItem *ain, const uint8_t *aref, int64_t n_ain) -> gq_status {
       const int scap = (int)std::max<unsigned long long>(hc.deep_max, (unsigned long long)kFastCap);
       const int maxg = 64 * kWideNS * (64 * kWideNS + 1) / 2;
-      const int64_t nw = std::min<int64_t>((int64_t)hc.n_wide, 16);  // (12.6 MB of genotype scratch per wave)
+      const int64_t nw = std::min<int64_t>(n_items, 16);  // (12.6 MB of genotype scratch per wave)
       const size_t wb = deep_wave_bytes(scap, maxg, kWideNS);
       HIP_TRY(c->deep_scratch.ensure((size_t)nw * wb + 256));
       HIP_TRY(hipEventRecord(c->ev[5], c->stream));
       hipLaunchKernelGGL((somatic_call_k<true, false, 3, kWideNS>), dim3((unsigned)((nw + kSomWaves - 1) / kSomWaves)),
                          dim3(kBlock), 0, c->stream, (const CandRec *)c->cands.p, t->d, n->d, *p, (SomRec *)c->srecs.p,
-                         rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)c->amb.p, amb_cap,
-                         (const AmbItem *)nullptr, (const uint8_t *)nullptr, (int64_t)0, rv, dbg,
-                         DeepIO{(int64_t *)c->deep_list.p + deep_cap, 0, (int64_t)hc.n_wide, (uint8_t *)c->deep_scratch.p,
+                         rec_cap, (uint8_t *)c->pool.p, pool_cap, og, ctr, sw, (AmbItem *)(ain ? nullptr : c->amb.p),
+                         ain ? (unsigned long long)0 : amb_cap, ain, aref, ain ? n_ain : (int64_t)0,
+                         ain ? RefView{nullptr, nullptr} : rv, dbg,
+                         DeepIO{(int64_t *)c->deep_list.p + deep_cap, 0, n_items, (uint8_t *)c->deep_scratch.p,
                                 scap, maxg, nullptr, 0},
                          ElemStore{});
       HIP_TRY(hipGetLastError());
@@ -1893,6 +1895,14 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
       float ms = 0;
       (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[3]);
       deep_ms += ms;
+      return GQ_OK;
+    };
+    if (!retry && hc.n_wide > 0 && !hc.err) {
+      st = run_wide((int64_t)hc.n_wide, nullptr, nullptr, 0);
+      if (st) {
+        free(res);
+        return st;
+      }
     }
     if (hc.n_amb > amb_cap) {
       amb_cap = hc.n_amb + 1024;
@@ -1910,10 +1920,23 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
         free(res);
         return st;
       }
+      // (the hand-over list of the replay starts empty: loci past the deep table go to the wide kernel)
+      HIP_TRY(hipMemsetAsync(&ctr->n_wide, 0, sizeof(ctr->n_wide), c->stream));
       st = run_deep((int64_t)amb.size(), (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p);
       if (st) {
         free(res);
         return st;
+      }
+      if (hc.n_wide > deep_cap) {
+        deep_cap = hc.n_wide + 1024;
+        retry = true;
+      }
+      if (!retry && hc.n_wide > 0 && !hc.err) {
+        st = run_wide((int64_t)hc.n_wide, (const AmbItem *)c->amb.p, (const uint8_t *)c->amb_ref.p, (int64_t)amb.size());
+        if (st) {
+          free(res);
+          return st;
+        }
       }
     }
     if (hc.n_rec > rec_cap) {
@@ -1977,7 +2000,9 @@ gq_status gq_variant_support(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *l
   c->timings = gq_timings{};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   Plan pl;
-  gq_status st = plan(c, rd, loci, 512, pl, c->tiles);
+  gq_status st = ensure_columns(c, rd);
+  if (st) return st;
+  st = plan(c, rd, loci, 512, pl, c->tiles);
   if (st) return st;
   gq_allele_counts *res = (gq_allele_counts *)calloc(1, sizeof(gq_allele_counts));
   if (!res) return set_err(GQ_E_NOMEM, "calloc");

@@ -872,7 +872,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     m.maxG = kMaxG;
   }
   static_assert(!(DEEP && BACK), "the deep kernel runs its own front");
-  const unsigned long long n_items = amb_in ? (unsigned long long)n_amb_in
+  // amb_sel: a heap-order replay over the amb_in positions listed in dio.list (the wide kernel
+  // over the replayed loci the deep kernel's table could not hold), not over all of amb_in
+  const bool amb_sel = DEEP && amb_in != nullptr && dio.n_in > 0;
+  const unsigned long long n_items = amb_sel  ? (unsigned long long)dio.n_in
+                                     : amb_in ? (unsigned long long)n_amb_in
                                      : DEEP ? (unsigned long long)dio.n_in
                                      : BACK ? (unsigned long long)es.b1
                                             : ctr->part_off[1][kParts];
@@ -895,19 +899,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
     }
   };
   // the next candidate's record is loaded one candidate ahead (it lands while this one runs)
-  auto fetch_item = [&](int64_t li, int64_t &it) -> CandRec {
-    it = amb_in ? amb_in[li].item : DEEP ? dio.list[li] : li;
+  // (la: the item's position in amb_in, whose resolved reference bases it reads)
+  auto fetch_item = [&](int64_t li, int64_t &it, int64_t &la) -> CandRec {
+    la = amb_sel ? dio.list[li] : li;
+    it = amb_in ? amb_in[la].item : DEEP ? dio.list[li] : li;
     return cands[it];
   };
-  int64_t it_next = 0;
+  int64_t it_next = 0, la_next = 0;
   CandRec item_next{};
-  if (li0 < (int64_t)n_items) item_next = fetch_item(li0, it_next);
+  if (li0 < (int64_t)n_items) item_next = fetch_item(li0, it_next, la_next);
   for (int64_t li = li0; li < (int64_t)n_items; li += nwaves_total) {
     tick(-1);
     if ((dbg & 16) && lane == 0) atomicAdd(&s_clk[5], 1ull);
-    const int64_t it = it_next;
+    const int64_t it = it_next, la = la_next;
     const CandRec item = item_next;
-    if (li + nwaves_total < (int64_t)n_items) item_next = fetch_item(li + nwaves_total, it_next);
+    if (li + nwaves_total < (int64_t)n_items) item_next = fetch_item(li + nwaves_total, it_next, la_next);
     const int32_t pos = item.pos;
     const int32_t t_contig = item.contig, t_L0 = item.L0;
     const int64_t t_ord0 = item.ord0;
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
       uint32_t mk = mask[s];
       for (int d = 1; d < 64; d <<= 1) mk |= __shfl_xor(mk, d, 64);
       PS[s].ambiguous = fb < 0 && __popc(mk) > 1;
-      PS[s].refbase = amb_in ? amb_ref[2 * li + s] : fb >= 0 ? (uint8_t)fb : mk ? bit_base(mk) : (uint8_t)'N';
+      PS[s].refbase = amb_in ? amb_ref[2 * la + s] : fb >= 0 ? (uint8_t)fb : mk ? bit_base(mk) : (uint8_t)'N';
     }
     tick(0);
     if (dbg & 2048) continue;  // ablation: covers + elements
@@ -1050,10 +1056,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DEEP ? 2
           if (k < dio.cap) dio.list[k] = it;
           atomicMax(&ctr->deep_max, (unsigned long long)max(nc[0], nc[1]));
         }
-      } else if (NS < kWideNS && !amb_in) {  // more than the deep table: the wide kernel's
-        if (lane == 0) {
+      } else if (NS < kWideNS) {  // more than the deep table: the wide kernel's (a replayed
+        if (lane == 0) {          // locus by its position in amb_in, with its resolved bases)
           const unsigned long long k = atomicAdd(&ctr->n_wide, 1ull);
-          if (k < dio.wcap) dio.wide[k] = it;
+          if (k < dio.wcap) dio.wide[k] = amb_in ? la : it;
         }
       } else {
         raise_at(ctr, GQ_E_CAPACITY, pos);

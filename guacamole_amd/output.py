@@ -64,8 +64,28 @@ ANNOTATIONS_SCHEMA: List[Tuple[str, str, object]] = [
 _ENUMS = {"GenotypeAllele": ["Ref", "Alt", "OtherAlt", "NoCall"],
           "StructuralVariantType": ["DELETION", "INSERTION", "INVERSION", "MOBILE_INSERTION", "MOBILE_DELETION",
                                     "DUPLICATION", "TANDEM_DUPLICATION"]}
+# The reads' record (adam.py: ADAM AlignmentRecord input, Read.scala:454-539), bdg-formats 0.6.1
+# as restated here (readNum in place of the older firstOfPair / secondOfPair), parity unpinned
+ALIGNMENT_RECORD_SCHEMA: List[Tuple[str, str, object]] = [
+    ("contig", "?Contig", None), ("start", "?long", None), ("oldPosition", "?long", None), ("end", "?long", None),
+    ("mapq", "?int", None), ("readName", "?string", None), ("sequence", "?string", None), ("qual", "?string", None),
+    ("cigar", "?string", None), ("oldCigar", "?string", None), ("basesTrimmedFromStart", "int?", 0),
+    ("basesTrimmedFromEnd", "int?", 0), ("readPaired", "boolean?", False), ("properPair", "boolean?", False),
+    ("readMapped", "boolean?", False), ("mateMapped", "boolean?", False), ("readNum", "int?", 0),
+    ("failedVendorQualityChecks", "boolean?", False), ("duplicateRead", "boolean?", False),
+    ("readNegativeStrand", "boolean?", False), ("mateNegativeStrand", "boolean?", False),
+    ("primaryAlignment", "boolean?", False), ("secondaryAlignment", "boolean?", False),
+    ("supplementaryAlignment", "boolean?", False), ("mismatchingPositions", "?string", None),
+    ("origQual", "?string", None), ("attributes", "?string", None), ("recordGroupName", "?string", None),
+    ("recordGroupSequencingCenter", "?string", None), ("recordGroupDescription", "?string", None),
+    ("recordGroupRunDateEpoch", "?long", None), ("recordGroupFlowOrder", "?string", None),
+    ("recordGroupKeySequence", "?string", None), ("recordGroupLibrary", "?string", None),
+    ("recordGroupPredictedMedianInsertSize", "?int", None), ("recordGroupPlatform", "?string", None),
+    ("recordGroupPlatformUnit", "?string", None), ("recordGroupSample", "?string", None),
+    ("mateAlignmentStart", "?long", None), ("mateAlignmentEnd", "?long", None), ("mateContig", "?Contig", None),
+    ("inferredInsertSize", "?long", None)]
 _ALL_RECORDS = dict(_RECORDS, StructuralVariant=STRUCTURAL_VARIANT_SCHEMA,
-                    VariantCallingAnnotations=ANNOTATIONS_SCHEMA)
+                    VariantCallingAnnotations=ANNOTATIONS_SCHEMA, AlignmentRecord=ALIGNMENT_RECORD_SCHEMA)
 
 
 def germline_genotype(contig: str, start: int, sample: str, alleles, ref: str, alt: str) -> Dict:
@@ -299,15 +319,16 @@ def unwrap_avro_json(record: str, datum: Optional[Dict]) -> Optional[Dict]:
 
 def write_parquet_dir(path: str, genotypes: List[Dict], part_of: Optional[Sequence[int]] = None, n_parts: int = 1,
                       codec: str = "GZIP", page_size: int = 1 << 20, block_size: int = 128 << 20,
-                      dictionary: bool = True) -> List[str]:
+                      dictionary: bool = True, record: str = "Genotype") -> List[str]:
     """adamParquetSave (Common.scala:294-302; ADAM 0.18 rdd.map((null, _)).saveAsNewAPIHadoopFile
     through AvroParquetOutputFormat) for Genotype records: the Hadoop output directory `path`
     with one part-r-NNNNN<codec>.parquet per RDD partition (record i goes to part part_of[i]; the
     callers' genotypes RDD has one partition per loci task, empty ones still written), the
     summary files _metadata / _common_metadata, and _SUCCESS.  Options are ParquetArgs'
     (-parquet_compression_codec GZIP, -parquet_page_size 1 MiB, -parquet_block_size 128 MiB,
-    dictionary encoding on).  The schema is the restated bdg-formats Genotype, with the Avro
-    schema in the footer; byte parity with parquet-mr's files is unpinned."""
+    dictionary encoding on).  The schema is the restated bdg-formats Genotype (or `record`, e.g.
+    AlignmentRecord for adam.write_alignment_parquet), with the Avro schema in the footer; byte
+    parity with parquet-mr's files is unpinned."""
     import os
     import pyarrow as pa
     import pyarrow.parquet as pq
@@ -315,8 +336,8 @@ def write_parquet_dir(path: str, genotypes: List[Dict], part_of: Optional[Sequen
         raise ValueError("-parquet_compression_codec %s is not available (one of %s)"
                          % (codec, ", ".join(sorted(PARQUET_CODECS))))
     comp, ext = PARQUET_CODECS[codec]
-    schema = pa.schema(_arrow_fields("Genotype"),
-                       metadata={"parquet.avro.schema": json.dumps(avro_schema()), "writer.model.name": "avro"})
+    schema = pa.schema(_arrow_fields(record),
+                       metadata={"parquet.avro.schema": json.dumps(avro_schema(record)), "writer.model.name": "avro"})
     os.makedirs(path, exist_ok=False)
     part_of = np.zeros(len(genotypes), np.int64) if part_of is None else np.asarray(part_of, np.int64)
     n_parts = max(1, int(n_parts), int(part_of.max()) + 1 if len(part_of) else 1)
@@ -324,7 +345,7 @@ def write_parquet_dir(path: str, genotypes: List[Dict], part_of: Optional[Sequen
     bounds = np.searchsorted(part_of[order], np.arange(n_parts + 1))
     collector, files = [], []
     for p in range(n_parts):
-        rows = [plain_record("Genotype", genotypes[i]) for i in order[bounds[p]:bounds[p + 1]]]
+        rows = [plain_record(record, genotypes[i]) for i in order[bounds[p]:bounds[p + 1]]]
         table = pa.Table.from_pylist(rows, schema=schema)
         per_row = table.nbytes / max(1, table.num_rows)
         name = "part-r-%05d%s.parquet" % (p, ext)

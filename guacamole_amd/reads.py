@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import gzip
 import io
+import os
 import struct
 import zlib
 from dataclasses import dataclass, field, replace
@@ -273,6 +274,10 @@ def load_reads(path: str, filters: InputFilters = InputFilters(), reference=None
         return rs
     if not contig_lengths_from_dictionary:
         return contig_lengths_from_reads(load_reads(path, filters))
+    from .adam import is_sam_or_bam
+    if not is_sam_or_bam(path):  # Read.scala:345-364: every other name is ADAM AlignmentRecord Parquet
+        from .adam import load_adam
+        return load_adam(path, filters)[0]
     if is_bam(path):
         from .ingest import load_bam  # native (libgqingest); raises if not built
         return load_bam(path, filters)
@@ -282,6 +287,8 @@ def load_reads(path: str, filters: InputFilters = InputFilters(), reference=None
 def is_bam(path: str) -> bool:
     """A BGZF/gzip stream holding BAM (a damaged first block counts: the BAM decoder names
     the fault); anything else is read as SAM text."""
+    if os.path.isdir(path):  # (an ADAM directory)
+        return False
     with open(path, "rb") as fh:
         head = fh.read(2)
     if head != b"\x1f\x8b":

@@ -146,6 +146,30 @@ def test_cli_parquet_equals_json(tmp_path):
             assert x == y
 
 
+def test_cli_adam_read_input_equals_sam(tmp_path):
+    """--reads / --tumor-reads / --normal-reads naming ADAM AlignmentRecord Parquet (any name but
+    .bam / .sam: Read.scala:345-364, 454-539): both callers write the records they write from the
+    SAM files the ADAM directories were converted from (adam.sam_to_alignment_records)."""
+    from guacamole_amd.adam import sam_to_alignment_records, write_alignment_parquet
+    from guacamole_amd.commands import main
+    ad = {}
+    for name in ("tumor.chr20.tough.sam", "normal.chr20.tough.sam"):
+        ad[name] = str(tmp_path / name.replace(".sam", ".adam"))
+        write_alignment_parquet(ad[name], sam_to_alignment_records(fixture(name)))
+    for cmd, swap in ((["germline-threshold", "--reads", "tumor.chr20.tough.sam", "--threshold", "5"], (2,)),
+                      (["somatic-standard", "--tumor-reads", "tumor.chr20.tough.sam", "--normal-reads",
+                        "normal.chr20.tough.sam", "--min-tumor-read-depth", "8"], (2, 4))):
+        outs = []
+        for src in ("sam", "adam"):
+            c = list(cmd)
+            for k in swap:
+                c[k] = fixture(c[k]) if src == "sam" else ad[c[k]]
+            js = str(tmp_path / ("%s_%s.json" % (cmd[0], src)))
+            assert main(c + ["--out", js]) == 0
+            outs.append(open(js).read())
+        assert outs[0] == outs[1] and len(outs[0]) > 100, cmd[0]
+
+
 def test_synthetic_column_path_dense_outputs(gpu_ctx):
     """emit_ref / emit_no_call through the column kernel (HomRef / NoCall rows inline,
     variant candidates through germline_expand); the column kernel keeps nearly every tile."""

@@ -178,12 +178,14 @@ def test_1000x_panel_over_several_tasks(gpu_ctx):
         assert_rows_match(got, want)
 
 
-def _insertion_sample(n_distinct, n_alt, n_ref, start=100):
+def _insertion_sample(n_distinct, n_alt, n_ref, start=100, n_md_conflict=0):
     """n_distinct reads of distinct 6-base insertions (base quality 2, so the pileup's genotype
     likelihoods stay above FP64 underflow), n_alt reads of one 7-base insertion and n_ref
-    reference reads: 10M kI 10M over a 20-base reference."""
+    reference reads: 10M kI 10M over a 20-base reference.  n_md_conflict more reads whose MD tag
+    puts a G at the insertions' anchor locus (offset 9, a C in the others' MD-derived reference):
+    the pileup reference base there depends on heap order (Pileup.scala:157-165)."""
     ref = "ACGTTGCAACGGTACCATGA"
-    reads = []
+    reads = [mr(ref[:9] + "T" + ref[10:], "20M", "9G10", start, mapq=60)] * n_md_conflict
     for i in range(n_distinct):
         ins = "".join("ACGT"[(i >> (2 * k)) & 3] for k in range(6))
         reads.append(mr(ref[:10] + ins + ref[10:], "10M6I10M", "20", start, quals=[2] * 26, mapq=60))
@@ -207,4 +209,48 @@ def test_more_alleles_than_the_deep_table(gpu_ctx, n_tumor, n_normal):
         got = somatic_standard_reads(gpu_ctx, t, n, loci, **params)
         want = O.somatic_standard(t, n, loci, **params)
         assert len(want) > 0
+        assert_rows_match(got, want)
+
+
+def test_wide_candidate_at_a_heap_order_locus(gpu_ctx):
+    """A tumor locus with more distinct insertion alleles than the deep table (the wide kernel's)
+    whose reference base depends on heap order (the reads' MD tags disagree there): the
+    heap-order replay hands it to the wide kernel with the resolved base instead of raising a
+    capacity error; rows equal the oracle's."""
+    t = _insertion_sample(200, 40, 100, n_md_conflict=30)
+    n = _insertion_sample(0, 0, 60)
+    loci = _loci(t, "chr1:90-130")
+    for mode in (0, 1):
+        got = somatic_standard_reads(gpu_ctx, t, n, loci, apply_filters=mode)
+        want = O.somatic_standard(t, n, loci, apply_filters=mode)
+        assert_rows_match(got, want)
+
+
+def test_reads_sharing_pool_words(gpu_ctx):
+    """Wrapped device reads whose MD events and CIGAR share pool words (a deduplicated pool):
+    the column records' auxiliary list is sized from the pools, so it cannot hold every read's
+    events; the reads past its allocation get no list and their tiles go to the walkers instead
+    of being written past its end.  Somatic rows equal the unshared upload's and the oracle's."""
+    from guacamole_amd import soa
+    from test_gpu_germline import _DeviceArray
+    ref = "ACGTTGCAACGGTACCATGACCGTAGGTCA"
+    alt = ref[:5] + "T" + ref[6:]  # read base T where the MD tag says G
+    t = make_read_set([mr(alt, "30M", "5G24", 100, mapq=60)] * 300 + [mr(ref, "30M", "30", 100, mapq=60)] * 100)
+    n = make_read_set([mr(ref, "30M", "30", 100, mapq=60)] * 60)
+    loci = _loci(t, "chr1:90-140")
+    a = soa.pack(t)
+    ev = a["n_md"] > 0
+    shared = dict(a, cigar=a["cigar"][:1].copy(), cigar_off=np.zeros_like(a["cigar_off"]),
+                  md_ev=a["md_ev"][a["md_off"][ev][:1]].copy(), md_off=np.zeros_like(a["md_off"]))
+    assert int(a["n_md"].sum()) > int(shared["md_ev"].shape[0]) + 6 * int(shared["cigar"].shape[0])
+    dev = {k: (_DeviceArray(v) if np.ndim(v) else v) for k, v in shared.items()}
+    tw = gpu_ctx.wrap_device(dev)
+    tu = gpu_ctx.upload(a)
+    nd = gpu_ctx.upload(soa.pack(n))
+    for mode in (0, 1):
+        got = gpu_ctx.somatic_standard(tw, nd, loci, apply_filters=mode).rows
+        assert got == gpu_ctx.somatic_standard(tu, nd, loci, apply_filters=mode).rows
+        got = [dict(r, contig=t.contig_names[r["contig"]]) for r in got]
+        want = O.somatic_standard(t, n, loci, apply_filters=mode)
+        assert len(want) == 1
         assert_rows_match(got, want)
