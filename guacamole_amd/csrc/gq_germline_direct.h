@@ -6,27 +6,31 @@
 // back, no row assignment, and no separate A/C/G/T/N scan of the pool (pool_clean).
 //
 // One WAVE per 512-locus tile (aligned to a 512-locus block B0), four waves per workgroup, each
-// on its own tiles, as germline_proj.  Lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8);
-// lanes 16g .. 16g + 15 own slice g (loci [B0 + 128g, B0 + 128g + 128)).  The tile's read window
-// goes through in rounds of 64 reads (SlidingWindow.scala:83-128: every read overlapping the
-// block, start-sorted):
+// on its own tiles, as germline_proj.  Lane l owns the 8-locus column [B0 + 8l, B0 + 8l + 8).
+// The tile's read window (SlidingWindow.scala:83-128: every read overlapping the block, in start
+// order) goes through in chunks of up to kSlots runs:
 //
-//   records   lane = read: its fields in one round of coalesced loads, a 16-byte record in LDS
-//             (loci [s, e) of its Match/Mismatch elements and the pool offset of the base at s);
-//             a general CIGAR's count segments (general_segments, PileupElement.scala:68-248)
-//             become records of their own; its complex ranges (insertion / deletion anchors,
-//             clipped N-skips) and MidDeletion ranges go into LDS difference words; MD events
-//             (PileupElement.scala:108-118, Pileup.scala:157-165) into the reference-base mask
-//             and the event read-base counts, as germline_proj's sparse entries do.
-//   counts    slice g walks the round's records that can overlap it (a start-sorted prefix,
-//             from the first read ending past the slice's first locus): lane l16 loads the 8
-//             bases of its column with one unaligned 8-byte load (four records' loads issued
-//             before any is used), masks the loci outside the record, and counts them in SWAR
-//             registers through v_perm tables (A C T G in nibbles folded into bytes every 12
-//             records, N in bytes, all widened into 16-bit pairs every 240).  The same v_perm
-//             checks every counted byte is one of A C G T N; a block with any other byte (an
-//             "other" base allele), a read without MD, a CIGAR the segments cannot express, or
-//             more than 65535 window reads goes to germline_walk, which is exact for every read.
+//   runs     lane = read, 64 reads a round: the read's fields in one round of coalesced loads;
+//            each run of its Match/Mismatch elements in the block (one for a [S|H]* M [S|H]*
+//            read, a general CIGAR's count segments from general_segments: PileupElement.scala:
+//            68-248) becomes an 8-byte slot in LDS (first / end locus relative to B0, the pool
+//            offset of the column's bytes relative to the tile's base); a slot marks the columns
+//            it spans in two per-column words (the last slot starting at or before the column,
+//            the first slot ending in or after it: LDS max / min).  A general CIGAR's complex
+//            ranges (insertion / deletion anchors, clipped N-skips) and MidDeletion ranges go
+//            into LDS difference words; MD events (PileupElement.scala:108-118, Pileup.scala:
+//            157-165) into the reference-base mask and the event read-base counts, as
+//            germline_proj's sparse entries do.
+//   counts   lane l walks only the slots that can cover its column: [first slot ending past the
+//            column's first locus, last slot starting before its end] — a prefix maximum and a
+//            suffix minimum of the per-column words.  One unaligned 8-byte buffer load per slot
+//            (three batches of four in flight), the loci outside the run masked, the bases
+//            counted in SWAR registers through v_perm tables (A C T G in nibbles folded into
+//            bytes every 12 slots, N in bytes; the DEEP instantiation widens into 16-bit pairs
+//            every 240).  The same v_perm checks every counted byte is one of A C G T N; a block
+//            with any other byte (an "other" base allele), a read without MD, a CIGAR the
+//            segments cannot express, a round of more than kSlots runs, or more than 65535 window
+//            reads goes to germline_walk, which is exact for every read.
 //
 // Then each lane makes the GermlineThreshold decision (GermlineThresholdCaller.scala:90-179) for
 // its eight loci exactly as germline_proj does (variant candidates, Ref / NoCall records and
@@ -44,19 +48,12 @@ struct DirCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = 4;     // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kU = 4;         // records per batch (their loads issued before use)
+  static constexpr int kU = 4;         // slots per batch (their loads issued before use)
   static constexpr int kRound = 64;    // window reads per round (a lane each)
-  static constexpr int kXCap = 48;     // count segments of a round's general-CIGAR reads
+  static constexpr int kSlots = 256;   // runs per chunk (LDS slots)
   static constexpr int64_t kMaxWin = 65535;  // window reads (16-bit counts); more: germline_walk
   static constexpr int64_t kShallow = 255;   // window reads of the byte-count instantiation
 };
-
-// A run of Match/Mismatch elements: loci [s, e) whose bases start at pool offset p (lo | hi << 32).
-struct __attribute__((aligned(16))) DirRec {
-  int32_t s, e;
-  uint32_t plo, phi;
-};
-static_assert(sizeof(DirRec) == 16, "DirRec: one 16-byte LDS read");
 
 // bytes [a, b) of a 64-bit word (0 <= a, b <= 8)
 __device__ __forceinline__ uint64_t byte_range_mask(int32_t a, int32_t b) {
@@ -65,37 +62,64 @@ __device__ __forceinline__ uint64_t byte_range_mask(int32_t a, int32_t b) {
   return lt & ge;
 }
 
+// Inclusive prefix maximum / suffix minimum over the 64 lanes (every lane active).
+__device__ __forceinline__ int32_t wave_incl_max_i(int32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v = max(v, y);
+  }
+  return v;
+}
+__device__ __forceinline__ int32_t wave_suffix_min_i(int32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t y = __shfl_down(v, d, 64);
+    if (lane + d < 64) v = min(v, y);
+  }
+  return v;
+}
+
 // DEEP = false: every tile whose window holds at most kShallow reads (per-locus counts fit bytes:
-// no 16-bit widening, three batches of loads in flight); deeper tiles are listed (deep,
-// ctr->n_deep) for the DEEP instantiation, whose waves take them from the list and widen the
-// counts into 16-bit pairs every 240 records (two batches in flight), writing into the walker's
-// output partitions.
+// no 16-bit widening; event counts in bytes); deeper tiles are listed (deep, ctr->n_deep) for the
+// DEEP instantiation, whose waves take them from the list, widen the counts into 16-bit pairs
+// every 240 slots, and write into the walker's output partitions.
 template <bool DEEP>
 __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_eu(GQ_DIR_WPE))) void germline_direct(
     const Tile *__restrict__ tiles, int64_t n_tiles, DevReads R, int threshold, int emit_ref, int emit_no_call,
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr, int32_t *__restrict__ slow,
     int32_t *__restrict__ deep, int dbg) {
   // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the base loads, 4 skip the
-  // decision, 16 phase clocks
+  // decision, 16 phase clocks, 32 skip the counting
   using C = DirCfg;
   constexpr int T = C::kT, U = C::kU;
-  // per locus, as germline_proj: event read bases (A | C << 16 at [x], T | G << 16 at [T + x]),
-  // MD bits 0-3 | complex diff << 16, MidDeletion diffs; locus x of the block at word
-  // ix(x) = (x & 7) * 64 + (x >> 3) (a lane's eight loci on 64 consecutive words each)
-  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][2 * T];
+  constexpr int EW = DEEP ? 2 * T : T;  // event words: 16-bit pairs (DEEP) or four bytes per locus
+  // per locus, locus x of the block at word ix(x) = (x & 7) * 64 + (x >> 3) (a lane's eight loci
+  // on 64 consecutive words each): event read bases (DEEP: A | C << 16 at [x], T | G << 16 at
+  // [T + x]; else A | C << 8 | T << 16 | G << 24 at [x]), MD bits 0-3 | complex diff << 16,
+  // MidDeletion diffs
+  __shared__ __attribute__((aligned(16))) uint32_t evw[C::kWaves][EW];
   __shared__ __attribute__((aligned(16))) uint32_t mkw[C::kWaves][T];
   __shared__ __attribute__((aligned(16))) uint32_t dlw[C::kWaves][T];
-  __shared__ DirRec rcw[C::kWaves][C::kRound + C::kXCap];  // the round's reads, then its segments
+  // the chunk's slots (first locus - B0 | end locus - B0 << 16 as int16s, pool offset of B0's
+  // column relative to the tile's base) and per column the last slot starting at or before it /
+  // the first slot ending in or after it
+  __shared__ __attribute__((aligned(16))) uint2 rcw[C::kWaves][C::kSlots];
+  __shared__ int32_t hxw[C::kWaves][64], hnw[C::kWaves][64];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint32_t *ev = evw[wave], *mk = mkw[wave], *dl = dlw[wave];
-  DirRec *rc = rcw[wave];
+  uint2 *rc = rcw[wave];
+  int32_t *hx = hxw[wave], *hn = hnw[wave];
   auto ix = [](int32_t x) { return ((x & 7) << 6) | (x >> 3); };
   auto zero_words = [&]() {  // 16-byte stores, lane l at 16 l (no conflicts)
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
     uint4 *e4 = reinterpret_cast<uint4 *>(ev), *m4 = reinterpret_cast<uint4 *>(mk), *d4 = reinterpret_cast<uint4 *>(dl);
-    e4[lane] = z4; e4[64 + lane] = z4; e4[128 + lane] = z4; e4[192 + lane] = z4;
+#pragma unroll
+    for (int q = 0; q < EW / 256; ++q) e4[64 * q + lane] = z4;
     m4[lane] = z4; m4[64 + lane] = z4; d4[lane] = z4; d4[64 + lane] = z4;
   };
   zero_words();
@@ -113,39 +137,36 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
   };
   unsigned visited = 0, amb = 0, ties = 0;
   uint64_t clk[6] = {0, 0, 0, 0, 0, 0};
-  const int g = lane >> 4;
   const bool multi_sample = R.n_samples > 1;
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
   const uint32_t thr1b = thr1u & 0xFFu;
   auto passes = [=](uint32_t count, uint32_t depth) { return (count & 0xFFFFu) * 100u >= thr1b * (depth & 0xFFFFu); };
-  // the Tile record of the wave's next tile (dword d on lane d < 16), one tile ahead
+  // a tile's record: dword d on lane d < 16, every field read into scalars at once (a VGPR read
+  // lane by lane later must not live across the tile: the register allocator may spill it under a
+  // partial exec mask, which keeps only the active lanes' values)
   const __amdgpu_buffer_rsrc_t trs =
       __builtin_amdgcn_make_buffer_rsrc((void *)tiles, (short)0, (int)(64 * n_tiles), 0x00020000);
   const uint32_t tvo = lane < 16 ? 4u * (uint32_t)lane : 0x80000000u;
   auto fetch = [&](int64_t t) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(trs, (int)tvo, (int)(64 * t), 0); };
   auto f32 = [](uint32_t rec, int d) { return (uint32_t)__builtin_amdgcn_readlane((int)rec, d); };
   auto f64 = [&](uint32_t rec, int d) { return (int64_t)((uint64_t)f32(rec, d) | ((uint64_t)f32(rec, d + 1) << 32)); };
+  const int32_t colr = 8 * lane;  // this lane's column, relative to the block: loci [B0 + colr, B0 + colr + 8)
   // DEEP: the listed tiles, a wave at a time over the grid; else this workgroup's run of tiles
   const int64_t n_deep = DEEP ? (int64_t)min(ctr->n_deep, (unsigned long long)n_tiles) : 0;
   const int64_t iend = DEEP ? n_deep : i1, istep = DEEP ? (int64_t)gridDim.x * C::kWaves : C::kWaves;
   int64_t i = DEEP ? (int64_t)blockIdx.x * C::kWaves + wave : i0 + wave;
-  uint32_t rec_c = !DEEP && i < i1 ? fetch(i) : 0u;
-  uint32_t rec_n = !DEEP && i + C::kWaves < i1 ? fetch(i + C::kWaves) : 0u;
   for (; i < iend; i += istep) {
     const uint64_t t_a = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     const int64_t tid = DEEP ? (int64_t)__builtin_amdgcn_readfirstlane(deep[i]) : i;  // the tile
-    uint32_t rec = rec_c;
-    if (DEEP) {
-      rec = fetch(tid);
-    } else {
-      rec_c = rec_n;
-      if (i + 2 * C::kWaves < i1) rec_n = fetch(i + 2 * C::kWaves);
-    }
     // Tile: ordinal0 dw 0-1, rb 2-3, re 4-5, contig 6, L0 7, L1 8
+    const uint32_t rec = fetch(tid);
+    const int64_t ord0 = f64(rec, 0);
+    const int32_t tcontig = (int32_t)f32(rec, 6);
     const int32_t L0 = (int32_t)f32(rec, 7), L1 = (int32_t)f32(rec, 8);
     const int64_t rb = f64(rec, 2), re = f64(rec, 4);
     const int32_t B0 = L0 & ~(T - 1);
+    const int32_t col = B0 + colr;
     if (re <= rb) continue;  // no reads: nothing visited
     if (re - rb > C::kMaxWin) {
       if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)tid;
@@ -156,10 +177,9 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       continue;
     }
     // ---- counters: nibbles (A | C << 4 per byte in nac, T | G << 4 in ntg; loci 0-3 of the
-    //      column in [0], 4-7 in [1]) folded into byte counters every 12 records, N straight
-    //      into bytes, widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 records
+    //      column in [0], 4-7 in [1]) folded into byte counters every 12 slots, N straight into
+    //      bytes; DEEP: widened into 16-bit pairs (loci 2q, 2q + 1 in w?[q]) every 240 slots
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0}, cn[2] = {0, 0};
-    // (DEEP only: the shallow instantiation's counts stay in the bytes)
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0},
              wN[4] = {0, 0, 0, 0};
     uint32_t nac[2] = {0, 0}, ntg[2] = {0, 0};
@@ -191,13 +211,10 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       w2(wG, cg);
       w2(wN, cn);
     };
-    const int32_t col = B0 + 8 * lane;  // this lane's column: loci [col, col + 8)
-    uint32_t started = 0;  // bit g: a window read ending past slice g's first locus was seen (uniform)
-    bool bad = false;      // this lane saw a read the kernel cannot take (the block goes to the walker)
-    uint32_t badb = 0;     // counted bytes other than A C G T N
+    bool bad = false;   // this lane saw a read the kernel cannot take (the block goes to the walker)
+    uint32_t badb = 0;  // counted bytes other than A C G T N
     const uint64_t t_b = (dbg & 16) ? __builtin_readcyclecounter() : 0;
-    // the round's fields (lane = read), loaded one round ahead: they are in flight while the
-    // previous round's bases are counted
+    // the round's fields (lane = read), loaded one round ahead
     struct Fields {
       int32_t s, e, nmd, ld;
       int64_t so, mo;
@@ -215,231 +232,207 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       }
       return f;
     };
+    // the tile's pool base: the lowest pool offset of its first round's reads, less 8 (a column
+    // may start up to 7 loci before its run); a run whose bytes lie below it or 2^31 past it
+    // sends the block to the walker.  A load of a dead (slot, column) pair takes an offset past
+    // the buffer's range and reads 0 without touching memory.
+    int64_t tbase = 0;
+    __amdgpu_buffer_rsrc_t srs;
     Fields nf = load_fields(rb);
-    for (int64_t c0 = rb; c0 < re; c0 += C::kRound) {
-      // ---- the round's reads, lane = read
-      const int64_t r = c0 + lane;
-      const bool valid = r < re;
-      const Fields f = nf;
-      if (c0 + C::kRound < re) nf = load_fields(c0 + C::kRound);
-      const int32_t s = f.s, e = f.e, nmd = f.nmd, ld = f.ld;
-      const int64_t so = f.so, mo = f.mo;
-      const bool nomd = valid && nmd < 0;  // MappedRead.scala:57-60: the walker raises it where it applies
-      const bool gen = valid && !nomd && ld < 0;
-      const int64_t p0 = so + (ld > 0 ? ld : 0);
-      {
-        DirRec d;
-        d.s = s;
-        d.e = valid && !nomd && !gen ? e : s;  // (a general read's runs: its segments below)
-        d.plo = (uint32_t)(uint64_t)p0;
-        d.phi = (uint32_t)((uint64_t)p0 >> 32);
-        rc[lane] = d;
-      }
-      bad = bad || nomd;
-      // the first four MD events in the block and the read bases under them: loaded now, applied
-      // after the counting (their latency hides behind it)
-      const bool evs = valid && !nomd && nmd > 0 && s < B0 + T;
-      uint32_t v4[4] = {0u, 0u, 0u, 0u}, b4 = 0u;  // (b4: byte j = event j's read base)
-      if (evs) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int32_t k = j < nmd ? j : nmd - 1;
-          v4[j] = R.md_ev[mo + k];
-          b4 |= (uint32_t)R.ev_rb[mo + k] << (8 * j);
-        }
-      }
-      // slice g's reads in this round: [lo_g, hi_g).  Reads are start-sorted, so those starting
-      // before the slice's end are a prefix; the first read overlapping the slice is at or after
-      // the window's first read ending past its first locus (pmax_end of the reads before the
-      // window is <= B0: the running maximum first exceeds a locus at the first such read).
-      int32_t lo4[4], hi4[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int32_t S0 = B0 + 128 * q;
-        const uint64_t hb = __ballot(valid && s < S0 + 128);
-        const uint64_t lb = __ballot(valid && e > S0);
-        hi4[q] = __popcll(hb);
-        lo4[q] = ((started >> q) & 1u) ? 0 : (lb ? __ffsll((long long)lb) - 1 : C::kRound);
-        started |= (lb ? 1u : 0u) << q;
-      }
-      // the round's bytes through one buffer from the lowest pool offset of its reads (less 8:
-      // a column may start up to 7 loci before its read); a load of a dead (record, column)
-      // pair takes an offset past the buffer's range and reads 0 without touching memory
-      int64_t so_min = valid ? so : INT64_MAX;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int64_t o = __shfl_xor(so_min, d, 64);
-        so_min = o < so_min ? o : so_min;
-      }
-      int64_t base = so_min >= 8 ? so_min - 8 : 0;  // (uniform: the buffer descriptor in scalar registers)
-      base = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)base >> 32)) << 32) |
-                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)base));
-      const int64_t span = R.seq_cap - base;
-      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(R.seq + base), (short)0, (int)(span < 0x7FFFFFFF ? span : 0x7FFFFFFF), 0x00020000);
-      // (a read whose bytes could lie past 2^31 - 16 of the buffer: the walker takes the block)
-      bad = bad || (valid && so + (ld > 0 ? ld : 0) + (e > s ? e - s : 0) + 16400 - base >= 0x7FFFFFF0ll);
-      // a general CIGAR (PileupElement.scala:68-248 as walk_read_lane): its complex / MidDeletion
-      // ranges as differences over the block; its count segments in the block counted here and
-      // written as records below, kXCap of the round's at a time
-      uint32_t nseg = 0;
-      if (gen) {
-        const bool ok = general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t, int32_t) {
-          const int32_t a = s + ro, b = a + len;
-          if (b <= B0 || a >= B0 + T) return;
-          if (kind == kSegCount) {
-            ++nseg;
-          } else {
-            const bool mid = kind == kSegMidDel;  // MidDeletion elements: their own count
-            uint32_t *dw = mid ? dl : mk;
-            const int32_t x0 = a > B0 ? a : B0, x1 = b < B0 + T ? b : B0 + T;
-            atomicAdd(&dw[ix(x0 - B0)], mid ? 1u : 1u << 16);
-            if (x1 < B0 + T) atomicAdd(&dw[ix(x1 - B0)], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
-          }
-        });
-        bad = bad || !ok;
-      }
-      const uint32_t seg_incl = wave_incl_scan(nseg);
-      const uint32_t seg_first = seg_incl - nseg;  // this lane's first segment in the round's list
-      const uint32_t seg_total = (uint32_t)__builtin_amdgcn_readlane((int)seg_incl, 63);
-      // ---- slice g's records: main [lo_g, hi_g) (first pass), then the segments, kXCap per pass
-      const int32_t glo = g == 0 ? lo4[0] : g == 1 ? lo4[1] : g == 2 ? lo4[2] : lo4[3];
-      const int32_t ghi = g == 0 ? hi4[0] : g == 1 ? hi4[1] : g == 2 ? hi4[2] : hi4[3];
-      int32_t kmain = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) kmain = max(kmain, hi4[q] > lo4[q] ? hi4[q] - lo4[q] : 0);
-      for (uint32_t xb = 0;; xb += (uint32_t)C::kXCap) {
-        const int32_t nx = seg_total > xb ? (int32_t)min(seg_total - xb, (uint32_t)C::kXCap) : 0;
-        if (nseg > 0 && seg_first < xb + (uint32_t)C::kXCap && seg_first + nseg > xb) {
-          uint32_t j = seg_first;
-          (void)general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t sp, int32_t) {
-            const int32_t a = s + ro, b = a + len;
-            if (kind != kSegCount || b <= B0 || a >= B0 + T) return;
-            if (j >= xb && j < xb + (uint32_t)C::kXCap) {
-              const int64_t p = so + sp;
-              DirRec d;
-              d.s = a;
-              d.e = b;
-              d.plo = (uint32_t)(uint64_t)p;
-              d.phi = (uint32_t)((uint64_t)p >> 32);
-              rc[C::kRound + (j - xb)] = d;
-            }
-            ++j;
-          });
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const int32_t nmain = xb == 0 && ghi > glo ? ghi - glo : 0;
-        const int32_t nl = nmain + nx;
-        const int32_t kmax = (xb == 0 ? kmain : 0) + nx;
-        // record j of slice g: rc[glo + j] (main), rc[kRound + j - nmain] (segments)
-        const int32_t off_main = glo, off_seg = C::kRound - nmain;
-        // a batch: U records' 8-byte loads, all issued before any is used; mt = the loci of the
-        // column inside the record [a, b) | the bytes the load starts early (p < 0) << 8
-        auto issue = [&](int32_t k0, uint2 (&x)[U], uint32_t (&mt)[U]) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int32_t j = k0 + u;
-            const bool mine = j < nl;
-            const int32_t idx = mine ? j + (j < nmain ? off_main : off_seg) : 0;
-            const DirRec d = rc[idx];
-            const int32_t rel = col - d.s;  // the column's first locus, as a read position
-            const int32_t len = mine ? d.e - d.s : 0;
-            const int32_t a = min(max(-rel, 0), 8), b = min(max(len - rel, 0), 8);
-            const int64_t p = (int64_t)(((uint64_t)d.phi << 32) | d.plo) + rel;
-            const int64_t q = p > 0 ? p : 0;
-            const uint32_t vo = b > a && !(dbg & 1) ? (uint32_t)(q - base) : 0x80000000u;
-            const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
-            x[u] = make_uint2(w[0], w[1]);
-            mt[u] = (uint32_t)a | ((uint32_t)(b > a ? b : a) << 4) | ((uint32_t)(q - p) << 8);
-          }
-        };
-        auto count = [&](const uint2 (&x)[U], const uint32_t (&mt)[U]) {
-          if (nn + U > 15) fold();
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            uint64_t w = (uint64_t)x[u].x | ((uint64_t)x[u].y << 32);
-            w <<= 8 * (mt[u] >> 8);  // byte j = pool[p + j]
-            const uint64_t m = byte_range_mask((int32_t)(mt[u] & 15u), (int32_t)((mt[u] >> 4) & 15u));
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const uint32_t wh = (uint32_t)(w >> (32 * h)), mh = (uint32_t)(m >> (32 * h));
-              const uint32_t xc = wh & 0x07070707u;
-              // the byte a code stands for: A 1, C 3, T 4, N 6, G 7 (codes 0 2 5: none)
-              const uint32_t ex = __builtin_amdgcn_perm(0x474EFF54u, 0x43FF41FFu, xc);
-              badb |= (dbg & 1) ? 0u : (wh ^ ex) & mh;
-              const uint32_t cd = xc & mh;
-              nac[h] += __builtin_amdgcn_perm(0u, 0x10000100u, cd);  // A -> 0x01, C -> 0x10
-              ntg[h] += __builtin_amdgcn_perm(0x10000001u, 0u, cd);  // T -> 0x01, G -> 0x10
-              cn[h] += __builtin_amdgcn_perm(0x00010000u, 0u, cd);   // N -> 0x01
-            }
-          }
-          nn += U;
-          since += U;
-          if (DEEP && since == 240) {  // uniform: bytes hold 240 records at most
-            fold();
-            widen();
-            since = 0;
-          }
-        };
-        if (kmax > 0 && DEEP) {  // one batch in flight while one is counted (the 16-bit counters' registers)
-          uint2 xa[U], xb2[U];
-          uint32_t ma[U], mb[U];
-          issue(0, xa, ma);
-          for (int32_t k0 = 0;; k0 += 2 * U) {
-            issue(k0 + U, xb2, mb);
-            count(xa, ma);
-            if (k0 + U >= kmax) break;
-            issue(k0 + 2 * U, xa, ma);
-            count(xb2, mb);
-            if (k0 + 2 * U >= kmax) break;
-          }
-        } else if (kmax > 0) {  // two batches in flight while one is counted
-          uint2 xa[U], xb2[U], xc2[U];
-          uint32_t ma[U], mb[U], mc[U];
-          issue(0, xa, ma);
-          issue(U, xb2, mb);
-          for (int32_t k0 = 0;; k0 += 3 * U) {
-            issue(k0 + 2 * U, xc2, mc);
-            count(xa, ma);
-            if (k0 + U >= kmax) break;
-            issue(k0 + 3 * U, xa, ma);
-            count(xb2, mb);
-            if (k0 + 2 * U >= kmax) break;
-            issue(k0 + 4 * U, xb2, mb);
-            count(xc2, mc);
-            if (k0 + 3 * U >= kmax) break;
-          }
-        }
-        if (xb + (uint32_t)C::kXCap >= seg_total) break;
-      }
-      // MD events in the block: the MD reference base's bit, and the read base's count where it
-      // is A C T G (an N there is counted with the bases; on a deletion there is no read base)
-      if (evs) {
-        for (int32_t k0 = 0; k0 < nmd; k0 += 4) {
-          if (k0 > 0) {  // (past the first four: rare)
-            b4 = 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int32_t k = k0 + j < nmd ? k0 + j : nmd - 1;
-              v4[j] = R.md_ev[mo + k];
-              b4 |= (uint32_t)R.ev_rb[mo + k] << (8 * j);
-            }
-          }
-          bool past = false;
+    int64_t c0 = rb;
+    bool first_round = true;
+    while (c0 < re) {  // ---- a chunk: rounds while their runs fit kSlots slots, then the counting
+      const uint64_t t_round = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+      hx[lane] = -1;
+      hn[lane] = 0x7FFFFFFF;
+      int32_t nslot = 0;
+      while (c0 < re) {
+        const int64_t r = c0 + lane;
+        const bool valid = r < re;
+        const Fields f = nf;
+        const int32_t s = f.s, e = f.e, nmd = f.nmd, ld = f.ld;
+        const int64_t so = f.so, mo = f.mo;
+        const bool nomd = valid && nmd < 0;  // MappedRead.scala:57-60: the walker raises it where it applies
+        const bool gen = valid && !nomd && ld < 0;
+        // runs of this read in the block: one for a simple read, the count segments of a general one
+        uint32_t nrun = valid && !nomd && !gen && e > B0 && s < B0 + T ? 1u : 0u;
+        // the read's first four MD events, in flight while its runs are placed
+        const bool evr = valid && !nomd && nmd > 0 && s < B0 + T;
+        uint32_t v4[4] = {0u, 0u, 0u, 0u}, b4 = 0u;  // (b4: byte j = event j's read base)
+        auto load_ev = [&](int32_t k0) {
+          b4 = 0u;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int32_t l = s + (int32_t)(v4[j] >> 8);
-            past = past || l >= B0 + T;
-            if (k0 + j >= nmd || l < B0 || l >= B0 + T) continue;
-            const int32_t x = ix(l - B0);
-            const uint32_t m = std_bit((uint8_t)(v4[j] & 0xFFu));
-            if (m) atomicOr(&mk[x], m);
-            const uint8_t rbj = (uint8_t)(b4 >> (8 * j));
-            const int cat = rbj == 0 ? 7 : base_cat(rbj);
-            if (cat < 4) atomicAdd(&ev[(cat >> 1) * T + x], 1u << (16 * (cat & 1)));
+            const int32_t k = k0 + j < nmd ? k0 + j : nmd - 1;
+            v4[j] = R.md_ev[mo + k];
+            b4 |= (uint32_t)R.ev_rb[mo + k] << (8 * j);
           }
-          if (past) break;
+        };
+        if (evr) load_ev(0);
+        if (gen) {
+          const bool ok = general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t, int32_t) {
+            const int32_t a = s + ro, b = a + len;
+            if (kind == kSegCount && b > B0 && a < B0 + T) ++nrun;
+          });
+          bad = bad || !ok;
         }
+        const uint32_t incl = wave_incl_scan(nrun);
+        const int32_t total = (int32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (nslot > 0 && nslot + total > C::kSlots) break;  // (the round opens the next chunk)
+        if (total > C::kSlots) {  // (one round's runs past the slots: the walker)
+          bad = true;
+          c0 = re;
+          break;
+        }
+        if (c0 + C::kRound < re) nf = load_fields(c0 + C::kRound);  // the next round's, in flight
+        if (first_round) {  // the tile's pool base, from the first round's reads
+          int64_t so_min = valid ? so : INT64_MAX;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_xor(so_min, d, 64);
+            so_min = o < so_min ? o : so_min;
+          }
+          tbase = so_min >= 8 ? so_min - 8 : 0;  // (uniform: the buffer descriptor in scalar registers)
+          tbase = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)tbase >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)tbase));
+          const int64_t span = R.seq_cap - tbase;
+          srs = __builtin_amdgcn_make_buffer_rsrc((void *)(R.seq + tbase), (short)0,
+                                                  (int)(span < 0x7FFFFFFF ? span : 0x7FFFFFFF), 0x00020000);
+          first_round = false;
+        }
+        bad = bad || nomd ||
+              (valid && (so < tbase || so + (ld > 0 ? ld : 0) + (e > s ? e - s : 0) + 16384 + 1024 - tbase >= 0x7FFFFFF0ll));
+        // the runs into their slots, each marking the columns it spans
+        int32_t slot = nslot + (int32_t)(incl - nrun);
+        auto put = [&](int32_t a, int32_t b, int64_t p) {  // loci [a, b) whose bases start at pool offset p
+          const int32_t s16 = min(max(a - B0, -32768), 32767), e16 = min(max(b - B0, -32768), 32767);
+          const int32_t K = (int32_t)(p - tbase - (int64_t)(a - B0));  // pool offset of locus B0 (a virtual one), from the base
+          rc[slot] = make_uint2((uint32_t)(uint16_t)s16 | ((uint32_t)(uint16_t)e16 << 16), (uint32_t)K);
+          atomicMax(&hx[min(max(s16, 0), T - 1) >> 3], slot);
+          atomicMin(&hn[min(max(e16 - 1, 0), T - 1) >> 3], slot);
+          ++slot;
+        };
+        if (nrun && !gen) put(s, e, so + (ld > 0 ? ld : 0));
+        if (gen) {  // count segments into slots; complex / MidDeletion ranges as differences over the block
+          (void)general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t sp, int32_t) {
+            const int32_t a = s + ro, b = a + len;
+            if (b <= B0 || a >= B0 + T) return;
+            if (kind == kSegCount) {
+              put(a, b, so + sp);
+            } else {
+              const bool mid = kind == kSegMidDel;  // MidDeletion elements: their own count
+              uint32_t *dw = mid ? dl : mk;
+              const int32_t x0 = a > B0 ? a : B0, x1 = b < B0 + T ? b : B0 + T;
+              atomicAdd(&dw[ix(x0 - B0)], mid ? 1u : 1u << 16);
+              if (x1 < B0 + T) atomicAdd(&dw[ix(x1 - B0)], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
+            }
+          });
+        }
+        // MD events in the block: the MD reference base's bit, and the read base's count where it
+        // is A C T G (an N there is counted with the bases; on a deletion there is no read base)
+        if (evr) {
+          for (int32_t k0 = 0;;) {
+            bool past = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int32_t l = s + (int32_t)(v4[j] >> 8);
+              past = past || l >= B0 + T;
+              if (k0 + j >= nmd || l < B0 || l >= B0 + T) continue;
+              const int32_t x = ix(l - B0);
+              const uint32_t m = std_bit((uint8_t)(v4[j] & 0xFFu));
+              if (m) atomicOr(&mk[x], m);
+              const uint8_t rbj = (uint8_t)(b4 >> (8 * j));
+              const int cat = rbj == 0 ? 7 : base_cat(rbj);
+              if (cat < 4) {
+                if (DEEP) atomicAdd(&ev[(cat >> 1) * T + x], 1u << (16 * (cat & 1)));
+                else atomicAdd(&ev[x], 1u << (8 * cat));
+              }
+            }
+            k0 += 4;
+            if (past || k0 >= nmd) break;
+            load_ev(k0);
+          }
+        }
+        nslot += total;
+        c0 += C::kRound;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint64_t t_r = (dbg & 16) ? __builtin_readcyclecounter() : 0;
+      // ---- this lane's slots: [first slot ending past its column's first locus, last slot
+      //      starting before its column's end]
+      const int32_t last = wave_incl_max_i(hx[lane]);
+      const int32_t first = wave_suffix_min_i(hn[lane]);
+      const int32_t nl = last >= first ? last - first + 1 : 0;
+      int32_t kmax = nl;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) kmax = max(kmax, __shfl_xor(kmax, d, 64));
+      kmax = (dbg & 32) ? 0 : __builtin_amdgcn_readfirstlane(kmax);  // (dbg & 32: no counting)
+      // a batch: U slots' 8-byte loads, all issued before any is used; mt = the column's loci
+      // inside the run [a, b)
+      auto issue = [&](int32_t k0, uint2 (&x)[U], uint32_t (&mt)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int32_t k = k0 + u;
+          const bool mine = k < nl;
+          const uint2 d = rc[mine ? first + k : 0];
+          const int32_t s16 = (int32_t)(int16_t)(d.x & 0xFFFFu), e16 = (int32_t)(int16_t)(d.x >> 16);
+          const int32_t a = min(max(s16 - colr, 0), 8), b = min(max(e16 - colr, 0), 8);
+          const bool live = mine && b > a && !(dbg & 1);
+          const int32_t vi = (int32_t)d.y + colr;  // (< 0: reads 0, the walker takes the block)
+          const uint32_t vo = live ? (uint32_t)vi : 0x80000000u;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
+          x[u] = make_uint2(w[0], w[1]);
+          mt[u] = live ? (uint32_t)a | ((uint32_t)b << 4) : 0u;
+        }
+      };
+      auto count = [&](const uint2 (&x)[U], const uint32_t (&mt)[U]) {
+        if (nn + U > 15) fold();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t m = byte_range_mask((int32_t)(mt[u] & 15u), (int32_t)((mt[u] >> 4) & 15u));
+          const uint64_t w64 = (uint64_t)x[u].x | ((uint64_t)x[u].y << 32);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t wh = (uint32_t)(w64 >> (32 * h)), mh = (uint32_t)(m >> (32 * h));
+            const uint32_t xc = wh & 0x07070707u;
+            // the byte a code stands for: A 1, C 3, T 4, N 6, G 7 (codes 0 2 5: none)
+            const uint32_t ex = __builtin_amdgcn_perm(0x474EFF54u, 0x43FF41FFu, xc);
+            badb |= (dbg & 1) ? 0u : (wh ^ ex) & mh;
+            const uint32_t cd = xc & mh;
+            nac[h] += __builtin_amdgcn_perm(0u, 0x10000100u, cd);  // A -> 0x01, C -> 0x10
+            ntg[h] += __builtin_amdgcn_perm(0x10000001u, 0u, cd);  // T -> 0x01, G -> 0x10
+            cn[h] += __builtin_amdgcn_perm(0x00010000u, 0u, cd);   // N -> 0x01
+          }
+        }
+        nn += U;
+        since += U;
+        if (DEEP && since == 240) {  // uniform: bytes hold 240 slots at most
+          fold();
+          widen();
+          since = 0;
+        }
+      };
+      if (kmax > 0) {  // two batches in flight while one is counted
+        uint2 xa[U], xb2[U], xc2[U];
+        uint32_t ma[U], mb[U], mc[U];
+        issue(0, xa, ma);
+        issue(U, xb2, mb);
+        for (int32_t k0 = 0;; k0 += 3 * U) {
+          issue(k0 + 2 * U, xc2, mc);
+          count(xa, ma);
+          if (k0 + U >= kmax) break;
+          issue(k0 + 3 * U, xa, ma);
+          count(xb2, mb);
+          if (k0 + 2 * U >= kmax) break;
+          issue(k0 + 4 * U, xb2, mb);
+          count(xc2, mc);
+          if (k0 + 3 * U >= kmax) break;
+        }
+      }
+      if (dbg & 16) {  // phase clocks: the chunk's runs (fields, slots, events) | its counting
+        const uint64_t t_s = __builtin_readcyclecounter();
+        clk[2] += t_r - t_round;
+        clk[3] += t_s - t_r;
       }
     }
     fold();
@@ -492,7 +485,10 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       //      (record pair), 3 complex
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint32_t eacj = ev[64 * j + lane], etgj = ev[T + 64 * j + lane], m8j = m8[j];
+        const uint32_t e0 = ev[64 * j + lane], e1 = DEEP ? ev[T + 64 * j + lane] : 0u;
+        const uint32_t eacj = DEEP ? e0 : (e0 & 0xFFu) | ((e0 & 0xFF00u) << 8);
+        const uint32_t etgj = DEEP ? e1 : ((e0 >> 16) & 0xFFu) | ((e0 >> 8) & 0xFF0000u);
+        const uint32_t m8j = m8[j];
         const int32_t ddj = (int32_t)d8[j];
         const uint32_t cA = cnt(wA, ca, j), cC = cnt(wC, cc, j), cT = cnt(wT, ct, j), cG = cnt(wG, cg, j);
         const uint32_t nN = cnt(wN, cn, j);
@@ -553,12 +549,14 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
         const uint32_t cA = cnt(wA, ca, j), cC = cnt(wC, cc, j), cT = cnt(wT, ct, j), cG = cnt(wG, cg, j);
         const uint32_t mw = mk[64 * j + lane];
         const uint32_t nN = cnt(wN, cn, j);
-        const uint32_t mask = ref_mask(mw, ev[64 * j + lane], ev[T + 64 * j + lane], cA, cC, cT, cG);
+        const uint32_t e0 = ev[64 * j + lane], e1 = DEEP ? ev[T + 64 * j + lane] : 0u;
+        const uint32_t mask = ref_mask(mw, DEEP ? e0 : (e0 & 0xFFu) | ((e0 & 0xFF00u) << 8),
+                                       DEEP ? e1 : ((e0 >> 16) & 0xFFu) | ((e0 >> 8) & 0xFF0000u), cA, cC, cT, cG);
         const uint8_t ref = mask ? bit_base(mask) : (uint8_t)'N';
-        const uint64_t ord = (uint64_t)(f64(rec, 0) + (pos - L0));
+        const uint64_t ord = (uint64_t)(ord0 + (pos - L0));
         CallRec rr;
         rr.key = ord << 12;
-        rr.contig = (int32_t)f32(rec, 6);
+        rr.contig = tcontig;
         rr.pos = pos;
         rr.sample = 0;
         if (kind == 1) {

@@ -1973,8 +1973,10 @@ __global__ void gather_keys(const CallRec *__restrict__ recs, const Counters *__
 // loops and no host round trip; the host reads the counters once, at the end.
 constexpr int kFinBlocks = 1024;  // grid of the record-slot kernels
 constexpr int kImgBlocks = 512;   // calls_image chunks (one workgroup each)
-__global__ __launch_bounds__(kBlock) void bucket_count(const CallRec *__restrict__ recs, const Counters *__restrict__ ctr,
-                                                        OutGeom og, uint64_t dead_key, int bshift,
+// (a record whose key lies past every bucket — a slot a kernel reserved and never wrote — is
+// dropped and raises GQ_E_ASSERT at the slot: an internal fault, reported instead of a wild write)
+__global__ __launch_bounds__(kBlock) void bucket_count(const CallRec *__restrict__ recs, Counters *__restrict__ ctr,
+                                                        OutGeom og, uint64_t dead_key, int bshift, int64_t nbk,
                                                         uint64_t *__restrict__ keys, int32_t *__restrict__ slot,
                                                         int64_t *__restrict__ bkt, uint32_t *__restrict__ cnt) {
   const int64_t n_all = (int64_t)ctr->n_rec;
@@ -1983,7 +1985,19 @@ __global__ __launch_bounds__(kBlock) void bucket_count(const CallRec *__restrict
     const uint64_t key = recs[src].key;
     keys[k] = key;
     slot[k] = (int32_t)src;
-    const int64_t b = key == dead_key ? -1 : (int64_t)(key >> (12 + bshift));
+    int64_t b = key == dead_key ? -1 : (int64_t)(key >> (12 + bshift));
+    if (b >= nbk) {
+      if (atomicCAS(&ctr->err, 0, 1 /*GQ_E_ASSERT*/) == 0) {  // (the record, for the host's message)
+        const CallRec r = recs[src];
+        ctr->err_pos = (long long)src;
+        ctr->prof[0] = key;
+        ctr->prof[1] = ((unsigned long long)(uint32_t)r.contig << 32) | (uint32_t)r.pos;
+        ctr->prof[2] = ((unsigned long long)r.flags << 24) | ((unsigned long long)r.gt1 << 16) | ((unsigned long long)r.gt0 << 8) | r.sample;
+        ctr->prof[3] = (unsigned long long)k;
+        ctr->prof[4] = ctr->n_rec;
+      }
+      b = -1;
+    }
     bkt[k] = b;
     if (b >= 0) atomicAdd(&cnt[b], 1u);
   }
@@ -2697,6 +2711,10 @@ gq_status gq::plan(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *loci, int T
 }
 
 gq_status gq::check_device_error(gq_ctx *c, const Counters &h) {
+  if (h.err == 1 && h.prof[4])  // bucket_count's record past every bucket (an internal fault): its fields
+    fprintf(stderr, "gq: record slot %lld (k %llu of %llu): key %llx contig %d pos %d flags/gt %llx\n",
+            (long long)h.err_pos, h.prof[3], h.prof[4], h.prof[0], (int)(h.prof[1] >> 32), (int)(uint32_t)h.prof[1],
+            h.prof[2]);
   if (h.err) {
     static const char *names[] = {"ok", "assertion", "invalid cigar element", "CIGAR / MD tag mismatch",
                                   "read without MD tag", "multiple reference bases", "unsorted", "argument", "hip",
@@ -2819,7 +2837,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
                        dim3(kBlock), 0, c->stream, cnt, 3 * (nbk + 1));  // counts, (offsets), fills
     const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(((int64_t)cap_rec + kBlock - 1) / kBlock, kFinBlocks));
     hipLaunchKernelGGL(bucket_count, dim3(gb), dim3(kBlock), 0, c->stream, (const CallRec *)c->recs.p,
-                       (const Counters *)ctr, og, dead_key, bshift, (uint64_t *)c->keys.p, (int32_t *)c->idx_sorted.p,
+                       ctr, og, dead_key, bshift, nbk, (uint64_t *)c->keys.p, (int32_t *)c->idx_sorted.p,
                        (int64_t *)c->idx.p, cnt);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, scan_tmp, cnt, off, (int)(nbk + 1), c->stream));
@@ -3041,7 +3059,7 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
             (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
   if ((gq_dbg() & 16) && hc.prof[5])
     fprintf(stderr,
-            "gq prof (cycles/tile/wave): setup+entries %.0f counting %.0f - %.0f widen %.0f decision %.0f (%llu)\n",
+            "gq prof (cycles/tile/wave): setup %.0f chunks %.0f (runs %.0f counting %.0f) decision %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
             (double)hc.prof[3] / hc.prof[5], (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
   for (int k = 0; k < kSpread; ++k) {

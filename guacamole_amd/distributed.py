@@ -30,6 +30,30 @@ def rank_info() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def hip_runtimes() -> List[str]:
+    """The HIP runtime libraries (libamdhip64) mapped into this process."""
+    try:
+        with open("/proc/self/maps") as fh:
+            return sorted({line.split()[-1] for line in fh if "libamdhip64" in line})
+    except OSError:
+        return []
+
+
+def check_hip_runtimes() -> None:
+    """torch ships its own HIP runtime (torch/lib/libamdhip64.so); libgqpileup.so links the
+    system's (/opt/rocm).  When torch is imported first, the library binds to torch's runtime (the
+    same SONAME) and both share one device context.  When libgqpileup.so is loaded first (a
+    native.Context opened before `import torch`), torch brings its own copy and the process holds
+    two HIP runtimes: torch then reports "No HIP GPUs are available" at its first device call.
+    Raise a clear error for that order instead (init_from_env / bench.py import torch before the
+    library at world > 1)."""
+    libs = hip_runtimes()
+    if len(libs) > 1:
+        raise RuntimeError("two HIP runtimes in this process (%s): libgqpileup.so was loaded before torch; import "
+                           "torch (or call guacamole_amd.distributed.init_from_env) before opening a native.Context"
+                           % ", ".join(libs))
+
+
 def init_from_env():
     """Join the process group torch.distributed.run set up (one rank per GPU).  Returns
     (rank, world, local GPU, gather device): the gather device is "cuda:<local>" for RCCL, or
@@ -39,9 +63,10 @@ def init_from_env():
         return rank, world, local, None
     import torch
     import torch.distributed as dist
+    check_hip_runtimes()
     backend = os.environ.get("GQ_DIST_BACKEND", "nccl")
     if dist.is_initialized():  # a caller's group (bench.py runs the commands in its ranks): joined, not owned
-        if backend == "nccl":
+        if dist.get_backend() == "nccl":  # (the group's own backend, not the environment's)
             return rank, world, local, "cuda:%d" % local
         return rank, world, local % max(1, torch.cuda.device_count()), "cpu"
     global OWN_GROUP

@@ -176,3 +176,39 @@ def test_somatic_two_ranks_device_ingest_equal_one(tmp_path):
     two = _run(args, 2, str(tmp_path / "two.json"), reps)
     assert one == two and one.count("\n") > 10
     assert all(r.get("ingest") == "device" for r in reps) and len(reps) == 2
+
+
+def test_native_context_before_torch_fails_clearly_or_works():
+    """The init order of a multi-GPU rank: a native.Context opened before torch
+    touches the GPU, then a torch cuda:0 tensor (the gather's device path).  Either it works, or
+    check_hip_runtimes names the cause (two HIP runtimes: torch's bundled one and the system's)
+    instead of torch's bare "No HIP GPUs are available"."""
+    import subprocess
+    import sys
+    code = ("from guacamole_amd import native\n"
+            "ctx = native.Context(0)\n"
+            "import torch\n"
+            "from guacamole_amd.distributed import check_hip_runtimes, hip_runtimes\n"
+            "print('runtimes', hip_runtimes(), flush=True)\n"
+            "try:\n"
+            "    check_hip_runtimes()\n"
+            "except RuntimeError as e:\n"
+            "    print('CLEAR', e)\n"
+            "    raise SystemExit(3)\n"
+            "x = torch.arange(4, device='cuda:0')\n"
+            "print('OK', int(x.sum().item()))\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    print(r.stdout, r.stderr[-2000:])
+    assert (r.returncode == 0 and "OK 6" in r.stdout) or (r.returncode == 3 and "CLEAR two HIP runtimes" in r.stdout)
+    # the supported order: torch first, one runtime, and it works
+    code2 = ("import torch\n"
+             "torch.cuda.set_device(0)\n"
+             "from guacamole_amd import native\n"
+             "ctx = native.Context(0)\n"
+             "from guacamole_amd.distributed import check_hip_runtimes\n"
+             "check_hip_runtimes()\n"
+             "print('OK', int(torch.arange(4, device='cuda:0').sum().item()))\n")
+    r = subprocess.run([sys.executable, "-c", code2], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and "OK 6" in r.stdout, r.stdout + r.stderr[-2000:]
