@@ -136,7 +136,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     return DEEP ? wave_reserve(&ctr->part[which][part], n) : (unsigned long long)wave_reserve_lds_n(outn + which, n);
   };
   unsigned visited = 0, amb = 0, ties = 0;
-  uint64_t clk[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bool multi_sample = R.n_samples > 1;
   const int64_t thr1 = (int64_t)threshold + 1;
   const uint32_t thr1u = (uint32_t)(thr1 < 0 ? 0 : thr1 > 101 ? 101 : thr1);
@@ -237,6 +237,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     // sends the block to the walker.  A load of a dead (slot, column) pair takes an offset past
     // the buffer's range and reads 0 without touching memory.
     int64_t tbase = 0;
+    bool defer = false;
     __amdgpu_buffer_rsrc_t srs;
     Fields nf = load_fields(rb);
     int64_t c0 = rb;
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       hn[lane] = 0x7FFFFFFF;
       int32_t nslot = 0;
       while (c0 < re) {
+        const uint64_t t_rd = (dbg & 16) ? __builtin_readcyclecounter() : 0;
         const int64_t r = c0 + lane;
         const bool valid = r < re;
         const Fields f = nf;
@@ -258,26 +260,27 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
         uint32_t nrun = valid && !nomd && !gen && e > B0 && s < B0 + T ? 1u : 0u;
         // the read's first four MD events, in flight while its runs are placed
         const bool evr = valid && !nomd && nmd > 0 && s < B0 + T;
-        uint32_t v4[4] = {0u, 0u, 0u, 0u}, b4 = 0u;  // (b4: byte j = event j's read base)
+        uint32_t v4[4] = {0u, 0u, 0u, 0u};
         auto load_ev = [&](int32_t k0) {
-          b4 = 0u;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int32_t k = k0 + j < nmd ? k0 + j : nmd - 1;
-            v4[j] = R.md_ev[mo + k];
-            b4 |= (uint32_t)R.ev_rb[mo + k] << (8 * j);
+          for (int j = 0; j < 4; ++j) v4[j] = R.md_ev[mo + (k0 + j < nmd ? k0 + j : nmd - 1)];
+        };
+        // an event's read base where it is A C T G (an N there is counted with the bases)
+        auto ev_add = [&](int32_t l, uint8_t base) {
+          const int cat = base_cat(base);
+          if (cat < 4) {
+            const int32_t x = ix(l - B0);
+            if (DEEP) atomicAdd(&ev[(cat >> 1) * T + x], 1u << (16 * (cat & 1)));
+            else atomicAdd(&ev[x], 1u << (8 * cat));
           }
         };
         if (evr) load_ev(0);
-        if (gen) {
-          const bool ok = general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t, int32_t) {
-            const int32_t a = s + ro, b = a + len;
-            if (kind == kSegCount && b > B0 && a < B0 + T) ++nrun;
-          });
-          bad = bad || !ok;
-        }
+        // (a general read: slots for its (M|=|X) operations, read_prep's bound on its count
+        // segments; those outside the block stay empty)
+        if (gen && e > B0 && s < B0 + T) nrun = (uint32_t)min(-1 - ld, C::kSlots);
         const uint32_t incl = wave_incl_scan(nrun);
         const int32_t total = (int32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint64_t t_f = (dbg & 16) ? __builtin_readcyclecounter() : 0;
         if (nslot > 0 && nslot + total > C::kSlots) break;  // (the round opens the next chunk)
         if (total > C::kSlots) {  // (one round's runs past the slots: the walker)
           bad = true;
@@ -292,6 +295,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
             const int64_t o = __shfl_xor(so_min, d, 64);
             so_min = o < so_min ? o : so_min;
           }
+          defer = !DEEP && so_min < 8;  // the pool's head: the DEEP instantiation (shifted loads)
           tbase = so_min >= 8 ? so_min - 8 : 0;  // (uniform: the buffer descriptor in scalar registers)
           tbase = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)tbase >> 32)) << 32) |
                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)tbase));
@@ -313,12 +317,27 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
           ++slot;
         };
         if (nrun && !gen) put(s, e, so + (ld > 0 ? ld : 0));
-        if (gen) {  // count segments into slots; complex / MidDeletion ranges as differences over the block
-          (void)general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t sp, int32_t) {
+        if (gen && e > B0 && s < B0 + T) {  // count segments into slots; complex / MidDeletion ranges as differences over the block
+          const int32_t slot_end = slot + (int32_t)nrun;
+          const bool ok = general_segments(R, r, [&](uint32_t kind, int32_t ro, int32_t len, int32_t sp, int32_t) {
             const int32_t a = s + ro, b = a + len;
             if (b <= B0 || a >= B0 + T) return;
             if (kind == kSegCount) {
-              put(a, b, so + sp);
+              if (slot < slot_end) put(a, b, so + sp);
+              else bad = true;  // (more count segments than read_prep's bound: not expected)
+              if (evr) {  // the segment's events in the block: their read bases
+                const int32_t x0 = a > B0 ? a : B0, x1 = b < B0 + T ? b : B0 + T;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const int32_t l = s + (int32_t)(v4[j] >> 8);
+                  if (j < nmd && l >= x0 && l < x1) ev_add(l, R.seq[so + sp + (l - a)]);
+                }
+                for (int32_t k = 4; k < nmd; ++k) {
+                  const int32_t l = s + (int32_t)(R.md_ev[mo + k] >> 8);
+                  if (l >= x1) break;
+                  if (l >= x0) ev_add(l, R.seq[so + sp + (l - a)]);
+                }
+              }
             } else {
               const bool mid = kind == kSegMidDel;  // MidDeletion elements: their own count
               uint32_t *dw = mid ? dl : mk;
@@ -327,26 +346,34 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
               if (x1 < B0 + T) atomicAdd(&dw[ix(x1 - B0)], mid ? 0xFFFFFFFFu : 0xFFFF0000u);
             }
           });
+          bad = bad || !ok;
+          for (; slot < slot_end; ++slot) rc[slot] = make_uint2(0u, 0u);  // empty: no column reads it live
         }
-        // MD events in the block: the MD reference base's bit, and the read base's count where it
-        // is A C T G (an N there is counted with the bases; on a deletion there is no read base)
+        if (dbg & 16) {  // round phase clocks: to the fields and run counts | slots and segments
+          const uint64_t t_g = __builtin_readcyclecounter();
+          clk[6] += t_f - t_rd;
+          clk[7] += t_g - t_f;
+        }
+        // MD events in the block: the MD reference base's bit, and (a simple read; a general
+        // one's went with its count segments) the read base's count: the base at lead + offset
+        // of the (M|=|X) run (lead + run <= sequence: read_prep's shape test)
         if (evr) {
           for (int32_t k0 = 0;;) {
             bool past = false;
+            uint8_t b4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int32_t o = (int32_t)(v4[j] >> 8);
+              b4[j] = !gen && o < e - s ? R.seq[so + ld + o] : (uint8_t)0;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int32_t l = s + (int32_t)(v4[j] >> 8);
               past = past || l >= B0 + T;
               if (k0 + j >= nmd || l < B0 || l >= B0 + T) continue;
-              const int32_t x = ix(l - B0);
               const uint32_t m = std_bit((uint8_t)(v4[j] & 0xFFu));
-              if (m) atomicOr(&mk[x], m);
-              const uint8_t rbj = (uint8_t)(b4 >> (8 * j));
-              const int cat = rbj == 0 ? 7 : base_cat(rbj);
-              if (cat < 4) {
-                if (DEEP) atomicAdd(&ev[(cat >> 1) * T + x], 1u << (16 * (cat & 1)));
-                else atomicAdd(&ev[x], 1u << (8 * cat));
-              }
+              if (m) atomicOr(&mk[ix(l - B0)], m);
+              if (b4[j]) ev_add(l, b4[j]);
             }
             k0 += 4;
             if (past || k0 >= nmd) break;
@@ -378,11 +405,13 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
           const int32_t s16 = (int32_t)(int16_t)(d.x & 0xFFFFu), e16 = (int32_t)(int16_t)(d.x >> 16);
           const int32_t a = min(max(s16 - colr, 0), 8), b = min(max(e16 - colr, 0), 8);
           const bool live = mine && b > a && !(dbg & 1);
-          const int32_t vi = (int32_t)d.y + colr;  // (< 0: reads 0, the walker takes the block)
-          const uint32_t vo = live ? (uint32_t)vi : 0x80000000u;
+          // (vi >= -7 for a live pair, byte a being the run's; < 0 only at the pool's head, whose
+          // tiles the DEEP instantiation takes: its load clamped to the base and shifted back)
+          const int32_t vi = (int32_t)d.y + colr;
+          const uint32_t vo = live ? (uint32_t)(DEEP ? max(vi, 0) : vi) : 0x80000000u;
           const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
           x[u] = make_uint2(w[0], w[1]);
-          mt[u] = live ? (uint32_t)a | ((uint32_t)b << 4) : 0u;
+          mt[u] = live ? (uint32_t)a | ((uint32_t)b << 4) | (DEEP ? (uint32_t)max(-vi, 0) << 8 : 0u) : 0u;
         }
       };
       auto count = [&](const uint2 (&x)[U], const uint32_t (&mt)[U]) {
@@ -390,7 +419,8 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint64_t m = byte_range_mask((int32_t)(mt[u] & 15u), (int32_t)((mt[u] >> 4) & 15u));
-          const uint64_t w64 = (uint64_t)x[u].x | ((uint64_t)x[u].y << 32);
+          uint64_t w64 = (uint64_t)x[u].x | ((uint64_t)x[u].y << 32);
+          if (DEEP) w64 <<= (mt[u] >> 5) & 56u;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const uint32_t wh = (uint32_t)(w64 >> (32 * h)), mh = (uint32_t)(m >> (32 * h));
@@ -440,7 +470,10 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     const uint64_t t_c = (dbg & 16) ? __builtin_readcyclecounter() : 0;
     if (__ballot(bad || badb != 0) != 0) {  // the walker takes the block (exact for every read)
       zero_words();
-      if (lane == 0) slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)tid;
+      if (lane == 0) {
+        if (defer) deep[atomicAdd(&ctr->n_deep, 1ull)] = (int32_t)tid;
+        else slow[atomicAdd(&ctr->n_slow, 1ull)] = (int32_t)tid;
+      }
       continue;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -596,7 +629,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     }
   }
   if ((dbg & 16) && lane == 0 && clk[5])
-    for (int k = 0; k < 6; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd(&ctr->prof[k], (unsigned long long)clk[k]);
   add_run_counters(ctr, visited, amb, ties, (int)blockIdx.x);
   if (!DEEP && threadIdx.x == 0) {  // this workgroup's partition counts (may exceed the capacity: host retry)
     ctr->part[0][blockIdx.x] = outn[0];

@@ -1298,6 +1298,7 @@ struct gq_dev_reads {
   int64_t n_rows = 0;                                      // projection rows (kProjRowBytes each, ProjRec)
   float h2d_ms = 0, derive_ms = 0;                         // upload wall times (gq_reads_info)
   bool columns = false;            // the column records and base classes are derived (ensure_columns)
+  bool ev_bases = false;           // ev_rb is derived (ensure_ev_bases)
   bool projected = false;          // the projection is derived (ensure_projection)
   void *nnb = nullptr;             // N bases per read (pool_clean), for the projection's sparse entries
   float proj_ms = 0;               // ensure_projection's wall time
@@ -1397,6 +1398,8 @@ struct H2DStager {
 gq_status derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len);
 // The column records (ColDesc, the auxiliary list, clean / N-base counts), derived on first use.
 gq_status ensure_columns(gq_ctx *c, const gq_dev_reads *d);
+// ev_rb (the read base under each MD event) of a resident read set, derived on first use
+gq_status ensure_ev_bases(gq_ctx *c, const gq_dev_reads *d);
 // The projection (ProjRec) of a resident read set, derived on first use.
 // A margin projection wanted with the projection (the somatic tumor, germline-standard): with
 // GQ_FILL_ONE both are filled in one read-major pass (fused_projection_fill) when the projection

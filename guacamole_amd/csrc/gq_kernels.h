@@ -296,12 +296,15 @@ __device__ __forceinline__ void bases_run(const DevReads &R, int32_t a, int32_t 
   }
 }
 
-// MD events of a read (reference offsets relative to its start s) at loci [lo, hi):
-// sink.event_i(i, read base, MD reference base).  Events past the first four are loaded
-// four at a time (all issued before use).
+// MD events of a read (reference offsets relative to its start s) at loci [lo, hi) of one
+// Match/Mismatch run: sink.event_i(i, read base, MD reference base).  The read base is the
+// derived ev_rb where the read set has it (ensure_ev_bases), else the run's own sequenced base:
+// seq[boff + l] for an event at locus l < rend (0 past the sequence, as ev_rb).  Events past the
+// first four are loaded four at a time (all issued before use).
 template <class Sink>
 __device__ __forceinline__ void events_run(const uint32_t *ev, const uint8_t *evb, uint4 e4, uint4 b4, int32_t nmd,
-                                           int32_t s, int32_t lo, int32_t hi, int32_t L0, uint8_t fl, Sink &sink) {
+                                           int32_t s, int32_t lo, int32_t hi, int32_t L0, uint8_t fl, Sink &sink,
+                                           const uint8_t *seq, int64_t boff, int32_t rend) {
   bool done = false;
   for (int k0 = 0; k0 < nmd && !done; k0 += 4) {
     uint32_t v4[4], r4[4];
@@ -311,7 +314,14 @@ __device__ __forceinline__ void events_run(const uint32_t *ev, const uint8_t *ev
       const uint32_t ef = u == 0 ? e4.x : u == 1 ? e4.y : u == 2 ? e4.z : e4.w;
       const uint32_t bf = u == 0 ? b4.x : u == 1 ? b4.y : u == 2 ? b4.z : b4.w;
       v4[u] = k0 == 0 ? ef : (k < nmd ? ev[k] : 0xFFFFFFFFu);
-      r4[u] = k0 == 0 ? bf : (k < nmd ? evb[k] : 0u);
+      r4[u] = evb ? (k0 == 0 ? bf : (k < nmd ? evb[k] : 0u)) : 0u;
+    }
+    if (!evb) {  // the bases of this run's events, from the pool
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int32_t l = s + (int32_t)(v4[u] >> 8);
+        if (k0 + u < nmd && l >= lo && l < hi && l < rend) r4[u] = seq[boff + l];
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -348,21 +358,24 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
   const int32_t lead = R.lead[r];
   const bool clean = R.clean && R.clean[r] != 0;  // (no column records: the checked path)
   const uint32_t *ev = R.md_ev + md_off;
-  const uint8_t *evb = R.ev_rb + md_off;
-  uint4 e4, b4;  // first four MD events and the read bases under them, loaded with the metadata
+  // first four MD events and (ev_rb derived) the read bases under them, loaded with the metadata
+  const uint8_t *evb = R.ev_rb ? R.ev_rb + md_off : nullptr;
+  uint4 e4, b4 = make_uint4(0u, 0u, 0u, 0u);
   e4.x = 0 < nmd ? ev[0] : 0xFFFFFFFFu;
   e4.y = 1 < nmd ? ev[1] : 0xFFFFFFFFu;
   e4.z = 2 < nmd ? ev[2] : 0xFFFFFFFFu;
   e4.w = 3 < nmd ? ev[3] : 0xFFFFFFFFu;
-  b4.x = 0 < nmd ? evb[0] : 0u;
-  b4.y = 1 < nmd ? evb[1] : 0u;
-  b4.z = 2 < nmd ? evb[2] : 0u;
-  b4.w = 3 < nmd ? evb[3] : 0u;
+  if (evb) {
+    b4.x = 0 < nmd ? evb[0] : 0u;
+    b4.y = 1 < nmd ? evb[1] : 0u;
+    b4.z = 2 < nmd ? evb[2] : 0u;
+    b4.w = 3 < nmd ? evb[3] : 0u;
+  }
   const int32_t a = s > L0 ? s : L0;
   const int32_t b = e < L1 ? e : L1;
   if (lead >= 0) {  // [S|H]* (M|=|X) [S|H]*: every element is a Match/Mismatch
     bases_run(R, a, b, seq_off + lead + (a - s), L0, fl, sink, sv, clean);
-    events_run(ev, evb, e4, b4, nmd, s, a, b, L0, fl, sink);
+    events_run(ev, evb, e4, b4, nmd, s, a, b, L0, fl, sink, R.seq, seq_off + lead - s, e);
     return;
   }
   // general CIGAR: operator by operator
@@ -407,7 +420,7 @@ __device__ __forceinline__ void walk_read_lane(const DevReads &R, int64_t r, int
           const int32_t rend = ra + (slen - rpos);  // first locus without a sequenced base
           if (xb > rend) sink.error(1 /*GQ_E_ASSERT*/, (int64_t)rend);
           bases_run(R, lo, hi < rend ? hi : rend, seq_off + rpos + (lo - ra), L0, fl, sink, sv, clean);
-          events_run(ev, evb, e4, b4, nmd, s, lo, hi, L0, fl, sink);
+          events_run(ev, evb, e4, b4, nmd, s, lo, hi, L0, fl, sink, R.seq, seq_off + rpos - ra, rend);
           auto special = [&](int32_t l, int kind) {  // an anchor element at l
             if (l < xa || l >= xb || rpos + (l - ra) >= slen) return;
             const uint8_t base = R.seq[seq_off + rpos + (l - ra)];

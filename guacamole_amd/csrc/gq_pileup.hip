@@ -325,12 +325,20 @@ __device__ bool general_segments(const DevReads &R, int64_t r, Emit emit) {
   if (ncig < 1 || ncig > 32 || slen >= 16384) return false;
   const uint32_t *cg = R.cigar + R.cigar_off[r];
   const uint32_t *ev = R.md_ev + R.md_off[r];
+  // the first five operations in one round of loads (past the last: the last again)
+  uint32_t c5[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) c5[j] = cg[j < ncig ? j : ncig - 1];
+  auto cig = [&](int32_t q) {
+    return q < 5 ? (q == 0 ? c5[0] : q == 1 ? c5[1] : q == 2 ? c5[2] : q == 3 ? c5[3] : c5[4]) : cg[q];
+  };
   int32_t ref = 0, rpos = 0, k = 0, nseg = 0;
   bool lead_ins = false, seen_ref = false;
   for (int32_t q = 0; q < ncig; ++q) {
-    const int op = (int)(cg[q] & 15u);
-    const int32_t len = (int32_t)(cg[q] >> 4);
-    const int nextop = q + 1 < ncig ? (int)(cg[q + 1] & 15u) : -1;
+    const uint32_t cq = cig(q);
+    const int op = (int)(cq & 15u);
+    const int32_t len = (int32_t)(cq >> 4);
+    const int nextop = q + 1 < ncig ? (int)(cig(q + 1) & 15u) : -1;
     if (op == OP_P || op > OP_X) return false;
     if (op == OP_I && !seen_ref && s == 0) lead_ins = true;
     if (consumes_ref(op)) {
@@ -1038,38 +1046,33 @@ __global__ void read_clean(DevReads R, uint8_t *__restrict__ clean, uint32_t *__
 }
 
 // CIGAR shape per read (derived once at upload): leading soft clip if the CIGAR is
-// [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -1 (general walker).
-__device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t *__restrict__ lead,
-                                          uint8_t *__restrict__ ev_rb, bool bad) {
-  // a read whose offsets lie outside their pools (bad) reads nothing: n = nmd = 0
+// [S|H]* (M|=|X) [S|H]* and the sequence covers it, else -(1 + the (M|=|X) operations) (general
+// walker; germline_direct reserves that many count segments).
+__device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t *__restrict__ lead, bool bad) {
+  // a read whose offsets lie outside their pools (bad) reads nothing: n = 0
   const int64_t off = R.cigar_off[r];
   const int32_t n = bad ? 0 : R.n_cigar[r];
-  const int32_t nmd = bad ? 0 : R.n_md[r];
-  const int64_t mdo = R.md_off[r];
-  // the first four CIGAR operations and MD events in one round of loads (past the last: the
-  // last again), ahead of the shape test that decides what they mean
-  // (indexes clamped into the pools: the loads do not wait for validate_one's verdict)
-  uint32_t c4[4] = {0u, 0u, 0u, 0u}, e4[4] = {0u, 0u, 0u, 0u};
-  const int32_t n_raw = R.n_cigar[r], nmd_raw = R.n_md[r];
+  // the first four CIGAR operations in one round of loads (past the last: the last again), ahead
+  // of the shape test that decides what they mean (indexes clamped into the pool: the loads do
+  // not wait for validate_one's verdict)
+  uint32_t c4[4] = {0u, 0u, 0u, 0u};
+  const int32_t n_raw = R.n_cigar[r];
   auto clampi = [](int64_t x, int64_t len) { return x < 0 ? (int64_t)0 : x >= len ? len - 1 : x; };
   if (R.cigar_len > 0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) c4[j] = R.cigar[clampi(off + (j < n_raw ? j : n_raw - 1), R.cigar_len)];
   }
-  if (R.md_len > 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) e4[j] = R.md_ev[clampi(mdo + (j < nmd_raw ? j : nmd_raw - 1), R.md_len)];
-  }
-  int32_t ld = 0, mlen = 0;
+  int32_t ld = 0, mlen = 0, n_m = 0;  // (n_m: the (M|=|X) operations)
   int mi = -1;
   bool simple = n > 0;
-  for (int k = 0; k < n && simple; ++k) {
+  for (int k = 0; k < n; ++k) {
     const uint32_t c = k < 4 ? (k == 0 ? c4[0] : k == 1 ? c4[1] : k == 2 ? c4[2] : c4[3]) : R.cigar[off + k];
     const int op = (int)(c & 15u);
     if (op == OP_M || op == OP_EQ || op == OP_X) {
       if (mi >= 0) simple = false;
       mi = k;
       mlen = (int32_t)(c >> 4);
+      n_m += n_m < 32766 ? 1 : 0;
     } else if (op == OP_S) {
       if (mi < 0) ld += (int32_t)(c >> 4);
     } else if (op != OP_H) {
@@ -1077,22 +1080,33 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
     }
   }
   if (mi < 0 || ld > 32767 || ld + mlen > R.seq_len[r]) simple = false;
-  lead[r] = bad ? (int16_t)-1 : simple ? (int16_t)ld : (int16_t)-1;
-  // sequenced base under each MD event (0 where the event sits on a deletion / outside M)
+  lead[r] = bad ? (int16_t)-1 : simple ? (int16_t)ld : (int16_t)(-1 - n_m);
+}
+
+// ev_rb: the sequenced base under each MD event (0 where the event sits on a deletion or
+// outside the Match/Mismatch operations), one thread per read, derived on first use
+// (ensure_ev_bases) by the kernels that read it: the column records and the projection.  The
+// walkers and germline_direct take the base from the pool where they meet the event.
+__global__ void ev_bases(DevReads R, uint8_t *__restrict__ ev_rb) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R.n_reads) return;
+  const int32_t nmd = R.n_md[r];
   if (nmd <= 0) return;
+  const int64_t mdo = R.md_off[r];
   const uint32_t *ev = R.md_ev + mdo;
   uint8_t *rb = ev_rb + mdo;
-  if (simple) {  // [S|H]* (M|=|X) [S|H]*: the event at reference offset o reads base lead + o
+  const int32_t ld = R.lead[r];
+  if (ld >= 0) {  // [S|H]* (M|=|X) [S|H]*: the event at reference offset o reads base lead + o
     const int64_t so = R.seq_off[r];
-    const int32_t sl = R.seq_len[r];  // (>= ld + mlen >= 1: a simple read has bases)
+    const int32_t mlen = R.end[r] - R.start[r];  // (lead + mlen <= seq_len: read_prep's shape test)
     for (int k0 = 0; k0 < nmd; k0 += 4) {  // four events, then their bases, per round of loads
       uint32_t o4[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o4[j] = (k0 == 0 ? e4[j] : ev[k0 + j < nmd ? k0 + j : nmd - 1]) >> 8;
+      for (int j = 0; j < 4; ++j) o4[j] = ev[k0 + j < nmd ? k0 + j : nmd - 1] >> 8;
       uint8_t b4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bool in = (int32_t)o4[j] < mlen && ld + (int32_t)o4[j] < sl;
+        const bool in = (int32_t)o4[j] < mlen;
         b4[j] = R.seq[in ? so + ld + (int32_t)o4[j] : so];
         b4[j] = in ? b4[j] : (uint8_t)0;
       }
@@ -1102,6 +1116,8 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
     }
     return;
   }
+  const int64_t off = R.cigar_off[r];
+  const int32_t n = R.n_cigar[r];
   int32_t ref = 0, rp = 0;
   int k = 0;
   for (int c = 0; c < n && k < nmd; ++c) {
@@ -1127,12 +1143,12 @@ __device__ __forceinline__ void shape_one(const DevReads &R, int64_t r, int16_t 
 // The upload-time checks (validate_one) and the read shapes (shape_one) in one pass over the
 // reads: a read whose own offsets lie outside their pools (bit 2) gets no shape (the upload fails
 // on the flag anyway).
-__global__ void read_prep(DevReads R, int *__restrict__ bad, int16_t *__restrict__ lead, uint8_t *__restrict__ ev_rb) {
+__global__ void read_prep(DevReads R, int *__restrict__ bad, int16_t *__restrict__ lead) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R.n_reads) return;
   const int b = validate_one(R, r);
   if (b) atomicOr(bad, b);
-  shape_one(R, r, lead, ev_rb, (b & 2) != 0);  // (its loads go out beside validate_one's)
+  shape_one(R, r, lead, (b & 2) != 0);  // (its loads go out beside validate_one's)
 }
 
 __device__ __forceinline__ uint64_t pack_inline(uint8_t r0, const uint8_t *alt, int alt_len) {
@@ -2268,11 +2284,11 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     for (size_t i = 1; i < b.size() && ok; ++i) ok = b[i] >= b[i - 1];
     if (!ok) return set_err(GQ_E_UNSORTED, "contig_read_begin must run from 0 to n_reads, non-decreasing");
   }
-  void *p = nullptr, *q = nullptr;
+  void *p = nullptr;
   HIP_TRY(d->dp.get(&p, sizeof(int16_t) * (size_t)std::max<int64_t>(d->d.n_reads, 1)));
-  HIP_TRY(d->dp.get(&q, (size_t)std::max<int64_t>(md_len, 16)));
   d->d.lead = (const int16_t *)p;
-  d->d.ev_rb = (const uint8_t *)q;
+  d->d.ev_rb = nullptr;  // (derived on first use: ensure_ev_bases)
+  d->ev_bases = false;
   int unordered = 0;
   const int nc = d->d.n_contigs;
   std::vector<int32_t> last((size_t)nc, 0);  // each contig's largest read end (pmax_end of its last read)
@@ -2282,7 +2298,7 @@ static gq_status derive_shape_impl(gq_ctx *c, gq_dev_reads *d, int64_t md_len, b
     HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
     const unsigned nb = (unsigned)((d->d.n_reads + kBlock - 1) / kBlock);
     // validation and the read shapes in one pass (a read out of its pools gets no shape)
-    hipLaunchKernelGGL(read_prep, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag, (int16_t *)p, (uint8_t *)q);
+    hipLaunchKernelGGL(read_prep, dim3(nb), dim3(kBlock), 0, c->stream, d->d, (int *)flag, (int16_t *)p);
     HIP_TRY(hipGetLastError());
     int bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -2570,6 +2586,7 @@ gq_status gq_reads_rederive(gq_ctx *c, gq_dev_reads *d) {
   R.prow = nullptr;
   d->projected = false;
   d->columns = false;
+  d->ev_bases = false;
   d->nnb = d->mproj = d->mnb = nullptr;
   d->mproj_mapq = -1;
   d->proj_bytes = d->pev_count = d->proj_reads = d->n_rows = d->n_slices = 0;
@@ -3059,9 +3076,11 @@ static gq_status germline_run(gq_ctx *c, const gq_dev_reads *rd, const gq_loci *
             (double)hc.prof[3] / hc.prof[4], hc.prof[4]);
   if ((gq_dbg() & 16) && hc.prof[5])
     fprintf(stderr,
-            "gq prof (cycles/tile/wave): setup %.0f chunks %.0f (runs %.0f counting %.0f) decision %.0f (%llu)\n",
+            "gq prof (cycles/tile/wave): setup %.0f chunks %.0f (runs %.0f [fields %.0f slots %.0f] counting %.0f) "
+            "decision %.0f (%llu)\n",
             (double)hc.prof[0] / hc.prof[5], (double)hc.prof[1] / hc.prof[5], (double)hc.prof[2] / hc.prof[5],
-            (double)hc.prof[3] / hc.prof[5], (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
+            (double)hc.prof[6] / hc.prof[5], (double)hc.prof[7] / hc.prof[5], (double)hc.prof[3] / hc.prof[5],
+            (double)hc.prof[4] / hc.prof[5], hc.prof[5]);
   for (int k = 0; k < kSpread; ++k) {
     hc.visited += hc.spread[0][k];
     hc.ambiguous += hc.spread[1][k];
@@ -3389,6 +3408,22 @@ void gq_free_counts(gq_counts *r) {
 
 gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return derive_shape_impl(c, d, md_len); }
 
+// The read base under each MD event (ev_bases), derived on first use by the column records.
+gq_status gq::ensure_ev_bases(gq_ctx *c, const gq_dev_reads *cd) {
+  gq_dev_reads *d = const_cast<gq_dev_reads *>(cd);
+  if (d->ev_bases) return GQ_OK;
+  void *q = nullptr;
+  HIP_TRY(d->dp.get(&q, (size_t)std::max<int64_t>(d->d.md_len, 16)));
+  if (d->d.n_reads > 0) {
+    hipLaunchKernelGGL(ev_bases, dim3((unsigned)((d->d.n_reads + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                       d->d, (uint8_t *)q);
+    HIP_TRY(hipGetLastError());
+  }
+  d->d.ev_rb = (const uint8_t *)q;
+  d->ev_bases = true;
+  return GQ_OK;
+}
+
 // The column records of a resident read set, derived on first use by a kernel that reads them
 // (the projection's fills and sparse entries, somatic_proj, the walkers' clean fast path):
 // clean[r] (every sequenced byte of read r is A C G T N) and its N bytes (pool_clean, or
@@ -3397,6 +3432,10 @@ gq_status gq::derive_shape(gq_ctx *c, gq_dev_reads *d, int64_t md_len) { return 
 gq_status gq::ensure_columns(gq_ctx *c, const gq_dev_reads *cd) {
   gq_dev_reads *d = const_cast<gq_dev_reads *>(cd);
   if (d->columns) return GQ_OK;
+  {
+    const gq_status se = ensure_ev_bases(c, d);  // (col_derive's event words carry them)
+    if (se) return se;
+  }
   const int64_t n = d->d.n_reads;
   void *cl = nullptr, *nnb = nullptr;
   HIP_TRY(d->dp.get(&cl, (size_t)std::max<int64_t>(n, 1)));
