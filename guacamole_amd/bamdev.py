@@ -140,6 +140,7 @@ class MappedBam:
         self.h = C.c_void_p()
         self.t = time.perf_counter()
         rc = native.lib().gq_bam_dev_map_ex(path.encode(), int(populate), C.byref(self.h))
+        self.t_mapped = time.perf_counter()
         self.ok = rc != GQ_E_NOT_BGZF
         if self.ok:
             _raise(rc)
@@ -267,10 +268,13 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
     if not m.ok:
         return None
     t0 = m.t
+    tp = time.perf_counter()
     plan = m.plan(region, halo, bai_path(path)) if planned else None
+    tl = time.perf_counter()
     h, m.h = m.h, C.c_void_p()  # the handle now belongs to this load
     try:
         rc = L.gq_bam_dev_load(ctx.h, h)
+        tl1 = time.perf_counter()
         if rc == GQ_E_HIP:  # out of device memory for the loader's buffers: the host loader's footprint is smaller
             L.gq_bam_dev_close(h)
             return None
@@ -321,6 +325,7 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
         sh = soa.sample_hashes(samples, n_samples)
         out = C.c_void_p()
         fill_ms = C.c_float()
+        t3 = time.perf_counter()
         rc = L.gq_bam_dev_reads(h, class_sample.ctypes.data, n_samples, sh.ctypes.data, C.byref(out), C.byref(fill_ms))
         if rc in (GQ_E_UNSORTED, GQ_E_HIP):
             L.gq_bam_dev_close(h)
@@ -329,11 +334,18 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
     except BaseException:
         L.gq_bam_dev_close(h)
         raise
+    t4 = time.perf_counter()
     dr = native.DeviceReads(ctx, out, None)
     timings = {k: float(getattr(z, k)) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms")}
     info = ctx.proj_stats(dr)
     timings.update(fill_ms=float(fill_ms.value), derive_ms=float(info.get("derive_ms", 0.0)),
                    open_s=t1 - t0, scan_s=t2 - t1, total_s=time.perf_counter() - t0,
+                   # open_s's parts: the host map (and the wait for it when mapped on a thread), the
+                   # plan (host probes or the BAI), gq_bam_dev_load (map_ms + h2d_ms + inflate_ms
+                   # and their allocations), the header; then the scan, the sample table, the reads
+                   wall_s={"map": (getattr(m, "t_mapped", tp) - t0), "to_plan": tp - getattr(m, "t_mapped", tp),
+                           "plan": tl - tp, "dev_load": tl1 - tl, "header": t1 - tl1, "scan": t2 - t1,
+                           "samples": t3 - t2, "dev_reads": t4 - t3, "stats": time.perf_counter() - t4},
                    records=int(z.n_records), comp_bytes=int(z.comp_bytes), bam_bytes=int(z.bam_bytes),
                    blocks=int(z.n_blocks), max_span=int(z.max_span), plan=plan)
     rs = DeviceReadSet(ctx, dr, names, lengths, samples, int(z.n_reads), timings)

@@ -250,7 +250,13 @@ def _all_flat(mine):
 def parquet_options(args, flat=None, contig_index=None, rows_contig=None, rows_pos=None) -> dict:
     """ParquetArgs (bdg-utils cli, mixed into Common.Arguments.Base, Common.scala:50) and the part
     file of each record: the loci task whose range holds it (flat = flatten_partitions arrays),
-    since the callers' genotypes RDD has one partition per task."""
+    since the callers' genotypes RDD has one partition per task.
+
+    Divergence (parity unpinned, no fixture covers it): after --dbsnp-vcf the reference's
+    keyBy + leftOuterJoin (SomaticStandardCaller.scala:143-144) reshuffles the records under a
+    hash partitioner before adamParquetSave, so its record-to-part mapping is the join's, not
+    the loci tasks'.  Here the parts stay per loci task in that case too; the records and their
+    order within the whole output are the same, only which part file holds a record differs."""
     opts = dict(codec=args.parquet_compression_codec, page_size=args.parquet_page_size,
                 block_size=args.parquet_block_size, dictionary=not args.parquet_disable_dictionary)
     if flat is not None and rows_pos is not None:

@@ -23,6 +23,7 @@ from .loci import LociSet, partition_loci_uniformly
 
 
 OWN_GROUP = False  # init_from_env created the process group (and _finish_rank ends it)
+SECOND_LOADS = 0  # rank_loci_and_reads calls whose ranks decoded their region again (a cut outside the probe)
 
 
 def rank_info() -> Tuple[int, int, int]:
@@ -334,12 +335,14 @@ def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accurac
         parts = partition_loci_by_counts(tasks, loci, micro, counts)
         flat = flatten_partitions(parts, cidx)
         sizes = np.array([inv[m].count for m in range(n_micro)], np.int64)
-        bounds = depth_bounds(sizes, counts, world)
+        bounds = depth_bounds(sizes, counts, world, slack=max(1, n_micro // world // 20))
     rr = ranks_by_position(flat, bounds)
     sel = rr == rank
     mine = tuple(np.ascontiguousarray(np.asarray(a)[sel]) for a in flat)
     region = loci_of(mine, names)
     if _any_true(sets is None or not covers(decoded, region), device):
+        global SECOND_LOADS
+        SECOND_LOADS += 1  # (every rank counts it: the branch is taken together)
         if sets is None or not covers(decoded, region):
             sets = None  # (the first load's memory goes before the second)
         sets = _together(lambda: load(region) if sets is None else sets, device)
@@ -349,12 +352,18 @@ def rank_loci_and_reads(load, names, lengths, builder, parallelism: int, accurac
     return None if sets is None else (sets, mine)
 
 
-def depth_bounds(sizes: np.ndarray, counts: np.ndarray, world: int) -> List[int]:
+def depth_bounds(sizes: np.ndarray, counts: np.ndarray, world: int, slack: Optional[int] = None) -> List[int]:
     """Rank bounds in loci positions from the all-reduced micro-partition read counts: rank r's
     block starts at the micro-partition edge nearest to where the cumulative count (+ 1e-3 per
     locus, so empty stretches still spread) crosses r / world of the total — balanced by read weight as
-    assign_tasks_to_ranks balances the host path, not by loci."""
+    assign_tasks_to_ranks balances the host path, not by loci.
+
+    slack (micro partitions): each cut stays within `slack` partitions of the loci-uniform cut
+    r * n / world, so it lies inside what both neighbouring ranks decoded for the counts
+    ([m0 - slack, m1 + slack)); on uneven depth the balance is then approximate, but no rank has to
+    decode its region a second time because a cut moved out of its probe window."""
     sizes = np.asarray(sizes, np.int64)
+    n = len(sizes)
     w = np.asarray(counts, np.float64) + 1e-3 * sizes
     cum = np.concatenate([[0.0], np.cumsum(w)])
     edge = np.concatenate([[0], np.cumsum(sizes)])
@@ -365,6 +374,9 @@ def depth_bounds(sizes: np.ndarray, counts: np.ndarray, world: int) -> List[int]
         m = int(np.searchsorted(cum, want, "left"))  # the nearer of the two micro-partition edges
         if m > 0 and (m >= len(cum) or want - cum[m - 1] < cum[m] - want):
             m -= 1
+        if slack is not None:
+            u = r * n // world
+            m = min(max(m, u - slack), u + slack)
         out.append(max(out[-1], int(edge[min(m, len(sizes))])))
     out.append(int(edge[-1]))
     return out

@@ -305,6 +305,26 @@ def test_depth_bounds_balance_reads_not_loci():
     assert depth_bounds(sizes, counts, 1) == [0, 8000]
 
 
+def test_depth_bounds_stay_inside_the_probe_windows():
+    """With slack, each cut stays within `slack` micro partitions of the loci-uniform cut, so both
+    neighbouring ranks decoded it for the counts (a cut far outside the window made
+    most ranks decode their region a second time)."""
+    from guacamole_amd.distributed import depth_bounds
+    sizes = np.full(100, 1000, np.int64)
+    counts = np.array([1000] * 10 + [1] * 90, np.int64)  # all the depth in the first tenth
+    free = depth_bounds(sizes, counts, 4)
+    assert free[1] < 10_000 and free[2] < 10_000  # read-balanced: cuts deep inside the first tenth
+    clamped = depth_bounds(sizes, counts, 4, slack=5)
+    for r in range(1, 4):
+        u = 25 * r * 1000
+        assert u - 5000 <= clamped[r] <= u + 5000
+    assert clamped[0] == 0 and clamped[-1] == 100_000
+    assert clamped == sorted(clamped)
+    # even depth: the clamp changes nothing
+    even = np.full(100, 7, np.int64)
+    assert depth_bounds(sizes, even, 4, slack=5) == depth_bounds(sizes, even, 4)
+
+
 def test_bench_refuses_a_world_size_other_than_gpus():
     """bench.py --gpus N under a launcher with WORLD_SIZE != N exits non-zero before any GPU work."""
     import subprocess
