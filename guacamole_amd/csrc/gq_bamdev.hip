@@ -75,30 +75,54 @@ typedef uint32_t u32u __attribute__((aligned(1)));  // unaligned dword access (g
 
 __host__ __device__ __forceinline__ uint32_t ld16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
-struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end.  The next
-                // word is loaded one refill ahead, so its latency overlaps the symbols between
-  const uint32_t *w, *wend;  // w: the word after `nw`
+struct BitIn {  // LSB-first bit reader over 32-bit words; zeros past the buffer's end.  The
+                // stream comes in 16-byte chunks (one dwordx4 load each) and the next chunk is in
+                // flight while the current one's four words are consumed: a refill waits on a load
+                // only every fourth word, and that load was issued ~128 bits (~16 symbols) earlier.
+                // (A one-word-ahead fetch waited on nearly every refill: the ~32 bits between
+                // refills decode faster than a load returns.)
+  const uint4 *p, *pend;  // the chunk after `nx`
+  uint4 nx;               // in flight
+  uint64_t q0, q1;        // the current chunk's words not yet taken (qn of them, lowest first)
+  int qn;
+  int64_t taken;          // words moved into bb
   uint64_t bb;
-  uint32_t nw;
   int bc;
-  __device__ __forceinline__ uint32_t fetch() {
-    const uint32_t v = w < wend ? *w : 0u;
-    ++w;
+  __device__ __forceinline__ uint4 fetch16() {
+    const uint4 v = p < pend ? *p : make_uint4(0u, 0u, 0u, 0u);
+    ++p;
     return v;
   }
+  __device__ __forceinline__ uint32_t word() {
+    if (qn == 0) {
+      q0 = (uint64_t)nx.x | ((uint64_t)nx.y << 32);
+      q1 = (uint64_t)nx.z | ((uint64_t)nx.w << 32);
+      qn = 4;
+      nx = fetch16();
+    }
+    const uint32_t v = (uint32_t)q0;
+    q0 = (q0 >> 32) | (q1 << 32);
+    q1 >>= 32;
+    --qn;
+    return v;
+  }
+  // base 16-byte aligned; base_len: readable bytes (the caller's buffer is padded past its data)
   __device__ void init(const uint8_t *base, int64_t off, int64_t base_len) {
-    wend = (const uint32_t *)(base + (base_len & ~int64_t(3)));
-    w = (const uint32_t *)(base + (off & ~int64_t(3)));
+    pend = (const uint4 *)(base + (base_len & ~int64_t(15)));
+    p = (const uint4 *)(base + (off & ~int64_t(15)));
+    nx = fetch16();
+    qn = 0;
+    for (int k = (int)((off >> 2) & 3); k > 0; --k) word();  // (the chunk's words before off's)
     const int sk = (int)(off & 3);
-    bb = (uint64_t)(fetch() >> (8 * sk));
+    bb = (uint64_t)(word() >> (8 * sk));
     bc = 32 - 8 * sk;
-    nw = fetch();
+    taken = 1;
   }
   __device__ __forceinline__ void need(int n) {  // n <= 32
     if (bc < n) {
-      bb |= (uint64_t)nw << bc;
+      bb |= (uint64_t)word() << bc;
       bc += 32;
-      nw = fetch();
+      ++taken;
     }
   }
   __device__ __forceinline__ void drop(int n) {
@@ -222,9 +246,8 @@ __device__ int inflate_one(const uint8_t *comp, int64_t comp_len, const BgzfBloc
   const int64_t osz = b.isize;
   int64_t op = 0;
   const int64_t in_bits = (int64_t)b.in_len * 8;
-  const uint32_t *w0 = (const uint32_t *)(comp + (b.in_off & ~int64_t(3)));
   const int sk = (int)(b.in_off & 3);
-  auto used_bits = [&]() -> int64_t { return (int64_t)(in.w - w0 - 1) * 32 - in.bc - 8 * sk; };
+  auto used_bits = [&]() -> int64_t { return in.taken * 32 - in.bc - 8 * sk; };
   int final_blk = 0;
   do {
     if (used_bits() > in_bits) return E_INFLATE;
