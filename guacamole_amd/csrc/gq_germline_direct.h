@@ -44,6 +44,12 @@
 #ifndef GQ_DIR_WPE
 #define GQ_DIR_WPE 4  // waves per SIMD the register budget must allow
 #endif
+#ifndef GQ_DIR_MASKED
+#define GQ_DIR_MASKED 0
+#endif
+#ifndef GQ_DIR_GROUP
+#define GQ_DIR_GROUP 4  // lanes (columns) walking their slots together: 1, 2, 4, 8, 16, 32 or 64
+#endif
 struct DirCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = 4;     // waves per workgroup, each on its own tiles
@@ -92,7 +98,8 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     CallRec *__restrict__ recs, ComplexItem *__restrict__ cplx, OutGeom og, Counters *ctr, int32_t *__restrict__ slow,
     int32_t *__restrict__ deep, int dbg) {
   // dbg (diagnostics, env GQ_DBG; results are wrong when set): 1 skip the base loads, 4 skip the
-  // decision, 16 phase clocks, 32 skip the counting
+  // decision, 16 phase clocks, 32 skip the counting, 64 skip the MD events, 128 skip the events'
+  // read-base loads
   using C = DirCfg;
   constexpr int T = C::kT, U = C::kU;
   constexpr int EW = DEEP ? 2 * T : T;  // event words: 16-bit pairs (DEEP) or four bytes per locus
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
         // runs of this read in the block: one for a simple read, the count segments of a general one
         uint32_t nrun = valid && !nomd && !gen && e > B0 && s < B0 + T ? 1u : 0u;
         // the read's first four MD events, in flight while its runs are placed
-        const bool evr = valid && !nomd && nmd > 0 && s < B0 + T;
+        const bool evr = valid && !nomd && nmd > 0 && s < B0 + T && !(dbg & 64);
         uint32_t v4[4] = {0u, 0u, 0u, 0u};
         auto load_ev = [&](int32_t k0) {
 #pragma unroll
@@ -364,7 +371,7 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int32_t o = (int32_t)(v4[j] >> 8);
-              b4[j] = !gen && o < e - s ? R.seq[so + ld + o] : (uint8_t)0;
+              b4[j] = !gen && o < e - s ? ((dbg & 128) ? (uint8_t)'A' : R.seq[so + ld + o]) : (uint8_t)0;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -387,8 +394,14 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
       const uint64_t t_r = (dbg & 16) ? __builtin_readcyclecounter() : 0;
       // ---- this lane's slots: [first slot ending past its column's first locus, last slot
       //      starting before its column's end]
-      const int32_t last = wave_incl_max_i(hx[lane]);
-      const int32_t first = wave_suffix_min_i(hn[lane]);
+      int32_t last = wave_incl_max_i(hx[lane]);
+      int32_t first = wave_suffix_min_i(hn[lane]);
+      if (GQ_DIR_GROUP > 1) {  // a group's lanes walk the group's slots together (first / last are
+                               // monotone in the column): one slot per step and group, so a load
+                               // instruction touches one read's bytes per group, not one per lane
+        first = __shfl(first, lane & ~(GQ_DIR_GROUP - 1), 64);
+        last = __shfl(last, lane | (GQ_DIR_GROUP - 1), 64);
+      }
       const int32_t nl = last >= first ? last - first + 1 : 0;
       int32_t kmax = nl;
 #pragma unroll
@@ -409,8 +422,16 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
           // tiles the DEEP instantiation takes: its load clamped to the base and shifted back)
           const int32_t vi = (int32_t)d.y + colr;
           const uint32_t vo = live ? (uint32_t)(DEEP ? max(vi, 0) : vi) : 0x80000000u;
-          const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
-          x[u] = make_uint2(w[0], w[1]);
+          if (GQ_DIR_MASKED) {  // dead lanes off the load (exec-masked) instead of out of range
+            x[u] = make_uint2(0u, 0u);
+            if (live) {
+              const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
+              x[u] = make_uint2(w[0], w[1]);
+            }
+          } else {
+            const auto w = __builtin_amdgcn_raw_buffer_load_b64(srs, (int)vo, 0, 0);
+            x[u] = make_uint2(w[0], w[1]);
+          }
           mt[u] = live ? (uint32_t)a | ((uint32_t)b << 4) | (DEEP ? (uint32_t)max(-vi, 0) << 8 : 0u) : 0u;
         }
       };
