@@ -3,8 +3,10 @@ restricted to the two callers on the accelerated path."""
 import os
 import sys
 
+from . import bamdev
 from .commands import main
 
+bamdev.DEFER_RELEASE = True  # this process ends after the command: the loaders' buffers go with it
 rc = main()
 # The output is written and closed: end the process here rather than tear the interpreter down
 # (collecting the resident read sets' device buffers one hipFree at a time and the HIP runtime's

@@ -352,6 +352,9 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
     # the loader's buffers (compressed file, inflated stream, record tables: ~2.5x the file's
     # inflated size) are released now, so the callers have the HBM; on a host thread, off the
     # load's critical path (their hipFree calls take ~45 ms at chr20 30x)
+    if DEFER_RELEASE and 3 * int(z.bam_bytes) < _free_device_bytes() // 4:  # (see DEFER_RELEASE)
+        _deferred.append(h)
+        return rs
     import threading
     th = threading.Thread(target=L.gq_bam_dev_close, args=(h,), name="gq_bam_dev_close")
     th.start()
@@ -360,6 +363,27 @@ def _load_reads_device(ctx, path, filters, mapped, region, halo, use_plan=True):
 
 
 _release_threads: List[object] = []
+# DEFER_RELEASE (set by `python -m guacamole_amd`, a process that exits after one command): the
+# loaders' buffers are not released after the load.  hipFree synchronises the device and holds
+# the HIP runtime while it runs (~45 ms for a chr20 30x BAM's buffers), so a release on a host
+# thread beside the call made the CLI's first call wait for it (call stage 40-60 ms against a
+# 3 ms cold call in-process).  The process ends with os._exit, which returns the memory; a
+# load whose buffers would not leave room for the call (over a quarter of the device's free
+# memory after the load) is released as before.
+DEFER_RELEASE = False
+_deferred: List[object] = []
+
+
+def _free_device_bytes() -> int:
+    """hipMemGetInfo's free bytes on the current device (0 if it cannot be read)."""
+    try:
+        hip = C.CDLL("libamdhip64.so.7")  # the HIP runtime libgqpileup.so already loaded
+        free, total = C.c_size_t(), C.c_size_t()
+        if hip.hipMemGetInfo(C.byref(free), C.byref(total)) != 0:
+            return 0
+        return int(free.value)
+    except OSError:
+        return 0
 
 
 def join_release_threads() -> None:

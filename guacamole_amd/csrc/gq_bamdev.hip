@@ -31,8 +31,10 @@
 #include <chrono>
 #include <climits>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -421,6 +423,20 @@ __global__ void __launch_bounds__(256) bgzf_crc(const uint8_t *out, const BgzfBl
 // ---- records ------------------------------------------------------------------------------
 // plausible alignment record at o: every length field consistent with block_size (as the host
 // loader's record_at)
+// the fixed fields of a record at h (36 bytes readable: block_size and the 32-byte core) are
+// plausible: references in the dictionary, a name, and a block size that holds the core's parts
+__host__ __device__ __forceinline__ bool record_head_ok(const uint8_t *h, int32_t n_ref) {
+  const int32_t bs = (int32_t)ld32(h);
+  if (bs < 32) return false;
+  const uint8_t *p = h + 4;
+  const int32_t ref_id = (int32_t)ld32(p), pos = (int32_t)ld32(p + 4), l_seq = (int32_t)ld32(p + 16),
+                next_ref = (int32_t)ld32(p + 20);
+  const uint32_t l_name = p[8], n_cig = ld16(p + 12);
+  if (ref_id < -1 || ref_id >= n_ref || next_ref < -1 || next_ref >= n_ref || pos < -1 || l_seq < 0 || l_name < 1)
+    return false;
+  return 32 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + l_seq <= bs;
+}
+
 __host__ __device__ bool record_at(const uint8_t *d, int64_t n, int64_t o, int32_t n_ref) {
   if (o + 40 > n) return false;
   const int32_t bs = (int32_t)ld32(d + o);
@@ -912,8 +928,9 @@ struct gq_bam_dev {
   std::vector<Seg> segs;
   std::vector<BgzfBlock> sel;  // the load's blocks (planned: segment by segment, stream offsets compacted)
   std::vector<int64_t> sel_seg0;  // first entry of each segment in `sel`
-  std::map<int64_t, Probe> probes;
-  int64_t n_probes = 0;
+  std::map<int64_t, Probe> probes;  // (the plan probes on several host threads: probe_mu)
+  std::mutex probe_mu;
+  std::atomic<int64_t> n_probes{0};
   std::vector<std::vector<uint64_t>> bai_ioff;
   std::string text;
   std::vector<std::string> names;
@@ -1038,17 +1055,20 @@ inline int64_t rec_key(int32_t ref, int32_t pos) {  // file order of a sorted BA
 // last record and the landing are true records.  has = false: no record starts in the block
 // (header bytes only, an empty block, or one inside a longer record).
 gq_status probe(gq_bam_dev *b, int64_t k, Probe &out) {
-  auto hit = b->probes.find(k);
-  if (hit != b->probes.end()) {
-    out = hit->second;
-    return GQ_OK;
+  {
+    std::lock_guard<std::mutex> g(b->probe_mu);
+    auto hit = b->probes.find(k);
+    if (hit != b->probes.end()) {
+      out = hit->second;
+      return GQ_OK;
+    }
   }
   Probe P;
   const BgzfBlock &blk = b->blocks[(size_t)k];
   const int64_t o0 = blk.out_off, hi = blk.isize, nb = (int64_t)b->blocks.size();
   const int32_t n_ref = (int32_t)b->names.size();
   if (hi > 0 && o0 + hi > b->rec0) {
-    ++b->n_probes;
+    b->n_probes.fetch_add(1);
     std::vector<uint8_t> buf;
     if (!host_inflate(b, k, buf)) return corrupt_block(b, k);
     int64_t next = k + 1;
@@ -1058,10 +1078,11 @@ gq_status probe(gq_bam_dev *b, int64_t k, Probe &out) {
       return GQ_OK;
     };
     auto rec_ok = [&](int64_t q, int64_t &key, int64_t &len, gq_status &st) -> bool {
-      if ((st = extend(q + 4))) return false;
-      if (q + 4 > (int64_t)buf.size()) return false;
+      // the fixed fields first: a false sync offset is nearly always rejected there, before its
+      // (garbage) block size makes extend() inflate the following blocks
+      if ((st = extend(q + 36))) return false;
+      if (q + 36 > (int64_t)buf.size() || !record_head_ok(buf.data() + q, n_ref)) return false;
       const int32_t bs = (int32_t)ld32(buf.data() + q);
-      if (bs < 32) return false;
       if ((st = extend(q + 4 + bs))) return false;
       if (!record_at(buf.data(), (int64_t)buf.size(), q, n_ref)) return false;
       key = rec_key((int32_t)ld32(buf.data() + q + 4), (int32_t)ld32(buf.data() + q + 8));
@@ -1094,7 +1115,10 @@ gq_status probe(gq_bam_dev *b, int64_t k, Probe &out) {
       P.land = o0 + q;
     }
   }
-  b->probes[k] = P;
+  {
+    std::lock_guard<std::mutex> g(b->probe_mu);
+    b->probes[k] = P;
+  }
   out = P;
   return GQ_OK;
 }
@@ -1222,25 +1246,103 @@ gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out
   b->map = (const uint8_t *)m;
   const uint8_t *p = b->map;
   const int64_t n = (int64_t)b->map_len;
-  int64_t off = 0, outn = 0;
-  while (off < n) {
+  // The block chain: each member's header gives the next member's offset.  Large files are
+  // walked in parallel (the walk is page-fault bound on a file not yet in memory): chunk t > 0
+  // starts at its first offset whose header chains through kVerify more members, each chunk's
+  // walk runs to its first member at or past the chunk's end, and the chunks are stitched along
+  // the true chain from offset 0 — a chunk whose guessed start is not where the previous chunk's
+  // true walk lands is walked again from there, so the result (and any error) is the sequential
+  // walk's.
+  struct Mem {
+    int64_t off;
+    int32_t payload, bsize;
+  };
+  // one member at off: 1 a BGZF member (m filled), 0 not a member, -1 gzip without BGZF sizes,
+  // -2 truncated
+  auto member = [&](int64_t off, Mem &m) -> int {
     int64_t payload, bsize;
-    if (!gzip_member(p + off, n - off, &payload, &bsize))
-      return set_err(GQ_E_BAM_FORMAT, "not a BGZF/gzip member at file offset %lld", (long long)off);
-    if (bsize < 0) return set_err(GQ_E_NOT_BGZF, "%s: a gzip stream without BGZF block sizes", path);
-    if (off + bsize > n || bsize < payload + 8)
-      return set_err(GQ_E_BAM_FORMAT, "truncated BGZF block at file offset %lld", (long long)off);
+    if (!gzip_member(p + off, n - off, &payload, &bsize)) return 0;
+    if (bsize < 0) return -1;
+    if (off + bsize > n || bsize < payload + 8) return -2;
+    m = Mem{off, (int32_t)payload, (int32_t)bsize};
+    return 1;
+  };
+  auto walk = [&](int64_t off, int64_t stop, std::vector<Mem> &v) -> int64_t {  // true-chain walk
+    Mem m;                                                                      // (-1: stopped on an error)
+    while (off < n && off < stop) {
+      if (member(off, m) != 1) return -1 - off;
+      v.push_back(m);
+      off += m.bsize;
+    }
+    return off;
+  };
+  constexpr int64_t kChunkMin = int64_t(64) << 20;
+  constexpr int kVerify = 4;
+  const char *env_nt = getenv("GQ_MAP_THREADS");  // (tests: 1 forces the sequential walk)
+  const int64_t max_nt = env_nt && atoi(env_nt) > 0 ? atoi(env_nt) : 16;
+  const int nt = (int)std::min<int64_t>(max_nt, std::max<int64_t>(1, n / kChunkMin));
+  std::vector<std::vector<Mem>> part((size_t)nt);
+  std::vector<int64_t> start((size_t)nt, -1), land((size_t)nt, -1);
+  auto spec = [&](int t) {  // chunk t's speculative walk
+    const int64_t c0 = n * t / nt, c1 = n * (t + 1) / nt;
+    int64_t o = c0;
+    if (t > 0) {
+      for (; o < c1; ++o) {
+        if (p[o] != 31 || p[o + 1 < n ? o + 1 : o] != 139) continue;
+        Mem m;
+        int64_t q = o;
+        int k = 0;
+        while (k < kVerify && q < n && member(q, m) == 1) {
+          q += m.bsize;
+          ++k;
+        }
+        if (k == kVerify || (k > 0 && q == n)) break;
+      }
+      if (o >= c1) return;
+    }
+    start[(size_t)t] = o;
+    land[(size_t)t] = walk(o, c1, part[(size_t)t]);
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(spec, t);
+    spec(0);
+    for (std::thread &x : th) x.join();
+  }
+  std::vector<Mem> mems;
+  int64_t off = 0;
+  for (int t = 0; t < nt && off >= 0 && off < n; ++t) {
+    const int64_t c1 = n * (t + 1) / nt;
+    if (start[(size_t)t] == off && land[(size_t)t] >= 0) {
+      mems.insert(mems.end(), part[(size_t)t].begin(), part[(size_t)t].end());
+      off = land[(size_t)t];
+    } else if (off < c1) {
+      off = walk(off, c1, mems);
+    }
+    part[(size_t)t] = std::vector<Mem>();
+  }
+  if (off < 0) {  // the true chain broke at -1 - off: the sequential walk's error
+    const int64_t at = -1 - off;
+    Mem m;
+    const int w = member(at, m);
+    if (w == -1) return set_err(GQ_E_NOT_BGZF, "%s: a gzip stream without BGZF block sizes", path);
+    if (w == -2) return set_err(GQ_E_BAM_FORMAT, "truncated BGZF block at file offset %lld", (long long)at);
+    return set_err(GQ_E_BAM_FORMAT, "not a BGZF/gzip member at file offset %lld", (long long)at);
+  }
+  int64_t outn = 0;
+  b->blocks.reserve(mems.size());
+  b->foff.reserve(mems.size());
+  for (const Mem &m : mems) {
     BgzfBlock k{};
-    k.in_off = off + payload;
-    k.in_len = (int32_t)(bsize - payload - 8);
-    memcpy(&k.crc, p + off + bsize - 8, 4);
-    memcpy(&k.isize, p + off + bsize - 4, 4);
+    k.in_off = m.off + m.payload;
+    k.in_len = (int32_t)(m.bsize - m.payload - 8);
+    memcpy(&k.crc, p + m.off + m.bsize - 8, 4);
+    memcpy(&k.isize, p + m.off + m.bsize - 4, 4);
     if (k.isize > 65536) return set_err(GQ_E_BAM_FORMAT, "BGZF block ISIZE %u > 65536", k.isize);
     k.out_off = outn;
     outn += k.isize;
     b->blocks.push_back(k);
-    b->foff.push_back(off);
-    off += bsize;
+    b->foff.push_back(m.off);
   }
   b->n_out = outn;
   gq_status hs = parse_header(b.get());
@@ -1286,60 +1388,98 @@ gq_status gq_bam_dev_plan(gq_bam_dev *b, const int64_t *loci_begin, const int64_
     struct stat sb, si;
     if (stat(bai_path, &si) == 0 && fstat(b->fd, &sb) == 0 && si.st_mtime >= sb.st_mtime) bai = load_bai(b, bai_path);
   }
-  std::vector<Seg> segs;
-  int64_t from = 0;  // the searches move forward (ranges in file order)
+  // the ranges (validated in order), then each range's segment on its own: the searches are
+  // independent (the probe cache is shared), so they run on several host threads — without a
+  // BAI, each is two binary searches of ~log2(blocks) probes, each probe a host inflate
+  struct Range {
+    int32_t c;
+    int64_t S, E;
+  };
+  std::vector<Range> ranges;
   for (int32_t c = 0; c < n_ref; ++c) {
     for (int64_t i = loci_begin[c]; i < loci_begin[c + 1]; ++i) {
       const int64_t S = loci_start[i], E = loci_end[i];
       if (E <= S) continue;
       if (i > loci_begin[c] && S < loci_end[i - 1]) return set_err(GQ_E_ARG, "gq_bam_dev_plan: unsorted loci");
-      Seg g{0, 0, 0, false};
-      bool have_start = false;
-      if (bai) {
-        const std::vector<uint64_t> &lx = b->bai_ioff[(size_t)c];
-        const int64_t w = S >> 14;
-        if (w >= (int64_t)lx.size()) continue;  // no record overlaps a window from here on
-        // the window's entry, or (an older writer's empty window) the first later one
-        int64_t j = w;
-        while (j < (int64_t)lx.size() && lx[(size_t)j] == 0) ++j;
-        if (j < (int64_t)lx.size()) {
-          if (!voff_pos(b, lx[(size_t)j], g.b0, g.first)) {
-            bai = false;
-            b->bai_ioff.clear();
-          } else {
-            have_start = true;
-          }
-        } else {
-          continue;
-        }
-      }
-      if (!have_start) {
-        int64_t bs;
-        gq_status st = first_block_at(b, from, rec_key(c, (int32_t)std::max<int64_t>(0, S - halo)), bs);
-        if (st) return st;
-        if (bs >= nb) continue;  // every record is before the range
-        // the first record starting at or after the end of the last block before it
-        int64_t kprev, land;
-        if (bs > 0) {
-          if ((st = key_upto(b, bs - 1, kprev, &land))) return st;
-        } else {
-          land = b->rec0;
-        }
-        stream_pos(b, land, g.b0, g.first);
-      }
-      // stop: the first block whose records all start at or past (c, E)
-      int64_t be;
-      gq_status st = first_block_at(b, std::max<int64_t>(g.b0, from), rec_key(c, (int32_t)std::min<int64_t>(E, INT32_MAX - 1)), be);
-      if (st) return st;
-      if (be + 1 >= nb) {
-        g.b1 = nb;
-        g.eof = true;
-      } else {
-        g.b1 = be + 2;  // records start up to block be; block be + 1 completes the last one
-      }
-      from = g.b0;
-      segs.push_back(g);
+      ranges.push_back(Range{c, S, E});
     }
+  }
+  // the index's start for a range: 1 found, 0 none (no record overlaps the range), -1 unusable index
+  auto bai_start = [&](const Range &r, Seg &g) -> int {
+    const std::vector<uint64_t> &lx = b->bai_ioff[(size_t)r.c];
+    const int64_t w = r.S >> 14;
+    if (w >= (int64_t)lx.size()) return 0;  // no record overlaps a window from here on
+    // the window's entry, or (an older writer's empty window) the first later one
+    int64_t j = w;
+    while (j < (int64_t)lx.size() && lx[(size_t)j] == 0) ++j;
+    if (j >= (int64_t)lx.size()) return 0;
+    return voff_pos(b, lx[(size_t)j], g.b0, g.first) ? 1 : -1;
+  };
+  if (bai) {  // an index naming a block that is not there is not used at all
+    for (const Range &r : ranges) {
+      Seg g{0, 0, 0, false};
+      if (bai_start(r, g) < 0) {
+        bai = false;
+        b->bai_ioff.clear();
+        break;
+      }
+    }
+  }
+  std::vector<Seg> per(ranges.size());
+  std::vector<char> keep(ranges.size(), 0);
+  std::vector<gq_status> sts(ranges.size(), GQ_OK);
+  std::vector<std::string> msgs(ranges.size());
+  auto plan_range = [&](size_t i) -> gq_status {
+    const Range &r = ranges[i];
+    Seg g{0, 0, 0, false};
+    if (bai) {
+      if (bai_start(r, g) == 0) return GQ_OK;
+    } else {
+      int64_t bs;
+      gq_status st = first_block_at(b, 0, rec_key(r.c, (int32_t)std::max<int64_t>(0, r.S - halo)), bs);
+      if (st) return st;
+      if (bs >= nb) return GQ_OK;  // every record is before the range
+      // the first record starting at or after the end of the last block before it
+      int64_t kprev, land;
+      if (bs > 0) {
+        if ((st = key_upto(b, bs - 1, kprev, &land))) return st;
+      } else {
+        land = b->rec0;
+      }
+      stream_pos(b, land, g.b0, g.first);
+    }
+    // stop: the first block whose records all start at or past (c, E)
+    int64_t be;
+    gq_status st = first_block_at(b, g.b0, rec_key(r.c, (int32_t)std::min<int64_t>(r.E, INT32_MAX - 1)), be);
+    if (st) return st;
+    if (be + 1 >= nb) {
+      g.b1 = nb;
+      g.eof = true;
+    } else {
+      g.b1 = be + 2;  // records start up to block be; block be + 1 completes the last one
+    }
+    per[i] = g;
+    keep[i] = 1;
+    return GQ_OK;
+  };
+  {
+    const int nt = (int)std::min<size_t>(ranges.size(), bai ? 1 : 16);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < ranges.size();) {
+        sts[i] = plan_range(i);
+        if (sts[i]) msgs[i] = gq_last_error();  // (the message is thread-local)
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (std::thread &t : th) t.join();
+  }
+  std::vector<Seg> segs;
+  for (size_t i = 0; i < ranges.size(); ++i) {
+    if (sts[i]) return set_err(sts[i], "%s", msgs[i].c_str());
+    if (keep[i]) segs.push_back(per[i]);
   }
   // file order, then merge segments whose blocks meet
   std::sort(segs.begin(), segs.end(), [](const Seg &x, const Seg &y) {

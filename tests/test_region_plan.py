@@ -128,3 +128,30 @@ def test_stale_or_foreign_index_is_ignored(tmp_path):
         fh.write(b"BAI\1" + struct.pack("<i", 7))  # another dictionary
     plan = bamdev.MappedBam(p, populate=False).plan(region, halo=4000, bai=q)
     assert not plan["used_index"]
+
+
+def test_parallel_block_walk_equals_the_sequential_one(tmp_path, monkeypatch):
+    """A file past 128 MB is walked in chunks on several host threads (gq_bam_dev_map_ex) and
+    stitched along the true chain: the block table must be the sequential walk's.  Compared through
+    the plan of the whole dictionary (every block, its stream bytes) and of a few ranges."""
+    from guacamole_amd import synthetic
+    g = synthetic.generate(5_000_000, 30.0, seed=3)
+    path = str(tmp_path / "big.bam")
+    g.write_bam(path, level=1)
+    import os
+    assert os.path.getsize(path) > (128 << 20)
+    names = g.contig_names
+    regions = [LociSet.parse("all").result(dict(zip(names, [5_000_000]))),
+               LociSet.parse("%s:1000000-1200000,%s:4000000-4100000" % (names[0], names[0])).result(
+                   dict(zip(names, [5_000_000])))]
+    out = {}
+    for nt in ("1", "16"):
+        monkeypatch.setenv("GQ_MAP_THREADS", nt)
+        got = []
+        for reg in regions:
+            m = bamdev.MappedBam(path, populate=False)
+            got.append(m.plan(reg, 1 << 20, None))
+            m.close()
+        out[nt] = got
+    assert out["1"] == out["16"]
+    assert out["1"][0]["n_blocks"] > 2000
