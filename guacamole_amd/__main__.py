@@ -3,8 +3,12 @@ restricted to the two callers on the accelerated path."""
 import os
 import sys
 
-from . import bamdev
-from .commands import main
+from . import _early
+
+_early.start(sys.argv[1:])  # the GPU context opens on a host thread while the imports below run
+
+from . import bamdev  # noqa: E402
+from .commands import main  # noqa: E402
 
 bamdev.DEFER_RELEASE = True  # this process ends after the command: the loaders' buffers go with it
 rc = main()

@@ -138,9 +138,15 @@ class MappedBam:
     def __init__(self, path: str, populate: bool = True):
         self.path = path
         self.h = C.c_void_p()
-        self.t = time.perf_counter()
-        rc = native.lib().gq_bam_dev_map_ex(path.encode(), int(populate), C.byref(self.h))
-        self.t_mapped = time.perf_counter()
+        from . import _early
+        got = _early.take_map(path) if populate else None  # (the CLI's map, made while it imported)
+        if got is not None and got[0] == 0:  # (a failed early map is redone here: its message is that thread's)
+            rc, self.h, self.t, self.t_mapped = got
+            native.lib()
+        else:
+            self.t = time.perf_counter()
+            rc = native.lib().gq_bam_dev_map_ex(path.encode(), int(populate), C.byref(self.h))
+            self.t_mapped = time.perf_counter()
         self.ok = rc != GQ_E_NOT_BGZF
         if self.ok:
             _raise(rc)

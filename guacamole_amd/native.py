@@ -286,8 +286,14 @@ class Context:
     """One gq_ctx per GPU (gq_open / gq_close)."""
 
     def __init__(self, device: int = 0):
+        from . import _early
+        h = _early.take(device)  # the CLI's context, opened while the interpreter imported
         self.h = C.c_void_p()
-        _check(lib().gq_open(int(device), C.byref(self.h)))
+        if h is not None and h.value:
+            lib()
+            self.h = h
+        else:
+            _check(lib().gq_open(int(device), C.byref(self.h)))
         self.device = device
         # germline calls reuse the context's result image: a DeviceCalls is valid until the
         # next germline call on this context (gqpileup.h, gq_calls_device)
