@@ -47,9 +47,6 @@
 #ifndef GQ_DIR_MASKED
 #define GQ_DIR_MASKED 0
 #endif
-#ifndef GQ_DIR_GROUP
-#define GQ_DIR_GROUP 4  // lanes (columns) walking their slots together: 1, 2, 4, 8, 16, 32 or 64
-#endif
 struct DirCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = 4;     // waves per workgroup, each on its own tiles
@@ -61,32 +58,7 @@ struct DirCfg {
   static constexpr int64_t kShallow = 255;   // window reads of the byte-count instantiation
 };
 
-// bytes [a, b) of a 64-bit word (0 <= a, b <= 8)
-__device__ __forceinline__ uint64_t byte_range_mask(int32_t a, int32_t b) {
-  const uint64_t lt = b > 0 ? (~0ull >> (64 - 8 * b)) : 0ull;
-  const uint64_t ge = a < 8 ? (~0ull << (8 * a)) : 0ull;
-  return lt & ge;
-}
-
-// Inclusive prefix maximum / suffix minimum over the 64 lanes (every lane active).
-__device__ __forceinline__ int32_t wave_incl_max_i(int32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t y = __shfl_up(v, d, 64);
-    if (lane >= d) v = max(v, y);
-  }
-  return v;
-}
-__device__ __forceinline__ int32_t wave_suffix_min_i(int32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t y = __shfl_down(v, d, 64);
-    if (lane + d < 64) v = min(v, y);
-  }
-  return v;
-}
+// (byte_range_mask, wave_incl_max_i, wave_suffix_min_i: gq_direct_common.h)
 
 // DEEP = false: every tile whose window holds at most kShallow reads (per-locus counts fit bytes:
 // no 16-bit widening; event counts in bytes); deeper tiles are listed (deep, ctr->n_deep) for the

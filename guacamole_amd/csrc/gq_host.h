@@ -1198,6 +1198,9 @@ struct gq_ctx {
   int proj_wg_per_cu = 0;  // resident germline_proj workgroups per CU (occupancy query, once)
   int dir_wg_per_cu = 0;   // resident germline_direct workgroups per CU (occupancy query, once)
   int som_wg_per_cu = 0;   // resident somatic_proj workgroups per CU
+  int somd_wg_per_cu = 0;  // resident somatic_direct workgroups per CU
+  gq::DevBuf mtab;         // somatic_direct: the margin-term table (margin_table, 64 KiB)
+  int mtab_key = -1;       // its probability model (1: including alignment), -1: not built
   int call_wg_per_cu = 0;  // resident somatic_call_k<false> workgroups per CU
   gq::DevBuf ranges, tiles, recs, recs_sorted, keys, keys_sorted, idx, idx_sorted, cplx, pool, counters, sort_tmp, image, tiles2, srecs;
   gq::DevBuf c_depth, c_pos, c_base, c_indel, c_ref, c_rb, c_amb, slow, deep_tiles;

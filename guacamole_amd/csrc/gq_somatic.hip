@@ -171,6 +171,8 @@ __device__ __forceinline__ void hom_ref_margin_lane(const DevReads &R, int64_t r
 }
 
 #include "gq_somatic_proj.h"
+#include "gq_direct_common.h"
+#include "gq_somatic_direct.h"
 
 // ------------------------------------------------------------------------------------------
 // somatic_tile: candidate loci (the tiles somatic_proj cannot take)
@@ -1635,8 +1637,12 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   // one loci plan per sample, 512-locus tiles aligned to 512-locus blocks (somatic_proj)
   Plan pt, pn;
+  // somatic_direct (straight from the reads) unless GQ_SOM=proj asks for somatic_proj over the
+  // projection and margin projection (A/B; the same candidates)
+  static const bool som_proj = getenv("GQ_SOM") && strcmp(getenv("GQ_SOM"), "proj") == 0;
+  const bool direct = !som_proj && t->d.seq_cap >= 8;
   const MarginReq mreq{(int)p->min_mapq, true};  // (with the projection, the margin projection in the same pass)
-  gq_status st = ensure_projection(c, t, &mreq);  // (derived on first use)
+  gq_status st = direct ? GQ_OK : ensure_projection(c, t, &mreq);  // (derived on first use)
   if (st) return st;
   st = plan(c, t, loci, SomProjCfg::kT, pt, c->tiles, 0, 0, 0, true);
   if (st) return st;
@@ -1663,8 +1669,18 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     free(res);
     return st;
   }
-  // the tumor's margin projection for this mapq filter (derived once per read set and filter)
-  st = ensure_margin_projection(c, t, (int)p->min_mapq);
+  // the tumor's margin projection for this mapq filter (derived once per read set and filter);
+  // somatic_direct: only the term table
+  if (direct) {
+    if (c->mtab_key != 1) {
+      HIP_TRY(c->mtab.ensure(256 * 256));
+      hipLaunchKernelGGL(margin_table, dim3(256), dim3(256), 0, c->stream, 1, (uint8_t *)c->mtab.p);
+      HIP_TRY(hipGetLastError());
+      c->mtab_key = 1;
+    }
+  } else {
+    st = ensure_margin_projection(c, t, (int)p->min_mapq);
+  }
   if (st) {
     free(res);
     return st;
@@ -1676,15 +1692,17 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     if (c->n_cu <= 0 &&
         hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
       c->n_cu = 256;
-    if (c->som_wg_per_cu <= 0) {
+    int &wg_cu = direct ? c->somd_wg_per_cu : c->som_wg_per_cu;
+    if (wg_cu <= 0) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0) != hipSuccess ||
-          nb <= 0)
-        nb = 4;
-      c->som_wg_per_cu = nb;
+      const hipError_t e =
+          direct ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_direct<false>, SomDirCfg::kThreads, 0)
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0);
+      if (e != hipSuccess || nb <= 0) nb = direct ? 2 : 4;
+      wg_cu = nb;
     }
     og.ncols = (int)std::max<int64_t>(1, std::min<int64_t>({(pt.n_tiles + SomProjCfg::kWaves - 1) / SomProjCfg::kWaves,
-                                                           (int64_t)c->som_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
+                                                           (int64_t)wg_cu * c->n_cu, (int64_t)kPartsCols}));
     const unsigned long long wg_loci = (unsigned long long)((pt.n_tiles + og.ncols - 1) / og.ncols) * SomProjCfg::kT;
     og.capA[1] = wg_loci / 16 + 256;
     og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;
@@ -1708,7 +1726,18 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
     Counters *ctr = (Counters *)c->counters.p;
     HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(Counters), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    if (rv.b)
+    if (direct) {
+      if (rv.b)
+        hipLaunchKernelGGL(somatic_direct<true>, dim3((unsigned)og.ncols), dim3(SomDirCfg::kThreads), 0, c->stream,
+                           (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d, n->d.start, n->d.end,
+                           (const uint8_t *)c->mtab.p, (int)p->min_mapq, (ComplexItem *)c->cplx.p, og, ctr,
+                           (int32_t *)c->slow.p, rv, 0, dbg);
+      else
+        hipLaunchKernelGGL(somatic_direct<false>, dim3((unsigned)og.ncols), dim3(SomDirCfg::kThreads), 0, c->stream,
+                           (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d, n->d.start, n->d.end,
+                           (const uint8_t *)c->mtab.p, (int)p->min_mapq, (ComplexItem *)c->cplx.p, og, ctr,
+                           (int32_t *)c->slow.p, rv, 0, dbg);
+    } else if (rv.b)
       hipLaunchKernelGGL(somatic_proj<true>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,
                          (const uint8_t *)t->mproj, (const uint8_t *)t->mnb, n->d.start, n->d.end, (ComplexItem *)c->cplx.p, og, ctr,
@@ -2209,20 +2238,23 @@ gq_status gq_germline_standard(gq_ctx *c, const gq_dev_reads *rd, const gq_loci 
   st = ensure_margin_projection(c, rd, (int)p->min_mapq, false);
   if (st) return fail(st);
   const int no_bound = rd->d.n_samples > 1 ? 1 : 0;
+  const bool direct = false;  // (germline-standard keeps somatic_proj over its margin projection)
   OutGeom og{};
   {
     if (c->n_cu <= 0 &&
         hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
       c->n_cu = 256;
-    if (c->som_wg_per_cu <= 0) {
+    int &wg_cu = direct ? c->somd_wg_per_cu : c->som_wg_per_cu;
+    if (wg_cu <= 0) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0) != hipSuccess ||
-          nb <= 0)
-        nb = 4;
-      c->som_wg_per_cu = nb;
+      const hipError_t e =
+          direct ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_direct<false>, SomDirCfg::kThreads, 0)
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, somatic_proj<false>, SomProjCfg::kThreads, 0);
+      if (e != hipSuccess || nb <= 0) nb = direct ? 2 : 4;
+      wg_cu = nb;
     }
     og.ncols = (int)std::max<int64_t>(1, std::min<int64_t>({(pt.n_tiles + SomProjCfg::kWaves - 1) / SomProjCfg::kWaves,
-                                                           (int64_t)c->som_wg_per_cu * c->n_cu, (int64_t)kPartsCols}));
+                                                           (int64_t)wg_cu * c->n_cu, (int64_t)kPartsCols}));
     const unsigned long long wg_loci = (unsigned long long)((pt.n_tiles + og.ncols - 1) / og.ncols) * SomProjCfg::kT;
     og.capA[1] = wg_loci / 16 + 256;
     og.capB[1] = (unsigned long long)pt.n_loci / 65536 + 1024;

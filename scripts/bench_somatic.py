@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--somatic-rate", type=float, default=2e-4)
     ap.add_argument("--cpu-window", type=int, default=200_000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--rederive", action="store_true", help="re-derive both read sets every step")
     args = ap.parse_args()
 
     from guacamole_amd import native, synthetic
@@ -50,12 +51,17 @@ def main():
     n = ctx.upload(ng.arrays)
     loci = (np.array([0], np.int32), np.array([0], np.int64), np.array([args.length - 1], np.int64),
             np.array([0], np.int64))
+    def step():
+        if args.rederive:
+            ctx.rederive(t)
+            ctx.rederive(n)
+        return ctx.somatic_standard(t, n, loci)
     for _ in range(args.warmup):
-        ctx.somatic_standard(t, n, loci)
+        step()
     stages = {"pileup_ms": [], "complex_ms": [], "finalize_ms": [], "total_ms": []}
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        calls = ctx.somatic_standard(t, n, loci)
+        calls = step()
         tm = ctx.timings()
         for k in stages:
             stages[k].append(tm[k])
