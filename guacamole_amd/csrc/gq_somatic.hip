@@ -1731,12 +1731,12 @@ gq_status gq_somatic_standard_ref(gq_ctx *c, const gq_dev_reads *t, const gq_dev
         hipLaunchKernelGGL(somatic_direct<true>, dim3((unsigned)og.ncols), dim3(SomDirCfg::kThreads), 0, c->stream,
                            (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d, n->d.start, n->d.end,
                            (const uint8_t *)c->mtab.p, (int)p->min_mapq, (ComplexItem *)c->cplx.p, og, ctr,
-                           (int32_t *)c->slow.p, rv, 0, dbg);
+                           (int32_t *)c->slow.p, rv, 0, (dbg >> 16) & 0xFF);
       else
         hipLaunchKernelGGL(somatic_direct<false>, dim3((unsigned)og.ncols), dim3(SomDirCfg::kThreads), 0, c->stream,
                            (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d, n->d.start, n->d.end,
                            (const uint8_t *)c->mtab.p, (int)p->min_mapq, (ComplexItem *)c->cplx.p, og, ctr,
-                           (int32_t *)c->slow.p, rv, 0, dbg);
+                           (int32_t *)c->slow.p, rv, 0, (dbg >> 16) & 0xFF);
     } else if (rv.b)
       hipLaunchKernelGGL(somatic_proj<true>, dim3((unsigned)og.ncols), dim3(SomProjCfg::kThreads), 0, c->stream,
                          (const Tile *)c->tiles.p, (const Tile *)c->tiles2.p, pt.n_tiles, t->d,

@@ -45,6 +45,8 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
     const int32_t *__restrict__ n_start, const int32_t *__restrict__ n_end, const uint8_t *__restrict__ tab,
     int min_mapq, ComplexItem *__restrict__ cand, OutGeom og, Counters *ctr, int32_t *__restrict__ slow, RefView ref,
     int no_bound, int dbg) {
+  // dbg (diagnostics: env GQ_DBG >> 16, clear of the callers' bits; results are wrong when set):
+  // 1 no margin lookups, 2 no normal depth, 32 no counting, 64 no MD events
   using C = SomDirCfg;
   constexpr int T = C::kT, U = C::kU;
   // per locus x of the block at word ix(x) = (x & 7) * 64 + (x >> 3): event read bases (A | C << 16
@@ -56,8 +58,10 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   __shared__ __attribute__((aligned(16))) int32_t mcw[C::kWaves][T];
   __shared__ __attribute__((aligned(16))) uint2 rcw[C::kWaves][C::kSlots];
   __shared__ uint16_t rqw[C::kWaves][C::kSlots];  // each slot's read: mapq | kept << 8 (0: no margin terms)
-  __shared__ __attribute__((aligned(16))) uint32_t lrw[C::kWaves][64];  // a margin-table row (256 bytes)
   __shared__ int32_t hxw[C::kWaves][64], hnw[C::kWaves][64];
+  // per workgroup: the Match terms of mapping qualities 0-63 (the aligners' range), byte
+  // mq << 7 | q (8 KiB; a read of higher mapq looks its terms up in the global table)
+  __shared__ __attribute__((aligned(16))) uint32_t mterm_w[64 * 128 / 4];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -77,10 +81,20 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   };
   zero_words();
   if (threadIdx.x < 2) outn[threadIdx.x] = 0;
-  __syncthreads();
   const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
   const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
+  for (int w = threadIdx.x; w < 64 * 128 / 4; w += C::kThreads) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = 4 * w + k;  // mq << 7 | q
+      v |= (uint32_t)tab[((b >> 7) << 8) | ((b & 127) << 1) | 1] << (8 * k);
+    }
+    mterm_w[w] = v;
+  }
+  __syncthreads();
+  const uint8_t *mterm = reinterpret_cast<const uint8_t *>(mterm_w);
   const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
   unsigned visited = 0;
   const int32_t colr = 8 * lane;
@@ -99,7 +113,7 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
       continue;
     }
     // ---- normal depth: each read spans [start, end) (any element), as +1 / -1 differences
-    for (int64_t q = tn.rb; q < tn.re; q += 64) {
+    for (int64_t q = tn.rb; q < ((dbg & 2) ? tn.rb : tn.re); q += 64) {
       const int64_t r = q + lane;
       if (r < tn.re) {
         const int32_t a = max(n_start[r], B0), b = min(n_end[r], B0 + T);
@@ -109,9 +123,6 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
         }
       }
     }
-    // ---- tumor: the margin-table row of the window's first read's mapq in LDS
-    const uint32_t lmq = re > rb ? (uint32_t)__builtin_amdgcn_readfirstlane((int)R.mapq[rb]) : 0u;
-    lrw[wave][lane] = reinterpret_cast<const uint32_t *>(tab + (lmq << 8))[lane];
     // counters: nibbles folded into bytes every 12 slots, widened into 16-bit pairs every 240
     uint32_t ca[2] = {0, 0}, cc[2] = {0, 0}, ct[2] = {0, 0}, cg[2] = {0, 0}, cn[2] = {0, 0};
     uint32_t wA[4] = {0, 0, 0, 0}, wC[4] = {0, 0, 0, 0}, wT[4] = {0, 0, 0, 0}, wG[4] = {0, 0, 0, 0},
@@ -194,7 +205,7 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
         const bool nomd = valid && nmd < 0;
         const bool gen = valid && !nomd && ld < 0;
         uint32_t nrun = valid && !nomd && !gen && e > B0 && s < B0 + T ? 1u : 0u;
-        const bool evr = valid && !nomd && nmd > 0 && s < B0 + T;
+        const bool evr = valid && !nomd && nmd > 0 && s < B0 + T && !(dbg & 64);
         uint32_t v4[4] = {0u, 0u, 0u, 0u};
         auto load_ev = [&](int32_t k0) {
 #pragma unroll
@@ -348,11 +359,10 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
       };
       auto count = [&](const uint2 (&x)[U], const uint2 (&y)[U], const uint32_t (&mt)[U]) {
         if (nn + U > 15) fold();
-        // (uniform) every slot of the batch with terms reads them from the staged row
-        bool lds_ok = true;
+        bool low_mq = true;  // (uniform) every slot of the batch with terms has its row in LDS
 #pragma unroll
-        for (int u = 0; u < U; ++u) lds_ok = lds_ok && (!((mt[u] >> 24) & 1u) || ((mt[u] >> 16) & 0xFFu) == lmq);
-        lds_ok = __ballot(!lds_ok) == 0;
+        for (int u = 0; u < U; ++u) low_mq = low_mq && (!((mt[u] >> 24) & 1u) || ((mt[u] >> 16) & 0xFFu) < 64u);
+        const bool lds_terms = __ballot(!low_mq) == 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t la = mt[u] & 15u, lb = (mt[u] >> 4) & 15u, sh = (mt[u] >> 5) & 56u;
@@ -372,20 +382,32 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
             ntg[h] += __builtin_amdgcn_perm(0x10000001u, 0u, cd);
             cn[h] += __builtin_amdgcn_perm(0x00010000u, 0u, cd);
           }
-          // margin terms of the Match elements (bytes outside the run or of a dropped read: 128)
-          uint32_t tv[2] = {0u, 0u};
-          auto terms = [&](const uint8_t *row) {
+          // margin terms of the Match elements (bytes outside the run or of a dropped read: 128):
+          // branch-free lookups (a quality past the table reads its byte and is replaced by
+          // kMargin8None), packed into two words, then masked
+          uint32_t tv[2];
+          const uint64_t live = kept_s ? m : 0ull;
+          if (dbg & 1) {
+            tv[0] = tv[1] = 0x80808080u;  // (diagnostics: no lookups)
+          } else {
+            uint32_t t8[8];
+            if (lds_terms) {
+              const uint8_t *rowl = mterm + ((mqs & 63u) << 7);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const bool lv = kept_s && k >= (int)la && k < (int)lb;
-              const uint32_t qb = (uint32_t)(q64 >> (8 * k)) & 0xFFu;
-              const uint32_t t = lv ? term(row, qb, 1u) : (uint32_t)kMargin8Zero;
-              none = none || t == kMargin8None;
-              tv[k >> 2] |= t << (8 * (k & 3));
+              for (int k = 0; k < 8; ++k) t8[k] = rowl[(uint32_t)(q64 >> (8 * k)) & 0x7Fu];
+            } else {
+              const uint8_t *rowg = tab + (mqs << 8);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) t8[k] = rowg[(((uint32_t)(q64 >> (8 * k)) & 0x7Fu) << 1) | 1u];
             }
-          };
-          if (lds_ok) terms(reinterpret_cast<const uint8_t *>(lrw[wave]));  // (LDS loads)
-          else terms(tab + (mqs << 8));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t8[k] = ((q64 >> (8 * k + 7)) & 1u) ? (uint32_t)kMargin8None : t8[k];
+            const uint32_t lo = (uint32_t)live, hi = (uint32_t)(live >> 32);
+            tv[0] = ((t8[0] | (t8[1] << 8) | (t8[2] << 16) | (t8[3] << 24)) & lo) | (0x80808080u & ~lo);
+            tv[1] = ((t8[4] | (t8[5] << 8) | (t8[6] << 16) | (t8[7] << 24)) & hi) | (0x80808080u & ~hi);
+            auto zb = [](uint32_t v) { return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u; };
+            none = none || zb(tv[0]) || zb(tv[1]);
+          }
           msum[0] += __builtin_amdgcn_perm(0u, tv[0], 0x0c010c00u);
           msum[1] += __builtin_amdgcn_perm(0u, tv[0], 0x0c030c02u);
           msum[2] += __builtin_amdgcn_perm(0u, tv[1], 0x0c010c00u);
