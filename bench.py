@@ -112,7 +112,7 @@ def main() -> int:
     ap.add_argument("--no-configs3", dest="configs3", action="store_false",
                     help="skip the configs[3] rank share (one rank's share of the 30x b37 genome through the "
                          "multi-GPU ingest path, on this GPU)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r06.json"),
                     help="PMC-derived HBM bytes per pileup launch (from a separate rocprofv3 --pmc pass)")
     args = ap.parse_args()
 
@@ -680,8 +680,9 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
     ach = b_alg / (k_ms * 1e-3) / 1e9
     visited = int(calls.visited_loci)
     pmc = somatic_pmc("panel" if tdepth >= 500 else "chr1", L, tdepth, ndepth)
+    som_kernel = "somatic_proj" if os.environ.get("GQ_SOM") == "proj" else "somatic_direct"
     traffic = None if pmc is None else next(
-        (v.get("hbm_bytes_per_launch") for k, v in sorted(pmc["kernels"].items()) if k.startswith("somatic_proj")), None)
+        (v.get("hbm_bytes_per_launch") for k, v in sorted(pmc["kernels"].items()) if k.startswith(som_kernel)), None)
     return {"metric": "somatic-standard loci/sec, tumor %gx / normal %gx" % (tdepth, ndepth),
             "value": visited * steps / el, "unit": "loci/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
             "warmup": warmup, "step": "re-derivation of both read sets (upload-time derivation, tumor projection and "
@@ -705,7 +706,7 @@ def somatic_run(ctx, args, steps: int = 3, warmup: int = 1, L: int = 0, tdepth: 
                        "deep_ms": float(np.mean(stages["deep_ms"])), "candidates": int(calls.candidate_loci),
                        "deep_candidates": int(tm["deep_loci"]), "deep_max_depth": int(tm["deep_max"]),
                        "ns_per_candidate": 1e6 * float(np.mean(stages["call_ms"])) / max(1, int(calls.candidate_loci))},
-            "roofline": {"bound": "hbm", "kernel": "somatic_proj", "kernel_ms": k_ms, "achieved": ach,
+            "roofline": {"bound": "hbm", "kernel": som_kernel, "kernel_ms": k_ms, "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "dram_frac": None if traffic is None else traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -949,7 +950,7 @@ def somatic_parity_window(ctx, t, n, tg, ng, L: int, width: int):
     return {"loci": [w0, w1], "calls": len(want), "identical": bool(ok), "oracle_s": cpu_s}
 
 
-SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r05.json")
+SOMATIC_PMC = os.path.join(ROOT, "profiles", "somatic_pmc_r06.json")
 
 
 def somatic_pmc(workload: str, L: int, tdepth: float, ndepth: float):

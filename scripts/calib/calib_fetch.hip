@@ -11,6 +11,8 @@
 //   u64_lane_ua   8 B per lane, each lane streaming its own 512 B stretch (+3), so one load
 //                 instruction touches 64 different lines (germline_direct's lane-private slot
 //                 walk: each lane on a different read's bytes)
+//   u64_g4_ua     8 B per lane, groups of four lanes on 32 contiguous bytes (+3), 16 groups on 16
+//                 different stretches (the direct kernels' group-of-four slot walk)
 //   b32_rows      4 B per lane, a wave's 256 B contiguous (germline_proj's projection rows)
 //   rec64_perm    a lane reads one 64-byte record (four 16-byte loads) at a permuted record
 //                 index (the callers' scattered per-read record loads)
@@ -85,6 +87,24 @@ __global__ __launch_bounds__(kThreads) void u64_lane_ua(const uint8_t *__restric
   sink[blockIdx.x * kThreads + threadIdx.x] = acc;
 }
 
+// groups of four lanes: each group streams its own 2 KiB stretch of the wave's 32 KiB chunk,
+// 32 contiguous bytes (+3) per instruction (germline_direct / somatic_direct's group-of-four
+// slot walk: a group's lanes on one read's 32 bytes, the 16 groups on 16 reads)
+__global__ __launch_bounds__(kThreads) void u64_g4_ua(const uint8_t *__restrict__ a, size_t nchunks, uint32_t *sink) {
+  const int lane = threadIdx.x & 63, g = lane >> 2, gl = lane & 3;
+  const size_t w0 = (blockIdx.x * (size_t)kThreads + threadIdx.x) >> 6, ws = ((size_t)gridDim.x * kThreads) >> 6;
+  uint32_t acc = 0;
+  for (size_t c = w0; c + 1 < nchunks; c += ws) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(a + 32768 * c), (short)0, 65536, 0x00020000);
+#pragma unroll 8
+    for (int i = 0; i < 64; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, 2048 * g + 32 * i + 8 * gl + 3, 0, 0);
+      acc ^= v[0] ^ v[1];
+    }
+  }
+  sink[blockIdx.x * kThreads + threadIdx.x] = acc;
+}
+
 __global__ __launch_bounds__(kThreads) void b32_rows(const uint32_t *__restrict__ a, size_t n4, uint32_t *sink) {
   uint32_t acc = 0;
   for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < n4; i += (size_t)gridDim.x * kThreads) acc ^= a[i];
@@ -152,6 +172,7 @@ int main(int argc, char **argv) {
   run("stream16", (double)kBytes, [&] { stream16<<<grid, kThreads>>>((const uint4 *)buf, n16, sink); });
   run("u64_coal_ua", (double)(nch512 - 1) * 512, [&] { u64_coal_ua<<<grid, kThreads>>>(buf, nch512, sink); });
   run("u64_lane_ua", (double)(nch32k - 1) * 32768, [&] { u64_lane_ua<<<grid, kThreads>>>(buf, nch32k, sink); });
+  run("u64_g4_ua", (double)(nch32k - 1) * 32768, [&] { u64_g4_ua<<<grid, kThreads>>>(buf, nch32k, sink); });
   run("b32_rows", (double)kBytes, [&] { b32_rows<<<grid, kThreads>>>((const uint32_t *)buf, n4, sink); });
   run("rec64_perm", (double)kBytes, [&] { rec64_perm<<<grid, kThreads>>>((const uint4 *)buf, nrec, sink); });
   // u16_perm reads 2 B of every 64-B record: the bytes of the lines it touches are the buffer

@@ -34,7 +34,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # dominant load shape per kernel (prefix match), a shape of the calibration file
 KERNEL_SHAPE = [
-    ("germline_direct", "u64_lane_ua"),   # each lane walks its own column's runs: 8-B loads on 64 different reads
+    ("germline_direct", "u64_g4_ua"),     # groups of four lanes on one read's 32 bytes, 16 reads per load
+    ("somatic_direct", "u64_g4_ua"),
     ("germline_complex", "rec64_perm"),   # a wave per queued locus: scattered per-read records
     ("germline_walk", "rec64_perm"),
     ("germline_standard", "rec64_perm"),
@@ -72,6 +73,8 @@ def main():
     ap.add_argument("--round", required=True)
     ap.add_argument("--calib", default=os.path.join(ROOT, "profiles", "r06_pmc_calibration.json"))
     ap.add_argument("--call-kernel", default="germline_direct<false>")
+    ap.add_argument("--somatic", default=None, help="also write somatic_pmc_<round>.json for this workload "
+                    "(chr1|panel:L:tumor_depth:normal_depth)")
     a = ap.parse_args()
     cal = json.load(open(a.calib))["shapes"]
     prof = os.path.join(ROOT, "profiles")
@@ -129,6 +132,17 @@ def main():
            "step": {"kernels": step, "hbm_bytes": tot,
                     "hbm_bytes_bounds": [sum(v["bounds"][0] for v in step.values()),
                                          sum(v["bounds"][1] for v in step.values())]}}
+    if a.somatic:  # the somatic bench's PMC summary (bench.somatic_pmc reads it)
+        wl, L, td, nd = a.somatic.split(":")
+        out_p = os.path.join(prof, "somatic_pmc_%s.json" % a.round)
+        doc = json.load(open(out_p)) if os.path.exists(out_p) else {}
+        ks = {k: dict(pm[k], **kern.get(k, {})) for k in pm}
+        doc[wl] = {"length": int(L), "tumor_depth": float(td), "normal_depth": float(nd),
+                   "source": "profiles/%s_pmc.csv" % a.tag, "kernels": ks, "calibration": out["calibration"],
+                   "correction": out["correction"]}
+        with open(out_p, "w") as fh:
+            json.dump(doc, fh, indent=1, sort_keys=True)
+        return
     with open(os.path.join(prof, "traffic_%s.json" % a.round), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     for k, v in sorted(step.items(), key=lambda kv: -kv[1]["hbm_bytes"]):
