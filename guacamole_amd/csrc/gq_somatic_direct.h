@@ -59,9 +59,10 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   __shared__ __attribute__((aligned(16))) uint2 rcw[C::kWaves][C::kSlots];
   __shared__ uint16_t rqw[C::kWaves][C::kSlots];  // each slot's read: mapq | kept << 8 (0: no margin terms)
   __shared__ int32_t hxw[C::kWaves][64], hnw[C::kWaves][64];
-  // per workgroup: the Match terms of mapping qualities 0-63 (the aligners' range), byte
-  // mq << 7 | q (8 KiB; a read of higher mapq looks its terms up in the global table)
-  __shared__ __attribute__((aligned(16))) uint32_t mterm_w[64 * 128 / 4];
+  // per workgroup: the margin_table rows of mapping qualities 0-63 (the aligners' range), byte
+  // mq << 8 | q << 1 | match as in the global table (16 KiB; a read of higher mapq looks its
+  // terms up there)
+  __shared__ __attribute__((aligned(16))) uint32_t mterm_w[64 * 256 / 4];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -84,15 +85,7 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   const int64_t per = n_tiles / gridDim.x, extra = n_tiles % gridDim.x;
   const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
-  for (int w = threadIdx.x; w < 64 * 128 / 4; w += C::kThreads) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int b = 4 * w + k;  // mq << 7 | q
-      v |= (uint32_t)tab[((b >> 7) << 8) | ((b & 127) << 1) | 1] << (8 * k);
-    }
-    mterm_w[w] = v;
-  }
+  for (int w = threadIdx.x; w < 64 * 256 / 4; w += C::kThreads) mterm_w[w] = reinterpret_cast<const uint32_t *>(tab)[w];
   __syncthreads();
   const uint8_t *mterm = reinterpret_cast<const uint8_t *>(mterm_w);
   const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
@@ -219,8 +212,14 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
           const int cat = base_cat(base);
           if (cat < 4) atomicAdd(&ev[(cat >> 1) * T + x], 1u << (16 * (cat & 1)));
           if (kept) {
-            const uint8_t *row = tab + (mq << 8);
-            const uint32_t t0 = term(row, qv, 0u), t1 = term(row, qv, 1u);
+            uint32_t t0, t1;
+            if (mq < 64u) {  // (the workgroup's LDS rows)
+              t0 = term(mterm + (mq << 8), qv, 0u);
+              t1 = term(mterm + (mq << 8), qv, 1u);
+            } else {
+              t0 = term(tab + (mq << 8), qv, 0u);
+              t1 = term(tab + (mq << 8), qv, 1u);
+            }
             none = none || t0 == kMargin8None || t1 == kMargin8None;
             if (t0 != t1) atomicAdd(&mc[x], (int32_t)t0 - (int32_t)t1);
           }
@@ -392,9 +391,9 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
           } else {
             uint32_t t8[8];
             if (lds_terms) {
-              const uint8_t *rowl = mterm + ((mqs & 63u) << 7);
+              const uint8_t *rowl = mterm + ((mqs & 63u) << 8);
 #pragma unroll
-              for (int k = 0; k < 8; ++k) t8[k] = rowl[(uint32_t)(q64 >> (8 * k)) & 0x7Fu];
+              for (int k = 0; k < 8; ++k) t8[k] = rowl[((((uint32_t)(q64 >> (8 * k))) & 0x7Fu) << 1) | 1u];
             } else {
               const uint8_t *rowg = tab + (mqs << 8);
 #pragma unroll
