@@ -47,11 +47,14 @@
 #ifndef GQ_DIR_MASKED
 #define GQ_DIR_MASKED 0
 #endif
+#ifndef GQ_DIR_U
+#define GQ_DIR_U 4
+#endif
 struct DirCfg {
   static constexpr int kT = 512;       // loci per tile: 64 lanes x 8 loci
   static constexpr int kWaves = 4;     // waves per workgroup, each on its own tiles
   static constexpr int kThreads = 64 * kWaves;
-  static constexpr int kU = 4;         // slots per batch (their loads issued before use)
+  static constexpr int kU = GQ_DIR_U;  // slots per batch (their loads issued before use; 240 % kU == 0)
   static constexpr int kRound = 64;    // window reads per round (a lane each)
   static constexpr int kSlots = 256;   // runs per chunk (LDS slots)
   static constexpr int64_t kMaxWin = 65535;  // window reads (16-bit counts); more: germline_walk

@@ -9,7 +9,9 @@ fills), GQ_ROWS=firstfit (first-fit row assignment instead of the parallel earli
 GQ_FILL=pieces (the projection by pieces instead of cells), GQ_MFILL=cells / pieces (the margin
 projection by cells / pieces instead of read-major), GQ_GERM=proj (germline-threshold through
 germline_proj over the projection instead of germline_direct straight from the reads; the
-projection-fill variants run with it, so their germline records come from the fill under test).
+projection-fill variants run with it, so their germline records come from the fill under test),
+GQ_SOM=proj (somatic-standard's candidates from somatic_proj over the projection and margin
+projection instead of somatic_direct; the projection and margin-fill variants run with it).
 A synthetic 300 kb 60x / 30x pair with a raised somatic
 rate, so hundreds of candidates and calls reach every path."""
 import json
@@ -34,11 +36,11 @@ def _run(extra):
 def test_kernel_variants_give_the_default_records():
     base = _run({})
     assert base["somatic"] > 20 and base["germline"] > 100
-    pj = {"GQ_GERM": "proj"}
+    pj = {"GQ_GERM": "proj", "GQ_SOM": "proj"}
     rw = dict(pj, GQ_FILL="rw")
-    for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, pj, rw, dict(rw, GQ_FILL_U="2"), dict(rw, GQ_FILL_U="4"),
-                  dict(rw, GQ_FILL_W="2"), dict(rw, GQ_FILL_W="4"), dict(rw, GQ_FILL_ONE="1"), dict(pj, GQ_FILL="slice"),
-                  dict(pj, GQ_ROWS="firstfit"), dict(pj, GQ_FILL="pieces"), dict(pj, GQ_FILL="cellsb"),
-                  {"GQ_MFILL": "cells"}, {"GQ_MFILL": "pieces"}):
+    for extra in ({"GQ_CALL_SPLIT": "1"}, {"GQ_CALL_WPE": "2"}, {"GQ_SOM": "proj"}, pj, rw, dict(rw, GQ_FILL_U="2"),
+                  dict(rw, GQ_FILL_U="4"), dict(rw, GQ_FILL_W="2"), dict(rw, GQ_FILL_W="4"), dict(rw, GQ_FILL_ONE="1"),
+                  dict(pj, GQ_FILL="slice"), dict(pj, GQ_ROWS="firstfit"), dict(pj, GQ_FILL="pieces"),
+                  dict(pj, GQ_FILL="cellsb"), dict(pj, GQ_MFILL="cells"), dict(pj, GQ_MFILL="pieces")):
         got = _run(extra)
         assert got == base, (extra, got, base)

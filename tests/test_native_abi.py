@@ -51,3 +51,35 @@ def test_bam_map_on_the_host(tmp_path):
         bamdev.MappedBam(str(bad))
     joined = bamdev.map_bams([fixture("chrM.sorted.bam")])["join"]()
     assert joined[fixture("chrM.sorted.bam")].ok
+
+
+def test_somatic_rows_from_columns():
+    """SomaticCalls.rows builds its dicts from column lists (one tolist per column): the same rows,
+    field for field and type for type, as indexing the numpy columns element by element."""
+    import numpy as np
+    from guacamole_amd import native as N
+    n = 257
+    rng = np.random.default_rng(7)
+    cols = {k: rng.integers(0, 9, n).astype(dt) for k, dt in
+            (("contig", np.int32), ("pos", np.int32), ("sample", np.int32), ("ref_len", np.int32),
+             ("alt_len", np.int32), ("gq", np.int32), ("flags", np.int32))}
+    cols["ref_off"] = rng.integers(0, 100, n).astype(np.int64)
+    cols["alt_off"] = rng.integers(0, 100, n).astype(np.int64)
+    cols["log_odds"] = rng.random(n) * 50
+    for s in ("tumor", "normal"):
+        a = np.zeros(n, dtype=N._EVIDENCE_DTYPE)
+        for f in N.EVIDENCE_FIELDS:
+            a[f] = rng.random(n) * 100
+        cols[s] = a
+    pool = bytes(rng.integers(65, 91, 120).astype(np.uint8))
+    got = N.SomaticCalls(cols, pool, 0, 0).rows
+    c = cols
+    ev = lambda e: tuple(e[k].item() for k in N.EVIDENCE_FIELDS)  # noqa: E731
+    want = [dict(contig=int(c["contig"][i]), locus=int(c["pos"][i]), sample=int(c["sample"][i]),
+                 ref=pool[c["ref_off"][i]:c["ref_off"][i] + c["ref_len"][i]].decode("latin-1"),
+                 alt=pool[c["alt_off"][i]:c["alt_off"][i] + c["alt_len"][i]].decode("latin-1"),
+                 log_odds=float(c["log_odds"][i]), gq=int(c["gq"][i]), tumor=ev(c["tumor"][i]),
+                 normal=ev(c["normal"][i]), flags=int(c["flags"][i])) for i in range(n)]
+    assert got == want
+    assert all(type(a) is type(b) for r, w in zip(got, want) for a, b in zip(r.values(), w.values()))
+    assert N.SomaticCalls({k: v[:0] for k, v in cols.items()}, b"", 0, 0).rows == []
