@@ -382,14 +382,21 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) kmax = max(kmax, __shfl_xor(kmax, d, 64));
       kmax = (dbg & 32) ? 0 : __builtin_amdgcn_readfirstlane(kmax);  // (dbg & 32: no counting)
+      // the slot schedule: iteration k takes the slot s of [first, first + kmax) with s = k (mod
+      // kmax), so every group reaches a slot at the same iteration (k = s mod kmax) and one load
+      // instruction reads a read's bytes for all the groups its run covers (the lines it touches
+      // are fetched once, while they are hot); t0 = the offset of iteration 0
+      const int32_t t0 = (GQ_GDIR_ROT && kmax > 0 && nl > 0) ? (kmax - first % kmax) % kmax : 0;
       // a batch: U slots' 8-byte loads, all issued before any is used; mt = the column's loci
       // inside the run [a, b)
       auto issue = [&](int32_t k0, uint2 (&x)[U], uint32_t (&mt)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int32_t k = k0 + u;
-          const bool mine = k < nl;
-          const uint2 d = rc[mine ? first + k : 0];
+          int32_t t = t0 + k;  // (GQ_GDIR_ROT) the lane's slot offset at iteration k
+          t = t >= kmax ? t - kmax : t;
+          const bool mine = GQ_GDIR_ROT ? (k < kmax && t < nl) : k < nl;
+          const uint2 d = rc[mine ? first + (GQ_GDIR_ROT ? t : k) : 0];
           const int32_t s16 = (int32_t)(int16_t)(d.x & 0xFFFFu), e16 = (int32_t)(int16_t)(d.x >> 16);
           const int32_t a = min(max(s16 - colr, 0), 8), b = min(max(e16 - colr, 0), 8);
           const bool live = mine && b > a && !(dbg & 1);

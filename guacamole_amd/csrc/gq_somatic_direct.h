@@ -335,13 +335,20 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) kmax = max(kmax, __shfl_xor(kmax, d, 64));
       kmax = (dbg & 32) ? 0 : __builtin_amdgcn_readfirstlane(kmax);
+      // the slot schedule: iteration k takes the slot s of [first, first + kmax) with s = k (mod
+      // kmax), so every group reaches a slot at the same iteration (k = s mod kmax) and one load
+      // instruction reads a read's bytes for all the groups its run covers (the lines it touches
+      // are fetched once, while they are hot); t0 = the offset of iteration 0
+      const int32_t t0 = (GQ_DIR_ROT && kmax > 0 && nl > 0) ? (kmax - first % kmax) % kmax : 0;
       // a batch: U slots' base and quality loads, all issued before any is used
       auto issue = [&](int32_t k0, uint2 (&x)[U], uint2 (&y)[U], uint32_t (&mt)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int32_t k = k0 + u;
-          const bool mine = k < nl;
-          const int32_t sl = mine ? first + k : 0;
+          int32_t t = t0 + k;  // (GQ_DIR_ROT) the lane's slot offset at iteration k
+          t = t >= kmax ? t - kmax : t;
+          const bool mine = GQ_DIR_ROT ? (k < kmax && t < nl) : k < nl;
+          const int32_t sl = mine ? first + (GQ_DIR_ROT ? t : k) : 0;
           const uint2 d = rc[sl];
           const uint32_t mqs = rq[sl];  // mapq | kept << 8
           const int32_t s16 = (int32_t)(int16_t)(d.x & 0xFFFFu), e16 = (int32_t)(int16_t)(d.x >> 16);
