@@ -29,6 +29,12 @@
 // is the same sum of the same bytes, so the same loci).
 #pragma once
 
+#ifndef GQ_SDIR_GROUP
+#define GQ_SDIR_GROUP 1  // lanes walking their slots together (under the rotated schedule every lane
+                         // covering a slot reads it at the same iteration: groups of 1 / 2 / 4 / 8
+                         // measured 6.25 / 6.36 / 6.61 / 7.02 ms at chr20 60x)
+#endif
+
 struct SomDirCfg {
   static constexpr int kT = 512;
   static constexpr int kWaves = 4;
@@ -326,9 +332,9 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
       // ---- this lane's group's slots
       int32_t last = wave_incl_max_i(hx[lane]);
       int32_t first = wave_suffix_min_i(hn[lane]);
-      if (GQ_DIR_GROUP > 1) {
-        first = __shfl(first, lane & ~(GQ_DIR_GROUP - 1), 64);
-        last = __shfl(last, lane | (GQ_DIR_GROUP - 1), 64);
+      if (GQ_SDIR_GROUP > 1) {
+        first = __shfl(first, lane & ~(GQ_SDIR_GROUP - 1), 64);
+        last = __shfl(last, lane | (GQ_SDIR_GROUP - 1), 64);
       }
       const int32_t nl = last >= first ? last - first + 1 : 0;
       int32_t kmax = nl;
