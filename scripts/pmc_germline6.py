@@ -35,7 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # dominant load shape per kernel (prefix match), a shape of the calibration file
 KERNEL_SHAPE = [
     ("germline_direct", "u64_g4_ua"),     # groups of four lanes on one read's 32 bytes, 16 reads per load
-    ("somatic_direct", "u64_g4_ua"),
+    ("somatic_direct", "u64_coal_ua"),   # rotated schedule: the lanes a slot covers read it together
     ("germline_complex", "rec64_perm"),   # a wave per queued locus: scattered per-read records
     ("germline_walk", "rec64_perm"),
     ("germline_standard", "rec64_perm"),
