@@ -390,9 +390,9 @@ def main() -> int:
     line["one_shot"] = {"upload_derive_ms": float(st_upload["derive_ms"]), "first_call_ms": cold_ms,
                         "projection_ms": float(st["proj_ms"]), "first_call_device_ms": float(cold_tm["total_ms"]),
                         "total_ms": one, "loci_per_s": visited / (one * 1e-3),
-                        "derivation_kernels": "validate_reads, read_shape, pool_clean, col_count, col_derive, "
-                                              "block_index (upload); prec_fill, slice_bad, slice_windows, row_count, "
-                                              "rows64, proj_count, proj_fill, pev_fill, proj_count_ok (first call)"}
+                        "derivation_kernels": "read_prep, block_index (upload); with GQ_GERM=proj also the "
+                                              "projection (proj_prep, slice_windows, row_count, proj_fill_cells, "
+                                              "pev_fill) on the first call"}
     if rank == 0:
         e2e = {"upload_ms": upload_ms, "upload_h2d_ms": st["h2d_ms"], "upload_derive_ms": st["derive_ms"],
                "step_ms": line["ms_per_step"], "step_with_d2h_ms": host_ms_step, "reads": n_reads}
