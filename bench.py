@@ -817,6 +817,13 @@ def configs3_rank_share(ctx, args, share_rank: int = 7, world: int = 8, margin: 
         t = time.perf_counter()
         rs = load_reads_device(ctx, path, filters, region=region)
         ingest_s = time.perf_counter() - t
+        # the loader's buffers (~2.5x the share's inflated BAM) are released on a host thread;
+        # their hipFree calls hold the HIP runtime, so the first call would wait for them: joined
+        # here and reported as their own stage
+        from guacamole_amd.bamdev import join_release_threads
+        t = time.perf_counter()
+        join_release_threads()
+        release_s = time.perf_counter() - t
         cidx = rs.contig_index()
         loci = (np.array([cidx[p[0]] for p in mine], np.int32), np.array([p[2] for p in mine], np.int64),
                 np.array([p[3] for p in mine], np.int64), np.array([p[4] for p in mine], np.int64))
@@ -843,7 +850,8 @@ def configs3_rank_share(ctx, args, share_rank: int = 7, world: int = 8, margin: 
         out.update({
             "loci": int(sum(p[3] - p[2] for p in mine)), "visited_loci": visited, "contigs": len(pieces),
             "reads": int(rs.n), "genome_loci": genome_loci,
-            "stages_s": {"ingest": ingest_s, "call": call_ms / 1e3, "result_image_d2h": image_ms / 1e3},
+            "stages_s": {"ingest": ingest_s, "loader_release": release_s, "call": call_ms / 1e3,
+                         "result_image_d2h": image_ms / 1e3},
             "ingest": {k: tm.get(k) for k in ("map_ms", "h2d_ms", "inflate_ms", "records_ms", "parse_ms", "fill_ms",
                                               "derive_ms", "comp_bytes", "bam_bytes", "blocks", "max_span", "replans",
                                               "open_s", "scan_s", "total_s", "wall_s")},

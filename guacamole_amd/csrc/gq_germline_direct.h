@@ -47,6 +47,9 @@
 #ifndef GQ_DIR_MASKED
 #define GQ_DIR_MASKED 0
 #endif
+#ifndef GQ_DIR_EVPF
+#define GQ_DIR_EVPF 0
+#endif
 #ifndef GQ_DIR_U
 #define GQ_DIR_U 4
 #endif
@@ -224,6 +227,10 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
     Fields nf = load_fields(rb);
     int64_t c0 = rb;
     bool first_round = true;
+    // GQ_DIR_EVPF: the next round's first four MD events, issued at the end of a round (its
+    // fields have arrived by then), so a round does not start with a dependent load
+    uint32_t pv4[4] = {0u, 0u, 0u, 0u};
+    int64_t pv_c0 = -1;  // the round pv4 belongs to
     while (c0 < re) {  // ---- a chunk: rounds while their runs fit kSlots slots, then the counting
       const uint64_t t_round = (dbg & 16) ? __builtin_readcyclecounter() : 0;
       hx[lane] = -1;
@@ -256,7 +263,14 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
             else atomicAdd(&ev[x], 1u << (8 * cat));
           }
         };
-        if (evr) load_ev(0);
+        if (evr) {
+          if (GQ_DIR_EVPF && pv_c0 == c0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v4[j] = pv4[j];
+          } else {
+            load_ev(0);
+          }
+        }
         // (a general read: slots for its (M|=|X) operations, read_prep's bound on its count
         // segments; those outside the block stay empty)
         if (gen && e > B0 && s < B0 + T) nrun = (uint32_t)min(-1 - ld, C::kSlots);
@@ -361,6 +375,12 @@ __global__ __launch_bounds__(DirCfg::kThreads) __attribute__((amdgpu_waves_per_e
             if (past || k0 >= nmd) break;
             load_ev(k0);
           }
+        }
+        if (GQ_DIR_EVPF && c0 + C::kRound < re) {  // the next round's first events (nf arrived)
+          const bool nv = c0 + C::kRound + lane < re && nf.nmd > 0 && nf.s < B0 + T;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pv4[j] = nv ? R.md_ev[nf.mo + (j < nf.nmd ? j : nf.nmd - 1)] : 0u;
+          pv_c0 = c0 + C::kRound;
         }
         nslot += total;
         c0 += C::kRound;
