@@ -1241,7 +1241,9 @@ gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out
   struct stat st;
   if (fstat(b->fd, &st) != 0 || st.st_size == 0) return set_err(GQ_E_BAM_IO, "cannot stat (or empty) %s", path);
   b->map_len = (size_t)st.st_size;
-  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), b->fd, 0);
+  // (populate: the pages are faulted in by the block walk's threads below, in parallel, rather
+  // than by MAP_POPULATE on this one thread)
+  void *m = mmap(nullptr, b->map_len, PROT_READ, MAP_PRIVATE, b->fd, 0);
   if (m == MAP_FAILED) return set_err(GQ_E_BAM_IO, "cannot map %s", path);
   b->map = (const uint8_t *)m;
   const uint8_t *p = b->map;
@@ -1283,6 +1285,19 @@ gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out
   const int nt = (int)std::min<int64_t>(max_nt, std::max<int64_t>(1, n / kChunkMin));
   std::vector<std::vector<Mem>> part((size_t)nt);
   std::vector<int64_t> start((size_t)nt, -1), land((size_t)nt, -1);
+  // populate: the file's pages mapped by 16 threads (a read per 4 KiB page), beside the walk
+  std::vector<std::thread> touch;
+  std::atomic<uint32_t> touched{0};
+  if (populate) {
+    const int ntt = (int)std::min<int64_t>(16, std::max<int64_t>(1, n >> 24));
+    for (int t = 0; t < ntt; ++t)
+      touch.emplace_back([&, t, ntt]() {  // (ntt by value: this block ends before the threads do)
+        const int64_t a = n * t / ntt, e = n * (t + 1) / ntt;
+        uint32_t acc = 0;
+        for (int64_t o = a; o < e; o += 4096) acc += p[o];
+        touched.fetch_add(acc, std::memory_order_relaxed);
+      });
+  }
   auto spec = [&](int t) {  // chunk t's speculative walk
     const int64_t c0 = n * t / nt, c1 = n * (t + 1) / nt;
     int64_t o = c0;
@@ -1309,6 +1324,7 @@ gq_status gq_bam_dev_map_ex(const char *path, int32_t populate, gq_bam_dev **out
     spec(0);
     for (std::thread &x : th) x.join();
   }
+  for (std::thread &x : touch) x.join();
   std::vector<Mem> mems;
   int64_t off = 0;
   for (int t = 0; t < nt && off >= 0 && off < n; ++t) {
