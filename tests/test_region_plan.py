@@ -155,3 +155,26 @@ def test_parallel_block_walk_equals_the_sequential_one(tmp_path, monkeypatch):
         out[nt] = got
     assert out["1"] == out["16"]
     assert out["1"][0]["n_blocks"] > 2000
+
+
+def test_early_map_is_adopted(tmp_path):
+    """The CLI's early host map (guacamole_amd._early: gq_bam_dev_map_ex on a thread while the
+    interpreter imports) is taken by the command's MappedBam for the same path, once, with the
+    same header; a second MappedBam of the path maps it again.  Without a GPU the early context
+    open fails quietly and take() gives None (the ordinary open reports the error)."""
+    from guacamole_amd import _early
+    from tests.conftest import fixture
+    bam = fixture("chrM.sorted.bam")
+    _early._maps.clear()
+    _early._map_threads.clear()
+    _early.start(["germline-threshold", "--reads", bam, "--device", "0"])
+    assert bam in _early._map_threads
+    m = bamdev.MappedBam(bam)
+    assert m.ok and bam not in _early._map_threads and bam not in _early._maps
+    names, lengths = m.contigs()
+    m2 = bamdev.MappedBam(bam)
+    assert m2.contigs() == (names, lengths) and "chrM" in names
+    m.close()
+    m2.close()
+    h = _early.take(0)
+    assert h is None or h.value  # (a GPU box: the opened context's handle)
