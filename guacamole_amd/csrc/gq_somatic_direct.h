@@ -29,6 +29,9 @@
 // is the same sum of the same bytes, so the same loci).
 #pragma once
 
+#ifndef GQ_SOMD_PAIR
+#define GQ_SOMD_PAIR 0
+#endif
 #ifndef GQ_SDIR_GROUP
 #define GQ_SDIR_GROUP 1  // lanes walking their slots together (under the rotated schedule every lane
                          // covering a slot reads it at the same iteration: groups of 1 / 2 / 4 / 8
@@ -69,6 +72,9 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   // mq << 8 | q << 1 | match as in the global table (16 KiB; a read of higher mapq looks its
   // terms up there)
   __shared__ __attribute__((aligned(16))) uint32_t mterm_w[64 * 256 / 4];
+  // GQ_SOMD_PAIR: the Match terms of a quality pair (q0, q1 < 64) of the workgroup's first
+  // tumor read's mapq, t(q0) | t(q1) << 8 at q0 | q1 << 6: one LDS read per two elements
+  __shared__ uint16_t ptab[GQ_SOMD_PAIR ? 4096 : 1];
   __shared__ unsigned outn[2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -92,6 +98,16 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
   const int64_t i0 = blockIdx.x * per + min((int64_t)blockIdx.x, extra);
   const int64_t i1 = i0 + per + ((int64_t)blockIdx.x < extra ? 1 : 0);
   for (int w = threadIdx.x; w < 64 * 256 / 4; w += C::kThreads) mterm_w[w] = reinterpret_cast<const uint32_t *>(tab)[w];
+  uint32_t pmq = 0x100u;  // (none)
+  if (GQ_SOMD_PAIR && i0 < i1) {
+    const Tile t0 = tiles_t[i0];
+    pmq = t0.re > t0.rb ? (uint32_t)R.mapq[t0.rb] : 0x100u;
+    if (pmq < 0x100u) {
+      const uint8_t *row = tab + (pmq << 8);
+      for (int e = threadIdx.x; e < 4096; e += C::kThreads)
+        ptab[e] = (uint16_t)((uint32_t)row[((e & 63) << 1) | 1] | ((uint32_t)row[(((e >> 6) & 63) << 1) | 1] << 8));
+    }
+  }
   __syncthreads();
   const uint8_t *mterm = reinterpret_cast<const uint8_t *>(mterm_w);
   const unsigned long long cbase = og.slot(1, (int)blockIdx.x, 0), ccap = og.capA[1];
@@ -399,8 +415,21 @@ __global__ __launch_bounds__(SomDirCfg::kThreads) void somatic_direct(
           // kMargin8None), packed into two words, then masked
           uint32_t tv[2];
           const uint64_t live = kept_s ? m : 0ull;
+          const bool pu = !kept_s || (mqs == pmq && (q64 & live & 0xC0C0C0C0C0C0C0C0ull) == 0ull);
           if (dbg & 1) {
             tv[0] = tv[1] = 0x80808080u;  // (diagnostics: no lookups)
+          } else if (GQ_SOMD_PAIR && __ballot(!pu) == 0) {  // (uniform) every slot on the pair table
+            uint32_t pr[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const uint32_t c2 = (uint32_t)(q64 >> (16 * j)) & 0xFFFFu;
+              pr[j] = ptab[(c2 & 63u) | ((c2 >> 2) & 0xFC0u)];
+            }
+            const uint32_t lo = (uint32_t)live, hi = (uint32_t)(live >> 32);
+            tv[0] = ((pr[0] | (pr[1] << 16)) & lo) | (0x80808080u & ~lo);
+            tv[1] = ((pr[2] | (pr[3] << 16)) & hi) | (0x80808080u & ~hi);
+            auto zb = [](uint32_t v) { return ((v - 0x01010101u) & ~v & 0x80808080u) != 0u; };
+            none = none || zb(tv[0]) || zb(tv[1]);
           } else {
             uint32_t t8[8];
             if (lds_terms) {
